@@ -1,0 +1,128 @@
+"""Task DTOs shared by the three services.
+
+Reference parity:
+* ``TaskModel`` / ``TaskAddModel`` / ``TaskUpdateModel`` -- Backend.Api/Models/TaskModel.cs:3-29,
+  the processor's copy Processor.Backend.Svc/Models/TaskModel.cs:3-13 and the UI copy with
+  ``[Required]``/``[Display]`` annotations Frontend.Ui/Pages/Tasks/Models/TasksModel.cs:6-49.
+
+One definition serves all three (the reference triplicates it).  UI-only metadata
+(display names, required flags) lives in ``FIELD_DISPLAY`` / ``REQUIRED_FIELDS`` and is
+enforced by the frontend's form binder, not by the API -- exactly like the reference,
+whose API models carry no validation attributes.
+"""
+from __future__ import annotations
+
+import json
+import uuid
+from datetime import datetime
+from typing import Annotated, Any, ClassVar
+
+from pydantic import BaseModel, BeforeValidator, ConfigDict, PlainSerializer, model_validator
+from pydantic.alias_generators import to_camel
+
+from .dotnet import DOTNET_MIN, GUID_EMPTY, format_datetime, parse_datetime, parse_guid
+
+DotNetDateTime = Annotated[
+    datetime,
+    BeforeValidator(parse_datetime),
+    PlainSerializer(format_datetime, return_type=str, when_used="json"),
+]
+Guid = Annotated[
+    uuid.UUID,
+    BeforeValidator(parse_guid),
+    PlainSerializer(lambda u: str(u), return_type=str, when_used="json"),
+]
+
+
+class WireModel(BaseModel):
+    """Base: camelCase on the wire, case-insensitive property matching on input,
+    unknown properties ignored (ASP.NET model binding drops extras, which is how the
+    processor's full ``TaskModel`` binds to the API's ``TaskAddModel``,
+    reference ExternalTasksProcessorController.cs:33 vs TasksController.cs:34-46)."""
+
+    model_config = ConfigDict(alias_generator=to_camel, populate_by_name=True, extra="ignore",
+                              validate_assignment=False)
+    _lower_aliases: ClassVar[dict[str, str]] = {}
+
+    def __init_subclass__(cls, **kw: Any) -> None:
+        super().__init_subclass__(**kw)
+        cls._lower_aliases = {}
+
+    @classmethod
+    def __pydantic_init_subclass__(cls, **kw: Any) -> None:
+        super().__pydantic_init_subclass__(**kw)
+        cls._lower_aliases = {
+            (f.alias or name).lower(): (f.alias or name) for name, f in cls.model_fields.items()
+        }
+
+    @model_validator(mode="before")
+    @classmethod
+    def _case_insensitive(cls, data: Any) -> Any:
+        if isinstance(data, dict):
+            la = cls._lower_aliases
+            out = {}
+            for k, v in data.items():
+                if isinstance(k, str):
+                    a = la.get(k.lower())
+                    if a is not None:
+                        out[a] = v
+                        continue
+                out[k] = v
+            return out
+        return data
+
+    def to_wire(self) -> dict[str, Any]:
+        return self.model_dump(mode="json", by_alias=True)
+
+    def to_json(self) -> str:
+        return self.model_dump_json(by_alias=True)
+
+    @classmethod
+    def from_wire(cls, data: Any):
+        if isinstance(data, (bytes, bytearray, str)):
+            data = json.loads(data)
+        return cls.model_validate(data)
+
+
+class TaskModel(WireModel):
+    task_id: Guid = GUID_EMPTY
+    task_name: str = ""
+    task_created_by: str = ""
+    task_created_on: DotNetDateTime = DOTNET_MIN
+    task_due_date: DotNetDateTime = DOTNET_MIN
+    task_assigned_to: str = ""
+    is_completed: bool = False
+    is_over_due: bool = False
+
+
+class TaskAddModel(WireModel):
+    task_name: str = ""
+    task_created_by: str = ""
+    task_due_date: DotNetDateTime = DOTNET_MIN
+    task_assigned_to: str = ""
+
+
+class TaskUpdateModel(WireModel):
+    task_id: Guid = GUID_EMPTY
+    task_name: str = ""
+    task_due_date: DotNetDateTime = DOTNET_MIN
+    task_assigned_to: str = ""
+
+
+# UI annotations (reference Frontend.Ui/Pages/Tasks/Models/TasksModel.cs:20-48)
+FIELD_DISPLAY = {
+    "taskName": "Task Name",
+    "taskDueDate": "Task DueDate",
+    "taskAssignedTo": "Assigned To",
+}
+REQUIRED_FIELDS = ("taskName", "taskDueDate", "taskAssignedTo")
+
+
+def tasks_to_json(tasks: list[TaskModel]) -> bytes:
+    return ("[" + ",".join(t.to_json() for t in tasks) + "]").encode()
+
+
+def tasks_from_json(data: Any) -> list[TaskModel]:
+    if isinstance(data, (bytes, bytearray, str)):
+        data = json.loads(data) if data else []
+    return [TaskModel.model_validate(d) for d in (data or [])]

@@ -1,0 +1,143 @@
+"""Backend API (app-id ``tasksmanager-backend-api``).
+
+Routes (reference SURVEY.md §2.11):
+
+=======  ==================================  ======================================  ==========================
+verb     route                               result                                  reference
+=======  ==================================  ======================================  ==========================
+GET      /api/tasks?createdBy=               200 [TaskModel] newest first            TasksController.cs:20-24
+GET      /api/tasks/{taskId}                 200 TaskModel / 404 / 400 bad guid      TasksController.cs:26-32
+POST     /api/tasks                          201 + Location, empty body              TasksController.cs:34-46
+PUT      /api/tasks/{taskId}                 200 / 400                               TasksController.cs:48-59
+PUT      /api/tasks/{taskId}/markcomplete    200 / 400                               TasksController.cs:61-67
+DELETE   /api/tasks/{taskId}                 200 / 404                               TasksController.cs:69-75
+GET      /api/overduetasks                   200 [TaskModel] oldest first            OverdueTasksController.cs:20-24
+POST     /api/overduetasks/markoverdue       200                                     OverdueTasksController.cs:26-32
+GET      /openapi/v1.json                    OpenAPI (Development only)              Program.cs:16,21-24
+=======  ==================================  ======================================  ==========================
+
+The manager implementation is chosen by ``TasksManager:Backend`` (``fake`` | ``store``).
+The reference hard-wires the fake (Program.cs:13) while its module-4 docs wire the
+store (docs/aca/04-aca-dapr-stateapi/Program-dotnet9.cs:7-9); here the default is
+``store`` when a sidecar is configured (``DAPR_HTTP_PORT`` / ``TT_SIDECAR_UDS``) and
+``fake`` otherwise, so ``python -m ...backend_api`` alone reproduces module 1.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import uuid
+from pathlib import Path
+
+from ...models import TaskAddModel, TaskModel, TaskUpdateModel, tasks_to_json
+from ...models.dotnet import is_guid
+from ...sdk.client import SidecarClient
+from ...web.app import WebApp, read_model
+from ...web.http import HTTPError, Request, Response, empty
+from ..hosting import create_host, map_openapi, run_host
+from .managers import FakeTasksManager, TasksManager, TasksStoreManager
+
+ROLE = "tasksmanager-backend-api"
+CONTENT_ROOT = Path(__file__).parent
+log = logging.getLogger("TasksController")
+
+
+def _task_id(req: Request) -> uuid.UUID:
+    raw = req.path_params["taskId"]
+    if not is_guid(raw):
+        raise HTTPError(400, detail={"taskId": [f"The value '{raw}' is not valid."]})
+    return uuid.UUID(raw.strip("{}"))
+
+
+def _json(body: bytes, status: int = 200) -> Response:
+    return Response(body, status, None, "application/json; charset=utf-8")
+
+
+def register_controllers(app: WebApp, manager: TasksManager) -> None:
+    # -- TasksController (reference Controllers/TasksController.cs) --------------
+    @app.route("/api/tasks", ("GET",), name="GetTasks", query=["createdBy"], tag="Tasks",
+               responses={200: [TaskModel]})
+    async def get_tasks(req: Request) -> Response:
+        return _json(tasks_to_json(await manager.get_tasks_by_creator(req.query_get("createdBy") or "")))
+
+    @app.route("/api/tasks/{taskId}", ("GET",), name="GetTask", tag="Tasks", responses={200: TaskModel, 404: None})
+    async def get_task(req: Request) -> Response:
+        t = await manager.get_task_by_id(_task_id(req))
+        if t is None:
+            return empty(404)
+        return _json(t.model_dump_json(by_alias=True).encode())
+
+    @app.route("/api/tasks", ("POST",), name="CreateTask", tag="Tasks", body=TaskAddModel, responses={201: None})
+    async def post_task(req: Request) -> Response:
+        m: TaskAddModel = await read_model(req, TaskAddModel)
+        tid = await manager.create_new_task(m.task_name, m.task_created_by, m.task_assigned_to, m.task_due_date)
+        return Response(b"", 201, [("Location", f"/api/tasks/{tid}")])
+
+    @app.route("/api/tasks/{taskId}", ("PUT",), name="UpdateTask", tag="Tasks", body=TaskUpdateModel,
+               responses={200: None, 400: None})
+    async def put_task(req: Request) -> Response:
+        tid = _task_id(req)
+        m: TaskUpdateModel = await read_model(req, TaskUpdateModel)
+        ok = await manager.update_task(tid, m.task_name, m.task_assigned_to, m.task_due_date)
+        return empty(200) if ok else empty(400)
+
+    @app.route("/api/tasks/{taskId}/markcomplete", ("PUT",), name="MarkComplete", tag="Tasks",
+               responses={200: None, 400: None})
+    async def mark_complete(req: Request) -> Response:
+        ok = await manager.mark_task_completed(_task_id(req))
+        return empty(200) if ok else empty(400)
+
+    @app.route("/api/tasks/{taskId}", ("DELETE",), name="DeleteTask", tag="Tasks", responses={200: None, 404: None})
+    async def delete_task(req: Request) -> Response:
+        ok = await manager.delete_task(_task_id(req))
+        return empty(200) if ok else empty(404)
+
+    # -- OverdueTasksController (reference Controllers/OverdueTasksController.cs) --
+    @app.route("/api/overduetasks", ("GET",), name="GetOverdueTasks", tag="OverdueTasks",
+               responses={200: [TaskModel]})
+    async def get_overdue(req: Request) -> Response:
+        return _json(tasks_to_json(await manager.get_yesterdays_due_tasks()))
+
+    @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",
+               body=[TaskModel], responses={200: None})
+    async def mark_overdue(req: Request) -> Response:
+        tasks = await read_model(req, [TaskModel])
+        await manager.mark_overdue_tasks(tasks)
+        return empty(200)
+
+
+def select_manager(config) -> TasksManager:
+    backend = (config.get_str("TasksManager:Backend") or "").lower()
+    has_sidecar = bool(config.get_str("DAPR_HTTP_PORT") or config.get_str("TT_SIDECAR_UDS")
+                       or config.get_str("DAPR_HTTP_ENDPOINT"))
+    if not backend:
+        backend = "store" if has_sidecar else "fake"
+    if backend == "fake":
+        return FakeTasksManager()
+    if backend == "store":
+        return TasksStoreManager(SidecarClient(),
+                                 store=config.get_str("TasksManager:StateStoreName", "statestore"),
+                                 pubsub=config.get_str("TasksManager:PubSubName", "dapr-pubsub-servicebus"),
+                                 topic=config.get_str("TasksManager:TopicName", "tasksavedtopic"))
+    raise ValueError(f"unknown TasksManager:Backend {backend!r}")
+
+
+def create_app(argv: list[str] | None = None, manager: TasksManager | None = None, config=None,
+               overrides: dict | None = None) -> WebApp:
+    app = create_host(ROLE, CONTENT_ROOT, argv, config=config, overrides=overrides)
+    app.openapi_info = {"title": "TasksTracker.TasksManager.Backend.Api | v1", "version": "1.0.0"}
+    if manager is None:
+        manager = select_manager(app.config)
+    app.services["tasks_manager"] = manager
+    register_controllers(app, manager)
+    map_openapi(app)
+    return app
+
+
+def main(argv: list[str] | None = None) -> None:
+    import sys
+    run_host(create_app(sys.argv[1:] if argv is None else argv))
+
+
+if __name__ == "__main__":
+    main()

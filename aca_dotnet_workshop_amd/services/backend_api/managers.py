@@ -1,0 +1,245 @@
+"""Task manager port and its two adapters.
+
+* ``TasksManager``       -- the ``ITasksManager`` port, 8 operations
+  (reference Backend.Api/Services/ITasksManager.cs:5-15).
+* ``FakeTasksManager``   -- in-memory list seeded with 10 tasks for
+  ``tjoudeh@bitoftech.net`` (reference Services/FakeTasksManager.cs:10-25).
+* ``TasksStoreManager``  -- sidecar-backed: state store ``statestore``, query API and
+  ``tasksavedtopic`` publication (reference Services/TasksStoreManager.cs:1-158).
+
+Deliberate deviations from the reference's latent bugs, all covered by
+tests/test_backend_api.py:
+* #1  the fake implements ``mark_overdue_tasks`` (the reference throws NotImplementedException);
+* #2  the fake's "yesterday" query compares calendar dates, filters open tasks and orders
+      ascending, matching the store semantics (the reference compares exact timestamps);
+* #3  ``update_task`` checks for a missing task *before* dereferencing it;
+* #4  ``delete_task`` reports a missing task (404) instead of always succeeding;
+* #5  query filters are built as JSON objects, not by string concatenation;
+* #11 asyncio single-threaded execution makes the fake's list race-free;
+* #12 read-modify-write operations use ETag first-write concurrency with bounded retry
+      instead of last-writer-wins.
+Everything else (status codes, orderings, the ``yyyy-MM-ddTHH:mm:ss`` due-date equality
+trap of #7, publish-on-create and publish-on-assignee-change) is kept.
+"""
+from __future__ import annotations
+
+import abc
+import logging
+import random
+import uuid
+from datetime import datetime, timedelta
+
+from ...models import TaskModel, format_fixed, naive_utc, today, utcnow
+from ...sdk.client import InvocationError, SidecarClient
+
+log = logging.getLogger("TasksManager")
+
+STORE_NAME = "statestore"
+PUBSUB_NAME = "dapr-pubsub-servicebus"
+TOPIC_NAME = "tasksavedtopic"
+SEED_CREATOR = "tjoudeh@bitoftech.net"
+
+
+class TasksManager(abc.ABC):
+    @abc.abstractmethod
+    async def get_tasks_by_creator(self, created_by: str) -> list[TaskModel]: ...
+
+    @abc.abstractmethod
+    async def get_task_by_id(self, task_id: uuid.UUID) -> TaskModel | None: ...
+
+    @abc.abstractmethod
+    async def create_new_task(self, task_name: str, created_by: str, assigned_to: str, due_date: datetime) -> uuid.UUID: ...
+
+    @abc.abstractmethod
+    async def update_task(self, task_id: uuid.UUID, task_name: str, assigned_to: str, due_date: datetime) -> bool: ...
+
+    @abc.abstractmethod
+    async def mark_task_completed(self, task_id: uuid.UUID) -> bool: ...
+
+    @abc.abstractmethod
+    async def delete_task(self, task_id: uuid.UUID) -> bool: ...
+
+    @abc.abstractmethod
+    async def mark_overdue_tasks(self, tasks: list[TaskModel]) -> None: ...
+
+    @abc.abstractmethod
+    async def get_yesterdays_due_tasks(self) -> list[TaskModel]: ...
+
+
+def _created_key(t: TaskModel) -> datetime:
+    return naive_utc(t.task_created_on)
+
+
+class FakeTasksManager(TasksManager):
+    def __init__(self, seed: bool = True, rng: random.Random | None = None) -> None:
+        self._tasks: list[TaskModel] = []
+        self._by_id: dict[uuid.UUID, TaskModel] = {}
+        rnd = rng or random.Random()
+        if seed:
+            now = utcnow()
+            for i in range(10):
+                self._add(TaskModel(task_id=uuid.uuid4(), task_name=f"Task number: {i}", task_created_by=SEED_CREATOR,
+                                    task_created_on=now + timedelta(minutes=i), task_due_date=now + timedelta(days=i),
+                                    task_assigned_to=f"assignee{rnd.randrange(50)}@mail.com"))
+
+    def _add(self, t: TaskModel) -> None:
+        self._tasks.append(t)
+        self._by_id[t.task_id] = t
+
+    async def create_new_task(self, task_name, created_by, assigned_to, due_date) -> uuid.UUID:
+        t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
+                      task_due_date=due_date, task_assigned_to=assigned_to)
+        self._add(t)
+        return t.task_id
+
+    async def delete_task(self, task_id) -> bool:
+        t = self._by_id.pop(task_id, None)
+        if t is None:
+            return False
+        self._tasks.remove(t)
+        return True
+
+    async def get_task_by_id(self, task_id) -> TaskModel | None:
+        return self._by_id.get(task_id)
+
+    async def get_tasks_by_creator(self, created_by) -> list[TaskModel]:
+        if not created_by:
+            return []
+        return sorted((t for t in self._tasks if t.task_created_by == created_by), key=_created_key, reverse=True)
+
+    async def mark_task_completed(self, task_id) -> bool:
+        t = self._by_id.get(task_id)
+        if t is None:
+            return False
+        t.is_completed = True
+        return True
+
+    async def update_task(self, task_id, task_name, assigned_to, due_date) -> bool:
+        t = self._by_id.get(task_id)
+        if t is None:
+            return False
+        t.task_name, t.task_assigned_to, t.task_due_date = task_name, assigned_to, due_date
+        return True
+
+    async def mark_overdue_tasks(self, tasks) -> None:
+        for incoming in tasks:
+            t = self._by_id.get(incoming.task_id)
+            if t is not None:
+                t.is_over_due = True
+
+    async def get_yesterdays_due_tasks(self) -> list[TaskModel]:
+        y = (today() - timedelta(days=1)).date()
+        return sorted((t for t in self._tasks if naive_utc(t.task_due_date).date() == y
+                       and not t.is_completed and not t.is_over_due), key=_created_key)
+
+
+class ConcurrencyConflict(Exception):
+    pass
+
+
+class TasksStoreManager(TasksManager):
+    """Sidecar-backed manager; ``client`` is the ``DaprClient`` equivalent."""
+
+    def __init__(self, client: SidecarClient, store: str = STORE_NAME, pubsub: str = PUBSUB_NAME,
+                 topic: str = TOPIC_NAME, max_retries: int = 5) -> None:
+        self.client = client
+        self.store = store
+        self.pubsub = pubsub
+        self.topic = topic
+        self.max_retries = max_retries
+
+    async def create_new_task(self, task_name, created_by, assigned_to, due_date) -> uuid.UUID:
+        t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
+                      task_due_date=due_date, task_assigned_to=assigned_to)
+        log.info("Save a new task with name: '%s' to state store", t.task_name)
+        await self.client.save_state(self.store, str(t.task_id), t)
+        await self._publish_task_saved(t)
+        return t.task_id
+
+    async def delete_task(self, task_id) -> bool:
+        log.info("Delete task with Id: '%s'", task_id)
+        data, etag = await self.client.get_state_and_etag(self.store, str(task_id))
+        if data is None:
+            return False
+        try:
+            await self.client.delete_state(self.store, str(task_id), etag=etag)
+        except InvocationError as e:
+            if e.status not in (409, 412):  # concurrently deleted/changed -> already gone is fine
+                raise
+        return True
+
+    async def get_task_by_id(self, task_id) -> TaskModel | None:
+        log.info("Getting task with Id: '%s'", task_id)
+        data = await self.client.get_state(self.store, str(task_id))
+        return TaskModel.model_validate(data) if data is not None else None
+
+    async def get_tasks_by_creator(self, created_by) -> list[TaskModel]:
+        if not created_by:
+            return []
+        q = {"filter": {"EQ": {"taskCreatedBy": created_by}}}
+        resp = await self.client.query_state(self.store, q)
+        tasks = [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
+        tasks.sort(key=_created_key, reverse=True)
+        return tasks
+
+    async def _read_modify_write(self, task_id: uuid.UUID, mutate) -> TaskModel | None:
+        for _ in range(self.max_retries):
+            data, etag = await self.client.get_state_and_etag(self.store, str(task_id))
+            if data is None:
+                return None
+            t = TaskModel.model_validate(data)
+            before = t.model_copy()
+            mutate(t)
+            try:
+                await self.client.save_state(self.store, str(t.task_id), t, etag=etag, concurrency="first-write")
+                return before, t  # type: ignore[return-value]
+            except InvocationError as e:
+                if e.status in (409, 412):
+                    continue  # lost a race: re-read and re-apply
+                raise
+        raise ConcurrencyConflict(f"task {task_id} kept changing under concurrent writers")
+
+    async def mark_task_completed(self, task_id) -> bool:
+        log.info("Mark task with Id: '%s' as completed", task_id)
+
+        def m(t: TaskModel) -> None:
+            t.is_completed = True
+        return (await self._read_modify_write(task_id, m)) is not None
+
+    async def update_task(self, task_id, task_name, assigned_to, due_date) -> bool:
+        log.info("Update task with Id: '%s'", task_id)
+
+        def m(t: TaskModel) -> None:
+            t.task_name, t.task_assigned_to, t.task_due_date = task_name, assigned_to, due_date
+        res = await self._read_modify_write(task_id, m)
+        if res is None:
+            return False
+        before, after = res
+        if after.task_assigned_to.lower() != before.task_assigned_to.lower():
+            await self._publish_task_saved(after)
+        return True
+
+    async def get_yesterdays_due_tasks(self) -> list[TaskModel]:
+        yesterday = today() - timedelta(days=1)
+        json_date = format_fixed(yesterday, "yyyy-MM-ddTHH:mm:ss")
+        log.info("Getting overdue tasks for yesterday date: '%s'", json_date)
+        q = {"filter": {"EQ": {"taskDueDate": json_date}}}
+        resp = await self.client.query_state(self.store, q)
+        tasks = [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
+        tasks = [t for t in tasks if not t.is_completed and not t.is_over_due]
+        tasks.sort(key=_created_key)
+        return tasks
+
+    async def mark_overdue_tasks(self, tasks) -> None:
+        items = []
+        for t in tasks:
+            log.info("Mark task with Id: '%s' as OverDue task", t.task_id)
+            t.is_over_due = True
+            items.append({"key": str(t.task_id), "value": t.to_wire()})
+        if items:
+            await self.client.save_bulk_state(self.store, items)
+
+    async def _publish_task_saved(self, t: TaskModel) -> None:
+        log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
+                 t.task_id, t.task_name, t.task_assigned_to)
+        await self.client.publish_event(self.pubsub, self.topic, t)

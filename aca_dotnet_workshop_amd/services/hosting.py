@@ -1,0 +1,132 @@
+"""Service host -- the ``WebApplication.CreateBuilder(args)`` / ``app.Run()`` equivalent.
+
+``create_host(role, content_root)`` loads layered configuration, configures structured
+logging and the tracer with the service's cloud role name (the reference's
+``AppInsightsTelemetryInitializer`` classes), and returns a ``WebApp`` with the standard
+pipeline: tracing -> metrics -> (service middlewares) -> routing.  ``/healthz`` and
+``/metrics`` are always mapped (used by the platform's probes and scaler).
+
+``run_host(app)`` binds the listener the way ASP.NET does: ``--urls`` /
+``ASPNETCORE_URLS`` (``http://+:8080`` in the reference Dockerfiles, e.g.
+Backend.Api/Dockerfile:3-5) or ``APP_PORT``; optionally a Unix socket ``TT_APP_UDS``
+for the co-located sidecar.  SIGTERM/SIGINT trigger a graceful drain.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import signal
+import sys
+from pathlib import Path
+from typing import Any, Callable
+
+from ..telemetry import REGISTRY, configure, configure_logging, metrics_middleware, server_middleware
+from ..utils.config import Configuration, load_configuration
+from ..web.app import WebApp
+from ..web.http import Response, empty, json_response, text_response
+from ..web.server import HttpServer
+
+log = logging.getLogger("hosting")
+
+
+def create_host(role: str, content_root: str | os.PathLike | None = None, argv: list[str] | None = None,
+                config: Configuration | None = None, overrides: dict[str, Any] | None = None) -> WebApp:
+    if config is None:
+        config = load_configuration(content_root, argv=argv or [], overrides=overrides)
+    role = config.get_str("TT_ROLE_NAME") or role
+    configure_logging(role, config)
+    tr = configure(role)
+    app = WebApp(role, config)
+    app.services["config"] = config
+    app.services["tracer"] = tr
+    app.use(server_middleware())
+    app.use(metrics_middleware())
+
+    async def healthz(req) -> Response:
+        return empty(204)
+
+    async def metrics(req) -> Response:
+        return text_response(REGISTRY.expose())
+
+    app.add_route("/healthz", healthz, ("GET",), include_in_schema=False)
+    app.add_route("/metrics", metrics, ("GET",), include_in_schema=False)
+
+    async def _flush() -> None:
+        tr.flush()
+    app.on_shutdown.append(_flush)
+    return app
+
+
+def map_openapi(app: WebApp, path: str = "/openapi/v1.json") -> None:
+    """``if (app.Environment.IsDevelopment()) app.MapOpenApi();``"""
+    if not app.is_development:
+        return
+
+    async def doc(req) -> Response:
+        return json_response(app.openapi())
+    app.add_route(path, doc, ("GET",), include_in_schema=False)
+
+
+def parse_urls(urls: str | None) -> list[tuple[str, int]]:
+    out = []
+    for u in (urls or "").split(";"):
+        u = u.strip()
+        if not u:
+            continue
+        rest = u.split("://", 1)[-1].rstrip("/")
+        host, _, port = rest.rpartition(":")
+        if host in ("+", "*", "[::]", "0.0.0.0", ""):
+            host = "0.0.0.0"
+        elif host == "localhost":
+            host = "127.0.0.1"
+        out.append((host, int(port)))
+    return out
+
+
+def listen_addresses(config: Configuration) -> list[tuple[str, int]]:
+    urls = config.get_str("urls") or config.get_str("ASPNETCORE_URLS")
+    addrs = parse_urls(urls)
+    if not addrs:
+        port = config.get_int("APP_PORT", config.get_int("PORT", 8080))
+        addrs = [(config.get_str("APP_HOST", "127.0.0.1"), port)]
+    return addrs
+
+
+async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
+                     ready: Callable[[list[int]], None] | None = None) -> None:
+    config: Configuration = app.services["config"]
+    loop = asyncio.get_running_loop()
+    srv = HttpServer(app, loop)
+    await app.startup()
+    ports = []
+    for host, port in listen_addresses(config):
+        ports.append(await srv.listen_tcp(host, port))
+    uds = config.get_str("TT_APP_UDS")
+    if uds:
+        await srv.listen_unix(uds)
+    stop = stop or asyncio.Event()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    log.info("%s listening on %s%s", app.name, ports, f" + {uds}" if uds else "")
+    if ready:
+        ready(ports)
+    port_file = config.get_str("TT_PORT_FILE")
+    if port_file:
+        tmp = port_file + ".tmp"
+        Path(tmp).write_text(str(ports[0]) if ports else "0")
+        os.replace(tmp, port_file)
+    await stop.wait()
+    await srv.close()
+    await app.shutdown()
+
+
+def run_host(app: WebApp) -> None:
+    try:
+        asyncio.run(serve_host(app))
+    except KeyboardInterrupt:
+        pass
+    sys.exit(0)

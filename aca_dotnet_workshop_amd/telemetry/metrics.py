@@ -1,0 +1,131 @@
+"""Counters / histograms with Prometheus text exposition (``GET /metrics``).
+
+Stands in for App Insights Live Metrics / Performance blades (reference
+docs/aca/08-aca-monitoring/index.md:383-408): request rates, failure counts and
+latency distributions per route, plus sidecar delivery counters used by the scaler.
+"""
+from __future__ import annotations
+
+import bisect
+import threading
+from typing import Iterable
+
+_DEFAULT_BUCKETS = (0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0, 10.0)
+
+
+def _labels(lbl: tuple[tuple[str, str], ...]) -> str:
+    if not lbl:
+        return ""
+    return "{" + ",".join(f'{k}="{v}"' for k, v in lbl) + "}"
+
+
+class Counter:
+    def __init__(self, name: str, help: str = "") -> None:
+        self.name, self.help = name, help
+        self.values: dict[tuple, float] = {}
+        self._lock = threading.Lock()
+
+    def inc(self, amount: float = 1.0, **labels: str) -> None:
+        key = tuple(sorted(labels.items()))
+        with self._lock:
+            self.values[key] = self.values.get(key, 0.0) + amount
+
+    def get(self, **labels: str) -> float:
+        return self.values.get(tuple(sorted(labels.items())), 0.0)
+
+    def expose(self) -> Iterable[str]:
+        yield f"# HELP {self.name} {self.help}"
+        yield f"# TYPE {self.name} counter"
+        for k, v in self.values.items():
+            yield f"{self.name}{_labels(k)} {v}"
+
+
+class Gauge(Counter):
+    def set(self, value: float, **labels: str) -> None:
+        with self._lock:
+            self.values[tuple(sorted(labels.items()))] = value
+
+    def expose(self) -> Iterable[str]:
+        yield f"# HELP {self.name} {self.help}"
+        yield f"# TYPE {self.name} gauge"
+        for k, v in self.values.items():
+            yield f"{self.name}{_labels(k)} {v}"
+
+
+class Histogram:
+    def __init__(self, name: str, help: str = "", buckets: tuple[float, ...] = _DEFAULT_BUCKETS) -> None:
+        self.name, self.help, self.buckets = name, help, buckets
+        self.series: dict[tuple, list] = {}
+        self._lock = threading.Lock()
+
+    def observe(self, value: float, **labels: str) -> None:
+        key = tuple(sorted(labels.items()))
+        with self._lock:
+            s = self.series.get(key)
+            if s is None:
+                s = self.series[key] = [[0] * (len(self.buckets) + 1), 0.0, 0]
+            s[0][bisect.bisect_left(self.buckets, value)] += 1
+            s[1] += value
+            s[2] += 1
+
+    def quantile(self, q: float, **labels: str) -> float:
+        s = self.series.get(tuple(sorted(labels.items())))
+        if not s or not s[2]:
+            return 0.0
+        target, acc = q * s[2], 0
+        for i, c in enumerate(s[0]):
+            acc += c
+            if acc >= target:
+                return self.buckets[i] if i < len(self.buckets) else float("inf")
+        return float("inf")
+
+    def expose(self) -> Iterable[str]:
+        yield f"# HELP {self.name} {self.help}"
+        yield f"# TYPE {self.name} histogram"
+        for k, (counts, total, n) in self.series.items():
+            acc = 0
+            for b, c in zip(self.buckets, counts):
+                acc += c
+                lk = k + (("le", str(b)),)
+                yield f"{self.name}_bucket{_labels(lk)} {acc}"
+            yield f"{self.name}_bucket{_labels(k + (('le', '+Inf'),))} {n}"
+            yield f"{self.name}_sum{_labels(k)} {total}"
+            yield f"{self.name}_count{_labels(k)} {n}"
+
+
+class Registry:
+    def __init__(self) -> None:
+        self.metrics: dict[str, object] = {}
+
+    def counter(self, name: str, help: str = "") -> Counter:
+        return self.metrics.setdefault(name, Counter(name, help))  # type: ignore[return-value]
+
+    def gauge(self, name: str, help: str = "") -> Gauge:
+        return self.metrics.setdefault(name, Gauge(name, help))  # type: ignore[return-value]
+
+    def histogram(self, name: str, help: str = "") -> Histogram:
+        return self.metrics.setdefault(name, Histogram(name, help))  # type: ignore[return-value]
+
+    def expose(self) -> str:
+        lines: list[str] = []
+        for m in self.metrics.values():
+            lines.extend(m.expose())  # type: ignore[attr-defined]
+        return "\n".join(lines) + "\n"
+
+
+REGISTRY = Registry()
+
+
+def metrics_middleware(registry: Registry = REGISTRY):
+    import time
+    reqs = registry.counter("http_requests_total", "HTTP requests served")
+    lat = registry.histogram("http_request_duration_seconds", "HTTP request latency")
+
+    async def mw(req, nxt):
+        t0 = time.perf_counter()
+        resp = await nxt(req)
+        route = getattr(req.route, "template", "unmatched")
+        reqs.inc(method=req.method, route=route, status=str(resp.status))
+        lat.observe(time.perf_counter() - t0, route=route)
+        return resp
+    return mw

@@ -1,0 +1,276 @@
+"""Pooled asyncio HTTP/1.1 client.
+
+Used by the SDK (app -> sidecar), by the sidecar (sidecar -> sidecar, sidecar -> app,
+sidecar -> backing services) and by tests.  Keep-alive connections are pooled per
+endpoint; endpoints are ``(host, port)`` TCP addresses or Unix-domain-socket paths
+(``unix:/path/to.sock``) -- the sidecar/app hop defaults to UDS when both sides run on
+one host, which removes the TCP loopback stack from every call.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import socket
+from collections import deque
+from typing import Any
+from urllib.parse import urlsplit
+
+from .http import Headers
+
+DEFAULT_TIMEOUT = 60.0
+
+
+class ClientResponse:
+    __slots__ = ("status", "headers", "body")
+
+    def __init__(self, status: int, headers: Headers, body: bytes) -> None:
+        self.status = status
+        self.headers = headers
+        self.body = body
+
+    def json(self) -> Any:
+        return json.loads(self.body) if self.body else None
+
+    @property
+    def text(self) -> str:
+        return self.body.decode("utf-8", "replace")
+
+    @property
+    def ok(self) -> bool:
+        return 200 <= self.status < 300
+
+    def __repr__(self) -> str:
+        return f"<ClientResponse {self.status} {len(self.body)}B>"
+
+
+class ConnectionClosed(ConnectionError):
+    pass
+
+
+class _Conn(asyncio.Protocol):
+    __slots__ = ("transport", "buf", "fut", "closed", "head", "got_bytes", "reused", "is_head", "key")
+
+    def __init__(self, key: Any) -> None:
+        self.key = key
+        self.transport: asyncio.Transport | None = None
+        self.buf = bytearray()
+        self.fut: asyncio.Future | None = None
+        self.closed = False
+        self.head = None
+        self.got_bytes = False
+        self.reused = False
+        self.is_head = False
+
+    def connection_made(self, transport: asyncio.BaseTransport) -> None:
+        self.transport = transport  # type: ignore[assignment]
+        sock = transport.get_extra_info("socket")
+        if sock is not None and sock.family in (socket.AF_INET, socket.AF_INET6):
+            try:
+                sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+
+    def connection_lost(self, exc: Exception | None) -> None:
+        self.closed = True
+        fut = self.fut
+        if fut is not None and not fut.done():
+            # close-delimited body?
+            if self.head is not None and self.head[2] is None:
+                status, headers, _ = self.head
+                fut.set_result((ClientResponse(status, headers, bytes(self.buf)), False))
+            else:
+                fut.set_exception(ConnectionClosed(str(exc) if exc else "connection closed"))
+
+    def data_received(self, data: bytes) -> None:
+        self.got_bytes = True
+        self.buf += data
+        if self.fut is None or self.fut.done():
+            return
+        try:
+            self._parse()
+        except Exception as e:
+            if not self.fut.done():
+                self.fut.set_exception(e)
+            if self.transport:
+                self.transport.close()
+
+    def _parse(self) -> None:
+        buf = self.buf
+        while self.head is None:
+            idx = buf.find(b"\r\n\r\n")
+            if idx < 0:
+                return
+            head = bytes(buf[:idx]).split(b"\r\n")
+            del buf[:idx + 4]
+            parts = head[0].decode("latin-1").split(" ", 2)
+            status = int(parts[1])
+            if 100 <= status < 200:
+                continue  # 100 Continue
+            headers = Headers()
+            for line in head[1:]:
+                k, _, v = line.partition(b":")
+                key = k.strip().lower().decode("latin-1")
+                val = v.strip().decode("latin-1")
+                if key in headers:
+                    if key == "set-cookie":
+                        prev = headers[key]
+                        headers[key] = (prev if isinstance(prev, list) else [prev]) + [val]
+                    else:
+                        headers[key] = headers[key] + ", " + val
+                else:
+                    headers[key] = val
+            if self.is_head or status in (204, 304):
+                length: Any = 0
+            elif "chunked" in headers.get("transfer-encoding", "").lower():
+                length = "chunked"
+            elif "content-length" in headers:
+                length = int(headers["content-length"])
+            else:
+                length = None  # read until close
+            self.head = (status, headers, length)
+        status, headers, length = self.head
+        keep = headers.get("connection", "").lower() != "close"
+        if length is None:
+            return
+        if length == "chunked":
+            from .server import _decode_chunked, _Incomplete
+            try:
+                body, used = _decode_chunked(buf)
+            except _Incomplete:
+                return
+            del buf[:used]
+        else:
+            if len(buf) < length:
+                return
+            body = bytes(buf[:length])
+            del buf[:length]
+        self.head = None
+        self.fut.set_result((ClientResponse(status, headers, body), keep))
+
+
+def parse_endpoint(url: str) -> tuple[Any, str]:
+    """Split ``url`` into (endpoint key, request target)."""
+    if url.startswith("unix:"):
+        # unix:/path/to.sock:/request/target
+        rest = url[5:]
+        sock, sep, target = rest.partition(".sock")
+        sock = sock + ".sock" if sep else sock
+        target = target.lstrip(":") or "/"
+        return ("unix", sock), target
+    sp = urlsplit(url)
+    port = sp.port or (443 if sp.scheme == "https" else 80)
+    target = sp.path or "/"
+    if sp.query:
+        target += "?" + sp.query
+    return ("tcp", sp.hostname or "127.0.0.1", port), target
+
+
+class HttpClient:
+    def __init__(self, max_idle_per_host: int = 256, timeout: float = DEFAULT_TIMEOUT) -> None:
+        self._idle: dict[Any, deque[_Conn]] = {}
+        self.max_idle = max_idle_per_host
+        self.timeout = timeout
+        self._closed = False
+
+    async def _connect(self, key: Any) -> _Conn:
+        loop = asyncio.get_running_loop()
+        if key[0] == "unix":
+            _, conn = await loop.create_unix_connection(lambda: _Conn(key), key[1])
+        else:
+            _, conn = await loop.create_connection(lambda: _Conn(key), key[1], key[2])
+        return conn
+
+    def _get_idle(self, key: Any) -> _Conn | None:
+        dq = self._idle.get(key)
+        while dq:
+            c = dq.pop()
+            if not c.closed:
+                return c
+        return None
+
+    def _release(self, c: _Conn) -> None:
+        if c.closed or self._closed:
+            if c.transport:
+                c.transport.close()
+            return
+        dq = self._idle.setdefault(c.key, deque())
+        if len(dq) >= self.max_idle:
+            c.transport.close()
+            return
+        dq.append(c)
+
+    async def request(self, method: str, url: str, *, headers: dict[str, str] | list[tuple[str, str]] | None = None,
+                      body: bytes | str | None = None, json_body: Any = None,
+                      timeout: float | None = None) -> ClientResponse:
+        key, target = parse_endpoint(url)
+        if json_body is not None:
+            body = json.dumps(json_body, separators=(",", ":")).encode()
+            hdrs = list(headers.items()) if isinstance(headers, dict) else list(headers or [])
+            if not any(k.lower() == "content-type" for k, _ in hdrs):
+                hdrs.append(("Content-Type", "application/json"))
+        else:
+            hdrs = list(headers.items()) if isinstance(headers, dict) else list(headers or [])
+        if isinstance(body, str):
+            body = body.encode()
+        body = body or b""
+        host = key[1] if key[0] == "tcp" else "localhost"
+        lines = [f"{method} {target} HTTP/1.1", f"Host: {host}"]
+        for k, v in hdrs:
+            lk = k.lower()
+            if lk in ("host", "content-length", "connection", "transfer-encoding"):
+                continue
+            lines.append(f"{k}: {v}")
+        if body or method in ("POST", "PUT", "PATCH"):
+            lines.append(f"Content-Length: {len(body)}")
+        payload = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1") + body
+        to = self.timeout if timeout is None else timeout
+        for attempt in (0, 1):
+            conn = self._get_idle(key)
+            if conn is None:
+                conn = await asyncio.wait_for(self._connect(key), to)
+            else:
+                conn.reused = True
+            loop = asyncio.get_running_loop()
+            conn.fut = loop.create_future()
+            conn.got_bytes = False
+            conn.is_head = method == "HEAD"
+            conn.transport.write(payload)
+            try:
+                resp, keep = await asyncio.wait_for(conn.fut, to)
+            except ConnectionClosed:
+                # stale keep-alive connection closed by the server: retry once on a fresh one
+                if conn.reused and not conn.got_bytes and attempt == 0:
+                    continue
+                raise
+            except BaseException:
+                if conn.transport:
+                    conn.transport.close()
+                conn.closed = True
+                raise
+            conn.fut = None
+            if keep:
+                self._release(conn)
+            else:
+                conn.transport.close()
+            return resp
+        raise ConnectionClosed("unreachable")
+
+    async def get(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("GET", url, **kw)
+
+    async def post(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("POST", url, **kw)
+
+    async def put(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("PUT", url, **kw)
+
+    async def delete(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("DELETE", url, **kw)
+
+    async def close(self) -> None:
+        self._closed = True
+        for dq in self._idle.values():
+            for c in dq:
+                if c.transport:
+                    c.transport.close()
+        self._idle.clear()
