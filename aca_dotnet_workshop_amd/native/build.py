@@ -1,0 +1,54 @@
+"""In-tree builder for the native extensions.
+
+* ``_ttnative``  -- C++17 document store + broker engines (g++/clang++, pybind11).
+* ``_ttgpu``     -- HIP kernels for gfx950 (see ``aca_dotnet_workshop_amd/ops``), built by
+  ``ops/build.py``.
+
+Builds are incremental (skipped when the ``.so`` is newer than every source) and land
+next to this file so the driver's gpurun snapshot carries them to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+SRC = HERE / "src"
+
+
+def ext_path(name: str) -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return HERE / f"{name}{suffix}"
+
+
+def _stale(target: Path, sources: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(s.stat().st_mtime > t for s in sources)
+
+
+def build_native(force: bool = False, verbose: bool = False) -> Path:
+    import pybind11
+
+    target = ext_path("_ttnative")
+    sources = sorted(SRC.glob("*.hpp")) + [SRC / "module.cpp"]
+    if not force and not _stale(target, sources):
+        return target
+    cxx = os.environ.get("CXX", "g++")
+    tmp = target.with_suffix(f".tmp{os.getpid()}.so")
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+           f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", str(SRC / "module.cpp"),
+           "-o", str(tmp), "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, target)
+    return target
+
+
+if __name__ == "__main__":
+    print(build_native(force="--force" in sys.argv, verbose=True))

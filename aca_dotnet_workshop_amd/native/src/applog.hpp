@@ -1,0 +1,143 @@
+// Append-only record log shared by the document store and the broker.
+//
+// Record: [u32 total_len][u8 kind][fields...] where every field is [u32 len][bytes].
+// Writes go straight to the fd (one write(2) per record) so a process crash never loses
+// an acknowledged mutation; fsync_mode=1 additionally fdatasync()s each record.
+#pragma once
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace tt {
+
+class AppLog {
+ public:
+  AppLog() = default;
+  AppLog(const AppLog&) = delete;
+  AppLog& operator=(const AppLog&) = delete;
+  ~AppLog() { close(); }
+
+  bool open(const std::string& path, int fsync_mode) {
+    path_ = path;
+    fsync_ = fsync_mode;
+    fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (fd_ < 0) throw std::runtime_error("cannot open log " + path + ": " + std::strerror(errno));
+    struct stat st;
+    if (::fstat(fd_, &st) == 0) bytes_ = (uint64_t)st.st_size;
+    return true;
+  }
+  bool is_open() const { return fd_ >= 0; }
+  uint64_t bytes() const { return bytes_; }
+  const std::string& path() const { return path_; }
+
+  void close() {
+    if (fd_ >= 0) { ::close(fd_); fd_ = -1; }
+  }
+
+  static void put_field(std::string& rec, std::string_view f) {
+    uint32_t n = (uint32_t)f.size();
+    rec.append(reinterpret_cast<const char*>(&n), 4);
+    rec.append(f.data(), f.size());
+  }
+  template <class T>
+  static std::string_view pod(const T& v) { return std::string_view(reinterpret_cast<const char*>(&v), sizeof(T)); }
+
+  void append(char kind, const std::vector<std::string_view>& fields) {
+    if (fd_ < 0) return;
+    std::string rec;
+    rec.resize(5);
+    rec[4] = kind;
+    for (auto f : fields) put_field(rec, f);
+    uint32_t total = (uint32_t)rec.size();
+    std::memcpy(&rec[0], &total, 4);
+    write_all(rec);
+  }
+
+  // Replays every complete record; a torn tail (crash mid-write) is truncated.
+  void replay(const std::function<void(char, std::vector<std::string_view>&)>& fn) {
+    if (fd_ < 0) return;
+    std::string data;
+    data.resize(bytes_);
+    size_t off = 0;
+    while (off < data.size()) {
+      ssize_t r = ::pread(fd_, &data[off], data.size() - off, (off_t)off);
+      if (r <= 0) break;
+      off += (size_t)r;
+    }
+    size_t pos = 0;
+    std::vector<std::string_view> fields;
+    while (pos + 5 <= off) {
+      uint32_t total;
+      std::memcpy(&total, &data[pos], 4);
+      if (total < 5 || pos + total > off) break;
+      char kind = data[pos + 4];
+      fields.clear();
+      size_t p = pos + 5, end = pos + total;
+      bool ok = true;
+      while (p < end) {
+        if (p + 4 > end) { ok = false; break; }
+        uint32_t n;
+        std::memcpy(&n, &data[p], 4);
+        p += 4;
+        if (p + n > end) { ok = false; break; }
+        fields.emplace_back(&data[p], n);
+        p += n;
+      }
+      if (!ok) break;
+      fn(kind, fields);
+      pos = end;
+    }
+    if (pos < bytes_) {
+      if (::ftruncate(fd_, (off_t)pos) == 0) bytes_ = pos;
+    }
+  }
+
+  // Atomically replace the log with the records produced by `writer`.
+  void rewrite(const std::function<void(AppLog&)>& writer) {
+    if (fd_ < 0) return;
+    std::string tmp = path_ + ".compact";
+    AppLog out;
+    ::unlink(tmp.c_str());
+    out.open(tmp, 0);
+    writer(out);
+    ::fdatasync(out.fd_);
+    out.close();
+    if (::rename(tmp.c_str(), path_.c_str()) != 0) throw std::runtime_error("log compaction rename failed");
+    close();
+    open(path_, fsync_);
+  }
+
+  void sync() { if (fd_ >= 0) ::fdatasync(fd_); }
+
+ private:
+  void write_all(const std::string& rec) {
+    size_t off = 0;
+    while (off < rec.size()) {
+      ssize_t w = ::write(fd_, rec.data() + off, rec.size() - off);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        throw std::runtime_error(std::string("log write failed: ") + std::strerror(errno));
+      }
+      off += (size_t)w;
+    }
+    bytes_ += rec.size();
+    if (fsync_ == 1) ::fdatasync(fd_);
+  }
+
+  int fd_ = -1;
+  int fsync_ = 0;
+  uint64_t bytes_ = 0;
+  std::string path_;
+};
+
+}  // namespace tt

@@ -1,0 +1,550 @@
+// Native document store: the state-store engine behind `state.azure.cosmosdb`,
+// `state.redis` and `state.in-memory` components.
+//
+// Capabilities mirrored from what the reference relies on:
+//   * key -> JSON document with a monotonically increasing ETag per write;
+//   * first-write / last-write optimistic concurrency (ETag mismatch -> EtagMismatch);
+//   * TTL (Dapr `ttlInSeconds` metadata);
+//   * multi-key atomic transactions;
+//   * the state query API: filter EQ/NEQ/GT/GTE/LT/LTE/IN/AND/OR over JSON paths, multi-key
+//     sort, limit + continuation token (reference Services/TasksStoreManager.cs:54-69, 104-139);
+//   * automatic secondary hash indexes on equality paths (Cosmos indexes every path by
+//     default) so `EQ taskCreatedBy` / `EQ taskDueDate` are O(matches), not O(collection);
+//   * durability through an append-only log with online compaction.
+#pragma once
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "applog.hpp"
+#include "json.hpp"
+
+namespace tt {
+
+struct EtagMismatch : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct QueryError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+inline int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+struct Filter {
+  enum Op { ALL, EQ, NEQ, GT, GTE, LT, LTE, IN, AND, OR } op = ALL;
+  std::string path;
+  Value val;
+  std::vector<Value> vals;
+  std::vector<Filter> kids;
+};
+
+inline bool ieq(std::string_view a, const char* b) {
+  size_t n = std::strlen(b);
+  if (a.size() != n) return false;
+  for (size_t i = 0; i < n; ++i)
+    if (std::toupper((unsigned char)a[i]) != b[i]) return false;
+  return true;
+}
+
+inline Filter compile_filter(const Value& f) {
+  Filter out;
+  if (f.t == Value::Null) return out;
+  if (f.t != Value::Object) throw QueryError("filter must be an object");
+  if (f.keys.empty()) return out;
+  if (f.keys.size() != 1) throw QueryError("filter object must have exactly one operator");
+  const std::string& op = f.keys[0];
+  const Value& arg = f.items[0];
+  if (ieq(op, "AND") || ieq(op, "OR")) {
+    out.op = ieq(op, "AND") ? Filter::AND : Filter::OR;
+    if (arg.t != Value::Array || arg.items.empty()) throw QueryError(op + " expects a non-empty array");
+    for (auto& k : arg.items) out.kids.push_back(compile_filter(k));
+    return out;
+  }
+  static const std::pair<const char*, Filter::Op> table[] = {
+      {"EQ", Filter::EQ}, {"NEQ", Filter::NEQ}, {"GT", Filter::GT}, {"GTE", Filter::GTE},
+      {"LT", Filter::LT}, {"LTE", Filter::LTE}, {"IN", Filter::IN}};
+  bool found = false;
+  for (auto& [name, code] : table)
+    if (ieq(op, name)) { out.op = code; found = true; }
+  if (!found) throw QueryError("unsupported filter operator " + op);
+  if (arg.t != Value::Object || arg.keys.size() != 1) throw QueryError(op + " expects {\"path\": value}");
+  out.path = arg.keys[0];
+  if (out.op == Filter::IN) {
+    if (arg.items[0].t != Value::Array) throw QueryError("IN expects an array of values");
+    out.vals = arg.items[0].items;
+  } else {
+    out.val = arg.items[0];
+  }
+  return out;
+}
+
+inline bool eval_filter(const Filter& f, const Value& doc) {
+  switch (f.op) {
+    case Filter::ALL: return true;
+    case Filter::AND:
+      for (auto& k : f.kids) if (!eval_filter(k, doc)) return false;
+      return true;
+    case Filter::OR:
+      for (auto& k : f.kids) if (eval_filter(k, doc)) return true;
+      return false;
+    case Filter::IN: {
+      const Value* v = doc.path(f.path);
+      if (!v) return false;
+      for (auto& x : f.vals) if (equals(*v, x)) return true;
+      return false;
+    }
+    default: {
+      const Value* v = doc.path(f.path);
+      if (!v) return f.op == Filter::NEQ;
+      if (f.op == Filter::EQ) return equals(*v, f.val);
+      if (f.op == Filter::NEQ) return !equals(*v, f.val);
+      if (v->t != f.val.t) return false;  // ranges only compare like types
+      int c = compare(*v, f.val);
+      switch (f.op) {
+        case Filter::GT: return c > 0;
+        case Filter::GTE: return c >= 0;
+        case Filter::LT: return c < 0;
+        case Filter::LTE: return c <= 0;
+        default: return false;
+      }
+    }
+  }
+}
+
+struct SortKey {
+  std::string path;
+  bool desc = false;
+};
+
+struct Doc {
+  std::string value;
+  Value parsed;
+  uint64_t etag = 0;
+  uint64_t seq = 0;
+  int64_t expire_ms = 0;
+};
+
+struct TxOp {
+  bool is_delete = false;
+  std::string key;
+  std::string value;
+  std::optional<std::string> etag;
+  bool first_write = false;
+  int64_t ttl_ms = 0;
+};
+
+class DocStore {
+ public:
+  explicit DocStore(const std::string& path = "", int fsync_mode = 0, size_t index_threshold = 256)
+      : index_threshold_(index_threshold) {
+    if (!path.empty()) {
+      log_.open(path, fsync_mode);
+      log_.replay([this](char kind, std::vector<std::string_view>& f) { apply_log(kind, f); });
+    }
+  }
+
+  // ---------------------------------------------------------------- writes
+  std::string set(const std::string& key, const std::string& value, const std::optional<std::string>& etag,
+                  bool first_write, int64_t ttl_ms) {
+    Value parsed = parse(value);  // validate before taking the lock
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = now_ms();
+    check_etag(key, etag, first_write, now);
+    uint64_t e = put(key, value, std::move(parsed), ttl_ms > 0 ? now + ttl_ms : 0);
+    log_put(key, value, e, docs_[key].expire_ms);
+    maybe_compact();
+    return std::to_string(e);
+  }
+
+  std::optional<std::pair<std::string, std::string>> get(const std::string& key) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = docs_.find(key);
+    if (it == docs_.end()) return std::nullopt;
+    if (expired(it->second, now_ms())) { erase_locked(key, true); return std::nullopt; }
+    return std::make_pair(it->second.value, std::to_string(it->second.etag));
+  }
+
+  bool del(const std::string& key, const std::optional<std::string>& etag) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = docs_.find(key);
+    int64_t now = now_ms();
+    if (it == docs_.end() || expired(it->second, now)) {
+      if (etag && !etag->empty()) throw EtagMismatch("possible etag mismatch: key not found");
+      return false;
+    }
+    if (etag && !etag->empty() && *etag != std::to_string(it->second.etag)) throw EtagMismatch("possible etag mismatch");
+    erase_locked(key, true);
+    maybe_compact();
+    return true;
+  }
+
+  // All-or-nothing: every precondition is checked before any mutation is applied.
+  void transact(const std::vector<TxOp>& ops) {
+    std::vector<Value> parsed(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i)
+      if (!ops[i].is_delete) parsed[i] = parse(ops[i].value);
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = now_ms();
+    for (auto& op : ops) {
+      if (op.is_delete) {
+        if (op.etag && !op.etag->empty()) {
+          auto it = docs_.find(op.key);
+          if (it == docs_.end() || *op.etag != std::to_string(it->second.etag)) throw EtagMismatch("possible etag mismatch in transaction");
+        }
+      } else {
+        check_etag(op.key, op.etag, op.first_write, now);
+      }
+    }
+    log_.append('T', {std::string_view("begin")});
+    for (size_t i = 0; i < ops.size(); ++i) {
+      auto& op = ops[i];
+      if (op.is_delete) {
+        if (docs_.count(op.key)) erase_locked(op.key, true);
+      } else {
+        uint64_t e = put(op.key, op.value, std::move(parsed[i]), op.ttl_ms > 0 ? now + op.ttl_ms : 0);
+        log_put(op.key, op.value, e, docs_[op.key].expire_ms);
+      }
+    }
+    log_.append('T', {std::string_view("commit")});
+    maybe_compact();
+  }
+
+  // ---------------------------------------------------------------- query
+  // Returns {"results":[{"key","data","etag"}...],"token":"..."} as JSON text.
+  std::string query(const std::string& query_json, const std::string& prefix) {
+    Value q = parse(query_json.empty() ? std::string("{}") : query_json);
+    if (q.t != Value::Object) throw QueryError("query must be a JSON object");
+    Filter f;
+    if (auto* fv = q.get_ci("filter")) f = compile_filter(*fv);
+    std::vector<SortKey> sort;
+    if (auto* sv = q.get_ci("sort")) {
+      if (sv->t != Value::Array) throw QueryError("sort must be an array");
+      for (auto& s : sv->items) {
+        const Value* k = s.get_ci("key");
+        if (!k || k->t != Value::String) throw QueryError("sort entry needs a string key");
+        SortKey sk{k->s, false};
+        if (auto* o = s.get_ci("order")) sk.desc = o->t == Value::String && ieq(o->s, "DESC");
+        sort.push_back(sk);
+      }
+    }
+    size_t limit = 0, offset = 0;
+    if (auto* pv = q.get_ci("page")) {
+      if (auto* l = pv->get_ci("limit")) limit = l->t == Value::Number && l->n > 0 ? (size_t)l->n : 0;
+      if (auto* t = pv->get_ci("token")) {
+        if (t->t == Value::String && !t->s.empty()) offset = (size_t)std::strtoull(t->s.c_str(), nullptr, 10);
+      }
+    }
+
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = now_ms();
+    ensure_indexes(f);
+    std::vector<std::pair<const std::string*, const Doc*>> hits;
+    auto consider = [&](const std::string& key, const Doc& d) {
+      if (!prefix.empty() && key.compare(0, prefix.size(), prefix) != 0) return;
+      if (expired(d, now)) return;
+      if (!eval_filter(f, d.parsed)) return;
+      hits.emplace_back(&key, &d);
+    };
+    std::unordered_set<std::string> cand;
+    if (candidates(f, cand)) {
+      ++stats_indexed_queries_;
+      for (auto& k : cand) {
+        auto it = docs_.find(k);
+        if (it != docs_.end()) consider(it->first, it->second);
+      }
+    } else {
+      ++stats_scan_queries_;
+      for (auto& [k, d] : docs_) consider(k, d);
+    }
+    if (sort.empty()) {
+      std::sort(hits.begin(), hits.end(), [](auto& a, auto& b) { return a.second->seq < b.second->seq; });
+    } else {
+      static const Value kNull;
+      std::stable_sort(hits.begin(), hits.end(), [&](auto& a, auto& b) {
+        for (auto& sk : sort) {
+          const Value* x = a.second->parsed.path(sk.path);
+          const Value* y = b.second->parsed.path(sk.path);
+          int c = compare(x ? *x : kNull, y ? *y : kNull);
+          if (c) return sk.desc ? c > 0 : c < 0;
+        }
+        return a.second->seq < b.second->seq;
+      });
+    }
+    size_t begin = std::min(offset, hits.size());
+    size_t end = limit ? std::min(hits.size(), begin + limit) : hits.size();
+    std::string out = "{\"results\":[";
+    for (size_t i = begin; i < end; ++i) {
+      if (i > begin) out += ',';
+      out += "{\"key\":";
+      escape_to(out, std::string_view(*hits[i].first).substr(prefix.size()));
+      out += ",\"data\":";
+      out += hits[i].second->value;
+      out += ",\"etag\":\"";
+      out += std::to_string(hits[i].second->etag);
+      out += "\"}";
+    }
+    out += "]";
+    if (limit && end < hits.size()) {
+      out += ",\"token\":\"" + std::to_string(end) + "\"";
+    }
+    out += "}";
+    return out;
+  }
+
+  std::vector<std::string> keys(const std::string& prefix, size_t limit) {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::pair<uint64_t, std::string>> ks;
+    int64_t now = now_ms();
+    for (auto& [k, d] : docs_)
+      if ((prefix.empty() || k.compare(0, prefix.size(), prefix) == 0) && !expired(d, now)) ks.emplace_back(d.seq, k);
+    std::sort(ks.begin(), ks.end());
+    std::vector<std::string> out;
+    for (auto& p : ks) { if (limit && out.size() >= limit) break; out.push_back(p.second); }
+    return out;
+  }
+
+  // Column export for the GPU scan path: one (seq-ordered) row per live document whose key
+  // starts with `prefix`; returns keys and, per path, the raw JSON scalar values.
+  std::pair<std::vector<std::string>, std::vector<std::vector<std::string>>> export_columns(
+      const std::string& prefix, const std::vector<std::string>& paths) {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = now_ms();
+    std::vector<std::pair<uint64_t, const std::pair<const std::string, Doc>*>> rows;
+    for (auto& kv : docs_)
+      if ((prefix.empty() || kv.first.compare(0, prefix.size(), prefix) == 0) && !expired(kv.second, now))
+        rows.emplace_back(kv.second.seq, &kv);
+    std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    std::vector<std::string> ks;
+    std::vector<std::vector<std::string>> cols(paths.size());
+    ks.reserve(rows.size());
+    for (auto& c : cols) c.reserve(rows.size());
+    for (auto& r : rows) {
+      ks.push_back(r.second->first);
+      for (size_t i = 0; i < paths.size(); ++i) {
+        const Value* v = r.second->second.parsed.path(paths[i]);
+        cols[i].push_back(v ? dump(*v) : std::string("null"));
+      }
+    }
+    return {std::move(ks), std::move(cols)};
+  }
+
+  size_t size() {
+    std::lock_guard<std::mutex> g(mu_);
+    return docs_.size();
+  }
+
+  void compact() {
+    std::lock_guard<std::mutex> g(mu_);
+    compact_locked();
+  }
+
+  void sync() { std::lock_guard<std::mutex> g(mu_); log_.sync(); }
+
+  std::unordered_map<std::string, uint64_t> stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    return {{"docs", docs_.size()}, {"live_bytes", live_bytes_}, {"log_bytes", log_.bytes()},
+            {"indexes", indexes_.size()}, {"indexed_queries", stats_indexed_queries_},
+            {"scan_queries", stats_scan_queries_}, {"etag", etag_}};
+  }
+
+  std::vector<std::string> indexed_paths() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::string> out;
+    for (auto& [p, _] : indexes_) out.push_back(p);
+    std::sort(out.begin(), out.end());
+    return out;
+  }
+
+ private:
+  using Index = std::unordered_map<std::string, std::unordered_set<std::string>>;
+
+  static bool expired(const Doc& d, int64_t now) { return d.expire_ms && d.expire_ms <= now; }
+
+  void check_etag(const std::string& key, const std::optional<std::string>& etag, bool first_write, int64_t now) {
+    auto it = docs_.find(key);
+    bool exists = it != docs_.end() && !expired(it->second, now);
+    if (etag && !etag->empty()) {
+      if (!exists || *etag != std::to_string(it->second.etag)) throw EtagMismatch("possible etag mismatch");
+    } else if (first_write && exists) {
+      throw EtagMismatch("possible etag mismatch: first-write on existing key without etag");
+    }
+  }
+
+  uint64_t put(const std::string& key, const std::string& value, Value parsed, int64_t expire_ms) {
+    auto it = docs_.find(key);
+    uint64_t e = ++etag_;
+    if (it == docs_.end()) {
+      Doc d;
+      d.value = value;
+      d.parsed = std::move(parsed);
+      d.etag = e;
+      d.seq = ++seq_;
+      d.expire_ms = expire_ms;
+      live_bytes_ += key.size() + value.size();
+      index_add(key, d.parsed);
+      docs_.emplace(key, std::move(d));
+    } else {
+      index_remove(key, it->second.parsed);
+      live_bytes_ += value.size();
+      live_bytes_ -= it->second.value.size();
+      it->second.value = value;
+      it->second.parsed = std::move(parsed);
+      it->second.etag = e;
+      it->second.expire_ms = expire_ms;
+      index_add(key, it->second.parsed);
+    }
+    return e;
+  }
+
+  void erase_locked(const std::string& key, bool log) {
+    auto it = docs_.find(key);
+    if (it == docs_.end()) return;
+    index_remove(key, it->second.parsed);
+    live_bytes_ -= key.size() + it->second.value.size();
+    docs_.erase(it);
+    if (log) log_.append('D', {key});
+  }
+
+  void log_put(const std::string& key, const std::string& value, uint64_t etag, int64_t expire) {
+    if (!log_.is_open()) return;
+    log_.append('P', {key, value, AppLog::pod(etag), AppLog::pod(expire)});
+  }
+
+  void apply_log(char kind, std::vector<std::string_view>& f) {
+    if (kind == 'P' && f.size() == 4) {
+      std::string key(f[0]), value(f[1]);
+      uint64_t e;
+      int64_t exp;
+      std::memcpy(&e, f[2].data(), 8);
+      std::memcpy(&exp, f[3].data(), 8);
+      Value parsed;
+      try { parsed = parse(value); } catch (...) { return; }
+      put(key, value, std::move(parsed), exp);
+      docs_[key].etag = e;
+      etag_ = std::max(etag_, e);
+    } else if (kind == 'D' && f.size() == 1) {
+      erase_locked(std::string(f[0]), false);
+    }
+  }
+
+  void maybe_compact() {
+    if (!log_.is_open()) return;
+    uint64_t live = live_bytes_ + docs_.size() * 40;
+    if (log_.bytes() > (1u << 20) && log_.bytes() > 4 * live) compact_locked();
+  }
+
+  void compact_locked() {
+    if (!log_.is_open()) return;
+    std::vector<std::pair<uint64_t, const std::pair<const std::string, Doc>*>> rows;
+    for (auto& kv : docs_) rows.emplace_back(kv.second.seq, &kv);
+    std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    log_.rewrite([&](AppLog& out) {
+      for (auto& r : rows)
+        out.append('P', {r.second->first, r.second->second.value, AppLog::pod(r.second->second.etag),
+                         AppLog::pod(r.second->second.expire_ms)});
+    });
+  }
+
+  // ----------------------------------------------------------- secondary indexes
+  void collect_eq_paths(const Filter& f, std::vector<std::string>& out) {
+    if (f.op == Filter::EQ || f.op == Filter::IN) out.push_back(f.path);
+    for (auto& k : f.kids) collect_eq_paths(k, out);
+  }
+
+  void ensure_indexes(const Filter& f) {
+    if (docs_.size() < index_threshold_) return;
+    std::vector<std::string> paths;
+    collect_eq_paths(f, paths);
+    for (auto& p : paths) {
+      if (indexes_.count(p)) continue;
+      Index& idx = indexes_[p];
+      for (auto& [k, d] : docs_) {
+        const Value* v = d.parsed.path(p);
+        if (v && v->t != Value::Array && v->t != Value::Object) idx[index_key(*v)].insert(k);
+      }
+    }
+  }
+
+  void index_add(const std::string& key, const Value& doc) {
+    for (auto& [p, idx] : indexes_) {
+      const Value* v = doc.path(p);
+      if (v && v->t != Value::Array && v->t != Value::Object) idx[index_key(*v)].insert(key);
+    }
+  }
+
+  void index_remove(const std::string& key, const Value& doc) {
+    for (auto& [p, idx] : indexes_) {
+      const Value* v = doc.path(p);
+      if (!v || v->t == Value::Array || v->t == Value::Object) continue;
+      auto it = idx.find(index_key(*v));
+      if (it != idx.end()) {
+        it->second.erase(key);
+        if (it->second.empty()) idx.erase(it);
+      }
+    }
+  }
+
+  // Candidate key set from indexes; false = needs a full scan.
+  bool candidates(const Filter& f, std::unordered_set<std::string>& out) {
+    switch (f.op) {
+      case Filter::EQ: {
+        auto ix = indexes_.find(f.path);
+        if (ix == indexes_.end() || f.val.t == Value::Array || f.val.t == Value::Object) return false;
+        auto it = ix->second.find(index_key(f.val));
+        if (it != ix->second.end()) out.insert(it->second.begin(), it->second.end());
+        return true;
+      }
+      case Filter::IN: {
+        auto ix = indexes_.find(f.path);
+        if (ix == indexes_.end()) return false;
+        for (auto& v : f.vals) {
+          if (v.t == Value::Array || v.t == Value::Object) return false;
+          auto it = ix->second.find(index_key(v));
+          if (it != ix->second.end()) out.insert(it->second.begin(), it->second.end());
+        }
+        return true;
+      }
+      case Filter::AND: {
+        bool any = false;
+        std::unordered_set<std::string> best;
+        for (auto& k : f.kids) {
+          std::unordered_set<std::string> c;
+          if (candidates(k, c) && (!any || c.size() < best.size())) { best.swap(c); any = true; }
+        }
+        if (any) out.insert(best.begin(), best.end());
+        return any;
+      }
+      case Filter::OR: {
+        std::unordered_set<std::string> acc;
+        for (auto& k : f.kids)
+          if (!candidates(k, acc)) return false;
+        out.insert(acc.begin(), acc.end());
+        return true;
+      }
+      default: return false;
+    }
+  }
+
+  std::mutex mu_;
+  std::unordered_map<std::string, Doc> docs_;
+  std::unordered_map<std::string, Index> indexes_;
+  AppLog log_;
+  uint64_t etag_ = 0;
+  uint64_t seq_ = 0;
+  uint64_t live_bytes_ = 0;
+  uint64_t stats_indexed_queries_ = 0;
+  uint64_t stats_scan_queries_ = 0;
+  size_t index_threshold_;
+};
+
+}  // namespace tt

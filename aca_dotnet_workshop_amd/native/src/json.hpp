@@ -1,0 +1,321 @@
+// Compact JSON DOM + parser + serializer used by the native document store and broker.
+//
+// Objects keep insertion order (two parallel vectors) so stored documents round-trip
+// byte-for-byte through the query path.  Numbers are doubles (JSON semantics).
+#pragma once
+
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace tt {
+
+struct Value {
+  enum Type : uint8_t { Null = 0, Bool = 1, Number = 2, String = 3, Array = 4, Object = 5 };
+  Type t = Null;
+  bool b = false;
+  double n = 0.0;
+  std::string s;                 // String payload
+  std::vector<Value> items;      // Array items / Object values
+  std::vector<std::string> keys; // Object keys (parallel to items)
+
+  static Value null() { return Value(); }
+  static Value boolean(bool v) { Value x; x.t = Bool; x.b = v; return x; }
+  static Value number(double v) { Value x; x.t = Number; x.n = v; return x; }
+  static Value string(std::string v) { Value x; x.t = String; x.s = std::move(v); return x; }
+
+  const Value* get(std::string_view key) const {
+    if (t != Object) return nullptr;
+    for (size_t i = 0; i < keys.size(); ++i)
+      if (keys[i] == key) return &items[i];
+    return nullptr;
+  }
+  // case-insensitive fallback (camelCase vs PascalCase producers)
+  const Value* get_ci(std::string_view key) const {
+    if (t != Object) return nullptr;
+    if (auto* v = get(key)) return v;
+    for (size_t i = 0; i < keys.size(); ++i) {
+      const std::string& k = keys[i];
+      if (k.size() != key.size()) continue;
+      bool eq = true;
+      for (size_t j = 0; j < k.size() && eq; ++j) eq = std::tolower((unsigned char)k[j]) == std::tolower((unsigned char)key[j]);
+      if (eq) return &items[i];
+    }
+    return nullptr;
+  }
+  // Dotted path lookup ("a.b.c"); array indices allowed as numeric segments.
+  const Value* path(std::string_view p) const {
+    const Value* cur = this;
+    size_t pos = 0;
+    while (cur && pos <= p.size()) {
+      size_t dot = p.find('.', pos);
+      std::string_view seg = p.substr(pos, dot == std::string_view::npos ? std::string_view::npos : dot - pos);
+      if (cur->t == Object) {
+        cur = cur->get_ci(seg);
+      } else if (cur->t == Array) {
+        size_t idx = 0;
+        bool ok = !seg.empty();
+        for (char c : seg) { if (c < '0' || c > '9') { ok = false; break; } idx = idx * 10 + (c - '0'); }
+        cur = (ok && idx < cur->items.size()) ? &cur->items[idx] : nullptr;
+      } else {
+        return nullptr;
+      }
+      if (dot == std::string_view::npos) break;
+      pos = dot + 1;
+    }
+    return cur;
+  }
+};
+
+struct ParseError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class Parser {
+ public:
+  explicit Parser(std::string_view s) : p_(s.data()), e_(s.data() + s.size()) {}
+  Value parse() {
+    Value v = value(0);
+    ws();
+    if (p_ != e_) throw ParseError("trailing characters after JSON value");
+    return v;
+  }
+
+ private:
+  const char* p_;
+  const char* e_;
+
+  void ws() { while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_; }
+  [[noreturn]] void fail(const char* m) { throw ParseError(m); }
+
+  Value value(int depth) {
+    if (depth > 256) fail("JSON nesting too deep");
+    ws();
+    if (p_ >= e_) fail("unexpected end of JSON");
+    char c = *p_;
+    if (c == '{') return object(depth);
+    if (c == '[') return array(depth);
+    if (c == '"') { Value v; v.t = Value::String; v.s = str(); return v; }
+    if (c == 't') { lit("true"); return Value::boolean(true); }
+    if (c == 'f') { lit("false"); return Value::boolean(false); }
+    if (c == 'n') { lit("null"); return Value(); }
+    return num();
+  }
+  void lit(const char* w) {
+    size_t n = std::strlen(w);
+    if ((size_t)(e_ - p_) < n || std::memcmp(p_, w, n) != 0) fail("invalid literal");
+    p_ += n;
+  }
+  Value num() {
+    const char* s = p_;
+    if (p_ < e_ && (*p_ == '-' || *p_ == '+')) ++p_;
+    while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' || *p_ == '-' || *p_ == '+')) ++p_;
+    if (p_ == s) fail("invalid JSON token");
+    std::string tmp(s, p_);
+    char* end = nullptr;
+    double d = std::strtod(tmp.c_str(), &end);
+    if (end != tmp.c_str() + tmp.size()) fail("invalid number");
+    return Value::number(d);
+  }
+  static void utf8(std::string& out, uint32_t cp) {
+    if (cp < 0x80) out += (char)cp;
+    else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 0x3F)); }
+    else if (cp < 0x10000) { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+    else { out += (char)(0xF0 | (cp >> 18)); out += (char)(0x80 | ((cp >> 12) & 0x3F)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+  }
+  uint32_t hex4() {
+    if (e_ - p_ < 4) fail("bad \\u escape");
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+      char c = *p_++;
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= c - '0';
+      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+      else fail("bad hex digit");
+    }
+    return v;
+  }
+  std::string str() {
+    ++p_;  // opening quote
+    std::string out;
+    const char* run = p_;
+    while (true) {
+      if (p_ >= e_) fail("unterminated string");
+      char c = *p_;
+      if (c == '"') { out.append(run, p_); ++p_; return out; }
+      if (c == '\\') {
+        out.append(run, p_);
+        ++p_;
+        if (p_ >= e_) fail("bad escape");
+        char x = *p_++;
+        switch (x) {
+          case '"': out += '"'; break;
+          case '\\': out += '\\'; break;
+          case '/': out += '/'; break;
+          case 'b': out += '\b'; break;
+          case 'f': out += '\f'; break;
+          case 'n': out += '\n'; break;
+          case 'r': out += '\r'; break;
+          case 't': out += '\t'; break;
+          case 'u': {
+            uint32_t cp = hex4();
+            if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+              p_ += 2;
+              uint32_t lo = hex4();
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            }
+            utf8(out, cp);
+            break;
+          }
+          default: fail("bad escape");
+        }
+        run = p_;
+        continue;
+      }
+      ++p_;
+    }
+  }
+  Value array(int depth) {
+    ++p_;
+    Value v; v.t = Value::Array;
+    ws();
+    if (p_ < e_ && *p_ == ']') { ++p_; return v; }
+    while (true) {
+      v.items.push_back(value(depth + 1));
+      ws();
+      if (p_ >= e_) fail("unterminated array");
+      if (*p_ == ',') { ++p_; continue; }
+      if (*p_ == ']') { ++p_; return v; }
+      fail("expected , or ]");
+    }
+  }
+  Value object(int depth) {
+    ++p_;
+    Value v; v.t = Value::Object;
+    ws();
+    if (p_ < e_ && *p_ == '}') { ++p_; return v; }
+    while (true) {
+      ws();
+      if (p_ >= e_ || *p_ != '"') fail("expected object key");
+      v.keys.push_back(str());
+      ws();
+      if (p_ >= e_ || *p_ != ':') fail("expected :");
+      ++p_;
+      v.items.push_back(value(depth + 1));
+      ws();
+      if (p_ >= e_) fail("unterminated object");
+      if (*p_ == ',') { ++p_; continue; }
+      if (*p_ == '}') { ++p_; return v; }
+      fail("expected , or }");
+    }
+  }
+};
+
+inline Value parse(std::string_view s) { return Parser(s).parse(); }
+
+inline void escape_to(std::string& out, std::string_view s) {
+  out += '"';
+  for (unsigned char c : s) {
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      case '\b': out += "\\b"; break;
+      case '\f': out += "\\f"; break;
+      default:
+        if (c < 0x20) {
+          char buf[8];
+          std::snprintf(buf, sizeof buf, "\\u%04x", c);
+          out += buf;
+        } else {
+          out += (char)c;
+        }
+    }
+  }
+  out += '"';
+}
+
+inline void number_to(std::string& out, double d) {
+  if (std::isfinite(d) && d == std::floor(d) && std::fabs(d) < 9.007199254740992e15) {
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%lld", (long long)d);
+    out += buf;
+  } else if (!std::isfinite(d)) {
+    out += "null";
+  } else {
+    char buf[32];
+    std::snprintf(buf, sizeof buf, "%.17g", d);
+    out += buf;
+  }
+}
+
+inline void dump_to(std::string& out, const Value& v) {
+  switch (v.t) {
+    case Value::Null: out += "null"; break;
+    case Value::Bool: out += v.b ? "true" : "false"; break;
+    case Value::Number: number_to(out, v.n); break;
+    case Value::String: escape_to(out, v.s); break;
+    case Value::Array:
+      out += '[';
+      for (size_t i = 0; i < v.items.size(); ++i) { if (i) out += ','; dump_to(out, v.items[i]); }
+      out += ']';
+      break;
+    case Value::Object:
+      out += '{';
+      for (size_t i = 0; i < v.items.size(); ++i) {
+        if (i) out += ',';
+        escape_to(out, v.keys[i]);
+        out += ':';
+        dump_to(out, v.items[i]);
+      }
+      out += '}';
+      break;
+  }
+}
+
+inline std::string dump(const Value& v) { std::string o; dump_to(o, v); return o; }
+
+// Total order across JSON values: null < bool < number < string < array < object.
+inline int compare(const Value& a, const Value& b) {
+  if (a.t != b.t) return a.t < b.t ? -1 : 1;
+  switch (a.t) {
+    case Value::Null: return 0;
+    case Value::Bool: return (int)a.b - (int)b.b;
+    case Value::Number: return a.n < b.n ? -1 : (a.n > b.n ? 1 : 0);
+    case Value::String: { int c = a.s.compare(b.s); return c < 0 ? -1 : (c > 0 ? 1 : 0); }
+    case Value::Array: {
+      size_t n = std::min(a.items.size(), b.items.size());
+      for (size_t i = 0; i < n; ++i) { int c = compare(a.items[i], b.items[i]); if (c) return c; }
+      return a.items.size() < b.items.size() ? -1 : (a.items.size() > b.items.size() ? 1 : 0);
+    }
+    case Value::Object: { std::string x = dump(a), y = dump(b); int c = x.compare(y); return c < 0 ? -1 : (c > 0 ? 1 : 0); }
+  }
+  return 0;
+}
+
+inline bool equals(const Value& a, const Value& b) { return compare(a, b) == 0; }
+
+// Canonical hash-index key for a scalar value.
+inline std::string index_key(const Value& v) {
+  std::string k;
+  k += (char)('0' + v.t);
+  switch (v.t) {
+    case Value::Bool: k += v.b ? '1' : '0'; break;
+    case Value::Number: number_to(k, v.n); break;
+    case Value::String: k += v.s; break;
+    case Value::Null: break;
+    default: dump_to(k, v); break;
+  }
+  return k;
+}
+
+}  // namespace tt

@@ -1,0 +1,143 @@
+// Python bindings for the native state-store and broker engines (`_ttnative`).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "broker.hpp"
+#include "docstore.hpp"
+
+namespace py = pybind11;
+using namespace tt;
+
+PYBIND11_MODULE(_ttnative, m) {
+  m.doc() = "Native document store + message broker engines (C++17)";
+
+  static py::exception<EtagMismatch> etag_exc(m, "EtagMismatch");
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const EtagMismatch& e) {
+      PyErr_SetString(etag_exc.ptr(), e.what());
+    } catch (const QueryError& e) {
+      PyErr_SetString(PyExc_ValueError, e.what());
+    } catch (const ParseError& e) {
+      PyErr_SetString(PyExc_ValueError, (std::string("invalid JSON: ") + e.what()).c_str());
+    }
+  });
+
+  py::class_<TxOp>(m, "TxOp")
+      .def(py::init([](bool is_delete, std::string key, std::string value, std::optional<std::string> etag,
+                       bool first_write, int64_t ttl_ms) {
+             TxOp op;
+             op.is_delete = is_delete;
+             op.key = std::move(key);
+             op.value = std::move(value);
+             op.etag = std::move(etag);
+             op.first_write = first_write;
+             op.ttl_ms = ttl_ms;
+             return op;
+           }),
+           py::arg("is_delete"), py::arg("key"), py::arg("value") = "", py::arg("etag") = std::nullopt,
+           py::arg("first_write") = false, py::arg("ttl_ms") = 0);
+
+  py::class_<DocStore>(m, "DocStore")
+      .def(py::init<const std::string&, int, size_t>(), py::arg("path") = "", py::arg("fsync_mode") = 0,
+           py::arg("index_threshold") = 256)
+      .def("set", &DocStore::set, py::arg("key"), py::arg("value"), py::arg("etag") = std::nullopt,
+           py::arg("first_write") = false, py::arg("ttl_ms") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("get", &DocStore::get, py::arg("key"))
+      .def("delete", &DocStore::del, py::arg("key"), py::arg("etag") = std::nullopt)
+      .def("transact", &DocStore::transact, py::arg("ops"), py::call_guard<py::gil_scoped_release>())
+      .def("query", &DocStore::query, py::arg("query"), py::arg("prefix") = "",
+           py::call_guard<py::gil_scoped_release>())
+      .def("keys", &DocStore::keys, py::arg("prefix") = "", py::arg("limit") = 0)
+      .def("export_columns", &DocStore::export_columns, py::arg("prefix"), py::arg("paths"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("size", &DocStore::size)
+      .def("__len__", &DocStore::size)
+      .def("compact", &DocStore::compact)
+      .def("sync", &DocStore::sync)
+      .def("stats", &DocStore::stats)
+      .def("indexed_paths", &DocStore::indexed_paths);
+
+  py::class_<QueueOptions>(m, "QueueOptions")
+      .def(py::init([](int64_t lock_ms, uint32_t max_delivery, int64_t default_ttl_ms, bool dead_letter_on_expiry) {
+             QueueOptions o;
+             o.lock_ms = lock_ms;
+             o.max_delivery = max_delivery;
+             o.default_ttl_ms = default_ttl_ms;
+             o.dead_letter_on_expiry = dead_letter_on_expiry;
+             return o;
+           }),
+           py::arg("lock_ms") = 60000, py::arg("max_delivery") = 10, py::arg("default_ttl_ms") = 0,
+           py::arg("dead_letter_on_expiry") = false)
+      .def_readwrite("lock_ms", &QueueOptions::lock_ms)
+      .def_readwrite("max_delivery", &QueueOptions::max_delivery)
+      .def_readwrite("default_ttl_ms", &QueueOptions::default_ttl_ms)
+      .def_readwrite("dead_letter_on_expiry", &QueueOptions::dead_letter_on_expiry);
+
+  py::class_<Received>(m, "Received")
+      .def_readonly("lock_token", &Received::lock_token)
+      .def_readonly("seq", &Received::seq)
+      .def_readonly("id", &Received::id)
+      .def_property_readonly("body", [](const Received& r) { return py::bytes(r.body); })
+      .def_readonly("content_type", &Received::content_type)
+      .def_readonly("props", &Received::props)
+      .def_readonly("delivery_count", &Received::delivery_count)
+      .def_readonly("enqueued_ms", &Received::enqueued_wall);
+
+  py::class_<Broker>(m, "Broker")
+      .def(py::init<const std::string&, int>(), py::arg("path") = "", py::arg("fsync_mode") = 0)
+      .def("create_queue", &Broker::create_queue, py::arg("name"), py::arg("options") = QueueOptions())
+      .def("create_topic", &Broker::create_topic)
+      .def("create_subscription", &Broker::create_subscription, py::arg("topic"), py::arg("subscription"),
+           py::arg("options") = QueueOptions())
+      .def("delete_entity", &Broker::delete_entity)
+      .def("subscriptions", &Broker::subscriptions)
+      .def("entities", &Broker::entities)
+      .def("publish",
+           [](Broker& b, const std::string& topic, py::bytes body, const std::string& ctype, const std::string& props,
+              const std::string& id, int64_t ttl_ms, int64_t delay_ms) {
+             std::string s = body;
+             py::gil_scoped_release r;
+             return b.publish(topic, s, ctype, props, id, ttl_ms, delay_ms);
+           },
+           py::arg("topic"), py::arg("body"), py::arg("content_type") = "application/json", py::arg("props") = "{}",
+           py::arg("id") = "", py::arg("ttl_ms") = 0, py::arg("delay_ms") = 0)
+      .def("send",
+           [](Broker& b, const std::string& q, py::bytes body, const std::string& ctype, const std::string& props,
+              const std::string& id, int64_t ttl_ms, int64_t delay_ms) {
+             std::string s = body;
+             py::gil_scoped_release r;
+             return b.send(q, s, ctype, props, id, ttl_ms, delay_ms);
+           },
+           py::arg("queue"), py::arg("body"), py::arg("content_type") = "application/json", py::arg("props") = "{}",
+           py::arg("id") = "", py::arg("ttl_ms") = 0, py::arg("delay_ms") = 0)
+      .def("receive", &Broker::receive, py::arg("path"), py::arg("max_messages") = 1, py::arg("lock_ms") = 0)
+      .def("complete", &Broker::complete)
+      .def("abandon", &Broker::abandon, py::arg("path"), py::arg("token"), py::arg("delay_ms") = 0)
+      .def("dead_letter", &Broker::dead_letter, py::arg("path"), py::arg("token"), py::arg("reason") = "")
+      .def("renew", &Broker::renew, py::arg("path"), py::arg("token"), py::arg("lock_ms") = 0)
+      .def("drain_dead_letters",
+           [](Broker& b, const std::string& path, size_t max) {
+             py::list out;
+             for (auto& [seq, id, body, reason, dc] : b.drain_dead_letters(path, max))
+               out.append(py::make_tuple(seq, id, py::bytes(body), reason, dc));
+             return out;
+           },
+           py::arg("path"), py::arg("max") = 100)
+      .def("counts",
+           [](Broker& b, const std::string& path) {
+             auto [a, s, l, d, e, c, r] = b.counts(path);
+             py::dict out;
+             out["active"] = a;
+             out["scheduled"] = s;
+             out["locked"] = l;
+             out["dead_letter"] = d;
+             out["enqueued"] = e;
+             out["completed"] = c;
+             out["received"] = r;
+             return out;
+           })
+      .def("purge", &Broker::purge)
+      .def("total_published", &Broker::total_published);
+}
