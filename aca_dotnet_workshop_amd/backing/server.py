@@ -1,0 +1,644 @@
+"""Backing-services emulator: one process standing in for the cloud services the
+reference's Dapr components talk to:
+
+============================  =================================  ==========================================
+reference service             component type(s)                  emulated here by
+============================  =================================  ==========================================
+Cosmos DB (SQL API)           state.azure.cosmosdb               ``/cosmos``  -> native ``DocStore``
+Redis (``dapr init``)          state.redis, pubsub.redis          ``/cosmos`` + ``/servicebus`` namespaces ``redis-*``
+Service Bus topics/subs        pubsub.azure.servicebus(.topics)   ``/servicebus`` -> native ``Broker``
+Storage Queue                  bindings.azure.storagequeues       ``/storage/.../queues`` -> native ``Broker``
+Blob Storage                   bindings.azure.blobstorage         ``/storage/.../blobs`` -> files
+Key Vault                      secretstores.azure.keyvault        ``/keyvault``
+SendGrid                       bindings.twilio.sendgrid           ``/sendgrid`` -> outbox (JSONL)
+============================  =================================  ==========================================
+
+Long-poll receive (``waitMs``) gives push-like latency without busy polling.  All state
+is persisted under ``--data-dir`` when given (append-only logs + files), so restarting
+the emulator keeps tasks, queued messages, blobs and secrets.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import base64
+import json
+import logging
+import os
+import re
+import tempfile
+import time
+from pathlib import Path
+from typing import Any
+
+from .. import native
+from ..telemetry import configure, configure_logging
+from ..web.app import WebApp
+from ..web.http import HTTPError, Request, Response, empty, json_response, problem
+from .auth import AccessPolicy
+
+log = logging.getLogger("backing")
+_SAFE = re.compile(r"[^A-Za-z0-9._-]")
+
+
+def _safe(name: str) -> str:
+    return _SAFE.sub("_", name)
+
+
+class Waiters:
+    """Per-entity wake-ups for long-poll receivers (replace-on-notify events)."""
+
+    def __init__(self) -> None:
+        self._ev: dict[str, asyncio.Event] = {}
+
+    def notify(self, key: str) -> None:
+        ev = self._ev.pop(key, None)
+        if ev is not None:
+            ev.set()
+
+    async def wait(self, key: str, timeout: float) -> None:
+        ev = self._ev.get(key)
+        if ev is None:
+            ev = self._ev[key] = asyncio.Event()
+        try:
+            await asyncio.wait_for(ev.wait(), timeout)
+        except asyncio.TimeoutError:
+            pass
+
+
+def _encode_body(body: bytes) -> dict[str, str]:
+    try:
+        return {"body": body.decode("utf-8")}
+    except UnicodeDecodeError:
+        return {"bodyB64": base64.b64encode(body).decode()}
+
+
+def _decode_body(entry: dict[str, Any]) -> bytes:
+    if "bodyB64" in entry:
+        return base64.b64decode(entry["bodyB64"])
+    b = entry.get("body", "")
+    if isinstance(b, str):
+        return b.encode()
+    return json.dumps(b).encode()
+
+
+class BackingServices:
+    def __init__(self, data_dir: str | None = None, policy: AccessPolicy | None = None, fsync: int = 0) -> None:
+        self.N = native.load()
+        self.data_dir = Path(data_dir) if data_dir else None
+        self._tmp = None
+        if self.data_dir is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="tt-backing-")
+            self.blob_root = Path(self._tmp.name) / "blobs"
+        else:
+            self.data_dir.mkdir(parents=True, exist_ok=True)
+            self.blob_root = self.data_dir / "storage"
+        self.policy = policy or AccessPolicy()
+        self.fsync = fsync
+        self.stores: dict[tuple[str, str, str], Any] = {}
+        self.brokers: dict[str, Any] = {}
+        self.waiters = Waiters()
+        self.vaults: dict[str, dict[str, str]] = {}
+        self.outbox: list[dict[str, Any]] = []
+        self._load_vaults()
+
+    # -- engines ---------------------------------------------------------------
+    def _path(self, *parts: str) -> str:
+        if self.data_dir is None:
+            return ""
+        p = self.data_dir.joinpath(*[_safe(x) for x in parts])
+        p.parent.mkdir(parents=True, exist_ok=True)
+        return str(p)
+
+    def store(self, account: str, db: str, coll: str):
+        key = (account, db, coll)
+        s = self.stores.get(key)
+        if s is None:
+            s = self.stores[key] = self.N.DocStore(self._path("cosmos", account, db, coll + ".log"), self.fsync)
+        return s
+
+    def broker(self, ns: str):
+        b = self.brokers.get(ns)
+        if b is None:
+            b = self.brokers[ns] = self.N.Broker(self._path("servicebus", ns + ".log"), self.fsync)
+        return b
+
+    def _load_vaults(self) -> None:
+        if self.data_dir is None:
+            return
+        f = self.data_dir / "keyvault.json"
+        if f.exists():
+            self.vaults = json.loads(f.read_text())
+        ob = self.data_dir / "sendgrid-outbox.jsonl"
+        if ob.exists():
+            self.outbox = [json.loads(x) for x in ob.read_text().splitlines() if x.strip()]
+
+    def _save_vaults(self) -> None:
+        if self.data_dir is None:
+            return
+        tmp = self.data_dir / "keyvault.json.tmp"
+        tmp.write_text(json.dumps(self.vaults))
+        os.replace(tmp, self.data_dir / "keyvault.json")
+
+    # -- auth ------------------------------------------------------------------
+    def authorize(self, req: Request, action: str, scope: str) -> None:
+        ident = req.headers.get("x-tt-identity")
+        key = req.headers.get("x-tt-key")
+        if not self.policy.check(action, scope, ident, key):
+            raise HTTPError(403, detail=f"{ident or 'anonymous'} is not authorized to perform {action} on {scope}")
+
+    # -- app -------------------------------------------------------------------
+    def build_app(self) -> WebApp:
+        app = WebApp("backing-services")
+        self._cosmos_routes(app)
+        self._servicebus_routes(app)
+        self._storage_routes(app)
+        self._keyvault_routes(app)
+        self._sendgrid_routes(app)
+        self._admin_routes(app)
+        return app
+
+    # ---------------------------------------------------------------- cosmos
+    def _cosmos_routes(self, app: WebApp) -> None:
+        base = "/cosmos/{account}/{db}/{coll}"
+
+        def st(req: Request, action: str):
+            p = req.path_params
+            self.authorize(req, action, f"cosmos/{p['account']}")
+            return self.store(p["account"], p["db"], p["coll"])
+
+        async def put_doc(req: Request) -> Response:
+            s = st(req, "cosmos.write")
+            etag = req.headers.get("if-match") or None
+            try:
+                e = s.set(req.path_params["key"], req.body.decode("utf-8"), etag,
+                          req.headers.get("x-tt-first-write") == "1", int(req.headers.get("x-tt-ttl-ms", "0") or 0))
+            except self.N.EtagMismatch as ex:
+                return problem(412, detail=str(ex))
+            except ValueError as ex:
+                return problem(400, detail=str(ex))
+            return json_response({"etag": e}, headers=[("ETag", e)])
+
+        async def get_doc(req: Request) -> Response:
+            s = st(req, "cosmos.read")
+            r = s.get(req.path_params["key"])
+            if r is None:
+                return empty(404)
+            return Response(r[0].encode(), 200, [("ETag", r[1])], "application/json")
+
+        async def del_doc(req: Request) -> Response:
+            s = st(req, "cosmos.write")
+            try:
+                ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
+            except self.N.EtagMismatch as ex:
+                return problem(412, detail=str(ex))
+            return empty(204 if ok else 404)
+
+        async def bulk_get(req: Request) -> Response:
+            s = st(req, "cosmos.read")
+            out = []
+            for k in (req.json() or {}).get("keys", []):
+                r = s.get(k)
+                out.append({"key": k, "data": json.loads(r[0]), "etag": r[1]} if r else {"key": k})
+            return json_response(out)
+
+        async def bulk_set(req: Request) -> Response:
+            s = st(req, "cosmos.write")
+            out = []
+            for it in req.json() or []:
+                try:
+                    e = s.set(it["key"], it["value"] if isinstance(it["value"], str) else json.dumps(it["value"]),
+                              it.get("etag") or None, bool(it.get("firstWrite")), int(it.get("ttlMs") or 0))
+                    out.append({"key": it["key"], "etag": e})
+                except self.N.EtagMismatch as ex:
+                    out.append({"key": it["key"], "error": "etag", "detail": str(ex)})
+                except ValueError as ex:
+                    out.append({"key": it["key"], "error": "invalid", "detail": str(ex)})
+            status = 412 if any(o.get("error") == "etag" for o in out) else (
+                400 if any("error" in o for o in out) else 200)
+            return json_response(out, status)
+
+        async def query(req: Request) -> Response:
+            s = st(req, "cosmos.read")
+            try:
+                text = s.query(req.body.decode("utf-8") or "{}", req.query_get("prefix", "") or "")
+            except ValueError as ex:
+                return problem(400, detail=str(ex))
+            return Response(text.encode(), 200, None, "application/json")
+
+        async def transaction(req: Request) -> Response:
+            s = st(req, "cosmos.write")
+            ops = []
+            for o in (req.json() or {}).get("ops", []):
+                is_del = o.get("op") == "delete"
+                val = o.get("value")
+                ops.append(self.N.TxOp(is_del, o["key"], "" if is_del else (val if isinstance(val, str) else json.dumps(val)),
+                                       o.get("etag") or None, bool(o.get("firstWrite")), int(o.get("ttlMs") or 0)))
+            try:
+                s.transact(ops)
+            except self.N.EtagMismatch as ex:
+                return problem(412, detail=str(ex))
+            except ValueError as ex:
+                return problem(400, detail=str(ex))
+            return empty(204)
+
+        async def stats(req: Request) -> Response:
+            s = st(req, "cosmos.read")
+            d = dict(s.stats())
+            d["indexedPaths"] = s.indexed_paths()
+            return json_response(d)
+
+        async def keys(req: Request) -> Response:
+            s = st(req, "cosmos.read")
+            return json_response(s.keys(req.query_get("prefix", "") or "", int(req.query_get("limit", "0") or 0)))
+
+        app.add_route(base + "/docs/{key}", put_doc, ("PUT",))
+        app.add_route(base + "/docs/{key}", get_doc, ("GET",))
+        app.add_route(base + "/docs/{key}", del_doc, ("DELETE",))
+        app.add_route(base + "/bulkget", bulk_get, ("POST",))
+        app.add_route(base + "/bulkset", bulk_set, ("POST",))
+        app.add_route(base + "/query", query, ("POST",))
+        app.add_route(base + "/transaction", transaction, ("POST",))
+        app.add_route(base + "/stats", stats, ("GET",))
+        app.add_route(base + "/keys", keys, ("GET",))
+
+    # ---------------------------------------------------------------- service bus
+    def _servicebus_routes(self, app: WebApp) -> None:
+        def opts(d: dict[str, Any]):
+            return self.N.QueueOptions(int(d.get("lockMs", 60000)), int(d.get("maxDelivery", 10)),
+                                       int(d.get("ttlMs", 0)), bool(d.get("deadLetterOnExpiry", False)))
+
+        async def create_topic(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.manage", f"servicebus/{p['ns']}")
+            self.broker(p["ns"]).create_topic(p["topic"])
+            return empty(204)
+
+        async def create_sub(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.manage", f"servicebus/{p['ns']}")
+            self.broker(p["ns"]).create_subscription(p["topic"], p["sub"], opts(req.json() or {}))
+            return empty(204)
+
+        async def create_queue(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.manage", f"servicebus/{p['ns']}")
+            self.broker(p["ns"]).create_queue(p["queue"], opts(req.json() or {}))
+            return empty(204)
+
+        def _notify_topic(ns: str, topic: str) -> None:
+            for sub in self.broker(ns).subscriptions(topic):
+                self.waiters.notify(f"{ns}|{topic}/subscriptions/{sub}")
+
+        async def publish(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.send", f"servicebus/{p['ns']}/topics/{p['topic']}")
+            h = req.headers
+            seq = self.broker(p["ns"]).publish(p["topic"], req.body, h.get("content-type", "application/json"),
+                                               h.get("x-tt-props", "{}"), h.get("x-tt-message-id", ""),
+                                               int(h.get("x-tt-ttl-ms", "0") or 0), int(h.get("x-tt-delay-ms", "0") or 0))
+            _notify_topic(p["ns"], p["topic"])
+            return json_response({"seq": seq}, 201)
+
+        async def publish_batch(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.send", f"servicebus/{p['ns']}/topics/{p['topic']}")
+            b = self.broker(p["ns"])
+            seqs = []
+            for e in req.json() or []:
+                seqs.append(b.publish(p["topic"], _decode_body(e), e.get("contentType", "application/json"),
+                                      json.dumps(e.get("props") or {}), e.get("id", ""), int(e.get("ttlMs", 0)), 0))
+            _notify_topic(p["ns"], p["topic"])
+            return json_response({"seqs": seqs}, 201)
+
+        async def send(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "sb.send", f"servicebus/{p['ns']}/queues/{p['queue']}")
+            h = req.headers
+            seq = self.broker(p["ns"]).send(p["queue"], req.body, h.get("content-type", "application/json"),
+                                            h.get("x-tt-props", "{}"), h.get("x-tt-message-id", ""),
+                                            int(h.get("x-tt-ttl-ms", "0") or 0), int(h.get("x-tt-delay-ms", "0") or 0))
+            self.waiters.notify(f"{p['ns']}|{p['queue']}")
+            return json_response({"seq": seq}, 201)
+
+        async def receive(req: Request) -> Response:
+            ns = req.path_params["ns"]
+            entity = req.query_get("entity") or ""
+            self.authorize(req, "sb.receive", f"servicebus/{ns}/{_entity_scope(entity)}")
+            mx = int(req.query_get("max", "1") or 1)
+            lock = int(req.query_get("lockMs", "0") or 0)
+            wait_s = int(req.query_get("waitMs", "0") or 0) / 1000.0
+            b = self.broker(ns)
+            key = f"{ns}|{entity}"
+            deadline = time.monotonic() + wait_s
+            while True:
+                msgs = b.receive(entity, mx, lock)
+                rem = deadline - time.monotonic()
+                if msgs or rem <= 0:
+                    break
+                await self.waiters.wait(key, min(rem, 0.2))
+            out = []
+            for m in msgs:
+                d = {"lockToken": m.lock_token, "seq": m.seq, "id": m.id, "contentType": m.content_type,
+                     "props": json.loads(m.props or "{}"), "deliveryCount": m.delivery_count, "enqueuedMs": m.enqueued_ms}
+                d.update(_encode_body(m.body))
+                out.append(d)
+            return json_response(out)
+
+        async def settle(req: Request) -> Response:
+            ns = req.path_params["ns"]
+            body = req.json() or {}
+            entity = body.get("entity", "")
+            self.authorize(req, "sb.receive", f"servicebus/{ns}/{_entity_scope(entity)}")
+            b = self.broker(ns)
+            res: dict[str, list[bool]] = {}
+            res["complete"] = [b.complete(entity, t) for t in body.get("complete", [])]
+            res["abandon"] = [b.abandon(entity, a["token"], int(a.get("delayMs", 0))) for a in body.get("abandon", [])]
+            res["deadletter"] = [b.dead_letter(entity, d["token"], d.get("reason", "")) for d in body.get("deadletter", [])]
+            res["renew"] = [b.renew(entity, r["token"], int(r.get("lockMs", 0))) for r in body.get("renew", [])]
+            if body.get("abandon"):
+                self.waiters.notify(f"{ns}|{entity}")
+            return json_response(res)
+
+        async def counts(req: Request) -> Response:
+            ns = req.path_params["ns"]
+            entity = req.query_get("entity") or ""
+            return json_response(dict(self.broker(ns).counts(entity)))
+
+        async def dead_letters(req: Request) -> Response:
+            ns = req.path_params["ns"]
+            entity = req.query_get("entity") or ""
+            self.authorize(req, "sb.receive", f"servicebus/{ns}/{_entity_scope(entity)}")
+            out = []
+            for seq, mid, body, reason, dc in self.broker(ns).drain_dead_letters(entity, int(req.query_get("max", "100"))):
+                d = {"seq": seq, "id": mid, "reason": reason, "deliveryCount": dc}
+                d.update(_encode_body(body))
+                out.append(d)
+            return json_response(out)
+
+        async def entities(req: Request) -> Response:
+            b = self.broker(req.path_params["ns"])
+            return json_response({e: dict(b.counts(e)) for e in b.entities()})
+
+        app.add_route("/servicebus/{ns}/topics/{topic}", create_topic, ("PUT",))
+        app.add_route("/servicebus/{ns}/topics/{topic}/subscriptions/{sub}", create_sub, ("PUT",))
+        app.add_route("/servicebus/{ns}/queues/{queue}", create_queue, ("PUT",))
+        app.add_route("/servicebus/{ns}/topics/{topic}/messages", publish, ("POST",))
+        app.add_route("/servicebus/{ns}/topics/{topic}/batch", publish_batch, ("POST",))
+        app.add_route("/servicebus/{ns}/queues/{queue}/messages", send, ("POST",))
+        app.add_route("/servicebus/{ns}/receive", receive, ("POST",))
+        app.add_route("/servicebus/{ns}/settle", settle, ("POST",))
+        app.add_route("/servicebus/{ns}/counts", counts, ("GET",))
+        app.add_route("/servicebus/{ns}/deadletters", dead_letters, ("POST",))
+        app.add_route("/servicebus/{ns}/entities", entities, ("GET",))
+
+    # ---------------------------------------------------------------- storage
+    def _storage_routes(self, app: WebApp) -> None:
+        def qbroker(account: str):
+            return self.broker(f"storage-{account}")
+
+        async def put_message(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "queue.send", f"storage/{p['account']}")
+            ttl = int(req.query_get("messagettl", "0") or 0) * 1000
+            delay = int(req.query_get("visibilitytimeout", "0") or 0) * 1000
+            seq = qbroker(p["account"]).send(p["queue"], req.body, "text/plain", "{}", "", ttl, delay)
+            self.waiters.notify(f"storage-{p['account']}|{p['queue']}")
+            return json_response({"messageId": str(seq)}, 201)
+
+        async def get_messages(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "queue.receive", f"storage/{p['account']}")
+            mx = int(req.query_get("numofmessages", "1") or 1)
+            vis = int(req.query_get("visibilityMs", "30000") or 30000)
+            wait_s = int(req.query_get("waitMs", "0") or 0) / 1000.0
+            b = qbroker(p["account"])
+            key = f"storage-{p['account']}|{p['queue']}"
+            deadline = time.monotonic() + wait_s
+            while True:
+                msgs = b.receive(p["queue"], mx, vis)
+                rem = deadline - time.monotonic()
+                if msgs or rem <= 0:
+                    break
+                await self.waiters.wait(key, min(rem, 0.2))
+            out = []
+            for m in msgs:
+                d = {"messageId": str(m.seq), "popReceipt": m.lock_token, "dequeueCount": m.delivery_count,
+                     "insertionMs": m.enqueued_ms}
+                d.update(_encode_body(m.body))
+                out.append(d)
+            return json_response(out)
+
+        async def delete_message(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "queue.receive", f"storage/{p['account']}")
+            ok = qbroker(p["account"]).complete(p["queue"], p["receipt"])
+            return empty(204 if ok else 404)
+
+        async def update_message(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "queue.receive", f"storage/{p['account']}")
+            delay = int(req.query_get("visibilityMs", "0") or 0)
+            ok = qbroker(p["account"]).abandon(p["queue"], p["receipt"], delay)
+            self.waiters.notify(f"storage-{p['account']}|{p['queue']}")
+            return empty(204 if ok else 404)
+
+        async def queue_count(req: Request) -> Response:
+            p = req.path_params
+            return json_response(dict(qbroker(p["account"]).counts(p["queue"])))
+
+        def blob_file(p: dict[str, Any]) -> Path:
+            root = (self.blob_root / _safe(p["account"]) / _safe(p["container"])).resolve()
+            f = (root / p["name"]).resolve()
+            if root not in f.parents:
+                raise HTTPError(400, detail="invalid blob name")
+            return f
+
+        async def put_blob(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "blob.write", f"storage/{p['account']}")
+            f = blob_file(p)
+            f.parent.mkdir(parents=True, exist_ok=True)
+            tmp = f.with_name(f.name + ".tmp")
+            tmp.write_bytes(req.body)
+            os.replace(tmp, f)
+            meta = {"contentType": req.headers.get("content-type", "application/octet-stream"),
+                    "lastModified": time.time(), "size": len(req.body)}
+            f.with_name(f.name + ".meta.json").write_text(json.dumps(meta))
+            return json_response({"blobURL": f"/storage/{p['account']}/blobs/{p['container']}/{p['name']}"}, 201)
+
+        async def get_blob(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "blob.read", f"storage/{p['account']}")
+            f = blob_file(p)
+            if not f.is_file():
+                return empty(404)
+            ctype = "application/octet-stream"
+            mf = f.with_name(f.name + ".meta.json")
+            if mf.exists():
+                ctype = json.loads(mf.read_text()).get("contentType", ctype)
+            return Response(f.read_bytes(), 200, None, ctype)
+
+        async def delete_blob(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "blob.write", f"storage/{p['account']}")
+            f = blob_file(p)
+            if not f.is_file():
+                return empty(404)
+            f.unlink()
+            mf = f.with_name(f.name + ".meta.json")
+            if mf.exists():
+                mf.unlink()
+            return empty(204)
+
+        async def list_blobs(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "blob.read", f"storage/{p['account']}")
+            root = self.blob_root / _safe(p["account"]) / _safe(p["container"])
+            prefix = req.query_get("prefix", "") or ""
+            out = []
+            if root.is_dir():
+                for f in sorted(root.rglob("*")):
+                    if f.is_file() and not f.name.endswith((".meta.json", ".tmp")):
+                        name = str(f.relative_to(root))
+                        if name.startswith(prefix):
+                            out.append({"name": name, "size": f.stat().st_size})
+            return json_response(out)
+
+        app.add_route("/storage/{account}/queues/{queue}/messages", put_message, ("POST",))
+        app.add_route("/storage/{account}/queues/{queue}/messages", get_messages, ("GET",))
+        app.add_route("/storage/{account}/queues/{queue}/messages/{receipt}", delete_message, ("DELETE",))
+        app.add_route("/storage/{account}/queues/{queue}/messages/{receipt}", update_message, ("PUT",))
+        app.add_route("/storage/{account}/queues/{queue}/count", queue_count, ("GET",))
+        app.add_route("/storage/{account}/blobs/{container}", list_blobs, ("GET",))
+        app.add_route("/storage/{account}/blobs/{container}/{*name}", put_blob, ("PUT",))
+        app.add_route("/storage/{account}/blobs/{container}/{*name}", get_blob, ("GET",))
+        app.add_route("/storage/{account}/blobs/{container}/{*name}", delete_blob, ("DELETE",))
+
+    # ---------------------------------------------------------------- key vault
+    def _keyvault_routes(self, app: WebApp) -> None:
+        async def get_secret(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "kv.get", f"keyvault/{p['vault']}")
+            v = self.vaults.get(p["vault"], {}).get(p["name"])
+            if v is None:
+                return problem(404, detail=f"secret {p['name']} not found")
+            return json_response({"name": p["name"], "value": v})
+
+        async def set_secret(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "kv.set", f"keyvault/{p['vault']}")
+            self.vaults.setdefault(p["vault"], {})[p["name"]] = (req.json() or {}).get("value", "")
+            self._save_vaults()
+            return empty(204)
+
+        async def list_secrets(req: Request) -> Response:
+            p = req.path_params
+            self.authorize(req, "kv.get", f"keyvault/{p['vault']}")
+            return json_response(sorted(self.vaults.get(p["vault"], {})))
+
+        app.add_route("/keyvault/{vault}/secrets", list_secrets, ("GET",))
+        app.add_route("/keyvault/{vault}/secrets/{name}", get_secret, ("GET",))
+        app.add_route("/keyvault/{vault}/secrets/{name}", set_secret, ("PUT",))
+
+    # ---------------------------------------------------------------- sendgrid
+    def _sendgrid_routes(self, app: WebApp) -> None:
+        async def send_mail(req: Request) -> Response:
+            auth = req.headers.get("authorization", "")
+            expected = self.policy.keys.get("sendgrid")
+            if self.policy.mode == "enforce" and expected and auth != f"Bearer {expected}":
+                return problem(401, detail="invalid SendGrid API key")
+            msg = req.json() or {}
+            if not msg.get("personalizations") or not msg.get("from"):
+                return problem(400, detail="personalizations and from are required")
+            rec = {"ts": time.time(), "message": msg}
+            self.outbox.append(rec)
+            if self.data_dir is not None:
+                with open(self.data_dir / "sendgrid-outbox.jsonl", "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+            return empty(202)
+
+        async def outbox(req: Request) -> Response:
+            return json_response(self.outbox)
+
+        app.add_route("/sendgrid/v3/mail/send", send_mail, ("POST",))
+        app.add_route("/sendgrid/outbox", outbox, ("GET",))
+
+    # ---------------------------------------------------------------- admin
+    def _admin_routes(self, app: WebApp) -> None:
+        async def health(req: Request) -> Response:
+            return empty(204)
+
+        async def overview(req: Request) -> Response:
+            out: dict[str, Any] = {"cosmos": {}, "servicebus": {}}
+            for (a, d, c), s in self.stores.items():
+                out["cosmos"][f"{a}/{d}/{c}"] = dict(s.stats())
+            for ns, b in self.brokers.items():
+                out["servicebus"][ns] = {e: dict(b.counts(e)) for e in b.entities()}
+            out["keyvault"] = {v: sorted(s) for v, s in self.vaults.items()}
+            out["sendgrid"] = {"sent": len(self.outbox)}
+            return json_response(out)
+
+        async def set_policy(req: Request) -> Response:
+            self.policy = AccessPolicy.from_dict(req.json())
+            return empty(204)
+
+        app.add_route("/admin/health", health, ("GET",))
+        app.add_route("/admin/overview", overview, ("GET",))
+        app.add_route("/admin/policy", set_policy, ("PUT",))
+
+
+def _entity_scope(entity: str) -> str:
+    if "/subscriptions/" in entity:
+        return "topics/" + entity.split("/subscriptions/")[0]
+    return "queues/" + entity
+
+
+async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | None = None,
+                        policy: dict[str, Any] | None = None, ready=None, stop: asyncio.Event | None = None) -> None:
+    from ..web.server import HttpServer
+    svc = BackingServices(data_dir, AccessPolicy.from_dict(policy))
+    app = svc.build_app()
+    srv = HttpServer(app, asyncio.get_running_loop())
+    bound = await srv.listen_tcp(host, port)
+    log.info("backing services listening on %s:%d (data=%s)", host, bound, data_dir)
+    if ready:
+        ready(bound)
+    stop = stop or asyncio.Event()
+    loop = asyncio.get_running_loop()
+    import signal
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    await stop.wait()
+    await srv.close()
+
+
+def main(argv: list[str] | None = None) -> None:
+    ap = argparse.ArgumentParser(description="Backing-services emulator (Cosmos/ServiceBus/Storage/KeyVault/SendGrid)")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=10000)
+    ap.add_argument("--data-dir", default=None)
+    ap.add_argument("--policy", default=None, help="JSON file with access policy (mode/keys/roleAssignments)")
+    ap.add_argument("--port-file", default=None)
+    a = ap.parse_args(argv)
+    configure_logging("backing-services")
+    configure("backing-services")
+    policy = json.loads(Path(a.policy).read_text()) if a.policy else None
+
+    def ready(port: int) -> None:
+        if a.port_file:
+            tmp = a.port_file + ".tmp"
+            Path(tmp).write_text(str(port))
+            os.replace(tmp, a.port_file)
+
+    try:
+        asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready))
+    except KeyboardInterrupt:
+        pass
+
+
+if __name__ == "__main__":
+    main()

@@ -23,6 +23,7 @@ import mimetypes
 import os
 import uuid
 from pathlib import Path
+from urllib.parse import unquote
 from typing import Any, Awaitable, Callable
 
 from ..models.dotnet import is_guid
@@ -153,7 +154,9 @@ class WebApp:
 
     # -- dispatch ---------------------------------------------------------------
     def match(self, method: str, path: str) -> tuple[Route | None, dict[str, Any], bool]:
-        parts = [p for p in path.split("/") if p]
+        """``path`` is the raw (still percent-encoded) path; segments are decoded after
+        splitting so an encoded ``%2F`` stays inside its segment."""
+        parts = [unquote(p) if "%" in p else p for p in path.split("/") if p]
         path_matched = False
         for r in self.routes:
             params = r.match(parts)
@@ -165,7 +168,7 @@ class WebApp:
         return None, {}, path_matched
 
     async def _dispatch(self, req: Request) -> Response:
-        route, params, path_matched = self.match(req.method, req.path)
+        route, params, path_matched = self.match(req.method, req.raw_path)
         if route is None:
             if req.method in ("GET", "HEAD") and self.static_dirs:
                 resp = self._static(req.path)

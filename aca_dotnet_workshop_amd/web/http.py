@@ -33,7 +33,7 @@ class HTTPError(Exception):
 
 
 class Request:
-    __slots__ = ("method", "target", "path", "query_string", "headers", "body", "client",
+    __slots__ = ("method", "target", "path", "raw_path", "query_string", "headers", "body", "client",
                  "path_params", "state", "_query", "_cookies", "version", "app", "route")
 
     def __init__(self, method: str, target: str, headers: Headers, body: bytes = b"",
@@ -42,11 +42,12 @@ class Request:
         self.target = target
         q = target.find("?")
         if q >= 0:
-            self.path = unquote(target[:q])
+            self.raw_path = target[:q]
             self.query_string = target[q + 1:]
         else:
-            self.path = unquote(target)
+            self.raw_path = target
             self.query_string = ""
+        self.path = unquote(self.raw_path) if "%" in self.raw_path else self.raw_path
         self.headers = headers
         self.body = body
         self.client = client

@@ -1,0 +1,132 @@
+"""Backing-services emulator tests over HTTP (Cosmos / Service Bus / Storage / Key Vault /
+SendGrid equivalents) including RBAC enforcement mirroring the Bicep role assignments."""
+import asyncio
+import json
+
+import pytest
+
+from aca_dotnet_workshop_amd.backing import AccessPolicy, BackingClient, BackingServices, EtagConflict
+from aca_dotnet_workshop_amd.backing.client import BackingError
+
+from helpers import run, served
+
+
+def _svc(tmp_path=None, policy=None):
+    return BackingServices(str(tmp_path) if tmp_path else None, AccessPolicy.from_dict(policy))
+
+
+def test_cosmos_roundtrip_query_and_persistence(tmp_path):
+    async def main(svc):
+        async with served(svc.build_app()) as (base, _):
+            c = BackingClient(base)
+            e = await c.doc_put("acct", "db", "coll", "api||1", json.dumps({"taskCreatedBy": "a", "n": 1}))
+            await c.doc_put("acct", "db", "coll", "api||2", json.dumps({"taskCreatedBy": "b", "n": 2}))
+            body, etag = await c.doc_get("acct", "db", "coll", "api||1")
+            assert json.loads(body)["n"] == 1 and etag == e
+            with pytest.raises(EtagConflict):
+                await c.doc_put("acct", "db", "coll", "api||1", "{}", etag="bogus")
+            res = json.loads(await c.doc_query("acct", "db", "coll", b'{"filter":{"EQ":{"taskCreatedBy":"b"}}}', "api||"))
+            assert [r["key"] for r in res["results"]] == ["2"]
+            assert await c.doc_delete("acct", "db", "coll", "api||2") is True
+            assert await c.doc_get("acct", "db", "coll", "api||2") is None
+            await c.close()
+    run(main(_svc(tmp_path)))
+    # a restarted emulator over the same data dir still has the document
+    run(_check_persisted(_svc(tmp_path)))
+
+
+async def _check_persisted(svc):
+    async with served(svc.build_app()) as (base, _):
+        c = BackingClient(base)
+        body, _ = await c.doc_get("acct", "db", "coll", "api||1")
+        assert json.loads(body)["n"] == 1
+        await c.close()
+
+
+def test_servicebus_long_poll_and_settle():
+    async def main():
+        svc = _svc()
+        async with served(svc.build_app()) as (base, _):
+            c = BackingClient(base)
+            await c.sb_create_subscription("ns", "tasksavedtopic", "processor")
+            ent = "tasksavedtopic/subscriptions/processor"
+            recv = asyncio.ensure_future(c.sb_receive("ns", ent, 10, wait_ms=3000))
+            await asyncio.sleep(0.05)
+            assert not recv.done()
+            await c.sb_publish("ns", "tasksavedtopic", b'{"x":1}', props={"a": "b"})
+            msgs = await asyncio.wait_for(recv, 2)
+            assert len(msgs) == 1 and msgs[0]["body"] == '{"x":1}' and msgs[0]["props"] == {"a": "b"}
+            res = await c.sb_settle("ns", ent, abandon=[{"token": msgs[0]["lockToken"]}])
+            assert res["abandon"] == [True]
+            m2 = (await c.sb_receive("ns", ent, 1))[0]
+            assert m2["deliveryCount"] == 2
+            await c.sb_settle("ns", ent, deadletter=[{"token": m2["lockToken"], "reason": "poison"}])
+            counts = await c.sb_counts("ns", ent)
+            assert counts["dead_letter"] == 1 and counts["active"] == 0
+            dl = await c.sb_dead_letters("ns", ent)
+            assert dl[0]["reason"] == "poison"
+            await c.close()
+    run(main())
+
+
+def test_storage_queue_blob_keyvault_sendgrid():
+    async def main():
+        svc = _svc()
+        async with served(svc.build_app()) as (base, _):
+            c = BackingClient(base)
+            await c.queue_put("acct", "external-tasks-queue", b"eyJhIjoxfQ==")
+            m = (await c.queue_get("acct", "external-tasks-queue", visibility_ms=50))[0]
+            assert m["body"] == "eyJhIjoxfQ==" and m["dequeueCount"] == 1
+            await asyncio.sleep(0.08)  # visibility timeout elapses -> message reappears
+            m = (await c.queue_get("acct", "external-tasks-queue"))[0]
+            assert m["dequeueCount"] == 2
+            assert await c.queue_delete("acct", "external-tasks-queue", m["popReceipt"])
+            assert (await c.queue_count("acct", "external-tasks-queue"))["active"] == 0
+            await c.blob_put("acct", "externaltaskscontainer", "abc.json", b'{"k":1}', "application/json")
+            assert await c.blob_get("acct", "externaltaskscontainer", "abc.json") == b'{"k":1}'
+            assert [b["name"] for b in await c.blob_list("acct", "externaltaskscontainer")] == ["abc.json"]
+            with pytest.raises(BackingError):
+                await c.blob_put("acct", "c", "../../escape", b"x")
+            await c.kv_set("tasks-tracker-akv", "sendgrid-api-key", "SG.x")
+            assert await c.kv_get("tasks-tracker-akv", "sendgrid-api-key") == "SG.x"
+            await c.sendgrid_send({"personalizations": [{"to": [{"email": "a@b"}], "subject": "s"}],
+                                   "from": {"email": "x@y"}, "content": [{"type": "text/plain", "value": "v"}]})
+            assert len(await c.sendgrid_outbox()) == 1
+            await c.close()
+    run(main())
+
+
+def test_rbac_enforcement():
+    policy = {"mode": "enforce",
+              "keys": {"cosmos/acct": "masterkey"},
+              "roleAssignments": [
+                  {"principal": "api-mi", "role": "Cosmos DB Built-in Data Contributor", "scope": "cosmos/acct"},
+                  {"principal": "api-mi", "role": "Azure Service Bus Data Sender", "scope": "servicebus/ns/topics/t"},
+                  {"principal": "proc-mi", "role": "Azure Service Bus Data Receiver", "scope": "servicebus/ns/topics/t"},
+                  {"principal": "proc-mi", "role": "Key Vault Secrets User", "scope": "keyvault/v"},
+                  {"principal": "admin", "role": "Owner", "scope": ""}]}
+
+    async def main():
+        svc = _svc(policy=policy)
+        async with served(svc.build_app()) as (base, _):
+            admin = BackingClient(base, identity="admin")
+            api = BackingClient(base, identity="api-mi")
+            proc = BackingClient(base, identity="proc-mi")
+            anon = BackingClient(base, identity="")
+            keyed = BackingClient(base, identity="", key="masterkey")
+            await admin.sb_create_subscription("ns", "t", "proc")
+            await admin.kv_set("v", "s", "secret")
+            await api.doc_put("acct", "db", "c", "k", "1")
+            await keyed.doc_put("acct", "db", "c", "k2", "2")
+            for call in (anon.doc_put("acct", "db", "c", "k", "1"), proc.doc_get("acct", "db", "c", "k"),
+                         proc.sb_publish("ns", "t", b"x"), api.sb_receive("ns", "t/subscriptions/proc"),
+                         api.kv_get("v", "s")):
+                with pytest.raises(BackingError) as ei:
+                    await call
+                assert ei.value.status == 403
+            await api.sb_publish("ns", "t", b"x")
+            assert len(await proc.sb_receive("ns", "t/subscriptions/proc")) == 1
+            assert await proc.kv_get("v", "s") == "secret"
+            for c in (admin, api, proc, anon, keyed):
+                await c.close()
+    run(main())
