@@ -1,1 +1,1 @@
-"""platform"""
+"""Platform layer (the Azure Container Apps environment equivalent)."""

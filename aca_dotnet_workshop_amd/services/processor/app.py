@@ -1,0 +1,160 @@
+"""Backend processor (app-id ``tasksmanager-backend-processor``, no ingress).
+
+Endpoints (reference SURVEY.md §2.2, §2.11):
+
+* ``POST /api/tasksnotifier/tasksaved`` -- subscriber of ``tasksavedtopic`` on both
+  ``dapr-pubsub-servicebus`` and ``taskspubsub`` (reference
+  Controllers/TasksNotifierController.cs:23-32).  Modes (``TasksNotifier:Mode``):
+    - ``log`` (default, the shipped controller): log and return 200 with a message;
+    - ``sendgrid-binding`` (reference docs/aca/06-aca-dapr-bindingsapi/TasksNotifierController.cs:22-77):
+      if ``SendGrid:IntegrationEnabled`` send the e-mail through the ``sendgrid`` output
+      binding, otherwise simulate ``SendGrid:SimulatedDelayMs`` (1000) of work -- the load
+      the KEDA scale-out test relies on; failures return 400 so the broker retries;
+    - ``sendgrid-api`` (reference docs/aca/05-aca-dapr-pubsubapi/TasksNotifierController-SendGrid.cs):
+      call the SendGrid-compatible HTTP API directly with ``SendGrid:ApiKey``.
+* ``POST /ExternalTasksProcessor/process`` -- storage-queue input binding handler
+  (reference Controllers/ExternalTasksProcessorController.cs:22-53): create the task via
+  the API, then archive it to ``externaltasksblobstore`` as ``<taskId>.json``.  Exceptions
+  propagate as 500 so the queue message is retried.  Deviation: the
+  blob is named after the id the API actually stored (parsed from its ``Location``
+  header), so the archive and the store agree.
+* ``POST /ScheduledTasksManager`` -- cron handler (reference
+  Controllers/ScheduledTasksManagerController.cs:19-46): fetch yesterday's open tasks,
+  keep those with ``runAt.Date > dueDate.Date``, mark them overdue.
+* ``GET /dapr/subscribe`` -- ``MapSubscribeHandler`` (reference Program.cs:33).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import uuid
+from pathlib import Path
+
+from ...models import TaskModel, naive_utc, tasks_from_json, utcnow
+from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
+from ...sdk.client import InvocationError
+from ...web.app import WebApp, read_model
+from ...web.http import Request, Response, empty, json_response, text_response
+from ..hosting import create_host, map_openapi, run_host
+
+ROLE = "tasksmanager-backend-processor"
+API_APP_ID = "tasksmanager-backend-api"
+CONTENT_ROOT = Path(__file__).parent
+OUTPUT_BINDING_NAME = "externaltasksblobstore"
+OUTPUT_BINDING_OPERATION = "create"
+
+log_notifier = logging.getLogger("TasksNotifierController")
+log_external = logging.getLogger("ExternalTasksProcessorController")
+log_sched = logging.getLogger("ScheduledTasksManagerController")
+
+
+def register_controllers(app: WebApp, client: SidecarClient) -> None:
+    cfg = app.config
+    api_app_id = cfg.get_str("Processor:BackendApiAppId", API_APP_ID)
+
+    # -- TasksNotifierController ----------------------------------------------
+    @app.route("/api/tasksnotifier/tasksaved", ("POST",), name="TaskSaved", tag="TasksNotifier", body=TaskModel)
+    @topic("dapr-pubsub-servicebus", "tasksavedtopic")
+    @topic("taskspubsub", "tasksavedtopic")
+    async def task_saved(req: Request) -> Response:
+        t: TaskModel = await read_model(req, TaskModel)
+        log_notifier.info("Started processing message with Task Name '%s'", t.task_name)
+        mode = (cfg.get_str("TasksNotifier:Mode") or "log").lower()
+        if mode == "log":
+            return text_response(f"Started processing message with Task Name '{t.task_name}'")
+        ok = await send_email(t)
+        return empty(200) if ok else Response(b"Failed to send an email", 400, None, "text/plain")
+
+    async def send_email(t: TaskModel) -> bool:
+        mode = (cfg.get_str("TasksNotifier:Mode") or "log").lower()
+        subject = f"Task '{t.task_name}' is assigned to you!"
+        due = naive_utc(t.task_due_date)
+        text = (f"Task '{t.task_name}' is assigned to you. Task should be completed by the end of: "
+                f"{due.day:02d}/{due.month:02d}/{due.year:04d}")
+        try:
+            if mode == "sendgrid-api":
+                from ...backing.client import BackingClient
+                bc = BackingClient(cfg.get_str("SendGrid:Endpoint"), http=client.http)
+                await bc.sendgrid_send({"personalizations": [{"to": [{"email": t.task_assigned_to,
+                                                                       "name": t.task_assigned_to}], "subject": subject}],
+                                        "from": {"email": cfg.get_str("SendGrid:FromEmail", "noreply@taskstracker.local"),
+                                                 "name": "Tasks Tracker Notification"},
+                                        "content": [{"type": "text/plain", "value": text},
+                                                    {"type": "text/html", "value": text}]},
+                                       cfg.get_str("SendGrid:ApiKey"))
+            elif cfg.get_bool("SendGrid:IntegrationEnabled"):
+                await client.invoke_binding("sendgrid", "create", text,
+                                            {"emailTo": t.task_assigned_to, "emailToName": t.task_assigned_to,
+                                             "subject": subject})
+            else:
+                log_notifier.info("Simulate slow processing for email sending for Email with Email subject '%s' "
+                                  "Email to: '%s'", subject, t.task_assigned_to)
+                await asyncio.sleep(cfg.get_int("SendGrid:SimulatedDelayMs", 1000) / 1000.0)
+            log_notifier.info("Email with subject '%s' sent to: '%s' successfully", subject, t.task_assigned_to)
+            return True
+        except Exception as e:
+            log_notifier.error("Failed to send email with subject '%s' To: '%s': %s", subject, t.task_assigned_to, e)
+            return False
+
+    # -- ExternalTasksProcessorController --------------------------------------
+    @app.route("/ExternalTasksProcessor/process", ("POST",), name="ProcessTaskAndStore", tag="ExternalTasksProcessor",
+               body=TaskModel)
+    async def process_task_and_store(req: Request) -> Response:
+        t: TaskModel = await read_model(req, TaskModel)
+        log_external.info("Started processing external task message from storage queue. Task Name: '%s'", t.task_name)
+        t.task_id = uuid.uuid4()
+        t.task_created_on = utcnow()
+        r = await client.invoke_method_raw("POST", api_app_id, "api/tasks", t)
+        if r.status >= 300:
+            raise InvocationError(r.status, r.body, f"invoke {api_app_id}/api/tasks")
+        loc = r.headers.get("location", "")
+        try:
+            t.task_id = uuid.UUID(loc.rstrip("/").rsplit("/", 1)[-1])
+        except ValueError:
+            pass
+        log_external.info("Saved external task to the state store successfully. Task name: '%s', Task Id: '%s'",
+                          t.task_name, t.task_id)
+        await client.invoke_binding(OUTPUT_BINDING_NAME, OUTPUT_BINDING_OPERATION, t, {"blobName": f"{t.task_id}.json"})
+        log_external.info("Invoked output binding '%s' for external task. Task name: '%s', Task Id: '%s'",
+                          OUTPUT_BINDING_NAME, t.task_name, t.task_id)
+        return empty(200)
+
+    # -- ScheduledTasksManagerController ---------------------------------------
+    @app.route("/ScheduledTasksManager", ("POST",), name="CheckOverDueTasksJob", tag="ScheduledTasksManager")
+    async def check_overdue_tasks_job(req: Request) -> Response:
+        run_at = utcnow()
+        log_sched.info("ScheduledTasksManager::Timer Services triggered at: %s", run_at)
+        tasks = tasks_from_json(await client.invoke_method("GET", api_app_id, "api/overduetasks"))
+        log_sched.info("ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d",
+                       len(tasks))
+        overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
+        if overdue:
+            log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", len(overdue))
+            await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", overdue)
+        return json_response({"runAt": run_at.isoformat(), "retrieved": len(tasks), "markedOverdue": len(overdue)})
+
+
+def create_app(argv: list[str] | None = None, client: SidecarClient | None = None, config=None,
+               overrides: dict | None = None) -> WebApp:
+    app = create_host(ROLE, CONTENT_ROOT, argv, config=config, overrides=overrides)
+    app.openapi_info = {"title": "TasksTracker.Processor.Backend.Svc | v1", "version": "1.0.0"}
+    client = client or SidecarClient()
+    app.services["dapr"] = client
+    app.use(cloud_events_middleware())  # app.UseCloudEvents()
+    register_controllers(app, client)
+    map_subscribe_handler(app)          # app.MapSubscribeHandler()
+    map_openapi(app)
+
+    async def _close() -> None:
+        await client.close()
+    app.on_shutdown.append(_close)
+    return app
+
+
+def main(argv: list[str] | None = None) -> None:
+    import sys
+    run_host(create_app(sys.argv[1:] if argv is None else argv))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+"""Shared plumbing for sidecar components: runtime context, backing-service endpoint
+resolution from Azure-style metadata, and the component type registry."""
+from __future__ import annotations
+
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any, Callable
+from urllib.parse import urlsplit
+
+from ..backing.client import BackingClient, backing_url
+from ..web.client import HttpClient
+from .components import Component, ComponentError
+
+
+@dataclass
+class RuntimeContext:
+    app_id: str
+    namespace: str = "default"
+    identity: str | None = None
+    backing_url: str = field(default_factory=backing_url)
+    http: HttpClient = field(default_factory=HttpClient)
+    environ: dict[str, str] = field(default_factory=lambda: dict(os.environ))
+
+    def backing(self, comp: Component, key: str | None = None) -> BackingClient:
+        base = comp.get("ttBackingUrl") or self.backing_url
+        return BackingClient(base, identity=self.identity or "", key=key, http=self.http)
+
+
+class ComponentBase:
+    """Every component is constructed from its resolved ``Component`` manifest."""
+
+    def __init__(self, comp: Component, ctx: RuntimeContext) -> None:
+        self.comp = comp
+        self.ctx = ctx
+        self.name = comp.name
+
+    async def init(self) -> None:
+        pass
+
+    async def close(self) -> None:
+        pass
+
+
+_REGISTRY: dict[str, type] = {}
+
+
+def register(*types: str) -> Callable[[type], type]:
+    def deco(cls: type) -> type:
+        for t in types:
+            _REGISTRY[t] = cls
+        return cls
+    return deco
+
+
+def create_component(comp: Component, ctx: RuntimeContext) -> ComponentBase:
+    cls = _REGISTRY.get(comp.type)
+    if cls is None:
+        raise ComponentError(f"component {comp.name}: unsupported type {comp.type!r} "
+                             f"(supported: {', '.join(sorted(_REGISTRY))})")
+    return cls(comp, ctx)
+
+
+def supported_types() -> list[str]:
+    return sorted(_REGISTRY)
+
+
+# -- Azure-style endpoint metadata -> emulator account names --------------------
+def cosmos_account(url: str) -> str:
+    host = urlsplit(url).hostname or url
+    return host.split(".")[0]
+
+
+def servicebus_namespace(comp: Component) -> tuple[str, str | None]:
+    cs = comp.get("connectionString")
+    if cs:
+        parts = dict(p.split("=", 1) for p in cs.split(";") if "=" in p)
+        ep = parts.get("Endpoint", "")
+        host = urlsplit(ep).hostname or ep.replace("sb://", "").strip("/")
+        return host.split(".")[0] or "default", parts.get("SharedAccessKey")
+    ns = comp.get("namespaceName")
+    if ns:
+        return ns.split(".")[0], None
+    return "default", None
+
+
+def redis_namespace(comp: Component) -> str:
+    host = comp.get("redisHost", "localhost:6379") or "localhost:6379"
+    return "redis-" + re.sub(r"[^A-Za-z0-9]", "-", host)
