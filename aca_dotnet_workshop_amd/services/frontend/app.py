@@ -1,0 +1,276 @@
+"""Web portal (app-id ``tasksmanager-frontend-webapp``, external ingress).
+
+Razor-Pages equivalent rendered with Jinja2 (reference SURVEY.md §2.3):
+
+==================================  ==========================================================
+page                                reference
+==================================  ==========================================================
+``GET/POST /``                      Pages/Index.cshtml(.cs): e-mail form -> ``TasksCreatedByCookie``
+``GET /Tasks/Index``                Pages/Tasks/Index.cshtml(.cs):23-55 (cookie or redirect to /)
+``POST /Tasks/Index?handler=...``   OnPostDeleteAsync / OnPostCompleteAsync (:57-71)
+``GET/POST /Tasks/Create``          Pages/Tasks/Create.cshtml(.cs) with ``[Required]`` validation
+``GET/POST /Tasks/Edit/{id:guid}``  Pages/Tasks/Edit.cshtml(.cs)
+``/Privacy``, ``/Error``            Pages/Privacy, Pages/Error (RequestId = trace id)
+==================================  ==========================================================
+
+Backend access (``Frontend:BackendMode``):
+* ``dapr`` (default; reference Index.cshtml.cs:48) -- ``DaprClient.InvokeMethodAsync`` via the sidecar;
+* ``http`` (module-2 variant, reference docs/aca/02-aca-comm/Tasks.Index.cshtml.cs:20-48) -- a
+  named HTTP client on ``BackendApiConfig:BaseUrlExternalHttp`` (required in this mode, as the
+  reference's startup check, Program.cs:15-27).
+
+Antiforgery: like Razor Pages, POSTs to ``/Tasks/*`` must carry a token bound to the
+antiforgery cookie; the landing page opts out (``[IgnoreAntiforgeryToken]``, Index.cshtml.cs:7).
+"""
+from __future__ import annotations
+
+import hashlib
+import hmac
+import logging
+import os
+import secrets
+import uuid
+from pathlib import Path
+from typing import Any
+from urllib.parse import quote
+
+from jinja2 import Environment, FileSystemLoader, select_autoescape
+
+from ...models import FIELD_DISPLAY, REQUIRED_FIELDS, TaskModel, parse_datetime, tasks_from_json
+from ...models.dotnet import is_guid, naive_utc
+from ...sdk import SidecarClient
+from ...web.app import WebApp
+from ...web.client import HttpClient
+from ...web.http import HTTPError, Request, Response, html_response, redirect
+from ..hosting import create_host, run_host
+
+ROLE = "tasksmanager-frontend-webapp"
+API_APP_ID = "tasksmanager-backend-api"
+COOKIE = "TasksCreatedByCookie"
+AF_COOKIE = ".AspNetCore.Antiforgery"
+AF_FIELD = "__RequestVerificationToken"
+HERE = Path(__file__).parent
+log = logging.getLogger("Frontend")
+
+
+class BackendGateway:
+    """The two ways the reference's pages reach the API."""
+
+    def __init__(self, mode: str, client: SidecarClient | None, base_url: str | None) -> None:
+        self.mode = mode
+        self.dapr = client
+        self.base = (base_url or "").rstrip("/")
+        self.http = HttpClient() if mode == "http" else None
+
+    async def call(self, method: str, path: str, data: Any = None) -> Any:
+        if self.mode == "dapr":
+            return await self.dapr.invoke_method(method, API_APP_ID, path, data)
+        import json
+        from ...sdk.client import InvocationError, to_jsonable
+        body = json.dumps(to_jsonable(data)).encode() if data is not None else None
+        r = await self.http.request(method, f"{self.base}/{path.lstrip('/')}", body=body,
+                                    headers={"Content-Type": "application/json"} if body else None)
+        if r.status >= 300:
+            raise InvocationError(r.status, r.body, f"{method} {path}")
+        return r.json() if r.body else None
+
+    async def close(self) -> None:
+        if self.dapr is not None:
+            await self.dapr.close()
+        if self.http is not None:
+            await self.http.close()
+
+
+class Antiforgery:
+    def __init__(self, key: bytes) -> None:
+        self.key = key
+
+    def token_for(self, cookie: str) -> str:
+        return hmac.new(self.key, cookie.encode(), hashlib.sha256).hexdigest()
+
+    def ensure_cookie(self, req: Request, resp: Response) -> str:
+        c = req.cookies.get(AF_COOKIE)
+        if not c:
+            c = secrets.token_hex(16)
+            resp.set_cookie(AF_COOKIE, c, httponly=True, samesite="strict")
+        return c
+
+    def validate(self, req: Request, form: dict[str, str]) -> bool:
+        c = req.cookies.get(AF_COOKIE)
+        t = form.get(AF_FIELD) or req.headers.get("requestverificationtoken")
+        return bool(c and t and hmac.compare_digest(self.token_for(c), t))
+
+
+def _fmt_date(dt) -> str:
+    d = naive_utc(dt)
+    return f"{d.day:02d}-{d.month:02d}-{d.year:04d}"
+
+
+def _input_date(dt) -> str:
+    d = naive_utc(dt)
+    return f"{d.year:04d}-{d.month:02d}-{d.day:02d}"
+
+
+def create_app(argv: list[str] | None = None, client: SidecarClient | None = None, config=None,
+               overrides: dict | None = None) -> WebApp:
+    app = create_host(ROLE, HERE, argv, config=config, overrides=overrides)
+    cfg = app.config
+    mode = (cfg.get_str("Frontend:BackendMode") or "dapr").lower()
+    base = cfg.get_str("BackendApiConfig:BaseUrlExternalHttp")
+    if mode == "http" and not base:
+        raise RuntimeError("BackendApiConfig:BaseUrlExternalHttp is not defined in App Settings.")
+    gw = BackendGateway(mode, client or (SidecarClient() if mode == "dapr" else None), base)
+    app.services["backend"] = gw
+    af = Antiforgery((cfg.get_str("Frontend:AntiforgeryKey") or secrets.token_hex(32)).encode())
+    env = Environment(loader=FileSystemLoader(str(HERE / "templates")), autoescape=select_autoescape(["html"]))
+    env.filters["ddmmyyyy"] = _fmt_date
+    env.filters["inputdate"] = _input_date
+    app.mount_static("/", HERE / "wwwroot")
+
+    def render(req: Request, name: str, status: int = 200, **ctx: Any) -> Response:
+        resp = Response(b"", status, None, "text/html; charset=utf-8")
+        cookie = af.ensure_cookie(req, resp)
+        ctx.setdefault("title", "Tasks Tracker")
+        html = env.get_template(name).render(af_field=AF_FIELD, af_token=af.token_for(cookie), request=req, **ctx)
+        resp.body = html.encode()
+        return resp
+
+    def require_af(req: Request, form: dict[str, str]) -> None:
+        if not af.validate(req, form):
+            raise HTTPError(400, detail="The antiforgery token could not be validated.")
+
+    # non-development: exception handler page (reference Program.cs:32-37)
+    if not app.is_development:
+        async def error_page(req: Request, nxt) -> Response:
+            try:
+                resp = await nxt(req)
+            except HTTPError:
+                raise
+            except Exception:
+                log.exception("unhandled error on %s", req.path)
+                return render(req, "error.html", 500, request_id=req.state.get("trace_id", ""))
+            return resp
+        app.use(error_page)
+
+    # -- Index (landing) --------------------------------------------------------
+    @app.route("/", ("GET",), name="Index", include_in_schema=False)
+    async def index_get(req: Request) -> Response:
+        return render(req, "index.html")
+
+    @app.route("/", ("POST",), name="IndexPost", include_in_schema=False)
+    async def index_post(req: Request) -> Response:
+        email = req.form().get("TasksCreatedBy", "").strip()
+        resp = redirect("/Tasks/Index")
+        if email:
+            resp.set_cookie(COOKIE, email)
+        return resp
+
+    # -- Tasks/Index ----------------------------------------------------------
+    @app.route("/Tasks/Index", ("GET",), name="TasksIndex", include_in_schema=False)
+    @app.route("/Tasks", ("GET",), name="TasksIndexShort", include_in_schema=False)
+    async def tasks_index(req: Request) -> Response:
+        created_by = req.cookies.get(COOKIE)
+        if not created_by:
+            return redirect("/")
+        tasks = tasks_from_json(await gw.call("GET", f"api/tasks?createdBy={quote(created_by)}"))
+        return render(req, "tasks_index.html", tasks=tasks, created_by=created_by)
+
+    @app.route("/Tasks/Index", ("POST",), name="TasksIndexPost", include_in_schema=False)
+    async def tasks_index_post(req: Request) -> Response:
+        form = req.form()
+        require_af(req, form)
+        handler = (req.query_get("handler") or form.get("handler") or "").lower()
+        tid = req.query_get("id") or form.get("id") or ""
+        if not is_guid(tid):
+            raise HTTPError(400, detail="invalid id")
+        if handler == "delete":
+            await gw.call("DELETE", f"api/tasks/{tid}")
+        elif handler == "complete":
+            await gw.call("PUT", f"api/tasks/{tid}/markcomplete")
+        else:
+            raise HTTPError(400, detail=f"unknown handler {handler!r}")
+        return redirect("/Tasks/Index")
+
+    # -- Tasks/Create -----------------------------------------------------------
+    @app.route("/Tasks/Create", ("GET",), name="TasksCreate", include_in_schema=False)
+    async def create_get(req: Request) -> Response:
+        if not req.cookies.get(COOKIE):
+            return redirect("/")
+        return render(req, "tasks_create.html", values={}, errors={}, display=FIELD_DISPLAY)
+
+    @app.route("/Tasks/Create", ("POST",), name="TasksCreatePost", include_in_schema=False)
+    async def create_post(req: Request) -> Response:
+        form = req.form()
+        require_af(req, form)
+        values, errors = _bind(form, "TaskAdd")
+        if errors:
+            return render(req, "tasks_create.html", 200, values=values, errors=errors, display=FIELD_DISPLAY)
+        created_by = req.cookies.get(COOKIE)
+        if created_by:
+            await gw.call("POST", "api/tasks", {"taskName": values["taskName"], "taskCreatedBy": created_by,
+                                                "taskDueDate": values["taskDueDate"], "taskAssignedTo": values["taskAssignedTo"]})
+        return redirect("/Tasks/Index")
+
+    # -- Tasks/Edit ---------------------------------------------------------------
+    @app.route("/Tasks/Edit/{id:guid}", ("GET",), name="TasksEdit", include_in_schema=False)
+    async def edit_get(req: Request) -> Response:
+        if not req.cookies.get(COOKIE):
+            return redirect("/")
+        data = await gw.call("GET", f"api/tasks/{req.path_params['id']}")
+        if not data:
+            return render(req, "not_found.html", 404)
+        t = TaskModel.model_validate(data)
+        values = {"taskId": str(t.task_id), "taskName": t.task_name, "taskAssignedTo": t.task_assigned_to,
+                  "taskDueDate": _input_date(t.task_due_date)}
+        return render(req, "tasks_edit.html", values=values, errors={}, display=FIELD_DISPLAY)
+
+    @app.route("/Tasks/Edit/{id:guid}", ("POST",), name="TasksEditPost", include_in_schema=False)
+    async def edit_post(req: Request) -> Response:
+        form = req.form()
+        require_af(req, form)
+        values, errors = _bind(form, "TaskUpdate")
+        values["taskId"] = form.get("TaskUpdate.TaskId") or str(req.path_params["id"])
+        if errors:
+            return render(req, "tasks_edit.html", 200, values=values, errors=errors, display=FIELD_DISPLAY)
+        await gw.call("PUT", f"api/tasks/{values['taskId']}", {"taskId": values["taskId"], "taskName": values["taskName"],
+                                                              "taskDueDate": values["taskDueDate"],
+                                                              "taskAssignedTo": values["taskAssignedTo"]})
+        return redirect("/Tasks/Index")
+
+    # -- Privacy / Error -----------------------------------------------------------
+    @app.route("/Privacy", ("GET",), name="Privacy", include_in_schema=False)
+    async def privacy(req: Request) -> Response:
+        return render(req, "privacy.html", title="Privacy Policy")
+
+    @app.route("/Error", ("GET",), name="Error", include_in_schema=False)
+    async def error(req: Request) -> Response:
+        return render(req, "error.html", request_id=req.state.get("trace_id", ""))
+
+    app.on_shutdown.append(gw.close)
+    return app
+
+
+def _bind(form: dict[str, str], prefix: str) -> tuple[dict[str, Any], dict[str, str]]:
+    """Razor model binding for ``TaskAdd.*`` / ``TaskUpdate.*`` fields + ``[Required]``."""
+    values: dict[str, Any] = {}
+    errors: dict[str, str] = {}
+    for field in REQUIRED_FIELDS:
+        raw = form.get(f"{prefix}.{field[0].upper()}{field[1:]}", "").strip()
+        values[field] = raw
+        if not raw:
+            errors[field] = f"The {FIELD_DISPLAY[field]} field is required."
+    if values.get("taskDueDate") and "taskDueDate" not in errors:
+        try:
+            values["taskDueDate"] = parse_datetime(values["taskDueDate"]).strftime("%Y-%m-%dT%H:%M:%S")
+        except ValueError:
+            errors["taskDueDate"] = f"The value '{values['taskDueDate']}' is not valid for {FIELD_DISPLAY['taskDueDate']}."
+    return values, errors
+
+
+def main(argv: list[str] | None = None) -> None:
+    import sys
+    run_host(create_app(sys.argv[1:] if argv is None else argv))
+
+
+if __name__ == "__main__":
+    main()
