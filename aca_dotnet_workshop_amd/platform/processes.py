@@ -1,0 +1,231 @@
+"""Multi-process local stack: the production process topology on one host.
+
+Every app replica is a pair of OS processes -- the sidecar (``sidecar run``) and the app
+(its child) -- talking over Unix sockets; sidecars find each other through the shared
+registry directory and reach the backing-services process over HTTP.  This is the
+``dapr run`` x N topology of the reference's local dev loop (snippets/dapr-run-*.md,
+.vscode/tasks.json:126-165) and the unit the platform layer scales.
+
+Children are started with ``subprocess.Popen`` (fork+exec of a fresh interpreter), never
+by ``exec`` in the calling process.
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import tempfile
+import time
+import urllib.request
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any
+
+REPO_ROOT = Path(__file__).resolve().parents[2]
+SERVICE_MODULES = {
+    "tasksmanager-backend-api": "aca_dotnet_workshop_amd.services.backend_api",
+    "tasksmanager-backend-processor": "aca_dotnet_workshop_amd.services.processor",
+    "tasksmanager-frontend-webapp": "aca_dotnet_workshop_amd.services.frontend",
+}
+
+
+@dataclass
+class ReplicaProc:
+    app_id: str
+    name: str
+    proc: subprocess.Popen
+    sidecar_uds: str
+    http_port: int | None = None
+    app_port_file: str | None = None
+    started: float = field(default_factory=time.time)
+
+    @property
+    def app_port(self) -> int | None:
+        if self.app_port_file and os.path.exists(self.app_port_file):
+            try:
+                return int(Path(self.app_port_file).read_text())
+            except ValueError:
+                return None
+        return None
+
+    def alive(self) -> bool:
+        return self.proc.poll() is None
+
+
+class LocalStack:
+    def __init__(self, root: str | os.PathLike | None = None, components: list[str] | None = None,
+                 env: dict[str, str] | None = None, log_dir: str | None = None, quiet: bool = True) -> None:
+        self.root = Path(root or tempfile.mkdtemp(prefix="tt-stack-"))
+        self.root.mkdir(parents=True, exist_ok=True)
+        self.sock_dir = Path(tempfile.mkdtemp(prefix="tts-"))
+        self.registry = self.root / "registry"
+        self.components = components or [str(REPO_ROOT / "deploy" / "components")]
+        self.base_env = dict(os.environ)
+        self.base_env["PYTHONPATH"] = str(REPO_ROOT) + os.pathsep + self.base_env.get("PYTHONPATH", "")
+        self.base_env.update(env or {})
+        self.log_dir = Path(log_dir) if log_dir else self.root / "logs"
+        self.log_dir.mkdir(parents=True, exist_ok=True)
+        self.quiet = quiet
+        self.backing_proc: subprocess.Popen | None = None
+        self.backing_url: str | None = None
+        self.replicas: dict[str, list[ReplicaProc]] = {}
+        self._seq = 0
+
+    # -- processes --------------------------------------------------------------
+    def _spawn(self, args: list[str], env: dict[str, str], log_name: str) -> subprocess.Popen:
+        out = open(self.log_dir / f"{log_name}.log", "ab")
+        return subprocess.Popen(args, env=env, stdout=out, stderr=subprocess.STDOUT, cwd=str(REPO_ROOT),
+                                start_new_session=True)
+
+    def start_backing(self, data_dir: str | None = None, policy: dict[str, Any] | None = None,
+                      timeout: float = 60.0) -> str:
+        pf = self.root / "backing.port"
+        if pf.exists():
+            pf.unlink()
+        args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
+        if data_dir:
+            args += ["--data-dir", data_dir]
+        if policy:
+            pp = self.root / "policy.json"
+            pp.write_text(json.dumps(policy))
+            args += ["--policy", str(pp)]
+        self.backing_proc = self._spawn(args, self.base_env, "backing")
+        port = _wait_file(pf, timeout, self.backing_proc)
+        self.backing_url = f"http://127.0.0.1:{port}"
+        return self.backing_url
+
+    def start_replica(self, app_id: str, config: dict[str, str] | None = None, extra_env: dict[str, str] | None = None,
+                      http_port: int | None = None, module: str | None = None, log_level: str = "warning",
+                      identity: str | None = None, external_port: int | None = None) -> ReplicaProc:
+        idx = self._seq
+        self._seq += 1
+        name = f"{app_id}-{idx}"
+        app_uds = str(self.sock_dir / f"{name}.a.sock")
+        port_file = str(self.root / f"{name}.app.port")
+        env = dict(self.base_env)
+        env.update({"TT_BACKING_URL": self.backing_url or "", "TT_REGISTRY_DIR": str(self.registry),
+                    "TT_REPLICA_NAME": name, "TT_APP_UDS": app_uds, "TT_PORT_FILE": port_file,
+                    "TT_IDENTITY": identity or app_id})
+        for k, v in (config or {}).items():
+            env[k.replace(":", "__")] = str(v)
+        env.update(extra_env or {})
+        urls = f"http://127.0.0.1:{external_port if external_port is not None else 0}"
+        args = [sys.executable, "-m", "aca_dotnet_workshop_amd.sidecar", "run", "--app-id", app_id,
+                "--app-uds", app_uds, "--dapr-http-port", str(http_port if http_port is not None else 0),
+                "--unix-socket-dir", str(self.sock_dir), "--replica-name", name, "--log-level", log_level]
+        for c in self.components:
+            args += ["--resources-path", c]
+        args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
+        p = self._spawn(args, env, name)
+        rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)
+        self.replicas.setdefault(app_id, []).append(rp)
+        return rp
+
+    def wait_ready(self, timeout: float = 90.0, replicas: list[ReplicaProc] | None = None) -> None:
+        """Sidecar socket up and the app handshake (subscriptions/bindings) complete."""
+        deadline = time.time() + timeout
+        pending = list(replicas or [r for rs in self.replicas.values() for r in rs])
+        while pending:
+            for r in list(pending):
+                if not r.alive():
+                    raise RuntimeError(f"replica {r.name} exited with {r.proc.returncode}; "
+                                       f"see {self.log_dir / (r.name + '.log')}")
+                meta = uds_get_json(r.sidecar_uds, "/v1.0/metadata")
+                if meta and meta.get("extended", {}).get("appReady"):
+                    pending.remove(r)
+            if time.time() > deadline:
+                raise TimeoutError(f"replicas not ready: {[r.name for r in pending]}")
+            time.sleep(0.05)
+
+    def stop_replica(self, r: ReplicaProc, timeout: float = 10.0) -> None:
+        _terminate(r.proc, timeout)
+        if r in self.replicas.get(r.app_id, []):
+            self.replicas[r.app_id].remove(r)
+
+    def stop(self) -> None:
+        for rs in list(self.replicas.values()):
+            for r in list(rs):
+                try:
+                    r.proc.send_signal(signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        for rs in list(self.replicas.values()):
+            for r in list(rs):
+                _terminate(r.proc, 10.0)
+        self.replicas.clear()
+        if self.backing_proc is not None:
+            _terminate(self.backing_proc, 10.0)
+            self.backing_proc = None
+        import shutil
+        shutil.rmtree(self.sock_dir, ignore_errors=True)
+
+    def __enter__(self) -> "LocalStack":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+
+def _terminate(p: subprocess.Popen, timeout: float) -> None:
+    if p.poll() is not None:
+        return
+    try:
+        p.send_signal(signal.SIGTERM)
+        p.wait(timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.wait(5)
+    except ProcessLookupError:
+        pass
+
+
+def _wait_file(path: Path, timeout: float, proc: subprocess.Popen | None = None) -> int:
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if path.exists():
+            try:
+                return int(path.read_text())
+            except ValueError:
+                pass
+        if proc is not None and proc.poll() is not None:
+            raise RuntimeError(f"process exited with {proc.returncode} before writing {path}")
+        time.sleep(0.02)
+    raise TimeoutError(f"{path} not written in {timeout}s")
+
+
+def uds_get_json(sock: str, path: str, timeout: float = 2.0) -> Any:
+    """Tiny blocking HTTP GET over a Unix socket (readiness probes)."""
+    import socket
+    if not os.path.exists(sock):
+        return None
+    try:
+        s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        s.settimeout(timeout)
+        s.connect(sock)
+        s.sendall(f"GET {path} HTTP/1.1\r\nHost: localhost\r\nConnection: close\r\n\r\n".encode())
+        data = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        s.close()
+        head, _, body = data.partition(b"\r\n\r\n")
+        if not head.startswith(b"HTTP/1.1 200"):
+            return None
+        return json.loads(body) if body else None
+    except (OSError, ValueError):
+        return None
+
+
+def http_get_json(url: str, timeout: float = 2.0) -> Any:
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:
+            return json.loads(r.read() or b"null")
+    except (OSError, ValueError):
+        return None

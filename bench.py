@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: end-to-end task-creation throughput of the Tasks Tracker mesh.
+
+The reference publishes no throughput number (BASELINE.md "Not published"),
+so this measures the survey's flagship flow (SURVEY.md §3.1 ``createTask``) on our stack
+and reports it as a *new* measurement (``vs_baseline: null``):
+
+    client -> API sidecar (invoke) -> Backend API -> sidecar state save -> backing "Cosmos"
+                                                 -> sidecar publish    -> backing "Service Bus"
+           -> processor sidecar (peek-lock receive) -> Processor /api/tasksnotifier/tasksaved -> complete
+
+One step = ``--batch`` createTask requests issued with ``--concurrency`` in flight, and the
+step ends only when the processor's subscription has completed every message of the batch
+(persisted AND delivered AND acknowledged).  Each rank runs its own full environment
+(backing services + API/processor apps + their sidecars as separate OS processes) -- weak
+scaling, like adding ACA environments.  Rank 0 prints ONE JSON line with the aggregate
+tasks/s over all ranks (time = max over ranks).
+
+    python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse() -> argparse.Namespace:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512, help="createTask requests per step per rank")
+    ap.add_argument("--concurrency", type=int, default=64, help="requests in flight per rank")
+    ap.add_argument("--api-replicas", type=int, default=1)
+    ap.add_argument("--processor-replicas", type=int, default=1)
+    ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
+    return ap.parse_args()
+
+
+class Dist:
+    """Rank coordination over torch.distributed (gloo: this workload has no tensors)."""
+
+    def __init__(self) -> None:
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", init_method="env://")
+            self.pg = dist
+
+    def barrier(self) -> None:
+        if self.pg is not None:
+            self.pg.barrier()
+
+    def max(self, v: float) -> float:
+        if self.pg is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.pg is None:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self) -> None:
+        if self.pg is not None:
+            self.pg.destroy_process_group()
+
+
+def device_sync() -> None:
+    """Contract: bracket the timed region with a device sync when a GPU is present."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+async def run_steps(sock: str, counts_url: str, entity: str, steps: int, batch: int, conc: int,
+                    lat: list[float] | None) -> float:
+    from aca_dotnet_workshop_amd.web.client import HttpClient
+    c = HttpClient()
+    url = f"unix:{sock}:/v1.0/invoke/tasksmanager-backend-api/method/api/tasks"
+    hdr = {"Content-Type": "application/json"}
+    bodies = [json.dumps({"taskName": f"bench task {i}", "taskCreatedBy": f"user{i % 97}@bench.local",
+                          "taskDueDate": "2030-01-01T00:00:00", "taskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
+              for i in range(batch)]
+
+    async def completed() -> int:
+        r = await c.get(counts_url)
+        return int(r.json()["completed"])
+
+    base = await completed()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        it = iter(range(batch))
+
+        async def worker() -> None:
+            for i in it:
+                t = time.perf_counter()
+                r = await c.post(url, body=bodies[i], headers=hdr)
+                if r.status != 201:
+                    raise RuntimeError(f"createTask failed: {r.status} {r.body[:200]!r}")
+                if lat is not None:
+                    lat.append(time.perf_counter() - t)
+        await asyncio.gather(*(worker() for _ in range(conc)))
+        base += batch
+        while await completed() < base:  # end-to-end: wait until the processor acked the batch
+            await asyncio.sleep(0.002)
+    dt = time.perf_counter() - t0
+    await c.close()
+    return dt
+
+
+def main() -> None:
+    a = parse()
+    d = Dist()
+    n = d.world if d.world > 1 else a.gpus
+    from aca_dotnet_workshop_amd.platform.processes import LocalStack
+    cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
+    stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
+    try:
+        backing = stack.start_backing()
+        for _ in range(a.api_replicas):
+            stack.start_replica("tasksmanager-backend-api", cfg)
+        for _ in range(a.processor_replicas):
+            stack.start_replica("tasksmanager-backend-processor", cfg)
+        stack.wait_ready()
+        sock = stack.replicas["tasksmanager-backend-api"][0].sidecar_uds
+        entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
+        counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
+        if a.warmup:
+            asyncio.run(run_steps(sock, counts_url, entity, a.warmup, a.batch, a.concurrency, None))
+        lat: list[float] = []
+        d.barrier()
+        device_sync()
+        dt = asyncio.run(run_steps(sock, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
+        device_sync()
+        d.barrier()
+        dt_max = d.max(dt)
+        lat.sort()
+        p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
+        p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0
+        total = a.batch * a.steps * (d.world if d.world > 1 else 1)
+        value = total / dt_max if dt_max > 0 else 0.0
+        if d.rank == 0:
+            print(json.dumps({
+                "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "n/a (JSON over HTTP)",
+                "data": "synthetic createTask payloads",
+                "config": {"model": "tasks-tracker createTask flow (API+sidecars+backing+processor)",
+                           "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
+                           "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
+                           "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
+                           "processor_replicas": a.processor_replicas, "create_latency_p50_ms": round(p50, 3),
+                           "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput"}}),
+                flush=True)
+    finally:
+        stack.stop()
+        d.close()
+
+
+if __name__ == "__main__":
+    main()
