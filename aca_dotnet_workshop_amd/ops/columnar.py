@@ -1,0 +1,452 @@
+"""Columnar, dictionary-encoded mirror of a state-store collection + the query compiler.
+
+Why: the reference's queries (``EQ taskCreatedBy``, ``EQ taskDueDate`` then in-app
+filtering, Services/TasksStoreManager.cs:54-69, 104-139) are whole-collection scans in
+Cosmos; equality is served by the native store's hash indexes, but range/NEQ/OR filters,
+the corrected overdue sweep (``taskDueDate < today AND NOT isCompleted AND NOT isOverDue``)
+and dashboard aggregates (open tasks per assignee) are O(collection).  Those run here,
+on the GPU when one is present (``ops/hip/query_scan.hip``), with a NumPy executor of the
+*same* compiled program as the CPU path and as the correctness oracle.
+
+Encoding: each indexed JSON path is an int32 column of dictionary ids (-1 = path missing).
+Equality and ordering semantics are evaluated on the host against the (small) dictionary,
+exactly mirroring the native engine's ``compare`` (type order null < bool < number < string;
+numbers by value; ranges only between like types), producing one bitmap per leaf.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass
+from typing import Any, Iterable
+
+import numpy as np
+
+OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ = 1, 2, 3, 4, 5, 6
+TILE = 4096
+_TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
+
+
+class Unsupported(Exception):
+    """Filter cannot run on the columnar engine (caller falls back to the native store)."""
+
+
+def vkey(v: Any) -> str:
+    """Canonical dictionary key with the native engine's equality semantics."""
+    if v is None:
+        return "n"
+    if isinstance(v, bool):
+        return "b1" if v else "b0"
+    if isinstance(v, (int, float)):
+        return "d" + repr(float(v))
+    if isinstance(v, str):
+        return "s" + v
+    return "j" + json.dumps(_norm(v), separators=(",", ":"))
+
+
+def _norm(v: Any) -> Any:
+    if isinstance(v, bool) or v is None or isinstance(v, str):
+        return v
+    if isinstance(v, (int, float)):
+        return float(v)
+    if isinstance(v, list):
+        return [_norm(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _norm(x) for k, x in v.items()}
+    return v
+
+
+def type_rank(v: Any) -> int:
+    return _TYPE_ORDER.get(type(v), 6)
+
+
+def compare(a: Any, b: Any) -> int:
+    ta, tb = type_rank(a), type_rank(b)
+    if ta != tb:
+        return -1 if ta < tb else 1
+    if ta == 0:
+        return 0
+    if ta in (1, 2, 3):
+        return (a > b) - (a < b)
+    if ta == 4:
+        for x, y in zip(a, b):
+            c = compare(x, y)
+            if c:
+                return c
+        return (len(a) > len(b)) - (len(a) < len(b))
+    sa, sb = json.dumps(a, separators=(",", ":")), json.dumps(b, separators=(",", ":"))
+    return (sa > sb) - (sa < sb)
+
+
+_MISSING = object()
+
+
+def get_path(doc: Any, path: str) -> Any:
+    cur = doc
+    for seg in path.split("."):
+        if isinstance(cur, dict):
+            if seg in cur:
+                cur = cur[seg]
+            else:
+                low = seg.lower()
+                for k, v in cur.items():
+                    if k.lower() == low:
+                        cur = v
+                        break
+                else:
+                    return _MISSING
+        elif isinstance(cur, list) and seg.isdigit():
+            i = int(seg)
+            if i >= len(cur):
+                return _MISSING
+            cur = cur[i]
+        else:
+            return _MISSING
+    return cur
+
+
+class Column:
+    def __init__(self, path: str) -> None:
+        self.path = path
+        self.ids: dict[str, int] = {}
+        self.values: list[Any] = []
+        self._num_cache: np.ndarray | None = None
+        self._rank_cache: np.ndarray | None = None
+
+    def encode(self, v: Any) -> int:
+        if v is _MISSING:
+            return -1
+        k = vkey(v)
+        i = self.ids.get(k)
+        if i is None:
+            i = self.ids[k] = len(self.values)
+            self.values.append(v)
+            self._num_cache = None
+            self._rank_cache = None
+        return i
+
+    def lookup(self, v: Any) -> int:
+        return self.ids.get(vkey(v), -2)
+
+    def satisfying(self, op: str, val: Any) -> np.ndarray:
+        """Boolean array over the dictionary: which ids satisfy ``<value> op val``."""
+        n = len(self.values)
+        out = np.zeros(n, dtype=bool)
+        if op == "IN":
+            for x in val:
+                i = self.lookup(x)
+                if i >= 0:
+                    out[i] = True
+            return out
+        tv = type_rank(val)
+        if tv == 2:  # numeric fast path (vectorised)
+            if self._num_cache is None:
+                self._num_cache = np.array([float(x) if type_rank(x) == 2 else np.nan for x in self.values],
+                                           dtype=np.float64)
+            arr = self._num_cache
+            with np.errstate(invalid="ignore"):
+                res = {"GT": arr > val, "GTE": arr >= val, "LT": arr < val, "LTE": arr <= val}[op]
+            return res & ~np.isnan(arr)
+        for i, x in enumerate(self.values):
+            if type_rank(x) != tv:
+                continue
+            c = compare(x, val)
+            out[i] = {"GT": c > 0, "GTE": c >= 0, "LT": c < 0, "LTE": c <= 0}[op]
+        return out
+
+    def missing_rank(self) -> int:
+        """A missing path sorts like JSON null (the native engine compares it as null)."""
+        i = self.ids.get("n")
+        return int(self.ranks()[i]) if i is not None else 0
+
+    def ranks(self) -> np.ndarray:
+        """Sort rank of every dictionary id (ties share a rank, ranks start at 1)."""
+        if self._rank_cache is None:
+            import functools
+            order = sorted(range(len(self.values)), key=functools.cmp_to_key(lambda a, b: compare(self.values[a], self.values[b])))
+            r = np.empty(len(order), dtype=np.int64)
+            rank = 0
+            for pos, i in enumerate(order):
+                if pos and compare(self.values[order[pos - 1]], self.values[i]) != 0:
+                    rank += 1
+                r[i] = rank + 1  # 0 reserved for missing (sorts like null, first)
+            self._rank_cache = r
+        return self._rank_cache
+
+
+@dataclass
+class Program:
+    code: np.ndarray      # [L, 4] int32
+    bitmaps: np.ndarray   # int32 words (uint32 bit patterns)
+    columns: list[int]
+
+
+class ColumnarIndex:
+    def __init__(self, paths: Iterable[str] = (), capacity: int = TILE) -> None:
+        self.columns: list[Column] = []
+        self.col_of: dict[str, int] = {}
+        self.cap = max(TILE, (capacity + TILE - 1) // TILE * TILE)
+        self.ids = np.full((0, self.cap), -1, dtype=np.int32)
+        self.live = np.zeros(self.cap, dtype=np.int32)
+        self.seq = np.zeros(self.cap, dtype=np.int64)
+        self._next_seq = 0
+        self.keys: list[str] = []
+        self.row_of: dict[str, int] = {}
+        self.docs: list[Any] = []
+        self.n = 0
+        self.version = 0
+        self._dev = None  # device mirror state
+        for p in paths:
+            self.add_column(p)
+
+    # -- maintenance ----------------------------------------------------------
+    def add_column(self, path: str) -> int:
+        if path in self.col_of:
+            return self.col_of[path]
+        c = Column(path)
+        idx = len(self.columns)
+        self.columns.append(c)
+        self.col_of[path] = idx
+        col = np.full((1, self.cap), -1, dtype=np.int32)
+        for r in range(self.n):
+            if self.live[r]:
+                col[0, r] = c.encode(get_path(self.docs[r], path))
+        self.ids = np.concatenate([self.ids, col], axis=0)
+        self.version += 1
+        return idx
+
+    def _grow(self, need: int) -> None:
+        if need <= self.cap:
+            return
+        cap = self.cap
+        while cap < need:
+            cap *= 2
+        ids = np.full((len(self.columns), cap), -1, dtype=np.int32)
+        ids[:, :self.n] = self.ids[:, :self.n]
+        live = np.zeros(cap, dtype=np.int32)
+        live[:self.n] = self.live[:self.n]
+        seq = np.zeros(cap, dtype=np.int64)
+        seq[:self.n] = self.seq[:self.n]
+        self.ids, self.live, self.seq, self.cap = ids, live, seq, cap
+
+    def upsert(self, key: str, doc: Any) -> None:
+        old = self.row_of.get(key)
+        if old is not None:
+            self.live[old] = 0
+            self.docs[old] = None
+            seq = int(self.seq[old])  # an update keeps the key's original position (native engine semantics)
+        else:
+            self._next_seq += 1
+            seq = self._next_seq
+        self._grow(self.n + 1)
+        r = self.n
+        self.seq[r] = seq
+        for i, c in enumerate(self.columns):
+            self.ids[i, r] = c.encode(get_path(doc, c.path))
+        self.live[r] = 1
+        self.keys.append(key)
+        self.docs.append(doc)
+        self.row_of[key] = r
+        self.n += 1
+        self.version += 1
+
+    def delete(self, key: str) -> None:
+        r = self.row_of.pop(key, None)
+        if r is not None:
+            self.live[r] = 0
+            self.docs[r] = None
+            self.version += 1
+
+    def bulk_load(self, items: Iterable[tuple[str, Any]]) -> None:
+        for k, d in items:
+            self.upsert(k, d)
+
+    def live_rows(self) -> int:
+        return len(self.row_of)
+
+    def compact(self) -> None:
+        """Drop tombstones (rows are renumbered in order)."""
+        keep = np.nonzero(self.live[:self.n])[0]
+        self.ids[:, :len(keep)] = self.ids[:, keep]
+        self.ids[:, len(keep):] = -1
+        self.seq[:len(keep)] = self.seq[keep]
+        self.live[:] = 0
+        self.live[:len(keep)] = 1
+        self.keys = [self.keys[i] for i in keep]
+        self.docs = [self.docs[i] for i in keep]
+        self.row_of = {k: i for i, k in enumerate(self.keys)}
+        self.n = len(keep)
+        self.version += 1
+
+    # -- compilation ---------------------------------------------------------
+    def compile(self, flt: Any) -> Program:
+        code: list[list[int]] = []
+        words: list[np.ndarray] = []
+        nwords = [0]
+        used: list[int] = []
+        depth = [0, 0]
+
+        def push() -> None:
+            depth[0] += 1
+            depth[1] = max(depth[1], depth[0])
+
+        def leaf_bitmap(col: int, sat: np.ndarray) -> None:
+            nbits = len(sat)
+            padded = np.zeros(((nbits + 31) // 32) * 32, dtype=bool)
+            padded[:nbits] = sat
+            w = np.packbits(padded, bitorder="little").view("<u4").astype(np.uint32)
+            if w.size == 0:
+                w = np.zeros(1, dtype=np.uint32)
+            code.append([OP_LEAF, col, nwords[0], nbits])
+            words.append(w)
+            nwords[0] += w.size
+            push()
+
+        def emit(f: Any) -> None:
+            if not isinstance(f, dict) or len(f) != 1:
+                raise Unsupported("filter node must be a single-operator object")
+            (op, arg), = f.items()
+            op = op.upper()
+            if op in ("AND", "OR"):
+                if not isinstance(arg, list) or not arg:
+                    raise Unsupported(f"{op} expects a non-empty array")
+                for x in arg:
+                    emit(x)
+                n = len(arg)
+                if n > 1:
+                    code.append([OP_AND if op == "AND" else OP_OR, n, 0, 0])
+                    depth[0] -= n - 1
+                return
+            if not isinstance(arg, dict) or len(arg) != 1:
+                raise Unsupported(f"{op} expects {{path: value}}")
+            (path, val), = arg.items()
+            col = self.col_of.get(path)
+            if col is None:
+                col = self.add_column(path)
+            used.append(col)
+            c = self.columns[col]
+            if op in ("EQ", "NEQ"):
+                if isinstance(val, (list, dict)):
+                    raise Unsupported("structured equality")
+                code.append([OP_EQ, col, c.lookup(val), 0])
+                push()
+                if op == "NEQ":
+                    code.append([OP_NOT, 0, 0, 0])
+            elif op == "IN":
+                if not isinstance(val, list):
+                    raise Unsupported("IN expects a list")
+                leaf_bitmap(col, c.satisfying("IN", val))
+            elif op in ("GT", "GTE", "LT", "LTE"):
+                leaf_bitmap(col, c.satisfying(op, val))
+            else:
+                raise Unsupported(f"operator {op}")
+
+        if not flt:
+            code.append([OP_TRUE, 0, 0, 0])
+            push()
+        else:
+            emit(flt)
+        if depth[1] > 32:
+            raise Unsupported("filter nesting too deep for the device stack")
+        bitmaps = np.concatenate(words) if words else np.zeros(1, dtype=np.uint32)
+        return Program(np.asarray(code, dtype=np.int32), bitmaps.view(np.int32), sorted(set(used)))
+
+    # -- execution -------------------------------------------------------------
+    def select_numpy(self, prog: Program) -> np.ndarray:
+        """Reference executor: identical semantics to the HIP kernel."""
+        n = self.n
+        stack: list[np.ndarray] = []
+        bm = prog.bitmaps.view(np.uint32)
+        for op, a, b, c in prog.code.tolist():
+            if op == OP_EQ:
+                stack.append(self.ids[a, :n] == b)
+            elif op == OP_LEAF:
+                v = self.ids[a, :n]
+                ok = (v >= 0) & (v < c)
+                vv = np.where(ok, v, 0)
+                bits = (bm[b + (vv >> 5)] >> (vv & 31).astype(np.uint32)) & 1
+                stack.append(ok & (bits == 1))
+            elif op in (OP_AND, OP_OR):
+                xs = stack[-a:]
+                del stack[-a:]
+                r = xs[0].copy()
+                for x in xs[1:]:
+                    r = (r & x) if op == OP_AND else (r | x)
+                stack.append(r)
+            elif op == OP_NOT:
+                stack[-1] = ~stack[-1]
+            else:
+                stack.append(np.ones(n, dtype=bool))
+        sel = stack[-1] & (self.live[:n] != 0)
+        return np.nonzero(sel)[0].astype(np.int32)
+
+    # device mirror -------------------------------------------------------------
+    def to_device(self, kernels) -> tuple[Any, Any]:
+        torch = kernels.torch
+        st = self._dev
+        if st is None or st["version"] != self.version or st["shape"] != self.ids.shape:
+            cols = torch.from_numpy(np.ascontiguousarray(self.ids)).to(kernels.device, non_blocking=False)
+            live = torch.from_numpy(self.live).to(kernels.device)
+            self._dev = st = {"version": self.version, "shape": self.ids.shape, "cols": cols, "live": live}
+        return st["cols"], st["live"]
+
+    def select_gpu(self, prog: Program, kernels) -> np.ndarray:
+        torch = kernels.torch
+        cols, live = self.to_device(kernels)
+        code = torch.from_numpy(prog.code).to(kernels.device)
+        bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
+        out = kernels.select(cols, live, self.n, code, bitmaps)
+        return out.cpu().numpy()
+
+    def group_count_gpu(self, prog: Program, group_path: str, kernels) -> dict[str, int]:
+        torch = kernels.torch
+        g = self.add_column(group_path)
+        cols, live = self.to_device(kernels)
+        code = torch.from_numpy(prog.code).to(kernels.device)
+        bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
+        _, mask = kernels.select(cols, live, self.n, code, bitmaps, return_mask=True)
+        col = self.columns[g]
+        if mask is None or not col.values:
+            return {}
+        counts = kernels.group_count(cols[g], mask, self.n, len(col.values)).cpu().numpy()
+        return {json.dumps(col.values[i]): int(x) for i, x in enumerate(counts) if x}
+
+    def group_count_numpy(self, prog: Program, group_path: str) -> dict[str, int]:
+        g = self.add_column(group_path)
+        rows = self.select_numpy(prog)
+        col = self.columns[g]
+        ids = self.ids[g, rows]
+        ids = ids[ids >= 0]
+        cnt = np.bincount(ids, minlength=len(col.values))
+        return {json.dumps(col.values[i]): int(x) for i, x in enumerate(cnt) if x}
+
+    # -- full query --------------------------------------------------------------
+    def order(self, rows: np.ndarray, sort: list[dict[str, Any]] | None) -> np.ndarray:
+        if rows.size == 0:
+            return rows
+        rows = rows[np.argsort(self.seq[rows], kind="stable")]  # insertion order, then stable sort keys
+        if not sort:
+            return rows
+        keys = []
+        for s in reversed(sort):  # np.lexsort: last key is primary
+            col = self.add_column(s["key"])
+            ranks = self.columns[col].ranks()
+            ids = self.ids[col, rows]
+            miss = self.columns[col].missing_rank()
+            r = np.where(ids >= 0, ranks[np.maximum(ids, 0)] if ranks.size else miss, miss)
+            if str(s.get("order", "ASC")).upper() == "DESC":
+                r = -r
+            keys.append(r)
+        return rows[np.lexsort(keys)]
+
+    def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
+        """Returns (keys in result order for the requested page, continuation token)."""
+        prog = self.compile(q.get("filter") or {})
+        rows = self.select_gpu(prog, kernels) if kernels is not None else self.select_numpy(prog)
+        rows = self.order(rows, q.get("sort"))
+        page = q.get("page") or {}
+        limit = int(page.get("limit") or 0)
+        offset = int(page.get("token") or 0)
+        end = min(rows.size, offset + limit) if limit else rows.size
+        sel = rows[offset:end]
+        token = str(end) if limit and end < rows.size else None
+        return [self.keys[i] for i in sel.tolist()], token
