@@ -280,7 +280,16 @@ class PubSub(ComponentBase):
                         on_drop=None) -> Consumer:
         group = self.consumer_group()
         lock = self.lock_ms()
-        await self.transport.ensure_subscription(topic, group, lock, self.max_delivery())
+        if not self.comp.get_bool("disableEntityManagement"):
+            try:
+                await self.transport.ensure_subscription(topic, group, lock, self.max_delivery())
+            except Exception as e:
+                # receive-only identities cannot manage entities; the subscription is expected
+                # to be provisioned by the environment (IaC), exactly like Dapr on Azure.
+                if getattr(e, "status", None) != 403:
+                    raise
+                log.info("%s: no permission to manage %s/subscriptions/%s; using the provisioned entity",
+                         self.name, topic, group)
         c = Consumer(self.transport, f"{topic}/subscriptions/{group}", handler,
                      max_concurrent=self.comp.get_int("maxConcurrentHandlers", self.default_concurrency) or 1 << 20,
                      prefetch=self.comp.get_int("maxActiveMessages", 64),

@@ -296,9 +296,23 @@ class Sidecar:
                 log.warning("sidecar %s: subscription to %s/%s skipped: pubsub component not loaded for this app",
                             self.app_id, s.pubsubname, s.topic)
                 continue
+            await self._subscribe_with_retry(ps, s)
+
+    async def _subscribe_with_retry(self, ps: PubSub, s: SubscriptionSpec, delay: float = 1.0) -> None:
+        try:
             c = await ps.subscribe(s.topic, self._make_delivery(ps, s), s.metadata, self._make_dead_letter(ps, s))
-            self.consumers.append(c)
-            log.info("sidecar %s: subscribed %s/%s -> /%s", self.app_id, s.pubsubname, s.topic, s.route)
+        except Exception as e:
+            log.error("sidecar %s: subscribing %s/%s failed (%s); retrying in %.0fs", self.app_id, s.pubsubname,
+                      s.topic, e, delay)
+
+            async def later() -> None:
+                await asyncio.sleep(delay)
+                if not self.stopped.is_set():
+                    await self._subscribe_with_retry(ps, s, min(delay * 2, 30.0))
+            self._bg.append(asyncio.ensure_future(later()))
+            return
+        self.consumers.append(c)
+        log.info("sidecar %s: subscribed %s/%s -> /%s", self.app_id, s.pubsubname, s.topic, s.route)
 
     def _make_delivery(self, ps: PubSub, sub: SubscriptionSpec):
         raw_sub = sub.metadata.get("rawPayload", "").lower() == "true"

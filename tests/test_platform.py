@@ -1,0 +1,169 @@
+"""Platform layer: manifest (Bicep equivalent), KEDA/HPA scaler semantics, and a
+multi-process environment deployed by the controller (ACA equivalent) -- module 2
+(internal ingress 403), module 9 (KEDA 1 -> 5 -> 1 replicas), module 10 (what-if/apply).
+"""
+import asyncio
+import json
+import os
+import signal
+import time
+import urllib.error
+import urllib.request
+from pathlib import Path
+
+import pytest
+
+from aca_dotnet_workshop_amd.platform.manifest import (ManifestError, load_manifest, substitute, unique_string,
+                                                       validate, what_if)
+from aca_dotnet_workshop_amd.platform.scaler import Autoscaler, ScaleRule, cron_metric
+
+from helpers import run
+
+ROOT = Path(__file__).resolve().parents[1]
+MAIN = ROOT / "deploy" / "main.yaml"
+PARAMS = ROOT / "deploy" / "main.parameters.json"
+
+
+def test_manifest_parameters_and_functions():
+    m = load_manifest(MAIN, PARAMS, {"sendGridKeySecretValue": "SG.key", "prefix": "dev-"})
+    assert m.name == "dev-cae-tasks-tracker"
+    proc = m.app("tasksmanager-backend-processor")
+    env = {e["name"]: e["value"] for e in proc["env"]}
+    assert env["SendGrid__IntegrationEnabled"] is True  # notEmpty(sendGridKeySecretValue)
+    assert proc["scale"]["maxReplicas"] == 5 and proc["scale"]["rules"][0]["custom"]["metadata"]["messageCount"] == 10
+    kv = m.resources["keyVault"]["secrets"][0]
+    assert kv["value"] == "SG.key"
+    m2 = load_manifest(MAIN, PARAMS)
+    assert m2.resources["keyVault"]["secrets"][0]["value"] == "dummy"  # coalesce(empty, 'dummy') like the bicep module
+    assert {ra["role"] for ra in m2.role_assignments() if ra["principal"] == "tasksmanager-backend-api-mi"} == {
+        "Cosmos DB Built-in Data Contributor", "Azure Service Bus Data Sender"}
+    assert unique_string("rg") == unique_string("rg") and len(unique_string("rg")) == 13
+    assert substitute("${concat('a', x)}-${toLower(y)}", {"x": "b", "y": "C"}) == "ab-c"
+    with pytest.raises(ManifestError):
+        substitute("${nope}", {})
+
+
+def test_validate_and_what_if(tmp_path):
+    m = load_manifest(MAIN, PARAMS)
+    assert validate(m) == []
+    changes = what_if(m, None)
+    assert all(c["change"] == "Create" for c in changes)
+    from aca_dotnet_workshop_amd.platform.manifest import desired_state
+    cur = desired_state(m)
+    assert {c["change"] for c in what_if(m, cur)} == {"NoChange"}
+    m2 = load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 5})
+    mod = [c["resource"] for c in what_if(m2, cur) if c["change"] == "Modify"]
+    assert mod == ["containerApps/tasksmanager-backend-processor"]
+    bad = tmp_path / "bad.yaml"
+    text = MAIN.read_text().replace("type: azure-servicebus", "type: kafka").replace(
+        "aca-components/containerapps-scheduled-cron.yaml", "aca-components/missing.yaml")
+    bad.write_text(text)
+    (tmp_path / "aca-components").symlink_to(ROOT / "deploy" / "aca-components")
+    errs = validate(load_manifest(bad, PARAMS))
+    assert any("unsupported type 'kafka'" in e for e in errs)
+    assert any("missing.yaml not found" in e for e in errs)
+
+
+def test_keda_hpa_semantics():
+    rule = ScaleRule("topic", "azure-servicebus", {"messageCount": "10"})
+    a = Autoscaler(1, 5, [rule], cooldown=300)
+    assert a.decide({"topic": 0}, 1, now=0) == 1
+    assert a.decide({"topic": 35}, 1, now=30) == 4          # ceil(35/10)
+    assert a.decide({"topic": 10_000}, 4, now=60) == 5      # clamp to maxReplicas
+    assert a.decide({"topic": 0}, 5, now=90) == 5           # stabilization window holds replicas
+    assert a.decide({"topic": 0}, 5, now=359) == 5
+    assert a.decide({"topic": 0}, 5, now=361) == 1          # one cooldown after the last high recommendation
+    z = Autoscaler(0, 3, [rule], cooldown=10)
+    assert z.decide({"topic": 0}, 0, now=100) == 0          # scale-to-zero stays at zero
+    assert z.decide({"topic": 1}, 0, now=101) == 1          # activation
+    assert z.decide({"topic": 0}, 1, now=105) == 1
+    assert z.decide({"topic": 0}, 1, now=120) == 0
+    http = ScaleRule("http", "http", {"concurrentRequests": "10"})
+    assert Autoscaler(1, 10, [http]).decide({"http": 55}, 1, now=0) == 6
+    assert ScaleRule.from_manifest({"name": "h", "http": {"metadata": {"concurrentRequests": "3"}}}).target() == 3
+
+
+def test_cron_scaler_window():
+    from datetime import datetime, timezone
+    r = ScaleRule("c", "cron", {"start": "0 8 * * *", "end": "0 18 * * *", "desiredReplicas": "4"})
+    assert cron_metric(r, datetime(2024, 5, 1, 12, 0, tzinfo=timezone.utc)) == 4
+    assert cron_metric(r, datetime(2024, 5, 1, 20, 0, tzinfo=timezone.utc)) == 0
+
+
+# --------------------------------------------------------------------- integration
+def _get(url, **kw):
+    return urllib.request.urlopen(url, timeout=10, **kw)
+
+
+@pytest.mark.slow
+def test_environment_lifecycle(tmp_path):
+    from aca_dotnet_workshop_amd.platform.controller import EnvironmentController
+
+    async def main():
+        m = load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 150})
+        ctl = EnvironmentController(m, tmp_path / "env", polling_interval=0.5, cooldown=3)
+        await ctl.up()
+        try:
+            st = ctl.status()
+            api = st["apps"]["tasksmanager-backend-api"]["ingress"]
+            fe = st["apps"]["tasksmanager-frontend-webapp"]["ingress"]
+            # module 2: internal ingress is 403 from outside the environment
+            with pytest.raises(urllib.error.HTTPError) as ei:
+                await asyncio.to_thread(_get, api["fqdn"] + "/api/tasks?createdBy=x")
+            assert ei.value.code == 403
+            r = await asyncio.to_thread(_get, fe["fqdn"] + "/")
+            assert r.status == 200
+            # the frontend -> API -> state store path works under RBAC (managed identities)
+            data = b"TasksCreatedBy=env%40test"
+            req = urllib.request.Request(fe["fqdn"] + "/", data=data, method="POST",
+                                         headers={"Content-Type": "application/x-www-form-urlencoded"})
+            opener = urllib.request.build_opener(_NoRedirect)
+            resp = await asyncio.to_thread(opener.open, req)
+            assert resp.status == 302
+            b = ctl.backing
+            # module 9: burst on the topic scales the processor out, then back in after the cooldown
+            ce = json.dumps({"specversion": "1.0", "id": "x", "source": "t", "type": "t", "datacontenttype": "application/json",
+                             "data": {"taskName": "burst", "taskAssignedTo": "a@x", "taskDueDate": "2030-01-01T00:00:00"}})
+            await b.sb_publish_batch("taskstracker", "tasksavedtopic",
+                                     [{"body": ce, "contentType": "application/cloudevents+json"} for _ in range(800)])
+            proc = ctl.apps["tasksmanager-backend-processor"]
+            peak = 1
+            for _ in range(100):
+                await asyncio.sleep(0.1)
+                peak = max(peak, len([r for r in proc.current.replicas if r.alive()]))
+                c = await b.sb_counts("taskstracker", "tasksavedtopic/subscriptions/tasksmanager-backend-processor")
+                if c["completed"] >= 800 and peak > 1:
+                    break
+            assert peak == 5
+            assert c["completed"] == 800 and c["dead_letter"] == 0
+            for _ in range(100):
+                await asyncio.sleep(0.1)
+                if len([r for r in proc.current.replicas if r.alive()]) == 1:
+                    break
+            assert len([r for r in proc.current.replicas if r.alive()]) == 1
+            # restart policy: a crashed replica is replaced
+            api_rt = ctl.apps["tasksmanager-backend-api"]
+            victim = api_rt.current.replicas[0]
+            os.killpg(victim.proc.pid, signal.SIGKILL)
+            for _ in range(200):
+                await asyncio.sleep(0.1)
+                if api_rt.restarts >= 1 and all(r.alive() for r in api_rt.current.replicas):
+                    break
+            assert api_rt.restarts >= 1 and api_rt.current.replicas[0].name != victim.name
+            # module 10: a changed template deploys a new revision and retires the old one
+            old = proc.current.name
+            res = await ctl.apply(load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 10}))
+            assert proc.current.name != old and res["newRevisions"] == [proc.current.name]
+            assert [r.active for r in proc.revisions] == [False, True]
+            assert (tmp_path / "env" / "state.json").exists()
+        finally:
+            await ctl.down()
+    run(main())
+
+
+class _NoRedirect(urllib.request.HTTPRedirectHandler):
+    def redirect_request(self, *a, **k):
+        return None
+
+    def http_error_302(self, req, fp, code, msg, headers):
+        return fp
