@@ -35,6 +35,7 @@ from .. import native
 from ..telemetry import configure, configure_logging
 from ..web.app import WebApp
 from ..web.http import HTTPError, Request, Response, empty, json_response, problem
+from .accel import CollectionAccelerator, accelerator_from_env
 from .auth import AccessPolicy
 
 log = logging.getLogger("backing")
@@ -96,6 +97,8 @@ class BackingServices:
         self.policy = policy or AccessPolicy()
         self.fsync = fsync
         self.stores: dict[tuple[str, str, str], Any] = {}
+        self.accel_mode, self.accel_min_docs = accelerator_from_env()
+        self.accels: dict[tuple[str, str, str], CollectionAccelerator] = {}
         self.brokers: dict[str, Any] = {}
         self.waiters = Waiters()
         self.vaults: dict[str, dict[str, str]] = {}
@@ -116,6 +119,13 @@ class BackingServices:
         if s is None:
             s = self.stores[key] = self.N.DocStore(self._path("cosmos", account, db, coll + ".log"), self.fsync)
         return s
+
+    def accel(self, account: str, db: str, coll: str) -> CollectionAccelerator:
+        key = (account, db, coll)
+        a = self.accels.get(key)
+        if a is None:
+            a = self.accels[key] = CollectionAccelerator(self.accel_mode, self.accel_min_docs)
+        return a
 
     def broker(self, ns: str):
         b = self.brokers.get(ns)
@@ -167,16 +177,22 @@ class BackingServices:
             self.authorize(req, action, f"cosmos/{p['account']}")
             return self.store(p["account"], p["db"], p["coll"])
 
+        def acc(req: Request) -> CollectionAccelerator:
+            p = req.path_params
+            return self.accel(p["account"], p["db"], p["coll"])
+
         async def put_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
             etag = req.headers.get("if-match") or None
+            value = req.body.decode("utf-8")
+            ttl = int(req.headers.get("x-tt-ttl-ms", "0") or 0)
             try:
-                e = s.set(req.path_params["key"], req.body.decode("utf-8"), etag,
-                          req.headers.get("x-tt-first-write") == "1", int(req.headers.get("x-tt-ttl-ms", "0") or 0))
+                e = s.set(req.path_params["key"], value, etag, req.headers.get("x-tt-first-write") == "1", ttl)
             except self.N.EtagMismatch as ex:
                 return problem(412, detail=str(ex))
             except ValueError as ex:
                 return problem(400, detail=str(ex))
+            acc(req).on_put(req.path_params["key"], value, ttl)
             return json_response({"etag": e}, headers=[("ETag", e)])
 
         async def get_doc(req: Request) -> Response:
@@ -192,6 +208,8 @@ class BackingServices:
                 ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
             except self.N.EtagMismatch as ex:
                 return problem(412, detail=str(ex))
+            if ok:
+                acc(req).on_delete(req.path_params["key"])
             return empty(204 if ok else 404)
 
         async def bulk_get(req: Request) -> Response:
@@ -205,10 +223,13 @@ class BackingServices:
         async def bulk_set(req: Request) -> Response:
             s = st(req, "cosmos.write")
             out = []
+            a = acc(req)
             for it in req.json() or []:
                 try:
-                    e = s.set(it["key"], it["value"] if isinstance(it["value"], str) else json.dumps(it["value"]),
-                              it.get("etag") or None, bool(it.get("firstWrite")), int(it.get("ttlMs") or 0))
+                    value = it["value"] if isinstance(it["value"], str) else json.dumps(it["value"])
+                    ttl = int(it.get("ttlMs") or 0)
+                    e = s.set(it["key"], value, it.get("etag") or None, bool(it.get("firstWrite")), ttl)
+                    a.on_put(it["key"], value, ttl)
                     out.append({"key": it["key"], "etag": e})
                 except self.N.EtagMismatch as ex:
                     out.append({"key": it["key"], "error": "etag", "detail": str(ex)})
@@ -220,8 +241,13 @@ class BackingServices:
 
         async def query(req: Request) -> Response:
             s = st(req, "cosmos.read")
+            raw = req.body.decode("utf-8") or "{}"
+            prefix = req.query_get("prefix", "") or ""
             try:
-                text = s.query(req.body.decode("utf-8") or "{}", req.query_get("prefix", "") or "")
+                q = json.loads(raw)
+                text = acc(req).query(q, prefix, s) if isinstance(q, dict) else None
+                if text is None:
+                    text = s.query(raw, prefix)
             except ValueError as ex:
                 return problem(400, detail=str(ex))
             return Response(text.encode(), 200, None, "application/json")
@@ -240,12 +266,20 @@ class BackingServices:
                 return problem(412, detail=str(ex))
             except ValueError as ex:
                 return problem(400, detail=str(ex))
+            a = acc(req)
+            for o in ops:
+                if o.is_delete:
+                    a.on_delete(o.key)
+                else:
+                    a.on_put(o.key, o.value, o.ttl_ms)
             return empty(204)
 
         async def stats(req: Request) -> Response:
             s = st(req, "cosmos.read")
             d = dict(s.stats())
             d["indexedPaths"] = s.indexed_paths()
+            a = acc(req)
+            d["accelerator"] = {"mode": a.mode, "rows": a.index.live_rows() if a.index else 0, **a.stats}
             return json_response(d)
 
         async def keys(req: Request) -> Response:

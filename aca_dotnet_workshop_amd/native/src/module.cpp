@@ -37,7 +37,11 @@ PYBIND11_MODULE(_ttnative, m) {
              return op;
            }),
            py::arg("is_delete"), py::arg("key"), py::arg("value") = "", py::arg("etag") = std::nullopt,
-           py::arg("first_write") = false, py::arg("ttl_ms") = 0);
+           py::arg("first_write") = false, py::arg("ttl_ms") = 0)
+      .def_readonly("is_delete", &TxOp::is_delete)
+      .def_readonly("key", &TxOp::key)
+      .def_readonly("value", &TxOp::value)
+      .def_readonly("ttl_ms", &TxOp::ttl_ms);
 
   py::class_<DocStore>(m, "DocStore")
       .def(py::init<const std::string&, int, size_t>(), py::arg("path") = "", py::arg("fsync_mode") = 0,

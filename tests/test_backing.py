@@ -130,3 +130,62 @@ def test_rbac_enforcement():
             for c in (admin, api, proc, anon, keyed):
                 await c.close()
     run(main())
+
+
+def _accel_roundtrip(mode):
+    import os
+    import random
+    os.environ["TT_QUERY_ACCEL"] = mode
+    os.environ["TT_QUERY_ACCEL_MIN_DOCS"] = "500"
+    try:
+        svc = _svc()
+    finally:
+        os.environ.pop("TT_QUERY_ACCEL")
+        os.environ.pop("TT_QUERY_ACCEL_MIN_DOCS")
+    rnd = random.Random(1)
+
+    def doc(i):
+        return {"taskCreatedBy": f"u{rnd.randrange(9)}", "taskDueDate": f"2024-05-{rnd.randrange(1, 29):02d}T00:00:00",
+                "isCompleted": rnd.random() < 0.4, "isOverDue": rnd.random() < 0.1, "n": rnd.randrange(100)}
+
+    queries = [
+        {"filter": {"AND": [{"LT": {"taskDueDate": "2024-05-10T00:00:00"}}, {"EQ": {"isCompleted": False}},
+                            {"EQ": {"isOverDue": False}}]}, "sort": [{"key": "taskDueDate"}]},
+        {"filter": {"OR": [{"GT": {"n": 90}}, {"NEQ": {"taskCreatedBy": "u1"}}]}, "page": {"limit": 25}},
+        {"filter": {"EQ": {"isCompleted": True}}, "sort": [{"key": "n", "order": "DESC"}], "page": {"limit": 10, "token": "10"}},
+        {"filter": {"EQ": {"taskCreatedBy": "u2"}}},  # selective equality: stays on the native hash index
+    ]
+
+    async def main():
+        async with served(svc.build_app()) as (base, _):
+            c = BackingClient(base)
+            await c.doc_bulk_set("acct", "db", "c", [{"key": f"app||{i}", "value": json.dumps(doc(i))} for i in range(2000)])
+            await c.doc_put("acct", "db", "c", "other||x", json.dumps(doc(0)))
+            st = svc.store("acct", "db", "c")
+
+            async def check():
+                for q in queries:
+                    got = json.loads(await c.doc_query("acct", "db", "c", json.dumps(q).encode(), "app||"))
+                    assert got == json.loads(st.query(json.dumps(q), "app||")), q
+            await check()
+            # writes after the columnar index exists are mirrored (upsert, delete, transaction)
+            for i in range(0, 300, 3):
+                await c.doc_put("acct", "db", "c", f"app||{i}", json.dumps(doc(i)))
+            for i in range(1, 300, 7):
+                await c.doc_delete("acct", "db", "c", f"app||{i}")
+            await c.doc_transaction("acct", "db", "c", [{"op": "upsert", "key": "app||new", "value": doc(5)},
+                                                        {"op": "delete", "key": "app||2"}])
+            await check()
+            stats = await c.doc_stats("acct", "db", "c")
+            assert stats["accelerator"][mode if mode != "auto" else "gpu"] >= 6 and stats["accelerator"]["native"] >= 2
+            await c.close()
+    run(main())
+
+
+def test_query_accelerator_cpu_matches_native():
+    _accel_roundtrip("cpu")
+
+
+@pytest.mark.gpu
+def test_query_accelerator_gpu_matches_native():
+    _accel_roundtrip("gpu")
