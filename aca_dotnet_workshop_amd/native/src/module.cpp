@@ -4,6 +4,7 @@
 
 #include "broker.hpp"
 #include "docstore.hpp"
+#include "httpparse.hpp"
 
 namespace py = pybind11;
 using namespace tt;
@@ -22,6 +23,37 @@ PYBIND11_MODULE(_ttnative, m) {
     } catch (const ParseError& e) {
       PyErr_SetString(PyExc_ValueError, (std::string("invalid JSON: ") + e.what()).c_str());
     }
+  });
+
+  // (start-line a, b, c, headers dict) with lower-cased names; repeated headers joined by
+  // ", " except set-cookie, which becomes a list.  Raises ValueError on malformed input.
+  m.def("parse_http_head", [](py::bytes raw) {
+    std::string_view sv = raw;
+    HttpHead h;
+    try {
+      h = parse_head(sv);
+    } catch (const std::invalid_argument& e) {
+      throw py::value_error(e.what());
+    }
+    py::dict hd;
+    for (auto& [k, v] : h.headers) {
+      py::str key(k);
+      if (hd.contains(key)) {
+        if (k == "set-cookie") {
+          py::object prev = hd[key];
+          py::list l;
+          if (py::isinstance<py::list>(prev)) l = prev.cast<py::list>();
+          else l.append(prev);
+          l.append(py::str(v));
+          hd[key] = l;
+        } else {
+          hd[key] = py::str(hd[key].cast<std::string>() + ", " + v);
+        }
+      } else {
+        hd[key] = py::str(v);
+      }
+    }
+    return py::make_tuple(py::str(h.a), py::str(h.b), py::str(h.c), hd);
   });
 
   py::class_<TxOp>(m, "TxOp")

@@ -116,6 +116,7 @@ class WebApp:
         self.static_dirs: list[tuple[str, Path]] = []
         self.openapi_info: dict[str, Any] = {"title": name, "version": "1.0"}
         self._pipeline: Callable[[Request], Awaitable[Response]] | None = None
+        self._route_cache: dict[str, list[Route]] = {}
 
     # -- registration ---------------------------------------------------------
     def route(self, template: str, methods: list[str] | tuple[str, ...] = ("GET",), name: str | None = None,
@@ -130,7 +131,17 @@ class WebApp:
         r = Route({m.upper() for m in methods}, template, fn, name, meta)
         self.routes.append(r)
         self._pipeline = None
+        self._route_cache.clear()
         return r
+
+    def _candidates(self, first: str) -> list[Route]:
+        """Routes that can match a path whose first segment is ``first`` (registration order)."""
+        c = self._route_cache.get(first)
+        if c is None:
+            c = [r for r in self.routes
+                 if not r.segments or r.segments[0][0] == "param" or r.segments[0][1] == first]
+            self._route_cache[first] = c
+        return c
 
     def get(self, template: str, **meta: Any):
         return self.route(template, ("GET", "HEAD"), **meta)
@@ -158,7 +169,7 @@ class WebApp:
         splitting so an encoded ``%2F`` stays inside its segment."""
         parts = [unquote(p) if "%" in p else p for p in path.split("/") if p]
         path_matched = False
-        for r in self.routes:
+        for r in self._candidates(parts[0].lower() if parts else ""):
             params = r.match(parts)
             if params is None:
                 continue

@@ -16,6 +16,7 @@ from typing import Any
 from urllib.parse import urlsplit
 
 from .http import Headers
+from .server import parse_head
 
 DEFAULT_TIMEOUT = 60.0
 
@@ -100,25 +101,13 @@ class _Conn(asyncio.Protocol):
             idx = buf.find(b"\r\n\r\n")
             if idx < 0:
                 return
-            head = bytes(buf[:idx]).split(b"\r\n")
+            head = bytes(buf[:idx])
             del buf[:idx + 4]
-            parts = head[0].decode("latin-1").split(" ", 2)
-            status = int(parts[1])
+            _, status_s, _, hd = parse_head(head)
+            status = int(status_s)
             if 100 <= status < 200:
                 continue  # 100 Continue
-            headers = Headers()
-            for line in head[1:]:
-                k, _, v = line.partition(b":")
-                key = k.strip().lower().decode("latin-1")
-                val = v.strip().decode("latin-1")
-                if key in headers:
-                    if key == "set-cookie":
-                        prev = headers[key]
-                        headers[key] = (prev if isinstance(prev, list) else [prev]) + [val]
-                    else:
-                        headers[key] = headers[key] + ", " + val
-                else:
-                    headers[key] = val
+            headers = Headers(hd)
             if self.is_head or status in (204, 304):
                 length: Any = 0
             elif "chunked" in headers.get("transfer-encoding", "").lower():
@@ -146,6 +135,11 @@ class _Conn(asyncio.Protocol):
             del buf[:length]
         self.head = None
         self.fut.set_result((ClientResponse(status, headers, body), keep))
+
+
+def _expire(fut: asyncio.Future) -> None:
+    if not fut.done():
+        fut.set_exception(asyncio.TimeoutError("HTTP request timed out"))
 
 
 def parse_endpoint(url: str) -> tuple[Any, str]:
@@ -235,8 +229,10 @@ class HttpClient:
             conn.got_bytes = False
             conn.is_head = method == "HEAD"
             conn.transport.write(payload)
+            fut = conn.fut
+            timer = loop.call_later(to, _expire, fut)
             try:
-                resp, keep = await asyncio.wait_for(conn.fut, to)
+                resp, keep = await fut
             except ConnectionClosed:
                 # stale keep-alive connection closed by the server: retry once on a fresh one
                 if conn.reused and not conn.got_bytes and attempt == 0:
@@ -247,6 +243,8 @@ class HttpClient:
                     conn.transport.close()
                 conn.closed = True
                 raise
+            finally:
+                timer.cancel()
             conn.fut = None
             if keep:
                 self._release(conn)

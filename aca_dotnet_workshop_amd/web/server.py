@@ -23,6 +23,39 @@ log = logging.getLogger("web.server")
 Handler = Callable[[Request], Awaitable[Response]]
 
 MAX_HEADER_BYTES = 64 * 1024
+
+
+def _py_parse_head(head: bytes) -> tuple[str, str, str, dict]:
+    lines = head.split(b"\r\n")
+    a, b, c = (lines[0].decode("latin-1").split(" ", 2) + ["", ""])[:3]
+    headers: dict = {}
+    for line in lines[1:]:
+        k, sep, v = line.partition(b":")
+        if not sep:
+            raise ValueError("malformed header line")
+        key = k.strip().lower().decode("latin-1")
+        val = v.strip().decode("latin-1")
+        if key in headers:
+            if key == "set-cookie":
+                prev = headers[key]
+                headers[key] = (prev if isinstance(prev, list) else [prev]) + [val]
+            else:
+                headers[key] = headers[key] + ", " + val
+        else:
+            headers[key] = val
+    return a, b, c, headers
+
+
+def _native_parser():
+    try:
+        from ..native import load
+        return load().parse_http_head
+    except Exception as e:  # pragma: no cover - build toolchain missing
+        log.warning("native HTTP parser unavailable (%s); using the Python parser", e)
+        return _py_parse_head
+
+
+parse_head = _native_parser()
 MAX_BODY_BYTES = 256 * 1024 * 1024
 
 
@@ -112,21 +145,8 @@ class HttpServerProtocol(asyncio.Protocol):
                 del buf[:idx + 4]
                 if not head:
                     continue  # stray CRLF between pipelined requests
-                lines = head.split(b"\r\n")
-                method, target, version = lines[0].decode("latin-1").split(" ", 2)
-                headers = Headers()
-                for line in lines[1:]:
-                    k, _, v = line.partition(b":")
-                    key = k.strip().lower().decode("latin-1")
-                    val = v.strip().decode("latin-1")
-                    if key in headers:
-                        if key == "set-cookie":
-                            prev = headers[key]
-                            headers[key] = (prev if isinstance(prev, list) else [prev]) + [val]
-                        else:
-                            headers[key] = headers[key] + ", " + val
-                    else:
-                        headers[key] = val
+                method, target, version, hd = parse_head(head)
+                headers = Headers(hd)
                 chunked = "chunked" in headers.get("transfer-encoding", "").lower()
                 length = 0 if chunked else int(headers.get("content-length", "0") or 0)
                 if length > MAX_BODY_BYTES:
