@@ -70,6 +70,7 @@ class LocalStack:
         self.quiet = quiet
         self.backing_proc: subprocess.Popen | None = None
         self.backing_url: str | None = None
+        self.extra_backing: dict[str, tuple[subprocess.Popen, str]] = {}
         self.replicas: dict[str, list[ReplicaProc]] = {}
         self._seq = 0
 
@@ -95,6 +96,24 @@ class LocalStack:
         port = _wait_file(pf, timeout, self.backing_proc)
         self.backing_url = f"http://127.0.0.1:{port}"
         return self.backing_url
+
+    def start_backing_family(self, families: list[str], timeout: float = 60.0) -> str:
+        """Run a separate backing-services process for some service families (e.g.
+        ``["SERVICEBUS", "STORAGE"]``); replicas started afterwards route those families to it."""
+        tag = "-".join(f.lower() for f in families)
+        pf = self.root / f"backing-{tag}.port"
+        if pf.exists():
+            pf.unlink()
+        args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
+        p = self._spawn(args, self.base_env, f"backing-{tag}")
+        url = f"http://127.0.0.1:{_wait_file(pf, timeout, p)}"
+        for f in families:
+            self.extra_backing[f] = (p, url)
+            self.base_env[f"TT_BACKING_URL_{f}"] = url
+        return url
+
+    def backing_url_for(self, family: str) -> str:
+        return self.extra_backing[family][1] if family in self.extra_backing else self.backing_url
 
     def start_replica(self, app_id: str, config: dict[str, str] | None = None, extra_env: dict[str, str] | None = None,
                       http_port: int | None = None, module: str | None = None, log_level: str = "warning",
@@ -158,6 +177,9 @@ class LocalStack:
         if self.backing_proc is not None:
             _terminate(self.backing_proc, 10.0)
             self.backing_proc = None
+        for p, _ in {id(p): (p, u) for p, u in self.extra_backing.values()}.values():
+            _terminate(p, 10.0)
+        self.extra_backing.clear()
         import shutil
         shutil.rmtree(self.sock_dir, ignore_errors=True)
 

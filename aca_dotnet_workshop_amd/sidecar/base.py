@@ -23,7 +23,13 @@ class RuntimeContext:
     environ: dict[str, str] = field(default_factory=lambda: dict(os.environ))
 
     def backing(self, comp: Component, key: str | None = None) -> BackingClient:
-        base = comp.get("ttBackingUrl") or self.backing_url
+        """Endpoint of the backing service for this component: explicit ``ttBackingUrl``
+        metadata, else a per-service-family URL (``TT_BACKING_URL_COSMOS`` /
+        ``_SERVICEBUS`` / ``_STORAGE`` / ``_KEYVAULT`` / ``_SENDGRID``), else the shared
+        ``TT_BACKING_URL`` -- Azure's services are separate endpoints, so they may be
+        separate emulator processes."""
+        base = comp.get("ttBackingUrl") or self.environ.get(f"TT_BACKING_URL_{service_family(comp.type)}") \
+            or self.backing_url
         return BackingClient(base, identity=self.identity or "", key=key, http=self.http)
 
 
@@ -63,6 +69,21 @@ def create_component(comp: Component, ctx: RuntimeContext) -> ComponentBase:
 
 def supported_types() -> list[str]:
     return sorted(_REGISTRY)
+
+
+def service_family(component_type: str) -> str:
+    t = component_type
+    if t.startswith("state."):
+        return "COSMOS"
+    if t.startswith("pubsub."):
+        return "SERVICEBUS"
+    if t.startswith("secretstores."):
+        return "KEYVAULT"
+    if "sendgrid" in t:
+        return "SENDGRID"
+    if t == "bindings.cron":
+        return "COSMOS"  # leases live in the document store
+    return "STORAGE"
 
 
 # -- Azure-style endpoint metadata -> emulator account names --------------------
