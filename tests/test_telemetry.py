@@ -1,0 +1,79 @@
+"""Telemetry: application map / failures / performance views over spans, traceparent
+parsing, JSON log records with trace ids, Prometheus exposition."""
+import json
+import logging
+
+from aca_dotnet_workshop_amd.telemetry import appmap, tracing
+from aca_dotnet_workshop_amd.telemetry.logging import JsonFormatter, _Ctx
+from aca_dotnet_workshop_amd.telemetry.metrics import Registry
+
+
+def _spans():
+    web = tracing.Tracer("tasksmanager-frontend-webapp")
+    web_sc = tracing.Tracer("tasksmanager-frontend-webapp.sidecar")
+    api_sc = tracing.Tracer("tasksmanager-backend-api.sidecar")
+    api = tracing.Tracer("tasksmanager-backend-api")
+    with web.start_span("GET /Tasks/Index", "server") as s1:
+        with web.start_span("invoke api", "client") as c1:
+            with web_sc.start_span("POST /v1.0/invoke", "server", parent=c1) as s2:
+                with api_sc.start_span("GET /api/tasks", "server", parent=s2) as s3:
+                    with api.start_span("GET /api/tasks", "server", parent=s3) as s4:
+                        s4.fail("boom")
+    out = []
+    for t in (web, web_sc, api_sc, api):
+        out += t.exporter.memory
+    return out, s1.trace_id
+
+
+def test_application_map_edges_and_views():
+    spans, tid = _spans()
+    m = appmap.application_map(spans)
+    assert {"from": "tasksmanager-frontend-webapp", "to": "tasksmanager-backend-api", "calls": 1, "failures": 0} == \
+        {k: v for k, v in m["edges"][0].items() if k != "avgMs"}
+    assert m["nodes"]["tasksmanager-backend-api"]["failures"] == 1
+    f = appmap.failures(spans)
+    assert f[0]["role"] == "tasksmanager-backend-api" and f[0]["count"] == 1
+    perf = appmap.performance(spans)
+    assert {p["role"] for p in perf} >= {"tasksmanager-backend-api", "tasksmanager-frontend-webapp"}
+    tx = appmap.transaction(spans, tid)
+    assert len(tx) == 5 and all(s["traceId"] == tid for s in tx)
+
+
+def test_spans_to_directory_and_load(tmp_path):
+    t = tracing.Tracer("svc", str(tmp_path))
+    with t.start_span("op", "server"):
+        pass
+    t.flush()
+    assert appmap.load_spans(tmp_path)[0]["role"] == "svc"
+
+
+def test_traceparent_parsing_and_sampling():
+    assert tracing.parse_traceparent("00-" + "a" * 32 + "-" + "b" * 16 + "-01") == ("a" * 32, "b" * 16, True)
+    assert tracing.parse_traceparent("00-" + "0" * 32 + "-" + "b" * 16 + "-01") is None
+    assert tracing.parse_traceparent("garbage") is None
+    t = tracing.Tracer("s", sample_rate=0.0)
+    with t.start_span("x", "server"):
+        pass
+    assert t.exporter.memory == []
+
+
+def test_json_log_record_carries_trace_ids():
+    t = tracing.Tracer("svc")
+    rec = logging.LogRecord("cat", logging.INFO, __file__, 1, "hello %s", ("w",), None)
+    with t.start_span("op", "server") as sp:
+        _Ctx("svc").filter(rec)
+    d = json.loads(JsonFormatter().format(rec))
+    assert d["message"] == "hello w" and d["role"] == "svc" and d["traceId"] == sp.trace_id
+
+
+def test_prometheus_exposition():
+    r = Registry()
+    c = r.counter("reqs", "requests")
+    c.inc(route="/a")
+    c.inc(2, route="/a")
+    h = r.histogram("lat", "latency")
+    for v in (0.001, 0.002, 0.2):
+        h.observe(v, route="/a")
+    text = r.expose()
+    assert 'reqs{route="/a"} 3.0' in text and 'lat_count{route="/a"} 3' in text
+    assert h.quantile(0.5, route="/a") == 0.0025
