@@ -22,7 +22,8 @@ from typing import Any, Iterable
 import numpy as np
 
 OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ = 1, 2, 3, 4, 5, 6
-TILE = 4096
+TILE = 8192           # rows per kernel tile (ops/hip/query_scan.hip kTileRows)
+MAX_DEPTH = 8         # device stack depth (16-bit masks in a 128-bit register)
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
 
 
@@ -195,6 +196,8 @@ class ColumnarIndex:
         self.n = 0
         self.version = 0
         self._dev = None  # device mirror state
+        self._tomb_dirty = False   # liveness changed for rows that are already on the device
+        self._full_dirty = True    # layout changed (compaction / new column / growth)
         for p in paths:
             self.add_column(p)
 
@@ -212,6 +215,7 @@ class ColumnarIndex:
                 col[0, r] = c.encode(get_path(self.docs[r], path))
         self.ids = np.concatenate([self.ids, col], axis=0)
         self.version += 1
+        self._full_dirty = True
         return idx
 
     def _grow(self, need: int) -> None:
@@ -227,12 +231,14 @@ class ColumnarIndex:
         seq = np.zeros(cap, dtype=np.int64)
         seq[:self.n] = self.seq[:self.n]
         self.ids, self.live, self.seq, self.cap = ids, live, seq, cap
+        self._full_dirty = True
 
     def upsert(self, key: str, doc: Any) -> None:
         old = self.row_of.get(key)
         if old is not None:
             self.live[old] = 0
             self.docs[old] = None
+            self._tomb_dirty = True
             seq = int(self.seq[old])  # an update keeps the key's original position (native engine semantics)
         else:
             self._next_seq += 1
@@ -254,6 +260,7 @@ class ColumnarIndex:
         if r is not None:
             self.live[r] = 0
             self.docs[r] = None
+            self._tomb_dirty = True
             self.version += 1
 
     def bulk_load(self, items: Iterable[tuple[str, Any]]) -> None:
@@ -276,6 +283,7 @@ class ColumnarIndex:
         self.row_of = {k: i for i, k in enumerate(self.keys)}
         self.n = len(keep)
         self.version += 1
+        self._full_dirty = True
 
     # -- compilation ---------------------------------------------------------
     def compile(self, flt: Any) -> Program:
@@ -345,7 +353,7 @@ class ColumnarIndex:
             push()
         else:
             emit(flt)
-        if depth[1] > 32:
+        if depth[1] > MAX_DEPTH:
             raise Unsupported("filter nesting too deep for the device stack")
         bitmaps = np.concatenate(words) if words else np.zeros(1, dtype=np.uint32)
         return Program(np.asarray(code, dtype=np.int32), bitmaps.view(np.int32), sorted(set(used)))
@@ -380,34 +388,76 @@ class ColumnarIndex:
         return np.nonzero(sel)[0].astype(np.int32)
 
     # device mirror -------------------------------------------------------------
-    def to_device(self, kernels) -> tuple[Any, Any]:
-        torch = kernels.torch
-        st = self._dev
-        if st is None or st["version"] != self.version or st["shape"] != self.ids.shape:
-            cols = torch.from_numpy(np.ascontiguousarray(self.ids)).to(kernels.device, non_blocking=False)
-            live = torch.from_numpy(self.live).to(kernels.device)
-            self._dev = st = {"version": self.version, "shape": self.ids.shape, "cols": cols, "live": live}
-        return st["cols"], st["live"]
+    @staticmethod
+    def width_for(dict_size: int) -> int:
+        """Bytes per row for a column whose dictionary has ``dict_size`` ids (all-ones = missing)."""
+        return 1 if dict_size <= 254 else 2 if dict_size <= 65534 else 4
 
-    def select_gpu(self, prog: Program, kernels) -> np.ndarray:
+    def _narrow(self, col: int, lo: int, hi: int, width: int) -> np.ndarray:
+        v = self.ids[col, lo:hi]
+        if width == 4:
+            return v
+        dt = np.uint8 if width == 1 else np.uint16
+        return np.where(v < 0, np.iinfo(dt).max, v).astype(dt)
+
+    def _live_words(self, lo_word: int, hi_word: int) -> np.ndarray:
+        bits = self.live[lo_word * 16:hi_word * 16].astype(np.uint8)
+        return np.packbits(bits, bitorder="little").view("<u2").view(np.int16)
+
+    def to_device(self, kernels):
+        """Sync the device mirror.  Columns are append-only between compactions, so only rows
+        added since the last sync are uploaded; tombstones re-upload the 1-bit liveness mask
+        (N/8 bytes); a column whose dictionary outgrows its width is re-encoded."""
         torch = kernels.torch
-        cols, live = self.to_device(kernels)
+        dev = kernels.device
+        st = self._dev
+        widths = [self.width_for(len(c.values)) for c in self.columns]
+        nwords = self.cap // 16
+        if st is None or self._full_dirty or st["cap"] != self.cap or len(st["cols"]) != len(self.columns):
+            cols = [torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
+                    for i, w in enumerate(widths)]
+            live = torch.from_numpy(self._live_words(0, nwords)).to(dev)
+            st = self._dev = {"cols": cols, "widths": widths, "live": live, "synced": self.n, "cap": self.cap}
+        else:
+            lo, hi = st["synced"], self.n
+            for i, w in enumerate(widths):
+                if w != st["widths"][i]:
+                    st["cols"][i] = torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
+                    st["widths"][i] = w
+                elif hi > lo:
+                    st["cols"][i][lo:hi].copy_(torch.from_numpy(self._narrow(i, lo, hi, w)))
+            if self._tomb_dirty:
+                st["live"].copy_(torch.from_numpy(self._live_words(0, nwords)))
+            elif hi > lo:
+                w0, w1 = lo // 16, (hi + 15) // 16
+                st["live"][w0:w1].copy_(torch.from_numpy(self._live_words(w0, w1)))
+            st["synced"] = hi
+        self._full_dirty = False
+        self._tomb_dirty = False
+        table = np.array([[c.data_ptr(), w] for c, w in zip(st["cols"], st["widths"])], dtype=np.int64).reshape(-1, 2)
+        st["table"] = torch.from_numpy(table).to(dev)
+        return st
+
+    def select_gpu(self, prog: Program, kernels, return_mask: bool = False):
+        torch = kernels.torch
+        leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ)
+        if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
+            raise ValueError("program references a column outside the index")
+        st = self.to_device(kernels)
         code = torch.from_numpy(prog.code).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
-        out = kernels.select(cols, live, self.n, code, bitmaps)
-        return out.cpu().numpy()
+        res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
+        if return_mask:
+            return res
+        return res.cpu().numpy()
 
     def group_count_gpu(self, prog: Program, group_path: str, kernels) -> dict[str, int]:
-        torch = kernels.torch
         g = self.add_column(group_path)
-        cols, live = self.to_device(kernels)
-        code = torch.from_numpy(prog.code).to(kernels.device)
-        bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
-        _, mask = kernels.select(cols, live, self.n, code, bitmaps, return_mask=True)
+        _, mask = self.select_gpu(prog, kernels, return_mask=True)
         col = self.columns[g]
         if mask is None or not col.values:
             return {}
-        counts = kernels.group_count(cols[g], mask, self.n, len(col.values)).cpu().numpy()
+        counts = kernels.group_count(self._dev["table"], g, mask, self.n, len(col.values)).cpu().numpy()
         return {json.dumps(col.values[i]): int(x) for i, x in enumerate(counts) if x}
 
     def group_count_numpy(self, prog: Program, group_path: str) -> dict[str, int]:

@@ -1,7 +1,7 @@
 """ctypes bindings to the gfx950 query kernels (``_ttgpu.so``) operating on torch tensors.
 
 No silent fallback: ``GpuKernels()`` raises if the library or a HIP device is missing; the
-caller (``ops.columnar``) decides whether to use the CPU path instead, explicitly.
+caller (``backing.accel``) decides explicitly whether to use the CPU executor instead.
 """
 from __future__ import annotations
 
@@ -23,13 +23,14 @@ def load_library(build: bool = True) -> ctypes.CDLL:
         raise RuntimeError(f"GPU kernel library {LIB} is missing; run `python -m aca_dotnet_workshop_amd.ops.build`")
     lib = ctypes.CDLL(str(LIB))
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
-    lib.tt_launch_scan_eval.argtypes = [P, I64, I64, P, P, I32, P, P, P, P]
+    lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
     lib.tt_launch_scan_compact.restype = ctypes.c_int
-    lib.tt_launch_group_count.argtypes = [P, P, I64, I32, P, P]
+    lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
+    lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
     return lib
 
@@ -43,26 +44,34 @@ class GpuKernels:
         self.lib = load_library()
         self.device = torch.device(device or "cuda")
         self.tile_rows = int(self.lib.tt_tile_rows())
+        self.max_depth = int(self.lib.tt_max_depth())
 
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def select(self, cols, live, nrows: int, prog, bitmaps, return_mask: bool = False):
-        """Row indices (int32, ascending) of live rows satisfying ``prog``."""
+    def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False):
+        """Row indices (int32, ascending) of live rows satisfying ``prog``.
+
+        ``table``: int64 [ncols, 2] of (device pointer, width) column descriptors, every column
+        allocated for ``capacity`` rows (a multiple of the kernel tile); ``live16``: uint16 liveness
+        bits for ``capacity`` rows."""
         torch = self.torch
         tiles = (nrows + self.tile_rows - 1) // self.tile_rows
         if tiles == 0:
             empty = torch.empty(0, dtype=torch.int32, device=self.device)
             return (empty, None) if return_mask else empty
-        assert cols.dtype == torch.int32 and cols.is_contiguous() and cols.shape[1] % self.tile_rows == 0
-        assert live.dtype == torch.int32 and live.shape[0] == cols.shape[1]
-        assert prog.dtype == torch.int32 and prog.ndim == 2 and prog.shape[1] == 4
-        assert bitmaps.dtype == torch.int32 and bitmaps.numel() > 0
-        mask = torch.empty(tiles * (self.tile_rows // 64), dtype=torch.int64, device=self.device)
+        if capacity % self.tile_rows or nrows > capacity:
+            raise ValueError("column capacity must be a multiple of the tile and >= nrows")
+        if live16.dtype != torch.int16 or live16.numel() * 16 < capacity:
+            raise ValueError("liveness mask must be int16 bits covering the capacity")
+        if table.dtype != torch.int64 or table.ndim != 2 or table.shape[1] != 2:
+            raise ValueError("column table must be int64 [ncols, 2]")
+        if prog.dtype != torch.int32 or prog.ndim != 2 or prog.shape[1] != 4:
+            raise ValueError("program must be int32 [L, 4]")
+        mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
-        rc = self.lib.tt_launch_scan_eval(cols.data_ptr(), cols.shape[1], nrows, live.data_ptr(), prog.data_ptr(),
-                                          prog.shape[0], bitmaps.data_ptr(), mask.data_ptr(), counts.data_ptr(),
-                                          self._stream())
+        rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
+                                          bitmaps.data_ptr(), mask.data_ptr(), counts.data_ptr(), self._stream())
         if rc != 0:
             raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
         incl = torch.cumsum(counts, 0, dtype=torch.int64)
@@ -70,17 +79,18 @@ class GpuKernels:
         offsets = incl - counts.to(torch.int64)
         out = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
         if total:
-            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), offsets.data_ptr(), nrows, out.data_ptr(), self._stream())
+            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), offsets.data_ptr(), nrows, out.data_ptr(),
+                                                 self._stream())
             if rc != 0:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
         out = out[:total]
         return (out, mask) if return_mask else out
 
-    def group_count(self, gcol, mask, nrows: int, ngroups: int):
+    def group_count(self, table, g: int, mask, nrows: int, ngroups: int):
         torch = self.torch
         counts = torch.zeros(max(ngroups, 1), dtype=torch.int32, device=self.device)
-        rc = self.lib.tt_launch_group_count(gcol.data_ptr(), mask.data_ptr(), nrows, max(ngroups, 1), counts.data_ptr(),
-                                            self._stream())
+        rc = self.lib.tt_launch_group_count(table.data_ptr(), g, mask.data_ptr(), nrows, max(ngroups, 1),
+                                            counts.data_ptr(), self._stream())
         if rc != 0:
             raise RuntimeError(f"tt_group_count launch failed ({rc})")
         return counts[:ngroups]

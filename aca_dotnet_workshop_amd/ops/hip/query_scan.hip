@@ -1,124 +1,139 @@
 // Columnar predicate scan + order-preserving compaction for the state-store query engine
-// (gfx950 / CDNA4, wave64).
+// (gfx950 / CDNA4, wave64).  Version 2: narrow columns, bit-sliced evaluation.
 //
 // Data model (built by ops/columnar.py): every queryable JSON path of a collection is a
-// dictionary-encoded int32 column (one id per document row); row liveness is column 0
-// semantics-free: tombstoned rows carry id -1 in the `live` column.  A query filter
-// (EQ/NEQ/IN/GT/GTE/LT/LTE/AND/OR of the Dapr state-query API) is compiled on the host into
-// a tiny postfix program whose leaves are "id of column c is in dictionary-id set S"; S is
-// a bitmap over the column's dictionary, so every comparison semantics (typed equality,
-// range order) is resolved exactly on the host against the dictionary and the device only
-// does bit tests.
+// dictionary-encoded column of 1, 2 or 4 bytes per row (width chosen from the dictionary
+// size; the all-ones value of the width means "path missing"), plus a 1-bit liveness mask.
+// A query filter (EQ/NEQ/IN/GT/GTE/LT/LTE/AND/OR of the Dapr state-query API) is compiled on
+// the host into a postfix program whose leaves are "id of column c == v" or "id in bitmap
+// S"; ordering/type semantics are resolved against the dictionary on the host, so the
+// device only compares ids and tests bits.
 //
-// Kernel 1 (tt_scan_eval): each lane evaluates the program for 4 consecutive rows loaded
-// as one int4 per referenced column (16 B/lane, 1 KiB per wave-instruction), the wave
-// forms 4 ballots and re-interleaves them into four 64-bit row-order mask words
-// (bit r of word w = row 64w + r), and the block writes its popcount.  Memory-bound: one
-// read of each referenced column + N/8 bytes of mask.
-// Kernel 2 (tt_scan_compact): per 4096-row tile, exclusive-scan the 64 word popcounts in
-// LDS, add the tile's global offset (exclusive scan of block counts), and each lane writes
-// its row index if its bit is set -- output is in row (= insertion) order, deterministic.
+// tt_scan_eval: each lane owns 16 consecutive rows.  For every leaf it loads the 16 ids with
+// one 16/32/64-byte vector load (width 1/2/4) and produces a 16-bit row mask; the program's
+// stack holds 16-bit masks packed in a 128-bit register (depth <= 8), so AND/OR/NOT are
+// plain bitwise ops on all 16 rows at once.  The lane ANDs the liveness bits and stores its
+// 16-bit slice straight into the row-order selection mask (64 lanes x 2 B = one coalesced
+// 128-B store); the block writes its selected count.  Traffic per row: sum of column
+// widths + 1/8 B liveness + 1/8 B mask.
+// tt_scan_compact: per 8192-row tile, 256 threads each take 32 mask bits, block-scan their
+// popcounts (wave shuffles + LDS), stage the selected row indices in LDS and write them out
+// contiguously (coalesced), at the tile's offset from the exclusive scan of block counts.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace {
 
-constexpr int kBlock = 256;              // 4 waves
-constexpr int kRowsPerLane = 4;          // one int4 load per column
-constexpr int kIters = 4;                // 256 lanes * 4 rows * 4 iters = 4096 rows per block
-constexpr int kTileRows = kBlock * kRowsPerLane * kIters;
-constexpr int kWordsPerTile = kTileRows / 64;
+constexpr int kBlock = 256;                    // 4 waves
+constexpr int kRowsPerLane = 16;
+constexpr int kIters = 2;
+constexpr int kTileRows = kBlock * kRowsPerLane * kIters;  // 8192 rows per block
+constexpr int kMaxDepth = 8;                   // 8 x 16-bit masks in a 128-bit stack
 
 enum Op : int32_t { OP_LEAF = 1, OP_AND = 2, OP_OR = 3, OP_NOT = 4, OP_TRUE = 5, OP_EQ = 6 };
 
-// Program layout (int32): [op, a, b, c] quads.
-//   OP_LEAF col bitmap_word_offset nbits : push(id in [0,nbits) && bitmap[id])
-//   OP_EQ   col id            -          : push(colval == id)
-//   OP_AND  n                            : pop n, push AND
-//   OP_OR   n                            : pop n, push OR
-//   OP_NOT                               : invert top
-//   OP_TRUE                              : push 1
-// The stack is a uint32 per row (depth <= 32, enforced by the compiler on the host).
+struct ColumnDesc {     // 16 bytes, host-built table
+  uint64_t ptr;         // device address of the column (row 0)
+  int32_t width;        // 1, 2 or 4 bytes per row
+  int32_t pad;
+};
 
-__device__ __forceinline__ uint64_t spread4(uint64_t x) {
-  x &= 0xFFFFull;
-  x = (x | (x << 24)) & 0x000000FF000000FFull;
-  x = (x | (x << 12)) & 0x000F000F000F000Full;
-  x = (x | (x << 6)) & 0x0303030303030303ull;
-  x = (x | (x << 3)) & 0x1111111111111111ull;
-  return x;
+using u128 = unsigned __int128;
+
+__device__ __forceinline__ int32_t id_of(uint32_t raw, int width) {
+  if (width == 1) return raw == 0xFFu ? -1 : (int32_t)raw;
+  if (width == 2) return raw == 0xFFFFu ? -1 : (int32_t)raw;
+  return (int32_t)raw;
 }
 
-__device__ __forceinline__ uint32_t bit_of(const uint32_t* __restrict__ bm, int32_t id, int32_t nbits) {
-  return (id >= 0 && id < nbits) ? ((bm[id >> 5] >> (id & 31)) & 1u) : 0u;
+// Load the 16 ids of rows [row0, row0+16) of one column.
+__device__ __forceinline__ void load16(const ColumnDesc& cd, int64_t row0, int32_t (&ids)[16]) {
+  if (cd.width == 1) {
+    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(cd.ptr) + row0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ids[i] = id_of((w[i >> 2] >> ((i & 3) * 8)) & 0xFFu, 1);
+  } else if (cd.width == 2) {
+    const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(cd.ptr) + row0);
+    const uint4 a = p[0], b = p[1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ids[i] = id_of((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu, 2);
+  } else {
+    const int4* p = reinterpret_cast<const int4*>(reinterpret_cast<const int32_t*>(cd.ptr) + row0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 v = p[q];
+      ids[q * 4 + 0] = v.x; ids[q * 4 + 1] = v.y; ids[q * 4 + 2] = v.z; ids[q * 4 + 3] = v.w;
+    }
+  }
 }
 
 }  // namespace
 
 extern "C" __global__ void __launch_bounds__(kBlock)
-tt_scan_eval(const int32_t* __restrict__ cols,      // [ncols, stride] dictionary ids, -1 = missing
-             int64_t stride,                         // row capacity per column (multiple of 4096)
+tt_scan_eval(const ColumnDesc* __restrict__ cols,
              int64_t nrows,
-             const int32_t* __restrict__ live,       // [stride] 1 = live row, 0 = tombstone / padding
+             const uint16_t* __restrict__ live,      // 1 bit per row, row order
              const int32_t* __restrict__ prog, int32_t prog_len,
              const uint32_t* __restrict__ bitmaps,
-             uint64_t* __restrict__ mask,            // [stride/64]
-             int32_t* __restrict__ block_counts) {   // [stride/4096]
+             uint16_t* __restrict__ mask,            // 1 bit per row, row order
+             int32_t* __restrict__ block_counts) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
   int32_t local = 0;
+#pragma unroll 1
   for (int it = 0; it < kIters; ++it) {
-    // rows handled by this lane: 4 consecutive rows
-    const int64_t wave_base = tile * kTileRows + (int64_t)it * (kBlock * kRowsPerLane) + wave * 256;
-    const int64_t row0 = wave_base + lane * 4;
-    uint32_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;  // per-row bool stacks
+    const int64_t row0 = tile * kTileRows + (int64_t)it * (kBlock * kRowsPerLane) + (int64_t)(wave * 64 + lane) * 16;
+    uint32_t sel = 0;
     if (row0 < nrows) {
-      const int4 lv = *reinterpret_cast<const int4*>(live + row0);
+      u128 st = 0;
+#pragma unroll 1
       for (int pc = 0; pc < prog_len; ++pc) {
         const int32_t op = prog[pc * 4 + 0];
         const int32_t a = prog[pc * 4 + 1];
         const int32_t b = prog[pc * 4 + 2];
         const int32_t c = prog[pc * 4 + 3];
         if (op == OP_LEAF || op == OP_EQ) {
-          const int4 v = *reinterpret_cast<const int4*>(cols + (int64_t)a * stride + row0);
-          uint32_t r0, r1, r2, r3;
+          const ColumnDesc cd = cols[a];
+          int32_t ids[16];
+          load16(cd, row0, ids);
+          uint32_t m = 0;
           if (op == OP_EQ) {
-            r0 = v.x == b; r1 = v.y == b; r2 = v.z == b; r3 = v.w == b;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[i] == b) << i;
           } else {
             const uint32_t* bm = bitmaps + b;
-            r0 = bit_of(bm, v.x, c); r1 = bit_of(bm, v.y, c); r2 = bit_of(bm, v.z, c); r3 = bit_of(bm, v.w, c);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int32_t id = ids[i];
+              const uint32_t bit = (id >= 0 && id < c) ? ((bm[id >> 5] >> (id & 31)) & 1u) : 0u;
+              m |= bit << i;
+            }
           }
-          st0 = (st0 << 1) | r0; st1 = (st1 << 1) | r1; st2 = (st2 << 1) | r2; st3 = (st3 << 1) | r3;
+          st = (st << 16) | (u128)m;
         } else if (op == OP_AND || op == OP_OR) {
-          const uint32_t m = (a >= 32) ? 0xFFFFFFFFu : ((1u << a) - 1u);
-          if (op == OP_AND) {
-            st0 = (st0 >> a << 1) | ((st0 & m) == m); st1 = (st1 >> a << 1) | ((st1 & m) == m);
-            st2 = (st2 >> a << 1) | ((st2 & m) == m); st3 = (st3 >> a << 1) | ((st3 & m) == m);
-          } else {
-            st0 = (st0 >> a << 1) | ((st0 & m) != 0); st1 = (st1 >> a << 1) | ((st1 & m) != 0);
-            st2 = (st2 >> a << 1) | ((st2 & m) != 0); st3 = (st3 >> a << 1) | ((st3 & m) != 0);
+          uint32_t r = (op == OP_AND) ? 0xFFFFu : 0u;
+          for (int k = 0; k < a; ++k) {
+            const uint32_t top = (uint32_t)(st & (u128)0xFFFFu);
+            r = (op == OP_AND) ? (r & top) : (r | top);
+            st >>= 16;
           }
+          st = (st << 16) | (u128)r;
         } else if (op == OP_NOT) {
-          st0 ^= 1u; st1 ^= 1u; st2 ^= 1u; st3 ^= 1u;
+          st ^= (u128)0xFFFFu;
         } else {  // OP_TRUE
-          st0 = (st0 << 1) | 1u; st1 = (st1 << 1) | 1u; st2 = (st2 << 1) | 1u; st3 = (st3 << 1) | 1u;
+          st = (st << 16) | (u128)0xFFFFu;
         }
       }
-      st0 &= (lv.x != 0); st1 &= (lv.y != 0); st2 &= (lv.z != 0); st3 &= (lv.w != 0);
-      // rows past nrows inside the last int4 are padding with live == 0
+      sel = (uint32_t)(st & (u128)0xFFFFu) & (uint32_t)live[row0 >> 4];
     }
-    const uint64_t b0 = __ballot(st0 & 1u);
-    const uint64_t b1 = __ballot(st1 & 1u);
-    const uint64_t b2 = __ballot(st2 & 1u);
-    const uint64_t b3 = __ballot(st3 & 1u);
-    if (lane < 4) {
-      const int sh = lane * 16;
-      const uint64_t w = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) | (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
-      mask[wave_base / 64 + lane] = w;
-    }
-    if (lane == 0) local += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+    mask[row0 >> 4] = (uint16_t)sel;  // the launched tiles are inside the buffers' capacity
+    local += __popc(sel);
   }
+  // block reduction of the per-lane counts
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
   __shared__ int32_t wave_counts[kBlock / 64];
   if (lane == 0) wave_counts[wave] = local;
   __syncthreads();
@@ -130,56 +145,65 @@ tt_scan_eval(const int32_t* __restrict__ cols,      // [ncols, stride] dictionar
 }
 
 extern "C" __global__ void __launch_bounds__(kBlock)
-tt_scan_compact(const uint64_t* __restrict__ mask,
+tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask viewed as 32-bit words
                 const int64_t* __restrict__ block_offsets,  // exclusive scan of block_counts
                 int32_t* __restrict__ out) {
-  __shared__ int32_t word_prefix[kWordsPerTile];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  __shared__ int32_t staged[kTileRows];
+  __shared__ int32_t wave_sums[kBlock / 64];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
   const int64_t tile = blockIdx.x;
-  const uint64_t* m = mask + tile * kWordsPerTile;
-  if (wave == 0) {
-    // inclusive scan of the 64 word popcounts across the wave, then make it exclusive
-    const int32_t pc = __popcll(m[lane]);
-    int32_t v = pc;
-    for (int off = 1; off < 64; off <<= 1) {
-      const int32_t y = __shfl_up(v, off, 64);
-      if (lane >= off) v += y;
-    }
-    word_prefix[lane] = v - pc;
+  const uint32_t bits = mask32[tile * kBlock + t];     // rows [tile*8192 + 32t, +32)
+  const int32_t cnt = __popc(bits);
+  int32_t incl = cnt;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wave_sums[wave] = incl;
+  __syncthreads();
+  int32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wave_sums[w];
+  int32_t pos = base + incl - cnt;
+  const int32_t total = wave_sums[0] + wave_sums[1] + wave_sums[2] + wave_sums[3];
+  const int32_t row_base = (int32_t)(tile * kTileRows) + t * 32;
+  uint32_t b = bits;
+  while (b) {
+    const int k = __ffs(b) - 1;
+    staged[pos++] = row_base + k;
+    b &= b - 1;
   }
   __syncthreads();
-  const int64_t base_out = block_offsets[tile];
-  for (int i = 0; i < kWordsPerTile / (kBlock / 64); ++i) {
-    const int w = wave * (kWordsPerTile / (kBlock / 64)) + i;
-    const uint64_t word = m[w];
-    if ((word >> lane) & 1ull) {
-      const uint64_t below = lane ? (word & ((1ull << lane) - 1ull)) : 0ull;
-      out[base_out + word_prefix[w] + __popcll(below)] = (int32_t)(tile * kTileRows + (int64_t)w * 64 + lane);
-    }
-  }
+  int32_t* dst = out + block_offsets[tile];
+  for (int i = t; i < total; i += kBlock) dst[i] = staged[i];
 }
 
-// Grouped count: histogram of column `gcol` dictionary ids over the rows selected in
-// `mask` (the "tasks per assignee / per creator" dashboard aggregate).  LDS-privatised
-// counters for small dictionaries, global atomics otherwise.
+// Grouped count: histogram of column `g` dictionary ids over the selected rows (the
+// "open tasks per assignee" dashboard aggregate).  LDS-privatised counters for dictionaries
+// up to 8192 entries, global atomics otherwise.
 extern "C" __global__ void __launch_bounds__(kBlock)
-tt_group_count(const int32_t* __restrict__ gcol, const uint64_t* __restrict__ mask, int64_t nwords,
+tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* __restrict__ mask, int64_t nrows,
                int32_t ngroups, uint32_t* __restrict__ counts) {
   extern __shared__ uint32_t hist[];
   const bool use_lds = ngroups <= 8192;
   if (use_lds)
     for (int i = threadIdx.x; i < ngroups; i += kBlock) hist[i] = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (int64_t w = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); w < nwords;
-       w += (int64_t)gridDim.x * (kBlock / 64)) {
-    const uint64_t word = mask[w];
-    if ((word >> lane) & 1ull) {
-      const int32_t g = gcol[w * 64 + lane];
-      if (g >= 0 && g < ngroups) {
-        if (use_lds) atomicAdd(&hist[g], 1u);
-        else atomicAdd(&counts[g], 1u);
+  const ColumnDesc cd = cols[g];
+  const int64_t nslices = (nrows + 15) / 16;
+  for (int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x; s < nslices; s += (int64_t)gridDim.x * kBlock) {
+    uint32_t m = mask[s];
+    if (!m) continue;
+    int32_t ids[16];
+    load16(cd, s * 16, ids);
+    while (m) {
+      const int k = __ffs(m) - 1;
+      m &= m - 1;
+      const int32_t id = ids[k];
+      if (id >= 0 && id < ngroups) {
+        if (use_lds) atomicAdd(&hist[id], 1u);
+        else atomicAdd(&counts[id], 1u);
       }
     }
   }
@@ -190,35 +214,40 @@ tt_group_count(const int32_t* __restrict__ gcol, const uint64_t* __restrict__ ma
 }
 
 // ------------------------------------------------------------------ host launchers
-extern "C" int tt_launch_scan_eval(const int32_t* cols, int64_t stride, int64_t nrows, const int32_t* live,
-                                   const int32_t* prog, int32_t prog_len, const uint32_t* bitmaps, uint64_t* mask,
-                                   int32_t* block_counts, hipStream_t stream) {
-  if (stride % kTileRows != 0 || nrows > stride || prog_len <= 0) return -1;
+// Preconditions (checked by the Python wrapper): every column and the live/mask buffers are
+// allocated for a capacity that is a multiple of kTileRows rows, nrows <= capacity.
+extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* prog,
+                                   int32_t prog_len, const uint32_t* bitmaps, uint16_t* mask, int32_t* block_counts,
+                                   hipStream_t stream) {
+  if (prog_len <= 0 || nrows < 0) return -1;
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
-  hipLaunchKernelGGL(tt_scan_eval, dim3((unsigned)tiles), dim3(kBlock), 0, stream, cols, stride, nrows, live, prog,
-                     prog_len, bitmaps, mask, block_counts);
+  hipLaunchKernelGGL(tt_scan_eval, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, mask, block_counts);
   return (int)hipGetLastError();
 }
 
-extern "C" int tt_launch_scan_compact(const uint64_t* mask, const int64_t* block_offsets, int64_t nrows,
-                                      int32_t* out, hipStream_t stream) {
+extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int64_t* block_offsets, int64_t nrows, int32_t* out,
+                                      hipStream_t stream) {
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
-  hipLaunchKernelGGL(tt_scan_compact, dim3((unsigned)tiles), dim3(kBlock), 0, stream, mask, block_offsets, out);
+  hipLaunchKernelGGL(tt_scan_compact, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const uint32_t*>(mask), block_offsets, out);
   return (int)hipGetLastError();
 }
 
-extern "C" int tt_launch_group_count(const int32_t* gcol, const uint64_t* mask, int64_t nrows, int32_t ngroups,
+extern "C" int tt_launch_group_count(const void* cols, int32_t g, const uint16_t* mask, int64_t nrows, int32_t ngroups,
                                      uint32_t* counts, hipStream_t stream) {
   if (ngroups <= 0) return -1;
-  const int64_t nwords = (nrows + 63) / 64;
-  int64_t blocks = (nwords + (kBlock / 64) - 1) / (kBlock / 64);
+  const int64_t nslices = (nrows + 15) / 16;
+  int64_t blocks = (nslices + kBlock - 1) / kBlock;
   if (blocks > 2048) blocks = 2048;
+  if (blocks == 0) return 0;
   const size_t lds = ngroups <= 8192 ? (size_t)ngroups * sizeof(uint32_t) : 0;
-  hipLaunchKernelGGL(tt_group_count, dim3((unsigned)blocks), dim3(kBlock), lds, stream, gcol, mask, nwords, ngroups,
-                     counts);
+  hipLaunchKernelGGL(tt_group_count, dim3((unsigned)blocks), dim3(kBlock), lds, stream,
+                     reinterpret_cast<const ColumnDesc*>(cols), g, mask, nrows, ngroups, counts);
   return (int)hipGetLastError();
 }
 
 extern "C" int tt_tile_rows() { return kTileRows; }
+extern "C" int tt_max_depth() { return kMaxDepth; }

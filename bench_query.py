@@ -60,28 +60,30 @@ def main() -> None:
     ix.n = n
     ix.keys = []  # not needed for the scan benchmark
     ix.version += 1
+    ix._full_dirty = True
 
     k = GpuKernels("cuda:0")
     flt = {"AND": [{"LT": {"taskDueDate": "2024-07-01T00:00:00"}}, {"EQ": {"isCompleted": False}},
                    {"EQ": {"isOverDue": False}}]}
     prog = ix.compile(flt)
-    dcols, dlive = ix.to_device(k)
+    st = ix.to_device(k)
     code = torch.from_numpy(prog.code).cuda()
     bm = torch.from_numpy(prog.bitmaps).cuda()
     for _ in range(a.warmup):
-        out = k.select(dcols, dlive, n, code, bm)
+        out = k.select(st["table"], st["live"], ix.cap, n, code, bm)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.iters):
-        out = k.select(dcols, dlive, n, code, bm)
+        out = k.select(st["table"], st["live"], ix.cap, n, code, bm)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
     selected = int(out.numel())
-    # bytes: 3 referenced columns + live (4 B/row each) + mask write/read (2 x N/8) + output indices
-    nbytes = n * 4 * 4 + 2 * n // 8 + selected * 4
+    # bytes: referenced columns at their narrow widths + liveness bit + mask write & read + output indices
+    widths = sum(st["widths"][c] for c in prog.columns)
+    nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
-           "device": torch.cuda.get_device_name(0), "tile_rows": TILE}
+           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "column_bytes_per_row": widths}
     if a.cpu:
         t0 = time.perf_counter()
         ref = ix.select_numpy(prog)

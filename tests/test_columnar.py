@@ -187,3 +187,29 @@ def test_gpu_group_count():
     ix = _random_collection(50_000, random.Random(3))
     prog = ix.compile({"EQ": {"isCompleted": False}})
     assert ix.group_count_gpu(prog, "taskCreatedBy", k) == ix.group_count_numpy(prog, "taskCreatedBy")
+
+
+@pytest.mark.gpu
+def test_gpu_incremental_sync_and_width_growth():
+    k = _kernels()
+    rnd = random.Random(11)
+    ix = ColumnarIndex(["v", "flag"])
+    for i in range(30000):
+        ix.upsert(str(i), {"v": rnd.randrange(200), "flag": i % 3 == 0})
+    prog = ix.compile({"AND": [{"LT": {"v": 100}}, {"EQ": {"flag": True}}]})
+    assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
+    assert ix._dev["widths"][ix.col_of["v"]] == 1
+    # appends + tombstones + a dictionary that outgrows 8 and then 16 bits
+    for i in range(30000, 100000):
+        ix.upsert(str(i), {"v": i, "flag": i % 5 == 0})
+    for i in rnd.sample(range(100000), 5000):
+        ix.delete(str(i))
+    for i in rnd.sample(range(100000), 3000):
+        ix.upsert(str(i), {"v": rnd.randrange(50), "flag": True})
+    for f in ({"AND": [{"LT": {"v": 100}}, {"EQ": {"flag": True}}]}, {"GTE": {"v": 70000}}, {"NEQ": {"flag": True}}):
+        prog = ix.compile(f)
+        assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog)), f
+    assert ix._dev["widths"][ix.col_of["v"]] == 4
+    ix.compact()
+    prog = ix.compile({"LT": {"v": 1000}})
+    assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
