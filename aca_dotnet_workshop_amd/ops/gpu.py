@@ -23,7 +23,7 @@ def load_library(build: bool = True) -> ctypes.CDLL:
         raise RuntimeError(f"GPU kernel library {LIB} is missing; run `python -m aca_dotnet_workshop_amd.ops.build`")
     lib = ctypes.CDLL(str(LIB))
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
-    lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, P, P, P]
+    lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, I32, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
     lib.tt_launch_scan_compact.restype = ctypes.c_int
@@ -71,7 +71,8 @@ class GpuKernels:
         mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
         rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
-                                          bitmaps.data_ptr(), mask.data_ptr(), counts.data_ptr(), self._stream())
+                                          bitmaps.data_ptr(), bitmaps.numel(), mask.data_ptr(), counts.data_ptr(),
+                                          self._stream())
         if rc != 0:
             raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
         incl = torch.cumsum(counts, 0, dtype=torch.int64)

@@ -29,6 +29,7 @@ constexpr int kRowsPerLane = 16;
 constexpr int kIters = 2;
 constexpr int kTileRows = kBlock * kRowsPerLane * kIters;  // 8192 rows per block
 constexpr int kMaxDepth = 8;                   // 8 x 16-bit masks in a 128-bit stack
+constexpr int kMaxLdsBitmapWords = 8192;       // stage up to 32 KiB of leaf bitmaps in LDS
 
 enum Op : int32_t { OP_LEAF = 1, OP_AND = 2, OP_OR = 3, OP_NOT = 4, OP_TRUE = 5, OP_EQ = 6 };
 
@@ -71,14 +72,82 @@ __device__ __forceinline__ void load16(const ColumnDesc& cd, int64_t row0, int32
 
 }  // namespace
 
+// Leaf test for 16 rows against a dictionary-id bitmap.  Dictionaries of <= 64 ids use a
+// register-resident 64-bit copy of the bitmap (no memory traffic per row); larger ones probe
+// the bitmap words, which the kernel staged in LDS when they fit (`bm` then points to LDS).
+template <typename BitmapPtr>
+__device__ __forceinline__ uint32_t leaf_mask(const int32_t (&ids)[16], BitmapPtr bm, int32_t nbits) {
+  uint32_t m = 0;
+  if (nbits <= 64) {
+    const uint64_t b64 = (uint64_t)bm[0] | ((nbits > 32) ? ((uint64_t)bm[1] << 32) : 0ull);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int32_t id = ids[i];
+      m |= (uint32_t)((id >= 0 && id < nbits) ? ((b64 >> id) & 1ull) : 0ull) << i;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int32_t id = ids[i];
+      m |= ((id >= 0 && id < nbits) ? ((bm[id >> 5] >> (id & 31)) & 1u) : 0u) << i;
+    }
+  }
+  return m;
+}
+
+template <typename BitmapPtr>
+__device__ __forceinline__ uint32_t run_program(const ColumnDesc* __restrict__ cols, const int32_t* __restrict__ prog,
+                                                int32_t prog_len, BitmapPtr bitmaps, int64_t row0) {
+  u128 st = 0;
+#pragma unroll 1
+  for (int pc = 0; pc < prog_len; ++pc) {
+    const int32_t op = prog[pc * 4 + 0];
+    const int32_t a = prog[pc * 4 + 1];
+    const int32_t b = prog[pc * 4 + 2];
+    const int32_t c = prog[pc * 4 + 3];
+    if (op == OP_LEAF || op == OP_EQ) {
+      const ColumnDesc cd = cols[a];
+      int32_t ids[16];
+      load16(cd, row0, ids);
+      uint32_t m = 0;
+      if (op == OP_EQ) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[i] == b) << i;
+      } else {
+        m = leaf_mask(ids, bitmaps + b, c);
+      }
+      st = (st << 16) | (u128)m;
+    } else if (op == OP_AND || op == OP_OR) {
+      uint32_t r = (op == OP_AND) ? 0xFFFFu : 0u;
+      for (int k = 0; k < a; ++k) {
+        const uint32_t top = (uint32_t)(st & (u128)0xFFFFu);
+        r = (op == OP_AND) ? (r & top) : (r | top);
+        st >>= 16;
+      }
+      st = (st << 16) | (u128)r;
+    } else if (op == OP_NOT) {
+      st ^= (u128)0xFFFFu;
+    } else {  // OP_TRUE
+      st = (st << 16) | (u128)0xFFFFu;
+    }
+  }
+  return (uint32_t)(st & (u128)0xFFFFu);
+}
+
 extern "C" __global__ void __launch_bounds__(kBlock)
 tt_scan_eval(const ColumnDesc* __restrict__ cols,
              int64_t nrows,
              const uint16_t* __restrict__ live,      // 1 bit per row, row order
              const int32_t* __restrict__ prog, int32_t prog_len,
-             const uint32_t* __restrict__ bitmaps,
+             const uint32_t* __restrict__ bitmaps, int32_t bitmap_words,
              uint16_t* __restrict__ mask,            // 1 bit per row, row order
              int32_t* __restrict__ block_counts) {
+  extern __shared__ uint32_t lds_bitmaps[];  // sized by the launcher: bitmap_words if they fit, else 0
+  const bool in_lds = bitmap_words <= kMaxLdsBitmapWords;
+  if (in_lds) {
+    for (int i = threadIdx.x; i < bitmap_words; i += kBlock) lds_bitmaps[i] = bitmaps[i];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
@@ -88,46 +157,9 @@ tt_scan_eval(const ColumnDesc* __restrict__ cols,
     const int64_t row0 = tile * kTileRows + (int64_t)it * (kBlock * kRowsPerLane) + (int64_t)(wave * 64 + lane) * 16;
     uint32_t sel = 0;
     if (row0 < nrows) {
-      u128 st = 0;
-#pragma unroll 1
-      for (int pc = 0; pc < prog_len; ++pc) {
-        const int32_t op = prog[pc * 4 + 0];
-        const int32_t a = prog[pc * 4 + 1];
-        const int32_t b = prog[pc * 4 + 2];
-        const int32_t c = prog[pc * 4 + 3];
-        if (op == OP_LEAF || op == OP_EQ) {
-          const ColumnDesc cd = cols[a];
-          int32_t ids[16];
-          load16(cd, row0, ids);
-          uint32_t m = 0;
-          if (op == OP_EQ) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[i] == b) << i;
-          } else {
-            const uint32_t* bm = bitmaps + b;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int32_t id = ids[i];
-              const uint32_t bit = (id >= 0 && id < c) ? ((bm[id >> 5] >> (id & 31)) & 1u) : 0u;
-              m |= bit << i;
-            }
-          }
-          st = (st << 16) | (u128)m;
-        } else if (op == OP_AND || op == OP_OR) {
-          uint32_t r = (op == OP_AND) ? 0xFFFFu : 0u;
-          for (int k = 0; k < a; ++k) {
-            const uint32_t top = (uint32_t)(st & (u128)0xFFFFu);
-            r = (op == OP_AND) ? (r & top) : (r | top);
-            st >>= 16;
-          }
-          st = (st << 16) | (u128)r;
-        } else if (op == OP_NOT) {
-          st ^= (u128)0xFFFFu;
-        } else {  // OP_TRUE
-          st = (st << 16) | (u128)0xFFFFu;
-        }
-      }
-      sel = (uint32_t)(st & (u128)0xFFFFu) & (uint32_t)live[row0 >> 4];
+      const uint32_t m = in_lds ? run_program(cols, prog, prog_len, lds_bitmaps, row0)
+                                : run_program(cols, prog, prog_len, bitmaps, row0);
+      sel = m & (uint32_t)live[row0 >> 4];
     }
     mask[row0 >> 4] = (uint16_t)sel;  // the launched tiles are inside the buffers' capacity
     local += __popc(sel);
@@ -217,13 +249,15 @@ tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* _
 // Preconditions (checked by the Python wrapper): every column and the live/mask buffers are
 // allocated for a capacity that is a multiple of kTileRows rows, nrows <= capacity.
 extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* prog,
-                                   int32_t prog_len, const uint32_t* bitmaps, uint16_t* mask, int32_t* block_counts,
-                                   hipStream_t stream) {
-  if (prog_len <= 0 || nrows < 0) return -1;
+                                   int32_t prog_len, const uint32_t* bitmaps, int32_t bitmap_words, uint16_t* mask,
+                                   int32_t* block_counts, hipStream_t stream) {
+  if (prog_len <= 0 || nrows < 0 || bitmap_words <= 0) return -1;
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
-  hipLaunchKernelGGL(tt_scan_eval, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
-                     reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, mask, block_counts);
+  const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
+  hipLaunchKernelGGL(tt_scan_eval, dim3((unsigned)tiles), dim3(kBlock), lds, stream,
+                     reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, bitmap_words,
+                     mask, block_counts);
   return (int)hipGetLastError();
 }
 
