@@ -1,0 +1,44 @@
+"""Race detection / memory safety for the native engines (SURVEY.md §5 "Race detection /
+sanitizers": the reference has none).  A multi-threaded stress program
+(``native/tests/stress.cpp``) is compiled twice -- ThreadSanitizer, and AddressSanitizer +
+UndefinedBehaviorSanitizer -- and must run clean.  Host code only (no GPU sanitizers)."""
+import os
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+SRC = ROOT / "aca_dotnet_workshop_amd" / "native" / "tests" / "stress.cpp"
+CXX = os.environ.get("CXX", "g++")
+
+
+def _build_and_run(tmp_path, flags, env_extra, args=("8", "1500")):
+    if shutil.which(CXX) is None:
+        pytest.skip("no C++ compiler")
+    exe = tmp_path / "stress"
+    cmd = [CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(SRC), "-o", str(exe), "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0 and "sanitize" in r.stderr and "cannot find" in r.stderr:
+        pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, **env_extra)
+    run = subprocess.run([str(exe), *args, str(tmp_path / "store.log")], capture_output=True, text=True, env=env,
+                         timeout=600)
+    out = run.stdout + run.stderr
+    assert run.returncode == 0, out[-5000:]
+    assert "ALL OK" in run.stdout
+    assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out and "runtime error" not in out
+    return run.stdout
+
+
+def test_native_engines_threadsanitizer(tmp_path):
+    out = _build_and_run(tmp_path, ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
+    assert "broker ok" in out and "docstore ok" in out
+
+
+def test_native_engines_address_ub_sanitizer(tmp_path):
+    out = _build_and_run(tmp_path, ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+                         {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"})
+    assert "broker ok" in out
