@@ -33,6 +33,7 @@ from typing import Any
 
 from .. import native
 from ..telemetry import configure, configure_logging
+from ..telemetry.profiler import maybe_profile
 from ..web.app import WebApp
 from ..web.http import HTTPError, Request, Response, empty, json_response, problem
 from .accel import CollectionAccelerator, accelerator_from_env
@@ -669,7 +670,8 @@ def main(argv: list[str] | None = None) -> None:
             os.replace(tmp, a.port_file)
 
     try:
-        asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready))
+        with maybe_profile(f"backing-{os.path.basename(a.port_file or str(a.port))}"):
+            asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready))
     except KeyboardInterrupt:
         pass
 

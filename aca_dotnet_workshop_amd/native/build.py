@@ -1,6 +1,8 @@
 """In-tree builder for the native extensions.
 
 * ``_ttnative``  -- C++17 document store + broker engines (g++/clang++, pybind11).
+* ``bin/ttsidecar-dataplane`` -- native sidecar data plane executable (epoll HTTP/1.1,
+  ``src/dataplane.cpp``), spawned by the Python sidecar when ``TT_SIDECAR_DATAPLANE=native``.
 * ``_ttgpu``     -- HIP kernels for gfx950 (see ``aca_dotnet_workshop_amd/ops``), built by
   ``ops/build.py``.
 
@@ -35,7 +37,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     import pybind11
 
     target = ext_path("_ttnative")
-    sources = sorted(SRC.glob("*.hpp")) + [SRC / "module.cpp"]
+    sources = [p for p in sorted(SRC.glob("*.hpp")) if p.name != "evhttp.hpp"] + [SRC / "module.cpp"]
     if not force and not _stale(target, sources):
         return target
     cxx = os.environ.get("CXX", "g++")
@@ -50,5 +52,24 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     return target
 
 
+DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
+
+
+def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
+    sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
+    if not force and not _stale(DATAPLANE, sources):
+        return DATAPLANE
+    DATAPLANE.parent.mkdir(exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    tmp = DATAPLANE.with_name(f".{DATAPLANE.name}.tmp{os.getpid()}")
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(SRC / "dataplane.cpp"), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, DATAPLANE)
+    return DATAPLANE
+
+
 if __name__ == "__main__":
     print(build_native(force="--force" in sys.argv, verbose=True))
+    print(build_dataplane(force="--force" in sys.argv, verbose=True))

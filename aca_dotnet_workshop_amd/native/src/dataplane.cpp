@@ -1,0 +1,1060 @@
+// ttsidecar-dataplane: the native data plane of the sidecar runtime (daprd equivalent).
+//
+// The Python sidecar (sidecar/runtime.py) stays the control plane: it loads components,
+// resolves secrets, runs subscriptions / bindings / cron and serves every API.  When the
+// native data plane is enabled it hands the public sidecar sockets to this process and
+// listens on a private socket instead.  This process answers the hot, request-per-task part
+// of the API in C++ and forwards everything else to the Python control plane unchanged:
+//
+//   POST|GET|...  /v1.0/invoke/{appId}/method/{*path}   service invocation (self or peer)
+//   POST|PUT      /v1.0/state/{store}                   save (backing cosmos / redis stores)
+//   GET|DELETE    /v1.0/state/{store}/{key}             get / delete
+//   POST|PUT      /v1.0/publish/{pubsub}/{*topic}        publish (backing service bus / redis)
+//   internal endpoint                                   peer sidecar -> this app
+//   GET /metrics                                        Python's exposition + ours
+//
+// Semantics mirror the Python handlers (sidecar/runtime.py h_invoke/_invoke/h_internal/
+// h_state_save/h_state_get/h_state_delete/h_publish) including error codes, ETag handling,
+// key prefixes, CloudEvent envelopes and W3C trace propagation; tests run the same API suite
+// against both planes (tests/test_dataplane.py).  Reference behaviour: the Dapr HTTP API as
+// used in docs/aca/03-aca-dapr-integration, 04-aca-dapr-stateapi, 05-aca-dapr-pubsubapi.
+//
+// Usage: ttsidecar-dataplane <config.json>   (written by the Python sidecar)
+#include <signal.h>
+#include <sys/prctl.h>
+#include <sys/signalfd.h>
+#include <sys/stat.h>
+#include <dirent.h>
+
+#include <cstdio>
+#include <ctime>
+#include <fstream>
+#include <map>
+#include <random>
+#include <sstream>
+
+#include "evhttp.hpp"
+#include "json.hpp"
+
+using namespace tt;
+using ev::ClientResult;
+using ev::Endpoint;
+using ev::HeaderList;
+using ev::Message;
+using ev::Reply;
+
+namespace {
+
+// ------------------------------------------------------------------------------ utilities
+std::mt19937_64& rng() {
+  static std::mt19937_64 r{std::random_device{}() ^ ((uint64_t)getpid() << 32)};
+  return r;
+}
+
+std::string hex_u64(uint64_t v, int digits = 16) {
+  static const char* d = "0123456789abcdef";
+  std::string s((size_t)digits, '0');
+  for (int i = digits - 1; i >= 0; --i, v >>= 4) s[(size_t)i] = d[v & 15];
+  return s;
+}
+
+std::string uuid4() {
+  uint64_t a = rng()(), b = rng()();
+  a = (a & 0xFFFFFFFFFFFF0FFFull) | 0x0000000000004000ull;
+  b = (b & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;
+  std::string h = hex_u64(a) + hex_u64(b);
+  return h.substr(0, 8) + "-" + h.substr(8, 4) + "-" + h.substr(12, 4) + "-" + h.substr(16, 4) + "-" + h.substr(20);
+}
+
+std::string utc_now_iso() {  // 2024-05-01T12:34:56.123456Z (models/dotnet.py format_datetime)
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  tm t;
+  gmtime_r(&ts.tv_sec, &t);
+  char buf[64];
+  std::snprintf(buf, sizeof buf, "%04d-%02d-%02dT%02d:%02d:%02d.%06ldZ", t.tm_year + 1900, t.tm_mon + 1, t.tm_mday,
+                t.tm_hour, t.tm_min, t.tm_sec, ts.tv_nsec / 1000);
+  return buf;
+}
+
+double wall_now() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (double)ts.tv_sec + ts.tv_nsec / 1e9;
+}
+
+int hexv(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+std::string unquote(std::string_view s, bool plus_space = false) {
+  std::string o;
+  o.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && hexv(s[i + 1]) >= 0 && hexv(s[i + 2]) >= 0) {
+      o += (char)(hexv(s[i + 1]) * 16 + hexv(s[i + 2]));
+      i += 2;
+    } else if (plus_space && s[i] == '+') {
+      o += ' ';
+    } else {
+      o += s[i];
+    }
+  }
+  return o;
+}
+
+std::string quote_all(std::string_view s) {  // urllib.parse.quote(s, safe="")
+  static const char* d = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : s) {
+    if (std::isalnum(c) || c == '_' || c == '.' || c == '-' || c == '~') {
+      o += (char)c;
+    } else {
+      o += '%';
+      o += d[c >> 4];
+      o += d[c & 15];
+    }
+  }
+  return o;
+}
+
+std::string lower(std::string_view s) {
+  std::string o(s);
+  for (auto& c : o) c = (char)std::tolower((unsigned char)c);
+  return o;
+}
+
+std::string json_str(std::string_view s) {
+  std::string o;
+  escape_to(o, s);
+  return o;
+}
+
+std::string error_json(std::string_view code, std::string_view msg) {
+  return "{\"errorCode\":" + json_str(code) + ",\"message\":" + json_str(msg) + "}";
+}
+
+const char* ws_end(const char* p, const char* e) {
+  while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  return p;
+}
+
+// End of the JSON value starting at p (input already validated by tt::Parser).
+const char* skip_value(const char* p, const char* e) {
+  p = ws_end(p, e);
+  if (p >= e) return p;
+  if (*p == '"') {
+    ++p;
+    while (p < e && *p != '"') p += (*p == '\\') ? 2 : 1;
+    return p + 1;
+  }
+  if (*p == '{' || *p == '[') {
+    int depth = 0;
+    while (p < e) {
+      char c = *p;
+      if (c == '"') {
+        p = skip_value(p, e);
+        continue;
+      }
+      if (c == '{' || c == '[') ++depth;
+      if (c == '}' || c == ']') {
+        if (--depth == 0) return p + 1;
+      }
+      ++p;
+    }
+    return p;
+  }
+  while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+  return p;
+}
+
+// Copy a validated JSON text without insignificant whitespace.
+std::string compact(std::string_view s) {
+  std::string o;
+  o.reserve(s.size());
+  bool in_str = false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    char c = s[i];
+    if (in_str) {
+      o += c;
+      if (c == '\\' && i + 1 < s.size()) o += s[++i];
+      else if (c == '"') in_str = false;
+    } else if (c == '"') {
+      in_str = true;
+      o += c;
+    } else if (c != ' ' && c != '\n' && c != '\r' && c != '\t') {
+      o += c;
+    }
+  }
+  return o;
+}
+
+bool valid_json(std::string_view s) {
+  try {
+    Parser(s).parse();
+    return true;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+bool valid_utf8(std::string_view s) {
+  for (size_t i = 0; i < s.size();) {
+    unsigned char c = (unsigned char)s[i];
+    size_t n = c < 0x80 ? 0 : (c >> 5) == 6 ? 1 : (c >> 4) == 14 ? 2 : (c >> 3) == 30 ? 3 : 99;
+    if (n == 99 || i + n >= s.size() + (n == 0)) return n == 0;
+    for (size_t k = 1; k <= n; ++k)
+      if (((unsigned char)s[i + k] >> 6) != 2) return false;
+    i += n + 1;
+  }
+  return true;
+}
+
+std::string base64(std::string_view in) {
+  static const char* t = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string o;
+  size_t i = 0;
+  for (; i + 2 < in.size(); i += 3) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += t[(v >> 6) & 63];
+    o += t[v & 63];
+  }
+  if (i + 1 == in.size()) {
+    uint32_t v = (uint8_t)in[i] << 16;
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += "==";
+  } else if (i + 2 == in.size()) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8);
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += t[(v >> 6) & 63];
+    o += '=';
+  }
+  return o;
+}
+
+std::string errno_text(int e) {
+  switch (e) {
+    case ETIMEDOUT: return "timeout";
+    case ECONNREFUSED: return "connection refused";
+    case ENOENT: return "no such socket";
+    case ECONNRESET: return "connection closed";
+    case EPROTO: return "malformed upstream response";
+    default: return std::string(strerror(e));
+  }
+}
+
+const std::string* opt_str(const Value& cfg, const char* k) {
+  auto* v = cfg.get(k);
+  return v && v->t == Value::String ? &v->s : nullptr;
+}
+
+// ------------------------------------------------------------------------------ tracing
+struct SpanCtx {
+  std::string trace_id, span_id, parent_id;
+  bool sampled = false;
+  double start_wall = 0, t0 = 0;
+  std::string traceparent() const { return "00-" + trace_id + "-" + span_id + (sampled ? "-01" : "-00"); }
+};
+
+bool parse_traceparent(const std::string* v, SpanCtx& out) {
+  if (!v) return false;
+  std::string_view s(*v);
+  // 00-<32 hex>-<16 hex>-<2 hex>
+  if (s.size() < 55 || s[2] != '-' || s[35] != '-' || s[52] != '-') return false;
+  std::string_view tid = s.substr(3, 32), pid = s.substr(36, 16);
+  if (tid == std::string(32, '0') || pid == std::string(16, '0')) return false;
+  for (char c : tid)
+    if (hexv(c) < 0) return false;
+  for (char c : pid)
+    if (hexv(c) < 0) return false;
+  int f1 = hexv(s[53]), f2 = hexv(s[54]);
+  if (f1 < 0 || f2 < 0) return false;
+  out.trace_id = std::string(tid);
+  out.parent_id = std::string(pid);
+  out.sampled = ((f1 * 16 + f2) & 1) != 0;
+  return true;
+}
+
+class Tracer {
+ public:
+  void init(const Value& cfg) {
+    if (auto* d = opt_str(cfg, "dir")) dir_ = *d;
+    if (auto* r = cfg.get("sampleRate"); r && r->t == Value::Number) rate_ = r->n;
+    if (auto* r = opt_str(cfg, "role")) role_ = *r;
+    if (auto* i = opt_str(cfg, "instance")) instance_ = *i;
+    if (auto* f = opt_str(cfg, "file")) path_ = *f;
+    if (auto* fe = cfg.get("flushEach"); fe && fe->t == Value::Bool) flush_each_ = fe->b;
+    if (!dir_.empty() && path_.empty()) {
+      mkdir(dir_.c_str(), 0755);
+      std::string safe = role_;
+      for (auto& c : safe)
+        if (c == '/') c = '_';
+      path_ = dir_ + "/spans-" + safe + "-" + std::to_string(getpid()) + ".jsonl";
+    }
+  }
+  SpanCtx start(const std::string* traceparent) {
+    SpanCtx s;
+    if (!parse_traceparent(traceparent, s)) {
+      s.trace_id = hex_u64(rng()()) + hex_u64(rng()());
+      s.parent_id.clear();
+      s.sampled = rate_ >= 1.0 || std::uniform_real_distribution<double>(0, 1)(rng()) < rate_;
+    }
+    s.span_id = hex_u64(rng()());
+    s.start_wall = wall_now();
+    s.t0 = ev::now_s();
+    return s;
+  }
+  void end(const SpanCtx& s, const std::string& name, int status, const std::vector<std::pair<std::string, std::string>>& attrs) {
+    if (!s.sampled || path_.empty()) return;
+    char dur[32];
+    std::snprintf(dur, sizeof dur, "%.3f", (ev::now_s() - s.t0) * 1000.0);
+    char ts[32];
+    std::snprintf(ts, sizeof ts, "%.6f", s.start_wall);
+    std::string l = "{\"type\":\"span\",\"role\":" + json_str(role_) + ",\"instance\":" + json_str(instance_) +
+                    ",\"name\":" + json_str(name) + ",\"kind\":\"server\",\"traceId\":\"" + s.trace_id +
+                    "\",\"spanId\":\"" + s.span_id + "\",\"parentId\":" +
+                    (s.parent_id.empty() ? std::string("null") : "\"" + s.parent_id + "\"") + ",\"ts\":" + ts +
+                    ",\"durationMs\":" + dur + ",\"status\":\"" + (status >= 500 ? "error" : "ok") +
+                    "\",\"attributes\":{\"http.status\":" + std::to_string(status);
+    for (auto& a : attrs) l += "," + json_str(a.first) + ":" + json_str(a.second);
+    l += "},\"plane\":\"native\"}\n";
+    buf_ += l;
+    if (flush_each_ || buf_.size() > 64 * 1024) flush();
+  }
+  void flush() {
+    if (buf_.empty() || path_.empty()) return;
+    if (FILE* f = std::fopen(path_.c_str(), "a")) {
+      std::fwrite(buf_.data(), 1, buf_.size(), f);
+      std::fclose(f);
+    }
+    buf_.clear();
+  }
+
+ private:
+  std::string dir_, path_, role_ = "sidecar", instance_;
+  double rate_ = 1.0;
+  bool flush_each_ = false;
+  std::string buf_;
+};
+
+// ------------------------------------------------------------------------------ registry
+// Same records the Python NameResolver writes: <dir>/<appId>/<instance>.json with
+// {"endpoint": ..., "pid": ...}; dead pids are skipped; results cached 0.5 s; round-robin.
+class Resolver {
+ public:
+  std::string dir;
+  std::vector<std::string> candidates(const std::string& app) {
+    auto& e = cache_[app];
+    double t = ev::now_s();
+    if (t - e.at > 0.5) {
+      e.eps.clear();
+      e.at = t;
+      std::string d = dir + "/" + app;
+      if (DIR* dh = opendir(d.c_str())) {
+        std::vector<std::string> files;
+        while (dirent* de = readdir(dh)) {
+          std::string n = de->d_name;
+          if (n.size() > 5 && n[0] != '.' && n.compare(n.size() - 5, 5, ".json") == 0) files.push_back(n);
+        }
+        closedir(dh);
+        std::sort(files.begin(), files.end());
+        for (auto& f : files) {
+          std::ifstream in(d + "/" + f);
+          std::stringstream ss;
+          ss << in.rdbuf();
+          try {
+            Value rec = parse(ss.str());
+            auto* ep = rec.get("endpoint");
+            auto* pid = rec.get("pid");
+            if (!ep || ep->t != Value::String) continue;
+            if (pid && pid->t == Value::Number && kill((pid_t)pid->n, 0) != 0 && errno == ESRCH) continue;
+            e.eps.push_back(ep->s);
+          } catch (const std::exception&) {
+          }
+        }
+      }
+    }
+    if (e.eps.size() <= 1) return e.eps;
+    size_t n = e.rr++ % e.eps.size();
+    std::vector<std::string> out(e.eps.begin() + (long)n, e.eps.end());
+    out.insert(out.end(), e.eps.begin(), e.eps.begin() + (long)n);
+    return out;
+  }
+  void invalidate(const std::string& app) { cache_.erase(app); }
+
+ private:
+  struct Entry {
+    double at = -1;
+    std::vector<std::string> eps;
+    size_t rr = 0;
+  };
+  std::map<std::string, Entry> cache_;
+};
+
+// ------------------------------------------------------------------------------ data plane
+struct Store {
+  Endpoint backing;
+  std::string coll_path;  // /cosmos/<acct>/<db>/<coll>
+  std::string prefix;
+  HeaderList auth;
+};
+struct Bus {
+  Endpoint backing;
+  std::string ns;
+  HeaderList auth;
+};
+
+bool is_invoke_hop(const std::string& k) {  // sidecar/runtime.py _HOP + traceparent
+  return ev::is_hop_header(k) || k == "dapr-api-token" || k == "dapr-app-id" || k == "traceparent";
+}
+
+class DataPlane {
+ public:
+  DataPlane(ev::Loop& loop, const Value& cfg) : loop_(loop), client_(loop) {
+    app_id_ = *opt_str(cfg, "appId");
+    if (auto* a = opt_str(cfg, "app")) {
+      app_ = Endpoint::parse(*a);
+      has_app_ = true;
+    }
+    if (auto* t = opt_str(cfg, "appToken")) app_token_ = *t;
+    if (auto* t = opt_str(cfg, "apiToken")) api_token_ = *t;
+    if (auto* t = opt_str(cfg, "meshToken")) mesh_token_ = *t;
+    if (auto* r = opt_str(cfg, "registryDir")) resolver_.dir = *r;
+    fallback_ = Endpoint::parse(*opt_str(cfg, "fallback"));
+    if (auto* v = cfg.get("invokeNative"); v && v->t == Value::Bool) invoke_native_ = v->b;
+    if (auto* v = cfg.get("appTimeout"); v && v->t == Value::Number) app_timeout_ = v->n;
+    if (auto* tr = cfg.get("trace")) tracer_.init(*tr);
+    if (auto* st = cfg.get("stores"); st && st->t == Value::Object)
+      for (size_t i = 0; i < st->keys.size(); ++i) {
+        const Value& s = st->items[i];
+        Store x;
+        x.backing = Endpoint::parse(*opt_str(s, "backing"));
+        x.coll_path = "/cosmos/" + quote_all(*opt_str(s, "account")) + "/" + quote_all(*opt_str(s, "db")) + "/" +
+                      quote_all(*opt_str(s, "coll"));
+        x.prefix = *opt_str(s, "prefix");
+        x.auth = auth_headers(s);
+        stores_[st->keys[i]] = std::move(x);
+      }
+    if (auto* ps = cfg.get("pubsubs"); ps && ps->t == Value::Object)
+      for (size_t i = 0; i < ps->keys.size(); ++i) {
+        const Value& s = ps->items[i];
+        Bus b;
+        b.backing = Endpoint::parse(*opt_str(s, "backing"));
+        b.ns = *opt_str(s, "ns");
+        b.auth = auth_headers(s);
+        buses_[ps->keys[i]] = std::move(b);
+      }
+  }
+
+  ev::Handler api_handler() {
+    return [this](Message&& m, Reply r) { on_api(std::move(m), std::move(r)); };
+  }
+  ev::Handler internal_handler() {
+    return [this](Message&& m, Reply r) { on_internal(std::move(m), std::move(r)); };
+  }
+  void flush() { tracer_.flush(); }
+  size_t inflight() const { return inflight_; }
+
+ private:
+  ev::Loop& loop_;
+  ev::Client client_;
+  Tracer tracer_;
+  Resolver resolver_;
+  std::string app_id_, app_token_, api_token_, mesh_token_;
+  Endpoint app_, fallback_;
+  bool has_app_ = false, invoke_native_ = true;
+  double app_timeout_ = 300;
+  std::map<std::string, Store> stores_;
+  std::map<std::string, Bus> buses_;
+  std::map<std::string, uint64_t> counters_;
+  size_t inflight_ = 0;
+
+  static HeaderList auth_headers(const Value& s) {
+    HeaderList h;
+    if (auto* i = opt_str(s, "identity"); i && !i->empty()) h.emplace_back("x-tt-identity", *i);
+    if (auto* k = opt_str(s, "key"); k && !k->empty()) h.emplace_back("x-tt-key", *k);
+    return h;
+  }
+
+  void count(const std::string& op, int status) {
+    counters_["app=\"" + app_id_ + "\",op=\"" + op + "\",status=\"" + std::to_string(status) + "\""]++;
+  }
+
+  // Wrap a Reply so every natively handled request gets a span, a counter and in-flight accounting.
+  struct Done {
+    DataPlane* dp;
+    Reply rep;
+    SpanCtx span;
+    std::string name, op;
+    std::vector<std::pair<std::string, std::string>> attrs;
+    void send(int status, const HeaderList& h, std::string_view body) {
+      rep.send(status, h, body);
+      dp->tracer_.end(span, name, status, attrs);
+      dp->count(op, status);
+      dp->inflight_--;
+    }
+    void json(int status, std::string_view body) { send(status, {{"content-type", "application/json"}}, body); }
+    void error(int status, std::string_view code, std::string_view msg) { json(status, error_json(code, msg)); }
+  };
+  std::shared_ptr<Done> begin(const Message& m, Reply&& r, std::string op, std::string_view path) {
+    inflight_++;
+    auto d = std::make_shared<Done>();
+    d->dp = this;
+    d->rep = std::move(r);
+    d->span = tracer_.start(m.header("traceparent"));
+    d->name = m.method + " " + std::string(path.substr(0, 80));
+    d->op = std::move(op);
+    return d;
+  }
+
+  static void split_target(const std::string& target, std::string& path, std::string& qs) {
+    auto q = target.find('?');
+    path = target.substr(0, q);
+    qs = q == std::string::npos ? "" : target.substr(q + 1);
+  }
+
+  // ---------------------------------------------------------------- routing
+  void on_api(Message&& m, Reply r) {
+    std::string path, qs;
+    split_target(m.target, path, qs);
+    if (!api_token_.empty() && path.rfind("/v1.0/healthz", 0) != 0) {
+      auto* t = m.header("dapr-api-token");
+      if (!t || *t != api_token_) {
+        r.json(401, error_json("ERR_API_TOKEN", "invalid api token"));
+        return;
+      }
+    }
+    std::vector<std::string_view> seg;
+    {
+      std::string_view p(path);
+      size_t i = 1;
+      while (i <= p.size()) {
+        size_t j = p.find('/', i);
+        if (j == std::string_view::npos) j = p.size();
+        seg.push_back(p.substr(i, j - i));
+        i = j + 1;
+      }
+    }
+    if (seg.size() >= 2 && lower(seg[0]) == "v1.0") {
+      std::string s1 = lower(seg[1]);
+      if (s1 == "invoke" && seg.size() >= 4 && lower(seg[3]) == "method" && invoke_native_) {
+        size_t off = (size_t)(seg[3].data() + seg[3].size() + 1 - path.data());
+        std::string method_path = off <= path.size() ? path.substr(off) : "";
+        std::string target = unquote(seg[2]);
+        target = target.substr(0, target.find('.'));
+        invoke(std::move(m), std::move(r), target, method_path, qs, path);
+        return;
+      }
+      if (s1 == "state" && seg.size() >= 3) {
+        std::string store = unquote(seg[2]);
+        auto it = stores_.find(store);
+        if (it != stores_.end()) {
+          if (seg.size() == 3 && (m.method == "POST" || m.method == "PUT")) {
+            state_save(std::move(m), std::move(r), store, it->second, path);
+            return;
+          }
+          if (seg.size() == 4 && m.method == "GET") {
+            state_get(std::move(m), std::move(r), it->second, unquote(seg[3]), path);
+            return;
+          }
+          if (seg.size() == 4 && m.method == "DELETE") {
+            state_delete(std::move(m), std::move(r), it->second, unquote(seg[3]), path);
+            return;
+          }
+        }
+      }
+      if (s1 == "publish" && seg.size() >= 4 && (m.method == "POST" || m.method == "PUT")) {
+        std::string name = unquote(seg[2]);
+        size_t off = (size_t)(seg[3].data() - path.data());
+        std::string topic = unquote(std::string_view(path).substr(off));
+        auto it = buses_.find(name);
+        if (it != buses_.end() && !topic.empty() && publish(m, r, name, topic, it->second, qs, path)) return;
+      }
+    }
+    if (path == "/metrics" && m.method == "GET") {
+      metrics(std::move(m), std::move(r));
+      return;
+    }
+    forward_to_control_plane(std::move(m), std::move(r));
+  }
+
+  // Everything the native plane does not own goes to the Python control plane verbatim.
+  void forward_to_control_plane(Message&& m, Reply r, std::function<void(std::string&)> amend = nullptr) {
+    HeaderList h;
+    for (auto& kv : m.headers)
+      if (!ev::is_hop_header(kv.first)) h.push_back(kv);
+    client_.request(fallback_, m.method, m.target, h, m.body, 0,
+                    [r, amend = std::move(amend)](ClientResult&& res) {
+                      if (res.err) {
+                        r.json(503, error_json("ERR_SIDECAR_CONTROL_PLANE", "control plane unreachable: " + errno_text(res.err)));
+                        return;
+                      }
+                      if (amend) amend(res.resp.body);
+                      r.send(res.resp.status, res.resp.headers, res.resp.body);
+                    });
+  }
+
+  void metrics(Message&& m, Reply r) {
+    std::string extra = "# HELP sidecar_native_requests_total requests served by the native data plane\n"
+                        "# TYPE sidecar_native_requests_total counter\n";
+    for (auto& kv : counters_) extra += "sidecar_native_requests_total{" + kv.first + "} " + std::to_string(kv.second) + "\n";
+    forward_to_control_plane(std::move(m), std::move(r), [extra](std::string& body) { body += extra; });
+  }
+
+  // ---------------------------------------------------------------- invoke
+  HeaderList fwd_headers(const Message& m, const std::string& traceparent, bool drop_mesh) {
+    HeaderList h;
+    h.reserve(m.headers.size() + 3);
+    for (auto& kv : m.headers) {
+      if (is_invoke_hop(kv.first)) continue;
+      if (drop_mesh && kv.first == "tt-mesh-token") continue;
+      h.push_back(kv);
+    }
+    h.emplace_back("traceparent", traceparent);
+    return h;
+  }
+
+  static void relay(Done& d, ClientResult& res) {
+    d.send(res.resp.status, res.resp.headers, res.resp.body);
+  }
+
+  void invoke(Message&& m, Reply&& r, const std::string& target, const std::string& method_path,
+              const std::string& qs, const std::string& path) {
+    auto d = begin(m, std::move(r), "invoke", path);
+    d->attrs.emplace_back("invoke.target", target);
+    HeaderList h = fwd_headers(m, d->span.traceparent(), false);
+    h.emplace_back("dapr-caller-app-id", app_id_);
+    std::string tgt = "/" + method_path + (qs.empty() ? "" : "?" + qs);
+    if (target == app_id_) {
+      call_app(m.method, tgt, std::move(h), std::move(m.body), [d, target](ClientResult&& res) {
+        if (res.err) {
+          d->error(500, "ERR_DIRECT_INVOKE", "failed to invoke, id: " + target + ", err: " + errno_text(res.err));
+          return;
+        }
+        relay(*d, res);
+      });
+      return;
+    }
+    auto cands = resolver_.candidates(target);
+    if (cands.empty()) {
+      resolver_.invalidate(target);
+      cands = resolver_.candidates(target);
+    }
+    if (cands.empty()) {
+      d->error(500, "ERR_DIRECT_INVOKE", "failed to resolve address for app-id '" + target + "'");
+      return;
+    }
+    if (!mesh_token_.empty()) h.emplace_back("tt-mesh-token", mesh_token_);
+    if (cands.size() > 3) cands.resize(3);
+    call_peer(std::make_shared<PeerCall>(PeerCall{d, target, m.method, tgt, std::move(h), std::move(m.body),
+                                                  std::move(cands), 0}));
+  }
+
+  struct PeerCall {
+    std::shared_ptr<Done> d;
+    std::string target, method, path;
+    HeaderList headers;
+    std::string body;
+    std::vector<std::string> cands;
+    size_t i;
+  };
+  void call_peer(std::shared_ptr<PeerCall> pc) {
+    Endpoint ep = Endpoint::parse(pc->cands[pc->i]);
+    client_.request(ep, pc->method, pc->path, pc->headers, pc->body, app_timeout_, [this, pc](ClientResult&& res) {
+      if (res.err == ECONNREFUSED || res.err == ENOENT || res.err == ECONNRESET) {
+        resolver_.invalidate(pc->target);  // replica went away: try the next one
+        if (++pc->i < pc->cands.size()) {
+          call_peer(pc);
+          return;
+        }
+      }
+      if (res.err) {
+        pc->d->error(500, "ERR_DIRECT_INVOKE", "failed to invoke, id: " + pc->target + ", err: " + errno_text(res.err));
+        return;
+      }
+      relay(*pc->d, res);
+    });
+  }
+
+  void call_app(const std::string& method, const std::string& target, HeaderList&& h, std::string&& body,
+                ev::ClientCallback cb) {
+    if (!has_app_) {
+      loop_.defer([cb = std::move(cb)]() mutable {
+        ClientResult r;
+        r.err = ECONNREFUSED;
+        cb(std::move(r));
+      });
+      return;
+    }
+    if (!app_token_.empty()) h.emplace_back("dapr-api-token", app_token_);
+    client_.request(app_, method, target, h, body, app_timeout_, std::move(cb));
+  }
+
+  void on_internal(Message&& m, Reply r) {
+    if (!mesh_token_.empty()) {
+      auto* t = m.header("tt-mesh-token");
+      if (!t || *t != mesh_token_) {
+        r.json(403, error_json("ERR_MESH_AUTH", "sidecar-to-sidecar call not authenticated"));
+        return;
+      }
+    }
+    std::string path, qs;
+    split_target(m.target, path, qs);
+    auto d = begin(m, std::move(r), "internal", path);
+    if (auto* c = m.header("dapr-caller-app-id")) d->attrs.emplace_back("caller", *c);
+    HeaderList h = fwd_headers(m, d->span.traceparent(), true);
+    if (auto* c = m.header("dapr-caller-app-id")) {
+      (void)c;  // already forwarded with the other headers
+    }
+    std::string app_id = app_id_;
+    call_app(m.method, m.target, std::move(h), std::move(m.body), [d, app_id](ClientResult&& res) {
+      if (res.err) {
+        d->error(502, "ERR_APP_CHANNEL", "app " + app_id + " unreachable: " + errno_text(res.err));
+        return;
+      }
+      relay(*d, res);
+    });
+  }
+
+  // ---------------------------------------------------------------- state
+  struct Item {
+    std::string key, value, etag;
+    bool first_write = false;
+    long long ttl_ms = 0;
+  };
+
+  // Parse the Dapr save-state body: [{"key","value","etag","options":{"concurrency"},"metadata":{"ttlInSeconds"}}]
+  static bool parse_items(const std::string& body, std::vector<Item>& items, std::string& err) {
+    if (!valid_json(body)) {
+      err = "request body is not valid JSON";
+      return false;
+    }
+    const char* p = ws_end(body.data(), body.data() + body.size());
+    const char* e = body.data() + body.size();
+    if (p >= e || *p != '[') {
+      err = "request body must be an array of state items";
+      return false;
+    }
+    ++p;
+    while (true) {
+      p = ws_end(p, e);
+      if (p < e && *p == ']') break;
+      if (p >= e || *p != '{') {
+        err = "state item without key";
+        return false;
+      }
+      Item it;
+      bool have_value = false;
+      ++p;
+      while (true) {
+        p = ws_end(p, e);
+        if (*p == '}') {
+          ++p;
+          break;
+        }
+        const char* ks = p;
+        p = skip_value(p, e);
+        std::string k = parse(std::string_view(ks, (size_t)(p - ks))).s;
+        p = ws_end(p, e) + 1;  // ':'
+        p = ws_end(p, e);
+        const char* vs = p;
+        p = skip_value(p, e);
+        std::string_view raw(vs, (size_t)(p - vs));
+        if (k == "key") {
+          Value v = parse(raw);
+          if (v.t == Value::String) it.key = v.s;
+        } else if (k == "value") {
+          it.value = compact(raw);
+          have_value = true;
+        } else if (k == "etag") {
+          Value v = parse(raw);
+          if (v.t == Value::String) it.etag = v.s;
+          else if (auto* x = v.get("value"); x && x->t == Value::String) it.etag = x->s;
+        } else if (k == "options") {
+          Value v = parse(raw);
+          if (auto* c = v.get("concurrency"); c && c->t == Value::String) it.first_write = c->s == "first-write";
+        } else if (k == "metadata") {
+          Value v = parse(raw);
+          if (auto* t = v.get("ttlInSeconds")) {
+            double s = t->t == Value::Number ? t->n : t->t == Value::String ? std::atof(t->s.c_str()) : 0.0;
+            it.ttl_ms = (long long)(s * 1000);
+          }
+        }
+        p = ws_end(p, e);
+        if (*p == ',') ++p;
+      }
+      if (it.key.empty()) {
+        err = "state item without key";
+        return false;
+      }
+      if (!have_value) it.value = "null";
+      items.push_back(std::move(it));
+      p = ws_end(p, e);
+      if (*p == ',') ++p;
+    }
+    return true;
+  }
+
+  void state_save(Message&& m, Reply&& r, const std::string& name, const Store& s, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.save", path);
+    std::vector<Item> items;
+    std::string err;
+    if (!parse_items(m.body, items, err)) {
+      d->error(400, "ERR_MALFORMED_REQUEST", err);
+      return;
+    }
+    auto done = [d, name](ClientResult&& res) {
+      if (!res.err && (res.resp.status == 409 || res.resp.status == 412)) {
+        d->error(409, "ERR_STATE_SAVE", "failed saving state in state store " + name + ": state save: HTTP " +
+                                            std::to_string(res.resp.status) + " " + res.resp.body.substr(0, 200));
+        return;
+      }
+      if (res.err || res.resp.status >= 300) {
+        d->error(500, "ERR_STATE_SAVE", "failed saving state in state store " + name + ": " +
+                                            (res.err ? errno_text(res.err) : "HTTP " + std::to_string(res.resp.status)));
+        return;
+      }
+      d->send(204, {}, {});
+    };
+    if (items.empty()) {
+      d->send(204, {}, {});
+      return;
+    }
+    HeaderList h = s.auth;
+    h.emplace_back("content-type", "application/json");
+    if (items.size() == 1) {
+      Item& it = items[0];
+      if (!it.etag.empty()) h.emplace_back("if-match", it.etag);
+      if (it.first_write) h.emplace_back("x-tt-first-write", "1");
+      if (it.ttl_ms) h.emplace_back("x-tt-ttl-ms", std::to_string(it.ttl_ms));
+      client_.request(s.backing, "PUT", s.coll_path + "/docs/" + quote_all(full_key(s, it.key)), h, it.value, 60,
+                      std::move(done));
+      return;
+    }
+    std::string body = "[";
+    for (size_t i = 0; i < items.size(); ++i) {
+      auto& it = items[i];
+      if (i) body += ',';
+      body += "{\"key\":" + json_str(full_key(s, it.key)) + ",\"value\":" + json_str(it.value) +
+              ",\"etag\":" + (it.etag.empty() ? std::string("null") : json_str(it.etag)) +
+              ",\"firstWrite\":" + (it.first_write ? "true" : "false") + ",\"ttlMs\":" + std::to_string(it.ttl_ms) + "}";
+    }
+    body += "]";
+    client_.request(s.backing, "POST", s.coll_path + "/bulkset", h, body, 60, std::move(done));
+  }
+
+  static std::string full_key(const Store& s, const std::string& key) {
+    if (s.prefix.empty() && key.find("||") != std::string::npos) return key;
+    return s.prefix + key;
+  }
+
+  void state_get(Message&& m, Reply&& r, const Store& s, const std::string& key, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.get", path);
+    client_.request(s.backing, "GET", s.coll_path + "/docs/" + quote_all(full_key(s, key)), s.auth, {}, 60,
+                    [d](ClientResult&& res) {
+                      if (res.err || (res.resp.status != 200 && res.resp.status != 404)) {
+                        d->error(500, "ERR_STATE_GET", "state get: " + (res.err ? errno_text(res.err)
+                                                                               : "HTTP " + std::to_string(res.resp.status)));
+                        return;
+                      }
+                      if (res.resp.status == 404) {
+                        d->send(204, {}, {});
+                        return;
+                      }
+                      const std::string* et = res.resp.header("etag");
+                      d->send(200, {{"etag", et ? *et : ""}, {"content-type", "application/json"}}, res.resp.body);
+                    });
+  }
+
+  void state_delete(Message&& m, Reply&& r, const Store& s, const std::string& key, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.delete", path);
+    HeaderList h = s.auth;
+    if (auto* im = m.header("if-match"); im && !im->empty()) h.emplace_back("if-match", *im);
+    client_.request(s.backing, "DELETE", s.coll_path + "/docs/" + quote_all(full_key(s, key)), h, {}, 60,
+                    [d](ClientResult&& res) {
+                      if (!res.err && (res.resp.status == 409 || res.resp.status == 412)) {
+                        d->error(409, "ERR_STATE_DELETE", "state delete: HTTP " + std::to_string(res.resp.status) +
+                                                              " " + res.resp.body.substr(0, 200));
+                        return;
+                      }
+                      if (res.err || (res.resp.status != 204 && res.resp.status != 404)) {
+                        d->error(500, "ERR_STATE_DELETE", "state delete: " + (res.err ? errno_text(res.err)
+                                                                                     : "HTTP " + std::to_string(res.resp.status)));
+                        return;
+                      }
+                      d->send(204, {}, {});
+                    });
+  }
+
+  // ---------------------------------------------------------------- publish
+  // Returns false when the request should go to the control plane (rare envelope shapes).
+  bool publish(Message& m, Reply& r, const std::string& name, const std::string& topic, const Bus& b,
+               const std::string& qs, const std::string& path) {
+    std::map<std::string, std::string> meta;
+    for (size_t i = 0; i <= qs.size() && !qs.empty();) {
+      size_t j = qs.find('&', i);
+      if (j == std::string::npos) j = qs.size();
+      std::string_view kv(qs.data() + i, j - i);
+      size_t eq = kv.find('=');
+      std::string k = unquote(kv.substr(0, eq), true);
+      std::string v = eq == std::string_view::npos ? "" : unquote(kv.substr(eq + 1), true);
+      if (k.rfind("metadata.", 0) == 0) meta[k.substr(9)] = v;
+      i = j + 1;
+    }
+    const std::string* ct = m.header("content-type");
+    std::string ctype = ct && !ct->empty() ? *ct : "application/json";
+    std::string base = lower(ctype.substr(0, ctype.find(';')));
+    while (!base.empty() && base.back() == ' ') base.pop_back();
+    while (!base.empty() && base.front() == ' ') base.erase(0, 1);
+    bool raw = lower(meta.count("rawPayload") ? meta["rawPayload"] : "") == "true";
+    if (!raw && base == "application/cloudevents+json") return false;
+    bool is_json = base.find("json") != std::string::npos;
+    bool json_body = is_json && !m.body.empty() && valid_json(m.body);
+    bool as_string = !json_body && (is_json || base.rfind("text/", 0) == 0 || m.body.empty());
+    if (!raw && as_string && !valid_utf8(m.body)) return false;  // Python decodes with replacement chars
+    auto d = begin(m, std::move(r), "publish", path);
+    d->attrs.emplace_back("topic", topic);
+    std::string body, out_ct;
+    if (raw) {
+      body = std::move(m.body);
+      out_ct = ctype;
+    } else {
+      std::string tp = d->span.traceparent();
+      body = "{\"specversion\":\"1.0\",\"id\":\"" + uuid4() + "\",\"source\":" + json_str(app_id_) +
+             ",\"type\":\"com.dapr.event.sent\",\"datacontenttype\":" + json_str(base.empty() ? "application/json" : base) +
+             ",\"topic\":" + json_str(topic) + ",\"pubsubname\":" + json_str(name) + ",\"time\":\"" + utc_now_iso() + "\"";
+      if (is_json) {
+        if (m.body.empty()) body += ",\"data\":null";
+        else if (json_body) body += ",\"data\":" + compact(m.body);
+        else body += ",\"data\":" + json_str(m.body);
+      } else if (base.rfind("text/", 0) == 0 || m.body.empty()) {
+        body += ",\"data\":" + json_str(m.body);
+      } else {
+        body += ",\"data_base64\":\"" + base64(m.body) + "\"";
+      }
+      body += ",\"traceparent\":\"" + tp + "\",\"traceid\":\"" + tp + "\"}";
+      out_ct = "application/cloudevents+json";
+    }
+    HeaderList h = b.auth;
+    h.emplace_back("content-type", out_ct);
+    std::string props;
+    for (auto& kv : meta) {
+      if (kv.first == "ttlInSeconds" || kv.first == "rawPayload") continue;
+      props += (props.empty() ? "{" : ",") + json_str(kv.first) + ":" + json_str(kv.second);
+    }
+    if (!props.empty()) h.emplace_back("x-tt-props", props + "}");
+    if (meta.count("ttlInSeconds")) {
+      long long ttl = (long long)(std::atof(meta["ttlInSeconds"].c_str()) * 1000);
+      if (ttl) h.emplace_back("x-tt-ttl-ms", std::to_string(ttl));
+    }
+    client_.request(b.backing, "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
+                    body, 60, [d, name, topic](ClientResult&& res) {
+                      if (res.err || res.resp.status >= 300) {
+                        d->error(500, "ERR_PUBSUB_PUBLISH_MESSAGE",
+                                 "error when publish to topic " + topic + " in pubsub " + name + ": " +
+                                     (res.err ? errno_text(res.err)
+                                              : "publish: HTTP " + std::to_string(res.resp.status) + " " +
+                                                    res.resp.body.substr(0, 200)));
+                        return;
+                      }
+                      d->send(204, {}, {});
+                    });
+    return true;
+  }
+};
+
+// ------------------------------------------------------------------------------ signals
+class SignalIo : public ev::IoObj {
+ public:
+  explicit SignalIo(std::function<void()> on) : on_(std::move(on)) {
+    sigset_t s;
+    sigemptyset(&s);
+    sigaddset(&s, SIGTERM);
+    sigaddset(&s, SIGINT);
+    sigprocmask(SIG_BLOCK, &s, nullptr);
+    fd = signalfd(-1, &s, SFD_NONBLOCK | SFD_CLOEXEC);
+  }
+  void on_event(uint32_t) override {
+    signalfd_siginfo si;
+    while (read(fd, &si, sizeof si) == (ssize_t)sizeof si) on_();
+  }
+
+ private:
+  std::function<void()> on_;
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s <config.json>\n", argv[0]);
+    return 2;
+  }
+  prctl(PR_SET_PDEATHSIG, SIGTERM);  // the Python control plane owns our lifetime
+  signal(SIGPIPE, SIG_IGN);
+  std::ifstream in(argv[1]);
+  std::stringstream ss;
+  ss << in.rdbuf();
+  Value cfg;
+  try {
+    cfg = parse(ss.str());
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "dataplane: bad config %s: %s\n", argv[1], e.what());
+    return 2;
+  }
+  ev::Loop loop;
+  DataPlane dp(loop, cfg);
+  ev::Handler api = dp.api_handler();
+  ev::Handler internal = dp.internal_handler();
+  std::string ports = "{";
+  try {
+    int http_port = 0;
+    if (auto* l = cfg.get("listen"); l && l->t == Value::Array)
+      for (auto& x : l->items) {
+        int p = ev::listen_on(loop, Endpoint::parse(x.s), api);
+        if (p) http_port = p;
+      }
+    ports += "\"http\":" + std::to_string(http_port);
+    std::string internal_ep;
+    if (auto* l = cfg.get("internal"); l && l->t == Value::Array)
+      for (auto& x : l->items) {
+        Endpoint ep = Endpoint::parse(x.s);
+        int p = ev::listen_on(loop, ep, internal);
+        if (internal_ep.empty())
+          internal_ep = ep.unix_socket ? "unix:" + ep.path + ":" : "http://127.0.0.1:" + std::to_string(p);
+      }
+    ports += ",\"internal\":" + json_str(internal_ep) + ",\"pid\":" + std::to_string(getpid()) + "}";
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "dataplane: %s\n", e.what());
+    return 1;
+  }
+  bool stopping = false;
+  double stop_deadline = 0;
+  loop.add(std::make_shared<SignalIo>([&] {
+             stopping = true;
+             stop_deadline = ev::now_s() + 5.0;
+           }),
+           EPOLLIN);
+  if (auto* pf = opt_str(cfg, "portFile")) {
+    std::string tmp = *pf + ".tmp";
+    std::ofstream(tmp) << ports;
+    std::rename(tmp.c_str(), pf->c_str());
+  }
+  double last_flush = ev::now_s();
+  loop.run([&](double t) {
+    if (t - last_flush > 1.0) {
+      dp.flush();
+      last_flush = t;
+    }
+    if (stopping && (dp.inflight() == 0 || t > stop_deadline)) loop.stop();
+  });
+  dp.flush();
+  return 0;
+}

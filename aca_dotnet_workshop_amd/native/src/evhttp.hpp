@@ -1,0 +1,904 @@
+// Single-threaded epoll event loop + HTTP/1.1 server and pooled client, used by the native
+// sidecar data plane (dataplane.cpp).
+//
+// * Loop        -- epoll (level-triggered), deferred destruction, coarse timer sweep.
+// * MsgParser   -- incremental HTTP/1.1 parser for requests and responses (Content-Length and
+//                  chunked bodies, keep-alive, pipelining).
+// * Server      -- listeners (TCP and Unix sockets) and connections that dispatch parsed
+//                  requests to a handler and write responses back in request order.
+// * Client      -- keep-alive connection pools per upstream endpoint (Unix socket or TCP), with
+//                  one transparent retry when a reused idle connection turns out to be stale.
+//
+// Everything runs on one thread; handlers complete asynchronously through Reply objects that
+// hold only weak references, so a downstream connection may close while its upstream call is
+// still in flight.
+#pragma once
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "httpparse.hpp"
+
+namespace tt::ev {
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+inline void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
+
+// ------------------------------------------------------------------------------ loop
+struct IoObj : std::enable_shared_from_this<IoObj> {
+  int fd = -1;
+  bool dead = false;
+  virtual ~IoObj() {
+    if (fd >= 0) ::close(fd);
+  }
+  virtual void on_event(uint32_t ev) = 0;
+  virtual void on_tick(double /*now*/) {}
+};
+
+class Loop {
+ public:
+  Loop() : ep_(epoll_create1(EPOLL_CLOEXEC)) {}
+  ~Loop() { ::close(ep_); }
+
+  void add(const std::shared_ptr<IoObj>& o, uint32_t ev) {
+    epoll_event e{};
+    e.events = ev;
+    e.data.ptr = o.get();
+    epoll_ctl(ep_, EPOLL_CTL_ADD, o->fd, &e);
+    objs_[o.get()] = o;
+  }
+  void mod(IoObj* o, uint32_t ev) {
+    epoll_event e{};
+    e.events = ev;
+    e.data.ptr = o;
+    epoll_ctl(ep_, EPOLL_CTL_MOD, o->fd, &e);
+  }
+  // Unregister now, destroy after the current dispatch batch (events for it may be pending).
+  void remove(IoObj* o) {
+    if (o->dead) return;
+    o->dead = true;
+    epoll_ctl(ep_, EPOLL_CTL_DEL, o->fd, nullptr);
+    auto it = objs_.find(o);
+    if (it != objs_.end()) {
+      graveyard_.push_back(std::move(it->second));
+      objs_.erase(it);
+    }
+  }
+  void defer(std::function<void()> f) { deferred_.push_back(std::move(f)); }
+  void stop() { running_ = false; }
+  bool running() const { return running_; }
+  size_t live_objects() const { return objs_.size(); }
+
+  void run(const std::function<void(double)>& tick = nullptr) {
+    epoll_event evs[256];
+    double last_tick = now_s();
+    while (running_) {
+      int n = epoll_wait(ep_, evs, 256, deferred_.empty() ? 50 : 0);
+      for (int i = 0; i < n; ++i) {
+        auto* o = static_cast<IoObj*>(evs[i].data.ptr);
+        if (!o->dead) o->on_event(evs[i].events);
+      }
+      while (!deferred_.empty()) {
+        auto d = std::move(deferred_);
+        deferred_.clear();
+        for (auto& f : d) f();
+      }
+      double t = now_s();
+      if (t - last_tick >= 0.05) {
+        last_tick = t;
+        std::vector<std::shared_ptr<IoObj>> snapshot;
+        snapshot.reserve(objs_.size());
+        for (auto& kv : objs_) snapshot.push_back(kv.second);
+        for (auto& o : snapshot)
+          if (!o->dead) o->on_tick(t);
+        if (tick) tick(t);
+      }
+      graveyard_.clear();
+    }
+  }
+
+ private:
+  int ep_;
+  bool running_ = true;
+  std::unordered_map<IoObj*, std::shared_ptr<IoObj>> objs_;
+  std::vector<std::shared_ptr<IoObj>> graveyard_;
+  std::vector<std::function<void()>> deferred_;
+};
+
+// ------------------------------------------------------------------------------ messages
+using HeaderList = std::vector<std::pair<std::string, std::string>>;
+
+struct Message {
+  // request: method/target; response: status/reason
+  std::string method, target, reason;
+  int status = 0;
+  bool http10 = false;
+  HeaderList headers;  // lower-cased names
+  std::string body;
+
+  const std::string* header(std::string_view name) const {
+    for (auto& h : headers)
+      if (h.first == name) return &h.second;
+    return nullptr;
+  }
+  bool keep_alive() const {
+    auto* c = header("connection");
+    if (!c) return !http10;
+    std::string v = *c;
+    for (auto& ch : v) ch = (char)std::tolower((unsigned char)ch);
+    if (v.find("close") != std::string::npos) return false;
+    if (http10) return v.find("keep-alive") != std::string::npos;
+    return true;
+  }
+};
+
+class MsgParser {
+ public:
+  enum Result { NEED_MORE, DONE, ERROR };
+  explicit MsgParser(bool request) : request_(request) {}
+  void expect_no_body() { no_body_ = true; }  // response to HEAD
+  std::string error;
+
+  // Consume bytes from buf[off..]; returns DONE with `out` filled when a full message is in.
+  Result feed(const std::string& buf, size_t& off, Message& out) {
+    while (true) {
+      switch (st_) {
+        case HEAD: {
+          size_t e = buf.find("\r\n\r\n", off);
+          if (e == std::string::npos) {
+            if (buf.size() - off > kMaxHead) return fail("header section too large");
+            return NEED_MORE;
+          }
+          try {
+            auto h = parse_head(std::string_view(buf).substr(off, e - off));
+            if (request_) {
+              msg_.method = std::move(h.a);
+              msg_.target = std::move(h.b);
+              msg_.http10 = h.c == "HTTP/1.0";
+            } else {
+              msg_.http10 = h.a == "HTTP/1.0";
+              msg_.status = std::atoi(h.b.c_str());
+              msg_.reason = std::move(h.c);
+            }
+            msg_.headers = std::move(h.headers);
+          } catch (const std::exception& ex) {
+            return fail(ex.what());
+          }
+          off = e + 4;
+          auto* te = msg_.header("transfer-encoding");
+          auto* cl = msg_.header("content-length");
+          bool bodyless = no_body_ || (!request_ && (msg_.status == 204 || msg_.status == 304 || msg_.status < 200));
+          if (bodyless) {
+            st_ = FINISH;
+          } else if (te && te->find("chunked") != std::string::npos) {
+            st_ = CHUNK_SIZE;
+          } else if (cl) {
+            char* end = nullptr;
+            long long n = std::strtoll(cl->c_str(), &end, 10);
+            if (n < 0 || end == cl->c_str()) return fail("bad content-length");
+            if ((size_t)n > kMaxBody) return fail("body too large");
+            remaining_ = (size_t)n;
+            st_ = remaining_ ? BODY : FINISH;
+          } else if (request_) {
+            st_ = FINISH;
+          } else {
+            st_ = UNTIL_CLOSE;  // response without length: body runs to EOF
+          }
+          break;
+        }
+        case BODY: {
+          size_t take = std::min(remaining_, buf.size() - off);
+          msg_.body.append(buf, off, take);
+          off += take;
+          remaining_ -= take;
+          if (remaining_) return NEED_MORE;
+          st_ = FINISH;
+          break;
+        }
+        case CHUNK_SIZE: {
+          size_t e = buf.find("\r\n", off);
+          if (e == std::string::npos) return buf.size() - off > 1024 ? fail("bad chunk header") : NEED_MORE;
+          remaining_ = std::strtoull(buf.c_str() + off, nullptr, 16);
+          off = e + 2;
+          if (msg_.body.size() + remaining_ > kMaxBody) return fail("body too large");
+          st_ = remaining_ ? CHUNK_DATA : TRAILERS;
+          break;
+        }
+        case CHUNK_DATA: {
+          size_t take = std::min(remaining_, buf.size() - off);
+          msg_.body.append(buf, off, take);
+          off += take;
+          remaining_ -= take;
+          if (remaining_) return NEED_MORE;
+          st_ = CHUNK_CRLF;
+          break;
+        }
+        case CHUNK_CRLF:
+          if (buf.size() - off < 2) return NEED_MORE;
+          off += 2;
+          st_ = CHUNK_SIZE;
+          break;
+        case TRAILERS: {
+          size_t e = buf.find("\r\n", off);
+          if (e == std::string::npos) return NEED_MORE;
+          bool empty = e == off;
+          off = e + 2;
+          if (empty) st_ = FINISH;
+          break;
+        }
+        case UNTIL_CLOSE:
+          msg_.body.append(buf, off, std::string::npos);
+          off = buf.size();
+          return NEED_MORE;
+        case FINISH:
+          out = std::move(msg_);
+          reset();
+          return DONE;
+      }
+    }
+  }
+  // EOF from the peer: completes a read-until-close response.
+  bool finish_on_eof(Message& out) {
+    if (st_ != UNTIL_CLOSE) return false;
+    out = std::move(msg_);
+    reset();
+    return true;
+  }
+  bool idle() const { return st_ == HEAD && msg_.headers.empty(); }
+
+ private:
+  static constexpr size_t kMaxHead = 64 * 1024;
+  static constexpr size_t kMaxBody = 256ull * 1024 * 1024;
+  enum St { HEAD, BODY, CHUNK_SIZE, CHUNK_DATA, CHUNK_CRLF, TRAILERS, UNTIL_CLOSE, FINISH } st_ = HEAD;
+  bool request_;
+  bool no_body_ = false;
+  size_t remaining_ = 0;
+  Message msg_;
+  Result fail(const char* m) {
+    error = m;
+    return ERROR;
+  }
+  void reset() {
+    msg_ = Message();
+    st_ = HEAD;
+    remaining_ = 0;
+    no_body_ = false;
+  }
+};
+
+inline const char* reason_phrase(int s) {
+  switch (s) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 202: return "Accepted";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 401: return "Unauthorized";
+    case 403: return "Forbidden";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 412: return "Precondition Failed";
+    case 413: return "Payload Too Large";
+    case 500: return "Internal Server Error";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    case 504: return "Gateway Timeout";
+    default: return "Status";
+  }
+}
+
+inline bool is_hop_header(std::string_view k) {
+  return k == "connection" || k == "keep-alive" || k == "transfer-encoding" || k == "content-length" ||
+         k == "upgrade" || k == "te" || k == "trailer" || k == "proxy-authorization" || k == "host" ||
+         k == "expect";
+}
+
+// Serialize a response; hop-by-hop headers in `headers` are dropped, framing is ours.
+inline void write_response(std::string& out, int status, const HeaderList& headers, std::string_view body,
+                           bool head_request, bool close) {
+  out += "HTTP/1.1 ";
+  out += std::to_string(status);
+  out += ' ';
+  out += reason_phrase(status);
+  out += "\r\n";
+  for (auto& h : headers) {
+    if (is_hop_header(h.first)) continue;
+    out += h.first;
+    out += ": ";
+    out += h.second;
+    out += "\r\n";
+  }
+  if (status != 204 && status != 304) {
+    out += "content-length: ";
+    out += std::to_string(body.size());
+    out += "\r\n";
+  }
+  if (close) out += "connection: close\r\n";
+  out += "\r\n";
+  if (!head_request && status != 204 && status != 304) out.append(body);
+}
+
+// ------------------------------------------------------------------------------ endpoints
+struct Endpoint {
+  bool unix_socket = true;
+  std::string path;  // unix
+  std::string host;  // tcp
+  int port = 0;
+  std::string key() const { return unix_socket ? "unix:" + path : host + ":" + std::to_string(port); }
+
+  // "unix:/path/to.sock[:]" | "http://host:port" | "tcp:host:port" | "host:port"
+  static Endpoint parse(std::string s) {
+    Endpoint e;
+    if (s.rfind("unix:", 0) == 0) {
+      s = s.substr(5);
+      if (!s.empty() && s.back() == ':') s.pop_back();
+      e.path = s;
+      return e;
+    }
+    if (s.rfind("http://", 0) == 0) s = s.substr(7);
+    if (s.rfind("tcp:", 0) == 0) s = s.substr(4);
+    while (!s.empty() && s.back() == '/') s.pop_back();
+    auto c = s.rfind(':');
+    e.unix_socket = false;
+    e.host = c == std::string::npos ? s : s.substr(0, c);
+    e.port = c == std::string::npos ? 80 : std::atoi(s.c_str() + c + 1);
+    if (e.host == "localhost") e.host = "127.0.0.1";
+    return e;
+  }
+};
+
+// ------------------------------------------------------------------------------ server
+class Server;
+class ServerConn;
+
+// Completes one request; safe to call after the connection went away.
+class Reply {
+ public:
+  Reply() = default;
+  Reply(std::weak_ptr<ServerConn> c, uint64_t seq, bool head) : conn_(std::move(c)), seq_(seq), head_(head) {}
+  void send(int status, const HeaderList& headers, std::string_view body) const;
+  void json(int status, std::string_view body) const {
+    send(status, {{"content-type", "application/json"}}, body);
+  }
+  void empty(int status) const { send(status, {}, {}); }
+
+ private:
+  std::weak_ptr<ServerConn> conn_;
+  uint64_t seq_ = 0;
+  bool head_ = false;
+};
+
+using Handler = std::function<void(Message&&, Reply)>;
+
+class ServerConn : public IoObj {
+ public:
+  ServerConn(Loop& loop, int fd, Handler& h) : loop_(loop), handler_(h), parser_(true) { this->fd = fd; }
+
+  void on_event(uint32_t ev) override {
+    if (!peer_closed_ && (ev & (EPOLLIN | EPOLLHUP | EPOLLERR))) {
+      char buf[65536];
+      while (true) {
+        ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+        if (n > 0) {
+          in_.append(buf, (size_t)n);
+          if ((size_t)n < sizeof buf) break;
+          continue;
+        }
+        if (n == 0) {
+          peer_closed_ = true;
+          break;
+        }
+        if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+        if (errno == EINTR) continue;
+        close_now();
+        return;
+      }
+      parse();
+      if (dead) return;
+      if (peer_closed_) {
+        if (pending_.empty() && out_off_ == out_.size()) {
+          close_now();
+          return;
+        }
+        update_interest();  // stop polling a half-closed socket; finish writing what is pending
+      }
+    }
+    if (ev & EPOLLOUT) flush();
+  }
+
+  void respond(uint64_t seq, int status, const HeaderList& headers, std::string_view body, bool head_request) {
+    if (dead || seq < head_seq_) return;
+    size_t idx = (size_t)(seq - head_seq_);
+    if (idx >= pending_.size() || pending_[idx].ready) return;
+    Slot& sl = pending_[idx];
+    sl.wire.reserve(body.size() + 256);
+    write_response(sl.wire, status, headers, body, head_request, sl.close_after);
+    sl.ready = true;
+    drain();
+    // resume a pipeline that was paused at its depth limit
+    if (!dead && !parsing_ && !close_after_write_ && in_off_ < in_.size()) parse();
+  }
+
+ private:
+  struct Slot {
+    bool ready = false;
+    bool close_after = false;
+    std::string wire;
+  };
+  Loop& loop_;
+  Handler& handler_;
+  MsgParser parser_;
+  std::string in_;
+  size_t in_off_ = 0;
+  std::string out_;
+  size_t out_off_ = 0;
+  std::deque<Slot> pending_;
+  uint64_t head_seq_ = 0;
+  bool peer_closed_ = false;
+  bool close_after_write_ = false;
+  bool parsing_ = false;
+  uint32_t interest_ = EPOLLIN;
+
+  void drain() {
+    while (!pending_.empty() && pending_.front().ready) {
+      out_ += pending_.front().wire;
+      if (pending_.front().close_after) close_after_write_ = true;
+      pending_.pop_front();
+      ++head_seq_;
+    }
+    flush();
+  }
+
+  void parse() {
+    parsing_ = true;
+    while (!dead && !close_after_write_ && pending_.size() < 64) {
+      Message m;
+      auto r = parser_.feed(in_, in_off_, m);
+      if (r == MsgParser::NEED_MORE) break;
+      if (r == MsgParser::ERROR) {
+        std::string w;
+        write_response(w, 400, {{"content-type", "text/plain"}}, parser_.error, false, true);
+        pending_.push_back(Slot{true, true, std::move(w)});
+        in_off_ = in_.size();
+        drain();
+        break;
+      }
+      bool ka = m.keep_alive();
+      bool head = m.method == "HEAD";
+      uint64_t seq = head_seq_ + pending_.size();
+      pending_.push_back(Slot{});
+      if (!ka) pending_.back().close_after = true, stop_reading_ = true;
+      auto self = std::static_pointer_cast<ServerConn>(shared_from_this());
+      handler_(std::move(m), Reply(self, seq, head));
+      if (stop_reading_) break;
+    }
+    parsing_ = false;
+    if (dead) return;
+    if (in_off_ > 0 && (in_off_ == in_.size() || in_off_ > 65536)) {
+      in_.erase(0, in_off_);
+      in_off_ = 0;
+    }
+  }
+  bool stop_reading_ = false;
+
+  void update_interest() {
+    uint32_t want = (peer_closed_ || stop_reading_ ? 0u : (uint32_t)EPOLLIN) |
+                    (out_off_ < out_.size() ? (uint32_t)EPOLLOUT : 0u);
+    if (want != interest_) {
+      interest_ = want;
+      loop_.mod(this, want);
+    }
+  }
+
+  void flush() {
+    while (out_off_ < out_.size()) {
+      ssize_t n = ::send(fd, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+      if (n > 0) {
+        out_off_ += (size_t)n;
+        continue;
+      }
+      if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+      if (n < 0 && errno == EINTR) continue;
+      close_now();
+      return;
+    }
+    if (out_off_ == out_.size()) {
+      out_.clear();
+      out_off_ = 0;
+      if ((close_after_write_ || peer_closed_) && pending_.empty()) {
+        close_now();
+        return;
+      }
+    }
+    update_interest();
+  }
+
+  void close_now() { loop_.remove(this); }
+};
+
+inline void Reply::send(int status, const HeaderList& headers, std::string_view body) const {
+  if (auto c = conn_.lock()) c->respond(seq_, status, headers, body, head_);
+}
+
+class Listener : public IoObj {
+ public:
+  Listener(Loop& loop, int fd, Handler& h) : loop_(loop), handler_(h) { this->fd = fd; }
+  void on_event(uint32_t) override {
+    while (true) {
+      int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (c < 0) {
+        if (errno == EINTR) continue;
+        return;  // EAGAIN or transient error (EMFILE ...): try again on the next readiness event
+      }
+      int one = 1;
+      setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // fails harmlessly on unix sockets
+      loop_.add(std::make_shared<ServerConn>(loop_, c, handler_), EPOLLIN);
+    }
+  }
+
+ private:
+  Loop& loop_;
+  Handler& handler_;
+};
+
+// Returns the bound port (tcp) or 0 (unix); throws on failure.
+inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h) {
+  int fd;
+  int port = 0;
+  if (ep.unix_socket) {
+    fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    sockaddr_un a{};
+    a.sun_family = AF_UNIX;
+    if (ep.path.size() >= sizeof a.sun_path) throw std::runtime_error("unix socket path too long: " + ep.path);
+    std::strcpy(a.sun_path, ep.path.c_str());
+    ::unlink(ep.path.c_str());
+    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0) throw std::runtime_error("bind " + ep.path + ": " + strerror(errno));
+  } else {
+    fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)ep.port);
+    inet_pton(AF_INET, ep.host.c_str(), &a.sin_addr);
+    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0)
+      throw std::runtime_error("bind " + ep.key() + ": " + strerror(errno));
+    socklen_t len = sizeof a;
+    getsockname(fd, (sockaddr*)&a, &len);
+    port = ntohs(a.sin_port);
+  }
+  if (::listen(fd, 1024) != 0) throw std::runtime_error(std::string("listen: ") + strerror(errno));
+  loop.add(std::make_shared<Listener>(loop, fd, h), EPOLLIN);
+  return port;
+}
+
+// ------------------------------------------------------------------------------ client
+struct ClientResult {
+  int err = 0;  // 0 = ok; otherwise errno-like (ECONNREFUSED, ENOENT, ETIMEDOUT, ECONNRESET ...)
+  Message resp;
+};
+using ClientCallback = std::function<void(ClientResult&&)>;
+
+class Client;
+
+class ClientConn : public IoObj {
+ public:
+  ClientConn(Loop& loop, Client& owner, std::string key) : loop_(loop), owner_(owner), key_(std::move(key)), parser_(false) {}
+  bool reused = false;
+  bool connecting = false;
+
+  void start(std::string&& wire, bool head, double deadline, ClientCallback&& cb) {
+    out_ = std::move(wire);
+    out_off_ = 0;
+    cb_ = std::move(cb);
+    deadline_ = deadline;
+    got_bytes_ = false;
+    busy_ = true;
+    if (head) parser_.expect_no_body();
+    if (!connecting) flush();
+  }
+  void on_event(uint32_t ev) override;
+  void on_tick(double now) override {
+    if (busy_ && deadline_ > 0 && now > deadline_) fail(ETIMEDOUT);
+    else if (!busy_ && now - idle_since_ > 30.0) loop_.remove(this);  // idle pool entry aged out
+  }
+  bool busy() const { return busy_; }
+  std::string wire_copy;  // kept for the stale-connection retry
+  bool head_req = false;
+
+ private:
+  friend class Client;
+  Loop& loop_;
+  Client& owner_;
+  std::string key_;
+  MsgParser parser_;
+  std::string in_;
+  size_t in_off_ = 0;
+  std::string out_;
+  size_t out_off_ = 0;
+  ClientCallback cb_;
+  double deadline_ = 0;
+  double idle_since_ = 0;
+  bool busy_ = false;
+  bool got_bytes_ = false;
+  bool want_out_ = false;
+
+  void flush();
+  void fail(int err);
+  void finish(Message&& m, bool keep);
+};
+
+class Client {
+ public:
+  explicit Client(Loop& loop) : loop_(loop) {}
+
+  // Issue `method target` with `headers`/`body` to `ep`; `cb` runs on completion or failure.
+  void request(const Endpoint& ep, std::string_view method, std::string_view target, const HeaderList& headers,
+               std::string_view body, double timeout_s, ClientCallback cb) {
+    std::string w;
+    w.reserve(body.size() + 512);
+    w.append(method);
+    w += ' ';
+    w.append(target);
+    w += " HTTP/1.1\r\nhost: ";
+    w += ep.unix_socket ? "localhost" : ep.host + ":" + std::to_string(ep.port);
+    w += "\r\n";
+    for (auto& h : headers) {
+      if (is_hop_header(h.first)) continue;
+      w += h.first;
+      w += ": ";
+      w += h.second;
+      w += "\r\n";
+    }
+    w += "content-length: ";
+    w += std::to_string(body.size());
+    w += "\r\n\r\n";
+    w.append(body);
+    dispatch(ep, std::move(w), method == "HEAD", timeout_s, std::move(cb), true);
+  }
+
+  void release(const std::shared_ptr<ClientConn>& c) {
+    auto& v = idle_[c->key_];
+    if (v.size() < 256) {
+      c->idle_since_ = now_s();
+      v.push_back(c);
+    } else {
+      loop_.remove(c.get());
+    }
+  }
+  void forget(ClientConn* c) {
+    auto it = idle_.find(c->key_);
+    if (it == idle_.end()) return;
+    auto& v = it->second;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i].get() == c) {
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+  }
+  Loop& loop() { return loop_; }
+
+  void dispatch(const Endpoint& ep, std::string&& wire, bool head, double timeout_s, ClientCallback&& cb,
+                bool allow_retry) {
+    std::string key = ep.key();
+    std::shared_ptr<ClientConn> c;
+    auto& v = idle_[key];
+    while (!v.empty()) {
+      c = v.back();
+      v.pop_back();
+      if (!c->dead) break;
+      c.reset();
+    }
+    double deadline = timeout_s > 0 ? now_s() + timeout_s : 0;
+    if (c) {
+      c->reused = true;
+    } else {
+      int err = 0;
+      c = connect(ep, key, err);
+      if (!c) {
+        loop_.defer([cb = std::move(cb), err]() mutable {
+          ClientResult r;
+          r.err = err;
+          cb(std::move(r));
+        });
+        return;
+      }
+    }
+    if (allow_retry && c->reused) {
+      // a reused keep-alive connection may have been closed by the peer: retry once on a new one
+      auto ep_copy = ep;
+      auto wire_copy = wire;
+      ClientCallback inner = [this, ep_copy, wire_copy = std::move(wire_copy), head, timeout_s,
+                              cb = std::move(cb)](ClientResult&& r) mutable {
+        if (r.err == ECONNRESET || r.err == EPIPE) {
+          dispatch(ep_copy, std::move(wire_copy), head, timeout_s, std::move(cb), false);
+          return;
+        }
+        cb(std::move(r));
+      };
+      c->start(std::move(wire), head, deadline, std::move(inner));
+    } else {
+      c->start(std::move(wire), head, deadline, std::move(cb));
+    }
+  }
+
+ private:
+  Loop& loop_;
+  std::unordered_map<std::string, std::vector<std::shared_ptr<ClientConn>>> idle_;
+
+  std::shared_ptr<ClientConn> connect(const Endpoint& ep, const std::string& key, int& err) {
+    int fd;
+    bool in_progress = false;
+    if (ep.unix_socket) {
+      fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      sockaddr_un a{};
+      a.sun_family = AF_UNIX;
+      std::strncpy(a.sun_path, ep.path.c_str(), sizeof a.sun_path - 1);
+      // blocking connect on a local socket: completes immediately (or waits for backlog room)
+      if (::connect(fd, (sockaddr*)&a, sizeof a) != 0) {
+        err = errno;
+        ::close(fd);
+        return nullptr;
+      }
+      set_nonblock(fd);
+    } else {
+      fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)ep.port);
+      inet_pton(AF_INET, ep.host.c_str(), &a.sin_addr);
+      if (::connect(fd, (sockaddr*)&a, sizeof a) != 0) {
+        if (errno != EINPROGRESS) {
+          err = errno;
+          ::close(fd);
+          return nullptr;
+        }
+        in_progress = true;
+      }
+    }
+    auto c = std::make_shared<ClientConn>(loop_, *this, key);
+    c->fd = fd;
+    c->connecting = in_progress;
+    loop_.add(c, in_progress ? (EPOLLOUT | EPOLLIN) : EPOLLIN);
+    if (in_progress) c->want_out_ = true;
+    return c;
+  }
+};
+
+inline void ClientConn::on_event(uint32_t ev) {
+  if (connecting && (ev & (EPOLLOUT | EPOLLERR | EPOLLHUP))) {
+    int e = 0;
+    socklen_t l = sizeof e;
+    getsockopt(fd, SOL_SOCKET, SO_ERROR, &e, &l);
+    if (e != 0) {
+      fail(e);
+      return;
+    }
+    connecting = false;
+  }
+  if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+    char buf[65536];
+    bool eof = false;
+    while (true) {
+      ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+      if (n > 0) {
+        in_.append(buf, (size_t)n);
+        got_bytes_ = true;
+        if ((size_t)n < sizeof buf) break;
+        continue;
+      }
+      if (n == 0) {
+        eof = true;
+        break;
+      }
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      if (errno == EINTR) continue;
+      fail(got_bytes_ ? EIO : ECONNRESET);
+      return;
+    }
+    if (busy_ && !in_.empty()) {
+      Message m;
+      auto r = parser_.feed(in_, in_off_, m);
+      if (r == MsgParser::DONE) {
+        bool keep = !eof && m.keep_alive() && in_off_ == in_.size();
+        finish(std::move(m), keep);
+        return;
+      }
+      if (r == MsgParser::ERROR) {
+        fail(EPROTO);
+        return;
+      }
+    }
+    if (eof) {
+      Message m;
+      if (busy_ && parser_.finish_on_eof(m)) {
+        finish(std::move(m), false);
+        return;
+      }
+      if (busy_) fail(got_bytes_ ? EIO : ECONNRESET);
+      else {
+        owner_.forget(this);
+        loop_.remove(this);
+      }
+      return;
+    }
+  }
+  if (!dead && (ev & EPOLLOUT) && busy_) flush();
+}
+
+inline void ClientConn::flush() {
+  while (out_off_ < out_.size()) {
+    ssize_t n = ::send(fd, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+    if (n > 0) {
+      out_off_ += (size_t)n;
+      continue;
+    }
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (n < 0 && errno == EINTR) continue;
+    fail(errno == EPIPE ? EPIPE : ECONNRESET);
+    return;
+  }
+  bool need_out = out_off_ < out_.size();
+  if (need_out != want_out_) {
+    want_out_ = need_out;
+    loop_.mod(this, need_out ? (EPOLLIN | EPOLLOUT) : EPOLLIN);
+  }
+  if (!need_out) {
+    out_.clear();
+    out_off_ = 0;
+  }
+}
+
+inline void ClientConn::fail(int err) {
+  auto self = shared_from_this();  // keep alive through the callback
+  busy_ = false;
+  owner_.forget(this);
+  loop_.remove(this);
+  if (cb_) {
+    auto cb = std::move(cb_);
+    cb_ = nullptr;
+    ClientResult r;
+    r.err = err;
+    cb(std::move(r));
+  }
+}
+
+inline void ClientConn::finish(Message&& m, bool keep) {
+  auto self = std::static_pointer_cast<ClientConn>(shared_from_this());
+  busy_ = false;
+  in_.erase(0, in_off_);
+  in_off_ = 0;
+  auto cb = std::move(cb_);
+  cb_ = nullptr;
+  if (keep) owner_.release(self);
+  else loop_.remove(this);
+  ClientResult r;
+  r.resp = std::move(m);
+  cb(std::move(r));
+}
+
+}  // namespace tt::ev

@@ -38,7 +38,7 @@ def vkey(v: Any) -> str:
     if isinstance(v, bool):
         return "b1" if v else "b0"
     if isinstance(v, (int, float)):
-        return "d" + repr(float(v))
+        return "d" + repr(float(v) + 0.0)  # + 0.0 folds -0.0 into 0.0 (IEEE equality)
     if isinstance(v, str):
         return "s" + v
     return "j" + json.dumps(_norm(v), separators=(",", ":"))
@@ -48,7 +48,7 @@ def _norm(v: Any) -> Any:
     if isinstance(v, bool) or v is None or isinstance(v, str):
         return v
     if isinstance(v, (int, float)):
-        return float(v)
+        return float(v) + 0.0
     if isinstance(v, list):
         return [_norm(x) for x in v]
     if isinstance(v, dict):

@@ -63,6 +63,8 @@ class LocalStack:
         self.registry = self.root / "registry"
         self.components = components or [str(REPO_ROOT / "deploy" / "components")]
         self.base_env = dict(os.environ)
+        # process-based deployments run the sidecar's native C++ data plane unless told otherwise
+        self.base_env.setdefault("TT_SIDECAR_DATAPLANE", "native")
         self.base_env["PYTHONPATH"] = str(REPO_ROOT) + os.pathsep + self.base_env.get("PYTHONPATH", "")
         self.base_env.update(env or {})
         self.log_dir = Path(log_dir) if log_dir else self.root / "logs"
@@ -158,6 +160,40 @@ class LocalStack:
                 raise TimeoutError(f"replicas not ready: {[r.name for r in pending]}")
             time.sleep(0.05)
 
+    def cpu_seconds(self) -> dict[str, float]:
+        """User+system CPU seconds consumed so far by every process of the stack, keyed by role
+        (``backing``, ``backing-<families>``, ``<replica>.sidecar``, ``<replica>.app``).  Used by
+        ``bench.py`` to attribute where the end-to-end flow spends its cycles."""
+        import psutil
+
+        def cpu(pid: int) -> float:
+            try:
+                t = psutil.Process(pid).cpu_times()
+                return t.user + t.system
+            except psutil.Error:
+                return 0.0
+
+        out: dict[str, float] = {}
+        if self.backing_proc is not None:
+            out["backing"] = cpu(self.backing_proc.pid)
+        seen = {self.backing_proc.pid} if self.backing_proc is not None else set()
+        for fam, (p, _url) in self.extra_backing.items():
+            if p.pid not in seen:  # one process may serve several service families
+                seen.add(p.pid)
+                out[f"backing-{fam.lower()}"] = cpu(p.pid)
+        for rs in self.replicas.values():
+            for r in rs:
+                out[f"{r.name}.sidecar"] = cpu(r.proc.pid)
+                try:
+                    kids = psutil.Process(r.proc.pid).children(recursive=True)
+                except psutil.Error:
+                    kids = []
+                dp = [k for k in kids if _is_dataplane(k)]
+                if dp:
+                    out[f"{r.name}.dataplane"] = sum(cpu(k.pid) for k in dp)
+                out[f"{r.name}.app"] = sum(cpu(k.pid) for k in kids if k not in dp)
+        return out
+
     def stop_replica(self, r: ReplicaProc, timeout: float = 10.0) -> None:
         _terminate(r.proc, timeout)
         if r in self.replicas.get(r.app_id, []):
@@ -188,6 +224,14 @@ class LocalStack:
 
     def __exit__(self, *exc) -> None:
         self.stop()
+
+
+def _is_dataplane(p) -> bool:
+    try:
+        cmd = p.cmdline()
+    except Exception:
+        return False
+    return bool(cmd) and cmd[0].endswith("ttsidecar-dataplane")
 
 
 def _terminate(p: subprocess.Popen, timeout: float) -> None:

@@ -22,6 +22,7 @@ from pathlib import Path
 from typing import Any, Callable
 
 from ..telemetry import REGISTRY, configure, configure_logging, metrics_middleware, server_middleware
+from ..telemetry.profiler import maybe_profile
 from ..utils.config import Configuration, load_configuration
 from ..web.app import WebApp
 from ..web.http import Response, empty, json_response, text_response
@@ -126,7 +127,8 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
 
 def run_host(app: WebApp) -> None:
     try:
-        asyncio.run(serve_host(app))
+        with maybe_profile(f"{os.environ.get('TT_REPLICA_NAME') or app.name}.app"):
+            asyncio.run(serve_host(app))
     except KeyboardInterrupt:
         pass
     sys.exit(0)

@@ -21,6 +21,7 @@ import subprocess
 import sys
 
 from ..telemetry import configure_logging
+from ..telemetry.profiler import maybe_profile
 from .runtime import Sidecar
 
 log = logging.getLogger("sidecar.cli")
@@ -105,7 +106,8 @@ def main(argv: list[str] | None = None) -> int:
     configure_logging(f"{a.app_id}.sidecar")
     logging.getLogger().setLevel(getattr(logging, a.log_level.upper(), logging.INFO))
     try:
-        return asyncio.run(_run(a))
+        with maybe_profile(f"{a.replica_name or a.app_id}.sidecar"):
+            return asyncio.run(_run(a))
     except KeyboardInterrupt:
         return 0
 

@@ -76,7 +76,7 @@ class Sidecar:
                  mesh_token: str | None = None, app_max_concurrency: int | None = None,
                  identity: str | None = None, backing_url: str | None = None, environ: dict[str, str] | None = None,
                  telemetry_dir: str | None = None, instance: str | None = None,
-                 app_health_path: str | None = None) -> None:
+                 app_health_path: str | None = None, data_plane: str | None = None) -> None:
         self.app_id = app_id
         self.app_port = app_port
         self.app_uds = app_uds
@@ -103,6 +103,12 @@ class Sidecar:
         self.tracer = Tracer(f"{app_id}.sidecar", telemetry_dir or self.environ.get("TT_TELEMETRY_DIR") or None,
                              float(self.environ.get("TT_TRACE_SAMPLE_RATE", "1.0")), self.instance)
         self.app_sem = asyncio.Semaphore(app_max_concurrency) if app_max_concurrency else None
+        # "native": hot API paths served by the C++ data plane (native/src/dataplane.cpp), this
+        # process keeps the control plane behind a private socket.  Not used with
+        # --app-max-concurrency (the app-channel semaphore lives here).
+        self.data_plane = (data_plane or self.environ.get("TT_SIDECAR_DATAPLANE") or "python").lower()
+        self._dp_proc: asyncio.subprocess.Process | None = None
+        self._dp_dir: str | None = None
         self.components: dict[str, Component] = {}
         self.secret_stores: dict[str, SecretStore] = {}
         self.state_stores: dict[str, StateStore] = {}
@@ -127,6 +133,24 @@ class Sidecar:
         api = self._build_api()
         internal = self._build_internal()
         loop = asyncio.get_running_loop()
+        if self.data_plane == "native" and self.app_sem is None:
+            await self._start_native_data_plane(api)
+        else:
+            await self._start_python_servers(api, internal, loop)
+        self.resolver.register(self.app_id, self.instance, self.bound_internal,
+                               {"httpPort": self.bound_http_port, "dataPlane": self.active_data_plane})
+        self.ready.set()
+        log.info("sidecar %s up: api=%s%s internal=%s plane=%s components=%s", self.app_id, self.bound_http_port,
+                 f" uds={self.uds}" if self.uds else "", self.bound_internal, self.active_data_plane,
+                 sorted(self.components))
+        if self.app_port is not None or self.app_uds:
+            self._bg.append(asyncio.ensure_future(self._app_startup()))
+
+    @property
+    def active_data_plane(self) -> str:
+        return "native" if self._dp_proc is not None else "python"
+
+    async def _start_python_servers(self, api: WebApp, internal: WebApp, loop) -> None:
         srv = HttpServer(api, loop)
         if self.http_port is not None:
             self.bound_http_port = await srv.listen_tcp(self.http_host, self.http_port)
@@ -142,13 +166,79 @@ class Sidecar:
             if self.bound_internal is None:
                 self.bound_internal = f"http://127.0.0.1:{p}"
         self._servers.append(isrv)
-        self.resolver.register(self.app_id, self.instance, self.bound_internal,
-                               {"httpPort": self.bound_http_port})
-        self.ready.set()
-        log.info("sidecar %s up: api=%s%s internal=%s components=%s", self.app_id, self.bound_http_port,
-                 f" uds={self.uds}" if self.uds else "", self.bound_internal, sorted(self.components))
-        if self.app_port is not None or self.app_uds:
-            self._bg.append(asyncio.ensure_future(self._app_startup()))
+
+    def data_plane_config(self, fallback: str) -> dict[str, Any]:
+        """What the native data plane needs to serve invoke/state/publish on its own."""
+        from .pubsub import BackingTransport
+        from .state import BackingStateStore
+        stores = {}
+        for name, st in self.state_stores.items():
+            if isinstance(st, BackingStateStore):
+                stores[name] = {"backing": st.client.base, "account": st.account, "db": st.db, "coll": st.coll,
+                                "prefix": st.prefix, "identity": st.client.identity or "", "key": st.client.key or ""}
+        buses = {}
+        for name, ps in self.pubsubs.items():
+            t = getattr(ps, "transport", None)
+            if isinstance(t, BackingTransport):
+                buses[name] = {"backing": t.client.base, "ns": t.ns, "identity": t.client.identity or "",
+                               "key": t.client.key or ""}
+        listen = []
+        if self.uds:
+            listen.append("unix:" + self.uds)
+        if self.http_port is not None:
+            listen.append(f"tcp:{self.http_host}:{self.http_port}")
+        internal = []
+        if self.internal_uds:
+            internal.append("unix:" + self.internal_uds)
+        if self.internal_port is not None and (self.internal_port or not self.internal_uds):
+            internal.append(f"tcp:127.0.0.1:{self.internal_port}")
+        app = None
+        if self.app_uds:
+            app = "unix:" + self.app_uds
+        elif self.app_port is not None:
+            app = f"tcp:127.0.0.1:{self.app_port}"
+        ex = self.tracer.exporter
+        return {"appId": self.app_id, "app": app, "appToken": self.app_token, "apiToken": self.api_token,
+                "meshToken": self.mesh_token, "registryDir": str(self.resolver.dir) if self.resolver.dir else None,
+                "fallback": fallback, "invokeNative": self.resolver.dir is not None, "appTimeout": 300.0,
+                "listen": listen, "internal": internal, "stores": stores, "pubsubs": buses,
+                "trace": {"dir": ex.directory, "sampleRate": self.tracer.sample_rate, "role": self.tracer.role,
+                          "instance": self.instance}}
+
+    async def _start_native_data_plane(self, api: WebApp) -> None:
+        import tempfile
+        from ..native.build import build_dataplane
+        exe = build_dataplane()  # no silent fallback: a requested native plane must run
+        self._dp_dir = tempfile.mkdtemp(prefix="ttdp-")
+        private = os.path.join(self._dp_dir, "cp.sock")
+        srv = HttpServer(api, asyncio.get_running_loop())
+        await srv.listen_unix(private)
+        self._servers.append(srv)
+        cfg = self.data_plane_config("unix:" + private)
+        cfg["portFile"] = os.path.join(self._dp_dir, "ports.json")
+        ex = self.tracer.exporter
+        if ex.keep_in_memory:
+            # no telemetry directory: the data plane writes its spans to a private file that is
+            # relayed into this tracer's in-memory sink on access
+            relay = os.path.join(self._dp_dir, "spans.jsonl")
+            cfg["trace"].update({"file": relay, "flushEach": True})
+            ex.attach_source(_span_file_reader(relay))
+        cfg_path = os.path.join(self._dp_dir, "config.json")
+        with open(cfg_path, "w") as f:
+            json.dump(cfg, f)
+        self._dp_proc = await asyncio.create_subprocess_exec(str(exe), cfg_path)
+        deadline = time.monotonic() + 30
+        while not os.path.exists(cfg["portFile"]):
+            if self._dp_proc.returncode is not None:
+                raise RuntimeError(f"native data plane exited with {self._dp_proc.returncode}")
+            if time.monotonic() > deadline:
+                raise TimeoutError("native data plane did not start")
+            await asyncio.sleep(0.01)
+        with open(cfg["portFile"]) as f:
+            ports = json.load(f)
+        if self.http_port is not None:
+            self.bound_http_port = ports["http"]
+        self.bound_internal = ports["internal"] or None
 
     async def stop(self, grace: float = 5.0) -> None:
         if self.stopped.is_set():
@@ -161,8 +251,18 @@ class Sidecar:
             await c.stop(grace)
         for b in self.bindings.values():
             await b.close()
+        if self._dp_proc is not None and self._dp_proc.returncode is None:
+            self._dp_proc.terminate()
+            try:
+                await asyncio.wait_for(self._dp_proc.wait(), grace + 1)
+            except asyncio.TimeoutError:
+                self._dp_proc.kill()
+                await self._dp_proc.wait()
         for srv in self._servers:
             await srv.close(grace)
+        if self._dp_dir:
+            import shutil
+            shutil.rmtree(self._dp_dir, ignore_errors=True)
         for group in (self.pubsubs, self.state_stores, self.secret_stores):
             for comp in group.values():
                 try:
@@ -788,6 +888,7 @@ class Sidecar:
             "id": self.app_id, "runtimeVersion": RUNTIME_VERSION, "components": comps, "subscriptions": subs,
             "inputBindings": self.input_bindings, "failedComponents": self.failed_components,
             "extended": {"instance": self.instance, "appReady": self.app_ready.is_set(),
+                         "dataPlane": self.active_data_plane,
                          "consumers": {c.name: c.stats for c in self.consumers}},
             "appConnectionProperties": {"port": self.app_port, "uds": self.app_uds, "protocol": "http"},
         })
@@ -801,6 +902,23 @@ class Sidecar:
 
     async def h_metrics(self, req: Request) -> Response:
         return Response(REGISTRY.expose().encode(), 200, None, "text/plain; version=0.0.4")
+
+
+def _span_file_reader(path: str):
+    pos = 0
+
+    def read() -> list[dict[str, Any]]:
+        nonlocal pos
+        try:
+            with open(path, "rb") as f:
+                f.seek(pos)
+                data = f.read()
+        except FileNotFoundError:
+            return []
+        end = data.rfind(b"\n") + 1
+        pos += end
+        return [json.loads(line) for line in data[:end].splitlines() if line.strip()]
+    return read
 
 
 def _metadata_from_query(qs: str) -> dict[str, str]:

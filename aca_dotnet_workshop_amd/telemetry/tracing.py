@@ -58,7 +58,8 @@ class Exporter:
         self._buf: list[str] = []
         self._lock = threading.Lock()
         self._fh = None
-        self.memory: list[dict[str, Any]] = []
+        self._memory: list[dict[str, Any]] = []
+        self._sources: list[Any] = []  # callables returning span records produced elsewhere
         self.keep_in_memory = directory is None
         if directory:
             os.makedirs(directory, exist_ok=True)
@@ -68,15 +69,27 @@ class Exporter:
 
     def export(self, rec: dict[str, Any]) -> None:
         if self.keep_in_memory:
-            self.memory.append(rec)
-            if len(self.memory) > 10000:
-                del self.memory[:5000]
+            self._memory.append(rec)
+            if len(self._memory) > 10000:
+                del self._memory[:5000]
             return
         line = json.dumps(rec, separators=(",", ":"))
         with self._lock:
             self._buf.append(line)
             if len(self._buf) >= 256:
                 self._flush_locked()
+
+    @property
+    def memory(self) -> list[dict[str, Any]]:
+        """In-memory spans (no telemetry directory), including those relayed by attached
+        sources such as the native sidecar data plane."""
+        for src in self._sources:
+            for rec in src():
+                self.export(rec)
+        return self._memory
+
+    def attach_source(self, fn) -> None:
+        self._sources.append(fn)
 
     def _flush_locked(self) -> None:
         if self._fh is not None and self._buf:

@@ -153,10 +153,17 @@ def main() -> None:
         lat: list[float] = []
         d.barrier()
         device_sync()
+        cpu0 = stack.cpu_seconds()
         dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
         device_sync()
         d.barrier()
+        cpu1 = stack.cpu_seconds()
         dt_max = d.max(dt)
+        if d.rank == 0:
+            # cores busy per process role during the timed region (where the E2E flow is CPU bound)
+            util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
+            print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2)}),
+                  file=sys.stderr, flush=True)
         lat.sort()
         p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
         p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0

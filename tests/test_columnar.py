@@ -8,7 +8,7 @@ import random
 
 import numpy as np
 import pytest
-from hypothesis import given, settings
+from hypothesis import example, given, settings
 from hypothesis import strategies as st
 
 from aca_dotnet_workshop_amd import native
@@ -70,6 +70,7 @@ def _columnar(ops):
 
 @settings(max_examples=250, deadline=None)
 @given(docs_st, filters_st, sort_st, st.integers(0, 1000))
+@example(docs=[{"f": None, "h": {"k": -0.0}}], flt={"EQ": {"h.k": 0}}, sort=None, seed=0)  # -0.0 == 0
 def test_numpy_executor_matches_native(docs, flt, sort, seed):
     if not docs:
         return

@@ -1,0 +1,289 @@
+"""Sidecar API parity: the same assertions run against the Python plane and the native C++
+data plane (native/src/dataplane.cpp) -- state save/get/delete with ETags and concurrency
+modes, publish envelopes, self and peer service invocation, API token, error codes,
+tracing propagation, HTTP framing (keep-alive, pipelining, Connection: close)."""
+import asyncio
+import json
+import re
+import socket
+
+import pytest
+
+from aca_dotnet_workshop_amd.backing import BackingServices
+from aca_dotnet_workshop_amd.sdk import cloud_events_middleware, map_subscribe_handler, topic
+from aca_dotnet_workshop_amd.sidecar import NameResolver, Sidecar, from_dict
+from aca_dotnet_workshop_amd.web import HttpClient, HttpServer, Response, WebApp, empty, json_response
+
+from helpers import run
+
+PLANES = ["python", "native"]
+
+
+def _comp(name, type_, meta, **extra):
+    d = {"apiVersion": "dapr.io/v1alpha1", "kind": "Component", "metadata": {"name": name},
+         "spec": {"type": type_, "version": "v1", "metadata": [{"name": k, "value": v} for k, v in meta.items()]}}
+    d.update(extra)
+    return from_dict(d)
+
+
+STORE = _comp("statestore", "state.azure.cosmosdb", {"url": "https://acct1.documents.azure.com:443/",
+                                                     "database": "db", "collection": "tasks"})
+BUS = _comp("bus", "pubsub.azure.servicebus", {"connectionString": "Endpoint=sb://ns1.servicebus.windows.net/"})
+MEM = _comp("mem", "state.in-memory", {})
+
+
+def _app(name, seen):
+    app = WebApp(name)
+    app.use(cloud_events_middleware())
+
+    async def echo(req):
+        seen.append(("echo", req.method, req.path, req.query_string, dict(req.headers.items()), req.body))
+        return Response(json.dumps({"app": name, "method": req.method, "q": req.query_string,
+                                    "body": req.body.decode()}).encode(), 201,
+                        [("X-Echo", "1"), ("Content-Type", "application/json")])
+
+    async def boom(req):
+        return json_response({"error": "boom"}, 500)
+
+    async def events(req):
+        seen.append(("event", req.headers.get("traceparent"), req.json()))
+        return empty(200)
+
+    async def raw_events(req):
+        seen.append(("raw", req.content_type, req.body))
+        return empty(200)
+
+    app.add_route("/api/echo/{*rest}", echo, ("GET", "POST", "PUT", "DELETE", "HEAD"))
+    app.add_route("/api/boom", boom, ("GET",))
+    topic("bus", "events")(events)
+    app.add_route("/events", events, ("POST",))
+    topic("bus", "rawtopic", metadata={"rawPayload": "true"})(raw_events)
+    app.add_route("/raw", raw_events, ("POST",))
+    map_subscribe_handler(app)
+    return app
+
+
+class Env:
+    """Backing services + N (app, sidecar) pairs sharing a registry directory."""
+
+    def __init__(self, plane, tmp_path, apps=("app-a",), **sc_kw):
+        self.plane, self.tmp, self.names, self.sc_kw = plane, tmp_path, apps, sc_kw
+        self.seen = {n: [] for n in apps}
+
+    async def __aenter__(self):
+        loop = asyncio.get_running_loop()
+        self.backing = BackingServices()
+        self.bsrv = HttpServer(self.backing.build_app(), loop)
+        self.burl = f"http://127.0.0.1:{await self.bsrv.listen_tcp('127.0.0.1', 0)}"
+        self.servers, self.sidecars, self.base = [], {}, {}
+        for n in self.names:
+            app = _app(n, self.seen[n])
+            srv = HttpServer(app, loop)
+            await app.startup()
+            port = await srv.listen_tcp("127.0.0.1", 0)
+            self.servers.append(srv)
+            sc = Sidecar(n, app_port=port, http_port=0, components=[STORE, BUS, MEM],
+                         resolver=NameResolver(str(self.tmp / "registry")), backing_url=self.burl,
+                         internal_uds=str(self.tmp / f"{n}.i.sock"), data_plane=self.plane, **self.sc_kw)
+            await sc.start()
+            await asyncio.wait_for(sc.app_ready.wait(), 10)
+            assert sc.active_data_plane == self.plane
+            self.sidecars[n] = sc
+            self.base[n] = f"http://127.0.0.1:{sc.bound_http_port}"
+        self.http = HttpClient()
+        return self
+
+    async def __aexit__(self, *exc):
+        for sc in self.sidecars.values():
+            await sc.stop(1.0)
+        for s in self.servers:
+            await s.close(1.0)
+        await self.bsrv.close(1.0)
+        await self.http.close()
+
+
+async def _until(pred, timeout=5.0):
+    end = asyncio.get_running_loop().time() + timeout
+    while asyncio.get_running_loop().time() < end:
+        if pred():
+            return True
+        await asyncio.sleep(0.02)
+    raise AssertionError("timeout")
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_state_api(plane, tmp_path):
+    async def main():
+        async with Env(plane, tmp_path) as e:
+            b, h = e.base["app-a"], e.http
+            st = f"{b}/v1.0/state/statestore"
+            assert (await h.post(st, json_body=[{"key": "k1", "value": {"a": 1, "s": "x y"}}])).status == 204
+            r = await h.get(f"{st}/k1")
+            assert r.status == 200 and r.json() == {"a": 1, "s": "x y"}
+            etag = r.headers.get("etag")
+            assert etag
+            # key prefix <app-id>|| in the backing store
+            coll = e.backing.store("acct1", "db", "tasks")
+            assert coll.get("app-a||k1") is not None
+            # stale etag -> 409, fresh etag -> 204
+            bad = await h.post(st, json_body=[{"key": "k1", "value": 2, "etag": "999"}])
+            assert bad.status == 409 and bad.json()["errorCode"] == "ERR_STATE_SAVE"
+            assert (await h.post(st, json_body=[{"key": "k1", "value": 2, "etag": etag}])).status == 204
+            # first-write concurrency on an existing key -> 409
+            fw = await h.post(st, json_body=[{"key": "k1", "value": 3, "options": {"concurrency": "first-write"}}])
+            assert fw.status == 409
+            # bulk save + special characters in keys
+            items = [{"key": f"bulk/{i} é", "value": {"i": i}} for i in range(3)]
+            assert (await h.post(st, json_body=items)).status == 204
+            from urllib.parse import quote
+            for i in range(3):
+                r = await h.get(f"{st}/{quote(f'bulk/{i} é', safe='')}")
+                assert r.status == 200 and r.json() == {"i": i}
+            # missing -> 204, delete with bad etag -> 409, delete -> 204 then missing
+            assert (await h.get(f"{st}/nope")).status == 204
+            r = await h.delete(f"{st}/k1", headers={"If-Match": "123"})
+            assert r.status == 409 and r.json()["errorCode"] == "ERR_STATE_DELETE"
+            assert (await h.delete(f"{st}/k1")).status == 204
+            assert (await h.get(f"{st}/k1")).status == 204
+            # malformed bodies
+            for body in (b"{not json", b'{"key": "x"}', b'[{"value": 1}]'):
+                r = await h.post(st, body=body, headers={"Content-Type": "application/json"})
+                assert r.status == 400 and r.json()["errorCode"] == "ERR_MALFORMED_REQUEST", body
+            # unknown store / in-memory store (served by the control plane in native mode)
+            r = await h.post(f"{b}/v1.0/state/nostore", json_body=[{"key": "a", "value": 1}])
+            assert r.status == 400 and r.json()["errorCode"] == "ERR_STATE_STORE_NOT_FOUND"
+            assert (await h.post(f"{b}/v1.0/state/mem", json_body=[{"key": "a", "value": 1}])).status == 204
+            assert (await h.get(f"{b}/v1.0/state/mem/a")).json() == 1
+            # ttl metadata is accepted
+            r = await h.post(st, json_body=[{"key": "t", "value": 1, "metadata": {"ttlInSeconds": "60"}}])
+            assert r.status == 204
+            # query goes through the control plane
+            r = await h.post(f"{b}/v1.0-alpha1/state/statestore/query", json_body={"filter": {"EQ": {"i": 1}}})
+            assert r.status == 200 and [x["key"] for x in r.json()["results"]] == ["bulk/1 é"]
+    run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_publish_api(plane, tmp_path):
+    async def main():
+        async with Env(plane, tmp_path) as e:
+            b, h, seen = e.base["app-a"], e.http, e.seen["app-a"]
+            tp = "00-" + "ab" * 16 + "-" + "cd" * 8 + "-01"
+            r = await h.post(f"{b}/v1.0/publish/bus/events", json_body={"n": 1, "s": "é"}, headers={"traceparent": tp})
+            assert r.status == 204
+            await _until(lambda: any(x[0] == "event" for x in seen))
+            ev = [x for x in seen if x[0] == "event"][0]
+            assert ev[2] == {"n": 1, "s": "é"}
+            assert ev[1].split("-")[1] == "ab" * 16  # same trace continues into the subscriber
+            # the envelope as stored in the broker
+            msgs = e.backing.broker("ns1")
+            # text payload + raw payload
+            r = await h.post(f"{b}/v1.0/publish/bus/rawtopic?metadata.rawPayload=true", body=b"plain bytes",
+                             headers={"Content-Type": "text/plain"})
+            assert r.status == 204
+            await _until(lambda: any(x[0] == "raw" for x in seen))
+            raw = [x for x in seen if x[0] == "raw"][0]
+            assert raw[2] == b"plain bytes"
+            # unknown pubsub -> 404, empty topic -> 404
+            r = await h.post(f"{b}/v1.0/publish/nope/x", json_body={})
+            assert r.status == 404 and r.json()["errorCode"] == "ERR_PUBSUB_NOT_FOUND"
+            # cloudevents passthrough
+            ce = {"specversion": "1.0", "id": "my-id", "source": "me", "type": "t", "data": {"x": 1}}
+            r = await h.post(f"{b}/v1.0/publish/bus/events", body=json.dumps(ce).encode(),
+                             headers={"Content-Type": "application/cloudevents+json"})
+            assert r.status == 204
+            await _until(lambda: sum(x[0] == "event" for x in seen) == 2)
+            assert [x for x in seen if x[0] == "event"][1][2] == {"x": 1}
+            assert msgs.counts("events/subscriptions/app-a")["completed"] >= 1
+    run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_invoke_api(plane, tmp_path):
+    async def main():
+        async with Env(plane, tmp_path, apps=("app-a", "app-b")) as e:
+            h = e.http
+            a = e.base["app-a"]
+            # self invocation with query string, custom headers and status/header relay
+            r = await h.post(f"{a}/v1.0/invoke/app-a/method/api/echo/x/y?p=1&q=a%20b", body=b"hello",
+                             headers={"X-Custom": "v", "Content-Type": "text/plain"})
+            assert r.status == 201 and r.headers.get("x-echo") == "1"
+            assert r.json() == {"app": "app-a", "method": "POST", "q": "p=1&q=a%20b", "body": "hello"}
+            call = e.seen["app-a"][-1]
+            assert call[2] == "/api/echo/x/y" and call[4]["x-custom"] == "v"
+            assert call[4]["dapr-caller-app-id"] == "app-a" and call[4].get("traceparent")
+            # peer invocation through the registry + internal endpoint
+            r = await h.get(f"{a}/v1.0/invoke/app-b/method/api/echo/z")
+            assert r.status == 201 and r.json()["app"] == "app-b"
+            assert e.seen["app-b"][-1][4]["dapr-caller-app-id"] == "app-a"
+            # namespace suffix is ignored
+            assert (await h.get(f"{a}/v1.0/invoke/app-b.default/method/api/echo/z")).status == 201
+            # app errors are relayed, unknown apps are ERR_DIRECT_INVOKE
+            r = await h.get(f"{a}/v1.0/invoke/app-b/method/api/boom")
+            assert r.status == 500 and r.json() == {"error": "boom"}
+            r = await h.get(f"{a}/v1.0/invoke/ghost/method/x")
+            assert r.status == 500 and r.json()["errorCode"] == "ERR_DIRECT_INVOKE"
+            assert "ghost" in r.json()["message"]
+            # HEAD and DELETE pass through
+            assert (await h.request("HEAD", f"{a}/v1.0/invoke/app-a/method/api/echo/h")).status == 201
+            assert (await h.delete(f"{a}/v1.0/invoke/app-b/method/api/echo/d")).json()["method"] == "DELETE"
+            # metadata reports the plane
+            meta = (await h.get(f"{a}/v1.0/metadata")).json()
+            assert meta["extended"]["dataPlane"] == plane
+    run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_api_token(plane, tmp_path):
+    async def main():
+        async with Env(plane, tmp_path, api_token="tok") as e:
+            b, h = e.base["app-a"], e.http
+            r = await h.get(f"{b}/v1.0/state/statestore/a")
+            assert r.status == 401 and r.json()["errorCode"] == "ERR_API_TOKEN"
+            assert (await h.get(f"{b}/v1.0/invoke/app-a/method/api/echo/x")).status == 401
+            assert (await h.get(f"{b}/v1.0/healthz")).status == 204
+            hdr = {"dapr-api-token": "tok"}
+            assert (await h.get(f"{b}/v1.0/state/statestore/a", headers=hdr)).status == 204
+            r = await h.get(f"{b}/v1.0/invoke/app-a/method/api/echo/x", headers=hdr)
+            assert r.status == 201
+            assert "dapr-api-token" not in e.seen["app-a"][-1][4]  # the API token is not leaked to the app
+    run(main())
+
+
+def _raw_exchange(port, payload: bytes, expect_responses: int, timeout=5.0) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    s.sendall(payload)
+    data = b""
+    while data.count(b"HTTP/1.1 ") < expect_responses or not data.endswith((b"}", b"\r\n\r\n")):
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    return data
+
+
+def test_native_http_framing(tmp_path):
+    """Pipelined requests answered in order; chunked request bodies; Connection: close."""
+    async def main():
+        async with Env("native", tmp_path) as e:
+            port = e.sidecars["app-a"].bound_http_port
+            loop = asyncio.get_running_loop()
+            req = (b"POST /v1.0/state/statestore HTTP/1.1\r\nHost: x\r\nContent-Length: 29\r\n\r\n"
+                   b'[{"key":"p","value":{"v":1}}]'
+                   b"GET /v1.0/state/statestore/p HTTP/1.1\r\nHost: x\r\n\r\n"
+                   b"GET /v1.0/state/statestore/nope HTTP/1.1\r\nHost: x\r\n\r\n")
+            data = await loop.run_in_executor(None, _raw_exchange, port, req, 3)
+            statuses = re.findall(rb"HTTP/1\.1 (\d{3})", data)
+            assert statuses == [b"204", b"200", b"204"], data
+            parts = [b'[{"key":"c","va', b'lue":"chunk"}]']
+            chunked = (b"POST /v1.0/state/statestore HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n"
+                       b"Connection: close\r\n\r\n" + b"".join(b"%x\r\n%s\r\n" % (len(p), p) for p in parts)
+                       + b"0\r\n\r\n")
+            data = await loop.run_in_executor(None, _raw_exchange, port, chunked, 1)
+            assert data.startswith(b"HTTP/1.1 204") and b"connection: close" in data.lower()
+            r = await e.http.get(f"{e.base['app-a']}/v1.0/state/statestore/c")
+            assert r.json() == "chunk"
+            m = await e.http.get(f"{e.base['app-a']}/metrics")
+            assert b"sidecar_native_requests_total" in m.body
+    run(main())
