@@ -239,6 +239,24 @@ std::string base64(std::string_view in) {
   return o;
 }
 
+std::string unbase64(std::string_view in) {
+  std::string o;
+  uint32_t acc = 0;
+  int bits = 0;
+  for (char c : in) {
+    int v = c >= 'A' && c <= 'Z' ? c - 'A' : c >= 'a' && c <= 'z' ? c - 'a' + 26 : c >= '0' && c <= '9' ? c - '0' + 52
+            : c == '+' ? 62 : c == '/' ? 63 : -1;
+    if (v < 0) continue;
+    acc = (acc << 6) | (uint32_t)v;
+    bits += 6;
+    if (bits >= 8) {
+      bits -= 8;
+      o += (char)((acc >> bits) & 0xFF);
+    }
+  }
+  return o;
+}
+
 std::string errno_text(int e) {
   switch (e) {
     case ETIMEDOUT: return "timeout";
@@ -459,8 +477,23 @@ class DataPlane {
   ev::Handler internal_handler() {
     return [this](Message&& m, Reply r) { on_internal(std::move(m), std::move(r)); };
   }
+  ev::Handler control_handler() {
+    return [this](Message&& m, Reply r) { on_control(std::move(m), std::move(r)); };
+  }
   void flush() { tracer_.flush(); }
   size_t inflight() const { return inflight_; }
+  void tick(double now) {
+    for (auto& c : consumers_) c->tick(now);
+  }
+  void begin_stop() {
+    for (auto& c : consumers_) c->stop();
+  }
+  bool drained() const {
+    if (inflight_) return false;
+    for (auto& c : consumers_)
+      if (!c->drained()) return false;
+    return true;
+  }
 
  private:
   ev::Loop& loop_;
@@ -518,6 +551,331 @@ class DataPlane {
     auto q = target.find('?');
     path = target.substr(0, q);
     qs = q == std::string::npos ? "" : target.substr(q + 1);
+  }
+
+  // ---------------------------------------------------------------- pub/sub consumer
+  // Competing consumer on one subscription entity: the native counterpart of
+  // sidecar/pubsub.py Consumer + runtime.py _make_delivery/_make_dead_letter.  Prefetches up
+  // to `prefetch` messages under peek-lock, runs at most `max_conc` app deliveries at once,
+  // renews locks of running deliveries, settles outcomes in batches (success -> complete,
+  // retry -> abandon, drop -> dead-letter or forward to the deadLetterTopic).
+  struct SubSpec {
+    std::string name, pubsub, topic, route, entity, ns, dlt;
+    Endpoint backing;
+    HeaderList auth;
+    int lock_ms = 60000, prefetch = 64, max_conc = 32, retry_delay_ms = 0;
+    bool raw = false;
+  };
+  class Consumer {
+   public:
+    Consumer(DataPlane& dp, SubSpec s) : s_(std::move(s)), dp_(dp) { next_renew_ = ev::now_s() + renew_period(); }
+    SubSpec s_;
+    uint64_t delivered = 0, succeeded = 0, retried = 0, dropped = 0, errors = 0;
+
+    void start() { pump(); }
+    void stop() {
+      stopping_ = true;
+      while (!queued_.empty()) {  // prefetched but never delivered: give them back
+        abandon_.emplace_back(queued_.front().token, 0);
+        locked_.erase(queued_.front().token);
+        queued_.pop_front();
+      }
+      schedule_flush();
+    }
+    // An outstanding long-poll receive is not waited for (its messages' locks simply expire).
+    bool drained() const { return running_ == 0 && !settling_ && pending_empty(); }
+    void tick(double now) {
+      if (!stopping_ && !receiving_ && retry_at_ > 0 && now >= retry_at_) {
+        retry_at_ = 0;
+        pump();
+      }
+      if (now >= next_renew_) {
+        next_renew_ = now + renew_period();
+        if (!locked_.empty() && !stopping_) renew();
+      }
+    }
+    std::string stats_json() const {
+      return "{\"delivered\":" + std::to_string(delivered) + ",\"succeeded\":" + std::to_string(succeeded) +
+             ",\"retried\":" + std::to_string(retried) + ",\"dropped\":" + std::to_string(dropped) +
+             ",\"errors\":" + std::to_string(errors) + ",\"plane\":\"native\"}";
+    }
+
+   private:
+    struct Msg {
+      std::string token, id, body, ctype;
+      long long delivery_count = 0;
+    };
+    DataPlane& dp_;
+    std::deque<Msg> queued_;
+    std::map<std::string, int> locked_;  // tokens we hold (queued + running)
+    int running_ = 0;
+    bool receiving_ = false, stopping_ = false, settling_ = false, flush_scheduled_ = false;
+    double retry_at_ = 0, backoff_ = 0.1, next_renew_ = 0;
+    std::vector<std::string> complete_;
+    std::vector<std::pair<std::string, int>> abandon_;
+    std::vector<std::pair<std::string, std::string>> deadletter_;
+
+    double renew_period() const { return std::max(s_.lock_ms / 3000.0, 0.05); }
+    bool pending_empty() const { return complete_.empty() && abandon_.empty() && deadletter_.empty(); }
+    std::string sb_path(const std::string& tail) const { return "/servicebus/" + quote_all(s_.ns) + tail; }
+
+    void pump() {
+      if (stopping_ || receiving_) return;
+      int room = s_.prefetch - (int)locked_.size();
+      if (room <= 0) return;
+      receiving_ = true;
+      std::string q = "?entity=" + quote_all(s_.entity) + "&max=" + std::to_string(std::min(room, 256)) +
+                      "&lockMs=" + std::to_string(s_.lock_ms) + "&waitMs=2000";
+      dp_.client_.request(s_.backing, "POST", sb_path("/receive" + q), s_.auth, {}, 32.0,
+                          [this](ClientResult&& res) { on_received(std::move(res)); });
+    }
+
+    void on_received(ClientResult&& res) {
+      receiving_ = false;
+      if (res.err || res.resp.status != 200) {
+        if (!stopping_) {
+          std::fprintf(stderr, "dataplane: %s: receive failed (%s); retrying in %.1fs\n", s_.name.c_str(),
+                       res.err ? errno_text(res.err).c_str() : ("HTTP " + std::to_string(res.resp.status)).c_str(),
+                       backoff_);
+          retry_at_ = ev::now_s() + backoff_;
+          backoff_ = std::min(backoff_ * 2, 5.0);
+        }
+        return;
+      }
+      backoff_ = 0.1;
+      try {
+        Value arr = parse(res.resp.body);
+        for (auto& v : arr.items) {
+          Msg m;
+          if (auto* t = v.get("lockToken")) m.token = t->s;
+          if (auto* t = v.get("id")) m.id = t->s;
+          if (auto* t = v.get("contentType"); t && t->t == Value::String) m.ctype = t->s;
+          if (auto* t = v.get("deliveryCount"); t && t->t == Value::Number) m.delivery_count = (long long)t->n;
+          if (auto* b = v.get("bodyB64"); b && b->t == Value::String) m.body = unbase64(b->s);
+          else if (auto* b = v.get("body"); b && b->t == Value::String) m.body = b->s;
+          if (stopping_) {
+            abandon_.emplace_back(m.token, 0);
+            continue;
+          }
+          locked_[m.token] = 1;
+          queued_.push_back(std::move(m));
+        }
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "dataplane: %s: bad receive payload: %s\n", s_.name.c_str(), e.what());
+      }
+      start_deliveries();
+      if (stopping_) schedule_flush();
+      pump();
+    }
+
+    void start_deliveries() {
+      while (!queued_.empty() && running_ < s_.max_conc) {
+        Msg m = std::move(queued_.front());
+        queued_.pop_front();
+        running_++;
+        delivered++;
+        deliver(std::move(m));
+      }
+    }
+
+    // Build the delivery request exactly like runtime.py _make_delivery.
+    void deliver(Msg&& m) {
+      std::string body = std::move(m.body);
+      std::string ctype = m.ctype.empty() ? "application/json" : m.ctype;
+      SpanCtx span;
+      bool is_ce = false;
+      std::string parent_tp;
+      if (ctype.rfind("application/cloudevents", 0) == 0) {
+        try {
+          Value ce = parse(body);
+          is_ce = true;
+          if (auto* tp = ce.get("traceparent"); tp && tp->t == Value::String) parent_tp = tp->s;
+        } catch (const std::exception&) {
+        }
+      }
+      if (!is_ce && !s_.raw) {
+        std::string base = lower(ctype.substr(0, ctype.find(';')));
+        std::string ce = "{\"specversion\":\"1.0\",\"id\":" + json_str(m.id.empty() ? uuid4() : m.id) +
+                         ",\"source\":\"unknown\",\"type\":\"com.dapr.event.sent\",\"datacontenttype\":" +
+                         json_str(base.empty() ? "application/json" : base) + ",\"topic\":" + json_str(s_.topic) +
+                         ",\"pubsubname\":" + json_str(s_.pubsub) + ",\"time\":\"" + utc_now_iso() + "\"";
+        if (base.find("json") != std::string::npos && !body.empty() && valid_json(body)) ce += ",\"data\":" + compact(body);
+        else if (base.find("json") != std::string::npos && body.empty()) ce += ",\"data\":null";
+        else if (base.rfind("text/", 0) == 0 || base.find("json") != std::string::npos || body.empty())
+          ce += ",\"data\":" + json_str(body);
+        else ce += ",\"data_base64\":\"" + base64(body) + "\"";
+        ce += "}";
+        body = std::move(ce);
+        is_ce = true;
+      }
+      span = dp_.tracer_.start(parent_tp.empty() ? nullptr : &parent_tp);
+      HeaderList h;
+      h.emplace_back("content-type", is_ce && !s_.raw ? "application/cloudevents+json" : ctype);
+      h.emplace_back("traceparent", span.traceparent());
+      h.emplace_back("pubsubname", s_.pubsub);
+      h.emplace_back("topic", s_.topic);
+      std::string token = m.token;
+      long long dc = m.delivery_count;
+      std::string raw_body = body;  // kept for a dead-letter-topic forward
+      std::string out_ct = h[0].second;
+      dp_.call_app("POST", "/" + s_.route, std::move(h), std::move(body),
+                   [this, token, span, dc, raw_body = std::move(raw_body), out_ct](ClientResult&& res) mutable {
+                     int outcome = 1;  // 0 success, 1 retry, 2 drop
+                     int status = res.err ? 0 : res.resp.status;
+                     if (res.err) {
+                       errors++;
+                     } else if (status >= 200 && status < 300) {
+                       outcome = 0;
+                       auto* ct = res.resp.header("content-type");
+                       if (!res.resp.body.empty() && ct && ct->find("json") != std::string::npos) {
+                         try {
+                           Value v = parse(res.resp.body);
+                           if (auto* st = v.get("status"); st && st->t == Value::String) {
+                             std::string u = st->s;
+                             for (auto& c : u) c = (char)std::toupper((unsigned char)c);
+                             outcome = u == "RETRY" ? 1 : u == "DROP" ? 2 : 0;
+                           }
+                         } catch (const std::exception&) {
+                         }
+                       }
+                     } else if (status == 404) {
+                       outcome = 2;
+                     }
+                     dp_.tracer_.end(span, "pubsub/" + s_.topic, outcome == 0 ? status : 500,
+                                     {{"messaging.delivery_count", std::to_string(dc)}});
+                     dp_.count("deliver", outcome == 0 ? 200 : outcome == 1 ? 503 : 404);
+                     finish(token, outcome, raw_body, out_ct);
+                   });
+    }
+
+    void finish(const std::string& token, int outcome, const std::string& body, const std::string& ctype) {
+      running_--;
+      if (outcome == 0) {
+        succeeded++;
+        complete_.push_back(token);
+        locked_.erase(token);
+      } else if (outcome == 1) {
+        retried++;
+        abandon_.emplace_back(token, s_.retry_delay_ms);
+        locked_.erase(token);
+      } else {
+        dropped++;
+        if (!s_.dlt.empty()) {
+          forward_dead_letter(token, body, ctype);
+        } else {
+          deadletter_.emplace_back(token, "dropped by application");
+          locked_.erase(token);
+        }
+      }
+      schedule_flush();
+      start_deliveries();
+      pump();
+    }
+
+    void forward_dead_letter(const std::string& token, const std::string& body, const std::string& ctype) {
+      HeaderList h = s_.auth;
+      h.emplace_back("content-type", ctype);
+      running_++;  // the forward keeps the message "in flight"
+      dp_.client_.request(s_.backing, "POST", sb_path("/topics/" + quote_all(s_.dlt) + "/messages"), h, body, 60,
+                          [this, token](ClientResult&& res) {
+                            running_--;
+                            if (!res.err && res.resp.status < 300) complete_.push_back(token);
+                            else deadletter_.emplace_back(token, "dropped by application");
+                            locked_.erase(token);
+                            schedule_flush();
+                          });
+    }
+
+    void schedule_flush() {
+      if (flush_scheduled_) return;
+      flush_scheduled_ = true;
+      dp_.loop_.defer([this] {
+        flush_scheduled_ = false;
+        flush();
+      });
+    }
+
+    void flush() {
+      if (settling_ || pending_empty()) return;
+      std::string b = "{\"entity\":" + json_str(s_.entity) + ",\"complete\":[";
+      for (size_t i = 0; i < complete_.size(); ++i) b += (i ? "," : "") + json_str(complete_[i]);
+      b += "],\"abandon\":[";
+      for (size_t i = 0; i < abandon_.size(); ++i)
+        b += (i ? ",{\"token\":" : "{\"token\":") + json_str(abandon_[i].first) + ",\"delayMs\":" +
+             std::to_string(abandon_[i].second) + "}";
+      b += "],\"deadletter\":[";
+      for (size_t i = 0; i < deadletter_.size(); ++i)
+        b += (i ? ",{\"token\":" : "{\"token\":") + json_str(deadletter_[i].first) + ",\"reason\":" +
+             json_str(deadletter_[i].second) + "}";
+      b += "]}";
+      complete_.clear();
+      abandon_.clear();
+      deadletter_.clear();
+      settling_ = true;
+      HeaderList h = s_.auth;
+      h.emplace_back("content-type", "application/json");
+      dp_.client_.request(s_.backing, "POST", sb_path("/settle"), h, b, 60, [this](ClientResult&& res) {
+        settling_ = false;
+        if (res.err || res.resp.status >= 300)  // locks expire and the broker redelivers (at-least-once)
+          std::fprintf(stderr, "dataplane: %s: settle failed\n", s_.name.c_str());
+        if (!pending_empty()) flush();
+      });
+    }
+
+    void renew() {
+      std::string b = "{\"entity\":" + json_str(s_.entity) + ",\"renew\":[";
+      size_t i = 0;
+      for (auto& kv : locked_)
+        b += (i++ ? ",{\"token\":" : "{\"token\":") + json_str(kv.first) + ",\"lockMs\":" + std::to_string(s_.lock_ms) + "}";
+      b += "]}";
+      HeaderList h = s_.auth;
+      h.emplace_back("content-type", "application/json");
+      dp_.client_.request(s_.backing, "POST", sb_path("/settle"), h, b, 60, [](ClientResult&&) {});
+    }
+  };
+  std::vector<std::unique_ptr<Consumer>> consumers_;
+
+  // Control socket (private to the Python control plane): start consumers, report stats.
+  void on_control(Message&& m, Reply r) {
+    std::string path, qs;
+    split_target(m.target, path, qs);
+    if (path == "/subscribe" && m.method == "POST") {
+      try {
+        Value v = parse(m.body);
+        SubSpec s;
+        auto str = [&](const char* k) { auto* x = opt_str(v, k); return x ? *x : std::string(); };
+        auto num = [&](const char* k, int d) { auto* x = v.get(k); return x && x->t == Value::Number ? (int)x->n : d; };
+        s.name = str("name");
+        s.pubsub = str("pubsub");
+        s.topic = str("topic");
+        s.route = str("route");
+        s.entity = str("entity");
+        s.ns = str("ns");
+        s.dlt = str("deadLetterTopic");
+        s.backing = Endpoint::parse(str("backing"));
+        s.auth = auth_headers(v);
+        s.lock_ms = num("lockMs", 60000);
+        s.prefetch = std::max(1, num("prefetch", 64));
+        s.max_conc = std::max(1, num("maxConcurrent", 32));
+        s.retry_delay_ms = num("retryDelayMs", 0);
+        if (auto* x = v.get("raw"); x && x->t == Value::Bool) s.raw = x->b;
+        consumers_.push_back(std::make_unique<Consumer>(*this, std::move(s)));
+        consumers_.back()->start();
+        r.empty(204);
+      } catch (const std::exception& e) {
+        r.json(400, error_json("ERR_MALFORMED_REQUEST", e.what()));
+      }
+      return;
+    }
+    if (path == "/stats" && m.method == "GET") {
+      std::string b = "{\"consumers\":{";
+      for (size_t i = 0; i < consumers_.size(); ++i)
+        b += (i ? "," : "") + json_str(consumers_[i]->s_.name) + ":" + consumers_[i]->stats_json();
+      b += "},\"inflight\":" + std::to_string(inflight_) + "}";
+      r.json(200, b);
+      return;
+    }
+    r.json(404, error_json("ERR_NOT_FOUND", "no such control route"));
   }
 
   // ---------------------------------------------------------------- routing
@@ -1013,6 +1371,7 @@ int main(int argc, char** argv) {
   DataPlane dp(loop, cfg);
   ev::Handler api = dp.api_handler();
   ev::Handler internal = dp.internal_handler();
+  ev::Handler control = dp.control_handler();
   std::string ports = "{";
   try {
     int http_port = 0;
@@ -1030,6 +1389,7 @@ int main(int argc, char** argv) {
         if (internal_ep.empty())
           internal_ep = ep.unix_socket ? "unix:" + ep.path + ":" : "http://127.0.0.1:" + std::to_string(p);
       }
+    if (auto* c = opt_str(cfg, "control")) ev::listen_on(loop, Endpoint::parse(*c), control);
     ports += ",\"internal\":" + json_str(internal_ep) + ",\"pid\":" + std::to_string(getpid()) + "}";
   } catch (const std::exception& e) {
     std::fprintf(stderr, "dataplane: %s\n", e.what());
@@ -1038,8 +1398,10 @@ int main(int argc, char** argv) {
   bool stopping = false;
   double stop_deadline = 0;
   loop.add(std::make_shared<SignalIo>([&] {
+             if (stopping) return;
              stopping = true;
              stop_deadline = ev::now_s() + 5.0;
+             dp.begin_stop();
            }),
            EPOLLIN);
   if (auto* pf = opt_str(cfg, "portFile")) {
@@ -1053,7 +1415,8 @@ int main(int argc, char** argv) {
       dp.flush();
       last_flush = t;
     }
-    if (stopping && (dp.inflight() == 0 || t > stop_deadline)) loop.stop();
+    dp.tick(t);
+    if (stopping && (dp.drained() || t > stop_deadline)) loop.stop();
   });
   dp.flush();
   return 0;

@@ -276,13 +276,13 @@ class PubSub(ComponentBase):
         props = {k: v for k, v in metadata.items() if k not in ("ttlInSeconds", "rawPayload")}
         await self.transport.publish(topic, body, ctype, props, ttl)
 
-    async def subscribe(self, topic: str, handler: Handler, sub_metadata: dict[str, str],
-                        on_drop=None) -> Consumer:
+    async def ensure_entity(self, topic: str) -> str:
+        """Create the topic subscription for this consumer group (unless entity management is
+        disabled or not permitted) and return its entity path."""
         group = self.consumer_group()
-        lock = self.lock_ms()
         if not self.comp.get_bool("disableEntityManagement"):
             try:
-                await self.transport.ensure_subscription(topic, group, lock, self.max_delivery())
+                await self.transport.ensure_subscription(topic, group, self.lock_ms(), self.max_delivery())
             except Exception as e:
                 # receive-only identities cannot manage entities; the subscription is expected
                 # to be provisioned by the environment (IaC), exactly like Dapr on Azure.
@@ -290,11 +290,20 @@ class PubSub(ComponentBase):
                     raise
                 log.info("%s: no permission to manage %s/subscriptions/%s; using the provisioned entity",
                          self.name, topic, group)
-        c = Consumer(self.transport, f"{topic}/subscriptions/{group}", handler,
-                     max_concurrent=self.comp.get_int("maxConcurrentHandlers", self.default_concurrency) or 1 << 20,
-                     prefetch=self.comp.get_int("maxActiveMessages", 64),
-                     lock_ms=lock, retry_delay_ms=self.comp.get_int("retryDelayMs", 0),
-                     on_drop=on_drop, name=f"{self.name}/{topic}")
+        return f"{topic}/subscriptions/{group}"
+
+    def consumer_settings(self) -> dict[str, int]:
+        return {"maxConcurrent": self.comp.get_int("maxConcurrentHandlers", self.default_concurrency) or 1 << 20,
+                "prefetch": self.comp.get_int("maxActiveMessages", 64), "lockMs": self.lock_ms(),
+                "retryDelayMs": self.comp.get_int("retryDelayMs", 0)}
+
+    async def subscribe(self, topic: str, handler: Handler, sub_metadata: dict[str, str],
+                        on_drop=None) -> Consumer:
+        entity = await self.ensure_entity(topic)
+        cs = self.consumer_settings()
+        c = Consumer(self.transport, entity, handler, max_concurrent=cs["maxConcurrent"], prefetch=cs["prefetch"],
+                     lock_ms=cs["lockMs"], retry_delay_ms=cs["retryDelayMs"], on_drop=on_drop,
+                     name=f"{self.name}/{topic}")
         c.start()
         return c
 
@@ -323,10 +332,10 @@ class RedisPubSub(PubSub):
     def max_delivery(self) -> int:
         return self.comp.get_int("maxDeliveryCount", 0) or 1 << 30
 
-    async def subscribe(self, topic, handler, sub_metadata, on_drop=None):
+    def consumer_settings(self) -> dict[str, int]:
         if not self.comp.get("maxConcurrentHandlers") and self.comp.get("concurrency"):
             self.comp.metadata["maxConcurrentHandlers"] = self.comp.get("concurrency")
-        return await super().subscribe(topic, handler, sub_metadata, on_drop)
+        return super().consumer_settings()
 
 
 @register("pubsub.in-memory")

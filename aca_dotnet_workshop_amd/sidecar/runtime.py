@@ -109,6 +109,7 @@ class Sidecar:
         self.data_plane = (data_plane or self.environ.get("TT_SIDECAR_DATAPLANE") or "python").lower()
         self._dp_proc: asyncio.subprocess.Process | None = None
         self._dp_dir: str | None = None
+        self._dp_control = ""
         self.components: dict[str, Component] = {}
         self.secret_stores: dict[str, SecretStore] = {}
         self.state_stores: dict[str, StateStore] = {}
@@ -216,6 +217,8 @@ class Sidecar:
         self._servers.append(srv)
         cfg = self.data_plane_config("unix:" + private)
         cfg["portFile"] = os.path.join(self._dp_dir, "ports.json")
+        cfg["control"] = "unix:" + os.path.join(self._dp_dir, "ctl.sock")
+        self._dp_control = cfg["control"] + ":"
         ex = self.tracer.exporter
         if ex.keep_in_memory:
             # no telemetry directory: the data plane writes its spans to a private file that is
@@ -398,7 +401,36 @@ class Sidecar:
                 continue
             await self._subscribe_with_retry(ps, s)
 
+    async def _subscribe_native(self, ps: PubSub, s: SubscriptionSpec) -> None:
+        """Hand the subscription's delivery loop to the native data plane."""
+        t = ps.transport
+        entity = await ps.ensure_entity(s.topic)
+        spec = {"name": f"{ps.name}/{s.topic}", "pubsub": ps.name, "topic": s.topic, "route": s.route,
+                "entity": entity, "ns": t.ns, "backing": t.client.base, "identity": t.client.identity or "",
+                "key": t.client.key or "", "deadLetterTopic": s.dead_letter_topic or "",
+                "raw": s.metadata.get("rawPayload", "").lower() == "true", **ps.consumer_settings()}
+        r = await self.http.request("POST", self._dp_control + "/subscribe", body=json.dumps(spec).encode(),
+                                    headers=[("Content-Type", "application/json")])
+        if r.status != 204:
+            raise RuntimeError(f"native data plane refused subscription: {r.status} {r.body[:200]!r}")
+
     async def _subscribe_with_retry(self, ps: PubSub, s: SubscriptionSpec, delay: float = 1.0) -> None:
+        from .pubsub import BackingTransport
+        if self._dp_proc is not None and isinstance(getattr(ps, "transport", None), BackingTransport):
+            try:
+                await self._subscribe_native(ps, s)
+                log.info("sidecar %s: subscribed %s/%s -> /%s (native)", self.app_id, s.pubsubname, s.topic, s.route)
+                return
+            except Exception as e:
+                log.error("sidecar %s: subscribing %s/%s failed (%s); retrying in %.0fs", self.app_id, s.pubsubname,
+                          s.topic, e, delay)
+
+                async def again() -> None:
+                    await asyncio.sleep(delay)
+                    if not self.stopped.is_set():
+                        await self._subscribe_with_retry(ps, s, min(delay * 2, 30.0))
+                self._bg.append(asyncio.ensure_future(again()))
+                return
         try:
             c = await ps.subscribe(s.topic, self._make_delivery(ps, s), s.metadata, self._make_dead_letter(ps, s))
         except Exception as e:
@@ -880,6 +912,13 @@ class Sidecar:
 
     # ---------------------------------------------------------------- runtime
     async def h_metadata(self, req: Request) -> Response:
+        consumers = {c.name: c.stats for c in self.consumers}
+        if self._dp_proc is not None:
+            try:
+                r = await self.http.request("GET", self._dp_control + "/stats", timeout=2.0)
+                consumers.update(r.json().get("consumers", {}))
+            except Exception as e:  # metadata stays available even if the data plane is wedged
+                log.warning("native data plane stats unavailable: %r", e)
         comps = [self.components[n].describe() for n in sorted(self.components) if n not in self.failed_components]
         subs = [{"pubsubname": s.pubsubname, "topic": s.topic, "rules": [{"path": "/" + s.route}],
                  "deadLetterTopic": s.dead_letter_topic or "", "type": "DECLARATIVE" if s.declarative else "PROGRAMMATIC"}
@@ -889,7 +928,7 @@ class Sidecar:
             "inputBindings": self.input_bindings, "failedComponents": self.failed_components,
             "extended": {"instance": self.instance, "appReady": self.app_ready.is_set(),
                          "dataPlane": self.active_data_plane,
-                         "consumers": {c.name: c.stats for c in self.consumers}},
+                         "consumers": consumers},
             "appConnectionProperties": {"port": self.app_port, "uds": self.app_uds, "protocol": "http"},
         })
 

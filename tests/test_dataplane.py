@@ -287,3 +287,76 @@ def test_native_http_framing(tmp_path):
             m = await e.http.get(f"{e.base['app-a']}/metrics")
             assert b"sidecar_native_requests_total" in m.body
     run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_delivery_outcomes(plane, tmp_path):
+    """SUCCESS / RETRY (-> DLQ after maxDeliveryCount) / DROP with deadLetterTopic / 404 /
+    non-2xx retried until success -- identical on both planes."""
+    app = WebApp("sub")
+    app.use(cloud_events_middleware())
+    seen = {k: [] for k in ("ok", "retry", "drop", "flaky", "gone", "poison")}
+    attempts = {"flaky": 0}
+
+    def handler(kind, resp):
+        async def h(req):
+            seen[kind].append(req.json())
+            return resp() if callable(resp) else resp
+        return h
+
+    def flaky():
+        attempts["flaky"] += 1
+        return Response(b"", 503) if attempts["flaky"] <= 2 else empty(200)
+
+    for kind, resp, extra in (("ok", json_response({"status": "SUCCESS"}), {}),
+                              ("retry", json_response({"status": "RETRY"}), {}),
+                              ("drop", json_response({"status": "DROP"}), {"dead_letter_topic": "poison"}),
+                              ("flaky", flaky, {}), ("gone", empty(404), {}), ("poison", empty(200), {})):
+        fn = handler(kind, resp)
+        topic("bus3", kind, **extra)(fn)
+        app.add_route(f"/{kind}", fn, ("POST",))
+    map_subscribe_handler(app)
+    bus = _comp("bus3", "pubsub.azure.servicebus", {"connectionString": "Endpoint=sb://ns3.servicebus.windows.net/",
+                                                     "maxDeliveryCount": "3"})
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        backing = BackingServices()
+        bsrv = HttpServer(backing.build_app(), loop)
+        burl = f"http://127.0.0.1:{await bsrv.listen_tcp('127.0.0.1', 0)}"
+        asrv = HttpServer(app, loop)
+        port = await asrv.listen_tcp("127.0.0.1", 0)
+        sc = Sidecar("subapp", app_port=port, http_port=0, components=[bus], backing_url=burl,
+                     resolver=NameResolver(str(tmp_path / "reg")), data_plane=plane)
+        await sc.start()
+        http = HttpClient()
+        try:
+            await asyncio.wait_for(sc.app_ready.wait(), 10)
+            base = f"http://127.0.0.1:{sc.bound_http_port}"
+            for t in ("ok", "retry", "drop", "flaky", "gone"):
+                assert (await http.post(f"{base}/v1.0/publish/bus3/{t}", json_body={"t": t})).status == 204
+            b = backing.broker("ns3")
+
+            def counts(t):
+                return b.counts(f"{t}/subscriptions/subapp")
+            await _until(lambda: counts("ok")["completed"] == 1)
+            assert seen["ok"] == [{"t": "ok"}]
+            await _until(lambda: counts("retry")["dead_letter"] == 1)
+            assert len(seen["retry"]) == 3
+            await _until(lambda: len(seen["poison"]) == 1)
+            await _until(lambda: counts("drop")["completed"] == 1)
+            assert counts("drop")["dead_letter"] == 0 and seen["poison"] == [{"t": "drop"}]
+            await _until(lambda: counts("flaky")["completed"] == 1)
+            assert attempts["flaky"] == 3
+            await _until(lambda: counts("gone")["dead_letter"] == 1)
+            assert len(seen["gone"]) == 1
+            meta = (await http.get(f"{base}/v1.0/metadata")).json()
+            st = meta["extended"]["consumers"]["bus3/ok"]
+            assert st["succeeded"] == 1 and st["delivered"] == 1
+            assert meta["extended"]["consumers"]["bus3/retry"]["retried"] == 3
+        finally:
+            await http.close()
+            await sc.stop(1.0)
+            await asrv.close(1.0)
+            await bsrv.close(1.0)
+    run(main())
