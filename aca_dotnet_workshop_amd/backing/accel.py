@@ -53,6 +53,7 @@ class CollectionAccelerator:
         self.disabled = mode == "off"
         self.stats = {"native": 0, "gpu": 0, "cpu": 0, "fallback": 0}
         self._kernels = None
+        self.before_build = None  # hook: route the collection's writes through on_put/on_delete
 
     # -- write mirroring ------------------------------------------------------
     def on_put(self, key: str, value: str, ttl_ms: int = 0) -> None:
@@ -94,6 +95,8 @@ class CollectionAccelerator:
         return self.index is not None or len(store) >= self.min_docs
 
     def build(self, store) -> None:
+        if self.before_build is not None:
+            self.before_build()
         res = json.loads(store.query("{}", ""))["results"]
         ix = ColumnarIndex(capacity=len(res) + 4096)
         ix.add_column(PREFIX_PATH)

@@ -52,11 +52,14 @@ class Waiters:
 
     def __init__(self) -> None:
         self._ev: dict[str, asyncio.Event] = {}
+        self.listeners: list[Any] = []  # e.g. the native front's parked receives
 
     def notify(self, key: str) -> None:
         ev = self._ev.pop(key, None)
         if ev is not None:
             ev.set()
+        for fn in self.listeners:
+            fn(key)
 
     async def wait(self, key: str, timeout: float) -> None:
         ev = self._ev.get(key)
@@ -104,7 +107,30 @@ class BackingServices:
         self.waiters = Waiters()
         self.vaults: dict[str, dict[str, str]] = {}
         self.outbox: list[dict[str, Any]] = []
+        self.front = None
         self._load_vaults()
+
+    # -- native front --------------------------------------------------------------
+    def attach_front(self, front) -> None:
+        """Let the native HTTP front (native/src/backingfront.hpp) serve hot routes against
+        this process's engines.  Engines created later are attached on creation."""
+        self.front = front
+        for (a, d, c), s in self.stores.items():
+            front.attach_store(a, d, c, s)
+        for ns, b in self.brokers.items():
+            front.attach_broker(ns, b)
+        for (a, d, c), acc in self.accels.items():
+            if acc.index is not None:
+                front.set_mirrored(a, d, c)
+        self._push_policy()
+        self.waiters.listeners.append(lambda key: front.notify(*key.split("|", 1)))
+
+    def _push_policy(self) -> None:
+        if self.front is None:
+            return
+        from .auth import ROLE_ACTIONS
+        grants = [(a.principal, a.scope, sorted(ROLE_ACTIONS.get(a.role, set()))) for a in self.policy.assignments]
+        self.front.set_policy(self.policy.mode, list(self.policy.keys.items()), grants)
 
     # -- engines ---------------------------------------------------------------
     def _path(self, *parts: str) -> str:
@@ -119,6 +145,8 @@ class BackingServices:
         s = self.stores.get(key)
         if s is None:
             s = self.stores[key] = self.N.DocStore(self._path("cosmos", account, db, coll + ".log"), self.fsync)
+            if self.front is not None:
+                self.front.attach_store(account, db, coll, s)
         return s
 
     def accel(self, account: str, db: str, coll: str) -> CollectionAccelerator:
@@ -126,12 +154,16 @@ class BackingServices:
         a = self.accels.get(key)
         if a is None:
             a = self.accels[key] = CollectionAccelerator(self.accel_mode, self.accel_min_docs)
+            # once the columnar mirror exists, writes must flow through the Python handlers
+            a.before_build = lambda: self.front.set_mirrored(account, db, coll) if self.front is not None else None
         return a
 
     def broker(self, ns: str):
         b = self.brokers.get(ns)
         if b is None:
             b = self.brokers[ns] = self.N.Broker(self._path("servicebus", ns + ".log"), self.fsync)
+            if self.front is not None:
+                self.front.attach_broker(ns, b)
         return b
 
     def _load_vaults(self) -> None:
@@ -616,11 +648,17 @@ class BackingServices:
 
         async def set_policy(req: Request) -> Response:
             self.policy = AccessPolicy.from_dict(req.json())
+            self._push_policy()
             return empty(204)
 
         app.add_route("/admin/health", health, ("GET",))
         app.add_route("/admin/overview", overview, ("GET",))
         app.add_route("/admin/policy", set_policy, ("PUT",))
+
+        async def front_stats(req: Request) -> Response:
+            return json_response({"front": "native" if self.front is not None else "python",
+                                  "requests": dict(self.front.stats()) if self.front is not None else {}})
+        app.add_route("/admin/front", front_stats, ("GET",))
 
 
 def _entity_scope(entity: str) -> str:
@@ -635,8 +673,19 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
     svc = BackingServices(data_dir, AccessPolicy.from_dict(policy))
     app = svc.build_app()
     srv = HttpServer(app, asyncio.get_running_loop())
-    bound = await srv.listen_tcp(host, port)
-    log.info("backing services listening on %s:%d (data=%s)", host, bound, data_dir)
+    front = None
+    priv_dir = None
+    if os.environ.get("TT_BACKING_FRONT", "native").lower() == "native":
+        # hot routes on the native front (own thread, GIL-free); Python serves the rest privately
+        priv_dir = tempfile.mkdtemp(prefix="ttbf-")
+        await srv.listen_unix(os.path.join(priv_dir, "py.sock"))
+        front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"))
+        svc.attach_front(front)
+        bound = front.port()
+    else:
+        bound = await srv.listen_tcp(host, port)
+    log.info("backing services listening on %s:%d (data=%s, front=%s)", host, bound, data_dir,
+             "native" if front is not None else "python")
     if ready:
         ready(bound)
     stop = stop or asyncio.Event()
@@ -648,7 +697,12 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         except (NotImplementedError, RuntimeError):
             pass
     await stop.wait()
+    if front is not None:
+        front.stop()
     await srv.close()
+    if priv_dir:
+        import shutil
+        shutil.rmtree(priv_dir, ignore_errors=True)
 
 
 def main(argv: list[str] | None = None) -> None:

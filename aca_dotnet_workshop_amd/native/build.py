@@ -37,7 +37,7 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
     import pybind11
 
     target = ext_path("_ttnative")
-    sources = [p for p in sorted(SRC.glob("*.hpp")) if p.name != "evhttp.hpp"] + [SRC / "module.cpp"]
+    sources = sorted(SRC.glob("*.hpp")) + [SRC / "module.cpp"]
     if not force and not _stale(target, sources):
         return target
     cxx = os.environ.get("CXX", "g++")

@@ -1,0 +1,549 @@
+// Native HTTP front for the backing-services emulator (backing/server.py).
+//
+// Runs an epoll loop on its own thread inside the backing-services process and serves the
+// per-task hot routes directly against the SAME DocStore / Broker engine objects the Python
+// handlers use (both are internally synchronised), without touching the GIL:
+//
+//   PUT|GET|DELETE /cosmos/{account}/{db}/{coll}/docs/{key}
+//   POST           /servicebus/{ns}/topics/{topic}/messages
+//   POST           /servicebus/{ns}/receive?entity&max&lockMs&waitMs   (long poll)
+//   POST           /servicebus/{ns}/settle
+//   GET            /servicebus/{ns}/counts?entity
+//
+// Everything else (entity management, queries, transactions, storage, key vault, sendgrid,
+// admin) and every request for an engine the Python side has not attached yet is forwarded
+// verbatim to the Python server on a private Unix socket.  Responses, status codes and RBAC
+// decisions mirror backing/server.py and backing/auth.py (role assignments are pushed down
+// as principal -> (scope prefix, actions)).  Collections whose writes must be mirrored into
+// the columnar query accelerator are flagged by Python (set_mirrored) and their writes are
+// forwarded; a per-collection shared mutex makes the hand-over race-free.
+#pragma once
+
+#include <sys/eventfd.h>
+
+#include <atomic>
+#include <map>
+#include <mutex>
+#include <shared_mutex>
+#include <thread>
+#include <unordered_map>
+
+#include "broker.hpp"
+#include "docstore.hpp"
+#include "evhttp.hpp"
+#include "json.hpp"
+
+namespace tt {
+
+namespace bf {
+
+inline int hexv(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+inline std::string unquote(std::string_view s, bool plus_space = false) {
+  std::string o;
+  o.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && hexv(s[i + 1]) >= 0 && hexv(s[i + 2]) >= 0) {
+      o += (char)(hexv(s[i + 1]) * 16 + hexv(s[i + 2]));
+      i += 2;
+    } else if (plus_space && s[i] == '+') {
+      o += ' ';
+    } else {
+      o += s[i];
+    }
+  }
+  return o;
+}
+
+inline std::string jstr(std::string_view s) {
+  std::string o;
+  escape_to(o, s);
+  return o;
+}
+
+inline bool utf8_ok(std::string_view s) {
+  for (size_t i = 0; i < s.size();) {
+    unsigned char c = (unsigned char)s[i];
+    size_t n = c < 0x80 ? 0 : (c >> 5) == 6 ? 1 : (c >> 4) == 14 ? 2 : (c >> 3) == 30 ? 3 : 99;
+    if (n == 99 || i + n >= s.size() + (n == 0)) return n == 0;
+    for (size_t k = 1; k <= n; ++k)
+      if (((unsigned char)s[i + k] >> 6) != 2) return false;
+    i += n + 1;
+  }
+  return true;
+}
+
+inline std::string b64(std::string_view in) {
+  static const char* t = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string o;
+  size_t i = 0;
+  for (; i + 2 < in.size(); i += 3) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += t[(v >> 6) & 63];
+    o += t[v & 63];
+  }
+  if (i + 1 == in.size()) {
+    uint32_t v = (uint8_t)in[i] << 16;
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += "==";
+  } else if (i + 2 == in.size()) {
+    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8);
+    o += t[v >> 18];
+    o += t[(v >> 12) & 63];
+    o += t[(v >> 6) & 63];
+    o += '=';
+  }
+  return o;
+}
+
+// RFC 7807 body exactly like web/http.py problem()
+inline std::string problem_json(int status, std::string_view detail) {
+  return "{\"type\": \"https://tools.ietf.org/html/rfc9110#section-15." + std::to_string(status / 100) +
+         "\", \"title\": " + jstr(ev::reason_phrase(status)) + ", \"status\": " + std::to_string(status) +
+         ", \"detail\": " + jstr(detail) + "}";
+}
+
+struct Grant {
+  std::string principal, scope;
+  std::vector<std::string> actions;  // "*" = any
+};
+
+}  // namespace bf
+
+class BackingFront {
+ public:
+  BackingFront(const std::string& host, int port, const std::string& fallback_uds)
+      : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)), client_(loop_) {
+    handler_ = [this](ev::Message&& m, ev::Reply r) { on_request(std::move(m), std::move(r)); };
+    ev::Endpoint ep;
+    ep.unix_socket = false;
+    ep.host = host;
+    ep.port = port;
+    port_ = ev::listen_on(loop_, ep, handler_);
+    wake_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    auto w = std::make_shared<Wake>(this);
+    w->fd = dup(wake_fd_);
+    loop_.add(w, EPOLLIN);
+    thread_ = std::thread([this] { loop_.run([this](double t) { on_tick(t); }); });
+  }
+  ~BackingFront() { stop(); }
+
+  int port() const { return port_; }
+
+  void stop() {
+    if (!thread_.joinable()) return;
+    stop_flag_ = true;
+    wake();
+    thread_.join();
+    ::close(wake_fd_);
+  }
+
+  // -- configuration pushed from Python (any thread) -----------------------------------
+  void attach_store(const std::string& account, const std::string& db, const std::string& coll, DocStore* s) {
+    std::unique_lock l(cfg_mu_);
+    auto& c = colls_[account + "\x1f" + db + "\x1f" + coll];
+    if (!c) c = std::make_unique<Coll>();
+    c->store = s;
+  }
+  void attach_broker(const std::string& ns, Broker* b) {
+    std::unique_lock l(cfg_mu_);
+    brokers_[ns] = b;
+  }
+  // Writes to this collection must go through Python from now on (accelerator mirror).
+  // Blocks until native writes already in progress on the collection have finished.
+  void set_mirrored(const std::string& account, const std::string& db, const std::string& coll) {
+    Coll* c;
+    {
+      std::unique_lock l(cfg_mu_);
+      auto& p = colls_[account + "\x1f" + db + "\x1f" + coll];
+      if (!p) p = std::make_unique<Coll>();
+      c = p.get();
+    }
+    std::unique_lock w(c->write_mu);
+    c->mirrored = true;
+  }
+  void set_policy(const std::string& mode, const std::vector<std::pair<std::string, std::string>>& keys,
+                  const std::vector<std::tuple<std::string, std::string, std::vector<std::string>>>& grants) {
+    std::unique_lock l(cfg_mu_);
+    enforce_ = mode == "enforce";
+    keys_ = keys;
+    grants_.clear();
+    for (auto& [p, s, a] : grants) grants_.push_back(bf::Grant{p, s, a});
+  }
+  // Python-side broker activity (publish / abandon) for parked native long-polls.
+  void notify(const std::string& ns, const std::string& entity) {
+    {
+      std::lock_guard l(notify_mu_);
+      notified_.push_back(ns + "|" + entity);
+    }
+    wake();
+  }
+  std::map<std::string, uint64_t> stats() {
+    std::lock_guard l(notify_mu_);
+    return stats_;
+  }
+
+ private:
+  struct Coll {
+    DocStore* store = nullptr;
+    bool mirrored = false;
+    std::shared_mutex write_mu;
+  };
+  struct Wake : ev::IoObj {
+    BackingFront* f;
+    explicit Wake(BackingFront* x) : f(x) {}
+    void on_event(uint32_t) override {
+      uint64_t v;
+      while (::read(fd, &v, sizeof v) == (ssize_t)sizeof v) {
+      }
+      f->on_wake();
+    }
+  };
+  struct Parked {
+    std::string ns, entity;
+    size_t max;
+    int64_t lock_ms;
+    double deadline;
+    ev::Reply reply;
+  };
+
+  ev::Loop loop_;
+  ev::Endpoint fallback_;
+  ev::Client client_;
+  ev::Handler handler_;
+  int port_ = 0;
+  int wake_fd_ = -1;
+  std::thread thread_;
+  std::atomic<bool> stop_flag_{false};
+
+  std::shared_mutex cfg_mu_;
+  std::unordered_map<std::string, std::unique_ptr<Coll>> colls_;
+  std::unordered_map<std::string, Broker*> brokers_;
+  bool enforce_ = false;
+  std::vector<std::pair<std::string, std::string>> keys_;
+  std::vector<bf::Grant> grants_;
+
+  std::mutex notify_mu_;
+  std::vector<std::string> notified_;
+  std::map<std::string, uint64_t> stats_;
+  std::multimap<std::string, Parked> parked_;  // "ns|entity" -> waiting receives (loop thread only)
+
+  void wake() {
+    uint64_t one = 1;
+    ssize_t r = ::write(wake_fd_, &one, sizeof one);
+    (void)r;
+  }
+  void count(const char* k) {
+    std::lock_guard l(notify_mu_);
+    stats_[k]++;
+  }
+
+  void on_wake() {
+    if (stop_flag_) {
+      for (auto& kv : parked_) kv.second.reply.json(503, bf::problem_json(503, "shutting down"));
+      parked_.clear();
+      loop_.stop();
+      return;
+    }
+    std::vector<std::string> keys;
+    {
+      std::lock_guard l(notify_mu_);
+      keys.swap(notified_);
+    }
+    for (auto& k : keys) retry_parked(k);
+  }
+  void on_tick(double now) {
+    if (stop_flag_) {
+      on_wake();
+      return;
+    }
+    // deadlines + periodic re-check (delayed / scheduled messages, expired locks)
+    std::vector<std::string> keys;
+    for (auto& kv : parked_)
+      if (keys.empty() || keys.back() != kv.first) keys.push_back(kv.first);
+    for (auto& k : keys) retry_parked(k, now);
+  }
+
+  // -- auth: backing/auth.py AccessPolicy.check ----------------------------------------
+  bool allowed(const ev::Message& m, const std::string& action, const std::string& scope) {
+    std::shared_lock l(cfg_mu_);
+    if (!enforce_) return true;
+    auto* key = m.header("x-tt-key");
+    if (key && !key->empty())
+      for (auto& [ks, k] : keys_)
+        if (scope.rfind(ks, 0) == 0 && *key == k) return true;
+    auto* ident = m.header("x-tt-identity");
+    if (ident && !ident->empty())
+      for (auto& g : grants_) {
+        if (g.principal != *ident || scope.rfind(g.scope, 0) != 0) continue;
+        for (auto& a : g.actions)
+          if (a == "*" || a == action) return true;
+      }
+    return false;
+  }
+  bool authorize(const ev::Message& m, const ev::Reply& r, const std::string& action, const std::string& scope) {
+    if (allowed(m, action, scope)) return true;
+    auto* ident = m.header("x-tt-identity");
+    std::string who = ident && !ident->empty() ? *ident : "anonymous";
+    r.send(403, {{"content-type", "application/problem+json; charset=utf-8"}},
+           bf::problem_json(403, who + " is not authorized to perform " + action + " on " + scope));
+    return false;
+  }
+
+  // -- dispatch ---------------------------------------------------------------------------
+  static void split(const std::string& target, std::string& path, std::string& qs) {
+    auto q = target.find('?');
+    path = target.substr(0, q);
+    qs = q == std::string::npos ? "" : target.substr(q + 1);
+  }
+  static std::string query_get(const std::string& qs, const std::string& name) {
+    size_t i = 0;
+    while (i <= qs.size() && !qs.empty()) {
+      size_t j = qs.find('&', i);
+      if (j == std::string::npos) j = qs.size();
+      std::string_view kv(qs.data() + i, j - i);
+      size_t eq = kv.find('=');
+      if (bf::unquote(kv.substr(0, eq), true) == name)
+        return eq == std::string_view::npos ? "" : bf::unquote(kv.substr(eq + 1), true);
+      i = j + 1;
+    }
+    return "";
+  }
+
+  void on_request(ev::Message&& m, ev::Reply r) {
+    std::string path, qs;
+    split(m.target, path, qs);
+    std::vector<std::string> seg;
+    for (size_t i = 1; i <= path.size();) {
+      size_t j = path.find('/', i);
+      if (j == std::string::npos) j = path.size();
+      seg.push_back(bf::unquote(std::string_view(path).substr(i, j - i)));
+      i = j + 1;
+    }
+    if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(m, r, seg)) return;
+    if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(m, r, seg, qs)) return;
+    forward(std::move(m), std::move(r));
+  }
+
+  void forward(ev::Message&& m, ev::Reply r) {
+    count("forwarded");
+    ev::HeaderList h;
+    for (auto& kv : m.headers)
+      if (!ev::is_hop_header(kv.first)) h.push_back(kv);
+    client_.request(fallback_, m.method, m.target, h, m.body, 0, [r](ev::ClientResult&& res) {
+      if (res.err) {
+        r.send(503, {{"content-type", "application/problem+json; charset=utf-8"}},
+               bf::problem_json(503, "backing control plane unreachable"));
+        return;
+      }
+      r.send(res.resp.status, res.resp.headers, res.resp.body);
+    });
+  }
+
+  // -- cosmos documents ----------------------------------------------------------------------
+  bool handle_doc(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
+    Coll* c = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
+      if (it != colls_.end() && it->second->store) c = it->second.get();
+    }
+    if (!c) return false;
+    const std::string& key = seg[5];
+    const std::string scope = "cosmos/" + seg[1];
+    if (m.method == "GET") {
+      if (!authorize(m, r, "cosmos.read", scope)) return true;
+      count("doc.get");
+      auto v = c->store->get(key);
+      if (!v) r.empty(404);
+      else r.send(200, {{"etag", v->second}, {"content-type", "application/json"}}, v->first);
+      return true;
+    }
+    if (m.method != "PUT" && m.method != "DELETE") return false;
+    auto* ttl = m.header("x-tt-ttl-ms");
+    if (ttl && !ttl->empty() && *ttl != "0") return false;  // TTL writes disable the accelerator (Python)
+    std::shared_lock w(c->write_mu);
+    if (c->mirrored) return false;
+    if (!authorize(m, r, "cosmos.write", scope)) return true;
+    auto* im = m.header("if-match");
+    std::optional<std::string> etag;
+    if (im && !im->empty()) etag = *im;
+    const char* pj = "application/problem+json; charset=utf-8";
+    if (m.method == "PUT") {
+      count("doc.put");
+      auto* fw = m.header("x-tt-first-write");
+      try {
+        std::string e = c->store->set(key, m.body, etag, fw && *fw == "1", 0);
+        r.send(200, {{"etag", e}, {"content-type", "application/json"}}, "{\"etag\": " + bf::jstr(e) + "}");
+      } catch (const EtagMismatch& ex) {
+        r.send(412, {{"content-type", pj}}, bf::problem_json(412, ex.what()));
+      } catch (const ParseError& ex) {
+        r.send(400, {{"content-type", pj}}, bf::problem_json(400, std::string("invalid JSON: ") + ex.what()));
+      }
+      return true;
+    }
+    count("doc.delete");
+    try {
+      bool ok = c->store->del(key, etag);
+      r.empty(ok ? 204 : 404);
+    } catch (const EtagMismatch& ex) {
+      r.send(412, {{"content-type", pj}}, bf::problem_json(412, ex.what()));
+    }
+    return true;
+  }
+
+  // -- service bus ---------------------------------------------------------------------------
+  static std::string entity_scope(const std::string& entity) {
+    auto p = entity.find("/subscriptions/");
+    if (p != std::string::npos) return "topics/" + entity.substr(0, p);
+    return "queues/" + entity;
+  }
+
+  bool handle_bus(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
+    Broker* b = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = brokers_.find(seg[1]);
+      if (it != brokers_.end()) b = it->second;
+    }
+    if (!b) return false;
+    const std::string& ns = seg[1];
+    if (seg.size() == 5 && seg[2] == "topics" && seg[4] == "messages" && m.method == "POST") {
+      if (!authorize(m, r, "sb.send", "servicebus/" + ns + "/topics/" + seg[3])) return true;
+      count("sb.publish");
+      auto* ct = m.header("content-type");
+      auto* props = m.header("x-tt-props");
+      auto* mid = m.header("x-tt-message-id");
+      auto* ttl = m.header("x-tt-ttl-ms");
+      auto* delay = m.header("x-tt-delay-ms");
+      uint64_t seq = b->publish(seg[3], m.body, ct ? *ct : "application/json", props ? *props : "{}", mid ? *mid : "",
+                                ttl && !ttl->empty() ? std::atoll(ttl->c_str()) : 0,
+                                delay && !delay->empty() ? std::atoll(delay->c_str()) : 0);
+      r.send(201, {{"content-type", "application/json"}}, "{\"seq\": " + std::to_string(seq) + "}");
+      for (auto& sub : b->subscriptions(seg[3])) retry_parked(ns + "|" + seg[3] + "/subscriptions/" + sub);
+      return true;
+    }
+    if (seg.size() == 3 && seg[2] == "receive" && m.method == "POST") {
+      std::string entity = query_get(qs, "entity");
+      if (!authorize(m, r, "sb.receive", "servicebus/" + ns + "/" + entity_scope(entity))) return true;
+      count("sb.receive");
+      std::string mx = query_get(qs, "max"), lk = query_get(qs, "lockMs"), wt = query_get(qs, "waitMs");
+      Parked p{ns, entity, (size_t)std::max(1, mx.empty() ? 1 : std::atoi(mx.c_str())),
+               lk.empty() ? 0 : std::atoll(lk.c_str()), ev::now_s() + (wt.empty() ? 0 : std::atoi(wt.c_str())) / 1000.0,
+               r};
+      if (!try_receive(b, p, false)) parked_.emplace(ns + "|" + entity, std::move(p));
+      return true;
+    }
+    if (seg.size() == 3 && seg[2] == "settle" && m.method == "POST") {
+      Value body;
+      try {
+        body = parse(m.body.empty() ? std::string_view("{}") : std::string_view(m.body));
+      } catch (const std::exception&) {
+        return false;  // let Python produce its error
+      }
+      std::string entity;
+      if (auto* e = body.get("entity"); e && e->t == Value::String) entity = e->s;
+      if (!authorize(m, r, "sb.receive", "servicebus/" + ns + "/" + entity_scope(entity))) return true;
+      count("sb.settle");
+      auto list = [&](const char* k) -> const std::vector<Value>* {
+        auto* v = body.get(k);
+        return v && v->t == Value::Array ? &v->items : nullptr;
+      };
+      auto str = [](const Value& o, const char* k) {
+        auto* v = o.get(k);
+        return v && v->t == Value::String ? v->s : std::string();
+      };
+      auto num = [](const Value& o, const char* k) {
+        auto* v = o.get(k);
+        return v && v->t == Value::Number ? (int64_t)v->n : (int64_t)0;
+      };
+      std::string out = "{\"complete\": [";
+      if (auto* l = list("complete"))
+        for (size_t i = 0; i < l->size(); ++i) out += std::string(i ? ", " : "") + (b->complete(entity, (*l)[i].s) ? "true" : "false");
+      out += "], \"abandon\": [";
+      bool abandoned = false;
+      if (auto* l = list("abandon"))
+        for (size_t i = 0; i < l->size(); ++i) {
+          abandoned = true;
+          out += std::string(i ? ", " : "") +
+                 (b->abandon(entity, str((*l)[i], "token"), num((*l)[i], "delayMs")) ? "true" : "false");
+        }
+      out += "], \"deadletter\": [";
+      if (auto* l = list("deadletter"))
+        for (size_t i = 0; i < l->size(); ++i)
+          out += std::string(i ? ", " : "") +
+                 (b->dead_letter(entity, str((*l)[i], "token"), str((*l)[i], "reason")) ? "true" : "false");
+      out += "], \"renew\": [";
+      if (auto* l = list("renew"))
+        for (size_t i = 0; i < l->size(); ++i)
+          out += std::string(i ? ", " : "") +
+                 (b->renew(entity, str((*l)[i], "token"), num((*l)[i], "lockMs")) ? "true" : "false");
+      out += "]}";
+      r.send(200, {{"content-type", "application/json"}}, out);
+      if (abandoned) retry_parked(ns + "|" + entity);
+      return true;
+    }
+    if (seg.size() == 3 && seg[2] == "counts" && m.method == "GET") {
+      auto [a, s, l, d, e, c, rc] = b->counts(query_get(qs, "entity"));
+      r.send(200, {{"content-type", "application/json"}},
+             "{\"active\": " + std::to_string(a) + ", \"scheduled\": " + std::to_string(s) + ", \"locked\": " +
+                 std::to_string(l) + ", \"dead_letter\": " + std::to_string(d) + ", \"enqueued\": " + std::to_string(e) +
+                 ", \"completed\": " + std::to_string(c) + ", \"received\": " + std::to_string(rc) + "}");
+      return true;
+    }
+    return false;
+  }
+
+  // Returns true when the request was answered (messages, or deadline reached).
+  bool try_receive(Broker* b, Parked& p, bool expired) {
+    std::vector<Received> msgs;
+    try {
+      msgs = b->receive(p.entity, p.max, p.lock_ms);
+    } catch (const std::exception& e) {
+      p.reply.send(404, {{"content-type", "application/problem+json; charset=utf-8"}}, bf::problem_json(404, e.what()));
+      return true;
+    }
+    if (msgs.empty() && !expired && ev::now_s() < p.deadline) return false;
+    std::string out = "[";
+    for (size_t i = 0; i < msgs.size(); ++i) {
+      auto& x = msgs[i];
+      if (i) out += ", ";
+      std::string props = x.props.empty() ? "{}" : x.props;
+      out += "{\"lockToken\": " + bf::jstr(x.lock_token) + ", \"seq\": " + std::to_string(x.seq) + ", \"id\": " +
+             bf::jstr(x.id) + ", \"contentType\": " + bf::jstr(x.content_type) + ", \"props\": " + props +
+             ", \"deliveryCount\": " + std::to_string(x.delivery_count) + ", \"enqueuedMs\": " +
+             std::to_string(x.enqueued_wall);
+      if (bf::utf8_ok(x.body)) out += ", \"body\": " + bf::jstr(x.body) + "}";
+      else out += ", \"bodyB64\": \"" + bf::b64(x.body) + "\"}";
+    }
+    out += "]";
+    p.reply.send(200, {{"content-type", "application/json"}}, out);
+    return true;
+  }
+
+  void retry_parked(const std::string& key, double now = 0) {
+    auto range = parked_.equal_range(key);
+    if (range.first == range.second) return;
+    Broker* b = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = brokers_.find(key.substr(0, key.find('|')));
+      if (it != brokers_.end()) b = it->second;
+    }
+    for (auto it = range.first; it != range.second;) {
+      bool expired = now > 0 && now >= it->second.deadline;
+      if (b && try_receive(b, it->second, expired)) it = parked_.erase(it);
+      else ++it;
+    }
+  }
+};
+
+}  // namespace tt

@@ -2,6 +2,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "backingfront.hpp"
 #include "broker.hpp"
 #include "docstore.hpp"
 #include "httpparse.hpp"
@@ -176,4 +177,24 @@ PYBIND11_MODULE(_ttnative, m) {
            })
       .def("purge", &Broker::purge)
       .def("total_published", &Broker::total_published);
+
+  // Native HTTP front of the backing-services process (backingfront.hpp): serves the hot
+  // document / message routes on its own thread against the engines attached here and
+  // forwards everything else to the Python server on `fallback_uds`.
+  py::class_<BackingFront>(m, "BackingFront")
+      .def(py::init<const std::string&, int, const std::string&>(), py::arg("host"), py::arg("port"),
+           py::arg("fallback_uds"))
+      .def("port", &BackingFront::port)
+      .def("attach_store",
+           [](BackingFront& f, const std::string& a, const std::string& d, const std::string& c, DocStore& s) {
+             f.attach_store(a, d, c, &s);
+           },
+           py::keep_alive<1, 5>())
+      .def("attach_broker", [](BackingFront& f, const std::string& ns, Broker& b) { f.attach_broker(ns, &b); },
+           py::keep_alive<1, 3>())
+      .def("set_mirrored", &BackingFront::set_mirrored, py::call_guard<py::gil_scoped_release>())
+      .def("set_policy", &BackingFront::set_policy, py::arg("mode"), py::arg("keys"), py::arg("grants"))
+      .def("notify", &BackingFront::notify)
+      .def("stats", &BackingFront::stats)
+      .def("stop", &BackingFront::stop, py::call_guard<py::gil_scoped_release>());
 }

@@ -1,0 +1,165 @@
+"""Backing-services parity between the Python handlers and the native HTTP front
+(native/src/backingfront.hpp): document CRUD with ETags, publish / long-poll receive /
+settle / counts, RBAC decisions, non-UTF-8 bodies, and the hand-over of a collection's writes
+to the Python path once the columnar query accelerator mirrors it."""
+import asyncio
+import time
+
+import pytest
+
+from aca_dotnet_workshop_amd.backing.client import BackingClient, BackingError, EtagConflict
+from aca_dotnet_workshop_amd.backing.server import serve_backing
+from aca_dotnet_workshop_amd.web import HttpClient
+
+from helpers import run
+
+FRONTS = ["python", "native"]
+
+
+class Backing:
+    def __init__(self, front, monkeypatch, policy=None):
+        monkeypatch.setenv("TT_BACKING_FRONT", front)
+        self.policy = policy
+
+    async def __aenter__(self):
+        ready = asyncio.get_running_loop().create_future()
+        self.stop = asyncio.Event()
+        self.task = asyncio.ensure_future(serve_backing("127.0.0.1", 0, None, self.policy, ready.set_result, self.stop))
+        port = await asyncio.wait_for(ready, 20)
+        self.base = f"http://127.0.0.1:{port}"
+        return self
+
+    async def __aexit__(self, *exc):
+        self.stop.set()
+        await asyncio.wait_for(self.task, 20)
+
+
+@pytest.mark.parametrize("front", FRONTS)
+def test_documents(front, monkeypatch):
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            e1 = await c.doc_put("acct", "db", "c", "k/1 é", '{"a": 1}')
+            got = await c.doc_get("acct", "db", "c", "k/1 é")
+            assert got == (b'{"a": 1}', e1) or got[1] == e1
+            with pytest.raises(EtagConflict):
+                await c.doc_put("acct", "db", "c", "k/1 é", "2", etag="bogus")
+            with pytest.raises(EtagConflict):
+                await c.doc_put("acct", "db", "c", "k/1 é", "2", first_write=True)
+            e2 = await c.doc_put("acct", "db", "c", "k/1 é", "2", etag=e1)
+            assert e2 != e1
+            assert await c.doc_get("acct", "db", "c", "missing") is None
+            with pytest.raises(EtagConflict):
+                await c.doc_delete("acct", "db", "c", "k/1 é", etag=e1)
+            assert await c.doc_delete("acct", "db", "c", "k/1 é") is True
+            assert await c.doc_delete("acct", "db", "c", "k/1 é") is False
+            with pytest.raises(BackingError) as ei:
+                await c.doc_put("acct", "db", "c", "bad", "{not json")
+            assert ei.value.status == 400
+            # query (always Python) sees documents written through the front
+            await c.doc_put("acct", "db", "c", "q1", '{"n": 5}')
+            res = await c.doc_query("acct", "db", "c", b'{"filter": {"EQ": {"n": 5}}}')
+            assert b'"q1"' in res
+            fs = (await c.http.get(b.base + "/admin/front")).json()
+            assert fs["front"] == front
+            if front == "native":
+                assert fs["requests"]["doc.put"] >= 4 and fs["requests"]["doc.get"] >= 2
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
+def test_messaging_and_long_poll(front, monkeypatch):
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.sb_create_subscription("ns", "t", "s", lock_ms=60000, max_delivery=2)
+            ent = "t/subscriptions/s"
+            # a receive parked before the publish wakes up promptly
+            t0 = time.monotonic()
+            recv = asyncio.ensure_future(c.sb_receive("ns", ent, 5, 0, 3000))
+            await asyncio.sleep(0.1)
+            await c.sb_publish("ns", "t", b'{"x": 1}', "application/json", {"k": "v"})
+            msgs = await recv
+            assert time.monotonic() - t0 < 1.5
+            assert len(msgs) == 1 and msgs[0]["body"] == '{"x": 1}' and msgs[0]["props"] == {"k": "v"}
+            assert msgs[0]["deliveryCount"] == 1
+            # abandon -> redelivered, then complete
+            res = await c.sb_settle("ns", ent, abandon=[{"token": msgs[0]["lockToken"]}])
+            assert res["abandon"] == [True]
+            again = await c.sb_receive("ns", ent, 5, 0, 1000)
+            assert again[0]["deliveryCount"] == 2
+            res = await c.sb_settle("ns", ent, complete=[again[0]["lockToken"], "nope"])
+            assert res["complete"] == [True, False]
+            cnt = await c.sb_counts("ns", ent)
+            assert cnt["completed"] == 1 and cnt["active"] == 0 and cnt["enqueued"] == 1
+            # binary payloads travel base64-encoded
+            await c.sb_publish("ns", "t", b"\xff\x00\x01", "application/octet-stream")
+            m = (await c.sb_receive("ns", ent, 1, 0, 1000))[0]
+            assert "bodyB64" in m and m["contentType"] == "application/octet-stream"
+            # an empty long-poll returns [] after its wait
+            await c.sb_settle("ns", ent, complete=[m["lockToken"]])
+            t0 = time.monotonic()
+            assert await c.sb_receive("ns", ent, 1, 0, 300) == []
+            assert 0.25 < time.monotonic() - t0 < 2.0
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
+def test_rbac(front, monkeypatch):
+    policy = {"mode": "enforce", "keys": {"cosmos/acct": "masterkey"},
+              "roleAssignments": [
+                  {"principal": "api-mi", "role": "Cosmos DB Built-in Data Contributor", "scope": "cosmos/acct"},
+                  {"principal": "api-mi", "role": "Azure Service Bus Data Sender", "scope": "servicebus/ns/topics/t"},
+                  {"principal": "proc-mi", "role": "Azure Service Bus Data Receiver", "scope": "servicebus/ns/topics/t"},
+                  {"principal": "admin", "role": "Owner", "scope": ""}]}
+
+    async def main():
+        async with Backing(front, monkeypatch, policy) as b:
+            admin, api = BackingClient(b.base, identity="admin"), BackingClient(b.base, identity="api-mi")
+            proc, anon = BackingClient(b.base, identity="proc-mi"), BackingClient(b.base, identity="")
+            keyed = BackingClient(b.base, identity="", key="masterkey")
+            await admin.sb_create_subscription("ns", "t", "proc")
+            await admin.doc_put("acct", "db", "c", "seed", "0")  # engines exist -> front serves
+            await api.doc_put("acct", "db", "c", "k", "1")
+            await keyed.doc_put("acct", "db", "c", "k2", "2")
+            for call in (anon.doc_put("acct", "db", "c", "k", "1"), proc.doc_get("acct", "db", "c", "k"),
+                         proc.sb_publish("ns", "t", b"x"), api.sb_receive("ns", "t/subscriptions/proc")):
+                with pytest.raises(BackingError) as ei:
+                    await call
+                assert ei.value.status == 403
+                assert b"not authorized" in ei.value.body
+            await api.sb_publish("ns", "t", b"x")
+            assert len(await proc.sb_receive("ns", "t/subscriptions/proc")) == 1
+            # a policy change at runtime reaches the front
+            h = HttpClient()
+            r = await h.put(b.base + "/admin/policy", json_body={"mode": "open"})
+            assert r.status in (200, 204)
+            await anon.doc_put("acct", "db", "c", "k3", "3")
+            await h.close()
+            for c in (admin, api, proc, anon, keyed):
+                await c.http.close()
+    run(main())
+
+
+def test_accelerator_handover(monkeypatch):
+    """Writes through the native front before the columnar index exists, through Python after."""
+    monkeypatch.setenv("TT_QUERY_ACCEL", "cpu")
+    monkeypatch.setenv("TT_QUERY_ACCEL_MIN_DOCS", "10")
+
+    async def main():
+        async with Backing("native", monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            for i in range(40):
+                await c.doc_put("acct", "db", "c", f"k{i}", '{"n": %d}' % i)
+            q = b'{"filter": {"GT": {"n": 30}}}'
+            assert (await c.doc_query("acct", "db", "c", q)).count(b'"key"') == 9  # builds the index
+            for i in range(40, 60):
+                await c.doc_put("acct", "db", "c", f"k{i}", '{"n": %d}' % i)
+            await c.doc_delete("acct", "db", "c", "k35")
+            assert (await c.doc_query("acct", "db", "c", q)).count(b'"key"') == 28
+            st = (await c.doc_stats("acct", "db", "c"))["accelerator"]
+            assert st["cpu"] == 2 and st["rows"] == 59
+            await c.http.close()
+    run(main())
