@@ -38,8 +38,10 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=512, help="createTask requests per step per rank")
     ap.add_argument("--concurrency", type=int, default=64, help="requests in flight per rank")
-    ap.add_argument("--api-replicas", type=int, default=2, help="API replicas behind the client's load balancing")
-    ap.add_argument("--processor-replicas", type=int, default=2, help="competing consumers on the subscription")
+    ap.add_argument("--api-replicas", type=int, default=0,
+                    help="API replicas behind the client's load balancing (0 = size to this rank's CPU share)")
+    ap.add_argument("--processor-replicas", type=int, default=0,
+                    help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
     ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
     return ap.parse_args()
@@ -80,6 +82,34 @@ class Dist:
     def close(self) -> None:
         if self.pg is not None:
             self.pg.destroy_process_group()
+
+
+def cpu_budget() -> float:
+    """CPUs this process may use: cgroup v2/v1 quota, else the affinity mask (a GPU box's
+    ``nproc`` shows the whole machine while the job gets a share of it)."""
+    n = float(len(os.sched_getaffinity(0)))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, int(quota) / int(period))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                n = min(n, q / p)
+        except (OSError, ValueError):
+            pass
+    return n
+
+
+def topology(cores: float) -> tuple[int, int]:
+    """Replica counts for one rank's environment.  Per-task CPU measured on the stack
+    (docs/PERFORMANCE.md): the Python API app is the costliest hop, then the processor app;
+    sidecar data planes and the backing front are native and cheap."""
+    api = max(1, min(6, int(cores // 3)))
+    proc = max(1, min(4, int(cores // 5)))
+    return max(api, 2 if cores >= 6 else 1), max(proc, 2 if cores >= 6 else 1)
 
 
 def device_sync() -> None:
@@ -133,6 +163,11 @@ def main() -> None:
     a = parse()
     d = Dist()
     n = d.world if d.world > 1 else a.gpus
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", d.world if d.world > 1 else 1))
+    cores = cpu_budget() / max(1, local)
+    auto_api, auto_proc = topology(cores)
+    a.api_replicas = a.api_replicas or auto_api
+    a.processor_replicas = a.processor_replicas or auto_proc
     from aca_dotnet_workshop_amd.platform.processes import LocalStack
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
     stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
@@ -153,16 +188,23 @@ def main() -> None:
         lat: list[float] = []
         d.barrier()
         device_sync()
+        import psutil
+        me = psutil.Process()
         cpu0 = stack.cpu_seconds()
+        t = me.cpu_times()
+        cpu0["bench-client"] = t.user + t.system
         dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
         device_sync()
         d.barrier()
         cpu1 = stack.cpu_seconds()
+        t = me.cpu_times()
+        cpu1["bench-client"] = t.user + t.system
         dt_max = d.max(dt)
         if d.rank == 0:
             # cores busy per process role during the timed region (where the E2E flow is CPU bound)
             util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
-            print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2)}),
+            print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
+                              "cpu_budget_per_rank": round(cores, 2)}),
                   file=sys.stderr, flush=True)
         lat.sort()
         p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
