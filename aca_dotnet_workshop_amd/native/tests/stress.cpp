@@ -15,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include "../src/backingfront.hpp"
 #include "../src/broker.hpp"
 #include "../src/docstore.hpp"
 #include "../src/httpparse.hpp"
@@ -153,6 +154,62 @@ int main(int argc, char** argv) {
       return fail("broker lost or duplicated messages");
     }
     std::printf("broker ok: %ld completed, %zu dead-lettered of %ld\n", (long)c, d, total);
+  }
+
+  // ---------------------------------------------------------------- backing front
+  // HTTP clients on several threads against the native front's loop thread while the
+  // "Python" thread reconfigures it (policy, attach, mirrored hand-over, notify).
+  {
+    DocStore store;
+    Broker broker;
+    QueueOptions o;
+    broker.create_subscription("t", "s", o);
+    BackingFront front("127.0.0.1", 0, "/nonexistent/fallback.sock");
+    front.attach_store("a", "d", "c", &store);
+    front.attach_broker("ns", &broker);
+    int port = front.port();
+    auto http = [port](const std::string& req) {
+      int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)port);
+      inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+      std::string out;
+      if (::connect(fd, (sockaddr*)&a, sizeof a) == 0) {
+        ::send(fd, req.data(), req.size(), MSG_NOSIGNAL);
+        char buf[8192];
+        ssize_t n;
+        while ((n = ::recv(fd, buf, sizeof buf, 0)) > 0) out.append(buf, (size_t)n);
+      }
+      ::close(fd);
+      return out;
+    };
+    std::atomic<int> ok{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 4; ++t)
+      ts.emplace_back([&, t] {
+        for (int i = 0; i < 100; ++i) {
+          std::string k = "k" + std::to_string((t * 100 + i) % 37), body = "{\"v\":" + std::to_string(i) + "}";
+          std::string r1 = http("PUT /cosmos/a/d/c/docs/" + k + " HTTP/1.1\r\nContent-Length: " +
+                                std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body);
+          std::string r2 = http("GET /cosmos/a/d/c/docs/" + k + " HTTP/1.1\r\nConnection: close\r\n\r\n");
+          std::string r3 = http("POST /servicebus/ns/topics/t/messages HTTP/1.1\r\nContent-Length: 2\r\n"
+                                "Connection: close\r\n\r\n{}");
+          std::string r4 = http("POST /servicebus/ns/receive?entity=t/subscriptions/s&max=4&waitMs=1 HTTP/1.1\r\n"
+                                "Connection: close\r\n\r\n");
+          if (r1.rfind("HTTP/1.1 ", 0) == 0 && r3.rfind("HTTP/1.1 201", 0) == 0 && r4.rfind("HTTP/1.1 200", 0) == 0) ok++;
+        }
+      });
+    for (int i = 0; i < 200; ++i) {
+      front.set_policy(i % 2 ? "open" : "open", {{"cosmos/a", "key"}}, {{"p", "cosmos/a", {"cosmos.read"}}});
+      front.notify("ns", "t/subscriptions/s");
+      if (i == 150) front.set_mirrored("a", "d", "c");  // later writes go to the (missing) fallback -> 503
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    for (auto& th : ts) th.join();
+    front.stop();
+    if (ok.load() < 100) return fail("backing front served too few requests");
+    std::printf("backing front ok: %d request rounds\n", ok.load());
   }
 
   // ---------------------------------------------------------------- http head parser

@@ -35,7 +35,7 @@ def _build_and_run(tmp_path, flags, env_extra, args=("8", "1500")):
 
 def test_native_engines_threadsanitizer(tmp_path):
     out = _build_and_run(tmp_path, ["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"})
-    assert "broker ok" in out and "docstore ok" in out
+    assert "broker ok" in out and "docstore ok" in out and "backing front ok" in out
 
 
 def test_native_engines_address_ub_sanitizer(tmp_path):
