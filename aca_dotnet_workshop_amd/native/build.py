@@ -70,6 +70,26 @@ def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
     return DATAPLANE
 
 
+LOADGEN = HERE / "bin" / "ttloadgen"
+
+
+def build_loadgen(force: bool = False, verbose: bool = False) -> Path:
+    """Closed-loop HTTP load generator used by bench.py (src/loadgen.cpp)."""
+    sources = [SRC / "loadgen.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
+    if not force and not _stale(LOADGEN, sources):
+        return LOADGEN
+    LOADGEN.parent.mkdir(exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    tmp = LOADGEN.with_name(f".{LOADGEN.name}.tmp{os.getpid()}")
+    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(SRC / "loadgen.cpp"), "-o", str(tmp)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LOADGEN)
+    return LOADGEN
+
+
 if __name__ == "__main__":
     print(build_native(force="--force" in sys.argv, verbose=True))
     print(build_dataplane(force="--force" in sys.argv, verbose=True))
+    print(build_loadgen(force="--force" in sys.argv, verbose=True))

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <string>
 #include <string_view>
@@ -86,6 +87,7 @@ class Loop {
     }
   }
   void defer(std::function<void()> f) { deferred_.push_back(std::move(f)); }
+  void call_later(double delay_s, std::function<void()> f) { timers_.emplace(now_s() + delay_s, std::move(f)); }
   void stop() { running_ = false; }
   bool running() const { return running_; }
   size_t live_objects() const { return objs_.size(); }
@@ -94,7 +96,13 @@ class Loop {
     epoll_event evs[256];
     double last_tick = now_s();
     while (running_) {
-      int n = epoll_wait(ep_, evs, 256, deferred_.empty() ? 50 : 0);
+      int timeout_ms = 50;
+      if (!deferred_.empty()) timeout_ms = 0;
+      else if (!timers_.empty()) {
+        double dt = timers_.begin()->first - now_s();
+        timeout_ms = dt <= 0 ? 0 : std::min(50, (int)(dt * 1000.0) + 1);
+      }
+      int n = epoll_wait(ep_, evs, 256, timeout_ms);
       for (int i = 0; i < n; ++i) {
         auto* o = static_cast<IoObj*>(evs[i].data.ptr);
         if (!o->dead) o->on_event(evs[i].events);
@@ -105,6 +113,11 @@ class Loop {
         for (auto& f : d) f();
       }
       double t = now_s();
+      while (!timers_.empty() && timers_.begin()->first <= t) {
+        auto f = std::move(timers_.begin()->second);
+        timers_.erase(timers_.begin());
+        f();
+      }
       if (t - last_tick >= 0.05) {
         last_tick = t;
         std::vector<std::shared_ptr<IoObj>> snapshot;
@@ -124,6 +137,7 @@ class Loop {
   std::unordered_map<IoObj*, std::shared_ptr<IoObj>> objs_;
   std::vector<std::shared_ptr<IoObj>> graveyard_;
   std::vector<std::function<void()>> deferred_;
+  std::multimap<double, std::function<void()>> timers_;
 };
 
 // ------------------------------------------------------------------------------ messages

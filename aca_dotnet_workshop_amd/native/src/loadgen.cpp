@@ -1,0 +1,201 @@
+// ttloadgen: closed-loop HTTP/1.1 load generator on the native event loop (evhttp.hpp).
+//
+// Drives `--concurrency` keep-alive request streams round-robin over one or more targets
+// (Unix sockets or TCP), in `--steps` steps of `--batch` requests.  With `--until-url` a
+// step ends only when the JSON counter at that URL (field `--until-field`) has advanced by
+// the batch size -- bench.py uses it to wait until the processor acknowledged every task.
+// Request bodies come from a file with one body per line (cycled).  Prints one JSON line:
+// {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
+//
+//   ttloadgen --target unix:/path/a.sock --target unix:/path/b.sock 
+//       --path /v1.0/invoke/api/method/api/tasks --bodies bodies.txt 
+//       --concurrency 128 --batch 1024 --steps 20 --expect 201 
+//       --until-url http://127.0.0.1:9000/servicebus/ns/counts?entity=... --until-field completed
+#include <algorithm>
+#include <csignal>
+#include <cstdio>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "evhttp.hpp"
+#include "json.hpp"
+
+using namespace tt;
+
+namespace {
+
+struct Opts {
+  std::vector<ev::Endpoint> targets;
+  std::string path = "/", method = "POST", ctype = "application/json", until_url, until_field = "completed";
+  std::vector<std::string> bodies{""};
+  int concurrency = 64, batch = 512, steps = 1, expect = 0;
+};
+
+class Gen {
+ public:
+  Gen(ev::Loop& loop, Opts o) : loop_(loop), client_(loop), o_(std::move(o)) {
+    if (!o_.until_url.empty()) {
+      std::string u = o_.until_url;
+      if (u.rfind("http://", 0) == 0) u = u.substr(7);
+      auto slash = u.find('/');
+      until_ep_ = ev::Endpoint::parse(u.substr(0, slash));
+      until_target_ = slash == std::string::npos ? "/" : u.substr(slash);
+    }
+  }
+
+  void start() {
+    t0_ = ev::now_s();
+    if (until_target_.empty()) begin_step();
+    else poll_counter([this](long long v) {
+      base_ = v;
+      begin_step();
+    });
+  }
+
+  std::string report() const {
+    std::vector<double> l = lat_;
+    std::sort(l.begin(), l.end());
+    auto pct = [&](double p) { return l.empty() ? 0.0 : l[std::min(l.size() - 1, (size_t)(l.size() * p))] * 1e3; };
+    char buf[512];
+    std::snprintf(buf, sizeof buf,
+                  "{\"requests\": %lld, \"errors\": %lld, \"elapsed_s\": %.6f, \"latency_ms\": {\"p50\": %.3f, "
+                  "\"p99\": %.3f, \"max\": %.3f}, \"first_error\": ",
+                  done_total_, errors_, t1_ - t0_, pct(0.5), pct(0.99), l.empty() ? 0.0 : l.back() * 1e3);
+    std::string s = buf;
+    escape_to(s, first_error_);
+    return s + "}";
+  }
+  long long errors() const { return errors_; }
+
+ private:
+  ev::Loop& loop_;
+  ev::Client client_;
+  Opts o_;
+  ev::Endpoint until_ep_;
+  std::string until_target_;
+  double t0_ = 0, t1_ = 0;
+  int step_ = 0;
+  long long issued_ = 0, done_ = 0, done_total_ = 0, errors_ = 0, base_ = 0;
+  size_t rr_ = 0;
+  std::vector<double> lat_;
+  std::string first_error_;
+
+  void begin_step() {
+    if (step_ == o_.steps) {
+      t1_ = ev::now_s();
+      loop_.stop();
+      return;
+    }
+    issued_ = done_ = 0;
+    int n = std::min(o_.concurrency, o_.batch);
+    for (int i = 0; i < n; ++i) issue();
+  }
+
+  void issue() {
+    if (issued_ >= o_.batch) return;
+    long long i = issued_++;
+    const ev::Endpoint& ep = o_.targets[rr_++ % o_.targets.size()];
+    const std::string& body = o_.bodies[(size_t)((step_ * (long long)o_.batch + i) % (long long)o_.bodies.size())];
+    double t = ev::now_s();
+    client_.request(ep, o_.method, o_.path, {{"content-type", o_.ctype}}, body, 60, [this, t](ev::ClientResult&& r) {
+      lat_.push_back(ev::now_s() - t);
+      bool bad = r.err || (o_.expect && r.resp.status != o_.expect);
+      if (bad) {
+        errors_++;
+        if (first_error_.empty())
+          first_error_ = r.err ? std::string("errno ") + std::to_string(r.err)
+                               : "HTTP " + std::to_string(r.resp.status) + " " + r.resp.body.substr(0, 200);
+      }
+      done_++;
+      done_total_++;
+      if (done_ == o_.batch) end_step();
+      else issue();
+    });
+  }
+
+  void end_step() {
+    base_ += o_.batch;
+    ++step_;
+    if (until_target_.empty()) {
+      begin_step();
+      return;
+    }
+    wait_counter();
+  }
+
+  void wait_counter() {
+    poll_counter([this](long long v) {
+      if (v >= base_) begin_step();
+      else loop_.call_later(0.001, [this] { wait_counter(); });
+    });
+  }
+
+  void poll_counter(std::function<void(long long)> cb) {
+    client_.request(until_ep_, "GET", until_target_, {}, {}, 30, [this, cb](ev::ClientResult&& r) {
+      long long v = -1;
+      if (!r.err && r.resp.status == 200) {
+        try {
+          Value j = parse(r.resp.body);
+          if (auto* f = j.get(o_.until_field); f && f->t == Value::Number) v = (long long)f->n;
+        } catch (const std::exception&) {
+        }
+      }
+      if (v < 0) {
+        errors_++;
+        if (first_error_.empty()) first_error_ = "counter poll failed";
+        t1_ = ev::now_s();
+        loop_.stop();
+        return;
+      }
+      cb(v);
+    });
+  }
+};
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Opts o;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", a.c_str());
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--target") o.targets.push_back(ev::Endpoint::parse(next()));
+    else if (a == "--path") o.path = next();
+    else if (a == "--method") o.method = next();
+    else if (a == "--content-type") o.ctype = next();
+    else if (a == "--concurrency") o.concurrency = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--batch") o.batch = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--steps") o.steps = std::max(0, std::atoi(next().c_str()));
+    else if (a == "--expect") o.expect = std::atoi(next().c_str());
+    else if (a == "--until-url") o.until_url = next();
+    else if (a == "--until-field") o.until_field = next();
+    else if (a == "--bodies") {
+      std::ifstream in(next());
+      o.bodies.clear();
+      for (std::string line; std::getline(in, line);)
+        if (!line.empty()) o.bodies.push_back(line);
+      if (o.bodies.empty()) o.bodies.push_back("");
+    } else {
+      std::fprintf(stderr, "unknown option %s\n", a.c_str());
+      return 2;
+    }
+  }
+  if (o.targets.empty()) {
+    std::fprintf(stderr, "at least one --target is required\n");
+    return 2;
+  }
+  signal(SIGPIPE, SIG_IGN);
+  ev::Loop loop;
+  Gen g(loop, o);
+  g.start();
+  loop.run();
+  std::printf("%s\n", g.report().c_str());
+  return g.errors() ? 1 : 0;
+}

@@ -36,14 +36,17 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="createTask requests per step per rank")
-    ap.add_argument("--concurrency", type=int, default=64, help="requests in flight per rank")
+    ap.add_argument("--batch", type=int, default=1024, help="createTask requests per step per rank")
+    ap.add_argument("--concurrency", type=int, default=0,
+                    help="requests in flight per rank (0 = 32 per API replica, at most 256)")
     ap.add_argument("--api-replicas", type=int, default=0,
                     help="API replicas behind the client's load balancing (0 = size to this rank's CPU share)")
     ap.add_argument("--processor-replicas", type=int, default=0,
                     help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
     ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
+    ap.add_argument("--client", choices=("native", "python"), default="native",
+                    help="load generator: native/bin/ttloadgen (C++) or the in-process asyncio client")
     return ap.parse_args()
 
 
@@ -128,9 +131,7 @@ async def run_steps(socks: list[str], counts_url: str, entity: str, steps: int, 
     c = HttpClient()
     urls = [f"unix:{s}:/v1.0/invoke/tasksmanager-backend-api/method/api/tasks" for s in socks]
     hdr = {"Content-Type": "application/json"}
-    bodies = [json.dumps({"taskName": f"bench task {i}", "taskCreatedBy": f"user{i % 97}@bench.local",
-                          "taskDueDate": "2030-01-01T00:00:00", "taskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
-              for i in range(batch)]
+    bodies = _bodies(batch)
 
     async def completed() -> int:
         r = await c.get(counts_url)
@@ -159,6 +160,29 @@ async def run_steps(socks: list[str], counts_url: str, entity: str, steps: int, 
     return dt
 
 
+def _bodies(batch: int) -> list[bytes]:
+    return [json.dumps({"taskName": f"bench task {i}", "taskCreatedBy": f"user{i % 97}@bench.local",
+                        "taskDueDate": "2030-01-01T00:00:00", "taskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
+            for i in range(batch)]
+
+
+def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: int, conc: int,
+                bodies_file: str) -> tuple[float, dict]:
+    """Closed-loop load from the native generator; returns (wall seconds, its report)."""
+    import subprocess
+    cmd = [exe, "--path", "/v1.0/invoke/tasksmanager-backend-api/method/api/tasks", "--bodies", bodies_file,
+           "--concurrency", str(conc), "--batch", str(batch), "--steps", str(steps), "--expect", "201",
+           "--until-url", counts_url, "--until-field", "completed"]
+    for s in socks:
+        cmd += ["--target", "unix:" + s]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    dt = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise RuntimeError(f"load generator failed ({p.returncode}): {p.stdout[-500:]} {p.stderr[-500:]}")
+    return dt, json.loads(p.stdout.strip().splitlines()[-1])
+
+
 def main() -> None:
     a = parse()
     d = Dist()
@@ -168,6 +192,7 @@ def main() -> None:
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
+    a.concurrency = a.concurrency or min(256, 32 * a.api_replicas)
     from aca_dotnet_workshop_amd.platform.processes import LocalStack
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
     stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
@@ -183,8 +208,17 @@ def main() -> None:
         socks = [r.sidecar_uds for r in stack.replicas["tasksmanager-backend-api"]]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
         counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
+        if a.client == "native":
+            from aca_dotnet_workshop_amd.native.build import build_loadgen
+            exe = str(build_loadgen())
+            bodies_file = str(stack.root / "bodies.jsonl")
+            with open(bodies_file, "wb") as f:
+                f.write(b"\n".join(_bodies(a.batch)) + b"\n")
         if a.warmup:
-            asyncio.run(run_steps(socks, counts_url, entity, a.warmup, a.batch, a.concurrency, None))
+            if a.client == "native":
+                run_loadgen(exe, socks, counts_url, a.warmup, a.batch, a.concurrency, bodies_file)
+            else:
+                asyncio.run(run_steps(socks, counts_url, entity, a.warmup, a.batch, a.concurrency, None))
         lat: list[float] = []
         d.barrier()
         device_sync()
@@ -192,13 +226,17 @@ def main() -> None:
         me = psutil.Process()
         cpu0 = stack.cpu_seconds()
         t = me.cpu_times()
-        cpu0["bench-client"] = t.user + t.system
-        dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
+        cpu0["bench-client"] = t.user + t.system + t.children_user + t.children_system
+        report = None
+        if a.client == "native":
+            dt, report = run_loadgen(exe, socks, counts_url, a.steps, a.batch, a.concurrency, bodies_file)
+        else:
+            dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
         device_sync()
         d.barrier()
         cpu1 = stack.cpu_seconds()
         t = me.cpu_times()
-        cpu1["bench-client"] = t.user + t.system
+        cpu1["bench-client"] = t.user + t.system + t.children_user + t.children_system
         dt_max = d.max(dt)
         if d.rank == 0:
             # cores busy per process role during the timed region (where the E2E flow is CPU bound)
@@ -207,8 +245,11 @@ def main() -> None:
                               "cpu_budget_per_rank": round(cores, 2)}),
                   file=sys.stderr, flush=True)
         lat.sort()
-        p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
-        p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0
+        if report is not None:
+            p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])
+        else:
+            p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
+            p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         if d.rank == 0:
@@ -221,7 +262,8 @@ def main() -> None:
                            "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
                            "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
-                           "processor_replicas": a.processor_replicas, "create_latency_p50_ms": round(p50, 3),
+                           "processor_replicas": a.processor_replicas, "load_generator": a.client,
+                           "create_latency_p50_ms": round(p50, 3),
                            "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput"}}),
                 flush=True)
     finally:
