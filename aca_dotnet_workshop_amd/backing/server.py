@@ -679,7 +679,8 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         # hot routes on the native front (own thread, GIL-free); Python serves the rest privately
         priv_dir = tempfile.mkdtemp(prefix="ttbf-")
         await srv.listen_unix(os.path.join(priv_dir, "py.sock"))
-        front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"))
+        threads = int(os.environ.get("TT_BACKING_FRONT_THREADS", "2"))
+        front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"), threads)
         svc.attach_front(front)
         bound = front.port()
     else:

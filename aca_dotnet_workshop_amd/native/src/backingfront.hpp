@@ -120,30 +120,32 @@ struct Grant {
 
 class BackingFront {
  public:
-  BackingFront(const std::string& host, int port, const std::string& fallback_uds)
-      : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)), client_(loop_) {
-    handler_ = [this](ev::Message&& m, ev::Reply r) { on_request(std::move(m), std::move(r)); };
+  // `threads` event loops share the port via SO_REUSEPORT (connections are spread by the kernel).
+  BackingFront(const std::string& host, int port, const std::string& fallback_uds, int threads = 1)
+      : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)) {
+    threads = std::max(1, std::min(threads, 64));
+    for (int i = 0; i < threads; ++i) shards_.push_back(std::make_unique<Shard>(*this));
     ev::Endpoint ep;
     ep.unix_socket = false;
     ep.host = host;
     ep.port = port;
-    port_ = ev::listen_on(loop_, ep, handler_);
-    wake_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
-    auto w = std::make_shared<Wake>(this);
-    w->fd = dup(wake_fd_);
-    loop_.add(w, EPOLLIN);
-    thread_ = std::thread([this] { loop_.run([this](double t) { on_tick(t); }); });
+    for (auto& sh : shards_) {
+      int p = ev::listen_on(sh->loop, ep, sh->handler, threads > 1);
+      if (ep.port == 0) ep.port = p;  // the other shards join the port the first one got
+    }
+    port_ = ep.port;
+    for (auto& sh : shards_) sh->start();
   }
   ~BackingFront() { stop(); }
 
   int port() const { return port_; }
+  int threads() const { return (int)shards_.size(); }
 
   void stop() {
-    if (!thread_.joinable()) return;
-    stop_flag_ = true;
-    wake();
-    thread_.join();
-    ::close(wake_fd_);
+    if (stopped_) return;
+    stopped_ = true;
+    for (auto& sh : shards_) sh->request_stop();
+    for (auto& sh : shards_) sh->join();
   }
 
   // -- configuration pushed from Python (any thread) -----------------------------------
@@ -180,11 +182,7 @@ class BackingFront {
   }
   // Python-side broker activity (publish / abandon) for parked native long-polls.
   void notify(const std::string& ns, const std::string& entity) {
-    {
-      std::lock_guard l(notify_mu_);
-      notified_.push_back(ns + "|" + entity);
-    }
-    wake();
+    for (auto& sh : shards_) sh->post(ns + "|" + entity);
   }
   std::map<std::string, uint64_t> stats() {
     std::lock_guard l(notify_mu_);
@@ -197,16 +195,6 @@ class BackingFront {
     bool mirrored = false;
     std::shared_mutex write_mu;
   };
-  struct Wake : ev::IoObj {
-    BackingFront* f;
-    explicit Wake(BackingFront* x) : f(x) {}
-    void on_event(uint32_t) override {
-      uint64_t v;
-      while (::read(fd, &v, sizeof v) == (ssize_t)sizeof v) {
-      }
-      f->on_wake();
-    }
-  };
   struct Parked {
     std::string ns, entity;
     size_t max;
@@ -214,15 +202,88 @@ class BackingFront {
     double deadline;
     ev::Reply reply;
   };
+  struct Shard;
+  struct Wake : ev::IoObj {
+    Shard* sh;
+    explicit Wake(Shard* x) : sh(x) {}
+    void on_event(uint32_t) override;  // defined after Shard
+  };
+  // One event loop + thread; parked long-polls live on the shard that received them.
+  struct Shard {
+    BackingFront& f;
+    ev::Loop loop;
+    ev::Client client;
+    ev::Handler handler;
+    std::thread thread;
+    int wake_fd = -1;
+    std::atomic<bool> stop_flag{false};
+    std::mutex mu;
+    std::vector<std::string> posted;               // cross-thread notifications
+    std::multimap<std::string, Parked> parked;     // "ns|entity" -> waiting receives
 
-  ev::Loop loop_;
+    explicit Shard(BackingFront& front) : f(front), client(loop) {
+      handler = [this](ev::Message&& m, ev::Reply r) { f.on_request(*this, std::move(m), std::move(r)); };
+      wake_fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+      auto w = std::make_shared<Wake>(this);
+      w->fd = dup(wake_fd);
+      loop.add(w, EPOLLIN);
+    }
+    ~Shard() {
+      if (wake_fd >= 0) ::close(wake_fd);
+    }
+    void start() {
+      thread = std::thread([this] { loop.run([this](double t) { on_tick(t); }); });
+    }
+    void wake() {
+      uint64_t one = 1;
+      ssize_t r = ::write(wake_fd, &one, sizeof one);
+      (void)r;
+    }
+    void post(std::string key) {
+      {
+        std::lock_guard l(mu);
+        posted.push_back(std::move(key));
+      }
+      wake();
+    }
+    void request_stop() {
+      stop_flag = true;
+      wake();
+    }
+    void join() {
+      if (thread.joinable()) thread.join();
+    }
+    void on_wake() {
+      if (stop_flag) {
+        for (auto& kv : parked) kv.second.reply.json(503, bf::problem_json(503, "shutting down"));
+        parked.clear();
+        loop.stop();
+        return;
+      }
+      std::vector<std::string> keys;
+      {
+        std::lock_guard l(mu);
+        keys.swap(posted);
+      }
+      for (auto& k : keys) f.retry_parked(*this, k);
+    }
+    void on_tick(double now) {
+      if (stop_flag) {
+        on_wake();
+        return;
+      }
+      // deadlines + periodic re-check (delayed / scheduled messages, expired locks)
+      std::vector<std::string> keys;
+      for (auto& kv : parked)
+        if (keys.empty() || keys.back() != kv.first) keys.push_back(kv.first);
+      for (auto& k : keys) f.retry_parked(*this, k, now);
+    }
+  };
+
   ev::Endpoint fallback_;
-  ev::Client client_;
-  ev::Handler handler_;
+  std::vector<std::unique_ptr<Shard>> shards_;
   int port_ = 0;
-  int wake_fd_ = -1;
-  std::thread thread_;
-  std::atomic<bool> stop_flag_{false};
+  bool stopped_ = false;
 
   std::shared_mutex cfg_mu_;
   std::unordered_map<std::string, std::unique_ptr<Coll>> colls_;
@@ -232,44 +293,18 @@ class BackingFront {
   std::vector<bf::Grant> grants_;
 
   std::mutex notify_mu_;
-  std::vector<std::string> notified_;
   std::map<std::string, uint64_t> stats_;
-  std::multimap<std::string, Parked> parked_;  // "ns|entity" -> waiting receives (loop thread only)
 
-  void wake() {
-    uint64_t one = 1;
-    ssize_t r = ::write(wake_fd_, &one, sizeof one);
-    (void)r;
-  }
   void count(const char* k) {
     std::lock_guard l(notify_mu_);
     stats_[k]++;
   }
-
-  void on_wake() {
-    if (stop_flag_) {
-      for (auto& kv : parked_) kv.second.reply.json(503, bf::problem_json(503, "shutting down"));
-      parked_.clear();
-      loop_.stop();
-      return;
-    }
-    std::vector<std::string> keys;
-    {
-      std::lock_guard l(notify_mu_);
-      keys.swap(notified_);
-    }
-    for (auto& k : keys) retry_parked(k);
-  }
-  void on_tick(double now) {
-    if (stop_flag_) {
-      on_wake();
-      return;
-    }
-    // deadlines + periodic re-check (delayed / scheduled messages, expired locks)
-    std::vector<std::string> keys;
-    for (auto& kv : parked_)
-      if (keys.empty() || keys.back() != kv.first) keys.push_back(kv.first);
-    for (auto& k : keys) retry_parked(k, now);
+  // A broker event on one shard wakes parked receives on every shard.
+  void broadcast(Shard& here, const std::string& key) {
+    retry_parked(here, key);
+    if (shards_.size() > 1)
+      for (auto& sh : shards_)
+        if (sh.get() != &here) sh->post(key);
   }
 
   // -- auth: backing/auth.py AccessPolicy.check ----------------------------------------
@@ -318,7 +353,7 @@ class BackingFront {
     return "";
   }
 
-  void on_request(ev::Message&& m, ev::Reply r) {
+  void on_request(Shard& sh, ev::Message&& m, ev::Reply r) {
     std::string path, qs;
     split(m.target, path, qs);
     std::vector<std::string> seg;
@@ -329,16 +364,16 @@ class BackingFront {
       i = j + 1;
     }
     if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(m, r, seg)) return;
-    if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(m, r, seg, qs)) return;
-    forward(std::move(m), std::move(r));
+    if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
+    forward(sh, std::move(m), std::move(r));
   }
 
-  void forward(ev::Message&& m, ev::Reply r) {
+  void forward(Shard& sh, ev::Message&& m, ev::Reply r) {
     count("forwarded");
     ev::HeaderList h;
     for (auto& kv : m.headers)
       if (!ev::is_hop_header(kv.first)) h.push_back(kv);
-    client_.request(fallback_, m.method, m.target, h, m.body, 0, [r](ev::ClientResult&& res) {
+    sh.client.request(fallback_, m.method, m.target, h, m.body, 0, [r](ev::ClientResult&& res) {
       if (res.err) {
         r.send(503, {{"content-type", "application/problem+json; charset=utf-8"}},
                bf::problem_json(503, "backing control plane unreachable"));
@@ -407,7 +442,8 @@ class BackingFront {
     return "queues/" + entity;
   }
 
-  bool handle_bus(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
+  bool handle_bus(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg,
+                  const std::string& qs) {
     Broker* b = nullptr;
     {
       std::shared_lock l(cfg_mu_);
@@ -428,7 +464,7 @@ class BackingFront {
                                 ttl && !ttl->empty() ? std::atoll(ttl->c_str()) : 0,
                                 delay && !delay->empty() ? std::atoll(delay->c_str()) : 0);
       r.send(201, {{"content-type", "application/json"}}, "{\"seq\": " + std::to_string(seq) + "}");
-      for (auto& sub : b->subscriptions(seg[3])) retry_parked(ns + "|" + seg[3] + "/subscriptions/" + sub);
+      for (auto& sub : b->subscriptions(seg[3])) broadcast(sh, ns + "|" + seg[3] + "/subscriptions/" + sub);
       return true;
     }
     if (seg.size() == 3 && seg[2] == "receive" && m.method == "POST") {
@@ -439,7 +475,7 @@ class BackingFront {
       Parked p{ns, entity, (size_t)std::max(1, mx.empty() ? 1 : std::atoi(mx.c_str())),
                lk.empty() ? 0 : std::atoll(lk.c_str()), ev::now_s() + (wt.empty() ? 0 : std::atoi(wt.c_str())) / 1000.0,
                r};
-      if (!try_receive(b, p, false)) parked_.emplace(ns + "|" + entity, std::move(p));
+      if (!try_receive(b, p, false)) sh.parked.emplace(ns + "|" + entity, std::move(p));
       return true;
     }
     if (seg.size() == 3 && seg[2] == "settle" && m.method == "POST") {
@@ -488,7 +524,7 @@ class BackingFront {
                  (b->renew(entity, str((*l)[i], "token"), num((*l)[i], "lockMs")) ? "true" : "false");
       out += "]}";
       r.send(200, {{"content-type", "application/json"}}, out);
-      if (abandoned) retry_parked(ns + "|" + entity);
+      if (abandoned) broadcast(sh, ns + "|" + entity);
       return true;
     }
     if (seg.size() == 3 && seg[2] == "counts" && m.method == "GET") {
@@ -529,8 +565,8 @@ class BackingFront {
     return true;
   }
 
-  void retry_parked(const std::string& key, double now = 0) {
-    auto range = parked_.equal_range(key);
+  void retry_parked(Shard& sh, const std::string& key, double now = 0) {
+    auto range = sh.parked.equal_range(key);
     if (range.first == range.second) return;
     Broker* b = nullptr;
     {
@@ -540,10 +576,17 @@ class BackingFront {
     }
     for (auto it = range.first; it != range.second;) {
       bool expired = now > 0 && now >= it->second.deadline;
-      if (b && try_receive(b, it->second, expired)) it = parked_.erase(it);
+      if (b && try_receive(b, it->second, expired)) it = sh.parked.erase(it);
       else ++it;
     }
   }
 };
+
+inline void BackingFront::Wake::on_event(uint32_t) {
+  uint64_t v;
+  while (::read(fd, &v, sizeof v) == (ssize_t)sizeof v) {
+  }
+  sh->on_wake();
+}
 
 }  // namespace tt

@@ -578,7 +578,9 @@ class Listener : public IoObj {
 };
 
 // Returns the bound port (tcp) or 0 (unix); throws on failure.
-inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h) {
+// `reuseport`: several loops (threads) bind the same TCP port and the kernel spreads
+// incoming connections over them.
+inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false) {
   int fd;
   int port = 0;
   if (ep.unix_socket) {
@@ -593,6 +595,7 @@ inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h) {
     fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     int one = 1;
     setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    if (reuseport) setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
     sockaddr_in a{};
     a.sin_family = AF_INET;
     a.sin_port = htons((uint16_t)ep.port);

@@ -182,9 +182,10 @@ PYBIND11_MODULE(_ttnative, m) {
   // document / message routes on its own thread against the engines attached here and
   // forwards everything else to the Python server on `fallback_uds`.
   py::class_<BackingFront>(m, "BackingFront")
-      .def(py::init<const std::string&, int, const std::string&>(), py::arg("host"), py::arg("port"),
-           py::arg("fallback_uds"))
+      .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
+           py::arg("fallback_uds"), py::arg("threads") = 1)
       .def("port", &BackingFront::port)
+      .def("threads", &BackingFront::threads)
       .def("attach_store",
            [](BackingFront& f, const std::string& a, const std::string& d, const std::string& c, DocStore& s) {
              f.attach_store(a, d, c, &s);

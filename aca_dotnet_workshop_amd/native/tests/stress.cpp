@@ -164,7 +164,7 @@ int main(int argc, char** argv) {
     Broker broker;
     QueueOptions o;
     broker.create_subscription("t", "s", o);
-    BackingFront front("127.0.0.1", 0, "/nonexistent/fallback.sock");
+    BackingFront front("127.0.0.1", 0, "/nonexistent/fallback.sock", 3);
     front.attach_store("a", "d", "c", &store);
     front.attach_broker("ns", &broker);
     int port = front.port();

@@ -38,7 +38,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024, help="createTask requests per step per rank")
     ap.add_argument("--concurrency", type=int, default=0,
-                    help="requests in flight per rank (0 = 32 per API replica, at most 256)")
+                    help="requests in flight per rank (0 = 48 per API replica, at most 384)")
     ap.add_argument("--api-replicas", type=int, default=0,
                     help="API replicas behind the client's load balancing (0 = size to this rank's CPU share)")
     ap.add_argument("--processor-replicas", type=int, default=0,
@@ -110,8 +110,8 @@ def topology(cores: float) -> tuple[int, int]:
     """Replica counts for one rank's environment.  Per-task CPU measured on the stack
     (docs/PERFORMANCE.md): the Python API app is the costliest hop, then the processor app;
     sidecar data planes and the backing front are native and cheap."""
-    api = max(1, min(6, int(cores // 3)))
-    proc = max(1, min(4, int(cores // 5)))
+    api = max(1, min(8, int(cores / 2.6)))
+    proc = max(1, min(5, int(cores // 5)))
     return max(api, 2 if cores >= 6 else 1), max(proc, 2 if cores >= 6 else 1)
 
 
@@ -192,7 +192,7 @@ def main() -> None:
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
-    a.concurrency = a.concurrency or min(256, 32 * a.api_replicas)
+    a.concurrency = a.concurrency or min(384, 48 * a.api_replicas)
     from aca_dotnet_workshop_amd.platform.processes import LocalStack
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
     stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
