@@ -11,6 +11,8 @@ next to this file so the driver's gpurun snapshot carries them to the GPU box.
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import os
 import subprocess
 import sys
@@ -26,6 +28,20 @@ def ext_path(name: str) -> Path:
     return HERE / f"{name}{suffix}"
 
 
+@contextlib.contextmanager
+def build_lock(name: str):
+    """Serialise concurrent builders (e.g. 8 bench ranks x N sidecars starting at once on a fresh
+    checkout): one compiles, the others wait and then find the target fresh."""
+    lock_dir = HERE / "bin"
+    lock_dir.mkdir(exist_ok=True)
+    with open(lock_dir / f".{name}.lock", "w") as fh:
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(fh, fcntl.LOCK_UN)
+
+
 def _stale(target: Path, sources: list[Path]) -> bool:
     if not target.exists():
         return True
@@ -34,12 +50,18 @@ def _stale(target: Path, sources: list[Path]) -> bool:
 
 
 def build_native(force: bool = False, verbose: bool = False) -> Path:
-    import pybind11
-
     target = ext_path("_ttnative")
     sources = sorted(SRC.glob("*.hpp")) + [SRC / "module.cpp"]
     if not force and not _stale(target, sources):
         return target
+    with build_lock("ttnative"):
+        if force or _stale(target, sources):
+            _compile_native(target, verbose)
+    return target
+
+
+def _compile_native(target: Path, verbose: bool) -> None:
+    import pybind11
     cxx = os.environ.get("CXX", "g++")
     tmp = target.with_suffix(f".tmp{os.getpid()}.so")
     cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
@@ -49,7 +71,6 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, target)
-    return target
 
 
 DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
@@ -57,17 +78,23 @@ DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
 
 def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
     sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
-    if not force and not _stale(DATAPLANE, sources):
-        return DATAPLANE
-    DATAPLANE.parent.mkdir(exist_ok=True)
-    cxx = os.environ.get("CXX", "g++")
-    tmp = DATAPLANE.with_name(f".{DATAPLANE.name}.tmp{os.getpid()}")
-    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(SRC / "dataplane.cpp"), "-o", str(tmp)]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, DATAPLANE)
-    return DATAPLANE
+    return _build_exe(DATAPLANE, SRC / "dataplane.cpp", sources, force, verbose)
+
+
+def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbose: bool) -> Path:
+    if not force and not _stale(target, sources):
+        return target
+    with build_lock(target.name):
+        if not force and not _stale(target, sources):
+            return target
+        cxx = os.environ.get("CXX", "g++")
+        tmp = target.with_name(f".{target.name}.tmp{os.getpid()}")
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(main), "-o", str(tmp)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, target)
+    return target
 
 
 LOADGEN = HERE / "bin" / "ttloadgen"
@@ -76,17 +103,7 @@ LOADGEN = HERE / "bin" / "ttloadgen"
 def build_loadgen(force: bool = False, verbose: bool = False) -> Path:
     """Closed-loop HTTP load generator used by bench.py (src/loadgen.cpp)."""
     sources = [SRC / "loadgen.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
-    if not force and not _stale(LOADGEN, sources):
-        return LOADGEN
-    LOADGEN.parent.mkdir(exist_ok=True)
-    cxx = os.environ.get("CXX", "g++")
-    tmp = LOADGEN.with_name(f".{LOADGEN.name}.tmp{os.getpid()}")
-    cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(SRC / "loadgen.cpp"), "-o", str(tmp)]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LOADGEN)
-    return LOADGEN
+    return _build_exe(LOADGEN, SRC / "loadgen.cpp", sources, force, verbose)
 
 
 if __name__ == "__main__":

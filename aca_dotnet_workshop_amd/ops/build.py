@@ -40,6 +40,14 @@ def stale() -> bool:
 def build_gpu(force: bool = False, verbose: bool = False) -> Path:
     if not force and not stale():
         return LIB
+    from ..native.build import build_lock
+    with build_lock("ttgpu"):
+        if force or stale():
+            _compile(verbose)
+    return LIB
+
+
+def _compile(verbose: bool) -> None:
     tmp = LIB.with_suffix(f".tmp{os.getpid()}.so")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
            *map(str, sources()), "-o", str(tmp)]
@@ -47,7 +55,6 @@ def build_gpu(force: bool = False, verbose: bool = False) -> Path:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
-    return LIB
 
 
 if __name__ == "__main__":

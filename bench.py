@@ -193,7 +193,10 @@ def main() -> None:
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
     a.concurrency = a.concurrency or min(384, 48 * a.api_replicas)
+    from aca_dotnet_workshop_amd.native.build import build_dataplane, build_loadgen, build_native
     from aca_dotnet_workshop_amd.platform.processes import LocalStack
+    for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
+        b()
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
     stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
     try:
