@@ -417,7 +417,9 @@ class ColumnarIndex:
             cols = [torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
                     for i, w in enumerate(widths)]
             live = torch.from_numpy(self._live_words(0, nwords)).to(dev)
-            st = self._dev = {"cols": cols, "widths": widths, "live": live, "synced": self.n, "cap": self.cap}
+            seq = torch.from_numpy(np.ascontiguousarray(self.seq[:self.cap])).to(dev)
+            st = self._dev = {"cols": cols, "widths": widths, "live": live, "synced": self.n, "cap": self.cap,
+                              "seq": seq}
         else:
             lo, hi = st["synced"], self.n
             for i, w in enumerate(widths):
@@ -426,6 +428,8 @@ class ColumnarIndex:
                     st["widths"][i] = w
                 elif hi > lo:
                     st["cols"][i][lo:hi].copy_(torch.from_numpy(self._narrow(i, lo, hi, w)))
+            if hi > lo:
+                st["seq"][lo:hi].copy_(torch.from_numpy(self.seq[lo:hi]))
             if self._tomb_dirty:
                 st["live"].copy_(torch.from_numpy(self._live_words(0, nwords)))
             elif hi > lo:
@@ -438,7 +442,7 @@ class ColumnarIndex:
         st["table"] = torch.from_numpy(table).to(dev)
         return st
 
-    def select_gpu(self, prog: Program, kernels, return_mask: bool = False):
+    def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
         torch = kernels.torch
         leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ)
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
@@ -447,7 +451,7 @@ class ColumnarIndex:
         code = torch.from_numpy(prog.code).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
         res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
-        if return_mask:
+        if return_mask or on_device:
             return res
         return res.cpu().numpy()
 
@@ -473,6 +477,15 @@ class ColumnarIndex:
     def order(self, rows: np.ndarray, sort: list[dict[str, Any]] | None) -> np.ndarray:
         if rows.size == 0:
             return rows
+        plan = self.sort_specs(sort)
+        if plan is not None:  # one argsort of packed keys (same keys the GPU path sorts)
+            return rows[np.argsort(self.sort_keys_numpy(rows, plan), kind="stable")]
+        return self.order_lexsort(rows, sort)
+
+    def order_lexsort(self, rows: np.ndarray, sort: list[dict[str, Any]] | None) -> np.ndarray:
+        """Reference ordering: insertion order, then a stable lexsort on the sort keys' ranks."""
+        if rows.size == 0:
+            return rows
         rows = rows[np.argsort(self.seq[rows], kind="stable")]  # insertion order, then stable sort keys
         if not sort:
             return rows
@@ -488,14 +501,78 @@ class ColumnarIndex:
             keys.append(r)
         return rows[np.lexsort(keys)]
 
+    def sort_specs(self, sort: list[dict[str, Any]] | None) -> tuple[np.ndarray, np.ndarray, int] | None:
+        """Device ordering plan: (specs int32 [nkeys, 8], concatenated rank tables, seq bits), or
+        None when the packed key would not fit 63 bits (the host path orders instead)."""
+        seq_bits = max(1, int(self.seq[:self.n].max(initial=0)).bit_length())
+        specs, tables, off, total = [], [], 0, seq_bits
+        for s in sort or []:
+            col = self.add_column(s["key"])
+            c = self.columns[col]
+            ranks = c.ranks().astype(np.int32) if c.values else np.zeros(0, dtype=np.int32)
+            miss = c.missing_rank()
+            max_rank = int(max(int(ranks.max(initial=0)), miss))
+            bits = max(1, max_rank.bit_length())
+            total += bits
+            desc = 1 if str(s.get("order", "ASC")).upper() == "DESC" else 0
+            specs.append([col, off, ranks.size, bits, desc, miss, max_rank, 0])
+            tables.append(ranks)
+            off += ranks.size
+        if total > 63:
+            return None
+        spec_arr = np.array(specs, dtype=np.int32).reshape(-1, 8)
+        rank_arr = np.concatenate(tables) if tables else np.zeros(1, dtype=np.int32)
+        return spec_arr, (rank_arr if rank_arr.size else np.zeros(1, dtype=np.int32)), seq_bits
+
+    def sort_keys_numpy(self, rows: np.ndarray, plan) -> np.ndarray:
+        """Host reference of ``hip/sort_keys.hip``: the packed ordering key of every row."""
+        specs, ranks, seq_bits = plan
+        k = np.zeros(rows.size, dtype=np.int64)
+        for col, off, nranks, bits, desc, miss, max_rank, _ in specs.tolist():
+            ids = self.ids[col, rows]
+            ok = (ids >= 0) & (ids < nranks)
+            r = np.full(rows.size, miss, dtype=np.int64)
+            r[ok] = ranks[off + ids[ok]]
+            if desc:
+                r = max_rank - r
+            k = (k << bits) | r
+        return (k << seq_bits) | self.seq[rows]
+
+    def order_gpu(self, rows, sort, kernels, k: int | None = None):
+        """Order a device selection on the GPU (``hip/sort_keys.hip`` + radix sort / top-k);
+        returns device rows, or None when the host path must order."""
+        plan = self.sort_specs(sort)
+        if plan is None or len(sort or []) > kernels.max_sort_keys:
+            return None
+        specs, ranks, seq_bits = plan
+        torch = kernels.torch
+        st = self.to_device(kernels)  # sort keys may have added columns
+        return kernels.order(st["table"], rows, torch.from_numpy(specs).to(kernels.device),
+                             torch.from_numpy(ranks).to(kernels.device), st["seq"], seq_bits, k)
+
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""
+        sort = q.get("sort")
+        for s in sort or []:
+            self.add_column(s["key"])  # before the device sync, so one upload covers filter + sort
         prog = self.compile(q.get("filter") or {})
-        rows = self.select_gpu(prog, kernels) if kernels is not None else self.select_numpy(prog)
-        rows = self.order(rows, q.get("sort"))
         page = q.get("page") or {}
         limit = int(page.get("limit") or 0)
         offset = int(page.get("token") or 0)
+        rows = None
+        if kernels is not None:
+            dev_rows = self.select_gpu(prog, kernels, on_device=True)
+            total = int(dev_rows.numel())
+            ordered = self.order_gpu(dev_rows, sort, kernels, offset + limit if limit else None)
+            if ordered is not None:
+                end = min(total, offset + limit) if limit else total
+                sel = ordered[offset:end].cpu().numpy()
+                token = str(end) if limit and end < total else None
+                return [self.keys[i] for i in sel.tolist()], token
+            rows = dev_rows.cpu().numpy()
+        if rows is None:
+            rows = self.select_numpy(prog)
+        rows = self.order(rows, sort)
         end = min(rows.size, offset + limit) if limit else rows.size
         sel = rows[offset:end]
         token = str(end) if limit and end < rows.size else None

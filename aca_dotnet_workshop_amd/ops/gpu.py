@@ -29,6 +29,9 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
+    lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P]
+    lib.tt_launch_sort_keys.restype = ctypes.c_int
+    lib.tt_sort_max_keys.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -45,6 +48,7 @@ class GpuKernels:
         self.device = torch.device(device or "cuda")
         self.tile_rows = int(self.lib.tt_tile_rows())
         self.max_depth = int(self.lib.tt_max_depth())
+        self.max_sort_keys = int(self.lib.tt_sort_max_keys())
 
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -95,3 +99,35 @@ class GpuKernels:
         if rc != 0:
             raise RuntimeError(f"tt_group_count launch failed ({rc})")
         return counts[:ngroups]
+
+    def sort_keys(self, table, rows, specs, ranks, seq, seq_bits: int):
+        """Packed 63-bit ordering keys (int64) for ``rows`` (int32, device): see
+        ``hip/sort_keys.hip``.  ``specs``: int32 [nkeys, 8] device tensor; ``ranks``: int32
+        rank tables (concatenated); ``seq``: int64 insertion sequence per row."""
+        torch = self.torch
+        n = rows.numel()
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        if specs.shape[0] > self.max_sort_keys:
+            raise ValueError("too many sort keys for the device path")
+        rc = self.lib.tt_launch_sort_keys(table.data_ptr(), rows.data_ptr(), n, specs.data_ptr(), specs.shape[0],
+                                          ranks.data_ptr(), ranks.numel(), seq.data_ptr(), seq_bits, keys.data_ptr(),
+                                          self._stream())
+        if rc != 0:
+            raise RuntimeError(f"tt_sort_keys launch failed ({rc})")
+        return keys[:n]
+
+    def order(self, table, rows, specs, ranks, seq, seq_bits: int, k: int | None = None):
+        """Rows in result order (device int32); only the first ``k`` when given (top-k)."""
+        torch = self.torch
+        n = rows.numel()
+        if n == 0:
+            return rows
+        keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits)
+        if k is not None and k < n and k <= 65536:
+            _, idx = torch.topk(keys, k, largest=False, sorted=True)
+        else:
+            _, idx = torch.sort(keys)
+            if k is not None:
+                idx = idx[:k]
+        return rows[idx]
+

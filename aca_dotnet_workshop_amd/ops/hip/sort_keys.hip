@@ -1,0 +1,103 @@
+// Ordering keys for state-store query results (gfx950).
+//
+// The query API orders results by up to a few document paths (ASC/DESC) with ties broken by
+// insertion order (backing/accel.py, ops/columnar.py ColumnarIndex.order -- the native
+// engine's semantics).  For a selection produced by tt_scan_compact this kernel packs, per
+// selected row, one 63-bit unsigned key
+//
+//     [rank(key0) | rank(key1) | ... | seq]          (most significant first)
+//
+// where rank(k) is the value's position in the column dictionary's sort order (missing paths
+// rank like null; DESC keys store max_rank - rank), and seq is the document's insertion
+// sequence.  Sorting the keys (radix sort / top-k) then yields exactly the host ordering.
+// Rank lookups go through a small per-key rank table (dictionary id -> rank) staged in LDS
+// when it fits (it is gathered once per row and per key, so LDS keeps those random reads
+// off HBM).
+//
+// Layout: one thread per selected row, 256-thread blocks; rows are ascending row ids, so the
+// id / seq gathers of neighbouring lanes hit neighbouring addresses.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxKeys = 4;
+constexpr int kLdsRankWords = 8192;  // 32 KiB of rank tables in LDS (all keys together)
+
+struct SortColumn {   // 16 bytes, same layout as the scan kernel's ColumnDesc
+  uint64_t ptr;
+  int32_t width;
+  int32_t pad;
+};
+
+struct SortSpec {     // host-built, one per sort key (primary first)
+  int32_t col;        // column index into the column table
+  int32_t rank_off;   // offset of this key's rank table in `ranks`
+  int32_t nranks;     // entries in this key's rank table (dictionary size)
+  int32_t bits;       // key field width
+  int32_t desc;       // 1 = descending
+  int32_t missing;    // rank of a missing path
+  int32_t max_rank;   // for DESC: stored value = max_rank - rank
+  int32_t pad;
+};
+
+__device__ __forceinline__ int32_t load_id(const SortColumn& c, int64_t row) {
+  if (c.width == 1) {
+    const uint32_t v = reinterpret_cast<const uint8_t*>(c.ptr)[row];
+    return v == 0xFFu ? -1 : (int32_t)v;
+  }
+  if (c.width == 2) {
+    const uint32_t v = reinterpret_cast<const uint16_t*>(c.ptr)[row];
+    return v == 0xFFFFu ? -1 : (int32_t)v;
+  }
+  return reinterpret_cast<const int32_t*>(c.ptr)[row];
+}
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kBlock)
+tt_sort_keys(const SortColumn* __restrict__ cols, const int32_t* __restrict__ rows, int64_t n,
+             const SortSpec* __restrict__ specs, int32_t nkeys, const int32_t* __restrict__ ranks,
+             int32_t rank_words, const int64_t* __restrict__ seq, int32_t seq_bits, uint64_t* __restrict__ keys) {
+  __shared__ int32_t lds_ranks[kLdsRankWords];
+  __shared__ SortSpec lds_specs[kMaxKeys];
+  __shared__ SortColumn lds_cols[kMaxKeys];
+  const bool staged = rank_words <= kLdsRankWords;
+  if (staged)
+    for (int i = threadIdx.x; i < rank_words; i += kBlock) lds_ranks[i] = ranks[i];
+  if (threadIdx.x < nkeys) {
+    lds_specs[threadIdx.x] = specs[threadIdx.x];
+    lds_cols[threadIdx.x] = cols[specs[threadIdx.x].col];
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = rows[i];
+  uint64_t k = 0;
+  for (int j = 0; j < nkeys; ++j) {
+    const SortSpec s = lds_specs[j];
+    const int32_t id = load_id(lds_cols[j], row);
+    int32_t r = s.missing;
+    if (id >= 0 && id < s.nranks) r = staged ? lds_ranks[s.rank_off + id] : ranks[s.rank_off + id];
+    if (s.desc) r = s.max_rank - r;
+    k = (k << s.bits) | (uint64_t)(uint32_t)r;
+  }
+  k = (k << seq_bits) | (uint64_t)seq[row];
+  keys[i] = k;
+}
+
+extern "C" int tt_launch_sort_keys(const void* cols, const int32_t* rows, int64_t n, const void* specs, int32_t nkeys,
+                                   const int32_t* ranks, int32_t rank_words, const int64_t* seq, int32_t seq_bits,
+                                   uint64_t* keys, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (nkeys < 0 || nkeys > kMaxKeys || seq_bits < 0 || seq_bits > 63) return -1;
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(tt_sort_keys, dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const SortColumn*>(cols), rows, n, reinterpret_cast<const SortSpec*>(specs), nkeys,
+                     ranks, rank_words, seq, seq_bits, keys);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int tt_sort_max_keys() { return kMaxKeys; }

@@ -88,6 +88,24 @@ def test_numpy_executor_matches_native(docs, flt, sort, seed):
         assert got == want
 
 
+@settings(max_examples=150, deadline=None)
+@given(docs_st, sort_st, st.integers(0, 1000))
+def test_packed_sort_keys_match_lexsort(docs, sort, seed):
+    """The packed 63-bit keys (what hip/sort_keys.hip computes) order rows exactly like the
+    reference lexsort path."""
+    if not docs:
+        return
+    ix = _columnar(_ops(docs, random.Random(seed)))
+    rows = ix.select_numpy(ix.compile({}))
+    if sort:
+        for s in sort:
+            ix.add_column(s["key"])
+    plan = ix.sort_specs(sort)
+    assert plan is not None
+    got = rows[np.argsort(ix.sort_keys_numpy(rows, plan), kind="stable")]
+    assert got.tolist() == ix.order_lexsort(rows, sort).tolist()
+
+
 def test_paging_and_compaction():
     ix = ColumnarIndex()
     for i in range(10000):
@@ -180,6 +198,22 @@ def test_gpu_query_matches_native_engine():
         want = [r["key"] for r in json.loads(s.query(json.dumps(q)))["results"]]
         got, _ = ix.query(q, k)
         assert got == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [3, 5000, 120_001])
+def test_gpu_ordering_matches_host(n):
+    """Device ordering (tt_sort_keys + radix sort / top-k) == host ordering, with paging."""
+    k = _kernels()
+    ix = _random_collection(n, random.Random(n + 1))
+    for sort in (None, [{"key": "taskDueDate", "order": "DESC"}],
+                 [{"key": "taskCreatedBy", "order": "ASC"}, {"key": "prio", "order": "DESC"}],
+                 [{"key": "isCompleted"}, {"key": "missing.path", "order": "DESC"}]):
+        for page in ({}, {"limit": 7}, {"limit": 50, "token": "10"}):
+            q = {"filter": {"NEQ": {"taskCreatedBy": "user5@x"}}, "sort": sort, "page": page}
+            if sort is None:
+                del q["sort"]
+            assert ix.query(q, k) == ix.query(q), (n, sort, page)
 
 
 @pytest.mark.gpu
