@@ -504,7 +504,7 @@ class ColumnarIndex:
     def sort_specs(self, sort: list[dict[str, Any]] | None) -> tuple[np.ndarray, np.ndarray, int] | None:
         """Device ordering plan: (specs int32 [nkeys, 8], concatenated rank tables, seq bits), or
         None when the packed key would not fit 63 bits (the host path orders instead)."""
-        seq_bits = max(1, int(self.seq[:self.n].max(initial=0)).bit_length())
+        seq_bits = max(1, int(self._next_seq).bit_length())  # every seq is <= the last one handed out
         specs, tables, off, total = [], [], 0, seq_bits
         for s in sort or []:
             col = self.add_column(s["key"])

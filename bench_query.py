@@ -59,6 +59,7 @@ def main() -> None:
         ix.ids[i, :n] = c
     ix.live[:n] = 1
     ix.seq[:n] = np.arange(1, n + 1)
+    ix._next_seq = n
     ix.n = n
     ix.keys = []  # not needed for the scan benchmark
     ix.version += 1
