@@ -547,8 +547,9 @@ class ColumnarIndex:
         specs, ranks, seq_bits = plan
         torch = kernels.torch
         st = self.to_device(kernels)  # sort keys may have added columns
+        key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
         return kernels.order(st["table"], rows, torch.from_numpy(specs).to(kernels.device),
-                             torch.from_numpy(ranks).to(kernels.device), st["seq"], seq_bits, k)
+                             torch.from_numpy(ranks).to(kernels.device), st["seq"], seq_bits, k, key_bits)
 
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""

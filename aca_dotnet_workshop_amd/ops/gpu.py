@@ -32,6 +32,11 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P]
     lib.tt_launch_sort_keys.restype = ctypes.c_int
     lib.tt_sort_max_keys.restype = ctypes.c_int
+    lib.tt_launch_key_histogram.argtypes = [P, I64, I32, P, P]
+    lib.tt_launch_key_histogram.restype = ctypes.c_int
+    lib.tt_launch_select_le_bin.argtypes = [P, P, I64, I32, ctypes.c_uint32, P, P, P, ctypes.c_uint32, P]
+    lib.tt_launch_select_le_bin.restype = ctypes.c_int
+    lib.tt_hist_bins.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -116,18 +121,45 @@ class GpuKernels:
             raise RuntimeError(f"tt_sort_keys launch failed ({rc})")
         return keys[:n]
 
-    def order(self, table, rows, specs, ranks, seq, seq_bits: int, k: int | None = None):
-        """Rows in result order (device int32); only the first ``k`` when given (top-k)."""
+    def order(self, table, rows, specs, ranks, seq, seq_bits: int, k: int | None = None, key_bits: int = 63):
+        """Rows in result order (device int32); only the first ``k`` when given (top-k by
+        radix select: histogram of the top 12 used key bits, compaction of the candidates at or
+        below the k-th key's bin, sort of the candidates only)."""
         torch = self.torch
         n = rows.numel()
         if n == 0:
             return rows
         keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits)
-        if k is not None and k < n and k <= 65536:
-            _, idx = torch.topk(keys, k, largest=False, sorted=True)
-        else:
-            _, idx = torch.sort(keys)
-            if k is not None:
-                idx = idx[:k]
+        if k is not None and k < n and n > 65536:
+            top = self._top_k(keys, rows, k, key_bits)
+            if top is not None:
+                return top
+        _, idx = torch.sort(keys)
+        if k is not None:
+            idx = idx[:k]
         return rows[idx]
+
+    def _top_k(self, keys, rows, k: int, key_bits: int):
+        import numpy as np
+        torch = self.torch
+        n = keys.numel()
+        bins = int(self.lib.tt_hist_bins())
+        shift = max(0, key_bits - (bins.bit_length() - 1))
+        hist = torch.zeros(bins, dtype=torch.int32, device=self.device)
+        if self.lib.tt_launch_key_histogram(keys.data_ptr(), n, shift, hist.data_ptr(), self._stream()) != 0:
+            raise RuntimeError("tt_key_histogram launch failed")
+        cum = np.cumsum(hist.cpu().numpy().astype(np.int64))
+        last = int(np.searchsorted(cum, k))  # first bin where the running count reaches k
+        cand = int(cum[last])
+        if cand > max(8 * k, 1 << 21):
+            return None  # keys too concentrated in one bin: a full sort is cheaper than refining
+        out_keys = torch.empty(cand, dtype=torch.int64, device=self.device)
+        out_rows = torch.empty(cand, dtype=torch.int32, device=self.device)
+        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        rc = self.lib.tt_launch_select_le_bin(keys.data_ptr(), rows.data_ptr(), n, shift, last, out_keys.data_ptr(),
+                                              out_rows.data_ptr(), counter.data_ptr(), cand, self._stream())
+        if rc != 0:
+            raise RuntimeError("tt_select_le_bin launch failed")
+        _, idx = torch.sort(out_keys)
+        return out_rows[idx[:k]]
 

@@ -101,3 +101,103 @@ extern "C" int tt_launch_sort_keys(const void* cols, const int32_t* rows, int64_
 }
 
 extern "C" int tt_sort_max_keys() { return kMaxKeys; }
+
+// ---------------------------------------------------------------------------------------
+// Top-k by radix select: a paged, ordered query needs only the first `k` keys of the
+// selection, so instead of sorting all of them (radix sort of tens of millions of 64-bit
+// keys) we (1) histogram the 12 most significant *used* key bits, (2) find on the host the
+// bin where the running count reaches k, (3) compact the (key, row) pairs at or below that bin
+// and (4) sort only those candidates.
+namespace {
+constexpr int kHistBins = 4096;     // 12 bits
+constexpr int kSelItems = 16;       // keys per thread per block-iteration
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kBlock)
+tt_key_histogram(const uint64_t* __restrict__ keys, int64_t n, int32_t shift, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kHistBins];
+  for (int i = threadIdx.x; i < kHistBins; i += kBlock) h[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    atomicAdd(&h[(uint32_t)(keys[i] >> shift) & (kHistBins - 1)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kHistBins; i += kBlock)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// Keep pairs whose bin <= `last_bin`; one global atomic per block reserves the block's range.
+extern "C" __global__ void __launch_bounds__(kBlock)
+tt_select_le_bin(const uint64_t* __restrict__ keys, const int32_t* __restrict__ rows, int64_t n, int32_t shift,
+                 uint32_t last_bin, uint64_t* __restrict__ out_keys, int32_t* __restrict__ out_rows,
+                 uint32_t* __restrict__ counter, uint32_t capacity) {
+  __shared__ uint32_t warp_counts[kBlock / 64];
+  __shared__ uint32_t block_base;
+  const int64_t base = (int64_t)blockIdx.x * kBlock * kSelItems;
+  // pass 1: count this thread's matches (no dynamically indexed register arrays -> no scratch)
+  uint32_t matchbits = 0, cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kSelItems; ++j) {
+    const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;  // coalesced across the block
+    if (i < n && ((uint32_t)(keys[i] >> shift) & (kHistBins - 1)) <= last_bin) {
+      matchbits |= 1u << j;
+      ++cnt;
+    }
+  }
+  // block-wide exclusive scan of per-thread counts (wave prefix via shuffles, then wave sums)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) warp_counts[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) {
+      const uint32_t c = warp_counts[w];
+      warp_counts[w] = s;
+      s += c;
+    }
+    block_base = s ? atomicAdd(counter, s) : 0;
+  }
+  __syncthreads();
+  // pass 2: write the matches (the keys were just read: this re-read hits the cache)
+  uint32_t pos = block_base + warp_counts[wave] + incl - cnt;
+#pragma unroll
+  for (int j = 0; j < kSelItems; ++j) {
+    if (!(matchbits & (1u << j))) continue;
+    const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    if (pos < capacity) {
+      out_keys[pos] = keys[i];
+      out_rows[pos] = rows[i];
+    }
+    ++pos;
+  }
+}
+
+extern "C" int tt_launch_key_histogram(const uint64_t* keys, int64_t n, int32_t shift, uint32_t* hist,
+                                       hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (shift < 0 || shift > 63) return -1;
+  int64_t blocks = (n + kBlock * 64 - 1) / (kBlock * 64);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(tt_key_histogram, dim3((unsigned)blocks), dim3(kBlock), 0, stream, keys, n, shift, hist);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int tt_launch_select_le_bin(const uint64_t* keys, const int32_t* rows, int64_t n, int32_t shift,
+                                       uint32_t last_bin, uint64_t* out_keys, int32_t* out_rows, uint32_t* counter,
+                                       uint32_t capacity, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (shift < 0 || shift > 63) return -1;
+  const int64_t blocks = (n + (int64_t)kBlock * kSelItems - 1) / ((int64_t)kBlock * kSelItems);
+  hipLaunchKernelGGL(tt_select_le_bin, dim3((unsigned)blocks), dim3(kBlock), 0, stream, keys, rows, n, shift, last_bin,
+                     out_keys, out_rows, counter, capacity);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int tt_hist_bins() { return kHistBins; }
