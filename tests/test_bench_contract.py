@@ -1,0 +1,54 @@
+"""bench.py contract: one JSON line from rank 0 with the fields the driver reads, for a single
+process and for a 2-rank torchrun launch over gloo (each rank runs its own environment)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+FIELDS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+          "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out: str) -> list[dict]:
+    return [json.loads(x) for x in out.splitlines() if x.startswith("{") and '"metric"' in x]
+
+
+def _check(line: dict, n: int, steps: int, warmup: int) -> None:
+    assert FIELDS <= set(line)
+    assert line["metric"] == "tasks_e2e_per_sec" and line["n_gpus"] == n
+    assert line["steps"] == steps and line["warmup"] == warmup
+    assert line["value"] > 0 and line["ms_per_step"] > 0 and line["higher_is_better"] is True
+    assert line["scaling"] == "weak" and line["vs_baseline"] is None
+    assert line["config"]["global_batch"] == 32 * n
+
+
+def test_bench_single_process():
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32",
+                        "--api-replicas", "1", "--processor-replicas", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 1, 2, 1)
+
+
+def test_bench_two_ranks_torchrun():
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "32", "--api-replicas", "1", "--processor-replicas", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2, 2, 1)
