@@ -417,7 +417,7 @@ class ColumnarIndex:
             cols = [torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
                     for i, w in enumerate(widths)]
             live = torch.from_numpy(self._live_words(0, nwords)).to(dev)
-            seq = torch.from_numpy(np.ascontiguousarray(self.seq[:self.cap])).to(dev)
+            seq = torch.from_numpy(self.seq[:self.cap].astype(np.int32)).to(dev)  # uint32 on device
             st = self._dev = {"cols": cols, "widths": widths, "live": live, "synced": self.n, "cap": self.cap,
                               "seq": seq}
         else:
@@ -429,7 +429,7 @@ class ColumnarIndex:
                 elif hi > lo:
                     st["cols"][i][lo:hi].copy_(torch.from_numpy(self._narrow(i, lo, hi, w)))
             if hi > lo:
-                st["seq"][lo:hi].copy_(torch.from_numpy(self.seq[lo:hi]))
+                st["seq"][lo:hi].copy_(torch.from_numpy(self.seq[lo:hi].astype(np.int32)))
             if self._tomb_dirty:
                 st["live"].copy_(torch.from_numpy(self._live_words(0, nwords)))
             elif hi > lo:
@@ -545,6 +545,8 @@ class ColumnarIndex:
         if plan is None or len(sort or []) > kernels.max_sort_keys:
             return None
         specs, ranks, seq_bits = plan
+        if seq_bits > 32:
+            return None  # the device keeps a 32-bit insertion sequence
         torch = kernels.torch
         st = self.to_device(kernels)  # sort keys may have added columns
         key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits

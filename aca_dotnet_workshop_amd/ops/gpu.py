@@ -29,11 +29,9 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
-    lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P]
+    lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P, I32, P]
     lib.tt_launch_sort_keys.restype = ctypes.c_int
     lib.tt_sort_max_keys.restype = ctypes.c_int
-    lib.tt_launch_key_histogram.argtypes = [P, I64, I32, P, P]
-    lib.tt_launch_key_histogram.restype = ctypes.c_int
     lib.tt_launch_select_le_bin.argtypes = [P, P, I64, I32, ctypes.c_uint32, P, P, P, ctypes.c_uint32, P]
     lib.tt_launch_select_le_bin.restype = ctypes.c_int
     lib.tt_hist_bins.restype = ctypes.c_int
@@ -105,18 +103,21 @@ class GpuKernels:
             raise RuntimeError(f"tt_group_count launch failed ({rc})")
         return counts[:ngroups]
 
-    def sort_keys(self, table, rows, specs, ranks, seq, seq_bits: int):
+    def sort_keys(self, table, rows, specs, ranks, seq, seq_bits: int, hist=None, shift: int = 0):
         """Packed 63-bit ordering keys (int64) for ``rows`` (int32, device): see
         ``hip/sort_keys.hip``.  ``specs``: int32 [nkeys, 8] device tensor; ``ranks``: int32
-        rank tables (concatenated); ``seq``: int64 insertion sequence per row."""
+        rank tables (concatenated); ``seq``: int32 (uint32) insertion sequence per row.  With
+        ``hist`` the 12-bit radix-select histogram of key bits [shift, shift+12) is fused in."""
         torch = self.torch
         n = rows.numel()
         keys = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
         if specs.shape[0] > self.max_sort_keys:
             raise ValueError("too many sort keys for the device path")
+        if seq.dtype != torch.int32 or seq_bits > 32:
+            raise ValueError("device sequence must be 32-bit")
         rc = self.lib.tt_launch_sort_keys(table.data_ptr(), rows.data_ptr(), n, specs.data_ptr(), specs.shape[0],
                                           ranks.data_ptr(), ranks.numel(), seq.data_ptr(), seq_bits, keys.data_ptr(),
-                                          self._stream())
+                                          hist.data_ptr() if hist is not None else None, shift, self._stream())
         if rc != 0:
             raise RuntimeError(f"tt_sort_keys launch failed ({rc})")
         return keys[:n]
@@ -129,25 +130,25 @@ class GpuKernels:
         n = rows.numel()
         if n == 0:
             return rows
-        keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits)
         if k is not None and k < n and n > 65536:
-            top = self._top_k(keys, rows, k, key_bits)
+            bins = int(self.lib.tt_hist_bins())
+            shift = max(0, key_bits - (bins.bit_length() - 1))
+            hist = torch.zeros(bins, dtype=torch.int32, device=self.device)
+            keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits, hist, shift)
+            top = self._top_k(keys, rows, k, shift, hist)
             if top is not None:
                 return top
+        else:
+            keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits)
         _, idx = torch.sort(keys)
         if k is not None:
             idx = idx[:k]
         return rows[idx]
 
-    def _top_k(self, keys, rows, k: int, key_bits: int):
+    def _top_k(self, keys, rows, k: int, shift: int, hist):
         import numpy as np
         torch = self.torch
         n = keys.numel()
-        bins = int(self.lib.tt_hist_bins())
-        shift = max(0, key_bits - (bins.bit_length() - 1))
-        hist = torch.zeros(bins, dtype=torch.int32, device=self.device)
-        if self.lib.tt_launch_key_histogram(keys.data_ptr(), n, shift, hist.data_ptr(), self._stream()) != 0:
-            raise RuntimeError("tt_key_histogram launch failed")
         cum = np.cumsum(hist.cpu().numpy().astype(np.int64))
         last = int(np.searchsorted(cum, k))  # first bin where the running count reaches k
         cand = int(cum[last])

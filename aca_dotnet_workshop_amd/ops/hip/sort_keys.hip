@@ -25,6 +25,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxKeys = 4;
 constexpr int kLdsRankWords = 8192;  // 32 KiB of rank tables in LDS (all keys together)
+constexpr int kHistBins = 4096;      // 12-bit radix-select histogram (top-k)
 
 struct SortColumn {   // 16 bytes, same layout as the scan kernel's ColumnDesc
   uint64_t ptr;
@@ -57,46 +58,63 @@ __device__ __forceinline__ int32_t load_id(const SortColumn& c, int64_t row) {
 
 }  // namespace
 
+
+// One thread per selected row in a grid-stride loop (a few rows per thread amortise the LDS
+// staging of the rank tables); `seq` is the 32-bit device copy of the insertion sequence.
+// With `hist != nullptr` the 12-bit radix-select histogram of the keys (bits [shift, shift+12))
+// is accumulated in the same pass (LDS-privatised, one global atomic per non-empty bin).
 extern "C" __global__ void __launch_bounds__(kBlock)
 tt_sort_keys(const SortColumn* __restrict__ cols, const int32_t* __restrict__ rows, int64_t n,
              const SortSpec* __restrict__ specs, int32_t nkeys, const int32_t* __restrict__ ranks,
-             int32_t rank_words, const int64_t* __restrict__ seq, int32_t seq_bits, uint64_t* __restrict__ keys) {
+             int32_t rank_words, const uint32_t* __restrict__ seq, int32_t seq_bits, uint64_t* __restrict__ keys,
+             uint32_t* __restrict__ hist, int32_t shift) {
   __shared__ int32_t lds_ranks[kLdsRankWords];
+  __shared__ uint32_t lds_hist[kHistBins];
   __shared__ SortSpec lds_specs[kMaxKeys];
   __shared__ SortColumn lds_cols[kMaxKeys];
   const bool staged = rank_words <= kLdsRankWords;
   if (staged)
     for (int i = threadIdx.x; i < rank_words; i += kBlock) lds_ranks[i] = ranks[i];
+  if (hist)
+    for (int i = threadIdx.x; i < kHistBins; i += kBlock) lds_hist[i] = 0;
   if (threadIdx.x < nkeys) {
     lds_specs[threadIdx.x] = specs[threadIdx.x];
     lds_cols[threadIdx.x] = cols[specs[threadIdx.x].col];
   }
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const int64_t row = rows[i];
-  uint64_t k = 0;
-  for (int j = 0; j < nkeys; ++j) {
-    const SortSpec s = lds_specs[j];
-    const int32_t id = load_id(lds_cols[j], row);
-    int32_t r = s.missing;
-    if (id >= 0 && id < s.nranks) r = staged ? lds_ranks[s.rank_off + id] : ranks[s.rank_off + id];
-    if (s.desc) r = s.max_rank - r;
-    k = (k << s.bits) | (uint64_t)(uint32_t)r;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const int64_t row = rows[i];
+    uint64_t k = 0;
+    for (int j = 0; j < nkeys; ++j) {
+      const SortSpec s = lds_specs[j];
+      const int32_t id = load_id(lds_cols[j], row);
+      int32_t r = s.missing;
+      if (id >= 0 && id < s.nranks) r = staged ? lds_ranks[s.rank_off + id] : ranks[s.rank_off + id];
+      if (s.desc) r = s.max_rank - r;
+      k = (k << s.bits) | (uint64_t)(uint32_t)r;
+    }
+    k = (k << seq_bits) | (uint64_t)seq[row];
+    keys[i] = k;
+    if (hist) atomicAdd(&lds_hist[(uint32_t)(k >> shift) & (kHistBins - 1)], 1u);
   }
-  k = (k << seq_bits) | (uint64_t)seq[row];
-  keys[i] = k;
+  if (hist) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kHistBins; i += kBlock)
+      if (lds_hist[i]) atomicAdd(&hist[i], lds_hist[i]);
+  }
 }
 
 extern "C" int tt_launch_sort_keys(const void* cols, const int32_t* rows, int64_t n, const void* specs, int32_t nkeys,
-                                   const int32_t* ranks, int32_t rank_words, const int64_t* seq, int32_t seq_bits,
-                                   uint64_t* keys, hipStream_t stream) {
+                                   const int32_t* ranks, int32_t rank_words, const uint32_t* seq, int32_t seq_bits,
+                                   uint64_t* keys, uint32_t* hist, int32_t shift, hipStream_t stream) {
   if (n <= 0) return 0;
-  if (nkeys < 0 || nkeys > kMaxKeys || seq_bits < 0 || seq_bits > 63) return -1;
-  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  if (nkeys < 0 || nkeys > kMaxKeys || seq_bits < 0 || seq_bits > 32 || shift < 0 || shift > 63) return -1;
+  int64_t blocks = (n + kBlock * 4 - 1) / (kBlock * 4);  // ~4 rows per thread
+  if (blocks > 65535) blocks = 65535;
   hipLaunchKernelGGL(tt_sort_keys, dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                      reinterpret_cast<const SortColumn*>(cols), rows, n, reinterpret_cast<const SortSpec*>(specs), nkeys,
-                     ranks, rank_words, seq, seq_bits, keys);
+                     ranks, rank_words, seq, seq_bits, keys, hist, shift);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -105,26 +123,13 @@ extern "C" int tt_sort_max_keys() { return kMaxKeys; }
 // ---------------------------------------------------------------------------------------
 // Top-k by radix select: a paged, ordered query needs only the first `k` keys of the
 // selection, so instead of sorting all of them (radix sort of tens of millions of 64-bit
-// keys) we (1) histogram the 12 most significant *used* key bits, (2) find on the host the
+// keys) we (1) histogram the 12 most significant *used* key bits (fused into tt_sort_keys),
+// (2) find on the host the
 // bin where the running count reaches k, (3) compact the (key, row) pairs at or below that bin
 // and (4) sort only those candidates.
 namespace {
-constexpr int kHistBins = 4096;     // 12 bits
 constexpr int kSelItems = 16;       // keys per thread per block-iteration
 }  // namespace
-
-extern "C" __global__ void __launch_bounds__(kBlock)
-tt_key_histogram(const uint64_t* __restrict__ keys, int64_t n, int32_t shift, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[kHistBins];
-  for (int i = threadIdx.x; i < kHistBins; i += kBlock) h[i] = 0;
-  __syncthreads();
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-    atomicAdd(&h[(uint32_t)(keys[i] >> shift) & (kHistBins - 1)], 1u);
-  __syncthreads();
-  for (int i = threadIdx.x; i < kHistBins; i += kBlock)
-    if (h[i]) atomicAdd(&hist[i], h[i]);
-}
 
 // Keep pairs whose bin <= `last_bin`; one global atomic per block reserves the block's range.
 extern "C" __global__ void __launch_bounds__(kBlock)
@@ -176,17 +181,6 @@ tt_select_le_bin(const uint64_t* __restrict__ keys, const int32_t* __restrict__ 
     }
     ++pos;
   }
-}
-
-extern "C" int tt_launch_key_histogram(const uint64_t* keys, int64_t n, int32_t shift, uint32_t* hist,
-                                       hipStream_t stream) {
-  if (n <= 0) return 0;
-  if (shift < 0 || shift > 63) return -1;
-  int64_t blocks = (n + kBlock * 64 - 1) / (kBlock * 64);
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(tt_key_histogram, dim3((unsigned)blocks), dim3(kBlock), 0, stream, keys, n, shift, hist);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 extern "C" int tt_launch_select_le_bin(const uint64_t* keys, const int32_t* rows, int64_t n, int32_t shift,
