@@ -35,6 +35,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_select_le_bin.argtypes = [P, P, I64, I32, ctypes.c_uint32, P, P, P, ctypes.c_uint32, P]
     lib.tt_launch_select_le_bin.restype = ctypes.c_int
     lib.tt_hist_bins.restype = ctypes.c_int
+    lib.tt_set_eval_groups.argtypes = [ctypes.c_int]
+    lib.tt_set_eval_groups.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -52,6 +54,11 @@ class GpuKernels:
         self.tile_rows = int(self.lib.tt_tile_rows())
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
+
+    def set_eval_groups(self, u: int) -> None:
+        """Row groups per lane in ``tt_scan_eval`` (1, 2 or 4): registers vs loads in flight."""
+        if self.lib.tt_set_eval_groups(int(u)) != 0:
+            raise ValueError("eval groups must be 1, 2 or 4")
 
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)

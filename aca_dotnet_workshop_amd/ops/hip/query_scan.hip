@@ -9,7 +9,7 @@
 // S"; ordering/type semantics are resolved against the dictionary on the host, so the
 // device only compares ids and tests bits.
 //
-// tt_scan_eval: each lane owns 16 consecutive rows.  For every leaf it loads the 16 ids with
+// tt_scan_eval: each lane owns 4 groups of 16 consecutive rows (loads for all 4 in flight).  For every leaf it loads the 16 ids with
 // one 16/32/64-byte vector load (width 1/2/4) and produces a 16-bit row mask; the program's
 // stack holds 16-bit masks packed in a 128-bit register (depth <= 8), so AND/OR/NOT are
 // plain bitwise ops on all 16 rows at once.  The lane ANDs the liveness bits and stores its
@@ -24,10 +24,10 @@
 
 namespace {
 
-constexpr int kBlock = 256;                    // 4 waves
+constexpr int kBlock = 256;                    // 4 waves (compaction, group count)
 constexpr int kRowsPerLane = 16;
-constexpr int kIters = 2;
-constexpr int kTileRows = kBlock * kRowsPerLane * kIters;  // 8192 rows per block
+constexpr int kTileRows = 8192;               // rows per scan / compaction block
+static_assert(kTileRows == kBlock * 32, "compaction takes 32 mask bits per thread per tile");
 constexpr int kMaxDepth = 8;                   // 8 x 16-bit masks in a 128-bit stack
 constexpr int kMaxLdsBitmapWords = 8192;       // stage up to 32 KiB of leaf bitmaps in LDS
 
@@ -95,10 +95,16 @@ __device__ __forceinline__ uint32_t leaf_mask(const int32_t (&ids)[16], BitmapPt
   return m;
 }
 
-template <typename BitmapPtr>
-__device__ __forceinline__ uint32_t run_program(const ColumnDesc* __restrict__ cols, const int32_t* __restrict__ prog,
-                                                int32_t prog_len, BitmapPtr bitmaps, int64_t row0) {
-  u128 st = 0;
+// Evaluate the program for U independent 16-row groups at once: every leaf issues its U vector
+// loads back to back, so each lane keeps U column loads in flight instead of one (the
+// interpreted program otherwise serialises load -> test -> next leaf).
+template <int U, typename BitmapPtr>
+__device__ __forceinline__ void run_program(const ColumnDesc* __restrict__ cols, const int32_t* __restrict__ prog,
+                                            int32_t prog_len, BitmapPtr bitmaps, const int64_t (&row0)[U],
+                                            uint32_t (&out)[U]) {
+  u128 st[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) st[u] = 0;
 #pragma unroll 1
   for (int pc = 0; pc < prog_len; ++pc) {
     const int32_t op = prog[pc * 4 + 0];
@@ -107,35 +113,48 @@ __device__ __forceinline__ uint32_t run_program(const ColumnDesc* __restrict__ c
     const int32_t c = prog[pc * 4 + 3];
     if (op == OP_LEAF || op == OP_EQ) {
       const ColumnDesc cd = cols[a];
-      int32_t ids[16];
-      load16(cd, row0, ids);
-      uint32_t m = 0;
-      if (op == OP_EQ) {
+      int32_t ids[U][16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[i] == b) << i;
-      } else {
-        m = leaf_mask(ids, bitmaps + b, c);
+      for (int u = 0; u < U; ++u) load16(cd, row0[u], ids[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t m = 0;
+        if (op == OP_EQ) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[u][i] == b) << i;
+        } else {
+          m = leaf_mask(ids[u], bitmaps + b, c);
+        }
+        st[u] = (st[u] << 16) | (u128)m;
       }
-      st = (st << 16) | (u128)m;
     } else if (op == OP_AND || op == OP_OR) {
-      uint32_t r = (op == OP_AND) ? 0xFFFFu : 0u;
-      for (int k = 0; k < a; ++k) {
-        const uint32_t top = (uint32_t)(st & (u128)0xFFFFu);
-        r = (op == OP_AND) ? (r & top) : (r | top);
-        st >>= 16;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t r = (op == OP_AND) ? 0xFFFFu : 0u;
+        for (int k = 0; k < a; ++k) {
+          const uint32_t top = (uint32_t)(st[u] & (u128)0xFFFFu);
+          r = (op == OP_AND) ? (r & top) : (r | top);
+          st[u] >>= 16;
+        }
+        st[u] = (st[u] << 16) | (u128)r;
       }
-      st = (st << 16) | (u128)r;
     } else if (op == OP_NOT) {
-      st ^= (u128)0xFFFFu;
+#pragma unroll
+      for (int u = 0; u < U; ++u) st[u] ^= (u128)0xFFFFu;
     } else {  // OP_TRUE
-      st = (st << 16) | (u128)0xFFFFu;
+#pragma unroll
+      for (int u = 0; u < U; ++u) st[u] = (st[u] << 16) | (u128)0xFFFFu;
     }
   }
-  return (uint32_t)(st & (u128)0xFFFFu);
+#pragma unroll
+  for (int u = 0; u < U; ++u) out[u] = (uint32_t)(st[u] & (u128)0xFFFFu);
 }
 
-extern "C" __global__ void __launch_bounds__(kBlock)
-tt_scan_eval(const ColumnDesc* __restrict__ cols,
+// One block per 8192-row tile; U = row groups per lane evaluated together (U x 16 rows per
+// lane, 8192 / (16 U) threads per block).  U trades registers (occupancy) for loads in flight.
+template <int U>
+__global__ void __launch_bounds__(kTileRows / (kRowsPerLane * U))
+tt_scan_eval_t(const ColumnDesc* __restrict__ cols,
              int64_t nrows,
              const uint16_t* __restrict__ live,      // 1 bit per row, row order
              const int32_t* __restrict__ prog, int32_t prog_len,
@@ -145,33 +164,39 @@ tt_scan_eval(const ColumnDesc* __restrict__ cols,
   extern __shared__ uint32_t lds_bitmaps[];  // sized by the launcher: bitmap_words if they fit, else 0
   const bool in_lds = bitmap_words <= kMaxLdsBitmapWords;
   if (in_lds) {
-    for (int i = threadIdx.x; i < bitmap_words; i += kBlock) lds_bitmaps[i] = bitmaps[i];
+    for (int i = threadIdx.x; i < bitmap_words; i += (kTileRows / (kRowsPerLane * U))) lds_bitmaps[i] = bitmaps[i];
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
+  int64_t row0[U];
+  uint16_t lv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    // group u covers rows [tile*8192 + u*2048, +2048): 16 per lane, lanes contiguous -> the
+    // per-group mask stores of a wave form one 128-byte segment
+    row0[u] = tile * kTileRows + (int64_t)u * ((kTileRows / (kRowsPerLane * U)) * kRowsPerLane) + (int64_t)threadIdx.x * kRowsPerLane;
+    lv[u] = live[row0[u] >> 4];  // issued early, consumed after the program
+  }
+  uint32_t m[U];
+  if (in_lds) run_program<U>(cols, prog, prog_len, lds_bitmaps, row0, m);
+  else run_program<U>(cols, prog, prog_len, bitmaps, row0, m);
   int32_t local = 0;
-#pragma unroll 1
-  for (int it = 0; it < kIters; ++it) {
-    const int64_t row0 = tile * kTileRows + (int64_t)it * (kBlock * kRowsPerLane) + (int64_t)(wave * 64 + lane) * 16;
-    uint32_t sel = 0;
-    if (row0 < nrows) {
-      const uint32_t m = in_lds ? run_program(cols, prog, prog_len, lds_bitmaps, row0)
-                                : run_program(cols, prog, prog_len, bitmaps, row0);
-      sel = m & (uint32_t)live[row0 >> 4];
-    }
-    mask[row0 >> 4] = (uint16_t)sel;  // the launched tiles are inside the buffers' capacity
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t sel = row0[u] < nrows ? (m[u] & (uint32_t)lv[u]) : 0u;
+    mask[row0[u] >> 4] = (uint16_t)sel;  // the launched tiles are inside the buffers' capacity
     local += __popc(sel);
   }
   // block reduction of the per-lane counts
   for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
-  __shared__ int32_t wave_counts[kBlock / 64];
+  __shared__ int32_t wave_counts[(kTileRows / (kRowsPerLane * U)) / 64];
   if (lane == 0) wave_counts[wave] = local;
   __syncthreads();
   if (threadIdx.x == 0) {
     int32_t s = 0;
-    for (int w = 0; w < kBlock / 64; ++w) s += wave_counts[w];
+    for (int w = 0; w < (kTileRows / (kRowsPerLane * U)) / 64; ++w) s += wave_counts[w];
     block_counts[tile] = s;
   }
 }
@@ -246,6 +271,14 @@ tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* _
 }
 
 // ------------------------------------------------------------------ host launchers
+// Row groups per lane of the scan kernel (1, 2 or 4); tunable for A/B measurements.
+static int g_eval_groups = 4;
+extern "C" int tt_set_eval_groups(int u) {
+  if (u != 1 && u != 2 && u != 4) return -1;
+  g_eval_groups = u;
+  return 0;
+}
+
 // Preconditions (checked by the Python wrapper): every column and the live/mask buffers are
 // allocated for a capacity that is a multiple of kTileRows rows, nrows <= capacity.
 extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* prog,
@@ -255,9 +288,20 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
   const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
-  hipLaunchKernelGGL(tt_scan_eval, dim3((unsigned)tiles), dim3(kBlock), lds, stream,
-                     reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, bitmap_words,
-                     mask, block_counts);
+  const ColumnDesc* cd = reinterpret_cast<const ColumnDesc*>(cols);
+  switch (g_eval_groups) {
+    case 1:
+      hipLaunchKernelGGL(tt_scan_eval_t<1>, dim3((unsigned)tiles), dim3(kTileRows / kRowsPerLane), lds, stream, cd,
+                         nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
+      break;
+    case 2:
+      hipLaunchKernelGGL(tt_scan_eval_t<2>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 2)), lds, stream,
+                         cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
+      break;
+    default:
+      hipLaunchKernelGGL(tt_scan_eval_t<4>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 4)), lds, stream,
+                         cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
+  }
   return (int)hipGetLastError();
 }
 

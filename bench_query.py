@@ -28,6 +28,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu", action="store_true", help="also time the NumPy executor (slow at 1e8 rows)")
+    ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4; 0 = default)")
     ap.add_argument("--sorted", action="store_true",
                     help="also time ORDER BY taskDueDate DESC: top-100 page and full ordering (tt_sort_keys + sort)")
     a = ap.parse_args()
@@ -66,6 +67,8 @@ def main() -> None:
     ix._full_dirty = True
 
     k = GpuKernels("cuda:0")
+    if a.eval_groups:
+        k.set_eval_groups(a.eval_groups)
     flt = {"AND": [{"LT": {"taskDueDate": "2024-07-01T00:00:00"}}, {"EQ": {"isCompleted": False}},
                    {"EQ": {"isOverDue": False}}]}
     prog = ix.compile(flt)
@@ -86,7 +89,7 @@ def main() -> None:
     nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
-           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "column_bytes_per_row": widths}
+           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "eval_groups": a.eval_groups or 4, "column_bytes_per_row": widths}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order
         ix._full_dirty = True
