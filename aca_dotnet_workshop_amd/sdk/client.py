@@ -119,7 +119,9 @@ class SidecarClient:
     async def _call(self, method: str, path: str, body: bytes = b"", ctype: str | None = None,
                     extra: dict[str, str] | None = None, span_name: str | None = None) -> ClientResponse:
         tr = tracing.tracer()
-        span = tr.start_span(span_name or f"{method} {path}", "client")
+        span = tr.start_span(span_name or method, "client")
+        if span.sampled and not span_name:
+            span.name = f"{method} {path}"
         try:
             resp = await self.http.request(method, self.base + path, headers=self._headers(ctype, extra), body=body)
             span.set("http.status", resp.status)

@@ -30,6 +30,11 @@ class Counter:
         with self._lock:
             self.values[key] = self.values.get(key, 0.0) + amount
 
+    def inc_key(self, key: tuple, amount: float = 1.0) -> None:
+        """``inc`` with a precomputed label key (``tuple(sorted(labels.items()))``)."""
+        with self._lock:
+            self.values[key] = self.values.get(key, 0.0) + amount
+
     def get(self, **labels: str) -> float:
         return self.values.get(tuple(sorted(labels.items())), 0.0)
 
@@ -59,7 +64,9 @@ class Histogram:
         self._lock = threading.Lock()
 
     def observe(self, value: float, **labels: str) -> None:
-        key = tuple(sorted(labels.items()))
+        self.observe_key(value, tuple(sorted(labels.items())))
+
+    def observe_key(self, value: float, key: tuple) -> None:
         with self._lock:
             s = self.series.get(key)
             if s is None:
@@ -121,11 +128,18 @@ def metrics_middleware(registry: Registry = REGISTRY):
     reqs = registry.counter("http_requests_total", "HTTP requests served")
     lat = registry.histogram("http_request_duration_seconds", "HTTP request latency")
 
+    keys: dict[tuple, tuple] = {}  # (method, route, status) -> precomputed label keys
+
     async def mw(req, nxt):
         t0 = time.perf_counter()
         resp = await nxt(req)
         route = getattr(req.route, "template", "unmatched")
-        reqs.inc(method=req.method, route=route, status=str(resp.status))
-        lat.observe(time.perf_counter() - t0, route=route)
+        ck = (req.method, route, resp.status)
+        k = keys.get(ck)
+        if k is None:
+            k = keys[ck] = (tuple(sorted({"method": req.method, "route": route, "status": str(resp.status)}.items())),
+                            (("route", route),))
+        reqs.inc_key(k[0])
+        lat.observe_key(time.perf_counter() - t0, k[1])
         return resp
     return mw

@@ -143,9 +143,10 @@ class Span:
         self.span_id = span_id
         self.parent_id = parent_id
         self.sampled = sampled
-        self.attributes = attributes or {}
-        self.start = time.time()
-        self._t0 = time.perf_counter()
+        self.attributes = attributes
+        # unsampled spans only carry context (ids for propagation): skip clocks and attributes
+        self.start = time.time() if sampled else 0.0
+        self._t0 = time.perf_counter() if sampled else 0.0
         self.status = "ok"
         self._token = None
         self.events: list[tuple[float, str]] | None = None
@@ -155,6 +156,10 @@ class Span:
         return f"00-{self.trace_id}-{self.span_id}-{'01' if self.sampled else '00'}"
 
     def set(self, key: str, value: Any) -> None:
+        if not self.sampled:
+            return
+        if self.attributes is None:
+            self.attributes = {}
         self.attributes[key] = value
 
     def event(self, name: str) -> None:
@@ -165,10 +170,9 @@ class Span:
     def fail(self, err: Any = None) -> None:
         self.status = "error"
         if err is not None:
-            self.attributes["error"] = str(err)
+            self.set("error", str(err))
 
     def end(self) -> None:
-        dur = (time.perf_counter() - self._t0) * 1000.0
         if self._token is not None:
             try:
                 _current.reset(self._token)
@@ -177,6 +181,7 @@ class Span:
             self._token = None
         if not self.sampled:
             return
+        dur = (time.perf_counter() - self._t0) * 1000.0
         rec = {"type": "span", "role": self.tracer.role, "instance": self.tracer.instance, "name": self.name,
                "kind": self.kind, "traceId": self.trace_id, "spanId": self.span_id, "parentId": self.parent_id,
                "ts": self.start, "durationMs": round(dur, 3), "status": self.status}
@@ -236,8 +241,8 @@ def server_middleware(role_attr: str = "http"):
 
     async def mw(req: Request, nxt) -> Response:
         tr = tracer()
-        parent = parse_traceparent(req.headers.get("traceparent"))
-        span = tr.start_span(f"{req.method} {req.path}", "server", parent)
+        tp = req.headers.get("traceparent")
+        span = tr.start_span(req.method, "server", parse_traceparent(tp) if tp else None)
         req.state["trace_id"] = span.trace_id
         req.state["span"] = span
         try:
@@ -247,12 +252,12 @@ def server_middleware(role_attr: str = "http"):
             span.set("http.status", 500)
             span.end()
             raise
-        span.set("http.status", resp.status)
+        if span.sampled:  # names and attributes only matter for exported spans
+            span.set("http.status", resp.status)
+            route = getattr(req.route, "template", None)
+            span.name = f"{req.method} {route or req.path}"
         if resp.status >= 500:
             span.status = "error"
-        route = getattr(req.route, "template", None)
-        if route:
-            span.name = f"{req.method} {route}"
         span.end()
         return resp
     return mw
