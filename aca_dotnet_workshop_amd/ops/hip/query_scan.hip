@@ -9,7 +9,8 @@
 // S"; ordering/type semantics are resolved against the dictionary on the host, so the
 // device only compares ids and tests bits.
 //
-// tt_scan_eval: each lane owns 4 groups of 16 consecutive rows (loads for all 4 in flight).  For every leaf it loads the 16 ids with
+// tt_scan_eval: each lane owns U groups of 16 consecutive rows (default 2; loads for all U in
+// flight).  For every leaf it loads the 16 ids with
 // one 16/32/64-byte vector load (width 1/2/4) and produces a 16-bit row mask; the program's
 // stack holds 16-bit masks packed in a 128-bit register (depth <= 8), so AND/OR/NOT are
 // plain bitwise ops on all 16 rows at once.  The lane ANDs the liveness bits and stores its
@@ -272,7 +273,7 @@ tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* _
 
 // ------------------------------------------------------------------ host launchers
 // Row groups per lane of the scan kernel (1, 2 or 4); tunable for A/B measurements.
-static int g_eval_groups = 4;
+static int g_eval_groups = 2;  // measured on MI355X: 1 -> 0.183 ms, 2 -> 0.175 ms, 4 -> 0.194 ms per 1e8-row query
 extern "C" int tt_set_eval_groups(int u) {
   if (u != 1 && u != 2 && u != 4) return -1;
   g_eval_groups = u;
@@ -294,11 +295,11 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
       hipLaunchKernelGGL(tt_scan_eval_t<1>, dim3((unsigned)tiles), dim3(kTileRows / kRowsPerLane), lds, stream, cd,
                          nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
       break;
-    case 2:
+    default:
       hipLaunchKernelGGL(tt_scan_eval_t<2>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 2)), lds, stream,
                          cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
       break;
-    default:
+    case 4:
       hipLaunchKernelGGL(tt_scan_eval_t<4>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 4)), lds, stream,
                          cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
   }

@@ -68,8 +68,10 @@ tt_sort_keys(const SortColumn* __restrict__ cols, const int32_t* __restrict__ ro
              const SortSpec* __restrict__ specs, int32_t nkeys, const int32_t* __restrict__ ranks,
              int32_t rank_words, const uint32_t* __restrict__ seq, int32_t seq_bits, uint64_t* __restrict__ keys,
              uint32_t* __restrict__ hist, int32_t shift) {
-  __shared__ int32_t lds_ranks[kLdsRankWords];
-  __shared__ uint32_t lds_hist[kHistBins];
+  // dynamic LDS: [hist (kHistBins words, only with `hist`)] [rank tables (rank_words, when they fit)]
+  extern __shared__ uint32_t lds_dyn[];
+  uint32_t* lds_hist = lds_dyn;
+  int32_t* lds_ranks = reinterpret_cast<int32_t*>(lds_dyn + (hist ? kHistBins : 0));
   __shared__ SortSpec lds_specs[kMaxKeys];
   __shared__ SortColumn lds_cols[kMaxKeys];
   const bool staged = rank_words <= kLdsRankWords;
@@ -110,9 +112,12 @@ extern "C" int tt_launch_sort_keys(const void* cols, const int32_t* rows, int64_
                                    uint64_t* keys, uint32_t* hist, int32_t shift, hipStream_t stream) {
   if (n <= 0) return 0;
   if (nkeys < 0 || nkeys > kMaxKeys || seq_bits < 0 || seq_bits > 32 || shift < 0 || shift > 63) return -1;
-  int64_t blocks = (n + kBlock * 4 - 1) / (kBlock * 4);  // ~4 rows per thread
-  if (blocks > 65535) blocks = 65535;
-  hipLaunchKernelGGL(tt_sort_keys, dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+  // a bounded grid (8 blocks per CU on 256 CUs): each thread loops over many rows, so the LDS
+  // staging and the histogram flush (<= 4096 global atomics per block) are amortised
+  int64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 2048) blocks = 2048;
+  const size_t lds = ((hist ? kHistBins : 0) + (rank_words <= kLdsRankWords ? rank_words : 0)) * sizeof(uint32_t);
+  hipLaunchKernelGGL(tt_sort_keys, dim3((unsigned)blocks), dim3(kBlock), lds, stream,
                      reinterpret_cast<const SortColumn*>(cols), rows, n, reinterpret_cast<const SortSpec*>(specs), nkeys,
                      ranks, rank_words, seq, seq_bits, keys, hist, shift);
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -89,7 +89,7 @@ def main() -> None:
     nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
-           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "eval_groups": a.eval_groups or 4, "column_bytes_per_row": widths}
+           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order
         ix._full_dirty = True
