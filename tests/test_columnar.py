@@ -174,11 +174,16 @@ GPU_FILTERS = [
 def test_gpu_scan_matches_numpy(n):
     k = _kernels()
     ix = _random_collection(n, random.Random(n))
-    for f in GPU_FILTERS:
-        prog = ix.compile(f)
-        want = ix.select_numpy(prog)
-        got = ix.select_gpu(prog, k)
-        assert np.array_equal(got, want), (n, f)
+    try:
+        for u in (1, 2, 4):  # every tt_scan_eval instantiation (row groups per lane)
+            k.set_eval_groups(u)
+            for f in GPU_FILTERS:
+                prog = ix.compile(f)
+                want = ix.select_numpy(prog)
+                got = ix.select_gpu(prog, k)
+                assert np.array_equal(got, want), (n, f, u)
+    finally:
+        k.set_eval_groups(2)
 
 
 @pytest.mark.gpu
