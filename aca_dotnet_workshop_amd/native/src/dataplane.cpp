@@ -448,6 +448,7 @@ class DataPlane {
     fallback_ = Endpoint::parse(*opt_str(cfg, "fallback"));
     if (auto* v = cfg.get("invokeNative"); v && v->t == Value::Bool) invoke_native_ = v->b;
     if (auto* v = cfg.get("appTimeout"); v && v->t == Value::Number) app_timeout_ = v->n;
+    if (auto* v = cfg.get("apiLogging"); v && v->t == Value::Bool) api_logging_ = v->b;
     if (auto* tr = cfg.get("trace")) tracer_.init(*tr);
     if (auto* st = cfg.get("stores"); st && st->t == Value::Object)
       for (size_t i = 0; i < st->keys.size(); ++i) {
@@ -502,7 +503,7 @@ class DataPlane {
   Resolver resolver_;
   std::string app_id_, app_token_, api_token_, mesh_token_;
   Endpoint app_, fallback_;
-  bool has_app_ = false, invoke_native_ = true;
+  bool has_app_ = false, invoke_native_ = true, api_logging_ = false;
   double app_timeout_ = 300;
   std::map<std::string, Store> stores_;
   std::map<std::string, Bus> buses_;
@@ -514,6 +515,22 @@ class DataPlane {
     if (auto* i = opt_str(s, "identity"); i && !i->empty()) h.emplace_back("x-tt-identity", *i);
     if (auto* k = opt_str(s, "key"); k && !k->empty()) h.emplace_back("x-tt-key", *k);
     return h;
+  }
+
+  // Dapr's enableApiLogging: one JSON line per API call on stderr (the replica's log stream),
+  // same shape as telemetry/logging.py JsonFormatter.
+  void api_log(const std::string& name, int status, const SpanCtx& span) {
+    char buf[96];
+    std::snprintf(buf, sizeof buf, " status=%d duration_ms=%.3f app_id=", status, (ev::now_s() - span.t0) * 1e3);
+    auto sp = name.find(' ');
+    std::string msg = "HTTP API Called method=" + name.substr(0, sp) + " path=" +
+                      (sp == std::string::npos ? "" : name.substr(sp + 1)) + buf + app_id_;
+    char ts[32];
+    std::snprintf(ts, sizeof ts, "%.6f", wall_now());
+    std::string line = std::string("{\"ts\":") + ts + ",\"level\":\"INFO\",\"role\":" + json_str(app_id_ + ".sidecar") +
+                       ",\"category\":\"sidecar.http-info\",\"message\":" + json_str(msg) + ",\"traceId\":\"" +
+                       span.trace_id + "\",\"spanId\":\"" + span.span_id + "\",\"plane\":\"native\"}\n";
+    std::fwrite(line.data(), 1, line.size(), stderr);
   }
 
   void count(const std::string& op, int status) {
@@ -529,6 +546,7 @@ class DataPlane {
     std::vector<std::pair<std::string, std::string>> attrs;
     void send(int status, const HeaderList& h, std::string_view body) {
       rep.send(status, h, body);
+      if (dp->api_logging_) dp->api_log(name, status, span);
       dp->tracer_.end(span, name, status, attrs);
       dp->count(op, status);
       dp->inflight_--;

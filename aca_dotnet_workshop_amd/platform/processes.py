@@ -119,7 +119,8 @@ class LocalStack:
 
     def start_replica(self, app_id: str, config: dict[str, str] | None = None, extra_env: dict[str, str] | None = None,
                       http_port: int | None = None, module: str | None = None, log_level: str = "warning",
-                      identity: str | None = None, external_port: int | None = None) -> ReplicaProc:
+                      identity: str | None = None, external_port: int | None = None,
+                      api_logging: bool = False) -> ReplicaProc:
         idx = self._seq
         self._seq += 1
         name = f"{app_id}-{idx}"
@@ -138,6 +139,8 @@ class LocalStack:
                 "--unix-socket-dir", str(self.sock_dir), "--replica-name", name, "--log-level", log_level]
         for c in self.components:
             args += ["--resources-path", c]
+        if api_logging:
+            args.append("--enable-api-logging")
         args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
         p = self._spawn(args, env, name)
         rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)

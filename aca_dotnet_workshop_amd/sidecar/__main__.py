@@ -44,6 +44,8 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--app-max-concurrency", type=int, default=None)
     r.add_argument("--app-health-check-path", default=None)
     r.add_argument("--log-level", default="info")
+    r.add_argument("--enable-api-logging", action="store_true",
+                   help="log every sidecar API call (Dapr's enableApiLogging)")
     r.add_argument("--replica-name", default=os.environ.get("TT_REPLICA_NAME"))
     r.add_argument("command", nargs=argparse.REMAINDER, help="-- <app command>")
     return ap
@@ -64,7 +66,8 @@ async def _run(a: argparse.Namespace) -> int:
                  resources_paths=a.resources, registry_dir=a.registry_dir, api_token=os.environ.get("DAPR_API_TOKEN"),
                  app_token=os.environ.get("APP_API_TOKEN"), mesh_token=os.environ.get("TT_MESH_TOKEN"),
                  app_max_concurrency=a.app_max_concurrency, identity=a.identity, backing_url=a.backing_url,
-                 instance=a.replica_name, app_health_path=a.app_health_check_path)
+                 instance=a.replica_name, app_health_path=a.app_health_check_path,
+                 api_logging=a.enable_api_logging)
     await sc.start()
     loop = asyncio.get_running_loop()
     stop = asyncio.Event()

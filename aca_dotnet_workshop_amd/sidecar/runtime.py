@@ -49,6 +49,7 @@ from .secrets import APP_SECRETS_STORE, AppSecretsStore, SecretStore
 from .state import EtagMismatch, SetRequest, StateStore
 
 log = logging.getLogger("sidecar")
+api_log = logging.getLogger("sidecar.http-info")
 
 RUNTIME_VERSION = "1.0.0-tt"
 _HOP = {"host", "content-length", "connection", "transfer-encoding", "keep-alive", "dapr-api-token", "dapr-app-id",
@@ -76,7 +77,8 @@ class Sidecar:
                  mesh_token: str | None = None, app_max_concurrency: int | None = None,
                  identity: str | None = None, backing_url: str | None = None, environ: dict[str, str] | None = None,
                  telemetry_dir: str | None = None, instance: str | None = None,
-                 app_health_path: str | None = None, data_plane: str | None = None) -> None:
+                 app_health_path: str | None = None, data_plane: str | None = None,
+                 api_logging: bool = False) -> None:
         self.app_id = app_id
         self.app_port = app_port
         self.app_uds = app_uds
@@ -95,6 +97,7 @@ class Sidecar:
         self.mesh_token = mesh_token
         self.instance = instance or f"{app_id}-{uuid.uuid4().hex[:8]}"
         self.app_health_path = app_health_path
+        self.api_logging = api_logging
         self.http = HttpClient(timeout=300)
         kw: dict[str, Any] = {"app_id": app_id, "identity": identity, "http": self.http, "environ": self.environ}
         if backing_url:
@@ -203,6 +206,7 @@ class Sidecar:
                 "meshToken": self.mesh_token, "registryDir": str(self.resolver.dir) if self.resolver.dir else None,
                 "fallback": fallback, "invokeNative": self.resolver.dir is not None, "appTimeout": 300.0,
                 "listen": listen, "internal": internal, "stores": stores, "pubsubs": buses,
+                "apiLogging": self.api_logging,
                 "trace": {"dir": ex.directory, "sampleRate": self.tracer.sample_rate, "role": self.tracer.role,
                           "instance": self.instance}}
 
@@ -555,11 +559,15 @@ class Sidecar:
             parent = parse_traceparent(req.headers.get("traceparent"))
             span = sc.tracer.start_span(f"{req.method} {req.path.split('?')[0][:80]}", "server", parent)
             req.state["span"] = span
+            t0 = time.perf_counter() if sc.api_logging else 0.0
             try:
                 resp = await nxt(req)
                 span.set("http.status", resp.status)
                 if resp.status >= 500:
                     span.status = "error"
+                if sc.api_logging:
+                    api_log.info("HTTP API Called method=%s path=%s status=%d duration_ms=%.3f app_id=%s",
+                                 req.method, req.path, resp.status, (time.perf_counter() - t0) * 1e3, sc.app_id)
                 return resp
             except BaseException as e:
                 span.fail(e)

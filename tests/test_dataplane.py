@@ -360,3 +360,20 @@ def test_delivery_outcomes(plane, tmp_path):
             await asrv.close(1.0)
             await bsrv.close(1.0)
     run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_api_logging(plane, tmp_path, capfd, caplog):
+    """enableApiLogging: every sidecar API call is logged (method, path, status, duration)."""
+    import logging
+    caplog.set_level(logging.INFO, logger="sidecar.http-info")
+
+    async def main():
+        async with Env(plane, tmp_path, api_logging=True) as e:
+            b = e.base["app-a"]
+            assert (await e.http.post(f"{b}/v1.0/state/statestore", json_body=[{"key": "L", "value": 1}])).status == 204
+            assert (await e.http.get(f"{b}/v1.0/invoke/app-a/method/api/echo/log")).status == 201
+    run(main())
+    text = capfd.readouterr().err + "\n".join(r.getMessage() for r in caplog.records)
+    assert "HTTP API Called method=POST path=/v1.0/state/statestore status=204" in text
+    assert "HTTP API Called method=GET path=/v1.0/invoke/app-a/method/api/echo/log status=201" in text
