@@ -97,11 +97,8 @@ class CollectionAccelerator:
     def build(self, store) -> None:
         if self.before_build is not None:
             self.before_build()
-        res = json.loads(store.query("{}", ""))["results"]
-        ix = ColumnarIndex(capacity=len(res) + 4096)
-        ix.add_column(PREFIX_PATH)
-        for r in res:
-            ix.upsert(r["key"], _with_prefix(r["key"], r["data"]))
+        # native bulk encode (DocStore.encode_columns): no per-document Python objects
+        ix = ColumnarIndex.from_source(lambda paths: store.encode_columns("", paths), [PREFIX_PATH])
         self.index = ix
         log.info("built columnar index over %d documents", ix.live_rows())
 

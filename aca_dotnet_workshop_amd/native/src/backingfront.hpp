@@ -5,6 +5,7 @@
 // handlers use (both are internally synchronised), without touching the GIL:
 //
 //   PUT|GET|DELETE /cosmos/{account}/{db}/{coll}/docs/{key}
+//   POST           /cosmos/{account}/{db}/{coll}/bulkset
 //   POST           /servicebus/{ns}/topics/{topic}/messages
 //   POST           /servicebus/{ns}/receive?entity&max&lockMs&waitMs   (long poll)
 //   POST           /servicebus/{ns}/settle
@@ -364,6 +365,8 @@ class BackingFront {
       i = j + 1;
     }
     if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(m, r, seg)) return;
+    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkset" && m.method == "POST" && handle_bulkset(m, r, seg))
+      return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
   }
@@ -432,6 +435,61 @@ class BackingFront {
     } catch (const EtagMismatch& ex) {
       r.send(412, {{"content-type", pj}}, bf::problem_json(412, ex.what()));
     }
+    return true;
+  }
+
+  // POST .../bulkset: [{"key", "value" (JSON text or value), "etag", "firstWrite", "ttlMs"}]
+  bool handle_bulkset(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
+    Coll* c = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
+      if (it != colls_.end() && it->second->store) c = it->second.get();
+    }
+    if (!c) return false;
+    Value items;
+    try {
+      items = parse(m.body.empty() ? std::string_view("[]") : std::string_view(m.body));
+    } catch (const std::exception&) {
+      return false;  // Python produces the error response
+    }
+    if (items.t != Value::Array) return false;
+    for (auto& it : items.items) {
+      auto* t = it.get("ttlMs");
+      if (t && t->t == Value::Number && t->n != 0) return false;  // TTL writes go through Python
+      auto* k = it.get("key");
+      if (!k || k->t != Value::String) return false;
+    }
+    std::shared_lock w(c->write_mu);
+    if (c->mirrored) return false;
+    if (!authorize(m, r, "cosmos.write", "cosmos/" + seg[1])) return true;
+    count("doc.bulkset");
+    std::string out = "[";
+    bool etag_err = false, other_err = false;
+    for (size_t i = 0; i < items.items.size(); ++i) {
+      const Value& it = items.items[i];
+      const std::string& key = it.get("key")->s;
+      const Value* v = it.get("value");
+      std::string value = v ? (v->t == Value::String ? v->s : dump(*v)) : std::string("null");
+      std::optional<std::string> etag;
+      if (auto* e = it.get("etag"); e && e->t == Value::String && !e->s.empty()) etag = e->s;
+      bool fw = false;
+      if (auto* f = it.get("firstWrite"); f && f->t == Value::Bool) fw = f->b;
+      if (i) out += ", ";
+      try {
+        std::string e = c->store->set(key, value, etag, fw, 0);
+        out += "{\"key\": " + bf::jstr(key) + ", \"etag\": " + bf::jstr(e) + "}";
+      } catch (const EtagMismatch& ex) {
+        etag_err = true;
+        out += "{\"key\": " + bf::jstr(key) + ", \"error\": \"etag\", \"detail\": " + bf::jstr(ex.what()) + "}";
+      } catch (const ParseError& ex) {
+        other_err = true;
+        out += "{\"key\": " + bf::jstr(key) + ", \"error\": \"invalid\", \"detail\": " +
+               bf::jstr(std::string("invalid JSON: ") + ex.what()) + "}";
+      }
+    }
+    out += "]";
+    r.send(etag_err ? 412 : other_err ? 400 : 200, {{"content-type", "application/json"}}, out);
     return true;
   }
 

@@ -315,27 +315,86 @@ class DocStore {
 
   // Column export for the GPU scan path: one (seq-ordered) row per live document whose key
   // starts with `prefix`; returns keys and, per path, the raw JSON scalar values.
-  std::pair<std::vector<std::string>, std::vector<std::vector<std::string>>> export_columns(
-      const std::string& prefix, const std::vector<std::string>& paths) {
+  // Dictionary-encoded columns of the documents under `prefix`, in insertion (seq) order: the
+  // bulk load of the columnar query accelerator (ops/columnar.py ColumnarIndex.from_encoded).
+  // Per path: the distinct values (JSON text, in order of first appearance) and one int32 id
+  // per document (-1 = path missing).  Equality follows the query engine: numbers by value
+  // (-0.0 == 0.0), strings/booleans/null by value, arrays/objects by canonical JSON.  Two
+  // pseudo-paths: "\x00keyprefix" = the key's "<app-id>||" prefix, "\x00value" = the document.
+  struct EncodedColumn {
+    std::vector<std::string> values;
+    std::vector<int32_t> ids;
+  };
+  struct Encoded {
+    std::vector<std::string> keys;
+    std::vector<int64_t> seqs;
+    std::vector<EncodedColumn> cols;
+  };
+  Encoded encode_columns(const std::string& prefix, const std::vector<std::string>& paths) {
     std::lock_guard<std::mutex> g(mu_);
     int64_t now = now_ms();
     std::vector<std::pair<uint64_t, const std::pair<const std::string, Doc>*>> rows;
+    rows.reserve(docs_.size());
     for (auto& kv : docs_)
       if ((prefix.empty() || kv.first.compare(0, prefix.size(), prefix) == 0) && !expired(kv.second, now))
         rows.emplace_back(kv.second.seq, &kv);
     std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
-    std::vector<std::string> ks;
-    std::vector<std::vector<std::string>> cols(paths.size());
-    ks.reserve(rows.size());
-    for (auto& c : cols) c.reserve(rows.size());
+    Encoded out;
+    out.keys.reserve(rows.size());
+    out.seqs.reserve(rows.size());
     for (auto& r : rows) {
-      ks.push_back(r.second->first);
-      for (size_t i = 0; i < paths.size(); ++i) {
-        const Value* v = r.second->second.parsed.path(paths[i]);
-        cols[i].push_back(v ? dump(*v) : std::string("null"));
+      out.keys.push_back(r.second->first);
+      out.seqs.push_back((int64_t)r.first);
+    }
+    out.cols.resize(paths.size());
+    for (size_t c = 0; c < paths.size(); ++c) {
+      const std::string& path = paths[c];
+      EncodedColumn& col = out.cols[c];
+      col.ids.resize(rows.size());
+      std::unordered_map<std::string, int32_t> dict;
+      std::string k;
+      for (size_t i = 0; i < rows.size(); ++i) {
+        const std::string& key = rows[i].second->first;
+        const Value& doc = rows[i].second->second.parsed;
+        Value tmp;
+        const Value* v;
+        if (path == std::string("\x00keyprefix", 10)) {
+          size_t p = key.find("||");
+          tmp = Value::string(p == std::string::npos ? std::string() : key.substr(0, p + 2));
+          v = &tmp;
+        } else if (path == std::string("\x00value", 6)) {
+          v = doc.t == Value::Object ? nullptr : &doc;
+        } else {
+          v = doc.path(path);
+        }
+        if (!v) {
+          col.ids[i] = -1;
+          continue;
+        }
+        k.clear();
+        switch (v->t) {
+          case Value::Null: k = "n"; break;
+          case Value::Bool: k = v->b ? "b1" : "b0"; break;
+          case Value::Number: {
+            double d = v->n + 0.0;  // folds -0.0
+            uint64_t bits;
+            std::memcpy(&bits, &d, sizeof bits);
+            k.assign("d");
+            k.append(reinterpret_cast<const char*>(&bits), sizeof bits);
+            break;
+          }
+          case Value::String: k = "s"; k += v->s; break;
+          default: k = "j"; dump_to(k, *v);
+        }
+        auto it = dict.find(k);
+        if (it == dict.end()) {
+          it = dict.emplace(k, (int32_t)col.values.size()).first;
+          col.values.push_back(dump(*v));
+        }
+        col.ids[i] = it->second;
       }
     }
-    return {std::move(ks), std::move(cols)};
+    return out;
   }
 
   size_t size() {

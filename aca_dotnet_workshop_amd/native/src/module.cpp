@@ -1,5 +1,6 @@
 // Python bindings for the native state-store and broker engines (`_ttnative`).
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include "backingfront.hpp"
@@ -87,8 +88,24 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("query", &DocStore::query, py::arg("query"), py::arg("prefix") = "",
            py::call_guard<py::gil_scoped_release>())
       .def("keys", &DocStore::keys, py::arg("prefix") = "", py::arg("limit") = 0)
-      .def("export_columns", &DocStore::export_columns, py::arg("prefix"), py::arg("paths"),
-           py::call_guard<py::gil_scoped_release>())
+      .def("encode_columns",
+           [](DocStore& s, const std::string& prefix, const std::vector<std::string>& paths) {
+             DocStore::Encoded e;
+             {
+               py::gil_scoped_release r;
+               e = s.encode_columns(prefix, paths);
+             }
+             py::list cols;
+             for (auto& c : e.cols) {
+               py::array_t<int32_t> ids((py::ssize_t)c.ids.size());
+               std::memcpy(ids.mutable_data(), c.ids.data(), c.ids.size() * sizeof(int32_t));
+               cols.append(py::make_tuple(py::cast(c.values), ids));
+             }
+             py::array_t<int64_t> seqs((py::ssize_t)e.seqs.size());
+             std::memcpy(seqs.mutable_data(), e.seqs.data(), e.seqs.size() * sizeof(int64_t));
+             return py::make_tuple(py::cast(e.keys), seqs, cols);
+           },
+           py::arg("prefix"), py::arg("paths"))
       .def("size", &DocStore::size)
       .def("__len__", &DocStore::size)
       .def("compact", &DocStore::compact)

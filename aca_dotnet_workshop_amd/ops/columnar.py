@@ -105,6 +105,19 @@ def get_path(doc: Any, path: str) -> Any:
     return cur
 
 
+def filter_paths(f: Any) -> list[str]:
+    """Every document path a filter references (so all columns are encoded in one pass)."""
+    out: list[str] = []
+    if isinstance(f, dict) and len(f) == 1:
+        (op, arg), = f.items()
+        if op.upper() in ("AND", "OR") and isinstance(arg, list):
+            for x in arg:
+                out += filter_paths(x)
+        elif isinstance(arg, dict) and len(arg) == 1:
+            out.append(next(iter(arg)))
+    return out
+
+
 class Column:
     def __init__(self, path: str) -> None:
         self.path = path
@@ -192,7 +205,8 @@ class ColumnarIndex:
         self._next_seq = 0
         self.keys: list[str] = []
         self.row_of: dict[str, int] = {}
-        self.docs: list[Any] = []
+        self.docs: list[Any] | None = []  # None when columns come from `source` (bulk-encoded)
+        self.source = None  # callable(paths) -> (keys, seqs, [(values_json, ids)]) for re-encoding
         self.n = 0
         self.version = 0
         self._dev = None  # device mirror state
@@ -201,9 +215,62 @@ class ColumnarIndex:
         for p in paths:
             self.add_column(p)
 
+    # -- bulk load ------------------------------------------------------------
+    @classmethod
+    def from_source(cls, source, paths: Iterable[str]) -> "ColumnarIndex":
+        """Index built from a native bulk encoder (``DocStore.encode_columns``): no per-document
+        Python objects are kept; a column added later re-encodes from ``source``."""
+        ix = cls()
+        ix.source = source
+        ix.docs = None
+        ix._load(list(dict.fromkeys(paths)))
+        return ix
+
+    def _load(self, paths: list[str]) -> None:
+        keys, seqs, cols = self.source(paths)
+        n = len(keys)
+        cap = max(TILE, (n + TILE - 1) // TILE * TILE)
+        self.cap = cap
+        self.columns, self.col_of = [], {}
+        self.ids = np.full((len(paths), cap), -1, dtype=np.int32)
+        for i, (path, (values, ids)) in enumerate(zip(paths, cols)):
+            c = Column(path)
+            remap = np.empty(len(values), dtype=np.int32)
+            for j, text in enumerate(values):  # dictionary built by Python's own equality (vkey)
+                remap[j] = c.encode(json.loads(text))
+            ids = np.asarray(ids, dtype=np.int32)
+            self.ids[i, :n] = np.where(ids >= 0, remap[np.maximum(ids, 0)] if remap.size else -1, -1)
+            self.columns.append(c)
+            self.col_of[path] = i
+        self.live = np.zeros(cap, dtype=np.int32)
+        self.live[:n] = 1
+        self.seq = np.zeros(cap, dtype=np.int64)
+        self.seq[:n] = seqs
+        self._next_seq = int(seqs.max()) if n else 0
+        self.keys = list(keys)
+        self.row_of = dict(zip(self.keys, range(n)))
+        self.n = n
+        self.version += 1
+        self._full_dirty = True
+        self._tomb_dirty = False
+
+    def ensure_columns(self, paths: Iterable[str]) -> None:
+        """Add every missing column at once (one re-encode for a source-backed index)."""
+        missing = [p for p in dict.fromkeys(paths) if p not in self.col_of]
+        if not missing:
+            return
+        if self.docs is None:
+            self._load([c.path for c in self.columns] + missing)
+        else:
+            for p in missing:
+                self.add_column(p)
+
     # -- maintenance ----------------------------------------------------------
     def add_column(self, path: str) -> int:
         if path in self.col_of:
+            return self.col_of[path]
+        if self.docs is None:
+            self.ensure_columns([path])
             return self.col_of[path]
         c = Column(path)
         idx = len(self.columns)
@@ -237,7 +304,8 @@ class ColumnarIndex:
         old = self.row_of.get(key)
         if old is not None:
             self.live[old] = 0
-            self.docs[old] = None
+            if self.docs is not None:
+                self.docs[old] = None
             self._tomb_dirty = True
             seq = int(self.seq[old])  # an update keeps the key's original position (native engine semantics)
         else:
@@ -250,7 +318,8 @@ class ColumnarIndex:
             self.ids[i, r] = c.encode(get_path(doc, c.path))
         self.live[r] = 1
         self.keys.append(key)
-        self.docs.append(doc)
+        if self.docs is not None:
+            self.docs.append(doc)
         self.row_of[key] = r
         self.n += 1
         self.version += 1
@@ -259,7 +328,8 @@ class ColumnarIndex:
         r = self.row_of.pop(key, None)
         if r is not None:
             self.live[r] = 0
-            self.docs[r] = None
+            if self.docs is not None:
+                self.docs[r] = None
             self._tomb_dirty = True
             self.version += 1
 
@@ -279,7 +349,8 @@ class ColumnarIndex:
         self.live[:] = 0
         self.live[:len(keep)] = 1
         self.keys = [self.keys[i] for i in keep]
-        self.docs = [self.docs[i] for i in keep]
+        if self.docs is not None:
+            self.docs = [self.docs[i] for i in keep]
         self.row_of = {k: i for i, k in enumerate(self.keys)}
         self.n = len(keep)
         self.version += 1
@@ -556,8 +627,9 @@ class ColumnarIndex:
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""
         sort = q.get("sort")
-        for s in sort or []:
-            self.add_column(s["key"])  # before the device sync, so one upload covers filter + sort
+        # every referenced column first: one re-encode (source-backed) and one device upload
+        self.ensure_columns(filter_paths(q.get("filter")) + [s["key"] for s in sort or []
+                                                             if isinstance(s, dict) and "key" in s])
         prog = self.compile(q.get("filter") or {})
         page = q.get("page") or {}
         limit = int(page.get("limit") or 0)

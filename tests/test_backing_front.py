@@ -60,6 +60,13 @@ def test_documents(front, monkeypatch):
             await c.doc_put("acct", "db", "c", "q1", '{"n": 5}')
             res = await c.doc_query("acct", "db", "c", b'{"filter": {"EQ": {"n": 5}}}')
             assert b'"q1"' in res
+            # bulk save (multi-item state saves): per-item etags, 412 on any etag conflict
+            res = await c.doc_bulk_set("acct", "db", "c", [{"key": f"b{i}", "value": '{"i": %d}' % i, "etag": None,
+                                                             "firstWrite": False, "ttlMs": 0} for i in range(3)])
+            assert [x["key"] for x in res] == ["b0", "b1", "b2"] and all(x.get("etag") for x in res)
+            with pytest.raises(EtagConflict):
+                await c.doc_bulk_set("acct", "db", "c", [{"key": "b0", "value": "1", "etag": "nope"}])
+            assert (await c.doc_get("acct", "db", "c", "b2"))[0] == b'{"i": 2}'
             fs = (await c.http.get(b.base + "/admin/front")).json()
             assert fs["front"] == front
             if front == "native":
