@@ -29,7 +29,6 @@ import hmac
 import logging
 import os
 import secrets
-import uuid
 from pathlib import Path
 from typing import Any
 from urllib.parse import quote
@@ -41,7 +40,7 @@ from ...models.dotnet import is_guid, naive_utc
 from ...sdk import SidecarClient
 from ...web.app import WebApp
 from ...web.client import HttpClient
-from ...web.http import HTTPError, Request, Response, html_response, redirect
+from ...web.http import HTTPError, Request, Response, redirect
 from ..hosting import create_host, run_host
 
 ROLE = "tasksmanager-frontend-webapp"

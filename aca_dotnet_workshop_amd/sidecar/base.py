@@ -5,7 +5,7 @@ from __future__ import annotations
 import os
 import re
 from dataclasses import dataclass, field
-from typing import Any, Callable
+from typing import Callable
 from urllib.parse import urlsplit
 
 from ..backing.client import BackingClient, backing_url
