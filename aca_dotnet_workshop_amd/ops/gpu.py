@@ -27,6 +27,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_scan_eval.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
     lib.tt_launch_scan_compact.restype = ctypes.c_int
+    lib.tt_launch_scan_select.argtypes = [P, I64, P, P, I32, P, I32, P, P, P, P, P]
+    lib.tt_launch_scan_select.restype = ctypes.c_int
     lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
     lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P, I32, P]
@@ -82,6 +84,8 @@ class GpuKernels:
             raise ValueError("column table must be int64 [ncols, 2]")
         if prog.dtype != torch.int32 or prog.ndim != 2 or prog.shape[1] != 4:
             raise ValueError("program must be int32 [L, 4]")
+        if not return_mask:
+            return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
         mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
         rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
@@ -100,6 +104,29 @@ class GpuKernels:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
         out = out[:total]
         return (out, mask) if return_mask else out
+
+    def _select_fused(self, table, live16, capacity: int, nrows: int, prog, bitmaps, tiles: int):
+        """Single pass (``tt_scan_select``): evaluation + compaction with decoupled look-back;
+        one host sync (the selected count) instead of a mid-pipeline scan and sync."""
+        torch = self.torch
+        work = torch.zeros(tiles + 2, dtype=torch.int64, device=self.device)  # tile status + ticket + total
+        out = self._out_buffer(capacity)
+        rc = self.lib.tt_launch_scan_select(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
+                                            bitmaps.data_ptr(), bitmaps.numel(), work.data_ptr(),
+                                            work[tiles:].data_ptr(), out.data_ptr(), work[tiles + 1:].data_ptr(),
+                                            self._stream())
+        if rc != 0:
+            raise RuntimeError(f"tt_scan_select launch failed ({rc})")
+        total = int(work[tiles + 1].item())
+        return out[:total]
+
+    def _out_buffer(self, capacity: int):
+        """Result buffer reused across queries (grows with the collection); callers that keep
+        a selection across queries must copy it."""
+        buf = getattr(self, "_out", None)
+        if buf is None or buf.numel() < capacity:
+            buf = self._out = self.torch.empty(capacity, dtype=self.torch.int32, device=self.device)
+        return buf
 
     def group_count(self, table, g: int, mask, nrows: int, ngroups: int):
         torch = self.torch

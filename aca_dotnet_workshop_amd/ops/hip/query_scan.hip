@@ -237,6 +237,124 @@ tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask view
   for (int i = t; i < total; i += kBlock) dst[i] = staged[i];
 }
 
+// ---------------------------------------------------------------------------------------
+// tt_scan_select: filter evaluation + order-preserving compaction in ONE pass (no selection
+// mask round trip through HBM, no separate scan of tile counts, no host sync in between).
+// Tiles are claimed through an atomic ticket, so every tile's predecessors have already
+// started; each tile publishes its count (flag 1) and then its inclusive prefix (flag 2) in
+// `status`, and finds its own offset by decoupled look-back over the predecessors' words
+// (one wave reads 64 of them at a time).  The selection bits of the tile stay in LDS and are
+// compacted exactly like tt_scan_compact.  The last tile writes the total.
+namespace {
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagPrefix = 2ull << 62, kValueMask = (1ull << 62) - 1;
+constexpr int kSelectBlock = 256;   // 4 waves: 2 row groups of 16 rows per lane for the scan,
+                                    // 32 selection bits per thread for the compaction
+static_assert(kSelectBlock * kRowsPerLane * 2 == kTileRows, "tile = 256 lanes x 2 groups x 16 rows");
+static_assert(kSelectBlock * 32 == kTileRows, "compaction takes 32 bits per thread");
+
+__device__ __forceinline__ uint64_t load_status(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kSelectBlock)
+tt_scan_select(const ColumnDesc* __restrict__ cols, int64_t nrows, int64_t ntiles,
+               const uint16_t* __restrict__ live, const int32_t* __restrict__ prog, int32_t prog_len,
+               const uint32_t* __restrict__ bitmaps, int32_t bitmap_words,
+               uint64_t* __restrict__ status,      // ntiles words, zeroed
+               uint32_t* __restrict__ ticket,      // zeroed
+               int32_t* __restrict__ out, int64_t* __restrict__ total) {
+  extern __shared__ uint32_t lds_bitmaps[];
+  __shared__ uint16_t sel_bits[kTileRows / 16];       // 1 KiB: the tile's selection
+  __shared__ int32_t staged[kTileRows];               // 32 KiB: selected row ids, tile order
+  __shared__ int32_t wave_sums[kSelectBlock / 64];
+  __shared__ int64_t tile_s, offset_s;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) tile_s = (int64_t)atomicAdd(ticket, 1u);
+  const bool in_lds = bitmap_words <= kMaxLdsBitmapWords;
+  if (in_lds)
+    for (int i = t; i < bitmap_words; i += kSelectBlock) lds_bitmaps[i] = bitmaps[i];
+  __syncthreads();
+  const int64_t tile = tile_s;
+  // ---- evaluate: 2 groups of 16 rows per lane, all leaf loads of both groups in flight
+  int64_t row0[2];
+  uint16_t lv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    row0[u] = tile * kTileRows + (int64_t)u * (kSelectBlock * kRowsPerLane) + (int64_t)t * kRowsPerLane;
+    lv[u] = live[row0[u] >> 4];
+  }
+  uint32_t m[2];
+  if (in_lds) run_program<2>(cols, prog, prog_len, lds_bitmaps, row0, m);
+  else run_program<2>(cols, prog, prog_len, bitmaps, row0, m);
+  int32_t local = 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const uint32_t sel = row0[u] < nrows ? (m[u] & (uint32_t)lv[u]) : 0u;
+    sel_bits[u * kSelectBlock + t] = (uint16_t)sel;
+    local += __popc(sel);
+  }
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if (lane == 0) wave_sums[wave] = local;
+  __syncthreads();
+  const int32_t count = wave_sums[0] + wave_sums[1] + wave_sums[2] + wave_sums[3];
+  // ---- publish the aggregate, then look back for the exclusive prefix (wave 0)
+  if (wave == 0) {
+    if (lane == 0) store_status(&status[tile], (tile == 0 ? kFlagPrefix : kFlagAgg) | (uint64_t)count);
+    int64_t exclusive = 0;
+    int64_t j = tile - 1;
+    while (j >= 0) {
+      // lane l inspects predecessor j - l; spin until every inspected word carries a flag
+      const int64_t idx = j - lane;
+      uint64_t w = idx >= 0 ? load_status(&status[idx]) : kFlagPrefix;
+      while (__any(w >> 62 == 0)) {
+        if (w >> 62 == 0) w = load_status(&status[idx]);
+      }
+      // nearest lane (lowest l) holding an inclusive prefix ends the walk
+      const uint64_t have_prefix = __ballot(w >> 62 == 2);
+      const int stop = have_prefix ? __ffsll((unsigned long long)have_prefix) - 1 : 64;
+      int64_t v = lane <= stop && lane < 64 ? (int64_t)(w & kValueMask) : 0;
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      exclusive += __shfl(v, 0, 64);
+      if (have_prefix) break;
+      j -= 64;
+    }
+    if (lane == 0) {
+      if (tile != 0) store_status(&status[tile], kFlagPrefix | (uint64_t)(exclusive + count));
+      offset_s = exclusive;
+      if (tile == ntiles - 1) *total = exclusive + count;
+    }
+  }
+  __syncthreads();
+  // ---- compaction from the LDS selection bits (as tt_scan_compact)
+  const uint32_t bits = (uint32_t)sel_bits[2 * t] | ((uint32_t)sel_bits[2 * t + 1] << 16);
+  const int32_t cnt = __popc(bits);
+  int32_t incl = cnt;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  __syncthreads();  // wave_sums reuse
+  if (lane == 63) wave_sums[wave] = incl;
+  __syncthreads();
+  int32_t base = 0;
+  for (int w = 0; w < wave; ++w) base += wave_sums[w];
+  int32_t pos = base + incl - cnt;
+  const int32_t row_base = (int32_t)(tile * kTileRows) + t * 32;
+  uint32_t b = bits;
+  while (b) {
+    const int k = __ffs(b) - 1;
+    staged[pos++] = row_base + k;
+    b &= b - 1;
+  }
+  __syncthreads();
+  int32_t* dst = out + offset_s;
+  for (int i = t; i < count; i += kSelectBlock) dst[i] = staged[i];
+}
+
 // Grouped count: histogram of column `g` dictionary ids over the selected rows (the
 // "open tasks per assignee" dashboard aggregate).  LDS-privatised counters for dictionaries
 // up to 8192 entries, global atomics otherwise.
@@ -312,6 +430,21 @@ extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int64_t* block
   if (tiles == 0) return 0;
   hipLaunchKernelGGL(tt_scan_compact, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
                      reinterpret_cast<const uint32_t*>(mask), block_offsets, out);
+  return (int)hipGetLastError();
+}
+
+// `status` (ntiles uint64) and `ticket` must be zeroed; `out` holds up to nrows ids; the
+// selected count lands in `total` (device int64).
+extern "C" int tt_launch_scan_select(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* prog,
+                                     int32_t prog_len, const uint32_t* bitmaps, int32_t bitmap_words, uint64_t* status,
+                                     uint32_t* ticket, int32_t* out, int64_t* total, hipStream_t stream) {
+  if (prog_len <= 0 || nrows < 0 || bitmap_words <= 0) return -1;
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles == 0) return 0;
+  const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
+  hipLaunchKernelGGL(tt_scan_select, dim3((unsigned)tiles), dim3(kSelectBlock), lds, stream,
+                     reinterpret_cast<const ColumnDesc*>(cols), nrows, tiles, live, prog, prog_len, bitmaps,
+                     bitmap_words, status, ticket, out, total);
   return (int)hipGetLastError();
 }
 
