@@ -18,7 +18,7 @@ import logging
 import os
 from typing import Any
 
-from ..ops.columnar import ColumnarIndex, Unsupported
+from ..ops.columnar import ColumnarIndex, Unsupported, filter_paths
 
 log = logging.getLogger("backing.accel")
 PREFIX_PATH = "\x00keyprefix"
@@ -94,11 +94,12 @@ class CollectionAccelerator:
             return False
         return self.index is not None or len(store) >= self.min_docs
 
-    def build(self, store) -> None:
+    def build(self, store, paths: list[str] = ()) -> None:
         if self.before_build is not None:
             self.before_build()
-        # native bulk encode (DocStore.encode_columns): no per-document Python objects
-        ix = ColumnarIndex.from_source(lambda paths: store.encode_columns("", paths), [PREFIX_PATH])
+        # native bulk encode (DocStore.encode_columns, one thread per column) of every column the
+        # triggering query needs: no per-document Python objects
+        ix = ColumnarIndex.from_source(lambda ps: store.encode_columns("", ps), [PREFIX_PATH, *paths])
         self.index = ix
         log.info("built columnar index over %d documents", ix.live_rows())
 
@@ -108,7 +109,8 @@ class CollectionAccelerator:
             self.stats["native"] += 1
             return None
         if self.index is None:
-            self.build(store)
+            self.build(store, filter_paths(q.get("filter")) + [s["key"] for s in q.get("sort") or []
+                                                               if isinstance(s, dict) and "key" in s])
         flt = q.get("filter") or {}
         if prefix:
             flt = {"AND": [{"EQ": {PREFIX_PATH: prefix}}, flt]} if flt else {"EQ": {PREFIX_PATH: prefix}}

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <optional>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -326,7 +327,8 @@ class DocStore {
     std::vector<int32_t> ids;
   };
   struct Encoded {
-    std::vector<std::string> keys;
+    std::string key_blob;          // all keys concatenated (seq order)
+    std::vector<int64_t> key_off;  // n + 1 offsets into key_blob
     std::vector<int64_t> seqs;
     std::vector<EncodedColumn> cols;
   };
@@ -340,14 +342,17 @@ class DocStore {
         rows.emplace_back(kv.second.seq, &kv);
     std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
     Encoded out;
-    out.keys.reserve(rows.size());
+    out.key_off.reserve(rows.size() + 1);
     out.seqs.reserve(rows.size());
+    out.key_off.push_back(0);
     for (auto& r : rows) {
-      out.keys.push_back(r.second->first);
+      out.key_blob += r.second->first;
+      out.key_off.push_back((int64_t)out.key_blob.size());
       out.seqs.push_back((int64_t)r.first);
     }
     out.cols.resize(paths.size());
-    for (size_t c = 0; c < paths.size(); ++c) {
+    // one worker thread per column (read-only over the locked store)
+    auto encode_one = [&](size_t c) {
       const std::string& path = paths[c];
       EncodedColumn& col = out.cols[c];
       col.ids.resize(rows.size());
@@ -393,6 +398,13 @@ class DocStore {
         }
         col.ids[i] = it->second;
       }
+        };
+    if (paths.size() <= 1 || rows.size() < 100000) {
+      for (size_t c = 0; c < paths.size(); ++c) encode_one(c);
+    } else {
+      std::vector<std::thread> ts;
+      for (size_t c = 0; c < paths.size(); ++c) ts.emplace_back(encode_one, c);
+      for (auto& t : ts) t.join();
     }
     return out;
   }

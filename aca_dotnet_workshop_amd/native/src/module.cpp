@@ -103,7 +103,10 @@ PYBIND11_MODULE(_ttnative, m) {
              }
              py::array_t<int64_t> seqs((py::ssize_t)e.seqs.size());
              std::memcpy(seqs.mutable_data(), e.seqs.data(), e.seqs.size() * sizeof(int64_t));
-             return py::make_tuple(py::cast(e.keys), seqs, cols);
+             py::array_t<int64_t> offs((py::ssize_t)e.key_off.size());
+             std::memcpy(offs.mutable_data(), e.key_off.data(), e.key_off.size() * sizeof(int64_t));
+             // keys stay one bytes blob + offsets: no per-document Python string objects
+             return py::make_tuple(py::make_tuple(py::bytes(e.key_blob), offs), seqs, cols);
            },
            py::arg("prefix"), py::arg("paths"))
       .def("size", &DocStore::size)

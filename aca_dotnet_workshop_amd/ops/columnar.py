@@ -118,6 +118,32 @@ def filter_paths(f: Any) -> list[str]:
     return out
 
 
+class KeyTable:
+    """Row -> document key.  Bulk-loaded keys stay in one UTF-8 blob with offsets (decoded on
+    access, so a 10 M-row index holds no 10 M Python strings); appended keys go to a list."""
+
+    def __init__(self, blob: bytes = b"", offsets: np.ndarray | None = None) -> None:
+        self.blob = blob
+        self.off = offsets if offsets is not None else np.zeros(1, dtype=np.int64)
+        self.base = len(self.off) - 1
+        self.extra: list[str] = []
+
+    def __len__(self) -> int:
+        return self.base + len(self.extra)
+
+    def __getitem__(self, i: int) -> str:
+        if i < self.base:
+            return self.blob[self.off[i]:self.off[i + 1]].decode()
+        return self.extra[i - self.base]
+
+    def append(self, key: str) -> None:
+        self.extra.append(key)
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+
 class Column:
     def __init__(self, path: str) -> None:
         self.path = path
@@ -203,8 +229,8 @@ class ColumnarIndex:
         self.live = np.zeros(self.cap, dtype=np.int32)
         self.seq = np.zeros(self.cap, dtype=np.int64)
         self._next_seq = 0
-        self.keys: list[str] = []
-        self.row_of: dict[str, int] = {}
+        self.keys: KeyTable | list[str] = []
+        self._row_of: dict[str, int] | None = {}
         self.docs: list[Any] | None = []  # None when columns come from `source` (bulk-encoded)
         self.source = None  # callable(paths) -> (keys, seqs, [(values_json, ids)]) for re-encoding
         self.n = 0
@@ -228,7 +254,7 @@ class ColumnarIndex:
 
     def _load(self, paths: list[str]) -> None:
         keys, seqs, cols = self.source(paths)
-        n = len(keys)
+        n = len(seqs)
         cap = max(TILE, (n + TILE - 1) // TILE * TILE)
         self.cap = cap
         self.columns, self.col_of = [], {}
@@ -247,12 +273,21 @@ class ColumnarIndex:
         self.seq = np.zeros(cap, dtype=np.int64)
         self.seq[:n] = seqs
         self._next_seq = int(seqs.max()) if n else 0
-        self.keys = list(keys)
-        self.row_of = dict(zip(self.keys, range(n)))
+        if isinstance(keys, tuple):  # (blob, offsets) from DocStore.encode_columns
+            self.keys = KeyTable(keys[0], np.asarray(keys[1], dtype=np.int64))
+        else:
+            self.keys = list(keys)
+        self._row_of = None  # built on the first write (read-only use never needs it)
         self.n = n
         self.version += 1
         self._full_dirty = True
         self._tomb_dirty = False
+
+    @property
+    def row_of(self) -> dict[str, int]:
+        if self._row_of is None:
+            self._row_of = {self.keys[r]: r for r in np.nonzero(self.live[:self.n])[0].tolist()}
+        return self._row_of
 
     def ensure_columns(self, paths: Iterable[str]) -> None:
         """Add every missing column at once (one re-encode for a source-backed index)."""
@@ -338,7 +373,7 @@ class ColumnarIndex:
             self.upsert(k, d)
 
     def live_rows(self) -> int:
-        return len(self.row_of)
+        return int(np.count_nonzero(self.live[:self.n]))
 
     def compact(self) -> None:
         """Drop tombstones (rows are renumbered in order)."""
@@ -348,10 +383,10 @@ class ColumnarIndex:
         self.seq[:len(keep)] = self.seq[keep]
         self.live[:] = 0
         self.live[:len(keep)] = 1
-        self.keys = [self.keys[i] for i in keep]
+        self.keys = [self.keys[i] for i in keep.tolist()]
         if self.docs is not None:
             self.docs = [self.docs[i] for i in keep]
-        self.row_of = {k: i for i, k in enumerate(self.keys)}
+        self._row_of = {k: i for i, k in enumerate(self.keys)}
         self.n = len(keep)
         self.version += 1
         self._full_dirty = True
