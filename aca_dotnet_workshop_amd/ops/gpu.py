@@ -56,6 +56,10 @@ class GpuKernels:
         self.tile_rows = int(self.lib.tt_tile_rows())
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
+        # Single-pass select (tt_scan_select, decoupled look-back) is opt-in: measured 1.40 ms vs
+        # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
+        # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
+        self.fused_select = False
 
     def set_eval_groups(self, u: int) -> None:
         """Row groups per lane in ``tt_scan_eval`` (1, 2 or 4): registers vs loads in flight."""
@@ -84,7 +88,7 @@ class GpuKernels:
             raise ValueError("column table must be int64 [ncols, 2]")
         if prog.dtype != torch.int32 or prog.ndim != 2 or prog.shape[1] != 4:
             raise ValueError("program must be int32 [L, 4]")
-        if not return_mask:
+        if self.fused_select and not return_mask:
             return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
         mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)

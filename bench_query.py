@@ -84,23 +84,25 @@ def main() -> None:
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
     selected = int(out.numel())
-    # A/B: the two-pass pipeline (tt_scan_eval -> scan of tile counts -> tt_scan_compact)
+    # A/B: the single-pass variant (tt_scan_select, decoupled look-back across tiles)
+    k.fused_select = True
     for _ in range(a.warmup):
-        two, _mask = k.select(st["table"], st["live"], ix.cap, n, code, bm, return_mask=True)
+        one = k.select(st["table"], st["live"], ix.cap, n, code, bm)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.iters):
-        two, _mask = k.select(st["table"], st["live"], ix.cap, n, code, bm, return_mask=True)
+        one = k.select(st["table"], st["live"], ix.cap, n, code, bm)
     torch.cuda.synchronize()
-    two_pass_ms = (time.perf_counter() - t0) / a.iters * 1e3
-    same = bool(torch.equal(two, out))
+    k.fused_select = False
+    single_pass_ms = (time.perf_counter() - t0) / a.iters * 1e3
+    same = bool(torch.equal(one, out))
     # bytes: referenced columns at their narrow widths + liveness bit + mask write & read + output indices
     widths = sum(st["widths"][c] for c in prog.columns)
     nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
-           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "two_pass_ms": round(two_pass_ms, 4),
-           "fused_matches_two_pass": same, "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths}
+           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "single_pass_ms": round(single_pass_ms, 4),
+           "single_pass_matches": same, "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order
         ix._full_dirty = True

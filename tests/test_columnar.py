@@ -216,6 +216,24 @@ def test_gpu_scan_matches_numpy(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 8193, 300_001])
+def test_gpu_single_pass_select_matches(n):
+    """tt_scan_select (one pass, decoupled look-back) == the two-pass pipeline."""
+    k = _kernels()
+    ix = _random_collection(n, random.Random(n + 7))
+    try:
+        for f in GPU_FILTERS:
+            prog = ix.compile(f)
+            k.fused_select = False
+            want = ix.select_gpu(prog, k)
+            k.fused_select = True
+            got = ix.select_gpu(prog, k)
+            assert np.array_equal(got, want), (n, f)
+    finally:
+        k.fused_select = False
+
+
+@pytest.mark.gpu
 def test_gpu_query_matches_native_engine():
     k = _kernels()
     rnd = random.Random(7)
