@@ -73,37 +73,6 @@ __device__ __forceinline__ void load16(const ColumnDesc& cd, int64_t row0, int32
 
 }  // namespace
 
-// SWAR equality: lane bit i set iff packed id i == v.  For bytes: x = w ^ (v * 0x01010101) has a
-// zero byte exactly where the ids match; ((x & 0x7f..) + 0x7f..) | x sets each byte's top bit
-// iff that byte is non-zero (no carries cross bytes), so its complement's top bits mark the
-// matches.  The "missing" code (all ones) never equals a dictionary id v < 255 / 65535.
-__device__ __forceinline__ uint32_t top_bits_u8(uint32_t z) {  // bits 7,15,23,31 -> 0..3
-  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-}
-__device__ __forceinline__ uint32_t eq_mask_u8(const uint4 w, uint32_t v) {
-  const uint32_t pat = v * 0x01010101u;
-  const uint32_t d[4] = {w.x ^ pat, w.y ^ pat, w.z ^ pat, w.w ^ pat};
-  uint32_t m = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t nz = ((d[q] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d[q];
-    m |= top_bits_u8(~nz & 0x80808080u) << (4 * q);
-  }
-  return m;
-}
-__device__ __forceinline__ uint32_t eq_mask_u16(const uint4 a, const uint4 b, uint32_t v) {
-  const uint32_t pat = v * 0x00010001u;
-  const uint32_t d[8] = {a.x ^ pat, a.y ^ pat, a.z ^ pat, a.w ^ pat, b.x ^ pat, b.y ^ pat, b.z ^ pat, b.w ^ pat};
-  uint32_t m = 0;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint32_t nz = ((d[q] & 0x7FFF7FFFu) + 0x7FFF7FFFu) | d[q];
-    const uint32_t z = ~nz & 0x80008000u;
-    m |= (((z >> 15) & 1u) | ((z >> 30) & 2u)) << (2 * q);
-  }
-  return m;
-}
-
 // Leaf test for 16 rows against a dictionary-id bitmap.  Dictionaries of <= 64 ids use a
 // register-resident 64-bit copy of the bitmap (no memory traffic per row); larger ones probe
 // the bitmap words, which the kernel staged in LDS when they fit (`bm` then points to LDS).
@@ -143,28 +112,7 @@ __device__ __forceinline__ void run_program(const ColumnDesc* __restrict__ cols,
     const int32_t a = prog[pc * 4 + 1];
     const int32_t b = prog[pc * 4 + 2];
     const int32_t c = prog[pc * 4 + 3];
-    if (op == OP_EQ && cols[a].width <= 2) {
-      // equality on a narrow column: SWAR compare of 4 (bytes) / 2 (shorts) ids per dword, no
-      // per-row id extraction (the scan is VALU-bound, profiles/r1_query_scan_pmc.md)
-      const ColumnDesc cd = cols[a];
-      uint4 raw[U][2];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (cd.width == 1) {
-          raw[u][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(cd.ptr) + row0[u]);
-        } else {
-          const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(cd.ptr) + row0[u]);
-          raw[u][0] = p[0];
-          raw[u][1] = p[1];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t m = b < 0 ? 0u : (cd.width == 1 ? eq_mask_u8(raw[u][0], (uint32_t)b)
-                                                       : eq_mask_u16(raw[u][0], raw[u][1], (uint32_t)b));
-        st[u] = (st[u] << 16) | (u128)m;
-      }
-    } else if (op == OP_LEAF || op == OP_EQ) {
+    if (op == OP_LEAF || op == OP_EQ) {
       const ColumnDesc cd = cols[a];
       int32_t ids[U][16];
 #pragma unroll
