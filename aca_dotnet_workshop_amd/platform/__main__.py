@@ -12,6 +12,7 @@ equivalent CLI.
     outputs   --env-dir DIR
     down      --env-dir DIR [--delete]                       stop (and delete = az group delete)
     appmap / failures / performance --env-dir DIR            telemetry views (App Insights blades)
+    metrics   [APP] --env-dir DIR [--interval S]             live metrics: request/failure/delivery rates, CPU
 """
 from __future__ import annotations
 
@@ -235,6 +236,55 @@ def cmd_down(a) -> int:
     return 0
 
 
+def live_rates(s0: dict, s1: dict) -> dict[str, dict[str, float]]:
+    """Per-app rates between two /metrics/live snapshots."""
+    dt = max(1e-6, s1["ts"] - s0["ts"])
+    out: dict[str, dict[str, float]] = {}
+
+    def tot(snap, app, part, key):
+        return sum(r.get(part, {}).get(key, 0.0) for r in snap["apps"].get(app, {}).values())
+
+    def fails(snap, app):
+        n = 0.0
+        for r in snap["apps"].get(app, {}).values():
+            for k, v in r.get("app", {}).items():
+                if k.startswith("http_requests_total{") and 'status="5' in k:
+                    n += v
+        return n
+
+    for app in s1["apps"]:
+        out[app] = {
+            "replicas": len(s1["apps"][app]),
+            "requests_per_s": (tot(s1, app, "app", "http_requests_total") - tot(s0, app, "app", "http_requests_total")) / dt,
+            "failures_per_s": (fails(s1, app) - fails(s0, app)) / dt,
+            "sidecar_native_per_s": (tot(s1, app, "sidecar", "sidecar_native_requests_total")
+                                     - tot(s0, app, "sidecar", "sidecar_native_requests_total")) / dt,
+            "cpu_cores": (sum(r.get("cpuSeconds", 0.0) for r in s1["apps"][app].values())
+                          - sum(r.get("cpuSeconds", 0.0) for r in s0["apps"].get(app, {}).values())) / dt,
+        }
+    return out
+
+
+def cmd_metrics(a) -> int:
+    st, s0 = _uds_request(_ctl(a.env_dir), "GET", "/metrics/live")
+    if st != 200:
+        print(json.dumps(s0), file=sys.stderr)
+        return 1
+    time.sleep(a.interval)
+    st, s1 = _uds_request(_ctl(a.env_dir), "GET", "/metrics/live")
+    rates = live_rates(s0, s1)
+    if a.app:
+        rates = {k: v for k, v in rates.items() if k == a.app}
+    if a.json:
+        print(json.dumps(rates, indent=1))
+        return 0
+    print(f"{'app':36} {'repl':>4} {'req/s':>10} {'fail/s':>8} {'native/s':>10} {'cpu':>6}")
+    for app, r in sorted(rates.items()):
+        print(f"{app:36} {r['replicas']:>4} {r['requests_per_s']:>10.1f} {r['failures_per_s']:>8.1f} "
+              f"{r['sidecar_native_per_s']:>10.1f} {r['cpu_cores']:>6.2f}")
+    return 0
+
+
 def cmd_telemetry(a) -> int:
     from ..telemetry import appmap
     tdir = Path(a.env_dir) / "telemetry"
@@ -290,6 +340,12 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("app")
     p.add_argument("--env-dir", required=True)
     p.set_defaults(fn=cmd_restart)
+    p = sub.add_parser("metrics")
+    p.add_argument("app", nargs="?")
+    p.add_argument("--env-dir", required=True)
+    p.add_argument("--interval", type=float, default=2.0)
+    p.add_argument("--json", action="store_true")
+    p.set_defaults(fn=cmd_metrics)
     p = sub.add_parser("logs")
     p.add_argument("app")
     p.add_argument("--env-dir", required=True)

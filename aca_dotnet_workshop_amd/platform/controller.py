@@ -403,6 +403,40 @@ class EnvironmentController:
                 "uptimeSeconds": round(time.time() - self.started, 1), "apps": apps,
                 "outputs": self.m.outputs(), "events": self.events[-30:]}
 
+    async def live_metrics(self) -> dict[str, Any]:
+        """Live Metrics snapshot (App Insights' Live Metrics blade): per replica, the sidecar's and
+        the app's Prometheus counters plus CPU seconds of the replica's processes."""
+        import psutil
+
+        from ..telemetry.metrics import parse_exposition
+        from ..web.client import HttpClient
+        http = HttpClient(timeout=2.0)
+        out: dict[str, Any] = {"ts": time.time(), "apps": {}}
+        try:
+            for rt in self.apps.values():
+                reps = {}
+                for r in (rt.current.replicas if rt.current else []):
+                    if not r.alive():
+                        continue
+                    rec: dict[str, Any] = {}
+                    for label, url in (("sidecar", f"unix:{r.sidecar_uds}:/metrics"),
+                                       ("app", f"unix:{self.stack.sock_dir / (r.name + '.a.sock')}:/metrics")):
+                        try:
+                            resp = await http.get(url)
+                            rec[label] = parse_exposition(resp.text) if resp.status == 200 else {}
+                        except Exception:
+                            rec[label] = {}
+                    try:
+                        procs = [psutil.Process(r.proc.pid)] + psutil.Process(r.proc.pid).children(recursive=True)
+                        rec["cpuSeconds"] = sum(sum(p.cpu_times()[:2]) for p in procs)
+                    except psutil.Error:
+                        rec["cpuSeconds"] = 0.0
+                    reps[r.name] = rec
+                out["apps"][rt.name] = reps
+        finally:
+            await http.close()
+        return out
+
     def _write_state(self) -> None:
         st = {"desired": desired_state(self.m), "status": self.status()}
         tmp = self.dir / "state.json.tmp"
@@ -475,7 +509,11 @@ class EnvironmentController:
             asyncio.get_running_loop().call_later(0.05, ctl.stop_event.set)
             return empty(202)
 
+        async def live(req: Request) -> Response:
+            return json_response(await ctl.live_metrics())
+
         app.add_route("/status", status, ("GET",))
+        app.add_route("/metrics/live", live, ("GET",))
         app.add_route("/apps/{app}/scale", scale, ("POST",))
         app.add_route("/apps/{app}/restart", restart, ("POST",))
         app.add_route("/apply", do_apply, ("POST",))

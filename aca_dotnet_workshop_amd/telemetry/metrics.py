@@ -143,3 +143,22 @@ def metrics_middleware(registry: Registry = REGISTRY):
         lat.observe_key(time.perf_counter() - t0, k[1])
         return resp
     return mw
+
+
+def parse_exposition(text: str) -> dict[str, float]:
+    """Sum every sample of a Prometheus text exposition by ``name{label=...}`` -> value and by
+    bare metric name (``name`` -> total over label sets); histogram ``_count``/``_sum`` kept."""
+    out: dict[str, float] = {}
+    for line in text.splitlines():
+        if not line or line.startswith("#"):
+            continue
+        try:
+            series, value = line.rsplit(" ", 1)
+            v = float(value)
+        except ValueError:
+            continue
+        out[series] = out.get(series, 0.0) + v
+        name = series.split("{", 1)[0]
+        if name != series:
+            out[name] = out.get(name, 0.0) + v
+    return out

@@ -136,6 +136,15 @@ def test_environment_lifecycle(tmp_path):
                     break
             assert peak == 5
             assert c["completed"] == 800 and c["dead_letter"] == 0
+            # live metrics (App Insights Live Metrics): native deliveries counted per replica
+            from aca_dotnet_workshop_amd.platform.__main__ import live_rates
+            s0 = await ctl.live_metrics()
+            procs = s0["apps"]["tasksmanager-backend-processor"]
+            assert sum(r["sidecar"].get("sidecar_native_requests_total", 0) for r in procs.values()) >= 800
+            assert all(r["cpuSeconds"] > 0 for r in procs.values())
+            s1 = await ctl.live_metrics()
+            rates = live_rates(s0, s1)
+            assert rates["tasksmanager-backend-processor"]["replicas"] == len(s1["apps"]["tasksmanager-backend-processor"])
             for _ in range(100):
                 await asyncio.sleep(0.1)
                 if len([r for r in proc.current.replicas if r.alive()]) == 1:
