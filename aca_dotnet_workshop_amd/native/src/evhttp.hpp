@@ -173,6 +173,9 @@ class MsgParser {
   explicit MsgParser(bool request) : request_(request) {}
   void expect_no_body() { no_body_ = true; }  // response to HEAD
   std::string error;
+  // Set when a request head carrying "Expect: 100-continue" was parsed and its body is still
+  // pending; the server answers "100 Continue" once and clears it.
+  bool continue_wanted = false;
 
   // Consume bytes from buf[off..]; returns DONE with `out` filled when a full message is in.
   Result feed(const std::string& buf, size_t& off, Message& out) {
@@ -200,6 +203,10 @@ class MsgParser {
             return fail(ex.what());
           }
           off = e + 4;
+          if (request_) {
+            auto* ex = msg_.header("expect");
+            if (ex && (*ex == "100-continue" || *ex == "100-Continue")) continue_wanted = true;
+          }
           auto* te = msg_.header("transfer-encoding");
           auto* cl = msg_.header("content-length");
           bool bodyless = no_body_ || (!request_ && (msg_.status == 204 || msg_.status == 304 || msg_.status < 200));
@@ -490,6 +497,14 @@ class ServerConn : public IoObj {
     while (!dead && !close_after_write_ && pending_.size() < 64) {
       Message m;
       auto r = parser_.feed(in_, in_off_, m);
+      if (parser_.continue_wanted) {  // client waits for this before sending the body
+        parser_.continue_wanted = false;
+        if (r == MsgParser::NEED_MORE && pending_.empty()) {
+          out_ += "HTTP/1.1 100 Continue\r\n\r\n";
+          flush();
+          if (dead) return;
+        }
+      }
       if (r == MsgParser::NEED_MORE) break;
       if (r == MsgParser::ERROR) {
         std::string w;

@@ -286,6 +286,22 @@ def test_native_http_framing(tmp_path):
             assert r.json() == "chunk"
             m = await e.http.get(f"{e.base['app-a']}/metrics")
             assert b"sidecar_native_requests_total" in m.body
+            # Expect: 100-continue -> interim response before the body is sent
+            body = b'[{"key":"x","value":2}]'
+
+            def expect_continue():
+                s = socket.create_connection(("127.0.0.1", port), timeout=5)
+                s.sendall(b"POST /v1.0/state/statestore HTTP/1.1\r\nHost: x\r\nExpect: 100-continue\r\n"
+                          b"Content-Length: %d\r\n\r\n" % len(body))
+                first = s.recv(4096)
+                s.sendall(body)
+                rest = b""
+                while b"\r\n\r\n" not in rest:
+                    rest += s.recv(4096)
+                s.close()
+                return first, rest
+            first, rest = await loop.run_in_executor(None, expect_continue)
+            assert first.startswith(b"HTTP/1.1 100 Continue") and rest.startswith(b"HTTP/1.1 204")
     run(main())
 
 
