@@ -21,7 +21,7 @@ from typing import Any, Iterable
 
 import numpy as np
 
-OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ = 1, 2, 3, 4, 5, 6
+OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ, OP_RANGE = 1, 2, 3, 4, 5, 6, 7
 TILE = 8192           # rows per kernel tile (ops/hip/query_scan.hip kTileRows)
 MAX_DEPTH = 8         # device stack depth (16-bit masks in a 128-bit register)
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
@@ -118,6 +118,23 @@ def filter_paths(f: Any) -> list[str]:
     return out
 
 
+def rank_interval(c: "Column", sat: np.ndarray) -> tuple[int, int] | None:
+    """A range predicate's satisfying dictionary ids as a half-open interval of sort ranks, when
+    they are exactly the ids whose rank falls in it (values of one JSON type are contiguous in
+    the sort order, so GT/GTE/LT/LTE always are)."""
+    if sat.size == 0:
+        return None
+    ranks = c.ranks()
+    if not sat.any():
+        return (1, 1)  # empty interval: no row satisfies
+    r = ranks[sat]
+    lo, hi = int(r.min()), int(r.max()) + 1
+    inside = (ranks >= lo) & (ranks < hi)
+    if not np.array_equal(inside, sat):
+        return None
+    return lo, hi
+
+
 class KeyTable:
     """Row -> document key.  Bulk-loaded keys stay in one UTF-8 blob with offsets (decoded on
     access, so a 10 M-row index holds no 10 M Python strings); appended keys go to a list."""
@@ -151,6 +168,7 @@ class Column:
         self.values: list[Any] = []
         self._num_cache: np.ndarray | None = None
         self._rank_cache: np.ndarray | None = None
+        self.rank_version = 0  # bumps whenever a new value may shift the sort ranks
 
     def encode(self, v: Any) -> int:
         if v is _MISSING:
@@ -162,6 +180,7 @@ class Column:
             self.values.append(v)
             self._num_cache = None
             self._rank_cache = None
+            self.rank_version += 1
         return i
 
     def lookup(self, v: Any) -> int:
@@ -450,7 +469,13 @@ class ColumnarIndex:
                     raise Unsupported("IN expects a list")
                 leaf_bitmap(col, c.satisfying("IN", val))
             elif op in ("GT", "GTE", "LT", "LTE"):
-                leaf_bitmap(col, c.satisfying(op, val))
+                sat = c.satisfying(op, val)
+                rng = rank_interval(c, sat)
+                if rng is None:
+                    leaf_bitmap(col, sat)
+                else:  # one integer compare per row on the rank-encoded column
+                    code.append([OP_RANGE, col, rng[0], rng[1]])
+                    push()
             else:
                 raise Unsupported(f"operator {op}")
 
@@ -473,6 +498,11 @@ class ColumnarIndex:
         for op, a, b, c in prog.code.tolist():
             if op == OP_EQ:
                 stack.append(self.ids[a, :n] == b)
+            elif op == OP_RANGE:
+                v = self.ids[a, :n]
+                ranks = self.columns[a].ranks()
+                r = np.where(v >= 0, ranks[np.maximum(v, 0)] if ranks.size else -1, -1)
+                stack.append((r >= b) & (r < c))
             elif op == OP_LEAF:
                 v = self.ids[a, :n]
                 ok = (v >= 0) & (v < c)
@@ -510,7 +540,7 @@ class ColumnarIndex:
         bits = self.live[lo_word * 16:hi_word * 16].astype(np.uint8)
         return np.packbits(bits, bitorder="little").view("<u2").view(np.int16)
 
-    def to_device(self, kernels):
+    def to_device(self, kernels, rank_cols=()):
         """Sync the device mirror.  Columns are append-only between compactions, so only rows
         added since the last sync are uploaded; tombstones re-upload the 1-bit liveness mask
         (N/8 bytes); a column whose dictionary outgrows its width is re-encoded."""
@@ -544,17 +574,52 @@ class ColumnarIndex:
             st["synced"] = hi
         self._full_dirty = False
         self._tomb_dirty = False
-        table = np.array([[c.data_ptr(), w] for c, w in zip(st["cols"], st["widths"])], dtype=np.int64).reshape(-1, 2)
+        rows = [[c.data_ptr(), w] for c, w in zip(st["cols"], st["widths"])]
+        table = np.array(rows, dtype=np.int64).reshape(-1, 2)
         st["table"] = torch.from_numpy(table).to(dev)
+        if rank_cols:
+            # rank-encoded copies of the columns that range leaves read (appended to the table)
+            ranks = st.setdefault("ranks", {})
+            slot = {}
+            for col in sorted(set(rank_cols)):
+                self._sync_rank_column(kernels, st, ranks, col)
+                slot[col] = len(rows)
+                rows.append([ranks[col]["t"].data_ptr(), ranks[col]["w"]])
+            st["rank_slot"] = slot
+            st["table"] = torch.from_numpy(np.array(rows, dtype=np.int64).reshape(-1, 2)).to(dev)
         return st
+
+    def _sync_rank_column(self, kernels, st, ranks, col: int) -> None:
+        torch = kernels.torch
+        c = self.columns[col]
+        w = st["widths"][col]
+        cur = ranks.get(col)
+        full = cur is None or cur["w"] != w or cur["ver"] != c.rank_version
+        lo = 0 if full else cur["synced"]
+        if not full and lo >= self.n:
+            return
+        if full:
+            dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[w]
+            cur = ranks[col] = {"t": torch.empty(self.cap, dtype=dt, device=kernels.device), "w": w,
+                                "ver": c.rank_version, "table": None, "synced": 0}
+            table = c.ranks().astype(np.int32) if c.values else np.zeros(1, dtype=np.int32)
+            cur["table"] = torch.from_numpy(table).to(kernels.device)
+        src = torch.from_numpy(np.array([[st["cols"][col].data_ptr(), w]], dtype=np.int64)).to(kernels.device)
+        kernels.rank_encode(src, cur["table"], lo, self.n, cur["t"], w)
+        cur["synced"] = self.n
 
     def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
         torch = kernels.torch
-        leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ)
+        leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ) | (prog.code[:, 0] == OP_RANGE)
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
             raise ValueError("program references a column outside the index")
-        st = self.to_device(kernels)
-        code = torch.from_numpy(prog.code).to(kernels.device)
+        rng = prog.code[:, 0] == OP_RANGE
+        st = self.to_device(kernels, prog.code[rng, 1].tolist())
+        code_np = prog.code
+        if rng.any():  # range leaves read the rank-encoded copy of their column
+            code_np = prog.code.copy()
+            code_np[rng, 1] = [st["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
+        code = torch.from_numpy(code_np).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
         res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
         if return_mask or on_device:

@@ -39,6 +39,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_hist_bins.restype = ctypes.c_int
     lib.tt_set_eval_groups.argtypes = [ctypes.c_int]
     lib.tt_set_eval_groups.restype = ctypes.c_int
+    lib.tt_launch_rank_encode.argtypes = [P, P, I32, I64, I64, P, I32, P]
+    lib.tt_launch_rank_encode.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -108,6 +110,14 @@ class GpuKernels:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
         out = out[:total]
         return (out, mask) if return_mask else out
+
+    def rank_encode(self, src_desc, rank_table, lo: int, hi: int, dst, width: int) -> None:
+        """dst[lo:hi] = sort rank of each row's dictionary id (``hip/query_scan.hip`` tt_rank_encode);
+        ``src_desc`` is the source column's 16-byte row of the column table."""
+        rc = self.lib.tt_launch_rank_encode(src_desc.data_ptr(), rank_table.data_ptr(), rank_table.numel(), lo, hi,
+                                            dst.data_ptr(), width, self._stream())
+        if rc != 0:
+            raise RuntimeError(f"tt_rank_encode launch failed ({rc})")
 
     def _select_fused(self, table, live16, capacity: int, nrows: int, prog, bitmaps, tiles: int):
         """Single pass (``tt_scan_select``): evaluation + compaction with decoupled look-back;

@@ -32,7 +32,7 @@ static_assert(kTileRows == kBlock * 32, "compaction takes 32 mask bits per threa
 constexpr int kMaxDepth = 8;                   // 8 x 16-bit masks in a 128-bit stack
 constexpr int kMaxLdsBitmapWords = 8192;       // stage up to 32 KiB of leaf bitmaps in LDS
 
-enum Op : int32_t { OP_LEAF = 1, OP_AND = 2, OP_OR = 3, OP_NOT = 4, OP_TRUE = 5, OP_EQ = 6 };
+enum Op : int32_t { OP_LEAF = 1, OP_AND = 2, OP_OR = 3, OP_NOT = 4, OP_TRUE = 5, OP_EQ = 6, OP_RANGE = 7 };
 
 struct ColumnDesc {     // 16 bytes, host-built table
   uint64_t ptr;         // device address of the column (row 0)
@@ -112,7 +112,22 @@ __device__ __forceinline__ void run_program(const ColumnDesc* __restrict__ cols,
     const int32_t a = prog[pc * 4 + 1];
     const int32_t b = prog[pc * 4 + 2];
     const int32_t c = prog[pc * 4 + 3];
-    if (op == OP_LEAF || op == OP_EQ) {
+    if (op == OP_RANGE) {
+      // range leaf on a rank-encoded column (`a` = its table row): b <= rank < c, one unsigned
+      // compare per row instead of a bitmap probe; the missing code never falls inside
+      const ColumnDesc cd = cols[a];
+      int32_t r[U][16];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load16(cd, row0[u], r[u]);
+      const uint32_t span = (uint32_t)(c - b);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m |= (uint32_t)((uint32_t)(r[u][i] - b) < span) << i;
+        st[u] = (st[u] << 16) | (u128)m;
+      }
+    } else if (op == OP_LEAF || op == OP_EQ) {
       const ColumnDesc cd = cols[a];
       int32_t ids[U][16];
 #pragma unroll
@@ -355,6 +370,31 @@ tt_scan_select(const ColumnDesc* __restrict__ cols, int64_t nrows, int64_t ntile
   for (int i = t; i < count; i += kSelectBlock) dst[i] = staged[i];
 }
 
+// Rank encoding of one column for range leaves: dst[row] = rank_table[id] (sort rank of the
+// dictionary value, 1-based), the all-ones missing code where the path is missing.  Rank
+// table staged in LDS when it fits.  Rows [lo, hi).
+extern "C" __global__ void __launch_bounds__(kBlock)
+tt_rank_encode(const ColumnDesc* __restrict__ src, const int32_t* __restrict__ rank_table, int32_t nranks,
+               int64_t lo, int64_t hi, uint64_t dst_ptr, int32_t dst_width) {
+  extern __shared__ int32_t lds_rank[];
+  const bool staged = nranks <= 8192;
+  if (staged)
+    for (int i = threadIdx.x; i < nranks; i += kBlock) lds_rank[i] = rank_table[i];
+  __syncthreads();
+  const ColumnDesc cd = *src;
+  for (int64_t row = lo + (int64_t)blockIdx.x * kBlock + threadIdx.x; row < hi; row += (int64_t)gridDim.x * kBlock) {
+    uint32_t raw;
+    if (cd.width == 1) raw = reinterpret_cast<const uint8_t*>(cd.ptr)[row];
+    else if (cd.width == 2) raw = reinterpret_cast<const uint16_t*>(cd.ptr)[row];
+    else raw = reinterpret_cast<const uint32_t*>(cd.ptr)[row];
+    const int32_t id = id_of(raw, cd.width);
+    const int32_t r = (id >= 0 && id < nranks) ? (staged ? lds_rank[id] : rank_table[id]) : -1;
+    if (dst_width == 1) reinterpret_cast<uint8_t*>(dst_ptr)[row] = (uint8_t)(r < 0 ? 0xFF : r);
+    else if (dst_width == 2) reinterpret_cast<uint16_t*>(dst_ptr)[row] = (uint16_t)(r < 0 ? 0xFFFF : r);
+    else reinterpret_cast<int32_t*>(dst_ptr)[row] = r;
+  }
+}
+
 // Grouped count: histogram of column `g` dictionary ids over the selected rows (the
 // "open tasks per assignee" dashboard aggregate).  LDS-privatised counters for dictionaries
 // up to 8192 entries, global atomics otherwise.
@@ -458,6 +498,18 @@ extern "C" int tt_launch_group_count(const void* cols, int32_t g, const uint16_t
   const size_t lds = ngroups <= 8192 ? (size_t)ngroups * sizeof(uint32_t) : 0;
   hipLaunchKernelGGL(tt_group_count, dim3((unsigned)blocks), dim3(kBlock), lds, stream,
                      reinterpret_cast<const ColumnDesc*>(cols), g, mask, nrows, ngroups, counts);
+  return (int)hipGetLastError();
+}
+
+extern "C" int tt_launch_rank_encode(const void* src, const int32_t* rank_table, int32_t nranks, int64_t lo, int64_t hi,
+                                     void* dst, int32_t dst_width, hipStream_t stream) {
+  if (hi <= lo) return 0;
+  if (nranks < 0 || (dst_width != 1 && dst_width != 2 && dst_width != 4)) return -1;
+  int64_t blocks = (hi - lo + kBlock - 1) / kBlock;
+  if (blocks > 8192) blocks = 8192;
+  const size_t lds = nranks <= 8192 ? (size_t)nranks * sizeof(int32_t) : 0;
+  hipLaunchKernelGGL(tt_rank_encode, dim3((unsigned)blocks), dim3(kBlock), lds, stream,
+                     reinterpret_cast<const ColumnDesc*>(src), rank_table, nranks, lo, hi, (uint64_t)dst, dst_width);
   return (int)hipGetLastError();
 }
 

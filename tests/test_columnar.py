@@ -269,6 +269,29 @@ def test_gpu_ordering_matches_host(n):
 
 
 @pytest.mark.gpu
+def test_gpu_range_leaves_track_rank_shifts():
+    """Range leaves read a rank-encoded device column: new dictionary values that shift the
+    ranks of existing ones (same width) force a re-encode; plain appends are incremental."""
+    k = _kernels()
+    ix = ColumnarIndex(["v"])
+    for i in range(20000):
+        ix.upsert(str(i), {"v": (i % 3 + 1) * 10})  # 10, 20, 30
+    for f in ({"LT": {"v": 25}}, {"GTE": {"v": 20}}):
+        prog = ix.compile(f)
+        assert (prog.code[:, 0] == 7).any()  # compiled to OP_RANGE
+        assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
+    for i in range(20000, 30000):
+        ix.upsert(str(i), {"v": 15 if i % 2 else 20})  # 15 lands between existing ranks
+    for f in ({"LT": {"v": 25}}, {"GT": {"v": 12}}, {"LTE": {"v": 15}}):
+        prog = ix.compile(f)
+        assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog)), f
+    for i in range(30000, 31000):
+        ix.upsert(str(i), {"v": 30})  # existing value: incremental rank sync
+    prog = ix.compile({"GTE": {"v": 30}})
+    assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
+
+
+@pytest.mark.gpu
 def test_gpu_group_count():
     k = _kernels()
     ix = _random_collection(50_000, random.Random(3))
