@@ -608,7 +608,9 @@ class ColumnarIndex:
         kernels.rank_encode(src, cur["table"], lo, self.n, cur["t"], w)
         cur["synced"] = self.n
 
-    def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
+    def device_program(self, prog: Program, kernels):
+        """Sync the device mirror for ``prog`` and return (state, program, bitmaps) tensors ready
+        for ``GpuKernels.select`` (range leaves remapped to their rank-encoded columns)."""
         torch = kernels.torch
         leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ) | (prog.code[:, 0] == OP_RANGE)
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
@@ -621,6 +623,10 @@ class ColumnarIndex:
             code_np[rng, 1] = [st["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
         code = torch.from_numpy(code_np).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
+        return st, code, bitmaps
+
+    def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
+        st, code, bitmaps = self.device_program(prog, kernels)
         res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
         if return_mask or on_device:
             return res

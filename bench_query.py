@@ -72,9 +72,7 @@ def main() -> None:
     flt = {"AND": [{"LT": {"taskDueDate": "2024-07-01T00:00:00"}}, {"EQ": {"isCompleted": False}},
                    {"EQ": {"isOverDue": False}}]}
     prog = ix.compile(flt)
-    st = ix.to_device(k)
-    code = torch.from_numpy(prog.code).cuda()
-    bm = torch.from_numpy(prog.bitmaps).cuda()
+    st, code, bm = ix.device_program(prog, k)  # includes rank-encoding range-leaf columns
     for _ in range(a.warmup):
         out = k.select(st["table"], st["live"], ix.cap, n, code, bm)
     torch.cuda.synchronize()
@@ -102,7 +100,8 @@ def main() -> None:
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
            "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "single_pass_ms": round(single_pass_ms, 4),
-           "single_pass_matches": same, "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths}
+           "single_pass_matches": same, "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths,
+           "range_leaves": int((prog.code[:, 0] == 7).sum())}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order
         ix._full_dirty = True
