@@ -34,8 +34,8 @@ sys.path.insert(0, ROOT)
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024, help="createTask requests per step per rank")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="requests in flight per rank (0 = 48 per API replica, at most 384)")
