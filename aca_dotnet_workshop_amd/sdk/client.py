@@ -57,9 +57,22 @@ class QueryResponse:
     metadata: dict[str, str] = field(default_factory=dict)
 
 
+class RawJson(str):
+    """A value that is already JSON text (e.g. ``TaskModel.to_json()``): sent verbatim, so a
+    model serialised once can be saved and published without re-encoding."""
+
+
+def _value_json(v: Any) -> str:
+    if isinstance(v, RawJson):
+        return v
+    return json.dumps(to_jsonable(v), separators=(",", ":"))
+
+
 def _encode(data: Any) -> tuple[bytes, str]:
     if data is None:
         return b"", "application/json"
+    if isinstance(data, RawJson):
+        return data.encode(), "application/json"
     if isinstance(data, (bytes, bytearray)):
         return bytes(data), "application/octet-stream"
     if isinstance(data, str):
@@ -176,7 +189,7 @@ class SidecarClient:
     async def save_state(self, store: str, key: str, value: Any, etag: str | None = None,
                          metadata: dict[str, str] | None = None, concurrency: str | None = None,
                          consistency: str | None = None) -> None:
-        item: dict[str, Any] = {"key": key, "value": to_jsonable(value)}
+        item: dict[str, Any] = {"key": key}
         if etag is not None:
             item["etag"] = etag
         if metadata:
@@ -184,10 +197,14 @@ class SidecarClient:
         opts = {k: v for k, v in (("concurrency", concurrency), ("consistency", consistency)) if v}
         if opts:
             item["options"] = opts
-        await self.save_bulk_state(store, [item])
+        # splice the value's JSON in (a RawJson value is not re-encoded)
+        body = "[" + json.dumps(item, separators=(",", ":"))[:-1] + ',"value":' + _value_json(value) + "}]"
+        await self._save_body(store, body.encode())
 
     async def save_bulk_state(self, store: str, items: list[dict[str, Any]]) -> None:
-        body = json.dumps(items, separators=(",", ":")).encode()
+        await self._save_body(store, json.dumps(items, separators=(",", ":")).encode())
+
+    async def _save_body(self, store: str, body: bytes) -> None:
         r = await self._call("POST", f"/v1.0/state/{store}", body, "application/json", span_name=f"state save {store}")
         if r.status >= 300:
             raise InvocationError(r.status, r.body, f"save state {store}")

@@ -30,7 +30,7 @@ import uuid
 from datetime import datetime, timedelta
 
 from ...models import TaskModel, format_fixed, naive_utc, today, utcnow
-from ...sdk.client import InvocationError, SidecarClient
+from ...sdk.client import InvocationError, RawJson, SidecarClient
 
 log = logging.getLogger("TasksManager")
 
@@ -152,8 +152,9 @@ class TasksStoreManager(TasksManager):
         t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
                       task_due_date=due_date, task_assigned_to=assigned_to)
         log.info("Save a new task with name: '%s' to state store", t.task_name)
-        await self.client.save_state(self.store, str(t.task_id), t)
-        await self._publish_task_saved(t)
+        payload = RawJson(t.to_json())  # serialised once for the save and the event
+        await self.client.save_state(self.store, str(t.task_id), payload)
+        await self._publish_task_saved(t, payload)
         return t.task_id
 
     async def delete_task(self, task_id) -> bool:
@@ -239,7 +240,7 @@ class TasksStoreManager(TasksManager):
         if items:
             await self.client.save_bulk_state(self.store, items)
 
-    async def _publish_task_saved(self, t: TaskModel) -> None:
+    async def _publish_task_saved(self, t: TaskModel, payload: RawJson | None = None) -> None:
         log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
                  t.task_id, t.task_name, t.task_assigned_to)
-        await self.client.publish_event(self.pubsub, self.topic, t)
+        await self.client.publish_event(self.pubsub, self.topic, payload if payload is not None else t)
