@@ -2,9 +2,9 @@
 PY ?= python
 ENV_DIR ?= .tt-env
 
-.PHONY: build test test-gpu bench bench-query up down status validate what-if docs docs-local clean
+.PHONY: build test test-gpu sanitize bench bench-query bench-query-e2e up down status metrics validate what-if docs docs-local clean
 
-build:            ## compile native (C++) engines and gfx950 HIP kernels in-tree
+build:            ## compile native engines, sidecar data plane, load generator and gfx950 HIP kernels in-tree
 	$(PY) -c "import __graft_entry__ as g; g.build()"
 
 test:             ## CPU test suite
@@ -13,11 +13,17 @@ test:             ## CPU test suite
 test-gpu:         ## GPU tests (MI355X)
 	$(PY) -m pytest tests -q -m gpu
 
+sanitize:         ## native engines + backing front under ThreadSanitizer and ASan/UBSan
+	$(PY) -m pytest tests/test_native_sanitizers.py -q
+
 bench:            ## end-to-end createTask throughput (one JSON line)
 	$(PY) bench.py
 
-bench-query:      ## GPU state-query scan microbenchmark
-	$(PY) bench_query.py
+bench-query:      ## GPU state-query scan microbenchmark (scan + ordering)
+	$(PY) bench_query.py --sorted
+
+bench-query-e2e:  ## state-query latency through the stack (GPU accelerator, 2M docs)
+	$(PY) bench_query_e2e.py --docs 2000000 --accel gpu
 
 validate:
 	$(PY) -m aca_dotnet_workshop_amd.platform validate -f deploy/main.yaml -p deploy/main.parameters.json
@@ -30,6 +36,9 @@ up:               ## deploy the environment locally (detached)
 
 status:
 	$(PY) -m aca_dotnet_workshop_amd.platform status --env-dir $(ENV_DIR)
+
+metrics:          ## live metrics of the running environment
+	$(PY) -m aca_dotnet_workshop_amd.platform metrics --env-dir $(ENV_DIR)
 
 down:
 	$(PY) -m aca_dotnet_workshop_amd.platform down --env-dir $(ENV_DIR)
