@@ -33,77 +33,16 @@
 #include "docstore.hpp"
 #include "evhttp.hpp"
 #include "json.hpp"
+#include "textutil.hpp"
 
 namespace tt {
 
 namespace bf {
 
-inline int hexv(char c) {
-  if (c >= '0' && c <= '9') return c - '0';
-  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-  return -1;
-}
-
-inline std::string unquote(std::string_view s, bool plus_space = false) {
-  std::string o;
-  o.reserve(s.size());
-  for (size_t i = 0; i < s.size(); ++i) {
-    if (s[i] == '%' && i + 2 < s.size() && hexv(s[i + 1]) >= 0 && hexv(s[i + 2]) >= 0) {
-      o += (char)(hexv(s[i + 1]) * 16 + hexv(s[i + 2]));
-      i += 2;
-    } else if (plus_space && s[i] == '+') {
-      o += ' ';
-    } else {
-      o += s[i];
-    }
-  }
-  return o;
-}
-
-inline std::string jstr(std::string_view s) {
-  std::string o;
-  escape_to(o, s);
-  return o;
-}
-
-inline bool utf8_ok(std::string_view s) {
-  for (size_t i = 0; i < s.size();) {
-    unsigned char c = (unsigned char)s[i];
-    size_t n = c < 0x80 ? 0 : (c >> 5) == 6 ? 1 : (c >> 4) == 14 ? 2 : (c >> 3) == 30 ? 3 : 99;
-    if (n == 99 || i + n >= s.size() + (n == 0)) return n == 0;
-    for (size_t k = 1; k <= n; ++k)
-      if (((unsigned char)s[i + k] >> 6) != 2) return false;
-    i += n + 1;
-  }
-  return true;
-}
-
-inline std::string b64(std::string_view in) {
-  static const char* t = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
-  std::string o;
-  size_t i = 0;
-  for (; i + 2 < in.size(); i += 3) {
-    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8) | (uint8_t)in[i + 2];
-    o += t[v >> 18];
-    o += t[(v >> 12) & 63];
-    o += t[(v >> 6) & 63];
-    o += t[v & 63];
-  }
-  if (i + 1 == in.size()) {
-    uint32_t v = (uint8_t)in[i] << 16;
-    o += t[v >> 18];
-    o += t[(v >> 12) & 63];
-    o += "==";
-  } else if (i + 2 == in.size()) {
-    uint32_t v = ((uint8_t)in[i] << 16) | ((uint8_t)in[i + 1] << 8);
-    o += t[v >> 18];
-    o += t[(v >> 12) & 63];
-    o += t[(v >> 6) & 63];
-    o += '=';
-  }
-  return o;
-}
+using text::unquote;
+inline std::string jstr(std::string_view s) { return text::json_str(s); }
+inline bool utf8_ok(std::string_view s) { return text::valid_utf8(s); }
+inline std::string b64(std::string_view in) { return text::base64(in); }
 
 // RFC 7807 body exactly like web/http.py problem()
 inline std::string problem_json(int status, std::string_view detail) {
