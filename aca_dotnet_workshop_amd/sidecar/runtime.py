@@ -213,7 +213,9 @@ class Sidecar:
     async def _start_native_data_plane(self, api: WebApp) -> None:
         import tempfile
         from ..native.build import build_dataplane
-        exe = build_dataplane()  # no silent fallback: a requested native plane must run
+        # no silent fallback: a requested native plane must run (TT_DATAPLANE_BIN: an alternative
+        # build of the same source, e.g. the sanitizer build used by the tests)
+        exe = self.environ.get("TT_DATAPLANE_BIN") or build_dataplane()
         self._dp_dir = tempfile.mkdtemp(prefix="ttdp-")
         private = os.path.join(self._dp_dir, "cp.sock")
         srv = HttpServer(api, asyncio.get_running_loop())
