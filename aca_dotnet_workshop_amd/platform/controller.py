@@ -222,7 +222,8 @@ class EnvironmentController:
         level = self.log_level if not dapr.get("enableApiLogging") else "info"
         rp = self.stack.start_replica(dapr.get("appId") or spec["name"], extra_env=self._app_env(spec),
                                       module=spec["module"], log_level=level, identity=identity_of(spec),
-                                      api_logging=bool(dapr.get("enableApiLogging")))
+                                      api_logging=bool(dapr.get("enableApiLogging")),
+                                      grpc=str(dapr.get("apiProtocol", "http")).lower() == "grpc")
         rp.revision = rev.name  # type: ignore[attr-defined]
         rev.replicas.append(rp)
         self.event("ReplicaStarted", app=rt.name, revision=rev.name, replica=rp.name)

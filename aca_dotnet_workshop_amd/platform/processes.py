@@ -120,7 +120,9 @@ class LocalStack:
     def start_replica(self, app_id: str, config: dict[str, str] | None = None, extra_env: dict[str, str] | None = None,
                       http_port: int | None = None, module: str | None = None, log_level: str = "warning",
                       identity: str | None = None, external_port: int | None = None,
-                      api_logging: bool = False) -> ReplicaProc:
+                      api_logging: bool = False, grpc: bool = False) -> ReplicaProc:
+        """``grpc``: the sidecar also serves its gRPC API and the app's SDK uses it
+        (``Dapr:ApiProtocol=grpc``), the transport of the reference's .NET ``DaprClient``."""
         idx = self._seq
         self._seq += 1
         name = f"{app_id}-{idx}"
@@ -141,6 +143,9 @@ class LocalStack:
             args += ["--resources-path", c]
         if api_logging:
             args.append("--enable-api-logging")
+        if grpc:
+            args += ["--dapr-grpc-port", "0"]
+            env["Dapr__ApiProtocol"] = "grpc"
         args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
         p = self._spawn(args, env, name)
         rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)

@@ -317,6 +317,11 @@ class SidecarClient:
         r = await self._call("GET", "/v1.0/metadata")
         return r.json()
 
+    async def set_metadata(self, key: str, value: str) -> None:
+        r = await self._call("PUT", f"/v1.0/metadata/{quote(key, safe='')}", value.encode(), "text/plain")
+        if r.status >= 300:
+            raise InvocationError(r.status, r.body, f"set metadata {key}")
+
     async def shutdown_sidecar(self) -> None:
         await self._call("POST", "/v1.0/shutdown")
 
@@ -325,6 +330,18 @@ class SidecarClient:
 
 
 DaprClient = SidecarClient  # familiar alias for users coming from the reference
+
+
+def client_from_config(config=None, environ: dict[str, str] | None = None):
+    """The sidecar client a service should use: HTTP by default, gRPC when
+    ``Dapr:ApiProtocol`` (or ``DAPR_API_PROTOCOL``) is ``grpc`` -- the transport the reference's
+    .NET ``DaprClient`` uses for state / pub/sub / bindings."""
+    env = os.environ if environ is None else environ
+    proto = (config.get_str("Dapr:ApiProtocol") if config is not None else None) or env.get("DAPR_API_PROTOCOL", "http")
+    if proto.lower() == "grpc":
+        from .grpc_client import GrpcSidecarClient, sidecar_grpc_target
+        return GrpcSidecarClient(sidecar_grpc_target(env))
+    return SidecarClient(sidecar_base_url(env))
 
 
 def b64(data: bytes) -> str:

@@ -31,7 +31,7 @@ from pathlib import Path
 
 from ...models import TaskAddModel, TaskModel, TaskUpdateModel, tasks_to_json
 from ...models.dotnet import is_guid
-from ...sdk.client import SidecarClient
+from ...sdk.client import client_from_config
 from ...web.app import WebApp, read_model
 from ...web.http import HTTPError, Request, Response, empty
 from ..hosting import create_host, map_openapi, run_host
@@ -115,7 +115,7 @@ def select_manager(config) -> TasksManager:
     if backend == "fake":
         return FakeTasksManager()
     if backend == "store":
-        return TasksStoreManager(SidecarClient(),
+        return TasksStoreManager(client_from_config(config),
                                  store=config.get_str("TasksManager:StateStoreName", "statestore"),
                                  pubsub=config.get_str("TasksManager:PubSubName", "dapr-pubsub-servicebus"),
                                  topic=config.get_str("TasksManager:TopicName", "tasksavedtopic"))

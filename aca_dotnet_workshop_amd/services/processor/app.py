@@ -32,7 +32,7 @@ from pathlib import Path
 
 from ...models import TaskModel, naive_utc, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
-from ...sdk.client import InvocationError
+from ...sdk.client import InvocationError, client_from_config
 from ...web.app import WebApp, read_model
 from ...web.http import Request, Response, empty, json_response, text_response
 from ..hosting import create_host, map_openapi, run_host
@@ -138,7 +138,7 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
                overrides: dict | None = None) -> WebApp:
     app = create_host(ROLE, CONTENT_ROOT, argv, config=config, overrides=overrides)
     app.openapi_info = {"title": "TasksTracker.Processor.Backend.Svc | v1", "version": "1.0.0"}
-    client = client or SidecarClient()
+    client = client or client_from_config(app.config)
     app.services["dapr"] = client
     app.use(cloud_events_middleware())  # app.UseCloudEvents()
     register_controllers(app, client)

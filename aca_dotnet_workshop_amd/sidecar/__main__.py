@@ -35,7 +35,10 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--app-port", type=int, default=None)
     r.add_argument("--app-uds", default=None, help="app listens on this Unix socket instead of a port")
     r.add_argument("--dapr-http-port", type=int, default=3500)
-    r.add_argument("--dapr-internal-port", "--dapr-grpc-port", dest="internal_port", type=int, default=0)
+    r.add_argument("--dapr-internal-port", "--dapr-internal-grpc-port", dest="internal_port", type=int, default=0,
+                   help="sidecar-to-sidecar port (0 = ephemeral)")
+    r.add_argument("--dapr-grpc-port", type=int, default=None,
+                   help="serve the gRPC API (dapr.proto.runtime.v1.Dapr) on this port (0 = ephemeral; off if unset)")
     r.add_argument("--unix-socket-dir", default=None, help="expose the sidecar API and internal port as Unix sockets here")
     r.add_argument("--resources-path", "--components-path", dest="resources", action="append", default=[])
     r.add_argument("--registry-dir", default=os.environ.get("TT_REGISTRY_DIR"))
@@ -56,9 +59,9 @@ async def _run(a: argparse.Namespace) -> int:
     if cmd and cmd[0] == "--":
         cmd = cmd[1:]
     sock_api = sock_int = None
+    tag = a.replica_name or f"{a.app_id}-{os.getpid()}"
     if a.unix_socket_dir:
         os.makedirs(a.unix_socket_dir, exist_ok=True)
-        tag = a.replica_name or f"{a.app_id}-{os.getpid()}"
         sock_api = os.path.join(a.unix_socket_dir, f"{tag}.d.sock")
         sock_int = os.path.join(a.unix_socket_dir, f"{tag}.i.sock")
     sc = Sidecar(a.app_id, app_port=a.app_port, app_uds=a.app_uds, http_port=a.dapr_http_port, uds=sock_api,
@@ -67,7 +70,9 @@ async def _run(a: argparse.Namespace) -> int:
                  app_token=os.environ.get("APP_API_TOKEN"), mesh_token=os.environ.get("TT_MESH_TOKEN"),
                  app_max_concurrency=a.app_max_concurrency, identity=a.identity, backing_url=a.backing_url,
                  instance=a.replica_name, app_health_path=a.app_health_check_path,
-                 api_logging=a.enable_api_logging)
+                 api_logging=a.enable_api_logging, grpc_port=a.dapr_grpc_port,
+                 grpc_uds=os.path.join(a.unix_socket_dir, f"{tag}.g.sock") if a.unix_socket_dir and a.dapr_grpc_port is not None
+                 else None)
     await sc.start()
     loop = asyncio.get_running_loop()
     stop = asyncio.Event()
@@ -80,6 +85,8 @@ async def _run(a: argparse.Namespace) -> int:
                     "APP_PORT": str(a.app_port or ""), "TT_APP_ID": a.app_id})
         if sock_api:
             env["TT_SIDECAR_UDS"] = sock_api
+        if sc.bound_grpc_port:
+            env["DAPR_GRPC_PORT"] = str(sc.bound_grpc_port)
         if a.app_uds:
             env["TT_APP_UDS"] = a.app_uds
         proc = await asyncio.create_subprocess_exec(*cmd, env=env)

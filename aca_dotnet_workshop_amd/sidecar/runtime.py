@@ -14,6 +14,7 @@ API                                             reference usage
 ``/v1.0/bindings/{name}``                        ExternalTasksProcessorController.cs:43 (row 8)
 ``/v1.0/secrets/{store}/{key}`` + bulk           secret store building block
 ``/v1.0/metadata``, ``/v1.0/healthz``            runtime introspection / readiness
+gRPC ``dapr.proto.runtime.v1.Dapr``              ``DaprClient``'s transport (``grpc_api.py``)
 ==============================================  ==============================================
 
 Inbound to the app: ``GET /dapr/subscribe`` discovery then CloudEvent deliveries to the
@@ -78,7 +79,7 @@ class Sidecar:
                  identity: str | None = None, backing_url: str | None = None, environ: dict[str, str] | None = None,
                  telemetry_dir: str | None = None, instance: str | None = None,
                  app_health_path: str | None = None, data_plane: str | None = None,
-                 api_logging: bool = False) -> None:
+                 api_logging: bool = False, grpc_port: int | None = None, grpc_uds: str | None = None) -> None:
         self.app_id = app_id
         self.app_port = app_port
         self.app_uds = app_uds
@@ -98,6 +99,11 @@ class Sidecar:
         self.instance = instance or f"{app_id}-{uuid.uuid4().hex[:8]}"
         self.app_health_path = app_health_path
         self.api_logging = api_logging
+        self.grpc_port = grpc_port  # None: no gRPC API; 0: ephemeral port
+        self.grpc_uds = grpc_uds
+        self.grpc_server = None
+        self.bound_grpc_port: int | None = None
+        self.extended_metadata: dict[str, str] = {}
         self.http = HttpClient(timeout=300)
         kw: dict[str, Any] = {"app_id": app_id, "identity": identity, "http": self.http, "environ": self.environ}
         if backing_url:
@@ -141,11 +147,16 @@ class Sidecar:
             await self._start_native_data_plane(api)
         else:
             await self._start_python_servers(api, internal, loop)
+        if self.grpc_port is not None or self.grpc_uds:
+            from .grpc_api import DaprGrpcServer
+            self.grpc_server = DaprGrpcServer(self, api)
+            self.bound_grpc_port = await self.grpc_server.start(self.grpc_port or 0, uds=self.grpc_uds)
         self.resolver.register(self.app_id, self.instance, self.bound_internal,
                                {"httpPort": self.bound_http_port, "dataPlane": self.active_data_plane})
         self.ready.set()
-        log.info("sidecar %s up: api=%s%s internal=%s plane=%s components=%s", self.app_id, self.bound_http_port,
-                 f" uds={self.uds}" if self.uds else "", self.bound_internal, self.active_data_plane,
+        log.info("sidecar %s up: api=%s%s grpc=%s internal=%s plane=%s components=%s", self.app_id,
+                 self.bound_http_port, f" uds={self.uds}" if self.uds else "", self.bound_grpc_port,
+                 self.bound_internal, self.active_data_plane,
                  sorted(self.components))
         if self.app_port is not None or self.app_uds:
             self._bg.append(asyncio.ensure_future(self._app_startup()))
@@ -260,6 +271,8 @@ class Sidecar:
             await c.stop(grace)
         for b in self.bindings.values():
             await b.close()
+        if self.grpc_server is not None:
+            await self.grpc_server.stop(min(grace, 1.0))
         if self._dp_proc is not None and self._dp_proc.returncode is None:
             self._dp_proc.terminate()
             try:
@@ -593,6 +606,7 @@ class Sidecar:
         app.add_route("/v1.0/secrets/{store}/bulk", self.h_secret_bulk, ("GET",))
         app.add_route("/v1.0/secrets/{store}/{key}", self.h_secret, ("GET",))
         app.add_route("/v1.0/metadata", self.h_metadata, ("GET",))
+        app.add_route("/v1.0/metadata/{key}", self.h_metadata_set, ("PUT",))
         app.add_route("/v1.0/healthz", self.h_healthz, ("GET",))
         app.add_route("/v1.0/healthz/outbound", self.h_healthz, ("GET",))
         app.add_route("/v1.0/shutdown", self.h_shutdown, ("POST",))
@@ -936,11 +950,17 @@ class Sidecar:
         return json_response({
             "id": self.app_id, "runtimeVersion": RUNTIME_VERSION, "components": comps, "subscriptions": subs,
             "inputBindings": self.input_bindings, "failedComponents": self.failed_components,
-            "extended": {"instance": self.instance, "appReady": self.app_ready.is_set(),
+            "extended": {**self.extended_metadata, "instance": self.instance, "appReady": self.app_ready.is_set(),
                          "dataPlane": self.active_data_plane,
                          "consumers": consumers},
             "appConnectionProperties": {"port": self.app_port, "uds": self.app_uds, "protocol": "http"},
+            "grpcPort": self.bound_grpc_port,
         })
+
+    async def h_metadata_set(self, req: Request) -> Response:
+        """``PUT /v1.0/metadata/{key}``: app-defined attributes shown under ``extended``."""
+        self.extended_metadata[req.path_params["key"]] = req.body.decode("utf-8", "replace")
+        return empty(204)
 
     async def h_healthz(self, req: Request) -> Response:
         return empty(204) if self.ready.is_set() else empty(500)

@@ -45,6 +45,8 @@ def parse() -> argparse.Namespace:
                     help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
     ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
+    ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
+                    help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")
     ap.add_argument("--client", choices=("native", "python"), default="native",
                     help="load generator: native/bin/ttloadgen (C++) or the in-process asyncio client")
     return ap.parse_args()
@@ -204,9 +206,9 @@ def main() -> None:
         if a.split_backing:
             backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
         for _ in range(a.api_replicas):
-            stack.start_replica("tasksmanager-backend-api", cfg)
+            stack.start_replica("tasksmanager-backend-api", cfg, grpc=a.api_protocol == "grpc")
         for _ in range(a.processor_replicas):
-            stack.start_replica("tasksmanager-backend-processor", cfg)
+            stack.start_replica("tasksmanager-backend-processor", cfg, grpc=a.api_protocol == "grpc")
         stack.wait_ready()
         socks = [r.sidecar_uds for r in stack.replicas["tasksmanager-backend-api"]]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
@@ -266,6 +268,7 @@ def main() -> None:
                            "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
+                           "sidecar_api_protocol": a.api_protocol,
                            "create_latency_p50_ms": round(p50, 3),
                            "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput"}}),
                 flush=True)
