@@ -46,7 +46,8 @@ def _stale(target: Path, sources: list[Path]) -> bool:
     if not target.exists():
         return True
     t = target.stat().st_mtime
-    return any(s.stat().st_mtime > t for s in sources)
+    # a deployed image ships the built extension without its sources: present means current
+    return any(s.exists() and s.stat().st_mtime > t for s in sources)
 
 
 def build_native(force: bool = False, verbose: bool = False) -> Path:

@@ -293,6 +293,13 @@ def cmd_telemetry(a) -> int:
     return 0
 
 
+def cmd_image(a) -> int:
+    from . import image
+    for row in image.report(a.out, a.service, a.verify):
+        print(json.dumps(row), flush=True)
+    return 0
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(prog="tt-platform", description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -352,6 +359,11 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--tail", type=int, default=50)
     p.add_argument("--follow", action="store_true")
     p.set_defaults(fn=cmd_logs)
+    p = sub.add_parser("image", help="build OCI images of the services (standard + chiseled; module 12)")
+    p.add_argument("--service", action="append", choices=["backend_api", "processor", "frontend"])
+    p.add_argument("--out", default="dist/images")
+    p.add_argument("--verify", action="store_true", help="run each image under chroot and probe it (root)")
+    p.set_defaults(fn=cmd_image)
     a = ap.parse_args(argv)
     try:
         return a.fn(a)
