@@ -43,10 +43,12 @@ class WireModel(BaseModel):
     model_config = ConfigDict(alias_generator=to_camel, populate_by_name=True, extra="ignore",
                               validate_assignment=False)
     _lower_aliases: ClassVar[dict[str, str]] = {}
+    _aliases: ClassVar[frozenset[str]] = frozenset()
 
     def __init_subclass__(cls, **kw: Any) -> None:
         super().__init_subclass__(**kw)
         cls._lower_aliases = {}
+        cls._aliases = frozenset()
 
     @classmethod
     def __pydantic_init_subclass__(cls, **kw: Any) -> None:
@@ -54,11 +56,14 @@ class WireModel(BaseModel):
         cls._lower_aliases = {
             (f.alias or name).lower(): (f.alias or name) for name, f in cls.model_fields.items()
         }
+        cls._aliases = frozenset(cls._lower_aliases.values())
 
     @model_validator(mode="before")
     @classmethod
     def _case_insensitive(cls, data: Any) -> Any:
         if isinstance(data, dict):
+            if cls._aliases.issuperset(data):  # already canonical camelCase (the common case)
+                return data
             la = cls._lower_aliases
             out = {}
             for k, v in data.items():
