@@ -142,6 +142,9 @@ def _expire(fut: asyncio.Future) -> None:
         fut.set_exception(asyncio.TimeoutError("HTTP request timed out"))
 
 
+_SWEEP_S = 0.1  # timeout resolution (per-request TimerHandles cost ~5 us each on the hot path)
+
+
 def parse_endpoint(url: str) -> tuple[Any, str]:
     """Split ``url`` into (endpoint key, request target)."""
     if url.startswith("unix:"):
@@ -165,6 +168,25 @@ class HttpClient:
         self.max_idle = max_idle_per_host
         self.timeout = timeout
         self._closed = False
+        self._deadlines: dict[asyncio.Future, float] = {}
+        self._sweeper: asyncio.TimerHandle | None = None
+        self._sweep_loop: asyncio.AbstractEventLoop | None = None
+
+    def _sweep(self) -> None:
+        """One coarse timer for every in-flight request of this client."""
+        self._sweeper = None
+        if not self._deadlines:
+            return
+        loop = asyncio.get_running_loop()
+        now = loop.time()
+        for fut, dl in list(self._deadlines.items()):
+            if fut.done():
+                self._deadlines.pop(fut, None)
+            elif now >= dl:
+                self._deadlines.pop(fut, None)
+                _expire(fut)
+        if self._deadlines:
+            self._sweeper = loop.call_at(now + _SWEEP_S, self._sweep)
 
     async def _connect(self, key: Any) -> _Conn:
         loop = asyncio.get_running_loop()
@@ -230,7 +252,10 @@ class HttpClient:
             conn.is_head = method == "HEAD"
             conn.transport.write(payload)
             fut = conn.fut
-            timer = loop.call_later(to, _expire, fut)
+            self._deadlines[fut] = loop.time() + to
+            if self._sweeper is None or self._sweep_loop is not loop:
+                self._sweep_loop = loop
+                self._sweeper = loop.call_at(loop.time() + min(_SWEEP_S, to), self._sweep)
             try:
                 resp, keep = await fut
             except ConnectionClosed:
@@ -244,7 +269,7 @@ class HttpClient:
                 conn.closed = True
                 raise
             finally:
-                timer.cancel()
+                self._deadlines.pop(fut, None)
             conn.fut = None
             if keep:
                 self._release(conn)
@@ -267,6 +292,9 @@ class HttpClient:
 
     async def close(self) -> None:
         self._closed = True
+        if self._sweeper is not None:
+            self._sweeper.cancel()
+            self._sweeper = None
         for dq in self._idle.values():
             for c in dq:
                 if c.transport:
