@@ -310,10 +310,17 @@ class MsgParser {
 
 inline const char* reason_phrase(int s) {
   switch (s) {
+    case 100: return "Continue";
     case 200: return "OK";
     case 201: return "Created";
     case 202: return "Accepted";
     case 204: return "No Content";
+    case 301: return "Moved Permanently";
+    case 302: return "Found";
+    case 303: return "See Other";
+    case 304: return "Not Modified";
+    case 307: return "Temporary Redirect";
+    case 308: return "Permanent Redirect";
     case 400: return "Bad Request";
     case 401: return "Unauthorized";
     case 403: return "Forbidden";
@@ -322,6 +329,10 @@ inline const char* reason_phrase(int s) {
     case 409: return "Conflict";
     case 412: return "Precondition Failed";
     case 413: return "Payload Too Large";
+    case 415: return "Unsupported Media Type";
+    case 422: return "Unprocessable Entity";
+    case 429: return "Too Many Requests";
+    case 501: return "Not Implemented";
     case 500: return "Internal Server Error";
     case 502: return "Bad Gateway";
     case 503: return "Service Unavailable";
@@ -583,9 +594,13 @@ class Listener : public IoObj {
       }
       int one = 1;
       setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // fails harmlessly on unix sockets
-      loop_.add(std::make_shared<ServerConn>(loop_, c, handler_), EPOLLIN);
+      auto conn = std::make_shared<ServerConn>(loop_, c, handler_);
+      loop_.add(conn, EPOLLIN);
+      if (on_accept) on_accept(conn);
     }
   }
+  // optional: observe accepted connections (the app host closes them when its server stops)
+  std::function<void(const std::shared_ptr<ServerConn>&)> on_accept;
 
  private:
   Loop& loop_;
@@ -595,7 +610,8 @@ class Listener : public IoObj {
 // Returns the bound port (tcp) or 0 (unix); throws on failure.
 // `reuseport`: several loops (threads) bind the same TCP port and the kernel spreads
 // incoming connections over them.
-inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false) {
+inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false,
+                     std::shared_ptr<IoObj>* listener_out = nullptr) {
   int fd;
   int port = 0;
   if (ep.unix_socket) {
@@ -622,7 +638,9 @@ inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport 
     port = ntohs(a.sin_port);
   }
   if (::listen(fd, 1024) != 0) throw std::runtime_error(std::string("listen: ") + strerror(errno));
-  loop.add(std::make_shared<Listener>(loop, fd, h), EPOLLIN);
+  auto l = std::make_shared<Listener>(loop, fd, h);
+  loop.add(l, EPOLLIN);
+  if (listener_out) *listener_out = l;
   return port;
 }
 

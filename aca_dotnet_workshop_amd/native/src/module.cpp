@@ -3,6 +3,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
+#include "apphost.hpp"
 #include "backingfront.hpp"
 #include "broker.hpp"
 #include "docstore.hpp"
@@ -10,6 +11,50 @@
 
 namespace py = pybind11;
 using namespace tt;
+
+// Lower-cased header list -> dict; repeated headers joined by ", " except set-cookie (a list).
+template <class List>
+static py::dict headers_dict(const List& headers) {
+  py::dict hd;
+  for (auto& [k, v] : headers) {
+    py::str key(k);
+    if (hd.contains(key)) {
+      if (k == "set-cookie") {
+        py::object prev = hd[key];
+        py::list l;
+        if (py::isinstance<py::list>(prev)) l = prev.cast<py::list>();
+        else l.append(prev);
+        l.append(py::str(v));
+        hd[key] = l;
+      } else {
+        hd[key] = py::str(hd[key].cast<std::string>() + ", " + v);
+      }
+    } else {
+      hd[key] = py::str(v);
+    }
+  }
+  return hd;
+}
+
+// [(name, value), ...] from Python -> header list with lower-cased names (framing headers are
+// filtered by the writer, which compares lower-case names).
+static ev::HeaderList header_list(const py::handle& seq) {
+  ev::HeaderList out;
+  for (auto item : seq) {
+    auto t = item.cast<py::tuple>();
+    std::string k = t[0].cast<std::string>();
+    for (auto& ch : k) ch = (char)std::tolower((unsigned char)ch);
+    out.emplace_back(std::move(k), t[1].cast<std::string>());
+  }
+  return out;
+}
+
+static std::string bytes_of(const py::handle& b) {
+  char* p;
+  Py_ssize_t n;
+  if (PyBytes_AsStringAndSize(b.ptr(), &p, &n) != 0) throw py::error_already_set();
+  return std::string(p, (size_t)n);
+}
 
 PYBIND11_MODULE(_ttnative, m) {
   m.doc() = "Native document store + message broker engines (C++17)";
@@ -37,25 +82,7 @@ PYBIND11_MODULE(_ttnative, m) {
     } catch (const std::invalid_argument& e) {
       throw py::value_error(e.what());
     }
-    py::dict hd;
-    for (auto& [k, v] : h.headers) {
-      py::str key(k);
-      if (hd.contains(key)) {
-        if (k == "set-cookie") {
-          py::object prev = hd[key];
-          py::list l;
-          if (py::isinstance<py::list>(prev)) l = prev.cast<py::list>();
-          else l.append(prev);
-          l.append(py::str(v));
-          hd[key] = l;
-        } else {
-          hd[key] = py::str(hd[key].cast<std::string>() + ", " + v);
-        }
-      } else {
-        hd[key] = py::str(v);
-      }
-    }
-    return py::make_tuple(py::str(h.a), py::str(h.b), py::str(h.c), hd);
+    return py::make_tuple(py::str(h.a), py::str(h.b), py::str(h.c), headers_dict(h.headers));
   });
 
   py::class_<TxOp>(m, "TxOp")
@@ -218,4 +245,61 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("notify", &BackingFront::notify)
       .def("stats", &BackingFront::stats)
       .def("stop", &BackingFront::stop, py::call_guard<py::gil_scoped_release>());
+
+  // Native HTTP host of an app process (apphost.hpp): its epoll thread owns the listeners and
+  // the client pools; Python hands it responses and outbound requests in batches (submit()),
+  // collects parsed requests and responses with drain() and waits on event_fd().
+  py::class_<apphost::AppHost>(m, "AppHost")
+      .def(py::init<>())
+      .def("start", &apphost::AppHost::start)
+      .def("stop", &apphost::AppHost::stop, py::call_guard<py::gil_scoped_release>())
+      .def("event_fd", &apphost::AppHost::event_fd)
+      .def("listen", &apphost::AppHost::listen, py::arg("server"), py::arg("endpoint"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("close_server", &apphost::AppHost::close_server)
+      .def("close_connections", &apphost::AppHost::close_connections)
+      .def("pending_replies", &apphost::AppHost::pending_replies)
+      // ops: [(0, token, status, headers, body) | (1, id, endpoint, method, target, headers, body, timeout)]
+      .def("submit",
+           [](apphost::AppHost& h, py::list ops) {
+             std::vector<apphost::AppHost::Op> v;
+             v.reserve(ops.size());
+             for (auto item : ops) {
+               auto t = item.cast<py::tuple>();
+               apphost::AppHost::Op op;
+               op.is_request = t[0].cast<int>() == 1;
+               op.id = t[1].cast<uint64_t>();
+               if (!op.is_request) {
+                 op.status = t[2].cast<int>();
+                 op.headers = header_list(t[3]);
+                 op.body = bytes_of(t[4]);
+               } else {
+                 op.endpoint = t[2].cast<std::string>();
+                 op.method = t[3].cast<std::string>();
+                 op.target = t[4].cast<std::string>();
+                 op.headers = header_list(t[5]);
+                 op.body = bytes_of(t[6]);
+                 op.timeout_s = t[7].cast<double>();
+               }
+               v.push_back(std::move(op));
+             }
+             h.submit(std::move(v));
+           })
+      // [(0, token, server, method, target, http10, headers, body) | (1, id, status, headers, body) |
+      //  (2, id, errno, message)]
+      .def("drain", [](apphost::AppHost& h) {
+        auto evs = h.drain();
+        py::list out;
+        for (auto& e : evs) {
+          if (e.kind == apphost::Event::REQUEST) {
+            out.append(py::make_tuple(0, e.id, e.server, py::str(e.msg.method), py::str(e.msg.target),
+                                      e.msg.http10, headers_dict(e.msg.headers), py::bytes(e.msg.body)));
+          } else if (e.kind == apphost::Event::RESPONSE) {
+            out.append(py::make_tuple(1, e.id, e.msg.status, headers_dict(e.msg.headers), py::bytes(e.msg.body)));
+          } else {
+            out.append(py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err))));
+          }
+        }
+        return out;
+      });
 }

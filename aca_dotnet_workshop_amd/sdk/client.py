@@ -112,7 +112,10 @@ class SidecarClient:
     def __init__(self, base_url: str | None = None, api_token: str | None = None,
                  http: HttpClient | None = None, timeout: float = 60.0) -> None:
         self.base = base_url or sidecar_base_url()
-        self.http = http or HttpClient(timeout=timeout)
+        if http is None:
+            from ..web import native_host
+            http = native_host.NativeHttpClient(timeout=timeout) if native_host.enabled() else HttpClient(timeout=timeout)
+        self.http = http
         self.api_token = api_token if api_token is not None else os.environ.get("DAPR_API_TOKEN")
 
     # -- plumbing -------------------------------------------------------------

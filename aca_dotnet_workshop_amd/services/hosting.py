@@ -98,7 +98,8 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
                      ready: Callable[[list[int]], None] | None = None) -> None:
     config: Configuration = app.services["config"]
     loop = asyncio.get_running_loop()
-    srv = HttpServer(app, loop)
+    from ..web import native_host
+    srv = native_host.NativeHttpServer(app, loop) if native_host.enabled() else HttpServer(app, loop)
     await app.startup()
     ports = []
     for host, port in listen_addresses(config):

@@ -1,0 +1,253 @@
+"""Native I/O host for app processes: HTTP server and client on a C++ epoll thread.
+
+``NativeHttpServer`` and ``NativeHttpClient`` are drop-in equivalents of ``HttpServer`` and
+``HttpClient`` whose sockets, HTTP parsing/serialisation, keep-alive pools and timeouts live in
+``native/src/apphost.hpp`` (one I/O thread per process and event loop), the way Kestrel runs an
+ASP.NET Core app's I/O on native threads while the app code runs elsewhere (reference
+SURVEY.md §2.9 X5).  The asyncio thread only runs handlers: it wakes on one eventfd per batch
+of completed I/O, turns each event into a ``Request`` (server side) or resolves a future with
+a ``ClientResponse`` (client side), and hands responses / new requests back in one call each.
+
+Selected with ``TT_APP_HOST=native`` (``hosting.serve_host`` and the SDK's ``SidecarClient``);
+the platform's process launcher sets it for the service processes.  Missing extension = hard
+error (no silent fallback when the native host was asked for).
+"""
+from __future__ import annotations
+
+import asyncio
+import errno as _errno
+import json
+import logging
+import os
+import weakref
+from typing import Any, Awaitable, Callable
+
+from .client import ClientResponse, ConnectionClosed, parse_endpoint
+from .http import Headers, Request, Response, problem
+
+log = logging.getLogger("web.native")
+
+Handler = Callable[[Request], Awaitable[Response]]
+
+
+def enabled(environ: dict[str, str] | None = None) -> bool:
+    env = os.environ if environ is None else environ
+    return env.get("TT_APP_HOST", "").lower() == "native"
+
+
+def _client_error(err: int, msg: str) -> BaseException:
+    if err == _errno.ECONNREFUSED:
+        return ConnectionRefusedError(err, msg)
+    if err == _errno.ENOENT:
+        return FileNotFoundError(err, msg)
+    if err == _errno.ETIMEDOUT:
+        return asyncio.TimeoutError("HTTP request timed out")
+    return ConnectionClosed(f"{msg} (errno {err})")
+
+
+class NativeHost:
+    """One ``AppHost`` (I/O thread) per event loop."""
+
+    _by_loop: "weakref.WeakKeyDictionary[asyncio.AbstractEventLoop, NativeHost]" = weakref.WeakKeyDictionary()
+
+    @classmethod
+    def get(cls, loop: asyncio.AbstractEventLoop | None = None) -> "NativeHost":
+        loop = loop or asyncio.get_running_loop()
+        h = cls._by_loop.get(loop)
+        if h is None or h.closed:
+            h = cls._by_loop[loop] = cls(loop)
+        return h
+
+    def __init__(self, loop: asyncio.AbstractEventLoop) -> None:
+        from ..native import load
+        self.loop = loop
+        self.h = load().AppHost()
+        self.h.start()
+        self.fd = self.h.event_fd()
+        loop.add_reader(self.fd, self._on_events)
+        self.servers: dict[int, NativeHttpServer] = {}
+        self.pending: dict[int, asyncio.Future] = {}
+        self._next_id = 1
+        self._next_server = 1
+        self.users = 0
+        self.closed = False
+        self._ops: list[tuple] = []  # respond/request operations of this loop iteration
+
+    def _queue(self, op: tuple) -> None:
+        if not self._ops:
+            self.loop.call_soon(self._flush)
+        self._ops.append(op)
+
+    def _flush(self) -> None:
+        ops, self._ops = self._ops, []
+        if ops and not self.closed:
+            self.h.submit(ops)
+
+    def respond(self, token: int, status: int, headers: list, body: bytes) -> None:
+        self._queue((0, token, status, headers, body))
+
+    def new_server_id(self, srv: "NativeHttpServer") -> int:
+        sid = self._next_server
+        self._next_server += 1
+        self.servers[sid] = srv
+        return sid
+
+    def _on_events(self) -> None:
+        for ev in self.h.drain():
+            kind = ev[0]
+            if kind == 0:
+                _, token, sid, method, target, http10, hd, body = ev
+                srv = self.servers.get(sid)
+                if srv is None:
+                    self.respond(token, 503, [], b"")
+                    continue
+                srv._dispatch(token, method, target, http10, hd, body)
+            elif kind == 1:
+                fut = self.pending.pop(ev[1], None)
+                if fut is not None and not fut.done():
+                    fut.set_result(ClientResponse(ev[2], Headers(ev[3]), ev[4]))
+            else:
+                fut = self.pending.pop(ev[1], None)
+                if fut is not None and not fut.done():
+                    fut.set_exception(_client_error(ev[2], ev[3]))
+
+    def request(self, endpoint: str, method: str, target: str, headers: list[tuple[str, str]], body: bytes,
+                timeout: float) -> asyncio.Future:
+        rid = self._next_id
+        self._next_id += 1
+        fut = self.loop.create_future()
+        self.pending[rid] = fut
+        self._queue((1, rid, endpoint, method, target, headers, body, timeout))
+        return fut
+
+    def release(self) -> None:
+        """Drop one user; the last one stops the I/O thread."""
+        self.users -= 1
+        if self.users <= 0 and not self.servers and not self.closed:
+            self.close()
+
+    def close(self) -> None:
+        if self.closed:
+            return
+        self.closed = True
+        try:
+            self.loop.remove_reader(self.fd)
+        except Exception:
+            pass
+        self.h.stop()
+        for fut in self.pending.values():
+            if not fut.done():
+                fut.set_exception(ConnectionClosed("native host stopped"))
+        self.pending.clear()
+
+
+class NativeHttpServer:
+    """``HttpServer`` on the native host."""
+
+    def __init__(self, handler: Handler, loop: asyncio.AbstractEventLoop | None = None) -> None:
+        self.handler = handler
+        self.loop = loop or asyncio.get_event_loop()
+        self.host = NativeHost.get(self.loop)
+        self.host.users += 1
+        self.sid = self.host.new_server_id(self)
+        self._inflight = 0
+        self._closing = False
+        self.ports: list[int] = []
+
+    async def listen_tcp(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
+                         sock=None) -> int:
+        if sock is not None:
+            raise ValueError("NativeHttpServer binds its own sockets")
+        p = self.host.h.listen(self.sid, f"tcp:{host}:{port}")
+        self.ports.append(p)
+        return p
+
+    async def listen_unix(self, path: str) -> str:
+        self.host.h.listen(self.sid, f"unix:{path}")
+        return path
+
+    @property
+    def port(self) -> int:
+        if not self.ports:
+            raise RuntimeError("no TCP listener")
+        return self.ports[0]
+
+    def _dispatch(self, token: int, method: str, target: str, http10: bool, hd: dict, body: bytes) -> None:
+        req = Request(method, target, Headers(hd), body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
+        self._inflight += 1
+        self.loop.create_task(self._serve(token, req))
+
+    async def _serve(self, token: int, req: Request) -> None:
+        try:
+            try:
+                resp = await self.handler(req)
+            except Exception:
+                log.exception("unhandled error serving %s %s", req.method, req.target)
+                resp = problem(500)
+            body = resp.body if isinstance(resp.body, bytes) else bytes(resp.body)
+            self.host.respond(token, resp.status, resp.headers, body)
+        finally:
+            self._inflight -= 1
+
+    async def close(self, grace: float = 5.0) -> None:
+        if self._closing:
+            return
+        self._closing = True
+        self.host.h.close_server(self.sid)
+        deadline = self.loop.time() + grace
+        while self._inflight and self.loop.time() < deadline:
+            await asyncio.sleep(0.01)
+        self.host._flush()  # responses queued this iteration go out before the connections close
+        self.host.h.close_connections(self.sid)
+        self.host.servers.pop(self.sid, None)
+        self.host.release()
+
+
+class NativeHttpClient:
+    """``HttpClient`` on the native host (keep-alive pools and timeouts in C++)."""
+
+    def __init__(self, max_idle_per_host: int = 256, timeout: float = 60.0) -> None:
+        self.timeout = timeout
+        self._host: NativeHost | None = None
+        self._endpoints: dict[Any, str] = {}
+
+    def _native(self) -> NativeHost:
+        h = self._host
+        if h is None or h.closed or h.loop is not asyncio.get_running_loop():
+            h = self._host = NativeHost.get()
+            h.users += 1
+        return h
+
+    async def request(self, method: str, url: str, *, headers: dict[str, str] | list[tuple[str, str]] | None = None,
+                      body: bytes | str | None = None, json_body: Any = None,
+                      timeout: float | None = None) -> ClientResponse:
+        key, target = parse_endpoint(url)
+        hdrs = list(headers.items()) if isinstance(headers, dict) else list(headers or [])
+        if json_body is not None:
+            body = json.dumps(json_body, separators=(",", ":")).encode()
+            if not any(k.lower() == "content-type" for k, _ in hdrs):
+                hdrs.append(("Content-Type", "application/json"))
+        if isinstance(body, str):
+            body = body.encode()
+        ep = self._endpoints.get(key)
+        if ep is None:
+            ep = self._endpoints[key] = f"unix:{key[1]}" if key[0] == "unix" else f"tcp:{key[1]}:{key[2]}"
+        to = self.timeout if timeout is None else timeout
+        return await self._native().request(ep, method, target, hdrs, body or b"", to)
+
+    async def get(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("GET", url, **kw)
+
+    async def post(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("POST", url, **kw)
+
+    async def put(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("PUT", url, **kw)
+
+    async def delete(self, url: str, **kw: Any) -> ClientResponse:
+        return await self.request("DELETE", url, **kw)
+
+    async def close(self) -> None:
+        if self._host is not None:
+            h, self._host = self._host, None
+            h.release()

@@ -66,3 +66,27 @@ def test_dataplane_under_address_sanitizer(tmp_path):
     out = run.stdout + run.stderr
     assert run.returncode == 0, out[-5000:]
     assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out
+
+
+@pytest.mark.parametrize("flags,env", [
+    (["-fsanitize=thread"], {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}),
+    (["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"], {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1"}),
+], ids=["tsan", "asan-ubsan"])
+def test_app_host_under_sanitizers(tmp_path, flags, env):
+    """The app-process native host (``apphost.hpp``): the submitting thread and the I/O thread
+    exchange 20k server requests and 20k client requests over Unix and TCP sockets; clean under
+    ThreadSanitizer and ASan+UBSan."""
+    if shutil.which(CXX) is None:
+        pytest.skip("no C++ compiler")
+    src = ROOT / "aca_dotnet_workshop_amd" / "native" / "tests" / "apphost_stress.cpp"
+    exe = tmp_path / "apphost_stress"
+    r = subprocess.run([CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(src), "-o", str(exe),
+                        "-lpthread"], capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
+    assert r.returncode == 0, r.stderr[-3000:]
+    run = subprocess.run([str(exe), "20000", "64", str(tmp_path / "ah.sock")], capture_output=True, text=True,
+                         env=dict(os.environ, **env), timeout=600)
+    out = run.stdout + run.stderr
+    assert run.returncode == 0 and "ALL OK" in run.stdout, out[-5000:]
+    assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out and "runtime error" not in out
