@@ -42,6 +42,7 @@ struct Event {
   uint64_t id = 0;      // REQUEST: reply token; RESPONSE/ERROR: the client request id
   int server = 0;       // REQUEST: which listener group (one per Python HttpServer)
   int err = 0;          // ERROR: errno-like code
+  double t = 0;         // loop-thread monotonic time when the event was queued (ev::now_s)
   Message msg;
 };
 
@@ -219,6 +220,7 @@ class AppHost {
   }
 
   void emit(Event&& e) {
+    e.t = ev::now_s();
     bool was_empty;
     {
       std::lock_guard<std::mutex> g(ev_mu_);

@@ -64,7 +64,13 @@ class Gen {
                   done_total_, errors_, t1_ - t0_, pct(0.5), pct(0.99), l.empty() ? 0.0 : l.back() * 1e3);
     std::string s = buf;
     escape_to(s, first_error_);
-    return s + "}";
+    // per step: [ms until the last create returned, ms until the step completed (counter reached)]
+    s += ", \"steps_ms\": [";
+    for (size_t i = 0; i < steps_.size(); ++i) {
+      std::snprintf(buf, sizeof buf, "%s[%.2f, %.2f]", i ? ", " : "", steps_[i].first * 1e3, steps_[i].second * 1e3);
+      s += buf;
+    }
+    return s + "]}";
   }
   long long errors() const { return errors_; }
 
@@ -80,14 +86,18 @@ class Gen {
   size_t rr_ = 0;
   std::vector<double> lat_;
   std::string first_error_;
+  std::vector<std::pair<double, double>> steps_;
+  double step_t0_ = 0, step_creates_ = 0;
 
   void begin_step() {
+    if (step_t0_ > 0) steps_.emplace_back(step_creates_, ev::now_s() - step_t0_);
     if (step_ == o_.steps) {
       t1_ = ev::now_s();
       loop_.stop();
       return;
     }
     issued_ = done_ = 0;
+    step_t0_ = ev::now_s();
     int n = std::min(o_.concurrency, o_.batch);
     for (int i = 0; i < n; ++i) issue();
   }
@@ -115,6 +125,7 @@ class Gen {
   }
 
   void end_step() {
+    step_creates_ = ev::now_s() - step_t0_;
     base_ += o_.batch;
     ++step_;
     if (until_target_.empty()) {

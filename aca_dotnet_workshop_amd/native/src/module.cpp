@@ -287,6 +287,22 @@ PYBIND11_MODULE(_ttnative, m) {
            })
       // [(0, token, server, method, target, http10, headers, body) | (1, id, status, headers, body) |
       //  (2, id, errno, message)]
+      .def("drain_times", [](apphost::AppHost& h) {
+        // same as drain() plus each event's queue time (monotonic seconds) as the last element
+        auto evs = h.drain();
+        py::list out;
+        for (auto& e : evs) {
+          if (e.kind == apphost::Event::REQUEST) {
+            out.append(py::make_tuple(0, e.id, e.server, py::str(e.msg.method), py::str(e.msg.target),
+                                      e.msg.http10, headers_dict(e.msg.headers), py::bytes(e.msg.body), e.t));
+          } else if (e.kind == apphost::Event::RESPONSE) {
+            out.append(py::make_tuple(1, e.id, e.msg.status, headers_dict(e.msg.headers), py::bytes(e.msg.body), e.t));
+          } else {
+            out.append(py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t));
+          }
+        }
+        return out;
+      })
       .def("drain", [](apphost::AppHost& h) {
         auto evs = h.drain();
         py::list out;

@@ -114,7 +114,7 @@ class SidecarClient:
         self.base = base_url or sidecar_base_url()
         if http is None:
             from ..web import native_host
-            http = native_host.NativeHttpClient(timeout=timeout) if native_host.enabled() else HttpClient(timeout=timeout)
+            http = native_host.NativeHttpClient(timeout=timeout) if native_host.enabled(part="client") else HttpClient(timeout=timeout)
         self.http = http
         self.api_token = api_token if api_token is not None else os.environ.get("DAPR_API_TOKEN")
 

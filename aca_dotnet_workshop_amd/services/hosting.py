@@ -99,7 +99,7 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
     config: Configuration = app.services["config"]
     loop = asyncio.get_running_loop()
     from ..web import native_host
-    srv = native_host.NativeHttpServer(app, loop) if native_host.enabled() else HttpServer(app, loop)
+    srv = native_host.NativeHttpServer(app, loop) if native_host.enabled(part="server") else HttpServer(app, loop)
     await app.startup()
     ports = []
     for host, port in listen_addresses(config):

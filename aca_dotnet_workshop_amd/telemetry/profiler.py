@@ -18,8 +18,33 @@ import sys
 from typing import Iterator
 
 
+def _install_gc_log(name: str, path: str, threshold_s: float = 0.02) -> None:
+    """``TT_GC_LOG=<file>``: append one JSON line per garbage-collector pause longer than 20 ms
+    (stall diagnostics: a gen-2 collection stops every Python thread of the process)."""
+    import gc
+    import json
+    import time
+    start = [0.0]
+    out = open(path, "a", buffering=1)
+
+    def cb(phase: str, info: dict) -> None:
+        if phase == "start":
+            start[0] = time.perf_counter()
+            return
+        d = time.perf_counter() - start[0]
+        if d > threshold_s:
+            out.write(json.dumps({"what": "gc-pause", "proc": name, "pid": os.getpid(), "gen": info["generation"],
+                                  "ms": round(d * 1e3, 2), "collected": info["collected"],
+                                  "objects": len(gc.get_objects(info["generation"])) if info["generation"] < 2 else None,
+                                  "wall": round(time.time(), 4)}) + "\n")
+    gc.callbacks.append(cb)
+
+
 @contextlib.contextmanager
 def maybe_profile(name: str) -> Iterator[None]:
+    gc_log = os.environ.get("TT_GC_LOG")
+    if gc_log:
+        _install_gc_log(name, gc_log)
     out_dir = os.environ.get("TT_PROFILE_DIR")
     if not out_dir:
         yield

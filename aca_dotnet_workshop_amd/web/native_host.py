@@ -30,9 +30,11 @@ log = logging.getLogger("web.native")
 Handler = Callable[[Request], Awaitable[Response]]
 
 
-def enabled(environ: dict[str, str] | None = None) -> bool:
+def enabled(environ: dict[str, str] | None = None, part: str = "") -> bool:
+    """``TT_APP_HOST=native`` (server and client), or ``native-server`` / ``native-client``."""
     env = os.environ if environ is None else environ
-    return env.get("TT_APP_HOST", "").lower() == "native"
+    v = env.get("TT_APP_HOST", "").lower()
+    return v == "native" or (bool(part) and v == f"native-{part}")
 
 
 def _client_error(err: int, msg: str) -> BaseException:
@@ -72,6 +74,54 @@ class NativeHost:
         self.users = 0
         self.closed = False
         self._ops: list[tuple] = []  # respond/request operations of this loop iteration
+        # TT_STALL_LOG=<file>: record every hand-off slower than 20 ms (diagnostics)
+        path = os.environ.get("TT_STALL_LOG")
+        self._stall = open(path, "a", buffering=1) if path else None
+        self._t_submit: dict[int, float] = {}
+        self._t_flush: dict[int, float] = {}
+        self._last_wake = 0.0
+
+    def _note(self, what: str, **kw: Any) -> None:
+        import time as _t
+        kw.update(what=what, pid=os.getpid(), wall=round(_t.time(), 4))
+        self._stall.write(json.dumps(kw) + "\n")
+
+    def _on_events_traced(self) -> None:
+        import time as _t
+        now = _t.monotonic()
+        evs = self.h.drain_times()
+        if self._last_wake and now - self._last_wake > 0.05:
+            self._note("python-idle-gap", gap_ms=round((now - self._last_wake) * 1e3, 2), events=len(evs))
+        self._last_wake = now
+        if evs:
+            lag = now - min(e[-1] for e in evs)
+            if lag > 0.02:
+                self._note("wake-lag", lag_ms=round(lag * 1e3, 2), batch=len(evs),
+                           kinds=sorted({e[0] for e in evs}))
+        for ev in evs:
+            lag = now - ev[-1]
+            kind = ev[0]
+            if kind == 0:
+                _, token, sid, method, target, http10, hd, body, _ = ev
+                srv = self.servers.get(sid)
+                if srv is None:
+                    self.respond(token, 503, [], b"")
+                    continue
+                srv._dispatch(token, method, target, http10, hd, body)
+            else:
+                rid = ev[1]
+                t0 = self._t_submit.pop(rid, None)
+                tf = self._t_flush.pop(rid, None)
+                if t0 is not None and tf is not None and ev[-1] - tf[0] > 0.02:
+                    self._note("client-slow", rid=rid, target=tf[1], queue_ms=round((tf[0] - t0) * 1e3, 2),
+                               io_ms=round((ev[-1] - tf[0]) * 1e3, 2), wake_ms=round(lag * 1e3, 2))
+                fut = self.pending.pop(rid, None)
+                if fut is None or fut.done():
+                    continue
+                if kind == 1:
+                    fut.set_result(ClientResponse(ev[2], Headers(ev[3]), ev[4]))
+                else:
+                    fut.set_exception(_client_error(ev[2], ev[3]))
 
     def _queue(self, op: tuple) -> None:
         if not self._ops:
@@ -80,6 +130,12 @@ class NativeHost:
 
     def _flush(self) -> None:
         ops, self._ops = self._ops, []
+        if self._stall is not None:
+            import time as _t
+            now = _t.monotonic()
+            for op in ops:
+                if op[0] == 1:
+                    self._t_flush[op[1]] = (now, op[4][:48])
         if ops and not self.closed:
             self.h.submit(ops)
 
@@ -93,6 +149,8 @@ class NativeHost:
         return sid
 
     def _on_events(self) -> None:
+        if self._stall is not None:
+            return self._on_events_traced()
         for ev in self.h.drain():
             kind = ev[0]
             if kind == 0:
@@ -117,6 +175,9 @@ class NativeHost:
         self._next_id += 1
         fut = self.loop.create_future()
         self.pending[rid] = fut
+        if self._stall is not None:
+            import time as _t
+            self._t_submit[rid] = _t.monotonic()
         self._queue((1, rid, endpoint, method, target, headers, body, timeout))
         return fut
 
@@ -173,6 +234,12 @@ class NativeHttpServer:
         return self.ports[0]
 
     def _dispatch(self, token: int, method: str, target: str, http10: bool, hd: dict, body: bytes) -> None:
+        if self.host._stall is not None:
+            import time as _t
+            self.loop.create_task(self._serve_traced(token, Request(method, target, Headers(hd), body, None,
+                                                                    "HTTP/1.0" if http10 else "HTTP/1.1"), _t.monotonic()))
+            self._inflight += 1
+            return
         req = Request(method, target, Headers(hd), body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
         self._inflight += 1
         self.loop.create_task(self._serve(token, req))
@@ -188,6 +255,15 @@ class NativeHttpServer:
             self.host.respond(token, resp.status, resp.headers, body)
         finally:
             self._inflight -= 1
+
+    async def _serve_traced(self, token: int, req: Request, t0: float) -> None:
+        import time as _t
+        t1 = _t.monotonic()
+        await self._serve(token, req)
+        t2 = _t.monotonic()
+        if t2 - t0 > 0.05:
+            self.host._note("handler-slow", target=req.target[:60], start_ms=round((t1 - t0) * 1e3, 2),
+                            run_ms=round((t2 - t1) * 1e3, 2))
 
     async def close(self, grace: float = 5.0) -> None:
         if self._closing:

@@ -45,6 +45,8 @@ def parse() -> argparse.Namespace:
                     help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
     ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
+    ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "python"),
+                    help="services' HTTP I/O: python (asyncio) | native (apphost.hpp) | api=native,processor=python")
     ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
                     help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")
     ap.add_argument("--client", choices=("native", "python"), default="native",
@@ -115,6 +117,27 @@ def topology(cores: float) -> tuple[int, int]:
     api = max(1, min(8, int(cores / 2.6)))
     proc = max(1, min(5, int(cores // 5)))
     return max(api, 2 if cores >= 6 else 1), max(proc, 2 if cores >= 6 else 1)
+
+
+def app_host(app: str, spec: str) -> str:
+    """``native`` / ``python`` for every app, or per app: ``api=native,processor=python``."""
+    if "=" not in spec:
+        return spec
+    return dict(p.split("=", 1) for p in spec.split(",")).get(app, "python")
+
+
+def cgroup_throttling() -> dict[str, int]:
+    """cgroup v2 ``cpu.stat`` throttling counters (the job's CPU quota being hit stalls every
+    thread of the job until the next CFS period)."""
+    out = {}
+    try:
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k in ("nr_periods", "nr_throttled", "throttled_usec"):
+                out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def device_sync() -> None:
@@ -206,9 +229,11 @@ def main() -> None:
         if a.split_backing:
             backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
         for _ in range(a.api_replicas):
-            stack.start_replica("tasksmanager-backend-api", cfg, grpc=a.api_protocol == "grpc")
+            stack.start_replica("tasksmanager-backend-api", cfg, grpc=a.api_protocol == "grpc",
+                                extra_env={"TT_APP_HOST": app_host("api", a.app_host)})
         for _ in range(a.processor_replicas):
-            stack.start_replica("tasksmanager-backend-processor", cfg, grpc=a.api_protocol == "grpc")
+            stack.start_replica("tasksmanager-backend-processor", cfg, grpc=a.api_protocol == "grpc",
+                                extra_env={"TT_APP_HOST": app_host("processor", a.app_host)})
         stack.wait_ready()
         socks = [r.sidecar_uds for r in stack.replicas["tasksmanager-backend-api"]]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
@@ -229,6 +254,7 @@ def main() -> None:
         device_sync()
         import psutil
         me = psutil.Process()
+        thr0 = cgroup_throttling()
         cpu0 = stack.cpu_seconds()
         t = me.cpu_times()
         cpu0["bench-client"] = t.user + t.system + t.children_user + t.children_system
@@ -240,6 +266,7 @@ def main() -> None:
         device_sync()
         d.barrier()
         cpu1 = stack.cpu_seconds()
+        thr1 = cgroup_throttling()
         t = me.cpu_times()
         cpu1["bench-client"] = t.user + t.system + t.children_user + t.children_system
         dt_max = d.max(dt)
@@ -247,7 +274,9 @@ def main() -> None:
             # cores busy per process role during the timed region (where the E2E flow is CPU bound)
             util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
             print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
-                              "cpu_budget_per_rank": round(cores, 2)}),
+                              "cpu_budget_per_rank": round(cores, 2),
+                              "cgroup_throttling": {k: thr1[k] - thr0.get(k, 0) for k in thr1},
+                              "loadgen": report}),
                   file=sys.stderr, flush=True)
         lat.sort()
         if report is not None:
@@ -269,6 +298,7 @@ def main() -> None:
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
                            "sidecar_api_protocol": a.api_protocol,
+                           "app_host": a.app_host,
                            "create_latency_p50_ms": round(p50, 3),
                            "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput"}}),
                 flush=True)
