@@ -25,6 +25,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <future>
 #include <mutex>
 #include <thread>
@@ -49,20 +52,32 @@ struct Event {
 class AppHost {
  public:
   AppHost() {
+    ev::reserve_fd_table();  // no fd-table growth (RCU waits) once the I/O thread runs
     to_py_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     auto w = std::make_shared<Waker>(*this);
     w->fd = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     to_loop_ = w->fd;
     loop_.add(w, EPOLLIN);
   }
-  ~AppHost() { stop(); ::close(to_py_); }
+  ~AppHost() {
+    stop();
+    ::close(to_py_);
+    if (trace_) std::fclose(trace_);
+  }
 
   int event_fd() const { return to_py_; }
 
   void start() {
     if (thread_.joinable()) return;
+    if (const char* p = std::getenv("TT_STALL_LOG"); p && *p) trace_ = std::fopen(p, "a");
     thread_ = std::thread([this] {
-      loop_.run();
+      if (!trace_) {
+        loop_.run();
+        return;
+      }
+      // diagnostics: loop iterations > 100 ms apart and slow command batches
+      ev::GapTracer gaps("apphost");
+      loop_.run([&gaps](double now) { gaps.tick(now); });
     });
   }
 
@@ -125,6 +140,15 @@ class AppHost {
   void submit(std::vector<Op>&& ops) {
     post([this, ops = std::move(ops)]() mutable {
       for (auto& op : ops) {
+        double t0 = trace_ ? ev::now_s() : 0;
+        struct OpTimer {  // diagnostics: one slow operation inside a batch
+          AppHost* h;
+          double t0;
+          bool req;
+          ~OpTimer() {
+            if (h->trace_ && ev::now_s() - t0 > 0.02) h->note(req ? "op-request-slow" : "op-respond-slow", (ev::now_s() - t0) * 1e3);
+          }
+        } timer{this, t0, op.is_request};
         if (!op.is_request) {
           auto it = replies_.find(op.id);
           if (it == replies_.end()) continue;
@@ -178,6 +202,14 @@ class AppHost {
 
   ev::Loop loop_;
   ev::Client client_{loop_};
+  FILE* trace_ = nullptr;
+
+  void note(const char* what, double ms, size_t n = 0) {
+    std::fprintf(trace_, "{\"what\": \"%s\", \"ms\": %.2f, \"n\": %zu, \"pid\": %d, \"wall\": %.4f}\n", what, ms, n,
+                 (int)::getpid(),
+                 std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count());
+    std::fflush(trace_);
+  }
   std::thread thread_;
   int to_py_ = -1;
   int to_loop_ = -1;
@@ -215,7 +247,9 @@ class AppHost {
       std::lock_guard<std::mutex> g(cmd_mu_);
       cmds.swap(cmds_);
     }
+    double t0 = trace_ ? ev::now_s() : 0;
     for (auto& c : cmds) c();
+    if (trace_ && ev::now_s() - t0 > 0.02) note("io-commands-slow", (ev::now_s() - t0) * 1e3, cmds.size());
     pending_replies_.store(replies_.size());
   }
 

@@ -63,6 +63,7 @@ class BackingFront {
   // `threads` event loops share the port via SO_REUSEPORT (connections are spread by the kernel).
   BackingFront(const std::string& host, int port, const std::string& fallback_uds, int threads = 1)
       : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)) {
+    ev::reserve_fd_table();  // accept() must not grow the fd table (RCU wait) under load
     threads = std::max(1, std::min(threads, 64));
     for (int i = 0; i < threads; ++i) shards_.push_back(std::make_unique<Shard>(*this));
     ev::Endpoint ep;
@@ -172,7 +173,13 @@ class BackingFront {
       if (wake_fd >= 0) ::close(wake_fd);
     }
     void start() {
-      thread = std::thread([this] { loop.run([this](double t) { on_tick(t); }); });
+      thread = std::thread([this] {
+        ev::GapTracer gaps("backing-front");
+        loop.run([this, &gaps](double t) {
+          gaps.tick(t);
+          on_tick(t);
+        });
+      });
     }
     void wake() {
       uint64_t one = 1;

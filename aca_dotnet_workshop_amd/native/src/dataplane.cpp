@@ -1324,7 +1324,9 @@ int main(int argc, char** argv) {
     std::rename(tmp.c_str(), pf->c_str());
   }
   double last_flush = ev::now_s();
+  ev::GapTracer gaps("dataplane");
   loop.run([&](double t) {
+    gaps.tick(t);
     if (t - last_flush > 1.0) {
       dp.flush();
       last_flush = t;

@@ -25,6 +25,9 @@
 
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <sys/resource.h>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -139,6 +142,63 @@ class Loop {
   std::vector<std::function<void()>> deferred_;
   std::multimap<double, std::function<void()>> timers_;
 };
+
+// Diagnostics: with TT_STALL_LOG=<file>, a loop's tick reports iterations more than 100 ms
+// apart (the thread was blocked or not scheduled) as JSON lines.
+class GapTracer {
+ public:
+  explicit GapTracer(const char* who) : who_(who) {
+    if (const char* p = std::getenv("TT_STALL_LOG"); p && *p) f_ = std::fopen(p, "a");
+  }
+  ~GapTracer() {
+    if (f_) std::fclose(f_);
+  }
+  void tick(double now) {
+    if (f_ && last_ > 0 && now - last_ > 0.1)
+      std::fprintf(f_, "{\"what\": \"loop-gap\", \"who\": \"%s\", \"ms\": %.2f, \"pid\": %d, \"wall\": %.4f}\n", who_,
+                   (now - last_) * 1e3, (int)::getpid(),
+                   std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count()),
+          std::fflush(f_);
+    last_ = now;
+  }
+
+ private:
+  const char* who_;
+  FILE* f_ = nullptr;
+  double last_ = 0;
+};
+
+// Grow this process's file-descriptor table once, up front.  The kernel expands the table in
+// powers of two as descriptors are allocated, and in a multi-threaded process every expansion
+// waits for an RCU grace period (expand_fdtable -> synchronize_rcu), which on a large busy host
+// takes 100+ ms -- measured as 90-175 ms socket()/connect() calls stalling a whole event loop.
+// Call before starting I/O threads (or any time: it is one expansion instead of several).
+inline void reserve_fd_table(int want = 1 << 16) {
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) != 0) return;
+  long top = std::min<long>((long)rl.rlim_cur, want) - 1;
+  if (top < 64) return;
+  int src = ::open("/dev/null", O_RDONLY | O_CLOEXEC);
+  if (src < 0) return;
+  int d = ::dup2(src, (int)top);  // allocates the slot -> table sized to cover `top`
+  if (d >= 0) ::close(d);
+  ::close(src);
+}
+
+inline FILE* stall_log() {  // TT_STALL_LOG, shared by the diagnostics below (nullptr when unset)
+  static FILE* f = [] {
+    const char* p = std::getenv("TT_STALL_LOG");
+    return p && *p ? std::fopen(p, "a") : nullptr;
+  }();
+  return f;
+}
+
+inline void stall_note(const char* what, double ms, long n = 0) {
+  if (FILE* f = stall_log()) {
+    std::fprintf(f, "{\"what\": \"%s\", \"ms\": %.2f, \"n\": %ld, \"pid\": %d}\n", what, ms, n, (int)::getpid());
+    std::fflush(f);
+  }
+}
 
 // ------------------------------------------------------------------------------ messages
 using HeaderList = std::vector<std::pair<std::string, std::string>>;
@@ -766,7 +826,20 @@ class Client {
       c->reused = true;
     } else {
       int err = 0;
+      double tc = stall_log() ? now_s() : 0;
       c = connect(ep, key, err);
+      if (tc > 0 && now_s() - tc > 0.02) stall_note("client-connect-slow", (now_s() - tc) * 1e3, err);
+      if (!c && err == EAGAIN && (deadline == 0 || now_s() < deadline)) {
+        // Unix listener backlog full: try again shortly instead of blocking the loop in connect()
+        auto ep_copy = ep;
+        loop_.call_later(0.0005, [this, ep_copy, wire = std::move(wire), head, timeout_s, cb = std::move(cb),
+                                  allow_retry, deadline]() mutable {
+          double left = deadline > 0 ? deadline - now_s() : 0;
+          dispatch(ep_copy, std::move(wire), head, deadline > 0 ? std::max(left, 1e-3) : timeout_s, std::move(cb),
+                   allow_retry);
+        });
+        return;
+      }
       if (!c) {
         loop_.defer([cb = std::move(cb), err]() mutable {
           ClientResult r;
@@ -788,9 +861,13 @@ class Client {
         }
         cb(std::move(r));
       };
+      double ts = stall_log() ? now_s() : 0;
       c->start(std::move(wire), head, deadline, std::move(inner));
+      if (ts > 0 && now_s() - ts > 0.02) stall_note("client-start-slow", (now_s() - ts) * 1e3, 1);
     } else {
+      double ts = stall_log() ? now_s() : 0;
       c->start(std::move(wire), head, deadline, std::move(cb));
+      if (ts > 0 && now_s() - ts > 0.02) stall_note("client-start-slow", (now_s() - ts) * 1e3, 0);
     }
   }
 
@@ -802,17 +879,18 @@ class Client {
     int fd;
     bool in_progress = false;
     if (ep.unix_socket) {
-      fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      // non-blocking: a local connect completes at once, or fails with EAGAIN while the
+      // listener's accept queue is full -- the caller retries then, rather than parking the
+      // whole event loop in connect() until the peer gets round to accept()
+      fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
       sockaddr_un a{};
       a.sun_family = AF_UNIX;
       std::strncpy(a.sun_path, ep.path.c_str(), sizeof a.sun_path - 1);
-      // blocking connect on a local socket: completes immediately (or waits for backlog room)
       if (::connect(fd, (sockaddr*)&a, sizeof a) != 0) {
-        err = errno;
+        err = errno == EWOULDBLOCK ? EAGAIN : errno;
         ::close(fd);
         return nullptr;
       }
-      set_nonblock(fd);
     } else {
       fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
       int one = 1;

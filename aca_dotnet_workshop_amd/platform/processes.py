@@ -65,6 +65,8 @@ class LocalStack:
         self.base_env = dict(os.environ)
         # process-based deployments run the sidecar's native C++ data plane unless told otherwise
         self.base_env.setdefault("TT_SIDECAR_DATAPLANE", "native")
+        # ... and the services' HTTP I/O on the native app host (native/src/apphost.hpp)
+        self.base_env.setdefault("TT_APP_HOST", "native")
         self.base_env["PYTHONPATH"] = str(REPO_ROOT) + os.pathsep + self.base_env.get("PYTHONPATH", "")
         self.base_env.update(env or {})
         self.log_dir = Path(log_dir) if log_dir else self.root / "logs"

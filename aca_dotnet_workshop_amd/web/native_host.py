@@ -9,7 +9,8 @@ of completed I/O, turns each event into a ``Request`` (server side) or resolves 
 a ``ClientResponse`` (client side), and hands responses / new requests back in one call each.
 
 Selected with ``TT_APP_HOST=native`` (``hosting.serve_host`` and the SDK's ``SidecarClient``);
-the platform's process launcher sets it for the service processes.  Missing extension = hard
+the platform's process launcher (``LocalStack``) sets it for the service processes unless the
+environment says otherwise; in-process uses (tests, ``inproc``) keep the asyncio I/O.  Missing extension = hard
 error (no silent fallback when the native host was asked for).
 """
 from __future__ import annotations

@@ -45,7 +45,7 @@ def parse() -> argparse.Namespace:
                     help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
     ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
-    ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "python"),
+    ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "native"),
                     help="services' HTTP I/O: python (asyncio) | native (apphost.hpp) | api=native,processor=python")
     ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
                     help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")

@@ -5,8 +5,8 @@ set -euo pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 cd "$(dirname "$0")/.."
-for i in 1 2; do
-  for mode in python native native-server native-client; do
+for i in 1 2 3; do
+  for mode in python native; do
     timeout -k 10 300 python bench.py --steps 40 --warmup 5 --app-host "$mode" > gpurun_out/ab_${mode}_$i.json 2> gpurun_out/ab_${mode}_$i.err
   done
 done
