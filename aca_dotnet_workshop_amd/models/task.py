@@ -56,13 +56,14 @@ class WireModel(BaseModel):
         cls._lower_aliases = {
             (f.alias or name).lower(): (f.alias or name) for name, f in cls.model_fields.items()
         }
-        cls._aliases = frozenset(cls._lower_aliases.values())
+        # keys that need no remapping: the camelCase aliases and the Python field names
+        cls._aliases = frozenset(cls._lower_aliases.values()) | frozenset(cls.model_fields)
 
     @model_validator(mode="before")
     @classmethod
     def _case_insensitive(cls, data: Any) -> Any:
         if isinstance(data, dict):
-            if cls._aliases.issuperset(data):  # already canonical camelCase (the common case)
+            if cls._aliases.issuperset(data):  # canonical camelCase or field names (the common case)
                 return data
             la = cls._lower_aliases
             out = {}
