@@ -44,7 +44,7 @@ static ev::HeaderList header_list(const py::handle& seq) {
     auto t = item.cast<py::tuple>();
     std::string k = t[0].cast<std::string>();
     for (auto& ch : k) ch = (char)std::tolower((unsigned char)ch);
-    out.emplace_back(std::move(k), t[1].cast<std::string>());
+    out.emplace_back(std::move(k), py::str(t[1]).cast<std::string>());  // any value, like f"{v}"
   }
   return out;
 }

@@ -79,7 +79,7 @@ class NativeHost:
         path = os.environ.get("TT_STALL_LOG")
         self._stall = open(path, "a", buffering=1) if path else None
         self._t_submit: dict[int, float] = {}
-        self._t_flush: dict[int, float] = {}
+        self._t_flush: dict[int, tuple[float, str]] = {}
         self._last_wake = 0.0
 
     def _note(self, what: str, **kw: Any) -> None:
@@ -138,7 +138,22 @@ class NativeHost:
                 if op[0] == 1:
                     self._t_flush[op[1]] = (now, op[4][:48])
         if ops and not self.closed:
-            self.h.submit(ops)
+            try:
+                self.h.submit(ops)
+            except Exception:
+                # one malformed operation must not lose the whole batch: retry one by one and
+                # fail only the bad ones (500 for a response, an exception for a request)
+                for op in ops:
+                    try:
+                        self.h.submit([op])
+                    except Exception as e:
+                        log.exception("native host rejected an operation")
+                        if op[0] == 0:
+                            self.h.submit([(0, op[1], 500, [], b"")])
+                        else:
+                            fut = self.pending.pop(op[1], None)
+                            if fut is not None and not fut.done():
+                                fut.set_exception(ValueError(f"invalid request: {e}"))
 
     def respond(self, token: int, status: int, headers: list, body: bytes) -> None:
         self._queue((0, token, status, headers, body))
@@ -153,22 +168,25 @@ class NativeHost:
         if self._stall is not None:
             return self._on_events_traced()
         for ev in self.h.drain():
-            kind = ev[0]
-            if kind == 0:
-                _, token, sid, method, target, http10, hd, body = ev
-                srv = self.servers.get(sid)
-                if srv is None:
-                    self.respond(token, 503, [], b"")
-                    continue
-                srv._dispatch(token, method, target, http10, hd, body)
-            elif kind == 1:
-                fut = self.pending.pop(ev[1], None)
-                if fut is not None and not fut.done():
-                    fut.set_result(ClientResponse(ev[2], Headers(ev[3]), ev[4]))
-            else:
-                fut = self.pending.pop(ev[1], None)
-                if fut is not None and not fut.done():
-                    fut.set_exception(_client_error(ev[2], ev[3]))
+            try:
+                kind = ev[0]
+                if kind == 0:
+                    _, token, sid, method, target, http10, hd, body = ev
+                    srv = self.servers.get(sid)
+                    if srv is None:
+                        self.respond(token, 503, [], b"")
+                        continue
+                    srv._dispatch(token, method, target, http10, hd, body)
+                elif kind == 1:
+                    fut = self.pending.pop(ev[1], None)
+                    if fut is not None and not fut.done():
+                        fut.set_result(ClientResponse(ev[2], Headers(ev[3]), ev[4]))
+                else:
+                    fut = self.pending.pop(ev[1], None)
+                    if fut is not None and not fut.done():
+                        fut.set_exception(_client_error(ev[2], ev[3]))
+            except Exception:  # one bad event must not strand the rest of the batch
+                log.exception("native host event %r failed", ev[:2])
 
     def request(self, endpoint: str, method: str, target: str, headers: list[tuple[str, str]], body: bytes,
                 timeout: float) -> asyncio.Future:

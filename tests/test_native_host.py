@@ -151,3 +151,29 @@ def test_client_errors_and_server_close(tmp_path):
 
 def test_enabled_switch():
     assert enabled({"TT_APP_HOST": "native"}) and not enabled({}) and not enabled({"TT_APP_HOST": "python"})
+
+
+def test_odd_header_values_and_bad_operations():
+    """Non-string header values are stringified (like the asyncio server's f"{k}: {v}"); a
+    request with an unusable body fails on its own without losing the rest of the batch."""
+    app = WebApp("odd")
+
+    @app.route("/odd", ("GET",))
+    async def odd(req):
+        return Response(b"ok", 200, [("X-Count", 5), ("X-Ratio", 0.5)])
+
+    async def main():
+        srv = NativeHttpServer(app, asyncio.get_running_loop())
+        port = await srv.listen_tcp("127.0.0.1", 0)
+        c = NativeHttpClient()
+        r = await c.get(f"http://127.0.0.1:{port}/odd")
+        assert r.status == 200 and r.headers["x-count"] == "5" and r.headers["x-ratio"] == "0.5"
+        host = c._native()
+        bad = host.request(f"tcp:127.0.0.1:{port}", "POST", "/odd", [], 12345, 5.0)  # body is not bytes
+        good = c.get(f"http://127.0.0.1:{port}/odd")
+        with pytest.raises(ValueError):
+            await bad
+        assert (await good).status == 200
+        await c.close()
+        await srv.close(1)
+    run(main())
