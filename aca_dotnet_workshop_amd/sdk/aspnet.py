@@ -73,6 +73,7 @@ def cloud_events_middleware():
                         req.body = d.encode()
                     else:
                         req.body = json.dumps(d).encode()
+                        req.state["json"] = (req.body, d)  # Request.json() reuses the parsed data
                 req.headers["content-type"] = dct
         return await nxt(req)
     return mw

@@ -95,6 +95,9 @@ class Request:
     def json(self) -> Any:
         if not self.body:
             return None
+        cached = self.state.get("json")  # set by middleware that already parsed the body
+        if cached is not None and cached[0] is self.body:
+            return cached[1]
         return json.loads(self.body)
 
     def form(self) -> dict[str, str]:

@@ -177,3 +177,18 @@ def test_odd_header_values_and_bad_operations():
         await c.close()
         await srv.close(1)
     run(main())
+
+
+def test_fd_table_reserved_before_io_thread():
+    """The host sizes the process's fd table up front (kernel fd-table growth in a multi-threaded
+    process waits for an RCU grace period: 100+ ms event-loop stalls, profiles/r1_native_app_host_ab.md)."""
+    import resource
+
+    from aca_dotnet_workshop_amd import native
+    h = native.load().AppHost()
+    try:
+        fdsize = int(open("/proc/self/status").read().split("FDSize:")[1].split()[0])
+        soft = resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+        assert fdsize >= min(soft, 1 << 16) - 1
+    finally:
+        h.stop()
