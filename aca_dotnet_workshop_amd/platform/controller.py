@@ -314,6 +314,16 @@ class EnvironmentController:
         backoff: dict[str, float] = {}
         while True:
             await asyncio.sleep(0.5)
+            if not self.stack.backing_alive():
+                # the managed services' equivalent: restart in place over the durable logs
+                code = self.stack.backing_proc.poll() if self.stack.backing_proc is not None else None
+                self.event("BackingServicesCrashed", code=code)
+                try:
+                    await asyncio.to_thread(self.stack.restart_backing)
+                    await self._provision()  # idempotent: entities already replayed from the logs
+                    self.event("BackingServicesRestarted", url=self.stack.backing_url)
+                except Exception as e:
+                    self.event("BackingServicesFailedToStart", error=str(e))
             for rt in self.apps.values():
                 rev = rt.current
                 if rev is None:

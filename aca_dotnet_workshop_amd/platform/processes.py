@@ -99,7 +99,35 @@ class LocalStack:
         self.backing_proc = self._spawn(args, self.base_env, "backing")
         port = _wait_file(pf, timeout, self.backing_proc)
         self.backing_url = f"http://127.0.0.1:{port}"
+        self._backing_args = args
+        self._backing_port = int(port)
         return self.backing_url
+
+    def backing_alive(self) -> bool:
+        return self.backing_proc is not None and self.backing_proc.poll() is None
+
+    def restart_backing(self, timeout: float = 60.0) -> str:
+        """Start the backing-services process again on the SAME port (sidecars keep their URL)
+        over the same data directory: documents, messages, subscriptions and locks come back from
+        the engines' durable logs (replayed on open)."""
+        if self.backing_proc is not None and self.backing_proc.poll() is None:
+            self.backing_proc.kill()
+            self.backing_proc.wait()
+        pf = self.root / "backing.port"
+        if pf.exists():
+            pf.unlink()
+        args = list(self._backing_args)
+        args[args.index("--port") + 1] = str(self._backing_port)
+        deadline = time.time() + timeout
+        while True:  # the old listener's port may take a moment to be released
+            self.backing_proc = self._spawn(args, self.base_env, "backing")
+            try:
+                _wait_file(pf, max(1.0, deadline - time.time()), self.backing_proc)
+                return self.backing_url
+            except Exception:
+                if time.time() > deadline:
+                    raise
+                time.sleep(0.2)
 
     def start_backing_family(self, families: list[str], timeout: float = 60.0) -> str:
         """Run a separate backing-services process for some service families (e.g.

@@ -165,6 +165,16 @@ def test_environment_lifecycle(tmp_path):
             assert proc.current.name != old and res["newRevisions"] == [proc.current.name]
             assert [r.active for r in proc.revisions] == [False, True]
             assert (tmp_path / "env" / "state.json").exists()
+            # the backing services crash: the supervisor restarts them in place over their logs
+            os.kill(ctl.stack.backing_proc.pid, signal.SIGKILL)
+            for _ in range(300):
+                await asyncio.sleep(0.1)
+                if any(e["kind"] == "BackingServicesRestarted" for e in ctl.events):
+                    break
+            kinds = [e["kind"] for e in ctl.events]
+            assert "BackingServicesCrashed" in kinds and "BackingServicesRestarted" in kinds
+            c2 = await b.sb_counts("taskstracker", "tasksavedtopic/subscriptions/tasksmanager-backend-processor")
+            assert c2["active"] == 0 and c2["dead_letter"] == 0  # settled messages stay settled after replay
         finally:
             await ctl.down()
     run(main())

@@ -64,3 +64,56 @@ def test_killed_consumer_messages_are_redelivered(tmp_path):
         assert victim.proc.wait(timeout=10) == -signal.SIGKILL
     finally:
         stack.stop()
+
+
+def test_backing_services_crash_and_restart_in_place(tmp_path):
+    """The backing-services process (Cosmos / Service Bus equivalents) is SIGKILLed mid-run and
+    restarted on the same port over its data directory: saved tasks and undelivered messages come
+    back from the engines' durable logs, the sidecars' native data planes reconnect, and the
+    createTask flow works again end to end."""
+    from aca_dotnet_workshop_amd.web.client import HttpClient
+    stack = LocalStack(root=tmp_path / "stack")
+    try:
+        backing = stack.start_backing(str(tmp_path / "data"))
+        cfg = {"Logging:LogLevel:Default": "Warning", "TasksNotifier:Mode": "log"}
+        api = stack.start_replica("tasksmanager-backend-api", cfg)
+        stack.wait_ready()
+        url = f"unix:{api.sidecar_uds}:/v1.0/invoke/tasksmanager-backend-api/method/api/tasks"
+        body = b'{"taskName":"%s","taskCreatedBy":"dur@x","taskDueDate":"2030-01-01T00:00:00","taskAssignedTo":"a@x"}'
+
+        def crash_and_restart():
+            os.kill(stack.backing_proc.pid, signal.SIGKILL)
+            stack.backing_proc.wait(timeout=10)
+            return stack.restart_backing()
+
+        async def main():
+            c = HttpClient()
+            b = BackingClient(backing, identity="tasksmanager-backend-api")
+
+            async def create(name):
+                r = await c.post(url, body=body % name.encode(), headers={"Content-Type": "application/json"})
+                return r.status
+            # the processor's subscription, provisioned as the platform does (no processor runs:
+            # the events wait in it)
+            await b.sb_create_topic("taskstracker", "tasksavedtopic")
+            await b.sb_create_subscription("taskstracker", "tasksavedtopic", "tasksmanager-backend-processor", 60000, 10)
+            assert [await create(f"t{i}") for i in range(20)] == [201] * 20
+            assert (await b.sb_counts("taskstracker", ENTITY))["active"] == 20
+            assert await asyncio.to_thread(crash_and_restart) == backing
+            for _ in range(100):  # the data plane's pooled connections to the dead process fail once
+                if await create("after") == 201:
+                    break
+                await asyncio.sleep(0.05)
+            else:
+                raise AssertionError("createTask did not recover after the backing restart")
+            r = await c.get(url + "?createdBy=dur@x")
+            names = sorted(t["taskName"] for t in r.json())
+            counts = await b.sb_counts("taskstracker", ENTITY)
+            await c.close()
+            await b.http.close()
+            return names, counts
+        names, counts = run(main())
+        assert names == sorted([f"t{i}" for i in range(20)] + ["after"])
+        assert counts["active"] == 21
+    finally:
+        stack.stop()
