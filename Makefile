@@ -2,7 +2,7 @@
 PY ?= python
 ENV_DIR ?= .tt-env
 
-.PHONY: build test test-gpu sanitize bench bench-query bench-query-e2e up down status metrics validate what-if docs docs-local clean
+.PHONY: build test test-gpu sanitize bench bench-query bench-query-e2e images up down status metrics validate what-if docs docs-local clean
 
 build:            ## compile native engines, sidecar data plane, load generator and gfx950 HIP kernels in-tree
 	$(PY) -c "import __graft_entry__ as g; g.build()"
@@ -24,6 +24,9 @@ bench-query:      ## GPU state-query scan microbenchmark (scan + ordering)
 
 bench-query-e2e:  ## state-query latency through the stack (GPU accelerator, 2M docs)
 	$(PY) bench_query_e2e.py --docs 2000000 --accel gpu
+
+images:           ## OCI images of the three services (standard + chiseled), verified under chroot when root
+	$(PY) -m aca_dotnet_workshop_amd.platform image --out dist/images --verify
 
 validate:
 	$(PY) -m aca_dotnet_workshop_amd.platform validate -f deploy/main.yaml -p deploy/main.parameters.json
