@@ -52,3 +52,15 @@ def test_bench_two_ranks_torchrun():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     _check(lines[0], 2, 2, 1)
+
+
+def test_bench_latency_runs():
+    """bench_latency.py (SURVEY §7.5's own latency benchmarks): 2-hop CRUD and publish->ack lines."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    r = subprocess.run([sys.executable, "bench_latency.py", "--ops", "3", "--events", "3", "--skip-scale"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert [x["metric"] for x in lines] == ["crud_latency_two_sidecar_hops", "publish_to_ack_latency"]
+    assert set(lines[0]["ops"]) == {"create", "get", "list", "update", "complete", "delete"}
+    assert lines[1]["n"] == 3 and lines[1]["p50_ms"] > 0
