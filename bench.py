@@ -31,6 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+from aca_dotnet_workshop_amd.parallel import Dist, cgroup_throttling, cpu_budget, topology  # noqa: E402
+
+
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,90 +57,11 @@ def parse() -> argparse.Namespace:
     return ap.parse_args()
 
 
-class Dist:
-    """Rank coordination over torch.distributed (gloo: this workload has no tensors)."""
-
-    def __init__(self) -> None:
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-            dist.init_process_group("gloo", init_method="env://")
-            self.pg = dist
-
-    def barrier(self) -> None:
-        if self.pg is not None:
-            self.pg.barrier()
-
-    def max(self, v: float) -> float:
-        if self.pg is None:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, v: float) -> float:
-        if self.pg is None:
-            return v
-        import torch
-        t = torch.tensor([v], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
-
-    def close(self) -> None:
-        if self.pg is not None:
-            self.pg.destroy_process_group()
-
-
-def cpu_budget() -> float:
-    """CPUs this process may use: cgroup v2/v1 quota, else the affinity mask (a GPU box's
-    ``nproc`` shows the whole machine while the job gets a share of it)."""
-    n = float(len(os.sched_getaffinity(0)))
-    try:
-        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if quota != "max":
-            n = min(n, int(quota) / int(period))
-    except (OSError, ValueError):
-        try:
-            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
-            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
-            if q > 0:
-                n = min(n, q / p)
-        except (OSError, ValueError):
-            pass
-    return n
-
-
-def topology(cores: float) -> tuple[int, int]:
-    """Replica counts for one rank's environment.  Per-task CPU measured on the stack
-    (docs/PERFORMANCE.md): the Python API app is the costliest hop, then the processor app;
-    sidecar data planes and the backing front are native and cheap."""
-    api = max(1, min(8, int(cores / 2.6)))
-    proc = max(1, min(5, int(cores // 5)))
-    return max(api, 2 if cores >= 6 else 1), max(proc, 2 if cores >= 6 else 1)
-
-
 def app_host(app: str, spec: str) -> str:
     """``native`` / ``python`` for every app, or per app: ``api=native,processor=python``."""
     if "=" not in spec:
         return spec
     return dict(p.split("=", 1) for p in spec.split(",")).get(app, "python")
-
-
-def cgroup_throttling() -> dict[str, int]:
-    """cgroup v2 ``cpu.stat`` throttling counters (the job's CPU quota being hit stalls every
-    thread of the job until the next CFS period)."""
-    out = {}
-    try:
-        for line in open("/sys/fs/cgroup/cpu.stat"):
-            k, v = line.split()
-            if k in ("nr_periods", "nr_throttled", "throttled_usec"):
-                out[k] = int(v)
-    except (OSError, ValueError):
-        pass
-    return out
 
 
 def device_sync() -> None:

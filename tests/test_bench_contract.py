@@ -64,3 +64,13 @@ def test_bench_latency_runs():
     assert [x["metric"] for x in lines] == ["crud_latency_two_sidecar_hops", "publish_to_ack_latency"]
     assert set(lines[0]["ops"]) == {"create", "get", "list", "update", "complete", "delete"}
     assert lines[1]["n"] == 3 and lines[1]["p50_ms"] > 0
+
+
+def test_parallel_helpers():
+    from aca_dotnet_workshop_amd.parallel import Dist, cpu_budget, topology
+    assert topology(2) == (1, 1) and topology(16) == (6, 3)
+    sizes = [topology(c) for c in (4, 8, 16, 32, 64)]
+    assert sizes == sorted(sizes) and sizes[-1] == (8, 5)  # grows with the share, capped like the reference (1..5)
+    assert cpu_budget() >= 1
+    d = Dist()  # single process: identities
+    assert (d.world, d.rank, d.max(3.0), d.sum(2.0)) == (1, 0, 3.0, 2.0)
