@@ -65,11 +65,13 @@ def app_host(app: str, spec: str) -> str:
 
 
 def device_sync() -> None:
-    """Contract: bracket the timed region with a device sync when a GPU is present."""
+    """Contract: bracket the timed region with a device sync when a GPU is present -- this
+    rank's own GPU (LOCAL_RANK), so N ranks do not all open a context on device 0."""
     try:
         import torch
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            dev = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+            torch.cuda.synchronize(dev)
     except Exception:
         pass
 
