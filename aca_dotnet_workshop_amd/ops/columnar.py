@@ -255,6 +255,10 @@ class ColumnarIndex:
         self.n = 0
         self.version = 0
         self._dev = None  # device mirror state
+        # compiled programs / device ordering plans, keyed by the query and the dictionaries'
+        # state (append-only dictionaries: sizes + rank versions identify their contents)
+        self._prog_cache: dict[Any, Program] = {}
+        self._plan_cache: dict[Any, Any] = {}
         self._tomb_dirty = False   # liveness changed for rows that are already on the device
         self._full_dirty = True    # layout changed (compaction / new column / growth)
         for p in paths:
@@ -411,6 +415,21 @@ class ColumnarIndex:
         self._full_dirty = True
 
     # -- compilation ---------------------------------------------------------
+    def _dict_state(self) -> tuple:
+        return tuple((len(c.values), c.rank_version) for c in self.columns)
+
+    def compile_cached(self, flt: Any) -> Program:
+        """``compile`` memoised per filter and dictionary state (queries repeat: the cron sweep,
+        the same creator's list page); bounded, oldest entries dropped."""
+        key = (json.dumps(flt, sort_keys=True, default=str), self._dict_state())
+        prog = self._prog_cache.get(key)
+        if prog is None:
+            prog = self.compile(flt)
+            if len(self._prog_cache) >= 128:
+                self._prog_cache.pop(next(iter(self._prog_cache)))
+            self._prog_cache[key] = prog
+        return prog
+
     def compile(self, flt: Any) -> Program:
         code: list[list[int]] = []
         words: list[np.ndarray] = []
@@ -575,8 +594,6 @@ class ColumnarIndex:
         self._full_dirty = False
         self._tomb_dirty = False
         rows = [[c.data_ptr(), w] for c, w in zip(st["cols"], st["widths"])]
-        table = np.array(rows, dtype=np.int64).reshape(-1, 2)
-        st["table"] = torch.from_numpy(table).to(dev)
         if rank_cols:
             # rank-encoded copies of the columns that range leaves read (appended to the table)
             ranks = st.setdefault("ranks", {})
@@ -586,7 +603,15 @@ class ColumnarIndex:
                 slot[col] = len(rows)
                 rows.append([ranks[col]["t"].data_ptr(), ranks[col]["w"]])
             st["rank_slot"] = slot
-            st["table"] = torch.from_numpy(np.array(rows, dtype=np.int64).reshape(-1, 2)).to(dev)
+        # the descriptor table only changes with the device buffers: no upload per query
+        tkey = tuple(tuple(r) for r in rows)
+        tables = st.setdefault("tables", {})
+        t = tables.get(tkey)
+        if t is None:
+            if len(tables) >= 16:
+                tables.clear()
+            t = tables[tkey] = torch.from_numpy(np.array(rows, dtype=np.int64).reshape(-1, 2)).to(dev)
+        st["table"] = t
         return st
 
     def _sync_rank_column(self, kernels, st, ranks, col: int) -> None:
@@ -617,12 +642,17 @@ class ColumnarIndex:
             raise ValueError("program references a column outside the index")
         rng = prog.code[:, 0] == OP_RANGE
         st = self.to_device(kernels, prog.code[rng, 1].tolist())
+        slots = tuple(sorted(st.get("rank_slot", {}).items())) if rng.any() else ()
+        cached = getattr(prog, "_dev", None)
+        if cached is not None and cached[0] == (slots, str(kernels.device)):
+            return st, cached[1], cached[2]
         code_np = prog.code
         if rng.any():  # range leaves read the rank-encoded copy of their column
             code_np = prog.code.copy()
             code_np[rng, 1] = [st["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
         code = torch.from_numpy(code_np).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
+        prog._dev = ((slots, str(kernels.device)), code, bitmaps)  # reused while the program is
         return st, code, bitmaps
 
     def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
@@ -718,17 +748,30 @@ class ColumnarIndex:
     def order_gpu(self, rows, sort, kernels, k: int | None = None):
         """Order a device selection on the GPU (``hip/sort_keys.hip`` + radix sort / top-k);
         returns device rows, or None when the host path must order."""
-        plan = self.sort_specs(sort)
-        if plan is None or len(sort or []) > kernels.max_sort_keys:
+        if len(sort or []) > kernels.max_sort_keys:
             return None
-        specs, ranks, seq_bits = plan
-        if seq_bits > 32:
-            return None  # the device keeps a 32-bit insertion sequence
-        torch = kernels.torch
+        for srt in sort or []:
+            self.add_column(srt["key"])
+        seq_bits_now = max(1, int(self._next_seq).bit_length())
+        pkey = (json.dumps(sort, sort_keys=True, default=str), self._dict_state(), seq_bits_now, str(kernels.device))
+        hit = self._plan_cache.get(pkey)
+        if hit is None:
+            plan = self.sort_specs(sort)
+            if plan is None:
+                return None
+            specs, ranks, seq_bits = plan
+            if seq_bits > 32:
+                return None  # the device keeps a 32-bit insertion sequence
+            torch = kernels.torch
+            key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
+            hit = (torch.from_numpy(specs).to(kernels.device), torch.from_numpy(ranks).to(kernels.device), seq_bits,
+                   key_bits)
+            if len(self._plan_cache) >= 64:
+                self._plan_cache.pop(next(iter(self._plan_cache)))
+            self._plan_cache[pkey] = hit
+        specs_t, ranks_t, seq_bits, key_bits = hit
         st = self.to_device(kernels)  # sort keys may have added columns
-        key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
-        return kernels.order(st["table"], rows, torch.from_numpy(specs).to(kernels.device),
-                             torch.from_numpy(ranks).to(kernels.device), st["seq"], seq_bits, k, key_bits)
+        return kernels.order(st["table"], rows, specs_t, ranks_t, st["seq"], seq_bits, k, key_bits)
 
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""
@@ -736,7 +779,7 @@ class ColumnarIndex:
         # every referenced column first: one re-encode (source-backed) and one device upload
         self.ensure_columns(filter_paths(q.get("filter")) + [s["key"] for s in sort or []
                                                              if isinstance(s, dict) and "key" in s])
-        prog = self.compile(q.get("filter") or {})
+        prog = self.compile_cached(q.get("filter") or {})
         page = q.get("page") or {}
         limit = int(page.get("limit") or 0)
         offset = int(page.get("token") or 0)

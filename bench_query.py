@@ -28,6 +28,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu", action="store_true", help="also time the NumPy executor (slow at 1e8 rows)")
+    ap.add_argument("--query", action="store_true", help="also time the whole paged query path (ColumnarIndex.query)")
     ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4; 0 = default)")
     ap.add_argument("--sorted", action="store_true",
                     help="also time ORDER BY taskDueDate DESC: top-100 page and full ordering (tt_sort_keys + sort)")
@@ -124,6 +125,40 @@ def main() -> None:
         host_keys = ix.sort_keys_numpy(sel, plan)
         top = sel[np.argsort(host_keys, kind="stable")[:100]]
         res["order_match"] = bool(np.array_equal(top, ordered[:100].cpu().numpy()))
+    if a.query:
+        # the whole state-query path the backing planner runs: filter + ORDER BY + first page
+        # (ColumnarIndex.query: select, device ordering/top-k, page copy, keys)
+        class _Keys:  # row -> key without materialising 1e8 strings
+            def __getitem__(self, i):
+                return f"task-{i}"
+        ix.keys = _Keys()
+        ix.seq[:n] = rng.permutation(n) + 1
+        ix._full_dirty = True
+        q = {"filter": flt, "sort": [{"key": "taskDueDate", "order": "DESC"}], "page": {"limit": 100}}
+        for _ in range(3):
+            ix.query(q, k)
+        stages = {"select": 0.0, "order": 0.0, "page": 0.0}
+        it = max(5, a.iters)
+        t0 = time.perf_counter()
+        for _ in range(it):
+            keys, token = ix.query(q, k)
+        res["query_page100_ms"] = round((time.perf_counter() - t0) / it * 1e3, 4)
+        # stage breakdown (synchronised after each stage)
+        for _ in range(it):
+            t = time.perf_counter()
+            dev_rows = ix.select_gpu(ix.compile_cached(flt), k, on_device=True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            ordered = ix.order_gpu(dev_rows, q["sort"], k, 100)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            page = ordered[:100].cpu().numpy()
+            t3 = time.perf_counter()
+            stages["select"] += t1 - t
+            stages["order"] += t2 - t1
+            stages["page"] += t3 - t2
+        res["query_stages_ms"] = {k2: round(v / it * 1e3, 4) for k2, v in stages.items()}
+        res["query_page_rows"] = len(keys)
     if a.cpu:
         t0 = time.perf_counter()
         ref = ix.select_numpy(prog)
