@@ -138,7 +138,9 @@ class Gen {
   void wait_counter() {
     poll_counter([this](long long v) {
       if (v >= base_) begin_step();
-      else loop_.call_later(0.001, [this] { wait_counter(); });
+      // poll again right away: a timer would add up to its 1 ms granularity to every step's
+      // measured duration (one counter read is ~50 us)
+      else loop_.defer([this] { wait_counter(); });
     });
   }
 
