@@ -9,6 +9,7 @@
 //   POST|GET|...  /v1.0/invoke/{appId}/method/{*path}   service invocation (self or peer)
 //   POST|PUT      /v1.0/state/{store}                   save (backing cosmos / redis stores)
 //   GET|DELETE    /v1.0/state/{store}/{key}             get / delete
+//   POST|PUT      /v1.0-alpha1/state/{store}/query      query (forwarded to the backing planner)
 //   POST|PUT      /v1.0/publish/{pubsub}/{*topic}        publish (backing service bus / redis)
 //   internal endpoint                                   peer sidecar -> this app
 //   GET /metrics                                        Python's exposition + ours
@@ -814,6 +815,14 @@ class DataPlane {
         i = j + 1;
       }
     }
+    if (seg.size() == 4 && (lower(seg[0]) == "v1.0-alpha1" || lower(seg[0]) == "v1.0-beta1") &&
+        lower(seg[1]) == "state" && lower(seg[3]) == "query" && (m.method == "POST" || m.method == "PUT")) {
+      auto it = stores_.find(unquote(seg[2]));
+      if (it != stores_.end()) {  // state query: straight to the backing's query planner
+        state_query(std::move(m), std::move(r), it->second, path);
+        return;
+      }
+    }
     if (seg.size() >= 2 && lower(seg[0]) == "v1.0") {
       std::string s1 = lower(seg[1]);
       if (s1 == "invoke" && seg.size() >= 4 && lower(seg[3]) == "method" && invoke_native_) {
@@ -1142,6 +1151,29 @@ class DataPlane {
                       }
                       const std::string* et = res.resp.header("etag");
                       d->send(200, {{"etag", et ? *et : ""}, {"content-type", "application/json"}}, res.resp.body);
+                    });
+  }
+
+  // sidecar/runtime.py h_state_query: the filter goes to the backing's query route (hash
+  // indexes / GPU columnar planner there) with the store's key prefix; 400 from the backing is
+  // the caller's filter, anything else a store failure.
+  void state_query(Message&& m, Reply&& r, const Store& s, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.query", path);
+    std::string target = s.coll_path + "/query";
+    if (!s.prefix.empty()) target += "?prefix=" + quote_all(s.prefix);
+    HeaderList h = s.auth;
+    h.emplace_back("content-type", "application/json");
+    client_.request(s.backing, "POST", target, h, m.body.empty() ? std::string("{}") : m.body, 60,
+                    [d](ClientResult&& res) {
+                      if (!res.err && res.resp.status == 200) {
+                        d->send(200, {{"content-type", "application/json"}}, res.resp.body);
+                        return;
+                      }
+                      int status = (!res.err && res.resp.status == 400) ? 400 : 500;
+                      d->error(status, "ERR_STATE_QUERY",
+                               "state query: " + (res.err ? errno_text(res.err)
+                                                          : "HTTP " + std::to_string(res.resp.status) + " " +
+                                                                res.resp.body.substr(0, 300)));
                     });
   }
 

@@ -157,9 +157,16 @@ def test_state_api(plane, tmp_path):
             # ttl metadata is accepted
             r = await h.post(st, json_body=[{"key": "t", "value": 1, "metadata": {"ttlInSeconds": "60"}}])
             assert r.status == 204
-            # query goes through the control plane
+            # state query (native plane: forwarded to the backing planner; Python: control plane)
             r = await h.post(f"{b}/v1.0-alpha1/state/statestore/query", json_body={"filter": {"EQ": {"i": 1}}})
             assert r.status == 200 and [x["key"] for x in r.json()["results"]] == ["bulk/1 é"]
+            r = await h.post(f"{b}/v1.0-beta1/state/statestore/query",
+                             json_body={"filter": {"OR": [{"EQ": {"i": 0}}, {"EQ": {"i": 2}}]},
+                                        "sort": [{"key": "i", "order": "DESC"}], "page": {"limit": 1}})
+            js = r.json()
+            assert r.status == 200 and [x["key"] for x in js["results"]] == ["bulk/2 é"] and js["token"]
+            r = await h.post(f"{b}/v1.0-alpha1/state/statestore/query", json_body={"filter": {"BOGUS": {"i": 1}}})
+            assert r.status == 400 and r.json()["errorCode"] == "ERR_STATE_QUERY"
     run(main())
 
 
