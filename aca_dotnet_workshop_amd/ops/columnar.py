@@ -259,6 +259,7 @@ class ColumnarIndex:
         # state (append-only dictionaries: sizes + rank versions identify their contents)
         self._prog_cache: dict[Any, Program] = {}
         self._plan_cache: dict[Any, Any] = {}
+        self._dict_gen = 0  # bumps when the dictionaries are rebuilt (re-encode from `source`)
         self._tomb_dirty = False   # liveness changed for rows that are already on the device
         self._full_dirty = True    # layout changed (compaction / new column / growth)
         for p in paths:
@@ -281,6 +282,7 @@ class ColumnarIndex:
         cap = max(TILE, (n + TILE - 1) // TILE * TILE)
         self.cap = cap
         self.columns, self.col_of = [], {}
+        self._dict_gen += 1
         self.ids = np.full((len(paths), cap), -1, dtype=np.int32)
         for i, (path, (values, ids)) in enumerate(zip(paths, cols)):
             c = Column(path)
@@ -416,7 +418,7 @@ class ColumnarIndex:
 
     # -- compilation ---------------------------------------------------------
     def _dict_state(self) -> tuple:
-        return tuple((len(c.values), c.rank_version) for c in self.columns)
+        return (self._dict_gen,) + tuple((len(c.values), c.rank_version) for c in self.columns)
 
     def compile_cached(self, flt: Any) -> Program:
         """``compile`` memoised per filter and dictionary state (queries repeat: the cron sweep,

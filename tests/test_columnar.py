@@ -323,3 +323,62 @@ def test_gpu_incremental_sync_and_width_growth():
     ix.compact()
     prog = ix.compile({"LT": {"v": 1000}})
     assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
+
+
+def _interleaved(ix, store, rnd, kernels=None, rounds=12):
+    """Repeat the same queries between writes that add dictionary values (new creators, new due
+    dates that land between existing ones) and delete rows: memoised programs / ordering plans
+    must never answer from a stale dictionary."""
+    qs = [{"filter": {"EQ": {"c": "u-new-3"}}},
+          {"filter": {"LT": {"d": "2024-05-10"}}, "sort": [{"key": "d", "order": "DESC"}], "page": {"limit": 25}},
+          {"filter": {"IN": {"c": ["u1", "u-new-1"]}}, "sort": [{"key": "c"}, {"key": "n", "order": "DESC"}]},
+          {"filter": {"OR": [{"GT": {"n": 40}}, {"EQ": {"d": "2024-05-09T12:00:00"}}]}}]
+    nxt = [1000]
+    for r in range(rounds):
+        for q in qs:
+            want = [x["key"] for x in json.loads(store.query(json.dumps(q)))["results"]]
+            assert ix.query(q, kernels)[0] == want, (r, q)
+        for _ in range(300):
+            k = str(nxt[0])
+            nxt[0] += 1
+            d = {"c": rnd.choice(["u0", "u1", "u2", f"u-new-{r}"]),
+                 "d": rnd.choice(["2024-05-01T00:00:00", "2024-05-20T00:00:00", f"2024-05-{r % 28 + 1:02d}T12:00:00"]),
+                 "n": rnd.randrange(r * 5 + 5)}
+            store.set(k, json.dumps(d))
+            ix.upsert(k, d)
+        for k in rnd.sample(range(1000, nxt[0]), 50):
+            store.delete(str(k))
+            ix.delete(str(k))
+
+
+def test_query_caches_follow_dictionary_growth():
+    rnd = random.Random(5)
+    store = N.DocStore()
+    ix = ColumnarIndex(["c", "d", "n"])
+    _interleaved(ix, store, rnd)
+    assert ix._prog_cache  # the repeated filters were memoised
+
+
+def test_query_caches_survive_reencode():
+    """A source-backed index rebuilds its dictionaries when a column is added: cached programs
+    keyed on the old dictionaries must not be reused."""
+    store = N.DocStore()
+    for i in range(500):
+        store.set(str(i), json.dumps({"c": f"u{i % 4}", "d": f"2024-05-{i % 28 + 1:02d}T00:00:00", "n": i % 50}))
+    ix = ColumnarIndex.from_source(lambda paths: store.encode_columns("", paths), ["c"])
+    q = {"filter": {"EQ": {"c": "u2"}}}
+    assert ix.query(q)[0] == [x["key"] for x in json.loads(store.query(json.dumps(q)))["results"]]
+    for i in range(0, 500, 4):  # u0 rows go away in the store; the index mirrors the deletes
+        store.delete(str(i))
+        ix.delete(str(i))
+    ix.add_column("d")  # re-encode: u0 leaves the dictionary, ids shift
+    assert ix.query(q)[0] == [x["key"] for x in json.loads(store.query(json.dumps(q)))["results"]]
+    _interleaved(ix, store, random.Random(6), rounds=4)
+
+
+@pytest.mark.gpu
+def test_gpu_query_caches_follow_dictionary_growth():
+    k = _kernels()
+    store = N.DocStore()
+    ix = ColumnarIndex(["c", "d", "n"])
+    _interleaved(ix, store, random.Random(9), kernels=k)
