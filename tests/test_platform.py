@@ -3,8 +3,10 @@ multi-process environment deployed by the controller (ACA equivalent) -- module 
 (internal ingress 403), module 9 (KEDA 1 -> 5 -> 1 replicas), module 10 (what-if/apply).
 """
 import asyncio
+import collections
 import json
 import os
+import re
 import signal
 import time
 import urllib.error
@@ -122,10 +124,13 @@ def test_environment_lifecycle(tmp_path):
             assert resp.status == 302
             b = ctl.backing
             # module 9: burst on the topic scales the processor out, then back in after the cooldown
-            ce = json.dumps({"specversion": "1.0", "id": "x", "source": "t", "type": "t", "datacontenttype": "application/json",
-                             "data": {"taskName": "burst", "taskAssignedTo": "a@x", "taskDueDate": "2030-01-01T00:00:00"}})
+            def ce(i):
+                return json.dumps({"specversion": "1.0", "id": f"x{i}", "source": "t", "type": "t",
+                                   "datacontenttype": "application/json",
+                                   "data": {"taskName": f"burst-{i}", "taskAssignedTo": "a@x",
+                                            "taskDueDate": "2030-01-01T00:00:00"}})
             await b.sb_publish_batch("taskstracker", "tasksavedtopic",
-                                     [{"body": ce, "contentType": "application/cloudevents+json"} for _ in range(800)])
+                                     [{"body": ce(i), "contentType": "application/cloudevents+json"} for i in range(800)])
             proc = ctl.apps["tasksmanager-backend-processor"]
             peak = 1
             for _ in range(100):
@@ -136,6 +141,12 @@ def test_environment_lifecycle(tmp_path):
                     break
             assert peak == 5
             assert c["completed"] == 800 and c["dead_letter"] == 0
+            # competing consumers across the 5 replicas: every message handled, none twice
+            # (the processor logs each delivery it starts; no lock expired, so no redelivery)
+            seen = collections.Counter()
+            for f in ctl.stack.log_dir.glob("tasksmanager-backend-processor*.log"):
+                seen.update(re.findall(r"Task Name 'burst-(\d+)'", f.read_text(errors="replace")))
+            assert len(seen) == 800 and set(seen.values()) == {1}, (len(seen), seen.most_common(3))
             # live metrics (App Insights Live Metrics): native deliveries counted per replica
             from aca_dotnet_workshop_amd.platform.__main__ import live_rates
             s0 = await ctl.live_metrics()
