@@ -24,6 +24,7 @@ import numpy as np
 OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ, OP_RANGE = 1, 2, 3, 4, 5, 6, 7
 TILE = 8192           # rows per kernel tile (ops/hip/query_scan.hip kTileRows)
 MAX_DEPTH = 8         # device stack depth (16-bit masks in a 128-bit register)
+MAX_FLAT_LEAVES = 8   # leaves of a flat program (ops/hip/query_scan.hip kMaxFlatLeaves)
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
 
 
@@ -133,6 +134,33 @@ def rank_interval(c: "Column", sat: np.ndarray) -> tuple[int, int] | None:
     if not np.array_equal(inside, sat):
         return None
     return lo, hi
+
+
+def flat_form(code: np.ndarray) -> tuple[np.ndarray, int] | None:
+    """(leaf rows, flip_result) when ``code`` is one AND / OR over leaves that may each be
+    negated -- the shape ``tt_scan_flat`` evaluates wave-wide -- else None.  Leaf rows are
+    ``[op | flip << 8, column, b, c]``; an OR is evaluated as NOT(AND(NOT leaf)), so every
+    leaf of an OR carries the extra flip and the result is flipped back."""
+    ops = code[:, 0].tolist()
+    if ops == [OP_TRUE]:  # no leaves: every live row
+        return np.zeros((0, 4), dtype=np.int32), 0
+    is_or, items, n = False, code, 1
+    if ops[-1] in (OP_AND, OP_OR):
+        is_or, items, n = ops[-1] == OP_OR, code[:-1], int(code[-1, 1])
+    leaves: list[list[int]] = []
+    i = 0
+    while i < len(items):
+        op, a, b, c = (int(x) for x in items[i])
+        if op not in (OP_EQ, OP_RANGE, OP_LEAF):
+            return None
+        neg = 0
+        if i + 1 < len(items) and int(items[i + 1, 0]) == OP_NOT:
+            neg, i = 1, i + 1
+        leaves.append([op | ((neg ^ int(is_or)) << 8), a, b, c])
+        i += 1
+    if len(leaves) != n or not 0 < n <= MAX_FLAT_LEAVES:
+        return None
+    return np.asarray(leaves, dtype=np.int32), int(is_or)
 
 
 class KeyTable:
@@ -606,6 +634,7 @@ class ColumnarIndex:
                 rows.append([ranks[col]["t"].data_ptr(), ranks[col]["w"]])
             st["rank_slot"] = slot
         # the descriptor table only changes with the device buffers: no upload per query
+        st["table_widths"] = np.array([w for _, w in rows], dtype=np.int64)
         tkey = tuple(tuple(r) for r in rows)
         tables = st.setdefault("tables", {})
         t = tables.get(tkey)
@@ -636,8 +665,9 @@ class ColumnarIndex:
         cur["synced"] = self.n
 
     def device_program(self, prog: Program, kernels):
-        """Sync the device mirror for ``prog`` and return (state, program, bitmaps) tensors ready
-        for ``GpuKernels.select`` (range leaves remapped to their rank-encoded columns)."""
+        """Sync the device mirror for ``prog`` and return (state, program, bitmaps, flat) ready
+        for ``GpuKernels.select`` (range leaves remapped to their rank-encoded columns; ``flat``:
+        the wave-wide leaf form of ``flat_form`` on the device, or None)."""
         torch = kernels.torch
         leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ) | (prog.code[:, 0] == OP_RANGE)
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
@@ -647,19 +677,31 @@ class ColumnarIndex:
         slots = tuple(sorted(st.get("rank_slot", {}).items())) if rng.any() else ()
         cached = getattr(prog, "_dev", None)
         if cached is not None and cached[0] == (slots, str(kernels.device)):
-            return st, cached[1], cached[2]
+            return st, cached[1], cached[2], self._flat_args(st, cached[3])
         code_np = prog.code
         if rng.any():  # range leaves read the rank-encoded copy of their column
             code_np = prog.code.copy()
             code_np[rng, 1] = [st["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
         code = torch.from_numpy(code_np).to(kernels.device)
         bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
-        prog._dev = ((slots, str(kernels.device)), code, bitmaps)  # reused while the program is
-        return st, code, bitmaps
+        ff = flat_form(code_np)
+        flat = None if ff is None else (torch.from_numpy(ff[0]).to(kernels.device), ff[1], ff[0][:, 1].copy())
+        prog._dev = ((slots, str(kernels.device)), code, bitmaps, flat)  # reused while the program is
+        return st, code, bitmaps, self._flat_args(st, flat)
+
+    @staticmethod
+    def _flat_args(st, flat):
+        """(device leaves, flip_result, widest leaf column now) -- widths grow with the
+        dictionaries, so the kernel instantiation is chosen per call."""
+        if flat is None:
+            return None
+        leaves, flip, cols = flat
+        return leaves, flip, int(st["table_widths"][cols].max()) if cols.size else 1
 
     def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
-        st, code, bitmaps = self.device_program(prog, kernels)
-        res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
+        st, code, bitmaps, flat = self.device_program(prog, kernels)
+        res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask,
+                             flat=flat)
         if return_mask or on_device:
             return res
         return res.cpu().numpy()

@@ -25,6 +25,11 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, I32, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int
+    lib.tt_launch_scan_flat.argtypes = [P, I64, P, P, I32, I32, I32, P, I32, P, P, P]
+    lib.tt_launch_scan_flat.restype = ctypes.c_int
+    lib.tt_max_flat_leaves.restype = ctypes.c_int
+    lib.tt_set_flat_grid.argtypes = [I64]
+    lib.tt_set_flat_grid.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_scan_select.argtypes = [P, I64, P, P, I32, P, I32, P, P, P, P, P]
@@ -62,6 +67,18 @@ class GpuKernels:
         # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
         # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
         self.fused_select = False
+        # Flat programs (one AND / OR over leaves) can run on tt_scan_flat (wave-wide compares,
+        # leaves combined in scalar registers: ~3x fewer VALU instructions).  Opt-in: on the 1e8-row
+        # overdue sweep it ties the interpreter (92.8 vs 92.8 µs) -- both stream the narrow
+        # columns at the same ~4.6 TB/s -- so the simpler path stays the default
+        # (profiles/r1_query_scan_flat_ab.md).
+        self.flat_eval = False
+        self.max_flat_leaves = int(self.lib.tt_max_flat_leaves())
+
+    def set_flat_grid(self, blocks: int) -> None:
+        """Workgroups of ``tt_scan_flat`` (grid-stride over tiles); 0 = one per tile."""
+        if self.lib.tt_set_flat_grid(int(blocks)) != 0:
+            raise ValueError("grid must be >= 0")
 
     def set_eval_groups(self, u: int) -> None:
         """Row groups per lane in ``tt_scan_eval`` (1, 2 or 4): registers vs loads in flight."""
@@ -71,7 +88,8 @@ class GpuKernels:
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False):
+    def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False,
+               flat=None):
         """Row indices (int32, ascending) of live rows satisfying ``prog``.
 
         ``table``: int64 [ncols, 2] of (device pointer, width) column descriptors, every column
@@ -94,11 +112,24 @@ class GpuKernels:
             return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
         mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
-        rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
-                                          bitmaps.data_ptr(), bitmaps.numel(), mask.data_ptr(), counts.data_ptr(),
-                                          self._stream())
-        if rc != 0:
-            raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
+        if flat is not None and self.flat_eval:
+            leaves, flip, max_width = flat
+            if leaves.dtype != torch.int32 or leaves.ndim != 2 or leaves.shape[1] != 4:
+                raise ValueError("flat leaves must be int32 [n, 4]")
+            if leaves.shape[0] > self.max_flat_leaves:
+                raise ValueError("too many leaves for tt_scan_flat")
+            rc = self.lib.tt_launch_scan_flat(table.data_ptr(), nrows, live16.data_ptr(), leaves.data_ptr(),
+                                              leaves.shape[0], int(flip), int(max_width), bitmaps.data_ptr(),
+                                              bitmaps.numel(),
+                                              mask.data_ptr(), counts.data_ptr(), self._stream())
+            if rc != 0:
+                raise RuntimeError(f"tt_scan_flat launch failed ({rc})")
+        else:
+            rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
+                                              prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(), mask.data_ptr(),
+                                              counts.data_ptr(), self._stream())
+            if rc != 0:
+                raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
         incl = torch.cumsum(counts, 0, dtype=torch.int64)
         total = int(incl[-1].item())
         offsets = incl - counts.to(torch.int64)

@@ -217,6 +217,196 @@ tt_scan_eval_t(const ColumnDesc* __restrict__ cols,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// tt_scan_flat: tt_scan_eval for FLAT programs -- one AND or OR over leaves, each optionally
+// negated (the creator page, the overdue sweep, a single EQ: nearly every query the services
+// issue) -- evaluated wave-wide instead of lane by lane.  Lane l owns rows 16l..16l+15 of a
+// 1024-row chunk (one 16/32/64-byte load per lane per leaf); the test of row position p is
+// ONE vector compare over the wave whose 64-bit result (bit l = row 16l+p) stays in scalar
+// registers, where the leaves are combined with scalar logic.  Only the chunk's final result
+// is turned back into per-lane bits (lane l: bit l of the 16 masks) -- the row-order 16-bit
+// selection word of rows 16l..16l+15, i.e. exactly tt_scan_eval's mask layout, so compaction
+// and grouped counts are shared.  Per row and leaf this is ~1/64 of a wave instruction (EQ)
+// instead of the interpreter's per-lane extract / translate / compare / assemble sequence.
+// Per chunk the column loads of up to four leaves are issued back to back before any compare,
+// so a wave keeps all of them in flight.
+//
+// Leaf rows (host-built, int32 x4): {op | flip << 8, column, b, c} with op OP_EQ (code == b),
+// OP_RANGE (b <= rank < c on a rank-encoded column) or OP_LEAF (bitmap words at b, c bits).
+// Everything is evaluated as an AND: the host folds NOT and OR (De Morgan: flip every leaf,
+// flip the result) into the flip bits and `flip_result`.
+// Raw column codes are compared unsigned: the all-ones missing code of each width is never a
+// dictionary id or rank (ColumnarIndex.width_for keeps dictionaries below it), so "missing"
+// fails every leaf test without translating it to -1 first.
+namespace {
+constexpr int kFlatRows = 16;                 // rows per lane per chunk
+constexpr int kFlatChunk = 64 * kFlatRows;    // 1024 rows per wave step
+constexpr int kFlatChunksPerWave = kTileRows / kFlatChunk / (kBlock / 64);
+constexpr int kMaxFlatLeaves = 8;
+static_assert(kFlatChunksPerWave == 2, "a tile is 4 waves x 2 chunks");
+
+// The lane's 16 rows of one column through a global (not flat) address (the column pointers
+// arrive as integers; flat loads would also wait on the LDS counter).  N = 4 x the widest
+// column of the program: always N/4 16-byte loads per leaf, a narrower column re-reading its
+// first piece (an L2 hit, never past the column's end), so every leaf step issues the same
+// number of loads and the compiler's wait counts stay exact across the pipelined loop.
+template <int N>
+__device__ __forceinline__ void issue_leaf_load(const ColumnDesc& cd, int64_t row0, uint32_t (&w)[N]) {
+  const __attribute__((address_space(1))) uint32_t* p =
+      reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(cd.ptr + (uint64_t)row0 * cd.width);
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    const int qq = q < cd.width ? q : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[4 * q + i] = p[4 * qq + i];
+  }
+}
+
+template <int W, int N>
+__device__ __forceinline__ uint32_t raw_at(const uint32_t (&w)[N], int i) {
+  if (W == 1) return (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+  if (W == 2) return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+  return w[i];
+}
+
+// acc[p] &= ballot(test(row 16 lane + p)) ^ flip, for one leaf over one chunk
+template <int W, int N, typename BitmapPtr>
+__device__ __forceinline__ void apply_leaf(int32_t op, uint32_t b, uint32_t c, uint64_t flip,
+                                           const uint32_t (&w)[N], BitmapPtr bitmaps, uint64_t (&acc)[16]) {
+  if (op == OP_EQ) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] &= __ballot(raw_at<W>(w, i) == b) ^ flip;
+  } else if (op == OP_RANGE) {
+    const uint32_t span = c - b;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] &= __ballot(raw_at<W>(w, i) - b < span) ^ flip;
+  } else if (c <= 64) {  // bitmap leaf, dictionary of <= 64 ids: register-resident bitmap
+    const BitmapPtr bm = bitmaps + b;
+    const uint64_t b64 = (uint64_t)bm[0] | ((c > 32) ? ((uint64_t)bm[1] << 32) : 0ull);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t r = raw_at<W>(w, i);
+      acc[i] &= __ballot(r < c && ((b64 >> (r & 63u)) & 1ull)) ^ flip;
+    }
+  } else {
+    const BitmapPtr bm = bitmaps + b;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t r = raw_at<W>(w, i);
+      acc[i] &= __ballot(r < c && ((bm[r >> 5] >> (r & 31u)) & 1u)) ^ flip;
+    }
+  }
+}
+
+template <int N, typename BitmapPtr>
+__device__ __forceinline__ void flat_step(const int32_t* __restrict__ leaf, int width, const uint32_t (&w)[N],
+                                          BitmapPtr bitmaps, uint64_t (&acc)[16]) {
+  const int32_t op = leaf[0] & 0xFF;
+  const uint64_t flip = (leaf[0] >> 8) ? ~0ull : 0ull;
+  const uint32_t b = (uint32_t)leaf[2], c = (uint32_t)leaf[3];
+  if (N == 4 || width == 1) apply_leaf<1>(op, b, c, flip, w, bitmaps, acc);
+  else if (N == 8 || width == 2) apply_leaf<2>(op, b, c, flip, w, bitmaps, acc);
+  else apply_leaf<4>(op, b, c, flip, w, bitmaps, acc);
+}
+
+// One wave's two chunks as a pipeline of (chunk, leaf) steps, chunk-major, with the column
+// loads of the next two steps in flight while a step's compares run (three register buffers
+// in rotation).  The liveness words are read up front and the two selection words stored at
+// the end, so the loop body issues nothing but the leaf loads.
+template <int N, typename BitmapPtr>
+__device__ __forceinline__ void scan_flat_wave(const ColumnDesc* __restrict__ cols, int64_t nrows,
+                                               const uint16_t* __restrict__ live, const int32_t* __restrict__ leaves,
+                                               int32_t nleaves, uint32_t res_flip, BitmapPtr bitmaps,
+                                               uint16_t* __restrict__ mask, int64_t wave_row0, int lane,
+                                               int32_t& local) {
+  static_assert(kFlatChunksPerWave == 2, "two selection words per lane");
+  const int64_t r0 = wave_row0 + (int64_t)lane * kFlatRows, r1 = r0 + kFlatChunk;
+  const uint32_t lv0 = live[r0 >> 4], lv1 = live[r1 >> 4];
+  uint32_t sel0 = 0xFFFFu, sel1 = 0xFFFFu;
+  uint64_t acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = ~0ull;
+  const int steps = kFlatChunksPerWave * nleaves;
+  auto issue = [&](int s, uint32_t (&w)[N]) {
+    s = s < steps ? s : steps - 1;  // past the end: re-read the last step (keeps wait counts exact)
+    const int j = s >= nleaves ? 1 : 0, k = s - j * nleaves;
+    issue_leaf_load(cols[leaves[4 * k + 1]], j ? r1 : r0, w);
+  };
+  auto consume = [&](int s, const uint32_t (&w)[N]) {
+    const int j = s >= nleaves ? 1 : 0, k = s - j * nleaves;
+    flat_step(leaves + 4 * k, cols[leaves[4 * k + 1]].width, w, bitmaps, acc);
+    if (k == nleaves - 1) {  // chunk done: back to per-lane bits (bit p = bit lane of acc[p])
+      uint32_t bits = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bits |= (uint32_t)((acc[i] >> lane) & 1ull) << i;
+      if (j) sel1 = bits;
+      else sel0 = bits;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = ~0ull;
+    }
+  };
+  if (steps > 0) {
+    uint32_t wa[N], wb[N], wc[N];
+    issue(0, wa);
+    issue(1, wb);
+#pragma unroll 1
+    for (int s = 0; s < steps; s += 3) {
+      issue(s + 2, wc);
+      consume(s, wa);
+      if (s + 1 >= steps) break;
+      issue(s + 3, wa);
+      consume(s + 1, wb);
+      if (s + 2 >= steps) break;
+      issue(s + 4, wb);
+      consume(s + 2, wc);
+    }
+  }
+  const uint32_t m0 = r0 < nrows ? ((sel0 ^ res_flip) & lv0) : 0u;
+  const uint32_t m1 = r1 < nrows ? ((sel1 ^ res_flip) & lv1) : 0u;
+  mask[r0 >> 4] = (uint16_t)m0;
+  mask[r1 >> 4] = (uint16_t)m1;
+  local += __popc(m0) + __popc(m1);
+}
+}  // namespace
+
+// N = 4 x the widest column the program reads (the launcher picks the instantiation)
+template <int N>
+__global__ void __launch_bounds__(kBlock)
+tt_scan_flat_t(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_t* __restrict__ live,
+               const int32_t* __restrict__ leaves, int32_t nleaves, int32_t flip_result,
+               const uint32_t* __restrict__ bitmaps, int32_t bitmap_words,
+               uint16_t* __restrict__ mask, int32_t* __restrict__ block_counts) {
+  extern __shared__ uint32_t lds_flat_bitmaps[];
+  const bool in_lds = bitmap_words <= kMaxLdsBitmapWords;
+  if (in_lds) {
+    for (int i = threadIdx.x; i < bitmap_words; i += kBlock) lds_flat_bitmaps[i] = bitmaps[i];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t res_flip = flip_result ? 0xFFFFu : 0u;
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  __shared__ int32_t wave_counts[2][kBlock / 64];
+  // a bounded grid walks the tiles (grid-stride): fewer, longer-lived workgroups keep the
+  // streams going instead of paying a dispatch and a ramp per 8192-row tile
+  int parity = 0;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x, parity ^= 1) {
+    const int64_t wave_row0 = tile * kTileRows + (int64_t)wave * kFlatChunksPerWave * kFlatChunk;
+    int32_t local = 0;
+    if (in_lds)
+      scan_flat_wave<N>(cols, nrows, live, leaves, nleaves, res_flip, (const uint32_t*)lds_flat_bitmaps, mask,
+                        wave_row0, lane, local);
+    else
+      scan_flat_wave<N>(cols, nrows, live, leaves, nleaves, res_flip, bitmaps, mask, wave_row0, lane, local);
+    for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+    if (lane == 0) wave_counts[parity][wave] = local;  // double-buffered: one barrier per tile
+    __syncthreads();
+    if (threadIdx.x == 0)
+      block_counts[tile] = wave_counts[parity][0] + wave_counts[parity][1] + wave_counts[parity][2] +
+                           wave_counts[parity][3];
+  }
+}
+
 extern "C" __global__ void __launch_bounds__(kBlock)
 tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask viewed as 32-bit words
                 const int64_t* __restrict__ block_offsets,  // exclusive scan of block_counts
@@ -463,6 +653,40 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
   }
   return (int)hipGetLastError();
 }
+
+// Workgroups of the flat scan (grid-stride over tiles); 0 = one per tile.  Tunable for A/B.
+static int64_t g_flat_grid = (int64_t)1 << 40;  // measured: one per tile 0.164 ms, 2048 0.171 ms
+extern "C" int tt_set_flat_grid(int64_t g) {
+  if (g < 0) return -1;
+  g_flat_grid = g == 0 ? (int64_t)1 << 40 : g;
+  return 0;
+}
+
+// Flat programs (see tt_scan_flat_t): `leaves` is int32 [nleaves, 4] on the device and
+// `max_width` the widest column (1, 2 or 4 bytes) any leaf reads.
+extern "C" int tt_launch_scan_flat(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* leaves,
+                                   int32_t nleaves, int32_t flip_result, int32_t max_width, const uint32_t* bitmaps,
+                                   int32_t bitmap_words, uint16_t* mask, int32_t* block_counts, hipStream_t stream) {
+  if (nleaves < 0 || nleaves > kMaxFlatLeaves || nrows < 0 || bitmap_words <= 0) return -1;
+  if (max_width != 1 && max_width != 2 && max_width != 4) return -1;
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles == 0) return 0;
+  const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
+  const ColumnDesc* cd = reinterpret_cast<const ColumnDesc*>(cols);
+  const unsigned grid = (unsigned)(tiles < g_flat_grid ? tiles : g_flat_grid);
+  if (max_width == 1)
+    hipLaunchKernelGGL(tt_scan_flat_t<4>, dim3(grid), dim3(kBlock), lds, stream, cd, nrows, live, leaves,
+                       nleaves, flip_result, bitmaps, bitmap_words, mask, block_counts);
+  else if (max_width == 2)
+    hipLaunchKernelGGL(tt_scan_flat_t<8>, dim3(grid), dim3(kBlock), lds, stream, cd, nrows, live, leaves,
+                       nleaves, flip_result, bitmaps, bitmap_words, mask, block_counts);
+  else
+    hipLaunchKernelGGL(tt_scan_flat_t<16>, dim3(grid), dim3(kBlock), lds, stream, cd, nrows, live, leaves,
+                       nleaves, flip_result, bitmaps, bitmap_words, mask, block_counts);
+  return (int)hipGetLastError();
+}
+
+extern "C" int tt_max_flat_leaves() { return kMaxFlatLeaves; }
 
 extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int64_t* block_offsets, int64_t nrows, int32_t* out,
                                       hipStream_t stream) {

@@ -382,3 +382,87 @@ def test_gpu_query_caches_follow_dictionary_growth():
     store = N.DocStore()
     ix = ColumnarIndex(["c", "d", "n"])
     _interleaved(ix, store, random.Random(9), kernels=k)
+
+
+@settings(max_examples=200, deadline=None)
+@given(docs_st, filters_st, st.integers(0, 1000))
+def test_flat_form_is_equivalent(docs, flt, seed):
+    """``flat_form`` (what tt_scan_flat evaluates: AND of possibly flipped leaves, OR folded by
+    De Morgan) selects exactly what the program selects."""
+    from aca_dotnet_workshop_amd.ops.columnar import OP_AND, OP_NOT, flat_form
+    if not docs:
+        return
+    ix = _columnar(_ops(docs, random.Random(seed)))
+    prog = ix.compile(flt)
+    ff = flat_form(prog.code)
+    if ff is None:  # nested AND / OR: the interpreter's job
+        assert ((prog.code[:, 0] == OP_AND) | (prog.code[:, 0] == 3)).sum() > 1 or (prog.code[:-1, 0] == OP_NOT).any()
+        return
+    leaves, flip = ff
+    code = []
+    for op, a, b, c in leaves.tolist():
+        code.append([op & 0xFF, a, b, c])
+        if op >> 8:
+            code.append([OP_NOT, 0, 0, 0])
+    if len(leaves) == 0:
+        code = [[5, 0, 0, 0]]
+    elif len(leaves) > 1:
+        code.append([OP_AND, len(leaves), 0, 0])
+    if flip:
+        code.append([OP_NOT, 0, 0, 0])
+    from aca_dotnet_workshop_amd.ops.columnar import Program
+    again = Program(np.asarray(code, dtype=np.int32), prog.bitmaps, prog.columns)
+    assert np.array_equal(ix.select_numpy(again), ix.select_numpy(prog))
+
+
+def test_flat_form_shapes():
+    from aca_dotnet_workshop_amd.ops.columnar import flat_form
+    ix = ColumnarIndex(["a", "b"])
+    for i in range(100):
+        ix.upsert(str(i), {"a": i % 7, "b": f"s{i % 3}"})
+    assert flat_form(ix.compile({}).code)[0].shape == (0, 4)
+    assert flat_form(ix.compile({"EQ": {"a": 1}}).code)[1] == 0
+    leaves, flip = flat_form(ix.compile({"OR": [{"EQ": {"a": 1}}, {"NEQ": {"b": "s1"}}]}).code)
+    assert flip == 1 and (leaves[:, 0] >> 8).tolist() == [1, 0]  # OR: leaves flipped, NEQ's NOT cancels
+    assert flat_form(ix.compile({"AND": [{"EQ": {"a": 1}}, {"OR": [{"EQ": {"b": "s1"}}, {"GT": {"a": 3}}]}]}).code) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 1000, 70_001])
+def test_gpu_flat_kernel_matches_interpreter(n):
+    """tt_scan_flat (wave-wide compares, scalar combine) == tt_scan_eval == NumPy, on 1-, 2- and
+    4-byte columns, register and LDS bitmaps, range leaves, NOT / OR folding."""
+    from aca_dotnet_workshop_amd.ops.columnar import flat_form
+    k = _kernels()
+    rnd = random.Random(n)
+    ix = ColumnarIndex(["s", "m", "w", "d"], capacity=n)
+    for i in range(n):
+        ix.upsert(str(i), {"s": rnd.randrange(20), "m": f"m{rnd.randrange(300)}", "w": rnd.randrange(100_000),
+                           "d": f"2024-05-{rnd.randrange(1, 29):02d}"} if rnd.random() < 0.95 else {"s": 1})
+    for i in rnd.sample(range(n), n // 10):
+        ix.delete(str(i))
+    filters = [{}, {"EQ": {"s": 3}}, {"NEQ": {"m": "m7"}}, {"IN": {"s": [1, 2, 19]}},
+               {"IN": {"m": [f"m{j}" for j in range(0, 300, 7)]}}, {"LT": {"d": "2024-05-10"}},
+               {"GTE": {"w": 50_000}}, {"EQ": {"w": 12345}}, {"EQ": {"missing": 1}},
+               {"AND": [{"LT": {"d": "2024-05-20"}}, {"NEQ": {"s": 4}}, {"IN": {"m": ["m1", "m2", "m299"]}}]},
+               {"OR": [{"EQ": {"s": 5}}, {"GT": {"w": 90_000}}, {"NEQ": {"d": "2024-05-03"}}]},
+               {"OR": [{"EQ": {"m": "m3"}}, {"EQ": {"s": 7}}]}]
+    try:
+        for f in filters:
+            prog = ix.compile(f)
+            assert flat_form(prog.code) is not None, f
+            want = ix.select_numpy(prog)
+            k.flat_eval = False
+            interp, imask = ix.select_gpu(prog, k, return_mask=True)
+            k.flat_eval = True
+            flat, fmask = ix.select_gpu(prog, k, return_mask=True)
+            assert np.array_equal(flat.cpu().numpy(), want), (n, f)
+            assert np.array_equal(interp.cpu().numpy(), want), (n, f)
+            assert torch_equal(fmask, imask), (n, f)
+    finally:
+        k.flat_eval = False
+
+
+def torch_equal(a, b):
+    import torch
+    return bool(torch.equal(a, b))
