@@ -466,3 +466,28 @@ def test_gpu_flat_kernel_matches_interpreter(n):
 def torch_equal(a, b):
     import torch
     return bool(torch.equal(a, b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ndistinct", [50, 3000, 70_000])
+def test_gpu_rank_encode_unaligned_ranges(ndistinct):
+    """tt_rank_encode: full encodes and incremental syncs whose [lo, hi) are not multiples of
+    16 rows (row-by-row head / tail + vectorised body), 1-, 2- and 4-byte rank columns."""
+    k = _kernels()
+    rnd = random.Random(ndistinct)
+    ix = ColumnarIndex(["v"])
+    n0 = 1000 + ndistinct
+    for i in range(n0):
+        v = i if i < ndistinct else rnd.randrange(ndistinct)  # every value present: width by ndistinct
+        ix.upsert(str(i), {"v": v} if i % 13 or i < ndistinct else {"w": 1})
+    lo_v = ndistinct // 3
+    for f in ({"LT": {"v": lo_v}}, {"GTE": {"v": lo_v}}):
+        prog = ix.compile(f)
+        assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog)), f
+    assert ix._dev["ranks"][ix.col_of["v"]]["w"] == {50: 1, 3000: 2, 70_000: 4}[ndistinct]
+    for extra in (37, 5, 16, 1):  # incremental syncs of existing values (no rank shift)
+        base = ix.n
+        for i in range(base, base + extra):
+            ix.upsert(str(i), {"v": rnd.randrange(ndistinct)})
+        prog = ix.compile({"LT": {"v": lo_v}})
+        assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog)), extra
