@@ -28,3 +28,15 @@ def test_sidecar_endpoint_resolution():
     assert sidecar_base_url({}) == "http://127.0.0.1:3500"
     assert sidecar_base_url({"DAPR_HTTP_PORT": "3501"}) == "http://127.0.0.1:3501"
     assert sidecar_base_url({"TT_SIDECAR_UDS": "/tmp/s.sock"}) == "unix:/tmp/s.sock:"
+
+
+def test_tune_gc_knob():
+    import gc
+    from aca_dotnet_workshop_amd.services.hosting import tune_gc
+    before = gc.get_threshold()
+    try:
+        assert tune_gc({"TT_GC_GEN0": "0"}) is False and gc.get_threshold() == before
+        assert tune_gc({"TT_GC_GEN0": "12345"}) is True and gc.get_threshold()[0] == 12345
+    finally:
+        gc.unfreeze()
+        gc.set_threshold(*before)
