@@ -64,6 +64,15 @@ def app_host(app: str, spec: str) -> str:
     return dict(p.split("=", 1) for p in spec.split(",")).get(app, "python")
 
 
+def rank_device_env(environ: dict[str, str] | None = None) -> dict[str, str]:
+    """The rank's environment processes see only the rank's own GPU: a document store that
+    turns on its GPU query path opens its context there, not on device 0 for every rank."""
+    env = os.environ if environ is None else environ
+    if int(env.get("WORLD_SIZE", "1")) <= 1 or "HIP_VISIBLE_DEVICES" in env or "LOCAL_RANK" not in env:
+        return {}
+    return {"HIP_VISIBLE_DEVICES": env["LOCAL_RANK"]}
+
+
 def device_sync() -> None:
     """Contract: bracket the timed region with a device sync when a GPU is present -- this
     rank's own GPU (LOCAL_RANK), so N ranks do not all open a context on device 0."""
@@ -149,7 +158,8 @@ def main() -> None:
     for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
         b()
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
-    stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01")})
+    stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01"),
+                            **rank_device_env()})
     try:
         backing = stack.start_backing()
         if a.split_backing:

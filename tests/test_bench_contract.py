@@ -74,3 +74,13 @@ def test_parallel_helpers():
     assert cpu_budget() >= 1
     d = Dist()  # single process: identities
     assert (d.world, d.rank, d.max(3.0), d.sum(2.0)) == (1, 0, 3.0, 2.0)
+
+
+def test_rank_device_env():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.rank_device_env({"WORLD_SIZE": "8", "LOCAL_RANK": "3"}) == {"HIP_VISIBLE_DEVICES": "3"}
+    assert b.rank_device_env({"WORLD_SIZE": "1", "LOCAL_RANK": "0"}) == {}
+    assert b.rank_device_env({"WORLD_SIZE": "2", "LOCAL_RANK": "1", "HIP_VISIBLE_DEVICES": "5"}) == {}
