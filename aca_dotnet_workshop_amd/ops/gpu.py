@@ -30,6 +30,10 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_max_flat_leaves.restype = ctypes.c_int
     lib.tt_set_flat_grid.argtypes = [I64]
     lib.tt_set_flat_grid.restype = ctypes.c_int
+    lib.tt_sort_pairs_temp_bytes.argtypes = [I64, I32]
+    lib.tt_sort_pairs_temp_bytes.restype = ctypes.c_int64
+    lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P]
+    lib.tt_sort_pairs.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_scan_select.argtypes = [P, I64, P, P, I32, P, I32, P, P, P, P, P]
@@ -74,6 +78,9 @@ class GpuKernels:
         # (profiles/r1_query_scan_flat_ab.md).
         self.flat_eval = False
         self.max_flat_leaves = int(self.lib.tt_max_flat_leaves())
+        # Result ordering sorts (key, row) pairs over the packed key's used bits only
+        # (hip/radix_pairs.hip); False = torch.sort argsort + gather, for A/B runs.
+        self.pair_sort = True
 
     def set_flat_grid(self, blocks: int) -> None:
         """Workgroups of ``tt_scan_flat`` (grid-stride over tiles); 0 = one per tile."""
@@ -214,17 +221,37 @@ class GpuKernels:
             shift = max(0, key_bits - (bins.bit_length() - 1))
             hist = torch.zeros(bins, dtype=torch.int32, device=self.device)
             keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits, hist, shift)
-            top = self._top_k(keys, rows, k, shift, hist)
+            top = self._top_k(keys, rows, k, shift, hist, key_bits)
             if top is not None:
                 return top
         else:
             keys = self.sort_keys(table, rows, specs, ranks, seq, seq_bits)
-        _, idx = torch.sort(keys)
-        if k is not None:
-            idx = idx[:k]
-        return rows[idx]
+        out = self._sorted_rows(keys, rows, key_bits)
+        return out[:k] if k is not None else out
 
-    def _top_k(self, keys, rows, k: int, shift: int, hist):
+    def _sorted_rows(self, keys, rows, key_bits: int):
+        """``rows`` ordered by ``keys`` (ascending, stable)."""
+        if not self.pair_sort or rows.dtype != self.torch.int32 or keys.dtype != self.torch.int64:
+            _, idx = self.torch.sort(keys)
+            return rows[idx]
+        keys, rows = keys.contiguous(), rows.contiguous()
+        n = keys.numel()
+        end_bit = max(1, min(64, int(key_bits)))
+        need = int(self.lib.tt_sort_pairs_temp_bytes(n, end_bit))
+        if need < 0:
+            raise RuntimeError("tt_sort_pairs: bad size or bit range")
+        temp = getattr(self, "_sort_temp", None)
+        if temp is None or temp.numel() < need:
+            temp = self._sort_temp = self.torch.empty(max(need, 1), dtype=self.torch.uint8, device=self.device)
+        keys_out = self.torch.empty_like(keys)
+        rows_out = self.torch.empty_like(rows)
+        rc = self.lib.tt_sort_pairs(keys.data_ptr(), keys_out.data_ptr(), rows.data_ptr(), rows_out.data_ptr(), n,
+                                    end_bit, temp.data_ptr(), need, self._stream())
+        if rc != 0:
+            raise RuntimeError(f"tt_sort_pairs failed ({rc})")
+        return rows_out
+
+    def _top_k(self, keys, rows, k: int, shift: int, hist, key_bits: int = 63):
         import numpy as np
         torch = self.torch
         n = keys.numel()
@@ -240,6 +267,5 @@ class GpuKernels:
                                               out_rows.data_ptr(), counter.data_ptr(), cand, self._stream())
         if rc != 0:
             raise RuntimeError("tt_select_le_bin launch failed")
-        _, idx = torch.sort(out_keys)
-        return out_rows[idx[:k]]
+        return self._sorted_rows(out_keys, out_rows, key_bits)[:k]
 

@@ -118,17 +118,23 @@ def main() -> None:
         ix._full_dirty = True
         sort = [{"key": "taskDueDate", "order": "DESC"}]
         st = ix.to_device(k)
-        for label, kk in (("top100", 100), ("full", None)):
-            for _ in range(2):
-                ix.order_gpu(out, sort, k, kk)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            it = max(1, a.iters // 4)
-            for _ in range(it):
-                ordered = ix.order_gpu(out, sort, k, kk)
-            torch.cuda.synchronize()
-            res[f"order_{label}_ms"] = round((time.perf_counter() - t0) / it * 1e3, 3)
+        # A/B: pair radix sort over the used key bits (default) vs torch.sort argsort + gather
+        for pair, suffix in ((False, "_argsort"), (True, "")):
+            k.pair_sort = pair
+            for label, kk in (("top100", 100), ("full", None)):
+                for _ in range(2):
+                    ix.order_gpu(out, sort, k, kk)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                it = max(1, a.iters // 4)
+                for _ in range(it):
+                    ordered = ix.order_gpu(out, sort, k, kk)
+                torch.cuda.synchronize()
+                res[f"order_{label}{suffix}_ms"] = round((time.perf_counter() - t0) / it * 1e3, 3)
+            if not pair:
+                full_argsort = ordered
         res["ordered_rows"] = int(ordered.numel())
+        res["pair_sort_matches_argsort"] = bool(torch.equal(ordered, full_argsort))
         # the first page must equal the host ordering of the same selection
         sel = out.cpu().numpy()
         plan = ix.sort_specs(sort)

@@ -491,3 +491,23 @@ def test_gpu_rank_encode_unaligned_ranges(ndistinct):
             ix.upsert(str(i), {"v": rnd.randrange(ndistinct)})
         prog = ix.compile({"LT": {"v": lo_v}})
         assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog)), extra
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [5, 70_000, 300_001])
+def test_gpu_pair_sort_matches_argsort(n):
+    """tt_sort_pairs over the used key bits orders rows exactly like torch.sort of the keys,
+    for full orderings and top-k pages."""
+    k = _kernels()
+    ix = _random_collection(n, random.Random(n + 3))
+    try:
+        for sort in ([{"key": "taskDueDate", "order": "DESC"}], [{"key": "taskCreatedBy"}, {"key": "prio", "order": "DESC"}]):
+            for page in ({}, {"limit": 25}, {"limit": 40, "token": "7"}):
+                q = {"filter": {"EQ": {"isCompleted": False}}, "sort": sort, "page": page}
+                k.pair_sort = False
+                want = ix.query(q, k)
+                k.pair_sort = True
+                assert ix.query(q, k) == want, (n, sort, page)
+                assert want == ix.query(q), (n, sort, page)
+    finally:
+        k.pair_sort = True
