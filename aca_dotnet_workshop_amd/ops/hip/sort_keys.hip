@@ -144,13 +144,28 @@ tt_select_le_bin(const uint64_t* __restrict__ keys, const int32_t* __restrict__ 
   __shared__ uint32_t warp_counts[kBlock / 64];
   __shared__ uint32_t block_base;
   const int64_t base = (int64_t)blockIdx.x * kBlock * kSelItems;
-  // pass 1: count this thread's matches (no dynamically indexed register arrays -> no scratch)
+  // pass 1: count this thread's matches (no dynamically indexed register arrays -> no scratch).
+  // Item j of a thread is key base + (j / 2) * 2 * kBlock + 2 * thread + (j & 1): pairs of keys
+  // come in one 16-byte load (8 per thread, 1 KiB per wave-instruction); a pair that straddles
+  // n (odd n, last pair) is read key by key.
   uint32_t matchbits = 0, cnt = 0;
 #pragma unroll
-  for (int j = 0; j < kSelItems; ++j) {
-    const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;  // coalesced across the block
-    if (i < n && ((uint32_t)(keys[i] >> shift) & (kHistBins - 1)) <= last_bin) {
-      matchbits |= 1u << j;
+  for (int j2 = 0; j2 < kSelItems / 2; ++j2) {
+    const int64_t i = base + (int64_t)j2 * 2 * kBlock + 2 * (int64_t)threadIdx.x;
+    uint64_t k0 = 0, k1 = 0;
+    if (i + 1 < n) {
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(keys + i);
+      k0 = v.x;
+      k1 = v.y;
+    } else if (i < n) {
+      k0 = keys[i];
+    }
+    if (i < n && ((uint32_t)(k0 >> shift) & (kHistBins - 1)) <= last_bin) {
+      matchbits |= 1u << (2 * j2);
+      ++cnt;
+    }
+    if (i + 1 < n && ((uint32_t)(k1 >> shift) & (kHistBins - 1)) <= last_bin) {
+      matchbits |= 1u << (2 * j2 + 1);
       ++cnt;
     }
   }
@@ -179,7 +194,7 @@ tt_select_le_bin(const uint64_t* __restrict__ keys, const int32_t* __restrict__ 
 #pragma unroll
   for (int j = 0; j < kSelItems; ++j) {
     if (!(matchbits & (1u << j))) continue;
-    const int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    const int64_t i = base + (int64_t)(j >> 1) * 2 * kBlock + 2 * (int64_t)threadIdx.x + (j & 1);
     if (pos < capacity) {
       out_keys[pos] = keys[i];
       out_rows[pos] = rows[i];
