@@ -16,6 +16,7 @@ the multi-rank side used by ``bench.py`` when the driver launches one process pe
 from __future__ import annotations
 
 import os
+import sys
 
 __all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling"]
 
@@ -29,7 +30,16 @@ class Dist:
         self.pg = None
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("gloo", init_method="env://")
+            # gloo announces its peer connections on fd 1; rank 0's stdout carries exactly one
+            # JSON result line (the bench contract), so route that chatter to stderr
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", init_method="env://")
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
             self.pg = dist
 
     def barrier(self) -> None:

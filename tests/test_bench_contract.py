@@ -51,6 +51,8 @@ def test_bench_two_ranks_torchrun():
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
+    # nothing else on stdout (gloo's connection messages go to stderr)
+    assert [x for x in r.stdout.splitlines() if x.strip() and not x.startswith("{")] == [], r.stdout
     _check(lines[0], 2, 2, 1)
 
 
