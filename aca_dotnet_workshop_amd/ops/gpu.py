@@ -72,9 +72,10 @@ class GpuKernels:
         # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
         self.fused_select = False
         # Flat programs (one AND / OR over leaves) can run on tt_scan_flat (wave-wide compares,
-        # leaves combined in scalar registers: ~3x fewer VALU instructions).  Opt-in: on the 1e8-row
-        # overdue sweep it ties the interpreter (92.8 vs 92.8 µs) -- both stream the narrow
-        # columns at the same ~4.6 TB/s -- so the simpler path stays the default
+        # leaves combined in scalar registers).  Opt-in: on the 1e8-row overdue sweep it ties
+        # the interpreter (92.8 vs 92.8 µs; PMC: similar VALU counts, half the wait cycles, same
+        # duration) -- both stream the narrow columns at the same ~4.6 TB/s -- so the simpler
+        # path stays the default
         # (profiles/r1_query_scan_flat_ab.md).
         self.flat_eval = False
         self.max_flat_leaves = int(self.lib.tt_max_flat_leaves())
