@@ -37,8 +37,8 @@ from aca_dotnet_workshop_amd.parallel import Dist, cgroup_throttling, cpu_budget
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1024, help="createTask requests per step per rank")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="requests in flight per rank (0 = 48 per API replica, at most 384)")
