@@ -6,16 +6,26 @@ needs a collection scan (ranges, NEQ, OR over non-equality leaves, no filter wit
 runs on the collection's ``ColumnarIndex``: on the GPU (``ops/hip/query_scan.hip``) when a
 HIP device is present, else the NumPy executor of the same compiled program.
 
+The index is fed by the document store's own column mirror (``DocStore.mirror_*``,
+native/src/docstore.hpp): every write -- from the GIL-free native HTTP front or from
+Python -- appends its row in C++ under the store lock, and a query first pulls only what
+changed since the previous one.  Turning the accelerator on therefore never moves a
+collection's writes off the native path.  Collections that use TTL are not mirrored
+(expiry is evaluated by the native engine) and fall back to it.
+
+``query`` blocks (mirror build / sync, kernel launches, result assembly): the backing
+server calls it from a worker thread, never on its event loop.
+
 Mode (``TT_QUERY_ACCEL``): ``off`` | ``cpu`` | ``gpu`` | ``auto`` (default: GPU if
-available, else CPU) and size threshold ``TT_QUERY_ACCEL_MIN_DOCS`` (default 20000).
-The index mirrors every write (upsert/delete/transaction); collections that use TTL fall
-back to the native engine (expiry is evaluated there).
+available, else CPU); size threshold ``TT_QUERY_ACCEL_MIN_DOCS`` (default 20000);
+``TT_QUERY_MIRROR_PATHS`` (comma separated): paths mirrored from a collection's first write,
+so the first scan-shaped query finds the mirror already built (Cosmos "indexing policy").
 """
 from __future__ import annotations
 
-import json
 import logging
 import os
+import threading
 from typing import Any
 
 from ..ops.columnar import ColumnarIndex, Unsupported, filter_paths
@@ -46,30 +56,21 @@ def indexable(f: Any) -> bool:
 
 
 class CollectionAccelerator:
-    def __init__(self, mode: str, min_docs: int) -> None:
+    def __init__(self, mode: str, min_docs: int, preload: list[str] | None = None) -> None:
         self.mode = mode
         self.min_docs = min_docs
+        self.preload = [p for p in (preload or []) if p]
         self.index: ColumnarIndex | None = None
         self.disabled = mode == "off"
-        self.stats = {"native": 0, "gpu": 0, "cpu": 0, "fallback": 0}
+        self.stats = {"native": 0, "gpu": 0, "cpu": 0, "fallback": 0, "skipped_rows": 0}
         self._kernels = None
-        self.before_build = None  # hook: route the collection's writes through on_put/on_delete
+        self.lock = threading.Lock()  # one query / sync at a time per collection
 
-    # -- write mirroring ------------------------------------------------------
-    def on_put(self, key: str, value: str, ttl_ms: int = 0) -> None:
-        if ttl_ms:
-            self.disabled = True
-            self.index = None
-            return
-        if self.index is not None:
-            try:
-                self.index.upsert(key, _with_prefix(key, json.loads(value)))
-            except ValueError:
-                self.index.delete(key)
-
-    def on_delete(self, key: str) -> None:
-        if self.index is not None:
-            self.index.delete(key)
+    def attach(self, store) -> None:
+        """New collection: start mirroring the configured paths from its first write."""
+        if self.preload and not self.disabled:
+            if not store.mirror_enable([PREFIX_PATH, *self.preload]):
+                self.disabled = True
 
     # -- querying ---------------------------------------------------------------
     def kernels(self):
@@ -95,56 +96,48 @@ class CollectionAccelerator:
         return self.index is not None or len(store) >= self.min_docs
 
     def build(self, store, paths: list[str] = ()) -> None:
-        if self.before_build is not None:
-            self.before_build()
-        # native bulk encode (DocStore.encode_columns, one thread per column) of every column the
-        # triggering query needs: no per-document Python objects
-        ix = ColumnarIndex.from_source(lambda ps: store.encode_columns("", ps), [PREFIX_PATH, *paths])
-        self.index = ix
-        log.info("built columnar index over %d documents", ix.live_rows())
+        # the store encodes every column the triggering query needs (one thread per column)
+        # and from then on appends a row per write itself
+        self.index = ColumnarIndex.from_native(store, [PREFIX_PATH, *self.preload, *paths])
+        log.info("columnar mirror over %d documents", self.index.live_rows())
 
     def query(self, q: dict[str, Any], prefix: str, store) -> str | None:
-        """JSON result text, or None to let the native engine answer."""
+        """JSON result text, or None to let the native engine answer.  Blocking."""
         if not self.should_accelerate(q, store):
             self.stats["native"] += 1
             return None
-        if self.index is None:
-            self.build(store, filter_paths(q.get("filter")) + [s["key"] for s in q.get("sort") or []
-                                                               if isinstance(s, dict) and "key" in s])
-        flt = q.get("filter") or {}
-        if prefix:
-            flt = {"AND": [{"EQ": {PREFIX_PATH: prefix}}, flt]} if flt else {"EQ": {PREFIX_PATH: prefix}}
-        qq = dict(q)
-        qq["filter"] = flt
-        k = self.kernels()
-        try:
-            keys, token = self.index.query(qq, k)
-        except Unsupported:
-            self.stats["fallback"] += 1
-            return None
-        self.stats["gpu" if k is not None else "cpu"] += 1
-        parts = []
-        for key in keys:
-            got = store.get(key)
-            if got is None:
-                continue
-            parts.append('{"key":' + json.dumps(key[len(prefix):]) + ',"data":' + got[0] + ',"etag":"' + got[1] + '"}')
-        out = '{"results":[' + ",".join(parts) + "]"
-        if token:
-            out += ',"token":"' + token + '"'
-        return out + "}"
-
-
-def _with_prefix(key: str, doc: Any) -> Any:
-    """Attach the key's ``<app-id>||`` prefix as a hidden column value."""
-    i = key.find("||")
-    pfx = key[:i + 2] if i >= 0 else ""
-    if isinstance(doc, dict):
-        d = dict(doc)
-        d[PREFIX_PATH] = pfx
-        return d
-    return {PREFIX_PATH: pfx, "\x00value": doc}
+        with self.lock:
+            try:
+                if self.index is None:
+                    self.build(store, filter_paths(q.get("filter")) + [s["key"] for s in q.get("sort") or []
+                                                                       if isinstance(s, dict) and "key" in s])
+                else:
+                    self.index.sync()
+            except Unsupported as e:
+                log.info("columnar accelerator off for this collection: %s", e)
+                self.disabled, self.index = True, None
+                self.stats["fallback"] += 1
+                return None
+            flt = q.get("filter") or {}
+            if prefix:
+                flt = {"AND": [{"EQ": {PREFIX_PATH: prefix}}, flt]} if flt else {"EQ": {PREFIX_PATH: prefix}}
+            qq = dict(q)
+            qq["filter"] = flt
+            k = self.kernels()
+            try:
+                rows, token = self.index.query_rows(qq, k)
+            except Unsupported:
+                self.stats["fallback"] += 1
+                return None
+            self.stats["gpu" if k is not None else "cpu"] += 1
+            text, skipped = store.mirror_results(rows, prefix, token or "")
+            self.stats["skipped_rows"] += skipped
+            return text.decode()
 
 
 def accelerator_from_env() -> tuple[str, int]:
     return os.environ.get("TT_QUERY_ACCEL", "auto").lower(), int(os.environ.get("TT_QUERY_ACCEL_MIN_DOCS", "20000"))
+
+
+def mirror_paths_from_env() -> list[str]:
+    return [p.strip() for p in os.environ.get("TT_QUERY_MIRROR_PATHS", "").split(",") if p.strip()]

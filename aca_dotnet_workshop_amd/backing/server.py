@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import base64
+import concurrent.futures
 import json
 import logging
 import os
@@ -36,7 +37,7 @@ from ..telemetry import configure, configure_logging
 from ..telemetry.profiler import maybe_profile
 from ..web.app import WebApp
 from ..web.http import HTTPError, Request, Response, empty, json_response, problem
-from .accel import CollectionAccelerator, accelerator_from_env
+from .accel import CollectionAccelerator, accelerator_from_env, mirror_paths_from_env
 from .auth import AccessPolicy
 
 log = logging.getLogger("backing")
@@ -102,6 +103,10 @@ class BackingServices:
         self.fsync = fsync
         self.stores: dict[tuple[str, str, str], Any] = {}
         self.accel_mode, self.accel_min_docs = accelerator_from_env()
+        self.mirror_paths = mirror_paths_from_env()
+        # blocking query work (columnar mirror sync, GPU kernels, native scans) runs here, never
+        # on the event loop; the per-collection accelerator lock serialises GPU use
+        self.query_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="tt-query")
         self.accels: dict[tuple[str, str, str], CollectionAccelerator] = {}
         self.brokers: dict[str, Any] = {}
         self.waiters = Waiters()
@@ -119,9 +124,6 @@ class BackingServices:
             front.attach_store(a, d, c, s)
         for ns, b in self.brokers.items():
             front.attach_broker(ns, b)
-        for (a, d, c), acc in self.accels.items():
-            if acc.index is not None:
-                front.set_mirrored(a, d, c)
         self._push_policy()
         self.waiters.listeners.append(lambda key: front.notify(*key.split("|", 1)))
 
@@ -145,6 +147,7 @@ class BackingServices:
         s = self.stores.get(key)
         if s is None:
             s = self.stores[key] = self.N.DocStore(self._path("cosmos", account, db, coll + ".log"), self.fsync)
+            self.accel(account, db, coll).attach(s)
             if self.front is not None:
                 self.front.attach_store(account, db, coll, s)
         return s
@@ -153,9 +156,7 @@ class BackingServices:
         key = (account, db, coll)
         a = self.accels.get(key)
         if a is None:
-            a = self.accels[key] = CollectionAccelerator(self.accel_mode, self.accel_min_docs)
-            # once the columnar mirror exists, writes must flow through the Python handlers
-            a.before_build = lambda: self.front.set_mirrored(account, db, coll) if self.front is not None else None
+            a = self.accels[key] = CollectionAccelerator(self.accel_mode, self.accel_min_docs, self.mirror_paths)
         return a
 
     def broker(self, ns: str):
@@ -165,6 +166,12 @@ class BackingServices:
             if self.front is not None:
                 self.front.attach_broker(ns, b)
         return b
+
+    def prewarm_accelerator(self) -> None:
+        try:
+            CollectionAccelerator(self.accel_mode, self.accel_min_docs).kernels()
+        except Exception as e:
+            log.warning("GPU query accelerator unavailable: %s", e)
 
     def _load_vaults(self) -> None:
         if self.data_dir is None:
@@ -225,7 +232,6 @@ class BackingServices:
                 return problem(412, detail=str(ex))
             except ValueError as ex:
                 return problem(400, detail=str(ex))
-            acc(req).on_put(req.path_params["key"], value, ttl)
             return json_response({"etag": e}, headers=[("ETag", e)])
 
         async def get_doc(req: Request) -> Response:
@@ -241,8 +247,6 @@ class BackingServices:
                 ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
             except self.N.EtagMismatch as ex:
                 return problem(412, detail=str(ex))
-            if ok:
-                acc(req).on_delete(req.path_params["key"])
             return empty(204 if ok else 404)
 
         async def bulk_get(req: Request) -> Response:
@@ -256,13 +260,11 @@ class BackingServices:
         async def bulk_set(req: Request) -> Response:
             s = st(req, "cosmos.write")
             out = []
-            a = acc(req)
             for it in req.json() or []:
                 try:
                     value = it["value"] if isinstance(it["value"], str) else json.dumps(it["value"])
                     ttl = int(it.get("ttlMs") or 0)
                     e = s.set(it["key"], value, it.get("etag") or None, bool(it.get("firstWrite")), ttl)
-                    a.on_put(it["key"], value, ttl)
                     out.append({"key": it["key"], "etag": e})
                 except self.N.EtagMismatch as ex:
                     out.append({"key": it["key"], "error": "etag", "detail": str(ex)})
@@ -276,11 +278,14 @@ class BackingServices:
             s = st(req, "cosmos.read")
             raw = req.body.decode("utf-8") or "{}"
             prefix = req.query_get("prefix", "") or ""
-            try:
+            a = acc(req)
+
+            def run() -> str:
                 q = json.loads(raw)
-                text = acc(req).query(q, prefix, s) if isinstance(q, dict) else None
-                if text is None:
-                    text = s.query(raw, prefix)
+                text = a.query(q, prefix, s) if isinstance(q, dict) else None
+                return s.query(raw, prefix) if text is None else text
+            try:
+                text = await asyncio.get_running_loop().run_in_executor(self.query_pool, run)
             except ValueError as ex:
                 return problem(400, detail=str(ex))
             return Response(text.encode(), 200, None, "application/json")
@@ -299,12 +304,6 @@ class BackingServices:
                 return problem(412, detail=str(ex))
             except ValueError as ex:
                 return problem(400, detail=str(ex))
-            a = acc(req)
-            for o in ops:
-                if o.is_delete:
-                    a.on_delete(o.key)
-                else:
-                    a.on_put(o.key, o.value, o.ttl_ms)
             return empty(204)
 
         async def stats(req: Request) -> Response:
@@ -312,7 +311,8 @@ class BackingServices:
             d = dict(s.stats())
             d["indexedPaths"] = s.indexed_paths()
             a = acc(req)
-            d["accelerator"] = {"mode": a.mode, "rows": a.index.live_rows() if a.index else 0, **a.stats}
+            d["accelerator"] = {"mode": a.mode, "rows": a.index.live_rows() if a.index else 0, **a.stats,
+                                "mirror": dict(s.mirror_stats())}
             return json_response(d)
 
         async def keys(req: Request) -> Response:
@@ -687,6 +687,10 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         bound = await srv.listen_tcp(host, port)
     log.info("backing services listening on %s:%d (data=%s, front=%s)", host, bound, data_dir,
              "native" if front is not None else "python")
+    if svc.mirror_paths and svc.accel_mode in ("auto", "gpu"):
+        # collections are mirrored from their first write: open the GPU context now, off the
+        # event loop, so the first scan-shaped query does not pay the HIP runtime start-up
+        svc.query_pool.submit(svc.prewarm_accelerator)
     if ready:
         ready(bound)
     stop = stop or asyncio.Event()

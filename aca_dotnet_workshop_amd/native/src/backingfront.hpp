@@ -15,9 +15,9 @@
 // admin) and every request for an engine the Python side has not attached yet is forwarded
 // verbatim to the Python server on a private Unix socket.  Responses, status codes and RBAC
 // decisions mirror backing/server.py and backing/auth.py (role assignments are pushed down
-// as principal -> (scope prefix, actions)).  Collections whose writes must be mirrored into
-// the columnar query accelerator are flagged by Python (set_mirrored) and their writes are
-// forwarded; a per-collection shared mutex makes the hand-over race-free.
+// as principal -> (scope prefix, actions)).  Collections mirrored by the columnar query
+// accelerator keep their writes here: the DocStore maintains its column mirror itself
+// (docstore.hpp ColumnMirror) on every write, whichever front made it.
 #pragma once
 
 #include <sys/eventfd.h>
@@ -100,19 +100,6 @@ class BackingFront {
     std::unique_lock l(cfg_mu_);
     brokers_[ns] = b;
   }
-  // Writes to this collection must go through Python from now on (accelerator mirror).
-  // Blocks until native writes already in progress on the collection have finished.
-  void set_mirrored(const std::string& account, const std::string& db, const std::string& coll) {
-    Coll* c;
-    {
-      std::unique_lock l(cfg_mu_);
-      auto& p = colls_[account + "\x1f" + db + "\x1f" + coll];
-      if (!p) p = std::make_unique<Coll>();
-      c = p.get();
-    }
-    std::unique_lock w(c->write_mu);
-    c->mirrored = true;
-  }
   void set_policy(const std::string& mode, const std::vector<std::pair<std::string, std::string>>& keys,
                   const std::vector<std::tuple<std::string, std::string, std::vector<std::string>>>& grants) {
     std::unique_lock l(cfg_mu_);
@@ -133,8 +120,6 @@ class BackingFront {
  private:
   struct Coll {
     DocStore* store = nullptr;
-    bool mirrored = false;
-    std::shared_mutex write_mu;
   };
   struct Parked {
     std::string ns, entity;
@@ -354,8 +339,6 @@ class BackingFront {
     if (m.method != "PUT" && m.method != "DELETE") return false;
     auto* ttl = m.header("x-tt-ttl-ms");
     if (ttl && !ttl->empty() && *ttl != "0") return false;  // TTL writes disable the accelerator (Python)
-    std::shared_lock w(c->write_mu);
-    if (c->mirrored) return false;
     if (!authorize(m, r, "cosmos.write", scope)) return true;
     auto* im = m.header("if-match");
     std::optional<std::string> etag;
@@ -406,8 +389,6 @@ class BackingFront {
       auto* k = it.get("key");
       if (!k || k->t != Value::String) return false;
     }
-    std::shared_lock w(c->write_mu);
-    if (c->mirrored) return false;
     if (!authorize(m, r, "cosmos.write", "cosmos/" + seg[1])) return true;
     count("doc.bulkset");
     std::string out = "[";

@@ -133,6 +133,67 @@ struct Doc {
   uint64_t etag = 0;
   uint64_t seq = 0;
   int64_t expire_ms = 0;
+  uint32_t mrow = UINT32_MAX;  // row in the column mirror (UINT32_MAX = none)
+};
+
+// Canonical dictionary key of a JSON scalar with the query engine's equality: numbers by
+// value (-0.0 == 0.0), strings / booleans / null by value, arrays / objects by canonical JSON.
+inline void mirror_key(const Value& v, std::string& k) {
+  k.clear();
+  switch (v.t) {
+    case Value::Null: k = "n"; break;
+    case Value::Bool: k = v.b ? "b1" : "b0"; break;
+    case Value::Number: {
+      double d = v.n + 0.0;  // folds -0.0
+      uint64_t bits;
+      std::memcpy(&bits, &d, sizeof bits);
+      k.assign("d");
+      k.append(reinterpret_cast<const char*>(&bits), sizeof bits);
+      break;
+    }
+    case Value::String: k = "s"; k += v.s; break;
+    default: k = "j"; dump_to(k, v);
+  }
+}
+
+// Columnar mirror of a collection, maintained on every write under the store lock -- the
+// source of the GPU query accelerator (ops/columnar.py ColumnarIndex.from_native).  One row
+// per document version: an update kills the document's row and appends a new one (same seq,
+// so orderings keep the native engine's insertion-order semantics); deletes kill the row.
+// Readers pull deltas (rows appended since a cursor, new dictionary values, killed rows)
+// instead of re-encoding, and the native write path never leaves C++.  Compaction drops dead
+// rows and bumps the generation (readers then reload).
+struct MirrorColumn {
+  std::string path;
+  std::unordered_map<std::string, int32_t> dict;  // canonical key -> id
+  std::vector<std::string> values;                // JSON text per id, in order of first use
+  std::vector<int32_t> ids;                       // per row (-1 = path missing)
+};
+
+struct ColumnMirror {
+  bool on = false;
+  bool disabled = false;  // TTL writes: expiry is evaluated by the native engine only
+  uint64_t gen = 1;
+  std::vector<MirrorColumn> cols;
+  std::vector<const std::string*> keys;  // per row: the owning map node's key (valid while live)
+  std::vector<int64_t> seqs;
+  std::vector<uint8_t> live;
+  std::vector<uint32_t> kills;  // rows killed since this generation began
+  size_t live_rows = 0;
+  uint64_t compactions = 0;
+};
+
+struct MirrorDelta {
+  uint64_t gen = 0;
+  bool on = false, disabled = false, full = false;
+  size_t n = 0, from = 0, kill_cursor = 0;
+  std::vector<std::string> paths;
+  std::vector<size_t> dict_from;
+  std::vector<std::vector<std::string>> new_values;
+  std::vector<std::vector<int32_t>> ids;
+  std::vector<int64_t> seqs;
+  std::vector<uint8_t> live;     // rows [from, n)  (from == 0 when full)
+  std::vector<uint32_t> kills;   // rows < from killed since the reader's kill cursor
 };
 
 struct TxOp {
@@ -376,21 +437,7 @@ class DocStore {
           col.ids[i] = -1;
           continue;
         }
-        k.clear();
-        switch (v->t) {
-          case Value::Null: k = "n"; break;
-          case Value::Bool: k = v->b ? "b1" : "b0"; break;
-          case Value::Number: {
-            double d = v->n + 0.0;  // folds -0.0
-            uint64_t bits;
-            std::memcpy(&bits, &d, sizeof bits);
-            k.assign("d");
-            k.append(reinterpret_cast<const char*>(&bits), sizeof bits);
-            break;
-          }
-          case Value::String: k = "s"; k += v->s; break;
-          default: k = "j"; dump_to(k, *v);
-        }
+        mirror_key(*v, k);
         auto it = dict.find(k);
         if (it == dict.end()) {
           it = dict.emplace(k, (int32_t)col.values.size()).first;
@@ -407,6 +454,119 @@ class DocStore {
       for (auto& t : ts) t.join();
     }
     return out;
+  }
+
+  // ------------------------------------------------------------ column mirror
+  // Mirror `paths` (added to the mirrored set; existing rows are encoded for new paths).  The
+  // first call builds the mirror from the live documents in insertion order.  Returns false
+  // when the collection cannot be mirrored (a TTL write was seen).
+  bool mirror_enable(const std::vector<std::string>& paths) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (mirror_.disabled) return false;
+    std::vector<std::string> add;
+    for (auto& p : paths) {
+      bool have = false;
+      for (auto& c : mirror_.cols) have = have || c.path == p;
+      for (auto& a : add) have = have || a == p;
+      if (!have) add.push_back(p);
+    }
+    if (mirror_.on && add.empty()) return true;
+    if (!mirror_.on) {
+      for (auto& [k, d] : docs_)
+        if (d.expire_ms) { mirror_.disabled = true; return false; }
+      mirror_.on = true;
+      mirror_.cols.clear();
+      for (auto& p : add) { mirror_.cols.emplace_back(); mirror_.cols.back().path = p; }
+      mirror_rebuild_rows();
+    } else {
+      size_t first = mirror_.cols.size();
+      for (auto& p : add) { mirror_.cols.emplace_back(); mirror_.cols.back().path = p; }
+      auto enc = [&](size_t c) {
+        MirrorColumn& col = mirror_.cols[c];
+        col.ids.assign(mirror_.keys.size(), -1);
+        std::string k;
+        for (size_t r = 0; r < mirror_.keys.size(); ++r) {
+          if (!mirror_.live[r]) continue;
+          auto it = docs_.find(*mirror_.keys[r]);
+          col.ids[r] = mirror_encode(col, it->first, it->second.parsed, k);
+        }
+      };
+      parallel_for_columns(first, mirror_.cols.size(), enc);
+      ++mirror_.gen;
+      mirror_.kills.clear();
+    }
+    return true;
+  }
+
+  // Changes since a reader's cursor (generation, rows seen, kill-log position, dictionary
+  // sizes per column); a different generation (or column set) returns everything.
+  MirrorDelta mirror_delta(uint64_t gen, size_t from, size_t kill_from, const std::vector<size_t>& dict_sizes) {
+    std::lock_guard<std::mutex> g(mu_);
+    MirrorDelta d;
+    d.gen = mirror_.gen;
+    d.on = mirror_.on;
+    d.disabled = mirror_.disabled;
+    if (!mirror_.on) return d;
+    size_t n = mirror_.keys.size();
+    d.full = gen != mirror_.gen || dict_sizes.size() != mirror_.cols.size() || from > n ||
+             kill_from > mirror_.kills.size();
+    if (d.full) from = 0, kill_from = mirror_.kills.size();
+    d.n = n;
+    d.from = from;
+    d.kill_cursor = mirror_.kills.size();
+    for (size_t i = kill_from; i < mirror_.kills.size(); ++i)
+      if (mirror_.kills[i] < from) d.kills.push_back(mirror_.kills[i]);
+    d.seqs.assign(mirror_.seqs.begin() + from, mirror_.seqs.end());
+    d.live.assign(mirror_.live.begin() + from, mirror_.live.end());
+    for (size_t c = 0; c < mirror_.cols.size(); ++c) {
+      auto& col = mirror_.cols[c];
+      size_t df = d.full ? 0 : std::min(dict_sizes[c], col.values.size());
+      d.paths.push_back(col.path);
+      d.dict_from.push_back(df);
+      d.new_values.emplace_back(col.values.begin() + df, col.values.end());
+      d.ids.emplace_back(col.ids.begin() + from, col.ids.end());
+    }
+    return d;
+  }
+
+  // Query result JSON for mirror rows (in the given order): {"results":[{"key","data","etag"}]}
+  // with `prefix` stripped from the keys.  Rows killed since the reader's sync (the document
+  // changed or went away) are skipped; `skipped` reports how many.
+  std::string mirror_results(const int32_t* rows, size_t nrows, const std::string& prefix, const std::string& token,
+                             size_t* skipped = nullptr) {
+    std::lock_guard<std::mutex> g(mu_);
+    int64_t now = now_ms();
+    std::string out = "{\"results\":[";
+    size_t skip = 0;
+    bool first = true;
+    for (size_t i = 0; i < nrows; ++i) {
+      uint32_t r = (uint32_t)rows[i];
+      if (r >= mirror_.keys.size() || !mirror_.live[r]) { ++skip; continue; }
+      const std::string& key = *mirror_.keys[r];
+      auto it = docs_.find(key);
+      if (it == docs_.end() || it->second.mrow != r || expired(it->second, now)) { ++skip; continue; }
+      if (!first) out += ',';
+      first = false;
+      out += "{\"key\":";
+      escape_to(out, std::string_view(key).substr(std::min(prefix.size(), key.size())));
+      out += ",\"data\":";
+      out += it->second.value;
+      out += ",\"etag\":\"";
+      out += std::to_string(it->second.etag);
+      out += "\"}";
+    }
+    out += "]";
+    if (!token.empty()) out += ",\"token\":\"" + token + "\"";
+    out += "}";
+    if (skipped) *skipped = skip;
+    return out;
+  }
+
+  std::unordered_map<std::string, uint64_t> mirror_stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    return {{"on", mirror_.on}, {"disabled", mirror_.disabled}, {"gen", mirror_.gen},
+            {"rows", mirror_.keys.size()}, {"live_rows", mirror_.live_rows}, {"columns", mirror_.cols.size()},
+            {"compactions", mirror_.compactions}};
   }
 
   size_t size() {
@@ -454,6 +614,7 @@ class DocStore {
   uint64_t put(const std::string& key, const std::string& value, Value parsed, int64_t expire_ms) {
     auto it = docs_.find(key);
     uint64_t e = ++etag_;
+    if (expire_ms && mirror_.on) mirror_disable();
     if (it == docs_.end()) {
       Doc d;
       d.value = value;
@@ -463,7 +624,7 @@ class DocStore {
       d.expire_ms = expire_ms;
       live_bytes_ += key.size() + value.size();
       index_add(key, d.parsed);
-      docs_.emplace(key, std::move(d));
+      it = docs_.emplace(key, std::move(d)).first;
     } else {
       index_remove(key, it->second.parsed);
       live_bytes_ += value.size();
@@ -473,7 +634,9 @@ class DocStore {
       it->second.etag = e;
       it->second.expire_ms = expire_ms;
       index_add(key, it->second.parsed);
+      mirror_kill(it->second);
     }
+    if (mirror_.on) mirror_append(*it);
     return e;
   }
 
@@ -481,6 +644,7 @@ class DocStore {
     auto it = docs_.find(key);
     if (it == docs_.end()) return;
     index_remove(key, it->second.parsed);
+    mirror_kill(it->second);
     live_bytes_ -= key.size() + it->second.value.size();
     docs_.erase(it);
     if (log) log_.append('D', {key});
@@ -524,6 +688,123 @@ class DocStore {
         out.append('P', {r.second->first, r.second->second.value, AppLog::pod(r.second->second.etag),
                          AppLog::pod(r.second->second.expire_ms)});
     });
+  }
+
+  // ----------------------------------------------------------- column mirror (locked)
+  template <class F>
+  void parallel_for_columns(size_t lo, size_t hi, F&& f) {
+    if (hi - lo <= 1 || mirror_.keys.size() < 100000) {
+      for (size_t c = lo; c < hi; ++c) f(c);
+      return;
+    }
+    std::vector<std::thread> ts;
+    for (size_t c = lo; c < hi; ++c) ts.emplace_back(f, c);
+    for (auto& t : ts) t.join();
+  }
+
+  // Dictionary id of `path` in document `doc` under `key` (pseudo-paths as encode_columns).
+  static int32_t mirror_encode(MirrorColumn& col, const std::string& key, const Value& doc, std::string& k) {
+    static const std::string kPrefix("\x00keyprefix", 10), kValue("\x00value", 6);
+    Value tmp;
+    const Value* v;
+    if (col.path == kPrefix) {
+      size_t p = key.find("||");
+      tmp = Value::string(p == std::string::npos ? std::string() : key.substr(0, p + 2));
+      v = &tmp;
+    } else if (col.path == kValue) {
+      v = doc.t == Value::Object ? nullptr : &doc;
+    } else {
+      v = doc.path(col.path);
+    }
+    if (!v) return -1;
+    mirror_key(*v, k);
+    auto it = col.dict.find(k);
+    if (it == col.dict.end()) {
+      it = col.dict.emplace(k, (int32_t)col.values.size()).first;
+      col.values.push_back(dump(*v));
+    }
+    return it->second;
+  }
+
+  void mirror_append(std::pair<const std::string, Doc>& kv) {
+    uint32_t r = (uint32_t)mirror_.keys.size();
+    mirror_.keys.push_back(&kv.first);
+    mirror_.seqs.push_back((int64_t)kv.second.seq);
+    mirror_.live.push_back(1);
+    std::string k;
+    for (auto& col : mirror_.cols) col.ids.push_back(mirror_encode(col, kv.first, kv.second.parsed, k));
+    kv.second.mrow = r;
+    ++mirror_.live_rows;
+    if (mirror_.keys.size() > 65536 && mirror_.keys.size() > 2 * mirror_.live_rows) mirror_compact();
+  }
+
+  void mirror_kill(Doc& d) {
+    if (d.mrow == UINT32_MAX) return;
+    if (mirror_.on && d.mrow < mirror_.live.size() && mirror_.live[d.mrow]) {
+      mirror_.live[d.mrow] = 0;
+      mirror_.kills.push_back(d.mrow);
+      --mirror_.live_rows;
+    }
+    d.mrow = UINT32_MAX;
+  }
+
+  void mirror_disable() {
+    for (auto& kv : docs_) kv.second.mrow = UINT32_MAX;
+    uint64_t gen = mirror_.gen;
+    mirror_ = ColumnMirror{};
+    mirror_.gen = gen + 1;
+    mirror_.disabled = true;
+  }
+
+  // Every live document, in insertion order, re-encoded into fresh rows (new generation).
+  void mirror_rebuild_rows() {
+    std::vector<std::pair<uint64_t, std::pair<const std::string, Doc>*>> rows;
+    rows.reserve(docs_.size());
+    for (auto& kv : docs_) rows.emplace_back(kv.second.seq, &kv);
+    std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
+    mirror_.keys.clear();
+    mirror_.seqs.clear();
+    mirror_.kills.clear();
+    mirror_.keys.reserve(rows.size());
+    for (auto& r : rows) {
+      r.second->second.mrow = (uint32_t)mirror_.keys.size();
+      mirror_.keys.push_back(&r.second->first);
+      mirror_.seqs.push_back((int64_t)r.first);
+    }
+    mirror_.live.assign(rows.size(), 1);
+    mirror_.live_rows = rows.size();
+    auto enc = [&](size_t c) {
+      MirrorColumn& col = mirror_.cols[c];
+      col.ids.resize(rows.size());
+      std::string k;
+      for (size_t i = 0; i < rows.size(); ++i)
+        col.ids[i] = mirror_encode(col, rows[i].second->first, rows[i].second->second.parsed, k);
+    };
+    parallel_for_columns(0, mirror_.cols.size(), enc);
+    ++mirror_.gen;
+  }
+
+  // Drop dead rows (renumbering the survivors in row order); dictionaries are kept.
+  void mirror_compact() {
+    size_t w = 0, n = mirror_.keys.size();
+    for (size_t r = 0; r < n; ++r) {
+      if (!mirror_.live[r]) continue;
+      if (w != r) {
+        mirror_.keys[w] = mirror_.keys[r];
+        mirror_.seqs[w] = mirror_.seqs[r];
+        for (auto& col : mirror_.cols) col.ids[w] = col.ids[r];
+        docs_.find(*mirror_.keys[w])->second.mrow = (uint32_t)w;
+      }
+      ++w;
+    }
+    mirror_.keys.resize(w);
+    mirror_.seqs.resize(w);
+    for (auto& col : mirror_.cols) col.ids.resize(w);
+    mirror_.live.assign(w, 1);
+    mirror_.live_rows = w;
+    mirror_.kills.clear();
+    ++mirror_.gen;
+    ++mirror_.compactions;
   }
 
   // ----------------------------------------------------------- secondary indexes
@@ -616,6 +897,7 @@ class DocStore {
   uint64_t stats_indexed_queries_ = 0;
   uint64_t stats_scan_queries_ = 0;
   size_t index_threshold_;
+  ColumnMirror mirror_;
 };
 
 }  // namespace tt

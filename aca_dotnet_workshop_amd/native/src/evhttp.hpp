@@ -300,9 +300,22 @@ class MsgParser {
         case CHUNK_SIZE: {
           size_t e = buf.find("\r\n", off);
           if (e == std::string::npos) return buf.size() - off > 1024 ? fail("bad chunk header") : NEED_MORE;
-          remaining_ = std::strtoull(buf.c_str() + off, nullptr, 16);
+          // chunk-size = 1*HEXDIG [ ";" ext ]: parse by hand so an over-long size cannot
+          // saturate/wrap and a line without digits is not read as the last chunk
+          size_t p = off, digits = 0, size = 0;
+          for (; p < e; ++p, ++digits) {
+            char c = buf[p];
+            int v = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10
+                  : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+            if (v < 0) break;
+            if (size > (kMaxBody >> 4)) return fail("body too large");  // next shift would exceed the cap
+            size = (size << 4) | (size_t)v;
+          }
+          if (!digits) return fail("bad chunk header");
+          if (p < e && buf[p] != ';' && buf[p] != ' ' && buf[p] != '\t') return fail("bad chunk header");
           off = e + 2;
-          if (msg_.body.size() + remaining_ > kMaxBody) return fail("body too large");
+          if (size > kMaxBody - msg_.body.size()) return fail("body too large");
+          remaining_ = size;
           st_ = remaining_ ? CHUNK_DATA : TRAILERS;
           break;
         }
@@ -317,6 +330,7 @@ class MsgParser {
         }
         case CHUNK_CRLF:
           if (buf.size() - off < 2) return NEED_MORE;
+          if (buf[off] != '\r' || buf[off + 1] != '\n') return fail("bad chunk terminator");
           off += 2;
           st_ = CHUNK_SIZE;
           break;

@@ -136,6 +136,53 @@ PYBIND11_MODULE(_ttnative, m) {
              return py::make_tuple(py::make_tuple(py::bytes(e.key_blob), offs), seqs, cols);
            },
            py::arg("prefix"), py::arg("paths"))
+      .def("mirror_enable", &DocStore::mirror_enable, py::arg("paths"), py::call_guard<py::gil_scoped_release>())
+      .def("mirror_delta",
+           [](DocStore& s, uint64_t gen, size_t from, size_t kill_from, const std::vector<size_t>& dict_sizes) {
+             MirrorDelta d;
+             {
+               py::gil_scoped_release r;
+               d = s.mirror_delta(gen, from, kill_from, dict_sizes);
+             }
+             auto arr = [](const auto& v) {
+               using T = typename std::decay_t<decltype(v)>::value_type;
+               py::array_t<T> a((py::ssize_t)v.size());
+               if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+               return a;
+             };
+             py::list cols;
+             for (size_t c = 0; c < d.paths.size(); ++c)
+               cols.append(py::make_tuple(d.paths[c], d.dict_from[c], py::cast(d.new_values[c]), arr(d.ids[c])));
+             py::dict out;
+             out["gen"] = d.gen;
+             out["on"] = d.on;
+             out["disabled"] = d.disabled;
+             out["full"] = d.full;
+             out["n"] = d.n;
+             out["from"] = d.from;
+             out["kill_cursor"] = d.kill_cursor;
+             out["kills"] = arr(d.kills);
+             out["seqs"] = arr(d.seqs);
+             out["live"] = arr(d.live);
+             out["columns"] = cols;
+             return out;
+           },
+           py::arg("gen"), py::arg("from_row"), py::arg("kill_from"), py::arg("dict_sizes"))
+      .def("mirror_results",
+           [](DocStore& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> rows,
+              const std::string& prefix, const std::string& token) {
+             size_t skipped = 0;
+             std::string out;
+             const int32_t* p = rows.data();
+             size_t n = (size_t)rows.size();
+             {
+               py::gil_scoped_release r;
+               out = s.mirror_results(p, n, prefix, token, &skipped);
+             }
+             return py::make_tuple(py::bytes(out), skipped);
+           },
+           py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "")
+      .def("mirror_stats", &DocStore::mirror_stats)
       .def("size", &DocStore::size)
       .def("__len__", &DocStore::size)
       .def("compact", &DocStore::compact)
@@ -240,7 +287,6 @@ PYBIND11_MODULE(_ttnative, m) {
            py::keep_alive<1, 5>())
       .def("attach_broker", [](BackingFront& f, const std::string& ns, Broker& b) { f.attach_broker(ns, &b); },
            py::keep_alive<1, 3>())
-      .def("set_mirrored", &BackingFront::set_mirrored, py::call_guard<py::gil_scoped_release>())
       .def("set_policy", &BackingFront::set_policy, py::arg("mode"), py::arg("keys"), py::arg("grants"))
       .def("notify", &BackingFront::notify)
       .def("stats", &BackingFront::stats)

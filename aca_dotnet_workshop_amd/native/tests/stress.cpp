@@ -158,7 +158,7 @@ int main(int argc, char** argv) {
 
   // ---------------------------------------------------------------- backing front
   // HTTP clients on several threads against the native front's loop thread while the
-  // "Python" thread reconfigures it (policy, attach, mirrored hand-over, notify).
+  // "Python" thread reconfigures it (policy, notify) and builds / reads the column mirror.
   {
     DocStore store;
     Broker broker;
@@ -203,7 +203,13 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 200; ++i) {
       front.set_policy(i % 2 ? "open" : "open", {{"cosmos/a", "key"}}, {{"p", "cosmos/a", {"cosmos.read"}}});
       front.notify("ns", "t/subscriptions/s");
-      if (i == 150) front.set_mirrored("a", "d", "c");  // later writes go to the (missing) fallback -> 503
+      // the columnar mirror is built and read while the front's threads keep writing natively
+      if (i == 50) store.mirror_enable({"v"});
+      if (i > 50) {
+        MirrorDelta d = store.mirror_delta(i % 7 ? 0 : 2, 0, 0, {});
+        int32_t rows[2] = {0, (int32_t)(d.n ? d.n - 1 : 0)};
+        store.mirror_results(rows, 2, "", "");
+      }
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     for (auto& th : ts) th.join();

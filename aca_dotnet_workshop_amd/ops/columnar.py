@@ -280,6 +280,8 @@ class ColumnarIndex:
         self._row_of: dict[str, int] | None = {}
         self.docs: list[Any] | None = []  # None when columns come from `source` (bulk-encoded)
         self.source = None  # callable(paths) -> (keys, seqs, [(values_json, ids)]) for re-encoding
+        self.native = None  # DocStore whose column mirror feeds this index (from_native)
+        self._dead = 0      # tombstoned rows since the last compaction (upsert/delete path)
         self.n = 0
         self.version = 0
         self._dev = None  # device mirror state
@@ -336,6 +338,68 @@ class ColumnarIndex:
         self._full_dirty = True
         self._tomb_dirty = False
 
+    # -- native mirror (DocStore column mirror, native/src/docstore.hpp) ---------------
+    @classmethod
+    def from_native(cls, store, paths: Iterable[str]) -> "ColumnarIndex":
+        """Index fed by the document store's own column mirror: the store appends a row per
+        write in C++ (the native HTTP front never hands writes to Python), and ``sync`` pulls
+        only what changed since the last sync (new rows, new dictionary values, killed rows).
+        Rows map back to documents through ``store.mirror_results``."""
+        ix = cls()
+        ix.native = store
+        ix.docs = None
+        ix._ncur = (0, 0, 0)  # (generation, rows seen, kill-log position)
+        ix._remap: list[np.ndarray] = []
+        if not store.mirror_enable(list(dict.fromkeys(paths))):
+            raise Unsupported("collection cannot be mirrored (TTL writes)")
+        ix.sync()
+        return ix
+
+    def sync(self) -> bool:
+        """Apply the native mirror's changes; returns True when anything changed."""
+        gen, rows, kc = self._ncur
+        d = self.native.mirror_delta(gen, rows, kc, [r.size for r in self._remap])
+        if d["disabled"] or not d["on"]:
+            raise Unsupported("collection mirror disabled (TTL writes)")
+        lo, hi = int(d["from"]), int(d["n"])
+        changed = d["full"] or hi > lo or d["kills"].size > 0
+        if d["full"]:
+            self.columns, self.col_of, self._remap = [], {}, []
+            for path, _, _, _ in d["columns"]:
+                self.col_of[path] = len(self.columns)
+                self.columns.append(Column(path))
+                self._remap.append(np.zeros(0, dtype=np.int32))
+            self.cap = max(TILE, (hi + TILE - 1) // TILE * TILE)
+            self.ids = np.full((len(self.columns), self.cap), -1, dtype=np.int32)
+            self.live = np.zeros(self.cap, dtype=np.int32)
+            self.seq = np.zeros(self.cap, dtype=np.int64)
+            self.n, self._next_seq = 0, 0
+            self._dict_gen += 1
+            self._full_dirty = True
+            self.keys = []
+        assert lo == self.n, (lo, self.n)
+        self._grow(hi)
+        for c, (path, dict_from, values, ids) in enumerate(d["columns"]):
+            col = self.columns[c]
+            if values:  # new dictionary values, mapped onto Python's equality (vkey)
+                add = np.fromiter((col.encode(json.loads(t)) for t in values), dtype=np.int32, count=len(values))
+                self._remap[c] = np.concatenate([self._remap[c][:dict_from], add])
+            rm = self._remap[c]
+            if hi > lo:
+                self.ids[c, lo:hi] = np.where(ids >= 0, rm[np.maximum(ids, 0)] if rm.size else -1, -1)
+        if hi > lo:
+            self.seq[lo:hi] = d["seqs"]
+            self.live[lo:hi] = d["live"]
+            self._next_seq = max(self._next_seq, int(d["seqs"].max()))
+        if d["kills"].size:
+            self.live[d["kills"].astype(np.int64)] = 0
+            self._tomb_dirty = True
+        self.n = hi
+        self._ncur = (int(d["gen"]), hi, int(d["kill_cursor"]))
+        if changed:
+            self.version += 1
+        return bool(changed)
+
     @property
     def row_of(self) -> dict[str, int]:
         if self._row_of is None:
@@ -347,7 +411,11 @@ class ColumnarIndex:
         missing = [p for p in dict.fromkeys(paths) if p not in self.col_of]
         if not missing:
             return
-        if self.docs is None:
+        if getattr(self, "native", None) is not None:
+            if not self.native.mirror_enable([c.path for c in self.columns] + missing):
+                raise Unsupported("collection mirror disabled (TTL writes)")
+            self.sync()  # a new column is a new mirror generation: full reload
+        elif self.docs is None:
             self._load([c.path for c in self.columns] + missing)
         else:
             for p in missing:
@@ -395,6 +463,7 @@ class ColumnarIndex:
             if self.docs is not None:
                 self.docs[old] = None
             self._tomb_dirty = True
+            self._dead += 1
             seq = int(self.seq[old])  # an update keeps the key's original position (native engine semantics)
         else:
             self._next_seq += 1
@@ -411,6 +480,7 @@ class ColumnarIndex:
         self.row_of[key] = r
         self.n += 1
         self.version += 1
+        self._maybe_compact()
 
     def delete(self, key: str) -> None:
         r = self.row_of.pop(key, None)
@@ -419,7 +489,14 @@ class ColumnarIndex:
             if self.docs is not None:
                 self.docs[r] = None
             self._tomb_dirty = True
+            self._dead += 1
             self.version += 1
+        self._maybe_compact()
+
+    def _maybe_compact(self) -> None:
+        """Keep the index proportional to the live documents, not to the number of writes."""
+        if self._dead > TILE and self._dead * 2 > self.n:
+            self.compact()
 
     def bulk_load(self, items: Iterable[tuple[str, Any]]) -> None:
         for k, d in items:
@@ -441,6 +518,7 @@ class ColumnarIndex:
             self.docs = [self.docs[i] for i in keep]
         self._row_of = {k: i for i, k in enumerate(self.keys)}
         self.n = len(keep)
+        self._dead = 0
         self.version += 1
         self._full_dirty = True
 
@@ -819,6 +897,11 @@ class ColumnarIndex:
 
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""
+        rows, token = self.query_rows(q, kernels)
+        return [self.keys[i] for i in rows.tolist()], token
+
+    def query_rows(self, q: dict[str, Any], kernels=None) -> tuple[np.ndarray, str | None]:
+        """(rows in result order for the requested page, continuation token)."""
         sort = q.get("sort")
         # every referenced column first: one re-encode (source-backed) and one device upload
         self.ensure_columns(filter_paths(q.get("filter")) + [s["key"] for s in sort or []
@@ -836,7 +919,7 @@ class ColumnarIndex:
                 end = min(total, offset + limit) if limit else total
                 sel = ordered[offset:end].cpu().numpy()
                 token = str(end) if limit and end < total else None
-                return [self.keys[i] for i in sel.tolist()], token
+                return sel.astype(np.int32, copy=False), token
             rows = dev_rows.cpu().numpy()
         if rows is None:
             rows = self.select_numpy(prog)
@@ -844,4 +927,4 @@ class ColumnarIndex:
         end = min(rows.size, offset + limit) if limit else rows.size
         sel = rows[offset:end]
         token = str(end) if limit and end < rows.size else None
-        return [self.keys[i] for i in sel.tolist()], token
+        return sel.astype(np.int32, copy=False), token

@@ -108,7 +108,15 @@ class Ingress:
                     out = [(k, x) for k, v in resp.headers.items() if k not in _HOP
                            for x in (v if isinstance(v, list) else [v])]
                     return Response(resp.body, resp.status, out)
-                except (ConnectionRefusedError, FileNotFoundError, ConnectionClosed, OSError) as e:
+                except (ConnectionRefusedError, FileNotFoundError) as e:
+                    last = e  # nothing was delivered: any method may go to the next replica
+                    continue
+                except (ConnectionClosed, OSError) as e:
+                    # the replica may already have acted on the request: replaying a
+                    # non-idempotent one (createTask) on another replica would duplicate it
+                    if req.method not in _IDEMPOTENT:
+                        r.failures += 1
+                        return problem(502, detail=f"{r.app} replica failed mid-request: {e!r}")
                     last = e
                     continue
             r.failures += 1
@@ -129,6 +137,9 @@ class Ingress:
             if s is not None:
                 await s.close(1.0)
         await self.http.close()
+
+
+_IDEMPOTENT = frozenset(("GET", "HEAD", "OPTIONS", "PUT", "DELETE"))
 
 
 def now_ms() -> int:

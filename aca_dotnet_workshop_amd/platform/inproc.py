@@ -156,17 +156,18 @@ def _clone(c: Component) -> Component:
 
 
 def tasks_tracker_specs(api_backend: str = "store", processor: dict[str, Any] | None = None,
-                        frontend: bool = True, processor_replicas: int = 1) -> list[AppSpec]:
+                        frontend: bool = True, processor_replicas: int = 1,
+                        api: dict[str, Any] | None = None) -> list[AppSpec]:
     """The reference topology: Backend API + Processor (+ Frontend)."""
     from ..services.backend_api.app import create_app as api_factory
     from ..services.backend_api.managers import FakeTasksManager, TasksStoreManager
     from ..services.processor.app import create_app as proc_factory
 
-    def api(config, client):
-        mgr = TasksStoreManager(client) if api_backend == "store" else FakeTasksManager()
+    def api_app(config, client):
+        mgr = TasksStoreManager.from_config(client, config) if api_backend == "store" else FakeTasksManager()
         return api_factory(config=config, manager=mgr)
 
-    specs = [AppSpec("tasksmanager-backend-api", api),
+    specs = [AppSpec("tasksmanager-backend-api", api_app, dict(api or {})),
              AppSpec("tasksmanager-backend-processor", proc_factory, dict(processor or {}), processor_replicas)]
     if frontend:
         from ..services.frontend.app import create_app as fe_factory

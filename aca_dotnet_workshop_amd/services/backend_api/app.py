@@ -93,10 +93,12 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
         return empty(200) if ok else empty(404)
 
     # -- OverdueTasksController (reference Controllers/OverdueTasksController.cs) --
-    @app.route("/api/overduetasks", ("GET",), name="GetOverdueTasks", tag="OverdueTasks",
+    @app.route("/api/overduetasks", ("GET",), name="GetOverdueTasks", tag="OverdueTasks", query=["limit"],
                responses={200: [TaskModel]})
     async def get_overdue(req: Request) -> Response:
-        return _json(tasks_to_json(await manager.get_yesterdays_due_tasks()))
+        raw = req.query_get("limit") or ""
+        limit = int(raw) if raw.isdigit() else None  # page size of the range sweep (OverdueTasks:Query=range)
+        return _json(tasks_to_json(await manager.get_yesterdays_due_tasks(limit)))
 
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",
                body=[TaskModel], responses={200: None})
@@ -115,10 +117,7 @@ def select_manager(config) -> TasksManager:
     if backend == "fake":
         return FakeTasksManager()
     if backend == "store":
-        return TasksStoreManager(client_from_config(config),
-                                 store=config.get_str("TasksManager:StateStoreName", "statestore"),
-                                 pubsub=config.get_str("TasksManager:PubSubName", "dapr-pubsub-servicebus"),
-                                 topic=config.get_str("TasksManager:TopicName", "tasksavedtopic"))
+        return TasksStoreManager.from_config(client_from_config(config), config)
     raise ValueError(f"unknown TasksManager:Backend {backend!r}")
 
 

@@ -63,7 +63,7 @@ class TasksManager(abc.ABC):
     async def mark_overdue_tasks(self, tasks: list[TaskModel]) -> None: ...
 
     @abc.abstractmethod
-    async def get_yesterdays_due_tasks(self) -> list[TaskModel]: ...
+    async def get_yesterdays_due_tasks(self, limit: int | None = None) -> list[TaskModel]: ...
 
 
 def _created_key(t: TaskModel) -> datetime:
@@ -127,7 +127,7 @@ class FakeTasksManager(TasksManager):
             if t is not None:
                 t.is_over_due = True
 
-    async def get_yesterdays_due_tasks(self) -> list[TaskModel]:
+    async def get_yesterdays_due_tasks(self, limit: int | None = None) -> list[TaskModel]:
         y = (today() - timedelta(days=1)).date()
         return sorted((t for t in self._tasks if naive_utc(t.task_due_date).date() == y
                        and not t.is_completed and not t.is_over_due), key=_created_key)
@@ -141,12 +141,26 @@ class TasksStoreManager(TasksManager):
     """Sidecar-backed manager; ``client`` is the ``DaprClient`` equivalent."""
 
     def __init__(self, client: SidecarClient, store: str = STORE_NAME, pubsub: str = PUBSUB_NAME,
-                 topic: str = TOPIC_NAME, max_retries: int = 5) -> None:
+                 topic: str = TOPIC_NAME, max_retries: int = 5, overdue_query: str = "equality",
+                 overdue_page: int = 1000) -> None:
         self.client = client
         self.store = store
         self.pubsub = pubsub
         self.topic = topic
         self.max_retries = max_retries
+        if overdue_query not in ("equality", "range"):
+            raise ValueError(f"OverdueTasks:Query must be 'equality' or 'range', not {overdue_query!r}")
+        self.overdue_query = overdue_query
+        self.overdue_page = overdue_page
+
+    @classmethod
+    def from_config(cls, client: SidecarClient, config) -> "TasksStoreManager":
+        """``TasksManager:*`` names and the ``OverdueTasks:*`` sweep settings from configuration."""
+        return cls(client, store=config.get_str("TasksManager:StateStoreName", STORE_NAME),
+                   pubsub=config.get_str("TasksManager:PubSubName", PUBSUB_NAME),
+                   topic=config.get_str("TasksManager:TopicName", TOPIC_NAME),
+                   overdue_query=(config.get_str("OverdueTasks:Query") or "equality").lower(),
+                   overdue_page=config.get_int("OverdueTasks:PageSize", 1000))
 
     async def create_new_task(self, task_name, created_by, assigned_to, due_date) -> uuid.UUID:
         t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
@@ -220,7 +234,9 @@ class TasksStoreManager(TasksManager):
             await self._publish_task_saved(after)
         return True
 
-    async def get_yesterdays_due_tasks(self) -> list[TaskModel]:
+    async def get_yesterdays_due_tasks(self, limit: int | None = None) -> list[TaskModel]:
+        if self.overdue_query == "range":
+            return await self._open_tasks_due_before_today(limit)
         yesterday = today() - timedelta(days=1)
         json_date = format_fixed(yesterday, "yyyy-MM-ddTHH:mm:ss")
         log.info("Getting overdue tasks for yesterday date: '%s'", json_date)
@@ -230,6 +246,21 @@ class TasksStoreManager(TasksManager):
         tasks = [t for t in tasks if not t.is_completed and not t.is_over_due]
         tasks.sort(key=_created_key)
         return tasks
+
+    async def _open_tasks_due_before_today(self, limit: int | None) -> list[TaskModel]:
+        """``OverdueTasks:Query=range`` (SURVEY.md §2.12 #7 fixed): every open task due before
+        today, whatever its time of day and however many daily runs were missed, filtered by
+        the store rather than in the app -- a range leaf plus two boolean leaves, which the
+        backing planner runs as a gfx950 columnar scan.  One page (oldest first) per call: the
+        processor marks a page overdue and asks again, and marked tasks drop out of the filter."""
+        midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
+        page = limit if limit and limit > 0 else self.overdue_page
+        log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
+        q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
+                                {"EQ": {"isOverDue": False}}]},
+             "page": {"limit": page}}
+        resp = await self.client.query_state(self.store, q)
+        return [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
 
     async def mark_overdue_tasks(self, tasks) -> None:
         items = []

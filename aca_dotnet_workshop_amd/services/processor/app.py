@@ -20,7 +20,10 @@ Endpoints (reference SURVEY.md §2.2, §2.11):
   header), so the archive and the store agree.
 * ``POST /ScheduledTasksManager`` -- cron handler (reference
   Controllers/ScheduledTasksManagerController.cs:19-46): fetch yesterday's open tasks,
-  keep those with ``runAt.Date > dueDate.Date``, mark them overdue.
+  keep those with ``runAt.Date > dueDate.Date``, mark them overdue.  With
+  ``OverdueTasks:PageSize`` > 0 it sweeps page by page (``GET /api/overduetasks?limit=``)
+  until a short page: the API's ``OverdueTasks:Query=range`` mode answers with every open
+  task due before today, filtered in the store (GPU columnar scan in the backing services).
 * ``GET /dapr/subscribe`` -- ``MapSubscribeHandler`` (reference Program.cs:33).
 """
 from __future__ import annotations
@@ -124,14 +127,27 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
     async def check_overdue_tasks_job(req: Request) -> Response:
         run_at = utcnow()
         log_sched.info("ScheduledTasksManager::Timer Services triggered at: %s", run_at)
-        tasks = tasks_from_json(await client.invoke_method("GET", api_app_id, "api/overduetasks"))
-        log_sched.info("ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d",
-                       len(tasks))
-        overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
-        if overdue:
-            log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", len(overdue))
-            await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", overdue)
-        return json_response({"runAt": run_at.isoformat(), "retrieved": len(tasks), "markedOverdue": len(overdue)})
+        # OverdueTasks:PageSize > 0 (with the API's OverdueTasks:Query=range): sweep page by page
+        # -- a marked page drops out of the API's filter, so each request asks for the next one
+        page = cfg.get_int("OverdueTasks:PageSize", 0)
+        max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
+        retrieved = marked = pages = 0
+        while pages < max_pages:
+            pages += 1
+            path = "api/overduetasks" + (f"?limit={page}" if page > 0 else "")
+            tasks = tasks_from_json(await client.invoke_method("GET", api_app_id, path))
+            retrieved += len(tasks)
+            log_sched.info("ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d",
+                           len(tasks))
+            overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
+            if overdue:
+                log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", len(overdue))
+                await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", overdue)
+                marked += len(overdue)
+            if page <= 0 or len(tasks) < page or not overdue:
+                break
+        return json_response({"runAt": run_at.isoformat(), "retrieved": retrieved, "markedOverdue": marked,
+                              "pages": pages})
 
 
 def create_app(argv: list[str] | None = None, client: SidecarClient | None = None, config=None,

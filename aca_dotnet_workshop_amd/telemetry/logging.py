@@ -4,15 +4,29 @@ Every record carries the role name and, when inside a request, the W3C trace/spa
 logs join traces (App Insights "Transaction Search").  Levels follow the reference's
 ``Logging:LogLevel`` section (``Default: Information``, ``Microsoft.AspNetCore: Warning``,
 reference Backend.Api/appsettings.json:2-8).  Records are also appended as JSON lines to
-``$TT_TELEMETRY_DIR/logs-<role>-<pid>.jsonl`` when the platform provides a telemetry dir.
+``$TT_TELEMETRY_DIR/logs-<role>-<pid>.jsonl`` when the platform provides a telemetry dir
+(the Log Analytics workspace of the environment); ``TT_LOG_CONSOLE=0`` keeps them off the
+console (the platform then ships only the JSON stream).
+
+Hot path.  The reference logs three Information lines per created task
+(TasksStoreManager.cs:34,153; TasksNotifierController.cs:27).  The standard ``logging``
+pipeline costs ~20 us per record here (LogRecord construction, caller lookup, handler
+locks, a flush per line), so loggers are switched to ``FastLogger``: while only this
+module's sinks are installed, ``info()`` & co. format the line directly (JSON via the C
+string encoder) into a buffered sink flushed every ``FLUSH_S`` / 64 KiB -- the equivalent of
+.NET's source-generated ``LoggerMessage`` + batched console/OTLP exporters.  Any foreign
+handler (pytest's ``caplog``, a user's handler), ``exc_info`` or ``extra`` takes the
+standard path, so behaviour is unchanged for them.
 """
 from __future__ import annotations
 
-import json
+import atexit
 import logging
 import os
 import sys
+import threading
 import time
+from json.encoder import encode_basestring
 from typing import Any
 
 from .tracing import current_span
@@ -20,6 +34,10 @@ from .tracing import current_span
 _LEVELS = {"trace": 5, "debug": logging.DEBUG, "information": logging.INFO, "info": logging.INFO,
            "warning": logging.WARNING, "warn": logging.WARNING, "error": logging.ERROR,
            "critical": logging.CRITICAL, "none": logging.CRITICAL + 10}
+# .NET level names in the JSON stream (Log Analytics "SeverityLevel" vocabulary)
+_NET_LEVEL = {logging.DEBUG: "Debug", logging.INFO: "Information", logging.WARNING: "Warning",
+              logging.ERROR: "Error", logging.CRITICAL: "Critical", 5: "Trace"}
+FLUSH_S = 0.2
 
 
 class _Ctx(logging.Filter):
@@ -35,16 +53,24 @@ class _Ctx(logging.Filter):
         return True
 
 
+def json_line(ts: float, level: int, role_json: str, category: str, message: str, trace_id: str = "",
+              span_id: str = "", exception: str | None = None) -> str:
+    out = ('{"ts":%.6f,"level":"%s","role":%s,"category":%s,"message":%s'
+           % (ts, _NET_LEVEL.get(level, logging.getLevelName(level)), role_json, encode_basestring(category),
+              encode_basestring(message)))
+    if trace_id:
+        out += ',"traceId":"%s","spanId":"%s"' % (trace_id, span_id)
+    if exception:
+        out += ',"exception":' + encode_basestring(exception)
+    return out + "}\n"
+
+
 class JsonFormatter(logging.Formatter):
     def format(self, record: logging.LogRecord) -> str:
-        rec: dict[str, Any] = {"ts": round(record.created, 6), "level": record.levelname, "role": getattr(record, "role", ""),
-                               "category": record.name, "message": record.getMessage()}
-        if getattr(record, "trace_id", ""):
-            rec["traceId"] = record.trace_id
-            rec["spanId"] = record.span_id
-        if record.exc_info:
-            rec["exception"] = self.formatException(record.exc_info)
-        return json.dumps(rec, separators=(",", ":"))
+        exc = self.formatException(record.exc_info) if record.exc_info else None
+        return json_line(record.created, record.levelno, encode_basestring(getattr(record, "role", "")), record.name,
+                         record.getMessage(), getattr(record, "trace_id", ""), getattr(record, "span_id", ""),
+                         exc)[:-1]
 
 
 class ConsoleFormatter(logging.Formatter):
@@ -56,11 +82,168 @@ class ConsoleFormatter(logging.Formatter):
         return base
 
 
+class BufferedSink(logging.Handler):
+    """Line sink with batched writes (``FLUSH_S`` / 64 KiB, and at exit).  Also a regular
+    ``logging.Handler`` for records that take the standard path."""
+
+    def __init__(self, stream, json_lines: bool, role: str, buffered: bool) -> None:
+        super().__init__()
+        self.stream = stream
+        self.json_lines = json_lines
+        self.role = role
+        self.role_json = encode_basestring(role)
+        self.buffered = buffered
+        self.setFormatter(JsonFormatter() if json_lines else ConsoleFormatter())
+        self._buf: list[str] = []
+        self._size = 0
+        self._mu = threading.Lock()
+        self._sec = -1
+        self._hms = ""
+        self._prefix: dict[tuple[int, str], str] = {}
+        if buffered:
+            _Flusher.add(self)
+
+    # fast path (FastLogger)
+    def write_fast(self, level: int, name: str, message: str, trace_id: str, span_id: str) -> None:
+        now = time.time()
+        if self.json_lines:
+            pre = self._prefix.get((level, name))
+            if pre is None:  # '{"level":..,"role":..,"category":..' per (level, logger)
+                pre = self._prefix[(level, name)] = '{"level":"%s","role":%s,"category":%s' % (
+                    _NET_LEVEL.get(level, logging.getLevelName(level)), self.role_json, encode_basestring(name))
+            if trace_id:
+                line = '%s,"ts":%.6f,"message":%s,"traceId":"%s","spanId":"%s"}\n' % (
+                    pre, now, encode_basestring(message), trace_id, span_id)
+            else:
+                line = '%s,"ts":%.6f,"message":%s}\n' % (pre, now, encode_basestring(message))
+        else:
+            sec = int(now)
+            if sec != self._sec:
+                self._sec, self._hms = sec, time.strftime("%H:%M:%S", time.localtime(now))
+            line = f"{self._hms} {_NET_LEVEL.get(level, 'info')[:4].lower()}: {self.role} {name}: {message}\n"
+        self._put(line)
+
+    def _put(self, line: str) -> None:
+        if not self.buffered:
+            try:
+                self.stream.write(line)
+                self.stream.flush()
+            except (OSError, ValueError):
+                pass
+            return
+        self._buf.append(line)
+        self._size += len(line)
+        if self._size >= 65536:
+            self.flush()
+
+    # standard path
+    def emit(self, record: logging.LogRecord) -> None:
+        try:
+            self._put(self.format(record) + "\n")
+        except Exception:
+            self.handleError(record)
+
+    def flush(self) -> None:
+        if not self._buf:
+            return
+        with self._mu:
+            buf, self._buf, self._size = self._buf, [], 0
+            try:
+                self.stream.write("".join(buf))
+                self.stream.flush()
+            except (OSError, ValueError):
+                pass
+
+    def close(self) -> None:
+        self.flush()
+        _Flusher.remove(self)
+        super().close()
+
+
+class _Flusher:
+    """One daemon thread per process flushing buffered sinks every ``FLUSH_S``."""
+    sinks: list[BufferedSink] = []
+    thread: threading.Thread | None = None
+
+    @classmethod
+    def add(cls, sink: BufferedSink) -> None:
+        cls.sinks.append(sink)
+        if cls.thread is None:
+            cls.thread = threading.Thread(target=cls._run, name="tt-log-flush", daemon=True)
+            cls.thread.start()
+            atexit.register(cls.flush_all)
+
+    @classmethod
+    def remove(cls, sink: BufferedSink) -> None:
+        if sink in cls.sinks:
+            cls.sinks.remove(sink)
+
+    @classmethod
+    def flush_all(cls) -> None:
+        for s in list(cls.sinks):
+            s.flush()
+
+    @classmethod
+    def _run(cls) -> None:
+        while True:
+            time.sleep(FLUSH_S)
+            cls.flush_all()
+
+
+class _State:
+    sinks: tuple[BufferedSink, ...] = ()
+    root_handlers: int = -1  # handler count of the root logger when only our sinks are installed
+
+
+class FastLogger(logging.Logger):
+    """``logging.Logger`` whose level methods bypass ``LogRecord`` while only this module's
+    sinks are installed (see module docstring)."""
+
+    def _fast(self, level: int, msg: Any, args: tuple, kw: dict) -> bool:
+        if kw or self.handlers or len(_root.handlers) != _State.root_handlers or not self.propagate:
+            return False
+        if self.isEnabledFor(level):
+            message = (msg % args) if args else str(msg)
+            s = current_span()
+            tid, sid = (s.trace_id, s.span_id) if s is not None else ("", "")
+            for sink in _State.sinks:
+                if level >= sink.level:
+                    sink.write_fast(level, self.name, message, tid, sid)
+        return True
+
+    def debug(self, msg, *args, **kw):
+        if not self._fast(logging.DEBUG, msg, args, kw):
+            super().debug(msg, *args, **kw)
+
+    def info(self, msg, *args, **kw):
+        if not self._fast(logging.INFO, msg, args, kw):
+            super().info(msg, *args, **kw)
+
+    def warning(self, msg, *args, **kw):
+        if not self._fast(logging.WARNING, msg, args, kw):
+            super().warning(msg, *args, **kw)
+
+    def error(self, msg, *args, **kw):
+        if not self._fast(logging.ERROR, msg, args, kw):
+            super().error(msg, *args, **kw)
+
+
+_root = logging.getLogger()
+
+
+def _adopt_fast_loggers() -> None:
+    logging.setLoggerClass(FastLogger)
+    for lg in list(logging.Logger.manager.loggerDict.values()):
+        if type(lg) is logging.Logger:  # created before us: same layout, switch behaviour
+            lg.__class__ = FastLogger
+
+
 def configure_logging(role: str, config: Any = None, json_console: bool | None = None) -> None:
     root = logging.getLogger()
     for h in list(root.handlers):
         if getattr(h, "_tt", False):
             root.removeHandler(h)
+            h.close()
     ctx = _Ctx(role)
     default = "information"
     if config is not None:
@@ -73,16 +256,24 @@ def configure_logging(role: str, config: Any = None, json_console: bool | None =
                 logging.getLogger(cat).setLevel(_LEVELS.get(str(v).lower(), logging.INFO))
     if json_console is None:
         json_console = os.environ.get("TT_LOG_FORMAT", "console") == "json"
-    h = logging.StreamHandler(sys.stderr)
-    h.setFormatter(JsonFormatter() if json_console else ConsoleFormatter())
-    h.addFilter(ctx)
-    h._tt = True  # type: ignore[attr-defined]
-    root.addHandler(h)
+    sinks: list[BufferedSink] = []
+    if os.environ.get("TT_LOG_CONSOLE", "1") != "0":
+        h = BufferedSink(sys.stderr, json_console, role, buffered=False)
+        sinks.append(h)
     d = os.environ.get("TT_TELEMETRY_DIR")
     if d:
         os.makedirs(d, exist_ok=True)
-        fh = logging.FileHandler(os.path.join(d, f"logs-{role}-{os.getpid()}.jsonl"))
-        fh.setFormatter(JsonFormatter())
-        fh.addFilter(ctx)
-        fh._tt = True  # type: ignore[attr-defined]
-        root.addHandler(fh)
+        fh = open(os.path.join(d, f"logs-{role}-{os.getpid()}.jsonl"), "a", encoding="utf-8")
+        sinks.append(BufferedSink(fh, True, role, buffered=True))
+    for h in sinks:
+        h.addFilter(ctx)
+        h._tt = True  # type: ignore[attr-defined]
+        root.addHandler(h)
+    _State.sinks = tuple(sinks)
+    # fast path only while the root logger's handlers are exactly these sinks
+    _State.root_handlers = len(root.handlers) if all(getattr(h, "_tt", False) for h in root.handlers) else -1
+    _adopt_fast_loggers()
+
+
+def flush_logs() -> None:
+    _Flusher.flush_all()

@@ -111,7 +111,8 @@ class _Conn(asyncio.Protocol):
             if self.is_head or status in (204, 304):
                 length: Any = 0
             elif "chunked" in headers.get("transfer-encoding", "").lower():
-                length = "chunked"
+                from .server import _ChunkedDecoder
+                length = _ChunkedDecoder()
             elif "content-length" in headers:
                 length = int(headers["content-length"])
             else:
@@ -121,13 +122,10 @@ class _Conn(asyncio.Protocol):
         keep = headers.get("connection", "").lower() != "close"
         if length is None:
             return
-        if length == "chunked":
-            from .server import _decode_chunked, _Incomplete
-            try:
-                body, used = _decode_chunked(buf)
-            except _Incomplete:
+        if not isinstance(length, int):  # chunked
+            body = length.feed(buf)
+            if body is None:
                 return
-            del buf[:used]
         else:
             if len(buf) < length:
                 return

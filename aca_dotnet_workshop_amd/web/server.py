@@ -59,35 +59,64 @@ parse_head = _native_parser()
 MAX_BODY_BYTES = 256 * 1024 * 1024
 
 
-class _Incomplete(Exception):
-    pass
+class _ChunkedDecoder:
+    """Incremental ``Transfer-Encoding: chunked`` decoder: consumes what it can from the front
+    of the connection buffer on each call (linear in the body size), enforces
+    ``MAX_BODY_BYTES`` on the decoded size and rejects malformed size lines."""
 
+    __slots__ = ("body", "need", "state")
 
-def _decode_chunked(buf: bytearray) -> tuple[bytes, int]:
-    """Return (body, consumed) or raise _Incomplete."""
-    pos = 0
-    out = bytearray()
-    n = len(buf)
-    while True:
-        eol = buf.find(b"\r\n", pos)
-        if eol < 0:
-            raise _Incomplete
-        size_s = bytes(buf[pos:eol]).split(b";")[0].strip()
-        size = int(size_s, 16)
-        pos = eol + 2
-        if size == 0:
-            # trailers until empty line
+    def __init__(self) -> None:
+        self.body = bytearray()
+        self.need = 0        # bytes left in the current chunk
+        self.state = 0       # 0 size line, 1 data, 2 CRLF after data, 3 trailers
+
+    def feed(self, buf: bytearray) -> bytes | None:
+        """Decode from ``buf`` (consumed bytes are deleted); the body when complete, else None."""
+        pos = 0
+        try:
             while True:
-                eol = buf.find(b"\r\n", pos)
-                if eol < 0:
-                    raise _Incomplete
-                if eol == pos:
-                    return bytes(out), eol + 2
-                pos = eol + 2
-        if pos + size + 2 > n:
-            raise _Incomplete
-        out += buf[pos:pos + size]
-        pos += size + 2
+                if self.state == 0:
+                    eol = buf.find(b"\r\n", pos)
+                    if eol < 0:
+                        if len(buf) - pos > 1024:
+                            raise ValueError("bad chunk header")
+                        return None
+                    size_s = bytes(buf[pos:eol]).split(b";")[0].strip()
+                    if not size_s or len(size_s) > 16 or any(c not in b"0123456789abcdefABCDEF" for c in size_s):
+                        raise ValueError("bad chunk header")
+                    size = int(size_s, 16)
+                    if size > MAX_BODY_BYTES - len(self.body):
+                        raise ValueError("body too large")
+                    pos = eol + 2
+                    self.need, self.state = size, (1 if size else 3)
+                elif self.state == 1:
+                    take = min(self.need, len(buf) - pos)
+                    self.body += buf[pos:pos + take]
+                    pos += take
+                    self.need -= take
+                    if self.need:
+                        return None
+                    self.state = 2
+                elif self.state == 2:
+                    if len(buf) - pos < 2:
+                        return None
+                    if buf[pos:pos + 2] != b"\r\n":
+                        raise ValueError("bad chunk terminator")
+                    pos += 2
+                    self.state = 0
+                else:  # trailers until the empty line
+                    eol = buf.find(b"\r\n", pos)
+                    if eol < 0:
+                        if len(buf) - pos > MAX_HEADER_BYTES:
+                            raise ValueError("trailers too large")
+                        return None
+                    done = eol == pos
+                    pos = eol + 2
+                    if done:
+                        return bytes(self.body)
+        finally:
+            del buf[:pos]
 
 
 class HttpServerProtocol(asyncio.Protocol):
@@ -147,20 +176,18 @@ class HttpServerProtocol(asyncio.Protocol):
                     continue  # stray CRLF between pipelined requests
                 method, target, version, hd = parse_head(head)
                 headers = Headers(hd)
-                chunked = "chunked" in headers.get("transfer-encoding", "").lower()
+                chunked = _ChunkedDecoder() if "chunked" in headers.get("transfer-encoding", "").lower() else None
                 length = 0 if chunked else int(headers.get("content-length", "0") or 0)
-                if length > MAX_BODY_BYTES:
+                if length < 0 or length > MAX_BODY_BYTES:
                     raise ValueError("body too large")
                 if headers.get("expect", "").lower() == "100-continue" and self.transport is not None:
                     self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
                 self.pending = (method, target, version, headers, length, chunked)
             method, target, version, headers, length, chunked = self.pending
             if chunked:
-                try:
-                    body, used = _decode_chunked(buf)
-                except _Incomplete:
+                body = chunked.feed(buf)
+                if body is None:
                     return
-                del buf[:used]
             else:
                 if len(buf) < length:
                     return

@@ -37,9 +37,10 @@ from aca_dotnet_workshop_amd.parallel import Dist, cgroup_throttling, cpu_budget
 def parse() -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024, help="createTask requests per step per rank")
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8192,
+                    help="createTask requests per step per rank (the step quantum: 20 steps >= 3 s timed)")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="requests in flight per rank (0 = 48 per API replica, at most 384)")
     ap.add_argument("--api-replicas", type=int, default=0,
@@ -47,7 +48,14 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--processor-replicas", type=int, default=0,
                     help="competing consumers on the subscription (0 = size to this rank's CPU share)")
     ap.add_argument("--split-backing", type=int, default=1, help="separate messaging (Service Bus/Storage) process")
-    ap.add_argument("--log-level", default="Warning", help="service log level (reference default: Information)")
+    ap.add_argument("--log-level", default="Information",
+                    help="service log level (reference default: Information, appsettings.json); records go as "
+                         "structured JSON to the environment's telemetry dir (Log Analytics equivalent)")
+    ap.add_argument("--overdue-sweep-ms", type=int, default=1000,
+                    help="mixed load: trigger the processor's overdue cron job every N ms during the run "
+                         "(OverdueTasks:Query=range -> GPU columnar scan in the backing services); 0 = off")
+    ap.add_argument("--past-due-every", type=int, default=64,
+                    help="every Nth createTask body is due yesterday, so the sweeps mark real tasks overdue")
     ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "native"),
                     help="services' HTTP I/O: python (asyncio) | native (apphost.hpp) | api=native,processor=python")
     ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
@@ -120,10 +128,82 @@ async def run_steps(socks: list[str], counts_url: str, entity: str, steps: int, 
     return dt
 
 
-def _bodies(batch: int) -> list[bytes]:
+def _bodies(batch: int, past_due_every: int = 0) -> list[bytes]:
+    from datetime import timedelta
+
+    from aca_dotnet_workshop_amd.models import format_fixed, today
+    yesterday = format_fixed(today() - timedelta(days=1))
     return [json.dumps({"taskName": f"bench task {i}", "taskCreatedBy": f"user{i % 97}@bench.local",
-                        "taskDueDate": "2030-01-01T00:00:00", "taskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
+                        "taskDueDate": yesterday if past_due_every and i % past_due_every == 0 else "2030-01-01T00:00:00",
+                        "taskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
             for i in range(batch)]
+
+
+class OverdueSweeper:
+    """Mixed load: fires the processor's overdue cron job (the reference's ScheduledTasksManager
+    binding, normally daily) every ``period_s`` while createTask load runs, through the
+    processor's sidecar exactly as the cron binding does -> API ``GET /api/overduetasks?limit=``
+    -> range query -> backing planner -> gfx950 columnar scan; then ``markoverdue`` bulk saves."""
+
+    def __init__(self, proc_sidecar_uds: str, period_s: float) -> None:
+        import threading
+        self.url = (f"unix:{proc_sidecar_uds}:/v1.0/invoke/tasksmanager-backend-processor/method/"
+                    "ScheduledTasksManager")
+        self.period_s = period_s
+        self.stop_ev = threading.Event()
+        self.runs: list[tuple[float, dict]] = []
+        self.errors: list[str] = []
+        self.thread = threading.Thread(target=self._run, name="overdue-sweeper", daemon=True)
+
+    def start(self) -> None:
+        self.thread.start()
+
+    def stop(self) -> None:
+        self.stop_ev.set()
+        self.thread.join(timeout=120)
+
+    def _run(self) -> None:
+        asyncio.run(self._loop())
+
+    async def _loop(self) -> None:
+        from aca_dotnet_workshop_amd.web.client import HttpClient
+        c = HttpClient()
+        try:
+            while not self.stop_ev.is_set():
+                t = time.perf_counter()
+                try:
+                    r = await c.post(self.url, body=b"{}", headers={"Content-Type": "application/json"}, timeout=60)
+                    if r.status == 200:
+                        self.runs.append((time.perf_counter() - t, r.json()))
+                    else:
+                        self.errors.append(f"{r.status} {r.body[:200]!r}")
+                except Exception as e:  # recorded, reported in the bench line
+                    self.errors.append(repr(e))
+                left = self.period_s - (time.perf_counter() - t)
+                if left > 0:
+                    await asyncio.get_running_loop().run_in_executor(None, self.stop_ev.wait, left)
+        finally:
+            await c.close()
+
+    def summary(self) -> dict:
+        ms = sorted(d * 1e3 for d, _ in self.runs)
+        return {"sweeps": len(self.runs), "errors": len(self.errors),
+                "sweep_p50_ms": round(ms[len(ms) // 2], 2) if ms else None,
+                "sweep_max_ms": round(ms[-1], 2) if ms else None,
+                "tasks_marked_overdue": sum(r.get("markedOverdue", 0) for _, r in self.runs),
+                "pages": sum(r.get("pages", 0) for _, r in self.runs),
+                "first_error": self.errors[0] if self.errors else None}
+
+
+def _collection_stats(backing: str) -> dict:
+    import urllib.request
+    url = f"{backing}/cosmos/taskstracker-state-store/tasksmanagerdb/taskscollection/stats"
+    req = urllib.request.Request(url, headers={"x-tt-identity": "bench"})
+    try:
+        with urllib.request.urlopen(req, timeout=30) as r:
+            return json.loads(r.read())
+    except Exception as e:
+        return {"error": repr(e)}
 
 
 def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: int, conc: int,
@@ -158,17 +238,29 @@ def main() -> None:
     for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
         b()
     cfg = {"Logging:LogLevel:Default": a.log_level, "TasksNotifier:Mode": "log"}
-    stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01"),
-                            **rank_device_env()})
+    api_cfg, proc_cfg = dict(cfg), dict(cfg)
+    sweep = a.overdue_sweep_ms > 0
+    if sweep:
+        api_cfg["OverdueTasks:Query"] = "range"
+        proc_cfg["OverdueTasks:PageSize"] = "1000"
+    import tempfile
+    root = tempfile.mkdtemp(prefix="tt-bench-")
+    env = {"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01"),
+           # logs as structured JSON into the environment's telemetry dir (Log Analytics), not the console
+           "TT_TELEMETRY_DIR": os.path.join(root, "telemetry"), "TT_LOG_CONSOLE": "0", **rank_device_env()}
+    if sweep:  # the task collection's column mirror is maintained from its first write
+        env["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue"
+    stack = LocalStack(root=root, env=env)
+    sweeper = None
     try:
-        backing = stack.start_backing()
+        backing = doc_backing = stack.start_backing()
         if a.split_backing:
             backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
         for _ in range(a.api_replicas):
-            stack.start_replica("tasksmanager-backend-api", cfg, grpc=a.api_protocol == "grpc",
+            stack.start_replica("tasksmanager-backend-api", api_cfg, grpc=a.api_protocol == "grpc",
                                 extra_env={"TT_APP_HOST": app_host("api", a.app_host)})
         for _ in range(a.processor_replicas):
-            stack.start_replica("tasksmanager-backend-processor", cfg, grpc=a.api_protocol == "grpc",
+            stack.start_replica("tasksmanager-backend-processor", proc_cfg, grpc=a.api_protocol == "grpc",
                                 extra_env={"TT_APP_HOST": app_host("processor", a.app_host)})
         stack.wait_ready()
         socks = [r.sidecar_uds for r in stack.replicas["tasksmanager-backend-api"]]
@@ -179,12 +271,15 @@ def main() -> None:
             exe = str(build_loadgen())
             bodies_file = str(stack.root / "bodies.jsonl")
             with open(bodies_file, "wb") as f:
-                f.write(b"\n".join(_bodies(a.batch)) + b"\n")
+                f.write(b"\n".join(_bodies(a.batch, a.past_due_every if sweep else 0)) + b"\n")
         if a.warmup:
             if a.client == "native":
                 run_loadgen(exe, socks, counts_url, a.warmup, a.batch, a.concurrency, bodies_file)
             else:
                 asyncio.run(run_steps(socks, counts_url, entity, a.warmup, a.batch, a.concurrency, None))
+        if sweep:
+            sweeper = OverdueSweeper(stack.replicas["tasksmanager-backend-processor"][0].sidecar_uds,
+                                     a.overdue_sweep_ms / 1000.0)
         lat: list[float] = []
         d.barrier()
         device_sync()
@@ -195,12 +290,16 @@ def main() -> None:
         t = me.cpu_times()
         cpu0["bench-client"] = t.user + t.system + t.children_user + t.children_system
         report = None
+        if sweeper is not None:
+            sweeper.start()
         if a.client == "native":
             dt, report = run_loadgen(exe, socks, counts_url, a.steps, a.batch, a.concurrency, bodies_file)
         else:
             dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
         device_sync()
         d.barrier()
+        if sweeper is not None:
+            sweeper.stop()
         cpu1 = stack.cpu_seconds()
         thr1 = cgroup_throttling()
         t = me.cpu_times()
@@ -220,6 +319,14 @@ def main() -> None:
         else:
             p50 = d.max(lat[len(lat) // 2] * 1e3) if lat else 0.0
             p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0
+        sweep_info = None
+        if sweeper is not None:
+            acc = _collection_stats(doc_backing).get("accelerator", {})
+            sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
+                          "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
+                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows")}
+            if d.rank == 0:
+                print(json.dumps({"overdue_sweeps": sweep_info}), file=sys.stderr, flush=True)
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         if d.rank == 0:
@@ -236,11 +343,20 @@ def main() -> None:
                            "sidecar_api_protocol": a.api_protocol,
                            "app_host": a.app_host,
                            "create_latency_p50_ms": round(p50, 3),
-                           "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput"}}),
+                           "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput",
+                           "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
+                           "timed_region_s": round(dt_max, 3), "log_level": a.log_level,
+                           "log_sink": "structured JSON lines in the environment telemetry dir",
+                           "overdue_sweeps": sweep_info}}),
                 flush=True)
     finally:
+        if sweeper is not None and sweeper.thread.is_alive():
+            sweeper.stop()
         stack.stop()
         d.close()
+        if not os.environ.get("TT_BENCH_KEEP"):
+            import shutil
+            shutil.rmtree(root, ignore_errors=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 """Backing-services parity between the Python handlers and the native HTTP front
 (native/src/backingfront.hpp): document CRUD with ETags, publish / long-poll receive /
-settle / counts, RBAC decisions, non-UTF-8 bodies, and the hand-over of a collection's writes
-to the Python path once the columnar query accelerator mirrors it."""
+settle / counts, RBAC decisions, non-UTF-8 bodies, and collections mirrored by the columnar
+query accelerator keeping their writes on the native front."""
 import asyncio
 import time
 
@@ -150,8 +150,10 @@ def test_rbac(front, monkeypatch):
     run(main())
 
 
-def test_accelerator_handover(monkeypatch):
-    """Writes through the native front before the columnar index exists, through Python after."""
+def test_accelerator_keeps_writes_native(monkeypatch):
+    """Once the columnar accelerator mirrors a collection its writes still go through the
+    native front: the DocStore appends mirror rows itself, and queries see every write
+    (updates, deletes, TTL writes turning the accelerator off) made through either front."""
     monkeypatch.setenv("TT_QUERY_ACCEL", "cpu")
     monkeypatch.setenv("TT_QUERY_ACCEL_MIN_DOCS", "10")
 
@@ -161,12 +163,25 @@ def test_accelerator_handover(monkeypatch):
             for i in range(40):
                 await c.doc_put("acct", "db", "c", f"k{i}", '{"n": %d}' % i)
             q = b'{"filter": {"GT": {"n": 30}}}'
-            assert (await c.doc_query("acct", "db", "c", q)).count(b'"key"') == 9  # builds the index
+            assert (await c.doc_query("acct", "db", "c", q)).count(b'"key"') == 9  # builds the mirror
+            puts0 = (await c.http.get(b.base + "/admin/front")).json()["requests"]["doc.put"]
             for i in range(40, 60):
                 await c.doc_put("acct", "db", "c", f"k{i}", '{"n": %d}' % i)
+            await c.doc_put("acct", "db", "c", "k31", '{"n": 1}')  # update drops out of the range
             await c.doc_delete("acct", "db", "c", "k35")
-            assert (await c.doc_query("acct", "db", "c", q)).count(b'"key"') == 28
+            await c.doc_bulk_set("acct", "db", "c", [{"key": "k2", "value": '{"n": 99}', "etag": None,
+                                                      "firstWrite": False, "ttlMs": 0}])
+            fs = (await c.http.get(b.base + "/admin/front")).json()
+            assert fs["requests"]["doc.put"] - puts0 == 21  # still served natively
+            res = await c.doc_query("acct", "db", "c", q)
+            assert res.count(b'"key"') == 28 and b'"k31"' not in res and b'"k2"' in res
             st = (await c.doc_stats("acct", "db", "c"))["accelerator"]
-            assert st["cpu"] == 2 and st["rows"] == 59
+            assert st["cpu"] == 2 and st["rows"] == 59 and st["mirror"]["on"] == 1
+            # a TTL write turns the mirror off; the native engine answers from then on
+            await c.doc_put("acct", "db", "c", "t1", '{"n": 77}', ttl_ms=60000)
+            res = await c.doc_query("acct", "db", "c", q)
+            assert res.count(b'"key"') == 29
+            st = (await c.doc_stats("acct", "db", "c"))["accelerator"]
+            assert st["cpu"] == 2 and st["mirror"]["disabled"] == 1
             await c.http.close()
     run(main())

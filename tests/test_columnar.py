@@ -511,3 +511,85 @@ def test_gpu_pair_sort_matches_argsort(n):
                 assert want == ix.query(q), (n, sort, page)
     finally:
         k.pair_sort = True
+
+
+@settings(max_examples=150, deadline=None)
+@given(docs_st, filters_st, sort_st, st.integers(0, 1000))
+def test_native_mirror_index_matches_native(docs, flt, sort, seed):
+    """ColumnarIndex.from_native (the DocStore's own column mirror, deltas pulled by ``sync``)
+    answers like the native engine, with writes made only to the store before and after the
+    mirror exists and a late column (new mirror generation)."""
+    if not docs:
+        return
+    rnd = random.Random(seed)
+    ops = _ops(docs, rnd)
+    store = N.DocStore()
+    for k, d in ops[: len(ops) // 2]:
+        store.delete(k) if d is None else store.set(k, json.dumps(d))
+    ix = ColumnarIndex.from_native(store, ["f"])
+    for k, d in ops[len(ops) // 2:]:  # the store mirrors these itself
+        store.delete(k) if d is None else store.set(k, json.dumps(d))
+    ix.sync()
+    q = {"filter": flt}
+    if sort:
+        q["sort"] = sort
+    want = json.loads(store.query(json.dumps(q)))["results"]
+    rows, _ = ix.query_rows(q)  # may add columns -> new generation, full reload
+    got = json.loads(store.mirror_results(rows, "", "")[0])["results"]
+    assert got == want
+
+
+def test_native_mirror_compacts_and_tracks_updates():
+    """Updates append rows and kill the old ones; the store compacts its mirror once dead rows
+    dominate (new generation) and the index reloads -- it stays proportional to live docs."""
+    store = N.DocStore()
+    ix = ColumnarIndex.from_native(store, ["n", "done"])
+    for i in range(20000):
+        store.set(f"k{i}", json.dumps({"n": i % 100, "done": False}))
+    q = {"filter": {"AND": [{"LT": {"n": 10}}, {"EQ": {"done": False}}]}, "page": {"limit": 50}}
+    ix.sync()
+    rows, tok = ix.query_rows(q)
+    assert len(rows) == 50 and tok == "50"
+    for rnd in range(4):  # rewrite everything 4x: 100k row appends
+        for i in range(20000):
+            store.set(f"k{i}", json.dumps({"n": i % 100, "done": i % 3 == rnd % 3}))
+        ix.sync()
+        st_ = store.mirror_stats()
+        assert st_["live_rows"] == 20000
+        assert st_["rows"] <= 2 * 20000 + 65536
+        full = dict(q, page={})
+        want = [r["key"] for r in json.loads(store.query(json.dumps(full)))["results"]]
+        rows, _ = ix.query_rows(full)
+        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "")[0])["results"]]
+        assert got == want
+    assert store.mirror_stats()["compactions"] >= 1
+    assert ix.n <= 2 * 20000 + 65536
+
+
+@pytest.mark.gpu
+def test_gpu_native_mirror_matches_native():
+    """The GPU path over a native-mirror index (incremental device sync of appended rows and
+    killed rows) equals the native engine after interleaved writes."""
+    k = _kernels()
+    rnd = random.Random(11)
+    store = N.DocStore()
+    for i in range(30000):
+        store.set(f"k{i}", json.dumps({"d": f"2024-05-{rnd.randrange(1, 29):02d}T00:00:00",
+                                       "c": rnd.random() < 0.3, "o": False}))
+    ix = ColumnarIndex.from_native(store, ["d", "c", "o"])
+    q = {"filter": {"AND": [{"LT": {"d": "2024-05-15T00:00:00"}}, {"EQ": {"c": False}}, {"EQ": {"o": False}}]},
+         "sort": [{"key": "d"}]}
+    for round_ in range(5):
+        ix.sync()
+        rows, _ = ix.query_rows(q, k)
+        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "")[0])["results"]]
+        want = [r["key"] for r in json.loads(store.query(json.dumps(q)))["results"]]
+        assert got == want, round_
+        for _ in range(3000):  # mark some overdue, complete some, add new due dates, delete some
+            i = rnd.randrange(40000)
+            r = rnd.random()
+            if r < 0.1:
+                store.delete(f"k{i}")
+            else:
+                store.set(f"k{i}", json.dumps({"d": f"2024-0{rnd.randrange(4, 7)}-{rnd.randrange(1, 29):02d}T00:00:00",
+                                               "c": r < 0.4, "o": r > 0.8}))

@@ -412,7 +412,13 @@ def test_native_http_parser_survives_garbage(tmp_path):
                b"POST /v1.0/state/statestore HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\nabc\r\n0\r\n\r\n",
                b"GET /" + b"a" * 70000 + b" HTTP/1.1\r\n\r\n", b"GET / HTTP/1.1\r\nNoColonHeader\r\n\r\n",
                b"POST /v1.0/state/statestore HTTP/1.1\r\nContent-Length: 3\r\n\r\n[{]",
-               b"POST /v1.0/publish/bus/t HTTP/1.1\r\nContent-Type: application/json\r\nContent-Length: 4\r\n\r\n\xff\xfe{]"]
+               b"POST /v1.0/publish/bus/t HTTP/1.1\r\nContent-Type: application/json\r\nContent-Length: 4\r\n\r\n\xff\xfe{]",
+               # 1-byte chunk, then a size that would saturate strtoull (and wrap the body cap)
+               b"POST /v1.0/state/statestore HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n1\r\n[\r\n"
+               b"FFFFFFFFFFFFFFFFF\r\n" + b"x" * 4096,
+               # a size line without digits is not the last chunk
+               b"POST /v1.0/state/statestore HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n;ext\r\n\r\n",
+               b"POST /v1.0/state/statestore HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabcXY0\r\n\r\n"]
     for _ in range(40):
         samples.append(bytes(rnd.randrange(256) for _ in range(rnd.randrange(1, 300))) + b"\r\n\r\n")
 

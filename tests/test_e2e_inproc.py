@@ -258,3 +258,70 @@ def test_trace_propagates_through_sidecars_and_pubsub():
         finally:
             await env.stop()
     run(main())
+
+
+def _fast_cron(schedule="@every 200ms"):
+    return from_dict({"apiVersion": "dapr.io/v1alpha1", "kind": "Component", "metadata": {"name": "FastCron"},
+                      "spec": {"type": "bindings.cron", "version": "v1", "metadata": [
+                          {"name": "schedule", "value": schedule}, {"name": "route", "value": "/ScheduledTasksManager"},
+                          {"name": "singleReplica", "value": "true"}]},
+                      "scopes": [PROC]})
+
+
+def _task_doc(i, due, done=False, overdue=False):
+    tid = f"00000000-0000-4000-8000-{i:012d}"
+    return f"{API}||{tid}", (
+        '{"taskId":"%s","taskName":"seed %d","taskCreatedBy":"seed%d@x","taskCreatedOn":"2024-01-01T00:00:00",'
+        '"taskDueDate":"%s","taskAssignedTo":"a@x","isCompleted":%s,"isOverDue":%s}'
+        % (tid, i, i % 97, due, "true" if done else "false", "true" if overdue else "false"))
+
+
+async def _range_sweep_env(monkeypatch, accel, page):
+    monkeypatch.setenv("TT_QUERY_ACCEL", accel)
+    monkeypatch.setenv("TT_QUERY_ACCEL_MIN_DOCS", "50")
+    env = InProcessEnvironment(extra_components=[_fast_cron()])
+    await env.start_backing()
+    for s in tasks_tracker_specs(frontend=False, api={"OverdueTasks:Query": "range"},
+                                 processor={"OverdueTasks:PageSize": page}):
+        await env.add_app(s)
+    await env.wait_ready()
+    return env
+
+
+def test_cron_range_sweep_marks_every_past_due_task(monkeypatch):
+    """OverdueTasks:Query=range + paged cron sweep (SURVEY §2.12 #7 fixed): tasks due before
+    today -- at any time of day, any number of days back -- are marked overdue page by page by
+    the cron job through API -> sidecar -> backing, where the filter runs on the columnar
+    accelerator (CPU executor here, gfx950 kernels in the GPU test); completed and future tasks
+    stay untouched, and tasks created after the mirror exists are swept too."""
+    async def main():
+        env = await _range_sweep_env(monkeypatch, "cpu", 7)
+        try:
+            st = env.backing.store("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
+            past = [format_fixed(today() - timedelta(days=d, hours=-h)) for d in (1, 2, 30) for h in (0, 13)]
+            fut = format_fixed(today() + timedelta(days=2))
+            want = set()
+            for i in range(120):
+                k, v = _task_doc(i, past[i % len(past)] if i % 3 else fut, done=i % 10 == 1)
+                st.set(k, v)
+                if i % 3 and i % 10 != 1:
+                    want.add(k.split("||")[1])
+            c = env.replicas[PROC][0].client
+
+            async def swept():
+                res = json.loads(st.query(json.dumps({"filter": {"EQ": {"isOverDue": True}}})))["results"]
+                out = {r["data"]["taskId"] for r in res}
+                return out if out == want else None
+            await _until(swept, timeout=15)
+            # a task created through the API afterwards (mirror already built) is swept as well
+            r = await c.invoke_method_raw("POST", API, "api/tasks", {"taskName": "late", "taskCreatedBy": "n@x",
+                                                                      "taskDueDate": past[-1], "taskAssignedTo": "a@x"})
+            tid = r.headers["location"].rsplit("/", 1)[1]
+            want.add(tid)
+            await _until(swept, timeout=15)
+            assert await c.invoke_method("GET", API, "api/overduetasks?limit=5") == []
+            acc = env.backing.accel("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
+            assert acc.stats["cpu"] >= 2 and acc.stats["fallback"] == 0
+        finally:
+            await env.stop()
+    run(main())
