@@ -2,6 +2,7 @@
 platform's provisioning step and tests)."""
 from __future__ import annotations
 
+import asyncio
 import json
 import os
 from typing import Any
@@ -37,6 +38,7 @@ class BackingClient:
         self.identity = identity if identity is not None else os.environ.get("TT_IDENTITY")
         self.key = key
         self.http = http or HttpClient()
+        self.throttled_retries = 0
 
     def _h(self, extra: dict[str, str] | None = None, key: str | None = None) -> list[tuple[str, str]]:
         h = []
@@ -49,9 +51,24 @@ class BackingClient:
             h.extend(extra.items())
         return h
 
+    # throttled (429) answers are retried after the store's hint, like the Cosmos SDK behind
+    # Dapr's state.azure.cosmosdb: at most THROTTLE_RETRIES times / THROTTLE_MAX_WAIT_S in total
+    THROTTLE_RETRIES = 9
+    THROTTLE_MAX_WAIT_S = 30.0
+
     async def _req(self, method: str, path: str, body: bytes | None = None, headers: dict[str, str] | None = None,
                    ok: tuple[int, ...] = (200, 201, 202, 204), what: str = "", timeout: float | None = None) -> ClientResponse:
-        r = await self.http.request(method, self.base + path, headers=self._h(headers), body=body, timeout=timeout)
+        waited = 0.0
+        for attempt in range(self.THROTTLE_RETRIES + 1):
+            r = await self.http.request(method, self.base + path, headers=self._h(headers), body=body, timeout=timeout)
+            if r.status != 429 or attempt == self.THROTTLE_RETRIES:
+                break
+            delay = min(max(float(r.headers.get("x-ms-retry-after-ms") or 100) / 1000.0, 0.001), 5.0)
+            if waited + delay > self.THROTTLE_MAX_WAIT_S:
+                break
+            waited += delay
+            self.throttled_retries += 1
+            await asyncio.sleep(delay)
         if r.status == 412 or r.status == 409:
             raise EtagConflict(r.status, r.body, what or path)
         if r.status not in ok:
@@ -109,6 +126,12 @@ class BackingClient:
 
     async def doc_stats(self, account: str, db: str, coll: str) -> dict[str, Any]:
         return (await self._req("GET", f"{self._coll(account, db, coll)}/stats")).json()
+
+    async def doc_set_throughput(self, account: str, db: str, coll: str, ru_per_s: float) -> dict[str, Any]:
+        """Provision a container's RU/s (0 = unlimited)."""
+        return (await self._req("PUT", f"{self._coll(account, db, coll)}/throughput",
+                                json.dumps({"ruPerSecond": ru_per_s}).encode(),
+                                {"Content-Type": "application/json"})).json()
 
     # -- service bus ----------------------------------------------------------
     async def sb_create_topic(self, ns: str, topic: str) -> None:

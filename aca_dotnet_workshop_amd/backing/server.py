@@ -221,8 +221,19 @@ class BackingServices:
             p = req.path_params
             return self.accel(p["account"], p["db"], p["coll"])
 
+        def throttled(s, ru: float) -> Response | None:
+            """Provisioned-throughput admission (DocStore.charge, shared with the native front)."""
+            wait_ms = s.charge(ru)
+            if not wait_ms:
+                return None
+            r = problem(429, detail="Request rate is large: the container's provisioned throughput is exhausted")
+            r.headers += [("x-ms-retry-after-ms", str(wait_ms)), ("Retry-After", str((wait_ms + 999) // 1000))]
+            return r
+
         async def put_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
+            if (t := throttled(s, s.write_ru(len(req.body)))) is not None:
+                return t
             etag = req.headers.get("if-match") or None
             value = req.body.decode("utf-8")
             ttl = int(req.headers.get("x-tt-ttl-ms", "0") or 0)
@@ -236,6 +247,8 @@ class BackingServices:
 
         async def get_doc(req: Request) -> Response:
             s = st(req, "cosmos.read")
+            if (t := throttled(s, s.read_ru(0))) is not None:
+                return t
             r = s.get(req.path_params["key"])
             if r is None:
                 return empty(404)
@@ -243,6 +256,8 @@ class BackingServices:
 
         async def del_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
+            if (t := throttled(s, s.write_ru(0))) is not None:
+                return t
             try:
                 ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
             except self.N.EtagMismatch as ex:
@@ -251,16 +266,22 @@ class BackingServices:
 
         async def bulk_get(req: Request) -> Response:
             s = st(req, "cosmos.read")
+            keys = (req.json() or {}).get("keys", [])
+            if (t := throttled(s, s.read_ru(0) * max(1, len(keys)))) is not None:
+                return t
             out = []
-            for k in (req.json() or {}).get("keys", []):
+            for k in keys:
                 r = s.get(k)
                 out.append({"key": k, "data": json.loads(r[0]), "etag": r[1]} if r else {"key": k})
             return json_response(out)
 
         async def bulk_set(req: Request) -> Response:
             s = st(req, "cosmos.write")
+            items = req.json() or []
+            if (t := throttled(s, sum(s.write_ru(len(str(it.get("value", "")))) for it in items) or 1)) is not None:
+                return t
             out = []
-            for it in req.json() or []:
+            for it in items:
                 try:
                     value = it["value"] if isinstance(it["value"], str) else json.dumps(it["value"])
                     ttl = int(it.get("ttlMs") or 0)
@@ -284,14 +305,19 @@ class BackingServices:
                 q = json.loads(raw)
                 text = a.query(q, prefix, s) if isinstance(q, dict) else None
                 return s.query(raw, prefix) if text is None else text
+            if (t := throttled(s, s.query_ru(0))) is not None:
+                return t
             try:
                 text = await asyncio.get_running_loop().run_in_executor(self.query_pool, run)
             except ValueError as ex:
                 return problem(400, detail=str(ex))
+            s.charge(s.query_ru(len(text)) - s.query_ru(0))  # result size part: charged after the fact
             return Response(text.encode(), 200, None, "application/json")
 
         async def transaction(req: Request) -> Response:
             s = st(req, "cosmos.write")
+            if (t := throttled(s, s.write_ru(len(req.body)))) is not None:
+                return t
             ops = []
             for o in (req.json() or {}).get("ops", []):
                 is_del = o.get("op") == "delete"
@@ -310,6 +336,7 @@ class BackingServices:
             s = st(req, "cosmos.read")
             d = dict(s.stats())
             d["indexedPaths"] = s.indexed_paths()
+            d["throughput"] = dict(s.throughput_stats())
             a = acc(req)
             d["accelerator"] = {"mode": a.mode, "rows": a.index.live_rows() if a.index else 0, **a.stats,
                                 "mirror": dict(s.mirror_stats())}
@@ -326,7 +353,16 @@ class BackingServices:
         app.add_route(base + "/bulkset", bulk_set, ("POST",))
         app.add_route(base + "/query", query, ("POST",))
         app.add_route(base + "/transaction", transaction, ("POST",))
+        async def set_throughput(req: Request) -> Response:
+            """Provision the container's RU/s (Bicep ``autoscaleSettings.maxThroughput`` /
+            ``options.throughput``; 0 = unlimited)."""
+            s = st(req, "cosmos.write")
+            body = req.json() or {}
+            s.set_throughput(float(body.get("ruPerSecond") or 0))
+            return json_response(dict(s.throughput_stats()))
+
         app.add_route(base + "/stats", stats, ("GET",))
+        app.add_route(base + "/throughput", set_throughput, ("PUT",))
         app.add_route(base + "/keys", keys, ("GET",))
 
     # ---------------------------------------------------------------- service bus

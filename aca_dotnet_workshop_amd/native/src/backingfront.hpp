@@ -317,6 +317,19 @@ class BackingFront {
     });
   }
 
+  // Provisioned-throughput admission (DocStore::charge): 429 + x-ms-retry-after-ms when the
+  // container's RU/s budget is spent, as Cosmos answers; the sidecars retry after the hint.
+  bool throttled(ev::Reply& r, DocStore* s, double ru) {
+    int64_t wait_ms = s->charge(ru);
+    if (!wait_ms) return false;
+    count("doc.throttled");
+    r.send(429, {{"x-ms-retry-after-ms", std::to_string(wait_ms)},
+                 {"retry-after", std::to_string((wait_ms + 999) / 1000)},
+                 {"content-type", "application/problem+json; charset=utf-8"}},
+           bf::problem_json(429, "Request rate is large: the container's provisioned throughput is exhausted"));
+    return true;
+  }
+
   // -- cosmos documents ----------------------------------------------------------------------
   bool handle_doc(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
     Coll* c = nullptr;
@@ -331,6 +344,7 @@ class BackingFront {
     if (m.method == "GET") {
       if (!authorize(m, r, "cosmos.read", scope)) return true;
       count("doc.get");
+      if (throttled(r, c->store, DocStore::read_ru(0))) return true;
       auto v = c->store->get(key);
       if (!v) r.empty(404);
       else r.send(200, {{"etag", v->second}, {"content-type", "application/json"}}, v->first);
@@ -344,6 +358,7 @@ class BackingFront {
     std::optional<std::string> etag;
     if (im && !im->empty()) etag = *im;
     const char* pj = "application/problem+json; charset=utf-8";
+    if (throttled(r, c->store, DocStore::write_ru(m.method == "PUT" ? m.body.size() : 0))) return true;
     if (m.method == "PUT") {
       count("doc.put");
       auto* fw = m.header("x-tt-first-write");
@@ -391,6 +406,12 @@ class BackingFront {
     }
     if (!authorize(m, r, "cosmos.write", "cosmos/" + seg[1])) return true;
     count("doc.bulkset");
+    double ru = 0;
+    for (auto& it : items.items) {
+      const Value* v = it.get("value");
+      ru += DocStore::write_ru(v ? (v->t == Value::String ? v->s.size() : dump(*v).size()) : 4);
+    }
+    if (throttled(r, c->store, ru)) return true;
     std::string out = "[";
     bool etag_err = false, other_err = false;
     for (size_t i = 0; i < items.items.size(); ++i) {

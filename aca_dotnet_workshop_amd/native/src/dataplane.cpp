@@ -211,7 +211,8 @@ class Tracer {
       std::string safe = role_;
       for (auto& c : safe)
         if (c == '/') c = '_';
-      path_ = dir_ + "/spans-" + safe + "-" + std::to_string(getpid()) + ".jsonl";
+      stem_ = dir_ + "/spans-" + safe + "-" + std::to_string(getpid()) + "-";
+      path_ = stem_;  // non-empty: tracing on; the file is per UTC day (log retention prunes days)
     }
   }
   SpanCtx start(const std::string* traceparent) {
@@ -245,7 +246,16 @@ class Tracer {
   }
   void flush() {
     if (buf_.empty() || path_.empty()) return;
-    if (FILE* f = std::fopen(path_.c_str(), "a")) {
+    std::string path = path_;
+    if (!stem_.empty()) {
+      time_t t = time(nullptr);
+      struct tm g;
+      gmtime_r(&t, &g);
+      char day[16];
+      std::strftime(day, sizeof day, "%Y%m%d", &g);
+      path = stem_ + day + ".jsonl";
+    }
+    if (FILE* f = std::fopen(path.c_str(), "a")) {
       std::fwrite(buf_.data(), 1, buf_.size(), f);
       std::fclose(f);
     }
@@ -253,7 +263,7 @@ class Tracer {
   }
 
  private:
-  std::string dir_, path_, role_ = "sidecar", instance_;
+  std::string dir_, path_, stem_, role_ = "sidecar", instance_;
   double rate_ = 1.0;
   bool flush_each_ = false;
   std::string buf_;
@@ -1083,6 +1093,49 @@ class DataPlane {
     return true;
   }
 
+  // Requests to the state store retry throttled answers (429, provisioned RU/s exhausted) after
+  // the store's x-ms-retry-after-ms, like the Cosmos SDK under Dapr's state.azure.cosmosdb:
+  // at most 9 retries and 30 s of accumulated waiting, then the 429 is the caller's.
+  struct StoreCall {
+    Endpoint ep;
+    std::string method, target, body;
+    HeaderList headers;
+    ev::ClientCallback cb;
+    int attempt = 0;
+    double waited = 0.0;
+  };
+
+  void store_request(const Endpoint& ep, std::string method, std::string target, HeaderList h, std::string body,
+                     ev::ClientCallback cb) {
+    auto c = std::make_shared<StoreCall>();
+    c->ep = ep;
+    c->method = std::move(method);
+    c->target = std::move(target);
+    c->headers = std::move(h);
+    c->body = std::move(body);
+    c->cb = std::move(cb);
+    store_send(std::move(c));
+  }
+
+  void store_send(std::shared_ptr<StoreCall> c) {
+    StoreCall& k = *c;
+    client_.request(k.ep, k.method, k.target, k.headers, k.body, 60, [this, c](ClientResult&& res) {
+      if (!res.err && res.resp.status == 429 && c->attempt < 9) {
+        const std::string* ra = res.resp.header("x-ms-retry-after-ms");
+        double delay = ra ? std::strtod(ra->c_str(), nullptr) / 1000.0 : 0.1;
+        delay = std::min(std::max(delay, 0.001), 5.0);
+        if (c->waited + delay <= 30.0) {
+          count("state.throttled_retry", 429);
+          c->attempt++;
+          c->waited += delay;
+          loop_.call_later(delay, [this, c] { store_send(c); });
+          return;
+        }
+      }
+      c->cb(std::move(res));
+    });
+  }
+
   void state_save(Message&& m, Reply&& r, const std::string& name, const Store& s, const std::string& path) {
     auto d = begin(m, std::move(r), "state.save", path);
     std::vector<Item> items;
@@ -1115,8 +1168,8 @@ class DataPlane {
       if (!it.etag.empty()) h.emplace_back("if-match", it.etag);
       if (it.first_write) h.emplace_back("x-tt-first-write", "1");
       if (it.ttl_ms) h.emplace_back("x-tt-ttl-ms", std::to_string(it.ttl_ms));
-      client_.request(s.backing, "PUT", s.coll_path + "/docs/" + quote_all(full_key(s, it.key)), h, it.value, 60,
-                      std::move(done));
+      store_request(s.backing, "PUT", s.coll_path + "/docs/" + quote_all(full_key(s, it.key)), h, it.value,
+                    std::move(done));
       return;
     }
     std::string body = "[";
@@ -1128,7 +1181,7 @@ class DataPlane {
               ",\"firstWrite\":" + (it.first_write ? "true" : "false") + ",\"ttlMs\":" + std::to_string(it.ttl_ms) + "}";
     }
     body += "]";
-    client_.request(s.backing, "POST", s.coll_path + "/bulkset", h, body, 60, std::move(done));
+    store_request(s.backing, "POST", s.coll_path + "/bulkset", h, std::move(body), std::move(done));
   }
 
   static std::string full_key(const Store& s, const std::string& key) {
@@ -1138,7 +1191,7 @@ class DataPlane {
 
   void state_get(Message&& m, Reply&& r, const Store& s, const std::string& key, const std::string& path) {
     auto d = begin(m, std::move(r), "state.get", path);
-    client_.request(s.backing, "GET", s.coll_path + "/docs/" + quote_all(full_key(s, key)), s.auth, {}, 60,
+    store_request(s.backing, "GET", s.coll_path + "/docs/" + quote_all(full_key(s, key)), s.auth, {},
                     [d](ClientResult&& res) {
                       if (res.err || (res.resp.status != 200 && res.resp.status != 404)) {
                         d->error(500, "ERR_STATE_GET", "state get: " + (res.err ? errno_text(res.err)
@@ -1163,7 +1216,7 @@ class DataPlane {
     if (!s.prefix.empty()) target += "?prefix=" + quote_all(s.prefix);
     HeaderList h = s.auth;
     h.emplace_back("content-type", "application/json");
-    client_.request(s.backing, "POST", target, h, m.body.empty() ? std::string("{}") : m.body, 60,
+    store_request(s.backing, "POST", target, h, m.body.empty() ? std::string("{}") : m.body,
                     [d](ClientResult&& res) {
                       if (!res.err && res.resp.status == 200) {
                         d->send(200, {{"content-type", "application/json"}}, res.resp.body);
@@ -1181,7 +1234,7 @@ class DataPlane {
     auto d = begin(m, std::move(r), "state.delete", path);
     HeaderList h = s.auth;
     if (auto* im = m.header("if-match"); im && !im->empty()) h.emplace_back("if-match", *im);
-    client_.request(s.backing, "DELETE", s.coll_path + "/docs/" + quote_all(full_key(s, key)), h, {}, 60,
+    store_request(s.backing, "DELETE", s.coll_path + "/docs/" + quote_all(full_key(s, key)), h, {},
                     [d](ClientResult&& res) {
                       if (!res.err && (res.resp.status == 409 || res.resp.status == 412)) {
                         d->error(409, "ERR_STATE_DELETE", "state delete: HTTP " + std::to_string(res.resp.status) +

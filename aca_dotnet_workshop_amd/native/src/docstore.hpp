@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -454,6 +455,45 @@ class DocStore {
       for (auto& t : ts) t.join();
     }
     return out;
+  }
+
+  // ------------------------------------------------------ provisioned throughput (RU/s)
+  // Cosmos request-unit budget of the container (bicep/modules/cosmos-db.bicep:68-72,
+  // autoscale max 4000 RU/s): a token bucket refilled at `ru_per_s` holding at most one second
+  // of budget.  `charge` admits an operation (returns 0) or says how many milliseconds until
+  // it would be admitted -- the caller answers 429 + x-ms-retry-after-ms and nothing is spent.
+  // 0 RU/s = not provisioned (unlimited).  Costs follow Cosmos' published shape: a point read
+  // is 1 RU per KiB, a write / delete 5 RU per KiB, a query 2.5 RU + 1 RU per KiB returned.
+  static double read_ru(size_t bytes) { return std::max<double>(1.0, std::ceil(bytes / 1024.0)); }
+  static double write_ru(size_t bytes) { return 5.0 * std::max<double>(1.0, std::ceil(bytes / 1024.0)); }
+  static double query_ru(size_t result_bytes) { return 2.5 + std::ceil(result_bytes / 1024.0); }
+
+  void set_throughput(double ru_per_s) {
+    std::lock_guard<std::mutex> g(ru_mu_);
+    ru_rate_ = std::max(0.0, ru_per_s);
+    ru_tokens_ = ru_rate_;
+    ru_last_ = mono_s();
+  }
+
+  int64_t charge(double ru) {
+    std::lock_guard<std::mutex> g(ru_mu_);
+    if (ru_rate_ <= 0) return 0;
+    double now = mono_s();
+    ru_tokens_ = std::min(ru_rate_, ru_tokens_ + (now - ru_last_) * ru_rate_);
+    ru_last_ = now;
+    ru = std::min(ru, ru_rate_);  // a request bigger than a second's budget waits for a full bucket
+    if (ru_tokens_ >= ru) {
+      ru_tokens_ -= ru;
+      ru_consumed_ += ru;
+      return 0;
+    }
+    ++ru_throttled_;
+    return std::max<int64_t>(1, (int64_t)std::ceil((ru - ru_tokens_) / ru_rate_ * 1000.0));
+  }
+
+  std::unordered_map<std::string, double> throughput_stats() {
+    std::lock_guard<std::mutex> g(ru_mu_);
+    return {{"ru_per_s", ru_rate_}, {"ru_consumed", ru_consumed_}, {"throttled", (double)ru_throttled_}};
   }
 
   // ------------------------------------------------------------ column mirror
@@ -898,6 +938,12 @@ class DocStore {
   uint64_t stats_scan_queries_ = 0;
   size_t index_threshold_;
   ColumnMirror mirror_;
+  std::mutex ru_mu_;
+  double ru_rate_ = 0, ru_tokens_ = 0, ru_last_ = 0, ru_consumed_ = 0;
+  uint64_t ru_throttled_ = 0;
+  static double mono_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
 };
 
 }  // namespace tt

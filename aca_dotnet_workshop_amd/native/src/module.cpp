@@ -183,6 +183,12 @@ PYBIND11_MODULE(_ttnative, m) {
            },
            py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "")
       .def("mirror_stats", &DocStore::mirror_stats)
+      .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"))
+      .def("charge", &DocStore::charge, py::arg("ru"))
+      .def("throughput_stats", &DocStore::throughput_stats)
+      .def_static("read_ru", &DocStore::read_ru)
+      .def_static("write_ru", &DocStore::write_ru)
+      .def_static("query_ru", &DocStore::query_ru)
       .def("size", &DocStore::size)
       .def("__len__", &DocStore::size)
       .def("compact", &DocStore::compact)

@@ -35,6 +35,7 @@ from ..web.app import WebApp
 from ..web.http import Request, Response, empty, json_response
 from ..web.server import HttpServer
 from .ingress import Backend, Ingress, IngressRoute
+from .limits import Limits, ResourceLimiter
 from .manifest import Manifest, ManifestError, desired_state, identity_of, template_hash, validate
 from .processes import LocalStack, ReplicaProc
 from .scaler import Autoscaler, ScaleRule, cron_metric
@@ -89,6 +90,10 @@ class EnvironmentController:
                "TT_TRACE_SAMPLE_RATE": str(float(ai.get("samplingPercentage", 100)) / 100.0),
                "TT_LOG_FORMAT": "console"}
         self.stack = LocalStack(self.dir / "runtime", components=[str(self.dir / "components")], env=env)
+        rl = manifest.environment.get("resourceLimits") or {}
+        self.limiter = ResourceLimiter(manifest.name, enforce_memory=_truthy(rl.get("memory", True)),
+                                       enforce_cpu=_truthy(rl.get("cpu", False)))
+        self._oom: set[str] = set()
         self.apps: dict[str, AppRuntime] = {}
         self.backing: BackingClient | None = None
         self.storage_keys: dict[str, str] = {}
@@ -123,6 +128,10 @@ class EnvironmentController:
         for rt in self.apps.values():
             if rt.autoscaler is not None:
                 self._tasks.append(asyncio.ensure_future(self._scale_loop(rt)))
+        self._tasks.append(asyncio.ensure_future(self._retention_loop()))
+        if self.limiter.enforce_cpu and self.limiter.mode == "watchdog":
+            self._tasks.append(asyncio.ensure_future(self._throttle_loop()))
+        self.event("ResourceLimitsApplied", **self.limiter.describe())
         if serve_control:
             await self._serve_control()
         self.event("EnvironmentReady", name=self.m.name, apps=list(self.apps))
@@ -133,6 +142,7 @@ class EnvironmentController:
         for rt in self.apps.values():
             if rt.ingress:
                 await rt.ingress.stop()
+        self.limiter.release_all()
         await asyncio.to_thread(self.stack.stop)
         if self._control is not None:
             await self._control.close(1.0)
@@ -177,6 +187,12 @@ class EnvironmentController:
                 q = {"name": q} if isinstance(q, str) else q
                 await b.sb_create_queue(sb["namespace"], q["name"], int(q.get("lockDurationSeconds", 60)) * 1000,
                                         int(q.get("maxDeliveryCount", 10)))
+        cdb = r.get("cosmosDb")
+        if cdb:  # provisioned throughput: autoscale max (cosmos-db.bicep:68-72) or manual RU/s
+            for d in cdb.get("databases") or []:
+                for c in d.get("containers") or []:
+                    ru = c.get("autoscaleMaxThroughput") or c.get("throughput") or 0
+                    await b.doc_set_throughput(cdb["account"], d["name"], c["name"], float(ru))
         kv = r.get("keyVault")
         if kv:
             for s in kv.get("secrets") or []:
@@ -226,6 +242,7 @@ class EnvironmentController:
                                       grpc=str(dapr.get("apiProtocol", "http")).lower() == "grpc")
         rp.revision = rev.name  # type: ignore[attr-defined]
         rev.replicas.append(rp)
+        self.limiter.add(rp.name, rp.proc.pid, Limits.from_spec(spec))
         self.event("ReplicaStarted", app=rt.name, revision=rev.name, replica=rp.name)
         return rp
 
@@ -262,6 +279,7 @@ class EnvironmentController:
     async def _retire(self, rt: AppRuntime, rev: Revision) -> None:
         self._refresh_backends(rt)
         for rp in list(rev.replicas):
+            self.limiter.remove(rp.name)
             await asyncio.to_thread(self.stack.stop_replica, rp)
         rev.replicas.clear()
         self.event("RevisionDeactivated", app=rt.name, revision=rev.name)
@@ -303,6 +321,7 @@ class EnvironmentController:
             elif n < len(live):
                 for rp in live[n:][::-1]:
                     rev.replicas.remove(rp)
+                    self.limiter.remove(rp.name)
                     await asyncio.to_thread(self.stack.stop_replica, rp)
             rt.desired = n
             rt.scale_events.append({"ts": time.time(), "replicas": n, "reason": reason})
@@ -314,6 +333,11 @@ class EnvironmentController:
         backoff: dict[str, float] = {}
         while True:
             await asyncio.sleep(0.5)
+            for name, used in await asyncio.to_thread(self.limiter.check_memory):
+                self._oom.add(name)
+                st = self.limiter.replicas.get(name)
+                self.event("ReplicaOOMKilled", replica=name, rssBytes=used,
+                           limitBytes=st.limits.memory if st else None)
             if not self.stack.backing_alive():
                 # the managed services' equivalent: restart in place over the durable logs
                 code = self.stack.backing_proc.poll() if self.stack.backing_proc is not None else None
@@ -332,7 +356,10 @@ class EnvironmentController:
                     if rp.alive():
                         continue
                     wait = backoff.get(rp.name, 0.5)
-                    self.event("ReplicaCrashed", app=rt.name, replica=rp.name, code=rp.proc.returncode)
+                    self.limiter.remove(rp.name)
+                    self.event("ReplicaCrashed", app=rt.name, replica=rp.name, code=rp.proc.returncode,
+                               reason="OOMKilled" if rp.name in self._oom else "Error")
+                    self._oom.discard(rp.name)
                     async with self._lock:
                         rev.replicas.remove(rp)
                         await asyncio.sleep(wait)
@@ -344,6 +371,31 @@ class EnvironmentController:
                     except Exception as e:
                         self.event("ReplicaFailedToStart", app=rt.name, replica=new.name, error=str(e))
                     self._refresh_backends(rt)
+
+    def retention_days(self) -> float:
+        return float((self.m.environment.get("logAnalytics") or {}).get("retentionInDays") or 0)
+
+    def prune_telemetry(self, now: float | None = None) -> dict:
+        """Log Analytics retention (``retentionInDays``) over the environment's telemetry dir."""
+        from ..telemetry.retention import prune
+        res = prune(self.dir / "telemetry", self.retention_days(), now)
+        if res["removed"]:
+            self.event("TelemetryPruned", retentionInDays=self.retention_days(), files=len(res["removed"]))
+        return res
+
+    async def _retention_loop(self) -> None:
+        while True:
+            try:
+                await asyncio.to_thread(self.prune_telemetry)
+            except Exception as e:
+                log.warning("telemetry retention: %r", e)
+            await asyncio.sleep(3600)
+
+    async def _throttle_loop(self) -> None:
+        """CPU duty cycle of every replica (watchdog mode, ``resourceLimits.cpu: true``)."""
+        while True:
+            await asyncio.to_thread(self.limiter.throttle_tick)
+            await asyncio.sleep(0.01)
 
     async def metric(self, rt: AppRuntime, rule: ScaleRule) -> float:
         md = rule.metadata
@@ -410,7 +462,12 @@ class EnvironmentController:
                     "internalUrl": f"unix:{self._ingress_uds(rt.name)}:", "inflight": ing.route.inflight,
                     "requests": ing.route.requests},
             }
+        limits = {**self.limiter.describe(),
+                  "replicas": {n: {"cpu": st.limits.cpu, "memoryBytes": st.limits.memory, "peakRssBytes": st.peak_rss,
+                                   "throttledPeriods": st.throttled_periods}
+                               for n, st in self.limiter.replicas.items()}}
         return {"name": self.m.name, "envDir": str(self.dir), "backingUrl": self.stack.backing_url,
+                "resourceLimits": limits,
                 "uptimeSeconds": round(time.time() - self.started, 1), "apps": apps,
                 "outputs": self.m.outputs(), "events": self.events[-30:]}
 
@@ -547,3 +604,7 @@ def reset_env_dir(env_dir: str | os.PathLike) -> None:
     if (p / "control.sock").exists():
         raise RuntimeError("environment is running; run `down` first")
     shutil.rmtree(p, ignore_errors=True)
+
+
+def _truthy(v) -> bool:
+    return v is True or str(v).strip().lower() in ("1", "true", "yes", "on")

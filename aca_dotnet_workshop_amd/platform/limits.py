@@ -1,0 +1,239 @@
+"""Per-replica resource limits: the Consumption workload profile's ``cpu`` / ``memory``
+(0.25 vCPU / 0.5 Gi for every app: reference bicep/modules/container-apps/
+processor-backend-service.bicep:143-146, webapi-backend-service.bicep:124-127,
+webapp-frontend-service.bicep:84-87).
+
+A replica is the process group of its sidecar (sidecar + native data plane + app).  Two
+enforcement mechanisms, chosen at start-up and reported in the environment status:
+
+* ``cgroup2`` -- a delegated cgroup v2 subtree is writable: one cgroup per replica with
+  ``cpu.max`` (quota per 100 ms period) and ``memory.max``; the kernel throttles and
+  OOM-kills, the controller sees the dead replica and restarts it (``ReplicaOOMKilled``
+  when ``memory.events`` counted an OOM kill).
+* ``watchdog`` -- no delegated cgroup (unprivileged containers, this CI box): memory is
+  enforced by the controller, which sums the RSS of the replica's processes every
+  supervision tick and kills + restarts a replica above its limit (``ReplicaOOMKilled``),
+  like ACA restarting an OOM-killed container; CPU is enforced, when enabled, by a duty-cycle
+  throttle (``CpuThrottle``: SIGSTOP the group once it has used its quota of the current
+  100 ms period, SIGCONT at the next period) -- otherwise only accounted.
+
+``environment.resourceLimits`` in the manifest: ``{memory: true|false, cpu: true|false}``
+(defaults: memory enforced, CPU accounted only, so a development box stays usable).
+"""
+from __future__ import annotations
+
+import os
+import signal
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import psutil
+
+CGROUP_ROOT = Path("/sys/fs/cgroup")
+PERIOD_S = 0.1
+
+
+def parse_memory(v: str | int | float) -> int:
+    """``0.5Gi`` / ``512Mi`` / ``1G`` / bytes -> bytes."""
+    s = str(v).strip()
+    units = {"Ki": 1 << 10, "Mi": 1 << 20, "Gi": 1 << 30, "Ti": 1 << 40, "K": 10 ** 3, "M": 10 ** 6, "G": 10 ** 9,
+             "T": 10 ** 12}
+    for u in sorted(units, key=len, reverse=True):
+        if s.endswith(u):
+            return int(float(s[:-len(u)]) * units[u])
+    return int(float(s))
+
+
+@dataclass
+class Limits:
+    cpu: float           # cores
+    memory: int          # bytes
+
+    @classmethod
+    def from_spec(cls, spec: dict) -> "Limits":
+        r = spec.get("resources") or {}
+        return cls(float(r.get("cpu", 0.25)), parse_memory(r.get("memory", "0.5Gi")))
+
+
+def tree(pid: int) -> list[psutil.Process]:
+    try:
+        p = psutil.Process(pid)
+        return [p] + p.children(recursive=True)
+    except psutil.Error:
+        return []
+
+
+def rss(procs: list[psutil.Process]) -> int:
+    total = 0
+    for p in procs:
+        try:
+            total += p.memory_info().rss
+        except psutil.Error:
+            pass
+    return total
+
+
+def cpu_seconds(procs: list[psutil.Process]) -> float:
+    total = 0.0
+    for p in procs:
+        try:
+            t = p.cpu_times()
+            total += t.user + t.system
+        except psutil.Error:
+            pass
+    return total
+
+
+def delegated_cgroup() -> Path | None:
+    """This process's cgroup v2 directory when we may create children with cpu+memory."""
+    try:
+        if not (CGROUP_ROOT / "cgroup.controllers").exists():
+            return None
+        rel = next((ln.split("::", 1)[1].strip() for ln in Path("/proc/self/cgroup").read_text().splitlines()
+                    if ln.startswith("0::")), None)
+        if rel is None:
+            return None
+        base = CGROUP_ROOT / rel.lstrip("/")
+        ctrls = (base / "cgroup.controllers").read_text().split()
+        if "cpu" not in ctrls or "memory" not in ctrls or not os.access(base, os.W_OK):
+            return None
+        return base
+    except OSError:
+        return None
+
+
+@dataclass
+class ReplicaState:
+    name: str
+    pid: int
+    limits: Limits
+    cgroup: Path | None = None
+    period_start: float = field(default_factory=time.monotonic)
+    period_cpu: float = 0.0
+    stopped: bool = False
+    throttled_periods: int = 0
+    peak_rss: int = 0
+
+
+class ResourceLimiter:
+    def __init__(self, env_name: str, enforce_memory: bool = True, enforce_cpu: bool = False,
+                 cgroup_base: Path | None = None, allow_cgroup: bool = True) -> None:
+        self.enforce_memory = enforce_memory
+        self.enforce_cpu = enforce_cpu
+        base = cgroup_base if cgroup_base is not None else (delegated_cgroup() if allow_cgroup else None)
+        self.mode = "cgroup2" if base is not None else "watchdog"
+        self.root: Path | None = None
+        if base is not None:
+            self.root = base / f"tt-{env_name}"
+            try:
+                self.root.mkdir(exist_ok=True)
+                (self.root / "cgroup.subtree_control").write_text("+cpu +memory")
+            except OSError:
+                self.mode, self.root = "watchdog", None
+        self.replicas: dict[str, ReplicaState] = {}
+
+    def describe(self) -> dict:
+        cpu = ("cgroup cpu.max" if self.mode == "cgroup2" else "duty-cycle throttle") if self.enforce_cpu else "accounted"
+        mem = ("cgroup memory.max" if self.mode == "cgroup2" else "RSS watchdog + restart") if self.enforce_memory \
+            else "accounted"
+        return {"mode": self.mode, "cpu": cpu, "memory": mem}
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def add(self, name: str, pid: int, limits: Limits) -> ReplicaState:
+        st = self.replicas[name] = ReplicaState(name, pid, limits)
+        if self.root is not None:
+            cg = self.root / name
+            try:
+                cg.mkdir(exist_ok=True)
+                if self.enforce_cpu:
+                    (cg / "cpu.max").write_text(f"{max(1000, int(limits.cpu * 100000))} 100000")
+                if self.enforce_memory:
+                    (cg / "memory.max").write_text(str(limits.memory))
+                st.cgroup = cg
+                self._adopt(st)
+            except OSError:
+                st.cgroup = None
+        st.period_cpu = cpu_seconds(tree(pid))
+        return st
+
+    def remove(self, name: str) -> None:
+        st = self.replicas.pop(name, None)
+        if st is None:
+            return
+        if st.stopped:
+            self._signal(st, signal.SIGCONT)
+        if st.cgroup is not None:
+            try:
+                st.cgroup.rmdir()
+            except OSError:
+                pass
+
+    def _adopt(self, st: ReplicaState) -> None:
+        """Move the replica's processes (children started since) into its cgroup."""
+        for p in tree(st.pid):
+            try:
+                (st.cgroup / "cgroup.procs").write_text(str(p.pid))
+            except OSError:
+                pass
+
+    def _signal(self, st: ReplicaState, sig: int) -> None:
+        try:
+            os.killpg(st.pid, sig)  # replicas run in their own session / process group
+        except (ProcessLookupError, PermissionError):
+            pass
+
+    # -- supervision tick: memory ---------------------------------------------------------------
+    def check_memory(self) -> list[tuple[str, int]]:
+        """Replicas over their memory limit, killed now: [(name, rss bytes)]."""
+        out = []
+        for st in list(self.replicas.values()):
+            if st.cgroup is not None:
+                self._adopt(st)
+                try:
+                    ev = dict(ln.split() for ln in (st.cgroup / "memory.events").read_text().splitlines())
+                    if int(ev.get("oom_kill", 0)):
+                        out.append((st.name, st.limits.memory))
+                except (OSError, ValueError):
+                    pass
+                continue
+            used = rss(tree(st.pid))
+            st.peak_rss = max(st.peak_rss, used)
+            if self.enforce_memory and used > st.limits.memory:
+                self._signal(st, signal.SIGCONT)
+                self._signal(st, signal.SIGKILL)
+                out.append((st.name, used))
+        return out
+
+    # -- CPU duty cycle (watchdog mode) ----------------------------------------------------------
+    def throttle_tick(self, now: float | None = None) -> None:
+        """Call every few ms: stop a replica's group once it has used ``cpu x PERIOD_S`` CPU
+        seconds in the current period, resume it when the next period starts."""
+        if not self.enforce_cpu or self.mode == "cgroup2":
+            return
+        now = time.monotonic() if now is None else now
+        for st in list(self.replicas.values()):
+            used = cpu_seconds(tree(st.pid))
+            if now - st.period_start >= PERIOD_S:
+                # unused quota does not carry over; an overrun does (paid off in later periods)
+                quota = st.limits.cpu * (now - st.period_start)
+                overrun = max(0.0, (used - st.period_cpu) - quota)
+                st.period_cpu = used - overrun  # the next period starts with the debt already spent
+                st.period_start = now
+                if st.stopped:
+                    self._signal(st, signal.SIGCONT)
+                    st.stopped = False
+                continue
+            if not st.stopped and used - st.period_cpu >= st.limits.cpu * PERIOD_S:
+                self._signal(st, signal.SIGSTOP)
+                st.stopped = True
+                st.throttled_periods += 1
+
+    def release_all(self) -> None:
+        for name in list(self.replicas):
+            self.remove(name)
+        if self.root is not None:
+            try:
+                self.root.rmdir()
+            except OSError:
+                pass

@@ -4,7 +4,7 @@ Every record carries the role name and, when inside a request, the W3C trace/spa
 logs join traces (App Insights "Transaction Search").  Levels follow the reference's
 ``Logging:LogLevel`` section (``Default: Information``, ``Microsoft.AspNetCore: Warning``,
 reference Backend.Api/appsettings.json:2-8).  Records are also appended as JSON lines to
-``$TT_TELEMETRY_DIR/logs-<role>-<pid>.jsonl`` when the platform provides a telemetry dir
+``$TT_TELEMETRY_DIR/logs-<role>-<pid>-<YYYYMMDD>.jsonl`` when the platform provides a telemetry dir
 (the Log Analytics workspace of the environment); ``TT_LOG_CONSOLE=0`` keeps them off the
 console (the platform then ships only the JSON stream).
 
@@ -263,8 +263,8 @@ def configure_logging(role: str, config: Any = None, json_console: bool | None =
     d = os.environ.get("TT_TELEMETRY_DIR")
     if d:
         os.makedirs(d, exist_ok=True)
-        fh = open(os.path.join(d, f"logs-{role}-{os.getpid()}.jsonl"), "a", encoding="utf-8")
-        sinks.append(BufferedSink(fh, True, role, buffered=True))
+        from .retention import DailyFile
+        sinks.append(BufferedSink(DailyFile(d, f"logs-{role}-{os.getpid()}"), True, role, buffered=True))
     for h in sinks:
         h.addFilter(ctx)
         h._tt = True  # type: ignore[attr-defined]

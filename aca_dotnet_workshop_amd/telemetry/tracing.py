@@ -64,7 +64,8 @@ class Exporter:
         if directory:
             os.makedirs(directory, exist_ok=True)
             safe = role.replace("/", "_")
-            self._fh = open(os.path.join(directory, f"spans-{safe}-{os.getpid()}.jsonl"), "a", buffering=1 << 16)
+            from .retention import DailyFile
+            self._fh = DailyFile(directory, f"spans-{safe}-{os.getpid()}")  # one file per UTC day
             atexit.register(self.flush)
 
     def export(self, rec: dict[str, Any]) -> None:

@@ -185,3 +185,33 @@ def test_accelerator_keeps_writes_native(monkeypatch):
             assert st["cpu"] == 2 and st["mirror"]["disabled"] == 1
             await c.http.close()
     run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
+def test_provisioned_throughput_429(front, monkeypatch):
+    """RU token bucket shared by both fronts: 429 with x-ms-retry-after-ms / Retry-After when spent,
+    nothing charged for a rejected call; the backing client retries after the hint."""
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.doc_set_throughput("acct", "db", "c", 10.0)
+            h = HttpClient()
+            statuses, hints = [], []
+            for i in range(5):
+                r = await h.put(f"{b.base}/cosmos/acct/db/c/docs/k{i}", body=b'{"a": 1}',
+                                headers={"Content-Type": "application/json", "x-tt-identity": "x"})
+                statuses.append(r.status)
+                if r.status == 429:
+                    hints.append(int(r.headers["x-ms-retry-after-ms"]))
+                    assert int(r.headers["retry-after"]) >= 1
+            assert statuses[:2] == [200, 200] and 429 in statuses and all(0 < x <= 1000 for x in hints)
+            await c.doc_put("acct", "db", "c", "late", '{"a": 2}')  # retried transparently
+            assert c.throttled_retries >= 1
+            st = await c.doc_stats("acct", "db", "c")
+            assert st["throughput"]["ru_per_s"] == 10.0 and st["throughput"]["throttled"] >= 1
+            await c.doc_set_throughput("acct", "db", "c", 0)  # unlimited again
+            for i in range(20):
+                await c.doc_put("acct", "db", "c", f"u{i}", "1")
+            await h.close()
+            await c.http.close()
+    run(main())

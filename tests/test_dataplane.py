@@ -444,3 +444,28 @@ def test_native_http_parser_survives_garbage(tmp_path):
             r = await e.http.post(f"{e.base['app-a']}/v1.0/state/statestore", json_body=[{"key": "ok", "value": 1}])
             assert r.status == 204
     run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_state_throttling_is_retried(plane, tmp_path):
+    """Provisioned RU/s (Cosmos 4000 RU/s in the reference's Bicep, scaled down here): the store
+    answers 429 + x-ms-retry-after-ms once the budget is spent, and both sidecar planes retry after
+    the hint, so the application sees success -- just later."""
+    import time
+
+    async def main():
+        async with Env(plane, tmp_path) as e:
+            st = e.backing.store("acct1", "db", "tasks")
+            st.set_throughput(50.0)  # 10 writes of <= 1 KiB per second, 1 s burst
+            b = e.base["app-a"]
+            t0 = time.perf_counter()
+            for i in range(20):
+                r = await e.http.post(f"{b}/v1.0/state/statestore", json_body=[{"key": f"k{i}", "value": {"i": i}}])
+                assert r.status == 204, r.body
+            dt = time.perf_counter() - t0
+            assert dt > 0.8  # 20 writes x 5 RU = 100 RU at 50 RU/s with a 50 RU burst
+            ts = st.throughput_stats()
+            assert ts["throttled"] >= 1 and ts["ru_consumed"] >= 100
+            r = await e.http.get(f"{b}/v1.0/state/statestore/k19")
+            assert r.status == 200 and r.json() == {"i": 19}
+    run(main())

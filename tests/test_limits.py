@@ -1,0 +1,73 @@
+"""Per-replica resource limits (platform/limits.py): the Consumption profile's 0.25 vCPU /
+0.5 Gi (reference processor-backend-service.bicep:143-146).  Exercised here in watchdog mode
+(no delegated cgroup in CI): the memory watchdog kills a replica over its limit, the CPU
+duty-cycle throttle holds a busy loop near its quota."""
+import os
+import subprocess
+import sys
+import time
+
+from aca_dotnet_workshop_amd.platform.limits import Limits, ResourceLimiter, cpu_seconds, parse_memory, tree
+
+
+def _spawn(code):
+    return subprocess.Popen([sys.executable, "-c", code], start_new_session=True)
+
+
+def test_parse_memory():
+    assert parse_memory("0.5Gi") == 512 << 20
+    assert parse_memory("256Mi") == 256 << 20
+    assert parse_memory("1G") == 10 ** 9
+    assert parse_memory(1024) == 1024
+
+
+def test_memory_watchdog_kills_replica_over_limit():
+    p = _spawn("import time\nx = bytearray(160 << 20)\nfor i in range(0, len(x), 4096): x[i] = 1\ntime.sleep(30)")
+    lim = ResourceLimiter("t", enforce_memory=True, allow_cgroup=False)
+    try:
+        lim.add("hog-0", p.pid, Limits(0.25, parse_memory("64Mi")))
+        assert lim.describe()["memory"] == "RSS watchdog + restart"
+        killed = []
+        deadline = time.time() + 20
+        while not killed and time.time() < deadline:
+            killed = lim.check_memory()
+            time.sleep(0.1)
+        assert killed and killed[0][0] == "hog-0" and killed[0][1] > (64 << 20)
+        assert p.wait(10) == -9
+    finally:
+        if p.poll() is None:
+            p.kill()
+        lim.release_all()
+
+
+def test_memory_under_limit_is_left_alone():
+    p = _spawn("import time\ntime.sleep(30)")
+    lim = ResourceLimiter("t", enforce_memory=True, allow_cgroup=False)
+    try:
+        lim.add("small-0", p.pid, Limits(0.25, parse_memory("0.5Gi")))
+        for _ in range(5):
+            assert lim.check_memory() == []
+            time.sleep(0.05)
+        assert p.poll() is None and lim.replicas["small-0"].peak_rss > 0
+    finally:
+        p.kill()
+        lim.release_all()
+
+
+def test_cpu_throttle_holds_quota():
+    p = _spawn("while True: pass")
+    lim = ResourceLimiter("t", enforce_cpu=True, allow_cgroup=False)
+    try:
+        st = lim.add("busy-0", p.pid, Limits(0.25, parse_memory("0.5Gi")))
+        c0, t0 = cpu_seconds(tree(p.pid)), time.monotonic()
+        while time.monotonic() - t0 < 3.0:
+            lim.throttle_tick()
+            time.sleep(0.005)
+        used = cpu_seconds(tree(p.pid)) - c0
+        wall = time.monotonic() - t0
+        assert used / wall < 0.45, used / wall  # ~0.25 cores (+ tick granularity), not 1.0
+        assert st.throttled_periods >= 10
+    finally:
+        lim.release_all()
+        os.killpg(p.pid, 9)
+        p.wait()

@@ -170,6 +170,30 @@ def test_environment_lifecycle(tmp_path):
                 if api_rt.restarts >= 1 and all(r.alive() for r in api_rt.current.replicas):
                     break
             assert api_rt.restarts >= 1 and api_rt.current.replicas[0].name != victim.name
+            # resource limits (0.25 vCPU / 0.5Gi per replica): a replica over its memory limit is
+            # killed and restarted like an OOM-killed container
+            lim = ctl.status()["resourceLimits"]
+            assert lim["mode"] in ("cgroup2", "watchdog") and len(lim["replicas"]) >= 3
+            assert all(r["memoryBytes"] == 512 << 20 and r["cpu"] == 0.25 for r in lim["replicas"].values())
+            oom = api_rt.current.replicas[0]
+            ctl.limiter.replicas[oom.name].limits.memory = 1 << 20  # as if it had grown past 0.5Gi
+            for _ in range(200):
+                await asyncio.sleep(0.1)
+                if api_rt.restarts >= 2 and all(r.alive() for r in api_rt.current.replicas):
+                    break
+            ev = [e for e in ctl.events if e["kind"] in ("ReplicaOOMKilled", "ReplicaCrashed") and e["replica"] == oom.name]
+            assert [e["kind"] for e in ev] == ["ReplicaOOMKilled", "ReplicaCrashed"] and ev[1]["reason"] == "OOMKilled"
+            assert api_rt.current.replicas[0].name != oom.name
+            # Cosmos provisioned throughput from the manifest (autoscale max 4000 RU/s)
+            ts = (await b.doc_stats("taskstracker-state-store", "tasksmanagerdb", "taskscollection"))["throughput"]
+            assert ts["ru_per_s"] == 4000
+            # Log Analytics retention (retentionInDays: 30): day files past the window are pruned
+            from aca_dotnet_workshop_amd.telemetry.retention import utc_day
+            tdir = tmp_path / "env" / "telemetry"
+            stale = tdir / f"logs-old-1-{utc_day(time.time() - 31 * 86400)}.jsonl"
+            stale.write_text("{}\n")
+            assert ctl.retention_days() == 30 and stale.name in ctl.prune_telemetry()["removed"]
+            assert any(tdir.glob(f"spans-*-{utc_day()}.jsonl"))  # today's telemetry stays
             # module 10: a changed template deploys a new revision and retires the old one
             old = proc.current.name
             res = await ctl.apply(load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 10}))

@@ -77,3 +77,30 @@ def test_prometheus_exposition():
     text = r.expose()
     assert 'reqs{route="/a"} 3.0' in text and 'lat_count{route="/a"} 3' in text
     assert h.quantile(0.5, route="/a") == 0.0025
+
+
+def test_log_retention_prunes_whole_days(tmp_path):
+    """retentionInDays (Log Analytics, 30 in the reference): telemetry is written one file per
+    process per UTC day, and pruning deletes the days that fell out of the window."""
+    import os
+    import time
+
+    from aca_dotnet_workshop_amd.telemetry.retention import DailyFile, prune, utc_day
+
+    now = time.time()
+    day = 86400.0
+    for age in (0, 1, 29, 30, 31, 45):
+        (tmp_path / f"logs-api-1-{utc_day(now - age * day)}.jsonl").write_text("{}\n")
+    legacy_old = tmp_path / "spans-old-7.jsonl"
+    legacy_old.write_text("{}\n")
+    os.utime(legacy_old, (now - 40 * day, now - 40 * day))
+    (tmp_path / "spans-new-8.jsonl").write_text("{}\n")
+    res = prune(tmp_path, 30, now)
+    assert sorted(res["removed"]) == sorted([f"logs-api-1-{utc_day(now - a * day)}.jsonl" for a in (31, 45)]
+                                            + ["spans-old-7.jsonl"])
+    assert res["kept"] == 5
+    f = DailyFile(str(tmp_path), "logs-x-9")
+    f.write("a\n")
+    f.close()
+    assert (tmp_path / f"logs-x-9-{utc_day()}.jsonl").read_text() == "a\n"
+    assert prune(tmp_path, 0, now)["removed"] == []  # 0 = keep forever
