@@ -67,7 +67,7 @@ def _compile_native(target: Path, verbose: bool) -> None:
     tmp = target.with_suffix(f".tmp{os.getpid()}.so")
     cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
            f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", str(SRC / "module.cpp"),
-           "-o", str(tmp), "-lpthread"]
+           "-o", str(tmp), "-lpthread", "-lssl", "-lcrypto"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -78,7 +78,8 @@ DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
 
 
 def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
-    sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp", SRC / "textutil.hpp"]
+    sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
+               SRC / "textutil.hpp"]
     return _build_exe(DATAPLANE, SRC / "dataplane.cpp", sources, force, verbose)
 
 
@@ -90,7 +91,8 @@ def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbo
             return target
         cxx = os.environ.get("CXX", "g++")
         tmp = target.with_name(f".{target.name}.tmp{os.getpid()}")
-        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(main), "-o", str(tmp)]
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(main), "-o", str(tmp), "-lssl",
+               "-lcrypto"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
@@ -103,7 +105,7 @@ LOADGEN = HERE / "bin" / "ttloadgen"
 
 def build_loadgen(force: bool = False, verbose: bool = False) -> Path:
     """Closed-loop HTTP load generator used by bench.py (src/loadgen.cpp)."""
-    sources = [SRC / "loadgen.cpp", SRC / "evhttp.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
+    sources = [SRC / "loadgen.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
     return _build_exe(LOADGEN, SRC / "loadgen.cpp", sources, force, verbose)
 
 

@@ -88,14 +88,23 @@ class AppHost {
   }
 
   // Bind a listener for server group `server`; returns the TCP port (0 for Unix sockets).
-  int listen(int server, const std::string& endpoint) {
+  // `cert` / `key` (PEM files): serve HTTPS on it (Kestrel's https endpoint).
+  int listen(int server, const std::string& endpoint, const std::string& cert = "", const std::string& key = "") {
     auto ep = ev::Endpoint::parse(endpoint);
-    if (!thread_.joinable()) return listen_now(server, ep);
+    std::shared_ptr<ev::TlsContext> tls;
+    if (!cert.empty()) {
+      ev::TlsConfig tc;
+      tc.cert = cert;
+      tc.key = key;
+      tc.verify_peer = false;
+      tls = std::make_shared<ev::TlsContext>(tc, true);
+    }
+    if (!thread_.joinable()) return listen_now(server, ep, tls);
     auto p = std::make_shared<std::promise<int>>();
     auto f = p->get_future();
-    post([this, server, ep, p] {
+    post([this, server, ep, p, tls] {
       try {
-        p->set_value(listen_now(server, ep));
+        p->set_value(listen_now(server, ep, tls));
       } catch (...) {
         p->set_exception(std::current_exception());
       }
@@ -268,7 +277,7 @@ class AppHost {
     }
   }
 
-  int listen_now(int server, const ev::Endpoint& ep) {
+  int listen_now(int server, const ev::Endpoint& ep, std::shared_ptr<ev::TlsContext> tls = nullptr) {
     auto& h = handlers_[server];
     if (!h) {
       h = std::make_unique<ev::Handler>([this, server](Message&& m, ev::Reply reply) {
@@ -283,7 +292,7 @@ class AppHost {
       });
     }
     std::shared_ptr<ev::IoObj> l;
-    int port = ev::listen_on(loop_, ep, *h, false, &l);
+    int port = ev::listen_on(loop_, ep, *h, false, &l, std::move(tls));
     std::static_pointer_cast<ev::Listener>(l)->on_accept = [this, server](const std::shared_ptr<ev::ServerConn>& c) {
       auto& v = conns_[server];
       if (v.size() >= 1024) {  // prune closed connections

@@ -351,6 +351,15 @@ class DataPlane {
     if (auto* t = opt_str(cfg, "appToken")) app_token_ = *t;
     if (auto* t = opt_str(cfg, "apiToken")) api_token_ = *t;
     if (auto* t = opt_str(cfg, "meshToken")) mesh_token_ = *t;
+    if (auto* t = cfg.get("mtls"); t && t->t == Value::Object) {
+      // mutual TLS with peer sidecars: our workload certificate for both directions
+      ev::TlsConfig tc;
+      tc.cert = *opt_str(*t, "cert");
+      tc.key = *opt_str(*t, "key");
+      tc.ca = *opt_str(*t, "ca");
+      mesh_server_tls = std::make_shared<ev::TlsContext>(tc, true);
+      client_.set_tls(std::make_shared<ev::TlsContext>(tc, false));
+    }
     if (auto* r = opt_str(cfg, "registryDir")) resolver_.dir = *r;
     fallback_ = Endpoint::parse(*opt_str(cfg, "fallback"));
     if (auto* v = cfg.get("invokeNative"); v && v->t == Value::Bool) invoke_native_ = v->b;
@@ -409,6 +418,12 @@ class DataPlane {
   Tracer tracer_;
   Resolver resolver_;
   std::string app_id_, app_token_, api_token_, mesh_token_;
+
+ public:
+  std::shared_ptr<ev::TlsContext> mesh_server_tls;  // internal listeners (mutual TLS), when configured
+  const std::string& app_id() const { return app_id_; }
+
+ private:
   Endpoint app_, fallback_;
   bool has_app_ = false, invoke_native_ = true, api_logging_ = false;
   double app_timeout_ = 300;
@@ -989,6 +1004,15 @@ class DataPlane {
   }
 
   void on_internal(Message&& m, Reply r) {
+    if (mesh_server_tls) {
+      // mutual TLS: the caller proved an environment workload identity; the app-id it claims
+      // must be one its certificate names (no spoofed dapr-caller-app-id)
+      auto* c = m.header("dapr-caller-app-id");
+      if (!m.tls || (c && !names_include(m.tls_peer, *c))) {
+        r.json(403, error_json("ERR_MESH_AUTH", "caller identity not proven by its mTLS certificate"));
+        return;
+      }
+    }
     if (!mesh_token_.empty()) {
       auto* t = m.header("tt-mesh-token");
       if (!t || *t != mesh_token_) {
@@ -1012,6 +1036,17 @@ class DataPlane {
       }
       relay(*d, res);
     });
+  }
+
+  static bool names_include(const std::string& csv, const std::string& name) {
+    size_t p = 0;
+    while (p <= csv.size()) {
+      size_t e = csv.find(',', p);
+      if (e == std::string::npos) e = csv.size();
+      if (csv.compare(p, e - p, name) == 0) return true;
+      p = e + 1;
+    }
+    return false;
   }
 
   // ---------------------------------------------------------------- state
@@ -1384,9 +1419,11 @@ int main(int argc, char** argv) {
     if (auto* l = cfg.get("internal"); l && l->t == Value::Array)
       for (auto& x : l->items) {
         Endpoint ep = Endpoint::parse(x.s);
-        int p = ev::listen_on(loop, ep, internal);
-        if (internal_ep.empty())
+        int p = ev::listen_on(loop, ep, internal, false, nullptr, dp.mesh_server_tls);
+        if (internal_ep.empty()) {
           internal_ep = ep.unix_socket ? "unix:" + ep.path + ":" : "http://127.0.0.1:" + std::to_string(p);
+          if (dp.mesh_server_tls) internal_ep = "mtls:" + dp.app_id() + "@" + internal_ep;
+        }
       }
     if (auto* c = opt_str(cfg, "control")) ev::listen_on(loop, Endpoint::parse(*c), control);
     ports += ",\"internal\":" + json_str(internal_ep) + ",\"pid\":" + std::to_string(getpid()) + "}";

@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "httpparse.hpp"
+#include "tls.hpp"
 
 namespace tt::ev {
 
@@ -210,6 +211,8 @@ struct Message {
   bool http10 = false;
   HeaderList headers;  // lower-cased names
   std::string body;
+  std::string tls_peer;  // server side over TLS: SAN names of the verified client certificate
+  bool tls = false;      // server side: arrived over TLS
 
   const std::string* header(std::string_view name) const {
     for (auto& h : headers)
@@ -452,10 +455,32 @@ struct Endpoint {
   std::string path;  // unix
   std::string host;  // tcp
   int port = 0;
-  std::string key() const { return unix_socket ? "unix:" + path : host + ":" + std::to_string(port); }
+  // TLS: 0 plain, 1 mutual TLS with the mesh context (peer certificate must name `tls_name`),
+  // 2 https verified by the mesh CA, 3 https without verification (`--app-ssl` dev certificates)
+  int tls = 0;
+  std::string tls_name;
+  std::string key() const {
+    std::string k = unix_socket ? "unix:" + path : host + ":" + std::to_string(port);
+    return tls ? "tls" + std::to_string(tls) + ":" + tls_name + "@" + k : k;
+  }
 
-  // "unix:/path/to.sock[:]" | "http://host:port" | "tcp:host:port" | "host:port"
+  // "unix:/path/to.sock[:]" | "http://host:port" | "tcp:host:port" | "host:port" |
+  // "https://host:port" | "https+insecure://host:port" | "mtls:<peer-name>@<any of these>"
   static Endpoint parse(std::string s) {
+    if (s.rfind("mtls:", 0) == 0) {
+      size_t at = s.find('@');
+      Endpoint e = parse(at == std::string::npos ? std::string() : s.substr(at + 1));
+      e.tls = 1;
+      e.tls_name = s.substr(5, at == std::string::npos ? std::string::npos : at - 5);
+      return e;
+    }
+    if (s.rfind("https://", 0) == 0 || s.rfind("https+insecure://", 0) == 0) {
+      bool insecure = s[5] == '+';
+      Endpoint e = parse("http://" + s.substr(insecure ? 17 : 8));
+      e.tls = insecure ? 3 : 2;
+      e.tls_name = e.host;
+      return e;
+    }
     Endpoint e;
     if (s.rfind("unix:", 0) == 0) {
       s = s.substr(5);
@@ -500,16 +525,21 @@ using Handler = std::function<void(Message&&, Reply)>;
 
 class ServerConn : public IoObj {
  public:
-  ServerConn(Loop& loop, int fd, Handler& h) : loop_(loop), handler_(h), parser_(true) { this->fd = fd; }
+  ServerConn(Loop& loop, int fd, Handler& h, const TlsContext* tls = nullptr)
+      : loop_(loop), handler_(h), parser_(true) {
+    this->fd = fd;
+    if (tls) tls_ = std::make_unique<TlsIo>(*tls, fd);
+  }
 
   void on_event(uint32_t ev) override {
-    if (!peer_closed_ && (ev & (EPOLLIN | EPOLLHUP | EPOLLERR))) {
+    // over TLS, writability may be what a pending handshake / read step waits for
+    if (!peer_closed_ && ((ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) || (tls_ && (ev & EPOLLOUT)))) {
       char buf[65536];
       while (true) {
-        ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+        ssize_t n = io_recv(buf, sizeof buf);
         if (n > 0) {
           in_.append(buf, (size_t)n);
-          if ((size_t)n < sizeof buf) break;
+          if (!tls_ && (size_t)n < sizeof buf) break;  // TLS: drain OpenSSL's buffered records too
           continue;
         }
         if (n == 0) {
@@ -531,7 +561,8 @@ class ServerConn : public IoObj {
         update_interest();  // stop polling a half-closed socket; finish writing what is pending
       }
     }
-    if (ev & EPOLLOUT) flush();
+    if ((ev & EPOLLOUT) || (tls_ && out_off_ < out_.size())) flush();
+    else if (tls_) update_interest();
   }
 
   void respond(uint64_t seq, int status, const HeaderList& headers, std::string_view body, bool head_request) {
@@ -566,6 +597,12 @@ class ServerConn : public IoObj {
   bool close_after_write_ = false;
   bool parsing_ = false;
   uint32_t interest_ = EPOLLIN;
+  std::unique_ptr<TlsIo> tls_;
+  std::string tls_peer_;
+  bool tls_peer_known_ = false;
+
+  ssize_t io_recv(char* buf, size_t n) { return tls_ ? tls_->recv(buf, n) : ::recv(fd, buf, n, 0); }
+  ssize_t io_send(const char* p, size_t n) { return tls_ ? tls_->send(p, n) : ::send(fd, p, n, MSG_NOSIGNAL); }
 
   void drain() {
     while (!pending_.empty() && pending_.front().ready) {
@@ -599,6 +636,11 @@ class ServerConn : public IoObj {
         drain();
         break;
       }
+      if (tls_) {
+        if (!tls_peer_known_) tls_peer_ = tls_->peer_names(), tls_peer_known_ = true;
+        m.tls = true;
+        m.tls_peer = tls_peer_;
+      }
       bool ka = m.keep_alive();
       bool head = m.method == "HEAD";
       uint64_t seq = head_seq_ + pending_.size();
@@ -618,8 +660,8 @@ class ServerConn : public IoObj {
   bool stop_reading_ = false;
 
   void update_interest() {
-    uint32_t want = (peer_closed_ || stop_reading_ ? 0u : (uint32_t)EPOLLIN) |
-                    (out_off_ < out_.size() ? (uint32_t)EPOLLOUT : 0u);
+    bool out = tls_ ? tls_->want_write : out_off_ < out_.size();
+    uint32_t want = (peer_closed_ || stop_reading_ ? 0u : (uint32_t)EPOLLIN) | (out ? (uint32_t)EPOLLOUT : 0u);
     if (want != interest_) {
       interest_ = want;
       loop_.mod(this, want);
@@ -628,7 +670,7 @@ class ServerConn : public IoObj {
 
   void flush() {
     while (out_off_ < out_.size()) {
-      ssize_t n = ::send(fd, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+      ssize_t n = io_send(out_.data() + out_off_, out_.size() - out_off_);
       if (n > 0) {
         out_off_ += (size_t)n;
         continue;
@@ -658,7 +700,10 @@ inline void Reply::send(int status, const HeaderList& headers, std::string_view 
 
 class Listener : public IoObj {
  public:
-  Listener(Loop& loop, int fd, Handler& h) : loop_(loop), handler_(h) { this->fd = fd; }
+  Listener(Loop& loop, int fd, Handler& h, std::shared_ptr<TlsContext> tls = nullptr)
+      : loop_(loop), handler_(h), tls_(std::move(tls)) {
+    this->fd = fd;
+  }
   void on_event(uint32_t) override {
     while (true) {
       int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
@@ -668,7 +713,13 @@ class Listener : public IoObj {
       }
       int one = 1;
       setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // fails harmlessly on unix sockets
-      auto conn = std::make_shared<ServerConn>(loop_, c, handler_);
+      std::shared_ptr<ServerConn> conn;
+      try {
+        conn = std::make_shared<ServerConn>(loop_, c, handler_, tls_.get());
+      } catch (const std::exception&) {
+        ::close(c);
+        continue;
+      }
       loop_.add(conn, EPOLLIN);
       if (on_accept) on_accept(conn);
     }
@@ -679,13 +730,15 @@ class Listener : public IoObj {
  private:
   Loop& loop_;
   Handler& handler_;
+  std::shared_ptr<TlsContext> tls_;
 };
 
 // Returns the bound port (tcp) or 0 (unix); throws on failure.
 // `reuseport`: several loops (threads) bind the same TCP port and the kernel spreads
 // incoming connections over them.
+// `tls`: serve HTTPS (with `verify_peer`: mutual TLS) on this listener.
 inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false,
-                     std::shared_ptr<IoObj>* listener_out = nullptr) {
+                     std::shared_ptr<IoObj>* listener_out = nullptr, std::shared_ptr<TlsContext> tls = nullptr) {
   int fd;
   int port = 0;
   if (ep.unix_socket) {
@@ -712,7 +765,7 @@ inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport 
     port = ntohs(a.sin_port);
   }
   if (::listen(fd, 1024) != 0) throw std::runtime_error(std::string("listen: ") + strerror(errno));
-  auto l = std::make_shared<Listener>(loop, fd, h);
+  auto l = std::make_shared<Listener>(loop, fd, h, std::move(tls));
   loop.add(l, EPOLLIN);
   if (listener_out) *listener_out = l;
   return port;
@@ -751,6 +804,10 @@ class ClientConn : public IoObj {
   bool busy() const { return busy_; }
   std::string wire_copy;  // kept for the stale-connection retry
   bool head_req = false;
+  std::unique_ptr<TlsIo> tls_;
+
+  ssize_t io_recv(char* buf, size_t n) { return tls_ ? tls_->recv(buf, n) : ::recv(fd, buf, n, 0); }
+  ssize_t io_send(const char* p, size_t n) { return tls_ ? tls_->send(p, n) : ::send(fd, p, n, MSG_NOSIGNAL); }
 
  private:
   friend class Client;
@@ -777,6 +834,9 @@ class ClientConn : public IoObj {
 class Client {
  public:
   explicit Client(Loop& loop) : loop_(loop) {}
+
+  // Mutual-TLS identity for "mtls:" endpoints (and the CA that verifies "https://" ones).
+  void set_tls(std::shared_ptr<TlsContext> mesh) { mesh_tls_ = std::move(mesh); }
 
   // Issue `method target` with `headers`/`body` to `ep`; `cb` runs on completion or failure.
   void request(const Endpoint& ep, std::string_view method, std::string_view target, const HeaderList& headers,
@@ -888,8 +948,36 @@ class Client {
  private:
   Loop& loop_;
   std::unordered_map<std::string, std::vector<std::shared_ptr<ClientConn>>> idle_;
+  std::shared_ptr<TlsContext> mesh_tls_, insecure_tls_, system_tls_;
+
+  const TlsContext* tls_for(const Endpoint& ep) {
+    if (ep.tls == 1) return mesh_tls_.get();
+    if (ep.tls == 2 && mesh_tls_) return mesh_tls_.get();
+    if (ep.tls == 2) {
+      if (!system_tls_) {
+        TlsConfig c;
+        c.verify_peer = false;  // no trust store configured: encrypt, but only the mesh CA can verify
+        system_tls_ = std::make_shared<TlsContext>(c, false);
+      }
+      return system_tls_.get();
+    }
+    if (!insecure_tls_) {
+      TlsConfig c;
+      c.verify_peer = false;
+      insecure_tls_ = std::make_shared<TlsContext>(c, false);
+    }
+    return insecure_tls_.get();
+  }
 
   std::shared_ptr<ClientConn> connect(const Endpoint& ep, const std::string& key, int& err) {
+    const TlsContext* tctx = nullptr;
+    if (ep.tls) {
+      tctx = tls_for(ep);
+      if (!tctx) {  // "mtls:" endpoint but this process has no mesh identity
+        err = EPROTO;
+        return nullptr;
+      }
+    }
     int fd;
     bool in_progress = false;
     if (ep.unix_socket) {
@@ -924,6 +1012,7 @@ class Client {
     }
     auto c = std::make_shared<ClientConn>(loop_, *this, key);
     c->fd = fd;
+    if (tctx) c->tls_ = std::make_unique<TlsIo>(*tctx, fd, ep.tls == 3 ? std::string() : ep.tls_name);
     c->connecting = in_progress;
     loop_.add(c, in_progress ? (EPOLLOUT | EPOLLIN) : EPOLLIN);
     if (in_progress) c->want_out_ = true;
@@ -942,15 +1031,15 @@ inline void ClientConn::on_event(uint32_t ev) {
     }
     connecting = false;
   }
-  if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+  if ((ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) || (tls_ && !connecting && (ev & EPOLLOUT))) {
     char buf[65536];
     bool eof = false;
     while (true) {
-      ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+      ssize_t n = io_recv(buf, sizeof buf);
       if (n > 0) {
         in_.append(buf, (size_t)n);
         got_bytes_ = true;
-        if ((size_t)n < sizeof buf) break;
+        if (!tls_ && (size_t)n < sizeof buf) break;
         continue;
       }
       if (n == 0) {
@@ -989,27 +1078,29 @@ inline void ClientConn::on_event(uint32_t ev) {
       return;
     }
   }
-  if (!dead && (ev & EPOLLOUT) && busy_) flush();
+  if (!dead && busy_ && ((ev & EPOLLOUT) || (tls_ && out_off_ < out_.size()))) flush();
+  else if (!dead && tls_) flush();  // re-evaluate write interest (handshake progress)
 }
 
 inline void ClientConn::flush() {
   while (out_off_ < out_.size()) {
-    ssize_t n = ::send(fd, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+    ssize_t n = io_send(out_.data() + out_off_, out_.size() - out_off_);
     if (n > 0) {
       out_off_ += (size_t)n;
       continue;
     }
     if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
     if (n < 0 && errno == EINTR) continue;
-    fail(errno == EPIPE ? EPIPE : ECONNRESET);
+    fail(tls_ ? EPROTO : errno == EPIPE ? EPIPE : ECONNRESET);
     return;
   }
-  bool need_out = out_off_ < out_.size();
+  // over TLS a pending write may be waiting for the handshake's next read, not writability
+  bool need_out = tls_ ? tls_->want_write : out_off_ < out_.size();
   if (need_out != want_out_) {
     want_out_ = need_out;
     loop_.mod(this, need_out ? (EPOLLIN | EPOLLOUT) : EPOLLIN);
   }
-  if (!need_out) {
+  if (out_off_ >= out_.size()) {
     out_.clear();
     out_off_ = 0;
   }

@@ -306,8 +306,8 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("start", &apphost::AppHost::start)
       .def("stop", &apphost::AppHost::stop, py::call_guard<py::gil_scoped_release>())
       .def("event_fd", &apphost::AppHost::event_fd)
-      .def("listen", &apphost::AppHost::listen, py::arg("server"), py::arg("endpoint"),
-           py::call_guard<py::gil_scoped_release>())
+      .def("listen", &apphost::AppHost::listen, py::arg("server"), py::arg("endpoint"), py::arg("cert") = "",
+           py::arg("key") = "", py::call_guard<py::gil_scoped_release>())
       .def("close_server", &apphost::AppHost::close_server)
       .def("close_connections", &apphost::AppHost::close_connections)
       .def("pending_replies", &apphost::AppHost::pending_replies)

@@ -36,6 +36,7 @@ from ..web.http import Request, Response, empty, json_response
 from ..web.server import HttpServer
 from .ingress import Backend, Ingress, IngressRoute
 from .limits import Limits, ResourceLimiter
+from .pki import EnvironmentPki
 from .manifest import Manifest, ManifestError, desired_state, identity_of, template_hash, validate
 from .processes import LocalStack, ReplicaProc
 from .scaler import Autoscaler, ScaleRule, cron_metric
@@ -94,6 +95,10 @@ class EnvironmentController:
         self.limiter = ResourceLimiter(manifest.name, enforce_memory=_truthy(rl.get("memory", True)),
                                        enforce_cpu=_truthy(rl.get("cpu", False)))
         self._oom: set[str] = set()
+        # environment CA: sidecar mTLS identities (Dapr Sentry) and the ingress certificate
+        tls = manifest.environment.get("tls") or {}
+        self.mtls = _truthy(tls.get("daprMtls", True))
+        self.pki = EnvironmentPki(self.dir / "pki", trust_domain=f"{manifest.name}.local")
         self.apps: dict[str, AppRuntime] = {}
         self.backing: BackingClient | None = None
         self.storage_keys: dict[str, str] = {}
@@ -223,6 +228,10 @@ class EnvironmentController:
         for e in spec.get("env") or []:
             v = secrets.get(e["secretRef"], "") if "secretRef" in e else e.get("value", "")
             env[e["name"]] = "true" if v is True else "false" if v is False else str(v)
+        app_id = (spec.get("dapr") or {}).get("appId") or spec["name"]
+        if self.mtls:
+            w = self.pki.workload(app_id)
+            env.update({"TT_MTLS_CERT": w.cert, "TT_MTLS_KEY": w.key, "TT_MTLS_CA": w.ca})
         for other in self.m.apps:
             if other.get("ingress") is not None:
                 env[f"TT_INTERNAL_URL_{other['name'].upper().replace('-', '_')}"] = \
@@ -291,8 +300,13 @@ class EnvironmentController:
         route = IngressRoute(rt.name, bool(ing.get("external", False)))
         rt.ingress = Ingress(route)
         port = int(ing.get("port") or 0)
-        await rt.ingress.start(port or None, self._ingress_uds(rt.name))
-        self.event("IngressReady", app=rt.name, external=route.external, port=rt.ingress.public_port)
+        tls = None
+        if route.external and str(ing.get("transport", "auto")).lower() != "http":
+            tls = self.pki.server(f"ingress-{rt.name}", [rt.name]).server_context()
+        await rt.ingress.start(port or None, self._ingress_uds(rt.name), tls=tls,
+                               allow_insecure=_truthy(ing.get("allowInsecure", False)))
+        self.event("IngressReady", app=rt.name, external=route.external, port=rt.ingress.public_port,
+                   tls=tls is not None, insecurePort=rt.ingress.insecure_port)
 
     def _refresh_backends(self, rt: AppRuntime) -> None:
         if rt.ingress is None:
@@ -458,7 +472,9 @@ class EnvironmentController:
                 "desiredReplicas": rt.desired, "restarts": rt.restarts,
                 "scale": rt.spec.get("scale"), "lastMetrics": rt.last_metrics, "scaleEvents": rt.scale_events[-20:],
                 "ingress": None if ing is None else {
-                    "external": ing.route.external, "fqdn": f"http://127.0.0.1:{ing.public_port}",
+                    "external": ing.route.external,
+                    "fqdn": f"{'https' if ing.tls else 'http'}://127.0.0.1:{ing.public_port}",
+                    "httpUrl": f"http://127.0.0.1:{ing.insecure_port}" if ing.insecure_port else None,
                     "internalUrl": f"unix:{self._ingress_uds(rt.name)}:", "inflight": ing.route.inflight,
                     "requests": ing.route.requests},
             }
@@ -467,6 +483,7 @@ class EnvironmentController:
                                    "throttledPeriods": st.throttled_periods}
                                for n, st in self.limiter.replicas.items()}}
         return {"name": self.m.name, "envDir": str(self.dir), "backingUrl": self.stack.backing_url,
+                "tls": {"caCert": str(self.pki.ca_crt), "daprMtls": self.mtls},
                 "resourceLimits": limits,
                 "uptimeSeconds": round(time.time() - self.started, 1), "apps": apps,
                 "outputs": self.m.outputs(), "events": self.events[-30:]}

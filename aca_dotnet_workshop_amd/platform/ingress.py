@@ -72,7 +72,10 @@ class Ingress:
         self.http = http or HttpClient()
         self.public: HttpServer | None = None
         self.internal: HttpServer | None = None
+        self.insecure: HttpServer | None = None
         self.public_port: int | None = None
+        self.insecure_port: int | None = None  # plain-HTTP listener next to an HTTPS one
+        self.tls = False
 
     def _app(self, internal_listener: bool) -> WebApp:
         app = WebApp(f"ingress-{self.route.app}")
@@ -100,7 +103,7 @@ class Ingress:
         try:
             headers = [(k, v) for k, v in req.headers.items() if k not in _HOP and not isinstance(v, list)]
             headers.append(("X-Forwarded-For", str(req.client[0]) if isinstance(req.client, tuple) else "local"))
-            headers.append(("X-Forwarded-Proto", "http"))
+            headers.append(("X-Forwarded-Proto", "https" if req.state.get("tls") is not None else "http"))
             last = None
             for b in r.pick()[:3]:
                 try:
@@ -124,16 +127,35 @@ class Ingress:
         finally:
             r.inflight -= 1
 
-    async def start(self, public_port: int | None, internal_uds: str | None) -> None:
+    def _redirect_app(self) -> WebApp:
+        """``allowInsecure: false``: plain HTTP is answered 301 to the HTTPS endpoint (ACA)."""
+        app = WebApp(f"ingress-{self.route.app}-redirect")
+
+        async def redirect(req: Request) -> Response:
+            host = (req.headers.get("host") or "127.0.0.1").rpartition(":")[0] or "127.0.0.1"
+            return Response(b"", 301, [("Location", f"https://{host}:{self.public_port}{req.target}")])
+        for path in ("/{*path}", "/"):
+            app.add_route(path, redirect, ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS"))
+        return app
+
+    async def start(self, public_port: int | None, internal_uds: str | None, tls=None,
+                    allow_insecure: bool = False) -> None:
+        """``tls``: an ``ssl.SSLContext`` -- the public listener serves HTTPS (ACA ingress
+        ``transport: auto`` with a managed certificate) and a second, plain-HTTP listener either
+        redirects (``allowInsecure: false``, the default) or proxies too."""
         loop = asyncio.get_running_loop()
         self.public = HttpServer(self._app(False), loop)
-        self.public_port = await self.public.listen_tcp("127.0.0.1", public_port or 0)
+        self.public_port = await self.public.listen_tcp("127.0.0.1", public_port or 0, ssl=tls)
+        self.tls = tls is not None
+        if tls is not None:
+            self.insecure = HttpServer(self._app(False) if allow_insecure else self._redirect_app(), loop)
+            self.insecure_port = await self.insecure.listen_tcp("127.0.0.1", 0)
         if internal_uds:
             self.internal = HttpServer(self._app(True), loop)
             await self.internal.listen_unix(internal_uds)
 
     async def stop(self) -> None:
-        for s in (self.public, self.internal):
+        for s in (self.public, self.internal, self.insecure):
             if s is not None:
                 await s.close(1.0)
         await self.http.close()

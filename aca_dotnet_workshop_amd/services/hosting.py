@@ -70,29 +70,64 @@ def map_openapi(app: WebApp, path: str = "/openapi/v1.json") -> None:
     app.add_route(path, doc, ("GET",), include_in_schema=False)
 
 
-def parse_urls(urls: str | None) -> list[tuple[str, int]]:
+def parse_urls(urls: str | None) -> list[tuple[str, str, int]]:
+    """``http://+:8080;https://localhost:7112`` -> [(scheme, host, port)]."""
     out = []
     for u in (urls or "").split(";"):
         u = u.strip()
         if not u:
             continue
-        rest = u.split("://", 1)[-1].rstrip("/")
+        scheme, sep, rest = u.partition("://")
+        if not sep:
+            scheme, rest = "http", u
+        rest = rest.rstrip("/")
         host, _, port = rest.rpartition(":")
         if host in ("+", "*", "[::]", "0.0.0.0", ""):
             host = "0.0.0.0"
         elif host == "localhost":
             host = "127.0.0.1"
-        out.append((host, int(port)))
+        out.append((scheme.lower(), host, int(port)))
     return out
 
 
-def listen_addresses(config: Configuration) -> list[tuple[str, int]]:
+def listen_addresses(config: Configuration) -> list[tuple[str, str, int]]:
     urls = config.get_str("urls") or config.get_str("ASPNETCORE_URLS")
     addrs = parse_urls(urls)
     if not addrs:
         port = config.get_int("APP_PORT", config.get_int("PORT", 8080))
-        addrs = [(config.get_str("APP_HOST", "127.0.0.1"), port)]
+        addrs = [("http", config.get_str("APP_HOST", "127.0.0.1"), port)]
     return addrs
+
+
+def https_certificate(config: Configuration) -> tuple[str, str]:
+    """Kestrel's default certificate: ``Kestrel:Certificates:Default:Path/KeyPath`` when
+    configured, else a development certificate for localhost (``dotnet dev-certs https``
+    equivalent), issued once under ``TT_DEV_CERTS_DIR`` (default ``~/.tt-dev-certs``)."""
+    cert = config.get_str("Kestrel:Certificates:Default:Path")
+    key = config.get_str("Kestrel:Certificates:Default:KeyPath")
+    if cert and key:
+        return cert, key
+    from ..platform.pki import EnvironmentPki
+    d = config.get_str("TT_DEV_CERTS_DIR") or os.path.join(os.path.expanduser("~"), ".tt-dev-certs")
+    pair = EnvironmentPki(d, trust_domain="localhost-dev").server("aspnetcore-dev")
+    return pair.cert, pair.key
+
+
+def https_redirect_app(https_port: int) -> WebApp:
+    """``app.UseHttpsRedirection()`` (reference Backend.Api/Program.cs:26): every request on the
+    plain-HTTP endpoint is answered 307 Temporary Redirect to the HTTPS one."""
+    app = WebApp("https-redirection")
+
+    async def redirect(req) -> Response:
+        host = req.headers.get("host") or "localhost"
+        if host.startswith("["):  # [v6]:port
+            host = host[:host.find("]") + 1]
+        elif ":" in host:
+            host = host.rpartition(":")[0]
+        return Response(b"", 307, [("Location", f"https://{host}:{https_port}{req.target}")])
+    app.add_route("/{*path}", redirect, ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS"))
+    app.add_route("/", redirect, ("GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS"))
+    return app
 
 
 def tune_gc(environ: dict[str, str] | None = None) -> bool:
@@ -119,8 +154,30 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
     srv = native_host.NativeHttpServer(app, loop) if native_host.enabled(part="server") else HttpServer(app, loop)
     await app.startup()
     ports = []
-    for host, port in listen_addresses(config):
-        ports.append(await srv.listen_tcp(host, port))
+    addrs = listen_addresses(config)
+    extra: list[HttpServer] = []
+    https_port = None
+    for scheme, host, port in addrs:  # HTTPS endpoints first: the redirect needs their port
+        if scheme != "https":
+            continue
+        cert, key = https_certificate(config)
+        if isinstance(srv, HttpServer):
+            from ..platform.pki import CertPair
+            p = await srv.listen_tcp(host, port, ssl=CertPair(cert, key, "").server_context())
+        else:
+            p = await srv.listen_tcp(host, port, tls_files=(cert, key))
+        https_port = https_port or p
+        ports.append(p)
+    redirect = https_port is not None and config.get_bool("HttpsRedirection:Enabled", True)
+    for scheme, host, port in addrs:
+        if scheme == "https":
+            continue
+        if redirect:  # UseHttpsRedirection: the HTTP endpoint only redirects
+            r = HttpServer(https_redirect_app(https_port), loop)
+            ports.append(await r.listen_tcp(host, port))
+            extra.append(r)
+        else:
+            ports.append(await srv.listen_tcp(host, port))
     uds = config.get_str("TT_APP_UDS")
     if uds:
         await srv.listen_unix(uds)
@@ -140,6 +197,8 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
         Path(tmp).write_text(str(ports[0]) if ports else "0")
         os.replace(tmp, port_file)
     await stop.wait()
+    for r in extra:
+        await r.close()
     await srv.close()
     await app.shutdown()
 

@@ -50,6 +50,12 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--enable-api-logging", action="store_true",
                    help="log every sidecar API call (Dapr's enableApiLogging)")
     r.add_argument("--replica-name", default=os.environ.get("TT_REPLICA_NAME"))
+    r.add_argument("--app-ssl", action="store_true", default=os.environ.get("TT_APP_SSL", "") in ("1", "true"),
+                   help="the app serves HTTPS on --app-port (its certificate is not verified, as in Dapr)")
+    r.add_argument("--mtls-cert", default=os.environ.get("TT_MTLS_CERT"),
+                   help="workload certificate for mutual TLS with peer sidecars (with --mtls-key/--mtls-ca)")
+    r.add_argument("--mtls-key", default=os.environ.get("TT_MTLS_KEY"))
+    r.add_argument("--mtls-ca", default=os.environ.get("TT_MTLS_CA"))
     r.add_argument("command", nargs=argparse.REMAINDER, help="-- <app command>")
     return ap
 
@@ -70,7 +76,9 @@ async def _run(a: argparse.Namespace) -> int:
                  app_token=os.environ.get("APP_API_TOKEN"), mesh_token=os.environ.get("TT_MESH_TOKEN"),
                  app_max_concurrency=a.app_max_concurrency, identity=a.identity, backing_url=a.backing_url,
                  instance=a.replica_name, app_health_path=a.app_health_check_path,
-                 api_logging=a.enable_api_logging, grpc_port=a.dapr_grpc_port,
+                 api_logging=a.enable_api_logging, grpc_port=a.dapr_grpc_port, app_ssl=a.app_ssl,
+                 mtls={"cert": a.mtls_cert, "key": a.mtls_key, "ca": a.mtls_ca}
+                 if a.mtls_cert and a.mtls_key and a.mtls_ca else None,
                  grpc_uds=os.path.join(a.unix_socket_dir, f"{tag}.g.sock") if a.unix_socket_dir and a.dapr_grpc_port is not None
                  else None)
     await sc.start()

@@ -79,7 +79,8 @@ class Sidecar:
                  identity: str | None = None, backing_url: str | None = None, environ: dict[str, str] | None = None,
                  telemetry_dir: str | None = None, instance: str | None = None,
                  app_health_path: str | None = None, data_plane: str | None = None,
-                 api_logging: bool = False, grpc_port: int | None = None, grpc_uds: str | None = None) -> None:
+                 api_logging: bool = False, grpc_port: int | None = None, grpc_uds: str | None = None,
+                 mtls: dict[str, str] | None = None, app_ssl: bool | None = None) -> None:
         self.app_id = app_id
         self.app_port = app_port
         self.app_uds = app_uds
@@ -104,7 +105,27 @@ class Sidecar:
         self.grpc_server = None
         self.bound_grpc_port: int | None = None
         self.extended_metadata: dict[str, str] = {}
-        self.http = HttpClient(timeout=300)
+        # mutual TLS between sidecars (Dapr Sentry equivalent): this app-id's workload certificate
+        # from the environment CA (platform/pki.py), presented and required on the internal endpoint
+        env_mtls = {k: self.environ.get(f"TT_MTLS_{k.upper()}", "") for k in ("cert", "key", "ca")}
+        self.mtls = mtls or (env_mtls if all(env_mtls.values()) else None)
+        # --app-ssl: the app serves HTTPS (its own dev certificate, not verified -- Dapr's behaviour)
+        self.app_ssl = bool(app_ssl) if app_ssl is not None else self.environ.get("TT_APP_SSL", "") in ("1", "true")
+        self._mesh_server_tls = None
+        mesh_client_tls = None
+        if self.mtls:
+            from ..platform.pki import CertPair
+            pair = CertPair(self.mtls["cert"], self.mtls["key"], self.mtls["ca"])
+            self._mesh_server_tls = pair.server_context(require_client_cert=True)
+            mesh_client_tls = pair.client_context()
+        self.http = HttpClient(timeout=300, tls=mesh_client_tls)
+        self.app_http = self.http
+        if self.app_ssl:
+            import ssl
+            insecure = ssl.SSLContext(ssl.PROTOCOL_TLS_CLIENT)
+            insecure.check_hostname = False
+            insecure.verify_mode = ssl.CERT_NONE
+            self.app_http = HttpClient(timeout=300, tls=insecure)
         kw: dict[str, Any] = {"app_id": app_id, "identity": identity, "http": self.http, "environ": self.environ}
         if backing_url:
             kw["backing_url"] = backing_url
@@ -173,13 +194,16 @@ class Sidecar:
             await srv.listen_unix(self.uds)
         self._servers.append(srv)
         isrv = HttpServer(internal, loop)
+        tls = self._mesh_server_tls
         if self.internal_uds:
-            await isrv.listen_unix(self.internal_uds)
+            await isrv.listen_unix(self.internal_uds, ssl=tls)
             self.bound_internal = f"unix:{self.internal_uds}:"
         if self.internal_port is not None and (self.internal_port or not self.internal_uds):
-            p = await isrv.listen_tcp("127.0.0.1", self.internal_port)
+            p = await isrv.listen_tcp("127.0.0.1", self.internal_port, ssl=tls)
             if self.bound_internal is None:
                 self.bound_internal = f"http://127.0.0.1:{p}"
+        if tls is not None and self.bound_internal:
+            self.bound_internal = f"mtls:{self.app_id}@{self.bound_internal}"
         self._servers.append(isrv)
 
     def data_plane_config(self, fallback: str) -> dict[str, Any]:
@@ -211,13 +235,13 @@ class Sidecar:
         if self.app_uds:
             app = "unix:" + self.app_uds
         elif self.app_port is not None:
-            app = f"tcp:127.0.0.1:{self.app_port}"
+            app = f"https+insecure://127.0.0.1:{self.app_port}" if self.app_ssl else f"tcp:127.0.0.1:{self.app_port}"
         ex = self.tracer.exporter
         return {"appId": self.app_id, "app": app, "appToken": self.app_token, "apiToken": self.api_token,
                 "meshToken": self.mesh_token, "registryDir": str(self.resolver.dir) if self.resolver.dir else None,
                 "fallback": fallback, "invokeNative": self.resolver.dir is not None, "appTimeout": 300.0,
                 "listen": listen, "internal": internal, "stores": stores, "pubsubs": buses,
-                "apiLogging": self.api_logging,
+                "apiLogging": self.api_logging, **({"mtls": dict(self.mtls)} if self.mtls else {}),
                 "trace": {"dir": ex.directory, "sampleRate": self.tracer.sample_rate, "role": self.tracer.role,
                           "instance": self.instance}}
 
@@ -293,6 +317,8 @@ class Sidecar:
                     pass
         self.tracer.flush()
         await self.http.close()
+        if self.app_http is not self.http:
+            await self.app_http.close()
 
     # ================================================================ components
     async def _load_components(self) -> None:
@@ -354,7 +380,7 @@ class Sidecar:
     def app_base(self) -> str:
         if self.app_uds:
             return f"unix:{self.app_uds}:"
-        return f"http://127.0.0.1:{self.app_port}"
+        return f"{'https' if self.app_ssl else 'http'}://127.0.0.1:{self.app_port}"
 
     async def call_app(self, method: str, path: str, headers: list[tuple[str, str]], body: bytes,
                        timeout: float | None = None):
@@ -362,9 +388,9 @@ class Sidecar:
             headers = headers + [("dapr-api-token", self.app_token)]
         url = self.app_base() + "/" + path.lstrip("/")
         if self.app_sem is None:
-            return await self.http.request(method, url, headers=headers, body=body, timeout=timeout)
+            return await self.app_http.request(method, url, headers=headers, body=body, timeout=timeout)
         async with self.app_sem:
-            return await self.http.request(method, url, headers=headers, body=body, timeout=timeout)
+            return await self.app_http.request(method, url, headers=headers, body=body, timeout=timeout)
 
     async def _wait_for_app(self, timeout: float = 120.0) -> None:
         deadline = time.monotonic() + timeout
@@ -376,7 +402,7 @@ class Sidecar:
                     r, w = await asyncio.wait_for(asyncio.open_connection("127.0.0.1", self.app_port), 1.0)
                 w.close()
                 if self.app_health_path:
-                    resp = await self.http.request("GET", self.app_base() + self.app_health_path, timeout=2.0)
+                    resp = await self.app_http.request("GET", self.app_base() + self.app_health_path, timeout=2.0)
                     if resp.status >= 300:
                         raise ConnectionError("app not healthy yet")
                 return
@@ -698,6 +724,12 @@ class Sidecar:
         raise last or ConnectionError("no reachable replica")
 
     async def h_internal(self, req: Request) -> Response:
+        if self.mtls:
+            # the caller's workload certificate must name the app-id it claims (no spoofing)
+            caller = req.headers.get("dapr-caller-app-id")
+            peer = (req.state.get("tls") or {}).get("peer")
+            if peer is None or (caller and caller not in peer):
+                return err(403, "ERR_MESH_AUTH", "caller identity not proven by its mTLS certificate")
         if self.mesh_token and req.headers.get("tt-mesh-token") != self.mesh_token:
             return err(403, "ERR_MESH_AUTH", "sidecar-to-sidecar call not authenticated")
         parent = parse_traceparent(req.headers.get("traceparent"))

@@ -144,7 +144,20 @@ _SWEEP_S = 0.1  # timeout resolution (per-request TimerHandles cost ~5 us each o
 
 
 def parse_endpoint(url: str) -> tuple[Any, str]:
-    """Split ``url`` into (endpoint key, request target)."""
+    """Split ``url`` into (endpoint key, request target).
+
+    ``unix:/path.sock:/target`` | ``http://host:port/target`` | ``https://host:port/target`` |
+    ``mtls:<peer-name>@<one of the above>`` -- mutual TLS to a peer whose certificate must carry
+    ``<peer-name>`` (the app-id of a sidecar: environment PKI, platform/pki.py)."""
+    if url.startswith("mtls:"):
+        name, _, rest = url[5:].partition("@")
+        inner, target = parse_endpoint(rest)
+        if inner[0] == "tls":
+            inner = inner[2]
+        return ("tls", name, inner), target
+    if url.startswith("https://"):
+        inner, target = parse_endpoint("http://" + url[8:])
+        return ("tls", inner[1], inner), target
     if url.startswith("unix:"):
         # unix:/path/to.sock:/request/target
         rest = url[5:]
@@ -161,7 +174,11 @@ def parse_endpoint(url: str) -> tuple[Any, str]:
 
 
 class HttpClient:
-    def __init__(self, max_idle_per_host: int = 256, timeout: float = DEFAULT_TIMEOUT) -> None:
+    def __init__(self, max_idle_per_host: int = 256, timeout: float = DEFAULT_TIMEOUT,
+                 tls: "ssl.SSLContext | None" = None) -> None:
+        """``tls``: context for ``https://`` / ``mtls:`` endpoints (client certificate for mutual
+        TLS, trusted CA); default: the system trust store."""
+        self.tls = tls
         self._idle: dict[Any, deque[_Conn]] = {}
         self.max_idle = max_idle_per_host
         self.timeout = timeout
@@ -188,6 +205,18 @@ class HttpClient:
 
     async def _connect(self, key: Any) -> _Conn:
         loop = asyncio.get_running_loop()
+        if key[0] == "tls":
+            if self.tls is None:
+                import ssl
+                self.tls = ssl.create_default_context()
+            inner = key[2]
+            if inner[0] == "unix":
+                _, conn = await loop.create_unix_connection(lambda: _Conn(key), inner[1], ssl=self.tls,
+                                                            server_hostname=key[1])
+            else:
+                _, conn = await loop.create_connection(lambda: _Conn(key), inner[1], inner[2], ssl=self.tls,
+                                                       server_hostname=key[1])
+            return conn
         if key[0] == "unix":
             _, conn = await loop.create_unix_connection(lambda: _Conn(key), key[1])
         else:
@@ -227,7 +256,8 @@ class HttpClient:
         if isinstance(body, str):
             body = body.encode()
         body = body or b""
-        host = key[1] if key[0] == "tcp" else "localhost"
+        inner = key[2] if key[0] == "tls" else key
+        host = f"{inner[1]}:{inner[2]}" if inner[0] == "tcp" else "localhost"
         lines = [f"{method} {target} HTTP/1.1", f"Host: {host}"]
         for k, v in hdrs:
             lk = k.lower()

@@ -235,10 +235,12 @@ class NativeHttpServer:
         self.ports: list[int] = []
 
     async def listen_tcp(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
-                         sock=None) -> int:
+                         sock=None, tls_files: tuple[str, str] | None = None) -> int:
+        """``tls_files``: (certificate, key) PEM paths -- HTTPS, terminated on the I/O thread."""
         if sock is not None:
             raise ValueError("NativeHttpServer binds its own sockets")
-        p = self.host.h.listen(self.sid, f"tcp:{host}:{port}")
+        cert, key = tls_files or ("", "")
+        p = self.host.h.listen(self.sid, f"tcp:{host}:{port}", cert, key)
         self.ports.append(p)
         return p
 

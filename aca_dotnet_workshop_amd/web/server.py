@@ -14,7 +14,7 @@ import logging
 import os
 import socket
 from collections import deque
-from typing import Awaitable, Callable
+from typing import Any, Awaitable, Callable
 
 from .http import Headers, Request, Response, encode_response, problem
 
@@ -120,7 +120,7 @@ class _ChunkedDecoder:
 
 
 class HttpServerProtocol(asyncio.Protocol):
-    __slots__ = ("server", "transport", "buf", "pending", "queue", "worker", "closed", "peer", "_paused")
+    __slots__ = ("server", "transport", "buf", "pending", "queue", "worker", "closed", "peer", "_paused", "tls")
 
     def __init__(self, server: "HttpServer") -> None:
         self.server = server
@@ -132,10 +132,16 @@ class HttpServerProtocol(asyncio.Protocol):
         self.closed = False
         self.peer = None
         self._paused = False
+        self.tls = None
 
     def connection_made(self, transport: asyncio.BaseTransport) -> None:
         self.transport = transport  # type: ignore[assignment]
         self.peer = transport.get_extra_info("peername")
+        # TLS connection: {"peer": [names in the client certificate's SAN]} (mutual TLS identity)
+        self.tls = None
+        if transport.get_extra_info("ssl_object") is not None:
+            cert = transport.get_extra_info("peercert") or {}
+            self.tls = {"peer": [v for _, v in cert.get("subjectAltName", ())]}
         sock = transport.get_extra_info("socket")
         if sock is not None and sock.family in (socket.AF_INET, socket.AF_INET6):
             try:
@@ -195,6 +201,8 @@ class HttpServerProtocol(asyncio.Protocol):
                 del buf[:length]
             self.pending = None
             req = Request(method, target, headers, body, self.peer, version)
+            if self.tls is not None:
+                req.state["tls"] = self.tls
             self.queue.append(req)
             if self.worker is None or self.worker.done():
                 self.worker = self.server.loop.create_task(self._drain())
@@ -242,22 +250,24 @@ class HttpServer:
         self.sockets: list[socket.socket] = []
 
     async def listen_tcp(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
-                         sock: socket.socket | None = None) -> int:
+                         sock: socket.socket | None = None, ssl: Any = None) -> int:
+        """``ssl``: an ``ssl.SSLContext`` serves HTTPS (Kestrel's https endpoint); with
+        ``verify_mode = CERT_REQUIRED`` clients must present a certificate (mutual TLS)."""
         if sock is not None:
-            srv = await self.loop.create_server(lambda: HttpServerProtocol(self), sock=sock, backlog=1024)
+            srv = await self.loop.create_server(lambda: HttpServerProtocol(self), sock=sock, backlog=1024, ssl=ssl)
         else:
             srv = await self.loop.create_server(lambda: HttpServerProtocol(self), host, port,
                                                 reuse_address=True, reuse_port=reuse_port or None,
-                                                backlog=1024)
+                                                backlog=1024, ssl=ssl)
         self._servers.append(srv)
         s = srv.sockets[0]
         self.sockets.append(s)
         return s.getsockname()[1]
 
-    async def listen_unix(self, path: str) -> str:
+    async def listen_unix(self, path: str, ssl: Any = None) -> str:
         if os.path.exists(path):
             os.unlink(path)
-        srv = await self.loop.create_unix_server(lambda: HttpServerProtocol(self), path, backlog=1024)
+        srv = await self.loop.create_unix_server(lambda: HttpServerProtocol(self), path, backlog=1024, ssl=ssl)
         self._servers.append(srv)
         return path
 

@@ -162,6 +162,8 @@ def main() -> None:
     ap.add_argument("--polling", type=float, default=0.5)
     ap.add_argument("--cooldown", type=float, default=3.0)
     ap.add_argument("--skip-scale", action="store_true")
+    ap.add_argument("--mtls", action="store_true",
+                    help="sidecar-to-sidecar mutual TLS (per-app-id certificates from an environment CA)")
     a = ap.parse_args()
     from aca_dotnet_workshop_amd.native.build import build_dataplane, build_native
     from aca_dotnet_workshop_amd.platform.processes import LocalStack
@@ -171,14 +173,23 @@ def main() -> None:
     stack = LocalStack(env={"TT_TRACE_SAMPLE_RATE": "0.01"})
     try:
         backing = stack.start_backing()
-        stack.start_replica("tasksmanager-backend-api", cfg)
-        stack.start_replica("tasksmanager-backend-processor", cfg)
+
+        def tls_env(app_id: str) -> dict[str, str]:
+            if not a.mtls:
+                return {}
+            from aca_dotnet_workshop_amd.platform.pki import EnvironmentPki
+            w = EnvironmentPki(stack.root / "pki").workload(app_id)
+            return {"TT_MTLS_CERT": w.cert, "TT_MTLS_KEY": w.key, "TT_MTLS_CA": w.ca}
+        stack.start_replica("tasksmanager-backend-api", cfg, extra_env=tls_env("tasksmanager-backend-api"))
+        stack.start_replica("tasksmanager-backend-processor", cfg, extra_env=tls_env("tasksmanager-backend-processor"))
         stack.start_replica("tasksmanager-frontend-webapp",
-                            {**cfg, "BackendApiConfig:BaseUrlExternalHttp": "http://127.0.0.1:9"})
+                            {**cfg, "BackendApiConfig:BaseUrlExternalHttp": "http://127.0.0.1:9"},
+                            extra_env=tls_env("tasksmanager-frontend-webapp"))
         stack.wait_ready()
         crud, pubsub = asyncio.run(crud_and_pubsub(stack, backing, a.ops, a.events))
     finally:
         stack.stop()
+    crud["sidecar_mtls"] = a.mtls
     print(json.dumps(crud), flush=True)
     print(json.dumps(pubsub), flush=True)
     if not a.skip_scale:

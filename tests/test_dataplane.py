@@ -66,8 +66,9 @@ def _app(name, seen):
 class Env:
     """Backing services + N (app, sidecar) pairs sharing a registry directory."""
 
-    def __init__(self, plane, tmp_path, apps=("app-a",), **sc_kw):
+    def __init__(self, plane, tmp_path, apps=("app-a",), pki=None, **sc_kw):
         self.plane, self.tmp, self.names, self.sc_kw = plane, tmp_path, apps, sc_kw
+        self.pki = pki  # platform.pki.EnvironmentPki: mutual TLS between the sidecars
         self.seen = {n: [] for n in apps}
 
     async def __aenter__(self):
@@ -84,7 +85,8 @@ class Env:
             self.servers.append(srv)
             sc = Sidecar(n, app_port=port, http_port=0, components=[STORE, BUS, MEM],
                          resolver=NameResolver(str(self.tmp / "registry")), backing_url=self.burl,
-                         internal_uds=str(self.tmp / f"{n}.i.sock"), data_plane=self.plane, **self.sc_kw)
+                         internal_uds=str(self.tmp / f"{n}.i.sock"), data_plane=self.plane,
+                         mtls=self.pki.workload(n).as_config() if self.pki else None, **self.sc_kw)
             await sc.start()
             await asyncio.wait_for(sc.app_ready.wait(), 10)
             assert sc.active_data_plane == self.plane
@@ -468,4 +470,55 @@ def test_state_throttling_is_retried(plane, tmp_path):
             assert ts["throttled"] >= 1 and ts["ru_consumed"] >= 100
             r = await e.http.get(f"{b}/v1.0/state/statestore/k19")
             assert r.status == 200 and r.json() == {"i": 19}
+    run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_sidecar_mutual_tls(plane, tmp_path):
+    """Sidecar-to-sidecar calls over mutual TLS with per-app-id workload certificates from the
+    environment CA (Dapr Sentry equivalent): invocation works; a peer without a certificate, with
+    one from another CA, or claiming another app-id than its certificate names is rejected."""
+    import ssl
+
+    from aca_dotnet_workshop_amd.platform.pki import EnvironmentPki
+
+    pki = EnvironmentPki(tmp_path / "pki")
+    rogue = EnvironmentPki(tmp_path / "rogue-pki")
+
+    async def main():
+        async with Env(plane, tmp_path, apps=("app-a", "app-b"), pki=pki) as e:
+            ep = e.sidecars["app-b"].bound_internal
+            assert ep.startswith("mtls:app-b@")
+            r = await e.http.post(f"{e.base['app-a']}/v1.0/invoke/app-b/method/api/echo/x", body=b"hi")
+            assert r.status == 201 and r.json()["app"] == "app-b" and r.json()["body"] == "hi"
+            sock = ep.split("@", 1)[1][len("unix:"):].rstrip(":")
+
+            async def raw(ctx, caller="app-a"):
+                rd, wr = await asyncio.open_unix_connection(sock, ssl=ctx, server_hostname="app-b")
+                wr.write(f"GET /api/echo/y HTTP/1.1\r\nHost: x\r\ndapr-caller-app-id: {caller}\r\n"
+                         "Connection: close\r\n\r\n".encode())
+                data = await rd.read()
+                wr.close()
+                return data
+            # a legitimate peer identity (app-a's workload certificate) gets through
+            ok = await raw(pki.workload("app-a").client_context())
+            assert ok.startswith(b"HTTP/1.1 201"), ok[:100]
+            # ... but may not claim to be someone else
+            spoof = await raw(pki.workload("app-a").client_context(), caller="app-c")
+            assert spoof.startswith(b"HTTP/1.1 403") and b"ERR_MESH_AUTH" in spoof
+            # no client certificate / a certificate from another CA: the handshake fails
+            for ctx in (pki.workload("app-a").client_context(present_cert=False),
+                        rogue.workload("app-a").client_context()):
+                if ctx is not None and ctx.verify_mode == ssl.CERT_REQUIRED and ctx is not None:
+                    ctx.load_verify_locations(pki.ca_crt)  # trust the real server, present whatever
+                try:
+                    got = await raw(ctx)
+                except (ssl.SSLError, ConnectionError, asyncio.IncompleteReadError):
+                    got = b""
+                assert not got.startswith(b"HTTP/1.1 2"), got[:100]
+            # the server side is verified too: a client trusting only another CA refuses app-b
+            bad = ssl.SSLContext(ssl.PROTOCOL_TLS_CLIENT)
+            bad.load_verify_locations(rogue.ca_crt)
+            with pytest.raises(ssl.SSLError):
+                await raw(bad)
     run(main())

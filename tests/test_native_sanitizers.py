@@ -19,7 +19,8 @@ def _build_and_run(tmp_path, flags, env_extra, args=("8", "1500")):
     if shutil.which(CXX) is None:
         pytest.skip("no C++ compiler")
     exe = tmp_path / "stress"
-    cmd = [CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(SRC), "-o", str(exe), "-lpthread"]
+    cmd = [CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(SRC), "-o", str(exe), "-lpthread",
+           "-lssl", "-lcrypto"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0 and "sanitize" in r.stderr and "cannot find" in r.stderr:
         pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
@@ -54,7 +55,8 @@ def test_dataplane_under_address_sanitizer(tmp_path):
     exe = tmp_path / "ttsidecar-dataplane-asan"
     src = ROOT / "aca_dotnet_workshop_amd" / "native" / "src" / "dataplane.cpp"
     r = subprocess.run([CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-                        "-fno-sanitize-recover=undefined", str(src), "-o", str(exe)], capture_output=True, text=True)
+                        "-fno-sanitize-recover=undefined", str(src), "-o", str(exe), "-lssl", "-lcrypto"],
+                       capture_output=True, text=True)
     if r.returncode != 0 and "cannot find" in r.stderr:
         pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
     assert r.returncode == 0, r.stderr[-3000:]
@@ -81,7 +83,7 @@ def test_app_host_under_sanitizers(tmp_path, flags, env):
     src = ROOT / "aca_dotnet_workshop_amd" / "native" / "tests" / "apphost_stress.cpp"
     exe = tmp_path / "apphost_stress"
     r = subprocess.run([CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", *flags, str(src), "-o", str(exe),
-                        "-lpthread"], capture_output=True, text=True)
+                        "-lpthread", "-lssl", "-lcrypto"], capture_output=True, text=True)
     if r.returncode != 0 and "cannot find" in r.stderr:
         pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
     assert r.returncode == 0, r.stderr[-3000:]

@@ -10,6 +10,7 @@ import re
 import signal
 import time
 import urllib.error
+import urllib.parse
 import urllib.request
 from pathlib import Path
 
@@ -113,16 +114,49 @@ def test_environment_lifecycle(tmp_path):
             with pytest.raises(urllib.error.HTTPError) as ei:
                 await asyncio.to_thread(_get, api["fqdn"] + "/api/tasks?createdBy=x")
             assert ei.value.code == 403
-            r = await asyncio.to_thread(_get, fe["fqdn"] + "/")
+            # external ingress: HTTPS with the environment CA's certificate; plain HTTP -> 301
+            import ssl
+            assert fe["fqdn"].startswith("https://")
+            tls = ssl.create_default_context(cafile=st["tls"]["caCert"])
+            r = await asyncio.to_thread(_get, fe["fqdn"] + "/", context=tls)
             assert r.status == 200
-            # the frontend -> API -> state store path works under RBAC (managed identities)
+            noredir = urllib.request.build_opener(_NoRedirect)
+            r = await asyncio.to_thread(noredir.open, fe["httpUrl"] + "/Tasks/Index")
+            assert r.status == 301 and r.headers["Location"] == fe["fqdn"] + "/Tasks/Index"
+            with pytest.raises(urllib.error.URLError):  # not trusted without the environment CA
+                await asyncio.to_thread(_get, fe["fqdn"] + "/")
+            # the frontend -> API -> state store path works under RBAC (managed identities), the
+            # sidecars talk mutual TLS (per-app-id workload certificates)
             data = b"TasksCreatedBy=env%40test"
             req = urllib.request.Request(fe["fqdn"] + "/", data=data, method="POST",
                                          headers={"Content-Type": "application/x-www-form-urlencoded"})
-            opener = urllib.request.build_opener(_NoRedirect)
+            opener = urllib.request.build_opener(_NoRedirect, urllib.request.HTTPSHandler(context=tls))
             resp = await asyncio.to_thread(opener.open, req)
             assert resp.status == 302
+            # create + list through frontend -> (sidecar mTLS) -> API -> state store
+            cookie = resp.headers["Set-Cookie"].split(";", 1)[0]
+            req = urllib.request.Request(fe["fqdn"] + "/Tasks/Create", headers={"Cookie": cookie})
+            r = await asyncio.to_thread(opener.open, req)
+            af = re.search(r"\.AspNetCore\.Antiforgery=([0-9a-f]+)", r.headers["Set-Cookie"]).group(1)
+            token = re.search(r'name="__RequestVerificationToken" value="([0-9a-f]+)"', r.read().decode()).group(1)
+            cookie += f"; .AspNetCore.Antiforgery={af}"
+            form = urllib.parse.urlencode({"__RequestVerificationToken": token, "TaskAdd.TaskName": "via mtls",
+                                           "TaskAdd.TaskAssignedTo": "a@x", "TaskAdd.TaskDueDate": "2030-01-01"}).encode()
+            req = urllib.request.Request(fe["fqdn"] + "/Tasks/Create", data=form, method="POST",
+                                         headers={"Content-Type": "application/x-www-form-urlencoded",
+                                                  "Cookie": cookie})
+            assert (await asyncio.to_thread(opener.open, req)).status == 302
+            req = urllib.request.Request(fe["fqdn"] + "/Tasks/Index", headers={"Cookie": cookie})
+            page = (await asyncio.to_thread(opener.open, req)).read().decode()
+            assert "via mtls" in page
+            regs = [json.loads(f.read_text()) for f in (tmp_path / "env" / "runtime" / "registry").glob("*/*.json")]
+            assert regs and all(r["endpoint"].startswith(f"mtls:{r['appId']}@") for r in regs)
             b = ctl.backing
+            entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
+            for _ in range(100):  # the created task's tasksaved event is delivered first
+                if (await b.sb_counts("taskstracker", entity))["completed"] == 1:
+                    break
+                await asyncio.sleep(0.1)
             # module 9: burst on the topic scales the processor out, then back in after the cooldown
             def ce(i):
                 return json.dumps({"specversion": "1.0", "id": f"x{i}", "source": "t", "type": "t",
@@ -137,10 +171,10 @@ def test_environment_lifecycle(tmp_path):
                 await asyncio.sleep(0.1)
                 peak = max(peak, len([r for r in proc.current.replicas if r.alive()]))
                 c = await b.sb_counts("taskstracker", "tasksavedtopic/subscriptions/tasksmanager-backend-processor")
-                if c["completed"] >= 800 and peak > 1:
+                if c["completed"] >= 801 and peak > 1:
                     break
             assert peak == 5
-            assert c["completed"] == 800 and c["dead_letter"] == 0
+            assert c["completed"] == 801 and c["dead_letter"] == 0
             # competing consumers across the 5 replicas: every message handled, none twice
             # (the processor logs each delivery it starts; no lock expired, so no redelivery)
             seen = collections.Counter()
@@ -221,6 +255,8 @@ class _NoRedirect(urllib.request.HTTPRedirectHandler):
 
     def http_error_302(self, req, fp, code, msg, headers):
         return fp
+
+    http_error_301 = http_error_302
 
 
 def test_ingress_never_replays_a_post_after_a_mid_request_failure():
