@@ -78,7 +78,7 @@ DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
 
 
 def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
-    sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
+    sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "h2.hpp", SRC / "pb.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
                SRC / "textutil.hpp"]
     return _build_exe(DATAPLANE, SRC / "dataplane.cpp", sources, force, verbose)
 

@@ -33,6 +33,7 @@
 #include <thread>
 
 #include "evhttp.hpp"
+#include "h2.hpp"
 
 namespace tt::apphost {
 
@@ -139,6 +140,7 @@ class AppHost {
   // one wake-up of the loop thread.
   struct Op {
     bool is_request = false;
+    bool is_grpc = false;  // a unary gRPC call: target = ":path", headers = metadata, body = message
     uint64_t id = 0;  // reply token or client request id
     int status = 0;
     std::string endpoint, method, target;
@@ -167,6 +169,26 @@ class AppHost {
           continue;
         }
         uint64_t id = op.id;
+        if (op.is_grpc) {
+          // RESPONSE: status = grpc-status, headers = metadata + grpc-message, body = message
+          grpc_.call(ev::Endpoint::parse(op.endpoint), std::move(op.target), op.headers, op.body, op.timeout_s,
+                     [this, id](h2::GrpcResult&& r) {
+                       Event e;
+                       e.id = id;
+                       if (r.err) {
+                         e.kind = Event::ERROR;
+                         e.err = r.err;
+                       } else {
+                         e.kind = Event::RESPONSE;
+                         e.msg.status = r.status;
+                         e.msg.headers = std::move(r.metadata);
+                         e.msg.headers.emplace_back("grpc-message", std::move(r.message));
+                         e.msg.body = std::move(r.payload);
+                       }
+                       emit(std::move(e));
+                     });
+          continue;
+        }
         client_.request(ev::Endpoint::parse(op.endpoint), op.method, op.target, op.headers, op.body, op.timeout_s,
                         [this, id](ev::ClientResult&& r) {
                           Event e;
@@ -211,6 +233,7 @@ class AppHost {
 
   ev::Loop loop_;
   ev::Client client_{loop_};
+  h2::GrpcClient grpc_{loop_};
   FILE* trace_ = nullptr;
 
   void note(const char* what, double ms, size_t n = 0) {

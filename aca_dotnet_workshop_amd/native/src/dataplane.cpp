@@ -35,7 +35,9 @@
 #include <sstream>
 
 #include "evhttp.hpp"
+#include "h2.hpp"
 #include "json.hpp"
+#include "pb.hpp"
 #include "textutil.hpp"
 
 using namespace tt;
@@ -1360,6 +1362,381 @@ class DataPlane {
                     });
     return true;
   }
+
+  // ---------------------------------------------------------------- gRPC API
+  // dapr.proto.runtime.v1.Dapr over HTTP/2 (h2.hpp): the hot unary RPCs of the reference's
+  // DaprClient -- SaveState / GetState / DeleteState / QueryStateAlpha1 / PublishEvent /
+  // InvokeService / InvokeBinding (Backend.Api Services/TasksStoreManager.cs:35-155, Processor
+  // ExternalTasksProcessorController.cs:33-43) -- are decoded here and run through on_api as
+  // the equivalent HTTP API request, so both protocols share one implementation of the
+  // semantics (ETags, key prefixes, CloudEvents, tracing, API token).  Every other RPC goes to
+  // the control plane's /_tt/grpc/{Method} route, which runs sidecar/grpc_api.py's handler for
+  // it.  Errors map HTTP statuses onto gRPC codes exactly like grpc_api.py (_CODES, _fail).
+ public:
+  h2::GrpcHandler grpc_handler() {
+    return [this](h2::GrpcCall&& c, h2::GrpcReply r) { on_grpc(std::move(c), std::move(r)); };
+  }
+
+ private:
+  static int grpc_code(int http) {
+    switch (http) {
+      case 400: return 3;   // INVALID_ARGUMENT
+      case 401: return 16;  // UNAUTHENTICATED
+      case 403: return 7;   // PERMISSION_DENIED
+      case 404: return 5;   // NOT_FOUND
+      case 405: case 501: return 12;  // UNIMPLEMENTED
+      case 409: return 10;  // ABORTED
+      case 429: return 8;   // RESOURCE_EXHAUSTED
+      case 500: return 13;  // INTERNAL
+      case 502: case 503: return 14;  // UNAVAILABLE
+      case 504: return 4;   // DEADLINE_EXCEEDED
+      default: return http >= 400 ? 2 : 0;  // UNKNOWN
+    }
+  }
+  static void grpc_fail(const h2::GrpcReply& r, int status, std::string_view body, const std::string& what) {
+    std::string msg;
+    try {
+      Value js = parse(body);
+      if (js.t == Value::Object) {
+        const Value* c = js.get("errorCode");
+        const Value* m = js.get("message");
+        msg = (c && c->t == Value::String ? c->s : std::string()) + ": " +
+              (m && m->t == Value::String ? m->s : dump(js));
+      } else {
+        msg = dump(js);
+      }
+    } catch (const std::exception&) {
+      msg = std::string(body.substr(0, 500));
+    }
+    r.error(grpc_code(status), what + ": " + msg, {{"dapr-http-status", std::to_string(status)}});
+  }
+  // A value carried as bytes on the gRPC side, as the HTTP API's JSON body expects it
+  // (grpc_api.py _json_or_text): JSON text embedded as JSON, else a string, else base64.
+  static std::string json_or_text(std::string_view raw) {
+    if (raw.empty()) return "null";
+    if (valid_json(raw)) return compact(raw);
+    if (valid_utf8(raw)) return json_str(raw);
+    return json_str(base64(raw));
+  }
+  static std::string meta_qs(const std::vector<std::pair<std::string, std::string>>& meta) {
+    std::string qs;
+    for (auto& kv : meta) qs += (qs.empty() ? "?" : "&") + quote_all("metadata." + kv.first) + "=" + quote_all(kv.second);
+    return qs;
+  }
+  static std::string quote_path(std::string_view s) {  // quote each '/'-separated segment
+    std::string o;
+    size_t i = 0;
+    while (true) {
+      size_t j = s.find('/', i);
+      o += quote_all(s.substr(i, j == std::string_view::npos ? std::string_view::npos : j - i));
+      if (j == std::string_view::npos) break;
+      o += '/';
+      i = j + 1;
+    }
+    return o;
+  }
+  // Runs a translated request through the HTTP API pipeline; `done` gets the HTTP result.
+  using HttpDone = std::function<void(int, const HeaderList&, std::string_view)>;
+  void grpc_http(const h2::GrpcCall& c, std::string method, std::string target, std::string body,
+                 std::string ctype, HeaderList extra, HttpDone done) {
+    Message m;
+    m.method = std::move(method);
+    m.target = std::move(target);
+    for (auto& kv : c.metadata)
+      if (kv.first == "dapr-api-token" || kv.first == "traceparent" || kv.first == "tracestate" ||
+          kv.first.rfind("dapr-", 0) == 0)
+        m.headers.push_back(kv);
+    if (!ctype.empty()) m.headers.emplace_back("content-type", std::move(ctype));
+    for (auto& kv : extra) m.headers.push_back(std::move(kv));
+    m.headers.emplace_back("content-length", std::to_string(body.size()));
+    m.body = std::move(body);
+    on_api(std::move(m), Reply(std::move(done)));
+  }
+
+  struct StateItemPb {
+    std::string key, value, etag;
+    bool has_etag = false;
+    std::vector<std::pair<std::string, std::string>> meta;
+    uint64_t concurrency = 0, consistency = 0;
+  };
+  static bool decode_state_item(std::string_view s, StateItemPb& it) {
+    pb::Reader r(s);
+    uint32_t f, wt;
+    std::string_view v;
+    while (r.next(f, wt)) {
+      if (f == 1 && wt == pb::LEN && r.bytes(v)) it.key.assign(v);
+      else if (f == 2 && wt == pb::LEN && r.bytes(v)) it.value.assign(v);
+      else if (f == 3 && wt == pb::LEN && r.bytes(v)) {  // Etag {value = 1}
+        it.has_etag = true;
+        pb::Reader er(v);
+        uint32_t ef, ewt;
+        std::string_view ev;
+        while (er.next(ef, ewt))
+          if (ef == 1 && ewt == pb::LEN && er.bytes(ev)) it.etag.assign(ev);
+          else if (!er.skip(ewt)) break;
+        if (!er.ok) return false;
+      } else if (f == 4 && wt == pb::LEN && r.bytes(v)) {
+        std::string k, val;
+        if (!pb::map_entry(v, k, val)) return false;
+        it.meta.emplace_back(std::move(k), std::move(val));
+      } else if (f == 5 && wt == pb::LEN && r.bytes(v)) {  // StateOptions {concurrency = 1, consistency = 2}
+        pb::Reader orr(v);
+        uint32_t of, owt;
+        uint64_t x;
+        while (orr.next(of, owt))
+          if ((of == 1 || of == 2) && owt == pb::VARINT && orr.varint(x)) (of == 1 ? it.concurrency : it.consistency) = x;
+          else if (!orr.skip(owt)) break;
+        if (!orr.ok) return false;
+      } else if (!r.skip(wt)) {
+        break;
+      }
+    }
+    return r.ok;
+  }
+  static std::string state_item_json(const StateItemPb& it) {
+    std::string o = "{\"key\":" + json_str(it.key) + ",\"value\":" + json_or_text(it.value);
+    if (it.has_etag) o += ",\"etag\":" + json_str(it.etag);
+    if (!it.meta.empty()) {
+      o += ",\"metadata\":{";
+      for (size_t i = 0; i < it.meta.size(); ++i)
+        o += (i ? "," : "") + json_str(it.meta[i].first) + ":" + json_str(it.meta[i].second);
+      o += "}";
+    }
+    std::string opts;
+    if (it.concurrency == 1 || it.concurrency == 2)
+      opts += std::string("\"concurrency\":\"") + (it.concurrency == 1 ? "first-write" : "last-write") + "\"";
+    if (it.consistency == 1 || it.consistency == 2)
+      opts += std::string(opts.empty() ? "" : ",") + "\"consistency\":\"" +
+              (it.consistency == 1 ? "eventual" : "strong") + "\"";
+    if (!opts.empty()) o += ",\"options\":{" + opts + "}";
+    return o + "}";
+  }
+
+  void on_grpc(h2::GrpcCall&& c, h2::GrpcReply r) {
+    static constexpr std::string_view kSvc = "/dapr.proto.runtime.v1.Dapr/";
+    if (c.path.compare(0, kSvc.size(), kSvc) != 0) {
+      r.error(12, "unknown service: " + c.path);
+      return;
+    }
+    std::string rpc = c.path.substr(kSvc.size());
+    counters_["app=\"" + app_id_ + "\",op=\"grpc." + rpc + "\",status=\"call\""]++;
+    pb::Reader rd(c.message);
+    uint32_t f, wt;
+    std::string_view v;
+    auto fail_decode = [&] { r.error(3, rpc + ": malformed request message"); };
+    auto empty_ok = [r, rpc](int status, const HeaderList&, std::string_view body) {
+      if (status >= 300) grpc_fail(r, status, body, rpc);
+      else r.ok({});
+    };
+
+    if (rpc == "SaveState") {
+      std::string store, items = "[";
+      bool first = true;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) store.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) {
+          StateItemPb it;
+          if (!decode_state_item(v, it)) return fail_decode();
+          items += (first ? "" : ",") + state_item_json(it);
+          first = false;
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      grpc_http(c, "POST", "/v1.0/state/" + quote_all(store), items + "]", "application/json", {}, empty_ok);
+      return;
+    }
+    if (rpc == "GetState") {
+      std::string store, key;
+      std::vector<std::pair<std::string, std::string>> meta;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) store.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) key.assign(v);
+        else if (f == 4 && wt == pb::LEN && rd.bytes(v)) {
+          std::string k, val;
+          if (!pb::map_entry(v, k, val)) return fail_decode();
+          meta.emplace_back(std::move(k), std::move(val));
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      grpc_http(c, "GET", "/v1.0/state/" + quote_all(store) + "/" + quote_all(key) + meta_qs(meta), {}, {}, {},
+                [r, rpc](int status, const HeaderList& h, std::string_view body) {
+                  if (status >= 300) return grpc_fail(r, status, body, rpc);
+                  pb::Writer w;  // GetStateResponse {data = 1, etag = 2}
+                  if (status == 200) {
+                    w.str(1, body);
+                    for (auto& kv : h)
+                      if (kv.first == "etag") w.str(2, kv.second);
+                  }
+                  r.ok(w.s);
+                });
+      return;
+    }
+    if (rpc == "DeleteState") {
+      std::string store, key, etag;
+      std::vector<std::pair<std::string, std::string>> meta;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) store.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) key.assign(v);
+        else if (f == 3 && wt == pb::LEN && rd.bytes(v)) {
+          pb::Reader er(v);
+          uint32_t ef, ewt;
+          std::string_view ev;
+          while (er.next(ef, ewt))
+            if (ef == 1 && ewt == pb::LEN && er.bytes(ev)) etag.assign(ev);
+            else if (!er.skip(ewt)) break;
+          if (!er.ok) return fail_decode();
+        } else if (f == 5 && wt == pb::LEN && rd.bytes(v)) {
+          std::string k, val;
+          if (!pb::map_entry(v, k, val)) return fail_decode();
+          meta.emplace_back(std::move(k), std::move(val));
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      HeaderList extra;
+      if (!etag.empty()) extra.emplace_back("if-match", etag);
+      grpc_http(c, "DELETE", "/v1.0/state/" + quote_all(store) + "/" + quote_all(key) + meta_qs(meta), {}, {},
+                std::move(extra), empty_ok);
+      return;
+    }
+    if (rpc == "QueryStateAlpha1") {
+      std::string store, query;
+      std::vector<std::pair<std::string, std::string>> meta;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) store.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) query.assign(v);
+        else if (f == 3 && wt == pb::LEN && rd.bytes(v)) {
+          std::string k, val;
+          if (!pb::map_entry(v, k, val)) return fail_decode();
+          meta.emplace_back(std::move(k), std::move(val));
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      grpc_http(c, "POST", "/v1.0-alpha1/state/" + quote_all(store) + "/query" + meta_qs(meta), std::move(query),
+                "application/json", {}, [r, rpc](int status, const HeaderList&, std::string_view body) {
+                  if (status >= 300) return grpc_fail(r, status, body, rpc);
+                  pb::Writer w;  // QueryStateResponse {results = 1 {key, data, etag, error}, token = 2, metadata = 3}
+                  try {
+                    Value js = body.empty() ? Value() : parse(body);
+                    if (const Value* res = js.get("results"); res && res->t == Value::Array)
+                      for (auto& it : res->items) {
+                        pb::Writer e;
+                        auto sv = [&](const char* k) -> std::string {
+                          const Value* x = it.get(k);
+                          return x && x->t == Value::String ? x->s : std::string();
+                        };
+                        e.str(1, sv("key"));
+                        if (const Value* d = it.get("data"); d && d->t != Value::Null) e.str(2, dump(*d));
+                        e.str(3, sv("etag"));
+                        e.str(4, sv("error"));
+                        w.len_field(1, e.s);
+                      }
+                    if (const Value* t = js.get("token"); t && t->t == Value::String) w.str(2, t->s);
+                    if (const Value* md = js.get("metadata"); md && md->t == Value::Object)
+                      for (size_t i = 0; i < md->keys.size(); ++i)
+                        w.map_entry(3, md->keys[i], md->items[i].t == Value::String ? md->items[i].s : dump(md->items[i]));
+                  } catch (const std::exception& ex) {
+                    return r.error(13, rpc + ": malformed query response: " + ex.what());
+                  }
+                  r.ok(w.s);
+                });
+      return;
+    }
+    if (rpc == "PublishEvent") {
+      std::string pubsub, topic, data, ctype;
+      std::vector<std::pair<std::string, std::string>> meta;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) pubsub.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) topic.assign(v);
+        else if (f == 3 && wt == pb::LEN && rd.bytes(v)) data.assign(v);
+        else if (f == 4 && wt == pb::LEN && rd.bytes(v)) ctype.assign(v);
+        else if (f == 5 && wt == pb::LEN && rd.bytes(v)) {
+          std::string k, val;
+          if (!pb::map_entry(v, k, val)) return fail_decode();
+          meta.emplace_back(std::move(k), std::move(val));
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      grpc_http(c, "POST", "/v1.0/publish/" + quote_all(pubsub) + "/" + quote_path(topic) + meta_qs(meta),
+                std::move(data), ctype.empty() ? "application/json" : ctype, {}, empty_ok);
+      return;
+    }
+    if (rpc == "InvokeService") {
+      std::string id, method, qs, ctype, data;
+      uint64_t verb = 0;
+      bool has_data = false;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) id.assign(v);
+        else if (f == 3 && wt == pb::LEN && rd.bytes(v)) {  // InvokeRequest
+          pb::Reader ir(v);
+          uint32_t g, gwt;
+          std::string_view x;
+          while (ir.next(g, gwt)) {
+            if (g == 1 && gwt == pb::LEN && ir.bytes(x)) method.assign(x);
+            else if (g == 2 && gwt == pb::LEN && ir.bytes(x)) {  // google.protobuf.Any {type_url = 1, value = 2}
+              has_data = true;
+              pb::Reader ar(x);
+              uint32_t a, awt;
+              std::string_view y;
+              while (ar.next(a, awt))
+                if (a == 2 && awt == pb::LEN && ar.bytes(y)) data.assign(y);
+                else if (!ar.skip(awt)) break;
+              if (!ar.ok) return fail_decode();
+            } else if (g == 3 && gwt == pb::LEN && ir.bytes(x)) ctype.assign(x);
+            else if (g == 4 && gwt == pb::LEN && ir.bytes(x)) {  // HTTPExtension {verb = 1, querystring = 2}
+              pb::Reader hr(x);
+              uint32_t hf, hwt;
+              std::string_view y;
+              uint64_t n;
+              while (hr.next(hf, hwt))
+                if (hf == 1 && hwt == pb::VARINT && hr.varint(n)) verb = n;
+                else if (hf == 2 && hwt == pb::LEN && hr.bytes(y)) qs.assign(y);
+                else if (!hr.skip(hwt)) break;
+              if (!hr.ok) return fail_decode();
+            } else if (!ir.skip(gwt)) break;
+          }
+          if (!ir.ok) return fail_decode();
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      static const char* kVerbs[] = {"NONE", "GET", "HEAD", "POST", "PUT", "DELETE", "CONNECT", "OPTIONS", "TRACE", "PATCH"};
+      std::string http_method = verb == 0 || verb > 9 ? "POST" : kVerbs[verb];
+      size_t s = method.find_first_not_of('/');
+      std::string target = "/v1.0/invoke/" + quote_all(id) + "/method/" + (s == std::string::npos ? "" : method.substr(s)) +
+                           (qs.empty() ? "" : "?" + qs);
+      if (ctype.empty() && has_data) ctype = "application/json";
+      std::string what = "InvokeService " + id + "/" + method;
+      grpc_http(c, http_method, target, std::move(data), ctype, {},
+                [r, what](int status, const HeaderList& h, std::string_view body) {
+                  if (status >= 300) return grpc_fail(r, status, body, what);
+                  pb::Writer any, w;  // InvokeResponse {data = 1 (Any {value = 2}), content_type = 2}
+                  any.str(2, body);
+                  w.len_field(1, any.s);
+                  for (auto& kv : h)
+                    if (kv.first == "content-type") w.str(2, kv.second);
+                  r.ok(w.s);
+                });
+      return;
+    }
+    // everything else: the control plane runs grpc_api.py's handler on the raw message
+    grpc_http(c, "POST", "/_tt/grpc/" + quote_all(rpc), std::move(c.message), "application/grpc+proto", {},
+              [r, rpc](int status, const HeaderList& h, std::string_view body) {
+                const std::string* gs = nullptr;
+                const std::string* gm = nullptr;
+                HeaderList trailers;
+                for (auto& kv : h) {
+                  if (kv.first == "grpc-status") gs = &kv.second;
+                  else if (kv.first == "grpc-message") gm = &kv.second;
+                  else if (kv.first == "dapr-http-status") trailers.push_back(kv);
+                }
+                if (!gs) {  // the HTTP pipeline refused it before the handler (e.g. the API token)
+                  if (status >= 300) return grpc_fail(r, status, body, rpc);
+                  return r.error(13, rpc + ": control plane gave no gRPC status");
+                }
+                int code = std::atoi(gs->c_str());
+                if (code == 0) return r.ok(body);
+                r.error(code, gm ? unquote(*gm) : std::string(), trailers);
+              });
+  }
 };
 
 // ------------------------------------------------------------------------------ signals
@@ -1406,6 +1783,7 @@ int main(int argc, char** argv) {
   ev::Handler api = dp.api_handler();
   ev::Handler internal = dp.internal_handler();
   ev::Handler control = dp.control_handler();
+  h2::GrpcHandler grpc = dp.grpc_handler();
   std::string ports = "{";
   try {
     int http_port = 0;
@@ -1426,6 +1804,13 @@ int main(int argc, char** argv) {
         }
       }
     if (auto* c = opt_str(cfg, "control")) ev::listen_on(loop, Endpoint::parse(*c), control);
+    int grpc_port = 0;
+    if (auto* l = cfg.get("grpcListen"); l && l->t == Value::Array)
+      for (auto& x : l->items) {
+        int p = h2::listen_grpc(loop, Endpoint::parse(x.s), grpc);
+        if (p) grpc_port = p;
+      }
+    ports += ",\"grpc\":" + std::to_string(grpc_port);
     ports += ",\"internal\":" + json_str(internal_ep) + ",\"pid\":" + std::to_string(getpid()) + "}";
   } catch (const std::exception& e) {
     std::fprintf(stderr, "dataplane: %s\n", e.what());

@@ -507,8 +507,11 @@ class ServerConn;
 // Completes one request; safe to call after the connection went away.
 class Reply {
  public:
+  // An in-process completion (e.g. a gRPC call translated into an API request).
+  using Sink = std::function<void(int status, const HeaderList& headers, std::string_view body)>;
   Reply() = default;
   Reply(std::weak_ptr<ServerConn> c, uint64_t seq, bool head) : conn_(std::move(c)), seq_(seq), head_(head) {}
+  explicit Reply(Sink sink) : sink_(std::make_shared<Sink>(std::move(sink))) {}
   void send(int status, const HeaderList& headers, std::string_view body) const;
   void json(int status, std::string_view body) const {
     send(status, {{"content-type", "application/json"}}, body);
@@ -519,6 +522,7 @@ class Reply {
   std::weak_ptr<ServerConn> conn_;
   uint64_t seq_ = 0;
   bool head_ = false;
+  std::shared_ptr<Sink> sink_;
 };
 
 using Handler = std::function<void(Message&&, Reply)>;
@@ -695,6 +699,10 @@ class ServerConn : public IoObj {
 };
 
 inline void Reply::send(int status, const HeaderList& headers, std::string_view body) const {
+  if (sink_) {
+    (*sink_)(status, headers, body);
+    return;
+  }
   if (auto c = conn_.lock()) c->respond(seq_, status, headers, body, head_);
 }
 
@@ -733,22 +741,27 @@ class Listener : public IoObj {
   std::shared_ptr<TlsContext> tls_;
 };
 
-// Returns the bound port (tcp) or 0 (unix); throws on failure.
-// `reuseport`: several loops (threads) bind the same TCP port and the kernel spreads
-// incoming connections over them.
-// `tls`: serve HTTPS (with `verify_peer`: mutual TLS) on this listener.
-inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false,
-                     std::shared_ptr<IoObj>* listener_out = nullptr, std::shared_ptr<TlsContext> tls = nullptr) {
+// Bind + listen on `ep`; returns the socket, and the bound port in `port` (tcp) or 0 (unix).
+// Throws on failure.  `reuseport`: several loops (threads) bind the same TCP port and the
+// kernel spreads incoming connections over them.
+inline int bind_listen(const Endpoint& ep, bool reuseport, int& port) {
   int fd;
-  int port = 0;
+  port = 0;
   if (ep.unix_socket) {
     fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     sockaddr_un a{};
     a.sun_family = AF_UNIX;
-    if (ep.path.size() >= sizeof a.sun_path) throw std::runtime_error("unix socket path too long: " + ep.path);
+    if (ep.path.size() >= sizeof a.sun_path) {
+      ::close(fd);
+      throw std::runtime_error("unix socket path too long: " + ep.path);
+    }
     std::strcpy(a.sun_path, ep.path.c_str());
     ::unlink(ep.path.c_str());
-    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0) throw std::runtime_error("bind " + ep.path + ": " + strerror(errno));
+    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0) {
+      int e = errno;
+      ::close(fd);
+      throw std::runtime_error("bind " + ep.path + ": " + strerror(e));
+    }
   } else {
     fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
     int one = 1;
@@ -758,13 +771,29 @@ inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport 
     a.sin_family = AF_INET;
     a.sin_port = htons((uint16_t)ep.port);
     inet_pton(AF_INET, ep.host.c_str(), &a.sin_addr);
-    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0)
-      throw std::runtime_error("bind " + ep.key() + ": " + strerror(errno));
+    if (::bind(fd, (sockaddr*)&a, sizeof a) != 0) {
+      int e = errno;
+      ::close(fd);
+      throw std::runtime_error("bind " + ep.key() + ": " + strerror(e));
+    }
     socklen_t len = sizeof a;
     getsockname(fd, (sockaddr*)&a, &len);
     port = ntohs(a.sin_port);
   }
-  if (::listen(fd, 1024) != 0) throw std::runtime_error(std::string("listen: ") + strerror(errno));
+  if (::listen(fd, 1024) != 0) {
+    int e = errno;
+    ::close(fd);
+    throw std::runtime_error(std::string("listen: ") + strerror(e));
+  }
+  return fd;
+}
+
+// Returns the bound port (tcp) or 0 (unix); throws on failure.
+// `tls`: serve HTTPS (with `verify_peer`: mutual TLS) on this listener.
+inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false,
+                     std::shared_ptr<IoObj>* listener_out = nullptr, std::shared_ptr<TlsContext> tls = nullptr) {
+  int port = 0;
+  int fd = bind_listen(ep, reuseport, port);
   auto l = std::make_shared<Listener>(loop, fd, h, std::move(tls));
   loop.add(l, EPOLLIN);
   if (listener_out) *listener_out = l;

@@ -311,7 +311,8 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("close_server", &apphost::AppHost::close_server)
       .def("close_connections", &apphost::AppHost::close_connections)
       .def("pending_replies", &apphost::AppHost::pending_replies)
-      // ops: [(0, token, status, headers, body) | (1, id, endpoint, method, target, headers, body, timeout)]
+      // ops: [(0, token, status, headers, body) | (1, id, endpoint, method, target, headers, body, timeout) |
+      //       (2, id, endpoint, "", grpc_path, metadata, message, timeout)]
       .def("submit",
            [](apphost::AppHost& h, py::list ops) {
              std::vector<apphost::AppHost::Op> v;
@@ -319,7 +320,9 @@ PYBIND11_MODULE(_ttnative, m) {
              for (auto item : ops) {
                auto t = item.cast<py::tuple>();
                apphost::AppHost::Op op;
-               op.is_request = t[0].cast<int>() == 1;
+               int kind = t[0].cast<int>();
+               op.is_request = kind == 1 || kind == 2;
+               op.is_grpc = kind == 2;
                op.id = t[1].cast<uint64_t>();
                if (!op.is_request) {
                  op.status = t[2].cast<int>();

@@ -11,6 +11,7 @@ HTTP equivalent of the gRPC code).
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import os
 from typing import Any
@@ -48,20 +49,92 @@ def _loads(b: bytes) -> Any:
         return b.decode("utf-8", "replace")
 
 
+class _NativeRpcError(Exception):
+    """A non-OK gRPC status from the native transport (shape of ``grpc.aio.AioRpcError``)."""
+
+    def __init__(self, code: grpc.StatusCode, details: str, trailing: list[tuple[str, str]]) -> None:
+        super().__init__(details)
+        self._code, self._details, self._trailing = code, details, trailing
+
+    def code(self) -> grpc.StatusCode:
+        return self._code
+
+    def details(self) -> str:
+        return self._details
+
+    def trailing_metadata(self):
+        return self._trailing
+
+
+_STATUS_OF = {c.value[0]: c for c in grpc.StatusCode}
+
+
+class _NativeChannel:
+    """Unary calls over the native app host's HTTP/2 client (native/src/h2.hpp GrpcClient): the
+    app process's gRPC to its sidecar leaves Python as one batched hand-off per loop iteration,
+    like the HTTP client's requests -- no grpcio completion-queue threads in the way."""
+
+    def __init__(self, target: str) -> None:
+        from ..web import native_host
+        self.endpoint = target if target.startswith("unix:") else f"tcp:{target}"
+        self._native = native_host.NativeHttpClient()
+
+    def unary_unary(self, path: str, request_serializer, response_deserializer):
+        async def call(req, metadata=None, timeout=None):
+            host = self._native._native()
+            try:
+                r = await host.grpc_call(self.endpoint, path, list(metadata or ()), request_serializer(req),
+                                         timeout or 0.0)
+            except OSError as e:
+                raise _NativeRpcError(grpc.StatusCode.UNAVAILABLE, f"sidecar unreachable: {e}", []) from None
+            except asyncio.TimeoutError:
+                raise _NativeRpcError(grpc.StatusCode.DEADLINE_EXCEEDED, "Deadline Exceeded", []) from None
+            if r.status != 0:
+                md = [(k, v) for k, v in r.headers.items() if isinstance(v, str)]
+                raise _NativeRpcError(_STATUS_OF.get(r.status, grpc.StatusCode.UNKNOWN),
+                                      r.headers.get("grpc-message", ""), md)
+            return response_deserializer(r.body)
+        return call
+
+    async def channel_ready(self) -> None:
+        host = self._native._native()
+        req_cls, resp_cls = P.rpc_types("GetMetadata")
+        deadline = asyncio.get_running_loop().time() + 30
+        while True:  # the sidecar's gRPC port may not be listening yet
+            try:
+                await host.grpc_call(self.endpoint, P.method_path("GetMetadata"), [], req_cls().SerializeToString(), 5.0)
+                return
+            except OSError:
+                if asyncio.get_running_loop().time() > deadline:
+                    raise
+                await asyncio.sleep(0.05)
+
+    async def close(self) -> None:
+        await self._native.close()
+
+
 class GrpcSidecarClient:
-    def __init__(self, target: str | None = None, api_token: str | None = None, timeout: float = 60.0) -> None:
+    def __init__(self, target: str | None = None, api_token: str | None = None, timeout: float = 60.0,
+                 transport: str | None = None) -> None:
         self.target = target or sidecar_grpc_target()
         self.api_token = api_token if api_token is not None else os.environ.get("DAPR_API_TOKEN")
         self.timeout = timeout
-        self._channel: grpc.aio.Channel | None = None
+        if transport is None:  # the native app host's HTTP/2 client when the app runs on it
+            from ..web import native_host
+            transport = "native" if native_host.enabled(part="client") else "grpcio"
+        self.transport = transport
+        self._channel: Any = None
         self._stubs: dict[str, Any] = {}
+
+    def _new_channel(self):
+        return _NativeChannel(self.target) if self.transport == "native" else grpc.aio.insecure_channel(self.target)
 
     # -- plumbing -------------------------------------------------------------
     def _stub(self, rpc: str):
         st = self._stubs.get(rpc)
         if st is None:
             if self._channel is None:
-                self._channel = grpc.aio.insecure_channel(self.target)
+                self._channel = self._new_channel()
             req_cls, resp_cls = P.rpc_types(rpc)
             st = self._channel.unary_unary(P.method_path(rpc), request_serializer=req_cls.SerializeToString,
                                            response_deserializer=resp_cls.FromString)
@@ -82,7 +155,7 @@ class GrpcSidecarClient:
         span.set("rpc.system", "grpc")
         try:
             return await self._stub(rpc)(req, metadata=self._metadata(), timeout=self.timeout)
-        except grpc.aio.AioRpcError as e:
+        except (grpc.aio.AioRpcError, _NativeRpcError) as e:
             span.fail(e)
             status = _HTTP_OF.get(e.code(), 500)
             for k, v in e.trailing_metadata() or ():
@@ -97,8 +170,7 @@ class GrpcSidecarClient:
 
     async def wait_for_sidecar(self, timeout: float = 30.0) -> None:
         if self._channel is None:
-            self._channel = grpc.aio.insecure_channel(self.target)
-        import asyncio
+            self._channel = self._new_channel()
         await asyncio.wait_for(self._channel.channel_ready(), timeout)
 
     # -- service invocation ---------------------------------------------------

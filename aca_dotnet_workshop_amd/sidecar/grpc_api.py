@@ -87,6 +87,40 @@ def _state_item_json(item) -> dict[str, Any]:
     return d
 
 
+def _percent(msg: str) -> str:
+    """grpc-message encoding: bytes outside printable ASCII and '%' as %XX."""
+    return "".join(chr(b) if 0x20 <= b <= 0x7e and b != 0x25 else f"%{b:02X}" for b in msg.encode("utf-8"))
+
+
+def _grpc_reply(code: int, message: str, trailing=()) -> Response:
+    h = [("content-type", "application/grpc+proto"), ("grpc-status", str(code)), ("grpc-message", _percent(message))]
+    h += [(k, v) for k, v in trailing or ()]
+    return Response(b"", 200, h)
+
+
+class _Abort(Exception):
+    def __init__(self, code: grpc.StatusCode, details: str, trailing) -> None:
+        super().__init__(details)
+        self.code, self.details, self.trailing = code, details, trailing
+
+
+class _BridgeContext:
+    """The slice of ``grpc.aio.ServicerContext`` the handlers use, over a bridged HTTP request."""
+
+    def __init__(self, req: Request) -> None:
+        self._md = [(k, v) for k, v in req.headers.items()
+                    if k not in ("content-type", "content-length", "host") and isinstance(v, str)]
+
+    def invocation_metadata(self):
+        return self._md
+
+    def peer(self) -> str:
+        return "native-dataplane"
+
+    async def abort(self, code, details="", trailing_metadata=()):
+        raise _Abort(code, details, trailing_metadata)
+
+
 class DaprGrpcServer:
     """gRPC front of one sidecar; ``api`` is the sidecar's HTTP API ``WebApp``."""
 
@@ -290,6 +324,29 @@ class DaprGrpcServer:
     async def Shutdown(self, req, ctx):
         await self._ok(ctx, await self._http(ctx, "POST", "/v1.0/shutdown"), "Shutdown")
         return P.message(".google.protobuf.Empty")()
+
+    # -------------------------------------------------------------- native data plane bridge
+    async def dispatch_raw(self, req: Request) -> Response:
+        """``POST /_tt/grpc/{Method}`` on the control plane's private socket: the native data
+        plane (native/src/h2.hpp + dataplane.cpp) serves the gRPC port and decodes the hot RPCs
+        itself; any other RPC arrives here as its serialized request message plus the call
+        metadata as headers, runs through the same handler as above, and goes back as the
+        serialized response with ``grpc-status`` / ``grpc-message`` (percent-encoded) headers."""
+        rpc = req.path_params["method"]
+        if rpc not in P.RPCS:
+            return _grpc_reply(12, f"unknown method {rpc}")
+        req_cls, _ = P.rpc_types(rpc)
+        try:
+            msg = req_cls.FromString(req.body)
+        except Exception as e:  # noqa: BLE001 - protobuf raises DecodeError and friends
+            return _grpc_reply(3, f"{rpc}: malformed request message: {e}")
+        ctx = _BridgeContext(req)
+        try:
+            out = await getattr(self, rpc)(msg, ctx)
+        except _Abort as a:
+            return _grpc_reply(a.code.value[0], a.details, a.trailing)
+        return Response(out.SerializeToString(), 200,
+                        [("content-type", "application/grpc+proto"), ("grpc-status", "0")])
 
     # -------------------------------------------------------------- server
     def handler(self) -> grpc.GenericRpcHandler:

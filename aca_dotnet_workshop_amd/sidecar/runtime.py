@@ -168,7 +168,7 @@ class Sidecar:
             await self._start_native_data_plane(api)
         else:
             await self._start_python_servers(api, internal, loop)
-        if self.grpc_port is not None or self.grpc_uds:
+        if (self.grpc_port is not None or self.grpc_uds) and self.grpc_server is None:
             from .grpc_api import DaprGrpcServer
             self.grpc_server = DaprGrpcServer(self, api)
             self.bound_grpc_port = await self.grpc_server.start(self.grpc_port or 0, uds=self.grpc_uds)
@@ -253,11 +253,22 @@ class Sidecar:
         exe = self.environ.get("TT_DATAPLANE_BIN") or build_dataplane()
         self._dp_dir = tempfile.mkdtemp(prefix="ttdp-")
         private = os.path.join(self._dp_dir, "cp.sock")
+        grpc_listen = []
+        if self.grpc_port is not None or self.grpc_uds:
+            # the gRPC API port is served natively too (h2.hpp); RPCs it does not decode itself
+            # come back here through /_tt/grpc/{Method} (grpc_api.py dispatch_raw)
+            from .grpc_api import DaprGrpcServer
+            self.grpc_server = DaprGrpcServer(self, api)
+            if self.grpc_uds:
+                grpc_listen.append("unix:" + self.grpc_uds)
+            if self.grpc_port is not None:
+                grpc_listen.append(f"tcp:127.0.0.1:{self.grpc_port}")
         srv = HttpServer(api, asyncio.get_running_loop())
         await srv.listen_unix(private)
         self._servers.append(srv)
         cfg = self.data_plane_config("unix:" + private)
         cfg["portFile"] = os.path.join(self._dp_dir, "ports.json")
+        cfg["grpcListen"] = grpc_listen
         cfg["control"] = "unix:" + os.path.join(self._dp_dir, "ctl.sock")
         self._dp_control = cfg["control"] + ":"
         ex = self.tracer.exporter
@@ -283,6 +294,8 @@ class Sidecar:
         if self.http_port is not None:
             self.bound_http_port = ports["http"]
         self.bound_internal = ports["internal"] or None
+        if self.grpc_port is not None:
+            self.bound_grpc_port = ports.get("grpc")
 
     async def stop(self, grace: float = 5.0) -> None:
         if self.stopped.is_set():
@@ -637,6 +650,7 @@ class Sidecar:
         app.add_route("/v1.0/healthz/outbound", self.h_healthz, ("GET",))
         app.add_route("/v1.0/shutdown", self.h_shutdown, ("POST",))
         app.add_route("/metrics", self.h_metrics, ("GET",))
+        app.add_route("/_tt/grpc/{method}", self.h_grpc_bridge, ("POST",))
         app.add_route("/{*path}", self.h_header_proxy, invoke_methods)
         return app
 
@@ -674,6 +688,12 @@ class Sidecar:
         target = req.path_params["appId"]
         method_path = req.path_params["method"]
         return await self._invoke(req, target, method_path)
+
+    async def h_grpc_bridge(self, req: Request) -> Response:
+        """RPCs the native data plane's gRPC port does not decode itself (grpc_api.py dispatch_raw)."""
+        if self.grpc_server is None or self._dp_proc is None:
+            return err(404, "ERR_NOT_FOUND", f"no route for {req.path}")
+        return await self.grpc_server.dispatch_raw(req)
 
     async def h_header_proxy(self, req: Request) -> Response:
         target = req.headers.get("dapr-app-id")

@@ -188,6 +188,18 @@ class NativeHost:
             except Exception:  # one bad event must not strand the rest of the batch
                 log.exception("native host event %r failed", ev[:2])
 
+    def grpc_call(self, endpoint: str, path: str, metadata: list[tuple[str, str]], message: bytes,
+                  timeout: float) -> asyncio.Future:
+        """A unary gRPC call on the host's HTTP/2 client (h2.hpp GrpcClient).  Resolves to a
+        ``ClientResponse`` whose ``status`` is the grpc-status, ``headers`` the response metadata
+        (with ``grpc-message``) and ``body`` the serialized response message."""
+        rid = self._next_id
+        self._next_id += 1
+        fut = self.loop.create_future()
+        self.pending[rid] = fut
+        self._queue((2, rid, endpoint, "", path, metadata, message, timeout))
+        return fut
+
     def request(self, endpoint: str, method: str, target: str, headers: list[tuple[str, str]], body: bytes,
                 timeout: float) -> asyncio.Future:
         rid = self._next_id

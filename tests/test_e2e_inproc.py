@@ -201,6 +201,13 @@ def test_frontend_pages_flow():
             cookie = "TasksCreatedByCookie=ui@user.com"
             r = await http.get(web + "/Tasks/Create", headers={"Cookie": cookie})
             assert r.status == 200
+            # client-side validation: unobtrusive data-val rules + message spans + the script
+            # (the reference's asp-validation-for + _ValidationScriptsPartial, Create.cshtml:13-29,45)
+            assert 'name="TaskAdd.TaskName"' in r.text and 'data-val="true"' in r.text
+            assert 'data-val-required="The Task Name field is required."' in r.text
+            assert 'data-val-email="The Assigned To field is not a valid e-mail address."' in r.text
+            assert 'data-valmsg-for="TaskAdd.TaskDueDate"' in r.text and '<script src="/js/validation.js">' in r.text
+            assert (await http.get(web + "/js/validation.js")).status == 200
             af_cookie = re.search(r"\.AspNetCore\.Antiforgery=([0-9a-f]+)", r.headers["set-cookie"]).group(1)
             token = re.search(r'name="__RequestVerificationToken" value="([0-9a-f]+)"', r.text).group(1)
             cookies = f"{cookie}; .AspNetCore.Antiforgery={af_cookie}"
@@ -209,6 +216,8 @@ def test_frontend_pages_flow():
             r = await http.post(web + "/Tasks/Create", body=f"__RequestVerificationToken={token}&TaskAdd.TaskName=",
                                 headers=form_h)
             assert r.status == 200 and "The Task Name field is required." in r.text
+            assert 'class="field-validation-error text-danger" data-valmsg-for="TaskAdd.TaskName"' in \
+                " ".join(r.text.split())
             # no antiforgery token -> 400
             r = await http.post(web + "/Tasks/Create", body=b"TaskAdd.TaskName=x", headers=form_h)
             assert r.status == 400

@@ -64,7 +64,11 @@ def _app(received: list):
     return app
 
 
-def test_grpc_and_http_clients_agree(tmp_path):
+PLANES = ["python", "native"]
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_grpc_and_http_clients_agree(plane, tmp_path):
     received: list = []
     secrets = tmp_path / "secrets.json"
     secrets.write_text('{"dbkey": "s3cr3t", "other": "x"}')
@@ -74,12 +78,15 @@ def test_grpc_and_http_clients_agree(tmp_path):
              _inline("secrets", "secretstores.local.file", {"secretsFile": str(secrets)})]
 
     async def main():
-        async with Harness(_app(received), comps, app_id="grpcapp", grpc_port=0) as h:
-            assert h.sc.bound_grpc_port
+        async with Harness(_app(received), comps, app_id="grpcapp", grpc_port=0, data_plane=plane) as h:
+            assert h.sc.bound_grpc_port and h.sc.active_data_plane == plane
             http = SidecarClient(h.base)
-            g = GrpcSidecarClient(f"127.0.0.1:{h.sc.bound_grpc_port}")
+            g = GrpcSidecarClient(f"127.0.0.1:{h.sc.bound_grpc_port}", transport="grpcio")
             await g.wait_for_sidecar(5)
-            for c, tag in ((http, "h"), (g, "g")):
+            # the native app host's HTTP/2 client (h2.hpp GrpcClient) as a third transport
+            n = GrpcSidecarClient(f"127.0.0.1:{h.sc.bound_grpc_port}", transport="native")
+            await n.wait_for_sidecar(5)
+            for c, tag in ((http, "h"), (g, "g"), (n, "n")):
                 doc = {"taskId": tag, "taskName": f"name {tag}", "isCompleted": False, "n": 3}
                 await c.save_state("statestore", f"k-{tag}", doc)
                 got, etag = await c.get_state_and_etag("statestore", f"k-{tag}")
@@ -128,19 +135,29 @@ def test_grpc_and_http_clients_agree(tmp_path):
                 meta = await c.get_metadata()
                 assert meta["id"] == "grpcapp" and meta["extended"][f"attr-{tag}"] == "v"
                 assert {x["name"] for x in meta["components"]} >= {"statestore", "bus", "files", "secrets"}
-            for tag in "gh":  # same bytes written through either transport
+            for tag in "ghn":  # same bytes written through every transport
                 assert (tmp_path / "blobs" / f"{tag}.json").read_bytes() == b'{"task":"%s"}' % tag.encode()
-            await _until(lambda: sum(1 for x in received if "i" in x) == 4)
+            await _until(lambda: sum(1 for x in received if "i" in x) == 6)
+            if plane == "native":
+                # the hot RPCs were decoded by the C++ plane (h2.hpp / dataplane.cpp) and ran its
+                # native state / publish paths; the rest were bridged to grpc_api.py
+                metrics = (await h.http.get(h.base + "/metrics")).body.decode()
+                for op in ("grpc.SaveState", "grpc.GetState", "grpc.DeleteState", "grpc.QueryStateAlpha1",
+                           "grpc.PublishEvent", "grpc.InvokeService", "grpc.GetSecret", "state.save",
+                           "state.get", "state.delete", "state.query", "publish"):
+                    assert f'op="{op}"' in metrics, op
             await http.close()
             await g.close()
+            await n.close()
     run(main())
 
 
-def test_grpc_api_token_and_client_factory():
+@pytest.mark.parametrize("plane", PLANES)
+def test_grpc_api_token_and_client_factory(plane):
     comps = [_inline("kv", "state.in-memory", {})]
 
     async def main():
-        async with Harness(WebApp("t"), comps, app_id="t", api_token="tok", grpc_port=0) as h:
+        async with Harness(WebApp("t"), comps, app_id="t", api_token="tok", grpc_port=0, data_plane=plane) as h:
             target = f"127.0.0.1:{h.sc.bound_grpc_port}"
             bad = GrpcSidecarClient(target, api_token="")
             with pytest.raises(InvocationError) as ei:
@@ -167,7 +184,8 @@ def test_grpc_api_token_and_client_factory():
     run(main())
 
 
-def test_backend_api_over_grpc_transport():
+@pytest.mark.parametrize("plane", PLANES)
+def test_backend_api_over_grpc_transport(plane):
     """The Backend API's store manager on the gRPC transport: createTask persists + publishes."""
     from aca_dotnet_workshop_amd.services.backend_api.app import create_app
     received: list = []
@@ -185,7 +203,7 @@ def test_backend_api_over_grpc_transport():
     map_subscribe_handler(sub)
 
     async def main():
-        async with Harness(sub, comps, app_id="tasksmanager-backend-api", grpc_port=0) as h:
+        async with Harness(sub, comps, app_id="tasksmanager-backend-api", grpc_port=0, data_plane=plane) as h:
             g = GrpcSidecarClient(f"127.0.0.1:{h.sc.bound_grpc_port}")
             api = create_app([], overrides={"TasksManager:Backend": "store", "Dapr:ApiProtocol": "grpc",
                                             "Logging:LogLevel:Default": "Warning"})

@@ -47,8 +47,8 @@ def test_native_engines_address_ub_sanitizer(tmp_path):
 
 
 def test_dataplane_under_address_sanitizer(tmp_path):
-    """The native sidecar data plane (callbacks, weak replies, pooled connections) built with
-    ASan+UBSan serves the full parity suite without a memory error: the suite's native cases run
+    """The native sidecar data plane (callbacks, weak replies, pooled connections, the HTTP/2 +
+    HPACK gRPC front) built with ASan+UBSan serves the full parity suite without a memory error: the suite's native cases run
     against the instrumented binary and any report fails the run (the data plane aborts)."""
     if shutil.which(CXX) is None:
         pytest.skip("no C++ compiler")
@@ -63,7 +63,8 @@ def test_dataplane_under_address_sanitizer(tmp_path):
     env = dict(os.environ, TT_DATAPLANE_BIN=str(exe), ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
                PYTHONPATH=str(ROOT))
     run = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                          str(ROOT / "tests" / "test_dataplane.py"), "-k", "native"],
+                          str(ROOT / "tests" / "test_dataplane.py"), str(ROOT / "tests" / "test_grpc_api.py"),
+                          str(ROOT / "tests" / "test_grpc_h2_native.py"), "-k", "native"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     out = run.stdout + run.stderr
     assert run.returncode == 0, out[-5000:]
