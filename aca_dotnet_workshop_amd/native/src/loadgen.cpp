@@ -4,6 +4,8 @@
 // (Unix sockets or TCP), in `--steps` steps of `--batch` requests.  With `--until-url` a
 // step ends only when the JSON counter at that URL (field `--until-field`) has advanced by
 // the batch size -- bench.py uses it to wait until the processor acknowledged every task.
+// `--until-base N --until-stride M`: start from counter value N and require an advance of M per
+// step (several generators sharing one subscription: M = ranks x batch).
 // Request bodies come from a file with one body per line (cycled).  Prints one JSON line:
 // {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
 //
@@ -30,6 +32,9 @@ struct Opts {
   std::string path = "/", method = "POST", ctype = "application/json", until_url, until_field = "completed";
   std::vector<std::string> bodies{""};
   int concurrency = 64, batch = 512, steps = 1, expect = 0;
+  // shared environments (bench.py --shared-env): several generators drive one subscription, so
+  // the counter's starting point and its advance per step are global, not this generator's own
+  long long until_base = -1, until_stride = 0;
 };
 
 class Gen {
@@ -47,7 +52,10 @@ class Gen {
   void start() {
     t0_ = ev::now_s();
     if (until_target_.empty()) begin_step();
-    else poll_counter([this](long long v) {
+    else if (o_.until_base >= 0) {
+      base_ = o_.until_base;
+      begin_step();
+    } else poll_counter([this](long long v) {
       base_ = v;
       begin_step();
     });
@@ -126,7 +134,7 @@ class Gen {
 
   void end_step() {
     step_creates_ = ev::now_s() - step_t0_;
-    base_ += o_.batch;
+    base_ += o_.until_stride > 0 ? o_.until_stride : o_.batch;
     ++step_;
     if (until_target_.empty()) {
       begin_step();
@@ -189,6 +197,8 @@ int main(int argc, char** argv) {
     else if (a == "--expect") o.expect = std::atoi(next().c_str());
     else if (a == "--until-url") o.until_url = next();
     else if (a == "--until-field") o.until_field = next();
+    else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
+    else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--bodies") {
       std::ifstream in(next());
       o.bodies.clear();

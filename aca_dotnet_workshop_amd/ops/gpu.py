@@ -34,7 +34,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_sort_pairs_temp_bytes.restype = ctypes.c_int64
     lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P]
     lib.tt_sort_pairs.restype = ctypes.c_int
-    lib.tt_launch_scan_compact.argtypes = [P, P, I64, P, P]
+    lib.tt_launch_scan_compact.argtypes = [P, P, P, I64, P, P, P, P]
+    lib.tt_chunk_tiles.restype = ctypes.c_int
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_scan_select.argtypes = [P, I64, P, P, I32, P, I32, P, P, P, P, P]
     lib.tt_launch_scan_select.restype = ctypes.c_int
@@ -67,6 +68,7 @@ class GpuKernels:
         self.tile_rows = int(self.lib.tt_tile_rows())
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
+        self.chunk_tiles = int(self.lib.tt_chunk_tiles())
         # Single-pass select (tt_scan_select, decoupled look-back) is opt-in: measured 1.40 ms vs
         # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
         # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
@@ -120,6 +122,7 @@ class GpuKernels:
             return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
         mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
         counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
+        stream = self._stream()
         if flat is not None and self.flat_eval:
             leaves, flip, max_width = flat
             if leaves.dtype != torch.int32 or leaves.ndim != 2 or leaves.shape[1] != 4:
@@ -128,27 +131,38 @@ class GpuKernels:
                 raise ValueError("too many leaves for tt_scan_flat")
             rc = self.lib.tt_launch_scan_flat(table.data_ptr(), nrows, live16.data_ptr(), leaves.data_ptr(),
                                               leaves.shape[0], int(flip), int(max_width), bitmaps.data_ptr(),
-                                              bitmaps.numel(),
-                                              mask.data_ptr(), counts.data_ptr(), self._stream())
+                                              bitmaps.numel(), mask.data_ptr(), counts.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_flat launch failed ({rc})")
         else:
             rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
                                               prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(), mask.data_ptr(),
-                                              counts.data_ptr(), self._stream())
+                                              counts.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
-        incl = torch.cumsum(counts, 0, dtype=torch.int64)
-        total = int(incl[-1].item())
-        offsets = incl - counts.to(torch.int64)
-        out = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
-        if total:
-            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), offsets.data_ptr(), nrows, out.data_ptr(),
-                                                 self._stream())
-            if rc != 0:
-                raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
+        # per-64-tile chunk counts (tt_chunk_sums), then the compaction finds each tile's offset
+        # from them and writes the total straight into pinned host memory: no full scan, no
+        # torch launches, no host sync between the kernels -- one event wait at the end
+        out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
+        scratch = torch.empty((tiles + self.chunk_tiles - 1) // self.chunk_tiles + 1, dtype=torch.int64,
+                              device=self.device)  # [0] = total (int64), then int32 chunk counts
+        pinned = self._pinned()
+        rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[1:].data_ptr(), nrows,
+                                             out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
+        self._total_event.record(torch.cuda.current_stream(self.device))
+        self._total_event.synchronize()
+        total = int(pinned[0])
         out = out[:total]
         return (out, mask) if return_mask else out
+
+    def _pinned(self):
+        p = getattr(self, "_pinned_total", None)
+        if p is None:
+            p = self._pinned_total = self.torch.zeros(1, dtype=self.torch.int64, pin_memory=True)
+            self._total_event = self.torch.cuda.Event()
+        return p
 
     def rank_encode(self, src_desc, rank_table, lo: int, hi: int, dst, width: int) -> None:
         """dst[lo:hi] = sort rank of each row's dictionary id (``hip/query_scan.hip`` tt_rank_encode);

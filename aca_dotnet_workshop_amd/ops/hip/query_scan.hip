@@ -28,6 +28,8 @@ namespace {
 constexpr int kBlock = 256;                    // 4 waves (compaction, group count)
 constexpr int kRowsPerLane = 16;
 constexpr int kTileRows = 8192;               // rows per scan / compaction block
+constexpr int kChunkShift = 6;                // 64 tiles per chunk: per-chunk selected counts let a
+                                              // compaction block find its offset with one wave
 static_assert(kTileRows == kBlock * 32, "compaction takes 32 mask bits per thread per tile");
 constexpr int kMaxDepth = 8;                   // 8 x 16-bit masks in a 128-bit stack
 constexpr int kMaxLdsBitmapWords = 8192;       // stage up to 32 KiB of leaf bitmaps in LDS
@@ -407,17 +409,63 @@ tt_scan_flat_t(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   }
 }
 
+// tt_chunk_sums: selected rows per 64-tile chunk -- one wave per chunk, one coalesced load per
+// lane, a shuffle reduction; ~190 waves for 1e8 rows.  (Accumulating these with atomics in the
+// scan kernel instead cost it 10-15 us at 1e8 rows; a "last block" ticket to reset them cost the
+// compaction 35 -> 460 us: single-address atomics serialize across the 8 XCDs.)
+extern "C" __global__ void __launch_bounds__(kBlock)
+tt_chunk_sums(const int32_t* __restrict__ block_counts, int64_t tiles, int32_t* __restrict__ chunk_sums) {
+  const int lane = threadIdx.x & 63;
+  const int64_t chunk = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t nchunks = (tiles + (1 << kChunkShift) - 1) >> kChunkShift;
+  if (chunk >= nchunks) return;
+  const int64_t j = (chunk << kChunkShift) + lane;
+  int32_t v = j < tiles ? block_counts[j] : 0;
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if (lane == 0) chunk_sums[chunk] = v;
+}
+
+// Each compaction block finds its tile's output offset itself -- one wave sums the selected
+// counts of the preceding chunks plus the preceding tiles of its own chunk -- so neither a
+// full scan of the tile counts nor a host round trip sits between the scan and the
+// compaction.  Block 0 also publishes the grand total: to `total` (device) and, when given,
+// straight into pinned host memory (`total_host`, system-scope store), which the host reads
+// after one event wait.
 extern "C" __global__ void __launch_bounds__(kBlock)
 tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask viewed as 32-bit words
-                const int64_t* __restrict__ block_offsets,  // exclusive scan of block_counts
-                int32_t* __restrict__ out) {
+                const int32_t* __restrict__ block_counts,  // selected rows per tile
+                const int32_t* __restrict__ chunk_sums,    // selected rows per 64-tile chunk
+                int64_t tiles, int32_t* __restrict__ out, int64_t* __restrict__ total, int64_t* total_host) {
   __shared__ int32_t staged[kTileRows];
   __shared__ int32_t wave_sums[kBlock / 64];
+  __shared__ int64_t tile_base;
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
   const int64_t tile = blockIdx.x;
   const uint32_t bits = mask32[tile * kBlock + t];     // rows [tile*8192 + 32t, +32)
+  if (wave == 0) {
+    const int64_t chunk = tile >> kChunkShift;
+    int64_t s = 0;
+    for (int64_t i = lane; i < chunk; i += 64) s += chunk_sums[i];
+    const int64_t j = (chunk << kChunkShift) + lane;   // 64 tiles per chunk = one per lane
+    if (j < tile) s += block_counts[j];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if (lane == 0) tile_base = s;
+    if (tile == 0) {
+      const int64_t nchunks = (tiles + (1 << kChunkShift) - 1) >> kChunkShift;
+      int64_t g = 0;
+      for (int64_t i = lane; i < nchunks; i += 64) g += chunk_sums[i];
+      for (int off = 32; off > 0; off >>= 1) g += __shfl_down(g, off, 64);
+      if (lane == 0) {
+        *total = g;
+        if (total_host) {
+          __hip_atomic_store(total_host, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __threadfence_system();
+        }
+      }
+    }
+  }
   const int32_t cnt = __popc(bits);
   int32_t incl = cnt;
   for (int off = 1; off < 64; off <<= 1) {
@@ -429,7 +477,7 @@ tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask view
   int32_t base = 0;
   for (int w = 0; w < wave; ++w) base += wave_sums[w];
   int32_t pos = base + incl - cnt;
-  const int32_t total = wave_sums[0] + wave_sums[1] + wave_sums[2] + wave_sums[3];
+  const int32_t count = wave_sums[0] + wave_sums[1] + wave_sums[2] + wave_sums[3];
   const int32_t row_base = (int32_t)(tile * kTileRows) + t * 32;
   uint32_t b = bits;
   while (b) {
@@ -438,8 +486,8 @@ tt_scan_compact(const uint32_t* __restrict__ mask32,      // selection mask view
     b &= b - 1;
   }
   __syncthreads();
-  int32_t* dst = out + block_offsets[tile];
-  for (int i = t; i < total; i += kBlock) dst[i] = staged[i];
+  int32_t* dst = out + tile_base;
+  for (int i = t; i < count; i += kBlock) dst[i] = staged[i];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -734,14 +782,21 @@ extern "C" int tt_launch_scan_flat(const void* cols, int64_t nrows, const uint16
 
 extern "C" int tt_max_flat_leaves() { return kMaxFlatLeaves; }
 
-extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int64_t* block_offsets, int64_t nrows, int32_t* out,
+// `chunk_sums`: scratch for ceil(tiles / 64) int32; `out` holds up to nrows ids; the selected
+// count lands in `total` (device) and `total_host` (pinned host memory, optional).
+extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int32_t* block_counts, int32_t* chunk_sums,
+                                      int64_t nrows, int32_t* out, int64_t* total, int64_t* total_host,
                                       hipStream_t stream) {
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
+  const int64_t nchunks = (tiles + (1 << kChunkShift) - 1) >> kChunkShift;
+  hipLaunchKernelGGL(tt_chunk_sums, dim3((unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
+                     stream, block_counts, tiles, chunk_sums);
   hipLaunchKernelGGL(tt_scan_compact, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
-                     reinterpret_cast<const uint32_t*>(mask), block_offsets, out);
+                     reinterpret_cast<const uint32_t*>(mask), block_counts, chunk_sums, tiles, out, total, total_host);
   return (int)hipGetLastError();
 }
+extern "C" int tt_chunk_tiles() { return 1 << kChunkShift; }
 
 // `status` (ntiles uint64) and `ticket` must be zeroed; `out` holds up to nrows ids; the
 // selected count lands in `total` (device int64).

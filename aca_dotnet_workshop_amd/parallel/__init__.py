@@ -62,6 +62,14 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
         return float(t.item())
 
+    def broadcast(self, obj, src: int = 0):
+        """``obj`` of rank ``src`` on every rank (a picklable object over gloo)."""
+        if self.pg is None:
+            return obj
+        box = [obj]
+        self.pg.broadcast_object_list(box, src=src)
+        return box[0]
+
     def close(self) -> None:
         if self.pg is not None:
             self.pg.destroy_process_group()

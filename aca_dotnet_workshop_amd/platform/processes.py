@@ -144,6 +144,21 @@ class LocalStack:
             self.base_env[f"TT_BACKING_URL_{f}"] = url
         return url
 
+    def shared_info(self) -> dict[str, Any]:
+        """What another stack needs to join this one's backing services and name registry."""
+        return {"backing": self.backing_url, "registry": str(self.registry),
+                "families": {f: url for f, (_p, url) in self.extra_backing.items()}}
+
+    def attach(self, info: dict[str, Any]) -> None:
+        """Join another stack's backing services (Cosmos/Service Bus/Storage equivalents) and
+        name registry instead of starting our own: replicas started afterwards share its state
+        store and compete on its subscriptions (one environment spread over several hosts'
+        worth of replicas)."""
+        self.backing_url = info["backing"]
+        self.registry = Path(info["registry"])
+        for f, url in info.get("families", {}).items():
+            self.base_env[f"TT_BACKING_URL_{f}"] = url
+
     def backing_url_for(self, family: str) -> str:
         return self.extra_backing[family][1] if family in self.extra_backing else self.backing_url
 

@@ -60,6 +60,10 @@ def parse() -> argparse.Namespace:
                     help="services' HTTP I/O: python (asyncio) | native (apphost.hpp) | api=native,processor=python")
     ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
                     help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")
+    ap.add_argument("--shared-env", action="store_true",
+                    help="multi-rank: ONE environment -- rank 0's backing services (state store, broker) shared by "
+                         "every rank's API and processor replicas, which compete on one subscription (the "
+                         "reference's KEDA scale axis); default: one environment per rank (weak scaling)")
     ap.add_argument("--client", choices=("native", "python"), default="native",
                     help="load generator: native/bin/ttloadgen (C++) or the in-process asyncio client")
     return ap.parse_args()
@@ -195,6 +199,16 @@ class OverdueSweeper:
                 "first_error": self.errors[0] if self.errors else None}
 
 
+def _counts(url: str) -> dict:
+    import urllib.request
+    with urllib.request.urlopen(url, timeout=30) as r:
+        return json.loads(r.read())
+
+
+def _counter(url: str) -> int:
+    return int(_counts(url)["completed"])
+
+
 def _collection_stats(backing: str) -> dict:
     import urllib.request
     url = f"{backing}/cosmos/taskstracker-state-store/tasksmanagerdb/taskscollection/stats"
@@ -207,12 +221,16 @@ def _collection_stats(backing: str) -> dict:
 
 
 def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: int, conc: int,
-                bodies_file: str) -> tuple[float, dict]:
-    """Closed-loop load from the native generator; returns (wall seconds, its report)."""
+                bodies_file: str, shared: tuple[int, int] | None = None) -> tuple[float, dict]:
+    """Closed-loop load from the native generator; returns (wall seconds, its report).
+    ``shared = (base, stride)``: the subscription's completed counter is shared with other
+    ranks' generators -- start from ``base`` and wait for ``stride`` more per step."""
     import subprocess
     cmd = [exe, "--path", "/v1.0/invoke/tasksmanager-backend-api/method/api/tasks", "--bodies", bodies_file,
            "--concurrency", str(conc), "--batch", str(batch), "--steps", str(steps), "--expect", "201",
            "--until-url", counts_url, "--until-field", "completed"]
+    if shared is not None:
+        cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     for s in socks:
         cmd += ["--target", "unix:" + s]
     t0 = time.perf_counter()
@@ -250,12 +268,22 @@ def main() -> None:
            "TT_TELEMETRY_DIR": os.path.join(root, "telemetry"), "TT_LOG_CONSOLE": "0", **rank_device_env()}
     if sweep:  # the task collection's column mirror is maintained from its first write
         env["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue"
+    shared = a.shared_env and d.world > 1
+    if shared and a.client != "native":
+        raise SystemExit("--shared-env needs the native load generator")
     stack = LocalStack(root=root, env=env)
     sweeper = None
     try:
-        backing = doc_backing = stack.start_backing()
-        if a.split_backing:
-            backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
+        if not shared or d.rank == 0:
+            backing = doc_backing = stack.start_backing()
+            if a.split_backing:
+                backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
+        if shared:  # every rank joins rank 0's backing services and name registry
+            info = d.broadcast(stack.shared_info() if d.rank == 0 else None)
+            if d.rank:
+                stack.attach(info)
+            doc_backing = info["backing"]
+            backing = info["families"].get("SERVICEBUS", doc_backing)
         for _ in range(a.api_replicas):
             stack.start_replica("tasksmanager-backend-api", api_cfg, grpc=a.api_protocol == "grpc",
                                 extra_env={"TT_APP_HOST": app_host("api", a.app_host)})
@@ -272,12 +300,18 @@ def main() -> None:
             bodies_file = str(stack.root / "bodies.jsonl")
             with open(bodies_file, "wb") as f:
                 f.write(b"\n".join(_bodies(a.batch, a.past_due_every if sweep else 0)) + b"\n")
+        gbase = None
+        if shared:  # the subscription's completed counter before anyone sends (global step targets)
+            d.barrier()
+            gbase = d.broadcast(_counter(counts_url) if d.rank == 0 else None)
+        stride = a.batch * d.world
         if a.warmup:
             if a.client == "native":
-                run_loadgen(exe, socks, counts_url, a.warmup, a.batch, a.concurrency, bodies_file)
+                run_loadgen(exe, socks, counts_url, a.warmup, a.batch, a.concurrency, bodies_file,
+                            (gbase, stride) if shared else None)
             else:
                 asyncio.run(run_steps(socks, counts_url, entity, a.warmup, a.batch, a.concurrency, None))
-        if sweep:
+        if sweep and (not shared or d.rank == 0):  # one cron trigger per environment
             sweeper = OverdueSweeper(stack.replicas["tasksmanager-backend-processor"][0].sidecar_uds,
                                      a.overdue_sweep_ms / 1000.0)
         lat: list[float] = []
@@ -293,7 +327,8 @@ def main() -> None:
         if sweeper is not None:
             sweeper.start()
         if a.client == "native":
-            dt, report = run_loadgen(exe, socks, counts_url, a.steps, a.batch, a.concurrency, bodies_file)
+            dt, report = run_loadgen(exe, socks, counts_url, a.steps, a.batch, a.concurrency, bodies_file,
+                                     (gbase + stride * a.warmup, stride) if shared else None)
         else:
             dt = asyncio.run(run_steps(socks, counts_url, entity, a.steps, a.batch, a.concurrency, lat))
         device_sync()
@@ -327,6 +362,13 @@ def main() -> None:
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows")}
             if d.rank == 0:
                 print(json.dumps({"overdue_sweeps": sweep_info}), file=sys.stderr, flush=True)
+        delivery = None
+        if shared:  # exactly-once across the competing consumers of every rank
+            c = _counts(counts_url)
+            sent = gbase + stride * (a.warmup + a.steps)
+            delivery = {"enqueued": c.get("enqueued"), "completed": c.get("completed"), "received": c.get("received"),
+                        "dead_lettered": c.get("dead_letter"), "expected": sent,
+                        "exactly_once": c.get("completed") == c.get("received") == c.get("enqueued") == sent}
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         if d.rank == 0:
@@ -337,7 +379,10 @@ def main() -> None:
                 "data": "synthetic createTask payloads",
                 "config": {"model": "tasks-tracker createTask flow (API+sidecars+backing+processor)",
                            "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
-                           "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
+                           "parallelism": (f"shared-env x{d.world} (one backing + subscription, "
+                                           f"{a.processor_replicas * d.world} competing processor replicas)"
+                                           if shared else f"env-per-rank x{d.world if d.world > 1 else 1}"),
+                           "delivery": delivery,
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
                            "sidecar_api_protocol": a.api_protocol,
@@ -352,6 +397,8 @@ def main() -> None:
     finally:
         if sweeper is not None and sweeper.thread.is_alive():
             sweeper.stop()
+        if shared and sys.exc_info()[0] is None:
+            d.barrier()  # rank 0 owns the shared backing services: stop them last
         stack.stop()
         d.close()
         if not os.environ.get("TT_BENCH_KEEP"):

@@ -56,6 +56,27 @@ def test_bench_two_ranks_torchrun():
     _check(lines[0], 2, 2, 1)
 
 
+def test_bench_shared_env_two_ranks():
+    """--shared-env: both ranks' API and processor replicas run against rank 0's backing services;
+    the processors of both ranks compete on ONE subscription (the reference's scale axis,
+    processor-backend-service.bicep:159-183) and every task is delivered and completed once."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "32", "--api-replicas", "1", "--processor-replicas", "1",
+           "--shared-env", "--overdue-sweep-ms", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check(lines[0], 2, 2, 1)
+    cfg = lines[0]["config"]
+    assert cfg["parallelism"].startswith("shared-env x2") and "2 competing processor replicas" in cfg["parallelism"]
+    dlv = cfg["delivery"]
+    assert dlv["exactly_once"] and dlv["completed"] == dlv["received"] == dlv["expected"] >= 2 * 32 * 3, dlv
+    assert dlv["dead_lettered"] == 0
+
+
 def test_bench_latency_runs():
     """bench_latency.py (SURVEY §7.5's own latency benchmarks): 2-hop CRUD and publish->ack lines."""
     env = dict(os.environ, PYTHONPATH=str(ROOT))
