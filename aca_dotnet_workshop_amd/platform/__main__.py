@@ -5,6 +5,8 @@ equivalent CLI.
     what-if   -f ... [--env-dir DIR]                        diff vs the running/recorded env
     up        -f ... --env-dir DIR [--detach]                deploy and run the environment
     status    --env-dir DIR                                  apps, revisions, replicas, ingress URLs
+    show      APP --env-dir DIR [--query ingress.fqdn]       one app (az containerapp show --query)
+    exec      APP --env-dir DIR -- CMD...                    run CMD in a replica's context (az containerapp exec)
     scale     APP --env-dir DIR [--min N] [--max N] [--replicas N]
     restart   APP --env-dir DIR                              restart the active revision
     apply     -f ... --env-dir DIR                           re-deploy changed apps as new revisions
@@ -208,6 +210,47 @@ def cmd_logs(a) -> int:
     return 0
 
 
+def cmd_show(a) -> int:
+    """``az containerapp show -n APP --query <path>``: one app's live description; ``--query``
+    takes a dotted path (``ingress.fqdn``, ``ingress.httpUrl``, ``desiredReplicas``) and prints the
+    bare value, for shell use (``FQDN=$(... show tasksmanager-frontend-webapp --query ingress.fqdn)``)."""
+    st, body = _uds_request(_ctl(a.env_dir), "GET", "/status")
+    app = body["apps"].get(a.app)
+    if app is None:
+        print(f"no app {a.app!r} in this environment", file=sys.stderr)
+        return 1
+    v = app
+    for part in (a.query.split(".") if a.query else []):
+        if isinstance(v, list) and part.isdigit() and int(part) < len(v):
+            v = v[int(part)]
+        elif isinstance(v, dict) and part in v:
+            v = v[part]
+        else:
+            print(f"{a.query!r} not found", file=sys.stderr)
+            return 1
+    print(v if isinstance(v, (str, int, float)) else json.dumps(v, indent=1))
+    return 0
+
+
+def cmd_exec(a) -> int:
+    """``az containerapp exec``: run a command inside a replica's context -- its sidecar is
+    reachable through ``DAPR_HTTP_UDS`` (a Unix socket: ``curl --unix-socket "$DAPR_HTTP_UDS"
+    http://localhost/v1.0/...``), as ``localhost:3500`` is from inside a Container App."""
+    st, body = _uds_request(_ctl(a.env_dir), "GET", "/status")
+    app = body["apps"].get(a.app)
+    reps = [p for r in (app or {}).get("revisions", []) if r["active"] for p in r["replicas"] if p["alive"]]
+    if not reps:
+        print(f"no running replica of {a.app!r}", file=sys.stderr)
+        return 1
+    rep = next((p for p in reps if p["name"] == a.replica), None) if a.replica else reps[0]
+    if rep is None:
+        print(f"no replica {a.replica!r}", file=sys.stderr)
+        return 1
+    cmd = a.command
+    env = dict(os.environ, DAPR_HTTP_UDS=rep["sidecar"], TT_REPLICA_NAME=rep["name"], CONTAINER_APP_NAME=a.app)
+    return subprocess.call(cmd or ["bash"], env=env)
+
+
 def cmd_outputs(a) -> int:
     st, body = _uds_request(_ctl(a.env_dir), "GET", "/status")
     print(json.dumps(body["outputs"], indent=1))
@@ -336,6 +379,16 @@ def main(argv: list[str] | None = None) -> int:
         if name == "down":
             p.add_argument("--delete", action="store_true")
         p.set_defaults(fn=fn)
+    p = sub.add_parser("show")
+    p.add_argument("app")
+    p.add_argument("--env-dir", required=True)
+    p.add_argument("--query", default=None)
+    p.set_defaults(fn=cmd_show)
+    p = sub.add_parser("exec")
+    p.add_argument("app")
+    p.add_argument("--env-dir", required=True)
+    p.add_argument("--replica", default=None)
+    p.set_defaults(fn=cmd_exec)  # the command follows "--"
     p = sub.add_parser("scale")
     p.add_argument("app")
     p.add_argument("--env-dir", required=True)
@@ -364,7 +417,13 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--out", default="dist/images")
     p.add_argument("--verify", action="store_true", help="run each image under chroot and probe it (root)")
     p.set_defaults(fn=cmd_image)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    tail: list[str] = []
+    if "--" in argv:  # exec APP ... -- CMD ARGS: everything after "--" is the command
+        i = argv.index("--")
+        argv, tail = argv[:i], argv[i + 1:]
     a = ap.parse_args(argv)
+    a.command = tail
     try:
         return a.fn(a)
     except ManifestError as e:

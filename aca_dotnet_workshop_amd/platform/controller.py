@@ -59,6 +59,7 @@ class AppRuntime:
     spec: dict[str, Any]
     revisions: list[Revision] = field(default_factory=list)
     ingress: Ingress | None = None
+    ingress_sig: str | None = None  # the ingress config the listener was opened with
     autoscaler: Autoscaler | None = None
     desired: int = 1
     restarts: int = 0
@@ -269,6 +270,7 @@ class EnvironmentController:
         rev_name = f"{spec['name']}--{spec.get('revisionSuffix') or tmpl[:7]}"
         cur = rt.current
         if cur is not None and cur.template == tmpl:
+            await self._reconcile_ingress(rt)  # app-level config: no new revision
             return rt
         rev = Revision(rev_name, tmpl)
         rt.revisions.append(rev)
@@ -293,10 +295,31 @@ class EnvironmentController:
         rev.replicas.clear()
         self.event("RevisionDeactivated", app=rt.name, revision=rev.name)
 
+    @staticmethod
+    def _ingress_sig(ing: dict[str, Any] | None) -> str | None:
+        """What needs a new listener when it changes (traffic weights are applied live)."""
+        if ing is None:
+            return None
+        return json.dumps({k: ing.get(k) for k in ("external", "port", "transport", "allowInsecure")}, sort_keys=True,
+                          default=str)
+
+    async def _reconcile_ingress(self, rt: AppRuntime) -> None:
+        """``az containerapp ingress update/enable/disable``: an ingress change is app-level
+        configuration -- the listener is replaced, the running revision stays."""
+        want = rt.spec.get("ingress")
+        if rt.ingress is not None and self._ingress_sig(want) != rt.ingress_sig:
+            await rt.ingress.stop()
+            rt.ingress = None
+            self.event("IngressRemoved" if want is None else "IngressUpdated", app=rt.name)
+        if want is not None and rt.ingress is None:
+            await self._ensure_ingress(rt)
+        self._refresh_backends(rt)
+
     async def _ensure_ingress(self, rt: AppRuntime) -> None:
         if rt.ingress is not None:
             return
         ing = rt.spec["ingress"]
+        rt.ingress_sig = self._ingress_sig(ing)
         route = IngressRoute(rt.name, bool(ing.get("external", False)))
         rt.ingress = Ingress(route)
         port = int(ing.get("port") or 0)
@@ -467,7 +490,8 @@ class EnvironmentController:
             ing = rt.ingress
             apps[rt.name] = {
                 "revisions": [{"name": r.name, "active": r.active, "created": r.created,
-                               "replicas": [{"name": p.name, "pid": p.proc.pid, "alive": p.alive(), "appPort": p.app_port}
+                               "replicas": [{"name": p.name, "pid": p.proc.pid, "alive": p.alive(), "appPort": p.app_port,
+                                             "sidecar": p.sidecar_uds}
                                             for p in r.replicas]} for r in rt.revisions],
                 "desiredReplicas": rt.desired, "restarts": rt.restarts,
                 "scale": rt.spec.get("scale"), "lastMetrics": rt.last_metrics, "scaleEvents": rt.scale_events[-20:],

@@ -16,6 +16,7 @@ import argparse
 import asyncio
 import logging
 import os
+import tempfile
 import signal
 import subprocess
 import sys
@@ -41,7 +42,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="serve the gRPC API (dapr.proto.runtime.v1.Dapr) on this port (0 = ephemeral; off if unset)")
     r.add_argument("--unix-socket-dir", default=None, help="expose the sidecar API and internal port as Unix sockets here")
     r.add_argument("--resources-path", "--components-path", dest="resources", action="append", default=[])
-    r.add_argument("--registry-dir", default=os.environ.get("TT_REGISTRY_DIR"))
+    r.add_argument("--registry-dir", default=os.environ.get("TT_REGISTRY_DIR") or default_registry_dir(),
+                   help="name-resolution directory shared by the sidecars of one host (self-hosted Dapr's mDNS); "
+                        "default: $TT_REGISTRY_DIR or /tmp/tt-registry-<uid>")
     r.add_argument("--backing-url", default=os.environ.get("TT_BACKING_URL"))
     r.add_argument("--identity", default=os.environ.get("TT_IDENTITY"))
     r.add_argument("--app-max-concurrency", type=int, default=None)
@@ -56,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="workload certificate for mutual TLS with peer sidecars (with --mtls-key/--mtls-ca)")
     r.add_argument("--mtls-key", default=os.environ.get("TT_MTLS_KEY"))
     r.add_argument("--mtls-ca", default=os.environ.get("TT_MTLS_CA"))
+    r.add_argument("--data-plane", choices=("native", "python"),
+                   default=os.environ.get("TT_SIDECAR_DATAPLANE") or "native",
+                   help="native: hot HTTP/gRPC API paths served by the C++ data plane (default); python: all in-process")
     r.add_argument("command", nargs=argparse.REMAINDER, help="-- <app command>")
     return ap
 
@@ -80,7 +86,7 @@ async def _run(a: argparse.Namespace) -> int:
                  mtls={"cert": a.mtls_cert, "key": a.mtls_key, "ca": a.mtls_ca}
                  if a.mtls_cert and a.mtls_key and a.mtls_ca else None,
                  grpc_uds=os.path.join(a.unix_socket_dir, f"{tag}.g.sock") if a.unix_socket_dir and a.dapr_grpc_port is not None
-                 else None)
+                 else None, data_plane=a.data_plane)
     await sc.start()
     loop = asyncio.get_running_loop()
     stop = asyncio.Event()
@@ -117,6 +123,11 @@ async def _run(a: argparse.Namespace) -> int:
         await asyncio.wait([stopper, done_sc], return_when=asyncio.FIRST_COMPLETED)
     await sc.stop()
     return proc.returncode if proc is not None and proc.returncode is not None else 0
+
+
+def default_registry_dir() -> str:
+    """One registry per user and host, like self-hosted Dapr's mDNS zone."""
+    return os.path.join(tempfile.gettempdir(), f"tt-registry-{os.getuid()}")
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -1015,7 +1015,15 @@ class Sidecar:
         return empty(204)
 
     async def h_healthz(self, req: Request) -> Response:
-        return empty(204) if self.ready.is_set() else empty(500)
+        """Dapr's health API: ``/v1.0/healthz`` is 204 once the sidecar is initialized AND its app
+        channel is up (daprd waits for the app port first); ``/v1.0/healthz/outbound`` only needs
+        the sidecar's own side (components loaded), for apps that call it during their startup."""
+        if not self.ready.is_set():
+            return empty(500)
+        has_app = self.app_port is not None or bool(self.app_uds)
+        if req.path.rstrip("/").endswith("/outbound") or not has_app or self.app_ready.is_set():
+            return empty(204)
+        return empty(500)
 
     async def h_shutdown(self, req: Request) -> Response:
         asyncio.get_running_loop().call_later(0.05, lambda: asyncio.ensure_future(self.stop()))
