@@ -434,7 +434,10 @@ class BackingServices:
             b = self.broker(ns)
             key = f"{ns}|{entity}"
             deadline = time.monotonic() + wait_s
+            conn = req.state.get("conn")
             while True:
+                if conn is not None and conn.closed:
+                    return json_response([])  # the receiver is gone: take no messages for it
                 msgs = b.receive(entity, mx, lock)
                 rem = deadline - time.monotonic()
                 if msgs or rem <= 0:

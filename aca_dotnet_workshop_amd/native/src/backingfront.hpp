@@ -546,6 +546,12 @@ class BackingFront {
 
   // Returns true when the request was answered (messages, or deadline reached).
   bool try_receive(Broker* b, Parked& p, bool expired) {
+    // a receiver that went away (its process died mid long poll) must not lock messages it can
+    // never settle -- they would sit out the whole lock duration before redelivery
+    if (p.reply.abandoned()) {
+      p.reply.send(204, {}, {});  // nobody reads it: lets the half-closed connection finish and close
+      return true;
+    }
     std::vector<Received> msgs;
     try {
       msgs = b->receive(p.entity, p.max, p.lock_ms);

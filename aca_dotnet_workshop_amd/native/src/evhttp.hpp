@@ -517,6 +517,9 @@ class Reply {
     send(status, {{"content-type", "application/json"}}, body);
   }
   void empty(int status) const { send(status, {}, {}); }
+  // The client is gone (connection closed, or the peer shut down its side): a parked long
+  // poll must not take messages for it.
+  bool abandoned() const;
 
  private:
   std::weak_ptr<ServerConn> conn_;
@@ -568,6 +571,8 @@ class ServerConn : public IoObj {
     if ((ev & EPOLLOUT) || (tls_ && out_off_ < out_.size())) flush();
     else if (tls_) update_interest();
   }
+
+  bool peer_gone() const { return dead || peer_closed_; }
 
   void respond(uint64_t seq, int status, const HeaderList& headers, std::string_view body, bool head_request) {
     if (dead || seq < head_seq_) return;
@@ -697,6 +702,12 @@ class ServerConn : public IoObj {
 
   void close_now() { loop_.remove(this); }
 };
+
+inline bool Reply::abandoned() const {
+  if (sink_) return false;
+  auto c = conn_.lock();
+  return !c || c->peer_gone();
+}
 
 inline void Reply::send(int status, const HeaderList& headers, std::string_view body) const {
   if (sink_) {

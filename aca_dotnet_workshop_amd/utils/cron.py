@@ -7,7 +7,8 @@ uses ``"5 0 * * *"``):
 * ``*``, ``?``, lists ``a,b``, ranges ``a-b``, steps ``*/n`` / ``a-b/n`` / ``a/n``,
   month names ``JAN..DEC`` and weekday names ``SUN..SAT`` (``7`` = Sunday);
 * descriptors ``@yearly @annually @monthly @weekly @daily @midnight @hourly`` and
-  ``@every <duration>`` (``10s``, ``1m30s``, ``2h``, ``500ms``).
+  ``@every <duration>`` (``10s``, ``1m30s``, ``2h``, ``500ms``), ticking on multiples of the
+  interval since the Unix epoch (replicas agree on the ticks).
 
 Day matching follows cron convention: when both day-of-month and day-of-week are
 restricted a day matches if *either* matches.
@@ -126,7 +127,14 @@ class CronSchedule:
     def next_after(self, after: datetime) -> datetime:
         """First fire time strictly after ``after`` (timezone preserved; naive = UTC)."""
         if self.every is not None:
-            return after + self.every
+            # aligned to multiples of the interval since the Unix epoch, so every replica of an
+            # app computes the same ticks (the singleReplica lease is keyed by the tick)
+            naive = after.tzinfo is None
+            base = after.replace(tzinfo=timezone.utc) if naive else after
+            step = int(round(self.every.total_seconds() * 1e6))
+            us = int(round(base.timestamp() * 1e6))
+            nxt = datetime.fromtimestamp((us // step + 1) * step / 1e6, tz=timezone.utc).astimezone(base.tzinfo)
+            return nxt.replace(tzinfo=None) if naive else nxt
         t = after.replace(microsecond=0) + timedelta(seconds=1)
         limit = after + timedelta(days=366 * 5)
         while t <= limit:

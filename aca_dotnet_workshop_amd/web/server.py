@@ -201,6 +201,7 @@ class HttpServerProtocol(asyncio.Protocol):
                 del buf[:length]
             self.pending = None
             req = Request(method, target, headers, body, self.peer, version)
+            req.state["conn"] = self  # long polls check conn.closed (the client went away)
             if self.tls is not None:
                 req.state["tls"] = self.tls
             self.queue.append(req)

@@ -114,6 +114,30 @@ def test_messaging_and_long_poll(front, monkeypatch):
 
 
 @pytest.mark.parametrize("front", FRONTS)
+def test_abandoned_long_poll_takes_no_messages(front, monkeypatch):
+    """A receiver that disconnects in the middle of its long poll (its process died) must not get
+    -- and lock -- the next message: a live receiver gets it at once, not after the lock expires."""
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.sb_create_subscription("ns", "t2", "s", lock_ms=60000, max_delivery=5)
+            host, port = b.base.rsplit(":", 1)
+            r, w = await asyncio.open_connection("127.0.0.1", int(port))
+            w.write(b"POST /servicebus/ns/receive?entity=t2/subscriptions/s&max=5&lockMs=60000&waitMs=10000 HTTP/1.1\r\n"
+                    b"host: x\r\nx-tt-identity: x\r\ncontent-length: 0\r\n\r\n")
+            await w.drain()
+            await asyncio.sleep(0.2)   # parked
+            w.close()                  # the receiver dies
+            await asyncio.sleep(0.3)
+            await c.sb_publish("ns", "t2", b'{"x": 1}', "application/json")
+            t0 = time.monotonic()
+            msgs = await c.sb_receive("ns", "t2/subscriptions/s", 5, 60000, 3000)
+            assert len(msgs) == 1 and msgs[0]["deliveryCount"] == 1 and time.monotonic() - t0 < 1.5
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
 def test_rbac(front, monkeypatch):
     policy = {"mode": "enforce", "keys": {"cosmos/acct": "masterkey"},
               "roleAssignments": [

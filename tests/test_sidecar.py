@@ -240,3 +240,50 @@ def test_cloudevent_envelope():
     assert ce["type"] == "com.dapr.event.sent" and ce["traceparent"].startswith("00-111")
     assert make_cloudevent(b"hi", "text/plain", "ps", "t", "app", None)["data"] == "hi"
     assert "data_base64" in make_cloudevent(b"\x00\x01", "application/octet-stream", "ps", "t", "app", None)
+
+
+def test_cron_single_replica_lease():
+    """``singleReplica: "true"``: several replicas of the processor run the same cron binding, and
+    each tick is delivered by exactly one of them (a first-write lease document per tick in the
+    state store) -- the scale-out vs. periodic-job conflict the reference leaves open
+    (docs/aca/07-aca-cron-bindings/index.md:234)."""
+    comp = _inline("tick", "bindings.cron", {"schedule": "@every 200ms", "singleReplica": "true"})
+    hits: list[tuple[str, str]] = []
+
+    def app(tag):
+        a = WebApp(f"cron-{tag}")
+
+        async def on_tick(req):
+            hits.append((tag, req.headers.get("x-fire-time") or req.headers.get("fireTime") or
+                         json.dumps(sorted(req.headers.items()))))
+            return empty(200)
+        a.add_route("/tick", on_tick, ("POST",))
+        return a
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        backing = BackingServices()
+        bsrv = HttpServer(backing.build_app(), loop)
+        burl = f"http://127.0.0.1:{await bsrv.listen_tcp('127.0.0.1', 0)}"
+        servers, cars = [], []
+        for tag in "abc":
+            a = app(tag)
+            s = HttpServer(a, loop)
+            await a.startup()
+            port = await s.listen_tcp("127.0.0.1", 0)
+            sc = Sidecar("proc", app_port=port, http_port=0, components=[comp], resolver=NameResolver(),
+                         backing_url=burl, identity="proc", instance=f"proc-{tag}")
+            await sc.start()
+            servers.append(s)
+            cars.append(sc)
+        await asyncio.sleep(2.1)
+        for sc in cars:
+            await sc.stop(1.0)
+        for s in servers:
+            await s.close(1.0)
+        await bsrv.close(1.0)
+        fired = sum(b.fired for sc in cars for b in sc.bindings.values())
+        assert 7 <= fired <= 12, fired                   # ~10 ticks in 2 s, each fired once
+        assert len(hits) == fired                        # every claimed tick was delivered once
+        assert len({t for t, _ in hits}) >= 1
+    run(main())
