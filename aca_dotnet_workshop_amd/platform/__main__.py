@@ -7,6 +7,8 @@ equivalent CLI.
     status    --env-dir DIR                                  apps, revisions, replicas, ingress URLs
     show      APP --env-dir DIR [--query ingress.fqdn]       one app (az containerapp show --query)
     exec      APP --env-dir DIR -- CMD...                    run CMD in a replica's context (az containerapp exec)
+    image     [--service S] [--verify] [--push ACR --variant V --tag T]   build (and push) the images
+    acr       NAME                                           a registry's repositories and tags
     scale     APP --env-dir DIR [--min N] [--max N] [--replicas N]
     restart   APP --env-dir DIR                              restart the active revision
     apply     -f ... --env-dir DIR                           re-deploy changed apps as new revisions
@@ -337,9 +339,26 @@ def cmd_telemetry(a) -> int:
 
 
 def cmd_image(a) -> int:
+    """Build (``az acr build`` / ``docker build``), optionally verify, and with ``--push REGISTRY``
+    push each service's ``--variant`` image as ``tasksmanager/<app id>:<tag>``."""
     from . import image
+    reg = None
+    if a.push:
+        from .registry import LocalRegistry
+        reg = LocalRegistry(a.push, a.registry_root)
     for row in image.report(a.out, a.service, a.verify):
+        if reg is not None and row["variant"] == a.variant:
+            repo = f"tasksmanager/{image.SERVICES[row['service']]}"
+            row["pushed"] = f"{reg.login_server}/{repo}:{a.tag}@{reg.push(row['archive'], repo, a.tag)}"
         print(json.dumps(row), flush=True)
+    return 0
+
+
+def cmd_acr(a) -> int:
+    """``az acr repository list/show-tags``: what a registry holds."""
+    from .registry import LocalRegistry
+    reg = LocalRegistry(a.name, a.registry_root)
+    print(json.dumps({"loginServer": reg.login_server, "repositories": reg.repositories()}, indent=1))
     return 0
 
 
@@ -416,7 +435,15 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--service", action="append", choices=["backend_api", "processor", "frontend"])
     p.add_argument("--out", default="dist/images")
     p.add_argument("--verify", action="store_true", help="run each image under chroot and probe it (root)")
+    p.add_argument("--push", metavar="REGISTRY", default=None, help="push to this registry (ACR name)")
+    p.add_argument("--variant", choices=["standard", "chiseled"], default="standard", help="which variant --push pushes")
+    p.add_argument("--tag", default="latest")
+    p.add_argument("--registry-root", default=None, help="where registries live ($TT_CONTAINER_REGISTRY_ROOT)")
     p.set_defaults(fn=cmd_image)
+    p = sub.add_parser("acr", help="list a registry's repositories and tags")
+    p.add_argument("name")
+    p.add_argument("--registry-root", default=None)
+    p.set_defaults(fn=cmd_acr)
     argv = list(sys.argv[1:] if argv is None else argv)
     tail: list[str] = []
     if "--" in argv:  # exec APP ... -- CMD ARGS: everything after "--" is the command

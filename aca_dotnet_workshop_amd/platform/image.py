@@ -11,14 +11,22 @@ itself and writes them as OCI image-layout archives that ``docker load`` / ``pod
     library (minus test suites / IDLE / Tk / ensurepip) with every extension module, the full
     site-packages distributions the service imports, and the service's package.
 ``chiseled``
-    Only what the service actually loads.  The service is started under a tracer, exercised
-    (``GET`` of its health/landing route), and the files it mapped or imported are recorded:
-    interpreter, the shared objects in ``/proc/self/maps`` (libc, libpython, the loader, ...),
-    every imported module -- compiled to sourceless ``.pyc`` -- plus the package's data files.
-    No shell, no pip, non-root user ``65532``.
+    Only what the service can load.  The closure is the union of
+    (a) traces: the service is started under a tracer in EVERY configuration it supports
+        (``MODES``: HTTP and gRPC SDK transport, asyncio and native app host, each notifier
+        mode, fake and store manager, Dapr and plain-HTTP frontend), probed, and the files it
+        mapped or imported are recorded -- interpreter, the shared objects of
+        ``/proc/self/maps`` (libc, libpython, the loader, our native host), every module; and
+    (b) the static import graph of the service's own package modules (``static_closure``:
+        every import statement, including the lazy ones inside functions, followed through
+        the package; the third-party and standard-library packages they name are shipped
+        whole), so a code path no trace exercised still finds its modules.
+    Python files are compiled to sourceless ``.pyc``; plus the package's data files.  No shell,
+    no pip, non-root user ``65532``.
 
 Each image is a single gzip layer; ``verify_image`` unpacks it and runs the service inside it
-with ``chroot`` (root only) to prove the closure is complete.  ``report`` prints the size table
+with ``chroot`` (root only) in every mode of ``MODES`` -- and drives the lazily imported paths
+(``VERIFY_CALLS``) -- to prove the closure is complete.  ``report`` prints the size table
 that docs/modules/12-optimize-containers.md compares with the reference's.
 """
 from __future__ import annotations
@@ -39,6 +47,7 @@ import tempfile
 import time
 from dataclasses import dataclass, field
 from pathlib import Path
+from typing import Any
 
 PKG = "aca_dotnet_workshop_amd"
 PKG_ROOT = Path(__file__).resolve().parents[1]
@@ -46,6 +55,26 @@ SERVICES = {"backend_api": "tasksmanager-backend-api", "processor": "tasksmanage
             "frontend": "tasksmanager-frontend-webapp"}
 PROBE = {"backend_api": "/api/tasks?createdBy=tjoudeh@bitoftech.net", "processor": "/dapr/subscribe",
          "frontend": "/"}
+# Every configuration a service supports (env overrides) -- each is traced into the chiseled
+# closure and verified inside the image.
+MODES: dict[str, list[dict[str, str]]] = {
+    "backend_api": [{}, {"TT_APP_HOST": "native"},
+                    {"TasksManager__Backend": "store", "Dapr__ApiProtocol": "grpc"},
+                    {"TasksManager__Backend": "store", "TT_APP_HOST": "native", "Dapr__ApiProtocol": "grpc"}],
+    "processor": [{}, {"TT_APP_HOST": "native"}, {"Dapr__ApiProtocol": "grpc"},
+                  {"TasksNotifier__Mode": "sendgrid-api", "SendGrid__Endpoint": "http://127.0.0.1:9"},
+                  {"TasksNotifier__Mode": "sendgrid-binding"}],
+    "frontend": [{}, {"TT_APP_HOST": "native"}, {"Frontend__BackendMode": "http"}, {"Dapr__ApiProtocol": "grpc"}],
+}
+# Requests that reach code paths importing modules lazily (a notifier mode's client, ...):
+# (mode index, method, path, body) -- run by verify_image after the probe.
+_TASK = json.dumps({"taskId": "00000000-0000-4000-8000-000000000001", "taskName": "probe", "taskCreatedBy": "a@b.c",
+                    "taskCreatedOn": "2030-01-01T00:00:00", "taskDueDate": "2030-01-02T00:00:00",
+                    "taskAssignedTo": "a@b.c", "isCompleted": False, "isOverDue": False})
+VERIFY_CALLS: dict[str, list[tuple[int, str, str, str]]] = {
+    "processor": [(3, "POST", "/api/tasksnotifier/tasksaved", _TASK), (4, "POST", "/api/tasksnotifier/tasksaved", _TASK)],
+}
+BUILD_ONLY = {"pybind11"}  # compiles the native module in-tree; images ship the built .so
 APP_DIR = "/app"
 NONROOT = 65532
 _STDLIB_SKIP = {"test", "idlelib", "tkinter", "turtledemo", "ensurepip", "lib2to3", "pydoc_data", "__pycache__",
@@ -133,12 +162,14 @@ def _service_env(port: int) -> dict[str, str]:
     return env
 
 
-def trace_closure(service: str) -> dict:
-    """Start the service under the tracer, probe it, and return the files it loaded."""
+def trace_closure(service: str, mode: dict[str, str] | None = None) -> dict:
+    """Start the service under the tracer (in configuration ``mode``), probe it, and return the
+    files it loaded."""
     port = _free_port()
     with tempfile.TemporaryDirectory(prefix="ttimg-") as d:
         dump = os.path.join(d, "closure.json")
-        env = {"PATH": os.environ.get("PATH", ""), "PYTHONPATH": str(PKG_ROOT.parent), **_service_env(port)}
+        env = {"PATH": os.environ.get("PATH", ""), "PYTHONPATH": str(PKG_ROOT.parent), **_service_env(port),
+               **(mode or {})}
         proc = subprocess.Popen([sys.executable, "-c", _BOOT, dump, f"{PKG}.services.{service}"], env=env,
                                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         try:
@@ -158,6 +189,132 @@ def trace_closure(service: str) -> dict:
             except subprocess.TimeoutExpired:
                 proc.kill()
                 proc.wait()
+
+
+def _module_file(mod: str) -> Path | None:
+    p = PKG_ROOT.joinpath(*mod.split(".")[1:])
+    if (p / "__init__.py").exists():
+        return p / "__init__.py"
+    if p.with_suffix(".py").exists():
+        return p.with_suffix(".py")
+    return None
+
+
+def static_closure(service: str) -> tuple[set[Path], set[str]]:
+    """The static import graph from the service's entry module through this package: (package
+    module files, dotted names of the external modules they import).  Every import statement
+    counts -- module level or inside a function -- except the lazy re-exports of a package's
+    ``__getattr__`` (PEP 562), which serve other importers, not the package itself."""
+    import ast
+    files: set[Path] = set()
+    external: set[str] = set()
+    todo = [f"{PKG}.services.{service}.__main__"]
+    seen: set[str] = set()
+    while todo:
+        mod = todo.pop()
+        if mod in seen:
+            continue
+        seen.add(mod)
+        f = _module_file(mod)
+        if f is None:
+            continue
+        files.add(f)
+        parts = mod.split(".")
+        todo.extend(".".join(parts[:i]) for i in range(2, len(parts)))  # parent packages' __init__
+        tree = ast.parse(f.read_text())
+        lazy: set[int] = set()
+        for fn in ast.walk(tree):
+            if isinstance(fn, ast.FunctionDef) and fn.name == "__getattr__":
+                lazy.update(id(x) for x in ast.walk(fn))
+        is_pkg = f.name == "__init__.py"
+        for n in ast.walk(tree):
+            if id(n) in lazy:
+                continue
+            names: list[str] = []
+            if isinstance(n, ast.Import):
+                names = [a.name for a in n.names]
+            elif isinstance(n, ast.ImportFrom):
+                if n.level:
+                    base = parts if is_pkg else parts[:-1]
+                    base = base[:len(base) - (n.level - 1)]
+                    head = ".".join(base + ([n.module] if n.module else []))
+                else:
+                    head = n.module or ""
+                names = [head] + [f"{head}.{a.name}" for a in n.names]
+            for nm in names:
+                if not nm:
+                    continue
+                if nm.split(".")[0] == PKG:
+                    todo.append(nm)
+                elif nm.split(".")[0] not in BUILD_ONLY:
+                    external.add(nm)
+    return files, external
+
+
+def _external_files(names: set[str]) -> tuple[set[Path], set[Path]]:
+    """(python files, shared objects) of the standard-library modules and site-packages
+    distributions named in ``names`` -- whole top-level packages (a namespace package such as
+    ``google``: its imported subpackage)."""
+    import importlib.util
+    py: set[Path] = set()
+    so: set[Path] = set()
+    done: set[str] = set()
+    for name in sorted(names):
+        parts = name.split(".")
+        top = parts[0]
+        try:
+            spec = importlib.util.find_spec(top)
+        except (ImportError, ValueError):
+            continue
+        if spec is None:
+            continue
+        if spec.origin is None and spec.submodule_search_locations and len(parts) > 1:  # namespace package
+            top = ".".join(parts[:2])
+            try:
+                spec = importlib.util.find_spec(top)
+            except (ImportError, ValueError):
+                continue
+            if spec is None:
+                continue
+        if top in done:
+            continue
+        done.add(top)
+        if spec.origin in (None, "built-in", "frozen"):
+            continue
+        origin = Path(spec.origin)
+        if spec.submodule_search_locations:  # package: ship it whole
+            for loc in spec.submodule_search_locations:
+                for f in Path(loc).rglob("*"):
+                    if not f.is_file() or "__pycache__" in f.parts or {"tests", "test"} & set(f.parts):
+                        continue
+                    if f.suffix == ".py":
+                        py.add(f)
+                    elif ".so" in f.name:
+                        so.add(f)
+        elif origin.suffix == ".py":
+            py.add(origin)
+        elif ".so" in origin.name:
+            so.add(origin)
+    return py, so
+
+
+def full_closure(service: str) -> dict:
+    """The chiseled closure: traces of every mode of ``MODES`` plus the static import graph."""
+    merged: dict[str, Any] = {"modules": set(), "maps": set()}
+    for mode in MODES.get(service, [{}]):
+        c = trace_closure(service, mode)
+        merged["exe"] = c["exe"]
+        merged["modules"].update(c["modules"])
+        merged["maps"].update(c["maps"])
+    files, external = static_closure(service)
+    py, so = _external_files(external)
+    merged["modules"].update(str(p.resolve()) for p in files | py)
+    merged["maps"].update(str(p.resolve()) for p in so)
+    merged["static"] = {"package_modules": len(files), "external": sorted(external)}
+    merged["modes"] = MODES.get(service, [{}])
+    merged["modules"] = sorted(merged["modules"])
+    merged["maps"] = sorted(merged["maps"])
+    return merged
 
 
 # --------------------------------------------------------------------------- file sets
@@ -448,7 +605,7 @@ def build_image(service: str, variant: str, out_dir: str | Path, closure: dict |
         raise ValueError(f"unknown service {service!r} (one of {sorted(SERVICES)})")
     if variant not in ("standard", "chiseled"):
         raise ValueError("variant must be 'standard' or 'chiseled'")
-    closure = closure or trace_closure(service)
+    closure = closure or full_closure(service)
     plan = plan_image(service, variant, closure)
     layer = _tar_layer(plan, variant)
     tag = f"tasksmanager/{SERVICES[service]}:{variant}"
@@ -473,53 +630,79 @@ def unpack_rootfs(archive: Path, dest: Path) -> dict:
     return cfg
 
 
-def verify_image(archive: Path, service: str, timeout: float = 60.0) -> dict:
-    """Run the image's entrypoint inside its own root filesystem (``chroot``, needs root), GET
-    the service's probe route, stop it; returns ``{"status", "body", "log"}`` (``log`` = its
-    stderr, where a missing module or extension would show)."""
+def _http(port: int, method: str, path: str, body: str, timeout: float = 10.0) -> int:
+    import http.client
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=timeout)
+    try:
+        c.request(method, path, body.encode(), {"content-type": "application/json"})
+        r = c.getresponse()
+        r.read()
+        return r.status
+    finally:
+        c.close()
+
+
+def verify_image(archive: Path, service: str, timeout: float = 60.0, modes: list[dict[str, str]] | None = None) -> dict:
+    """Run the image's entrypoint inside its own root filesystem (``chroot``, needs root) in every
+    mode (default ``MODES[service]``): GET the probe route, issue the mode's ``VERIFY_CALLS``
+    (lazily imported code paths), stop it.  Returns ``{"status", "body", "log", "modes"}``
+    (``log`` = stderr of all runs, where a missing module or extension would show)."""
     if os.geteuid() != 0:
         raise PermissionError("verify_image needs root (chroot)")
+    modes = MODES.get(service, [{}]) if modes is None else modes
     with tempfile.TemporaryDirectory(prefix="ttroot-") as d:
         root = Path(d)
         root.chmod(0o755)  # mkdtemp is 0700: the non-root user must traverse "/"
         cfg = unpack_rootfs(archive, root)["config"]
-        port = _free_port()
-        env = {e.split("=", 1)[0]: e.split("=", 1)[1] for e in cfg["Env"]}
-        env.update(_service_env(port))
-        env["Logging__LogLevel__Default"] = "Information"
         user = cfg.get("User", "0:0")
         cmd = [shutil.which("chroot") or "/usr/sbin/chroot", f"--userspec={user}", str(root)] + cfg["Entrypoint"]
-        with tempfile.TemporaryFile() as errf:
-            proc = subprocess.Popen(cmd, env=env, cwd=str(root), stdout=subprocess.DEVNULL, stderr=errf)
-            try:
-                status, body = _wait_http(port, PROBE[service], proc, timeout)
-            except Exception as e:
-                proc.kill()
-                proc.wait()
+        logs, first, results = [], None, []
+        for i, mode in enumerate(modes):
+            port = _free_port()
+            env = {e.split("=", 1)[0]: e.split("=", 1)[1] for e in cfg["Env"]}
+            env.update(_service_env(port))
+            env.update(mode)
+            env["Logging__LogLevel__Default"] = "Information"
+            with tempfile.TemporaryFile() as errf:
+                proc = subprocess.Popen(cmd, env=env, cwd=str(root), stdout=subprocess.DEVNULL, stderr=errf)
+                try:
+                    status, body = _wait_http(port, PROBE[service], proc, timeout)
+                    calls = [(m, p, _http(port, m, p, b)) for k, m, p, b in VERIFY_CALLS.get(service, []) if k == i]
+                except Exception as e:
+                    proc.kill()
+                    proc.wait()
+                    errf.seek(0)
+                    raise RuntimeError(f"image {archive.name} failed in mode {mode}: {e}\n"
+                                       f"{errf.read().decode('utf-8', 'replace')[-2000:]}") from None
+                proc.terminate()
+                try:
+                    proc.wait(10)
+                except subprocess.TimeoutExpired:
+                    proc.kill()
+                    proc.wait()
                 errf.seek(0)
-                raise RuntimeError(f"image {archive.name} failed: {e}\n"
-                                   f"{errf.read().decode('utf-8', 'replace')[-2000:]}") from None
-            proc.terminate()
-            try:
-                proc.wait(10)
-            except subprocess.TimeoutExpired:
-                proc.kill()
-                proc.wait()
-            errf.seek(0)
-            return {"status": status, "body": body, "log": errf.read().decode("utf-8", "replace")}
+                log = errf.read().decode("utf-8", "replace")
+            logs.append(log)
+            results.append({"mode": mode, "status": status, "calls": calls,
+                            "clean": "Traceback" not in log and "ModuleNotFoundError" not in log})
+            if first is None:
+                first = (status, body)
+        return {"status": first[0], "body": first[1], "log": "\n".join(logs), "modes": results}
 
 
 def report(out_dir: str | Path, services: list[str] | None = None, verify: bool = False) -> list[dict]:
     rows = []
     for svc in services or list(SERVICES):
-        closure = trace_closure(svc)
+        closure = full_closure(svc)
         for variant in ("standard", "chiseled"):
             r = build_image(svc, variant, out_dir, closure)
             row = r.row()
+            row["traced_modes"] = len(closure.get("modes", [])) or 1
             if verify:
                 v = verify_image(r.path, svc)
                 row["verified_status"] = v["status"]
-                row["verified_clean_log"] = "Traceback" not in v["log"] and "unavailable" not in v["log"]
+                row["verified_modes"] = len(v["modes"])
+                row["verified_clean_log"] = all(m["clean"] for m in v["modes"]) and "unavailable" not in v["log"]
             rows.append(row)
     return rows
 

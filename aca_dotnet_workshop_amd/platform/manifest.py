@@ -18,7 +18,7 @@ A manifest declares, in one YAML document, what the reference's IaC provisions
 Parameters: ``parameters:`` defaults, overridden by a parameters file (the
 ``main.parameters.json`` shape: ``{"parameters": {"x": {"value": ...}}}`` or flat JSON/YAML)
 and by ``--param k=v``.  Strings may contain ``${name}`` references and a handful of
-functions: ``${uniqueString(seed)}``, ``${empty(x)}``, ``${notEmpty(x)}``, ``${toLower(x)}``,
+functions: ``${uniqueString(seed)}``, ``${empty(x)}``, ``${notEmpty(x)}``, ``${toLower(x)}``, ``${if(c, a, b)}``,
 ``${concat(a,b,...)}``, ``${coalesce(a,b,...)}``.
 
 ``validate`` lints the manifest (the ``az bicep build`` + ARM ``Validate`` stage of
@@ -88,6 +88,10 @@ def _eval(expr: str, params: dict[str, Any]) -> Any:
             return "".join(map(str, args))
         if fn == "coalesce":
             return next((a for a in args if a not in (None, "")), "")
+        if fn == "if":  # Bicep's  cond ? a : b
+            if len(args) != 3:
+                raise ManifestError([f"if() takes 3 arguments in ${{{expr}}}"])
+            return args[1] if args[0] else args[2]
         raise ManifestError([f"unknown function {fn}() in ${{{expr}}}"])
     if (expr.startswith("'") and expr.endswith("'")) or (expr.startswith('"') and expr.endswith('"')):
         return expr[1:-1]
@@ -102,11 +106,30 @@ def substitute(node: Any, params: dict[str, Any]) -> Any:
         if m:  # whole-string expression keeps its type (bool/int/list)
             return _eval(m.group(1), params)
         return _EXPR.sub(lambda mm: _fmt(_eval(mm.group(1), params)), node)
-    if isinstance(node, list):
-        return [substitute(x, params) for x in node]
+    if isinstance(node, list):  # Bicep's conditional deployment: items with a false ``if:`` drop out
+        out = []
+        for x in node:
+            x = substitute(x, params)
+            if isinstance(x, dict) and "if" in x:
+                if not _truthy_cond(x.pop("if")):
+                    continue
+            out.append(x)
+        return out
     if isinstance(node, dict):
-        return {k: substitute(v, params) for k, v in node.items()}
+        d = {k: substitute(v, params) for k, v in node.items()}
+        for k, v in list(d.items()):  # a conditional object member (``resource x = if (...) {}``)
+            if isinstance(v, dict) and "if" in v:
+                if _truthy_cond(v.pop("if")):
+                    continue
+                del d[k]
+        return d
     return node
+
+
+def _truthy_cond(v: Any) -> bool:
+    if isinstance(v, str):
+        return v.strip().lower() not in ("", "false", "0", "no")
+    return bool(v)
 
 
 def _fmt(v: Any) -> str:
