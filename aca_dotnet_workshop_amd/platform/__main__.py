@@ -99,7 +99,7 @@ async def _up(a) -> int:
     from .controller import EnvironmentController
     configure_logging("platform")
     m = load_manifest(a.file, a.parameters, _params(a))
-    ctl = EnvironmentController(m, a.env_dir, a.polling_interval, a.cooldown)
+    ctl = EnvironmentController(m, a.env_dir, a.polling_interval, a.cooldown, registry_root=a.registry_root)
     import signal
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):
@@ -128,6 +128,8 @@ def cmd_up(a) -> int:
             args += ["--polling-interval", str(a.polling_interval)]
         if a.cooldown is not None:
             args += ["--cooldown", str(a.cooldown)]
+        if a.registry_root:
+            args += ["--registry-root", a.registry_root]
         logf = open(Path(a.env_dir) / "controller.log", "ab")
         p = subprocess.Popen(args, stdout=logf, stderr=subprocess.STDOUT, start_new_session=True)
         deadline = time.time() + a.timeout
@@ -385,6 +387,8 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--timeout", type=float, default=180.0)
     p.add_argument("--polling-interval", type=float, default=None)
     p.add_argument("--cooldown", type=float, default=None)
+    p.add_argument("--registry-root", default=None,
+                   help="where container registries live ($TT_CONTAINER_REGISTRY_ROOT); apps with an image pull from there")
     p.set_defaults(fn=cmd_up)
     p = sub.add_parser("apply")
     manifest_args(p, True)
@@ -436,7 +440,7 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--out", default="dist/images")
     p.add_argument("--verify", action="store_true", help="run each image under chroot and probe it (root)")
     p.add_argument("--push", metavar="REGISTRY", default=None, help="push to this registry (ACR name)")
-    p.add_argument("--variant", choices=["standard", "chiseled"], default="standard", help="which variant --push pushes")
+    p.add_argument("--variant", choices=["standard", "chiseled"], default="chiseled", help="which variant --push pushes")
     p.add_argument("--tag", default="latest")
     p.add_argument("--registry-root", default=None, help="where registries live ($TT_CONTAINER_REGISTRY_ROOT)")
     p.set_defaults(fn=cmd_image)

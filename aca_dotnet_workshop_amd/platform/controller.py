@@ -39,10 +39,16 @@ from .limits import Limits, ResourceLimiter
 from .pki import EnvironmentPki
 from .manifest import Manifest, ManifestError, desired_state, identity_of, template_hash, validate
 from .processes import LocalStack, ReplicaProc
+from .registry import LocalRegistry, RegistryError
 from .scaler import Autoscaler, ScaleRule, cron_metric
 
 log = logging.getLogger("platform")
 ADMIN = "platform-admin"
+
+
+class ImagePullError(Exception):
+    """A revision's image could not be pulled (unknown image, or the app identity lacks AcrPull):
+    ACA reports the revision as failed to provision."""
 
 
 @dataclass
@@ -78,7 +84,8 @@ class AppRuntime:
 
 class EnvironmentController:
     def __init__(self, manifest: Manifest, env_dir: str | os.PathLike, polling_interval: float | None = None,
-                 cooldown: float | None = None, log_level: str = "warning") -> None:
+                 cooldown: float | None = None, log_level: str = "warning",
+                 registry_root: str | os.PathLike | None = None) -> None:
         self.m = manifest
         self.dir = Path(env_dir).resolve()
         self.dir.mkdir(parents=True, exist_ok=True)
@@ -103,6 +110,9 @@ class EnvironmentController:
         self.apps: dict[str, AppRuntime] = {}
         self.backing: BackingClient | None = None
         self.storage_keys: dict[str, str] = {}
+        self.registry_root = registry_root
+        self.registry: LocalRegistry | None = None
+        self._pulled: dict[str, dict[str, Any]] = {}  # manifest digest -> unpacked container
         self.events: list[dict[str, Any]] = []
         self.stop_event = asyncio.Event()
         self._tasks: list[asyncio.Task] = []
@@ -199,6 +209,11 @@ class EnvironmentController:
                 for c in d.get("containers") or []:
                     ru = c.get("autoscaleMaxThroughput") or c.get("throughput") or 0
                     await b.doc_set_throughput(cdb["account"], d["name"], c["name"], float(ru))
+        acr = r.get("containerRegistry")
+        if acr and acr.get("name"):
+            self.registry = LocalRegistry(acr["name"], self.registry_root)
+            self.event("ContainerRegistryAttached", loginServer=self.registry.login_server,
+                       repositories=[x["repository"] for x in self.registry.repositories()])
         kv = r.get("keyVault")
         if kv:
             for s in kv.get("secrets") or []:
@@ -242,14 +257,45 @@ class EnvironmentController:
     def _ingress_uds(self, app: str) -> str:
         return str(self.stack.sock_dir / f"{app}.ingress.sock")
 
+    def _pull(self, spec: dict[str, Any]) -> dict[str, Any]:
+        """Pull the app's image from the environment's registry with the app identity: the
+        ``registries`` entry names the identity, which needs **AcrPull** on the registry
+        (container-apps.bicep:113-127).  Unpacked once per digest under ``runtime/images``."""
+        ref = spec["image"]
+        ident = identity_of(spec)
+        try:
+            if self.registry is None:
+                raise ImagePullError(f"{spec['name']}: image {ref}: the environment has no containerRegistry")
+            server = ref.split("/", 1)[0]
+            reg = next((r for r in spec.get("registries") or [] if r.get("server") == server), None)
+            if reg is None:
+                raise ImagePullError(f"{spec['name']}: no registry credentials for {server}")
+            scope = f"registry/{self.registry.name}"
+            if not any(ra["principal"] == ident and ra["role"] == "AcrPull" and ra["scope"] == scope
+                       for ra in self.m.role_assignments()):
+                raise ImagePullError(f"{spec['name']}: UNAUTHORIZED: identity {ident!r} has no AcrPull role on {scope}")
+            digest = self.registry.resolve(ref)
+            if digest in self._pulled:
+                return dict(self._pulled[digest], image=ref)
+            rootfs, cfg = self.registry.unpack(digest, self.dir / "runtime" / "images")
+        except (ImagePullError, RegistryError) as e:
+            self.event("ImagePullFailed", app=spec["name"], image=ref, error=str(e))
+            raise ImagePullError(str(e)) from None
+        c = {"image": ref, "digest": digest, "rootfs": str(rootfs), "config": cfg["config"]}
+        self._pulled[digest] = c
+        self.event("ImagePulled", app=spec["name"], image=ref, digest=digest, identity=ident)
+        return c
+
     def _start_replica(self, rt: AppRuntime, rev: Revision) -> ReplicaProc:
         spec = rt.spec
         dapr = spec.get("dapr") or {}
         level = self.log_level if not dapr.get("enableApiLogging") else "info"
+        container = self._pull(spec) if spec.get("image") else None
         rp = self.stack.start_replica(dapr.get("appId") or spec["name"], extra_env=self._app_env(spec),
-                                      module=spec["module"], log_level=level, identity=identity_of(spec),
+                                      module=spec.get("module"), log_level=level, identity=identity_of(spec),
                                       api_logging=bool(dapr.get("enableApiLogging")),
-                                      grpc=str(dapr.get("apiProtocol", "http")).lower() == "grpc")
+                                      grpc=str(dapr.get("apiProtocol", "http")).lower() == "grpc",
+                                      container=container)
         rp.revision = rev.name  # type: ignore[attr-defined]
         rev.replicas.append(rp)
         self.limiter.add(rp.name, rp.proc.pid, Limits.from_spec(spec))
@@ -491,8 +537,11 @@ class EnvironmentController:
             apps[rt.name] = {
                 "revisions": [{"name": r.name, "active": r.active, "created": r.created,
                                "replicas": [{"name": p.name, "pid": p.proc.pid, "alive": p.alive(), "appPort": p.app_port,
-                                             "sidecar": p.sidecar_uds}
+                                             "sidecar": p.sidecar_uds,
+                                             **({"image": p.container["digest"], "isolation": p.container["isolation"]}
+                                                if p.container else {})}
                                             for p in r.replicas]} for r in rt.revisions],
+                "image": rt.spec.get("image") or None,
                 "desiredReplicas": rt.desired, "restarts": rt.restarts,
                 "scale": rt.spec.get("scale"), "lastMetrics": rt.last_metrics, "scaleEvents": rt.scale_events[-20:],
                 "ingress": None if ing is None else {
@@ -528,8 +577,9 @@ class EnvironmentController:
                     if not r.alive():
                         continue
                     rec: dict[str, Any] = {}
-                    for label, url in (("sidecar", f"unix:{r.sidecar_uds}:/metrics"),
-                                       ("app", f"unix:{self.stack.sock_dir / (r.name + '.a.sock')}:/metrics")):
+                    app_url = (f"http://127.0.0.1:{r.app_port}/metrics" if r.container else
+                               f"unix:{self.stack.sock_dir / (r.name + '.a.sock')}:/metrics")
+                    for label, url in (("sidecar", f"unix:{r.sidecar_uds}:/metrics"), ("app", app_url)):
                         try:
                             resp = await http.get(url)
                             rec[label] = parse_exposition(resp.text) if resp.status == 200 else {}

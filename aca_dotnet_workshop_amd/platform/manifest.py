@@ -10,7 +10,8 @@ A manifest declares, in one YAML document, what the reference's IaC provisions
   subscriptions (E5), Cosmos account/db/container (E6), Storage account/queues/containers
   (E7) -- provisioned into the backing-services emulator;
 * ``daprComponents`` -- component name -> ACA-dialect file (E8);
-* ``containerApps``  -- per app: module ("image"), ingress (internal/external), Dapr
+* ``containerApps``  -- per app: ``image`` (from the environment's ``containerRegistry``, pulled
+  with the app identity's AcrPull role) or ``module`` (the dev loop: code from the source tree), ingress (internal/external), Dapr
   settings, managed identity + role assignments, env/secrets, resources, scale rules
   (E9-E12, KEDA ``azure-servicebus`` rule of processor-backend-service.bicep:159-183);
 * ``outputs``        -- like main.bicep:243-256.
@@ -234,8 +235,19 @@ def validate(m: Manifest) -> list[str]:
     app_ids = set()
     for a in m.apps:
         n = a.get("name", "<unnamed>")
-        if not a.get("module"):
-            errs.append(f"{n}: 'module' (the app image) is required")
+        if not a.get("module") and not a.get("image"):
+            errs.append(f"{n}: 'image' or 'module' (the app's code from the source tree) is required")
+        if a.get("image"):
+            server = str(a["image"]).split("/", 1)[0]
+            regs = [r for r in a.get("registries") or [] if r.get("server") == server]
+            if not regs:
+                errs.append(f"{n}: image {a['image']} needs a 'registries' entry for {server}")
+            acr = m.resources.get("containerRegistry") or {}
+            if not acr.get("name") or server != f"{acr['name']}.azurecr.io":
+                errs.append(f"{n}: image registry {server} is not the environment's containerRegistry")
+            for r in regs:
+                if r.get("identity") and r["identity"] != identity_of(a):
+                    errs.append(f"{n}: registry identity {r['identity']!r} is not the app's identity")
         ing = a.get("ingress")
         if ing is not None and not isinstance(ing.get("external", False), bool):
             errs.append(f"{n}: ingress.external must be a boolean")
@@ -297,6 +309,9 @@ def desired_state(m: Manifest) -> dict[str, Any]:
     """Flattened resource inventory used by what-if and recorded after a deployment."""
     res: dict[str, Any] = {}
     r = m.resources
+    acr = r.get("containerRegistry")
+    if acr and acr.get("name"):
+        res[f"containerRegistry/{acr['name']}"] = {"loginServer": f"{acr['name']}.azurecr.io"}
     kv = r.get("keyVault")
     if kv:
         res[f"keyVault/{kv['name']}"] = {"secrets": sorted(s["name"] for s in kv.get("secrets") or [])}
@@ -326,6 +341,8 @@ def desired_state(m: Manifest) -> dict[str, Any]:
     for a in m.apps:
         res[f"containerApps/{a['name']}"] = {"template": template_hash(a), "ingress": a.get("ingress"),
                                              "scale": a.get("scale"), "identity": identity_of(a)}
+        if a.get("image"):
+            res[f"containerApps/{a['name']}"]["image"] = a["image"]
     for ra in m.role_assignments():
         res[f"roleAssignments/{ra['principal']}/{ra['role']}/{ra['scope']}"] = {}
     return res
@@ -334,6 +351,8 @@ def desired_state(m: Manifest) -> dict[str, Any]:
 def template_hash(app: dict[str, Any]) -> str:
     """Revision-scope fields: a change here creates a new revision (ACA semantics)."""
     scoped = {k: app.get(k) for k in ("module", "args", "env", "resources", "dapr", "secrets", "revisionSuffix")}
+    if app.get("image"):  # a new image reference is a new revision (the dev loop's apps have none)
+        scoped["image"] = app["image"]
     return hashlib.sha256(json.dumps(scoped, sort_keys=True, default=str).encode()).hexdigest()[:10]
 
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 import signal
 import subprocess
 import sys
@@ -40,9 +41,13 @@ class ReplicaProc:
     http_port: int | None = None
     app_port_file: str | None = None
     started: float = field(default_factory=time.time)
+    fixed_app_port: int | None = None  # container replicas: the port the platform mapped for the app
+    container: dict[str, Any] | None = None
 
     @property
     def app_port(self) -> int | None:
+        if self.fixed_app_port is not None:
+            return self.fixed_app_port
         if self.app_port_file and os.path.exists(self.app_port_file):
             try:
                 return int(Path(self.app_port_file).read_text())
@@ -165,9 +170,17 @@ class LocalStack:
     def start_replica(self, app_id: str, config: dict[str, str] | None = None, extra_env: dict[str, str] | None = None,
                       http_port: int | None = None, module: str | None = None, log_level: str = "warning",
                       identity: str | None = None, external_port: int | None = None,
-                      api_logging: bool = False, grpc: bool = False) -> ReplicaProc:
+                      api_logging: bool = False, grpc: bool = False,
+                      container: dict[str, Any] | None = None) -> ReplicaProc:
         """``grpc``: the sidecar also serves its gRPC API and the app's SDK uses it
-        (``Dapr:ApiProtocol=grpc``), the transport of the reference's .NET ``DaprClient``."""
+        (``Dapr:ApiProtocol=grpc``), the transport of the reference's .NET ``DaprClient``.
+
+        ``container`` = ``{"rootfs", "config"}`` of a pulled image (``registry.unpack``): the app
+        runs the image's entrypoint inside the image's root filesystem -- ``chroot`` as the image's
+        ``User`` when the platform runs as root, otherwise the host interpreter over the image's
+        ``/app`` (``isolation: none``) -- with only the image's ``Env`` plus the app settings.  Like
+        a container sharing the replica's network namespace with its sidecar, it reaches the sidecar
+        on ``DAPR_HTTP_PORT``/``DAPR_GRPC_PORT`` and serves a TCP port the sidecar calls."""
         idx = self._seq
         self._seq += 1
         name = f"{app_id}-{idx}"
@@ -191,9 +204,29 @@ class LocalStack:
         if grpc:
             args += ["--dapr-grpc-port", "0"]
             env["Dapr__ApiProtocol"] = "grpc"
-        args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
-        p = self._spawn(args, env, name)
-        rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)
+        if container is None:
+            args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
+            p = self._spawn(args, env, name)
+            rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)
+        else:
+            app_port = free_port()
+            cmd, app_env, isolation = container_command(container, f"http://127.0.0.1:{app_port}")
+            for k, v in (config or {}).items():
+                app_env[k.replace(":", "__")] = str(v)
+            for k, v in (extra_env or {}).items():  # the app's settings; platform paths stay outside
+                if not k.startswith(("TT_MTLS_", "TT_INTERNAL_URL_")):
+                    app_env[k] = v
+            for k in ("TT_APP_HOST", "TT_REPLICA_NAME", "Dapr__ApiProtocol"):
+                if k in env:
+                    app_env[k] = env[k]
+            env_file = self.root / f"{name}.app-env.json"
+            env_file.write_text(json.dumps(app_env))
+            i = args.index("--app-uds")
+            args[i:i + 2] = ["--app-port", str(app_port)]
+            args += ["--app-env-file", str(env_file), "--"] + cmd
+            p = self._spawn(args, env, name)
+            rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, None,
+                             fixed_app_port=app_port, container={**container, "isolation": isolation})
         self.replicas.setdefault(app_id, []).append(rp)
         return rp
 
@@ -277,6 +310,30 @@ class LocalStack:
 
     def __exit__(self, *exc) -> None:
         self.stop()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def container_command(container: dict[str, Any], urls: str) -> tuple[list[str], dict[str, str], str]:
+    """(argv, environment, isolation) that run an unpacked image's entrypoint serving ``urls``."""
+    cfg = container["config"]
+    rootfs = Path(container["rootfs"])
+    env = dict(e.split("=", 1) for e in cfg.get("Env") or [])
+    env.update({"ASPNETCORE_URLS": urls, "TT_LOG_CONSOLE": "1", "PATH": "/usr/local/bin:/usr/bin:/bin"})
+    entry = list(cfg["Entrypoint"]) + list(cfg.get("Cmd") or [])
+    if os.geteuid() == 0:
+        from .image import populate_dev
+        populate_dev(rootfs)
+        chroot = shutil.which("chroot") or "/usr/sbin/chroot"
+        return [chroot, f"--userspec={cfg.get('User') or '0:0'}", str(rootfs)] + entry, env, "chroot"
+    # no privileges for a root-filesystem switch: the image's code on the host interpreter
+    env["PYTHONPATH"] = str(rootfs / cfg.get("WorkingDir", "/app").lstrip("/"))
+    return [sys.executable] + entry[1:], env, "none"
 
 
 def _is_dataplane(p) -> bool:

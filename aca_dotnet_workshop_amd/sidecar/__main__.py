@@ -8,12 +8,14 @@ exactly like the reference's local recipe (snippets/dapr-run-backend-api.md):
         -- python -m aca_dotnet_workshop_amd.services.backend_api --urls http://127.0.0.1:7088
 
 The child receives ``DAPR_HTTP_PORT`` (and ``TT_SIDECAR_UDS`` when ``--unix-socket-dir``
-is used), ``APP_ID``, ``APP_PORT``.  The sidecar stops when the app exits and vice versa.
+is used), ``APP_ID``, ``APP_PORT``; with ``--app-env-file`` (an app running from its container
+image) it gets that environment only, plus the Dapr ports.  The sidecar stops when the app exits and vice versa.
 """
 from __future__ import annotations
 
 import argparse
 import asyncio
+import json
 import logging
 import os
 import tempfile
@@ -62,6 +64,9 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--data-plane", choices=("native", "python"),
                    default=os.environ.get("TT_SIDECAR_DATAPLANE") or "native",
                    help="native: hot HTTP/gRPC API paths served by the C++ data plane (default); python: all in-process")
+    r.add_argument("--app-env-file", default=None,
+                   help="JSON object: the app's whole environment (a container's: nothing inherited from the "
+                        "sidecar's, no Unix-socket paths; the app reaches the sidecar on DAPR_HTTP_PORT/DAPR_GRPC_PORT)")
     r.add_argument("command", nargs=argparse.REMAINDER, help="-- <app command>")
     return ap
 
@@ -94,10 +99,15 @@ async def _run(a: argparse.Namespace) -> int:
         loop.add_signal_handler(sig, stop.set)
     proc = None
     if cmd:
-        env = dict(os.environ)
+        container = a.app_env_file is not None
+        if container:
+            with open(a.app_env_file) as fh:
+                env = {str(k): str(v) for k, v in json.load(fh).items()}
+        else:
+            env = dict(os.environ)
         env.update({"DAPR_HTTP_PORT": str(sc.bound_http_port or ""), "APP_ID": a.app_id,
                     "APP_PORT": str(a.app_port or ""), "TT_APP_ID": a.app_id})
-        if sock_api:
+        if sock_api and not container:
             env["TT_SIDECAR_UDS"] = sock_api
         if sc.bound_grpc_port:
             env["DAPR_GRPC_PORT"] = str(sc.bound_grpc_port)

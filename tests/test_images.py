@@ -27,7 +27,7 @@ def _read(archive):
 @pytest.fixture(scope="module")
 def built(tmp_path_factory):
     out = tmp_path_factory.mktemp("images")
-    closure = image.trace_closure("backend_api")
+    closure = image.full_closure("backend_api")
     return {v: image.build_image("backend_api", v, out, closure) for v in ("standard", "chiseled")}
 
 
@@ -70,9 +70,11 @@ def test_chiseled_is_minimal_and_nonroot(built):
 
 @pytest.mark.skipif(os.geteuid() != 0, reason="chroot needs root")
 @pytest.mark.parametrize("variant", ["standard", "chiseled"])
-def test_image_runs_module1_acceptance(built, variant):
+def test_image_runs_module1_acceptance(built, variant):  # every mode of MODES, incl. gRPC
     v = image.verify_image(built[variant].path, "backend_api")
     assert v["status"] == 200
     tasks = json.loads(v["body"])
     assert len(tasks) == 10 and all(t["taskCreatedBy"] == "tjoudeh@bitoftech.net" for t in tasks)
-    assert "Traceback" not in v["log"] and "unavailable" not in v["log"], v["log"][-2000:]
+    # every mode (incl. the gRPC sidecar protocol) finds all the code its paths import
+    assert [m["mode"] for m in v["modes"]] == image.MODES["backend_api"]
+    assert all(m["clean"] for m in v["modes"]), v["log"][-3000:]

@@ -16,7 +16,7 @@ from pathlib import Path
 
 import pytest
 
-from aca_dotnet_workshop_amd.platform.manifest import (ManifestError, load_manifest, substitute, unique_string,
+from aca_dotnet_workshop_amd.platform.manifest import (ManifestError, identity_of, load_manifest, substitute, unique_string,
                                                        validate, what_if)
 from aca_dotnet_workshop_amd.platform.scaler import Autoscaler, ScaleRule, cron_metric
 
@@ -98,16 +98,73 @@ def _get(url, **kw):
     return urllib.request.urlopen(url, timeout=10, **kw)
 
 
+@pytest.fixture(scope="module")
+def lifecycle_acr(tmp_path_factory):
+    """Chiseled images of the three services, pushed to a registry (module 12 -> module 10)."""
+    from aca_dotnet_workshop_amd.platform import image
+    from aca_dotnet_workshop_amd.platform.registry import LocalRegistry
+    reg = LocalRegistry("lifecycleacr", tmp_path_factory.mktemp("acr"))
+    out = tmp_path_factory.mktemp("images")
+    for svc, name in image.SERVICES.items():
+        reg.push(image.build_image(svc, "chiseled", out).path, f"tasksmanager/{name}", "r2")
+    return reg
+
+
+def test_image_pull_needs_acrpull(tmp_path, lifecycle_acr):
+    """An app pulls its image only with AcrPull on the registry for its own identity; an unknown
+    tag fails the pull (the revision's provisioning error in ACA)."""
+    from aca_dotnet_workshop_amd.platform.controller import EnvironmentController, ImagePullError
+    from aca_dotnet_workshop_amd.platform.registry import LocalRegistry
+    m = load_manifest(MAIN, PARAMS, {"containerRegistryName": lifecycle_acr.name, "imageTag": "r2"})
+    assert validate(m) == []
+    ctl = EnvironmentController(m, tmp_path / "env", registry_root=lifecycle_acr.dir.parent)
+    ctl.registry = LocalRegistry(lifecycle_acr.name, lifecycle_acr.dir.parent)
+    api = m.app("tasksmanager-backend-api")
+    c = ctl._pull(api)
+    root = Path(c["rootfs"])
+    assert (root / "app" / "aca_dotnet_workshop_amd" / "services" / "backend_api").is_dir()
+    assert not (root / "bin" / "sh").exists() and c["config"]["User"] != "0:0"
+    api["roleAssignments"] = [ra for ra in api["roleAssignments"] if ra["role"] != "AcrPull"]
+    with pytest.raises(ImagePullError, match="no AcrPull"):
+        ctl._pull(api)  # the earlier pull by digest does not bypass the check
+    fe = m.app("tasksmanager-frontend-webapp")
+    fe["image"] = fe["image"].replace(":r2", ":missing")
+    with pytest.raises(ImagePullError, match="manifest unknown"):
+        ctl._pull(fe)
+    assert [e["kind"] for e in ctl.events] == ["ImagePulled", "ImagePullFailed", "ImagePullFailed"]
+    m2 = load_manifest(MAIN, PARAMS, {"containerRegistryName": lifecycle_acr.name})
+    m2.app("tasksmanager-backend-api")["registries"] = []
+    assert any("needs a 'registries' entry" in e for e in validate(m2))
+
+
 @pytest.mark.slow
-def test_environment_lifecycle(tmp_path):
+@pytest.mark.parametrize("source", ["module", "image"])
+def test_environment_lifecycle(tmp_path, source, request):
+    """The whole environment, with the apps' code from the source tree (the dev loop) or pulled
+    as chiseled images from the environment's registry with each identity's AcrPull role -- then
+    the API also talks gRPC to its sidecar."""
     from aca_dotnet_workshop_amd.platform.controller import EnvironmentController
+    over = {"notifierSimulatedDelayMs": 150}
+    reg_root = None
+    if source == "image":
+        acr = request.getfixturevalue("lifecycle_acr")
+        over.update({"containerRegistryName": acr.name, "imageTag": "r2", "backendApiDaprApiProtocol": "grpc"})
+        reg_root = acr.dir.parent
 
     async def main():
-        m = load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 150})
-        ctl = EnvironmentController(m, tmp_path / "env", polling_interval=0.5, cooldown=3)
+        m = load_manifest(MAIN, PARAMS, over)
+        ctl = EnvironmentController(m, tmp_path / "env", polling_interval=0.5, cooldown=3, registry_root=reg_root)
         await ctl.up()
         try:
             st = ctl.status()
+            if source == "image":  # every replica runs its image's entrypoint in the image's root fs
+                for name, app in st["apps"].items():
+                    assert app["image"] == f"{acr.login_server}/tasksmanager/{name}:r2"
+                    reps = app["revisions"][-1]["replicas"]
+                    assert reps and all(r["image"].startswith("sha256:") for r in reps)
+                    assert all(r["isolation"] == ("chroot" if os.geteuid() == 0 else "none") for r in reps)
+                pulls = [e for e in ctl.events if e["kind"] == "ImagePulled"]
+                assert sorted(e["identity"] for e in pulls) == sorted(identity_of(a) for a in m.apps)
             api = st["apps"]["tasksmanager-backend-api"]["ingress"]
             fe = st["apps"]["tasksmanager-frontend-webapp"]["ingress"]
             # module 2: internal ingress is 403 from outside the environment
@@ -149,6 +206,17 @@ def test_environment_lifecycle(tmp_path):
             req = urllib.request.Request(fe["fqdn"] + "/Tasks/Index", headers={"Cookie": cookie})
             page = (await asyncio.to_thread(opener.open, req)).read().decode()
             assert "via mtls" in page
+            if source == "image":  # the API saved it through its sidecar's gRPC API
+                from aca_dotnet_workshop_amd.web.client import HttpClient
+                http = HttpClient(timeout=5.0)
+                try:
+                    api_rep = ctl.apps["tasksmanager-backend-api"].current.replicas[0]
+                    text = (await http.get(f"unix:{api_rep.sidecar_uds}:/metrics")).text
+                    assert 'op="grpc.SaveState"' in text and 'op="grpc.PublishEvent"' in text, text[-1500:]
+                    app_metrics = await http.get(f"http://127.0.0.1:{api_rep.app_port}/metrics")
+                    assert app_metrics.status == 200
+                finally:
+                    await http.close()
             regs = [json.loads(f.read_text()) for f in (tmp_path / "env" / "runtime" / "registry").glob("*/*.json")]
             assert regs and all(r["endpoint"].startswith(f"mtls:{r['appId']}@") for r in regs)
             b = ctl.backing
@@ -230,7 +298,7 @@ def test_environment_lifecycle(tmp_path):
             assert any(tdir.glob(f"spans-*-{utc_day()}.jsonl"))  # today's telemetry stays
             # module 10: a changed template deploys a new revision and retires the old one
             old = proc.current.name
-            res = await ctl.apply(load_manifest(MAIN, PARAMS, {"notifierSimulatedDelayMs": 10}))
+            res = await ctl.apply(load_manifest(MAIN, PARAMS, {**over, "notifierSimulatedDelayMs": 10}))
             assert proc.current.name != old and res["newRevisions"] == [proc.current.name]
             assert [r.active for r in proc.revisions] == [False, True]
             assert (tmp_path / "env" / "state.json").exists()
