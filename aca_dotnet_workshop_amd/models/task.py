@@ -124,6 +124,42 @@ FIELD_DISPLAY = {
 REQUIRED_FIELDS = ("taskName", "taskDueDate", "taskAssignedTo")
 
 
+_native_codec: Any = None
+
+
+def create_task_wire(body: bytes) -> tuple[str, str, str, bytes, bytes] | None:
+    """Bind a ``TaskAddModel`` body and build the new ``TaskModel`` in one native pass
+    (``native/src/taskcodec.hpp``): ``(taskId, taskName, taskAssignedTo, TaskModel JSON,
+    state-save body)``, byte-identical to binding with ``TaskAddModel`` and serialising
+    ``TaskModel(task_id=uuid4(), task_created_on=utcnow(), ...)``.  ``None`` when the body is
+    outside the codec's envelope (unusual property casing, offsets, invalid values, ...) or the
+    native module is absent: the caller binds it with pydantic, which decides those cases."""
+    global _native_codec
+    if _native_codec is None:
+        try:
+            from ..native import load
+            _native_codec = load().task_create
+        except Exception:  # no native module in this process: the pydantic binder serves
+            _native_codec = False
+    return _native_codec(body) if _native_codec else None
+
+
+def task_model_name(body: bytes) -> str | None:
+    """``taskName`` of a ``TaskModel`` JSON body when it binds within the native codec's envelope
+    (``native/src/taskcodec.hpp``), else ``None`` (bind with ``TaskModel``)."""
+    global _native_name
+    if _native_name is None:
+        try:
+            from ..native import load
+            _native_name = load().task_model_name
+        except Exception:
+            _native_name = False
+    return _native_name(body) if _native_name else None
+
+
+_native_name: Any = None
+
+
 def tasks_to_json(tasks: list[TaskModel]) -> bytes:
     return ("[" + ",".join(t.to_json() for t in tasks) + "]").encode()
 

@@ -8,6 +8,7 @@
 #include "broker.hpp"
 #include "docstore.hpp"
 #include "httpparse.hpp"
+#include "taskcodec.hpp"
 
 namespace py = pybind11;
 using namespace tt;
@@ -49,6 +50,142 @@ static ev::HeaderList header_list(const py::handle& seq) {
   return out;
 }
 
+// ---- raw CPython conversions for the app host's per-request hand-offs (submit / drain run for
+// every request and response of a service process; pybind11's generic casters cost several
+// microseconds per operation there).
+static std::string_view utf8_view(PyObject* o) {
+  Py_ssize_t n;
+  const char* p = PyUnicode_AsUTF8AndSize(o, &n);
+  if (p == nullptr) throw py::error_already_set();
+  return std::string_view(p, (size_t)n);
+}
+
+static std::string str_of(PyObject* o) {  // like f"{o}"
+  if (PyUnicode_Check(o)) return std::string(utf8_view(o));
+  py::object s = py::reinterpret_steal<py::object>(PyObject_Str(o));
+  if (!s) throw py::error_already_set();
+  return std::string(utf8_view(s.ptr()));
+}
+
+static std::string_view need_str(PyObject* o, const char* what) {
+  if (!PyUnicode_Check(o)) throw py::type_error(std::string(what) + " must be a str");
+  return utf8_view(o);
+}
+
+static long long need_int(PyObject* o, const char* what) {
+  long long v = PyLong_AsLongLong(o);
+  if (v == -1 && PyErr_Occurred()) {
+    PyErr_Clear();
+    throw py::type_error(std::string(what) + " must be an int");
+  }
+  return v;
+}
+
+static py::object seq_fast(PyObject* o, const char* what) {
+  py::object f = py::reinterpret_steal<py::object>(PySequence_Fast(o, what));
+  if (!f) throw py::error_already_set();
+  return f;
+}
+
+static ev::HeaderList header_list_fast(PyObject* seq) {
+  py::object f = seq_fast(seq, "headers must be a sequence of (name, value)");
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(f.ptr());
+  PyObject** items = PySequence_Fast_ITEMS(f.ptr());
+  ev::HeaderList out;
+  out.reserve((size_t)n);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    py::object kv = seq_fast(items[i], "a header must be a (name, value) pair");
+    if (PySequence_Fast_GET_SIZE(kv.ptr()) != 2) throw py::value_error("a header must be a (name, value) pair");
+    PyObject** p = PySequence_Fast_ITEMS(kv.ptr());
+    std::string k(need_str(p[0], "header name"));
+    for (auto& ch : k) ch = (char)std::tolower((unsigned char)ch);
+    out.emplace_back(std::move(k), str_of(p[1]));
+  }
+  return out;
+}
+
+static std::string body_of(PyObject* o) {
+  char* p;
+  Py_ssize_t n;
+  if (PyBytes_AsStringAndSize(o, &p, &n) != 0) throw py::error_already_set();
+  return std::string(p, (size_t)n);
+}
+
+// Steals `v`; throws if it is null (a failed allocation / conversion).
+static void set_item(PyObject* tup, Py_ssize_t i, PyObject* v) {
+  if (v == nullptr) throw py::error_already_set();
+  PyTuple_SET_ITEM(tup, i, v);
+}
+
+static PyObject* new_str(const std::string& s) { return PyUnicode_DecodeUTF8(s.data(), (Py_ssize_t)s.size(), "replace"); }
+
+// headers_dict() without pybind11: lower-cased names, repeats joined by ", ", set-cookie a list.
+static PyObject* headers_dict_fast(const ev::HeaderList& headers) {
+  py::object d = py::reinterpret_steal<py::object>(PyDict_New());
+  if (!d) throw py::error_already_set();
+  for (auto& [k, v] : headers) {
+    py::object key = py::reinterpret_steal<py::object>(new_str(k));
+    py::object val = py::reinterpret_steal<py::object>(new_str(v));
+    if (!key || !val) throw py::error_already_set();
+    PyObject* prev = PyDict_GetItemWithError(d.ptr(), key.ptr());  // borrowed
+    if (prev == nullptr && PyErr_Occurred()) throw py::error_already_set();
+    if (prev == nullptr) {
+      if (PyDict_SetItem(d.ptr(), key.ptr(), val.ptr()) != 0) throw py::error_already_set();
+    } else if (k == "set-cookie") {
+      if (PyList_Check(prev)) {
+        if (PyList_Append(prev, val.ptr()) != 0) throw py::error_already_set();
+      } else {
+        py::object l = py::reinterpret_steal<py::object>(PyList_New(2));
+        if (!l) throw py::error_already_set();
+        Py_INCREF(prev);
+        PyList_SET_ITEM(l.ptr(), 0, prev);
+        PyList_SET_ITEM(l.ptr(), 1, val.release().ptr());
+        if (PyDict_SetItem(d.ptr(), key.ptr(), l.ptr()) != 0) throw py::error_already_set();
+      }
+    } else {
+      std::string joined = str_of(prev) + ", " + v;
+      py::object j = py::reinterpret_steal<py::object>(new_str(joined));
+      if (!j || PyDict_SetItem(d.ptr(), key.ptr(), j.ptr()) != 0) throw py::error_already_set();
+    }
+  }
+  return d.release().ptr();
+}
+
+static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) {
+  py::list out(evs.size());
+  for (size_t i = 0; i < evs.size(); ++i) {
+    auto& e = evs[i];
+    py::object t;
+    if (e.kind == apphost::Event::REQUEST) {
+      t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 9 : 8));
+      if (!t) throw py::error_already_set();
+      set_item(t.ptr(), 0, PyLong_FromLong(0));
+      set_item(t.ptr(), 1, PyLong_FromUnsignedLongLong(e.id));
+      set_item(t.ptr(), 2, PyLong_FromLong(e.server));
+      set_item(t.ptr(), 3, new_str(e.msg.method));
+      set_item(t.ptr(), 4, new_str(e.msg.target));
+      set_item(t.ptr(), 5, PyBool_FromLong(e.msg.http10));
+      set_item(t.ptr(), 6, headers_dict_fast(e.msg.headers));
+      set_item(t.ptr(), 7, PyBytes_FromStringAndSize(e.msg.body.data(), (Py_ssize_t)e.msg.body.size()));
+      if (with_times) set_item(t.ptr(), 8, PyFloat_FromDouble(e.t));
+    } else if (e.kind == apphost::Event::RESPONSE) {
+      t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 6 : 5));
+      if (!t) throw py::error_already_set();
+      set_item(t.ptr(), 0, PyLong_FromLong(1));
+      set_item(t.ptr(), 1, PyLong_FromUnsignedLongLong(e.id));
+      set_item(t.ptr(), 2, PyLong_FromLong(e.msg.status));
+      set_item(t.ptr(), 3, headers_dict_fast(e.msg.headers));
+      set_item(t.ptr(), 4, PyBytes_FromStringAndSize(e.msg.body.data(), (Py_ssize_t)e.msg.body.size()));
+      if (with_times) set_item(t.ptr(), 5, PyFloat_FromDouble(e.t));
+    } else {
+      if (with_times) t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t);
+      else t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)));
+    }
+    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, t.release().ptr());
+  }
+  return out;
+}
+
 static std::string bytes_of(const py::handle& b) {
   char* p;
   Py_ssize_t n;
@@ -83,6 +220,49 @@ PYBIND11_MODULE(_ttnative, m) {
       throw py::value_error(e.what());
     }
     return py::make_tuple(py::str(h.a), py::str(h.b), py::str(h.c), headers_dict(h.headers));
+  });
+
+  // TaskAddModel body -> (id, taskName, taskAssignedTo, TaskModel JSON, state-save body), or
+  // None when the general (pydantic) binder must decide (taskcodec.hpp).
+  m.def("task_create", [](py::bytes body) -> py::object {
+    static taskcodec::Entropy rng;  // called with the GIL held
+    static taskcodec::Created c;
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    if (!taskcodec::create(std::string_view(p, (size_t)n), rng, c)) return py::none();
+    return py::make_tuple(py::str(c.id), py::str(c.name), py::str(c.assigned_to),
+                          py::bytes(c.task_json), py::bytes(c.state_body));
+  });
+
+  // CloudEvents envelope -> (data JSON, datacontenttype, attributes dict), or None (taskcodec.hpp).
+  m.def("cloudevent_unwrap", [](py::bytes body) -> py::object {
+    static taskcodec::Unwrapped u;
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    if (!taskcodec::unwrap_cloudevent(std::string_view(p, (size_t)n), u)) return py::none();
+    py::dict attrs;
+    for (const auto& kv : u.attrs) {
+      const tt::Value& v = *kv.second;
+      py::object o;
+      if (v.t == tt::Value::String) o = py::str(v.s);
+      else if (v.t == tt::Value::Bool) o = py::bool_(v.b);
+      else if (v.t == tt::Value::Null) o = py::none();
+      else o = py::module_::import("json").attr("loads")(py::str(tt::dump(v)));
+      attrs[py::str(kv.first)] = o;
+    }
+    return py::make_tuple(py::bytes(u.data), py::str(u.content_type), attrs);
+  });
+
+  // TaskModel JSON -> taskName when it binds within the codec's envelope, else None.
+  m.def("task_model_name", [](py::bytes body) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    std::string name;
+    if (!taskcodec::task_model_name(std::string_view(p, (size_t)n), name)) return py::none();
+    return py::str(name);
   });
 
   py::class_<TxOp>(m, "TxOp")
@@ -316,61 +496,45 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("submit",
            [](apphost::AppHost& h, py::list ops) {
              std::vector<apphost::AppHost::Op> v;
-             v.reserve(ops.size());
-             for (auto item : ops) {
-               auto t = item.cast<py::tuple>();
+             Py_ssize_t n = PyList_GET_SIZE(ops.ptr());
+             v.reserve((size_t)n);
+             for (Py_ssize_t i = 0; i < n; ++i) {
+               py::object t = seq_fast(PyList_GET_ITEM(ops.ptr(), i), "an operation must be a tuple");
+               Py_ssize_t len = PySequence_Fast_GET_SIZE(t.ptr());
+               PyObject** f = PySequence_Fast_ITEMS(t.ptr());
+               if (len < 2) throw py::value_error("operation too short");
                apphost::AppHost::Op op;
-               int kind = t[0].cast<int>();
+               long long kind = need_int(f[0], "operation kind");
                op.is_request = kind == 1 || kind == 2;
                op.is_grpc = kind == 2;
-               op.id = t[1].cast<uint64_t>();
+               op.id = (uint64_t)need_int(f[1], "operation id");
                if (!op.is_request) {
-                 op.status = t[2].cast<int>();
-                 op.headers = header_list(t[3]);
-                 op.body = bytes_of(t[4]);
+                 if (len != 5) throw py::value_error("respond operation: (0, token, status, headers, body)");
+                 op.status = (int)need_int(f[2], "status");
+                 op.headers = header_list_fast(f[3]);
+                 op.body = body_of(f[4]);
                } else {
-                 op.endpoint = t[2].cast<std::string>();
-                 op.method = t[3].cast<std::string>();
-                 op.target = t[4].cast<std::string>();
-                 op.headers = header_list(t[5]);
-                 op.body = bytes_of(t[6]);
-                 op.timeout_s = t[7].cast<double>();
+                 if (len != 8) throw py::value_error("request operation: (1, id, endpoint, method, target, headers, body, timeout)");
+                 op.endpoint = std::string(need_str(f[2], "endpoint"));
+                 op.method = std::string(need_str(f[3], "method"));
+                 op.target = std::string(need_str(f[4], "target"));
+                 op.headers = header_list_fast(f[5]);
+                 op.body = body_of(f[6]);
+                 op.timeout_s = PyFloat_AsDouble(f[7]);
+                 if (op.timeout_s == -1.0 && PyErr_Occurred()) throw py::error_already_set();
                }
                v.push_back(std::move(op));
              }
              h.submit(std::move(v));
            })
       // [(0, token, server, method, target, http10, headers, body) | (1, id, status, headers, body) |
-      //  (2, id, errno, message)]
+      //  (2, id, errno, message)] (+ each event's queue time, monotonic seconds, with drain_times)
       .def("drain_times", [](apphost::AppHost& h) {
-        // same as drain() plus each event's queue time (monotonic seconds) as the last element
         auto evs = h.drain();
-        py::list out;
-        for (auto& e : evs) {
-          if (e.kind == apphost::Event::REQUEST) {
-            out.append(py::make_tuple(0, e.id, e.server, py::str(e.msg.method), py::str(e.msg.target),
-                                      e.msg.http10, headers_dict(e.msg.headers), py::bytes(e.msg.body), e.t));
-          } else if (e.kind == apphost::Event::RESPONSE) {
-            out.append(py::make_tuple(1, e.id, e.msg.status, headers_dict(e.msg.headers), py::bytes(e.msg.body), e.t));
-          } else {
-            out.append(py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t));
-          }
-        }
-        return out;
+        return events_to_py(evs, true);
       })
       .def("drain", [](apphost::AppHost& h) {
         auto evs = h.drain();
-        py::list out;
-        for (auto& e : evs) {
-          if (e.kind == apphost::Event::REQUEST) {
-            out.append(py::make_tuple(0, e.id, e.server, py::str(e.msg.method), py::str(e.msg.target),
-                                      e.msg.http10, headers_dict(e.msg.headers), py::bytes(e.msg.body)));
-          } else if (e.kind == apphost::Event::RESPONSE) {
-            out.append(py::make_tuple(1, e.id, e.msg.status, headers_dict(e.msg.headers), py::bytes(e.msg.body)));
-          } else {
-            out.append(py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err))));
-          }
-        }
-        return out;
+        return events_to_py(evs, false);
       });
 }

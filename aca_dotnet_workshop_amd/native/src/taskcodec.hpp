@@ -1,0 +1,363 @@
+// TaskModel wire codec for the Backend API's create path (POST /api/tasks).
+//
+// The reference binds the request body to TaskAddModel, creates a TaskModel with a new Guid and
+// DateTime.UtcNow (Backend.Api Services/TasksStoreManager.cs:27-38), serialises it once for
+// SaveStateAsync and PublishEventAsync.  The Python service does the same through pydantic
+// (models/task.py); this is the same binding and serialisation in one pass over the body:
+//
+//   * the body is a JSON object; the four TaskAddModel properties are taken by their camelCase
+//     names, unrelated properties are ignored (ASP.NET drops extras);
+//   * taskDueDate accepts the ISO-8601 forms of models/dotnet.py:parse_datetime without a UTC
+//     offset ("YYYY-MM-DD", "...THH:MM[:SS[.fffffff]]", optional "Z") and is written back the way
+//     System.Text.Json writes it (trimmed fraction, "Z" only for UTC values);
+//   * the id is a random (version 4) Guid, taskCreatedOn the current UTC time in microseconds.
+//
+// Anything outside that envelope -- a differently cased or snake_case property name, a duplicate,
+// a non-string value, an offset, an out-of-range date, invalid UTF-8 -- is NOT decided here:
+// create() returns false and the caller runs the general binder, which produces the exact
+// validation error (400 ProblemDetails) or the remapped value.  Output is byte-identical to
+// TaskModel.model_dump_json(by_alias=True) (tests/test_task_codec.py).
+#pragma once
+
+#include <sys/random.h>
+
+#include <cstdint>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+#include "json.hpp"
+
+namespace taskcodec {
+
+struct Created {
+  std::string id;           // lowercase hyphenated Guid
+  std::string name;         // decoded taskName (log lines)
+  std::string assigned_to;  // decoded taskAssignedTo
+  std::string task_json;    // TaskModel JSON (state value and event data)
+  std::string state_body;   // [{"key":"<id>","value":<task_json>}]
+};
+
+inline bool valid_utf8(std::string_view s) {
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(s.data());
+  const unsigned char* e = p + s.size();
+  while (p < e) {
+    unsigned char c = *p;
+    if (c < 0x80) { ++p; continue; }
+    int n;
+    uint32_t cp;
+    if ((c & 0xE0) == 0xC0) { n = 1; cp = c & 0x1F; if (c < 0xC2) return false; }
+    else if ((c & 0xF0) == 0xE0) { n = 2; cp = c & 0x0F; }
+    else if ((c & 0xF8) == 0xF0) { n = 3; cp = c & 0x07; if (c > 0xF4) return false; }
+    else return false;
+    if (e - p <= n) return false;
+    for (int i = 1; i <= n; ++i) {
+      if ((p[i] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (p[i] & 0x3F);
+    }
+    if ((n == 2 && (cp < 0x800 || (cp >= 0xD800 && cp < 0xE000))) || (n == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
+      return false;
+    p += n + 1;
+  }
+  return true;
+}
+
+// Random bytes from the kernel CSPRNG (what uuid.uuid4 / Guid.NewGuid use), drawn in blocks.
+class Entropy {
+ public:
+  bool take(uint8_t* out, size_t n) {
+    if (pos_ + n > sizeof buf_) {
+      size_t got = 0;
+      while (got < sizeof buf_) {
+        ssize_t r = getrandom(buf_ + got, sizeof buf_ - got, 0);
+        if (r <= 0) return false;
+        got += (size_t)r;
+      }
+      pos_ = 0;
+    }
+    std::memcpy(out, buf_ + pos_, n);
+    pos_ += n;
+    return true;
+  }
+
+ private:
+  uint8_t buf_[4096];
+  size_t pos_ = sizeof buf_;
+};
+
+inline bool new_guid(Entropy& rng, std::string& out) {
+  uint8_t b[16];
+  if (!rng.take(b, 16)) return false;
+  b[6] = (uint8_t)((b[6] & 0x0F) | 0x40);  // version 4
+  b[8] = (uint8_t)((b[8] & 0x3F) | 0x80);  // RFC 4122 variant
+  static const char* hx = "0123456789abcdef";
+  out.clear();
+  for (int i = 0; i < 16; ++i) {
+    if (i == 4 || i == 6 || i == 8 || i == 10) out += '-';
+    out += hx[b[i] >> 4];
+    out += hx[b[i] & 15];
+  }
+  return true;
+}
+
+inline void put2(std::string& o, int v) { o += (char)('0' + v / 10); o += (char)('0' + v % 10); }
+inline void put4(std::string& o, int v) { put2(o, v / 100); put2(o, v % 100); }
+
+// System.Text.Json DateTime: "yyyy-MM-ddTHH:mm:ss[.f{1,6} trimmed][Z]"
+inline void format_dt(std::string& o, int y, int mo, int d, int h, int mi, int s, int us, bool utc) {
+  put4(o, y); o += '-'; put2(o, mo); o += '-'; put2(o, d); o += 'T';
+  put2(o, h); o += ':'; put2(o, mi); o += ':'; put2(o, s);
+  if (us) {
+    char f[7];
+    for (int i = 5; i >= 0; --i) { f[i] = (char)('0' + us % 10); us /= 10; }
+    int n = 6;
+    while (n > 0 && f[n - 1] == '0') --n;
+    o += '.';
+    o.append(f, n);
+  }
+  if (utc) o += 'Z';
+}
+
+inline bool leap(int y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+
+// parse_datetime's grammar minus offsets; false = let the general binder decide.
+inline bool parse_due(std::string_view v, std::string& out) {
+  auto dig = [&](size_t i, size_t n, int& r) {
+    if (i + n > v.size()) return false;
+    r = 0;
+    for (size_t k = i; k < i + n; ++k) {
+      if (v[k] < '0' || v[k] > '9') return false;
+      r = r * 10 + (v[k] - '0');
+    }
+    return true;
+  };
+  int y, mo, d, h = 0, mi = 0, s = 0, us = 0;
+  bool utc = false;
+  if (!dig(0, 4, y) || v.size() < 10 || v[4] != '-' || !dig(5, 2, mo) || v[7] != '-' || !dig(8, 2, d)) return false;
+  size_t i = 10;
+  if (i < v.size() && (v[i] == 'T' || v[i] == ' ')) {
+    if (!dig(i + 1, 2, h) || i + 3 >= v.size() || v[i + 3] != ':' || !dig(i + 4, 2, mi)) return false;
+    i += 6;
+    if (i < v.size() && v[i] == ':') {
+      if (!dig(i + 1, 2, s)) return false;
+      i += 3;
+      if (i < v.size() && (v[i] == '.' || v[i] == ',')) {
+        size_t j = i + 1, n = 0;
+        while (j < v.size() && v[j] >= '0' && v[j] <= '9') { if (n < 6) us = us * 10 + (v[j] - '0'); ++j; ++n; }
+        if (n == 0 || n > 9) return false;
+        for (size_t k = n; k < 6; ++k) us *= 10;
+        i = j;
+      }
+    }
+  }
+  if (i < v.size() && (v[i] == 'Z' || v[i] == 'z')) { utc = true; ++i; }
+  if (i != v.size()) return false;  // offsets, whitespace, junk
+  static const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  if (y < 1 || mo < 1 || mo > 12 || d < 1 || d > mdays[mo - 1] + (mo == 2 && leap(y)) || h > 23 || mi > 59 || s > 59)
+    return false;
+  format_dt(out, y, mo, d, h, mi, s, us, utc);
+  return true;
+}
+
+// json.loads (strict) rejects raw control characters inside strings; tt::Parser does not.
+inline bool no_raw_controls_in_strings(std::string_view s) {
+  bool in = false;
+  for (size_t i = 0; i < s.size(); ++i) {
+    unsigned char c = (unsigned char)s[i];
+    if (!in) { if (c == '"') in = true; continue; }
+    if (c == '\\') { ++i; continue; }
+    if (c == '"') in = false;
+    else if (c < 0x20) return false;
+  }
+  return true;
+}
+
+inline bool create(std::string_view body, Entropy& rng, Created& out) {
+  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  if (doc.t != tt::Value::Object) return false;
+  static const char* names[4] = {"taskName", "taskCreatedBy", "taskDueDate", "taskAssignedTo"};
+  static const char* other[8] = {"task_name", "task_created_by", "task_due_date", "task_assigned_to",
+                                 "taskname", "taskcreatedby", "taskduedate", "taskassignedto"};
+  const tt::Value* f[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (size_t k = 0; k < doc.keys.size(); ++k) {
+    const std::string& key = doc.keys[k];
+    int hit = -1;
+    for (int j = 0; j < 4; ++j)
+      if (key == names[j]) hit = j;
+    if (hit >= 0) {
+      if (f[hit] != nullptr) return false;  // duplicate: json.loads keeps the last one
+      f[hit] = &doc.items[k];
+      continue;
+    }
+    // an unrelated property: only scalars whose grammar both parsers share (numbers and nested
+    // values go to the general binder, whose JSON parser is the authority on them)
+    const tt::Value& x = doc.items[k];
+    if (x.t != tt::Value::String && x.t != tt::Value::Bool && x.t != tt::Value::Null) return false;
+    std::string low(key);
+    for (char& c : low) c = (char)std::tolower((unsigned char)c);
+    for (const char* o : other)
+      if (key == o || low == o) return false;  // remapped by the general binder
+  }
+  for (int j = 0; j < 4; ++j)  // strings only, and no lone surrogates from \\u escapes
+    if (f[j] != nullptr && (f[j]->t != tt::Value::String || !valid_utf8(f[j]->s))) return false;
+  std::string due;
+  if (f[2] == nullptr) due = "0001-01-01T00:00:00";
+  else if (!parse_due(f[2]->s, due)) return false;
+
+  if (!new_guid(rng, out.id)) return false;
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  time_t secs = ts.tv_sec;
+  struct tm tmv;
+  gmtime_r(&secs, &tmv);
+  std::string& j = out.task_json;
+  j.clear();
+  j.reserve(256 + body.size());
+  j += "{\"taskId\":\"";
+  j += out.id;
+  j += "\",\"taskName\":";
+  tt::escape_to(j, f[0] ? std::string_view(f[0]->s) : std::string_view());
+  j += ",\"taskCreatedBy\":";
+  tt::escape_to(j, f[1] ? std::string_view(f[1]->s) : std::string_view());
+  j += ",\"taskCreatedOn\":\"";
+  format_dt(j, tmv.tm_year + 1900, tmv.tm_mon + 1, tmv.tm_mday, tmv.tm_hour, tmv.tm_min, tmv.tm_sec,
+            (int)(ts.tv_nsec / 1000), true);
+  j += "\",\"taskDueDate\":\"";
+  j += due;
+  j += "\",\"taskAssignedTo\":";
+  tt::escape_to(j, f[3] ? std::string_view(f[3]->s) : std::string_view());
+  j += ",\"isCompleted\":false,\"isOverDue\":false}";
+  out.name = f[0] ? f[0]->s : std::string();
+  out.assigned_to = f[3] ? f[3]->s : std::string();
+  out.state_body.clear();
+  out.state_body.reserve(j.size() + 64);
+  out.state_body += "[{\"key\":\"";
+  out.state_body += out.id;
+  out.state_body += "\",\"value\":";
+  out.state_body += j;
+  out.state_body += "}]";
+  return true;
+}
+
+// -------------------------------------------------------------------------------------------
+// The processor's side: a CloudEvents envelope from the sidecar and the TaskModel inside it.
+
+// CloudEvents 1.0 structured mode (what app.UseCloudEvents() unwraps, Processor/Program.cs:29):
+// the envelope's attributes and its JSON `data` re-serialised compactly.  false = the general
+// (Python) unwrapper decides: not an object, data_base64, a string payload, or numbers anywhere in
+// the data (their text form is the Python parser's business).
+struct Unwrapped {
+  std::string data;
+  std::string content_type = "application/json";
+  std::vector<std::pair<std::string, const tt::Value*>> attrs;
+  tt::Value doc;
+};
+
+inline bool has_number(const tt::Value& v) {
+  if (v.t == tt::Value::Number) return true;
+  for (const auto& x : v.items)
+    if (has_number(x)) return true;
+  return false;
+}
+
+inline bool unwrap_cloudevent(std::string_view body, Unwrapped& out) {
+  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  try {
+    out.doc = tt::parse(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  const tt::Value& ce = out.doc;
+  if (ce.t != tt::Value::Object) return false;
+  const tt::Value* data = nullptr;
+  out.attrs.clear();
+  for (size_t i = 0; i < ce.keys.size(); ++i) {
+    const std::string& k = ce.keys[i];
+    for (size_t j = 0; j < i; ++j)
+      if (ce.keys[j] == k) return false;  // duplicate attribute
+    if (k == "data_base64") return false;
+    if (k == "data") { data = &ce.items[i]; continue; }
+    if (k == "datacontenttype") {
+      if (ce.items[i].t != tt::Value::String) return false;
+      out.content_type = ce.items[i].s;
+    }
+    out.attrs.emplace_back(k, &ce.items[i]);
+  }
+  if (data == nullptr || data->t == tt::Value::String || has_number(*data)) return false;
+  for (const auto& kv : out.attrs)
+    if (has_number(*kv.second) || (kv.second->t == tt::Value::String && !valid_utf8(kv.second->s))) return false;
+  out.data.clear();
+  tt::dump_to(out.data, *data);
+  return valid_utf8(out.data);
+}
+
+inline bool is_guid36(const std::string& s) {
+  if (s.size() != 36) return false;
+  for (size_t i = 0; i < 36; ++i) {
+    char c = s[i];
+    if (i == 8 || i == 13 || i == 18 || i == 23) { if (c != '-') return false; continue; }
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'))) return false;
+  }
+  return true;
+}
+
+// TaskModel binding check (TaskModel.model_validate of the event data, Processor
+// TasksNotifierController.cs:26): the taskName when the object binds within the envelope of
+// create(); false = the general binder decides (and produces any 400).
+inline bool task_model_name(std::string_view body, std::string& name) {
+  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  if (doc.t != tt::Value::Object) return false;
+  static const char* names[8] = {"taskId", "taskName", "taskCreatedBy", "taskCreatedOn",
+                                 "taskDueDate", "taskAssignedTo", "isCompleted", "isOverDue"};
+  static const char* snake[8] = {"task_id", "task_name", "task_created_by", "task_created_on",
+                                 "task_due_date", "task_assigned_to", "is_completed", "is_over_due"};
+  const tt::Value* f[8] = {nullptr};
+  for (size_t k = 0; k < doc.keys.size(); ++k) {
+    const std::string& key = doc.keys[k];
+    int hit = -1;
+    for (int j = 0; j < 8; ++j)
+      if (key == names[j]) hit = j;
+    if (hit >= 0) {
+      if (f[hit] != nullptr) return false;
+      f[hit] = &doc.items[k];
+      continue;
+    }
+    const tt::Value& x = doc.items[k];
+    if (x.t != tt::Value::String && x.t != tt::Value::Bool && x.t != tt::Value::Null) return false;
+    std::string low(key);
+    for (char& c : low) c = (char)std::tolower((unsigned char)c);
+    for (int j = 0; j < 8; ++j) {
+      std::string ln(names[j]);
+      for (char& c : ln) c = (char)std::tolower((unsigned char)c);
+      if (key == snake[j] || low == ln) return false;
+    }
+  }
+  std::string scratch;
+  for (int j = 0; j < 8; ++j) {
+    const tt::Value* v = f[j];
+    if (v == nullptr) continue;
+    if (j == 6 || j == 7) { if (v->t != tt::Value::Bool) return false; continue; }
+    if (v->t != tt::Value::String || !valid_utf8(v->s)) return false;
+    if (j == 0 && !is_guid36(v->s)) return false;
+    if ((j == 3 || j == 4) && !parse_due(v->s, scratch)) return false;
+  }
+  name = f[1] ? f[1]->s : std::string();
+  return true;
+}
+
+}  // namespace taskcodec

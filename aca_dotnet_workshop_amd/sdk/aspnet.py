@@ -55,9 +55,26 @@ def map_subscribe_handler(app: WebApp) -> None:
     app.add_route("/dapr/subscribe", dapr_subscribe, ("GET",), name="dapr_subscribe", include_in_schema=False)
 
 
+def _native_unwrap():
+    try:
+        from ..native import load
+        return load().cloudevent_unwrap
+    except Exception:  # no native module in this process: the Python unwrapper serves
+        return None
+
+
 def cloud_events_middleware():
+    native = _native_unwrap()
+
     async def mw(req: Request, nxt) -> Response:
         if req.content_type == "application/cloudevents+json" and req.body:
+            # one native pass (native/src/taskcodec.hpp) for the common envelope: JSON data
+            # re-serialised compactly, attributes as a dict; anything else is unwrapped below
+            u = native(req.body) if native is not None else None
+            if u is not None:
+                req.body, dct, req.state["cloudevent"] = u
+                req.headers["content-type"] = dct
+                return await nxt(req)
             try:
                 ce = json.loads(req.body)
             except ValueError:

@@ -117,6 +117,13 @@ class SidecarClient:
             http = native_host.NativeHttpClient(timeout=timeout) if native_host.enabled(part="client") else HttpClient(timeout=timeout)
         self.http = http
         self.api_token = api_token if api_token is not None else os.environ.get("DAPR_API_TOKEN")
+        # the native host takes requests to a pre-split endpoint (no URL parsing per call)
+        self._at = None
+        if hasattr(http, "request_at"):
+            from ..web.client import parse_endpoint
+            key, prefix = parse_endpoint(self.base + "/")
+            if key[0] in ("unix", "tcp"):
+                self._at, self._key, self._prefix = http.request_at, key, prefix.rstrip("/")
 
     # -- plumbing -------------------------------------------------------------
     def _headers(self, ctype: str | None = None, extra: dict[str, str] | None = None) -> list[tuple[str, str]]:
@@ -134,6 +141,17 @@ class SidecarClient:
 
     async def _call(self, method: str, path: str, body: bytes = b"", ctype: str | None = None,
                     extra: dict[str, str] | None = None, span_name: str | None = None) -> ClientResponse:
+        parent = tracing.current_span()
+        if parent is not None and not parent.sampled and self._at is not None:
+            # inside an unsampled trace nothing is recorded: propagate the context, skip the span
+            h = [("traceparent", parent.traceparent)]
+            if self.api_token:
+                h.append(("dapr-api-token", self.api_token))
+            if ctype:
+                h.append(("Content-Type", ctype))
+            if extra:
+                h.extend(extra.items())
+            return await self._at(self._key, method, self._prefix + path, h, body)
         tr = tracing.tracer()
         span = tr.start_span(span_name or method, "client")
         if span.sampled and not span_name:
@@ -206,6 +224,12 @@ class SidecarClient:
 
     async def save_bulk_state(self, store: str, items: list[dict[str, Any]]) -> None:
         await self._save_body(store, json.dumps(items, separators=(",", ":")).encode())
+
+    async def save_state_body(self, store: str, body: bytes) -> None:
+        """Save with a request body already in the state API's form (``[{"key", "value", ...}]``)."""
+        r = await self._call("POST", f"/v1.0/state/{store}", body, "application/json", span_name=f"state save {store}")
+        if r.status >= 300:
+            raise InvocationError(r.status, r.body, f"save state {store}")
 
     async def _save_body(self, store: str, body: bytes) -> None:
         r = await self._call("POST", f"/v1.0/state/{store}", body, "application/json", span_name=f"state save {store}")

@@ -29,7 +29,7 @@ import random
 import uuid
 from datetime import datetime, timedelta
 
-from ...models import TaskModel, format_fixed, naive_utc, today, utcnow
+from ...models import TaskModel, create_task_wire, format_fixed, naive_utc, today, utcnow
 from ...sdk.client import InvocationError, RawJson, SidecarClient
 
 log = logging.getLogger("TasksManager")
@@ -170,6 +170,25 @@ class TasksStoreManager(TasksManager):
         await self.client.save_state(self.store, str(t.task_id), payload)
         await self._publish_task_saved(t, payload)
         return t.task_id
+
+    async def create_new_task_from_body(self, body: bytes) -> str | None:
+        """``create_new_task`` straight from the request body: binding, the new TaskModel and its
+        JSON come from the native codec in one pass (``models.create_task_wire``); the same log
+        lines, state save and event follow.  ``None``: the body needs the general binder."""
+        made = create_task_wire(body)
+        if made is None:
+            return None
+        tid, name, assignee, task_json, state_body = made
+        log.info("Save a new task with name: '%s' to state store", name)
+        save_body = getattr(self.client, "save_state_body", None)  # HTTP: the state API's body as is
+        if save_body is not None:
+            await save_body(self.store, state_body)
+        else:  # gRPC: the value goes into a SaveStateRequest
+            await self.client.save_state(self.store, tid, RawJson(task_json.decode()))
+        log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
+                 tid, name, assignee)
+        await self.client.publish_event(self.pubsub, self.topic, task_json, content_type="application/json")
+        return tid
 
     async def delete_task(self, task_id) -> bool:
         log.info("Delete task with Id: '%s'", task_id)

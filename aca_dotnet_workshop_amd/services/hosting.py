@@ -22,7 +22,8 @@ import sys
 from pathlib import Path
 from typing import Any, Callable
 
-from ..telemetry import REGISTRY, configure, configure_logging, metrics_middleware, server_middleware
+from ..telemetry import REGISTRY, configure, configure_logging
+from ..telemetry.metrics import request_telemetry_middleware
 from ..telemetry.profiler import maybe_profile
 from ..utils.config import Configuration, load_configuration
 from ..web.app import WebApp
@@ -42,8 +43,7 @@ def create_host(role: str, content_root: str | os.PathLike | None = None, argv: 
     app = WebApp(role, config)
     app.services["config"] = config
     app.services["tracer"] = tr
-    app.use(server_middleware())
-    app.use(metrics_middleware())
+    app.use(request_telemetry_middleware())  # request span + request metrics
 
     async def healthz(req) -> Response:
         return empty(204)

@@ -33,7 +33,7 @@ import logging
 import uuid
 from pathlib import Path
 
-from ...models import TaskModel, naive_utc, tasks_from_json, utcnow
+from ...models import TaskModel, naive_utc, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
 from ...sdk.client import InvocationError, client_from_config
 from ...web.app import WebApp, read_model
@@ -60,9 +60,15 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
     @topic("dapr-pubsub-servicebus", "tasksavedtopic")
     @topic("taskspubsub", "tasksavedtopic")
     async def task_saved(req: Request) -> Response:
+        mode = (cfg.get_str("TasksNotifier:Mode") or "log").lower()
+        if mode == "log":  # the shipped controller needs the name only: a native binding check
+            ctype = req.content_type
+            name = task_model_name(req.body) if not ctype or "json" in ctype else None
+            if name is not None:
+                log_notifier.info("Started processing message with Task Name '%s'", name)
+                return text_response(f"Started processing message with Task Name '{name}'")
         t: TaskModel = await read_model(req, TaskModel)
         log_notifier.info("Started processing message with Task Name '%s'", t.task_name)
-        mode = (cfg.get_str("TasksNotifier:Mode") or "log").lower()
         if mode == "log":
             return text_response(f"Started processing message with Task Name '{t.task_name}'")
         ok = await send_email(t)

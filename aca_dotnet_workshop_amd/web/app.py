@@ -117,6 +117,7 @@ class WebApp:
         self.openapi_info: dict[str, Any] = {"title": name, "version": "1.0"}
         self._pipeline: Callable[[Request], Awaitable[Response]] | None = None
         self._route_cache: dict[str, list[Route]] = {}
+        self._exact: dict[tuple[str, str], Route] = {}  # (method, raw path) -> literal route
 
     # -- registration ---------------------------------------------------------
     def route(self, template: str, methods: list[str] | tuple[str, ...] = ("GET",), name: str | None = None,
@@ -132,6 +133,7 @@ class WebApp:
         self.routes.append(r)
         self._pipeline = None
         self._route_cache.clear()
+        self._exact.clear()
         return r
 
     def _candidates(self, first: str) -> list[Route]:
@@ -167,6 +169,9 @@ class WebApp:
     def match(self, method: str, path: str) -> tuple[Route | None, dict[str, Any], bool]:
         """``path`` is the raw (still percent-encoded) path; segments are decoded after
         splitting so an encoded ``%2F`` stays inside its segment."""
+        hit = self._exact.get((method, path))
+        if hit is not None:  # a literal route this exact request line resolved to before
+            return hit, {}, True
         parts = [unquote(p) if "%" in p else p for p in path.split("/") if p]
         path_matched = False
         for r in self._candidates(parts[0].lower() if parts else ""):
@@ -174,6 +179,8 @@ class WebApp:
             if params is None:
                 continue
             if method in r.methods or (method == "HEAD" and "GET" in r.methods):
+                if r.catch_all is None and all(k == "lit" for k, _ in r.segments) and len(self._exact) < 256:
+                    self._exact[(method, path)] = r
                 return r, params, True
             path_matched = True
         return None, {}, path_matched
@@ -230,10 +237,11 @@ class WebApp:
                 return problem(500, detail=detail, trace_id=req.state.get("trace_id"))
         return entry
 
-    async def __call__(self, req: Request) -> Response:
+    def __call__(self, req: Request) -> Awaitable[Response]:
+        """The pipeline's coroutine for ``req`` (no extra await layer per request)."""
         if self._pipeline is None:
             self._pipeline = self.build()
-        return await self._pipeline(req)
+        return self._pipeline(req)
 
     @property
     def is_development(self) -> bool:
@@ -309,10 +317,20 @@ def _schema_ref(model: Any, schemas: dict[str, Any]) -> dict[str, Any]:
     return {"$ref": f"#/components/schemas/{name}"}
 
 
+class _Bound:
+    """``mw`` with its ``next`` bound: calling it returns ``mw``'s own coroutine, so a middleware
+    adds one frame to a request's await chain, not two."""
+    __slots__ = ("mw", "nxt")
+
+    def __init__(self, mw: Middleware, nxt: Callable[[Request], Awaitable[Response]]) -> None:
+        self.mw, self.nxt = mw, nxt
+
+    def __call__(self, req: Request) -> Awaitable[Response]:
+        return self.mw(req, self.nxt)
+
+
 def _bind(mw: Middleware, nxt: Callable[[Request], Awaitable[Response]]) -> Callable[[Request], Awaitable[Response]]:
-    async def h(req: Request) -> Response:
-        return await mw(req, nxt)
-    return h
+    return _Bound(mw, nxt)
 
 
 def to_response(result: Any) -> Response:

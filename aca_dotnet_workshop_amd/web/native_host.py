@@ -170,17 +170,17 @@ class NativeHost:
         for ev in self.h.drain():
             try:
                 kind = ev[0]
-                if kind == 0:
+                if kind == 1:  # a client response: resolve the caller's future (headers: lower-cased dict)
+                    fut = self.pending.pop(ev[1], None)
+                    if fut is not None and not fut.done():
+                        fut.set_result(ClientResponse(ev[2], ev[3], ev[4]))
+                elif kind == 0:
                     _, token, sid, method, target, http10, hd, body = ev
                     srv = self.servers.get(sid)
                     if srv is None:
                         self.respond(token, 503, [], b"")
                         continue
                     srv._dispatch(token, method, target, http10, hd, body)
-                elif kind == 1:
-                    fut = self.pending.pop(ev[1], None)
-                    if fut is not None and not fut.done():
-                        fut.set_result(ClientResponse(ev[2], Headers(ev[3]), ev[4]))
                 else:
                     fut = self.pending.pop(ev[1], None)
                     if fut is not None and not fut.done():
@@ -273,7 +273,7 @@ class NativeHttpServer:
                                                                     "HTTP/1.0" if http10 else "HTTP/1.1"), _t.monotonic()))
             self._inflight += 1
             return
-        req = Request(method, target, Headers(hd), body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
+        req = Request(method, target, hd, body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
         self._inflight += 1
         self.loop.create_task(self._serve(token, req))
 
@@ -343,6 +343,15 @@ class NativeHttpClient:
             ep = self._endpoints[key] = f"unix:{key[1]}" if key[0] == "unix" else f"tcp:{key[1]}:{key[2]}"
         to = self.timeout if timeout is None else timeout
         return await self._native().request(ep, method, target, hdrs, body or b"", to)
+
+    def request_at(self, key: Any, method: str, target: str, headers: list[tuple[str, str]], body: bytes,
+                   timeout: float | None = None) -> "asyncio.Future[ClientResponse]":
+        """``request`` to an endpoint already split off by ``parse_endpoint`` (the SDK's sidecar
+        endpoint): no URL parsing per call; returns the future of the response."""
+        ep = self._endpoints.get(key)
+        if ep is None:
+            ep = self._endpoints[key] = f"unix:{key[1]}" if key[0] == "unix" else f"tcp:{key[1]}:{key[2]}"
+        return self._native().request(ep, method, target, headers, body, self.timeout if timeout is None else timeout)
 
     async def get(self, url: str, **kw: Any) -> ClientResponse:
         return await self.request("GET", url, **kw)

@@ -1,0 +1,236 @@
+"""The native TaskModel codec (native/src/taskcodec.hpp) against the pydantic binder it shortcuts.
+
+Invariant: for any body, the codec either declines (``None``: the general binder decides) or
+produces exactly what binding the body with ``TaskAddModel`` and serialising the new
+``TaskModel`` produces -- and it declines every body the binder rejects (400)."""
+import json
+import uuid
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from aca_dotnet_workshop_amd.models import TaskAddModel, TaskModel, create_task_wire, parse_datetime
+
+pytestmark = pytest.mark.skipif(create_task_wire(b"{}") is None, reason="native module not built")
+
+
+def _reference(body: bytes, made) -> bytes | None:
+    """What the pydantic path produces for ``body`` with the codec's id and timestamp."""
+    try:
+        m = TaskAddModel.model_validate(json.loads(body))
+        created = json.loads(made[3])["taskCreatedOn"] if made else "2030-01-01T00:00:00Z"
+        t = TaskModel(task_id=uuid.UUID(made[0]) if made else uuid.uuid4(), task_name=m.task_name,
+                      task_created_by=m.task_created_by, task_created_on=parse_datetime(created),
+                      task_due_date=m.task_due_date, task_assigned_to=m.task_assigned_to)
+        return t.to_json().encode()
+    except Exception:  # rejected by the binder (400) or unserialisable (500)
+        return None
+
+
+def _check(body: bytes) -> bool:
+    made = create_task_wire(body)
+    ref = _reference(body, made)
+    if made is None:
+        return False
+    assert ref is not None, f"codec accepted a body the binder rejects: {body!r}"
+    assert made[3] == ref, (body, made[3], ref)
+    doc = json.loads(made[3])
+    assert made[1] == doc["taskName"] and made[2] == doc["taskAssignedTo"] and made[0] == doc["taskId"]
+    assert json.loads(made[4]) == [{"key": made[0], "value": doc}]
+    return True
+
+
+def _body(**kw) -> bytes:
+    base = {"taskName": "Task 1", "taskCreatedBy": "b@example.com", "taskDueDate": "2030-01-01T00:00:00",
+            "taskAssignedTo": "a@example.com"}
+    base.update(kw)
+    return json.dumps({k: v for k, v in base.items() if v is not ...}).encode()
+
+
+@pytest.mark.parametrize("body", [
+    _body(),
+    _body(taskDueDate="2030-01-01"),
+    _body(taskDueDate="2030-01-01T10:20"),
+    _body(taskDueDate="2030-01-01 10:20:30"),
+    _body(taskDueDate="2030-01-01T10:20:30.1200000"),
+    _body(taskDueDate="2030-01-01T10:20:30,000001Z"),
+    _body(taskDueDate="2024-02-29T00:00:00z"),
+    _body(taskDueDate="2030-01-01T00:00:00.123456789"),
+    _body(taskName='quote " backslash \\ tab \t nl \n bell \x07 del \x7f', taskAssignedTo="é ✓ 😀  "),
+    _body(taskName=...),
+    _body(taskDueDate=...),
+    _body(extra="ignored", another=True, third=None),
+    b'{"taskName":"\\u00e9\\ud83d\\ude00","taskDueDate":"2030-01-01T00:00:00"}',
+    b' {"taskName" : "spaced" ,\n "taskDueDate":"2030-01-01"} ',
+    b"{}",
+])
+def test_codec_matches_binder(body):
+    assert _check(body), f"codec declined a plain body: {body!r}"
+
+
+@pytest.mark.parametrize("body", [
+    _body(TaskName="case"),                      # remapped case-insensitively by the binder
+    _body(task_name="snake"),                    # populate_by_name
+    _body(taskDueDate="2030-01-01T00:00:00+02:00"),
+    _body(taskDueDate=" 2030-01-01"),            # stripped by the binder
+    _body(taskDueDate="2030-02-30"),             # invalid day -> 400
+    _body(taskDueDate="2023-02-29"),
+    _body(taskDueDate="0000-01-01"),
+    _body(taskDueDate="2030-01-01T24:00:00"),
+    _body(taskDueDate="2030-01-01T00:00:00.1234567890"),
+    _body(taskDueDate="not a date"),
+    _body(taskDueDate=20300101),
+    _body(taskName=None),
+    _body(taskName=7),
+    _body(count=3),                              # numbers: the binder's JSON parser decides
+    _body(nested={"a": [1]}),
+    b'{"taskName":"a","taskName":"b"}',          # duplicate: json.loads keeps the last
+    b'{"taskName":"raw\tcontrol"}',              # invalid JSON (strict)
+    b'{"taskName":"\\ud800"}',                   # lone surrogate
+    b'{"taskName":"\xff"}',                      # invalid UTF-8
+    b'\xef\xbb\xbf{"taskName":"bom"}',
+    b'[]', b'"x"', b'', b'{', b'{"taskName":"x"} trailing',
+])
+def test_codec_declines_what_it_does_not_decide(body):
+    assert create_task_wire(body) is None
+    _check(body)  # (and the invariant holds trivially)
+
+
+def test_ids_are_random_v4_and_created_is_now():
+    from datetime import datetime, timezone
+    ids = set()
+    for _ in range(2000):
+        made = create_task_wire(_body())
+        u = uuid.UUID(made[0])
+        assert u.version == 4 and u.variant == uuid.RFC_4122 and str(u) == made[0]
+        ids.add(made[0])
+    assert len(ids) == 2000
+    created = parse_datetime(json.loads(made[3])["taskCreatedOn"])
+    assert abs((datetime.now(timezone.utc) - created).total_seconds()) < 5
+
+
+_text = st.text(st.characters(blacklist_categories=("Cs",)), max_size=12)
+_date = st.one_of(
+    st.datetimes(min_value=__import__("datetime").datetime(1, 1, 1)).map(lambda d: d.isoformat()),
+    st.from_regex(r"\A\d{4}-\d{2}-\d{2}([T ]\d{2}:\d{2}(:\d{2}([.,]\d{1,10})?)?)?([Zz]|[+-]\d{2}:?\d{2})?\Z"),
+    _text)
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.dictionaries(st.sampled_from(["taskName", "taskCreatedBy", "taskAssignedTo", "TaskName", "x"]),
+                       st.one_of(_text, st.none(), st.booleans(), st.integers()), max_size=4), _date)
+def test_codec_fuzz_parity(fields, due):
+    fields["taskDueDate"] = due
+    _check(json.dumps(fields).encode())
+    _check(json.dumps(fields, ensure_ascii=False).encode())
+
+
+def test_api_uses_codec_and_general_binder():
+    """POST /api/tasks: plain bodies take the native pass, others the binder (same responses)."""
+    import asyncio
+
+    from aca_dotnet_workshop_amd.sdk.client import SidecarClient
+    from aca_dotnet_workshop_amd.services.backend_api.app import create_app
+    from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
+    from aca_dotnet_workshop_amd.web.client import ClientResponse
+    from aca_dotnet_workshop_amd.web.http import Headers, Request
+
+    sent = []
+
+    class Http:
+        async def request(self, method, url, *, headers=None, body=None, json_body=None, timeout=None):
+            sent.append((url.split(":", 2)[-1], body))
+            return ClientResponse(204, Headers({}), b"")
+
+        async def close(self):
+            pass
+
+    app = create_app([], manager=TasksStoreManager(SidecarClient("unix:/x:", http=Http())))
+
+    async def post(body, ctype="application/json"):
+        return await app(Request("POST", "/api/tasks", Headers({"content-type": ctype}), body, None, "HTTP/1.1"))
+
+    async def main():
+        r1 = await post(_body())
+        r2 = await post(_body(TaskName="Cased", taskName=...))
+        r3 = await post(_body(taskDueDate="2030-02-30"))
+        r4 = await post(_body(), "text/plain")
+        return r1, r2, r3, r4
+    r1, r2, r3, r4 = asyncio.run(main())
+    assert r1.status == 201 and r2.status == 201 and r3.status == 400 and r4.status == 415
+    tid = dict(r1.headers)["Location"].rsplit("/", 1)[1]
+    (p1, save1), (p2, pub1), (p3, save2), (p4, pub2) = sent
+    assert p1 == "/v1.0/state/statestore" and p2 == "/v1.0/publish/dapr-pubsub-servicebus/tasksavedtopic"
+    assert json.loads(save1)[0]["key"] == tid and json.loads(pub1)["taskId"] == tid
+    assert json.loads(pub2)["taskName"] == "Cased"   # the binder's remapping
+    assert set(json.loads(pub1)) == set(json.loads(pub2))
+
+
+# ---------------------------------------------------------------------- the processor's side
+def _native():
+    from aca_dotnet_workshop_amd.native import load
+    return load()
+
+
+def _envelope(data, **kw):
+    ce = {"specversion": "1.0", "id": "e1", "source": "tasksmanager-backend-api", "type": "com.dapr.event.sent",
+          "topic": "tasksavedtopic", "pubsubname": "dapr-pubsub-servicebus", "datacontenttype": "application/json",
+          "traceparent": "00-4bf92f3577b34da6a3ce929d0e0e4736-00f067aa0ba902b7-00", "data": data}
+    ce.update(kw)
+    return json.dumps(ce).encode()
+
+
+_TASK = {"taskId": "0f8fad5b-d9cb-469f-a165-70867728950e", "taskName": "Task 1", "taskCreatedBy": "b@x",
+         "taskCreatedOn": "2030-01-01T00:00:00.1234567Z", "taskDueDate": "2030-01-02T00:00:00",
+         "taskAssignedTo": "a@x", "isCompleted": False, "isOverDue": False}
+
+
+@pytest.mark.parametrize("data", [_TASK, {"a": ["x", None, True, {"b": "é\n\""}]}, [], {}])
+def test_cloudevent_unwrap_matches_python(data):
+    body = _envelope(data, extra={"k": "v"})
+    u = _native().cloudevent_unwrap(body)
+    ce = json.loads(body)
+    assert u is not None
+    assert json.loads(u[0]) == ce.pop("data") and u[1] == "application/json" and u[2] == ce
+
+
+@pytest.mark.parametrize("body", [
+    _envelope({"n": 1}),                                   # numbers: Python's parser decides
+    _envelope("text", datacontenttype="text/plain"),
+    json.dumps({"specversion": "1.0", "data_base64": "eyJ9"}).encode(),
+    b'{"data":{},"data":{}}', b"[]", b"{", _envelope(_TASK, id=5),
+])
+def test_cloudevent_unwrap_declines(body):
+    assert _native().cloudevent_unwrap(body) is None
+
+
+def _model_ref(body: bytes):
+    try:
+        return TaskModel.model_validate(json.loads(body)).task_name
+    except Exception:
+        return None
+
+
+@pytest.mark.parametrize("kw", [{}, {"taskId": "0F8FAD5B-D9CB-469F-A165-70867728950E"}, {"isCompleted": True},
+                                {"taskCreatedOn": "2030-01-01"}, {"extra": "x"}])
+def test_task_model_name_matches_binder(kw):
+    body = json.dumps({**_TASK, **kw}).encode()
+    assert _native().task_model_name(body) == _model_ref(body) == "Task 1"
+
+
+@pytest.mark.parametrize("kw", [{"taskId": "{0f8fad5b-d9cb-469f-a165-70867728950e}"}, {"taskId": "nope"},
+                                {"isCompleted": "true"}, {"isCompleted": 1}, {"taskDueDate": "2030-13-01"},
+                                {"TaskName": "x"}, {"task_name": "x"}, {"taskName": None}])
+def test_task_model_name_declines(kw):
+    assert _native().task_model_name(json.dumps({**_TASK, **kw}).encode()) is None
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.dictionaries(st.sampled_from(list(_TASK) + ["TaskName", "x"]),
+                       st.one_of(_text, st.none(), st.booleans(), _date, st.uuids().map(str)), max_size=8))
+def test_task_model_name_fuzz(fields):
+    body = json.dumps(fields).encode()
+    got = _native().task_model_name(body)
+    if got is not None:
+        assert got == _model_ref(body), body
