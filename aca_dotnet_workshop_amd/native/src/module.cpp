@@ -6,6 +6,7 @@
 #include "apphost.hpp"
 #include "backingfront.hpp"
 #include "broker.hpp"
+#include "cpuscan.hpp"
 #include "docstore.hpp"
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
@@ -264,6 +265,49 @@ PYBIND11_MODULE(_ttnative, m) {
     if (!taskcodec::task_model_name(std::string_view(p, (size_t)n), name)) return py::none();
     return py::str(name);
   });
+
+  // Columnar query program on the host (cpuscan.hpp): columns = [(uint8 array of the narrow
+  // codes, width)], live = uint16 words (1 bit per row), code = int32 [L, 4], bitmaps = uint32.
+  // Returns the ascending selected row ids (int32 array).  GIL released while scanning.
+  m.def("scan_select",
+        [](py::list columns, py::array_t<uint16_t, py::array::c_style> live, int64_t nrows,
+           py::array_t<int32_t, py::array::c_style> code, py::array_t<uint32_t, py::array::c_style> bitmaps,
+           int threads, bool simd) {
+          std::vector<cpuscan::Col> cols;
+          std::vector<py::array> keep;
+          const int64_t padded = (nrows + 63) / 64 * 64;
+          for (auto item : columns) {
+            auto t = item.cast<py::tuple>();
+            py::array a = t[0].cast<py::array>();
+            int w = t[1].cast<int>();
+            if (w != 1 && w != 2 && w != 4) throw py::value_error("column width must be 1, 2 or 4");
+            if (!(a.flags() & py::array::c_style)) throw py::value_error("columns must be contiguous");
+            if ((int64_t)a.nbytes() < padded * w) throw py::value_error("column shorter than the padded row count");
+            cols.push_back({static_cast<const uint8_t*>(a.data()), w});
+            keep.push_back(a);
+          }
+          if ((int64_t)live.size() * 16 < padded) throw py::value_error("liveness shorter than the padded row count");
+          if (code.ndim() != 2 || code.shape(1) != 4) throw py::value_error("code must be [L, 4]");
+          cpuscan::Program pg;
+          pg.code.assign(code.data(), code.data() + code.size());
+          pg.bitmaps.assign(bitmaps.data(), bitmaps.data() + bitmaps.size());
+          cpuscan::Selection sel(cols, live.data(), nrows, pg, std::max(1, threads), simd);
+          int64_t total;
+          {
+            py::gil_scoped_release rel;
+            total = sel.count();
+          }
+          // the result is written in place on 2 MiB pages (no copy, few first-touch faults)
+          int32_t* dst = static_cast<int32_t*>(cpuscan::huge_alloc((size_t)std::max<int64_t>(total, 1) * sizeof(int32_t)));
+          py::capsule owner(dst, [](void* p) { std::free(p); });
+          {
+            py::gil_scoped_release rel;
+            sel.write(dst);
+          }
+          return py::array_t<int32_t>({(py::ssize_t)total}, {(py::ssize_t)sizeof(int32_t)}, dst, owner);
+        },
+        py::arg("columns"), py::arg("live"), py::arg("nrows"), py::arg("code"), py::arg("bitmaps"), py::arg("threads"),
+        py::arg("simd") = true);
 
   py::class_<TxOp>(m, "TxOp")
       .def(py::init([](bool is_delete, std::string key, std::string value, std::optional<std::string> etag,

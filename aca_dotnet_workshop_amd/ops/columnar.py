@@ -16,6 +16,7 @@ numbers by value; ranges only between like types), producing one bitmap per leaf
 from __future__ import annotations
 
 import json
+import os
 from dataclasses import dataclass
 from typing import Any, Iterable
 
@@ -26,6 +27,18 @@ TILE = 8192           # rows per kernel tile (ops/hip/query_scan.hip kTileRows)
 MAX_DEPTH = 8         # device stack depth (16-bit masks in a 128-bit register)
 MAX_FLAT_LEAVES = 8   # leaves of a flat program (ops/hip/query_scan.hip kMaxFlatLeaves)
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
+
+
+def cpu_share() -> int:
+    """CPUs this process may use: the cgroup quota (``cpu.max``) when set, else its affinity."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(quota) // int(period))
+    except (OSError, ValueError):
+        pass
+    return max(1, len(os.sched_getaffinity(0)))
 
 
 class Unsupported(Exception):
@@ -650,6 +663,49 @@ class ColumnarIndex:
         sel = stack[-1] & (self.live[:n] != 0)
         return np.nonzero(sel)[0].astype(np.int32)
 
+    def select_native(self, prog: Program, threads: int | None = None, simd: bool = True) -> np.ndarray:
+        """The program on the host's CPU share (``native/src/cpuscan.hpp``): every core, SIMD
+        compares, over the same narrow codes / rank copies / liveness bits the GPU kernels read
+        -- the fair CPU baseline for ``select_gpu`` and the executor without a GPU.  Same result
+        as ``select_numpy`` (the reference)."""
+        from ..native import load
+        hm = self._host_mirror(prog)
+        code = prog.code
+        rng = code[:, 0] == OP_RANGE
+        if rng.any():  # range leaves read the rank-encoded copy of their column
+            code = code.copy()
+            code[rng, 1] = [hm["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
+        return load().scan_select(hm["cols"], hm["live"], self.n, np.ascontiguousarray(code, dtype=np.int32),
+                                  prog.bitmaps.view(np.uint32), threads or cpu_share(), simd)
+
+    def _host_mirror(self, prog: Program) -> dict:
+        """Host copies of the columns in the device layout (narrow codes, rank-encoded copies for
+        the program's range leaves, 1-bit liveness), rebuilt when the index changed."""
+        key = (self.version, self.n, self.cap, self._dict_state())
+        hm = getattr(self, "_host", None)
+        if hm is None or hm["key"] != key:
+            widths = [self.width_for(len(c.values)) for c in self.columns]
+            hm = self._host = {"key": key, "widths": widths, "ranks": {},
+                               "cols": [(np.ascontiguousarray(self._narrow(i, 0, self.cap, w)).view(np.uint8), w)
+                                        for i, w in enumerate(widths)],
+                               "live": np.ascontiguousarray(self._live_words(0, self.cap // 16)).view(np.uint16)}
+        rank_cols = sorted(set(prog.code[prog.code[:, 0] == OP_RANGE, 1].tolist()))
+        slots = {}
+        cols = list(hm["cols"][:len(self.columns)])
+        for col in rank_cols:
+            r = hm["ranks"].get(col)
+            if r is None:
+                w = hm["widths"][col]
+                table = self.columns[col].ranks()
+                v = self.ids[col, :self.cap]
+                rk = np.where(v >= 0, table[np.maximum(v, 0)] if table.size else -1, -1)
+                dt = np.uint8 if w == 1 else np.uint16 if w == 2 else np.int32
+                rk = np.where(rk < 0, np.iinfo(dt).max if w < 4 else -1, rk).astype(dt)
+                r = hm["ranks"][col] = (np.ascontiguousarray(rk).view(np.uint8), w)
+            slots[col] = len(cols)
+            cols.append(r)
+        return {"cols": cols, "live": hm["live"], "rank_slot": slots}
+
     # device mirror -------------------------------------------------------------
     @staticmethod
     def width_for(dict_size: int) -> int:
@@ -921,8 +977,11 @@ class ColumnarIndex:
                 token = str(end) if limit and end < total else None
                 return sel.astype(np.int32, copy=False), token
             rows = dev_rows.cpu().numpy()
-        if rows is None:
-            rows = self.select_numpy(prog)
+        if rows is None:  # no GPU: every core of the CPU share over the same narrow codes
+            try:
+                rows = self.select_native(prog)
+            except ImportError:
+                rows = self.select_numpy(prog)
         rows = self.order(rows, sort)
         end = min(rows.size, offset + limit) if limit else rows.size
         sel = rows[offset:end]

@@ -7,8 +7,10 @@ in columnar form, then times the corrected overdue sweep
 
     taskDueDate < today AND isCompleted == false AND isOverDue == false
 
-(scan + order-preserving compaction) on the GPU and, for reference, the same compiled
-program in NumPy on the host.  Reports rows scanned per second and effective HBM GB/s.
+(scan + order-preserving compaction) on the GPU and, as the host baseline, the same compiled
+program over the same narrow codes on every core of the process's CPU share
+(``ColumnarIndex.select_native``, AVX-512); ``--cpu`` adds the single-threaded NumPy reference.
+Reports rows scanned per second and effective HBM GB/s.
 """
 from __future__ import annotations
 
@@ -28,6 +30,8 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu", action="store_true", help="also time the NumPy executor (slow at 1e8 rows)")
+    ap.add_argument("--no-cpu-native", action="store_true",
+                    help="skip the multi-threaded native CPU executor (the fair host baseline)")
     ap.add_argument("--query", action="store_true", help="also time the whole paged query path (ColumnarIndex.query)")
     ap.add_argument("--flat-grid", type=int, default=None, help="tt_scan_flat workgroups (0 = one per tile)")
     ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4; 0 = default)")
@@ -175,6 +179,21 @@ def main() -> None:
             stages["page"] += t3 - t2
         res["query_stages_ms"] = {k2: round(v / it * 1e3, 4) for k2, v in stages.items()}
         res["query_page_rows"] = len(keys)
+    if not a.no_cpu_native:
+        # the fair host baseline: the same program over the same narrow codes, every core of this
+        # process's CPU share, AVX-512 compares (native/src/cpuscan.hpp)
+        from aca_dotnet_workshop_amd.ops.columnar import cpu_share
+        threads = cpu_share()
+        ref = ix.select_native(prog, threads)  # builds the host mirror (narrow copies, rank column)
+        res["cpu_native_matches"] = bool(np.array_equal(ref, out.cpu().numpy()))
+        for label, th in (("cpu_native_ms", threads), ("cpu_native_1thread_ms", 1)):
+            it = max(3, a.iters // (4 if th == 1 else 1))
+            t0 = time.perf_counter()
+            for _ in range(it):
+                ix.select_native(prog, th)
+            res[label] = round((time.perf_counter() - t0) / it * 1e3, 3)
+        res["cpu_threads"] = threads
+        res["gpu_speedup_vs_cpu_native"] = round(res["cpu_native_ms"] / res["ms_per_query"], 1)
     if a.cpu:
         t0 = time.perf_counter()
         ref = ix.select_numpy(prog)

@@ -170,6 +170,44 @@ def test_group_count_numpy():
     assert res == {json.dumps(f"a{j}"): 100 for j in range(5)}
 
 
+@settings(max_examples=150, deadline=None)
+@given(docs_st, filters_st, st.integers(0, 1000), st.integers(1, 4))
+def test_native_cpu_executor_matches_numpy(docs, flt, seed, threads):
+    """native/src/cpuscan.hpp runs the same program over the device-layout narrow codes."""
+    if not docs:
+        return
+    ix = _columnar(_ops(docs, random.Random(seed)))
+    prog = ix.compile(flt)
+    want = ix.select_numpy(prog).tolist()
+    assert ix.select_native(prog, threads).tolist() == want
+    assert ix.select_native(prog, threads, simd=False).tolist() == want
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097, 70_001])
+def test_native_cpu_executor_all_widths(n):
+    """1-, 2- and 4-byte code columns (dictionary sizes 3 / 300 / 70,000), range leaves on
+    their rank copies, missing paths, tombstones, several threads -- against the NumPy reference."""
+    rnd = random.Random(n)
+    ix = ColumnarIndex(capacity=n)
+    for i in range(n):
+        d = {"small": rnd.choice([True, False, None]), "mid": f"m{rnd.randrange(300)}", "big": i % 70_000}
+        if rnd.random() < 0.05:
+            del d["mid"]
+        ix.upsert(str(i), d)
+    for i in rnd.sample(range(n), n // 20):
+        ix.delete(str(i))
+    filters = [{}, {"EQ": {"small": False}}, {"NEQ": {"mid": "m7"}}, {"LT": {"mid": "m150"}},
+               {"AND": [{"GTE": {"big": 100}}, {"LT": {"big": 60_000}}, {"EQ": {"small": True}}]},
+               {"OR": [{"IN": {"mid": ["m1", "m2", "m299"]}}, {"GT": {"big": 69_990}}]},
+               {"EQ": {"nowhere": 1}}, {"EQ": {"mid": "not-a-value"}}]
+    for f in filters:
+        prog = ix.compile(f)
+        want = ix.select_numpy(prog)
+        for threads in (1, 3, 16):
+            assert np.array_equal(ix.select_native(prog, threads), want), (n, f, threads)
+        assert np.array_equal(ix.select_native(prog, 2, simd=False), want), (n, f, "scalar")
+
+
 # ----------------------------------------------------------------------------- GPU
 def _kernels():
     from aca_dotnet_workshop_amd.ops.gpu import GpuKernels
