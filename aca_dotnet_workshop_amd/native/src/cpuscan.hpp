@@ -31,16 +31,18 @@ constexpr int kMaxDepth = 8;
 
 struct Col {
   const uint8_t* p = nullptr;
-  int width = 1;  // bytes per row
+  int width = 1;  // bytes per row; 0 = 2 bits per row (4 rows per byte, row r in bits 2(r mod 4))
 };
 
 inline uint32_t raw_at(const Col& c, int64_t row) {
+  if (c.width == 0) return (c.p[row >> 2] >> ((row & 3) * 2)) & 3u;
   if (c.width == 1) return c.p[row];
   if (c.width == 2) return reinterpret_cast<const uint16_t*>(c.p)[row];
   return reinterpret_cast<const uint32_t*>(c.p)[row];
 }
 
 inline int32_t id_of(uint32_t raw, int width) {
+  if (width == 0) return raw == 3u ? -1 : (int32_t)raw;
   if (width == 1) return raw == 0xFFu ? -1 : (int32_t)raw;
   if (width == 2) return raw == 0xFFFFu ? -1 : (int32_t)raw;
   return (int32_t)raw;
@@ -68,8 +70,25 @@ inline uint64_t bitmap_scalar(const Col& c, int64_t r0, const uint32_t* bm, int3
   return m;
 }
 
+// 2-bit codes of 64 rows (16 bytes) equal to `b`: XOR with the replicated code leaves a zero
+// pair exactly where they match; the even bits of (pair == 0) gathered with PEXT.
+__attribute__((target("bmi2"))) inline uint64_t eq_2bit(const Col& c, int64_t r0, int32_t b) {
+  if (b < 0 || b > 2) return 0;
+  uint64_t w[2];
+  std::memcpy(w, c.p + (r0 >> 2), 16);
+  const uint64_t pat = 0x5555555555555555ull * (uint64_t)b;
+  uint64_t m = 0;
+  for (int h = 0; h < 2; ++h) {
+    const uint64_t x = w[h] ^ pat;
+    const uint64_t zero = ~(x | (x >> 1)) & 0x5555555555555555ull;
+    m |= (uint64_t)_pext_u64(zero, 0x5555555555555555ull) << (32 * h);
+  }
+  return m;
+}
+
 // AVX-512BW: one compare instruction per 64 (1-byte) / 32 (2-byte) / 16 (4-byte) rows.
-__attribute__((target("avx512f,avx512bw"))) inline uint64_t eq_avx512(const Col& c, int64_t r0, int32_t b) {
+__attribute__((target("avx512f,avx512bw,bmi2"))) inline uint64_t eq_avx512(const Col& c, int64_t r0, int32_t b) {
+  if (c.width == 0) return eq_2bit(c, r0, b);
   if (c.width == 1) {
     if (b < 0 || b >= 0xFF) return 0;  // ids of a 1-byte column are < 255; -1/-2 never stored
     return _mm512_cmpeq_epi8_mask(_mm512_loadu_si512(c.p + r0), _mm512_set1_epi8((char)b));
@@ -112,7 +131,7 @@ __attribute__((target("avx512f,avx512bw"))) inline uint64_t range_avx512(const C
 }
 
 inline bool range_ok(const Col& c, int32_t b, int32_t hi) {
-  if (b < 0 || hi < b) return false;
+  if (b < 0 || hi < b || c.width == 0) return false;
   return c.width == 4 || (c.width == 1 ? hi <= 0xFF : hi <= 0xFFFF);
 }
 
@@ -122,7 +141,8 @@ struct Program {
 };
 
 inline bool has_avx512() {
-  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                         __builtin_cpu_supports("bmi2");
   return ok;
 }
 
@@ -166,13 +186,13 @@ inline bool has_avx512() {
 inline uint64_t range_leaf_scalar(const Col& c, int64_t r0, int32_t b, int32_t hi) {
   return range_scalar(c, r0, (uint32_t)b, (uint32_t)(hi - b));
 }
-__attribute__((target("avx512f,avx512bw"))) inline uint64_t range_leaf_avx512(const Col& c, int64_t r0, int32_t b,
+__attribute__((target("avx512f,avx512bw,bmi2"))) inline uint64_t range_leaf_avx512(const Col& c, int64_t r0, int32_t b,
                                                                              int32_t hi) {
   return range_ok(c, b, hi) ? range_avx512(c, r0, (uint32_t)b, (uint32_t)(hi - b))
                             : range_scalar(c, r0, (uint32_t)b, (uint32_t)(hi - b));
 }
 
-TT_CPUSCAN_EVAL64(eval64_avx512, __attribute__((target("avx512f,avx512bw"))), eq_avx512, range_leaf_avx512)
+TT_CPUSCAN_EVAL64(eval64_avx512, __attribute__((target("avx512f,avx512bw,bmi2"))), eq_avx512, range_leaf_avx512)
 TT_CPUSCAN_EVAL64(eval64_scalar, , eq_scalar, range_leaf_scalar)
 #undef TT_CPUSCAN_EVAL64
 
@@ -193,7 +213,7 @@ TT_CPUSCAN_EVAL64(eval64_scalar, , eq_scalar, range_leaf_scalar)
     }                                                                                                     \
     return cnt;                                                                                           \
   }
-TT_CPUSCAN_PASS1(pass1_avx512, __attribute__((target("avx512f,avx512bw,popcnt"))), eval64_avx512)
+TT_CPUSCAN_PASS1(pass1_avx512, __attribute__((target("avx512f,avx512bw,bmi2,popcnt"))), eval64_avx512)
 TT_CPUSCAN_PASS1(pass1_scalar, , eval64_scalar)
 #undef TT_CPUSCAN_PASS1
 

@@ -280,9 +280,10 @@ PYBIND11_MODULE(_ttnative, m) {
             auto t = item.cast<py::tuple>();
             py::array a = t[0].cast<py::array>();
             int w = t[1].cast<int>();
-            if (w != 1 && w != 2 && w != 4) throw py::value_error("column width must be 1, 2 or 4");
+            if (w != 0 && w != 1 && w != 2 && w != 4) throw py::value_error("column width must be 0 (2 bits), 1, 2 or 4");
             if (!(a.flags() & py::array::c_style)) throw py::value_error("columns must be contiguous");
-            if ((int64_t)a.nbytes() < padded * w) throw py::value_error("column shorter than the padded row count");
+            if ((int64_t)a.nbytes() < (w == 0 ? padded / 4 : padded * w))
+              throw py::value_error("column shorter than the padded row count");
             cols.push_back({static_cast<const uint8_t*>(a.data()), w});
             keep.push_back(a);
           }

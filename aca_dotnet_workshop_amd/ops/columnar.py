@@ -695,7 +695,7 @@ class ColumnarIndex:
         for col in rank_cols:
             r = hm["ranks"].get(col)
             if r is None:
-                w = hm["widths"][col]
+                w = max(1, hm["widths"][col])
                 table = self.columns[col].ranks()
                 v = self.ids[col, :self.cap]
                 rk = np.where(v >= 0, table[np.maximum(v, 0)] if table.size else -1, -1)
@@ -709,15 +709,33 @@ class ColumnarIndex:
     # device mirror -------------------------------------------------------------
     @staticmethod
     def width_for(dict_size: int) -> int:
-        """Bytes per row for a column whose dictionary has ``dict_size`` ids (all-ones = missing)."""
-        return 1 if dict_size <= 254 else 2 if dict_size <= 65534 else 4
+        """Code width of a column whose dictionary has ``dict_size`` ids (all-ones = missing):
+        0 = 2 bits per row (<= 3 ids: booleans, with or without null), else bytes per row."""
+        return 0 if dict_size <= 3 else 1 if dict_size <= 254 else 2 if dict_size <= 65534 else 4
+
+    @staticmethod
+    def col_bytes(rows: int, width: int) -> int:
+        return rows // 4 if width == 0 else rows * width
 
     def _narrow(self, col: int, lo: int, hi: int, width: int) -> np.ndarray:
+        """Codes of rows [lo, hi) in the device layout (width 0: ``lo``/``hi`` multiples of 4,
+        four rows per byte, row r in bits 2(r mod 4))."""
         v = self.ids[col, lo:hi]
         if width == 4:
             return v
+        if width == 0:
+            c = np.where(v < 0, 3, v).astype(np.uint8).reshape(-1, 4)
+            return c[:, 0] | (c[:, 1] << 2) | (c[:, 2] << 4) | (c[:, 3] << 6)
         dt = np.uint8 if width == 1 else np.uint16
         return np.where(v < 0, np.iinfo(dt).max, v).astype(dt)
+
+    def _device_codes(self, col: int, width: int) -> np.ndarray:
+        """The whole column in the device layout; 2-bit columns get 16 bytes of padding (the
+        flat scan reads them with the same 16-byte loads as the byte-wide ones)."""
+        v = self._narrow(col, 0, self.cap, width)
+        if width == 0:
+            v = np.concatenate([v, np.zeros(16, dtype=np.uint8)])
+        return np.ascontiguousarray(v)
 
     def _live_words(self, lo_word: int, hi_word: int) -> np.ndarray:
         bits = self.live[lo_word * 16:hi_word * 16].astype(np.uint8)
@@ -733,8 +751,7 @@ class ColumnarIndex:
         widths = [self.width_for(len(c.values)) for c in self.columns]
         nwords = self.cap // 16
         if st is None or self._full_dirty or st["cap"] != self.cap or len(st["cols"]) != len(self.columns):
-            cols = [torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
-                    for i, w in enumerate(widths)]
+            cols = [torch.from_numpy(self._device_codes(i, w)).to(dev) for i, w in enumerate(widths)]
             live = torch.from_numpy(self._live_words(0, nwords)).to(dev)
             seq = torch.from_numpy(self.seq[:self.cap].astype(np.int32)).to(dev)  # uint32 on device
             st = self._dev = {"cols": cols, "widths": widths, "live": live, "synced": self.n, "cap": self.cap,
@@ -743,8 +760,11 @@ class ColumnarIndex:
             lo, hi = st["synced"], self.n
             for i, w in enumerate(widths):
                 if w != st["widths"][i]:
-                    st["cols"][i] = torch.from_numpy(np.ascontiguousarray(self._narrow(i, 0, self.cap, w))).to(dev)
+                    st["cols"][i] = torch.from_numpy(self._device_codes(i, w)).to(dev)
                     st["widths"][i] = w
+                elif hi > lo and w == 0:  # whole bytes of 4 rows: re-pack the edge bytes
+                    a, b = lo // 4, (hi + 3) // 4
+                    st["cols"][i][a:b].copy_(torch.from_numpy(self._narrow(i, 4 * a, 4 * b, 0)))
                 elif hi > lo:
                     st["cols"][i][lo:hi].copy_(torch.from_numpy(self._narrow(i, lo, hi, w)))
             if hi > lo:
@@ -782,7 +802,7 @@ class ColumnarIndex:
     def _sync_rank_column(self, kernels, st, ranks, col: int) -> None:
         torch = kernels.torch
         c = self.columns[col]
-        w = st["widths"][col]
+        w = max(1, st["widths"][col])  # ranks run 1..n and need a distinct missing code: >= 1 byte
         cur = ranks.get(col)
         full = cur is None or cur["w"] != w or cur["ver"] != c.rank_version
         lo = 0 if full else cur["synced"]
@@ -794,7 +814,7 @@ class ColumnarIndex:
                                 "ver": c.rank_version, "table": None, "synced": 0}
             table = c.ranks().astype(np.int32) if c.values else np.zeros(1, dtype=np.int32)
             cur["table"] = torch.from_numpy(table).to(kernels.device)
-        src = torch.from_numpy(np.array([[st["cols"][col].data_ptr(), w]], dtype=np.int64)).to(kernels.device)
+        src = torch.from_numpy(np.array([[st["cols"][col].data_ptr(), st["widths"][col]]], dtype=np.int64)).to(kernels.device)
         kernels.rank_encode(src, cur["table"], lo, self.n, cur["t"], w)
         cur["synced"] = self.n
 
@@ -830,7 +850,8 @@ class ColumnarIndex:
         if flat is None:
             return None
         leaves, flip, cols = flat
-        return leaves, flip, int(st["table_widths"][cols].max()) if cols.size else 1
+        # kernel instantiation by the widest byte width (2-bit columns ride on the 1-byte one)
+        return leaves, flip, max(1, int(st["table_widths"][cols].max())) if cols.size else 1
 
     def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
         st, code, bitmaps, flat = self.device_program(prog, kernels)
@@ -859,13 +880,20 @@ class ColumnarIndex:
         return {json.dumps(col.values[i]): int(x) for i, x in enumerate(cnt) if x}
 
     # -- full query --------------------------------------------------------------
-    def order(self, rows: np.ndarray, sort: list[dict[str, Any]] | None) -> np.ndarray:
+    def order(self, rows: np.ndarray, sort: list[dict[str, Any]] | None, k: int | None = None) -> np.ndarray:
+        """``rows`` in result order; with ``k``, only the first ``k`` of that order (a page: one
+        partition of the packed keys, then a sort of those ``k``, instead of a full sort)."""
         if rows.size == 0:
             return rows
         plan = self.sort_specs(sort)
-        if plan is not None:  # one argsort of packed keys (same keys the GPU path sorts)
-            return rows[np.argsort(self.sort_keys_numpy(rows, plan), kind="stable")]
-        return self.order_lexsort(rows, sort)
+        if plan is not None:  # packed keys (the ones the GPU path sorts; unique: seq is the tail)
+            keys = self.sort_keys_numpy(rows, plan)
+            if k is not None and 0 < k < rows.size:
+                part = np.argpartition(keys, k - 1)[:k]
+                return rows[part[np.argsort(keys[part])]]
+            return rows[np.argsort(keys, kind="stable")]
+        out = self.order_lexsort(rows, sort)
+        return out[:k] if k else out
 
     def order_lexsort(self, rows: np.ndarray, sort: list[dict[str, Any]] | None) -> np.ndarray:
         """Reference ordering: insertion order, then a stable lexsort on the sort keys' ranks."""
@@ -982,8 +1010,9 @@ class ColumnarIndex:
                 rows = self.select_native(prog)
             except ImportError:
                 rows = self.select_numpy(prog)
-        rows = self.order(rows, sort)
-        end = min(rows.size, offset + limit) if limit else rows.size
+        total = rows.size
+        rows = self.order(rows, sort, offset + limit if limit else None)
+        end = min(total, offset + limit) if limit else total
         sel = rows[offset:end]
-        token = str(end) if limit and end < rows.size else None
+        token = str(end) if limit and end < total else None
         return sel.astype(np.int32, copy=False), token

@@ -91,9 +91,9 @@ class GpuKernels:
             raise ValueError("grid must be >= 0")
 
     def set_eval_groups(self, u: int) -> None:
-        """Row groups per lane in ``tt_scan_eval`` (1, 2 or 4): registers vs loads in flight."""
+        """Row groups per lane in ``tt_scan_eval`` (1, 2, 4 or 8): registers vs loads in flight."""
         if self.lib.tt_set_eval_groups(int(u)) != 0:
-            raise ValueError("eval groups must be 1, 2 or 4")
+            raise ValueError("eval groups must be 1, 2, 4 or 8")
 
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)

@@ -2,8 +2,10 @@
 // (gfx950 / CDNA4, wave64).  Version 2: narrow columns, bit-sliced evaluation.
 //
 // Data model (built by ops/columnar.py): every queryable JSON path of a collection is a
-// dictionary-encoded column of 1, 2 or 4 bytes per row (width chosen from the dictionary
-// size; the all-ones value of the width means "path missing"), plus a 1-bit liveness mask.
+// dictionary-encoded column of 2 bits (width code 0: dictionaries of <= 3 values -- booleans),
+// 1, 2 or 4 bytes per row (width chosen from the dictionary size; the all-ones value of the
+// width means "path missing"), plus a 1-bit liveness mask.  A 2-bit column packs 16 rows per
+// 32-bit word, row r in bits 2(r mod 16) of word r / 16.
 // A query filter (EQ/NEQ/IN/GT/GTE/LT/LTE/AND/OR of the Dapr state-query API) is compiled on
 // the host into a postfix program whose leaves are "id of column c == v" or "id in bitmap
 // S"; ordering/type semantics are resolved against the dictionary on the host, so the
@@ -38,13 +40,14 @@ enum Op : int32_t { OP_LEAF = 1, OP_AND = 2, OP_OR = 3, OP_NOT = 4, OP_TRUE = 5,
 
 struct ColumnDesc {     // 16 bytes, host-built table
   uint64_t ptr;         // device address of the column (row 0)
-  int32_t width;        // 1, 2 or 4 bytes per row
+  int32_t width;        // 1, 2 or 4 bytes per row; 0 = 2 bits per row
   int32_t pad;
 };
 
 using u128 = unsigned __int128;
 
 __device__ __forceinline__ int32_t id_of(uint32_t raw, int width) {
+  if (width == 0) return raw == 3u ? -1 : (int32_t)raw;
   if (width == 1) return raw == 0xFFu ? -1 : (int32_t)raw;
   if (width == 2) return raw == 0xFFFFu ? -1 : (int32_t)raw;
   return (int32_t)raw;
@@ -52,7 +55,11 @@ __device__ __forceinline__ int32_t id_of(uint32_t raw, int width) {
 
 // Load the 16 ids of rows [row0, row0+16) of one column.
 __device__ __forceinline__ void load16(const ColumnDesc& cd, int64_t row0, int32_t (&ids)[16]) {
-  if (cd.width == 1) {
+  if (cd.width == 0) {  // one dword: 16 two-bit codes (row0 is a multiple of 16)
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(cd.ptr) + (row0 >> 2));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ids[i] = id_of((w >> (2 * i)) & 3u, 0);
+  } else if (cd.width == 1) {
     const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(cd.ptr) + row0);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -75,27 +82,90 @@ __device__ __forceinline__ void load16(const ColumnDesc& cd, int64_t row0, int32
 
 }  // namespace
 
-// Leaf test for 16 rows against a dictionary-id bitmap.  Dictionaries of <= 64 ids use a
-// register-resident 64-bit copy of the bitmap (no memory traffic per row); larger ones probe
-// the bitmap words, which the kernel staged in LDS when they fit (`bm` then points to LDS).
-template <typename BitmapPtr>
-__device__ __forceinline__ uint32_t leaf_mask(const int32_t (&ids)[16], BitmapPtr bm, int32_t nbits) {
-  uint32_t m = 0;
-  if (nbits <= 64) {
-    const uint64_t b64 = (uint64_t)bm[0] | ((nbits > 32) ? ((uint64_t)bm[1] << 32) : 0ull);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int32_t id = ids[i];
-      m |= (uint32_t)((id >= 0 && id < nbits) ? ((b64 >> id) & 1ull) : 0ull) << i;
-    }
+// Raw code words of one 16-row group: 2-bit columns one dword, 1/2/4-byte columns 4/8/16.
+template <int W>
+struct GroupWords {
+  static constexpr int n = W == 0 ? 1 : 4 * W;
+};
+
+template <int W>
+__device__ __forceinline__ void load_words(const ColumnDesc& cd, int64_t row0, uint32_t (&w)[GroupWords<W>::n]) {
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(cd.ptr);
+  if constexpr (W == 0) {
+    w[0] = *reinterpret_cast<const uint32_t*>(base + (row0 >> 2));
   } else {
+    const uint4* p = reinterpret_cast<const uint4*>(base + row0 * W);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int32_t id = ids[i];
-      m |= ((id >= 0 && id < nbits) ? ((bm[id >> 5] >> (id & 31)) & 1u) : 0u) << i;
+    for (int q = 0; q < W; ++q) {
+      const uint4 v = p[q];
+      w[4 * q + 0] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+  }
+}
+
+template <int W, int N>
+__device__ __forceinline__ uint32_t code_at(const uint32_t (&w)[N], int i) {
+  if constexpr (W == 0) return (w[0] >> (2 * i)) & 3u;
+  if constexpr (W == 1) return (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+  if constexpr (W == 2) return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
+  return w[i];
+}
+
+// 16-row mask of one leaf straight from the raw codes (no translation to ids: the all-ones
+// missing code of a width is never a dictionary id, a bitmap bit or inside a rank range).
+// EQ on 2-bit codes is SWAR over the whole dword: XOR with the replicated code, a zero pair
+// marks a match, and the even bits are compacted to 16 bits.
+template <int W, typename BitmapPtr>
+__device__ __forceinline__ uint32_t leaf_bits(int32_t op, int32_t b, int32_t c, const uint32_t (&w)[GroupWords<W>::n],
+                                              BitmapPtr bitmaps) {
+  uint32_t m = 0;
+  if (op == OP_EQ) {
+    if constexpr (W == 0) {
+      if ((uint32_t)b > 2u) return 0;
+      const uint32_t x = w[0] ^ (0x55555555u * (uint32_t)b);
+      uint32_t z = ~(x | (x >> 1)) & 0x55555555u;
+      z = (z | (z >> 1)) & 0x33333333u;
+      z = (z | (z >> 2)) & 0x0F0F0F0Fu;
+      z = (z | (z >> 4)) & 0x00FF00FFu;
+      return (z | (z >> 8)) & 0x0000FFFFu;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m |= (uint32_t)(code_at<W>(w, i) == (uint32_t)b) << i;
+    }
+  } else if (op == OP_RANGE) {  // b <= rank < c on a rank-encoded column
+    const uint32_t span = (uint32_t)(c - b);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m |= (uint32_t)(code_at<W>(w, i) - (uint32_t)b < span) << i;
+  } else {  // OP_LEAF: dictionary-id bitmap (register copy for <= 64 ids, else LDS / global words)
+    const BitmapPtr bm = bitmaps + b;
+    const uint32_t nbits = (uint32_t)c;
+    if (nbits <= 64) {
+      const uint64_t b64 = (uint64_t)bm[0] | ((nbits > 32) ? ((uint64_t)bm[1] << 32) : 0ull);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t r = code_at<W>(w, i);
+        m |= (uint32_t)(r < nbits && ((b64 >> (r & 63u)) & 1ull)) << i;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t r = code_at<W>(w, i);
+        m |= (uint32_t)(r < nbits && ((bm[r >> 5] >> (r & 31u)) & 1u)) << i;
+      }
     }
   }
   return m;
+}
+
+// One leaf over the lane's U groups: all U loads first (U loads in flight), then the tests.
+template <int W, int U, typename BitmapPtr>
+__device__ __forceinline__ void leaf_groups(const ColumnDesc& cd, const int64_t (&row0)[U], int32_t op, int32_t b,
+                                            int32_t c, BitmapPtr bitmaps, uint32_t (&m)[U]) {
+  uint32_t w[U][GroupWords<W>::n];
+#pragma unroll
+  for (int u = 0; u < U; ++u) load_words<W>(cd, row0[u], w[u]);
+#pragma unroll
+  for (int u = 0; u < U; ++u) m[u] = leaf_bits<W>(op, b, c, w[u], bitmaps);
 }
 
 // Evaluate the program for U independent 16-row groups at once: every leaf issues its U vector
@@ -114,37 +184,17 @@ __device__ __forceinline__ void run_program(const ColumnDesc* __restrict__ cols,
     const int32_t a = prog[pc * 4 + 1];
     const int32_t b = prog[pc * 4 + 2];
     const int32_t c = prog[pc * 4 + 3];
-    if (op == OP_RANGE) {
-      // range leaf on a rank-encoded column (`a` = its table row): b <= rank < c, one unsigned
-      // compare per row instead of a bitmap probe; the missing code never falls inside
+    if (op == OP_RANGE || op == OP_LEAF || op == OP_EQ) {
       const ColumnDesc cd = cols[a];
-      int32_t r[U][16];
-#pragma unroll
-      for (int u = 0; u < U; ++u) load16(cd, row0[u], r[u]);
-      const uint32_t span = (uint32_t)(c - b);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) m |= (uint32_t)((uint32_t)(r[u][i] - b) < span) << i;
-        st[u] = (st[u] << 16) | (u128)m;
+      uint32_t m[U];
+      switch (cd.width) {  // uniform per leaf: one code path per wave
+        case 0: leaf_groups<0, U>(cd, row0, op, b, c, bitmaps, m); break;
+        case 1: leaf_groups<1, U>(cd, row0, op, b, c, bitmaps, m); break;
+        case 2: leaf_groups<2, U>(cd, row0, op, b, c, bitmaps, m); break;
+        default: leaf_groups<4, U>(cd, row0, op, b, c, bitmaps, m); break;
       }
-    } else if (op == OP_LEAF || op == OP_EQ) {
-      const ColumnDesc cd = cols[a];
-      int32_t ids[U][16];
 #pragma unroll
-      for (int u = 0; u < U; ++u) load16(cd, row0[u], ids[u]);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        uint32_t m = 0;
-        if (op == OP_EQ) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) m |= (uint32_t)(ids[u][i] == b) << i;
-        } else {
-          m = leaf_mask(ids[u], bitmaps + b, c);
-        }
-        st[u] = (st[u] << 16) | (u128)m;
-      }
+      for (int u = 0; u < U; ++u) st[u] = (st[u] << 16) | (u128)m[u];
     } else if (op == OP_AND || op == OP_OR) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -252,10 +302,13 @@ static_assert(kFlatChunksPerWave == 2, "a tile is 4 waves x 2 chunks");
 // column of the program: always N/4 16-byte loads per leaf, a narrower column re-reading its
 // first piece (an L2 hit, never past the column's end), so every leaf step issues the same
 // number of loads and the compiler's wait counts stay exact across the pipelined loop.
+// A 2-bit column needs one dword per lane (16 rows) and is read with the same 16-byte loads as
+// the others (its device buffer carries 16 bytes of padding, ColumnarIndex.to_device); only
+// w[0] is used.
 template <int N>
 __device__ __forceinline__ void issue_leaf_load(const ColumnDesc& cd, int64_t row0, uint32_t (&w)[N]) {
-  const __attribute__((address_space(1))) uint32_t* p =
-      reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(cd.ptr + (uint64_t)row0 * cd.width);
+  const __attribute__((address_space(1))) uint32_t* p = reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(
+      cd.ptr + (cd.width == 0 ? (uint64_t)row0 / 4 : (uint64_t)row0 * cd.width));
 #pragma unroll
   for (int q = 0; q < N / 4; ++q) {
     const int qq = q < cd.width ? q : 0;
@@ -266,6 +319,7 @@ __device__ __forceinline__ void issue_leaf_load(const ColumnDesc& cd, int64_t ro
 
 template <int W, int N>
 __device__ __forceinline__ uint32_t raw_at(const uint32_t (&w)[N], int i) {
+  if (W == 0) return (w[0] >> (2 * i)) & 3u;
   if (W == 1) return (w[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
   if (W == 2) return (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu;
   return w[i];
@@ -306,7 +360,8 @@ __device__ __forceinline__ void flat_step(const int32_t* __restrict__ leaf, int 
   const int32_t op = leaf[0] & 0xFF;
   const uint64_t flip = (leaf[0] >> 8) ? ~0ull : 0ull;
   const uint32_t b = (uint32_t)leaf[2], c = (uint32_t)leaf[3];
-  if (N == 4 || width == 1) apply_leaf<1>(op, b, c, flip, w, bitmaps, acc);
+  if (width == 0) apply_leaf<0>(op, b, c, flip, w, bitmaps, acc);
+  else if (N == 4 || width == 1) apply_leaf<1>(op, b, c, flip, w, bitmaps, acc);
   else if (N == 8 || width == 2) apply_leaf<2>(op, b, c, flip, w, bitmaps, acc);
   else apply_leaf<4>(op, b, c, flip, w, bitmaps, acc);
 }
@@ -640,7 +695,8 @@ tt_rank_encode(const ColumnDesc* __restrict__ src, const int32_t* __restrict__ r
   const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   auto one = [&](int64_t row) {
     uint32_t raw;
-    if (cd.width == 1) raw = reinterpret_cast<const uint8_t*>(cd.ptr)[row];
+    if (cd.width == 0) raw = (reinterpret_cast<const uint8_t*>(cd.ptr)[row >> 2] >> ((row & 3) * 2)) & 3u;
+    else if (cd.width == 1) raw = reinterpret_cast<const uint8_t*>(cd.ptr)[row];
     else if (cd.width == 2) raw = reinterpret_cast<const uint16_t*>(cd.ptr)[row];
     else raw = reinterpret_cast<const uint32_t*>(cd.ptr)[row];
     store_rank(dst_ptr, dst_width, row, rank_of(id_of(raw, cd.width), lds_rank, rank_table, nranks, staged));
@@ -717,7 +773,7 @@ tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* _
 // Row groups per lane of the scan kernel (1, 2 or 4); tunable for A/B measurements.
 static int g_eval_groups = 2;  // measured on MI355X: 1 -> 0.183 ms, 2 -> 0.175 ms, 4 -> 0.194 ms per 1e8-row query
 extern "C" int tt_set_eval_groups(int u) {
-  if (u != 1 && u != 2 && u != 4) return -1;
+  if (u != 1 && u != 2 && u != 4 && u != 8) return -1;
   g_eval_groups = u;
   return 0;
 }
@@ -743,6 +799,10 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
       break;
     case 4:
       hipLaunchKernelGGL(tt_scan_eval_t<4>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 4)), lds, stream,
+                         cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
+      break;
+    case 8:
+      hipLaunchKernelGGL(tt_scan_eval_t<8>, dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * 8)), lds, stream,
                          cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
   }
   return (int)hipGetLastError();

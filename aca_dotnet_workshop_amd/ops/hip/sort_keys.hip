@@ -29,7 +29,7 @@ constexpr int kHistBins = 4096;      // 12-bit radix-select histogram (top-k)
 
 struct SortColumn {   // 16 bytes, same layout as the scan kernel's ColumnDesc
   uint64_t ptr;
-  int32_t width;
+  int32_t width;      // 1, 2 or 4 bytes per row; 0 = 2 bits per row
   int32_t pad;
 };
 
@@ -45,6 +45,10 @@ struct SortSpec {     // host-built, one per sort key (primary first)
 };
 
 __device__ __forceinline__ int32_t load_id(const SortColumn& c, int64_t row) {
+  if (c.width == 0) {  // 2-bit codes, 3 = missing
+    const uint32_t v = (reinterpret_cast<const uint8_t*>(c.ptr)[row >> 2] >> ((row & 3) * 2)) & 3u;
+    return v == 3u ? -1 : (int32_t)v;
+  }
   if (c.width == 1) {
     const uint32_t v = reinterpret_cast<const uint8_t*>(c.ptr)[row];
     return v == 0xFFu ? -1 : (int32_t)v;

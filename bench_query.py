@@ -108,7 +108,10 @@ def main() -> None:
     single_pass_ms = dt_one * 1e3
     same = bool(torch.equal(one, out))
     # bytes: referenced columns at their narrow widths + liveness bit + mask write & read + output indices
-    widths = sum(st["widths"][c] for c in prog.columns)
+    # bytes per row of the columns the scan reads (2-bit codes: width 0 = 1/4 byte; range leaves
+    # read their rank-encoded copy, at least one byte)
+    rank_cols = set(prog.code[prog.code[:, 0] == 7, 1].tolist())
+    widths = sum((max(1, st["widths"][c]) if c in rank_cols else (st["widths"][c] or 0.25)) for c in prog.columns)
     nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),

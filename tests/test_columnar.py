@@ -135,6 +135,25 @@ def test_bulk_encoded_index_matches_native(docs, flt, sort, seed):
     assert got == want
 
 
+@settings(max_examples=120, deadline=None)
+@given(docs_st, filters_st, sort_st, st.integers(1, 7), st.integers(0, 1000))
+def test_pages_concatenate_to_the_full_order(docs, flt, sort, limit, seed):
+    """Paged queries (top-k partition per page on the host) walk the same order as one full query."""
+    if not docs:
+        return
+    ix = _columnar(_ops(docs, random.Random(seed)))
+    q = {"filter": flt, **({"sort": sort} if sort else {})}
+    full, _ = ix.query(q)
+    got, token = [], None
+    while True:
+        page = {"limit": limit, **({"token": token} if token else {})}
+        keys, token = ix.query({**q, "page": page})
+        got += keys
+        if token is None:
+            break
+    assert got == full
+
+
 def test_paging_and_compaction():
     ix = ColumnarIndex()
     for i in range(10000):
@@ -242,7 +261,7 @@ def test_gpu_scan_matches_numpy(n):
     k = _kernels()
     ix = _random_collection(n, random.Random(n))
     try:
-        for u in (1, 2, 4):  # every tt_scan_eval instantiation (row groups per lane)
+        for u in (1, 2, 4, 8):  # every tt_scan_eval instantiation (row groups per lane)
             k.set_eval_groups(u)
             for f in GPU_FILTERS:
                 prog = ix.compile(f)
@@ -393,6 +412,50 @@ def test_gpu_incremental_sync_and_width_growth():
     ix.compact()
     prog = ix.compile({"LT": {"v": 1000}})
     assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))
+
+
+@pytest.mark.gpu
+def test_gpu_two_bit_columns():
+    """Dictionaries of <= 3 values (booleans, with null) are 2-bit codes on the device: appends
+    that end mid-byte, EQ / NEQ / IN / range leaves, ordering and grouping by such a column, and
+    the re-encode when the dictionary outgrows 2 bits -- all against the host executors."""
+    k = _kernels()
+    rnd = random.Random(5)
+    ix = ColumnarIndex(["done", "state"])
+    flags = [True, False]
+
+    def check(label):
+        for f in ({"EQ": {"done": False}}, {"NEQ": {"done": True}}, {"IN": {"state": [None, "b"]}},
+                  {"AND": [{"EQ": {"done": True}}, {"GTE": {"state": "b"}}]}, {"OR": [{"EQ": {"state": "a"}}, {"EQ": {"done": True}}]},
+                  {"LT": {"done": True}}):
+            prog = ix.compile(f)
+            want = ix.select_numpy(prog)
+            for flat in (False, True):
+                k.flat_eval = flat
+                assert np.array_equal(ix.select_gpu(prog, k), want), (label, f, flat)
+            assert np.array_equal(ix.select_native(prog, 2), want), (label, f)
+        k.flat_eval = False
+        q = {"filter": {"EQ": {"done": False}}, "sort": [{"key": "state", "order": "DESC"}, {"key": "done"}],
+             "page": {"limit": 50}}
+        assert ix.query(q, k) == ix.query(q), label
+        assert ix.group_count_gpu(ix.compile({}), "state", k) == ix.group_count_numpy(ix.compile({}), "state"), label
+
+    n = 0
+    for batch in (4097, 3, 1, 20000, 7):  # every append ends at a different row mod 4
+        for _ in range(batch):
+            d = {"done": rnd.choice(flags)}
+            if rnd.random() < 0.9:
+                d["state"] = rnd.choice(["a", "b", None])
+            ix.upsert(str(n), d)
+            n += 1
+        check(f"n={n}")
+    assert ix._dev["widths"][ix.col_of["done"]] == 0 and ix._dev["widths"][ix.col_of["state"]] == 0
+    for i in rnd.sample(range(n), 300):
+        ix.delete(str(i))
+    check("tombstones")
+    ix.upsert("grow", {"done": True, "state": "c"})  # 4 distinct values: the column becomes 1 byte
+    check("grown")
+    assert ix._dev["widths"][ix.col_of["state"]] == 1
 
 
 def _interleaved(ix, store, rnd, kernels=None, rounds=12):
