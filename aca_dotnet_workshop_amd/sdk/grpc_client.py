@@ -49,6 +49,34 @@ def _loads(b: bytes) -> Any:
         return b.decode("utf-8", "replace")
 
 
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def _ld(field: int, data: bytes) -> bytes:
+    """One length-delimited protobuf field (strings, bytes, sub-messages)."""
+    return _varint((field << 3) | 2) + _varint(len(data)) + data
+
+
+def encode_save_state(store: str, key: str, value_json: bytes) -> bytes:
+    """``SaveStateRequest{store_name, states: [StateItem{key, value}]}`` without message objects
+    (the common save: no ETag, metadata or options)."""
+    return _ld(1, store.encode()) + _ld(2, _ld(1, key.encode()) + _ld(2, value_json))
+
+
+def encode_publish_event(pubsub: str, topic: str, data: bytes, content_type: str) -> bytes:
+    """``PublishEventRequest{pubsub_name, topic, data, data_content_type}`` (no metadata)."""
+    return _ld(1, pubsub.encode()) + _ld(2, topic.encode()) + _ld(3, data) + _ld(4, content_type.encode())
+
+
 class _NativeRpcError(Exception):
     """A non-OK gRPC status from the native transport (shape of ``grpc.aio.AioRpcError``)."""
 
@@ -150,6 +178,33 @@ class GrpcSidecarClient:
             md.append(("dapr-api-token", self.api_token))
         return md
 
+    async def _call_encoded(self, rpc: str, payload: bytes, span_name: str) -> None:
+        """A unary call whose request is already serialized and whose response is ignored
+        (SaveState, PublishEvent: ``Empty``).  On the native transport inside an unsampled trace
+        it goes straight to the app host's HTTP/2 client, without a span."""
+        parent = tracing.current_span()
+        if self.transport == "native" and parent is not None and not parent.sampled:
+            if self._channel is None:
+                self._channel = self._new_channel()
+            md = [("traceparent", parent.traceparent)]
+            if self.api_token:
+                md.append(("dapr-api-token", self.api_token))
+            try:
+                r = await self._channel._native._native().grpc_call(self._channel.endpoint, P.method_path(rpc), md,
+                                                                     payload, self.timeout)
+            except OSError as e:
+                raise InvocationError(503, f"sidecar unreachable: {e}".encode(), rpc) from None
+            except asyncio.TimeoutError:
+                raise InvocationError(504, b"Deadline Exceeded", rpc) from None
+            if r.status != 0:
+                status = _HTTP_OF.get(_STATUS_OF.get(r.status, grpc.StatusCode.UNKNOWN), 500)
+                if "dapr-http-status" in r.headers:
+                    status = int(r.headers["dapr-http-status"])
+                raise InvocationError(status, r.headers.get("grpc-message", "").encode(), rpc)
+            return
+        req_cls, _ = P.rpc_types(rpc)
+        await self._call(rpc, req_cls.FromString(payload), span_name)
+
     async def _call(self, rpc: str, req, span_name: str):
         span = tracing.tracer().start_span(span_name, "client")
         span.set("rpc.system", "grpc")
@@ -219,6 +274,10 @@ class GrpcSidecarClient:
     async def save_state(self, store: str, key: str, value: Any, etag: str | None = None,
                          metadata: dict[str, str] | None = None, concurrency: str | None = None,
                          consistency: str | None = None) -> None:
+        if etag is None and not metadata and not concurrency and not consistency:
+            await self._call_encoded("SaveState", encode_save_state(store, key, _value_json(value).encode()),
+                                     f"state save {store}")
+            return
         req = P.rt("SaveStateRequest")(store_name=store)
         self._item(req.states.add(), key, value, etag, metadata, concurrency, consistency)
         await self._call("SaveState", req, f"state save {store}")
@@ -286,6 +345,10 @@ class GrpcSidecarClient:
     async def publish_event(self, pubsub: str, topic: str, data: Any, content_type: str | None = None,
                             metadata: dict[str, str] | None = None) -> None:
         body, ctype = _encode(data)
+        if not metadata:
+            await self._call_encoded("PublishEvent", encode_publish_event(pubsub, topic, body, content_type or ctype),
+                                     f"publish {pubsub}/{topic}")
+            return
         req = P.rt("PublishEventRequest")(pubsub_name=pubsub, topic=topic, data=body,
                                           data_content_type=content_type or ctype, metadata=metadata or {})
         await self._call("PublishEvent", req, f"publish {pubsub}/{topic}")

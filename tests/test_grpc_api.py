@@ -218,5 +218,21 @@ def test_backend_api_over_grpc_transport(plane):
             assert [x.task_id for x in tasks] == [t.task_id]
             assert await _until(lambda: len(received) == 1)
             assert received[0]["taskName"] == "grpc task" and received[0]["taskId"] == str(tid)
+            # the request path of a running service: inside an unsampled trace the native transport
+            # sends pre-encoded SaveState / PublishEvent straight to the app host (no span)
+            from aca_dotnet_workshop_amd.telemetry import tracing
+            n = GrpcSidecarClient(f"127.0.0.1:{h.sc.bound_grpc_port}", transport="native")
+            mgr.client = n
+            span = tracing.Tracer("t", None, sample_rate=0.0).start_span("POST", "server")
+            try:
+                assert not span.sampled
+                tid2 = await mgr.create_new_task_from_body(
+                    b'{"taskName":"fast grpc","taskCreatedBy":"me@x","taskDueDate":"2030-01-02","taskAssignedTo":"a@x"}')
+            finally:
+                span.end()
+            assert (await mgr.get_task_by_id(tid2)).task_name == "fast grpc"
+            assert await _until(lambda: len(received) == 2)
+            assert received[1]["taskId"] == tid2 and received[1]["taskDueDate"] == "2030-01-02T00:00:00"
             await g.close()
+            await n.close()
     run(main())
