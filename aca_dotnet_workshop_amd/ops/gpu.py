@@ -28,6 +28,10 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_scan_flat.argtypes = [P, I64, P, P, I32, I32, I32, P, I32, P, P, P]
     lib.tt_launch_scan_flat.restype = ctypes.c_int
     lib.tt_max_flat_leaves.restype = ctypes.c_int
+    lib.tt_set_eval_nt.argtypes = [ctypes.c_int]
+    lib.tt_set_eval_nt.restype = ctypes.c_int
+    lib.tt_set_compact_nt.argtypes = [ctypes.c_int]
+    lib.tt_set_compact_nt.restype = ctypes.c_int
     lib.tt_set_flat_grid.argtypes = [I64]
     lib.tt_set_flat_grid.restype = ctypes.c_int
     lib.tt_sort_pairs_temp_bytes.argtypes = [I64, I32]
@@ -89,6 +93,14 @@ class GpuKernels:
         """Workgroups of ``tt_scan_flat`` (grid-stride over tiles); 0 = one per tile."""
         if self.lib.tt_set_flat_grid(int(blocks)) != 0:
             raise ValueError("grid must be >= 0")
+
+    def set_compact_nt(self, on: bool) -> None:
+        """Non-temporal stores for the compacted row ids (default on; A/B)."""
+        self.lib.tt_set_compact_nt(1 if on else 0)
+
+    def set_eval_nt(self, on: bool) -> None:
+        """Non-temporal column loads in ``tt_scan_eval`` (default off; A/B)."""
+        self.lib.tt_set_eval_nt(1 if on else 0)
 
     def set_eval_groups(self, u: int) -> None:
         """Row groups per lane in ``tt_scan_eval`` (1, 2, 4 or 8): registers vs loads in flight."""
