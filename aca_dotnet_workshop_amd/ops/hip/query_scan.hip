@@ -551,7 +551,19 @@ tt_scan_compact_t(const uint32_t* __restrict__ mask32,      // selection mask vi
   __syncthreads();
   int32_t* dst = out + tile_base;
   if constexpr (NT) {
-    for (int i = t; i < count; i += kBlock) __builtin_nontemporal_store(staged[i], dst + i);
+    // 16-byte stores: a scalar head up to the first 16-byte aligned output slot, then each
+    // thread writes 4 consecutive ids per store (4x fewer store instructions), a scalar tail
+    const int head = (int)((4 - (tile_base & 3)) & 3) < count ? (int)((4 - (tile_base & 3)) & 3) : count;
+    if (t < head) __builtin_nontemporal_store(staged[t], dst + t);
+    const int body = (count - head) >> 2;
+    typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+    i32x4* dst4 = reinterpret_cast<i32x4*>(dst + head);
+    for (int q = t; q < body; q += kBlock) {
+      const int i = head + 4 * q;
+      i32x4 v = {staged[i], staged[i + 1], staged[i + 2], staged[i + 3]};
+      __builtin_nontemporal_store(v, dst4 + q);
+    }
+    for (int i = head + 4 * body + t; i < count; i += kBlock) __builtin_nontemporal_store(staged[i], dst + i);
   } else {
     for (int i = t; i < count; i += kBlock) dst[i] = staged[i];
   }
