@@ -158,6 +158,35 @@ def task_model_name(body: bytes) -> str | None:
 
 
 _native_name: Any = None
+_native_lists: Any = None
+
+
+def _lists():
+    global _native_lists
+    if _native_lists is None:
+        try:
+            from ..native import load
+            n = load()
+            _native_lists = (n.tasks_mark_overdue, n.tasks_overdue_filter)
+        except Exception:
+            _native_lists = False
+    return _native_lists
+
+
+def mark_overdue_wire(body: bytes) -> tuple[list[str], bytes] | None:
+    """``POST markoverdue`` body -> (task ids, the state API's bulk-save body with every task
+    ``isOverDue = true``), each TaskModel written like ``to_wire()``; ``None``: bind with
+    ``[TaskModel]`` (``native/src/taskcodec.hpp``)."""
+    fns = _lists()
+    return fns[0](body) if fns else None
+
+
+def overdue_filter_wire(body: bytes, run_day: str) -> tuple[int, int, bytes] | None:
+    """The cron job's filter over an overdue page: (tasks on the page, tasks due before
+    ``run_day`` (YYYY-MM-DD, UTC), those tasks as a TaskModel JSON array); ``None``: bind with
+    ``TaskModel`` and filter in Python."""
+    fns = _lists()
+    return fns[1](body, run_day) if fns else None
 
 
 def tasks_to_json(tasks: list[TaskModel]) -> bytes:

@@ -256,6 +256,30 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(py::bytes(u.data), py::str(u.content_type), attrs);
   });
 
+  // markoverdue body -> (ids, bulk-save body) or None (taskcodec.hpp mark_overdue).
+  m.def("tasks_mark_overdue", [](py::bytes body) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    std::vector<std::string> ids;
+    std::string bulk;
+    if (!taskcodec::mark_overdue(std::string_view(p, (size_t)n), ids, bulk)) return py::none();
+    py::list l(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) l[i] = py::str(ids[i]);
+    return py::make_tuple(l, py::bytes(bulk));
+  });
+
+  // overdue page + run date (YYYY-MM-DD) -> (retrieved, kept, TaskModel JSON array) or None.
+  m.def("tasks_overdue_filter", [](py::bytes body, const std::string& run_day) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    size_t retrieved = 0, kept = 0;
+    std::string out;
+    if (!taskcodec::overdue_filter(std::string_view(p, (size_t)n), run_day, retrieved, kept, out)) return py::none();
+    return py::make_tuple(retrieved, kept, py::bytes(out));
+  });
+
   // TaskModel JSON -> taskName when it binds within the codec's envelope, else None.
   m.def("task_model_name", [](py::bytes body) -> py::object {
     char* p;

@@ -360,4 +360,133 @@ inline bool task_model_name(std::string_view body, std::string& name) {
   return true;
 }
 
+// -------------------------------------------------------------------------------------------
+// Lists of TaskModels: the overdue sweep (Processor ScheduledTasksManagerController.cs:19-46 ->
+// API OverdueTasksController.cs:26-32 -> TasksStoreManager.MarkOverdueTasks).  A TaskModel object
+// that binds within the envelope of task_model_name() is written back canonically -- model
+// property order, Guid lower-case, DateTimes as System.Text.Json writes them, defaults for
+// missing properties -- the JSON of TaskModel.to_wire().
+
+inline bool task_fields(const tt::Value& doc, const tt::Value* (&f)[8]) {
+  if (doc.t != tt::Value::Object) return false;
+  static const char* names[8] = {"taskId", "taskName", "taskCreatedBy", "taskCreatedOn",
+                                 "taskDueDate", "taskAssignedTo", "isCompleted", "isOverDue"};
+  static const char* snake[8] = {"task_id", "task_name", "task_created_by", "task_created_on",
+                                 "task_due_date", "task_assigned_to", "is_completed", "is_over_due"};
+  for (auto& x : f) x = nullptr;
+  for (size_t k = 0; k < doc.keys.size(); ++k) {
+    const std::string& key = doc.keys[k];
+    int hit = -1;
+    for (int j = 0; j < 8; ++j)
+      if (key == names[j]) hit = j;
+    if (hit >= 0) {
+      if (f[hit] != nullptr) return false;
+      f[hit] = &doc.items[k];
+      continue;
+    }
+    const tt::Value& x = doc.items[k];
+    if (x.t != tt::Value::String && x.t != tt::Value::Bool && x.t != tt::Value::Null) return false;
+    std::string low(key);
+    for (char& c : low) c = (char)std::tolower((unsigned char)c);
+    for (int j = 0; j < 8; ++j) {
+      std::string ln(names[j]);
+      for (char& c : ln) c = (char)std::tolower((unsigned char)c);
+      if (key == snake[j] || low == ln) return false;
+    }
+  }
+  return true;
+}
+
+// Canonical TaskModel JSON of `doc` (isOverDue forced true when `overdue`); `due_day` receives
+// the due date's "YYYY-MM-DD".  false = outside the envelope.
+inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std::string& id, std::string& due_day) {
+  const tt::Value* f[8];
+  if (!task_fields(doc, f)) return false;
+  for (int j = 0; j < 6; ++j)
+    if (f[j] != nullptr && (f[j]->t != tt::Value::String || !valid_utf8(f[j]->s))) return false;
+  for (int j = 6; j < 8; ++j)
+    if (f[j] != nullptr && f[j]->t != tt::Value::Bool) return false;
+  id = f[0] ? f[0]->s : std::string("00000000-0000-0000-0000-000000000000");
+  if (!is_guid36(id)) return false;
+  for (char& c : id) c = (char)std::tolower((unsigned char)c);
+  std::string created = "0001-01-01T00:00:00", due = "0001-01-01T00:00:00";
+  if (f[3] && (created.clear(), !parse_due(f[3]->s, created))) return false;
+  if (f[4] && (due.clear(), !parse_due(f[4]->s, due))) return false;
+  due_day = due.substr(0, 10);
+  static const std::string empty;
+  out += "{\"taskId\":\"";
+  out += id;
+  out += "\",\"taskName\":";
+  tt::escape_to(out, f[1] ? std::string_view(f[1]->s) : std::string_view(empty));
+  out += ",\"taskCreatedBy\":";
+  tt::escape_to(out, f[2] ? std::string_view(f[2]->s) : std::string_view(empty));
+  out += ",\"taskCreatedOn\":\"";
+  out += created;
+  out += "\",\"taskDueDate\":\"";
+  out += due;
+  out += "\",\"taskAssignedTo\":";
+  tt::escape_to(out, f[5] ? std::string_view(f[5]->s) : std::string_view(empty));
+  out += ",\"isCompleted\":";
+  out += (f[6] && f[6]->b) ? "true" : "false";
+  out += ",\"isOverDue\":";
+  out += (overdue || (f[7] && f[7]->b)) ? "true" : "false";
+  out += '}';
+  return true;
+}
+
+inline bool parse_array(std::string_view body, tt::Value& doc) {
+  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  try {
+    doc = tt::parse(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  return doc.t == tt::Value::Array;
+}
+
+// POST api/overduetasks/markoverdue: the ids (for the per-task log lines) and the state API's
+// bulk-save body [{"key": id, "value": TaskModel with isOverDue = true}, ...].
+inline bool mark_overdue(std::string_view body, std::vector<std::string>& ids, std::string& bulk) {
+  tt::Value doc;
+  if (!parse_array(body, doc)) return false;
+  ids.clear();
+  bulk.assign("[");
+  std::string id, day;
+  for (size_t i = 0; i < doc.items.size(); ++i) {
+    if (i) bulk += ',';
+    bulk += "{\"key\":\"";
+    const size_t key_at = bulk.size();
+    bulk += "\",\"value\":";
+    if (!write_task(doc.items[i], true, bulk, id, day)) return false;
+    bulk += '}';
+    bulk.insert(key_at, id);
+    ids.push_back(id);
+  }
+  bulk += ']';
+  return true;
+}
+
+// The cron job's filter (ScheduledTasksManagerController.cs:31-36): of the API's overdue page,
+// the tasks whose due date is before the run's date (UTC), as a TaskModel JSON array; also the
+// page's size.
+inline bool overdue_filter(std::string_view body, std::string_view run_day, size_t& retrieved, size_t& kept,
+                           std::string& out) {
+  tt::Value doc;
+  if (!parse_array(body, doc) || run_day.size() != 10) return false;
+  retrieved = doc.items.size();
+  kept = 0;
+  out.assign("[");
+  std::string one, id, day;
+  for (const auto& item : doc.items) {
+    one.clear();
+    if (!write_task(item, false, one, id, day)) return false;
+    if (std::string_view(day) < run_day) {
+      if (kept++) out += ',';
+      out += one;
+    }
+  }
+  out += ']';
+  return true;
+}
+
 }  // namespace taskcodec

@@ -68,6 +68,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
         return _json(t.model_dump_json(by_alias=True).encode())
 
     fast_create = getattr(manager, "create_new_task_from_body", None)
+    fast_mark = getattr(manager, "mark_overdue_from_body", None)
 
     @app.route("/api/tasks", ("POST",), name="CreateTask", tag="Tasks", body=TaskAddModel, responses={201: None})
     async def post_task(req: Request) -> Response:
@@ -110,6 +111,9 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",
                body=[TaskModel], responses={200: None})
     async def mark_overdue(req: Request) -> Response:
+        ctype = req.content_type
+        if fast_mark is not None and (not ctype or "json" in ctype) and await fast_mark(req.body):
+            return empty(200)
         tasks = await read_model(req, [TaskModel])
         await manager.mark_overdue_tasks(tasks)
         return empty(200)

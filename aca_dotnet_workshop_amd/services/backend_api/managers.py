@@ -29,7 +29,7 @@ import random
 import uuid
 from datetime import datetime, timedelta
 
-from ...models import TaskModel, create_task_wire, format_fixed, naive_utc, today, utcnow
+from ...models import TaskModel, create_task_wire, format_fixed, mark_overdue_wire, naive_utc, today, utcnow
 from ...sdk.client import InvocationError, RawJson, SidecarClient
 
 log = logging.getLogger("TasksManager")
@@ -280,6 +280,21 @@ class TasksStoreManager(TasksManager):
              "page": {"limit": page}}
         resp = await self.client.query_state(self.store, q)
         return [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
+
+    async def mark_overdue_from_body(self, body: bytes) -> bool:
+        """``mark_overdue_tasks`` straight from the request body (``models.mark_overdue_wire``:
+        binding and the bulk-save body in one native pass); the same log line per task and one
+        bulk save.  False: the body needs the general binder (or the client has no raw save)."""
+        save_body = getattr(self.client, "save_state_body", None)
+        made = mark_overdue_wire(body) if save_body is not None else None
+        if made is None:
+            return False
+        ids, bulk = made
+        for tid in ids:
+            log.info("Mark task with Id: '%s' as OverDue task", tid)
+        if ids:
+            await save_body(self.store, bulk)
+        return True
 
     async def mark_overdue_tasks(self, tasks) -> None:
         items = []

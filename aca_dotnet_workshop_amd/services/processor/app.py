@@ -33,9 +33,9 @@ import logging
 import uuid
 from pathlib import Path
 
-from ...models import TaskModel, naive_utc, task_model_name, tasks_from_json, utcnow
+from ...models import TaskModel, naive_utc, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
-from ...sdk.client import InvocationError, client_from_config
+from ...sdk.client import InvocationError, RawJson, client_from_config
 from ...web.app import WebApp, read_model
 from ...web.http import Request, Response, empty, json_response, text_response
 from ..hosting import create_host, map_openapi, run_host
@@ -138,19 +138,30 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
         page = cfg.get_int("OverdueTasks:PageSize", 0)
         max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
         retrieved = marked = pages = 0
+        run_day = naive_utc(run_at).date().isoformat()
         while pages < max_pages:
             pages += 1
             path = "api/overduetasks" + (f"?limit={page}" if page > 0 else "")
-            tasks = tasks_from_json(await client.invoke_method("GET", api_app_id, path))
-            retrieved += len(tasks)
+            r = await client.invoke_method_raw("GET", api_app_id, path)
+            if r.status >= 300:
+                raise InvocationError(r.status, r.body, f"invoke {api_app_id}/{path}")
+            # the page bound and filtered in one native pass; any other shape binds with TaskModel
+            fast = overdue_filter_wire(r.body, run_day) if r.body else None
+            if fast is not None:
+                n_page, n_overdue, overdue = fast
+            else:
+                tasks = tasks_from_json(r.body or b"[]")
+                overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
+                n_page, n_overdue = len(tasks), len(overdue)
+            retrieved += n_page
             log_sched.info("ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d",
-                           len(tasks))
-            overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
-            if overdue:
-                log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", len(overdue))
-                await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", overdue)
-                marked += len(overdue)
-            if page <= 0 or len(tasks) < page or not overdue:
+                           n_page)
+            if n_overdue:
+                log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", n_overdue)
+                data = RawJson(overdue.decode()) if isinstance(overdue, bytes) else overdue
+                await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
+                marked += n_overdue
+            if page <= 0 or n_page < page or not n_overdue:
                 break
         return json_response({"runAt": run_at.isoformat(), "retrieved": retrieved, "markedOverdue": marked,
                               "pages": pages})

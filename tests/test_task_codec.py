@@ -234,3 +234,57 @@ def test_task_model_name_fuzz(fields):
     got = _native().task_model_name(body)
     if got is not None:
         assert got == _model_ref(body), body
+
+
+# ---------------------------------------------------------------------- the overdue sweep's lists
+def _binder_list(body: bytes):
+    try:
+        return [TaskModel.model_validate(x) for x in json.loads(body)]
+    except Exception:
+        return None
+
+
+def _check_lists(tasks_json: bytes, run_day: str) -> None:
+    from datetime import date
+
+    from aca_dotnet_workshop_amd.models import mark_overdue_wire, naive_utc, overdue_filter_wire
+    ref = _binder_list(tasks_json)
+    if not isinstance(json.loads(tasks_json), list):
+        ref = None
+    made = mark_overdue_wire(tasks_json)
+    if made is not None:
+        assert ref is not None, f"accepted a list the binder rejects: {tasks_json!r}"
+        want = [{"key": str(t.task_id), "value": {**t.to_wire(), "isOverDue": True}} for t in ref]
+        assert made[0] == [str(t.task_id) for t in ref] and json.loads(made[1]) == want
+    f = overdue_filter_wire(tasks_json, run_day)
+    if f is not None:
+        assert ref is not None
+        day = date.fromisoformat(run_day)
+        keep = [t.to_wire() for t in ref if day > naive_utc(t.task_due_date).date()]
+        assert f[0] == len(ref) and f[1] == len(keep) and json.loads(f[2]) == keep
+
+
+@pytest.mark.parametrize("tasks", [
+    [], [_TASK], [_TASK, {**_TASK, "taskId": "0F8FAD5B-D9CB-469F-A165-70867728950F", "taskDueDate": "2029-12-31Z"}],
+    [{"taskName": "defaults only"}], [{**_TASK, "isOverDue": True, "extra": "x"}],
+])
+def test_overdue_lists_match_binder(tasks):
+    body = json.dumps(tasks).encode()
+    for day in ("2030-01-02", "2030-01-03", "2000-01-01"):
+        _check_lists(body, day)
+    assert _native().tasks_mark_overdue(body) is not None
+
+
+@pytest.mark.parametrize("body", [b"{}", b"[1]", b'[{"TaskName":"x"}]', b'[{"taskId":"nope"}]', b'[{"isOverDue":"yes"}]',
+                                  json.dumps([_TASK, {**_TASK, "taskDueDate": "2030-02-30"}]).encode()])
+def test_overdue_lists_decline(body):
+    assert _native().tasks_mark_overdue(body) is None and _native().tasks_overdue_filter(body, "2030-01-01") is None
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.dictionaries(st.sampled_from(list(_TASK) + ["x"]),
+                                st.one_of(_text, st.booleans(), _date, st.uuids().map(str)), max_size=8), max_size=4),
+       st.dates().map(lambda d: d.isoformat()))
+def test_overdue_lists_fuzz(tasks, day):
+    _check_lists(json.dumps(tasks).encode(), day)
+    _check_lists(json.dumps(tasks, ensure_ascii=False).encode(), day)
