@@ -15,6 +15,7 @@ numbers by value; ranges only between like types), producing one bitmap per leaf
 """
 from __future__ import annotations
 
+import functools
 import json
 import os
 from dataclasses import dataclass
@@ -29,8 +30,10 @@ MAX_FLAT_LEAVES = 8   # leaves of a flat program (ops/hip/query_scan.hip kMaxFla
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
 
 
+@functools.lru_cache(maxsize=1)
 def cpu_share() -> int:
-    """CPUs this process may use: the cgroup quota (``cpu.max``) when set, else its affinity."""
+    """CPUs this process may use: the cgroup quota (``cpu.max``) when set, else its affinity
+    (read once per process)."""
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             quota, period = f.read().split()[:2]
