@@ -181,6 +181,22 @@ def mark_overdue_wire(body: bytes) -> tuple[list[str], bytes] | None:
     return fns[0](body) if fns else None
 
 
+def tasks_from_query_wire(body: bytes) -> tuple[int, bytes] | None:
+    """State-query response -> (tasks, TaskModel JSON array of the results with data, in order),
+    each written like ``to_wire()``; ``None``: bind the results with ``TaskModel``."""
+    global _native_query
+    if _native_query is None:
+        try:
+            from ..native import load
+            _native_query = load().tasks_from_query
+        except Exception:
+            _native_query = False
+    return _native_query(body) if _native_query else None
+
+
+_native_query: Any = None
+
+
 def overdue_filter_wire(body: bytes, run_day: str) -> tuple[int, int, bytes] | None:
     """The cron job's filter over an overdue page: (tasks on the page, tasks due before
     ``run_day`` (YYYY-MM-DD, UTC), those tasks as a TaskModel JSON array); ``None``: bind with

@@ -280,6 +280,17 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(retrieved, kept, py::bytes(out));
   });
 
+  // state-query response -> (task count, TaskModel JSON array) or None (taskcodec.hpp query_tasks).
+  m.def("tasks_from_query", [](py::bytes body) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    std::string out;
+    size_t count = 0;
+    if (!taskcodec::query_tasks(std::string_view(p, (size_t)n), out, count)) return py::none();
+    return py::make_tuple(count, py::bytes(out));
+  });
+
   // TaskModel JSON -> taskName when it binds within the codec's envelope, else None.
   m.def("task_model_name", [](py::bytes body) -> py::object {
     char* p;

@@ -489,4 +489,37 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
   return true;
 }
 
+// State-query response of the task collection (Dapr `{"results": [{"key", "data", "etag"}],
+// "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data, in order:
+// the API's GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).
+inline bool query_tasks(std::string_view body, std::string& out, size_t& count) {
+  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  if (doc.t != tt::Value::Object) return false;
+  const tt::Value* results = doc.get("results");
+  if (results == nullptr || results->t == tt::Value::Null) {
+    out = "[]";
+    count = 0;
+    return true;
+  }
+  if (results->t != tt::Value::Array) return false;
+  out.assign("[");
+  count = 0;
+  std::string id, day;
+  for (const auto& r : results->items) {
+    if (r.t != tt::Value::Object) return false;
+    const tt::Value* data = r.get("data");
+    if (data == nullptr || data->t == tt::Value::Null) continue;
+    if (count++) out += ',';
+    if (!write_task(*data, false, out, id, day)) return false;
+  }
+  out += ']';
+  return true;
+}
+
 }  // namespace taskcodec

@@ -272,8 +272,9 @@ class SidecarClient:
         if r.status >= 300:
             raise InvocationError(r.status, r.body, f"transaction {store}")
 
-    async def query_state(self, store: str, query: dict[str, Any] | str,
-                          metadata: dict[str, str] | None = None) -> QueryResponse:
+    async def query_state_raw(self, store: str, query: dict[str, Any] | str,
+                              metadata: dict[str, str] | None = None) -> bytes:
+        """The state-query API's response body as is (``{"results": [...], "token": ...}``)."""
         body = query.encode() if isinstance(query, str) else json.dumps(query).encode()
         path = f"/v1.0-alpha1/state/{store}/query"
         if metadata:
@@ -281,7 +282,12 @@ class SidecarClient:
         r = await self._call("POST", path, body, "application/json", span_name=f"state query {store}")
         if r.status >= 300:
             raise InvocationError(r.status, r.body, f"query state {store}")
-        js = r.json() or {}
+        return r.body
+
+    async def query_state(self, store: str, query: dict[str, Any] | str,
+                          metadata: dict[str, str] | None = None) -> QueryResponse:
+        raw = await self.query_state_raw(store, query, metadata)
+        js = json.loads(raw) if raw else {}
         items = [StateItem(x.get("key"), x.get("data"), x.get("etag")) for x in js.get("results") or []]
         return QueryResponse(items, js.get("token"), js.get("metadata") or {})
 

@@ -69,6 +69,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
 
     fast_create = getattr(manager, "create_new_task_from_body", None)
     fast_mark = getattr(manager, "mark_overdue_from_body", None)
+    fast_page = getattr(manager, "overdue_page_json", None)
 
     @app.route("/api/tasks", ("POST",), name="CreateTask", tag="Tasks", body=TaskAddModel, responses={201: None})
     async def post_task(req: Request) -> Response:
@@ -106,6 +107,10 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     async def get_overdue(req: Request) -> Response:
         raw = req.query_get("limit") or ""
         limit = int(raw) if raw.isdigit() else None  # page size of the range sweep (OverdueTasks:Query=range)
+        if fast_page is not None:
+            body = await fast_page(limit)
+            if body is not None:
+                return _json(body)
         return _json(tasks_to_json(await manager.get_yesterdays_due_tasks(limit)))
 
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",

@@ -24,12 +24,14 @@ trap of #7, publish-on-create and publish-on-assignee-change) is kept.
 from __future__ import annotations
 
 import abc
+import json
 import logging
 import random
 import uuid
 from datetime import datetime, timedelta
 
-from ...models import TaskModel, create_task_wire, format_fixed, mark_overdue_wire, naive_utc, today, utcnow
+from ...models import (TaskModel, create_task_wire, format_fixed, mark_overdue_wire, naive_utc, tasks_from_query_wire,
+                       today, utcnow)
 from ...sdk.client import InvocationError, RawJson, SidecarClient
 
 log = logging.getLogger("TasksManager")
@@ -266,18 +268,40 @@ class TasksStoreManager(TasksManager):
         tasks.sort(key=_created_key)
         return tasks
 
+    async def overdue_page_json(self, limit: int | None = None) -> bytes | None:
+        """``get_yesterdays_due_tasks`` as the response body, for the range sweep: the query
+        results turned into the TaskModel JSON array in one native pass
+        (``models.tasks_from_query_wire``).  ``None``: equality mode, or a response outside the
+        codec's envelope -- the caller binds the TaskModels."""
+        raw_query = getattr(self.client, "query_state_raw", None)
+        if self.overdue_query != "range" or raw_query is None:
+            return None
+        q, midnight, page = self._range_query(limit)
+        log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
+        raw = await raw_query(self.store, q)
+        made = tasks_from_query_wire(raw)
+        if made is not None:
+            return made[1]
+        results = (json.loads(raw) if raw else {}).get("results") or []
+        return ("[" + ",".join(TaskModel.model_validate(r["data"]).to_json() for r in results
+                               if r.get("data") is not None) + "]").encode()
+
+    def _range_query(self, limit: int | None) -> tuple[dict, str, int]:
+        midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
+        page = limit if limit and limit > 0 else self.overdue_page
+        q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
+                                {"EQ": {"isOverDue": False}}]},
+             "page": {"limit": page}}
+        return q, midnight, page
+
     async def _open_tasks_due_before_today(self, limit: int | None) -> list[TaskModel]:
         """``OverdueTasks:Query=range`` (SURVEY.md §2.12 #7 fixed): every open task due before
         today, whatever its time of day and however many daily runs were missed, filtered by
         the store rather than in the app -- a range leaf plus two boolean leaves, which the
         backing planner runs as a gfx950 columnar scan.  One page (oldest first) per call: the
         processor marks a page overdue and asks again, and marked tasks drop out of the filter."""
-        midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
-        page = limit if limit and limit > 0 else self.overdue_page
+        q, midnight, page = self._range_query(limit)
         log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
-        q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
-                                {"EQ": {"isOverDue": False}}]},
-             "page": {"limit": page}}
         resp = await self.client.query_state(self.store, q)
         return [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
 

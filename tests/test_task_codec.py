@@ -288,3 +288,20 @@ def test_overdue_lists_decline(body):
 def test_overdue_lists_fuzz(tasks, day):
     _check_lists(json.dumps(tasks).encode(), day)
     _check_lists(json.dumps(tasks, ensure_ascii=False).encode(), day)
+
+
+@pytest.mark.parametrize("results", [[], None, [{"key": "a", "data": _TASK, "etag": "1"}, {"key": "b", "data": None}],
+                                     [{"key": "c", "data": {**_TASK, "taskId": _TASK["taskId"].upper()}}]])
+def test_query_results_to_tasks(results):
+    from aca_dotnet_workshop_amd.models import tasks_from_query_wire
+    body = json.dumps({"results": results, "token": "100"}).encode()
+    made = tasks_from_query_wire(body)
+    want = [TaskModel.model_validate(r["data"]).to_wire() for r in results or [] if r.get("data") is not None]
+    assert made is not None and made[0] == len(want) and json.loads(made[1]) == want
+
+
+@pytest.mark.parametrize("body", [b"[]", b'{"results": 5}', b'{"results": [{"data": "text"}]}',
+                                  json.dumps({"results": [{"data": {"TaskName": "x"}}]}).encode()])
+def test_query_results_decline(body):
+    from aca_dotnet_workshop_amd.models import tasks_from_query_wire
+    assert tasks_from_query_wire(body) is None
