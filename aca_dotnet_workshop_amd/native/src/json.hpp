@@ -4,6 +4,8 @@
 // byte-for-byte through the query path.  Numbers are doubles (JSON semantics).
 #pragma once
 
+#include <emmintrin.h>
+
 #include <cctype>
 #include <cmath>
 #include <cstdio>
@@ -77,11 +79,16 @@ struct ParseError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// Recursive-descent parser that builds each value in place (no temporaries moved into the
+// parent's vectors), reserves small containers up front, finds the end of a string run 16 bytes
+// at a time (SSE2) and converts plain integers without strtod.  `strict`: raw control characters
+// inside strings are an error (Python's json.loads), which the task codecs need.
 class Parser {
  public:
-  explicit Parser(std::string_view s) : p_(s.data()), e_(s.data() + s.size()) {}
+  explicit Parser(std::string_view s, bool strict = false) : p_(s.data()), e_(s.data() + s.size()), strict_(strict) {}
   Value parse() {
-    Value v = value(0);
+    Value v;
+    value(v, 0);
     ws();
     if (p_ != e_) throw ParseError("trailing characters after JSON value");
     return v;
@@ -90,38 +97,61 @@ class Parser {
  private:
   const char* p_;
   const char* e_;
+  bool strict_;
 
   void ws() { while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_; }
   [[noreturn]] void fail(const char* m) { throw ParseError(m); }
 
-  Value value(int depth) {
+  void value(Value& v, int depth) {
     if (depth > 256) fail("JSON nesting too deep");
     ws();
     if (p_ >= e_) fail("unexpected end of JSON");
-    char c = *p_;
-    if (c == '{') return object(depth);
-    if (c == '[') return array(depth);
-    if (c == '"') { Value v; v.t = Value::String; v.s = str(); return v; }
-    if (c == 't') { lit("true"); return Value::boolean(true); }
-    if (c == 'f') { lit("false"); return Value::boolean(false); }
-    if (c == 'n') { lit("null"); return Value(); }
-    return num();
+    switch (*p_) {
+      case '{': object(v, depth); return;
+      case '[': array(v, depth); return;
+      case '"': v.t = Value::String; str(v.s); return;
+      case 't': lit("true", 4); v.t = Value::Bool; v.b = true; return;
+      case 'f': lit("false", 5); v.t = Value::Bool; v.b = false; return;
+      case 'n': lit("null", 4); return;
+      default: num(v);
+    }
   }
-  void lit(const char* w) {
-    size_t n = std::strlen(w);
+  void lit(const char* w, size_t n) {
     if ((size_t)(e_ - p_) < n || std::memcmp(p_, w, n) != 0) fail("invalid literal");
     p_ += n;
   }
-  Value num() {
+  // The token is the longest run of [0-9.eE+-] after an optional sign, and must be a complete
+  // strtod number; up to 15 plain digits are exact as an integer conversion.
+  void num(Value& v) {
     const char* s = p_;
     if (p_ < e_ && (*p_ == '-' || *p_ == '+')) ++p_;
+    const char* d0 = p_;
+    while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
+    const char* d1 = p_;
     while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' || *p_ == '-' || *p_ == '+')) ++p_;
     if (p_ == s) fail("invalid JSON token");
-    std::string tmp(s, p_);
+    v.t = Value::Number;
+    if (p_ == d1 && d1 > d0 && d1 - d0 <= 15) {
+      int64_t x = 0;
+      for (const char* q = d0; q < d1; ++q) x = x * 10 + (*q - '0');
+      v.n = *s == '-' ? -(double)x : (double)x;
+      return;
+    }
+    char buf[64];
+    std::string big;
+    const size_t n = (size_t)(p_ - s);
+    const char* c;
+    if (n < sizeof buf) {
+      std::memcpy(buf, s, n);
+      buf[n] = 0;
+      c = buf;
+    } else {
+      big.assign(s, n);
+      c = big.c_str();
+    }
     char* end = nullptr;
-    double d = std::strtod(tmp.c_str(), &end);
-    if (end != tmp.c_str() + tmp.size()) fail("invalid number");
-    return Value::number(d);
+    v.n = std::strtod(c, &end);
+    if (end != c + n) fail("invalid number");
   }
   static void utf8(std::string& out, uint32_t cp) {
     if (cp < 0x80) out += (char)cp;
@@ -142,83 +172,102 @@ class Parser {
     }
     return v;
   }
-  std::string str() {
+  // First '"' or '\\' (strict: or control character) at or after p, else e.
+  const char* stop(const char* p) const {
+    const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), ctl = _mm_set1_epi8(0x1F);
+    while (e_ - p >= 16) {
+      __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+      __m128i hit = _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs));
+      if (strict_) hit = _mm_or_si128(hit, _mm_cmpeq_epi8(_mm_max_epu8(x, ctl), ctl));
+      int m = _mm_movemask_epi8(hit);
+      if (m) return p + __builtin_ctz((unsigned)m);
+      p += 16;
+    }
+    while (p < e_ && *p != '"' && *p != '\\' && !(strict_ && (unsigned char)*p < 0x20)) ++p;
+    return p;
+  }
+  void str(std::string& out) {
     ++p_;  // opening quote
-    std::string out;
     const char* run = p_;
     while (true) {
+      p_ = stop(p_);
       if (p_ >= e_) fail("unterminated string");
       char c = *p_;
-      if (c == '"') { out.append(run, p_); ++p_; return out; }
-      if (c == '\\') {
-        out.append(run, p_);
-        ++p_;
-        if (p_ >= e_) fail("bad escape");
-        char x = *p_++;
-        switch (x) {
-          case '"': out += '"'; break;
-          case '\\': out += '\\'; break;
-          case '/': out += '/'; break;
-          case 'b': out += '\b'; break;
-          case 'f': out += '\f'; break;
-          case 'n': out += '\n'; break;
-          case 'r': out += '\r'; break;
-          case 't': out += '\t'; break;
-          case 'u': {
-            uint32_t cp = hex4();
-            if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
-              p_ += 2;
-              uint32_t lo = hex4();
-              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-            }
-            utf8(out, cp);
-            break;
-          }
-          default: fail("bad escape");
-        }
-        run = p_;
-        continue;
-      }
+      if (c == '"') { out.append(run, p_); ++p_; return; }
+      if (c != '\\') fail("control character in string");
+      out.append(run, p_);
       ++p_;
+      if (p_ >= e_) fail("bad escape");
+      char x = *p_++;
+      switch (x) {
+        case '"': out += '"'; break;
+        case '\\': out += '\\'; break;
+        case '/': out += '/'; break;
+        case 'b': out += '\b'; break;
+        case 'f': out += '\f'; break;
+        case 'n': out += '\n'; break;
+        case 'r': out += '\r'; break;
+        case 't': out += '\t'; break;
+        case 'u': {
+          uint32_t cp = hex4();
+          if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+            p_ += 2;
+            uint32_t lo = hex4();
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          }
+          utf8(out, cp);
+          break;
+        }
+        default: fail("bad escape");
+      }
+      run = p_;
     }
   }
-  Value array(int depth) {
+  void array(Value& v, int depth) {
     ++p_;
-    Value v; v.t = Value::Array;
+    v.t = Value::Array;
     ws();
-    if (p_ < e_ && *p_ == ']') { ++p_; return v; }
+    if (p_ < e_ && *p_ == ']') { ++p_; return; }
+    v.items.reserve(4);
     while (true) {
-      v.items.push_back(value(depth + 1));
+      v.items.emplace_back();
+      value(v.items.back(), depth + 1);
       ws();
       if (p_ >= e_) fail("unterminated array");
       if (*p_ == ',') { ++p_; continue; }
-      if (*p_ == ']') { ++p_; return v; }
+      if (*p_ == ']') { ++p_; return; }
       fail("expected , or ]");
     }
   }
-  Value object(int depth) {
+  void object(Value& v, int depth) {
     ++p_;
-    Value v; v.t = Value::Object;
+    v.t = Value::Object;
     ws();
-    if (p_ < e_ && *p_ == '}') { ++p_; return v; }
+    if (p_ < e_ && *p_ == '}') { ++p_; return; }
+    v.keys.reserve(8);
+    v.items.reserve(8);
     while (true) {
       ws();
       if (p_ >= e_ || *p_ != '"') fail("expected object key");
-      v.keys.push_back(str());
+      v.keys.emplace_back();
+      str(v.keys.back());
       ws();
       if (p_ >= e_ || *p_ != ':') fail("expected :");
       ++p_;
-      v.items.push_back(value(depth + 1));
+      v.items.emplace_back();
+      value(v.items.back(), depth + 1);
       ws();
       if (p_ >= e_) fail("unterminated object");
       if (*p_ == ',') { ++p_; continue; }
-      if (*p_ == '}') { ++p_; return v; }
+      if (*p_ == '}') { ++p_; return; }
       fail("expected , or }");
     }
   }
 };
 
 inline Value parse(std::string_view s) { return Parser(s).parse(); }
+// json.loads' strictness: raw control characters inside strings are rejected.
+inline Value parse_strict(std::string_view s) { return Parser(s, true).parse(); }
 
 inline void escape_to(std::string& out, std::string_view s) {
   out += '"';

@@ -46,7 +46,16 @@ inline bool valid_utf8(std::string_view s) {
   const unsigned char* e = p + s.size();
   while (p < e) {
     unsigned char c = *p;
-    if (c < 0x80) { ++p; continue; }
+    if (c < 0x80) {
+      ++p;
+      while (e - p >= 8) {  // ASCII runs 8 bytes at a time
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        if (w & 0x8080808080808080ull) break;
+        p += 8;
+      }
+      continue;
+    }
     int n;
     uint32_t cp;
     if ((c & 0xE0) == 0xC0) { n = 1; cp = c & 0x1F; if (c < 0xC2) return false; }
@@ -162,7 +171,7 @@ inline bool parse_due(std::string_view v, std::string& out) {
   return true;
 }
 
-// json.loads (strict) rejects raw control characters inside strings; tt::Parser does not.
+// json.loads (strict) rejects raw control characters inside strings (tt::parse_strict does too).
 inline bool no_raw_controls_in_strings(std::string_view s) {
   bool in = false;
   for (size_t i = 0; i < s.size(); ++i) {
@@ -176,10 +185,10 @@ inline bool no_raw_controls_in_strings(std::string_view s) {
 }
 
 inline bool create(std::string_view body, Entropy& rng, Created& out) {
-  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  if (!valid_utf8(body)) return false;
   tt::Value doc;
   try {
-    doc = tt::parse(body);
+    doc = tt::parse_strict(body);
   } catch (const tt::ParseError&) {
     return false;
   }
@@ -270,9 +279,9 @@ inline bool has_number(const tt::Value& v) {
 }
 
 inline bool unwrap_cloudevent(std::string_view body, Unwrapped& out) {
-  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  if (!valid_utf8(body)) return false;
   try {
-    out.doc = tt::parse(body);
+    out.doc = tt::parse_strict(body);
   } catch (const tt::ParseError&) {
     return false;
   }
@@ -314,10 +323,10 @@ inline bool is_guid36(const std::string& s) {
 // TasksNotifierController.cs:26): the taskName when the object binds within the envelope of
 // create(); false = the general binder decides (and produces any 400).
 inline bool task_model_name(std::string_view body, std::string& name) {
-  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  if (!valid_utf8(body)) return false;
   tt::Value doc;
   try {
-    doc = tt::parse(body);
+    doc = tt::parse_strict(body);
   } catch (const tt::ParseError&) {
     return false;
   }
@@ -435,9 +444,9 @@ inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std
 }
 
 inline bool parse_array(std::string_view body, tt::Value& doc) {
-  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  if (!valid_utf8(body)) return false;
   try {
-    doc = tt::parse(body);
+    doc = tt::parse_strict(body);
   } catch (const tt::ParseError&) {
     return false;
   }
@@ -493,10 +502,10 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
 // "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data, in order:
 // the API's GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).
 inline bool query_tasks(std::string_view body, std::string& out, size_t& count) {
-  if (!valid_utf8(body) || !no_raw_controls_in_strings(body)) return false;
+  if (!valid_utf8(body)) return false;
   tt::Value doc;
   try {
-    doc = tt::parse(body);
+    doc = tt::parse_strict(body);
   } catch (const tt::ParseError&) {
     return false;
   }
