@@ -32,6 +32,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_set_eval_nt.restype = ctypes.c_int
     lib.tt_set_compact_nt.argtypes = [ctypes.c_int]
     lib.tt_set_compact_nt.restype = ctypes.c_int
+    lib.tt_set_compact_mode.argtypes = [ctypes.c_int]
+    lib.tt_set_compact_mode.restype = ctypes.c_int
     lib.tt_set_flat_grid.argtypes = [I64]
     lib.tt_set_flat_grid.restype = ctypes.c_int
     lib.tt_sort_pairs_temp_bytes.argtypes = [I64, I32]
@@ -98,6 +100,12 @@ class GpuKernels:
         """Non-temporal stores for the compacted row ids (default on; A/B)."""
         self.lib.tt_set_compact_nt(1 if on else 0)
 
+    def set_compact_mode(self, mode: int) -> None:
+        """1: tile offsets in one block + wave-independent compaction (default); 0: chunk sums +
+        wave 0 of each block finds the block's offset (A/B)."""
+        if self.lib.tt_set_compact_mode(int(mode)) != 0:
+            raise ValueError("compaction mode must be 0 or 1")
+
     def set_eval_nt(self, on: bool) -> None:
         """Non-temporal column loads in ``tt_scan_eval`` (default off; A/B)."""
         self.lib.tt_set_eval_nt(1 if on else 0)
@@ -152,14 +160,14 @@ class GpuKernels:
                                               counts.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
-        # per-64-tile chunk counts (tt_chunk_sums), then the compaction finds each tile's offset
-        # from them and writes the total straight into pinned host memory: no full scan, no
-        # torch launches, no host sync between the kernels -- one event wait at the end
+        # the tiles' output offsets in one block (tt_tile_offsets, which also writes the total
+        # straight into pinned host memory), then the wave-independent compaction: no torch
+        # launches, no host sync between the kernels -- one event wait at the end
         out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
-        scratch = torch.empty((tiles + self.chunk_tiles - 1) // self.chunk_tiles + 1, dtype=torch.int64,
-                              device=self.device)  # [0] = total (int64), then int32 chunk counts
+        # [0] = total (int64), [2:] = 16-byte aligned int32 tile offsets (mode 0: chunk counts)
+        scratch = torch.empty(tiles // 2 + 3, dtype=torch.int64, device=self.device)
         pinned = self._pinned()
-        rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[1:].data_ptr(), nrows,
+        rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[2:].data_ptr(), nrows,
                                              out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
         if rc != 0:
             raise RuntimeError(f"tt_scan_compact launch failed ({rc})")

@@ -570,6 +570,137 @@ tt_scan_compact_t(const uint32_t* __restrict__ mask32,      // selection mask vi
 }
 
 // ---------------------------------------------------------------------------------------
+// Wave-independent compaction (default).  tt_tile_offsets turns the per-tile counts into
+// exclusive output offsets in ONE block (1024 threads x 16 tiles per pass with 16-byte loads and
+// stores: 1e8 rows = 12.2k tiles is one pass) and publishes the total; tt_scan_compact_w then
+// needs no block-level step: each wave of a tile owns 2048 rows, finds its base as
+// tile_off[tile] + the popcounts of the preceding waves' mask words (L1 hits: the sibling waves
+// load the same words), stages its ids in its own LDS slice and writes its segment with 16-byte
+// stores.  No __syncthreads and no dependent chain through wave 0 (tt_scan_compact_t: one wave
+// sums up to ~190 chunk counts while the other three wait at a barrier).
+constexpr int kOffBlock = 1024;
+constexpr int kOffPer = 16;
+
+extern "C" __global__ void __launch_bounds__(kOffBlock)
+tt_tile_offsets(const int32_t* __restrict__ block_counts, int64_t tiles, int32_t* __restrict__ tile_off,
+                int64_t* __restrict__ total, int64_t* total_host) {
+  typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+  __shared__ int32_t wsum[kOffBlock / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < tiles; base += (int64_t)kOffBlock * kOffPer) {
+    const int64_t i0 = base + (int64_t)t * kOffPer;
+    const bool full = i0 + kOffPer <= tiles;  // i0 is a multiple of 16: 64-byte aligned
+    int32_t v[kOffPer];
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kOffPer / 4; ++q) {
+        const i32x4 x = reinterpret_cast<const i32x4*>(block_counts + i0)[q];
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kOffPer; ++k) v[k] = i0 + k < tiles ? block_counts[i0 + k] : 0;
+    }
+    int32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kOffPer; ++k) s += v[k];
+    int32_t incl = s;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int32_t y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kOffBlock / 64; ++w) {
+      const int32_t x = wsum[w];
+      before += w < wave ? x : 0;
+      all += x;
+    }
+    int32_t o[kOffPer];
+    int32_t run = (int32_t)carry + before + incl - s;  // ids are int32: every offset < 2^31
+#pragma unroll
+    for (int k = 0; k < kOffPer; ++k) {
+      o[k] = run;
+      run += v[k];
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kOffPer / 4; ++q)
+        reinterpret_cast<i32x4*>(tile_off + i0)[q] = i32x4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < kOffPer; ++k)
+        if (i0 + k < tiles) tile_off[i0 + k] = o[k];
+    }
+    carry += all;
+    __syncthreads();  // wsum is rewritten by the next pass
+  }
+  if (t == 0) {
+    *total = carry;
+    if (total_host) {
+      __hip_atomic_store(total_host, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
+  }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(kBlock)
+tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict__ tile_off,
+                  int32_t* __restrict__ out) {
+  __shared__ int32_t staged[kBlock / 64][64 * 32];  // one 2048-id slice per wave
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t tile = blockIdx.x;
+  const uint32_t* m = mask32 + tile * kBlock;
+  const int32_t tbase = tile_off[tile];
+  const uint32_t bits = m[t];
+  int32_t before = 0;  // selected rows of the tile's preceding waves
+  for (int w = 0; w < wave; ++w) before += __popc(m[w * 64 + lane]);
+  for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off, 64);
+  const int32_t cnt = __popc(bits);
+  int32_t incl = cnt;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  const int32_t count = __shfl(incl, 63, 64);
+  int32_t* st = staged[wave];
+  int32_t pos = incl - cnt;
+  const int32_t row_base = (int32_t)(tile * kTileRows) + t * 32;
+  uint32_t b = bits;
+  while (b) {
+    const int k = __ffs(b) - 1;
+    st[pos++] = row_base + k;
+    b &= b - 1;
+  }
+  // the slice is read back by other lanes of the same wave only
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int64_t a = (int64_t)tbase + before;
+  int32_t* dst = out + a;
+  int head = (int)((4 - (a & 3)) & 3);
+  if (head > count) head = count;
+  const int body = (count - head) >> 2;
+  if constexpr (NT) {
+    if (lane < head) __builtin_nontemporal_store(st[lane], dst + lane);
+    typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+    i32x4* dst4 = reinterpret_cast<i32x4*>(dst + head);
+    for (int q = lane; q < body; q += 64) {
+      const int i = head + 4 * q;
+      i32x4 v = {st[i], st[i + 1], st[i + 2], st[i + 3]};
+      __builtin_nontemporal_store(v, dst4 + q);
+    }
+    for (int i = head + 4 * body + lane; i < count; i += 64) __builtin_nontemporal_store(st[i], dst + i);
+  } else {
+    for (int i = lane; i < count; i += 64) dst[i] = st[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // tt_scan_select: filter evaluation + order-preserving compaction in ONE pass (no selection
 // mask round trip through HBM, no separate scan of tile counts, no host sync in between).
 // Tiles are claimed through an atomic ticket, so every tile's predecessors have already
@@ -887,13 +1018,34 @@ extern "C" int tt_set_compact_nt(int on) {
   return 0;
 }
 
-// `chunk_sums`: scratch for ceil(tiles / 64) int32; `out` holds up to nrows ids; the selected
-// count lands in `total` (device) and `total_host` (pinned host memory, optional).
+// Compaction variant (A/B): 1 = tt_tile_offsets + tt_scan_compact_w (default), 0 = chunk sums +
+// tt_scan_compact_t (wave 0 of each block finds the block's offset).
+static int g_compact_mode = 1;
+extern "C" int tt_set_compact_mode(int mode) {
+  if (mode != 0 && mode != 1) return 1;
+  g_compact_mode = mode;
+  return 0;
+}
+
+// `chunk_sums`: 16-byte aligned scratch for `tiles` int32 (mode 1: the tiles' output offsets;
+// mode 0: the ceil(tiles / 64) chunk counts); `out` holds up to nrows ids; the selected count
+// lands in `total` (device) and `total_host` (pinned host memory, optional).
 extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int32_t* block_counts, int32_t* chunk_sums,
                                       int64_t nrows, int32_t* out, int64_t* total, int64_t* total_host,
                                       hipStream_t stream) {
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
+  if (g_compact_mode == 1) {  // tile offsets in one block, then wave-independent compaction
+    hipLaunchKernelGGL(tt_tile_offsets, dim3(1), dim3(kOffBlock), 0, stream, block_counts, tiles, chunk_sums, total,
+                       total_host);
+    if (g_compact_nt)
+      hipLaunchKernelGGL(tt_scan_compact_w<true>, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
+                         reinterpret_cast<const uint32_t*>(mask), chunk_sums, out);
+    else
+      hipLaunchKernelGGL(tt_scan_compact_w<false>, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
+                         reinterpret_cast<const uint32_t*>(mask), chunk_sums, out);
+    return (int)hipGetLastError();
+  }
   const int64_t nchunks = (tiles + (1 << kChunkShift) - 1) >> kChunkShift;
   hipLaunchKernelGGL(tt_chunk_sums, dim3((unsigned)((nchunks + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0,
                      stream, block_counts, tiles, chunk_sums);

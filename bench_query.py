@@ -36,6 +36,8 @@ def main() -> None:
     ap.add_argument("--flat-grid", type=int, default=None, help="tt_scan_flat workgroups (0 = one per tile)")
     ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4/8; 0 = default)")
     ap.add_argument("--compact-nt", type=int, default=1, help="non-temporal stores for the compacted row ids (1/0)")
+    ap.add_argument("--compact-mode", type=int, default=1,
+                    help="1: wave-independent compaction, 0: per-block offsets found by wave 0")
     ap.add_argument("--eval-nt", type=int, default=0, help="non-temporal column loads in the scan (1/0)")
     ap.add_argument("--sorted", action="store_true",
                     help="also time ORDER BY taskDueDate DESC: top-100 page and full ordering (tt_sort_keys + sort)")
@@ -78,6 +80,7 @@ def main() -> None:
     if a.eval_groups:
         k.set_eval_groups(a.eval_groups)
     k.set_compact_nt(bool(a.compact_nt))
+    k.set_compact_mode(a.compact_mode)
     k.set_eval_nt(bool(a.eval_nt))
     if a.flat_grid is not None:
         k.set_flat_grid(a.flat_grid)
@@ -123,7 +126,7 @@ def main() -> None:
            "single_pass_matches": same, "flat_kernel": flat is not None,
            "flat_ms": round(flat_dt * 1e3, 4) if flat_dt else None, "flat_matches_interpreter": flat_matches,
            "eval_groups": a.eval_groups or 2, "flat_grid": a.flat_grid, "column_bytes_per_row": widths,
-           "compact_nt": bool(a.compact_nt), "eval_nt": bool(a.eval_nt),
+           "compact_nt": bool(a.compact_nt), "compact_mode": a.compact_mode, "eval_nt": bool(a.eval_nt),
            "range_leaves": int((prog.code[:, 0] == 7).sum())}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order

@@ -273,12 +273,14 @@ def test_gpu_scan_matches_numpy(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tiles", [1, 63, 64, 65, 1025, 12_207])
-def test_gpu_compaction_offsets_over_many_chunks(tiles):
-    """tt_chunk_sums + tt_scan_compact: each compaction block finds its tile's output offset from
-    the per-64-tile chunk counts (plus the preceding tiles of its chunk) and block 0 publishes the
-    total to device and pinned host memory -- on a synthetic selection mask far larger than the
-    other tests' collections (12,207 tiles = 1e8 rows)."""
+@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("tiles", [1, 63, 64, 65, 1025, 12_207, 16_385])
+def test_gpu_compaction_offsets_over_many_chunks(tiles, mode):
+    """Both compaction variants on a synthetic selection mask far larger than the other tests'
+    collections (12,207 tiles = 1e8 rows; 16,385 = one past the offset kernel's first pass, with
+    a partial 16-tile group): mode 1 -- tt_tile_offsets (exclusive offsets of all tiles in one
+    block, total to device and pinned host memory) + tt_scan_compact_w (every wave finds its own
+    base); mode 0 -- tt_chunk_sums + tt_scan_compact_t (wave 0 finds the block's offset)."""
     import torch
     k = _kernels()
     g = torch.Generator().manual_seed(tiles)
@@ -288,20 +290,28 @@ def test_gpu_compaction_offsets_over_many_chunks(tiles):
     words = (bits.view(-1, 16).to(torch.int32) << torch.arange(16)).sum(1).to(torch.int16)  # row r -> bit r % 16
     mask, counts_d = words.to(k.device), counts.to(k.device)
     nchunks = (tiles + k.chunk_tiles - 1) // k.chunk_tiles
-    chunk = torch.full((nchunks,), -1, dtype=torch.int32, device=k.device)
+    scratch = torch.full((tiles,), -1, dtype=torch.int32, device=k.device)
     nrows = tiles * 8192
     out = torch.empty(nrows, dtype=torch.int32, device=k.device)
     total = torch.empty(1, dtype=torch.int64, device=k.device)
     pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-    assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), chunk.data_ptr(), nrows,
-                                        out.data_ptr(), total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
-    torch.cuda.synchronize()
+    k.set_compact_mode(mode)
+    try:
+        assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
+                                            out.data_ptr(), total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
+        torch.cuda.synchronize()
+    finally:
+        k.set_compact_mode(1)
     want = torch.nonzero(bits.view(-1)).view(-1).to(torch.int32)
     n = int(total.item())
     assert n == want.numel() == int(pinned[0])
     assert torch.equal(out[:n].cpu(), want)
-    ref = torch.nn.functional.pad(counts, (0, nchunks * k.chunk_tiles - tiles)).view(nchunks, -1).sum(1)
-    assert torch.equal(chunk.cpu(), ref.to(torch.int32))
+    if mode == 1:
+        ref = torch.cumsum(counts.to(torch.int64), 0) - counts
+        assert torch.equal(scratch.cpu(), ref.to(torch.int32))
+    else:
+        ref = torch.nn.functional.pad(counts, (0, nchunks * k.chunk_tiles - tiles)).view(nchunks, -1).sum(1)
+        assert torch.equal(scratch[:nchunks].cpu(), ref.to(torch.int32))
 
 
 @pytest.mark.gpu
