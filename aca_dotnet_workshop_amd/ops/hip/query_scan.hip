@@ -651,7 +651,7 @@ template <bool NT>
 __global__ void __launch_bounds__(kBlock)
 tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict__ tile_off,
                   int32_t* __restrict__ out) {
-  __shared__ int32_t staged[kBlock / 64][64 * 32];  // one 2048-id slice per wave
+  __shared__ uint16_t staged[kBlock / 64][64 * 32];  // one slice per wave: row - wave_base (11 bits)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t tile = blockIdx.x;
   const uint32_t* m = mask32 + tile * kBlock;
@@ -667,13 +667,14 @@ tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict
     if (lane >= off) incl += y;
   }
   const int32_t count = __shfl(incl, 63, 64);
-  int32_t* st = staged[wave];
+  uint16_t* st = staged[wave];
   int32_t pos = incl - cnt;
-  const int32_t row_base = (int32_t)(tile * kTileRows) + t * 32;
+  const int32_t wave_base = (int32_t)(tile * kTileRows) + wave * 2048;
+  const int lane_base = lane * 32;
   uint32_t b = bits;
   while (b) {
     const int k = __ffs(b) - 1;
-    st[pos++] = row_base + k;
+    st[pos++] = (uint16_t)(lane_base + k);
     b &= b - 1;
   }
   // the slice is read back by other lanes of the same wave only
@@ -686,17 +687,17 @@ tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict
   if (head > count) head = count;
   const int body = (count - head) >> 2;
   if constexpr (NT) {
-    if (lane < head) __builtin_nontemporal_store(st[lane], dst + lane);
+    if (lane < head) __builtin_nontemporal_store(wave_base + st[lane], dst + lane);
     typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
     i32x4* dst4 = reinterpret_cast<i32x4*>(dst + head);
     for (int q = lane; q < body; q += 64) {
       const int i = head + 4 * q;
-      i32x4 v = {st[i], st[i + 1], st[i + 2], st[i + 3]};
+      i32x4 v = {wave_base + st[i], wave_base + st[i + 1], wave_base + st[i + 2], wave_base + st[i + 3]};
       __builtin_nontemporal_store(v, dst4 + q);
     }
-    for (int i = head + 4 * body + lane; i < count; i += 64) __builtin_nontemporal_store(st[i], dst + i);
+    for (int i = head + 4 * body + lane; i < count; i += 64) __builtin_nontemporal_store(wave_base + st[i], dst + i);
   } else {
-    for (int i = lane; i < count; i += 64) dst[i] = st[i];
+    for (int i = lane; i < count; i += 64) dst[i] = wave_base + st[i];
   }
 }
 
