@@ -126,35 +126,7 @@ const char* skip_value(const char* p, const char* e) {
   return p;
 }
 
-// Copy a validated JSON text without insignificant whitespace.
-std::string compact(std::string_view s) {
-  std::string o;
-  o.reserve(s.size());
-  bool in_str = false;
-  for (size_t i = 0; i < s.size(); ++i) {
-    char c = s[i];
-    if (in_str) {
-      o += c;
-      if (c == '\\' && i + 1 < s.size()) o += s[++i];
-      else if (c == '"') in_str = false;
-    } else if (c == '"') {
-      in_str = true;
-      o += c;
-    } else if (c != ' ' && c != '\n' && c != '\r' && c != '\t') {
-      o += c;
-    }
-  }
-  return o;
-}
-
-bool valid_json(std::string_view s) {
-  try {
-    Parser(s).parse();
-    return true;
-  } catch (const std::exception&) {
-    return false;
-  }
-}
+bool valid_json(std::string_view s) { return tt::valid(s); }  // compact(): tt::compact
 
 std::string errno_text(int e) {
   switch (e) {
@@ -173,11 +145,25 @@ const std::string* opt_str(const Value& cfg, const char* k) {
 }
 
 // ------------------------------------------------------------------------------ tracing
+void hex16(uint64_t v, char* out) {  // 16 lowercase hex digits, no terminator
+  static const char* d = "0123456789abcdef";
+  for (int i = 15; i >= 0; --i, v >>= 4) out[i] = d[v & 15];
+}
+
+// Span ids in fixed buffers: starting a span (every natively handled request) allocates nothing.
 struct SpanCtx {
-  std::string trace_id, span_id, parent_id;
-  bool sampled = false;
+  char trace_id[32], span_id[16], parent_id[16];
+  bool has_parent = false, sampled = false;
   double start_wall = 0, t0 = 0;
-  std::string traceparent() const { return "00-" + trace_id + "-" + span_id + (sampled ? "-01" : "-00"); }
+  std::string_view tid() const { return {trace_id, 32}; }
+  std::string_view sid() const { return {span_id, 16}; }
+  std::string_view pid() const { return {parent_id, 16}; }
+  std::string traceparent() const {
+    std::string s;
+    s.reserve(55);
+    s.append("00-", 3).append(trace_id, 32).append(1, '-').append(span_id, 16).append(sampled ? "-01" : "-00", 3);
+    return s;
+  }
 };
 
 bool parse_traceparent(const std::string* v, SpanCtx& out) {
@@ -185,16 +171,21 @@ bool parse_traceparent(const std::string* v, SpanCtx& out) {
   std::string_view s(*v);
   // 00-<32 hex>-<16 hex>-<2 hex>
   if (s.size() < 55 || s[2] != '-' || s[35] != '-' || s[52] != '-') return false;
-  std::string_view tid = s.substr(3, 32), pid = s.substr(36, 16);
-  if (tid == std::string(32, '0') || pid == std::string(16, '0')) return false;
-  for (char c : tid)
-    if (hexv(c) < 0) return false;
-  for (char c : pid)
-    if (hexv(c) < 0) return false;
+  bool tz = true, pz = true;
+  for (size_t i = 3; i < 35; ++i) {
+    if (hexv(s[i]) < 0) return false;
+    tz = tz && s[i] == '0';
+  }
+  for (size_t i = 36; i < 52; ++i) {
+    if (hexv(s[i]) < 0) return false;
+    pz = pz && s[i] == '0';
+  }
+  if (tz || pz) return false;
   int f1 = hexv(s[53]), f2 = hexv(s[54]);
   if (f1 < 0 || f2 < 0) return false;
-  out.trace_id = std::string(tid);
-  out.parent_id = std::string(pid);
+  std::memcpy(out.trace_id, s.data() + 3, 32);
+  std::memcpy(out.parent_id, s.data() + 36, 16);
+  out.has_parent = true;
   out.sampled = ((f1 * 16 + f2) & 1) != 0;
   return true;
 }
@@ -220,12 +211,13 @@ class Tracer {
   SpanCtx start(const std::string* traceparent) {
     SpanCtx s;
     if (!parse_traceparent(traceparent, s)) {
-      s.trace_id = hex_u64(rng()()) + hex_u64(rng()());
-      s.parent_id.clear();
+      hex16(rng()(), s.trace_id);
+      hex16(rng()(), s.trace_id + 16);
+      s.has_parent = false;
       s.sampled = rate_ >= 1.0 || std::uniform_real_distribution<double>(0, 1)(rng()) < rate_;
     }
-    s.span_id = hex_u64(rng()());
-    s.start_wall = wall_now();
+    hex16(rng()(), s.span_id);
+    if (s.sampled) s.start_wall = wall_now();  // only recorded spans carry a timestamp
     s.t0 = ev::now_s();
     return s;
   }
@@ -236,9 +228,9 @@ class Tracer {
     char ts[32];
     std::snprintf(ts, sizeof ts, "%.6f", s.start_wall);
     std::string l = "{\"type\":\"span\",\"role\":" + json_str(role_) + ",\"instance\":" + json_str(instance_) +
-                    ",\"name\":" + json_str(name) + ",\"kind\":\"server\",\"traceId\":\"" + s.trace_id +
-                    "\",\"spanId\":\"" + s.span_id + "\",\"parentId\":" +
-                    (s.parent_id.empty() ? std::string("null") : "\"" + s.parent_id + "\"") + ",\"ts\":" + ts +
+                    ",\"name\":" + json_str(name) + ",\"kind\":\"server\",\"traceId\":\"" + std::string(s.tid()) +
+                    "\",\"spanId\":\"" + std::string(s.sid()) + "\",\"parentId\":" +
+                    (s.has_parent ? "\"" + std::string(s.pid()) + "\"" : std::string("null")) + ",\"ts\":" + ts +
                     ",\"durationMs\":" + dur + ",\"status\":\"" + (status >= 500 ? "error" : "ok") +
                     "\",\"attributes\":{\"http.status\":" + std::to_string(status);
     for (auto& a : attrs) l += "," + json_str(a.first) + ":" + json_str(a.second);
@@ -453,7 +445,8 @@ class DataPlane {
     std::snprintf(ts, sizeof ts, "%.6f", wall_now());
     std::string line = std::string("{\"ts\":") + ts + ",\"level\":\"INFO\",\"role\":" + json_str(app_id_ + ".sidecar") +
                        ",\"category\":\"sidecar.http-info\",\"message\":" + json_str(msg) + ",\"traceId\":\"" +
-                       span.trace_id + "\",\"spanId\":\"" + span.span_id + "\",\"plane\":\"native\"}\n";
+                       std::string(span.tid()) + "\",\"spanId\":\"" + std::string(span.sid()) +
+                       "\",\"plane\":\"native\"}\n";
     std::fwrite(line.data(), 1, line.size(), stderr);
   }
 
@@ -1089,15 +1082,22 @@ class DataPlane {
         }
         const char* ks = p;
         p = skip_value(p, e);
-        std::string k = parse(std::string_view(ks, (size_t)(p - ks))).s;
+        std::string_view ktok(ks, (size_t)(p - ks));
+        std::string k = ktok.size() >= 2 && ktok.find('\\') == std::string_view::npos
+                            ? std::string(ktok.substr(1, ktok.size() - 2))  // plain key: no unescaping
+                            : parse(ktok).s;
         p = ws_end(p, e) + 1;  // ':'
         p = ws_end(p, e);
         const char* vs = p;
         p = skip_value(p, e);
         std::string_view raw(vs, (size_t)(p - vs));
         if (k == "key") {
-          Value v = parse(raw);
-          if (v.t == Value::String) it.key = v.s;
+          if (raw.size() >= 2 && raw.front() == '"' && raw.find('\\') == std::string_view::npos) {
+            it.key.assign(raw.data() + 1, raw.size() - 2);
+          } else {
+            Value v = parse(raw);
+            if (v.t == Value::String) it.key = v.s;
+          }
         } else if (k == "value") {
           it.value = compact(raw);
           have_value = true;

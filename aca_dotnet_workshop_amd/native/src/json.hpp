@@ -269,6 +269,195 @@ inline Value parse(std::string_view s) { return Parser(s).parse(); }
 // json.loads' strictness: raw control characters inside strings are rejected.
 inline Value parse_strict(std::string_view s) { return Parser(s, true).parse(); }
 
+// Allocation-free check that `s` is one JSON value Parser would accept (same grammar: number
+// tokens, escapes, nesting limit), for the data plane's "is this body JSON?" questions.
+class Validator {
+ public:
+  explicit Validator(std::string_view s) : p_(s.data()), e_(s.data() + s.size()) {}
+  bool ok() {
+    if (!value(0)) return false;
+    ws();
+    return p_ == e_;
+  }
+
+ private:
+  const char* p_;
+  const char* e_;
+  void ws() { while (p_ < e_ && (*p_ == ' ' || *p_ == '\n' || *p_ == '\r' || *p_ == '\t')) ++p_; }
+  bool value(int depth) {
+    if (depth > 256) return false;
+    ws();
+    if (p_ >= e_) return false;
+    switch (*p_) {
+      case '{': return object(depth);
+      case '[': return array(depth);
+      case '"': return str();
+      case 't': return lit("true", 4);
+      case 'f': return lit("false", 5);
+      case 'n': return lit("null", 4);
+      default: return num();
+    }
+  }
+  bool lit(const char* w, size_t n) {
+    if ((size_t)(e_ - p_) < n || std::memcmp(p_, w, n) != 0) return false;
+    p_ += n;
+    return true;
+  }
+  bool num() {
+    const char* s = p_;
+    if (p_ < e_ && (*p_ == '-' || *p_ == '+')) ++p_;
+    const char* d0 = p_;
+    while (p_ < e_ && *p_ >= '0' && *p_ <= '9') ++p_;
+    const char* d1 = p_;
+    while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' || *p_ == '-' || *p_ == '+')) ++p_;
+    if (p_ == s) return false;
+    if (p_ == d1 && d1 > d0) return true;  // sign + digits: always a complete strtod number
+    char buf[64];
+    std::string big;
+    const size_t n = (size_t)(p_ - s);
+    const char* c;
+    if (n < sizeof buf) {
+      std::memcpy(buf, s, n);
+      buf[n] = 0;
+      c = buf;
+    } else {
+      big.assign(s, n);
+      c = big.c_str();
+    }
+    char* end = nullptr;
+    std::strtod(c, &end);
+    return end == c + n;
+  }
+  bool str() {
+    ++p_;
+    const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+    while (true) {
+      while (e_ - p_ >= 16) {
+        __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p_));
+        int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)));
+        if (m) {
+          p_ += __builtin_ctz((unsigned)m);
+          break;
+        }
+        p_ += 16;
+      }
+      while (p_ < e_ && *p_ != '"' && *p_ != '\\') ++p_;
+      if (p_ >= e_) return false;
+      if (*p_ == '"') {
+        ++p_;
+        return true;
+      }
+      ++p_;  // backslash
+      if (p_ >= e_) return false;
+      char x = *p_++;
+      switch (x) {
+        case '"': case '\\': case '/': case 'b': case 'f': case 'n': case 'r': case 't': break;
+        case 'u': {
+          if (!hex4()) return false;
+          break;
+        }
+        default: return false;
+      }
+    }
+  }
+  bool hex4() {
+    if (e_ - p_ < 4) return false;
+    uint32_t cp = 0;
+    for (int i = 0; i < 4; ++i) {
+      char c = *p_++;
+      cp <<= 4;
+      if (c >= '0' && c <= '9') cp |= c - '0';
+      else if (c >= 'a' && c <= 'f') cp |= c - 'a' + 10;
+      else if (c >= 'A' && c <= 'F') cp |= c - 'A' + 10;
+      else return false;
+    }
+    // Parser: a high surrogate followed by "\u" consumes the second escape as its low half
+    if (cp >= 0xD800 && cp < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+      p_ += 2;
+      for (int i = 0; i < 4; ++i) {
+        char c = *p_++;
+        if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'))) return false;
+      }
+    }
+    return true;
+  }
+  bool array(int depth) {
+    ++p_;
+    ws();
+    if (p_ < e_ && *p_ == ']') { ++p_; return true; }
+    while (true) {
+      if (!value(depth + 1)) return false;
+      ws();
+      if (p_ >= e_) return false;
+      if (*p_ == ',') { ++p_; continue; }
+      if (*p_ == ']') { ++p_; return true; }
+      return false;
+    }
+  }
+  bool object(int depth) {
+    ++p_;
+    ws();
+    if (p_ < e_ && *p_ == '}') { ++p_; return true; }
+    while (true) {
+      ws();
+      if (p_ >= e_ || *p_ != '"' || !str()) return false;
+      ws();
+      if (p_ >= e_ || *p_ != ':') return false;
+      ++p_;
+      if (!value(depth + 1)) return false;
+      ws();
+      if (p_ >= e_) return false;
+      if (*p_ == ',') { ++p_; continue; }
+      if (*p_ == '}') { ++p_; return true; }
+      return false;
+    }
+  }
+};
+
+inline bool valid(std::string_view s) { return Validator(s).ok(); }
+
+// Copy of a valid JSON text without insignificant whitespace; runs without quotes, backslashes
+// or whitespace are copied 16 bytes at a time.
+inline std::string compact(std::string_view s) {
+  std::string o;
+  o.reserve(s.size());
+  const char* p = s.data();
+  const char* e = p + s.size();
+  bool in_str = false;
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), sp = _mm_set1_epi8(' '), nl = _mm_set1_epi8('\n'),
+                cr = _mm_set1_epi8('\r'), tb = _mm_set1_epi8('\t');
+  while (p < e) {
+    if (e - p >= 16) {
+      __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+      __m128i hit = _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs));
+      if (!in_str)
+        hit = _mm_or_si128(hit, _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, sp), _mm_cmpeq_epi8(x, nl)),
+                                             _mm_or_si128(_mm_cmpeq_epi8(x, cr), _mm_cmpeq_epi8(x, tb))));
+      int m = _mm_movemask_epi8(hit);
+      if (m == 0) {
+        o.append(p, 16);
+        p += 16;
+        continue;
+      }
+      int k = __builtin_ctz((unsigned)m);
+      o.append(p, (size_t)k);
+      p += k;
+    }
+    char c = *p++;
+    if (in_str) {
+      o += c;
+      if (c == '\\' && p < e) o += *p++;
+      else if (c == '"') in_str = false;
+    } else if (c == '"') {
+      in_str = true;
+      o += c;
+    } else if (c != ' ' && c != '\n' && c != '\r' && c != '\t') {
+      o += c;
+    }
+  }
+  return o;
+}
+
 inline void escape_to(std::string& out, std::string_view s) {
   out += '"';
   for (unsigned char c : s) {

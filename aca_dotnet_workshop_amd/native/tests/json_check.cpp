@@ -1,6 +1,7 @@
 // Conformance driver for native/src/json.hpp (tests/test_native_json.py): reads one JSON text per
 // line (hex-encoded, so any byte can appear), parses it lax and strict and prints, per line,
-// "<lax>\t<strict>" where each is the re-serialised value or "ERR".
+// "<lax>\t<strict>\t<valid>\t<compact>": the re-serialised values or "ERR", tt::valid's verdict
+// (1/0) and, for valid texts, the hex of tt::compact's output.
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -32,7 +33,13 @@ int main() {
     std::unique_ptr<char[]> buf(new char[text.size() + (text.empty() ? 1 : 0)]);
     std::memcpy(buf.get(), text.data(), text.size());
     std::string_view view(buf.get(), text.size());
-    std::cout << run(view, false) << '\t' << run(view, true) << '\n';
+    const bool ok = tt::valid(view);
+    std::string hex;
+    if (ok) {
+      static const char* d = "0123456789abcdef";
+      for (unsigned char c : tt::compact(view)) hex += d[c >> 4], hex += d[c & 15];
+    }
+    std::cout << run(view, false) << '\t' << run(view, true) << '\t' << (ok ? 1 : 0) << '\t' << hex << '\n';
   }
   return 0;
 }

@@ -246,16 +246,17 @@ class LocalStack:
                 raise TimeoutError(f"replicas not ready: {[r.name for r in pending]}")
             time.sleep(0.05)
 
-    def cpu_seconds(self) -> dict[str, float]:
-        """User+system CPU seconds consumed so far by every process of the stack, keyed by role
-        (``backing``, ``backing-<families>``, ``<replica>.sidecar``, ``<replica>.app``).  Used by
-        ``bench.py`` to attribute where the end-to-end flow spends its cycles."""
+    def cpu_seconds(self, part: str = "total") -> dict[str, float]:
+        """User+system (``part="system"``: kernel-mode only) CPU seconds consumed so far by every
+        process of the stack, keyed by role (``backing``, ``backing-<families>``,
+        ``<replica>.sidecar``, ``<replica>.app``).  Used by ``bench.py`` to attribute where the
+        end-to-end flow spends its cycles."""
         import psutil
 
         def cpu(pid: int) -> float:
             try:
                 t = psutil.Process(pid).cpu_times()
-                return t.user + t.system
+                return t.system if part == "system" else t.user + t.system
             except psutil.Error:
                 return 0.0
 

@@ -321,6 +321,7 @@ def main() -> None:
         me = psutil.Process()
         thr0 = cgroup_throttling()
         cpu0 = stack.cpu_seconds()
+        sys0 = stack.cpu_seconds("system")
         t = me.cpu_times()
         cpu0["bench-client"] = t.user + t.system + t.children_user + t.children_system
         report = None
@@ -336,6 +337,7 @@ def main() -> None:
         if sweeper is not None:
             sweeper.stop()
         cpu1 = stack.cpu_seconds()
+        sys1 = stack.cpu_seconds("system")
         thr1 = cgroup_throttling()
         t = me.cpu_times()
         cpu1["bench-client"] = t.user + t.system + t.children_user + t.children_system
@@ -343,7 +345,9 @@ def main() -> None:
         if d.rank == 0:
             # cores busy per process role during the timed region (where the E2E flow is CPU bound)
             util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
+            kern = {k: round((sys1.get(k, 0.0) - v) / dt, 2) for k, v in sys0.items()}  # kernel-mode part
             print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
+                              "cpu_cores_busy_kernel_mode": kern,
                               "cpu_budget_per_rank": round(cores, 2),
                               "cgroup_throttling": {k: thr1[k] - thr0.get(k, 0) for k in thr1},
                               "loadgen": report}),

@@ -5,7 +5,9 @@ UndefinedBehaviorSanitizer so reads past the end of a text fail the run.
 * every text Python's ``json.loads`` accepts, the native parser accepts with the same value
   (lax and strict; strict also rejects what ``json.loads(strict=True)`` rejects for raw control
   characters inside strings);
-* arbitrary and truncated byte strings never crash it."""
+* the allocation-free validator (``tt::valid``) accepts exactly what the parser accepts, and
+  ``tt::compact`` (16-byte runs) strips exactly the whitespace outside strings;
+* arbitrary and truncated byte strings never crash them."""
 import json
 import os
 import random
@@ -32,7 +34,7 @@ def checker(tmp_path_factory):
         pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
     assert r.returncode == 0, r.stderr[-3000:]
 
-    def run(texts: list[bytes]) -> list[tuple[str, str]]:
+    def run(texts: list[bytes]) -> list[tuple[str, str, str, str]]:
         inp = "".join(t.hex() + "\n" for t in texts)
         p = subprocess.run([str(exe)], input=inp, capture_output=True, text=True, timeout=300,
                            env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"))
@@ -40,8 +42,32 @@ def checker(tmp_path_factory):
         assert "ERROR: AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, p.stderr[-3000:]
         rows = [tuple(line.split("\t")) for line in p.stdout.split("\n")[:-1]]
         assert len(rows) == len(texts)
-        return rows
+        for t, (lax, _strict, ok, comp) in zip(texts, rows):
+            assert (ok == "1") == (lax != "ERR"), t  # validator == parser acceptance
+            if ok == "1":
+                assert bytes.fromhex(comp) == _compact_ref(t), t
+        return [r[:2] for r in rows]
     return run
+
+
+def _compact_ref(t: bytes) -> bytes:
+    out, in_str, i = bytearray(), False, 0
+    while i < len(t):
+        c = t[i]
+        if in_str:
+            out.append(c)
+            if c == 0x5C and i + 1 < len(t):
+                i += 1
+                out.append(t[i])
+            elif c == 0x22:
+                in_str = False
+        elif c == 0x22:
+            in_str = True
+            out.append(c)
+        elif c not in b" \n\r\t":
+            out.append(c)
+        i += 1
+    return bytes(out)
 
 
 ALPHABET = "abcXYZ 019_-\"\\/\u00e9\u4e2d\U0001F600\t\n\x01"
