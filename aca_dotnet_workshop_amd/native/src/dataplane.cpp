@@ -424,6 +424,7 @@ class DataPlane {
   std::map<std::string, Store> stores_;
   std::map<std::string, Bus> buses_;
   std::map<std::string, uint64_t> counters_;
+  std::map<std::pair<std::string, int>, uint64_t> op_counts_;  // (op, status): no label string per request
   size_t inflight_ = 0;
 
   static HeaderList auth_headers(const Value& s) {
@@ -451,7 +452,7 @@ class DataPlane {
   }
 
   void count(const std::string& op, int status) {
-    counters_["app=\"" + app_id_ + "\",op=\"" + op + "\",status=\"" + std::to_string(status) + "\""]++;
+    op_counts_[{op, status}]++;
   }
 
   // Wrap a Reply so every natively handled request gets a span, a counter and in-flight accounting.
@@ -905,7 +906,11 @@ class DataPlane {
   void metrics(Message&& m, Reply r) {
     std::string extra = "# HELP sidecar_native_requests_total requests served by the native data plane\n"
                         "# TYPE sidecar_native_requests_total counter\n";
-    for (auto& kv : counters_) extra += "sidecar_native_requests_total{" + kv.first + "} " + std::to_string(kv.second) + "\n";
+    std::map<std::string, uint64_t> all = counters_;
+    for (auto& kv : op_counts_)
+      all["app=\"" + app_id_ + "\",op=\"" + kv.first.first + "\",status=\"" + std::to_string(kv.first.second) + "\""] +=
+          kv.second;
+    for (auto& kv : all) extra += "sidecar_native_requests_total{" + kv.first + "} " + std::to_string(kv.second) + "\n";
     forward_to_control_plane(std::move(m), std::move(r), [extra](std::string& body) { body += extra; });
   }
 
