@@ -6,6 +6,7 @@ caller (``backing.accel``) decides explicitly whether to use the CPU executor in
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Any
 
 from .build import LIB, build_gpu
@@ -75,6 +76,10 @@ class GpuKernels:
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
         self.chunk_tiles = int(self.lib.tt_chunk_tiles())
+        # the pinned total and its event are shared by every caller of this object (queries of
+        # different collections run on different threads): one select at a time from the
+        # compaction launch to the read of the total
+        self._total_lock = threading.Lock()
         # Single-pass select (tt_scan_select, decoupled look-back) is opt-in: measured 1.40 ms vs
         # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
         # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
@@ -166,14 +171,15 @@ class GpuKernels:
         out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
         # [0] = total (int64), [2:] = 16-byte aligned int32 tile offsets (mode 0: chunk counts)
         scratch = torch.empty(tiles // 2 + 3, dtype=torch.int64, device=self.device)
-        pinned = self._pinned()
-        rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[2:].data_ptr(), nrows,
-                                             out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
-        if rc != 0:
-            raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
-        self._total_event.record(torch.cuda.current_stream(self.device))
-        self._total_event.synchronize()
-        total = int(pinned[0])
+        with self._total_lock:
+            pinned = self._pinned()
+            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[2:].data_ptr(), nrows,
+                                                 out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
+            if rc != 0:
+                raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
+            self._total_event.record(torch.cuda.current_stream(self.device))
+            self._total_event.synchronize()
+            total = int(pinned[0])
         out = out[:total]
         return (out, mask) if return_mask else out
 

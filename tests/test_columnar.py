@@ -315,6 +315,34 @@ def test_gpu_compaction_offsets_over_many_chunks(tiles, mode):
 
 
 @pytest.mark.gpu
+def test_gpu_concurrent_selects_from_threads():
+    """Queries of different collections run on different threads of the backing (one lock per
+    collection): the shared pinned total / event of the kernels object must not mix results."""
+    import threading
+    k = _kernels()
+    cols = [_random_collection(n, random.Random(n)) for n in (50_001, 120_007)]
+    wants = [[ix.select_numpy(ix.compile(f)) for f in GPU_FILTERS] for ix in cols]
+    errors = []
+
+    def worker(i):
+        ix = cols[i]
+        try:
+            for _ in range(15):
+                for f, want in zip(GPU_FILTERS, wants[i]):
+                    got = ix.select_gpu(ix.compile(f), k)
+                    if not np.array_equal(got, want):
+                        errors.append((i, f))
+        except Exception as e:  # surfaced below
+            errors.append((i, repr(e)))
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:3]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 8193, 300_001])
 def test_gpu_single_pass_select_matches(n):
     """tt_scan_select (one pass, decoupled look-back) == the two-pass pipeline."""
