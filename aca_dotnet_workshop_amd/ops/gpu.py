@@ -76,10 +76,11 @@ class GpuKernels:
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
         self.chunk_tiles = int(self.lib.tt_chunk_tiles())
-        # the pinned total and its event are shared by every caller of this object (queries of
-        # different collections run on different threads): one select at a time from the
-        # compaction launch to the read of the total
+        # the pinned total, its event and the cached scratch buffers are shared by every caller
+        # of this object (queries of different collections run on different threads): one
+        # select at a time
         self._total_lock = threading.Lock()
+        self._bufs: dict[str, Any] = {}
         # Single-pass select (tt_scan_select, decoupled look-back) is opt-in: measured 1.40 ms vs
         # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
         # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
@@ -145,35 +146,37 @@ class GpuKernels:
             raise ValueError("program must be int32 [L, 4]")
         if self.fused_select and not return_mask:
             return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
-        mask = torch.empty(tiles * self.tile_rows // 16, dtype=torch.int16, device=self.device)
-        counts = torch.empty(tiles, dtype=torch.int32, device=self.device)
-        stream = self._stream()
-        if flat is not None and self.flat_eval:
-            leaves, flip, max_width = flat
-            if leaves.dtype != torch.int32 or leaves.ndim != 2 or leaves.shape[1] != 4:
-                raise ValueError("flat leaves must be int32 [n, 4]")
-            if leaves.shape[0] > self.max_flat_leaves:
-                raise ValueError("too many leaves for tt_scan_flat")
-            rc = self.lib.tt_launch_scan_flat(table.data_ptr(), nrows, live16.data_ptr(), leaves.data_ptr(),
-                                              leaves.shape[0], int(flip), int(max_width), bitmaps.data_ptr(),
-                                              bitmaps.numel(), mask.data_ptr(), counts.data_ptr(), stream)
-            if rc != 0:
-                raise RuntimeError(f"tt_scan_flat launch failed ({rc})")
-        else:
-            rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
-                                              prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(), mask.data_ptr(),
-                                              counts.data_ptr(), stream)
-            if rc != 0:
-                raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
-        # the tiles' output offsets in one block (tt_tile_offsets, which also writes the total
-        # straight into pinned host memory), then the wave-independent compaction: no torch
-        # launches, no host sync between the kernels -- one event wait at the end
-        out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
-        # [0] = total (int64), [2:] = 16-byte aligned int32 tile offsets (mode 0: chunk counts)
-        scratch = torch.empty(tiles // 2 + 3, dtype=torch.int64, device=self.device)
-        with self._total_lock:
+        with self._total_lock:  # also guards the cached scratch buffers
+            nmask = tiles * self.tile_rows // 16
+            mask = (torch.empty(nmask, dtype=torch.int16, device=self.device) if return_mask
+                    else self._buf("mask", nmask, torch.int16))
+            counts = self._buf("counts", tiles, torch.int32)
+            stream = self._stream()
+            if flat is not None and self.flat_eval:
+                leaves, flip, max_width = flat
+                if leaves.dtype != torch.int32 or leaves.ndim != 2 or leaves.shape[1] != 4:
+                    raise ValueError("flat leaves must be int32 [n, 4]")
+                if leaves.shape[0] > self.max_flat_leaves:
+                    raise ValueError("too many leaves for tt_scan_flat")
+                rc = self.lib.tt_launch_scan_flat(table.data_ptr(), nrows, live16.data_ptr(), leaves.data_ptr(),
+                                                  leaves.shape[0], int(flip), int(max_width), bitmaps.data_ptr(),
+                                                  bitmaps.numel(), mask.data_ptr(), counts.data_ptr(), stream)
+                if rc != 0:
+                    raise RuntimeError(f"tt_scan_flat launch failed ({rc})")
+            else:
+                rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
+                                                  prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(),
+                                                  mask.data_ptr(), counts.data_ptr(), stream)
+                if rc != 0:
+                    raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
+            # the tiles' output offsets in one block (tt_tile_offsets, which also writes the total
+            # straight into pinned host memory), then the wave-independent compaction: no torch
+            # launches, no host sync between the kernels -- one event wait at the end
+            out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
+            # [0] = total (int64), byte 16 on: int32 tile offsets (mode 0: chunk counts)
+            scratch = self._buf("scratch", tiles // 2 + 3, torch.int64)
             pinned = self._pinned()
-            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch[2:].data_ptr(), nrows,
+            rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch.data_ptr() + 16, nrows,
                                                  out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
@@ -182,6 +185,13 @@ class GpuKernels:
             total = int(pinned[0])
         out = out[:total]
         return (out, mask) if return_mask else out
+
+    def _buf(self, name: str, n: int, dtype):
+        """Cached device scratch of at least ``n`` elements (caller holds ``_total_lock``)."""
+        t = self._bufs.get(name)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = self._bufs[name] = self.torch.empty(max(n, 1), dtype=dtype, device=self.device)
+        return t
 
     def _pinned(self):
         p = getattr(self, "_pinned_total", None)
