@@ -11,6 +11,8 @@ the multi-rank side used by ``bench.py`` when the driver launches one process pe
   nothing to carry -- SURVEY.md §5 "Distributed communication backend");
 * ``cpu_budget`` / ``topology`` -- each rank runs its own environment (weak scaling, like adding
   Container Apps environments) sized to its share of the host's CPUs;
+* ``pin_rank`` / ``partition_cpus`` -- NUMA- and core-aware CPU partitions, one per rank on a
+  host, so N environments do not migrate across each other's cores and sockets;
 * ``cgroup_throttling`` -- CFS quota throttling counters for the bench report.
 """
 from __future__ import annotations
@@ -18,7 +20,7 @@ from __future__ import annotations
 import os
 import sys
 
-__all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling"]
+__all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling", "partition_cpus", "pin_rank"]
 
 
 class Dist:
@@ -73,6 +75,69 @@ class Dist:
     def close(self) -> None:
         if self.pg is not None:
             self.pg.destroy_process_group()
+
+
+def _cpulist(text: str) -> set[int]:
+    """Kernel cpulist syntax (``0-3,8,10-11``) -> CPU ids."""
+    out: set[int] = set()
+    for part in text.strip().split(","):
+        if part:
+            lo, _, hi = part.partition("-")
+            out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def host_topology() -> tuple[list[set[int]], dict[int, int]]:
+    """(NUMA nodes as CPU sets, CPU -> first SMT sibling) from sysfs; one node and no SMT
+    grouping when sysfs does not say."""
+    nodes, core = [], {}
+    base = "/sys/devices/system/node"
+    try:
+        for d in sorted(os.listdir(base)):
+            if d.startswith("node") and d[4:].isdigit():
+                nodes.append(_cpulist(open(f"{base}/{d}/cpulist").read()))
+    except OSError:
+        pass
+    for c in os.sched_getaffinity(0):
+        try:
+            core[c] = min(_cpulist(open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read()))
+        except (OSError, ValueError):
+            core[c] = c
+    return [n for n in nodes if n], core
+
+
+def partition_cpus(allowed: set[int], nodes: list[set[int]], core: dict[int, int],
+                   local_rank: int, local_world: int, min_cpus: int = 2) -> set[int] | None:
+    """The CPUs of one rank when ``local_world`` ranks share a host: ranks are spread over the
+    NUMA nodes (each rank's processes -- API/processor replicas, sidecars, backing, load
+    generator -- talk over loopback/UDS, so keeping them on one socket keeps that traffic in
+    one L3/memory domain), and each node's CPUs are cut into contiguous runs of whole cores
+    (SMT siblings stay together, so two ranks never share a physical core).  ``None`` when a
+    rank would get fewer than ``min_cpus`` CPUs (no pinning then)."""
+    if local_world <= 1:
+        return None
+    nodes = [n & allowed for n in nodes if n & allowed] or [set(allowed)]
+    if local_world < len(nodes):  # fewer ranks than nodes: each rank takes whole nodes
+        lo, hi = local_rank * len(nodes) // local_world, (local_rank + 1) * len(nodes) // local_world
+        cpus = set().union(*nodes[lo:hi])
+        return cpus if len(cpus) >= min_cpus else None
+    node = local_rank * len(nodes) // local_world
+    peers = [r for r in range(local_world) if r * len(nodes) // local_world == node]
+    k, i = len(peers), peers.index(local_rank)
+    order = sorted(nodes[node], key=lambda c: (core.get(c, c), c))
+    cpus = set(order[i * len(order) // k:(i + 1) * len(order) // k])
+    return cpus if len(cpus) >= min_cpus else None
+
+
+def pin_rank(local_rank: int, local_world: int) -> set[int] | None:
+    """Pin this process (and every child it starts later) to its rank's CPU partition."""
+    if local_world <= 1 or os.environ.get("TT_BENCH_PIN", "1") == "0":
+        return None
+    nodes, core = host_topology()
+    cpus = partition_cpus(set(os.sched_getaffinity(0)), nodes, core, local_rank, local_world)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
 
 
 def cpu_budget() -> float:

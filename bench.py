@@ -247,6 +247,9 @@ def main() -> None:
     n = d.world if d.world > 1 else a.gpus
     local = int(os.environ.get("LOCAL_WORLD_SIZE", d.world if d.world > 1 else 1))
     cores = cpu_budget() / max(1, local)
+    from aca_dotnet_workshop_amd.parallel import pin_rank
+    # ranks sharing a host get disjoint NUMA-local core sets (inherited by the whole stack)
+    pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local) if d.world > 1 else None
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
@@ -391,6 +394,8 @@ def main() -> None:
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
                            "sidecar_api_protocol": a.api_protocol,
                            "app_host": a.app_host,
+                           "cpu_pinning": (f"{len(pinned)} CPUs per rank (NUMA-local whole cores)"
+                                           if pinned else "none"),
                            "create_latency_p50_ms": round(p50, 3),
                            "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput",
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",

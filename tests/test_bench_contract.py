@@ -54,6 +54,8 @@ def test_bench_two_ranks_torchrun():
     # nothing else on stdout (gloo's connection messages go to stderr)
     assert [x for x in r.stdout.splitlines() if x.strip() and not x.startswith("{")] == [], r.stdout
     _check(lines[0], 2, 2, 1)
+    # 8 CPUs here: each rank pinned to its own 4 (the stack inherits the mask)
+    assert lines[0]["config"]["cpu_pinning"] == f"{len(os.sched_getaffinity(0)) // 2} CPUs per rank (NUMA-local whole cores)"
 
 
 def test_bench_shared_env_two_ranks():
@@ -97,6 +99,30 @@ def test_parallel_helpers():
     assert cpu_budget() >= 1
     d = Dist()  # single process: identities
     assert (d.world, d.rank, d.max(3.0), d.sum(2.0)) == (1, 0, 3.0, 2.0)
+
+
+def test_partition_cpus_numa_and_smt():
+    from aca_dotnet_workshop_amd.parallel import host_topology, partition_cpus
+    from aca_dotnet_workshop_amd.parallel import _cpulist
+    assert _cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    # 2 sockets x 64 cores x 2 threads, Linux numbering: socket0 = 0-63 + 128-191
+    nodes = [set(range(0, 64)) | set(range(128, 192)), set(range(64, 128)) | set(range(192, 256))]
+    core = {c: c % 128 for c in range(256)}
+    allowed = set(range(256))
+    parts = [partition_cpus(allowed, nodes, core, r, 8) for r in range(8)]
+    assert all(len(p) == 32 for p in parts)
+    assert set().union(*parts) == allowed and sum(map(len, parts)) == 256  # disjoint cover
+    for r, p in enumerate(parts):
+        assert p <= nodes[r * 2 // 8]                     # ranks 0-3 on socket 0, 4-7 on socket 1
+        assert {c ^ 128 for c in p} == p                  # SMT siblings stay with their core
+    # fewer ranks than nodes: whole nodes; a quota-restricted affinity mask is respected
+    assert partition_cpus(allowed, nodes, core, 1, 2) == nodes[1]
+    sub = set(range(0, 16))
+    assert partition_cpus(sub, nodes, core, 1, 2) == set(range(8, 16))
+    assert partition_cpus({0, 1}, nodes, core, 1, 4) is None  # too small to pin
+    assert partition_cpus(allowed, nodes, core, 0, 1) is None
+    ns, cr = host_topology()  # real sysfs of this host: readable, every allowed CPU mapped
+    assert set(cr) == set(os.sched_getaffinity(0))
 
 
 def test_rank_device_env():
