@@ -249,7 +249,7 @@ def main() -> None:
     cores = cpu_budget() / max(1, local)
     from aca_dotnet_workshop_amd.parallel import pin_rank
     # ranks sharing a host get disjoint NUMA-local core sets (inherited by the whole stack)
-    pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local) if d.world > 1 else None
+    pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local)
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
