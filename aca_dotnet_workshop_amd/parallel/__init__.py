@@ -132,8 +132,9 @@ def partition_cpus(allowed: set[int], nodes: list[set[int]], core: dict[int, int
 def pin_rank(local_rank: int, local_world: int, spec: str | None = None) -> set[int] | None:
     """Pin this process (and every child it starts later) to its rank's CPU partition.
     ``spec`` (default ``$TT_BENCH_PIN``): ``0`` never pins; with several ranks on the host any
-    other value partitions (``partition_cpus``); a single rank pins only on ``node`` (its first
-    NUMA node) or ``<n>`` (the first n CPUs of that node, whole cores first)."""
+    other value partitions (``partition_cpus``); a single rank pins to its first NUMA node on
+    ``1`` (default) / ``node``, or to ``<n>`` > 1 CPUs of that node (whole cores first).  On the
+    MI355X box one stack on one socket ran +24 % vs unpinned (profiles/r2_rank_pinning.md)."""
     spec = os.environ.get("TT_BENCH_PIN", "1") if spec is None else spec
     if spec == "0":
         return None
@@ -141,10 +142,10 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None) -> set[
     allowed = set(os.sched_getaffinity(0))
     if local_world > 1:
         cpus = partition_cpus(allowed, nodes, core, local_rank, local_world)
-    elif spec == "node" or spec.isdigit() and int(spec) > 1:
+    elif spec in ("1", "node") or spec.isdigit() and int(spec) > 1:
         first = next((n & allowed for n in nodes if n & allowed), allowed)
         order = sorted(first, key=lambda c: (core.get(c, c), c))
-        cpus = set(order if spec == "node" else order[:int(spec)])
+        cpus = set(order if spec in ("1", "node") else order[:int(spec)])
     else:
         cpus = None
     if cpus:
