@@ -39,7 +39,7 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=12288,
+    ap.add_argument("--batch", type=int, default=16384,
                     help="createTask requests per step per rank (the step quantum: 20 steps >= 3 s timed)")
     ap.add_argument("--concurrency", type=int, default=0,
                     help="requests in flight per rank (0 = 48 per API replica, at most 384)")
