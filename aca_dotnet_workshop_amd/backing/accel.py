@@ -124,13 +124,30 @@ class CollectionAccelerator:
             qq = dict(q)
             qq["filter"] = flt
             k = self.kernels()
-            try:
-                rows, token = self.index.query_rows(qq, k)
-            except Unsupported:
+            # the row numbers are only meaningful in the mirror generation they were selected
+            # from: a write that compacts the mirror between the sync and the lookup (the native
+            # front writes without the GIL) renumbers them -- re-sync and select again
+            for _ in range(3):
+                try:
+                    rows, token = self.index.query_rows(qq, k)
+                except Unsupported:
+                    self.stats["fallback"] += 1
+                    return None
+                res = store.mirror_results(rows, prefix, token or "", gen=self.index.generation)
+                if res is not None:
+                    break
+                self.stats["stale_retries"] = self.stats.get("stale_retries", 0) + 1
+                try:
+                    self.index.sync()
+                except Unsupported:
+                    self.disabled, self.index = True, None
+                    self.stats["fallback"] += 1
+                    return None
+            else:  # compacting faster than we can select: the native engine answers
                 self.stats["fallback"] += 1
                 return None
             self.stats["gpu" if k is not None else "cpu"] += 1
-            text, skipped = store.mirror_results(rows, prefix, token or "")
+            text, skipped = res
             self.stats["skipped_rows"] += skipped
             return text.decode()
 

@@ -181,9 +181,11 @@ def mark_overdue_wire(body: bytes) -> tuple[list[str], bytes] | None:
     return fns[0](body) if fns else None
 
 
-def tasks_from_query_wire(body: bytes) -> tuple[int, bytes] | None:
-    """State-query response -> (tasks, TaskModel JSON array of the results with data, in order),
-    each written like ``to_wire()``; ``None``: bind the results with ``TaskModel``."""
+def tasks_from_query_wire(body: bytes, by_created: bool = False) -> tuple[int, bytes, bool] | None:
+    """State-query response -> (tasks, TaskModel JSON array of the results with data, whether the
+    response carries a continuation token), each task written like ``to_wire()``; in result
+    order, or with ``by_created`` ordered by ``TaskCreatedOn`` as a DateTime (ascending, stable:
+    the reference's ``OrderBy``, TasksStoreManager.cs:136).  ``None``: bind with ``TaskModel``."""
     global _native_query
     if _native_query is None:
         try:
@@ -191,7 +193,7 @@ def tasks_from_query_wire(body: bytes) -> tuple[int, bytes] | None:
             _native_query = load().tasks_from_query
         except Exception:
             _native_query = False
-    return _native_query(body) if _native_query else None
+    return _native_query(body, by_created) if _native_query else None
 
 
 _native_query: Any = None

@@ -911,6 +911,10 @@ class DataPlane {
       all["app=\"" + app_id_ + "\",op=\"" + kv.first.first + "\",status=\"" + std::to_string(kv.first.second) + "\""] +=
           kv.second;
     for (auto& kv : all) extra += "sidecar_native_requests_total{" + kv.first + "} " + std::to_string(kv.second) + "\n";
+    extra += "# HELP sidecar_mtls_handshake_rejected_total mesh TLS handshakes this sidecar refused\n"
+             "# TYPE sidecar_mtls_handshake_rejected_total counter\n"
+             "sidecar_mtls_handshake_rejected_total{app=\"" + app_id_ + "\"} " +
+             std::to_string(ev::tls_server_handshake_rejects.load(std::memory_order_relaxed)) + "\n";
     forward_to_control_plane(std::move(m), std::move(r), [extra](std::string& body) { body += extra; });
   }
 

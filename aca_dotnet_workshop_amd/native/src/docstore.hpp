@@ -571,12 +571,17 @@ class DocStore {
 
   // Query result JSON for mirror rows (in the given order): {"results":[{"key","data","etag"}]}
   // with `prefix` stripped from the keys.  Rows killed since the reader's sync (the document
-  // changed or went away) are skipped; `skipped` reports how many.
-  std::string mirror_results(const int32_t* rows, size_t nrows, const std::string& prefix, const std::string& token,
-                             size_t* skipped = nullptr) {
+  // changed or went away) are skipped; `skipped` reports how many.  `gen` is the mirror
+  // generation the reader's row numbers come from: a compaction (or a new column) renumbers the
+  // rows, so a different generation returns false (`*stale` = true) without touching `out` --
+  // a stale row number could name another live document, which would then be returned for a
+  // filter it does not match.
+  bool mirror_results(const int32_t* rows, size_t nrows, const std::string& prefix, const std::string& token,
+                      uint64_t gen, std::string& out, size_t* skipped = nullptr) {
     std::lock_guard<std::mutex> g(mu_);
+    if (gen != mirror_.gen) return false;
     int64_t now = now_ms();
-    std::string out = "{\"results\":[";
+    out = "{\"results\":[";
     size_t skip = 0;
     bool first = true;
     for (size_t i = 0; i < nrows; ++i) {
@@ -599,7 +604,7 @@ class DocStore {
     if (!token.empty()) out += ",\"token\":\"" + token + "\"";
     out += "}";
     if (skipped) *skipped = skip;
-    return out;
+    return true;
   }
 
   std::unordered_map<std::string, uint64_t> mirror_stats() {

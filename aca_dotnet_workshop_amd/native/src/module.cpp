@@ -280,16 +280,18 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(retrieved, kept, py::bytes(out));
   });
 
-  // state-query response -> (task count, TaskModel JSON array) or None (taskcodec.hpp query_tasks).
-  m.def("tasks_from_query", [](py::bytes body) -> py::object {
+  // state-query response -> (task count, TaskModel JSON array, has a continuation token) or None
+  // (taskcodec.hpp query_tasks); `by_created`: ordered by TaskCreatedOn as a DateTime.
+  m.def("tasks_from_query", [](py::bytes body, bool by_created) -> py::object {
     char* p;
     Py_ssize_t n;
     if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
     std::string out;
     size_t count = 0;
-    if (!taskcodec::query_tasks(std::string_view(p, (size_t)n), out, count)) return py::none();
-    return py::make_tuple(count, py::bytes(out));
-  });
+    bool more = false;
+    if (!taskcodec::query_tasks(std::string_view(p, (size_t)n), out, count, by_created, &more)) return py::none();
+    return py::make_tuple(count, py::bytes(out), more);
+  }, py::arg("body"), py::arg("by_created") = false);
 
   // TaskModel JSON -> taskName when it binds within the codec's envelope, else None.
   m.def("task_model_name", [](py::bytes body) -> py::object {
@@ -430,18 +432,20 @@ PYBIND11_MODULE(_ttnative, m) {
            py::arg("gen"), py::arg("from_row"), py::arg("kill_from"), py::arg("dict_sizes"))
       .def("mirror_results",
            [](DocStore& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> rows,
-              const std::string& prefix, const std::string& token) {
+              const std::string& prefix, const std::string& token, uint64_t gen) -> py::object {
              size_t skipped = 0;
              std::string out;
              const int32_t* p = rows.data();
              size_t n = (size_t)rows.size();
+             bool ok;
              {
                py::gil_scoped_release r;
-               out = s.mirror_results(p, n, prefix, token, &skipped);
+               ok = s.mirror_results(p, n, prefix, token, gen, out, &skipped);
              }
+             if (!ok) return py::none();  // the rows come from another mirror generation
              return py::make_tuple(py::bytes(out), skipped);
            },
-           py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "")
+           py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "", py::arg("gen") = 0)
       .def("mirror_stats", &DocStore::mirror_stats)
       .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"))
       .def("charge", &DocStore::charge, py::arg("ru"))

@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <ctime>
+#include <algorithm>
 #include <string>
 #include <string_view>
 #include <utility>
@@ -499,9 +500,25 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
 }
 
 // State-query response of the task collection (Dapr `{"results": [{"key", "data", "etag"}],
-// "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data, in order:
-// the API's GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).
-inline bool query_tasks(std::string_view body, std::string& out, size_t& count) {
+// "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data: the API's
+// GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).  With
+// `by_created` the tasks come out ordered by TaskCreatedOn as a DateTime, ascending and stable
+// (the reference's `.OrderBy(o => o.TaskCreatedOn)`, TasksStoreManager.cs:136): System.Text.Json
+// trims the fraction, so the strings do not sort chronologically within one second ("...:42Z"
+// is earlier than "...:42.1Z").  `more`: the response carries a continuation token.
+inline std::string created_sort_key(const std::string& canon) {
+  // "yyyy-MM-ddTHH:mm:ss[.f{1,6}][Z]" -> "yyyy-MM-ddTHH:mm:ss.ffffff" (fixed width)
+  std::string k = canon.substr(0, 19);
+  k += '.';
+  size_t i = 19, n = 0;
+  if (i < canon.size() && canon[i] == '.')
+    for (++i; i < canon.size() && canon[i] >= '0' && canon[i] <= '9'; ++i, ++n) k += canon[i];
+  for (; n < 6; ++n) k += '0';
+  return k;
+}
+
+inline bool query_tasks(std::string_view body, std::string& out, size_t& count, bool by_created = false,
+                        bool* more = nullptr) {
   if (!valid_utf8(body)) return false;
   tt::Value doc;
   try {
@@ -510,6 +527,10 @@ inline bool query_tasks(std::string_view body, std::string& out, size_t& count) 
     return false;
   }
   if (doc.t != tt::Value::Object) return false;
+  if (more) {
+    const tt::Value* tok = doc.get("token");
+    *more = tok != nullptr && tok->t == tt::Value::String && !tok->s.empty();
+  }
   const tt::Value* results = doc.get("results");
   if (results == nullptr || results->t == tt::Value::Null) {
     out = "[]";
@@ -517,15 +538,40 @@ inline bool query_tasks(std::string_view body, std::string& out, size_t& count) 
     return true;
   }
   if (results->t != tt::Value::Array) return false;
-  out.assign("[");
   count = 0;
   std::string id, day;
+  if (!by_created) {
+    out.assign("[");
+    for (const auto& r : results->items) {
+      if (r.t != tt::Value::Object) return false;
+      const tt::Value* data = r.get("data");
+      if (data == nullptr || data->t == tt::Value::Null) continue;
+      if (count++) out += ',';
+      if (!write_task(*data, false, out, id, day)) return false;
+    }
+    out += ']';
+    return true;
+  }
+  std::vector<std::pair<std::string, std::string>> rows;  // (fixed-width created key, task JSON)
+  rows.reserve(results->items.size());
   for (const auto& r : results->items) {
     if (r.t != tt::Value::Object) return false;
     const tt::Value* data = r.get("data");
     if (data == nullptr || data->t == tt::Value::Null) continue;
+    std::string one;
+    if (!write_task(*data, false, one, id, day)) return false;
+    // the canonical created-on string sits at a fixed spot: after `"taskCreatedOn":"`
+    size_t at = one.find("\"taskCreatedOn\":\"");
+    if (at == std::string::npos) return false;
+    at += 17;
+    size_t end = one.find('"', at);
+    rows.emplace_back(created_sort_key(one.substr(at, end - at)), std::move(one));
+  }
+  std::stable_sort(rows.begin(), rows.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  out.assign("[");
+  for (auto& r : rows) {
     if (count++) out += ',';
-    if (!write_task(*data, false, out, id, day)) return false;
+    out += r.second;
   }
   out += ']';
   return true;

@@ -16,6 +16,7 @@
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 
+#include <atomic>
 #include <cerrno>
 #include <memory>
 #include <stdexcept>
@@ -28,6 +29,12 @@ struct TlsConfig {
   std::string cert, key, ca;
   bool verify_peer = true;  // server: require a client certificate (mutual TLS); client: verify the server
 };
+
+// Server-side handshakes refused (no client certificate, one from another CA, a protocol
+// error before the handshake finished): the data plane's evidence that mTLS turned a peer away
+// (`sidecar_mtls_handshake_rejected_total` on its /metrics), independent of how the refused
+// client happened to report it.
+inline std::atomic<uint64_t> tls_server_handshake_rejects{0};
 
 inline std::string tls_error_text() {
   unsigned long e = ERR_get_error();
@@ -156,6 +163,8 @@ class TlsIo {
         return -1;
       default:
         last_error = tls_error_text();
+        if (SSL_is_server(ssl_) && !SSL_is_init_finished(ssl_))
+          tls_server_handshake_rejects.fetch_add(1, std::memory_order_relaxed);
         errno = ECONNRESET;  // handshake / verification failure or a corrupt record
         return -1;
     }

@@ -208,7 +208,8 @@ int main(int argc, char** argv) {
       if (i > 50) {
         MirrorDelta d = store.mirror_delta(i % 7 ? 0 : 2, 0, 0, {});
         int32_t rows[2] = {0, (int32_t)(d.n ? d.n - 1 : 0)};
-        store.mirror_results(rows, 2, "", "");
+        std::string res;
+        store.mirror_results(rows, 2, "", "", d.gen, res);
       }
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     }

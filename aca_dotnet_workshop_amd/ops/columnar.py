@@ -264,16 +264,66 @@ class Column:
     def ranks(self) -> np.ndarray:
         """Sort rank of every dictionary id (ties share a rank, ranks start at 1)."""
         if self._rank_cache is None:
-            import functools
-            order = sorted(range(len(self.values)), key=functools.cmp_to_key(lambda a, b: compare(self.values[a], self.values[b])))
-            r = np.empty(len(order), dtype=np.int64)
-            rank = 0
-            for pos, i in enumerate(order):
-                if pos and compare(self.values[order[pos - 1]], self.values[i]) != 0:
-                    rank += 1
-                r[i] = rank + 1  # 0 reserved for missing (sorts like null, first)
-            self._rank_cache = r
+            self._rank_cache = self._string_ranks() if self._all_strings() else self._general_ranks()
         return self._rank_cache
+
+    def _all_strings(self) -> bool:
+        n0 = getattr(self, "_str_checked", 0)
+        if n0 > len(self.values):  # dictionary rebuilt
+            n0 = 0
+            self._str_sorted = None
+        # (numpy's fixed-width strings drop trailing NULs: such values take the general path)
+        ok = all(type(v) is str and not v.endswith("\x00") for v in self.values[n0:])
+        if ok:
+            self._str_checked = len(self.values)
+        else:
+            self._str_checked = 0
+            self._str_sorted = None
+        return ok
+
+    def _string_ranks(self) -> np.ndarray:
+        """A dictionary of strings only (timestamps, e-mails, names): distinct values never tie
+        and Python's string order is ``compare``'s, so the ranks are positions in the sorted
+        dictionary.  Kept incrementally: values appended since the last call are sorted alone
+        and merged in (``searchsorted`` + ``insert``), an O(dictionary) vector pass instead of a
+        comparison sort of the whole dictionary per new value -- the overdue sweep orders by
+        ``taskCreatedOn``, whose dictionary grows with every created task."""
+        n = len(self.values)
+        prev = getattr(self, "_str_sorted", None)
+        if prev is None or prev[1] > n:
+            arr = np.array(self.values, dtype=str) if n else np.zeros(0, dtype="<U1")
+            order = np.argsort(arr, kind="stable")
+            r = np.empty(n, dtype=np.int64)
+            r[order] = np.arange(1, n + 1)
+            self._str_sorted = (arr[order], n, r)
+            return r.copy()
+        srt, m, old_r = prev
+        if m == n:
+            return old_r.copy()
+        new = np.array(self.values[m:], dtype=str)
+        width = max(srt.dtype.itemsize, new.dtype.itemsize) // 4
+        srt = srt.astype(f"<U{max(width, 1)}", copy=False)
+        new = new.astype(srt.dtype, copy=False)
+        norder = np.argsort(new, kind="stable")
+        new_sorted = new[norder]
+        pos = np.searchsorted(srt, new_sorted)            # insertion points in the old order
+        before = np.searchsorted(pos, old_r - 1, side="right")  # new values ahead of each old one
+        r = np.empty(n, dtype=np.int64)
+        r[:m] = old_r + before
+        r[m + norder] = pos + np.arange(new.size) + 1
+        self._str_sorted = (np.insert(srt, pos, new_sorted), n, r)
+        return r.copy()
+
+    def _general_ranks(self) -> np.ndarray:
+        import functools
+        order = sorted(range(len(self.values)), key=functools.cmp_to_key(lambda a, b: compare(self.values[a], self.values[b])))
+        r = np.empty(len(order), dtype=np.int64)
+        rank = 0
+        for pos, i in enumerate(order):
+            if pos and compare(self.values[order[pos - 1]], self.values[i]) != 0:
+                rank += 1
+            r[i] = rank + 1  # 0 reserved for missing (sorts like null, first)
+        return r
 
 
 @dataclass
@@ -415,6 +465,11 @@ class ColumnarIndex:
         if changed:
             self.version += 1
         return bool(changed)
+
+    @property
+    def generation(self) -> int:
+        """Mirror generation the row numbers belong to (``DocStore.mirror_results`` checks it)."""
+        return int(self._ncur[0]) if getattr(self, "native", None) is not None else 0
 
     @property
     def row_of(self) -> dict[str, int]:

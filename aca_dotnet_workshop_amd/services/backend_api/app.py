@@ -40,6 +40,7 @@ from .managers import FakeTasksManager, TasksManager, TasksStoreManager
 ROLE = "tasksmanager-backend-api"
 CONTENT_ROOT = Path(__file__).parent
 log = logging.getLogger("TasksController")
+MORE_HEADER = "x-tt-more-results"  # GET api/overduetasks?limit= in range mode: the store has more matches
 
 
 def _task_id(req: Request) -> uuid.UUID:
@@ -108,9 +109,13 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
         raw = req.query_get("limit") or ""
         limit = int(raw) if raw.isdigit() else None  # page size of the range sweep (OverdueTasks:Query=range)
         if fast_page is not None:
-            body = await fast_page(limit)
-            if body is not None:
-                return _json(body)
+            made = await fast_page(limit)
+            if made is not None:
+                # the sweep pages until the store reports no more matches, not until a short page:
+                # rows changed since the store's selection are skipped and shorten a page
+                resp = _json(made[0])
+                resp.headers.append((MORE_HEADER, "true" if made[1] else "false"))
+                return resp
         return _json(tasks_to_json(await manager.get_yesterdays_due_tasks(limit)))
 
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",

@@ -268,29 +268,36 @@ class TasksStoreManager(TasksManager):
         tasks.sort(key=_created_key)
         return tasks
 
-    async def overdue_page_json(self, limit: int | None = None) -> bytes | None:
+    async def overdue_page_json(self, limit: int | None = None) -> tuple[bytes, bool] | None:
         """``get_yesterdays_due_tasks`` as the response body, for the range sweep: the query
-        results turned into the TaskModel JSON array in one native pass
-        (``models.tasks_from_query_wire``).  ``None``: equality mode, or a response outside the
-        codec's envelope -- the caller binds the TaskModels."""
+        results turned into the TaskModel JSON array in one native pass, ordered by
+        ``TaskCreatedOn`` (``models.tasks_from_query_wire``), plus whether the store has more
+        matches than this page (its continuation token).  ``None``: equality mode, or a response
+        outside the codec's envelope -- the caller binds the TaskModels."""
         raw_query = getattr(self.client, "query_state_raw", None)
         if self.overdue_query != "range" or raw_query is None:
             return None
         q, midnight, page = self._range_query(limit)
         log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
         raw = await raw_query(self.store, q)
-        made = tasks_from_query_wire(raw)
+        made = tasks_from_query_wire(raw, by_created=True)
         if made is not None:
-            return made[1]
-        results = (json.loads(raw) if raw else {}).get("results") or []
-        return ("[" + ",".join(TaskModel.model_validate(r["data"]).to_json() for r in results
-                               if r.get("data") is not None) + "]").encode()
+            return made[1], made[2]
+        doc = json.loads(raw) if raw else {}
+        tasks = [TaskModel.model_validate(r["data"]) for r in doc.get("results") or [] if r.get("data") is not None]
+        tasks.sort(key=_created_key)
+        return ("[" + ",".join(t.to_json() for t in tasks) + "]").encode(), bool(doc.get("token"))
 
     def _range_query(self, limit: int | None) -> tuple[dict, str, int]:
+        """The open tasks due before today's midnight, oldest first: ``ORDER BY taskCreatedOn``
+        in the store picks the page (reference ``.OrderBy(o => o.TaskCreatedOn)``,
+        TasksStoreManager.cs:136); the page itself is then ordered by the DateTime value (the
+        stored strings carry a trimmed fraction, see ``tasks_from_query_wire``)."""
         midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
         page = limit if limit and limit > 0 else self.overdue_page
         q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
                                 {"EQ": {"isOverDue": False}}]},
+             "sort": [{"key": "taskCreatedOn", "order": "ASC"}],
              "page": {"limit": page}}
         return q, midnight, page
 
@@ -303,7 +310,9 @@ class TasksStoreManager(TasksManager):
         q, midnight, page = self._range_query(limit)
         log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
         resp = await self.client.query_state(self.store, q)
-        return [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
+        tasks = [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
+        tasks.sort(key=_created_key)
+        return tasks
 
     async def mark_overdue_from_body(self, body: bytes) -> bool:
         """``mark_overdue_tasks`` straight from the request body (``models.mark_overdue_wire``:

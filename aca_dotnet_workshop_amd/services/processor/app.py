@@ -161,7 +161,15 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                 data = RawJson(overdue.decode()) if isinstance(overdue, bytes) else overdue
                 await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
                 marked += n_overdue
-            if page <= 0 or n_page < page or not n_overdue:
+            if page <= 0:
+                break
+            more = (r.headers.get("x-tt-more-results") or "").lower()
+            if more:  # the API says whether the store holds more matches than this page
+                # a short (even empty) page with more matches: rows that changed after the
+                # store's selection were skipped -- ask again; a page of nothing to mark stops
+                if more != "true" or (n_page and not n_overdue):
+                    break
+            elif n_page < page or not n_overdue:
                 break
         return json_response({"runAt": run_at.isoformat(), "retrieved": retrieved, "markedOverdue": marked,
                               "pages": pages})

@@ -270,7 +270,7 @@ def main() -> None:
            # logs as structured JSON into the environment's telemetry dir (Log Analytics), not the console
            "TT_TELEMETRY_DIR": os.path.join(root, "telemetry"), "TT_LOG_CONSOLE": "0", **rank_device_env()}
     if sweep:  # the task collection's column mirror is maintained from its first write
-        env["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue"
+        env["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue,taskCreatedOn"
     shared = a.shared_env and d.world > 1
     if shared and a.client != "native":
         raise SystemExit("--shared-env needs the native load generator")

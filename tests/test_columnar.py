@@ -706,7 +706,7 @@ def test_native_mirror_index_matches_native(docs, flt, sort, seed):
         q["sort"] = sort
     want = json.loads(store.query(json.dumps(q)))["results"]
     rows, _ = ix.query_rows(q)  # may add columns -> new generation, full reload
-    got = json.loads(store.mirror_results(rows, "", "")[0])["results"]
+    got = json.loads(store.mirror_results(rows, "", "", gen=ix.generation)[0])["results"]
     assert got == want
 
 
@@ -731,10 +731,73 @@ def test_native_mirror_compacts_and_tracks_updates():
         full = dict(q, page={})
         want = [r["key"] for r in json.loads(store.query(json.dumps(full)))["results"]]
         rows, _ = ix.query_rows(full)
-        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "")[0])["results"]]
+        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "", gen=ix.generation)[0])["results"]]
         assert got == want
     assert store.mirror_stats()["compactions"] >= 1
     assert ix.n <= 2 * 20000 + 65536
+
+
+def _compact_mirror(store, n: int) -> None:
+    """Rewrite every document until the store compacts its mirror (a new generation)."""
+    before = store.mirror_stats()["compactions"]
+    for rnd in range(8):
+        for i in range(n):
+            store.set(f"k{i}", json.dumps({"n": i % 100, "done": True}))
+        if store.mirror_stats()["compactions"] > before:
+            return
+    raise AssertionError("the mirror never compacted")
+
+
+def test_mirror_results_refuses_rows_of_another_generation():
+    """Row numbers selected before a compaction must not be mapped onto the renumbered mirror:
+    the store answers None (stale) instead of returning whatever document now sits there."""
+    store = N.DocStore()
+    n = 40000
+    for i in range(n):
+        store.set(f"k{i}", json.dumps({"n": i % 100, "done": False}))
+    ix = ColumnarIndex.from_native(store, ["n", "done"])
+    q = {"filter": {"AND": [{"LT": {"n": 10}}, {"EQ": {"done": False}}]}}
+    rows, _ = ix.query_rows(q)
+    gen = ix.generation
+    assert store.mirror_results(rows, "", "", gen=gen) is not None
+    _compact_mirror(store, n)
+    assert store.mirror_results(rows, "", "", gen=gen) is None
+    ix.sync()
+    rows, _ = ix.query_rows(q)
+    assert json.loads(store.mirror_results(rows, "", "", gen=ix.generation)[0])["results"] == []
+
+
+def test_accelerator_reselects_after_a_concurrent_compaction():
+    """A compaction that lands between the accelerator's selection and the result lookup (a
+    GIL-free native write) makes it re-sync and select again: every returned document matches
+    the filter (a stale row could name a completed task for the overdue sweep)."""
+    from aca_dotnet_workshop_amd.backing.accel import CollectionAccelerator
+    store = N.DocStore()
+    n = 40000
+    for i in range(n):
+        store.set(f"k{i}", json.dumps({"n": i % 100, "done": i % 2 == 0}))
+    acc = CollectionAccelerator("cpu", 0)
+    q = {"filter": {"AND": [{"LT": {"n": 10}}, {"EQ": {"done": False}}]}}
+    assert acc.query(q, "", store) is not None  # builds the mirror-fed index
+    real = acc.index.query_rows
+    fired = []
+
+    def racing_query_rows(qq, k=None):
+        out = real(qq, k)
+        if not fired:  # the race: the store compacts right after the selection
+            fired.append(1)
+            for rnd in range(8):
+                for i in range(n):
+                    store.set(f"k{i}", json.dumps({"n": (i + 7) % 100, "done": (i + rnd) % 3 == 0}))
+                if store.mirror_stats()["compactions"]:
+                    break
+        return out
+    acc.index.query_rows = racing_query_rows
+    res = json.loads(acc.query(q, "", store))["results"]
+    assert fired and acc.stats.get("stale_retries", 0) >= 1
+    want = json.loads(store.query(json.dumps(q)))["results"]
+    assert sorted(r["key"] for r in res) == sorted(r["key"] for r in want)
+    assert all(r["data"]["n"] < 10 and not r["data"]["done"] for r in res)
 
 
 @pytest.mark.gpu
@@ -753,7 +816,7 @@ def test_gpu_native_mirror_matches_native():
     for round_ in range(5):
         ix.sync()
         rows, _ = ix.query_rows(q, k)
-        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "")[0])["results"]]
+        got = [r["key"] for r in json.loads(store.mirror_results(rows, "", "", gen=ix.generation)[0])["results"]]
         want = [r["key"] for r in json.loads(store.query(json.dumps(q)))["results"]]
         assert got == want, round_
         for _ in range(3000):  # mark some overdue, complete some, add new due dates, delete some
@@ -764,3 +827,20 @@ def test_gpu_native_mirror_matches_native():
             else:
                 store.set(f"k{i}", json.dumps({"d": f"2024-0{rnd.randrange(4, 7)}-{rnd.randrange(1, 29):02d}T00:00:00",
                                                "c": r < 0.4, "o": r > 0.8}))
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.lists(st.text(max_size=6), max_size=30), min_size=1, max_size=6))
+def test_string_ranks_incremental_match_the_comparison_sort(batches):
+    """The incremental string-dictionary ranks (merge of each batch of new values) equal the
+    general comparison sort after every batch; a non-string value switches to the general path."""
+    from aca_dotnet_workshop_amd.ops.columnar import Column
+    c = Column("p")
+    for b in batches:
+        for v in b:
+            c.encode(v)
+        c._rank_cache = None
+        assert c.ranks().tolist() == c._general_ranks().tolist()
+    c.encode(5)
+    c._rank_cache = None
+    assert c.ranks().tolist() == c._general_ranks().tolist()

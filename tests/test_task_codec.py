@@ -297,7 +297,23 @@ def test_query_results_to_tasks(results):
     body = json.dumps({"results": results, "token": "100"}).encode()
     made = tasks_from_query_wire(body)
     want = [TaskModel.model_validate(r["data"]).to_wire() for r in results or [] if r.get("data") is not None]
-    assert made is not None and made[0] == len(want) and json.loads(made[1]) == want
+    assert made is not None and made[0] == len(want) and json.loads(made[1]) == want and made[2] is True
+
+
+def test_query_results_ordered_by_created_datetime():
+    """``by_created``: DateTime order, not string order -- System.Text.Json trims the fraction,
+    so "...:42Z" < "...:42.1Z" < "...:42.12Z" chronologically although not as strings."""
+    from aca_dotnet_workshop_amd.models import tasks_from_query_wire
+    stamps = ["2026-01-02T03:04:42.12Z", "2026-01-02T03:04:42Z", "2026-01-01T23:59:59.9999Z",
+              "2026-01-02T03:04:42.1Z", "2026-01-02T03:04:43Z", "2026-01-02T03:04:42.12Z"]
+    results = [{"key": str(i), "data": {**_TASK, "taskId": f"00000000-0000-0000-0000-00000000000{i}",
+                                        "taskCreatedOn": t}} for i, t in enumerate(stamps)]
+    made = tasks_from_query_wire(json.dumps({"results": results}).encode(), by_created=True)
+    got = [(t["taskCreatedOn"], t["taskId"][-1]) for t in json.loads(made[1])]
+    want = sorted(((TaskModel.model_validate(r["data"]), r["key"]) for r in results),
+                  key=lambda x: x[0].task_created_on)
+    assert [k for _, k in got] == [k for _, k in want]  # stable: the two equal stamps keep their order
+    assert made[2] is False
 
 
 @pytest.mark.parametrize("body", [b"[]", b'{"results": 5}', b'{"results": [{"data": "text"}]}',
