@@ -477,7 +477,10 @@ class DocStore {
 
   int64_t charge(double ru) {
     std::lock_guard<std::mutex> g(ru_mu_);
-    if (ru_rate_ <= 0) return 0;
+    if (ru_rate_ <= 0) {  // not provisioned: admitted, still metered (what the workload would need)
+      ru_consumed_ += ru;
+      return 0;
+    }
     double now = mono_s();
     ru_tokens_ = std::min(ru_rate_, ru_tokens_ + (now - ru_last_) * ru_rate_);
     ru_last_ = now;

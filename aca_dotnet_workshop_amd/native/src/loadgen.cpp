@@ -6,7 +6,8 @@
 // the batch size -- bench.py uses it to wait until the processor acknowledged every task.
 // `--until-base N --until-stride M`: start from counter value N and require an advance of M per
 // step (several generators sharing one subscription: M = ranks x batch).
-// Request bodies come from a file with one body per line (cycled).  Prints one JSON line:
+// Request bodies come from a file with one body per line (cycled); `--header "name: value"`
+// (repeatable) adds request headers (the frontend entry sends its cookies).  Prints one JSON line:
 // {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
 //
 //   ttloadgen --target unix:/path/a.sock --target unix:/path/b.sock 
@@ -31,6 +32,7 @@ struct Opts {
   std::vector<ev::Endpoint> targets;
   std::string path = "/", method = "POST", ctype = "application/json", until_url, until_field = "completed";
   std::vector<std::string> bodies{""};
+  ev::HeaderList headers;
   int concurrency = 64, batch = 512, steps = 1, expect = 0;
   // shared environments (bench.py --shared-env): several generators drive one subscription, so
   // the counter's starting point and its advance per step are global, not this generator's own
@@ -40,6 +42,8 @@ struct Opts {
 class Gen {
  public:
   Gen(ev::Loop& loop, Opts o) : loop_(loop), client_(loop), o_(std::move(o)) {
+    hdrs_.emplace_back("content-type", o_.ctype);
+    for (auto& h : o_.headers) hdrs_.push_back(h);
     if (!o_.until_url.empty()) {
       std::string u = o_.until_url;
       if (u.rfind("http://", 0) == 0) u = u.substr(7);
@@ -86,6 +90,7 @@ class Gen {
   ev::Loop& loop_;
   ev::Client client_;
   Opts o_;
+  ev::HeaderList hdrs_;
   ev::Endpoint until_ep_;
   std::string until_target_;
   double t0_ = 0, t1_ = 0;
@@ -116,7 +121,7 @@ class Gen {
     const ev::Endpoint& ep = o_.targets[rr_++ % o_.targets.size()];
     const std::string& body = o_.bodies[(size_t)((step_ * (long long)o_.batch + i) % (long long)o_.bodies.size())];
     double t = ev::now_s();
-    client_.request(ep, o_.method, o_.path, {{"content-type", o_.ctype}}, body, 60, [this, t](ev::ClientResult&& r) {
+    client_.request(ep, o_.method, o_.path, hdrs_, body, 60, [this, t](ev::ClientResult&& r) {
       lat_.push_back(ev::now_s() - t);
       bool bad = r.err || (o_.expect && r.resp.status != o_.expect);
       if (bad) {
@@ -191,6 +196,18 @@ int main(int argc, char** argv) {
     else if (a == "--path") o.path = next();
     else if (a == "--method") o.method = next();
     else if (a == "--content-type") o.ctype = next();
+    else if (a == "--header") {
+      std::string h = next();
+      size_t c = h.find(':');
+      if (c == std::string::npos) {
+        std::fprintf(stderr, "--header wants \"name: value\"\n");
+        return 2;
+      }
+      std::string name = h.substr(0, c), value = h.substr(c + 1);
+      for (char& ch : name) ch = (char)std::tolower((unsigned char)ch);
+      while (!value.empty() && value.front() == ' ') value.erase(0, 1);
+      o.headers.emplace_back(name, value);
+    }
     else if (a == "--concurrency") o.concurrency = std::max(1, std::atoi(next().c_str()));
     else if (a == "--batch") o.batch = std::max(1, std::atoi(next().c_str()));
     else if (a == "--steps") o.steps = std::max(0, std::atoi(next().c_str()));

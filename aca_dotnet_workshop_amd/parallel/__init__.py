@@ -20,7 +20,8 @@ from __future__ import annotations
 import os
 import sys
 
-__all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling", "partition_cpus", "pin_rank"]
+__all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling", "partition_cpus", "pin_rank", "gpu_numa_nodes",
+           "PIN_INFO"]
 
 
 class Dist:
@@ -129,25 +130,86 @@ def partition_cpus(allowed: set[int], nodes: list[set[int]], core: dict[int, int
     return cpus if len(cpus) >= min_cpus else None
 
 
-def pin_rank(local_rank: int, local_world: int, spec: str | None = None) -> set[int] | None:
+PIN_INFO: dict[str, str] = {}  # how the last pin_rank chose its CPUs (for the bench report)
+
+
+def gpu_numa_nodes(sysfs: str = "/sys/class/drm") -> list[int]:
+    """NUMA node of every AMD GPU, in PCI address order -- the order HIP numbers the devices (a
+    rank with ``HIP_VISIBLE_DEVICES=<local rank>`` drives the ``<local rank>``-th).  -1 where
+    sysfs has no node.  Read from sysfs only: no HIP context is opened."""
+    out: dict[str, int] = {}
+    try:
+        names = os.listdir(sysfs)
+    except OSError:
+        return []
+    for d in names:
+        if not (d.startswith("card") and d[4:].isdigit()):
+            continue
+        dev = os.path.join(sysfs, d, "device")
+        try:
+            if open(os.path.join(dev, "vendor")).read().strip() != "0x1002":
+                continue
+            bdf = os.path.basename(os.path.realpath(dev))
+            node = int(open(os.path.join(dev, "numa_node")).read().strip())
+        except (OSError, ValueError):
+            continue
+        out[bdf] = node
+    return [out[k] for k in sorted(out)]
+
+
+def rank_gpu_node(local_rank: int, nodes: list[set[int]], gpu_nodes: list[int] | None = None) -> int | None:
+    """Index into ``nodes`` of the NUMA node the rank's GPU hangs off, when known."""
+    gpu_nodes = gpu_numa_nodes() if gpu_nodes is None else gpu_nodes
+    visible = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    idx = local_rank
+    if visible:
+        ids = [x for x in visible.split(",") if x.strip().isdigit()]
+        if ids:
+            idx = int(ids[0]) if len(ids) == 1 else int(ids[local_rank % len(ids)])
+    if not gpu_nodes or idx >= len(gpu_nodes) or gpu_nodes[idx] < 0 or gpu_nodes[idx] >= len(nodes):
+        return None
+    return gpu_nodes[idx]
+
+
+def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
+             gpu_nodes: list[int] | None = None) -> set[int] | None:
     """Pin this process (and every child it starts later) to its rank's CPU partition.
-    ``spec`` (default ``$TT_BENCH_PIN``): ``0`` never pins; with several ranks on the host any
-    other value partitions (``partition_cpus``); a single rank pins to its first NUMA node on
-    ``1`` (default) / ``node``, or to ``<n>`` > 1 CPUs of that node (whole cores first).  On the
-    MI355X box one stack on one socket ran +24 % vs unpinned (profiles/r2_rank_pinning.md)."""
+    ``spec`` (default ``$TT_BENCH_PIN``): ``0`` never pins; otherwise the rank's CPUs come from
+    the NUMA node of its own GPU when sysfs names one (``gpu_numa_nodes``), shared with the
+    other ranks whose GPUs sit on that node (whole cores each); without that, ranks split the
+    nodes (``partition_cpus``) and a single rank takes its first node.  ``<n>`` > 1 (single
+    rank): only n CPUs of that node.  On the MI355X box one stack on one socket ran +24 % vs
+    unpinned (profiles/r2_rank_pinning.md)."""
     spec = os.environ.get("TT_BENCH_PIN", "1") if spec is None else spec
+    PIN_INFO.clear()
     if spec == "0":
         return None
     nodes, core = host_topology()
     allowed = set(os.sched_getaffinity(0))
-    if local_world > 1:
+    gnodes = gpu_numa_nodes() if gpu_nodes is None else gpu_nodes
+    mine = rank_gpu_node(local_rank, nodes, gnodes)
+    cpus = None
+    if mine is not None and nodes[mine] & allowed:
+        # the ranks whose GPUs share my node split its CPUs, whole cores each
+        peers = [r for r in range(max(1, local_world)) if rank_gpu_node(r, nodes, gnodes) == mine]
+        if local_rank not in peers:
+            peers = [local_rank]
+        order = sorted(nodes[mine] & allowed, key=lambda c: (core.get(c, c), c))
+        k, i = len(peers), peers.index(local_rank)
+        cpus = set(order[i * len(order) // k:(i + 1) * len(order) // k])
+        if local_world <= 1 and spec.isdigit() and int(spec) > 1:
+            cpus = set(order[:int(spec)])
+        PIN_INFO["mode"] = f"GPU-local NUMA node {mine}, whole cores"
+        if len(cpus) < 2:
+            cpus = None
+    if cpus is None and local_world > 1:
         cpus = partition_cpus(allowed, nodes, core, local_rank, local_world)
-    elif spec in ("1", "node") or spec.isdigit() and int(spec) > 1:
+        PIN_INFO["mode"] = "NUMA-local whole cores (rank order)"
+    elif cpus is None and (spec in ("1", "node") or spec.isdigit() and int(spec) > 1):
         first = next((n & allowed for n in nodes if n & allowed), allowed)
         order = sorted(first, key=lambda c: (core.get(c, c), c))
         cpus = set(order if spec in ("1", "node") else order[:int(spec)])
-    else:
-        cpus = None
+        PIN_INFO["mode"] = "first NUMA node, whole cores"
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus

@@ -238,8 +238,23 @@ class EnvironmentController:
         self.event("DaprComponentsInstalled", components=[c["name"] for c in self.m.components])
 
     # ------------------------------------------------------------------ apps
+    def _generated_secret(self, app: str, name: str) -> str:
+        """A ``generate: true`` app secret: random, created once per environment and kept in the
+        environment directory (every replica and revision of the app gets the same value)."""
+        f = self.dir / "generated-secrets.json"
+        vals = json.loads(f.read_text()) if f.exists() else {}
+        key = f"{app}/{name}"
+        if key not in vals:
+            vals[key] = pysecrets.token_hex(32)
+            tmp = self.dir / "generated-secrets.json.tmp"
+            tmp.write_text(json.dumps(vals))
+            os.chmod(tmp, 0o600)
+            os.replace(tmp, f)
+        return vals[key]
+
     def _app_env(self, spec: dict[str, Any]) -> dict[str, str]:
-        secrets = {s["name"]: str(s.get("value", "")) for s in spec.get("secrets") or []}
+        secrets = {s["name"]: self._generated_secret(spec["name"], s["name"]) if _truthy(s.get("generate", False))
+                   else str(s.get("value", "")) for s in spec.get("secrets") or []}
         env: dict[str, str] = {"TT_APP_SECRETS": json.dumps(secrets), "TT_ROLE_NAME": spec["name"]}
         for e in spec.get("env") or []:
             v = secrets.get(e["secretRef"], "") if "secretRef" in e else e.get("value", "")

@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: end-to-end task-creation throughput of the Tasks Tracker mesh.
+"""Flagship benchmark: end-to-end task-creation throughput of the Tasks Tracker environment.
 
 The reference publishes no throughput number (BASELINE.md "Not published"),
-so this measures the survey's flagship flow (SURVEY.md §3.1 ``createTask``) on our stack
-and reports it as a *new* measurement (``vs_baseline: null``):
+so this measures the survey's flagship flow (SURVEY.md §3.1 ``createTask``) and reports it as a
+*new* measurement (``vs_baseline: null``).  Default (``--entry frontend``): the environment is
+deployed from ``deploy/main.yaml`` by the platform controller (the ``az deployment`` + ACA
+equivalent: backing services, RBAC, Dapr components, mTLS identities, revisions, replicas,
+resource limits) and load enters where a browser's does -- the frontend's Create page:
 
-    client -> API sidecar (invoke) -> Backend API -> sidecar state save -> backing "Cosmos"
-                                                 -> sidecar publish    -> backing "Service Bus"
-           -> processor sidecar (peek-lock receive) -> Processor /api/tasksnotifier/tasksaved -> complete
+    POST /Tasks/Create (form + cookies)  -> Frontend app (Pages/Tasks/Create.cshtml.cs:46)
+      -> frontend sidecar invoke -> mTLS -> API sidecar -> Backend API (TasksController.Post)
+         -> state save -> backing "Cosmos" (RU/s budget) ; publish -> backing "Service Bus"
+      <- 201 <- 302 redirect to /Tasks/Index
+    processor sidecar (peek-lock) -> Processor /api/tasksnotifier/tasksaved -> complete
 
-One step = ``--batch`` createTask requests issued with ``--concurrency`` in flight, and the
-step ends only when the processor's subscription has completed every message of the batch
-(persisted AND delivered AND acknowledged).  Each rank runs its own full environment
-(backing services + API/processor apps + their sidecars as separate OS processes) -- weak
-scaling, like adding ACA environments.  Rank 0 prints ONE JSON line with the aggregate
-tasks/s over all ranks (time = max over ranks).
+One step = ``--batch`` creates with ``--concurrency`` in flight; a step ends only when the
+processor's subscription completed every message of the batch (persisted AND delivered AND
+acknowledged).  ``config`` states the entry, mTLS, the RU/s budget, the CPU limits and every
+replica count; ``config.api_sidecar_direct`` is a second, shorter run in the same environment
+with load sent straight to the API sidecars' invoke (round 2's headline topology).
+``--entry api-sidecar`` runs round 2's hand-assembled ``LocalStack`` instead.
+
+Each rank runs its own environment (weak scaling, like adding Container Apps environments);
+rank 0 prints ONE JSON line with the aggregate tasks/s (time = max over ranks).
 
     python bench.py --gpus N --steps K --warmup W
 """
@@ -66,6 +74,21 @@ def parse() -> argparse.Namespace:
                          "reference's KEDA scale axis); default: one environment per rank (weak scaling)")
     ap.add_argument("--client", choices=("native", "python"), default="native",
                     help="load generator: native/bin/ttloadgen (C++) or the in-process asyncio client")
+    ap.add_argument("--entry", choices=("frontend", "api-sidecar"), default="frontend",
+                    help="frontend: manifest-deployed environment, load at the frontend's POST /Tasks/Create "
+                         "(SURVEY §3.1); api-sidecar: round 2's LocalStack with load at the API sidecars")
+    ap.add_argument("--frontend-replicas", type=int, default=0, help="frontend replicas (0 = size to the CPU share)")
+    ap.add_argument("--mtls", type=int, choices=(0, 1), default=1, help="sidecar-to-sidecar mutual TLS (ACA default: on)")
+    ap.add_argument("--ru-per-s", type=float, default=0.0,
+                    help="Cosmos container throughput budget in RU/s (reference: 4000 autoscale max); 0 = unlimited")
+    ap.add_argument("--cpu-limits", type=int, choices=(0, 1), default=1,
+                    help="enforce each replica's vCPU share (manifest resourceLimits.cpu)")
+    ap.add_argument("--app-cpu", type=float, default=0.0,
+                    help="vCPU per replica (reference: 0.25); 0 = this rank's CPUs divided over its replicas")
+    ap.add_argument("--trace-sampling", type=float, default=1.0,
+                    help="App Insights sampling percentage of request traces (the manifest default is 100)")
+    ap.add_argument("--direct-steps", type=int, default=-1,
+                    help="steps of the api_sidecar_direct comparison run (-1 = a quarter of --steps, 0 = skip)")
     return ap.parse_args()
 
 
@@ -212,7 +235,7 @@ def _counter(url: str) -> int:
 def _collection_stats(backing: str) -> dict:
     import urllib.request
     url = f"{backing}/cosmos/taskstracker-state-store/tasksmanagerdb/taskscollection/stats"
-    req = urllib.request.Request(url, headers={"x-tt-identity": "bench"})
+    req = urllib.request.Request(url, headers={"x-tt-identity": "platform-admin"})  # the environment owner
     try:
         with urllib.request.urlopen(req, timeout=30) as r:
             return json.loads(r.read())
@@ -244,12 +267,22 @@ def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: 
 def main() -> None:
     a = parse()
     d = Dist()
-    n = d.world if d.world > 1 else a.gpus
     local = int(os.environ.get("LOCAL_WORLD_SIZE", d.world if d.world > 1 else 1))
-    cores = cpu_budget() / max(1, local)
     from aca_dotnet_workshop_amd.parallel import pin_rank
-    # ranks sharing a host get disjoint NUMA-local core sets (inherited by the whole stack)
+    # ranks sharing a host get disjoint NUMA-local core sets (inherited by the whole stack), on
+    # the NUMA node of the rank's GPU when sysfs tells; the CPU budget is read after pinning
+    share = cpu_budget() / max(1, local)  # a job-wide CPU quota is shared by the host's ranks
     pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local)
+    cores = min(cpu_budget(), share) if pinned else share
+    if a.entry == "frontend":
+        if a.shared_env and d.world > 1:
+            raise SystemExit("--shared-env is an --entry api-sidecar mode")
+        return main_frontend(a, d, cores, pinned)
+    return main_localstack(a, d, cores, pinned)
+
+
+def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
+    n = d.world if d.world > 1 else a.gpus
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
@@ -394,8 +427,8 @@ def main() -> None:
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
                            "sidecar_api_protocol": a.api_protocol,
                            "app_host": a.app_host,
-                           "cpu_pinning": (f"{len(pinned)} CPUs per rank (NUMA-local whole cores)"
-                                           if pinned else "none"),
+                           "cpu_pinning": pin_label(pinned),
+                           "entry": "api-sidecar", "mtls": False, "ru_per_s": None, "cpu_limits": None,
                            "create_latency_p50_ms": round(p50, 3),
                            "create_latency_p99_ms": round(p99, 3), "baseline": "reference publishes no throughput",
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
@@ -412,6 +445,219 @@ def main() -> None:
         d.close()
         if not os.environ.get("TT_BENCH_KEEP"):
             import shutil
+            shutil.rmtree(root, ignore_errors=True)
+
+
+def pin_label(pinned) -> str:
+    from aca_dotnet_workshop_amd.parallel import PIN_INFO
+    if not pinned:
+        return "none"
+    return f"{len(pinned)} CPUs per rank ({PIN_INFO.get('mode', 'pinned')})"
+
+
+FRONTEND, API, PROC = "tasksmanager-frontend-webapp", "tasksmanager-backend-api", "tasksmanager-backend-processor"
+
+
+def frontend_topology(cores: float) -> tuple[int, int, int]:
+    """(frontend, API, processor) replicas for one rank's CPU share: the two Python web apps on
+    the request path get one replica per ~4 CPUs each, the processor (its app only acks) half."""
+    fe = max(1, min(12, int(cores / 4)))
+    return fe, fe, max(1, min(8, int(cores / 8)))
+
+
+def _form_session(port: int, created_by: str) -> tuple[str, str]:
+    """What a browser holds after opening Tasks/Create: (Cookie header, antiforgery token)."""
+    import re
+    import urllib.request
+    req = urllib.request.Request(f"http://127.0.0.1:{port}/Tasks/Create",
+                                 headers={"Cookie": f"TasksCreatedByCookie={created_by}"})
+    with urllib.request.urlopen(req, timeout=30) as r:
+        html = r.read().decode()
+        cookies = [c.split(";", 1)[0] for c in r.headers.get_all("Set-Cookie") or []]
+    m = re.search(r'name="__RequestVerificationToken" value="([^"]+)"', html)
+    if not m or not cookies:
+        raise RuntimeError("Tasks/Create did not hand out an antiforgery cookie and token")
+    return "; ".join([f"TasksCreatedByCookie={created_by}"] + cookies), m.group(1)
+
+
+def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
+    """The Create page's form posts (Pages/Tasks/Create.cshtml: TaskAdd.* fields, type=date)."""
+    from datetime import timedelta
+    from urllib.parse import urlencode
+
+    from aca_dotnet_workshop_amd.models import today
+    yesterday = (today() - timedelta(days=1)).strftime("%Y-%m-%d")
+    return [urlencode({"__RequestVerificationToken": token, "TaskAdd.TaskName": f"bench task {i}",
+                       "TaskAdd.TaskDueDate": yesterday if past_due_every and i % past_due_every == 0 else "2030-01-01",
+                       "TaskAdd.TaskAssignedTo": f"assignee{i % 13}@bench.local"}).encode()
+            for i in range(batch)]
+
+
+def run_form_loadgen(exe: str, ports: list[int], cookie: str, counts_url: str, steps: int, batch: int, conc: int,
+                     bodies_file: str) -> tuple[float, dict]:
+    import subprocess
+    cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies_file, "--content-type",
+           "application/x-www-form-urlencoded", "--header", f"Cookie: {cookie}", "--concurrency", str(conc),
+           "--batch", str(batch), "--steps", str(steps), "--expect", "302", "--until-url", counts_url,
+           "--until-field", "completed"]
+    for p in ports:
+        cmd += ["--target", f"127.0.0.1:{p}"]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    dt = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise RuntimeError(f"load generator failed ({p.returncode}): {p.stdout[-500:]} {p.stderr[-500:]}")
+    return dt, json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def _cpu_by_role(stack) -> dict[str, float]:
+    """CPU seconds so far per process role (replicas summed per app)."""
+    raw = stack.cpu_seconds()
+    out: dict[str, float] = {}
+    for k, v in raw.items():
+        role = k
+        for app in (FRONTEND, API, PROC):
+            if k.startswith(app + "-"):
+                role = app + "." + k.rsplit(".", 1)[1]
+        out[role] = out.get(role, 0.0) + v
+    return out
+
+
+def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
+    import shutil
+    import tempfile
+
+    import psutil
+
+    from aca_dotnet_workshop_amd.native.build import build_dataplane, build_loadgen, build_native
+    from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
+    from aca_dotnet_workshop_amd.platform.manifest import load_manifest
+    n = d.world if d.world > 1 else a.gpus
+    fe, api, proc = frontend_topology(cores)
+    fe = a.frontend_replicas or fe
+    api = a.api_replicas or api
+    proc = a.processor_replicas or proc
+    conc = a.concurrency or min(512, 48 * fe)
+    nrep = fe + api + proc
+    app_cpu = a.app_cpu or round(max(0.25, (cores - 2.0) / nrep), 2)  # 2 CPUs: backing + load generator
+    for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
+        b()
+    exe = str(build_loadgen())
+    sweep = a.overdue_sweep_ms > 0
+    root = tempfile.mkdtemp(prefix="tt-bench-")
+    # the environment's processes inherit these: JSON logs to the telemetry dir only (Log
+    # Analytics), the rank's own GPU for the store's query path, the sweep's mirrored columns
+    os.environ.update({"TT_LOG_CONSOLE": "0", **rank_device_env()})
+    if sweep:
+        os.environ["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue,taskCreatedOn"
+    overrides = {"backendApiMinReplicas": api, "backendApiMaxReplicas": api, "frontendMinReplicas": fe,
+                 "frontendMaxReplicas": fe, "processorMinReplicas": proc, "processorMaxReplicas": proc,
+                 "notifierMode": "log", "cosmosAutoscaleMaxThroughput": a.ru_per_s, "daprMtls": bool(a.mtls),
+                 "enforceCpuLimits": bool(a.cpu_limits), "appCpu": app_cpu, "appMemory": "2Gi",
+                 "appInsightsSamplingPercentage": a.trace_sampling,
+                 "overdueQuery": "range" if sweep else "equality", "overduePageSize": 1000 if sweep else 0,
+                 "environmentName": f"cae-bench-r{d.rank}"}
+    m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
+                      overrides)
+    env = BackgroundEnvironment(m, os.path.join(root, "env"), log_level="warning")
+    sweeper = None
+    try:
+        env.start()
+        lim = env.ctl.limiter.describe()
+        fe_ports = [r.app_port for r in env.replicas(FRONTEND)]
+        backing = env.backing_url
+        entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
+        counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
+        cookie, token = _form_session(fe_ports[0], "bench@bench.local")
+        bodies_file = os.path.join(root, "form-bodies.txt")
+        with open(bodies_file, "wb") as f:
+            f.write(b"\n".join(_form_bodies(a.batch, token, a.past_due_every if sweep else 0)) + b"\n")
+        if a.warmup:
+            run_form_loadgen(exe, fe_ports, cookie, counts_url, a.warmup, a.batch, conc, bodies_file)
+        if sweep:  # one cron trigger per environment
+            sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
+        d.barrier()
+        device_sync()
+        me = psutil.Process()
+        cpu0 = _cpu_by_role(env.stack)
+        t = me.cpu_times()
+        cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
+        ru0 = _collection_stats(backing).get("throughput", {})
+        if sweeper is not None:
+            sweeper.start()
+        dt, report = run_form_loadgen(exe, fe_ports, cookie, counts_url, a.steps, a.batch, conc, bodies_file)
+        device_sync()
+        d.barrier()
+        if sweeper is not None:
+            sweeper.stop()
+        cpu1 = _cpu_by_role(env.stack)
+        t = me.cpu_times()
+        cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
+        ru1 = _collection_stats(backing).get("throughput", {})
+        dt_max = d.max(dt)
+        util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
+        sweep_info = None
+        if sweeper is not None:
+            acc = _collection_stats(backing).get("accelerator", {})
+            sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
+                          "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
+                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows")}
+        # the same environment, load straight at the API sidecars' invoke (round 2's topology)
+        direct = None
+        dsteps = a.direct_steps if a.direct_steps >= 0 else max(1, a.steps // 4)
+        if dsteps:
+            socks = [r.sidecar_uds for r in env.replicas(API)]
+            jb = os.path.join(root, "json-bodies.jsonl")
+            with open(jb, "wb") as f:
+                f.write(b"\n".join(_bodies(a.batch)) + b"\n")
+            ddt, drep = run_loadgen(exe, socks, counts_url, dsteps, a.batch, conc, jb)
+            ddt = d.max(ddt)
+            direct = {"value": round(a.batch * dsteps * (d.world if d.world > 1 else 1) / ddt, 2), "steps": dsteps,
+                      "create_latency_p50_ms": drep["latency_ms"]["p50"], "create_latency_p99_ms": drep["latency_ms"]["p99"],
+                      "note": "same environment, load at the API sidecars' invoke (no frontend, no mTLS hop)"}
+        total = a.batch * a.steps * (d.world if d.world > 1 else 1)
+        value = total / dt_max if dt_max > 0 else 0.0
+        p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])
+        ru_used = None
+        if ru0 and ru1 and "ru_consumed" in ru1:
+            ru_used = round((ru1["ru_consumed"] - ru0.get("ru_consumed", 0.0)) / dt, 1)
+        if d.rank == 0:
+            print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
+                              "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
+                              "overdue_sweeps": sweep_info, "resource_limits": lim}), file=sys.stderr, flush=True)
+            print(json.dumps({
+                "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "n/a (JSON over HTTP)",
+                "data": "synthetic createTask form posts",
+                "config": {"model": "tasks-tracker createTask flow, SURVEY §3.1 (frontend -> mTLS -> API -> store + "
+                                    "publish -> processor ack)",
+                           "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
+                           "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
+                           "environment": "deploy/main.yaml via the platform controller",
+                           "entry": "frontend", "entry_request": "POST /Tasks/Create (form, antiforgery + identity "
+                                                                  "cookies) -> 302, redirect not followed",
+                           "ingress": "bypassed: the load generator balances over the frontend replicas",
+                           "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
+                           "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": app_cpu,
+                                          "mechanism": lim.get("cpu"), "mode": lim.get("mode")},
+                           "replicas": {"frontend": fe, "api": api, "processor": proc},
+                           "notifier": "TasksNotifier:Mode=log (the shipped controller)",
+                           "dapr_api_logging": True, "trace_sampling_percent": a.trace_sampling,
+                           "concurrency_per_rank": conc, "load_generator": "native",
+                           "cpu_pinning": pin_label(pinned),
+                           "create_latency_p50_ms": round(p50, 3), "create_latency_p99_ms": round(p99, 3),
+                           "baseline": "reference publishes no throughput",
+                           "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
+                           "timed_region_s": round(dt_max, 3), "log_level": "Information",
+                           "log_sink": "structured JSON lines in the environment telemetry dir",
+                           "overdue_sweeps": sweep_info, "api_sidecar_direct": direct}}), flush=True)
+    finally:
+        if sweeper is not None and sweeper.thread.is_alive():
+            sweeper.stop()
+        env.stop()
+        d.close()
+        if not os.environ.get("TT_BENCH_KEEP"):
             shutil.rmtree(root, ignore_errors=True)
 
 

@@ -54,8 +54,11 @@ def test_bench_two_ranks_torchrun():
     # nothing else on stdout (gloo's connection messages go to stderr)
     assert [x for x in r.stdout.splitlines() if x.strip() and not x.startswith("{")] == [], r.stdout
     _check(lines[0], 2, 2, 1)
-    # 8 CPUs here: each rank pinned to its own 4 (the stack inherits the mask)
-    assert lines[0]["config"]["cpu_pinning"] == f"{len(os.sched_getaffinity(0)) // 2} CPUs per rank (NUMA-local whole cores)"
+    # each rank pinned to its own partition of the host (the stack inherits the mask)
+    from aca_dotnet_workshop_amd.parallel import host_topology, partition_cpus
+    part = partition_cpus(set(os.sched_getaffinity(0)), *host_topology(), 0, 2)
+    want = f"{len(part)} CPUs per rank (NUMA-local whole cores (rank order))" if part else "none"
+    assert lines[0]["config"]["cpu_pinning"] == want
 
 
 def test_bench_shared_env_two_ranks():
@@ -66,7 +69,7 @@ def test_bench_shared_env_two_ranks():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--batch", "32", "--api-replicas", "1", "--processor-replicas", "1",
-           "--shared-env", "--overdue-sweep-ms", "0"]
+           "--shared-env", "--overdue-sweep-ms", "0", "--entry", "api-sidecar"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
