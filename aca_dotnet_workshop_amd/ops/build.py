@@ -34,7 +34,7 @@ def stale() -> bool:
     if not LIB.exists():
         return True
     t = LIB.stat().st_mtime
-    return any(s.stat().st_mtime > t for s in sources())
+    return any(s.stat().st_mtime > t for s in sources() + sorted(HIP_DIR.glob("*.h")))
 
 
 def build_gpu(force: bool = False, verbose: bool = False) -> Path:

@@ -26,7 +26,6 @@ import numpy as np
 OP_LEAF, OP_AND, OP_OR, OP_NOT, OP_TRUE, OP_EQ, OP_RANGE = 1, 2, 3, 4, 5, 6, 7
 TILE = 8192           # rows per kernel tile (ops/hip/query_scan.hip kTileRows)
 MAX_DEPTH = 8         # device stack depth (16-bit masks in a 128-bit register)
-MAX_FLAT_LEAVES = 8   # leaves of a flat program (ops/hip/query_scan.hip kMaxFlatLeaves)
 _TYPE_ORDER = {type(None): 0, bool: 1, int: 2, float: 2, str: 3, list: 4, dict: 5}
 
 
@@ -150,33 +149,6 @@ def rank_interval(c: "Column", sat: np.ndarray) -> tuple[int, int] | None:
     if not np.array_equal(inside, sat):
         return None
     return lo, hi
-
-
-def flat_form(code: np.ndarray) -> tuple[np.ndarray, int] | None:
-    """(leaf rows, flip_result) when ``code`` is one AND / OR over leaves that may each be
-    negated -- the shape ``tt_scan_flat`` evaluates wave-wide -- else None.  Leaf rows are
-    ``[op | flip << 8, column, b, c]``; an OR is evaluated as NOT(AND(NOT leaf)), so every
-    leaf of an OR carries the extra flip and the result is flipped back."""
-    ops = code[:, 0].tolist()
-    if ops == [OP_TRUE]:  # no leaves: every live row
-        return np.zeros((0, 4), dtype=np.int32), 0
-    is_or, items, n = False, code, 1
-    if ops[-1] in (OP_AND, OP_OR):
-        is_or, items, n = ops[-1] == OP_OR, code[:-1], int(code[-1, 1])
-    leaves: list[list[int]] = []
-    i = 0
-    while i < len(items):
-        op, a, b, c = (int(x) for x in items[i])
-        if op not in (OP_EQ, OP_RANGE, OP_LEAF):
-            return None
-        neg = 0
-        if i + 1 < len(items) and int(items[i + 1, 0]) == OP_NOT:
-            neg, i = 1, i + 1
-        leaves.append([op | ((neg ^ int(is_or)) << 8), a, b, c])
-        i += 1
-    if len(leaves) != n or not 0 < n <= MAX_FLAT_LEAVES:
-        return None
-    return np.asarray(leaves, dtype=np.int32), int(is_or)
 
 
 class KeyTable:
@@ -358,6 +330,9 @@ class ColumnarIndex:
         self._dict_gen = 0  # bumps when the dictionaries are rebuilt (re-encode from `source`)
         self._tomb_dirty = False   # liveness changed for rows that are already on the device
         self._full_dirty = True    # layout changed (compaction / new column / growth)
+        # zone maps of the paged device path, per sort spec (page_gpu): per tile the row with the
+        # smallest ordering key, re-computed for the tiles whose rows changed
+        self._zones: dict[Any, dict] = {}
         for p in paths:
             self.add_column(p)
 
@@ -403,6 +378,7 @@ class ColumnarIndex:
         self.version += 1
         self._full_dirty = True
         self._tomb_dirty = False
+        self._zones_reset()
 
     # -- native mirror (DocStore column mirror, native/src/docstore.hpp) ---------------
     @classmethod
@@ -457,9 +433,13 @@ class ColumnarIndex:
             self.seq[lo:hi] = d["seqs"]
             self.live[lo:hi] = d["live"]
             self._next_seq = max(self._next_seq, int(d["seqs"].max()))
+            self._zones_touch(np.arange(lo // TILE, (hi - 1) // TILE + 1))
         if d["kills"].size:
             self.live[d["kills"].astype(np.int64)] = 0
             self._tomb_dirty = True
+            self._zones_touch(np.unique(d["kills"].astype(np.int64) // TILE))
+        if d["full"]:
+            self._zones_reset()
         self.n = hi
         self._ncur = (int(d["gen"]), hi, int(d["kill_cursor"]))
         if changed:
@@ -491,6 +471,16 @@ class ColumnarIndex:
         else:
             for p in missing:
                 self.add_column(p)
+
+    # -- zone maps (paged device path) ---------------------------------------------------
+    def _zones_touch(self, tiles) -> None:
+        for z in self._zones.values():
+            if not z["all"]:
+                z["dirty"].update(int(t) for t in tiles)
+
+    def _zones_reset(self) -> None:
+        for z in self._zones.values():
+            z["all"], z["dirty"] = True, set()
 
     # -- maintenance ----------------------------------------------------------
     def add_column(self, path: str) -> int:
@@ -551,6 +541,7 @@ class ColumnarIndex:
         self.row_of[key] = r
         self.n += 1
         self.version += 1
+        self._zones_touch([r // TILE] if old is None else [r // TILE, old // TILE])
         self._maybe_compact()
 
     def delete(self, key: str) -> None:
@@ -562,6 +553,7 @@ class ColumnarIndex:
             self._tomb_dirty = True
             self._dead += 1
             self.version += 1
+            self._zones_touch([r // TILE])
         self._maybe_compact()
 
     def _maybe_compact(self) -> None:
@@ -592,6 +584,7 @@ class ColumnarIndex:
         self._dead = 0
         self.version += 1
         self._full_dirty = True
+        self._zones_reset()
 
     # -- compilation ---------------------------------------------------------
     def _dict_state(self) -> tuple:
@@ -789,7 +782,7 @@ class ColumnarIndex:
 
     def _device_codes(self, col: int, width: int) -> np.ndarray:
         """The whole column in the device layout; 2-bit columns get 16 bytes of padding (the
-        flat scan reads them with the same 16-byte loads as the byte-wide ones)."""
+        reads past the end of a partial group stay inside the buffer)."""
         v = self._narrow(col, 0, self.cap, width)
         if width == 0:
             v = np.concatenate([v, np.zeros(16, dtype=np.uint8)])
@@ -809,6 +802,8 @@ class ColumnarIndex:
         widths = [self.width_for(len(c.values)) for c in self.columns]
         nwords = self.cap // 16
         if st is None or self._full_dirty or st["cap"] != self.cap or len(st["cols"]) != len(self.columns):
+            if self._full_dirty:
+                self._zones_reset()
             cols = [torch.from_numpy(self._device_codes(i, w)).to(dev) for i, w in enumerate(widths)]
             live = torch.from_numpy(self._live_words(0, nwords)).to(dev)
             seq = torch.from_numpy(self.seq[:self.cap].astype(np.int32)).to(dev)  # uint32 on device
@@ -877,10 +872,8 @@ class ColumnarIndex:
         cur["synced"] = self.n
 
     def device_program(self, prog: Program, kernels):
-        """Sync the device mirror for ``prog`` and return (state, program, bitmaps, flat) ready
-        for ``GpuKernels.select`` (range leaves remapped to their rank-encoded columns; ``flat``:
-        the wave-wide leaf form of ``flat_form`` on the device, or None)."""
-        torch = kernels.torch
+        """Sync the device mirror for ``prog`` and return (state, program, bitmaps) ready for
+        ``GpuKernels.select`` (range leaves remapped to their rank-encoded columns)."""
         leaf = (prog.code[:, 0] == OP_LEAF) | (prog.code[:, 0] == OP_EQ) | (prog.code[:, 0] == OP_RANGE)
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
             raise ValueError("program references a column outside the index")
@@ -889,32 +882,19 @@ class ColumnarIndex:
         slots = tuple(sorted(st.get("rank_slot", {}).items())) if rng.any() else ()
         cached = getattr(prog, "_dev", None)
         if cached is not None and cached[0] == (slots, str(kernels.device)):
-            return st, cached[1], cached[2], self._flat_args(st, cached[3])
+            return st, cached[1], cached[2]
         code_np = prog.code
         if rng.any():  # range leaves read the rank-encoded copy of their column
             code_np = prog.code.copy()
             code_np[rng, 1] = [st["rank_slot"][c] for c in prog.code[rng, 1].tolist()]
-        code = torch.from_numpy(code_np).to(kernels.device)
-        bitmaps = torch.from_numpy(prog.bitmaps).to(kernels.device)
-        ff = flat_form(code_np)
-        flat = None if ff is None else (torch.from_numpy(ff[0]).to(kernels.device), ff[1], ff[0][:, 1].copy())
-        prog._dev = ((slots, str(kernels.device)), code, bitmaps, flat)  # reused while the program is
-        return st, code, bitmaps, self._flat_args(st, flat)
-
-    @staticmethod
-    def _flat_args(st, flat):
-        """(device leaves, flip_result, widest leaf column now) -- widths grow with the
-        dictionaries, so the kernel instantiation is chosen per call."""
-        if flat is None:
-            return None
-        leaves, flip, cols = flat
-        # kernel instantiation by the widest byte width (2-bit columns ride on the 1-byte one)
-        return leaves, flip, max(1, int(st["table_widths"][cols].max())) if cols.size else 1
+        code = kernels.torch.from_numpy(code_np).to(kernels.device)
+        bitmaps = kernels.torch.from_numpy(prog.bitmaps).to(kernels.device)
+        prog._dev = ((slots, str(kernels.device)), code, bitmaps)  # reused while the program is
+        return st, code, bitmaps
 
     def select_gpu(self, prog: Program, kernels, return_mask: bool = False, on_device: bool = False):
-        st, code, bitmaps, flat = self.device_program(prog, kernels)
-        res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask,
-                             flat=flat)
+        st, code, bitmaps = self.device_program(prog, kernels)
+        res = kernels.select(st["table"], st["live"], self.cap, self.n, code, bitmaps, return_mask=return_mask)
         if return_mask or on_device:
             return res
         return res.cpu().numpy()
@@ -1009,9 +989,10 @@ class ColumnarIndex:
             k = (k << bits) | r
         return (k << seq_bits) | self.seq[rows]
 
-    def order_gpu(self, rows, sort, kernels, k: int | None = None):
-        """Order a device selection on the GPU (``hip/sort_keys.hip`` + radix sort / top-k);
-        returns device rows, or None when the host path must order."""
+    def _device_sort_plan(self, sort, kernels):
+        """(specs, rank tables, seq bits, key bits) on the device and the host plan of the same
+        packed key, cached per sort spec and dictionary state; None when the device cannot
+        order by it (too many keys, a key over 63 bits, a sequence over 32 bits)."""
         if len(sort or []) > kernels.max_sort_keys:
             return None
         for srt in sort or []:
@@ -1029,13 +1010,97 @@ class ColumnarIndex:
             torch = kernels.torch
             key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
             hit = (torch.from_numpy(specs).to(kernels.device), torch.from_numpy(ranks).to(kernels.device), seq_bits,
-                   key_bits)
+                   key_bits, plan)
             if len(self._plan_cache) >= 64:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
             self._plan_cache[pkey] = hit
-        specs_t, ranks_t, seq_bits, key_bits = hit
+        return hit
+
+    def order_gpu(self, rows, sort, kernels, k: int | None = None):
+        """Order a device selection on the GPU (``hip/sort_keys.hip`` + radix sort / top-k);
+        returns device rows, or None when the host path must order."""
+        hit = self._device_sort_plan(sort, kernels)
+        if hit is None:
+            return None
+        specs_t, ranks_t, seq_bits, key_bits, _ = hit
         st = self.to_device(kernels)  # sort keys may have added columns
         return kernels.order(st["table"], rows, specs_t, ranks_t, st["seq"], seq_bits, k, key_bits)
+
+    def page_gpu(self, prog: Program, sort, kernels, offset: int, limit: int):
+        """A page [offset, offset + limit) of an ordered query without scanning the collection
+        (``hip/page_topk.hip``): zone maps pick the tiles that can hold the page, only those are
+        evaluated, one workgroup orders the candidates.  Returns (rows, token) or None when the
+        page does not fit the device top-k (the caller takes the full path)."""
+        k_total = offset + limit
+        if limit <= 0 or k_total > kernels.page_cap:
+            return None
+        hit = self._device_sort_plan(sort, kernels)
+        if hit is None:
+            return None
+        specs_t, ranks_t, seq_bits, _, plan = hit
+        st, code, bitmaps = self.device_program(prog, kernels)
+        ntiles = (self.n + TILE - 1) // TILE
+        if ntiles == 0:
+            return np.zeros(0, dtype=np.int32), None
+        zkey = json.dumps(sort, sort_keys=True, default=str)
+        z = self._zones.get(zkey)
+        if z is None:
+            z = self._zones[zkey] = {"zarg": np.zeros(0, dtype=np.int32), "dirty": set(), "all": True, "density": {}}
+        if z["zarg"].size < ntiles:  # new tiles: not computed yet
+            z["dirty"].update(range(z["zarg"].size, ntiles))
+            z["zarg"] = np.concatenate([z["zarg"], np.full(ntiles - z["zarg"].size, -1, dtype=np.int32)])
+        z["zarg"] = z["zarg"][:ntiles]
+        todo = np.arange(ntiles, dtype=np.int32) if z["all"] else \
+            np.fromiter((t for t in z["dirty"] if t < ntiles), dtype=np.int32)
+        if todo.size:
+            z["zarg"][todo] = kernels.zone_argmin(st["table"], st["live"], self.n, specs_t, ranks_t, st["seq"],
+                                                  seq_bits, todo)
+        z["all"], z["dirty"] = False, set()
+        zarg = z["zarg"]
+        valid = zarg >= 0
+        nvalid = int(valid.sum())
+        if nvalid == 0:
+            return np.zeros(0, dtype=np.int32), None
+        top = np.iinfo(np.uint64).max
+        keys = np.full(ntiles, top, dtype=np.uint64)
+        keys[valid] = self.sort_keys_numpy(zarg[valid], plan).astype(np.uint64)
+        pkey = (prog.code.tobytes(), prog.bitmaps.tobytes())
+        dens = z["density"].get(pkey, 0.25)  # candidates per row of a chosen tile, from the last page
+        b = min(nvalid, max(1, int(np.ceil(1.5 * k_total / max(dens * TILE, 1.0)))))
+        lo_b, hi_b = 0, None  # largest tile count seen short of k candidates / smallest that overflowed
+        for _ in range(24):
+            if b >= nvalid:
+                chosen, bound = np.nonzero(valid)[0].astype(np.int32), top
+            else:
+                part = np.argpartition(keys, b)
+                chosen, bound = part[:b].astype(np.int32), int(keys[part[b]])
+            rows, total, complete = kernels.page(st["table"], st["live"], self.n, code, bitmaps, specs_t, ranks_t,
+                                                 st["seq"], seq_bits, chosen, k_total, offset, bound)
+            if complete:
+                break
+            if total > kernels.page_cap:  # more candidates than one workgroup sorts: fewer tiles
+                hi_b = b
+            else:
+                lo_b = b
+            if hi_b is None:
+                b = min(nvalid, b * 4)
+            elif hi_b - lo_b <= 1:
+                return None  # no tile count gives k candidates the LDS sort holds
+            else:
+                b = (lo_b + hi_b) // 2
+        else:
+            return None
+        if len(chosen):
+            z["density"][pkey] = max(total / (len(chosen) * TILE), 1e-4)
+            if len(z["density"]) > 64:
+                z["density"].pop(next(iter(z["density"])))
+        if total > k_total:
+            more = True
+        elif bound == top:
+            more = False
+        else:  # the page used every candidate: are there matches in the tiles left out?
+            more = int(self.select_gpu(prog, kernels, on_device=True).numel()) > k_total
+        return rows, (str(k_total) if more else None)
 
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:
         """Returns (keys in result order for the requested page, continuation token)."""
@@ -1053,6 +1118,10 @@ class ColumnarIndex:
         limit = int(page.get("limit") or 0)
         offset = int(page.get("token") or 0)
         rows = None
+        if kernels is not None and limit:
+            paged = self.page_gpu(prog, sort, kernels, offset, limit)
+            if paged is not None:
+                return paged
         if kernels is not None:
             dev_rows = self.select_gpu(prog, kernels, on_device=True)
             total = int(dev_rows.numel())

@@ -26,26 +26,12 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, I32, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int
-    lib.tt_launch_scan_flat.argtypes = [P, I64, P, P, I32, I32, I32, P, I32, P, P, P]
-    lib.tt_launch_scan_flat.restype = ctypes.c_int
-    lib.tt_max_flat_leaves.restype = ctypes.c_int
-    lib.tt_set_eval_nt.argtypes = [ctypes.c_int]
-    lib.tt_set_eval_nt.restype = ctypes.c_int
-    lib.tt_set_compact_nt.argtypes = [ctypes.c_int]
-    lib.tt_set_compact_nt.restype = ctypes.c_int
-    lib.tt_set_compact_mode.argtypes = [ctypes.c_int]
-    lib.tt_set_compact_mode.restype = ctypes.c_int
-    lib.tt_set_flat_grid.argtypes = [I64]
-    lib.tt_set_flat_grid.restype = ctypes.c_int
     lib.tt_sort_pairs_temp_bytes.argtypes = [I64, I32]
     lib.tt_sort_pairs_temp_bytes.restype = ctypes.c_int64
     lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P]
     lib.tt_sort_pairs.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, P, I64, P, P, P, P]
-    lib.tt_chunk_tiles.restype = ctypes.c_int
     lib.tt_launch_scan_compact.restype = ctypes.c_int
-    lib.tt_launch_scan_select.argtypes = [P, I64, P, P, I32, P, I32, P, P, P, P, P]
-    lib.tt_launch_scan_select.restype = ctypes.c_int
     lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
     lib.tt_launch_sort_keys.argtypes = [P, P, I64, P, I32, P, I32, P, I32, P, P, I32, P]
@@ -58,6 +44,12 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_set_eval_groups.restype = ctypes.c_int
     lib.tt_launch_rank_encode.argtypes = [P, P, I32, I64, I64, P, I32, P]
     lib.tt_launch_rank_encode.restype = ctypes.c_int
+    lib.tt_page_cap.restype = ctypes.c_int
+    lib.tt_launch_zone_argmin.argtypes = [P, I64, P, P, I32, P, P, I32, P, I32, P, P]
+    lib.tt_launch_zone_argmin.restype = ctypes.c_int
+    lib.tt_launch_page.argtypes = [P, I64, P, P, I32, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, I32,
+                                   ctypes.c_uint64, P, P, P]
+    lib.tt_launch_page.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -75,46 +67,15 @@ class GpuKernels:
         self.tile_rows = int(self.lib.tt_tile_rows())
         self.max_depth = int(self.lib.tt_max_depth())
         self.max_sort_keys = int(self.lib.tt_sort_max_keys())
-        self.chunk_tiles = int(self.lib.tt_chunk_tiles())
         # the pinned total, its event and the cached scratch buffers are shared by every caller
         # of this object (queries of different collections run on different threads): one
         # select at a time
         self._total_lock = threading.Lock()
         self._bufs: dict[str, Any] = {}
-        # Single-pass select (tt_scan_select, decoupled look-back) is opt-in: measured 1.40 ms vs
-        # 0.175 ms for the two-pass pipeline on 1e8 rows -- the look-back's agent-scope status
-        # reads cross the 8 XCDs' private L2s (profiles/r1_query_scan_fused_ab.md).
-        self.fused_select = False
-        # Flat programs (one AND / OR over leaves) can run on tt_scan_flat (wave-wide compares,
-        # leaves combined in scalar registers).  Opt-in: on the 1e8-row overdue sweep it ties
-        # the interpreter (92.8 vs 92.8 µs; PMC: similar VALU counts, half the wait cycles, same
-        # duration) -- both stream the narrow columns at the same ~4.6 TB/s -- so the simpler
-        # path stays the default
-        # (profiles/r1_query_scan_flat_ab.md).
-        self.flat_eval = False
-        self.max_flat_leaves = int(self.lib.tt_max_flat_leaves())
+        self.page_cap = int(self.lib.tt_page_cap())
         # Result ordering sorts (key, row) pairs over the packed key's used bits only
         # (hip/radix_pairs.hip); False = torch.sort argsort + gather, for A/B runs.
         self.pair_sort = True
-
-    def set_flat_grid(self, blocks: int) -> None:
-        """Workgroups of ``tt_scan_flat`` (grid-stride over tiles); 0 = one per tile."""
-        if self.lib.tt_set_flat_grid(int(blocks)) != 0:
-            raise ValueError("grid must be >= 0")
-
-    def set_compact_nt(self, on: bool) -> None:
-        """Non-temporal stores for the compacted row ids (default on; A/B)."""
-        self.lib.tt_set_compact_nt(1 if on else 0)
-
-    def set_compact_mode(self, mode: int) -> None:
-        """1: tile offsets in one block + wave-independent compaction (default); 0: chunk sums +
-        wave 0 of each block finds the block's offset (A/B)."""
-        if self.lib.tt_set_compact_mode(int(mode)) != 0:
-            raise ValueError("compaction mode must be 0 or 1")
-
-    def set_eval_nt(self, on: bool) -> None:
-        """Non-temporal column loads in ``tt_scan_eval`` (default off; A/B)."""
-        self.lib.tt_set_eval_nt(1 if on else 0)
 
     def set_eval_groups(self, u: int) -> None:
         """Row groups per lane in ``tt_scan_eval`` (1, 2, 4 or 8): registers vs loads in flight."""
@@ -124,8 +85,7 @@ class GpuKernels:
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False,
-               flat=None):
+    def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False):
         """Row indices (int32, ascending) of live rows satisfying ``prog``.
 
         ``table``: int64 [ncols, 2] of (device pointer, width) column descriptors, every column
@@ -144,36 +104,23 @@ class GpuKernels:
             raise ValueError("column table must be int64 [ncols, 2]")
         if prog.dtype != torch.int32 or prog.ndim != 2 or prog.shape[1] != 4:
             raise ValueError("program must be int32 [L, 4]")
-        if self.fused_select and not return_mask:
-            return self._select_fused(table, live16, capacity, nrows, prog, bitmaps, tiles)
         with self._total_lock:  # also guards the cached scratch buffers
             nmask = tiles * self.tile_rows // 16
             mask = (torch.empty(nmask, dtype=torch.int16, device=self.device) if return_mask
                     else self._buf("mask", nmask, torch.int16))
             counts = self._buf("counts", tiles, torch.int32)
             stream = self._stream()
-            if flat is not None and self.flat_eval:
-                leaves, flip, max_width = flat
-                if leaves.dtype != torch.int32 or leaves.ndim != 2 or leaves.shape[1] != 4:
-                    raise ValueError("flat leaves must be int32 [n, 4]")
-                if leaves.shape[0] > self.max_flat_leaves:
-                    raise ValueError("too many leaves for tt_scan_flat")
-                rc = self.lib.tt_launch_scan_flat(table.data_ptr(), nrows, live16.data_ptr(), leaves.data_ptr(),
-                                                  leaves.shape[0], int(flip), int(max_width), bitmaps.data_ptr(),
-                                                  bitmaps.numel(), mask.data_ptr(), counts.data_ptr(), stream)
-                if rc != 0:
-                    raise RuntimeError(f"tt_scan_flat launch failed ({rc})")
-            else:
-                rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
-                                                  prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(),
-                                                  mask.data_ptr(), counts.data_ptr(), stream)
-                if rc != 0:
-                    raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
+            rc = self.lib.tt_launch_scan_eval(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(),
+                                              prog.shape[0], bitmaps.data_ptr(), bitmaps.numel(),
+                                              mask.data_ptr(), counts.data_ptr(), stream)
+            if rc != 0:
+                raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
             # the tiles' output offsets in one block (tt_tile_offsets, which also writes the total
             # straight into pinned host memory), then the wave-independent compaction: no torch
-            # launches, no host sync between the kernels -- one event wait at the end
-            out = torch.empty(max(nrows, 1), dtype=torch.int32, device=self.device)
-            # [0] = total (int64), byte 16 on: int32 tile offsets (mode 0: chunk counts)
+            # launches, no host sync between the kernels -- one event wait at the end.  The ids
+            # land in a cached buffer; the caller gets its own copy of the selected prefix.
+            out = self._buf("out", max(nrows, 1), torch.int32)
+            # [0] = total (int64), byte 16 on: int32 tile offsets
             scratch = self._buf("scratch", tiles // 2 + 3, torch.int64)
             pinned = self._pinned()
             rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch.data_ptr() + 16, nrows,
@@ -183,7 +130,7 @@ class GpuKernels:
             self._total_event.record(torch.cuda.current_stream(self.device))
             self._total_event.synchronize()
             total = int(pinned[0])
-        out = out[:total]
+            out = out[:total].clone()  # a selection-sized result; the scratch stays for the next query
         return (out, mask) if return_mask else out
 
     def _buf(self, name: str, n: int, dtype):
@@ -208,28 +155,56 @@ class GpuKernels:
         if rc != 0:
             raise RuntimeError(f"tt_rank_encode launch failed ({rc})")
 
-    def _select_fused(self, table, live16, capacity: int, nrows: int, prog, bitmaps, tiles: int):
-        """Single pass (``tt_scan_select``): evaluation + compaction with decoupled look-back;
-        one host sync (the selected count) instead of a mid-pipeline scan and sync."""
+    # -- paged ordered queries (hip/page_topk.hip) -------------------------------------------
+    def _h2d_i32(self, name: str, arr):
+        """A small int32 host array in a cached device buffer (one copy, no allocation per call)."""
+        import numpy as np
         torch = self.torch
-        work = torch.zeros(tiles + 2, dtype=torch.int64, device=self.device)  # tile status + ticket + total
-        out = self._out_buffer(capacity)
-        rc = self.lib.tt_launch_scan_select(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
-                                            bitmaps.data_ptr(), bitmaps.numel(), work.data_ptr(),
-                                            work[tiles:].data_ptr(), out.data_ptr(), work[tiles + 1:].data_ptr(),
-                                            self._stream())
-        if rc != 0:
-            raise RuntimeError(f"tt_scan_select launch failed ({rc})")
-        total = int(work[tiles + 1].item())
-        return out[:total]
-
-    def _out_buffer(self, capacity: int):
-        """Result buffer reused across queries (grows with the collection); callers that keep
-        a selection across queries must copy it."""
-        buf = getattr(self, "_out", None)
-        if buf is None or buf.numel() < capacity:
-            buf = self._out = self.torch.empty(capacity, dtype=self.torch.int32, device=self.device)
+        arr = np.ascontiguousarray(arr, dtype=np.int32)
+        buf = self._buf(name, max(1, arr.size), torch.int32)
+        if arr.size:
+            buf[:arr.size].copy_(torch.from_numpy(arr), non_blocking=False)
         return buf
+
+    def zone_argmin(self, table, live16, nrows: int, specs, ranks, seq, seq_bits: int, tiles):
+        """Per listed tile (numpy int32), the live row with the smallest packed key (-1: none)."""
+        import numpy as np
+        with self._total_lock:
+            t = self._h2d_i32("zone_tiles", tiles)
+            out = self._buf("zone_out", max(1, len(tiles)), self.torch.int32)
+            rc = self.lib.tt_launch_zone_argmin(table.data_ptr(), nrows, live16.data_ptr(), specs.data_ptr(),
+                                                specs.shape[0], ranks.data_ptr(), seq.data_ptr(), seq_bits,
+                                                t.data_ptr(), len(tiles), out.data_ptr(), self._stream())
+            if rc != 0:
+                raise RuntimeError(f"tt_zone_argmin launch failed ({rc})")
+            return out[:len(tiles)].cpu().numpy().astype(np.int32)
+
+    def page(self, table, live16, nrows: int, prog, bitmaps, specs, ranks, seq, seq_bits: int, tiles, k: int,
+             offset: int, bound: int):
+        """The rows [offset, k) of the key order among the matches in ``tiles`` (numpy int32), and
+        (candidates, complete): see hip/page_topk.hip."""
+        import numpy as np
+        torch = self.torch
+        if not 0 < k <= self.page_cap or not 0 <= offset <= k:
+            raise ValueError("page outside the device top-k capacity")
+        with self._total_lock:
+            t = self._h2d_i32("page_tiles", tiles)
+            ck = self._buf("page_keys", self.page_cap, torch.int64)
+            cr = self._buf("page_rows", self.page_cap, torch.int32)
+            if "page_counter" not in self._bufs:  # zeroed once; tt_page_topk resets it after each query
+                self._bufs["page_counter"] = torch.zeros(1, dtype=torch.int32, device=self.device)
+            out = self._buf("page_out", 4 + self.page_cap, torch.int32)
+            rc = self.lib.tt_launch_page(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
+                                         bitmaps.data_ptr(), bitmaps.numel(), specs.data_ptr(), specs.shape[0],
+                                         ranks.data_ptr(), seq.data_ptr(), seq_bits, t.data_ptr(), len(tiles),
+                                         ck.data_ptr(), cr.data_ptr(), self._bufs["page_counter"].data_ptr(), k,
+                                         offset, ctypes.c_uint64(bound), out.data_ptr(), out.data_ptr() + 16,
+                                         self._stream())
+            if rc != 0:
+                raise RuntimeError(f"tt_page launch failed ({rc})")
+            host = out[:4 + k - offset].cpu().numpy()
+        total, complete, written = int(host[0]), bool(host[1]), int(host[2])
+        return host[4:4 + written].astype(np.int32), total, complete
 
     def group_count(self, table, g: int, mask, nrows: int, ngroups: int):
         torch = self.torch

@@ -1,0 +1,293 @@
+// Paged, ordered state queries without a collection scan (gfx950 / CDNA4, wave64).
+//
+// A page of an ordered query -- the overdue sweep's `ORDER BY taskCreatedOn ASC LIMIT 1000`, a
+// Dapr client's `page.limit` -- needs the first k = offset + limit rows in the order of the
+// packed key [rank(sort key 0) | ... | seq] (sort_keys.hip).  Scanning every tile, compacting
+// every match and radix-sorting them (the unpaged path) costs O(collection).  Here:
+//
+// * zone maps: per 8192-row tile, the row holding the smallest key among its live rows
+//   (tt_zone_argmin).  The row -- not its key -- is kept: inserting new dictionary values shifts
+//   ranks but never reorders existing values, so a tile's argmin stays its argmin until the
+//   tile gets new rows or loses rows (the host re-runs those tiles only).  The host turns the
+//   argmins into keys with the current rank tables and picks the B tiles with the smallest
+//   ones; `bound` = the smallest key among the tiles left out (no row outside the chosen tiles
+//   can order before it).
+// * tt_page_gather: the filter program (scan_common.h) over the chosen tiles only; every match
+//   whose key orders before `bound` appends its (key, row) pair to a candidate buffer (one
+//   atomic per tile).  Matches at or after `bound` cannot be on the page unless fewer than k
+//   orders before it, and then the host takes more tiles anyway.
+// * tt_page_topk: ONE workgroup sorts the candidates in LDS (bitonic, <= 8192 pairs) and writes
+//   the page's rows plus [candidates, complete, written].  complete = at least k candidates
+//   (all of them order before every unread row), or every tile was read.  Otherwise the host
+//   widens B and repeats; with more candidates than the LDS sort holds it narrows B.  It also
+//   resets the candidate counter for the next query, so the page path launches no fill kernel.
+//
+// At 1e8 rows the page costs a handful of tiles instead of 12,207 (profiles/r3_page_topk.md).
+#include "scan_common.h"
+
+namespace {
+
+constexpr int kPageCap = 8192;       // candidate pairs one workgroup sorts in LDS (96 KiB)
+constexpr int kTopkBlock = 1024;
+constexpr int kGatherBlock = kTileRows / kRowsPerLane;  // 512 lanes x 16 rows = one tile
+constexpr int kZoneBlock = 256;      // 32 rows per lane
+constexpr int kMaxSortKeys = 4;
+
+struct SortSpec {     // host-built, one per sort key (primary first); layout of sort_keys.hip's
+  int32_t col;        // column index into the column table
+  int32_t rank_off;   // offset of this key's rank table in `ranks`
+  int32_t nranks;     // entries in this key's rank table (dictionary size)
+  int32_t bits;       // key field width
+  int32_t desc;       // 1 = descending
+  int32_t missing;    // rank of a missing path
+  int32_t max_rank;   // for DESC: stored value = max_rank - rank
+  int32_t pad;
+};
+
+__device__ __forceinline__ int32_t load_id(const ColumnDesc& c, int64_t row) {
+  if (c.width == 0) return id_of((reinterpret_cast<const uint8_t*>(c.ptr)[row >> 2] >> ((row & 3) * 2)) & 3u, 0);
+  if (c.width == 1) return id_of(reinterpret_cast<const uint8_t*>(c.ptr)[row], 1);
+  if (c.width == 2) return id_of(reinterpret_cast<const uint16_t*>(c.ptr)[row], 2);
+  return reinterpret_cast<const int32_t*>(c.ptr)[row];
+}
+
+// The packed ordering key of one row (identical to tt_sort_keys and ColumnarIndex.sort_keys_numpy).
+__device__ __forceinline__ uint64_t row_key(const ColumnDesc* cols, const SortSpec* specs, int nkeys,
+                                            const int32_t* __restrict__ ranks, const uint32_t* __restrict__ seq,
+                                            int seq_bits, int64_t row) {
+  uint64_t k = 0;
+  for (int j = 0; j < nkeys; ++j) {
+    const SortSpec s = specs[j];
+    const int32_t id = load_id(cols[s.col], row);
+    int32_t r = s.missing;
+    if (id >= 0 && id < s.nranks) r = ranks[s.rank_off + id];
+    if (s.desc) r = s.max_rank - r;
+    k = (k << s.bits) | (uint64_t)(uint32_t)r;
+  }
+  return (k << seq_bits) | (uint64_t)seq[row];
+}
+
+__device__ __forceinline__ void min_pair(uint64_t& k, int32_t& r, uint64_t k2, int32_t r2) {
+  if (k2 < k || (k2 == k && (uint32_t)r2 < (uint32_t)r)) {
+    k = k2;
+    r = r2;
+  }
+}
+
+}  // namespace
+
+// One workgroup per listed tile: zarg[i] = the live row of tiles[i] with the smallest key, -1 if
+// the tile has no live row.
+extern "C" __global__ void __launch_bounds__(kZoneBlock)
+tt_zone_argmin(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_t* __restrict__ live,
+               const SortSpec* __restrict__ specs, int32_t nkeys, const int32_t* __restrict__ ranks,
+               const uint32_t* __restrict__ seq, int32_t seq_bits, const int32_t* __restrict__ tiles,
+               int32_t* __restrict__ zarg) {
+  __shared__ SortSpec s_specs[kMaxSortKeys];
+  __shared__ ColumnDesc s_cols[kMaxSortKeys];
+  __shared__ uint64_t w_key[kZoneBlock / 64];
+  __shared__ int32_t w_row[kZoneBlock / 64];
+  if (threadIdx.x < nkeys) {
+    SortSpec s = specs[threadIdx.x];
+    s_cols[threadIdx.x] = cols[s.col];
+    s.col = threadIdx.x;  // the key's column now sits at s_cols[j]
+    s_specs[threadIdx.x] = s;
+  }
+  __syncthreads();
+  const int64_t tile = tiles[blockIdx.x];
+  const int64_t r0 = tile * kTileRows + (int64_t)threadIdx.x * 32;
+  uint64_t best = ~0ull;
+  int32_t arg = -1;
+  if (r0 < nrows) {
+    uint32_t lv = (uint32_t)live[r0 >> 4] | ((uint32_t)live[(r0 >> 4) + 1] << 16);
+    if (r0 + 32 > nrows) lv &= (nrows - r0 >= 32) ? ~0u : ((1u << (uint32_t)(nrows - r0)) - 1u);
+    while (lv) {
+      const int b = __ffs(lv) - 1;
+      lv &= lv - 1;
+      const int64_t row = r0 + b;
+      min_pair(best, arg, row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row), (int32_t)row);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t k2 = __shfl_down(best, off, 64);
+    const int32_t r2 = __shfl_down(arg, off, 64);
+    if (r2 >= 0 && (arg < 0 || k2 < best || (k2 == best && r2 < arg))) {
+      best = k2;
+      arg = r2;
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    w_key[wave] = best;
+    w_row[wave] = arg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t k = ~0ull;
+    int32_t r = -1;
+    for (int w = 0; w < kZoneBlock / 64; ++w)
+      if (w_row[w] >= 0 && (r < 0 || w_key[w] < k || (w_key[w] == k && w_row[w] < r))) {
+        k = w_key[w];
+        r = w_row[w];
+      }
+    zarg[blockIdx.x] = r;
+  }
+}
+
+// One workgroup per candidate tile: evaluate the filter on the tile's 8192 rows (16 per lane),
+// append (key, row) of every live match.  Pairs beyond `cap` are counted, not written.
+extern "C" __global__ void __launch_bounds__(kGatherBlock)
+tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_t* __restrict__ live,
+               const int32_t* __restrict__ prog, int32_t prog_len, const uint32_t* __restrict__ bitmaps,
+               int32_t bitmap_words, const SortSpec* __restrict__ specs, int32_t nkeys,
+               const int32_t* __restrict__ ranks, const uint32_t* __restrict__ seq, int32_t seq_bits,
+               const int32_t* __restrict__ tiles, uint64_t bound, uint64_t* __restrict__ cand_keys,
+               int32_t* __restrict__ cand_rows, uint32_t* __restrict__ counter, uint32_t cap) {
+  extern __shared__ uint32_t lds_bitmaps[];
+  __shared__ SortSpec s_specs[kMaxSortKeys];
+  __shared__ ColumnDesc s_cols[kMaxSortKeys];
+  __shared__ uint32_t wave_counts[kGatherBlock / 64];
+  __shared__ uint32_t block_base;
+  const bool in_lds = bitmap_words <= kMaxLdsBitmapWords;
+  if (in_lds)
+    for (int i = threadIdx.x; i < bitmap_words; i += kGatherBlock) lds_bitmaps[i] = bitmaps[i];
+  if (threadIdx.x < nkeys) {
+    SortSpec s = specs[threadIdx.x];
+    s_cols[threadIdx.x] = cols[s.col];
+    s.col = threadIdx.x;
+    s_specs[threadIdx.x] = s;
+  }
+  __syncthreads();
+  const int64_t tile = tiles[blockIdx.x];
+  const int64_t row0[1] = {tile * kTileRows + (int64_t)threadIdx.x * kRowsPerLane};
+  uint32_t m[1];
+  if (in_lds) run_program<1>(cols, prog, prog_len, (const uint32_t*)lds_bitmaps, row0, m);
+  else run_program<1>(cols, prog, prog_len, bitmaps, row0, m);
+  uint32_t sel = row0[0] < nrows ? (m[0] & (uint32_t)live[row0[0] >> 4]) : 0u;
+  if (row0[0] < nrows && row0[0] + 16 > nrows) sel &= (1u << (uint32_t)(nrows - row0[0])) - 1u;
+  if (bound != ~0ull) {  // keep the matches that order before every unread tile
+    uint32_t keep = 0, b = sel;
+    while (b) {
+      const int i = __ffs(b) - 1;
+      b &= b - 1;
+      if (row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row0[0] + i) < bound) keep |= 1u << i;
+    }
+    sel = keep;
+  }
+  const uint32_t cnt = __popc(sel);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = cnt;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wave_counts[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int w = 0; w < kGatherBlock / 64; ++w) {
+      const uint32_t c = wave_counts[w];
+      wave_counts[w] = s;
+      s += c;
+    }
+    block_base = s ? atomicAdd(counter, s) : 0u;
+  }
+  __syncthreads();
+  uint32_t pos = block_base + wave_counts[wave] + incl - cnt;
+  while (sel) {
+    const int b = __ffs(sel) - 1;
+    sel &= sel - 1;
+    if (pos < cap) {
+      const int64_t row = row0[0] + b;
+      cand_keys[pos] = row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row);
+      cand_rows[pos] = (int32_t)row;
+    }
+    ++pos;
+  }
+}
+
+// ONE workgroup: bitonic sort of the candidates in LDS, then the page [offset, k) of the order.
+// info = [candidates, complete, written, 0]; out_rows = the page's rows.
+extern "C" __global__ void __launch_bounds__(kTopkBlock)
+tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__ cand_rows,
+             uint32_t* __restrict__ counter, uint32_t cap, int32_t k, int32_t offset, uint64_t bound,
+             int32_t* __restrict__ info, int32_t* __restrict__ out_rows) {
+  __shared__ uint64_t keys[kPageCap];
+  __shared__ int32_t rows[kPageCap];
+  const uint32_t total = *counter;
+  const int n = (int)(total < cap ? total : cap);
+  int p = 1;
+  while (p < n) p <<= 1;
+  for (int i = threadIdx.x; i < p; i += kTopkBlock) {
+    keys[i] = i < n ? cand_keys[i] : ~0ull;
+    rows[i] = i < n ? cand_rows[i] : -1;
+  }
+  __syncthreads();
+  for (int size = 2; size <= p; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < (p >> 1); i += kTopkBlock) {
+        // i-th compare-exchange pair of this pass: lo has bit `stride` clear
+        const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int hi = lo | stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t a = keys[lo], b = keys[hi];
+        if ((a > b) == up) {
+          keys[lo] = b;
+          keys[hi] = a;
+          const int32_t t = rows[lo];
+          rows[lo] = rows[hi];
+          rows[hi] = t;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int upto = n < k ? n : k;
+  const int written = upto > offset ? upto - offset : 0;
+  for (int i = threadIdx.x; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];
+  if (threadIdx.x == 0) {
+    int complete;
+    if (total > cap) complete = 0;                     // overflow: the host takes fewer tiles
+    else if (n >= k) complete = 1;                     // k candidates, all before every unread row
+    else complete = bound == ~0ull;                    // every tile was read
+    info[0] = (int32_t)total;
+    info[1] = complete;
+    info[2] = written;
+    info[3] = 0;
+    *counter = 0;  // ready for the next query's gather (stream order)
+  }
+}
+
+extern "C" int tt_page_cap() { return kPageCap; }
+
+extern "C" int tt_launch_zone_argmin(const void* cols, int64_t nrows, const uint16_t* live, const void* specs,
+                                     int32_t nkeys, const int32_t* ranks, const uint32_t* seq, int32_t seq_bits,
+                                     const int32_t* tiles, int32_t ntiles, int32_t* zarg, hipStream_t stream) {
+  if (ntiles <= 0) return 0;
+  if (nkeys < 0 || nkeys > kMaxSortKeys || seq_bits < 0 || seq_bits > 32) return -1;
+  hipLaunchKernelGGL(tt_zone_argmin, dim3((unsigned)ntiles), dim3(kZoneBlock), 0, stream,
+                     reinterpret_cast<const ColumnDesc*>(cols), nrows, live, reinterpret_cast<const SortSpec*>(specs),
+                     nkeys, ranks, seq, seq_bits, tiles, zarg);
+  return (int)hipGetLastError();
+}
+
+// `counter` must be 0 before the first query (tt_page_topk resets it after each).
+extern "C" int tt_launch_page(const void* cols, int64_t nrows, const uint16_t* live, const int32_t* prog, int32_t prog_len,
+                              const uint32_t* bitmaps, int32_t bitmap_words, const void* specs, int32_t nkeys,
+                              const int32_t* ranks, const uint32_t* seq, int32_t seq_bits, const int32_t* tiles,
+                              int32_t ntiles, uint64_t* cand_keys, int32_t* cand_rows, uint32_t* counter, int32_t k,
+                              int32_t offset, uint64_t bound, int32_t* info, int32_t* out_rows, hipStream_t stream) {
+  if (prog_len <= 0 || bitmap_words <= 0 || ntiles < 0) return -1;
+  if (nkeys < 0 || nkeys > kMaxSortKeys || seq_bits < 0 || seq_bits > 32) return -1;
+  if (k <= 0 || k > kPageCap || offset < 0 || offset > k) return -1;
+  if (ntiles > 0) {
+    const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
+    hipLaunchKernelGGL(tt_page_gather, dim3((unsigned)ntiles), dim3(kGatherBlock), lds, stream,
+                       reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, bitmap_words,
+                       reinterpret_cast<const SortSpec*>(specs), nkeys, ranks, seq, seq_bits, tiles, bound, cand_keys,
+                       cand_rows, counter, (uint32_t)kPageCap);
+  }
+  hipLaunchKernelGGL(tt_page_topk, dim3(1), dim3(kTopkBlock), 0, stream, cand_keys, cand_rows, counter,
+                     (uint32_t)kPageCap, k, offset, bound, info, out_rows);
+  return (int)hipGetLastError();
+}

@@ -33,12 +33,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-native", action="store_true",
                     help="skip the multi-threaded native CPU executor (the fair host baseline)")
     ap.add_argument("--query", action="store_true", help="also time the whole paged query path (ColumnarIndex.query)")
-    ap.add_argument("--flat-grid", type=int, default=None, help="tt_scan_flat workgroups (0 = one per tile)")
     ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4/8; 0 = default)")
-    ap.add_argument("--compact-nt", type=int, default=1, help="non-temporal stores for the compacted row ids (1/0)")
-    ap.add_argument("--compact-mode", type=int, default=1,
-                    help="1: wave-independent compaction, 0: per-block offsets found by wave 0")
-    ap.add_argument("--eval-nt", type=int, default=0, help="non-temporal column loads in the scan (1/0)")
     ap.add_argument("--sorted", action="store_true",
                     help="also time ORDER BY taskDueDate DESC: top-100 page and full ordering (tt_sort_keys + sort)")
     a = ap.parse_args()
@@ -79,15 +74,10 @@ def main() -> None:
     k = GpuKernels("cuda:0")
     if a.eval_groups:
         k.set_eval_groups(a.eval_groups)
-    k.set_compact_nt(bool(a.compact_nt))
-    k.set_compact_mode(a.compact_mode)
-    k.set_eval_nt(bool(a.eval_nt))
-    if a.flat_grid is not None:
-        k.set_flat_grid(a.flat_grid)
     flt = {"AND": [{"LT": {"taskDueDate": "2024-07-01T00:00:00"}}, {"EQ": {"isCompleted": False}},
                    {"EQ": {"isOverDue": False}}]}
     prog = ix.compile(flt)
-    st, code, bm, flat = ix.device_program(prog, k)  # includes rank-encoding range-leaf columns
+    st, code, bm = ix.device_program(prog, k)  # includes rank-encoding range-leaf columns
 
     def timed(**kw):
         for _ in range(a.warmup):
@@ -99,21 +89,8 @@ def main() -> None:
         torch.cuda.synchronize()
         return res, (time.perf_counter() - t0) / a.iters
 
-    # A/B: the program interpreter (tt_scan_eval) vs the wave-wide flat kernel (tt_scan_flat)
     out, dt = timed()
-    flat_dt, flat_matches = None, None
-    if flat is not None:
-        k.flat_eval = True
-        flat_out, flat_dt = timed(flat=flat)
-        k.flat_eval = False
-        flat_matches = bool(torch.equal(flat_out, out))
     selected = int(out.numel())
-    # A/B: the single-pass variant (tt_scan_select, decoupled look-back across tiles)
-    k.fused_select = True
-    one, dt_one = timed()
-    k.fused_select = False
-    single_pass_ms = dt_one * 1e3
-    same = bool(torch.equal(one, out))
     # bytes: referenced columns at their narrow widths + liveness bit + mask write & read + output indices
     # bytes per row of the columns the scan reads (2-bit codes: width 0 = 1/4 byte; range leaves
     # read their rank-encoded copy, at least one byte)
@@ -122,11 +99,8 @@ def main() -> None:
     nbytes = n * widths + n // 8 + 2 * n // 8 + selected * 4
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
-           "device": torch.cuda.get_device_name(0), "tile_rows": TILE, "single_pass_ms": round(single_pass_ms, 4),
-           "single_pass_matches": same, "flat_kernel": flat is not None,
-           "flat_ms": round(flat_dt * 1e3, 4) if flat_dt else None, "flat_matches_interpreter": flat_matches,
-           "eval_groups": a.eval_groups or 2, "flat_grid": a.flat_grid, "column_bytes_per_row": widths,
-           "compact_nt": bool(a.compact_nt), "compact_mode": a.compact_mode, "eval_nt": bool(a.eval_nt),
+           "device": torch.cuda.get_device_name(0), "tile_rows": TILE,
+           "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths,
            "range_leaves": int((prog.code[:, 0] == 7).sum())}
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order

@@ -273,14 +273,12 @@ def test_gpu_scan_matches_numpy(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [1, 0])
 @pytest.mark.parametrize("tiles", [1, 63, 64, 65, 1025, 12_207, 16_385])
-def test_gpu_compaction_offsets_over_many_chunks(tiles, mode):
-    """Both compaction variants on a synthetic selection mask far larger than the other tests'
+def test_gpu_compaction_offsets_over_many_chunks(tiles):
+    """The compaction on a synthetic selection mask far larger than the other tests'
     collections (12,207 tiles = 1e8 rows; 16,385 = one past the offset kernel's first pass, with
-    a partial 16-tile group): mode 1 -- tt_tile_offsets (exclusive offsets of all tiles in one
-    block, total to device and pinned host memory) + tt_scan_compact_w (every wave finds its own
-    base); mode 0 -- tt_chunk_sums + tt_scan_compact_t (wave 0 finds the block's offset)."""
+    a partial 16-tile group): tt_tile_offsets (exclusive offsets of all tiles in one block, total
+    to device and pinned host memory) + tt_scan_compact_w (every wave finds its own base)."""
     import torch
     k = _kernels()
     g = torch.Generator().manual_seed(tiles)
@@ -289,29 +287,20 @@ def test_gpu_compaction_offsets_over_many_chunks(tiles, mode):
     counts = bits.sum(1).to(torch.int32)
     words = (bits.view(-1, 16).to(torch.int32) << torch.arange(16)).sum(1).to(torch.int16)  # row r -> bit r % 16
     mask, counts_d = words.to(k.device), counts.to(k.device)
-    nchunks = (tiles + k.chunk_tiles - 1) // k.chunk_tiles
     scratch = torch.full((tiles,), -1, dtype=torch.int32, device=k.device)
     nrows = tiles * 8192
     out = torch.empty(nrows, dtype=torch.int32, device=k.device)
     total = torch.empty(1, dtype=torch.int64, device=k.device)
     pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-    k.set_compact_mode(mode)
-    try:
-        assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
-                                            out.data_ptr(), total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
-        torch.cuda.synchronize()
-    finally:
-        k.set_compact_mode(1)
+    assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
+                                        out.data_ptr(), total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
+    torch.cuda.synchronize()
     want = torch.nonzero(bits.view(-1)).view(-1).to(torch.int32)
     n = int(total.item())
     assert n == want.numel() == int(pinned[0])
     assert torch.equal(out[:n].cpu(), want)
-    if mode == 1:
-        ref = torch.cumsum(counts.to(torch.int64), 0) - counts
-        assert torch.equal(scratch.cpu(), ref.to(torch.int32))
-    else:
-        ref = torch.nn.functional.pad(counts, (0, nchunks * k.chunk_tiles - tiles)).view(nchunks, -1).sum(1)
-        assert torch.equal(scratch[:nchunks].cpu(), ref.to(torch.int32))
+    ref = torch.cumsum(counts.to(torch.int64), 0) - counts
+    assert torch.equal(scratch.cpu(), ref.to(torch.int32))
 
 
 @pytest.mark.gpu
@@ -340,24 +329,6 @@ def test_gpu_concurrent_selects_from_threads():
     for t in ts:
         t.join()
     assert not errors, errors[:3]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 8193, 300_001])
-def test_gpu_single_pass_select_matches(n):
-    """tt_scan_select (one pass, decoupled look-back) == the two-pass pipeline."""
-    k = _kernels()
-    ix = _random_collection(n, random.Random(n + 7))
-    try:
-        for f in GPU_FILTERS:
-            prog = ix.compile(f)
-            k.fused_select = False
-            want = ix.select_gpu(prog, k)
-            k.fused_select = True
-            got = ix.select_gpu(prog, k)
-            assert np.array_equal(got, want), (n, f)
-    finally:
-        k.fused_select = False
 
 
 @pytest.mark.gpu
@@ -468,11 +439,8 @@ def test_gpu_two_bit_columns():
                   {"LT": {"done": True}}):
             prog = ix.compile(f)
             want = ix.select_numpy(prog)
-            for flat in (False, True):
-                k.flat_eval = flat
-                assert np.array_equal(ix.select_gpu(prog, k), want), (label, f, flat)
+            assert np.array_equal(ix.select_gpu(prog, k), want), (label, f)
             assert np.array_equal(ix.select_native(prog, 2), want), (label, f)
-        k.flat_eval = False
         q = {"filter": {"EQ": {"done": False}}, "sort": [{"key": "state", "order": "DESC"}, {"key": "done"}],
              "page": {"limit": 50}}
         assert ix.query(q, k) == ix.query(q), label
@@ -555,55 +523,11 @@ def test_gpu_query_caches_follow_dictionary_growth():
     _interleaved(ix, store, random.Random(9), kernels=k)
 
 
-@settings(max_examples=200, deadline=None)
-@given(docs_st, filters_st, st.integers(0, 1000))
-def test_flat_form_is_equivalent(docs, flt, seed):
-    """``flat_form`` (what tt_scan_flat evaluates: AND of possibly flipped leaves, OR folded by
-    De Morgan) selects exactly what the program selects."""
-    from aca_dotnet_workshop_amd.ops.columnar import OP_AND, OP_NOT, flat_form
-    if not docs:
-        return
-    ix = _columnar(_ops(docs, random.Random(seed)))
-    prog = ix.compile(flt)
-    ff = flat_form(prog.code)
-    if ff is None:  # nested AND / OR: the interpreter's job
-        assert ((prog.code[:, 0] == OP_AND) | (prog.code[:, 0] == 3)).sum() > 1 or (prog.code[:-1, 0] == OP_NOT).any()
-        return
-    leaves, flip = ff
-    code = []
-    for op, a, b, c in leaves.tolist():
-        code.append([op & 0xFF, a, b, c])
-        if op >> 8:
-            code.append([OP_NOT, 0, 0, 0])
-    if len(leaves) == 0:
-        code = [[5, 0, 0, 0]]
-    elif len(leaves) > 1:
-        code.append([OP_AND, len(leaves), 0, 0])
-    if flip:
-        code.append([OP_NOT, 0, 0, 0])
-    from aca_dotnet_workshop_amd.ops.columnar import Program
-    again = Program(np.asarray(code, dtype=np.int32), prog.bitmaps, prog.columns)
-    assert np.array_equal(ix.select_numpy(again), ix.select_numpy(prog))
-
-
-def test_flat_form_shapes():
-    from aca_dotnet_workshop_amd.ops.columnar import flat_form
-    ix = ColumnarIndex(["a", "b"])
-    for i in range(100):
-        ix.upsert(str(i), {"a": i % 7, "b": f"s{i % 3}"})
-    assert flat_form(ix.compile({}).code)[0].shape == (0, 4)
-    assert flat_form(ix.compile({"EQ": {"a": 1}}).code)[1] == 0
-    leaves, flip = flat_form(ix.compile({"OR": [{"EQ": {"a": 1}}, {"NEQ": {"b": "s1"}}]}).code)
-    assert flip == 1 and (leaves[:, 0] >> 8).tolist() == [1, 0]  # OR: leaves flipped, NEQ's NOT cancels
-    assert flat_form(ix.compile({"AND": [{"EQ": {"a": 1}}, {"OR": [{"EQ": {"b": "s1"}}, {"GT": {"a": 3}}]}]}).code) is None
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 1000, 70_001])
-def test_gpu_flat_kernel_matches_interpreter(n):
-    """tt_scan_flat (wave-wide compares, scalar combine) == tt_scan_eval == NumPy, on 1-, 2- and
-    4-byte columns, register and LDS bitmaps, range leaves, NOT / OR folding."""
-    from aca_dotnet_workshop_amd.ops.columnar import flat_form
+def test_gpu_interpreter_over_column_widths(n):
+    """tt_scan_eval == NumPy on 1-, 2- and 4-byte columns, register and LDS bitmaps, range
+    leaves, NOT / OR, and the mask it returns for grouped counts."""
     k = _kernels()
     rnd = random.Random(n)
     ix = ColumnarIndex(["s", "m", "w", "d"], capacity=n)
@@ -618,20 +542,14 @@ def test_gpu_flat_kernel_matches_interpreter(n):
                {"AND": [{"LT": {"d": "2024-05-20"}}, {"NEQ": {"s": 4}}, {"IN": {"m": ["m1", "m2", "m299"]}}]},
                {"OR": [{"EQ": {"s": 5}}, {"GT": {"w": 90_000}}, {"NEQ": {"d": "2024-05-03"}}]},
                {"OR": [{"EQ": {"m": "m3"}}, {"EQ": {"s": 7}}]}]
-    try:
-        for f in filters:
-            prog = ix.compile(f)
-            assert flat_form(prog.code) is not None, f
-            want = ix.select_numpy(prog)
-            k.flat_eval = False
-            interp, imask = ix.select_gpu(prog, k, return_mask=True)
-            k.flat_eval = True
-            flat, fmask = ix.select_gpu(prog, k, return_mask=True)
-            assert np.array_equal(flat.cpu().numpy(), want), (n, f)
-            assert np.array_equal(interp.cpu().numpy(), want), (n, f)
-            assert torch_equal(fmask, imask), (n, f)
-    finally:
-        k.flat_eval = False
+    for f in filters:
+        prog = ix.compile(f)
+        want = ix.select_numpy(prog)
+        interp, imask = ix.select_gpu(prog, k, return_mask=True)
+        assert np.array_equal(interp.cpu().numpy(), want), (n, f)
+        bits = imask.cpu().numpy().view(np.uint16)
+        rows = np.nonzero(np.unpackbits(bits.view(np.uint8), bitorder="little")[:ix.n])[0]
+        assert np.array_equal(rows, want), (n, f)
 
 
 def torch_equal(a, b):
@@ -844,3 +762,176 @@ def test_string_ranks_incremental_match_the_comparison_sort(batches):
     c.encode(5)
     c._rank_cache = None
     assert c.ranks().tolist() == c._general_ranks().tolist()
+
+
+class _FakePageKernels:
+    """The page path's kernels (hip/page_topk.hip) emulated on the host over the index's own
+    arrays, so ``ColumnarIndex.page_gpu``'s zone maps, tile choice, retries and continuation
+    tokens run in the CPU suite; the real kernels are pinned by the GPU tests below."""
+
+    def __init__(self, ix, cap=8192):
+        import torch
+        self.torch, self.device, self.page_cap, self.max_sort_keys = torch, torch.device("cpu"), cap, 4
+        self.ix, self.prog, self.sort = ix, None, None
+        self.calls = {"zone_tiles": 0, "page_tiles": 0, "pages": 0}
+
+    def rank_encode(self, *a):  # device rank columns are not read by the emulation
+        pass
+
+    def _keys(self, rows):
+        return self.ix.sort_keys_numpy(rows, self.ix.sort_specs(self.sort)).astype(np.uint64)
+
+    def zone_argmin(self, table, live16, nrows, specs, ranks, seq, seq_bits, tiles):
+        ix, out = self.ix, []
+        self.calls["zone_tiles"] += len(tiles)
+        for t in tiles.tolist():
+            rows = np.arange(t * 8192, min((t + 1) * 8192, ix.n))
+            rows = rows[ix.live[rows] != 0]
+            out.append(int(rows[np.argmin(self._keys(rows))]) if rows.size else -1)
+        return np.asarray(out, dtype=np.int32)
+
+    def page(self, table, live16, nrows, prog, bitmaps, specs, ranks, seq, seq_bits, tiles, k, offset, bound):
+        self.calls["pages"] += 1
+        self.calls["page_tiles"] += len(tiles)
+        sel = self.ix.select_numpy(self.prog)
+        sel = sel[np.isin(sel // 8192, tiles)]
+        keys = self._keys(sel)
+        sel = sel[keys < np.uint64(bound)] if bound != np.iinfo(np.uint64).max else sel
+        keys = self._keys(sel)
+        total = sel.size
+        order = sel[np.argsort(keys, kind="stable")][: self.page_cap]
+        n = min(total, self.page_cap)
+        if total > self.page_cap:
+            complete = False
+        elif n >= k:
+            complete = True
+        else:
+            complete = bound == np.iinfo(np.uint64).max
+        return order[offset:min(n, k)].astype(np.int32), total, complete
+
+    def select(self, table, live16, capacity, nrows, prog, bitmaps, return_mask=False):
+        return self.torch.from_numpy(self.ix.select_numpy(self.prog))
+
+
+@settings(max_examples=20, deadline=None)
+@given(st.integers(0, 10_000), st.sampled_from([None, [{"key": "c"}], [{"key": "d", "order": "DESC"}, {"key": "c"}]]),
+       st.sampled_from([1, 7, 100, 900]))
+def test_page_path_host_logic_matches_full_order(seed, sort, limit):
+    """page_gpu (zone maps + tile choice + bound check + token) walks the same pages as the full
+    host query, through interleaved writes that dirty tiles, for sorted and unsorted queries."""
+    rnd = random.Random(seed)
+    ix = ColumnarIndex(["c", "d", "x"])
+    for i in range(30_000):
+        ix.upsert(f"k{i}", {"c": f"2025-01-{rnd.randrange(1, 29):02d}T{rnd.randrange(24):02d}:00:00",
+                            "d": rnd.randrange(50), "x": rnd.random() < 0.2})
+    fk = _FakePageKernels(ix)
+    fk.sort = sort
+    flt = {"AND": [{"EQ": {"x": False}}, {"LT": {"d": 40}}]}
+    for rnd_ in range(3):
+        q = {"filter": flt, **({"sort": sort} if sort else {})}
+        full, _ = ix.query(q)
+        prog = ix.compile(flt)
+        fk.prog = prog
+        got, token, ended = [], None, False
+        for _ in range(25):
+            off = int(token or 0)
+            res = ix.page_gpu(prog, sort, fk, off, limit)
+            if res is None:  # keys not clustered by tile / past what one workgroup sorts: the full path's job
+                assert sort is not None or off + limit > 1000
+                break
+            rows, token = res
+            got += [ix.keys[r] for r in rows.tolist()]
+            if token is None:
+                ended = True
+                break
+        assert got == full[:len(got)] and (not ended or got == full), (rnd_, len(got), len(full))
+        for _ in range(500):  # dirty some tiles: updates re-append rows, deletes kill them
+            i = rnd.randrange(30_000)
+            if rnd.random() < 0.2:
+                ix.delete(f"k{i}")
+            else:
+                ix.upsert(f"k{i}", {"c": f"2025-01-{rnd.randrange(1, 29):02d}T00:00:00", "d": rnd.randrange(50),
+                                    "x": rnd.random() < 0.2})
+    # the zone maps did their job: pages read a few tiles, not the collection
+    assert fk.calls["page_tiles"] / max(1, fk.calls["pages"]) < (ix.n + 8191) // 8192
+
+
+def test_page_path_overflow_and_tiny_cap_fall_back():
+    """More candidates than the device top-k holds: fewer tiles are taken, and a page that
+    cannot fit at all is left to the full path (None)."""
+    ix = ColumnarIndex(["c"])
+    for i in range(40_000):
+        ix.upsert(f"k{i}", {"c": i // 40})  # clustered by tile, like a creation timestamp
+    fk = _FakePageKernels(ix)  # the device cap is one tile: a single tile always fits
+    fk.sort = [{"key": "c"}]
+    prog = ix.compile({})
+    fk.prog = prog
+    rows, token = ix.page_gpu(prog, fk.sort, fk, 0, 100)
+    assert [ix.keys[r] for r in rows] == ix.query({"sort": fk.sort, "page": {"limit": 100}})[0] and token == "100"
+    assert ix.page_gpu(prog, fk.sort, fk, 8100, 200) is None  # beyond the capacity
+    fk.page_cap = 16  # a tile's matches alone overflow: the full path answers
+    assert ix.page_gpu(prog, fk.sort, fk, 0, 10) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sort", [None, [{"key": "c"}], [{"key": "d", "order": "DESC"}, {"key": "c"}]])
+def test_gpu_page_path_matches_host(sort):
+    """hip/page_topk.hip (zone argmins, gather of the chosen tiles, LDS bitonic top-k) pages
+    exactly like the host path -- rows and continuation tokens -- over a collection whose sort
+    key is clustered by insertion (a creation timestamp), through updates that re-append rows
+    and deletes that kill them."""
+    k = _kernels()
+    rnd = random.Random(3)
+    ix = ColumnarIndex(["c", "d", "x"])
+    n = 120_000
+    for i in range(n):
+        ix.upsert(f"k{i}", {"c": f"2025-03-01T{i // 3600:02d}:{i // 60 % 60:02d}:{i % 60:02d}",
+                            "d": rnd.randrange(40), "x": rnd.random() < 0.3})
+    flt = {"AND": [{"EQ": {"x": False}}, {"LT": {"d": 30}}]}
+    used = 0
+    for round_ in range(3):
+        q = {"filter": flt, **({"sort": sort} if sort else {})}
+        for limit in (1, 64, 1000):
+            token = None
+            for _ in range(3):
+                page = {"limit": limit, **({"token": token} if token else {})}
+                before = ix._zones.copy()
+                got = ix.query({**q, "page": page}, k)
+                want = ix.query({**q, "page": page})
+                assert got == want, (round_, limit, token)
+                used += bool(ix._zones) or bool(before)
+                token = got[1]
+                if token is None:
+                    break
+        for _ in range(4000):  # updates land at the end (new tiles), deletes punch holes
+            i = rnd.randrange(n)
+            if rnd.random() < 0.2:
+                ix.delete(f"k{i}")
+            else:
+                ix.upsert(f"k{i}", {"c": f"2025-03-01T{i // 3600:02d}:{i // 60 % 60:02d}:{i % 60:02d}",
+                                    "d": rnd.randrange(40), "x": rnd.random() < 0.3})
+    assert used and ix._zones
+
+
+@pytest.mark.gpu
+def test_gpu_zone_argmin_matches_numpy():
+    k = _kernels()
+    rnd = random.Random(8)
+    ix = ColumnarIndex(["c"])
+    for i in range(50_000):
+        ix.upsert(str(i), {"c": rnd.randrange(1000)})
+    for i in rnd.sample(range(50_000), 9000):
+        ix.delete(str(i))
+    sort = [{"key": "c", "order": "DESC"}]
+    specs_t, ranks_t, seq_bits, _, plan = ix._device_sort_plan(sort, k)
+    st = ix.to_device(k)
+    tiles = np.arange((ix.n + TILE_ROWS - 1) // TILE_ROWS, dtype=np.int32)
+    got = k.zone_argmin(st["table"], st["live"], ix.n, specs_t, ranks_t, st["seq"], seq_bits, tiles)
+    for t, r in zip(tiles.tolist(), got.tolist()):
+        rows = np.arange(t * TILE_ROWS, min((t + 1) * TILE_ROWS, ix.n))
+        rows = rows[ix.live[rows] != 0]
+        want = int(rows[np.argmin(ix.sort_keys_numpy(rows, plan))]) if rows.size else -1
+        assert r == want, t
+
+
+TILE_ROWS = 8192
