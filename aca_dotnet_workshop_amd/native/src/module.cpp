@@ -10,6 +10,7 @@
 #include "docstore.hpp"
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
+#include "formcodec.hpp"
 
 namespace py = pybind11;
 using namespace tt;
@@ -278,6 +279,23 @@ PYBIND11_MODULE(_ttnative, m) {
     std::string out;
     if (!taskcodec::overdue_filter(std::string_view(p, (size_t)n), run_day, retrieved, kept, out)) return py::none();
     return py::make_tuple(retrieved, kept, py::bytes(out));
+  });
+
+  // The frontend's Create post (formcodec.hpp): None = the page decides; (True, TaskAddModel JSON)
+  // = send it to api/tasks; (False, b"") = the antiforgery token is invalid (400).
+  m.def("frontend_create_form", [](py::bytes body, py::bytes cookie, py::bytes key) -> py::object {
+    char *pb, *pc, *pk;
+    Py_ssize_t nb, nc, nk;
+    if (PyBytes_AsStringAndSize(body.ptr(), &pb, &nb) != 0 || PyBytes_AsStringAndSize(cookie.ptr(), &pc, &nc) != 0 ||
+        PyBytes_AsStringAndSize(key.ptr(), &pk, &nk) != 0)
+      throw py::error_already_set();
+    std::string json;
+    auto v = formcodec::create_task(std::string_view(pb, (size_t)nb), std::string_view(pc, (size_t)nc),
+                                    std::string_view(pk, (size_t)nk), ".AspNetCore.Antiforgery", "TasksCreatedByCookie",
+                                    json);
+    if (v == formcodec::Verdict::kDecline) return py::none();
+    if (v == formcodec::Verdict::kBadToken) return py::make_tuple(false, py::bytes(""));
+    return py::make_tuple(true, py::bytes(json));
   });
 
   // state-query response -> (task count, TaskModel JSON array, has a continuation token) or None

@@ -44,27 +44,41 @@ struct SortSpec {     // host-built, one per sort key (primary first); layout of
   int32_t pad;
 };
 
-__device__ __forceinline__ int32_t load_id(const ColumnDesc& c, int64_t row) {
-  if (c.width == 0) return id_of((reinterpret_cast<const uint8_t*>(c.ptr)[row >> 2] >> ((row & 3) * 2)) & 3u, 0);
-  if (c.width == 1) return id_of(reinterpret_cast<const uint8_t*>(c.ptr)[row], 1);
-  if (c.width == 2) return id_of(reinterpret_cast<const uint16_t*>(c.ptr)[row], 2);
-  return reinterpret_cast<const int32_t*>(c.ptr)[row];
-}
-
-// The packed ordering key of one row (identical to tt_sort_keys and ColumnarIndex.sort_keys_numpy).
-__device__ __forceinline__ uint64_t row_key(const ColumnDesc* cols, const SortSpec* specs, int nkeys,
-                                            const int32_t* __restrict__ ranks, const uint32_t* __restrict__ seq,
-                                            int seq_bits, int64_t row) {
-  uint64_t k = 0;
+// The packed ordering keys (identical to tt_sort_keys and ColumnarIndex.sort_keys_numpy) of the
+// 16 rows [row0, row0 + 16) (row0 a multiple of 16), for the rows set in
+// `sel` (others are left 0): per sort key one vector load of the 16 codes, then the rank lookups
+// of all selected rows issued back to back, then one 64-byte load of the sequences -- three
+// dependent memory rounds per group instead of three per row.
+__device__ __forceinline__ void keys16(const ColumnDesc* cols, const SortSpec* specs, int nkeys,
+                                       const int32_t* __restrict__ ranks, const uint32_t* __restrict__ seq,
+                                       int seq_bits, int64_t row0, uint32_t sel, uint64_t (&k)[16]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) k[i] = 0;
   for (int j = 0; j < nkeys; ++j) {
     const SortSpec s = specs[j];
-    const int32_t id = load_id(cols[s.col], row);
-    int32_t r = s.missing;
-    if (id >= 0 && id < s.nranks) r = ranks[s.rank_off + id];
-    if (s.desc) r = s.max_rank - r;
-    k = (k << s.bits) | (uint64_t)(uint32_t)r;
+    int32_t ids[16];
+    load16(cols[s.col], row0, ids);
+    int32_t r[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      r[i] = s.missing;
+      if (((sel >> i) & 1u) && ids[i] >= 0 && ids[i] < s.nranks) r[i] = ranks[s.rank_off + ids[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int32_t v = s.desc ? s.max_rank - r[i] : r[i];
+      k[i] = (k[i] << s.bits) | (uint64_t)(uint32_t)v;
+    }
   }
-  return (k << seq_bits) | (uint64_t)seq[row];
+  const uint4* sp = reinterpret_cast<const uint4*>(seq + row0);
+  uint32_t q[16];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const uint4 x = sp[v];
+    q[4 * v] = x.x; q[4 * v + 1] = x.y; q[4 * v + 2] = x.z; q[4 * v + 3] = x.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) k[i] = (k[i] << seq_bits) | (uint64_t)q[i];
 }
 
 __device__ __forceinline__ void min_pair(uint64_t& k, int32_t& r, uint64_t k2, int32_t r2) {
@@ -101,11 +115,15 @@ tt_zone_argmin(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   if (r0 < nrows) {
     uint32_t lv = (uint32_t)live[r0 >> 4] | ((uint32_t)live[(r0 >> 4) + 1] << 16);
     if (r0 + 32 > nrows) lv &= (nrows - r0 >= 32) ? ~0u : ((1u << (uint32_t)(nrows - r0)) - 1u);
-    while (lv) {
-      const int b = __ffs(lv) - 1;
-      lv &= lv - 1;
-      const int64_t row = r0 + b;
-      min_pair(best, arg, row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row), (int32_t)row);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const uint32_t sel = (lv >> (16 * g)) & 0xFFFFu;
+      if (!sel) continue;
+      uint64_t k[16];
+      keys16(s_cols, s_specs, nkeys, ranks, seq, seq_bits, r0 + 16 * g, sel, k);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if ((sel >> i) & 1u) min_pair(best, arg, k[i], (int32_t)(r0 + 16 * g + i));
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -165,13 +183,12 @@ tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   else run_program<1>(cols, prog, prog_len, bitmaps, row0, m);
   uint32_t sel = row0[0] < nrows ? (m[0] & (uint32_t)live[row0[0] >> 4]) : 0u;
   if (row0[0] < nrows && row0[0] + 16 > nrows) sel &= (1u << (uint32_t)(nrows - row0[0])) - 1u;
+  uint64_t key[16];
+  keys16(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row0[0], sel, key);
   if (bound != ~0ull) {  // keep the matches that order before every unread tile
-    uint32_t keep = 0, b = sel;
-    while (b) {
-      const int i = __ffs(b) - 1;
-      b &= b - 1;
-      if (row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row0[0] + i) < bound) keep |= 1u << i;
-    }
+    uint32_t keep = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) keep |= (uint32_t)(((sel >> i) & 1u) && key[i] < bound) << i;
     sel = keep;
   }
   const uint32_t cnt = __popc(sel);
@@ -194,13 +211,12 @@ tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   }
   __syncthreads();
   uint32_t pos = block_base + wave_counts[wave] + incl - cnt;
-  while (sel) {
-    const int b = __ffs(sel) - 1;
-    sel &= sel - 1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (!((sel >> i) & 1u)) continue;
     if (pos < cap) {
-      const int64_t row = row0[0] + b;
-      cand_keys[pos] = row_key(s_cols, s_specs, nkeys, ranks, seq, seq_bits, row);
-      cand_rows[pos] = (int32_t)row;
+      cand_keys[pos] = key[i];
+      cand_rows[pos] = (int32_t)(row0[0] + i);
     }
     ++pos;
   }
@@ -223,25 +239,54 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
     rows[i] = i < n ? cand_rows[i] : -1;
   }
   __syncthreads();
+  // Bitonic network over p elements.  Each wave owns a contiguous chunk of C = p / 16 elements
+  // (the whole array in wave 0 when p < 32): every pass whose stride is below C only pairs
+  // elements inside one chunk, so it runs under a wave barrier; only the strides >= C (cross-
+  // chunk, ~10 passes at p = 4096) need the workgroup barrier -- instead of one per pass (78).
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int chunk = p >= 32 ? p / (kTopkBlock / 64) : p;
+  const bool owner = p >= 32 || wave == 0;
+  const int base = p >= 32 ? wave * chunk : 0;
+  auto cmpx = [&](int lo, int stride, int size) {
+    const int hi = lo | stride;
+    const bool up = (lo & size) == 0;
+    const uint64_t a = keys[lo], b = keys[hi];
+    if ((a > b) == up) {
+      keys[lo] = b;
+      keys[hi] = a;
+      const int32_t t = rows[lo];
+      rows[lo] = rows[hi];
+      rows[hi] = t;
+    }
+  };
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto local_passes = [&](int size, int from_stride) {  // strides from_stride .. 1 inside the chunk
+    if (!owner) return;
+    for (int stride = from_stride; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (chunk >> 1); i += 64) {
+        const int li = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        cmpx(base + li, stride, size);
+      }
+      wave_sync();
+    }
+  };
   for (int size = 2; size <= p; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+    int stride = size >> 1;
+    if (stride >= chunk) __syncthreads();  // the chunks' wave-local passes are done
+    for (; stride >= chunk && stride > 0; stride >>= 1) {  // cross-chunk: the whole workgroup
       for (int i = threadIdx.x; i < (p >> 1); i += kTopkBlock) {
-        // i-th compare-exchange pair of this pass: lo has bit `stride` clear
         const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
-        const int hi = lo | stride;
-        const bool up = (lo & size) == 0;
-        const uint64_t a = keys[lo], b = keys[hi];
-        if ((a > b) == up) {
-          keys[lo] = b;
-          keys[hi] = a;
-          const int32_t t = rows[lo];
-          rows[lo] = rows[hi];
-          rows[hi] = t;
-        }
+        cmpx(lo, stride, size);
       }
       __syncthreads();
     }
+    local_passes(size, stride);
   }
+  __syncthreads();
   const int upto = n < k ? n : k;
   const int written = upto > offset ? upto - offset : 0;
   for (int i = threadIdx.x; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];

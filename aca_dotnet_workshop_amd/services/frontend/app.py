@@ -38,6 +38,7 @@ from jinja2 import Environment, FileSystemLoader, select_autoescape
 from ...models import FIELD_DISPLAY, REQUIRED_FIELDS, TaskModel, parse_datetime, tasks_from_json
 from ...models.dotnet import is_guid, naive_utc
 from ...sdk import SidecarClient
+from ...sdk.client import RawJson
 from ...web.app import WebApp
 from ...web.client import HttpClient
 from ...web.http import HTTPError, Request, Response, redirect
@@ -197,8 +198,15 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
             return redirect("/")
         return render(req, "tasks_create.html", values={}, errors={}, display=FIELD_DISPLAY)
 
+    fast_form = _native_form() if mode == "dapr" else None
+
     @app.route("/Tasks/Create", ("POST",), name="TasksCreatePost", include_in_schema=False)
     async def create_post(req: Request) -> Response:
+        if fast_form is not None:  # form, cookies, antiforgery and binding in one native pass
+            made = fast_form(req.body, (req.headers.get("cookie") or "").encode(), af.key)
+            if made is not None and made[0]:
+                await gw.call("POST", "api/tasks", RawJson(made[1].decode()))
+                return redirect("/Tasks/Index")
         form = req.form()
         require_af(req, form)
         values, errors = _bind(form, "TaskAdd")
@@ -247,6 +255,16 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
 
     app.on_shutdown.append(gw.close)
     return app
+
+
+def _native_form():
+    """``native/src/formcodec.hpp``'s Create-post binder, or None without the native module: it
+    answers exactly like the page below for the posts it accepts and declines the rest."""
+    try:
+        from ...native import load
+        return load().frontend_create_form
+    except Exception:
+        return None
 
 
 def _bind(form: dict[str, str], prefix: str) -> tuple[dict[str, Any], dict[str, str]]:

@@ -34,6 +34,9 @@ def main() -> None:
                     help="skip the multi-threaded native CPU executor (the fair host baseline)")
     ap.add_argument("--query", action="store_true", help="also time the whole paged query path (ColumnarIndex.query)")
     ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4/8; 0 = default)")
+    ap.add_argument("--page", action="store_true",
+                    help="also time the paged sweep query: ORDER BY taskCreatedOn (clustered by insertion) LIMIT 1000 "
+                         "through the zone-map page path (hip/page_topk.hip)")
     ap.add_argument("--sorted", action="store_true",
                     help="also time ORDER BY taskDueDate DESC: top-100 page and full ordering (tt_sort_keys + sort)")
     a = ap.parse_args()
@@ -102,6 +105,52 @@ def main() -> None:
            "device": torch.cuda.get_device_name(0), "tile_rows": TILE,
            "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths,
            "range_leaves": int((prog.code[:, 0] == 7).sum())}
+    if a.page:
+        # creation timestamps: one per 64 rows, rising with the row (rows are appended as tasks
+        # are created), 1.56 M distinct values at 1e8 rows -- a 4-byte dictionary column
+        c = Column("taskCreatedOn")
+        ndist = (n + 63) // 64
+        t_enc = time.perf_counter()
+        for i in range(ndist):
+            c.encode(f"2025-{1 + i // 2_678_400 % 12:02d}-{1 + i // 86_400 % 28:02d}T{i // 3600 % 24:02d}:"
+                     f"{i // 60 % 60:02d}:{i % 60:02d}.{i % 7}Z")
+        ix.columns.append(c)
+        ix.col_of["taskCreatedOn"] = len(ix.columns) - 1
+        ids = np.full((1, ix.cap), -1, dtype=np.int32)
+        ids[0, :n] = np.arange(n, dtype=np.int64) // 64
+        ix.ids = np.concatenate([ix.ids, ids])
+        ix.version += 1
+        ix._full_dirty = True
+        ix.seq[:n] = np.arange(1, n + 1)
+        sort = [{"key": "taskCreatedOn", "order": "ASC"}]
+        q = {"filter": flt, "sort": sort, "page": {"limit": 1000}}
+        c.ranks()
+        res["page_setup_s"] = round(time.perf_counter() - t_enc, 2)
+        t0 = time.perf_counter()
+        rows, token = ix.query_rows(q, k)  # first page: uploads the column, builds every tile's zone argmin
+        torch.cuda.synchronize()
+        res["page_first_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+        calls = {"pages": 0, "tiles": 0}
+        real_page = k.page
+
+        def counted(*args, **kw):
+            calls["pages"] += 1
+            calls["tiles"] += len(args[9])
+            return real_page(*args, **kw)
+        k.page = counted
+        it = max(5, a.iters)
+        t0 = time.perf_counter()
+        for _ in range(it):
+            rows, token = ix.query_rows(q, k)
+        res["page1000_ms"] = round((time.perf_counter() - t0) / it * 1e3, 4)
+        k.page = real_page
+        res["page_kernel_calls_per_query"] = calls["pages"] / it
+        res["page_tiles_per_query"] = calls["tiles"] / it
+        # the page equals the host ordering of the full selection (first 1000)
+        sel = out.cpu().numpy()
+        plan = ix.sort_specs(sort)
+        want = sel[np.argsort(ix.sort_keys_numpy(sel, plan), kind="stable")[:1000]]
+        res["page_match"] = bool(np.array_equal(rows, want)) and token == "1000"
     if a.sorted:
         ix.seq[:n] = rng.permutation(n) + 1  # updates move rows: result order != row order
         ix._full_dirty = True
