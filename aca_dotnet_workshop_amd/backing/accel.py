@@ -26,6 +26,7 @@ from __future__ import annotations
 import logging
 import os
 import threading
+import time
 from typing import Any
 
 from ..ops.columnar import ColumnarIndex, Unsupported, filter_paths
@@ -106,7 +107,9 @@ class CollectionAccelerator:
         if not self.should_accelerate(q, store):
             self.stats["native"] += 1
             return None
+        t_wait = time.perf_counter()
         with self.lock:
+            t0 = time.perf_counter()
             try:
                 if self.index is None:
                     self.build(store, filter_paths(q.get("filter")) + [s["key"] for s in q.get("sort") or []
@@ -118,6 +121,7 @@ class CollectionAccelerator:
                 self.disabled, self.index = True, None
                 self.stats["fallback"] += 1
                 return None
+            t1 = time.perf_counter()
             flt = q.get("filter") or {}
             if prefix:
                 flt = {"AND": [{"EQ": {PREFIX_PATH: prefix}}, flt]} if flt else {"EQ": {PREFIX_PATH: prefix}}
@@ -149,7 +153,12 @@ class CollectionAccelerator:
             self.stats["gpu" if k is not None else "cpu"] += 1
             text, skipped = res
             self.stats["skipped_rows"] += skipped
-            return text.decode()
+            out = text.decode()
+            t2 = time.perf_counter()
+            # where an accelerated query spends its time (summed; stats route reports them)
+            for key, v in (("lock_wait_ms", t0 - t_wait), ("sync_ms", t1 - t0), ("select_and_results_ms", t2 - t1)):
+                self.stats[key] = round(self.stats.get(key, 0.0) + v * 1e3, 3)
+            return out
 
 
 def accelerator_from_env() -> tuple[str, int]:

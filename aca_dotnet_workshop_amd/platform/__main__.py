@@ -348,18 +348,35 @@ def cmd_image(a) -> int:
     if a.push:
         from .registry import LocalRegistry
         reg = LocalRegistry(a.push, a.registry_root)
+    tags = a.tag or ["latest"]
     for row in image.report(a.out, a.service, a.verify):
         if reg is not None and row["variant"] == a.variant:
             repo = f"tasksmanager/{image.SERVICES[row['service']]}"
-            row["pushed"] = f"{reg.login_server}/{repo}:{a.tag}@{reg.push(row['archive'], repo, a.tag)}"
+            row["pushed"] = [f"{reg.login_server}/{repo}:{t}@{reg.push(row['archive'], repo, t)}" for t in tags]
         print(json.dumps(row), flush=True)
     return 0
 
 
 def cmd_acr(a) -> int:
-    """``az acr repository list/show-tags``: what a registry holds."""
-    from .registry import LocalRegistry
+    """``az acr create`` / ``az acr import`` / ``az acr repository list``."""
+    from .registry import LocalRegistry, RegistryError
     reg = LocalRegistry(a.name, a.registry_root)
+    if a.action == "create":
+        print(f"ACR {reg.login_server} created" if reg.create() else f"ACR {reg.login_server} already exists.")
+        return 0
+    if a.action == "import":
+        if not reg.exists():
+            print(f"ERROR: registry {a.name} does not exist", file=sys.stderr)
+            return 1
+        server, _, rest = a.source.partition("/")
+        src = LocalRegistry(server.split(".", 1)[0], a.registry_root)
+        try:
+            digest = reg.import_image(src, a.source, a.image, force=a.force)
+        except RegistryError as e:
+            print(f"ERROR: {e}", file=sys.stderr)
+            return 1
+        print(f"imported {a.source} -> {reg.login_server}/{a.image}@{digest}")
+        return 0
     print(json.dumps({"loginServer": reg.login_server, "repositories": reg.repositories()}, indent=1))
     return 0
 
@@ -441,11 +458,15 @@ def main(argv: list[str] | None = None) -> int:
     p.add_argument("--verify", action="store_true", help="run each image under chroot and probe it (root)")
     p.add_argument("--push", metavar="REGISTRY", default=None, help="push to this registry (ACR name)")
     p.add_argument("--variant", choices=["standard", "chiseled"], default="chiseled", help="which variant --push pushes")
-    p.add_argument("--tag", default="latest")
+    p.add_argument("--tag", action="append", default=None, help="tag to push (repeatable; default latest)")
     p.add_argument("--registry-root", default=None, help="where registries live ($TT_CONTAINER_REGISTRY_ROOT)")
     p.set_defaults(fn=cmd_image)
-    p = sub.add_parser("acr", help="list a registry's repositories and tags")
+    p = sub.add_parser("acr", help="registries: create, import an image, list repositories and tags")
+    p.add_argument("action", nargs="?", choices=["list", "create", "import"], default="list")
     p.add_argument("name")
+    p.add_argument("--source", help="import: <registry login server>/<repo>:<tag>")
+    p.add_argument("--image", help="import: <repo>[:tag] in this registry")
+    p.add_argument("--force", action="store_true")
     p.add_argument("--registry-root", default=None)
     p.set_defaults(fn=cmd_acr)
     argv = list(sys.argv[1:] if argv is None else argv)

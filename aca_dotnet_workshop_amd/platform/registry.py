@@ -85,6 +85,7 @@ class LocalRegistry:
     # ------------------------------------------------------------------ push / resolve
     def push(self, archive: str | os.PathLike, repo: str, tag: str = "latest") -> str:
         """``docker push`` of an OCI image-layout archive; returns the manifest digest."""
+        self.create()  # a push to a registry nobody created yet creates it (the dev-loop shortcut)
         with tarfile.open(archive) as tf:
             index = json.load(tf.extractfile("index.json"))
             man_digest = index["manifests"][0]["digest"]
@@ -141,6 +142,38 @@ class LocalRegistry:
             repo = str(tags.parent.relative_to(base))
             out.append({"repository": repo, "tags": {t.name: t.read_text().strip() for t in sorted(tags.iterdir())}})
         return out
+
+    # ------------------------------------------------------------------ create / import
+    def exists(self) -> bool:
+        return (self.dir / "registry.json").exists()
+
+    def create(self, sku: str = "Basic") -> bool:
+        """``az acr create``: True when the registry was created, False when it already existed."""
+        if self.exists():
+            return False
+        self.dir.mkdir(parents=True, exist_ok=True)
+        tmp = self.dir / "registry.json.tmp"
+        tmp.write_text(json.dumps({"name": self.name, "loginServer": self.login_server, "sku": sku}))
+        os.replace(tmp, self.dir / "registry.json")
+        return True
+
+    def import_image(self, source: "LocalRegistry", ref: str, image: str, force: bool = False) -> str:
+        """``az acr import --source <source>/<repo>:<tag> --image <repo>[:tag]``: copy the manifest
+        and its blobs from another registry, tag it here; returns the manifest digest."""
+        digest = source.resolve(ref)
+        repo, _, tag = image.partition(":")
+        tag = tag or "latest"
+        tf_ = self._tag_file(repo, tag)
+        if tf_.exists() and not force and tf_.read_text().strip() != digest:
+            raise RegistryError(f"{self.login_server}/{repo}:{tag} exists (use force to overwrite)")
+        man_bytes = source.read_blob(digest)
+        man = json.loads(man_bytes)
+        for ref_ in [man["config"]] + man["layers"]:
+            self._put_blob(source.read_blob(ref_["digest"]))
+        self._put_blob(man_bytes)
+        tf_.parent.mkdir(parents=True, exist_ok=True)
+        tf_.write_text(digest)
+        return digest
 
     # ------------------------------------------------------------------ pull
     def unpack(self, digest: str, cache: str | os.PathLike) -> tuple[Path, dict[str, Any]]:

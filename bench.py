@@ -219,6 +219,9 @@ class OverdueSweeper:
                 "sweep_max_ms": round(ms[-1], 2) if ms else None,
                 "tasks_marked_overdue": sum(r.get("markedOverdue", 0) for _, r in self.runs),
                 "pages": sum(r.get("pages", 0) for _, r in self.runs),
+                # the job's two hops (GET api/overduetasks, POST markoverdue), summed over sweeps
+                "query_ms_total": round(sum(r.get("queryMs", 0.0) for _, r in self.runs), 1),
+                "mark_ms_total": round(sum(r.get("markMs", 0.0) for _, r in self.runs), 1),
                 "first_error": self.errors[0] if self.errors else None}
 
 
@@ -601,7 +604,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             acc = _collection_stats(backing).get("accelerator", {})
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
-                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows")}
+                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
+                          "store_ms_total": {k2: acc.get(k2) for k2 in ("lock_wait_ms", "sync_ms",
+                                                                         "select_and_results_ms")}}
         # the same environment, load straight at the API sidecars' invoke (round 2's topology)
         direct = None
         dsteps = a.direct_steps if a.direct_steps >= 0 else max(1, a.steps // 4)
