@@ -2,7 +2,7 @@
 PY ?= python
 ENV_DIR ?= .tt-env
 
-.PHONY: build test test-gpu sanitize bench bench-query bench-query-e2e images up down status metrics validate what-if docs docs-local clean
+.PHONY: build test test-gpu sanitize bench bench-query bench-query-e2e images up down status metrics validate what-if docs docs-local build-docs-website pipeline clean
 
 build:            ## compile native engines, sidecar data plane, load generator and gfx950 HIP kernels in-tree
 	$(PY) -c "import __graft_entry__ as g; g.build()"
@@ -46,8 +46,16 @@ metrics:          ## live metrics of the running environment
 down:
 	$(PY) -m aca_dotnet_workshop_amd.platform down --env-dir $(ENV_DIR)
 
-docs:             ## build the docs site (needs mkdocs-material)
+SITE_DIR ?= dist/site
+
+build-docs-website:  ## the workshop site, strict (reference Makefile target; used by the docs workflows)
+	$(PY) -m aca_dotnet_workshop_amd.utils.docsite build --out $(SITE_DIR)
+
+docs:             ## build the docs site with mkdocs-material instead (needs mkdocs)
 	mkdocs build --strict
+
+pipeline:         ## run a workflow locally: make pipeline FILE=.github/workflows/infra-deploy.yml ARGS="--var X=y"
+	$(PY) -m aca_dotnet_workshop_amd.utils.pipeline $(FILE) $(ARGS)
 
 docs-local:
 	mkdocs serve

@@ -103,7 +103,8 @@ def publish(site: str | os.PathLike, pages: str | os.PathLike, dest: str = "", a
     site, pages = Path(site), Path(pages)
     pages.mkdir(parents=True, exist_ok=True)
     target = pages / dest if dest else pages
-    keep = {"pr-preview", "versions.json"} | {v["version"] for v in _versions(pages)} | ({alias} if alias else set())
+    keep = {"pr-preview", "versions.json"} | {v["version"] for v in _versions(pages)} | \
+        {a for v in _versions(pages) for a in v.get("aliases", [])} | ({alias} if alias else set())
     if target.exists():
         for p in target.iterdir():
             if dest or p.name not in keep:

@@ -380,8 +380,9 @@ def run(pipeline: Pipeline, ctx: dict[str, Any] | None = None, workdir: str | os
     params = dict(pipeline.parameters)
     params.update(ctx.get("parameters") or {})
     ctx["parameters"] = params
-    gh = ctx["github"]
-    gh.setdefault("event", {}).setdefault("inputs", dict(ctx["inputs"]))
+    gh = ctx["github"] = json.loads(json.dumps(ctx["github"]))  # the caller's context stays untouched
+    gh.setdefault("event", {}).setdefault("inputs", {})
+    gh["event"]["inputs"].update({k: (str(v).lower() if isinstance(v, bool) else v) for k, v in ctx["inputs"].items()})
     base_env = {**pipeline.env, **(env_overrides or {})}
     results: dict[str, list[Result]] = {}
     done: list[Result] = []
@@ -458,7 +459,8 @@ def _run_job(p: Pipeline, job: Job, jctx: dict, status: dict, workdir: Path, bas
     env.update(base_env)
     env.update(job.env)
     env.update(job.variables)
-    env.update({"GITHUB_ENV": str(genv), "GITHUB_OUTPUT": str(gout), "CI": "true",
+    (tmp / "runner-temp").mkdir()
+    env.update({"GITHUB_ENV": str(genv), "GITHUB_OUTPUT": str(gout), "CI": "true", "RUNNER_TEMP": str(tmp / "runner-temp"),
                 "PYTHONPATH": str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")})
     steps_ctx: dict[str, dict] = {}
     failed = False
