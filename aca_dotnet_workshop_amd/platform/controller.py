@@ -232,8 +232,17 @@ class EnvironmentController:
             doc = yaml.safe_load(self.m.component_path(c).read_text())
             if "componentType" in doc:
                 doc["name"] = c["name"]
+                items = doc.setdefault("metadata", [])
             else:
                 doc.setdefault("metadata", {})["name"] = c["name"]
+                items = doc.setdefault("spec", {}).setdefault("metadata", [])
+            # manifest-level metadata overrides (dapr-components.bicep sets metadata per deployment)
+            for ov in c.get("metadata") or []:
+                hit = next((m for m in items if m.get("name") == ov["name"]), None)
+                if hit is None:
+                    items.append({"name": ov["name"], "value": str(ov.get("value", ""))})
+                else:
+                    hit["value"] = str(ov.get("value", ""))
             (cdir / f"{c['name']}.yaml").write_text(yaml.safe_dump(doc, sort_keys=False))
         self.event("DaprComponentsInstalled", components=[c["name"] for c in self.m.components])
 

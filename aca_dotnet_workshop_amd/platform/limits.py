@@ -10,7 +10,10 @@ enforcement mechanisms, chosen at start-up and reported in the environment statu
   ``cpu.max`` (quota per 100 ms period) and ``memory.max``; the kernel throttles and
   OOM-kills, the controller sees the dead replica and restarts it (``ReplicaOOMKilled``
   when ``memory.events`` counted an OOM kill).
-* ``watchdog`` -- no delegated cgroup (unprivileged containers, this CI box): memory is
+* ``cgroup1-cpu`` -- no delegated v2 subtree, but a writable cgroup v1 ``cpu`` hierarchy (a
+  root container on a v1 host): one cgroup per replica with ``cpu.cfs_quota_us`` -- the same
+  kernel CFS bandwidth control as ``cpu.max`` -- and memory by the watchdog below.
+* ``watchdog`` -- no writable cgroup at all (unprivileged containers): memory is
   enforced by the controller, which sums the RSS of the replica's processes every
   supervision tick and kills + restarts a replica above its limit (``ReplicaOOMKilled``),
   like ACA restarting an OOM-killed container; CPU is enforced, when enabled, by a duty-cycle
@@ -18,7 +21,8 @@ enforcement mechanisms, chosen at start-up and reported in the environment statu
   100 ms period, SIGCONT at the next period) -- otherwise only accounted.
 
 ``environment.resourceLimits`` in the manifest: ``{memory: true|false, cpu: true|false}``
-(defaults: memory enforced, CPU accounted only, so a development box stays usable).
+(both enforced in ``deploy/main.yaml``; the controller's own default without the key is memory
+enforced, CPU accounted).  ``describe()`` reports which mechanism is in force.
 """
 from __future__ import annotations
 
@@ -85,6 +89,22 @@ def cpu_seconds(procs: list[psutil.Process]) -> float:
     return total
 
 
+def cgroup1_cpu() -> Path | None:
+    """This process's writable cgroup v1 ``cpu`` directory (CFS bandwidth control), if any."""
+    try:
+        rel = next((ln.split(":", 2)[2].strip() for ln in Path("/proc/self/cgroup").read_text().splitlines()
+                    if ln.split(":", 2)[1] in ("cpu", "cpu,cpuacct", "cpuacct,cpu")), None)
+        for mount in ("cpu", "cpu,cpuacct"):
+            base = CGROUP_ROOT / mount
+            if rel is not None and (base / "cpu.cfs_quota_us").exists():
+                d = base / rel.lstrip("/")
+                if (d / "cpu.cfs_quota_us").exists() and os.access(d, os.W_OK):
+                    return d
+    except (OSError, IndexError):
+        pass
+    return None
+
+
 def delegated_cgroup() -> Path | None:
     """This process's cgroup v2 directory when we may create children with cpu+memory."""
     try:
@@ -114,6 +134,7 @@ class ReplicaState:
     stopped: bool = False
     throttled_periods: int = 0
     peak_rss: int = 0
+    cpu_cgroup: Path | None = None   # cgroup v1 cpu directory (mode cgroup1-cpu)
 
 
 class ResourceLimiter:
@@ -124,6 +145,7 @@ class ResourceLimiter:
         base = cgroup_base if cgroup_base is not None else (delegated_cgroup() if allow_cgroup else None)
         self.mode = "cgroup2" if base is not None else "watchdog"
         self.root: Path | None = None
+        self.cpu_root: Path | None = None  # cgroup v1 cpu hierarchy (mode cgroup1-cpu)
         if base is not None:
             self.root = base / f"tt-{env_name}"
             try:
@@ -131,10 +153,21 @@ class ResourceLimiter:
                 (self.root / "cgroup.subtree_control").write_text("+cpu +memory")
             except OSError:
                 self.mode, self.root = "watchdog", None
+        if self.mode == "watchdog" and enforce_cpu and allow_cgroup and cgroup_base is None:
+            v1 = cgroup1_cpu()
+            if v1 is not None:
+                try:
+                    self.cpu_root = v1 / f"tt-{env_name}"
+                    self.cpu_root.mkdir(exist_ok=True)
+                    self.mode = "cgroup1-cpu"
+                except OSError:
+                    self.cpu_root = None
         self.replicas: dict[str, ReplicaState] = {}
 
     def describe(self) -> dict:
-        cpu = ("cgroup cpu.max" if self.mode == "cgroup2" else "duty-cycle throttle") if self.enforce_cpu else "accounted"
+        cpu = {"cgroup2": "cgroup cpu.max", "cgroup1-cpu": "cgroup v1 cpu.cfs_quota_us",
+               "watchdog": f"duty-cycle throttle (SIGSTOP/SIGCONT, {int(PERIOD_S * 1000)} ms period)"}[self.mode] \
+            if self.enforce_cpu else "accounted"
         mem = ("cgroup memory.max" if self.mode == "cgroup2" else "RSS watchdog + restart") if self.enforce_memory \
             else "accounted"
         return {"mode": self.mode, "cpu": cpu, "memory": mem}
@@ -154,8 +187,25 @@ class ResourceLimiter:
                 self._adopt(st)
             except OSError:
                 st.cgroup = None
+        elif self.cpu_root is not None:
+            cg = self.cpu_root / name
+            try:
+                cg.mkdir(exist_ok=True)
+                (cg / "cpu.cfs_period_us").write_text("100000")
+                (cg / "cpu.cfs_quota_us").write_text(str(max(1000, int(limits.cpu * 100000))))
+                st.cpu_cgroup = cg
+                self._adopt_v1(st)
+            except OSError:
+                st.cpu_cgroup = None
         st.period_cpu = cpu_seconds(tree(pid))
         return st
+
+    def _adopt_v1(self, st: ReplicaState) -> None:
+        for p in tree(st.pid):
+            try:
+                (st.cpu_cgroup / "cgroup.procs").write_text(str(p.pid))
+            except OSError:
+                pass
 
     def remove(self, name: str) -> None:
         st = self.replicas.pop(name, None)
@@ -163,11 +213,12 @@ class ResourceLimiter:
             return
         if st.stopped:
             self._signal(st, signal.SIGCONT)
-        if st.cgroup is not None:
-            try:
-                st.cgroup.rmdir()
-            except OSError:
-                pass
+        for cg in (st.cgroup, st.cpu_cgroup):
+            if cg is not None:
+                try:
+                    cg.rmdir()
+                except OSError:
+                    pass
 
     def _adopt(self, st: ReplicaState) -> None:
         """Move the replica's processes (children started since) into its cgroup."""
@@ -197,6 +248,8 @@ class ResourceLimiter:
                 except (OSError, ValueError):
                     pass
                 continue
+            if st.cpu_cgroup is not None:
+                self._adopt_v1(st)  # children the replica started since (its app, the data plane)
             used = rss(tree(st.pid))
             st.peak_rss = max(st.peak_rss, used)
             if self.enforce_memory and used > st.limits.memory:
@@ -209,7 +262,7 @@ class ResourceLimiter:
     def throttle_tick(self, now: float | None = None) -> None:
         """Call every few ms: stop a replica's group once it has used ``cpu x PERIOD_S`` CPU
         seconds in the current period, resume it when the next period starts."""
-        if not self.enforce_cpu or self.mode == "cgroup2":
+        if not self.enforce_cpu or self.mode != "watchdog":
             return
         now = time.monotonic() if now is None else now
         for st in list(self.replicas.values()):
@@ -232,8 +285,9 @@ class ResourceLimiter:
     def release_all(self) -> None:
         for name in list(self.replicas):
             self.remove(name)
-        if self.root is not None:
-            try:
-                self.root.rmdir()
-            except OSError:
-                pass
+        for root in (self.root, self.cpu_root):
+            if root is not None:
+                try:
+                    root.rmdir()
+                except OSError:
+                    pass

@@ -7,6 +7,8 @@ import subprocess
 import sys
 import time
 
+import pytest
+
 from aca_dotnet_workshop_amd.platform.limits import Limits, ResourceLimiter, cpu_seconds, parse_memory, tree
 
 
@@ -67,6 +69,29 @@ def test_cpu_throttle_holds_quota():
         wall = time.monotonic() - t0
         assert used / wall < 0.45, used / wall  # ~0.25 cores (+ tick granularity), not 1.0
         assert st.throttled_periods >= 10
+    finally:
+        lim.release_all()
+        os.killpg(p.pid, 9)
+        p.wait()
+
+
+def test_cpu_quota_by_cgroup_v1_when_writable():
+    """Where a cgroup v1 ``cpu`` hierarchy is writable (a root container on a v1 host), the
+    replica gets CFS bandwidth control -- the kernel holds it at its share, no signals."""
+    from aca_dotnet_workshop_amd.platform.limits import cgroup1_cpu, delegated_cgroup
+    if delegated_cgroup() is not None or cgroup1_cpu() is None:
+        pytest.skip("no writable cgroup v1 cpu hierarchy here (or v2 is delegated)")
+    p = _spawn("while True: pass")
+    lim = ResourceLimiter("tv1", enforce_cpu=True)
+    try:
+        assert lim.describe() == {"mode": "cgroup1-cpu", "cpu": "cgroup v1 cpu.cfs_quota_us",
+                                  "memory": "RSS watchdog + restart"}
+        st = lim.add("busy-0", p.pid, Limits(0.25, parse_memory("0.5Gi")))
+        assert (st.cpu_cgroup / "cpu.cfs_quota_us").read_text().strip() == "25000"
+        c0, t0 = cpu_seconds(tree(p.pid)), time.monotonic()
+        time.sleep(2.0)
+        used = cpu_seconds(tree(p.pid)) - c0
+        assert used / (time.monotonic() - t0) < 0.35
     finally:
         lim.release_all()
         os.killpg(p.pid, 9)
