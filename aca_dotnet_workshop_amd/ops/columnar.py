@@ -185,6 +185,10 @@ class Column:
         self._num_cache: np.ndarray | None = None
         self._rank_cache: np.ndarray | None = None
         self.rank_version = 0  # bumps whenever a new value may shift the sort ranks
+        # every value a str without a trailing NUL (numpy's fixed-width strings drop those):
+        # the ranks are then positions in the sorted dictionary (_string_ranks)
+        self.str_only = True
+        self._str_sorted = None
 
     def encode(self, v: Any) -> int:
         if v is _MISSING:
@@ -194,10 +198,35 @@ class Column:
         if i is None:
             i = self.ids[k] = len(self.values)
             self.values.append(v)
+            if type(v) is not str or v.endswith("\x00"):
+                self.str_only = False
             self._num_cache = None
             self._rank_cache = None
             self.rank_version += 1
         return i
+
+    def encode_json_many(self, texts: list[str]) -> np.ndarray:
+        """Dictionary ids of JSON value texts (the native mirror's new dictionary entries).
+        Strings -- timestamps, names, e-mails, the values a growing collection adds on every
+        write -- are decoded in one ``json.loads`` and appended in bulk: the native dictionary
+        holds each string once, so none is already here (the dictionary's size confirms it) and
+        no per-value ``vkey`` or dictionary probe is needed."""
+        if texts and all(t[:1] == '"' for t in texts):
+            joined = ",".join(texts)
+            strs = json.loads("[" + joined + "]")
+            base = len(self.values)
+            self.ids.update(zip(["s" + x for x in strs], range(base, base + len(strs))))
+            if len(self.ids) == base + len(strs):
+                self.values.extend(strs)
+                if self.str_only and "\\u0000" in joined and any(x.endswith("\x00") for x in strs):
+                    self.str_only = False
+                self._num_cache = None
+                self._rank_cache = None
+                self.rank_version += 1
+                return np.arange(base, base + len(strs), dtype=np.int32)
+            # a value was already here (not the native dictionary's invariant): per value
+            self.ids = {vkey(v): i for i, v in enumerate(self.values)}
+        return np.fromiter((self.encode(json.loads(t)) for t in texts), dtype=np.int32, count=len(texts))
 
     def lookup(self, v: Any) -> int:
         return self.ids.get(vkey(v), -2)
@@ -240,18 +269,9 @@ class Column:
         return self._rank_cache
 
     def _all_strings(self) -> bool:
-        n0 = getattr(self, "_str_checked", 0)
-        if n0 > len(self.values):  # dictionary rebuilt
-            n0 = 0
+        if not self.str_only:
             self._str_sorted = None
-        # (numpy's fixed-width strings drop trailing NULs: such values take the general path)
-        ok = all(type(v) is str and not v.endswith("\x00") for v in self.values[n0:])
-        if ok:
-            self._str_checked = len(self.values)
-        else:
-            self._str_checked = 0
-            self._str_sorted = None
-        return ok
+        return self.str_only
 
     def _string_ranks(self) -> np.ndarray:
         """A dictionary of strings only (timestamps, e-mails, names): distinct values never tie
@@ -259,32 +279,48 @@ class Column:
         dictionary.  Kept incrementally: values appended since the last call are sorted alone
         and merged in (``searchsorted`` + ``insert``), an O(dictionary) vector pass instead of a
         comparison sort of the whole dictionary per new value -- the overdue sweep orders by
-        ``taskCreatedOn``, whose dictionary grows with every created task."""
+        ``taskCreatedOn``, whose dictionary grows with every created task.  When every new value
+        sorts after the old ones (timestamps of new writes) the sorted copy and the ranks grow
+        in place, in capacity-doubling buffers: O(new values), not O(dictionary)."""
         n = len(self.values)
-        prev = getattr(self, "_str_sorted", None)
+        prev = self._str_sorted
         if prev is None or prev[1] > n:
             arr = np.array(self.values, dtype=str) if n else np.zeros(0, dtype="<U1")
             order = np.argsort(arr, kind="stable")
             r = np.empty(n, dtype=np.int64)
             r[order] = np.arange(1, n + 1)
             self._str_sorted = (arr[order], n, r)
-            return r.copy()
+            return r[:n]
         srt, m, old_r = prev
         if m == n:
-            return old_r.copy()
+            return old_r[:n]
         new = np.array(self.values[m:], dtype=str)
-        width = max(srt.dtype.itemsize, new.dtype.itemsize) // 4
-        srt = srt.astype(f"<U{max(width, 1)}", copy=False)
-        new = new.astype(srt.dtype, copy=False)
         norder = np.argsort(new, kind="stable")
         new_sorted = new[norder]
+        if new_sorted.dtype.itemsize <= srt.dtype.itemsize and (m == 0 or new_sorted[0] > srt[m - 1]):
+            if srt.size < n:  # grow the buffers (doubling): amortised O(1) per appended value
+                cap = max(n, 2 * srt.size, 1024)
+                srt2 = np.empty(cap, dtype=srt.dtype)
+                srt2[:m] = srt[:m]
+                r2 = np.empty(cap, dtype=np.int64)
+                r2[:m] = old_r[:m]
+                srt, old_r = srt2, r2
+            srt[m:n] = new_sorted
+            old_r[m + norder] = np.arange(m + 1, n + 1)
+            self._str_sorted = (srt, n, old_r)
+            return old_r[:n]
+        srt = srt[:m]
+        old_r = old_r[:m]
+        width = max(srt.dtype.itemsize, new.dtype.itemsize) // 4
+        srt = srt.astype(f"<U{max(width, 1)}", copy=False)
+        new_sorted = new_sorted.astype(srt.dtype, copy=False)
         pos = np.searchsorted(srt, new_sorted)            # insertion points in the old order
         before = np.searchsorted(pos, old_r - 1, side="right")  # new values ahead of each old one
         r = np.empty(n, dtype=np.int64)
         r[:m] = old_r + before
         r[m + norder] = pos + np.arange(new.size) + 1
         self._str_sorted = (np.insert(srt, pos, new_sorted), n, r)
-        return r.copy()
+        return r
 
     def _general_ranks(self) -> np.ndarray:
         import functools
@@ -424,7 +460,7 @@ class ColumnarIndex:
         for c, (path, dict_from, values, ids) in enumerate(d["columns"]):
             col = self.columns[c]
             if values:  # new dictionary values, mapped onto Python's equality (vkey)
-                add = np.fromiter((col.encode(json.loads(t)) for t in values), dtype=np.int32, count=len(values))
+                add = col.encode_json_many(values)
                 self._remap[c] = np.concatenate([self._remap[c][:dict_from], add])
             rm = self._remap[c]
             if hi > lo:

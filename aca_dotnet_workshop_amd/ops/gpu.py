@@ -50,6 +50,14 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_page.argtypes = [P, I64, P, P, I32, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, I32,
                                    ctypes.c_uint64, P, P, P]
     lib.tt_launch_page.restype = ctypes.c_int
+    lib.tt_host_alloc.argtypes = [I64]
+    lib.tt_host_alloc.restype = ctypes.c_void_p
+    lib.tt_host_device_ptr.argtypes = [P]
+    lib.tt_host_device_ptr.restype = ctypes.c_void_p
+    lib.tt_host_free.argtypes = [P]
+    lib.tt_host_free.restype = ctypes.c_int
+    lib.tt_stream_sync.argtypes = [P]
+    lib.tt_stream_sync.restype = ctypes.c_int
     lib.tt_tile_rows.restype = ctypes.c_int
     lib.tt_max_depth.restype = ctypes.c_int
     _lib = lib
@@ -156,55 +164,72 @@ class GpuKernels:
             raise RuntimeError(f"tt_rank_encode launch failed ({rc})")
 
     # -- paged ordered queries (hip/page_topk.hip) -------------------------------------------
-    def _h2d_i32(self, name: str, arr):
-        """A small int32 host array in a cached device buffer (one copy, no allocation per call)."""
+    def _mailbox(self, name: str, n: int):
+        """Pinned, coherent, device-mapped host int32 array of at least ``n`` elements (caller
+        holds ``_total_lock``): the page kernels read their tile list from it and write their
+        answer into it, so a page query moves no data through copy kernels."""
         import numpy as np
-        torch = self.torch
-        arr = np.ascontiguousarray(arr, dtype=np.int32)
-        buf = self._buf(name, max(1, arr.size), torch.int32)
-        if arr.size:
-            buf[:arr.size].copy_(torch.from_numpy(arr), non_blocking=False)
-        return buf
+        mb = self._bufs.get(name)
+        if mb is None or mb[2].size < n:
+            if mb is not None:
+                self.lib.tt_host_free(ctypes.c_void_p(mb[0]))
+            size = max(1024, 1 << max(0, int(n) - 1).bit_length())
+            host = self.lib.tt_host_alloc(4 * size)
+            dev = self.lib.tt_host_device_ptr(ctypes.c_void_p(host)) if host else None
+            if not host or not dev:
+                raise RuntimeError("pinned host mailbox allocation failed")
+            arr = np.ctypeslib.as_array((ctypes.c_int32 * size).from_address(host))
+            mb = self._bufs[name] = (host, dev, arr)
+        return mb
+
+    def _sync(self, stream) -> None:
+        rc = self.lib.tt_stream_sync(stream)
+        if rc != 0:
+            raise RuntimeError(f"stream synchronise failed ({rc})")
 
     def zone_argmin(self, table, live16, nrows: int, specs, ranks, seq, seq_bits: int, tiles):
         """Per listed tile (numpy int32), the live row with the smallest packed key (-1: none)."""
-        import numpy as np
+        n = len(tiles)
         with self._total_lock:
-            t = self._h2d_i32("zone_tiles", tiles)
-            out = self._buf("zone_out", max(1, len(tiles)), self.torch.int32)
+            _, tdev, tarr = self._mailbox("zone_tiles", n)
+            _, odev, oarr = self._mailbox("zone_out", n)
+            tarr[:n] = tiles
+            stream = self._stream()
             rc = self.lib.tt_launch_zone_argmin(table.data_ptr(), nrows, live16.data_ptr(), specs.data_ptr(),
                                                 specs.shape[0], ranks.data_ptr(), seq.data_ptr(), seq_bits,
-                                                t.data_ptr(), len(tiles), out.data_ptr(), self._stream())
+                                                tdev, n, odev, stream)
             if rc != 0:
                 raise RuntimeError(f"tt_zone_argmin launch failed ({rc})")
-            return out[:len(tiles)].cpu().numpy().astype(np.int32)
+            self._sync(stream)
+            return oarr[:n].copy()
 
     def page(self, table, live16, nrows: int, prog, bitmaps, specs, ranks, seq, seq_bits: int, tiles, k: int,
              offset: int, bound: int):
         """The rows [offset, k) of the key order among the matches in ``tiles`` (numpy int32), and
         (candidates, complete): see hip/page_topk.hip."""
-        import numpy as np
         torch = self.torch
         if not 0 < k <= self.page_cap or not 0 <= offset <= k:
             raise ValueError("page outside the device top-k capacity")
+        n = len(tiles)
         with self._total_lock:
-            t = self._h2d_i32("page_tiles", tiles)
+            _, tdev, tarr = self._mailbox("page_tiles", n)
+            _, odev, oarr = self._mailbox("page_out", 4 + self.page_cap)
+            tarr[:n] = tiles
             ck = self._buf("page_keys", self.page_cap, torch.int64)
             cr = self._buf("page_rows", self.page_cap, torch.int32)
             if "page_counter" not in self._bufs:  # zeroed once; tt_page_topk resets it after each query
                 self._bufs["page_counter"] = torch.zeros(1, dtype=torch.int32, device=self.device)
-            out = self._buf("page_out", 4 + self.page_cap, torch.int32)
+            stream = self._stream()
             rc = self.lib.tt_launch_page(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
                                          bitmaps.data_ptr(), bitmaps.numel(), specs.data_ptr(), specs.shape[0],
-                                         ranks.data_ptr(), seq.data_ptr(), seq_bits, t.data_ptr(), len(tiles),
+                                         ranks.data_ptr(), seq.data_ptr(), seq_bits, tdev, n,
                                          ck.data_ptr(), cr.data_ptr(), self._bufs["page_counter"].data_ptr(), k,
-                                         offset, ctypes.c_uint64(bound), out.data_ptr(), out.data_ptr() + 16,
-                                         self._stream())
+                                         offset, ctypes.c_uint64(bound), odev, odev + 16, stream)
             if rc != 0:
                 raise RuntimeError(f"tt_page launch failed ({rc})")
-            host = out[:4 + k - offset].cpu().numpy()
-        total, complete, written = int(host[0]), bool(host[1]), int(host[2])
-        return host[4:4 + written].astype(np.int32), total, complete
+            self._sync(stream)
+            total, complete, written = int(oarr[0]), bool(oarr[1]), int(oarr[2])
+            return oarr[4:4 + written].copy(), total, complete
 
     def group_count(self, table, g: int, mask, nrows: int, ngroups: int):
         torch = self.torch

@@ -336,3 +336,23 @@ extern "C" int tt_launch_page(const void* cols, int64_t nrows, const uint16_t* l
                      (uint32_t)kPageCap, k, offset, bound, info, out_rows);
   return (int)hipGetLastError();
 }
+
+// Host-mapped mailboxes for the page path: its inputs (tile ids) and outputs (info + rows) live
+// in pinned, coherent host memory that the kernels read and write directly, so a page query is
+// two kernel launches and one stream synchronise -- no copy kernels, no DMA, no allocation.
+extern "C" void* tt_host_alloc(int64_t bytes) {
+  void* p = nullptr;
+  if (bytes <= 0 || hipHostMalloc(&p, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return nullptr;
+  return p;
+}
+
+extern "C" void* tt_host_device_ptr(void* host) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  return d;
+}
+
+extern "C" int tt_host_free(void* p) { return p ? (int)hipHostFree(p) : 0; }
+
+extern "C" int tt_stream_sync(hipStream_t stream) { return (int)hipStreamSynchronize(stream); }

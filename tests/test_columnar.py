@@ -764,6 +764,35 @@ def test_string_ranks_incremental_match_the_comparison_sort(batches):
     assert c.ranks().tolist() == c._general_ranks().tolist()
 
 
+def test_bulk_string_encode_and_append_ranks():
+    """``encode_json_many`` (the mirror sync's bulk path) gives the ids per-value ``encode``
+    would, the in-place append path (every new value sorts last: new timestamps) keeps the ranks
+    equal to the comparison sort, a value already present falls back per value, and non-string
+    or NUL-terminated values leave the string-only path."""
+    import json as _json
+    from aca_dotnet_workshop_amd.ops.columnar import Column
+    a, b = Column("p"), Column("p")
+    ts = [f"2026-10-17T10:{m:02d}:{s:02d}" for m in range(60) for s in range(0, 60, 7)]
+    for lo in range(0, len(ts), 97):  # ascending batches: the append path
+        batch = ts[lo:lo + 97]
+        got = a.encode_json_many([_json.dumps(x) for x in batch])
+        assert got.tolist() == [b.encode(x) for x in batch]
+        a._rank_cache = None
+        assert a.ranks().tolist() == a._general_ranks().tolist()
+    older = ["2026-10-16T00:00:0" + str(i) for i in range(5)] + ["z\"q\u00e9"]
+    a.encode_json_many([_json.dumps(x) for x in older])  # sorts before the old values: the merge path
+    a._rank_cache = None
+    assert a.ranks().tolist() == a._general_ranks().tolist() and a.str_only
+    n = len(a.values)
+    assert a.encode_json_many([_json.dumps(ts[3]), _json.dumps("new")]).tolist() == [3, n]  # ts[3] exists
+    assert a.lookup(ts[3]) == 3 and a.lookup("new") == n and len(a.ids) == len(a.values)
+    a.encode_json_many([_json.dumps("nul\x00")])
+    assert not a.str_only
+    a._rank_cache = None
+    assert a.ranks().tolist() == a._general_ranks().tolist()
+    assert a.encode_json_many(["1", "true", "null"]).tolist() == [a.lookup(1), a.lookup(True), a.lookup(None)]
+
+
 class _FakePageKernels:
     """The page path's kernels (hip/page_topk.hip) emulated on the host over the index's own
     arrays, so ``ColumnarIndex.page_gpu``'s zone maps, tile choice, retries and continuation
