@@ -318,17 +318,44 @@ class Resolver {
 };
 
 // ------------------------------------------------------------------------------ data plane
+// A partitioned store or broker (backing/shards.py): the collection and the topics are split
+// over several backing processes, one per rank, and a document or message lives on the shard
+// its partition key hashes to (FNV-1a 64 of the key's bytes, modulo the shard count; the
+// Python side computes the same hash).  No shard list: one backing.
+inline uint64_t fnv1a64(std::string_view s) {
+  uint64_t h = 14695981039346656037ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
 struct Store {
   Endpoint backing;
+  std::vector<Endpoint> shards;
   std::string coll_path;  // /cosmos/<acct>/<db>/<coll>
   std::string prefix;
   HeaderList auth;
+  size_t shard_of(std::string_view full_key) const { return shards.empty() ? 0 : fnv1a64(full_key) % shards.size(); }
+  const Endpoint& ep(size_t shard) const { return shards.empty() ? backing : shards[shard]; }
 };
 struct Bus {
   Endpoint backing;
+  std::vector<Endpoint> shards;
   std::string ns;
   HeaderList auth;
+  const Endpoint& ep(std::string_view partition_key) const {
+    return shards.empty() ? backing : shards[fnv1a64(partition_key) % shards.size()];
+  }
 };
+inline std::vector<Endpoint> shard_list(const Value& s) {
+  std::vector<Endpoint> out;
+  if (auto* sh = s.get("shards"); sh && sh->t == Value::Array)
+    for (auto& u : sh->items)
+      if (u.t == Value::String) out.push_back(Endpoint::parse(u.s));
+  if (out.size() == 1) out.clear();
+  return out;
+}
 
 bool is_invoke_hop(const std::string& k) {  // sidecar/runtime.py _HOP + traceparent
   return ev::is_hop_header(k) || k == "dapr-api-token" || k == "dapr-app-id" || k == "traceparent";
@@ -369,6 +396,7 @@ class DataPlane {
                       quote_all(*opt_str(s, "coll"));
         x.prefix = *opt_str(s, "prefix");
         x.auth = auth_headers(s);
+        x.shards = shard_list(s);
         stores_[st->keys[i]] = std::move(x);
       }
     if (auto* ps = cfg.get("pubsubs"); ps && ps->t == Value::Object)
@@ -378,6 +406,7 @@ class DataPlane {
         b.backing = Endpoint::parse(*opt_str(s, "backing"));
         b.ns = *opt_str(s, "ns");
         b.auth = auth_headers(s);
+        b.shards = shard_list(s);
         buses_[ps->keys[i]] = std::move(b);
       }
   }
@@ -839,7 +868,9 @@ class DataPlane {
     if (seg.size() == 4 && (lower(seg[0]) == "v1.0-alpha1" || lower(seg[0]) == "v1.0-beta1") &&
         lower(seg[1]) == "state" && lower(seg[3]) == "query" && (m.method == "POST" || m.method == "PUT")) {
       auto it = stores_.find(unquote(seg[2]));
-      if (it != stores_.end()) {  // state query: straight to the backing's query planner
+      // state query: straight to the backing's query planner (a partitioned store's
+      // cross-partition query fans out and merges in the control plane, sidecar/state.py)
+      if (it != stores_.end() && it->second.shards.empty()) {
         state_query(std::move(m), std::move(r), it->second, path);
         return;
       }
@@ -1209,12 +1240,47 @@ class DataPlane {
     }
     HeaderList h = s.auth;
     h.emplace_back("content-type", "application/json");
+    if (s.shards.empty()) {
+      save_on(s, 0, h, items, std::move(done));
+      return;
+    }
+    // partitioned: one request per shard the items hash to, answered when all have answered
+    // (a bulk save is not atomic in Dapr either; the worst status wins)
+    std::map<size_t, std::vector<Item>> by_shard;
+    for (auto& it : items) by_shard[s.shard_of(full_key(s, it.key))].push_back(std::move(it));
+    if (by_shard.size() == 1) {
+      save_on(s, by_shard.begin()->first, h, by_shard.begin()->second, std::move(done));
+      return;
+    }
+    struct Join {
+      size_t left;
+      ClientResult worst;
+      bool have = false;
+      ev::ClientCallback done;
+    };
+    auto j = std::make_shared<Join>();
+    j->left = by_shard.size();
+    j->done = std::move(done);
+    for (auto& kv : by_shard)
+      save_on(s, kv.first, h, kv.second, [j](ClientResult&& res) {
+        auto rank = [](const ClientResult& r) {
+          return r.err ? 3 : (r.resp.status == 409 || r.resp.status == 412) ? 2 : r.resp.status >= 300 ? 1 : 0;
+        };
+        if (!j->have || rank(res) > rank(j->worst)) {
+          j->worst = std::move(res);
+          j->have = true;
+        }
+        if (--j->left == 0) j->done(std::move(j->worst));
+      });
+  }
+
+  void save_on(const Store& s, size_t shard, HeaderList h, std::vector<Item>& items, ev::ClientCallback done) {
     if (items.size() == 1) {
       Item& it = items[0];
       if (!it.etag.empty()) h.emplace_back("if-match", it.etag);
       if (it.first_write) h.emplace_back("x-tt-first-write", "1");
       if (it.ttl_ms) h.emplace_back("x-tt-ttl-ms", std::to_string(it.ttl_ms));
-      store_request(s.backing, "PUT", s.coll_path + "/docs/" + quote_all(full_key(s, it.key)), h, it.value,
+      store_request(s.ep(shard), "PUT", s.coll_path + "/docs/" + quote_all(full_key(s, it.key)), std::move(h), it.value,
                     std::move(done));
       return;
     }
@@ -1227,7 +1293,7 @@ class DataPlane {
               ",\"firstWrite\":" + (it.first_write ? "true" : "false") + ",\"ttlMs\":" + std::to_string(it.ttl_ms) + "}";
     }
     body += "]";
-    store_request(s.backing, "POST", s.coll_path + "/bulkset", h, std::move(body), std::move(done));
+    store_request(s.ep(shard), "POST", s.coll_path + "/bulkset", std::move(h), std::move(body), std::move(done));
   }
 
   static std::string full_key(const Store& s, const std::string& key) {
@@ -1237,7 +1303,8 @@ class DataPlane {
 
   void state_get(Message&& m, Reply&& r, const Store& s, const std::string& key, const std::string& path) {
     auto d = begin(m, std::move(r), "state.get", path);
-    store_request(s.backing, "GET", s.coll_path + "/docs/" + quote_all(full_key(s, key)), s.auth, {},
+    const std::string fk = full_key(s, key);
+    store_request(s.ep(s.shard_of(fk)), "GET", s.coll_path + "/docs/" + quote_all(fk), s.auth, {},
                     [d](ClientResult&& res) {
                       if (res.err || (res.resp.status != 200 && res.resp.status != 404)) {
                         d->error(500, "ERR_STATE_GET", "state get: " + (res.err ? errno_text(res.err)
@@ -1280,7 +1347,8 @@ class DataPlane {
     auto d = begin(m, std::move(r), "state.delete", path);
     HeaderList h = s.auth;
     if (auto* im = m.header("if-match"); im && !im->empty()) h.emplace_back("if-match", *im);
-    store_request(s.backing, "DELETE", s.coll_path + "/docs/" + quote_all(full_key(s, key)), h, {},
+    const std::string fk = full_key(s, key);
+    store_request(s.ep(s.shard_of(fk)), "DELETE", s.coll_path + "/docs/" + quote_all(fk), h, {},
                     [d](ClientResult&& res) {
                       if (!res.err && (res.resp.status == 409 || res.resp.status == 412)) {
                         d->error(409, "ERR_STATE_DELETE", "state delete: HTTP " + std::to_string(res.resp.status) +
@@ -1324,13 +1392,14 @@ class DataPlane {
     if (!raw && as_string && !valid_utf8(m.body)) return false;  // Python decodes with replacement chars
     auto d = begin(m, std::move(r), "publish", path);
     d->attrs.emplace_back("topic", topic);
-    std::string body, out_ct;
+    std::string body, out_ct, event_id;
     if (raw) {
       body = std::move(m.body);
       out_ct = ctype;
     } else {
       std::string tp = d->span.traceparent();
-      body = "{\"specversion\":\"1.0\",\"id\":\"" + uuid4() + "\",\"source\":" + json_str(app_id_) +
+      event_id = uuid4();
+      body = "{\"specversion\":\"1.0\",\"id\":\"" + event_id + "\",\"source\":" + json_str(app_id_) +
              ",\"type\":\"com.dapr.event.sent\",\"datacontenttype\":" + json_str(base.empty() ? "application/json" : base) +
              ",\"topic\":" + json_str(topic) + ",\"pubsubname\":" + json_str(name) + ",\"time\":\"" + utc_now_iso() + "\"";
       if (is_json) {
@@ -1357,7 +1426,10 @@ class DataPlane {
       long long ttl = (long long)(std::atof(meta["ttlInSeconds"].c_str()) * 1000);
       if (ttl) h.emplace_back("x-tt-ttl-ms", std::to_string(ttl));
     }
-    client_.request(b.backing, "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
+    // partitioned broker: the message's partitionKey metadata (Service Bus partitioning), else
+    // its CloudEvent id, picks the shard
+    const std::string pkey = meta.count("partitionKey") ? meta["partitionKey"] : event_id.empty() ? uuid4() : event_id;
+    client_.request(b.ep(pkey), "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
                     body, 60, [d, name, topic](ClientResult&& res) {
                       if (res.err || res.resp.status >= 300) {
                         d->error(500, "ERR_PUBSUB_PUBLISH_MESSAGE",

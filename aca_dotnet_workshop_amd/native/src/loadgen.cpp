@@ -5,7 +5,8 @@
 // step ends only when the JSON counter at that URL (field `--until-field`) has advanced by
 // the batch size -- bench.py uses it to wait until the processor acknowledged every task.
 // `--until-base N --until-stride M`: start from counter value N and require an advance of M per
-// step (several generators sharing one subscription: M = ranks x batch).
+// step (several generators sharing one subscription: M = ranks x batch).  `--until-url` may be
+// repeated: the counter is then the sum over every URL (a partitioned broker, one per shard).
 // Request bodies come from a file with one body per line (cycled); `--header "name: value"`
 // (repeatable) adds request headers (the frontend entry sends its cookies).  Prints one JSON line:
 // {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
@@ -30,7 +31,8 @@ namespace {
 
 struct Opts {
   std::vector<ev::Endpoint> targets;
-  std::string path = "/", method = "POST", ctype = "application/json", until_url, until_field = "completed";
+  std::string path = "/", method = "POST", ctype = "application/json", until_field = "completed";
+  std::vector<std::string> until_urls;
   std::vector<std::string> bodies{""};
   ev::HeaderList headers;
   int concurrency = 64, batch = 512, steps = 1, expect = 0;
@@ -44,18 +46,16 @@ class Gen {
   Gen(ev::Loop& loop, Opts o) : loop_(loop), client_(loop), o_(std::move(o)) {
     hdrs_.emplace_back("content-type", o_.ctype);
     for (auto& h : o_.headers) hdrs_.push_back(h);
-    if (!o_.until_url.empty()) {
-      std::string u = o_.until_url;
+    for (std::string u : o_.until_urls) {
       if (u.rfind("http://", 0) == 0) u = u.substr(7);
       auto slash = u.find('/');
-      until_ep_ = ev::Endpoint::parse(u.substr(0, slash));
-      until_target_ = slash == std::string::npos ? "/" : u.substr(slash);
+      until_.emplace_back(ev::Endpoint::parse(u.substr(0, slash)), slash == std::string::npos ? "/" : u.substr(slash));
     }
   }
 
   void start() {
     t0_ = ev::now_s();
-    if (until_target_.empty()) begin_step();
+    if (until_.empty()) begin_step();
     else if (o_.until_base >= 0) {
       base_ = o_.until_base;
       begin_step();
@@ -91,8 +91,7 @@ class Gen {
   ev::Client client_;
   Opts o_;
   ev::HeaderList hdrs_;
-  ev::Endpoint until_ep_;
-  std::string until_target_;
+  std::vector<std::pair<ev::Endpoint, std::string>> until_;
   double t0_ = 0, t1_ = 0;
   int step_ = 0;
   long long issued_ = 0, done_ = 0, done_total_ = 0, errors_ = 0, base_ = 0;
@@ -141,7 +140,7 @@ class Gen {
     step_creates_ = ev::now_s() - step_t0_;
     base_ += o_.until_stride > 0 ? o_.until_stride : o_.batch;
     ++step_;
-    if (until_target_.empty()) {
+    if (until_.empty()) {
       begin_step();
       return;
     }
@@ -157,25 +156,37 @@ class Gen {
     });
   }
 
+  // the counter: the field summed over every --until-url, read concurrently
   void poll_counter(std::function<void(long long)> cb) {
-    client_.request(until_ep_, "GET", until_target_, {}, {}, 30, [this, cb](ev::ClientResult&& r) {
-      long long v = -1;
-      if (!r.err && r.resp.status == 200) {
-        try {
-          Value j = parse(r.resp.body);
-          if (auto* f = j.get(o_.until_field); f && f->t == Value::Number) v = (long long)f->n;
-        } catch (const std::exception&) {
+    struct Sum {
+      size_t left;
+      long long total = 0;
+      bool failed = false;
+    };
+    auto sum = std::make_shared<Sum>();
+    sum->left = until_.size();
+    for (auto& u : until_)
+      client_.request(u.first, "GET", u.second, {}, {}, 30, [this, cb, sum](ev::ClientResult&& r) {
+        long long v = -1;
+        if (!r.err && r.resp.status == 200) {
+          try {
+            Value j = parse(r.resp.body);
+            if (auto* f = j.get(o_.until_field); f && f->t == Value::Number) v = (long long)f->n;
+          } catch (const std::exception&) {
+          }
         }
-      }
-      if (v < 0) {
-        errors_++;
-        if (first_error_.empty()) first_error_ = "counter poll failed";
-        t1_ = ev::now_s();
-        loop_.stop();
-        return;
-      }
-      cb(v);
-    });
+        if (v < 0) sum->failed = true;
+        else sum->total += v;
+        if (--sum->left) return;
+        if (sum->failed) {
+          errors_++;
+          if (first_error_.empty()) first_error_ = "counter poll failed";
+          t1_ = ev::now_s();
+          loop_.stop();
+          return;
+        }
+        cb(sum->total);
+      });
   }
 };
 
@@ -212,7 +223,7 @@ int main(int argc, char** argv) {
     else if (a == "--batch") o.batch = std::max(1, std::atoi(next().c_str()));
     else if (a == "--steps") o.steps = std::max(0, std::atoi(next().c_str()));
     else if (a == "--expect") o.expect = std::atoi(next().c_str());
-    else if (a == "--until-url") o.until_url = next();
+    else if (a == "--until-url") o.until_urls.push_back(next());
     else if (a == "--until-field") o.until_field = next();
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());

@@ -73,6 +73,14 @@ class Dist:
         self.pg.broadcast_object_list(box, src=src)
         return box[0]
 
+    def allgather(self, obj) -> list:
+        """Every rank's ``obj``, in rank order (picklable objects over gloo)."""
+        if self.pg is None:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self) -> None:
         if self.pg is not None:
             self.pg.destroy_process_group()

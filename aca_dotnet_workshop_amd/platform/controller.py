@@ -26,11 +26,12 @@ import shutil
 import time
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Any
+from typing import Any, Callable
 
 import yaml
 
 from ..backing.client import BackingClient
+from ..backing.shards import PARTITIONED_FAMILIES, ShardedBackingClient
 from ..web.app import WebApp
 from ..web.http import Request, Response, empty, json_response
 from ..web.server import HttpServer
@@ -85,8 +86,14 @@ class AppRuntime:
 class EnvironmentController:
     def __init__(self, manifest: Manifest, env_dir: str | os.PathLike, polling_interval: float | None = None,
                  cooldown: float | None = None, log_level: str = "warning",
-                 registry_root: str | os.PathLike | None = None) -> None:
+                 registry_root: str | os.PathLike | None = None,
+                 shard_exchange: Callable[[str], list[str]] | None = None) -> None:
         self.m = manifest
+        # partitioned shared environment (backing/shards.py): called with this environment's
+        # backing URL once it is up, returns every shard's URL in rank order (bench.py
+        # --shared-env exchanges them over torch.distributed)
+        self.shard_exchange = shard_exchange
+        self.shards: list[str] = []
         self.dir = Path(env_dir).resolve()
         self.dir.mkdir(parents=True, exist_ok=True)
         (self.dir / "components").mkdir(exist_ok=True)
@@ -185,7 +192,16 @@ class EnvironmentController:
             policy["keys"][f"storage/{st['account']}"] = keys[st["account"]]
         url = await asyncio.to_thread(self.stack.start_backing, str(self.dir / "backing"), policy)
         self.backing = BackingClient(url, identity=ADMIN)
-        self.event("BackingServicesStarted", url=url, rbac=policy["mode"])
+        if self.shard_exchange is not None:
+            urls = [u.rstrip("/") for u in await asyncio.to_thread(self.shard_exchange, url)]
+            if len(urls) > 1:
+                # the document store and the broker are partitioned over every rank's backing;
+                # provisioning (topics, subscriptions, RU/s split) reaches all of them
+                self.shards = urls
+                for fam in PARTITIONED_FAMILIES:
+                    self.stack.base_env[f"TT_BACKING_SHARDS_{fam}"] = ",".join(urls)
+                self.backing = ShardedBackingClient(urls, identity=ADMIN, home=url)
+        self.event("BackingServicesStarted", url=url, rbac=policy["mode"], shards=self.shards)
 
     async def _provision(self) -> None:
         r = self.m.resources

@@ -9,6 +9,7 @@ from typing import Callable
 from urllib.parse import urlsplit
 
 from ..backing.client import BackingClient, backing_url
+from ..backing.shards import PARTITIONED_FAMILIES, ShardedBackingClient, shard_urls
 from ..web.client import HttpClient
 from .components import Component, ComponentError
 
@@ -27,9 +28,14 @@ class RuntimeContext:
         metadata, else a per-service-family URL (``TT_BACKING_URL_COSMOS`` /
         ``_SERVICEBUS`` / ``_STORAGE`` / ``_KEYVAULT`` / ``_SENDGRID``), else the shared
         ``TT_BACKING_URL`` -- Azure's services are separate endpoints, so they may be
-        separate emulator processes."""
-        base = comp.get("ttBackingUrl") or self.environ.get(f"TT_BACKING_URL_{service_family(comp.type)}") \
-            or self.backing_url
+        separate emulator processes.  ``TT_BACKING_SHARDS_COSMOS`` / ``_SERVICEBUS`` (URLs in
+        rank order) make the store / broker partitioned over several backings."""
+        family = service_family(comp.type)
+        base = comp.get("ttBackingUrl") or self.environ.get(f"TT_BACKING_URL_{family}") or self.backing_url
+        if not comp.get("ttBackingUrl") and family in PARTITIONED_FAMILIES:
+            urls = shard_urls(self.environ, family)
+            if urls:  # a partitioned collection / namespace (backing/shards.py)
+                return ShardedBackingClient(urls, identity=self.identity or "", key=key, http=self.http, home=base)
         return BackingClient(base, identity=self.identity or "", key=key, http=self.http)
 
 

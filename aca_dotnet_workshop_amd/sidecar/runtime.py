@@ -214,13 +214,14 @@ class Sidecar:
         for name, st in self.state_stores.items():
             if isinstance(st, BackingStateStore):
                 stores[name] = {"backing": st.client.base, "account": st.account, "db": st.db, "coll": st.coll,
-                                "prefix": st.prefix, "identity": st.client.identity or "", "key": st.client.key or ""}
+                                "prefix": st.prefix, "identity": st.client.identity or "", "key": st.client.key or "",
+                                "shards": list(getattr(st.client, "bases", []))}
         buses = {}
         for name, ps in self.pubsubs.items():
             t = getattr(ps, "transport", None)
             if isinstance(t, BackingTransport):
                 buses[name] = {"backing": t.client.base, "ns": t.ns, "identity": t.client.identity or "",
-                               "key": t.client.key or ""}
+                               "key": t.client.key or "", "shards": list(getattr(t.client, "bases", []))}
         listen = []
         if self.uds:
             listen.append("unix:" + self.uds)
@@ -467,10 +468,18 @@ class Sidecar:
                 "entity": entity, "ns": t.ns, "backing": t.client.base, "identity": t.client.identity or "",
                 "key": t.client.key or "", "deadLetterTopic": s.dead_letter_topic or "",
                 "raw": s.metadata.get("rawPayload", "").lower() == "true", **ps.consumer_settings()}
-        r = await self.http.request("POST", self._dp_control + "/subscribe", body=json.dumps(spec).encode(),
-                                    headers=[("Content-Type", "application/json")])
-        if r.status != 204:
-            raise RuntimeError(f"native data plane refused subscription: {r.status} {r.body[:200]!r}")
+        shards = list(getattr(t.client, "bases", []))
+        specs = [spec]
+        if shards:  # partitioned namespace: a receiver per shard, the replica's limits split over them
+            n = len(shards)
+            specs = [dict(spec, name=f"{spec['name']}#{i}", backing=url,
+                          maxConcurrent=max(1, -(-spec["maxConcurrent"] // n)), prefetch=max(1, -(-spec["prefetch"] // n)))
+                     for i, url in enumerate(shards)]
+        for sp in specs:
+            r = await self.http.request("POST", self._dp_control + "/subscribe", body=json.dumps(sp).encode(),
+                                        headers=[("Content-Type", "application/json")])
+            if r.status != 204:
+                raise RuntimeError(f"native data plane refused subscription: {r.status} {r.body[:200]!r}")
 
     async def _subscribe_with_retry(self, ps: PubSub, s: SubscriptionSpec, delay: float = 1.0) -> None:
         from .pubsub import BackingTransport

@@ -69,9 +69,11 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
                     help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")
     ap.add_argument("--shared-env", action="store_true",
-                    help="multi-rank: ONE environment -- rank 0's backing services (state store, broker) shared by "
-                         "every rank's API and processor replicas, which compete on one subscription (the "
-                         "reference's KEDA scale axis); default: one environment per rank (weak scaling)")
+                    help="multi-rank: ONE partitioned environment -- every rank hosts one shard of the state store "
+                         "and of the broker (backing/shards.py: documents and messages by partition-key hash, "
+                         "cross-partition queries merged), every rank's replicas reach all shards and the "
+                         "processors of all ranks compete on the one subscription (the reference's KEDA scale "
+                         "axis); default: one environment per rank (weak scaling)")
     ap.add_argument("--client", choices=("native", "python"), default="native",
                     help="load generator: native/bin/ttloadgen (C++) or the in-process asyncio client")
     ap.add_argument("--entry", choices=("frontend", "api-sidecar"), default="frontend",
@@ -225,14 +227,38 @@ class OverdueSweeper:
                 "first_error": self.errors[0] if self.errors else None}
 
 
-def _counts(url: str) -> dict:
+def _counts(url: str | list[str]) -> dict:
+    """The subscription's counters; several URLs (a partitioned broker): summed."""
     import urllib.request
-    with urllib.request.urlopen(url, timeout=30) as r:
-        return json.loads(r.read())
+    out: dict = {}
+    for u in [url] if isinstance(url, str) else url:
+        with urllib.request.urlopen(u, timeout=30) as r:
+            for k, v in json.loads(r.read()).items():
+                out[k] = out.get(k, 0) + v if isinstance(v, (int, float)) else v
+    return out
 
 
-def _counter(url: str) -> int:
+def _counter(url: str | list[str]) -> int:
     return int(_counts(url)["completed"])
+
+
+def _until(urls: str | list[str]) -> list[str]:
+    out = []
+    for u in [urls] if isinstance(urls, str) else urls:
+        out += ["--until-url", u]
+    return out + ["--until-field", "completed"]
+
+
+def _accel_stats(backings: list[str]) -> dict:
+    """The task collection's accelerator stats summed over its shards (one per backing)."""
+    out: dict = {}
+    for b in backings:
+        for k, v in (_collection_stats(b).get("accelerator") or {}).items():
+            if isinstance(v, (int, float)) and not isinstance(v, bool):
+                out[k] = round(out.get(k, 0) + v, 3)
+            else:
+                out.setdefault(k, v)
+    return out
 
 
 def _collection_stats(backing: str) -> dict:
@@ -246,7 +272,7 @@ def _collection_stats(backing: str) -> dict:
         return {"error": repr(e)}
 
 
-def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: int, conc: int,
+def run_loadgen(exe: str, socks: list[str], counts_url: str | list[str], steps: int, batch: int, conc: int,
                 bodies_file: str, shared: tuple[int, int] | None = None) -> tuple[float, dict]:
     """Closed-loop load from the native generator; returns (wall seconds, its report).
     ``shared = (base, stride)``: the subscription's completed counter is shared with other
@@ -254,7 +280,7 @@ def run_loadgen(exe: str, socks: list[str], counts_url: str, steps: int, batch: 
     import subprocess
     cmd = [exe, "--path", "/v1.0/invoke/tasksmanager-backend-api/method/api/tasks", "--bodies", bodies_file,
            "--concurrency", str(conc), "--batch", str(batch), "--steps", str(steps), "--expect", "201",
-           "--until-url", counts_url, "--until-field", "completed"]
+           *_until(counts_url)]
     if shared is not None:
         cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     for s in socks:
@@ -278,8 +304,6 @@ def main() -> None:
     pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local)
     cores = min(cpu_budget(), share) if pinned else share
     if a.entry == "frontend":
-        if a.shared_env and d.world > 1:
-            raise SystemExit("--shared-env is an --entry api-sidecar mode")
         return main_frontend(a, d, cores, pinned)
     return main_localstack(a, d, cores, pinned)
 
@@ -313,16 +337,14 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
     stack = LocalStack(root=root, env=env)
     sweeper = None
     try:
-        if not shared or d.rank == 0:
-            backing = doc_backing = stack.start_backing()
-            if a.split_backing:
-                backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
-        if shared:  # every rank joins rank 0's backing services and name registry
-            info = d.broadcast(stack.shared_info() if d.rank == 0 else None)
-            if d.rank:
-                stack.attach(info)
-            doc_backing = info["backing"]
-            backing = info["families"].get("SERVICEBUS", doc_backing)
+        backing = doc_backing = stack.start_backing()
+        if a.split_backing:
+            backing = stack.start_backing_family(["SERVICEBUS", "STORAGE"])
+        shards, bus_shards = [doc_backing], [backing]
+        if shared:  # one shard of the store and of the broker per rank (backing/shards.py)
+            shards, bus_shards = d.allgather(doc_backing), d.allgather(backing)
+            stack.base_env["TT_BACKING_SHARDS_COSMOS"] = ",".join(shards)
+            stack.base_env["TT_BACKING_SHARDS_SERVICEBUS"] = ",".join(bus_shards)
         for _ in range(a.api_replicas):
             stack.start_replica("tasksmanager-backend-api", api_cfg, grpc=a.api_protocol == "grpc",
                                 extra_env={"TT_APP_HOST": app_host("api", a.app_host)})
@@ -333,7 +355,8 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
         socks = [r.sidecar_uds for r in stack.replicas["tasksmanager-backend-api"]]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
         counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
-        if a.client == "native":
+        if shared:
+            counts_url = [f"{u}/servicebus/taskstracker/counts?entity={entity}" for u in bus_shards]
             from aca_dotnet_workshop_amd.native.build import build_loadgen
             exe = str(build_loadgen())
             bodies_file = str(stack.root / "bodies.jsonl")
@@ -399,10 +422,11 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
             p99 = d.max(lat[min(len(lat) - 1, int(len(lat) * 0.99))] * 1e3) if lat else 0.0
         sweep_info = None
         if sweeper is not None:
-            acc = _collection_stats(doc_backing).get("accelerator", {})
+            acc = _accel_stats(shards if shared else [doc_backing])
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
-                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows")}
+                          "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
+                          "shards": len(shards)}
             if d.rank == 0:
                 print(json.dumps({"overdue_sweeps": sweep_info}), file=sys.stderr, flush=True)
         delivery = None
@@ -422,8 +446,9 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
                 "data": "synthetic createTask payloads",
                 "config": {"model": "tasks-tracker createTask flow (API+sidecars+backing+processor)",
                            "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
-                           "parallelism": (f"shared-env x{d.world} (one backing + subscription, "
-                                           f"{a.processor_replicas * d.world} competing processor replicas)"
+                           "parallelism": (f"shared-env x{d.world} (store and broker partitioned over {len(shards)} "
+                                           f"shards, one per rank; {a.processor_replicas * d.world} competing "
+                                           f"processor replicas)"
                                            if shared else f"env-per-rank x{d.world if d.world > 1 else 1}"),
                            "delivery": delivery,
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
@@ -496,13 +521,14 @@ def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
             for i in range(batch)]
 
 
-def run_form_loadgen(exe: str, ports: list[int], cookie: str, counts_url: str, steps: int, batch: int, conc: int,
-                     bodies_file: str) -> tuple[float, dict]:
+def run_form_loadgen(exe: str, ports: list[int], cookie: str, counts_url: str | list[str], steps: int, batch: int,
+                     conc: int, bodies_file: str, shared: tuple[int, int] | None = None) -> tuple[float, dict]:
     import subprocess
     cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies_file, "--content-type",
            "application/x-www-form-urlencoded", "--header", f"Cookie: {cookie}", "--concurrency", str(conc),
-           "--batch", str(batch), "--steps", str(steps), "--expect", "302", "--until-url", counts_url,
-           "--until-field", "completed"]
+           "--batch", str(batch), "--steps", str(steps), "--expect", "302", *_until(counts_url)]
+    if shared is not None:
+        cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     for p in ports:
         cmd += ["--target", f"127.0.0.1:{p}"]
     t0 = time.perf_counter()
@@ -562,22 +588,32 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                  "environmentName": f"cae-bench-r{d.rank}"}
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
                       overrides)
-    env = BackgroundEnvironment(m, os.path.join(root, "env"), log_level="warning")
+    shared = a.shared_env and d.world > 1
+    # --shared-env: every rank's controller hosts one shard of the state store and the broker;
+    # the shard URLs are exchanged once the backings are up (platform/controller.py)
+    env = BackgroundEnvironment(m, os.path.join(root, "env"), log_level="warning",
+                                shard_exchange=d.allgather if shared else None)
     sweeper = None
     try:
         env.start()
         lim = env.ctl.limiter.describe()
         fe_ports = [r.app_port for r in env.replicas(FRONTEND)]
         backing = env.backing_url
+        shards = env.ctl.shards or [backing]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
-        counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
+        counts_url = [f"{u}/servicebus/taskstracker/counts?entity={entity}" for u in shards]
         cookie, token = _form_session(fe_ports[0], "bench@bench.local")
         bodies_file = os.path.join(root, "form-bodies.txt")
         with open(bodies_file, "wb") as f:
             f.write(b"\n".join(_form_bodies(a.batch, token, a.past_due_every if sweep else 0)) + b"\n")
+        gbase, stride = None, a.batch * d.world
+        if shared:  # the subscription's completed counter before anyone sends (global step targets)
+            d.barrier()
+            gbase = d.broadcast(_counter(counts_url) if d.rank == 0 else None)
         if a.warmup:
-            run_form_loadgen(exe, fe_ports, cookie, counts_url, a.warmup, a.batch, conc, bodies_file)
-        if sweep:  # one cron trigger per environment
+            run_form_loadgen(exe, fe_ports, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
+                             (gbase, stride) if shared else None)
+        if sweep and (not shared or d.rank == 0):  # one cron trigger per environment
             sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
         d.barrier()
         device_sync()
@@ -588,7 +624,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         ru0 = _collection_stats(backing).get("throughput", {})
         if sweeper is not None:
             sweeper.start()
-        dt, report = run_form_loadgen(exe, fe_ports, cookie, counts_url, a.steps, a.batch, conc, bodies_file)
+        dt, report = run_form_loadgen(exe, fe_ports, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
+                                      (gbase + stride * a.warmup, stride) if shared else None)
         device_sync()
         d.barrier()
         if sweeper is not None:
@@ -601,15 +638,24 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
         sweep_info = None
         if sweeper is not None:
-            acc = _collection_stats(backing).get("accelerator", {})
+            acc = _accel_stats(shards)
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
+                          "shards": len(shards),
                           "store_ms_total": {k2: acc.get(k2) for k2 in ("lock_wait_ms", "sync_ms",
                                                                          "select_and_results_ms")}}
-        # the same environment, load straight at the API sidecars' invoke (round 2's topology)
+        delivery = None
+        if shared:  # exactly-once across the competing consumers of every rank, over every shard
+            c = _counts(counts_url)
+            sent = gbase + stride * (a.warmup + a.steps)
+            delivery = {"enqueued": c.get("enqueued"), "completed": c.get("completed"), "received": c.get("received"),
+                        "dead_lettered": c.get("dead_letter"), "expected": sent,
+                        "exactly_once": c.get("completed") == c.get("received") == c.get("enqueued") == sent}
+        # the same environment, load straight at the API sidecars' invoke (round 2's topology);
+        # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
-        dsteps = a.direct_steps if a.direct_steps >= 0 else max(1, a.steps // 4)
+        dsteps = 0 if shared else a.direct_steps if a.direct_steps >= 0 else max(1, a.steps // 4)
         if dsteps:
             socks = [r.sidecar_uds for r in env.replicas(API)]
             jb = os.path.join(root, "json-bodies.jsonl")
@@ -638,7 +684,10 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                 "config": {"model": "tasks-tracker createTask flow, SURVEY §3.1 (frontend -> mTLS -> API -> store + "
                                     "publish -> processor ack)",
                            "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
-                           "parallelism": f"env-per-rank x{d.world if d.world > 1 else 1}",
+                           "parallelism": (f"shared-env x{d.world} (store and broker partitioned over {len(shards)} "
+                                           f"shards, one per rank; {proc * d.world} competing processor replicas)"
+                                           if shared else f"env-per-rank x{d.world if d.world > 1 else 1}"),
+                           "delivery": delivery,
                            "environment": "deploy/main.yaml via the platform controller",
                            "entry": "frontend", "entry_request": "POST /Tasks/Create (form, antiforgery + identity "
                                                                   "cookies) -> 302, redirect not followed",

@@ -62,9 +62,10 @@ def test_bench_two_ranks_torchrun():
 
 
 def test_bench_shared_env_two_ranks():
-    """--shared-env: both ranks' API and processor replicas run against rank 0's backing services;
-    the processors of both ranks compete on ONE subscription (the reference's scale axis,
-    processor-backend-service.bicep:159-183) and every task is delivered and completed once."""
+    """--shared-env: the state store and the broker are partitioned over both ranks' backings
+    (backing/shards.py); the processors of both ranks compete on the ONE subscription (the
+    reference's scale axis, processor-backend-service.bicep:159-183), receiving from every shard,
+    and every task is delivered and completed once."""
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
@@ -76,7 +77,8 @@ def test_bench_shared_env_two_ranks():
     assert len(lines) == 1, r.stdout
     _check(lines[0], 2, 2, 1)
     cfg = lines[0]["config"]
-    assert cfg["parallelism"].startswith("shared-env x2") and "2 competing processor replicas" in cfg["parallelism"]
+    assert cfg["parallelism"].startswith("shared-env x2 (store and broker partitioned over 2 shards")
+    assert "2 competing processor replicas" in cfg["parallelism"]
     dlv = cfg["delivery"]
     assert dlv["exactly_once"] and dlv["completed"] == dlv["received"] == dlv["expected"] >= 2 * 32 * 3, dlv
     assert dlv["dead_lettered"] == 0

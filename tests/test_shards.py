@@ -1,0 +1,248 @@
+"""The partitioned shared environment (backing/shards.py; VERDICT r2 "partitioned shared env"):
+documents and messages spread over several backing processes by partition-key hash, the
+cross-partition query merged page by page with a composite continuation token, transactions
+held to one partition, the broker's receivers draining every shard exactly once, and the
+native data plane routing with the same hash as the Python client."""
+import asyncio
+import json
+import os
+import socket
+import subprocess
+import sys
+import urllib.request
+from pathlib import Path
+
+import pytest
+
+from aca_dotnet_workshop_amd.backing.client import BackingClient, BackingError
+from aca_dotnet_workshop_amd.backing.shards import (ShardedBackingClient, decode_token, encode_token, fnv1a64,
+                                                    merge_pages, shard_of)
+from aca_dotnet_workshop_amd.platform.processes import LocalStack
+
+from helpers import run
+
+ROOT = Path(__file__).resolve().parents[1]
+ACCT, DB, COLL = "taskstracker-state-store", "tasksmanagerdb", "taskscollection"
+PREFIX = "tasksmanager-backend-api||"
+
+
+def test_fnv1a64_reference_vectors():
+    assert fnv1a64(b"") == 0xcbf29ce484222325
+    assert fnv1a64(b"a") == 0xaf63dc4c8601ec8c
+    assert fnv1a64("foobar") == 0x85944171f73967e8
+    assert shard_of("anything", 1) == 0 and {shard_of(f"k{i}", 4) for i in range(64)} == {0, 1, 2, 3}
+
+
+def test_token_roundtrip_and_rejection():
+    assert encode_token([None, None]) is None
+    t = encode_token([3, None, 0])
+    assert decode_token(t, 3) == [3, None, 0] and decode_token(None, 3) == [0, 0, 0]
+    for bad in ("42", t + "x", encode_token([1, 2])):
+        with pytest.raises(BackingError) as e:
+            decode_token(bad, 3)
+        assert e.value.status == 400
+
+
+def test_merge_pages_offsets():
+    """A shard whose page was only partly used resumes at its offset; a shard that returned its
+    last matches and had them all taken is exhausted."""
+    q = {"sort": [{"key": "v", "order": "ASC"}], "page": {"limit": 3}}
+    pages = [(0, {"results": [{"key": "a", "data": {"v": 1}}, {"key": "b", "data": {"v": 5}}], "token": "2"}),
+             (1, {"results": [{"key": "c", "data": {"v": 2}}, {"key": "d", "data": {"v": 3}}]}),
+             (2, None)]
+    out = merge_pages(q, pages, [0, 0, None])
+    assert [r["key"] for r in out["results"]] == ["a", "c", "d"]
+    assert decode_token(out["token"], 3) == [1, None, None]
+    # a missing sort path sorts like null (first), DESC reverses, ties go in shard order
+    q2 = {"sort": [{"key": "v", "order": "DESC"}]}
+    pages2 = [(0, {"results": [{"key": "x", "data": {"v": 1}}, {"key": "m", "data": {}}]}),
+              (1, {"results": [{"key": "y", "data": {"v": 1}}]})]
+    assert [r["key"] for r in merge_pages(q2, pages2, [0, 0])["results"]] == ["x", "y", "m"]
+
+
+def _task(i: int) -> dict:
+    return {"taskId": f"00000000-0000-4000-8000-{i:012d}", "taskName": f"Task {i % 17}",
+            "taskCreatedBy": f"user{i % 5}@x", "taskCreatedOn": f"2026-10-{1 + i % 28:02d}T10:{i % 60:02d}:{i // 60:02d}",
+            "taskDueDate": f"2026-10-{1 + (i * 7) % 28:02d}T00:00:00", "taskAssignedTo": "a@x",
+            "isCompleted": i % 9 == 0, "isOverDue": i % 11 == 0}
+
+
+async def _pages(client, q: dict) -> list[str]:
+    keys, token = [], None
+    for _ in range(1000):
+        qq = json.loads(json.dumps(q))
+        if token:
+            qq.setdefault("page", {})["token"] = token
+        res = json.loads(await client.doc_query(ACCT, DB, COLL, json.dumps(qq).encode(), PREFIX))
+        keys += [r["key"] for r in res["results"]]
+        token = res.get("token")
+        if not token:
+            return keys
+    raise AssertionError("paging did not end")
+
+
+@pytest.fixture(scope="module")
+def backings(tmp_path_factory):
+    """Three shard backings (columnar accelerator on, CPU executor) and one single store."""
+    base = tmp_path_factory.mktemp("shards")
+    stacks = []
+    try:
+        for i in range(4):
+            env = {"TT_QUERY_ACCEL": "cpu", "TT_QUERY_ACCEL_MIN_DOCS": "0",
+                   "TT_QUERY_MIRROR_PATHS": "taskDueDate,isCompleted,isOverDue,taskCreatedOn"} if i < 3 else {}
+            s = LocalStack(root=base / f"s{i}", env=env)
+            s.start_backing()
+            stacks.append(s)
+        yield [s.backing_url for s in stacks]
+    finally:
+        for s in stacks:
+            s.stop()
+
+
+def test_partitioned_store_matches_one_store(backings):
+    async def main():
+        sh = ShardedBackingClient(backings[:3], identity="platform-admin")
+        one = BackingClient(backings[3], identity="platform-admin")
+        try:
+            docs = {f"{PREFIX}{_task(i)['taskId']}": _task(i) for i in range(600)}
+            items = [{"key": k, "value": json.dumps(v)} for k, v in docs.items()]
+            for lo in range(0, len(items), 100):
+                await sh.doc_bulk_set(ACCT, DB, COLL, items[lo:lo + 100])
+                await one.doc_bulk_set(ACCT, DB, COLL, items[lo:lo + 100])
+            # every document on the shard its key hashes to, and only there
+            for k in list(docs)[:60]:
+                home = shard_of(k, 3)
+                for i, c in enumerate(sh.shards):
+                    assert (await c.doc_get(ACCT, DB, COLL, k) is not None) == (i == home)
+            per = [(await c.doc_stats(ACCT, DB, COLL))["docs"] for c in sh.shards]
+            assert sum(per) == 600 and min(per) > 120, per
+            got = await sh.doc_bulk_get(ACCT, DB, COLL, list(docs)[:50] + ["missing"])
+            assert [g["key"] for g in got] == list(docs)[:50] + ["missing"] and "data" not in got[-1]
+            # the overdue sweep's query (range + ORDER BY taskCreatedOn + page), page by page
+            sweep = {"filter": {"AND": [{"LT": {"taskDueDate": "2026-10-15T00:00:00"}}, {"EQ": {"isCompleted": False}},
+                                        {"EQ": {"isOverDue": False}}]},
+                     "sort": [{"key": "taskCreatedOn", "order": "ASC"}], "page": {"limit": 37}}
+            a, b = await _pages(sh, sweep), await _pages(one, sweep)
+            assert a == b and len(a) > 100
+            desc = dict(sweep, sort=[{"key": "taskCreatedOn", "order": "DESC"}], page={"limit": 64})
+            assert await _pages(sh, desc) == await _pages(one, desc)
+            eq = {"filter": {"EQ": {"taskCreatedBy": "user3@x"}}, "page": {"limit": 25}}
+            assert sorted(await _pages(sh, eq)) == sorted(await _pages(one, eq))
+            assert sorted(await _pages(sh, {"filter": {"EQ": {"taskName": "Task 4"}}})) == \
+                sorted(await _pages(one, {"filter": {"EQ": {"taskName": "Task 4"}}}))
+            # transactions stay within one partition
+            k0 = next(k for k in docs if shard_of(k, 3) == 0)
+            k1 = next(k for k in docs if shard_of(k, 3) == 1)
+            with pytest.raises(BackingError) as e:
+                await sh.doc_transaction(ACCT, DB, COLL, [{"op": "delete", "key": k0}, {"op": "delete", "key": k1}])
+            assert e.value.status == 400
+            await sh.doc_transaction(ACCT, DB, COLL, [{"op": "upsert", "key": k0, "value": json.dumps({"x": 1})}])
+            assert json.loads((await sh.doc_get(ACCT, DB, COLL, k0))[0]) == {"x": 1}
+            # provisioned throughput is split over the partitions
+            r = await sh.doc_set_throughput(ACCT, DB, COLL, 3000)
+            assert r["perShard"] == 1000.0
+            await sh.doc_set_throughput(ACCT, DB, COLL, 0)
+        finally:
+            await sh.close()
+            await one.close()
+    run(main())
+
+
+def test_partitioned_broker_exactly_once(backings):
+    async def main():
+        sh = ShardedBackingClient(backings[:3], identity="platform-admin")
+        try:
+            await sh.sb_create_topic("ns1", "t")
+            await sh.sb_create_subscription("ns1", "t", "g", 30000, 5)
+            for i in range(90):
+                await sh.sb_publish("ns1", "t", json.dumps({"i": i}).encode(), message_id=f"m{i}")
+            await sh.sb_publish_batch("ns1", "t", [{"body": json.dumps({"i": 90 + i}), "contentType": "application/json",
+                                                   "entryId": f"e{i}"} for i in range(30)])
+            per = [(await c.sb_counts("ns1", "t/subscriptions/g"))["enqueued"] for c in sh.shards]
+            assert sum(per) == 120 and min(per) > 15, per
+            seen: list[int] = []
+            for _ in range(200):
+                msgs = await sh.sb_receive("ns1", "t/subscriptions/g", 16, 30000, 50)
+                if not msgs and len(seen) >= 120:
+                    break
+                seen += [json.loads(m["body"])["i"] if "body" in m else None for m in msgs]
+                res = await sh.sb_settle("ns1", "t/subscriptions/g", complete=[m["lockToken"] for m in msgs])
+                assert all(res["complete"])
+            assert sorted(seen) == list(range(120))
+            c = await sh.sb_counts("ns1", "t/subscriptions/g")
+            assert c["completed"] == c["received"] == 120, c
+        finally:
+            await sh.close()
+    run(main())
+
+
+def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
+    """An API replica whose sidecar runs the native data plane over two shards: the documents it
+    saves land where the Python client's hash says, its publishes spread over both brokers, and
+    the cross-partition query of GET /api/tasks?createdBy= (forwarded to the control plane,
+    which fans out) returns every task."""
+    urls = backings[:2]
+    stack = LocalStack(root=tmp_path / "app")
+    try:
+        stack.start_backing()  # the replica's home backing (Key Vault, Storage, ...)
+        for fam in ("COSMOS", "SERVICEBUS"):
+            stack.base_env[f"TT_BACKING_SHARDS_{fam}"] = ",".join(urls)
+        api = stack.start_replica("tasksmanager-backend-api", {"Logging:LogLevel:Default": "Warning"})
+        stack.wait_ready()
+
+        async def main():
+            from aca_dotnet_workshop_amd.web.client import HttpClient
+            http = HttpClient()
+            sh = ShardedBackingClient(urls, identity="platform-admin")
+            try:
+                await sh.sb_create_topic("taskstracker", "tasksavedtopic")  # the processor's subscription
+                await sh.sb_create_subscription("taskstracker", "tasksavedtopic", "tasksmanager-backend-processor")
+                base = f"unix:{api.sidecar_uds}:/v1.0/invoke/tasksmanager-backend-api/method/api/tasks"
+                ids = []
+                for i in range(40):
+                    body = json.dumps({"taskName": f"n{i}", "taskCreatedBy": "route@x", "taskAssignedTo": "a@x",
+                                       "taskDueDate": "2030-01-01T00:00:00"}).encode()
+                    r = await http.request("POST", base, body=body, headers=[("Content-Type", "application/json")])
+                    assert r.status == 201, r.body
+                    ids.append(r.headers["location"].rsplit("/", 1)[1])
+                for tid in ids:
+                    k = f"{PREFIX}{tid}"
+                    assert await sh.shards[shard_of(k, 2)].doc_get(ACCT, DB, COLL, k) is not None
+                    assert await sh.shards[1 - shard_of(k, 2)].doc_get(ACCT, DB, COLL, k) is None
+                r = await http.request("GET", base + "?createdBy=route@x")
+                assert r.status == 200 and sorted(t["taskId"] for t in json.loads(r.body)) == sorted(ids)
+                per = [(await c.sb_counts("taskstracker", "tasksavedtopic/subscriptions/tasksmanager-backend-processor"))
+                       ["enqueued"] for c in sh.shards]
+                assert sum(per) >= 40 and min(per) > 0, per
+            finally:
+                await sh.close()
+                await http.close()
+        run(main())
+    finally:
+        stack.stop()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shared_env_four_ranks_exactly_once():
+    """Four ranks, one partitioned environment: every rank hosts one shard of the store and of
+    the broker; the four processors compete on the one subscription over all four shards and
+    every task is delivered and completed exactly once (bench.py --shared-env, gloo)."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4",
+           "--steps", "2", "--warmup", "1", "--batch", "24", "--api-replicas", "1", "--processor-replicas", "1",
+           "--shared-env", "--overdue-sweep-ms", "0", "--entry", "api-sidecar", "--split-backing", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"metric"' in x]
+    assert len(line) == 1
+    cfg = line[0]["config"]
+    assert cfg["parallelism"].startswith("shared-env x4 (store and broker partitioned over 4 shards")
+    dlv = cfg["delivery"]
+    assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] == 4 * 24 * 3, dlv
+    assert dlv["dead_lettered"] == 0
