@@ -552,6 +552,11 @@ def _cpu_by_role(stack) -> dict[str, float]:
     return out
 
 
+# relative CPU per created task of one replica of each app (app process + its sidecar), from the
+# per-process attribution of the frontend-entry bench at ~40k tasks/s (profiles/r3_mtls_cost.md)
+CPU_WEIGHT = {"frontend": 1.0, "api": 1.32, "processor": 0.6}
+
+
 def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     import shutil
     import tempfile
@@ -567,8 +572,17 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     api = a.api_replicas or api
     proc = a.processor_replicas or proc
     conc = a.concurrency or min(512, 48 * fe)
-    nrep = fe + api + proc
-    app_cpu = a.app_cpu or round(max(0.25, (cores - 2.0) / nrep), 2)  # 2 CPUs: backing + load generator
+    # per-replica vCPU caps: the rank's CPUs less 2 (backing + load generator), split over the
+    # replicas in proportion to each app's measured CPU per created task (app + its sidecar; the
+    # API does the most work per task, the processor the least: profiles/r3_mtls_cost.md); each
+    # reference app module sets its own resources, so the manifest takes one cap per app
+    if a.app_cpu:
+        caps = {"frontend": a.app_cpu, "api": a.app_cpu, "processor": a.app_cpu}
+    else:
+        w = CPU_WEIGHT
+        unit = (cores - 2.0) / (fe * w["frontend"] + api * w["api"] + proc * w["processor"])
+        caps = {k: round(max(0.25, unit * w[k]), 2) for k in w}
+    app_cpu = caps["frontend"]
     for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
         b()
     exe = str(build_loadgen())
@@ -582,7 +596,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     overrides = {"backendApiMinReplicas": api, "backendApiMaxReplicas": api, "frontendMinReplicas": fe,
                  "frontendMaxReplicas": fe, "processorMinReplicas": proc, "processorMaxReplicas": proc,
                  "notifierMode": "log", "cosmosAutoscaleMaxThroughput": a.ru_per_s, "daprMtls": bool(a.mtls),
-                 "enforceCpuLimits": bool(a.cpu_limits), "appCpu": app_cpu, "appMemory": "2Gi",
+                 "enforceCpuLimits": bool(a.cpu_limits), "appCpu": app_cpu, "frontendCpu": caps["frontend"],
+                 "backendApiCpu": caps["api"], "processorCpu": caps["processor"], "appMemory": "2Gi",
                  "appInsightsSamplingPercentage": a.trace_sampling,
                  "overdueQuery": "range" if sweep else "equality", "overduePageSize": 1000 if sweep else 0,
                  "environmentName": f"cae-bench-r{d.rank}"}
@@ -693,7 +708,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                                                   "cookies) -> 302, redirect not followed",
                            "ingress": "bypassed: the load generator balances over the frontend replicas",
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
-                           "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": app_cpu,
+                           "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
                                           "mechanism": lim.get("cpu"), "mode": lim.get("mode")},
                            "replicas": {"frontend": fe, "api": api, "processor": proc},
                            "notifier": "TasksNotifier:Mode=log (the shipped controller)",

@@ -275,7 +275,7 @@ def test_environment_lifecycle(tmp_path, source, request):
             # resource limits (0.25 vCPU / 0.5Gi per replica): a replica over its memory limit is
             # killed and restarted like an OOM-killed container
             lim = ctl.status()["resourceLimits"]
-            assert lim["mode"] in ("cgroup2", "watchdog") and len(lim["replicas"]) >= 3
+            assert lim["mode"] in ("cgroup2", "cgroup1-cpu", "watchdog") and len(lim["replicas"]) >= 3
             assert all(r["memoryBytes"] == 512 << 20 and r["cpu"] == 0.25 for r in lim["replicas"].values())
             oom = api_rt.current.replicas[0]
             ctl.limiter.replicas[oom.name].limits.memory = 1 << 20  # as if it had grown past 0.5Gi
