@@ -1,4 +1,6 @@
 // Python bindings for the native state-store and broker engines (`_ttnative`).
+#include <unistd.h>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
@@ -213,6 +215,26 @@ PYBIND11_MODULE(_ttnative, m) {
 
   // (start-line a, b, c, headers dict) with lower-cased names; repeated headers joined by
   // ", " except set-cookie, which becomes a list.  Raises ValueError on malformed input.
+  // CPU time (ns) of each thread whose /proc/<pid>/task/<tid>/schedstat is open on the given
+  // descriptor (-1: unreadable, e.g. the thread exited): the watchdog CPU throttle of
+  // platform/limits.py reads every replica thread each tick in one call, at nanosecond
+  // resolution (utime/stime in /proc/<pid>/stat count 10 ms clock ticks).
+  m.def("schedstat_ns", [](const std::vector<int>& fds) {
+    std::vector<long long> out(fds.size(), -1);
+    {
+      py::gil_scoped_release r;
+      char buf[128];
+      for (size_t i = 0; i < fds.size(); ++i) {
+        ssize_t n = ::pread(fds[i], buf, sizeof buf - 1, 0);
+        if (n <= 0) continue;
+        buf[n] = 0;
+        char* end = nullptr;
+        long long v = std::strtoll(buf, &end, 10);
+        if (end != buf) out[i] = v;
+      }
+    }
+    return out;
+  });
   m.def("parse_http_head", [](py::bytes raw) {
     std::string_view sv = raw;
     HttpHead h;

@@ -516,9 +516,10 @@ class EnvironmentController:
 
     async def _throttle_loop(self) -> None:
         """CPU duty cycle of every replica (watchdog mode, ``resourceLimits.cpu: true``)."""
-        while True:
+        from .limits import PERIOD_S
+        while True:  # a few ticks per period: a replica overruns its quota by at most a tick
             await asyncio.to_thread(self.limiter.throttle_tick)
-            await asyncio.sleep(0.01)
+            await asyncio.sleep(PERIOD_S / 4)
 
     async def metric(self, rt: AppRuntime, rule: ScaleRule) -> float:
         md = rule.metadata

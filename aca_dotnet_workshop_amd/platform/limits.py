@@ -17,8 +17,12 @@ enforcement mechanisms, chosen at start-up and reported in the environment statu
   enforced by the controller, which sums the RSS of the replica's processes every
   supervision tick and kills + restarts a replica above its limit (``ReplicaOOMKilled``),
   like ACA restarting an OOM-killed container; CPU is enforced, when enabled, by a duty-cycle
-  throttle (``CpuThrottle``: SIGSTOP the group once it has used its quota of the current
-  100 ms period, SIGCONT at the next period) -- otherwise only accounted.
+  throttle: SIGSTOP the group once it has used its quota of the current period, SIGCONT at the
+  next -- otherwise only accounted.  The period is 20 ms (``TT_CPU_PERIOD_MS``), five times
+  finer than CFS's 100 ms, so a throttled replica stalls for at most a few ms instead of tens;
+  its CPU time is read per thread from ``/proc/<pid>/task/<tid>/schedstat`` (nanoseconds,
+  one native call per tick for every replica) because ``/proc/<pid>/stat`` counts 10 ms clock
+  ticks -- as coarse as the period itself.
 
 ``environment.resourceLimits`` in the manifest: ``{memory: true|false, cpu: true|false}``
 (both enforced in ``deploy/main.yaml``; the controller's own default without the key is memory
@@ -35,7 +39,8 @@ from pathlib import Path
 import psutil
 
 CGROUP_ROOT = Path("/sys/fs/cgroup")
-PERIOD_S = 0.1
+PERIOD_S = max(0.005, float(os.environ.get("TT_CPU_PERIOD_MS", "20")) / 1000.0)
+TREE_REFRESH_S = 0.5  # how often a replica's process / thread list is re-read
 
 
 def parse_memory(v: str | int | float) -> int:
@@ -135,6 +140,83 @@ class ReplicaState:
     throttled_periods: int = 0
     peak_rss: int = 0
     cpu_cgroup: Path | None = None   # cgroup v1 cpu directory (mode cgroup1-cpu)
+    clock: "ThreadClock | None" = None
+
+
+class ThreadClock:
+    """CPU seconds a replica has used, at nanosecond resolution: the per-thread CPU time of
+    every thread of the replica's processes (``/proc/<pid>/task/<tid>/schedstat``, read in one
+    native call), summed as deltas so a thread that exits keeps what it used.  Threads found
+    after the first read count from zero (they started inside the window)."""
+
+    def __init__(self, pid: int, reader) -> None:
+        self.pid = pid
+        self.reader = reader
+        self.fds: dict[tuple[int, int], int] = {}
+        self.last: dict[tuple[int, int], int] = {}
+        self.total_ns = 0
+        self.refreshed = 0.0
+        self._first = True
+
+    def refresh(self, now: float) -> None:
+        seen = set()
+        for p in tree(self.pid):
+            try:
+                tids = os.listdir(f"/proc/{p.pid}/task")
+            except OSError:
+                continue
+            for t in tids:
+                key = (p.pid, int(t))
+                seen.add(key)
+                if key in self.fds:
+                    continue
+                try:
+                    self.fds[key] = os.open(f"/proc/{p.pid}/task/{t}/schedstat", os.O_RDONLY)
+                except OSError:
+                    continue
+                if not self._first:
+                    self.last[key] = 0
+        for key in [k for k in self.fds if k not in seen]:
+            self._drop(key)
+        self._first = False
+        self.refreshed = now
+
+    def _drop(self, key) -> None:
+        try:
+            os.close(self.fds.pop(key))
+        except OSError:
+            pass
+        self.last.pop(key, None)
+
+    def seconds(self, now: float) -> float:
+        if now - self.refreshed >= TREE_REFRESH_S:
+            self.refresh(now)
+        keys = list(self.fds)
+        vals = self.reader([self.fds[k] for k in keys])
+        for k, v in zip(keys, vals):
+            if v < 0:
+                self._drop(k)
+                continue
+            prev = self.last.get(k)
+            if prev is not None and v > prev:
+                self.total_ns += v - prev
+            self.last[k] = v
+        return self.total_ns / 1e9
+
+    def close(self) -> None:
+        for key in list(self.fds):
+            self._drop(key)
+
+
+def _schedstat_reader():
+    """The native per-thread CPU reader, if this kernel exposes schedstat (else None)."""
+    try:
+        if not os.path.exists(f"/proc/self/task/{os.getpid()}/schedstat"):
+            return None
+        from .. import native
+        return native.load().schedstat_ns
+    except Exception:
+        return None
 
 
 class ResourceLimiter:
@@ -163,10 +245,12 @@ class ResourceLimiter:
                 except OSError:
                     self.cpu_root = None
         self.replicas: dict[str, ReplicaState] = {}
+        self._reader = _schedstat_reader() if self.mode == "watchdog" and enforce_cpu else None
 
     def describe(self) -> dict:
+        acct = "per-thread schedstat ns" if self._reader else "process clock ticks"
         cpu = {"cgroup2": "cgroup cpu.max", "cgroup1-cpu": "cgroup v1 cpu.cfs_quota_us",
-               "watchdog": f"duty-cycle throttle (SIGSTOP/SIGCONT, {int(PERIOD_S * 1000)} ms period)"}[self.mode] \
+               "watchdog": f"duty-cycle throttle (SIGSTOP/SIGCONT, {PERIOD_S * 1000:g} ms period, {acct})"}[self.mode] \
             if self.enforce_cpu else "accounted"
         mem = ("cgroup memory.max" if self.mode == "cgroup2" else "RSS watchdog + restart") if self.enforce_memory \
             else "accounted"
@@ -197,8 +281,13 @@ class ResourceLimiter:
                 self._adopt_v1(st)
             except OSError:
                 st.cpu_cgroup = None
-        st.period_cpu = cpu_seconds(tree(pid))
+        if self._reader is not None:
+            st.clock = ThreadClock(pid, self._reader)
+        st.period_cpu = self._used(st, time.monotonic())
         return st
+
+    def _used(self, st: ReplicaState, now: float) -> float:
+        return st.clock.seconds(now) if st.clock is not None else cpu_seconds(tree(st.pid))
 
     def _adopt_v1(self, st: ReplicaState) -> None:
         for p in tree(st.pid):
@@ -213,6 +302,8 @@ class ResourceLimiter:
             return
         if st.stopped:
             self._signal(st, signal.SIGCONT)
+        if st.clock is not None:
+            st.clock.close()
         for cg in (st.cgroup, st.cpu_cgroup):
             if cg is not None:
                 try:
@@ -266,7 +357,7 @@ class ResourceLimiter:
             return
         now = time.monotonic() if now is None else now
         for st in list(self.replicas.values()):
-            used = cpu_seconds(tree(st.pid))
+            used = self._used(st, now)
             if now - st.period_start >= PERIOD_S:
                 # unused quota does not carry over; an overrun does (paid off in later periods)
                 quota = st.limits.cpu * (now - st.period_start)
