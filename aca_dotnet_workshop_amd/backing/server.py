@@ -27,6 +27,7 @@ import json
 import logging
 import os
 import re
+import sys
 import tempfile
 import time
 from pathlib import Path
@@ -757,6 +758,10 @@ def main(argv: list[str] | None = None) -> None:
     ap.add_argument("--policy", default=None, help="JSON file with access policy (mode/keys/roleAssignments)")
     ap.add_argument("--port-file", default=None)
     a = ap.parse_args(argv)
+    # queries run on worker threads next to the event loop; every native call that releases the
+    # GIL (mirror sync, result assembly, device copies) waits for it again, up to the switch
+    # interval (5 ms by default) when the loop is busy -- tens of ms per query under write load
+    sys.setswitchinterval(0.0002)
     configure_logging("backing-services")
     configure("backing-services")
     policy = json.loads(Path(a.policy).read_text()) if a.policy else None

@@ -180,7 +180,8 @@ class KeyTable:
 class Column:
     def __init__(self, path: str) -> None:
         self.path = path
-        self.ids: dict[str, int] = {}
+        self._ids: dict[str, int] = {}
+        self._ids_n = 0  # values[:_ids_n] are in _ids (bulk-appended strings are keyed lazily)
         self.values: list[Any] = []
         self._num_cache: np.ndarray | None = None
         self._rank_cache: np.ndarray | None = None
@@ -190,14 +191,30 @@ class Column:
         self.str_only = True
         self._str_sorted = None
 
+    @property
+    def ids(self) -> dict[str, int]:
+        """vkey -> dictionary id.  Strings appended in bulk by ``encode_json_many`` are keyed on
+        first use: a column only ordered or range-filtered (timestamps) never pays for it."""
+        n = len(self.values)
+        if self._ids_n < n:
+            self._ids.update(zip([vkey(v) for v in self.values[self._ids_n:]], range(self._ids_n, n)))
+            self._ids_n = n
+        return self._ids
+
+    @ids.setter
+    def ids(self, d: dict[str, int]) -> None:
+        self._ids, self._ids_n = d, len(self.values)
+
     def encode(self, v: Any) -> int:
         if v is _MISSING:
             return -1
         k = vkey(v)
-        i = self.ids.get(k)
+        ids = self.ids
+        i = ids.get(k)
         if i is None:
-            i = self.ids[k] = len(self.values)
+            i = ids[k] = len(self.values)
             self.values.append(v)
+            self._ids_n += 1
             if type(v) is not str or v.endswith("\x00"):
                 self.str_only = False
             self._num_cache = None
@@ -209,23 +226,19 @@ class Column:
         """Dictionary ids of JSON value texts (the native mirror's new dictionary entries).
         Strings -- timestamps, names, e-mails, the values a growing collection adds on every
         write -- are decoded in one ``json.loads`` and appended in bulk: the native dictionary
-        holds each string once, so none is already here (the dictionary's size confirms it) and
-        no per-value ``vkey`` or dictionary probe is needed."""
+        holds each string once (strings compare by value there, as here), so none is already
+        here and no per-value ``vkey`` or dictionary probe is needed."""
         if texts and all(t[:1] == '"' for t in texts):
             joined = ",".join(texts)
             strs = json.loads("[" + joined + "]")
             base = len(self.values)
-            self.ids.update(zip(["s" + x for x in strs], range(base, base + len(strs))))
-            if len(self.ids) == base + len(strs):
-                self.values.extend(strs)
-                if self.str_only and "\\u0000" in joined and any(x.endswith("\x00") for x in strs):
-                    self.str_only = False
-                self._num_cache = None
-                self._rank_cache = None
-                self.rank_version += 1
-                return np.arange(base, base + len(strs), dtype=np.int32)
-            # a value was already here (not the native dictionary's invariant): per value
-            self.ids = {vkey(v): i for i, v in enumerate(self.values)}
+            self.values.extend(strs)  # keyed lazily (``ids``)
+            if self.str_only and "\\u0000" in joined and any(x.endswith("\x00") for x in strs):
+                self.str_only = False
+            self._num_cache = None
+            self._rank_cache = None
+            self.rank_version += 1
+            return np.arange(base, base + len(strs), dtype=np.int32)
         return np.fromiter((self.encode(json.loads(t)) for t in texts), dtype=np.int32, count=len(texts))
 
     def lookup(self, v: Any) -> int:

@@ -22,7 +22,11 @@ def load_library(build: bool = True) -> ctypes.CDLL:
         build_gpu()
     if not LIB.exists():
         raise RuntimeError(f"GPU kernel library {LIB} is missing; run `python -m aca_dotnet_workshop_amd.ops.build`")
-    lib = ctypes.CDLL(str(LIB))
+    # PyDLL: calls keep the GIL.  Every entry point is a kernel launch (microseconds) or a
+    # stream synchronise on a query's own kernels (tens of microseconds); releasing the GIL
+    # around them costs more -- a query thread next to a busy event loop waits up to the switch
+    # interval to get it back, once per call
+    lib = ctypes.PyDLL(str(LIB))
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, I32, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int

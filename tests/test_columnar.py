@@ -784,8 +784,8 @@ def test_bulk_string_encode_and_append_ranks():
     a._rank_cache = None
     assert a.ranks().tolist() == a._general_ranks().tolist() and a.str_only
     n = len(a.values)
-    assert a.encode_json_many([_json.dumps(ts[3]), _json.dumps("new")]).tolist() == [3, n]  # ts[3] exists
-    assert a.lookup(ts[3]) == 3 and a.lookup("new") == n and len(a.ids) == len(a.values)
+    assert a.lookup(ts[5]) == 5 and a.lookup("z\"q\u00e9") == n - 1 and len(a.ids) == n  # keyed on first use
+    assert a.encode(ts[3]) == 3 and a.encode("new") == n and a.lookup("new") == n
     a.encode_json_many([_json.dumps("nul\x00")])
     assert not a.str_only
     a._rank_cache = None
