@@ -742,6 +742,8 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         except (NotImplementedError, RuntimeError):
             pass
     await stop.wait()
+    for a in svc.accels.values():
+        a.close()
     if front is not None:
         front.stop()
     await srv.close()

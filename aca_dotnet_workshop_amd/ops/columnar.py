@@ -927,7 +927,8 @@ class ColumnarIndex:
         if leaf.any() and int(prog.code[leaf, 1].max()) >= len(self.columns):
             raise ValueError("program references a column outside the index")
         rng = prog.code[:, 0] == OP_RANGE
-        st = self.to_device(kernels, prog.code[rng, 1].tolist())
+        self._warm_rank_cols = prog.code[rng, 1].tolist()
+        st = self.to_device(kernels, self._warm_rank_cols)
         slots = tuple(sorted(st.get("rank_slot", {}).items())) if rng.any() else ()
         cached = getattr(prog, "_dev", None)
         if cached is not None and cached[0] == (slots, str(kernels.device)):
@@ -1075,6 +1076,32 @@ class ColumnarIndex:
         st = self.to_device(kernels)  # sort keys may have added columns
         return kernels.order(st["table"], rows, specs_t, ranks_t, st["seq"], seq_bits, k, key_bits)
 
+    def _zone_refresh(self, z: dict, kernels, st: dict, specs_t, ranks_t, seq_bits: int) -> None:
+        """Recompute the zone argmin of the tiles that changed since the last refresh."""
+        ntiles = (self.n + TILE - 1) // TILE
+        if z["zarg"].size < ntiles:  # new tiles: not computed yet
+            z["dirty"].update(range(z["zarg"].size, ntiles))
+            z["zarg"] = np.concatenate([z["zarg"], np.full(ntiles - z["zarg"].size, -1, dtype=np.int32)])
+        z["zarg"] = z["zarg"][:ntiles]
+        todo = np.arange(ntiles, dtype=np.int32) if z["all"] else \
+            np.fromiter((t for t in z["dirty"] if t < ntiles), dtype=np.int32)
+        if todo.size:
+            z["zarg"][todo] = kernels.zone_argmin(st["table"], st["live"], self.n, specs_t, ranks_t, st["seq"],
+                                                  seq_bits, todo)
+        z["all"], z["dirty"] = False, set()
+
+    def warm(self, kernels) -> None:
+        """Bring the device mirror up to the host index between queries: upload the rows
+        synced since the last query (with the rank-encoded columns the last queries read) and
+        refresh the zone maps of the sorts already served, so a query finds little to do.
+        Called by the accelerator's background sync (backing/accel.py) under its lock."""
+        st = self.to_device(kernels, getattr(self, "_warm_rank_cols", ()))
+        for z in list(self._zones.values()):
+            if z["all"] or z["dirty"] or z["zarg"].size < (self.n + TILE - 1) // TILE:
+                hit = self._device_sort_plan(z["sort"], kernels)
+                if hit is not None:
+                    self._zone_refresh(z, kernels, st, hit[0], hit[1], hit[2])
+
     def page_gpu(self, prog: Program, sort, kernels, offset: int, limit: int):
         """A page [offset, offset + limit) of an ordered query without scanning the collection
         (``hip/page_topk.hip``): zone maps pick the tiles that can hold the page, only those are
@@ -1094,17 +1121,9 @@ class ColumnarIndex:
         zkey = json.dumps(sort, sort_keys=True, default=str)
         z = self._zones.get(zkey)
         if z is None:
-            z = self._zones[zkey] = {"zarg": np.zeros(0, dtype=np.int32), "dirty": set(), "all": True, "density": {}}
-        if z["zarg"].size < ntiles:  # new tiles: not computed yet
-            z["dirty"].update(range(z["zarg"].size, ntiles))
-            z["zarg"] = np.concatenate([z["zarg"], np.full(ntiles - z["zarg"].size, -1, dtype=np.int32)])
-        z["zarg"] = z["zarg"][:ntiles]
-        todo = np.arange(ntiles, dtype=np.int32) if z["all"] else \
-            np.fromiter((t for t in z["dirty"] if t < ntiles), dtype=np.int32)
-        if todo.size:
-            z["zarg"][todo] = kernels.zone_argmin(st["table"], st["live"], self.n, specs_t, ranks_t, st["seq"],
-                                                  seq_bits, todo)
-        z["all"], z["dirty"] = False, set()
+            z = self._zones[zkey] = {"zarg": np.zeros(0, dtype=np.int32), "dirty": set(), "all": True, "density": {},
+                                     "sort": sort}
+        self._zone_refresh(z, kernels, st, specs_t, ranks_t, seq_bits)
         zarg = z["zarg"]
         valid = zarg >= 0
         nvalid = int(valid.sum())
@@ -1116,6 +1135,10 @@ class ColumnarIndex:
         pkey = (prog.code.tobytes(), prog.bitmaps.tobytes())
         dens = z["density"].get(pkey, 0.25)  # candidates per row of a chosen tile, from the last page
         b = min(nvalid, max(1, int(np.ceil(1.5 * k_total / max(dens * TILE, 1.0)))))
+        if z.setdefault("short", {}).get(pkey):
+            # the last page of this filter held every match in the collection (fewer than the
+            # page): start from every tile instead of growing towards it one launch at a time
+            b = nvalid
         lo_b, hi_b = 0, None  # largest tile count seen short of k candidates / smallest that overflowed
         for _ in range(24):
             if b >= nvalid:
@@ -1143,6 +1166,9 @@ class ColumnarIndex:
             z["density"][pkey] = max(total / (len(chosen) * TILE), 1e-4)
             if len(z["density"]) > 64:
                 z["density"].pop(next(iter(z["density"])))
+        z["short"][pkey] = bound == top and total < k_total
+        if len(z["short"]) > 64:
+            z["short"].pop(next(iter(z["short"])))
         if total > k_total:
             more = True
         elif bound == top:

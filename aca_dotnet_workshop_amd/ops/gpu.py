@@ -49,6 +49,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_rank_encode.argtypes = [P, P, I32, I64, I64, P, I32, P]
     lib.tt_launch_rank_encode.restype = ctypes.c_int
     lib.tt_page_cap.restype = ctypes.c_int
+    lib.tt_launch_page_reset.argtypes = [P, P]
+    lib.tt_launch_page_reset.restype = ctypes.c_int
     lib.tt_launch_zone_argmin.argtypes = [P, I64, P, P, I32, P, P, I32, P, I32, P, P]
     lib.tt_launch_zone_argmin.restype = ctypes.c_int
     lib.tt_launch_page.argtypes = [P, I64, P, P, I32, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, I32,
@@ -221,9 +223,11 @@ class GpuKernels:
             tarr[:n] = tiles
             ck = self._buf("page_keys", self.page_cap, torch.int64)
             cr = self._buf("page_rows", self.page_cap, torch.int32)
-            if "page_counter" not in self._bufs:  # zeroed once; tt_page_topk resets it after each query
-                self._bufs["page_counter"] = torch.zeros(1, dtype=torch.int32, device=self.device)
             stream = self._stream()
+            if "page_counter" not in self._bufs:  # zeroed once; tt_page_topk resets it after each query
+                self._bufs["page_counter"] = torch.empty(1, dtype=torch.int32, device=self.device)
+                if self.lib.tt_launch_page_reset(self._bufs["page_counter"].data_ptr(), stream) != 0:
+                    raise RuntimeError("tt_page_reset launch failed")
             rc = self.lib.tt_launch_page(table.data_ptr(), nrows, live16.data_ptr(), prog.data_ptr(), prog.shape[0],
                                          bitmaps.data_ptr(), bitmaps.numel(), specs.data_ptr(), specs.shape[0],
                                          ranks.data_ptr(), seq.data_ptr(), seq_bits, tdev, n,

@@ -303,7 +303,17 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
   }
 }
 
+extern "C" __global__ void tt_page_reset(uint32_t* __restrict__ counter) {
+  if (threadIdx.x == 0) *counter = 0;
+}
+
 extern "C" int tt_page_cap() { return kPageCap; }
+
+// The candidate counter's first zeroing (tt_page_topk resets it after every query).
+extern "C" int tt_launch_page_reset(uint32_t* counter, hipStream_t stream) {
+  hipLaunchKernelGGL(tt_page_reset, dim3(1), dim3(64), 0, stream, counter);
+  return (int)hipGetLastError();
+}
 
 extern "C" int tt_launch_zone_argmin(const void* cols, int64_t nrows, const uint16_t* live, const void* specs,
                                      int32_t nkeys, const int32_t* ranks, const uint32_t* seq, int32_t seq_bits,

@@ -659,7 +659,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
                           "shards": len(shards),
                           "store_ms_total": {k2: acc.get(k2) for k2 in ("lock_wait_ms", "sync_ms",
-                                                                         "select_and_results_ms")}}
+                                                                         "select_and_results_ms", "select_ms",
+                                                                         "results_ms", "bg_sync_ms", "bg_syncs")}}
         delivery = None
         if shared:  # exactly-once across the competing consumers of every rank, over every shard
             c = _counts(counts_url)
