@@ -196,6 +196,8 @@ class CollectionAccelerator:
             for key, v in (("lock_wait_ms", t0 - t_wait), ("sync_ms", t1 - t0), ("select_and_results_ms", t2 - t1),
                            ("select_ms", t_sel), ("results_ms", t_res)):
                 self.stats[key] = round(self.stats.get(key, 0.0) + v * 1e3, 3)
+            for key, v in self.index.timing.items():  # the paged device path's own breakdown
+                self.stats[key] = round(v, 3)
             return out
 
 

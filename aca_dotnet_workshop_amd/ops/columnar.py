@@ -18,6 +18,7 @@ from __future__ import annotations
 import functools
 import json
 import os
+import time
 from dataclasses import dataclass
 from typing import Any, Iterable
 
@@ -382,6 +383,7 @@ class ColumnarIndex:
         # zone maps of the paged device path, per sort spec (page_gpu): per tile the row with the
         # smallest ordering key, re-computed for the tiles whose rows changed
         self._zones: dict[Any, dict] = {}
+        self.timing: dict[str, float] = {}  # where the paged device path spends its time (summed)
         for p in paths:
             self.add_column(p)
 
@@ -1110,11 +1112,17 @@ class ColumnarIndex:
         k_total = offset + limit
         if limit <= 0 or k_total > kernels.page_cap:
             return None
+        tm = self.timing
+        t0 = time.perf_counter()
         hit = self._device_sort_plan(sort, kernels)
         if hit is None:
             return None
         specs_t, ranks_t, seq_bits, _, plan = hit
+        t1 = time.perf_counter()
         st, code, bitmaps = self.device_program(prog, kernels)
+        t2 = time.perf_counter()
+        tm["page_plan_ms"] = tm.get("page_plan_ms", 0.0) + (t1 - t0) * 1e3
+        tm["page_program_ms"] = tm.get("page_program_ms", 0.0) + (t2 - t1) * 1e3
         ntiles = (self.n + TILE - 1) // TILE
         if ntiles == 0:
             return np.zeros(0, dtype=np.int32), None
@@ -1124,6 +1132,8 @@ class ColumnarIndex:
             z = self._zones[zkey] = {"zarg": np.zeros(0, dtype=np.int32), "dirty": set(), "all": True, "density": {},
                                      "sort": sort}
         self._zone_refresh(z, kernels, st, specs_t, ranks_t, seq_bits)
+        t3 = time.perf_counter()
+        tm["page_zones_ms"] = tm.get("page_zones_ms", 0.0) + (t3 - t2) * 1e3
         zarg = z["zarg"]
         valid = zarg >= 0
         nvalid = int(valid.sum())
@@ -1140,6 +1150,7 @@ class ColumnarIndex:
             # page): start from every tile instead of growing towards it one launch at a time
             b = nvalid
         lo_b, hi_b = 0, None  # largest tile count seen short of k candidates / smallest that overflowed
+        launches = 0
         for _ in range(24):
             if b >= nvalid:
                 chosen, bound = np.nonzero(valid)[0].astype(np.int32), top
@@ -1148,6 +1159,7 @@ class ColumnarIndex:
                 chosen, bound = part[:b].astype(np.int32), int(keys[part[b]])
             rows, total, complete = kernels.page(st["table"], st["live"], self.n, code, bitmaps, specs_t, ranks_t,
                                                  st["seq"], seq_bits, chosen, k_total, offset, bound)
+            launches += 1
             if complete:
                 break
             if total > kernels.page_cap:  # more candidates than one workgroup sorts: fewer tiles
@@ -1169,12 +1181,16 @@ class ColumnarIndex:
         z["short"][pkey] = bound == top and total < k_total
         if len(z["short"]) > 64:
             z["short"].pop(next(iter(z["short"])))
+        t4 = time.perf_counter()
+        tm["page_kernels_ms"] = tm.get("page_kernels_ms", 0.0) + (t4 - t3) * 1e3
+        tm["page_launches"] = tm.get("page_launches", 0) + launches
         if total > k_total:
             more = True
         elif bound == top:
             more = False
         else:  # the page used every candidate: are there matches in the tiles left out?
             more = int(self.select_gpu(prog, kernels, on_device=True).numel()) > k_total
+            tm["page_more_ms"] = tm.get("page_more_ms", 0.0) + (time.perf_counter() - t4) * 1e3
         return rows, (str(k_total) if more else None)
 
     def query(self, q: dict[str, Any], kernels=None) -> tuple[list[str], str | None]:

@@ -187,6 +187,10 @@ class OverdueSweeper:
     def start(self) -> None:
         self.thread.start()
 
+    def reset(self) -> None:
+        """Forget the sweeps so far (the warmup's): the summary covers what follows."""
+        self.runs, self.errors = [], []
+
     def stop(self) -> None:
         self.stop_ev.set()
         self.thread.join(timeout=120)
@@ -625,11 +629,14 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if shared:  # the subscription's completed counter before anyone sends (global step targets)
             d.barrier()
             gbase = d.broadcast(_counter(counts_url) if d.rank == 0 else None)
+        if sweep and (not shared or d.rank == 0):  # one cron trigger per environment
+            # running from the warmup on: the timed region sees the steady state of a periodic
+            # job (mirror built, device columns and zone maps resident), not its first run
+            sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
+            sweeper.start()
         if a.warmup:
             run_form_loadgen(exe, fe_ports, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
                              (gbase, stride) if shared else None)
-        if sweep and (not shared or d.rank == 0):  # one cron trigger per environment
-            sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
         d.barrier()
         device_sync()
         me = psutil.Process()
@@ -637,8 +644,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
         ru0 = _collection_stats(backing).get("throughput", {})
+        acc0 = _accel_stats(shards) if sweeper is not None else {}
         if sweeper is not None:
-            sweeper.start()
+            sweeper.reset()  # sweeps of the timed region only
         dt, report = run_form_loadgen(exe, fe_ports, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
                                       (gbase + stride * a.warmup, stride) if shared else None)
         device_sync()
@@ -653,14 +661,19 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
         sweep_info = None
         if sweeper is not None:
-            acc = _accel_stats(shards)
+            acc1 = _accel_stats(shards)  # the timed region's share of the accelerator counters
+            acc = {k: (round(v - acc0.get(k, 0), 3) if isinstance(v, (int, float)) and k != "rows" else v)
+                   for k, v in acc1.items()}
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
                           "shards": len(shards),
                           "store_ms_total": {k2: acc.get(k2) for k2 in ("lock_wait_ms", "sync_ms",
                                                                          "select_and_results_ms", "select_ms",
-                                                                         "results_ms", "bg_sync_ms", "bg_syncs")}}
+                                                                         "results_ms", "bg_sync_ms", "bg_syncs", "page_plan_ms",
+                                                                         "page_program_ms", "page_zones_ms",
+                                                                         "page_kernels_ms", "page_launches",
+                                                                         "page_more_ms")}}
         delivery = None
         if shared:  # exactly-once across the competing consumers of every rank, over every shard
             c = _counts(counts_url)
