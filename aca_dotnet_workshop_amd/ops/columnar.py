@@ -16,6 +16,7 @@ numbers by value; ranges only between like types), producing one bitmap per leaf
 from __future__ import annotations
 
 import functools
+import itertools
 import json
 import os
 import time
@@ -178,6 +179,9 @@ class KeyTable:
             yield self[i]
 
 
+_RANK_EPOCHS = itertools.count(1)
+
+
 class Column:
     def __init__(self, path: str) -> None:
         self.path = path
@@ -187,6 +191,8 @@ class Column:
         self._num_cache: np.ndarray | None = None
         self._rank_cache: np.ndarray | None = None
         self.rank_version = 0  # bumps whenever a new value may shift the sort ranks
+        self.rank_epoch = next(_RANK_EPOCHS)  # changes when the ranks of existing ids changed (unique)
+        self._appended_only = False
         # every value a str without a trailing NUL (numpy's fixed-width strings drop those):
         # the ranks are then positions in the sorted dictionary (_string_ranks)
         self.str_only = True
@@ -273,13 +279,18 @@ class Column:
 
     def missing_rank(self) -> int:
         """A missing path sorts like JSON null (the native engine compares it as null)."""
+        if self.str_only:
+            return 0  # no null in a string-only dictionary (and no need to key it)
         i = self.ids.get("n")
         return int(self.ranks()[i]) if i is not None else 0
 
     def ranks(self) -> np.ndarray:
         """Sort rank of every dictionary id (ties share a rank, ranks start at 1)."""
         if self._rank_cache is None:
+            self._appended_only = False
             self._rank_cache = self._string_ranks() if self._all_strings() else self._general_ranks()
+            if not self._appended_only:
+                self.rank_epoch = next(_RANK_EPOCHS)  # ranks of existing ids may have moved
         return self._rank_cache
 
     def _all_strings(self) -> bool:
@@ -307,6 +318,7 @@ class Column:
             return r[:n]
         srt, m, old_r = prev
         if m == n:
+            self._appended_only = True
             return old_r[:n]
         new = np.array(self.values[m:], dtype=str)
         norder = np.argsort(new, kind="stable")
@@ -322,6 +334,7 @@ class Column:
             srt[m:n] = new_sorted
             old_r[m + norder] = np.arange(m + 1, n + 1)
             self._str_sorted = (srt, n, old_r)
+            self._appended_only = True  # every old id keeps its rank
             return old_r[:n]
         srt = srt[:m]
         old_r = old_r[:m]
@@ -1043,30 +1056,65 @@ class ColumnarIndex:
 
     def _device_sort_plan(self, sort, kernels):
         """(specs, rank tables, seq bits, key bits) on the device and the host plan of the same
-        packed key, cached per sort spec and dictionary state; None when the device cannot
-        order by it (too many keys, a key over 63 bits, a sequence over 32 bits)."""
+        packed key, kept per sort spec; None when the device cannot order by it (too many keys,
+        a key over 63 bits, a sequence over 32 bits).
+
+        The rank tables live in one buffer, one capacity-doubled region per sort key, on the
+        device and (for ``sort_keys_numpy``) on the host.  While a key's dictionary only grows
+        at the end of its order -- the timestamps of new writes -- the old ranks stay valid and
+        only the new ids' ranks are copied: O(new values) per query instead of re-deriving and
+        re-uploading the whole table (``taskCreatedOn`` has one value per task)."""
         if len(sort or []) > kernels.max_sort_keys:
             return None
-        for srt in sort or []:
-            self.add_column(srt["key"])
-        seq_bits_now = max(1, int(self._next_seq).bit_length())
-        pkey = (json.dumps(sort, sort_keys=True, default=str), self._dict_state(), seq_bits_now, str(kernels.device))
-        hit = self._plan_cache.get(pkey)
-        if hit is None:
-            plan = self.sort_specs(sort)
-            if plan is None:
-                return None
-            specs, ranks, seq_bits = plan
-            if seq_bits > 32:
-                return None  # the device keeps a 32-bit insertion sequence
-            torch = kernels.torch
-            key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
-            hit = (torch.from_numpy(specs).to(kernels.device), torch.from_numpy(ranks).to(kernels.device), seq_bits,
-                   key_bits, plan)
+        cols = [self.add_column(srt["key"]) for srt in sort or []]
+        seq_bits = max(1, int(self._next_seq).bit_length())
+        if seq_bits > 32:
+            return None  # the device keeps a 32-bit insertion sequence
+        torch = kernels.torch
+        pkey = (json.dumps(sort, sort_keys=True, default=str), str(kernels.device), self._dict_gen)
+        ent = self._plan_cache.get(pkey)
+        tables, specs_rows, total = [], [], seq_bits
+        for srt, col in zip(sort or [], cols):
+            c = self.columns[col]
+            r = c.ranks() if c.values else np.zeros(0, dtype=np.int64)
+            miss = c.missing_rank()
+            max_rank = len(c.values) if c.str_only else int(r.max(initial=0))
+            max_rank = max(max_rank, miss)
+            bits = max(1, max_rank.bit_length())
+            total += bits
+            desc = 1 if str(srt.get("order", "ASC")).upper() == "DESC" else 0
+            tables.append((r, c.rank_epoch))
+            specs_rows.append([col, 0, r.size, bits, desc, miss, max_rank, 0])
+        if total > 63:
+            return None
+        rebuild = ent is None or any(ep != e for (_, ep), e in zip(tables, ent["epochs"])) or \
+            any(r.size > cap for (r, _), cap in zip(tables, ent["caps"]))
+        if rebuild:
+            caps = [max(1024, 1 << max(0, int(r.size * 1.25) + 1).bit_length()) for r, _ in tables]
+            offs = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64) if caps else np.zeros(0, np.int64)
+            host = np.zeros(max(1, int(sum(caps))), dtype=np.int32)
+            for (r, _), off in zip(tables, offs):
+                host[off:off + r.size] = r
+            ent = {"caps": caps, "offs": offs, "n": [r.size for r, _ in tables], "epochs": [e for _, e in tables],
+                   "host": host, "dev": torch.from_numpy(host).to(kernels.device), "specs": None, "specs_dev": None}
             if len(self._plan_cache) >= 64:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
-            self._plan_cache[pkey] = hit
-        return hit
+            self._plan_cache[pkey] = ent
+        else:
+            for i, (r, _) in enumerate(tables):
+                lo, off = ent["n"][i], int(ent["offs"][i])
+                if r.size > lo:  # the new ids' ranks (the old ones did not move)
+                    tail = r[lo:].astype(np.int32)
+                    ent["host"][off + lo:off + r.size] = tail
+                    ent["dev"][off + lo:off + r.size].copy_(torch.from_numpy(tail))
+                    ent["n"][i] = r.size
+        for row, off in zip(specs_rows, ent["offs"]):
+            row[1] = int(off)
+        specs = np.array(specs_rows, dtype=np.int32).reshape(-1, 8)
+        if ent["specs"] is None or not np.array_equal(specs, ent["specs"]):
+            ent["specs"], ent["specs_dev"] = specs, torch.from_numpy(specs).to(kernels.device)
+        key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
+        return ent["specs_dev"], ent["dev"], seq_bits, key_bits, (specs, ent["host"], seq_bits)
 
     def order_gpu(self, rows, sort, kernels, k: int | None = None):
         """Order a device selection on the GPU (``hip/sort_keys.hip`` + radix sort / top-k);

@@ -885,6 +885,39 @@ def test_page_path_host_logic_matches_full_order(seed, sort, limit):
     assert fk.calls["page_tiles"] / max(1, fk.calls["pages"]) < (ix.n + 8191) // 8192
 
 
+def test_device_sort_plan_grows_in_place_and_matches_the_host_keys():
+    """The paged path's sort plan keeps its rank tables across queries: new timestamps that sort
+    last only append their ranks (no rebuild, same device buffer); a value that lands inside the
+    order, a new sort key or a numeric column rebuilds.  The packed keys it yields always equal
+    the host reference's."""
+    import torch
+    ix = ColumnarIndex(["c", "d"])
+    fk = _FakePageKernels(ix)
+    sort = [{"key": "c"}, {"key": "d", "order": "DESC"}]
+
+    def check():
+        hit = ix._device_sort_plan(sort, fk)
+        rows = np.nonzero(ix.live[:ix.n])[0]
+        want = ix.sort_keys_numpy(rows, ix.sort_specs(sort))
+        assert np.array_equal(ix.sort_keys_numpy(rows, hit[4]), want)
+        assert torch.equal(hit[1], torch.from_numpy(hit[4][1]))  # device table == host table
+        return hit
+    for i in range(3000):
+        ix.upsert(f"k{i}", {"c": f"2026-01-01T00:{i // 60:02d}:{i % 60:02d}", "d": i % 7})
+    buf, rebuilds = check()[1], 0
+    for lo in range(3000, 9000, 500):  # newer timestamps only: appended in place
+        for i in range(lo, lo + 500):
+            ix.upsert(f"k{i}", {"c": f"2026-01-02T{i // 3600:02d}:{i // 60 % 60:02d}:{i % 60:02d}", "d": i % 7})
+        hit = check()
+        rebuilds += hit[1] is not buf
+        buf = hit[1]
+    assert rebuilds <= 2  # capacity doublings only (3,000 -> 9,000 ranks)
+    ix.upsert("old", {"c": "2025-12-31T00:00:00", "d": 3})  # sorts first: existing ranks move
+    assert check()[1] is not buf
+    ix.upsert("k5", {"c": "2026-01-03T00:00:00", "d": 99})   # update: a new row, a new d value
+    check()
+
+
 def test_page_path_overflow_and_tiny_cap_fall_back():
     """More candidates than the device top-k holds: fewer tiles are taken, and a page that
     cannot fit at all is left to the full path (None)."""
