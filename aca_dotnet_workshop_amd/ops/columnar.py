@@ -191,8 +191,12 @@ class Column:
         self._num_cache: np.ndarray | None = None
         self._rank_cache: np.ndarray | None = None
         self.rank_version = 0  # bumps whenever a new value may shift the sort ranks
-        self.rank_epoch = next(_RANK_EPOCHS)  # changes when the ranks of existing ids changed (unique)
-        self._appended_only = False
+        # which ids' ranks each recomputation changed: (recomputation number, first id whose rank
+        # moved); consumers that keep a copy of the ranks (the device sort plan) re-copy only
+        # ids >= that bound (the newest ids, for timestamps written roughly in order)
+        self.rank_seq = next(_RANK_EPOCHS)
+        self._rank_log: list[tuple[int, int]] = []
+        self._rank_lo = 0
         # every value a str without a trailing NUL (numpy's fixed-width strings drop those):
         # the ranks are then positions in the sorted dictionary (_string_ranks)
         self.str_only = True
@@ -287,11 +291,23 @@ class Column:
     def ranks(self) -> np.ndarray:
         """Sort rank of every dictionary id (ties share a rank, ranks start at 1)."""
         if self._rank_cache is None:
-            self._appended_only = False
+            self._rank_lo = 0
             self._rank_cache = self._string_ranks() if self._all_strings() else self._general_ranks()
-            if not self._appended_only:
-                self.rank_epoch = next(_RANK_EPOCHS)  # ranks of existing ids may have moved
+            self.rank_seq = next(_RANK_EPOCHS)
+            self._rank_log.append((self.rank_seq, self._rank_lo))
+            if len(self._rank_log) > 64:
+                del self._rank_log[0]
         return self._rank_cache
+
+    def rank_changes_since(self, seq: int) -> int | None:
+        """The first id whose rank may differ from the ranks of recomputation ``seq`` (the
+        dictionary size when none moved); None when ``seq`` is too old to tell."""
+        self.ranks()
+        if seq == self.rank_seq:
+            return len(self.values)
+        if not any(s == seq for s, _ in self._rank_log):
+            return None
+        return min([lo for s, lo in self._rank_log if s > seq] or [len(self.values)])
 
     def _all_strings(self) -> bool:
         if not self.str_only:
@@ -314,11 +330,12 @@ class Column:
             order = np.argsort(arr, kind="stable")
             r = np.empty(n, dtype=np.int64)
             r[order] = np.arange(1, n + 1)
-            self._str_sorted = (arr[order], n, r)
+            self._str_sorted = (arr[order], n, r, order.astype(np.int64))
+            self._rank_lo = 0
             return r[:n]
-        srt, m, old_r = prev
+        srt, m, old_r, ids = prev  # sorted values, count, rank per id, id per sorted position
         if m == n:
-            self._appended_only = True
+            self._rank_lo = n
             return old_r[:n]
         new = np.array(self.values[m:], dtype=str)
         norder = np.argsort(new, kind="stable")
@@ -330,14 +347,18 @@ class Column:
                 srt2[:m] = srt[:m]
                 r2 = np.empty(cap, dtype=np.int64)
                 r2[:m] = old_r[:m]
-                srt, old_r = srt2, r2
+                i2 = np.empty(cap, dtype=np.int64)
+                i2[:m] = ids[:m]
+                srt, old_r, ids = srt2, r2, i2
             srt[m:n] = new_sorted
             old_r[m + norder] = np.arange(m + 1, n + 1)
-            self._str_sorted = (srt, n, old_r)
-            self._appended_only = True  # every old id keeps its rank
+            ids[m:n] = m + norder
+            self._str_sorted = (srt, n, old_r, ids)
+            self._rank_lo = m  # every old id keeps its rank
             return old_r[:n]
         srt = srt[:m]
         old_r = old_r[:m]
+        ids = ids[:m]
         width = max(srt.dtype.itemsize, new.dtype.itemsize) // 4
         srt = srt.astype(f"<U{max(width, 1)}", copy=False)
         new_sorted = new_sorted.astype(srt.dtype, copy=False)
@@ -346,7 +367,11 @@ class Column:
         r = np.empty(n, dtype=np.int64)
         r[:m] = old_r + before
         r[m + norder] = pos + np.arange(new.size) + 1
-        self._str_sorted = (np.insert(srt, pos, new_sorted), n, r)
+        # the old values at or after the first insertion point moved up: the first id among
+        # them bounds what changed (new timestamps arriving a little out of order: recent ids)
+        moved = ids[int(pos[0]):]
+        self._rank_lo = int(min(int(moved.min()), m)) if moved.size else m
+        self._str_sorted = (np.insert(srt, pos, new_sorted), n, r, np.insert(ids, pos, m + norder))
         return r
 
     def _general_ranks(self) -> np.ndarray:
@@ -1060,10 +1085,11 @@ class ColumnarIndex:
         a key over 63 bits, a sequence over 32 bits).
 
         The rank tables live in one buffer, one capacity-doubled region per sort key, on the
-        device and (for ``sort_keys_numpy``) on the host.  While a key's dictionary only grows
-        at the end of its order -- the timestamps of new writes -- the old ranks stay valid and
-        only the new ids' ranks are copied: O(new values) per query instead of re-deriving and
-        re-uploading the whole table (``taskCreatedOn`` has one value per task)."""
+        device and (for ``sort_keys_numpy``) on the host.  Only the ids whose rank is new or moved
+        since the last query are copied (``Column.rank_changes_since``): for the timestamps of
+        new writes, which arrive nearly in order, those are the newest ids -- O(new values) per
+        query instead of re-uploading the whole table (``taskCreatedOn`` has one value per
+        task)."""
         if len(sort or []) > kernels.max_sort_keys:
             return None
         cols = [self.add_column(srt["key"]) for srt in sort or []]
@@ -1083,11 +1109,13 @@ class ColumnarIndex:
             bits = max(1, max_rank.bit_length())
             total += bits
             desc = 1 if str(srt.get("order", "ASC")).upper() == "DESC" else 0
-            tables.append((r, c.rank_epoch))
+            tables.append((r, c))
             specs_rows.append([col, 0, r.size, bits, desc, miss, max_rank, 0])
         if total > 63:
             return None
-        rebuild = ent is None or any(ep != e for (_, ep), e in zip(tables, ent["epochs"])) or \
+        los = [None] * len(tables) if ent is None else \
+            [c.rank_changes_since(sq) for (_, c), sq in zip(tables, ent["seqs"])]
+        rebuild = ent is None or any(lo is None for lo in los) or \
             any(r.size > cap for (r, _), cap in zip(tables, ent["caps"]))
         if rebuild:
             caps = [max(1024, 1 << max(0, int(r.size * 1.25) + 1).bit_length()) for r, _ in tables]
@@ -1095,19 +1123,19 @@ class ColumnarIndex:
             host = np.zeros(max(1, int(sum(caps))), dtype=np.int32)
             for (r, _), off in zip(tables, offs):
                 host[off:off + r.size] = r
-            ent = {"caps": caps, "offs": offs, "n": [r.size for r, _ in tables], "epochs": [e for _, e in tables],
+            ent = {"caps": caps, "offs": offs, "seqs": [c.rank_seq for _, c in tables],
                    "host": host, "dev": torch.from_numpy(host).to(kernels.device), "specs": None, "specs_dev": None}
             if len(self._plan_cache) >= 64:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
             self._plan_cache[pkey] = ent
         else:
-            for i, (r, _) in enumerate(tables):
-                lo, off = ent["n"][i], int(ent["offs"][i])
-                if r.size > lo:  # the new ids' ranks (the old ones did not move)
+            for i, ((r, c), lo) in enumerate(zip(tables, los)):
+                off = int(ent["offs"][i])
+                if r.size > lo:  # the ids whose rank is new or moved (the newest ones)
                     tail = r[lo:].astype(np.int32)
                     ent["host"][off + lo:off + r.size] = tail
                     ent["dev"][off + lo:off + r.size].copy_(torch.from_numpy(tail))
-                    ent["n"][i] = r.size
+                ent["seqs"][i] = c.rank_seq
         for row, off in zip(specs_rows, ent["offs"]):
             row[1] = int(off)
         specs = np.array(specs_rows, dtype=np.int32).reshape(-1, 8)
