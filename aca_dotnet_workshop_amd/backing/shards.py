@@ -143,6 +143,8 @@ class ShardedBackingClient:
         self._rr = itertools.count()
 
     def __getattr__(self, name: str):  # non-partitioned services: the rank's own backing
+        if name.startswith("__") or name in ("home", "shards"):
+            raise AttributeError(name)  # not set yet (construction, copy): no recursion
         return getattr(self.home, name)
 
     @property

@@ -983,6 +983,28 @@ def test_gpu_page_path_matches_host(sort):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 700, 1023, 1024, 1025, 2583, 4096, 4097, 8191, 8192])
+def test_gpu_page_topk_sorts_every_candidate_count(n):
+    """tt_page_topk (register / cross-lane / LDS bitonic network over E = 1, 2, 4, 8 elements
+    per thread) returns the [offset, k) slice of the key order for every candidate count up to
+    the LDS capacity, with the completeness flag the host relies on."""
+    import torch
+    k = _kernels()
+    rng = np.random.default_rng(n)
+    keys = (rng.integers(0, 1 << 40, n, dtype=np.int64) << 20) | np.arange(n, dtype=np.int64)  # unique
+    rows = rng.permutation(n).astype(np.int32)
+    dk, dr = torch.from_numpy(keys).to(k.device), torch.from_numpy(rows).to(k.device)
+    order = rows[np.argsort(keys.astype(np.uint64), kind="stable")]
+    for kk, off in ((1, 0), (1000, 0), (1000, 400), (8192, 0), (64, 64)):
+        got, info = k.page_topk(dk, dr, kk, off, np.iinfo(np.uint64).max)
+        assert got.tolist() == order[off:min(n, kk)].tolist(), (n, kk, off)
+        assert info[0] == n and info[2] == max(0, min(n, kk) - off)
+        assert info[1] == 1  # bound = all tiles read: complete
+    got, info = k.page_topk(dk, dr, 1000, 0, 12345)  # a bound: complete only with k candidates
+    assert info[1] == (1 if n >= 1000 else 0)
+
+
+@pytest.mark.gpu
 def test_gpu_zone_argmin_matches_numpy():
     k = _kernels()
     rnd = random.Random(8)
