@@ -62,7 +62,7 @@ def test_merge_pages_offsets():
 
 def _task(i: int) -> dict:
     return {"taskId": f"00000000-0000-4000-8000-{i:012d}", "taskName": f"Task {i % 17}",
-            "taskCreatedBy": f"user{i % 5}@x", "taskCreatedOn": f"2026-10-{1 + i % 28:02d}T10:{i % 60:02d}:{i // 60:02d}",
+            "taskCreatedBy": f"user{i % 5}@x", "taskCreatedOn": f"2026-10-{1 + i % 28:02d}T{i // 3600 % 24:02d}:{i % 60:02d}:{i // 60 % 60:02d}",
             "taskDueDate": f"2026-10-{1 + (i * 7) % 28:02d}T00:00:00", "taskAssignedTo": "a@x",
             "isCompleted": i % 9 == 0, "isOverDue": i % 11 == 0}
 
@@ -220,6 +220,100 @@ def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
         run(main())
     finally:
         stack.stop()
+
+
+def _sweep_env(tmp: Path, name: str, shard_urls: list[str] | None, single_url: str | None):
+    """An API (range overdue query) + processor (pages of 50) pair over either the shards or one
+    backing; returns (stack, processor sidecar socket)."""
+    stack = LocalStack(root=tmp / name)
+    if shard_urls:
+        stack.start_backing()  # home services; the store and the broker are the shards
+        for fam in ("COSMOS", "SERVICEBUS"):
+            stack.base_env[f"TT_BACKING_SHARDS_{fam}"] = ",".join(shard_urls)
+    else:
+        stack.base_env["TT_BACKING_URL"] = single_url
+        stack.backing_url = single_url
+    cfg = {"Logging:LogLevel:Default": "Warning", "TasksNotifier:Mode": "log"}
+    stack.start_replica("tasksmanager-backend-api", {**cfg, "OverdueTasks:Query": "range"})
+    proc = stack.start_replica("tasksmanager-backend-processor", {**cfg, "OverdueTasks:PageSize": "50"})
+    stack.wait_ready()
+    return stack, proc.sidecar_uds
+
+
+@pytest.fixture
+def sweep_backings(tmp_path):
+    """Fresh backings for the sweep test: two shards and one single store (columnar CPU path)."""
+    stacks = []
+    try:
+        for i in range(3):
+            st = LocalStack(root=tmp_path / f"b{i}", env={"TT_QUERY_ACCEL": "cpu", "TT_QUERY_ACCEL_MIN_DOCS": "0",
+                                                          "TT_QUERY_MIRROR_PATHS": "taskDueDate,isCompleted,isOverDue,taskCreatedOn"})
+            st.start_backing()
+            stacks.append(st)
+        yield [st.backing_url for st in stacks]
+    finally:
+        for st in stacks:
+            st.stop()
+
+
+def test_sharded_overdue_sweep_marks_the_same_tasks_as_one_store(tmp_path, sweep_backings):
+    """The cron job (processor -> API range query -> cross-partition merge of both shards'
+    columnar pages -> markoverdue bulk save routed per shard) marks exactly the tasks a
+    single-store environment marks, page by page across the shards."""
+    from datetime import datetime, timedelta
+    past = (datetime.utcnow() - timedelta(days=3)).strftime("%Y-%m-%dT00:00:00")
+    future = (datetime.utcnow() + timedelta(days=3)).strftime("%Y-%m-%dT00:00:00")
+    docs = {}
+    for i in range(400):
+        t = _task(10_000 + i)
+        t["taskDueDate"] = past if i % 3 else future
+        t["isCompleted"], t["isOverDue"] = i % 7 == 0, i % 11 == 0
+        docs[f"{PREFIX}{t['taskId']}"] = t
+    want = {k for k, t in docs.items() if t["taskDueDate"] == past and not t["isCompleted"] and not t["isOverDue"]}
+    stacks = []
+    try:
+        async def load(client):
+            items = [{"key": k, "value": json.dumps(v)} for k, v in docs.items()]
+            await client.doc_bulk_set("taskstracker-state-store", DB, COLL, items)
+            await client.close()
+        backings = sweep_backings
+        run(load(ShardedBackingClient(backings[:2], identity="platform-admin")))
+        one_url = backings[2]
+        run(load(BackingClient(one_url, identity="platform-admin")))
+        results = []
+        for name, shard_urls, single in (("sharded", backings[:2], None), ("single", None, one_url)):
+            stack, sock = _sweep_env(tmp_path, name, shard_urls, single)
+            stacks.append(stack)
+
+            async def sweep(sock=sock):
+                from aca_dotnet_workshop_amd.web.client import HttpClient
+                http = HttpClient()
+                try:
+                    r = await http.request("POST", f"unix:{sock}:/v1.0/invoke/tasksmanager-backend-processor/method/"
+                                           "ScheduledTasksManager", body=b"{}",
+                                           headers=[("Content-Type", "application/json")], timeout=120)
+                    assert r.status == 200, r.body
+                    return json.loads(r.body)
+                finally:
+                    await http.close()
+            results.append(run(sweep()))
+
+        async def marked(client):
+            try:
+                got = await client.doc_bulk_get("taskstracker-state-store", DB, COLL, sorted(want))
+                return {g["key"] for g in got if g.get("data") and g["data"].get("isOverDue")}
+            finally:
+                await client.close()
+        sharded = run(marked(ShardedBackingClient(backings[:2], identity="platform-admin")))
+        single = run(marked(BackingClient(one_url, identity="platform-admin")))
+        assert sharded == single == want, (len(sharded), len(single), len(want))
+        assert results[0]["markedOverdue"] == results[1]["markedOverdue"] == len(want)
+        assert results[0]["pages"] >= len(want) // 50  # paged through the merged order
+        per_shard = {shard_of(k, 2) for k in want}
+        assert per_shard == {0, 1}
+    finally:
+        for st in stacks:
+            st.stop()
 
 
 def _free_port() -> int:
