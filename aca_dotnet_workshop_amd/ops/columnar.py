@@ -340,7 +340,13 @@ class Column:
         new = np.array(self.values[m:], dtype=str)
         norder = np.argsort(new, kind="stable")
         new_sorted = new[norder]
-        if new_sorted.dtype.itemsize <= srt.dtype.itemsize and (m == 0 or new_sorted[0] > srt[m - 1]):
+        k = new.size
+        # insertion point of the smallest new value: only the old values from there on move
+        pos0 = m if m == 0 or new_sorted[0] > srt[m - 1] else int(np.searchsorted(srt[:m], new_sorted[0]))
+        if new_sorted.dtype.itemsize <= srt.dtype.itemsize and m - pos0 <= 4 * k + 65536:
+            # new values land in (or just before) the tail of the order -- new timestamps,
+            # written a little out of order by concurrent writers: re-sort only that tail with
+            # them, in capacity-doubling buffers; O(tail + new), not O(dictionary)
             if srt.size < n:  # grow the buffers (doubling): amortised O(1) per appended value
                 cap = max(n, 2 * srt.size, 1024)
                 srt2 = np.empty(cap, dtype=srt.dtype)
@@ -350,11 +356,19 @@ class Column:
                 i2 = np.empty(cap, dtype=np.int64)
                 i2[:m] = ids[:m]
                 srt, old_r, ids = srt2, r2, i2
-            srt[m:n] = new_sorted
-            old_r[m + norder] = np.arange(m + 1, n + 1)
-            ids[m:n] = m + norder
+            tail_ids = ids[pos0:m].copy()
+            if pos0 == m:
+                srt[m:n] = new_sorted
+                ids[m:n] = m + norder
+            else:
+                vals = np.concatenate([srt[pos0:m], new_sorted])
+                who = np.concatenate([tail_ids, m + norder])
+                o = np.argsort(vals, kind="stable")
+                srt[pos0:n] = vals[o]
+                ids[pos0:n] = who[o]
+            old_r[ids[pos0:n]] = np.arange(pos0 + 1, n + 1)
             self._str_sorted = (srt, n, old_r, ids)
-            self._rank_lo = m  # every old id keeps its rank
+            self._rank_lo = int(min(int(tail_ids.min()), m)) if tail_ids.size else m
             return old_r[:n]
         srt = srt[:m]
         old_r = old_r[:m]
