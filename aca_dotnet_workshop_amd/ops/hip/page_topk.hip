@@ -222,30 +222,15 @@ tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   }
 }
 
-// ONE workgroup: bitonic sort of the candidates in LDS, then the page [offset, k) of the order.
-// info = [candidates, complete, written, 0]; out_rows = the page's rows.
+// Bitonic network over keys/rows[0, p) in LDS (p a power of two, the pad is ~0).  Each wave owns
+// a contiguous chunk of C = p / 16 elements (the whole array in wave 0 when p < 32): every pass
+// whose stride is below C only pairs elements inside one chunk, so it runs under a wave barrier;
+// only the strides >= C (cross-chunk, ~10 passes at p = 4096) need the workgroup barrier --
+// instead of one per pass (78).  Entered and left with the workgroup synchronised.
 // (A register-resident variant -- E elements per thread, cross-lane exchanges by ds_bpermute
-// inside a wave, LDS only for cross-wave strides -- measured 56 us against this version's 39 us
-// at 2,600 candidates: the bpermute chains are latency bound with 16 waves on one CU.)
-extern "C" __global__ void __launch_bounds__(kTopkBlock)
-tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__ cand_rows,
-             uint32_t* __restrict__ counter, uint32_t cap, int32_t k, int32_t offset, uint64_t bound,
-             int32_t* __restrict__ info, int32_t* __restrict__ out_rows) {
-  __shared__ uint64_t keys[kPageCap];
-  __shared__ int32_t rows[kPageCap];
-  const uint32_t total = *counter;
-  const int n = (int)(total < cap ? total : cap);
-  int p = 1;
-  while (p < n) p <<= 1;
-  for (int i = threadIdx.x; i < p; i += kTopkBlock) {
-    keys[i] = i < n ? cand_keys[i] : ~0ull;
-    rows[i] = i < n ? cand_rows[i] : -1;
-  }
-  __syncthreads();
-  // Bitonic network over p elements.  Each wave owns a contiguous chunk of C = p / 16 elements
-  // (the whole array in wave 0 when p < 32): every pass whose stride is below C only pairs
-  // elements inside one chunk, so it runs under a wave barrier; only the strides >= C (cross-
-  // chunk, ~10 passes at p = 4096) need the workgroup barrier -- instead of one per pass (78).
+// inside a wave, LDS only for cross-wave strides -- measured 56 us against this network's 39 us
+// for 4,096 elements: the bpermute chains are latency bound with 16 waves on one CU.)
+__device__ __forceinline__ void lds_bitonic(uint64_t* keys, int32_t* rows, int p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int chunk = p >= 32 ? p / (kTopkBlock / 64) : p;
   const bool owner = p >= 32 || wave == 0;
@@ -290,10 +275,162 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
     local_passes(size, stride);
   }
   __syncthreads();
+}
+
+// Inclusive prefix sum across the 64 lanes of a wave.
+__device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// ONE workgroup: the page [offset, k) of the candidates' key order.
+// info = [candidates, complete, written, 0]; out_rows = the page's rows.
+//
+// n <= k: a bitonic sort of all n (padded to a power of two).  n > k (a bound that let more
+// candidates through than the page holds -- 2,600 for a 1,000-row page at 1e8 rows): the k-th
+// smallest key is found first by a most-significant-digit radix select over the LDS copy
+// (8-bit digits, starting at the highest bit in which the candidates differ: 5-6 histogram
+// passes for clustered keys), then only the k keys at or below it are compacted and sorted --
+// a 1,024-element network instead of 4,096.  Keys are unique (the insertion sequence is their
+// low bits), so exactly k keys are at or below the k-th.
+extern "C" __global__ void __launch_bounds__(kTopkBlock)
+tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__ cand_rows,
+             uint32_t* __restrict__ counter, uint32_t cap, int32_t k, int32_t offset, uint64_t bound,
+             int32_t* __restrict__ info, int32_t* __restrict__ out_rows) {
+  __shared__ uint64_t keys[kPageCap];
+  __shared__ int32_t rows[kPageCap];
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_lo, s_hi, s_prefix;
+  __shared__ uint32_t s_need, s_count;
+  const uint32_t total = *counter;
+  const int n = (int)(total < cap ? total : cap);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int p = 1;
+  if (n <= k) {
+    while (p < n) p <<= 1;
+    for (int i = tid; i < p; i += kTopkBlock) {
+      keys[i] = i < n ? cand_keys[i] : ~0ull;
+      rows[i] = i < n ? cand_rows[i] : -1;
+    }
+    __syncthreads();
+  } else {
+    // the candidates' range: min and max key (wave reductions, then wave 0 over the waves)
+    uint64_t lo = ~0ull, hi = 0;
+    for (int i = tid; i < n; i += kTopkBlock) {
+      const uint64_t x = cand_keys[i];
+      keys[i] = x;
+      rows[i] = cand_rows[i];
+      lo = x < lo ? x : lo;
+      hi = x > hi ? x : hi;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const uint64_t ol = __shfl_xor(lo, d), oh = __shfl_xor(hi, d);
+      lo = ol < lo ? ol : lo;
+      hi = oh > hi ? oh : hi;
+    }
+    if (tid == 0) {
+      s_lo = ~0ull;
+      s_hi = 0;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      atomicMin(reinterpret_cast<unsigned long long*>(&s_lo), (unsigned long long)lo);
+      atomicMax(reinterpret_cast<unsigned long long*>(&s_hi), (unsigned long long)hi);
+    }
+    __syncthreads();
+    const uint64_t diff = s_lo ^ s_hi;
+    const int top = diff ? 63 - __clzll((long long)diff) : 0;  // highest bit in which keys differ
+    int shift = (top / 8) * 8;                                  // its 8-bit digit
+    if (tid == 0) {
+      s_prefix = shift + 8 >= 64 ? 0 : (s_lo >> (shift + 8)) << (shift + 8);  // the common high bits
+      s_need = (uint32_t)k;
+    }
+    __syncthreads();
+    for (; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += kTopkBlock) hist[i] = 0;
+      __syncthreads();
+      const uint64_t prefix = s_prefix;
+      const uint64_t above = shift + 8 >= 64 ? 0 : ~0ull << (shift + 8);
+      for (int i = tid; i < n; i += kTopkBlock) {
+        const uint64_t x = keys[i];
+        if ((x & above) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (wave == 0) {  // the digit holding the need-th key of the remaining range
+        uint32_t c[4];
+        uint32_t own = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c[j] = hist[lane * 4 + j];
+          own += c[j];
+        }
+        const uint32_t incl = wave_inclusive_sum(own);
+        const uint32_t need = s_need;
+        uint32_t before = incl - own;
+        if (before < need && need <= incl) {  // exactly one lane holds the digit
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (need <= before + c[j]) {
+              s_prefix = prefix | ((uint64_t)(lane * 4 + j) << shift);
+              s_need = need - before;
+              break;
+            }
+            before += c[j];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // keys <= the k-th key: exactly k of them, compacted to the front (read, barrier, write)
+    const uint64_t kth = s_prefix;
+    constexpr int kPer = kPageCap / kTopkBlock;  // candidates per thread (8), held in registers
+    uint64_t xk[kPer];
+    int32_t xr[kPer];
+    bool sel[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int i = tid + r * kTopkBlock;
+      sel[r] = false;
+      xk[r] = 0;
+      xr[r] = -1;
+      if (i < n) {
+        xk[r] = keys[i];
+        xr[r] = rows[i];
+        sel[r] = xk[r] <= kth;
+      }
+    }
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+    while (p < k) p <<= 1;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      if (sel[r]) {
+        const uint32_t slot = atomicAdd(&s_count, 1u);
+        if ((int)slot < p) {
+          keys[slot] = xk[r];
+          rows[slot] = xr[r];
+        }
+      }
+    }
+    __syncthreads();
+    const int got = (int)(s_count < (uint32_t)p ? s_count : (uint32_t)p);
+    for (int i = got + tid; i < p; i += kTopkBlock) {
+      keys[i] = ~0ull;
+      rows[i] = -1;
+    }
+    __syncthreads();
+  }
+  lds_bitonic(keys, rows, p);
   const int upto = n < k ? n : k;
   const int written = upto > offset ? upto - offset : 0;
-  for (int i = threadIdx.x; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];
-  if (threadIdx.x == 0) {
+  for (int i = tid; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];
+  if (tid == 0) {
     int complete;
     if (total > cap) complete = 0;                     // overflow: the host takes fewer tiles
     else if (n >= k) complete = 1;                     // k candidates, all before every unread row

@@ -983,15 +983,22 @@ def test_gpu_page_path_matches_host(sort):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 700, 1023, 1024, 1025, 2583, 4096, 4097, 8191, 8192])
-def test_gpu_page_topk_sorts_every_candidate_count(n):
-    """tt_page_topk (register / cross-lane / LDS bitonic network over E = 1, 2, 4, 8 elements
-    per thread) returns the [offset, k) slice of the key order for every candidate count up to
-    the LDS capacity, with the completeness flag the host relies on."""
+@pytest.mark.parametrize("n,wide", [(0, False), (1, False), (63, False), (64, False), (65, False), (700, False),
+                                    (1023, False), (1024, False), (1025, False), (2583, False), (2583, True),
+                                    (4096, False), (4097, True), (8191, False), (8192, True)])
+def test_gpu_page_topk_sorts_every_candidate_count(n, wide):
+    """tt_page_topk (bitonic sort of all candidates, or -- more candidates than the page --
+    a radix select of the k-th key, compaction of the k smallest and a sort of those) returns the
+    [offset, k) slice of the key order for every candidate count up to the LDS capacity, for
+    clustered and full-width 63-bit keys, with the completeness flag the host relies on."""
     import torch
     k = _kernels()
     rng = np.random.default_rng(n)
-    keys = (rng.integers(0, 1 << 40, n, dtype=np.int64) << 20) | np.arange(n, dtype=np.int64)  # unique
+    if wide:  # keys over the whole 63-bit range
+        keys = np.unique(rng.integers(0, np.iinfo(np.int64).max, n + 64, dtype=np.int64))[:n]
+        rng.shuffle(keys)
+    else:  # clustered: a narrow band, like one tile's packed keys
+        keys = (rng.integers(0, 1 << 40, n, dtype=np.int64) << 20) | np.arange(n, dtype=np.int64)
     rows = rng.permutation(n).astype(np.int32)
     dk, dr = torch.from_numpy(keys).to(k.device), torch.from_numpy(rows).to(k.device)
     order = rows[np.argsort(keys.astype(np.uint64), kind="stable")]
