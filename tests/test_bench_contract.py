@@ -84,6 +84,28 @@ def test_bench_shared_env_two_ranks():
     assert dlv["dead_lettered"] == 0
 
 
+def test_bench_shared_env_frontend_two_ranks():
+    """--shared-env at the frontend entry: each rank's platform controller starts its backing,
+    the ranks exchange the shard URLs (EnvironmentController.shard_exchange over gloo), and the
+    manifest-deployed apps of both ranks run against the partitioned store and broker, with the
+    overdue sweep on; every task is delivered and completed exactly once."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "32", "--shared-env", "--overdue-sweep-ms", "300"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check(lines[0], 2, 2, 1)
+    cfg = lines[0]["config"]
+    assert cfg["entry"] == "frontend" and cfg["mtls"] is True
+    assert cfg["parallelism"].startswith("shared-env x2 (store and broker partitioned over 2 shards")
+    dlv = cfg["delivery"]
+    assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] >= 2 * 32 * 3, dlv
+    assert cfg["overdue_sweeps"]["shards"] == 2 and cfg["overdue_sweeps"]["errors"] == 0
+
+
 def test_bench_latency_runs():
     """bench_latency.py (SURVEY §7.5's own latency benchmarks): 2-hop CRUD and publish->ack lines."""
     env = dict(os.environ, PYTHONPATH=str(ROOT))
