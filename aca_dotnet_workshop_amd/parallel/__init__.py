@@ -141,6 +141,16 @@ def partition_cpus(allowed: set[int], nodes: list[set[int]], core: dict[int, int
 PIN_INFO: dict[str, str] = {}  # how the last pin_rank chose its CPUs (for the bench report)
 
 
+def one_thread_per_core(cpus: set[int], core: dict[int, int]) -> set[int]:
+    """The first hardware thread of every physical core in ``cpus`` (``core``: CPU -> its
+    core's first sibling, ``host_topology``); a core whose first sibling is outside ``cpus``
+    keeps its lowest CPU in the set."""
+    by_core: dict[int, int] = {}
+    for c in sorted(cpus):
+        by_core.setdefault(core.get(c, c), c)
+    return set(by_core.values())
+
+
 def gpu_numa_nodes(sysfs: str = "/sys/class/drm") -> list[int]:
     """NUMA node of every AMD GPU, in PCI address order -- the order HIP numbers the devices (a
     rank with ``HIP_VISIBLE_DEVICES=<local rank>`` drives the ``<local rank>``-th).  -1 where
@@ -186,8 +196,9 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     the NUMA node of its own GPU when sysfs names one (``gpu_numa_nodes``), shared with the
     other ranks whose GPUs sit on that node (whole cores each); without that, ranks split the
     nodes (``partition_cpus``) and a single rank takes its first node.  ``<n>`` > 1 (single
-    rank): only n CPUs of that node.  On the MI355X box one stack on one socket ran +24 % vs
-    unpinned (profiles/r2_rank_pinning.md)."""
+    rank): only n CPUs of that node; ``phys``: the same set, one hardware thread per physical
+    core.  On the MI355X box one stack on one socket ran +24 % vs unpinned
+    (profiles/r2_rank_pinning.md)."""
     spec = os.environ.get("TT_BENCH_PIN", "1") if spec is None else spec
     PIN_INFO.clear()
     if spec == "0":
@@ -213,11 +224,19 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     if cpus is None and local_world > 1:
         cpus = partition_cpus(allowed, nodes, core, local_rank, local_world)
         PIN_INFO["mode"] = "NUMA-local whole cores (rank order)"
-    elif cpus is None and (spec in ("1", "node") or spec.isdigit() and int(spec) > 1):
+    elif cpus is None and (spec in ("1", "node", "phys") or spec.isdigit() and int(spec) > 1):
         first = next((n & allowed for n in nodes if n & allowed), allowed)
         order = sorted(first, key=lambda c: (core.get(c, c), c))
-        cpus = set(order if spec in ("1", "node") else order[:int(spec)])
+        cpus = set(order if spec in ("1", "node", "phys") else order[:int(spec)])
         PIN_INFO["mode"] = "first NUMA node, whole cores"
+    if cpus and spec == "phys":
+        # one hardware thread per physical core: under a CPU quota smaller than the set, busy
+        # threads never share a core with a sibling (SMT halves each one's speed while both
+        # still draw on the quota)
+        primary = one_thread_per_core(cpus, core)
+        if len(primary) >= 2:
+            cpus = primary
+            PIN_INFO["mode"] = PIN_INFO.get("mode", "first NUMA node") + ", one thread per core"
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus

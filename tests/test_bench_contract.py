@@ -152,6 +152,13 @@ def test_partition_cpus_numa_and_smt():
     assert set(cr) == set(os.sched_getaffinity(0))
 
 
+def test_one_thread_per_core():
+    from aca_dotnet_workshop_amd.parallel import one_thread_per_core
+    core = {c: c % 128 for c in range(256)}  # Linux numbering: cpu c and c + 128 share a core
+    assert one_thread_per_core(set(range(0, 64)) | set(range(128, 192)), core) == set(range(64))
+    assert one_thread_per_core({130, 131, 3}, core) == {130, 3}  # core 2 via its second thread
+
+
 def test_rank_device_env():
     import importlib.util
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
