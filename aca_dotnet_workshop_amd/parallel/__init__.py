@@ -20,8 +20,8 @@ from __future__ import annotations
 import os
 import sys
 
-__all__ = ["Dist", "cpu_budget", "topology", "cgroup_throttling", "partition_cpus", "pin_rank", "gpu_numa_nodes",
-           "PIN_INFO"]
+__all__ = ["Dist", "cpu_budget", "cpu_quota", "one_thread_per_core", "topology", "cgroup_throttling",
+           "partition_cpus", "pin_rank", "gpu_numa_nodes", "PIN_INFO"]
 
 
 class Dist:
@@ -197,8 +197,10 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     other ranks whose GPUs sit on that node (whole cores each); without that, ranks split the
     nodes (``partition_cpus``) and a single rank takes its first node.  ``<n>`` > 1 (single
     rank): only n CPUs of that node; ``phys``: the same set, one hardware thread per physical
-    core.  On the MI355X box one stack on one socket ran +24 % vs unpinned
-    (profiles/r2_rank_pinning.md)."""
+    core -- the default (``1``/``auto``) when the CPU quota's share of this rank is no more
+    than the set's physical cores.  On the MI355X box one stack on one socket ran +24 % vs
+    unpinned (profiles/r2_rank_pinning.md), one thread per core of that socket another +6 %
+    (16-CPU quota, 64 cores: profiles/r3_cpu_envelope.md)."""
     spec = os.environ.get("TT_BENCH_PIN", "1") if spec is None else spec
     PIN_INFO.clear()
     if spec == "0":
@@ -224,11 +226,17 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     if cpus is None and local_world > 1:
         cpus = partition_cpus(allowed, nodes, core, local_rank, local_world)
         PIN_INFO["mode"] = "NUMA-local whole cores (rank order)"
-    elif cpus is None and (spec in ("1", "node", "phys") or spec.isdigit() and int(spec) > 1):
+    elif cpus is None and (spec in ("1", "auto", "node", "phys") or spec.isdigit() and int(spec) > 1):
         first = next((n & allowed for n in nodes if n & allowed), allowed)
         order = sorted(first, key=lambda c: (core.get(c, c), c))
-        cpus = set(order if spec in ("1", "node", "phys") else order[:int(spec)])
+        cpus = set(order if spec in ("1", "auto", "node", "phys") else order[:int(spec)])
         PIN_INFO["mode"] = "first NUMA node, whole cores"
+    if cpus and spec in ("1", "auto"):
+        # default: one thread per core when the job's CPU quota (this rank's share) does not
+        # even cover the set's physical cores -- siblings would only split the quota's time
+        q = cpu_quota()
+        if q is not None and q / max(1, local_world) <= len(one_thread_per_core(cpus, core)):
+            spec = "phys"
     if cpus and spec == "phys":
         # one hardware thread per physical core: under a CPU quota smaller than the set, busy
         # threads never share a core with a sibling (SMT halves each one's speed while both
@@ -242,23 +250,26 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     return cpus
 
 
-def cpu_budget() -> float:
-    """CPUs this process may use: cgroup v2/v1 quota, else the affinity mask (a GPU box's
-    ``nproc`` shows the whole machine while the job gets a share of it)."""
-    n = float(len(os.sched_getaffinity(0)))
+def cpu_quota() -> float | None:
+    """The cgroup (v2, else v1) CPU quota in CPUs, None when unlimited or unreadable."""
     try:
         quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if quota != "max":
-            n = min(n, int(quota) / int(period))
+        return None if quota == "max" else int(quota) / int(period)
     except (OSError, ValueError):
         try:
             q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
             p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
-            if q > 0:
-                n = min(n, q / p)
+            return q / p if q > 0 else None
         except (OSError, ValueError):
-            pass
-    return n
+            return None
+
+
+def cpu_budget() -> float:
+    """CPUs this process may use: cgroup v2/v1 quota, else the affinity mask (a GPU box's
+    ``nproc`` shows the whole machine while the job gets a share of it)."""
+    n = float(len(os.sched_getaffinity(0)))
+    q = cpu_quota()
+    return min(n, q) if q is not None else n
 
 
 def topology(cores: float) -> tuple[int, int]:

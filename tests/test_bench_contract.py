@@ -55,9 +55,15 @@ def test_bench_two_ranks_torchrun():
     assert [x for x in r.stdout.splitlines() if x.strip() and not x.startswith("{")] == [], r.stdout
     _check(lines[0], 2, 2, 1)
     # each rank pinned to its own partition of the host (the stack inherits the mask)
-    from aca_dotnet_workshop_amd.parallel import host_topology, partition_cpus
-    part = partition_cpus(set(os.sched_getaffinity(0)), *host_topology(), 0, 2)
+    from aca_dotnet_workshop_amd.parallel import cpu_quota, host_topology, one_thread_per_core, partition_cpus
+    nodes, core = host_topology()
+    part = partition_cpus(set(os.sched_getaffinity(0)), nodes, core, 0, 2)
     want = f"{len(part)} CPUs per rank (NUMA-local whole cores (rank order))" if part else "none"
+    q = cpu_quota()
+    if part and q is not None and q / 2 <= len(one_thread_per_core(part, core)):  # quota below the cores
+        phys = one_thread_per_core(part, core)
+        if len(phys) >= 2:
+            want = f"{len(phys)} CPUs per rank (NUMA-local whole cores (rank order), one thread per core)"
     assert lines[0]["config"]["cpu_pinning"] == want
 
 
