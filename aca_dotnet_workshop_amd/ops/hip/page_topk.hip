@@ -29,8 +29,7 @@ namespace {
 
 constexpr int kPageCap = 8192;       // candidate pairs one workgroup sorts in LDS (96 KiB)
 constexpr int kTopkBlock = 1024;
-constexpr int kGatherSplit = 4;      // workgroups per candidate tile (a page often reads one tile)
-constexpr int kGatherBlock = kTileRows / kRowsPerLane / kGatherSplit;  // 128 lanes x 16 rows
+constexpr int kGatherBlock = kTileRows / kRowsPerLane;  // 512 lanes x 16 rows = one tile
 constexpr int kZoneBlock = 256;      // 32 rows per lane
 constexpr int kMaxSortKeys = 4;
 
@@ -153,9 +152,8 @@ tt_zone_argmin(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
   }
 }
 
-// kGatherSplit workgroups per candidate tile, each evaluating the filter on a quarter of the
-// tile's 8192 rows (16 per lane) and appending (key, row) of every live match -- a page that
-// needs one tile runs on four CUs instead of one.  Pairs beyond `cap` are counted, not written.
+// One workgroup per candidate tile: evaluate the filter on the tile's 8192 rows (16 per lane),
+// append (key, row) of every live match.  Pairs beyond `cap` are counted, not written.
 extern "C" __global__ void __launch_bounds__(kGatherBlock)
 tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_t* __restrict__ live,
                const int32_t* __restrict__ prog, int32_t prog_len, const uint32_t* __restrict__ bitmaps,
@@ -178,9 +176,8 @@ tt_page_gather(const ColumnDesc* __restrict__ cols, int64_t nrows, const uint16_
     s_specs[threadIdx.x] = s;
   }
   __syncthreads();
-  const int64_t tile = tiles[blockIdx.x / kGatherSplit];
-  const int64_t part = blockIdx.x % kGatherSplit;
-  const int64_t row0[1] = {tile * kTileRows + (part * kGatherBlock + (int64_t)threadIdx.x) * kRowsPerLane};
+  const int64_t tile = tiles[blockIdx.x];
+  const int64_t row0[1] = {tile * kTileRows + (int64_t)threadIdx.x * kRowsPerLane};
   uint32_t m[1];
   if (in_lds) run_program<1>(cols, prog, prog_len, (const uint32_t*)lds_bitmaps, row0, m);
   else run_program<1>(cols, prog, prog_len, bitmaps, row0, m);
@@ -491,7 +488,7 @@ extern "C" int tt_launch_page(const void* cols, int64_t nrows, const uint16_t* l
   if (k <= 0 || k > kPageCap || offset < 0 || offset > k) return -1;
   if (ntiles > 0) {
     const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
-    hipLaunchKernelGGL(tt_page_gather, dim3((unsigned)ntiles * kGatherSplit), dim3(kGatherBlock), lds, stream,
+    hipLaunchKernelGGL(tt_page_gather, dim3((unsigned)ntiles), dim3(kGatherBlock), lds, stream,
                        reinterpret_cast<const ColumnDesc*>(cols), nrows, live, prog, prog_len, bitmaps, bitmap_words,
                        reinterpret_cast<const SortSpec*>(specs), nkeys, ranks, seq, seq_bits, tiles, bound, cand_keys,
                        cand_rows, counter, (uint32_t)kPageCap);
