@@ -34,7 +34,9 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_sort_pairs_temp_bytes.restype = ctypes.c_int64
     lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P]
     lib.tt_sort_pairs.restype = ctypes.c_int
-    lib.tt_launch_scan_compact.argtypes = [P, P, P, I64, P, P, P, P]
+    lib.tt_launch_scan_compact.argtypes = [P, P, P, I64, P, I64, P, P, P]
+    lib.tt_launch_compact.argtypes = [P, P, I64, P, I64, P]
+    lib.tt_launch_compact.restype = ctypes.c_int
     lib.tt_launch_scan_compact.restype = ctypes.c_int
     lib.tt_launch_group_count.argtypes = [P, I32, P, I64, I32, P, P]
     lib.tt_launch_group_count.restype = ctypes.c_int
@@ -88,6 +90,7 @@ class GpuKernels:
         # select at a time
         self._total_lock = threading.Lock()
         self._bufs: dict[str, Any] = {}
+        self._est: dict[int, int] = {}  # last selection count per device program: output sizing
         self.page_cap = int(self.lib.tt_page_cap())
         # Result ordering sorts (key, row) pairs over the packed key's used bits only
         # (hip/radix_pairs.hip); False = torch.sort argsort + gather, for A/B runs.
@@ -133,20 +136,34 @@ class GpuKernels:
                 raise RuntimeError(f"tt_scan_eval launch failed ({rc})")
             # the tiles' output offsets in one block (tt_tile_offsets, which also writes the total
             # straight into pinned host memory), then the wave-independent compaction: no torch
-            # launches, no host sync between the kernels -- one event wait at the end.  The ids
-            # land in a cached buffer; the caller gets its own copy of the selected prefix.
-            out = self._buf("out", max(nrows, 1), torch.int32)
+            # launches, no host sync between the kernels -- one event wait at the end.  The ids go
+            # into a fresh buffer the caller owns, sized from the previous count of this program
+            # (+12.5 %); when the selection grew past it, the compaction alone runs again into an
+            # exact one (no full-collection buffer held by a result, no copy of the ids).
+            key = prog.data_ptr()
+            est = self._est.get(key)
+            cap = nrows if est is None else min(nrows, est + est // 8 + 4096)
+            out = torch.empty(max(cap, 1), dtype=torch.int32, device=self.device)
             # [0] = total (int64), byte 16 on: int32 tile offsets
             scratch = self._buf("scratch", tiles // 2 + 3, torch.int64)
             pinned = self._pinned()
             rc = self.lib.tt_launch_scan_compact(mask.data_ptr(), counts.data_ptr(), scratch.data_ptr() + 16, nrows,
-                                                 out.data_ptr(), scratch.data_ptr(), pinned.data_ptr(), stream)
+                                                 out.data_ptr(), cap, scratch.data_ptr(), pinned.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
             self._total_event.record(torch.cuda.current_stream(self.device))
             self._total_event.synchronize()
             total = int(pinned[0])
-            out = out[:total].clone()  # a selection-sized result; the scratch stays for the next query
+            if total > cap:
+                out = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
+                rc = self.lib.tt_launch_compact(mask.data_ptr(), scratch.data_ptr() + 16, nrows, out.data_ptr(),
+                                                total, stream)
+                if rc != 0:
+                    raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
+            if len(self._est) > 256:
+                self._est.clear()
+            self._est[key] = total
+            out = out[:total]
         return (out, mask) if return_mask else out
 
     def _buf(self, name: str, n: int, dtype):

@@ -158,7 +158,7 @@ tt_tile_offsets(const int32_t* __restrict__ block_counts, int64_t tiles, int32_t
 
 __global__ void __launch_bounds__(kBlock)
 tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict__ tile_off,
-                  int32_t* __restrict__ out) {
+                  int32_t* __restrict__ out, int64_t cap) {
   __shared__ uint16_t staged[kBlock / 64][64 * 32];  // one slice per wave: row - wave_base (11 bits)
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t tile = blockIdx.x;
@@ -190,6 +190,7 @@ tt_scan_compact_w(const uint32_t* __restrict__ mask32, const int32_t* __restrict
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int64_t a = (int64_t)tbase + before;
+  if (a + count > cap) return;  // the output was sized from an estimate: the host re-runs this
   int32_t* dst = out + a;
   int head = (int)((4 - (a & 3)) & 3);
   if (head > count) head = count;
@@ -348,15 +349,27 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
 // holds up to nrows ids; the selected count lands in `total` (device) and `total_host` (pinned
 // host memory, optional).  Non-temporal id stores: measured on MI355X (1e8 rows, 31.5M
 // selected) 0.1215 -> 0.111 ms per query -- the ids stream past L2, the next scan keeps its cache.
+// `out` holds `cap` ids: a wave whose segment would end past it writes nothing (the host sized
+// `out` from the previous selection's count, sees the total and re-runs the compaction alone
+// into an exact buffer when it did not fit: tt_launch_compact).
 extern "C" int tt_launch_scan_compact(const uint16_t* mask, const int32_t* block_counts, int32_t* tile_off,
-                                      int64_t nrows, int32_t* out, int64_t* total, int64_t* total_host,
+                                      int64_t nrows, int32_t* out, int64_t cap, int64_t* total, int64_t* total_host,
                                       hipStream_t stream) {
   const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
   if (tiles == 0) return 0;
   hipLaunchKernelGGL(tt_tile_offsets, dim3(1), dim3(kOffBlock), 0, stream, block_counts, tiles, tile_off, total,
                      total_host);
   hipLaunchKernelGGL(tt_scan_compact_w, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
-                     reinterpret_cast<const uint32_t*>(mask), tile_off, out);
+                     reinterpret_cast<const uint32_t*>(mask), tile_off, out, cap);
+  return (int)hipGetLastError();
+}
+
+extern "C" int tt_launch_compact(const uint16_t* mask, const int32_t* tile_off, int64_t nrows, int32_t* out,
+                                 int64_t cap, hipStream_t stream) {
+  const int64_t tiles = (nrows + kTileRows - 1) / kTileRows;
+  if (tiles == 0) return 0;
+  hipLaunchKernelGGL(tt_scan_compact_w, dim3((unsigned)tiles), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const uint32_t*>(mask), tile_off, out, cap);
   return (int)hipGetLastError();
 }
 extern "C" int tt_launch_group_count(const void* cols, int32_t g, const uint16_t* mask, int64_t nrows, int32_t ngroups,

@@ -1012,6 +1012,23 @@ def test_gpu_page_topk_sorts_every_candidate_count(n, wide):
 
 
 @pytest.mark.gpu
+def test_gpu_select_grows_past_its_estimated_output():
+    """tt_scan_compact sizes its output from the previous count of the same program; a
+    selection that outgrew that estimate is compacted again into an exact buffer."""
+    k = _kernels()
+    ix = ColumnarIndex(["v"])
+    for i in range(60_000):
+        ix.upsert(str(i), {"v": 1 if i < 100 else 0})
+    prog = ix.compile({"EQ": {"v": 1}})
+    assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))  # 100 rows: the estimate
+    assert np.array_equal(ix.select_gpu(prog, k), ix.select_numpy(prog))  # sized from it
+    for i in range(100, 40_000):
+        ix.upsert(str(i), {"v": 1})
+    got, want = ix.select_gpu(prog, k), ix.select_numpy(prog)
+    assert got.size == want.size == 40_000 and np.array_equal(got, want)
+
+
+@pytest.mark.gpu
 def test_gpu_zone_argmin_matches_numpy():
     k = _kernels()
     rnd = random.Random(8)
