@@ -292,10 +292,23 @@ def test_gpu_compaction_offsets_over_many_chunks(tiles):
     out = torch.empty(nrows, dtype=torch.int32, device=k.device)
     total = torch.empty(1, dtype=torch.int64, device=k.device)
     pinned = torch.zeros(1, dtype=torch.int64, pin_memory=True)
-    assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
-                                        out.data_ptr(), total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
-    torch.cuda.synchronize()
     want = torch.nonzero(bits.view(-1)).view(-1).to(torch.int32)
+    # an output sized from a too-small estimate: the waves past it write nothing, the total is
+    # exact, and the compaction alone re-runs into a buffer of that size
+    small = max(1, want.numel() // 2)
+    sentinel = torch.full((small + 64,), -7, dtype=torch.int32, device=k.device)
+    assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
+                                        sentinel.data_ptr(), small, total.data_ptr(), pinned.data_ptr(),
+                                        k._stream()) == 0
+    torch.cuda.synchronize()
+    assert int(total.item()) == want.numel() and bool((sentinel[small:] == -7).all())
+    assert k.lib.tt_launch_compact(mask.data_ptr(), scratch.data_ptr(), nrows, out.data_ptr(), want.numel(),
+                                   k._stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out[:want.numel()].cpu(), want)
+    assert k.lib.tt_launch_scan_compact(mask.data_ptr(), counts_d.data_ptr(), scratch.data_ptr(), nrows,
+                                        out.data_ptr(), nrows, total.data_ptr(), pinned.data_ptr(), k._stream()) == 0
+    torch.cuda.synchronize()
     n = int(total.item())
     assert n == want.numel() == int(pinned[0])
     assert torch.equal(out[:n].cpu(), want)
