@@ -361,6 +361,7 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
         counts_url = f"{backing}/servicebus/taskstracker/counts?entity={entity}"
         if shared:
             counts_url = [f"{u}/servicebus/taskstracker/counts?entity={entity}" for u in bus_shards]
+        if a.client == "native":
             from aca_dotnet_workshop_amd.native.build import build_loadgen
             exe = str(build_loadgen())
             bodies_file = str(stack.root / "bodies.jsonl")

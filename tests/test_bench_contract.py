@@ -42,6 +42,18 @@ def test_bench_single_process():
     _check(lines[0], 1, 2, 1)
 
 
+def test_bench_api_sidecar_entry_single_process():
+    """--entry api-sidecar (round 2's topology, kept as a secondary mode) on one rank."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT))
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32", "--entry",
+                        "api-sidecar", "--api-replicas", "1", "--processor-replicas", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["config"]["entry"] == "api-sidecar"
+    _check(lines[0], 1, 2, 1)
+
+
 def test_bench_two_ranks_torchrun():
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
