@@ -83,18 +83,28 @@ def decode_token(token: str | None, n: int) -> list[int | None]:
         raise BackingError(400, b"invalid continuation token for a partitioned collection", "state query") from None
 
 
-def _sort_cmp(sort: list[dict[str, Any]]):
-    from ..ops.columnar import _MISSING, compare, get_path
-    specs = [(s["key"], -1 if str(s.get("order", "ASC")).upper() == "DESC" else 1) for s in sort or []
-             if isinstance(s, dict) and "key" in s]
+def _sort_specs(sort: list[dict[str, Any]]) -> list[tuple[str, int]]:
+    return [(s["key"], -1 if str(s.get("order", "ASC")).upper() == "DESC" else 1) for s in sort or []
+            if isinstance(s, dict) and "key" in s]
 
-    def value(r: dict, key: str):
+
+def _sort_values(r: dict, specs: list[tuple[str, int]]) -> tuple:
+    """The result's sort-key values, extracted once (a missing path sorts like null, the
+    store's order)."""
+    from ..ops.columnar import _MISSING, get_path
+    out = []
+    for key, _ in specs:
         v = get_path(r.get("data"), key)
-        return None if v is _MISSING else v  # a missing path sorts like null (the store's order)
+        out.append(None if v is _MISSING else v)
+    return tuple(out)
 
-    def cmp(a: tuple, b: tuple) -> int:
-        for key, sign in specs:
-            c = compare(value(a[0], key), value(b[0], key))
+
+def _sort_cmp(specs: list[tuple[str, int]]):
+    from ..ops.columnar import compare
+
+    def cmp(a: tuple, b: tuple) -> int:  # (values, shard, result)
+        for (_, sign), x, y in zip(specs, a[0], b[0]):
+            c = compare(x, y)
             if c:
                 return c * sign
         return (a[1] > b[1]) - (a[1] < b[1])  # ties: shard order
@@ -106,12 +116,14 @@ def merge_pages(query: dict[str, Any], pages: list[tuple[int, dict[str, Any]] | 
     """Merge every shard's sorted page: ``pages[i]`` is (shard, response) for the shards still
     holding matches (None for exhausted ones), ``offsets`` their positions before this page."""
     limit = int((query.get("page") or {}).get("limit") or 0)
-    key = functools.cmp_to_key(_sort_cmp(query.get("sort") or []))
-    streams = [[(r, i) for r in resp.get("results") or []] for i, resp in pages if resp is not None]
-    merged = heapq.merge(*streams, key=key)
+    specs = _sort_specs(query.get("sort") or [])
+    key = functools.cmp_to_key(_sort_cmp(specs))
+    streams = [[(_sort_values(r, specs) if specs else (), i, r) for r in resp.get("results") or []]
+               for i, resp in pages if resp is not None]
+    merged = heapq.merge(*streams, key=key) if specs else itertools.chain(*streams)
     take = list(itertools.islice(merged, limit)) if limit else list(merged)
     used = [0] * len(offsets)
-    for _, i in take:
+    for _, i, _ in take:
         used[i] += 1
     new: list[int | None] = []
     for i, off in enumerate(offsets):
@@ -121,7 +133,7 @@ def merge_pages(query: dict[str, Any], pages: list[tuple[int, dict[str, Any]] | 
             continue
         n_i = len(resp.get("results") or [])
         new.append(None if (not resp.get("token") and used[i] == n_i) else off + used[i])
-    out: dict[str, Any] = {"results": [r for r, _ in take]}
+    out: dict[str, Any] = {"results": [r for _, _, r in take]}
     tok = encode_token(new) if limit else None
     if tok:
         out["token"] = tok
