@@ -88,14 +88,13 @@ def _sort_specs(sort: list[dict[str, Any]]) -> list[tuple[str, int]]:
             if isinstance(s, dict) and "key" in s]
 
 
-def _sort_values(r: dict, specs: list[tuple[str, int]]) -> tuple:
+def _sort_values(r: dict, specs: list[tuple[str, int]], get_path, missing) -> tuple:
     """The result's sort-key values, extracted once (a missing path sorts like null, the
     store's order)."""
-    from ..ops.columnar import _MISSING, get_path
     out = []
     for key, _ in specs:
         v = get_path(r.get("data"), key)
-        out.append(None if v is _MISSING else v)
+        out.append(None if v is missing else v)
     return tuple(out)
 
 
@@ -111,16 +110,37 @@ def _sort_cmp(specs: list[tuple[str, int]]):
     return cmp
 
 
+def _plain_order(streams: list[list[tuple]], nkeys: int) -> bool:
+    """Every sort column holds one plain type across the merged results (all strings, or all
+    non-boolean numbers): Python's own tuple order is then the store's order."""
+    for k in range(nkeys):
+        kinds = set()
+        for st in streams:
+            for vals, _, _ in st:
+                v = vals[k]
+                kinds.add("s" if type(v) is str else "n" if type(v) in (int, float) else "x")
+                if len(kinds) > 1 or "x" in kinds:
+                    return False
+    return True
+
+
 def merge_pages(query: dict[str, Any], pages: list[tuple[int, dict[str, Any]] | None],
                 offsets: list[int | None]) -> dict[str, Any]:
     """Merge every shard's sorted page: ``pages[i]`` is (shard, response) for the shards still
     holding matches (None for exhausted ones), ``offsets`` their positions before this page."""
+    from ..ops.columnar import _MISSING, get_path
     limit = int((query.get("page") or {}).get("limit") or 0)
     specs = _sort_specs(query.get("sort") or [])
-    key = functools.cmp_to_key(_sort_cmp(specs))
-    streams = [[(_sort_values(r, specs) if specs else (), i, r) for r in resp.get("results") or []]
+    streams = [[(_sort_values(r, specs, get_path, _MISSING) if specs else (), i, r) for r in resp.get("results") or []]
                for i, resp in pages if resp is not None]
-    merged = heapq.merge(*streams, key=key) if specs else itertools.chain(*streams)
+    if not specs:
+        merged = itertools.chain(*streams)
+    elif len({sign for _, sign in specs}) == 1 and _plain_order(streams, len(specs)):
+        # one direction over plain values (the overdue sweep's taskCreatedOn strings): the
+        # values themselves are the merge key; equal keys keep shard order
+        merged = heapq.merge(*streams, key=lambda t: t[0], reverse=specs[0][1] < 0)
+    else:
+        merged = heapq.merge(*streams, key=functools.cmp_to_key(_sort_cmp(specs)))
     take = list(itertools.islice(merged, limit)) if limit else list(merged)
     used = [0] * len(offsets)
     for _, i, _ in take:
