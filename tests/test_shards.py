@@ -211,9 +211,18 @@ def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
                     assert await sh.shards[1 - shard_of(k, 2)].doc_get(ACCT, DB, COLL, k) is None
                 r = await http.request("GET", base + "?createdBy=route@x")
                 assert r.status == 200 and sorted(t["taskId"] for t in json.loads(r.body)) == sorted(ids)
-                per = [(await c.sb_counts("taskstracker", "tasksavedtopic/subscriptions/tasksmanager-backend-processor"))
-                       ["enqueued"] for c in sh.shards]
+                ent = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
+                per = [(await c.sb_counts("taskstracker", ent))["enqueued"] for c in sh.shards]
                 assert sum(per) >= 40 and min(per) > 0, per
+                # the Service Bus partitionKey metadata pins messages to one shard
+                pub = f"unix:{api.sidecar_uds}:/v1.0/publish/dapr-pubsub-servicebus/tasksavedtopic"
+                for i in range(12):
+                    r = await http.request("POST", pub + "?metadata.partitionKey=tenant-7", body=b'{"n": 1}',
+                                           headers=[("Content-Type", "application/json")])
+                    assert r.status == 204, r.body
+                after = [(await c.sb_counts("taskstracker", ent))["enqueued"] for c in sh.shards]
+                home = shard_of("tenant-7", 2)
+                assert after[home] - per[home] == 12 and after[1 - home] == per[1 - home], (per, after)
             finally:
                 await sh.close()
                 await http.close()
