@@ -52,7 +52,7 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_rank_encode.restype = ctypes.c_int
     lib.tt_page_cap.restype = ctypes.c_int
     lib.tt_launch_page_reset.argtypes = [P, P]
-    lib.tt_launch_page_topk.argtypes = [P, P, P, I32, I32, ctypes.c_uint64, P, P, P]
+    lib.tt_launch_page_topk.argtypes = [P, P, P, I32, I32, ctypes.c_uint64, P, P, P, P]
     lib.tt_launch_page_topk.restype = ctypes.c_int
     lib.tt_launch_page_reset.restype = ctypes.c_int
     lib.tt_launch_zone_argmin.argtypes = [P, I64, P, P, I32, P, P, I32, P, I32, P, P]
@@ -258,10 +258,11 @@ class GpuKernels:
             total, complete, written = int(oarr[0]), bool(oarr[1]), int(oarr[2])
             return oarr[4:4 + written].copy(), total, complete
 
-    def page_topk(self, cand_keys, cand_rows, k: int, offset: int, bound: int):
+    def page_topk(self, cand_keys, cand_rows, k: int, offset: int, bound: int, stamps=None):
         """``tt_page_topk`` alone over caller-filled device candidates (uint64 keys as int64,
         int32 rows; their number = ``cand_keys.numel()``): (rows [offset, k) of the key order,
-        info [total, complete, written]).  For the kernel tests."""
+        info [total, complete, written]).  ``stamps``: an int64 device tensor of 6 that gets
+        the kernel's shader clock at its phase boundaries.  For the kernel tests."""
         import numpy as np
         torch = self.torch
         n = int(cand_keys.numel())
@@ -272,7 +273,8 @@ class GpuKernels:
             _, odev, oarr = self._mailbox("topk_out", 4 + self.page_cap)
             stream = self._stream()
             rc = self.lib.tt_launch_page_topk(cand_keys.data_ptr(), cand_rows.data_ptr(), counter.data_ptr(), k,
-                                              offset, ctypes.c_uint64(bound), odev, odev + 16, stream)
+                                              offset, ctypes.c_uint64(bound), odev, odev + 16,
+                                              None if stamps is None else stamps.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_page_topk launch failed ({rc})")
             self._sync(stream)

@@ -277,6 +277,86 @@ __device__ __forceinline__ void lds_bitonic(uint64_t* keys, int32_t* rows, int p
   __syncthreads();
 }
 
+// Lane exchange of x with lane ^ J: ds_swizzle (bitmask mode, within 32 lanes) for J < 32, a
+// bpermute for 32.  No LDS memory is touched.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x) {
+  if constexpr (J < 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (J << 10));
+  else return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x & 63) ^ 32) << 2, (int)x);
+}
+
+template <int J>
+__device__ __forceinline__ void cmpx_lanes(uint64_t& key, int32_t& row, int lane, int size) {
+  const uint64_t ok = ((uint64_t)xor_lane<J>((uint32_t)(key >> 32)) << 32) | xor_lane<J>((uint32_t)key);
+  const int32_t orow = (int32_t)xor_lane<J>((uint32_t)row);
+  // branch-free: keep the partner's pair if it is the min (max) this lane keeps; equal keys:
+  // both lanes keep their own
+  const uint32_t keep_min = (uint32_t)(((lane & J) == 0) == ((lane & size) == 0));
+  const uint32_t take = ((uint32_t)(ok < key) & keep_min) | ((uint32_t)(key < ok) & (keep_min ^ 1u));
+  key = take ? ok : key;
+  row = take ? orow : row;
+}
+
+// Bitonic sort of the wave's 64 (key, row) pairs, one per lane, ascending by lane: 21
+// compare-exchange steps, each three lane exchanges -- no LDS traffic, no barriers.
+__device__ __forceinline__ void wave_sort64(uint64_t& key, int32_t& row) {
+  const int lane = threadIdx.x & 63;
+  cmpx_lanes<1>(key, row, lane, 2);
+  cmpx_lanes<2>(key, row, lane, 4); cmpx_lanes<1>(key, row, lane, 4);
+  cmpx_lanes<4>(key, row, lane, 8); cmpx_lanes<2>(key, row, lane, 8); cmpx_lanes<1>(key, row, lane, 8);
+  cmpx_lanes<8>(key, row, lane, 16); cmpx_lanes<4>(key, row, lane, 16); cmpx_lanes<2>(key, row, lane, 16);
+  cmpx_lanes<1>(key, row, lane, 16);
+  cmpx_lanes<16>(key, row, lane, 32); cmpx_lanes<8>(key, row, lane, 32); cmpx_lanes<4>(key, row, lane, 32);
+  cmpx_lanes<2>(key, row, lane, 32); cmpx_lanes<1>(key, row, lane, 32);
+  cmpx_lanes<32>(key, row, lane, 64); cmpx_lanes<16>(key, row, lane, 64); cmpx_lanes<8>(key, row, lane, 64);
+  cmpx_lanes<4>(key, row, lane, 64); cmpx_lanes<2>(key, row, lane, 64); cmpx_lanes<1>(key, row, lane, 64);
+}
+
+// Sort of p <= 1024 pairs (p a power of two, pad keys ~0), writing only the page's rows:
+// wave w sorts elements [64w, 64w + 64) in registers (wave_sort64), then the sorted runs merge
+// pairwise, log2(p / 64) levels: every element finds its place in the merged run as its index
+// in its own run plus the number of the partner run's keys before it (a branchless binary
+// search; equal keys order by run).  An element stays in its thread's registers throughout; only
+// its key is published in LDS at each level (two ping-pong areas above the first 1,024 keys, so
+// the caller's unsorted pairs there are not overwritten).  At the end the element goes straight
+// to out_rows if its position is in [offset, upto).  log2(p / 64) barriers, against ~15 for the
+// LDS network at p = 1024 (profiles/r3_page_topk.md: 37 k of the kernel's 61 k shader clocks
+// were that network).  `key`/`row`: this thread's element (threads >= max(p, 64) are idle but
+// reach the barriers).
+__device__ __forceinline__ void rank_sort_1024(uint64_t key, int32_t row, int p, uint64_t* keys, int offset,
+                                               int upto, int32_t* __restrict__ out_rows) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  const int runs = p > 64 ? p >> 6 : 1;
+  const bool active = wave < runs;
+  if (active) wave_sort64(key, row);
+  uint64_t* cur = keys + kTopkBlock;
+  uint64_t* nxt = keys + 2 * kTopkBlock;
+  int pos = tid;
+  if (active) cur[pos] = key;
+  for (int lg = 6; (1 << lg) < 64 * runs; ++lg) {
+    __syncthreads();  // this level's run keys are published
+    if (active) {
+      const int len = 1 << lg;
+      const int r = pos >> lg, i = pos & (len - 1), q = r ^ 1;
+      const uint64_t* run = cur + q * len;
+      const uint32_t lower = (uint32_t)(q < r);
+      uint32_t at = 0;
+      for (int s = len >> 1; s > 0; s >>= 1) {
+        const uint64_t a = run[at + s - 1];
+        at += ((uint32_t)(a < key) | (lower & (uint32_t)(a == key))) * (uint32_t)s;
+      }
+      const uint64_t a = run[at];
+      at += (uint32_t)(a < key) | (lower & (uint32_t)(a == key));
+      pos = ((r >> 1) << (lg + 1)) + i + (int)at;
+      nxt[pos] = key;
+    }
+    uint64_t* t = cur;
+    cur = nxt;
+    nxt = t;
+  }
+  if (active && pos >= offset && pos < upto) out_rows[pos - offset] = row;
+}
+
 // Inclusive prefix sum across the 64 lanes of a wave.
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
   const int lane = threadIdx.x & 63;
@@ -291,27 +371,41 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
 // ONE workgroup: the page [offset, k) of the candidates' key order.
 // info = [candidates, complete, written, 0]; out_rows = the page's rows.
 //
-// n <= k: a bitonic sort of all n (padded to a power of two).  n > k (a bound that let more
-// candidates through than the page holds -- 2,600 for a 1,000-row page at 1e8 rows): the k-th
-// smallest key is found first by a most-significant-digit radix select over the LDS copy
-// (8-bit digits, starting at the highest bit in which the candidates differ: 5-6 histogram
-// passes for clustered keys), then only the k keys at or below it are compacted and sorted --
-// a 1,024-element network instead of 4,096.  Keys are unique (the insertion sequence is their
-// low bits), so exactly k keys are at or below the k-th.
+// n <= k: a sort of all n (padded to a power of two): up to 1,024 in registers plus a merge tree
+// (rank_sort_1024), more by the LDS network.  n > k (a bound that let more candidates through than
+// the page holds -- 2,600 for a 1,000-row page at 1e8 rows): the k-th smallest key is found first
+// by a most-significant-digit radix select over the LDS copy (8-bit digits, starting at the
+// highest bit in which the candidates differ; it stops at the first digit whose keys end exactly
+// at the k-th -- usually the second), then only the k keys at or below it are compacted (one LDS
+// atomic per wave) and sorted.  Keys are unique (the insertion sequence is their low bits), so
+// exactly k keys are at or below the k-th.  `stamps` (kernel tests only, else null): thread 0's
+// shader clock at the phase boundaries (scripts/topk_phases.py).
 extern "C" __global__ void __launch_bounds__(kTopkBlock)
 tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__ cand_rows,
              uint32_t* __restrict__ counter, uint32_t cap, int32_t k, int32_t offset, uint64_t bound,
-             int32_t* __restrict__ info, int32_t* __restrict__ out_rows) {
+             int32_t* __restrict__ info, int32_t* __restrict__ out_rows, int64_t* __restrict__ stamps) {
+  auto stamp = [&](int i) {
+    if (stamps && threadIdx.x == 0) stamps[i] = clock64();
+  };
+  stamp(0);
   __shared__ uint64_t keys[kPageCap];
   __shared__ int32_t rows[kPageCap];
   __shared__ uint32_t hist[256];
   __shared__ uint64_t s_lo, s_hi, s_prefix;
-  __shared__ uint32_t s_need, s_count;
+  __shared__ uint32_t s_need, s_count, s_done;
   const uint32_t total = *counter;
   const int n = (int)(total < cap ? total : cap);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int p = 1;
-  if (n <= k) {
+  const int upto = n < k ? n : k;
+  const int written = upto > offset ? upto - offset : 0;
+  if (n <= k && n <= kTopkBlock) {  // the common page: one element per thread, straight from memory
+    while (p < n) p <<= 1;
+    stamp(3);
+    rank_sort_1024(tid < n ? cand_keys[tid] : ~0ull, tid < n ? cand_rows[tid] : -1, p, keys, offset, upto,
+                   out_rows);
+    stamp(4);
+  } else if (n <= k) {
     while (p < n) p <<= 1;
     for (int i = tid; i < p; i += kTopkBlock) {
       keys[i] = i < n ? cand_keys[i] : ~0ull;
@@ -344,15 +438,17 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
       atomicMax(reinterpret_cast<unsigned long long*>(&s_hi), (unsigned long long)hi);
     }
     __syncthreads();
+    stamp(1);
     const uint64_t diff = s_lo ^ s_hi;
     const int top = diff ? 63 - __clzll((long long)diff) : 0;  // highest bit in which keys differ
     int shift = (top / 8) * 8;                                  // its 8-bit digit
     if (tid == 0) {
       s_prefix = shift + 8 >= 64 ? 0 : (s_lo >> (shift + 8)) << (shift + 8);  // the common high bits
       s_need = (uint32_t)k;
+      s_done = 0;
     }
     __syncthreads();
-    for (; shift >= 0; shift -= 8) {
+    for (; shift >= 0 && !s_done; shift -= 8) {
       for (int i = tid; i < 256; i += kTopkBlock) hist[i] = 0;
       __syncthreads();
       const uint64_t prefix = s_prefix;
@@ -377,8 +473,12 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             if (need <= before + c[j]) {
-              s_prefix = prefix | ((uint64_t)(lane * 4 + j) << shift);
+              // the k-th key is the last of its digit's keys: every key up to the digit's end
+              // is on the page -- the threshold is found without the lower digits' passes
+              const bool last = need == before + c[j];
+              s_prefix = prefix | ((uint64_t)(lane * 4 + j) << shift) | (last ? (1ull << shift) - 1 : 0);
               s_need = need - before;
+              s_done = last;
               break;
             }
             before += c[j];
@@ -388,6 +488,7 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
       __syncthreads();
     }
     // keys <= the k-th key: exactly k of them, compacted to the front (read, barrier, write)
+    stamp(2);
     const uint64_t kth = s_prefix;
     constexpr int kPer = kPageCap / kTopkBlock;  // candidates per thread (8), held in registers
     uint64_t xk[kPer];
@@ -409,27 +510,38 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
     __syncthreads();
     while (p < k) p <<= 1;
 #pragma unroll
-    for (int r = 0; r < kPer; ++r) {
-      if (sel[r]) {
-        const uint32_t slot = atomicAdd(&s_count, 1u);
-        if ((int)slot < p) {
-          keys[slot] = xk[r];
-          rows[slot] = xr[r];
-        }
+    for (int r = 0; r < kPer; ++r) {  // one LDS atomic per wave and round: ballot + lane offsets
+      const uint64_t m = __ballot(sel[r]);
+      if (!m) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&s_count, (uint32_t)__popcll(m));
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl(base, 0));
+      const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (sel[r] && (int)slot < p) {
+        keys[slot] = xk[r];
+        rows[slot] = xr[r];
       }
     }
     __syncthreads();
     const int got = (int)(s_count < (uint32_t)p ? s_count : (uint32_t)p);
-    for (int i = got + tid; i < p; i += kTopkBlock) {
-      keys[i] = ~0ull;
-      rows[i] = -1;
+    if (p <= kTopkBlock) {  // k <= 1024: the selected k straight from the compaction
+      stamp(3);
+      rank_sort_1024(tid < got ? keys[tid] : ~0ull, tid < got ? rows[tid] : -1, p, keys, offset, upto, out_rows);
+      stamp(4);
+    } else {
+      for (int i = got + tid; i < p; i += kTopkBlock) {
+        keys[i] = ~0ull;
+        rows[i] = -1;
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
-  lds_bitonic(keys, rows, p);
-  const int upto = n < k ? n : k;
-  const int written = upto > offset ? upto - offset : 0;
-  for (int i = tid; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];
+  if (p > kTopkBlock || (n <= k && n > kTopkBlock)) {
+    stamp(3);
+    lds_bitonic(keys, rows, p);
+    stamp(4);
+    for (int i = tid; i < written; i += kTopkBlock) out_rows[i] = rows[offset + i];
+  }
   if (tid == 0) {
     int complete;
     if (total > cap) complete = 0;                     // overflow: the host takes fewer tiles
@@ -441,6 +553,7 @@ tt_page_topk(const uint64_t* __restrict__ cand_keys, const int32_t* __restrict__
     info[3] = 0;
     *counter = 0;  // ready for the next query's gather (stream order)
   }
+  stamp(5);
 }
 
 extern "C" __global__ void tt_page_reset(uint32_t* __restrict__ counter) {
@@ -470,10 +583,10 @@ extern "C" int tt_launch_zone_argmin(const void* cols, int64_t nrows, const uint
 // kernel tests drive it with every candidate count from 0 to kPageCap.
 extern "C" int tt_launch_page_topk(const uint64_t* cand_keys, const int32_t* cand_rows, uint32_t* counter, int32_t k,
                                    int32_t offset, uint64_t bound, int32_t* info, int32_t* out_rows,
-                                   hipStream_t stream) {
+                                   int64_t* stamps, hipStream_t stream) {
   if (k <= 0 || k > kPageCap || offset < 0 || offset > k) return -1;
   hipLaunchKernelGGL(tt_page_topk, dim3(1), dim3(kTopkBlock), 0, stream, cand_keys, cand_rows, counter,
-                     (uint32_t)kPageCap, k, offset, bound, info, out_rows);
+                     (uint32_t)kPageCap, k, offset, bound, info, out_rows, stamps);
   return (int)hipGetLastError();
 }
 
@@ -494,7 +607,7 @@ extern "C" int tt_launch_page(const void* cols, int64_t nrows, const uint16_t* l
                        cand_rows, counter, (uint32_t)kPageCap);
   }
   hipLaunchKernelGGL(tt_page_topk, dim3(1), dim3(kTopkBlock), 0, stream, cand_keys, cand_rows, counter,
-                     (uint32_t)kPageCap, k, offset, bound, info, out_rows);
+                     (uint32_t)kPageCap, k, offset, bound, info, out_rows, (int64_t*)nullptr);
   return (int)hipGetLastError();
 }
 

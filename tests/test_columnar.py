@@ -1022,6 +1022,13 @@ def test_gpu_page_topk_sorts_every_candidate_count(n, wide):
         assert info[1] == 1  # bound = all tiles read: complete
     got, info = k.page_topk(dk, dr, 1000, 0, 12345)  # a bound: complete only with k candidates
     assert info[1] == (1 if n >= 1000 else 0)
+    # the phase clocks (scripts/topk_phases.py): the stamps a branch writes never go backwards,
+    # and setting them does not change the answer
+    stamps = torch.zeros(6, dtype=torch.int64, device=k.device)
+    got, info = k.page_topk(dk, dr, 1000, 0, np.iinfo(np.uint64).max, stamps=stamps)
+    assert got.tolist() == order[:min(n, 1000)].tolist()
+    s = [int(x) for x in stamps.cpu().tolist() if x != 0]
+    assert len(s) >= 4 and s == sorted(s)
 
 
 @pytest.mark.gpu
