@@ -35,6 +35,7 @@ from typing import Any
 
 from .. import native
 from ..telemetry import configure, configure_logging
+from ..telemetry.tracing import parse_traceparent, tracer
 from ..telemetry.profiler import maybe_profile
 from ..web.app import WebApp
 from ..web.http import HTTPError, Request, Response, empty, json_response, problem
@@ -301,19 +302,41 @@ class BackingServices:
             raw = req.body.decode("utf-8") or "{}"
             prefix = req.query_get("prefix", "") or ""
             a = acc(req)
+            # a sampled caller (the data plane passes the trace on for queries) gets the
+            # store's share as spans: this handler, and the planner + page run on the pool
+            tp = parse_traceparent(req.headers.get("traceparent"))
+            span = tracer().start_span("POST query", "server", parent=tp, activate=False) if tp and tp[2] else None
+            if span is not None:  # the hops before this handler, from the callers' monotonic stamps
+                now = time.monotonic()
+                for k, at in (("since_sidecar_sent_ms", "x-tt-sent-mono"), ("since_front_forwarded_ms", "x-tt-front-mono")):
+                    try:
+                        span.set(k, round((now - float(req.headers.get(at))) * 1e3, 3))
+                    except (TypeError, ValueError):
+                        pass
 
             def run() -> str:
-                q = json.loads(raw)
-                text = a.query(q, prefix, s) if isinstance(q, dict) else None
-                return s.query(raw, prefix) if text is None else text
+                inner = tracer().start_span("query run", "internal", parent=span) if span is not None else None
+                try:
+                    q = json.loads(raw)
+                    text = a.query(q, prefix, s) if isinstance(q, dict) else None
+                    return s.query(raw, prefix) if text is None else text
+                finally:
+                    if inner is not None:
+                        inner.end()
             if (t := throttled(s, s.query_ru(0))) is not None:
                 return t
             try:
                 text = await asyncio.get_running_loop().run_in_executor(self.query_pool, run)
             except ValueError as ex:
+                if span is not None:
+                    span.end()
                 return problem(400, detail=str(ex))
             s.charge(s.query_ru(len(text)) - s.query_ru(0))  # result size part: charged after the fact
-            return Response(text.encode(), 200, None, "application/json")
+            body = text.encode()
+            if span is not None:
+                span.set("bytes", len(body))
+                span.end()
+            return Response(body, 200, None, "application/json")
 
         async def transaction(req: Request) -> Response:
             s = st(req, "cosmos.write")

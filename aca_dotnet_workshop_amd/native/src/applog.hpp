@@ -2,7 +2,9 @@
 //
 // Record: [u32 total_len][u8 kind][fields...] where every field is [u32 len][bytes].
 // Writes go straight to the fd (one write(2) per record) so a process crash never loses
-// an acknowledged mutation; fsync_mode=1 additionally fdatasync()s each record.
+// an acknowledged mutation; fsync_mode=1 additionally fdatasync()s each record.  A batch
+// (BatchScope: a bulk write acknowledged as a whole) collects its records and writes them with
+// one write(2) when the scope ends, before the caller acknowledges.
 #pragma once
 
 #include <fcntl.h>
@@ -12,6 +14,7 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <stdexcept>
 #include <string>
@@ -60,8 +63,37 @@ class AppLog {
     for (auto f : fields) put_field(rec, f);
     uint32_t total = (uint32_t)rec.size();
     std::memcpy(&rec[0], &total, 4);
+    if (batching_) {
+      batch_ += rec;
+      return;
+    }
     write_all(rec);
   }
+
+  // Records appended while a BatchScope is alive go out in one write(2) when it ends.
+  class BatchScope {
+   public:
+    explicit BatchScope(AppLog& log) : log_(log) { log_.batching_ = true; }
+    ~BatchScope() noexcept(false) {
+      log_.batching_ = false;
+      if (log_.batch_.empty()) return;
+      std::string b;
+      b.swap(log_.batch_);
+      if (std::uncaught_exceptions() == 0) {
+        log_.write_all(b);
+        return;
+      }
+      try {  // unwinding already: keep what was applied, do not throw a second time
+        log_.write_all(b);
+      } catch (...) {
+      }
+    }
+    BatchScope(const BatchScope&) = delete;
+    BatchScope& operator=(const BatchScope&) = delete;
+
+   private:
+    AppLog& log_;
+  };
 
   // Replays every complete record; a torn tail (crash mid-write) is truncated.
   void replay(const std::function<void(char, std::vector<std::string_view>&)>& fn) {
@@ -138,6 +170,8 @@ class AppLog {
   int fsync_ = 0;
   uint64_t bytes_ = 0;
   std::string path_;
+  bool batching_ = false;
+  std::string batch_;
 };
 
 }  // namespace tt

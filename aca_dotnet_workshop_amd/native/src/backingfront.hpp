@@ -307,6 +307,11 @@ class BackingFront {
     ev::HeaderList h;
     for (auto& kv : m.headers)
       if (!ev::is_hop_header(kv.first)) h.push_back(kv);
+    if (m.header("traceparent")) {  // a traced caller: when the front forwarded (CLOCK_MONOTONIC s)
+      char t[32];
+      std::snprintf(t, sizeof t, "%.6f", ev::now_s());
+      h.emplace_back("x-tt-front-mono", t);
+    }
     sh.client.request(fallback_, m.method, m.target, h, m.body, 0, [r](ev::ClientResult&& res) {
       if (res.err) {
         r.send(503, {{"content-type", "application/problem+json; charset=utf-8"}},
@@ -412,28 +417,32 @@ class BackingFront {
       ru += DocStore::write_ru(v ? (v->t == Value::String ? v->s.size() : dump(*v).size()) : 4);
     }
     if (throttled(r, c->store, ru)) return true;
+    std::vector<DocStore::BulkItem> batch(items.items.size());
+    for (size_t i = 0; i < items.items.size(); ++i) {
+      Value& it = items.items[i];
+      DocStore::BulkItem& b = batch[i];
+      for (size_t f = 0; f < it.keys.size(); ++f) {  // the body is ours: move its strings out
+        Value& v = it.items[f];
+        const std::string& k = it.keys[f];
+        if (k == "key") b.key = std::move(v.s);
+        else if (k == "value") b.value = v.t == Value::String ? std::move(v.s) : dump(v);
+        else if (k == "etag" && v.t == Value::String && !v.s.empty()) b.etag = std::move(v.s);
+        else if (k == "firstWrite" && v.t == Value::Bool) b.first_write = v.b;
+      }
+      if (!it.get("value")) b.value = "null";
+    }
+    const std::vector<DocStore::BulkResult> res = c->store->set_many(batch);
     std::string out = "[";
     bool etag_err = false, other_err = false;
-    for (size_t i = 0; i < items.items.size(); ++i) {
-      const Value& it = items.items[i];
-      const std::string& key = it.get("key")->s;
-      const Value* v = it.get("value");
-      std::string value = v ? (v->t == Value::String ? v->s : dump(*v)) : std::string("null");
-      std::optional<std::string> etag;
-      if (auto* e = it.get("etag"); e && e->t == Value::String && !e->s.empty()) etag = e->s;
-      bool fw = false;
-      if (auto* f = it.get("firstWrite"); f && f->t == Value::Bool) fw = f->b;
+    for (size_t i = 0; i < res.size(); ++i) {
       if (i) out += ", ";
-      try {
-        std::string e = c->store->set(key, value, etag, fw, 0);
-        out += "{\"key\": " + bf::jstr(key) + ", \"etag\": " + bf::jstr(e) + "}";
-      } catch (const EtagMismatch& ex) {
-        etag_err = true;
-        out += "{\"key\": " + bf::jstr(key) + ", \"error\": \"etag\", \"detail\": " + bf::jstr(ex.what()) + "}";
-      } catch (const ParseError& ex) {
-        other_err = true;
-        out += "{\"key\": " + bf::jstr(key) + ", \"error\": \"invalid\", \"detail\": " +
-               bf::jstr(std::string("invalid JSON: ") + ex.what()) + "}";
+      out += "{\"key\": " + bf::jstr(batch[i].key);
+      if (res[i].err == 0) {
+        out += ", \"etag\": " + bf::jstr(res[i].etag) + "}";
+      } else {
+        (res[i].err == 1 ? etag_err : other_err) = true;
+        out += std::string(", \"error\": ") + (res[i].err == 1 ? "\"etag\"" : "\"invalid\"") +
+               ", \"detail\": " + bf::jstr(res[i].detail) + "}";
       }
     }
     out += "]";

@@ -1329,6 +1329,12 @@ class DataPlane {
     if (!s.prefix.empty()) target += "?prefix=" + quote_all(s.prefix);
     HeaderList h = s.auth;
     h.emplace_back("content-type", "application/json");
+    if (d->span.sampled) {  // the store's spans join the trace, with when this hop sent (CLOCK_MONOTONIC s)
+      h.emplace_back("traceparent", d->span.traceparent());
+      char t[32];
+      std::snprintf(t, sizeof t, "%.6f", ev::now_s());
+      h.emplace_back("x-tt-sent-mono", t);
+    }
     store_request(s.backing, "POST", target, h, m.body.empty() ? std::string("{}") : m.body,
                     [d](ClientResult&& res) {
                       if (!res.err && res.resp.status == 200) {

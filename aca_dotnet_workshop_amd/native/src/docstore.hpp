@@ -229,6 +229,54 @@ class DocStore {
     return std::to_string(e);
   }
 
+  // Bulk write (Dapr BulkSet: not atomic -- every item succeeds or fails on its own): values
+  // parsed before the lock, then ONE lock hold and ONE log write(2) for the whole batch, instead
+  // of one of each per item.  Per item: the new etag, or err 1 (etag precondition) / 2 (invalid
+  // JSON) with its detail.
+  struct BulkItem {
+    std::string key, value;
+    std::optional<std::string> etag;
+    bool first_write = false;
+  };
+  struct BulkResult {
+    std::string etag;
+    int err = 0;
+    std::string detail;
+  };
+  std::vector<BulkResult> set_many(std::vector<BulkItem>& items) {
+    std::vector<BulkResult> out(items.size());
+    std::vector<Value> parsed(items.size());
+    for (size_t i = 0; i < items.size(); ++i) {
+      try {
+        parsed[i] = parse(items[i].value);
+      } catch (const ParseError& e) {
+        out[i].err = 2;
+        out[i].detail = std::string("invalid JSON: ") + e.what();
+      }
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    {
+      AppLog::BatchScope batch(log_);
+      const int64_t now = now_ms();
+      for (size_t i = 0; i < items.size(); ++i) {
+        if (out[i].err) continue;
+        BulkItem& it = items[i];
+        try {
+          check_etag(it.key, it.etag, it.first_write, now);
+        } catch (const EtagMismatch& e) {
+          out[i].err = 1;
+          out[i].detail = e.what();
+          continue;
+        }
+        const uint64_t e = put(it.key, it.value, std::move(parsed[i]), 0);
+        log_put(it.key, it.value, e, docs_[it.key].expire_ms);
+        out[i].etag = std::to_string(e);
+      }
+    }
+    maybe_compact();
+    return out;
+  }
+
   std::optional<std::pair<std::string, std::string>> get(const std::string& key) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = docs_.find(key);

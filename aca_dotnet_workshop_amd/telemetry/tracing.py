@@ -60,6 +60,7 @@ class Exporter:
         self._fh = None
         self._memory: list[dict[str, Any]] = []
         self._sources: list[Any] = []  # callables returning span records produced elsewhere
+        self._timer: threading.Thread | None = None
         self.keep_in_memory = directory is None
         if directory:
             os.makedirs(directory, exist_ok=True)
@@ -79,6 +80,14 @@ class Exporter:
             self._buf.append(line)
             if len(self._buf) >= 256:
                 self._flush_locked()
+            elif self._timer is None:  # batched, but never held back more than a second
+                self._timer = threading.Thread(target=self._flush_every_second, name="tt-span-flush", daemon=True)
+                self._timer.start()
+
+    def _flush_every_second(self) -> None:
+        while True:
+            time.sleep(1.0)
+            self.flush()
 
     @property
     def memory(self) -> list[dict[str, Any]]:

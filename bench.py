@@ -182,6 +182,7 @@ class OverdueSweeper:
         self.stop_ev = threading.Event()
         self.runs: list[tuple[float, dict]] = []
         self.errors: list[str] = []
+        self.trace_ids: list[str] = []  # every sweep is a sampled trace (per-hop spans)
         self.thread = threading.Thread(target=self._run, name="overdue-sweeper", daemon=True)
 
     def start(self) -> None:
@@ -189,7 +190,7 @@ class OverdueSweeper:
 
     def reset(self) -> None:
         """Forget the sweeps so far (the warmup's): the summary covers what follows."""
-        self.runs, self.errors = [], []
+        self.runs, self.errors, self.trace_ids = [], [], []
 
     def stop(self) -> None:
         self.stop_ev.set()
@@ -204,10 +205,14 @@ class OverdueSweeper:
         try:
             while not self.stop_ev.is_set():
                 t = time.perf_counter()
+                tid = os.urandom(16).hex()
                 try:
-                    r = await c.post(self.url, body=b"{}", headers={"Content-Type": "application/json"}, timeout=60)
+                    r = await c.post(self.url, body=b"{}", timeout=60,
+                                     headers={"Content-Type": "application/json",
+                                              "traceparent": f"00-{tid}-{os.urandom(8).hex()}-01"})
                     if r.status == 200:
                         self.runs.append((time.perf_counter() - t, r.json()))
+                        self.trace_ids.append(tid)
                     else:
                         self.errors.append(f"{r.status} {r.body[:200]!r}")
                 except Exception as e:  # recorded, reported in the bench line
@@ -229,6 +234,41 @@ class OverdueSweeper:
                 "query_ms_total": round(sum(r.get("queryMs", 0.0) for _, r in self.runs), 1),
                 "mark_ms_total": round(sum(r.get("markMs", 0.0) for _, r in self.runs), 1),
                 "first_error": self.errors[0] if self.errors else None}
+
+
+def sweep_trace(telemetry_dir: str, trace_ids: list[str]) -> dict | None:
+    """Per-hop time of the sweeps from their spans (every sweep is a sampled trace): for every
+    span of the job -- server spans of each sidecar data plane and app, the apps' client calls
+    -- the median duration over the sweeps, in the order of the first sweep.  Keys are
+    ``role kind name``."""
+    from aca_dotnet_workshop_amd.telemetry.appmap import load_spans
+    want = set(trace_ids)
+    if not want:
+        return None
+    by_trace: dict[str, list[dict]] = {}
+    for sp in load_spans(telemetry_dir):
+        if sp.get("traceId") in want:
+            by_trace.setdefault(sp["traceId"], []).append(sp)
+    if not by_trace:
+        return None
+    order: list[str] = []
+    durs: dict[str, list[float]] = {}
+    attrs: dict[str, list[float]] = {}  # numeric span attributes (the store's hop stamps)
+    for tid in trace_ids:
+        for sp in sorted(by_trace.get(tid, []), key=lambda x: x.get("ts", 0.0)):
+            k = f"{sp.get('role')} {sp.get('kind')} {sp.get('name')}"
+            if k not in durs:
+                order.append(k)
+                durs[k] = []
+            durs[k].append(float(sp.get("durationMs", 0.0)))
+            for ak, av in (sp.get("attributes") or {}).items():
+                if ak.endswith("_ms") and isinstance(av, (int, float)):
+                    attrs.setdefault(f"{k} {ak}", []).append(float(av))
+
+    def med(xs: list[float]) -> float:
+        return round(sorted(xs)[len(xs) // 2], 2)
+    return {"sweeps_traced": len(by_trace), "spans_p50_ms": {k: med(durs[k]) for k in order},
+            "stamps_p50_ms": {k: med(v) for k, v in attrs.items()}}
 
 
 def _counts(url: str | list[str]) -> dict:
@@ -696,6 +736,10 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             direct = {"value": round(a.batch * dsteps * (d.world if d.world > 1 else 1) / ddt, 2), "steps": dsteps,
                       "create_latency_p50_ms": drep["latency_ms"]["p50"], "create_latency_p99_ms": drep["latency_ms"]["p99"],
                       "note": "same environment, load at the API sidecars' invoke (no frontend, no mTLS hop)"}
+        if sweep_info is not None:  # span exporters flush at least once a second
+            if not dsteps:
+                time.sleep(1.5)
+            sweep_info["trace"] = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids)
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])

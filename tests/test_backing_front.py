@@ -76,6 +76,56 @@ def test_documents(front, monkeypatch):
 
 
 @pytest.mark.parametrize("front", FRONTS)
+def test_bulk_set_items_fail_alone_and_persist(front, monkeypatch, tmp_path):
+    """A bulk save is not atomic: an item with a failed ETag precondition or invalid JSON fails
+    alone (412 wins over 400), the others are applied in order -- the native front writes the
+    whole batch under one store lock with one log write -- and the batch survives a restart of
+    the store from its log."""
+    import json as _json
+
+    items = [{"key": "a", "value": '{"v": 1}'}, {"key": "a", "value": '{"v": 2}'},
+             {"key": "b", "value": '{"v": 3}', "etag": "nope"}, {"key": "c", "value": "{not json"},
+             {"key": "d", "value": {"v": [4]}}, {"key": "e", "value": '"x"', "firstWrite": True}]
+
+    class Persisted(Backing):
+        async def __aenter__(self):
+            ready = asyncio.get_running_loop().create_future()
+            self.stop = asyncio.Event()
+            self.task = asyncio.ensure_future(serve_backing("127.0.0.1", 0, str(tmp_path), None, ready.set_result,
+                                                            self.stop))
+            self.base = f"http://127.0.0.1:{await asyncio.wait_for(ready, 20)}"
+            return self
+
+    async def main():
+        async with Persisted(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.doc_put("acct", "db", "c", "seed", "0")
+            r = await c.http.post(b.base + "/cosmos/acct/db/c/bulkset", body=_json.dumps(items).encode(),
+                                  headers={"Content-Type": "application/json"})
+            assert r.status == 412
+            out = r.json()
+            assert [o["key"] for o in out] == ["a", "a", "b", "c", "d", "e"]
+            assert [o.get("error") for o in out] == [None, None, "etag", "invalid", None, None]
+            assert int(out[1]["etag"]) > int(out[0]["etag"])
+            assert (await c.doc_get("acct", "db", "c", "a"))[0] == b'{"v": 2}'
+            assert await c.doc_get("acct", "db", "c", "b") is None
+            assert await c.doc_get("acct", "db", "c", "c") is None
+            assert _json.loads((await c.doc_get("acct", "db", "c", "d"))[0]) == {"v": [4]}
+            r = await c.http.post(b.base + "/cosmos/acct/db/c/bulkset", headers={"Content-Type": "application/json"},
+                                  body=_json.dumps([{"key": "f", "value": "1"}, {"key": "g", "value": "{"}]).encode())
+            assert r.status == 400 and [o.get("error") for o in r.json()] == [None, "invalid"]
+            await c.http.close()
+        async with Persisted(front, monkeypatch) as b:  # replayed from the log
+            c = BackingClient(b.base, identity="x")
+            assert (await c.doc_get("acct", "db", "c", "a"))[0] == b'{"v": 2}'
+            assert (await c.doc_get("acct", "db", "c", "e"))[0] == b'"x"'
+            assert (await c.doc_get("acct", "db", "c", "f"))[0] == b"1"
+            assert await c.doc_get("acct", "db", "c", "b") is None
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
 def test_messaging_and_long_poll(front, monkeypatch):
     async def main():
         async with Backing(front, monkeypatch) as b:

@@ -185,3 +185,28 @@ def test_rank_device_env():
     assert b.rank_device_env({"WORLD_SIZE": "8", "LOCAL_RANK": "3"}) == {"HIP_VISIBLE_DEVICES": "3"}
     assert b.rank_device_env({"WORLD_SIZE": "1", "LOCAL_RANK": "0"}) == {}
     assert b.rank_device_env({"WORLD_SIZE": "2", "LOCAL_RANK": "1", "HIP_VISIBLE_DEVICES": "5"}) == {}
+
+
+def test_sweep_trace_summarises_the_sweeps_spans(tmp_path):
+    """bench.sweep_trace: the sweeps are sampled traces; their spans (any process, any file)
+    become per-hop medians in the order of the first sweep, plus the store's numeric hop stamps;
+    spans of other traces are ignored."""
+    sys.path.insert(0, str(ROOT))
+    from bench import sweep_trace
+
+    def span(tid, role, kind, name, ts, ms, attrs=None):
+        return json.dumps({"type": "span", "role": role, "kind": kind, "name": name, "traceId": tid, "spanId": os.urandom(8).hex(),
+                           "parentId": None, "ts": ts, "durationMs": ms, **({"attributes": attrs} if attrs else {})})
+    a, b, other = "a" * 32, "b" * 32, "c" * 32
+    (tmp_path / "spans-proc-1-x.jsonl").write_text("\n".join([
+        span(a, "proc", "server", "POST /job", 1.0, 20.0), span(b, "proc", "server", "POST /job", 2.0, 30.0),
+        span(other, "proc", "server", "POST /job", 3.0, 999.0)]) + "\n")
+    (tmp_path / "spans-backing-2-x.jsonl").write_text("\n".join([
+        span(a, "backing", "server", "POST query", 1.1, 4.0, {"since_front_forwarded_ms": 0.5, "bytes": 10}),
+        span(b, "backing", "server", "POST query", 2.1, 6.0, {"since_front_forwarded_ms": 0.7})]) + "\n")
+    got = sweep_trace(str(tmp_path), [a, b])
+    assert got["sweeps_traced"] == 2
+    assert list(got["spans_p50_ms"]) == ["proc server POST /job", "backing server POST query"]
+    assert got["spans_p50_ms"]["proc server POST /job"] == 30.0  # upper median of 2
+    assert got["stamps_p50_ms"] == {"backing server POST query since_front_forwarded_ms": 0.7}
+    assert sweep_trace(str(tmp_path), []) is None
