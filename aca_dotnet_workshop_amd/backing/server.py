@@ -336,6 +336,7 @@ class BackingServices:
             if span is not None:
                 span.set("bytes", len(body))
                 span.end()
+                return Response(body, 200, [("x-tt-handler-end-mono", f"{time.monotonic():.6f}")], "application/json")
             return Response(body, 200, None, "application/json")
 
         async def transaction(req: Request) -> Response:

@@ -318,6 +318,14 @@ class BackingFront {
                bf::problem_json(503, "backing control plane unreachable"));
         return;
       }
+      if (res.resp.header("x-tt-handler-end-mono")) {  // a traced query: when the front had the answer
+        ev::HeaderList h2 = res.resp.headers;
+        char t[32];
+        std::snprintf(t, sizeof t, "%.6f", ev::now_s());
+        h2.emplace_back("x-tt-front-rx-mono", t);
+        r.send(res.resp.status, h2, res.resp.body);
+        return;
+      }
       r.send(res.resp.status, res.resp.headers, res.resp.body);
     });
   }

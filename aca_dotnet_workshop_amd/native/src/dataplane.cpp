@@ -1338,6 +1338,16 @@ class DataPlane {
     store_request(s.backing, "POST", target, h, m.body.empty() ? std::string("{}") : m.body,
                     [d](ClientResult&& res) {
                       if (!res.err && res.resp.status == 200) {
+                        if (d->span.sampled) {  // the return path, from the store's monotonic stamps
+                          const double now = ev::now_s();
+                          for (auto [attr, hdr] : {std::pair{"store_handler_end_to_sidecar_ms", "x-tt-handler-end-mono"},
+                                                   std::pair{"store_front_rx_to_sidecar_ms", "x-tt-front-rx-mono"}})
+                            if (const std::string* t = res.resp.header(hdr)) {
+                              char b[32];
+                              std::snprintf(b, sizeof b, "%.3f", (now - std::strtod(t->c_str(), nullptr)) * 1e3);
+                              d->attrs.emplace_back(attr, b);
+                            }
+                        }
                         d->send(200, {{"content-type", "application/json"}}, res.resp.body);
                         return;
                       }

@@ -50,6 +50,15 @@ inline double now_s() {
 
 inline void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
+// Local (unix) stream sockets carry whole pages of query results and bulk saves (200-300 KB)
+// between the apps, the sidecars and the backing.  The default send buffer (net.core.wmem_default,
+// ~208 KB) splits such a message over several event-loop turns of a busy reader; asking for more
+// gets the kernel's maximum (wmem_max, doubled), enough for one message in one write.
+inline void widen_local_sndbuf(int fd) {
+  int sz = 4 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
+}
+
 // ------------------------------------------------------------------------------ loop
 struct IoObj : std::enable_shared_from_this<IoObj> {
   int fd = -1;
@@ -722,6 +731,9 @@ class Listener : public IoObj {
   Listener(Loop& loop, int fd, Handler& h, std::shared_ptr<TlsContext> tls = nullptr)
       : loop_(loop), handler_(h), tls_(std::move(tls)) {
     this->fd = fd;
+    sockaddr_storage ss{};
+    socklen_t len = sizeof ss;
+    unix_ = ::getsockname(fd, (sockaddr*)&ss, &len) == 0 && ss.ss_family == AF_UNIX;
   }
   void on_event(uint32_t) override {
     while (true) {
@@ -731,7 +743,8 @@ class Listener : public IoObj {
         return;  // EAGAIN or transient error (EMFILE ...): try again on the next readiness event
       }
       int one = 1;
-      setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // fails harmlessly on unix sockets
+      if (unix_) widen_local_sndbuf(c);
+      else setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
       std::shared_ptr<ServerConn> conn;
       try {
         conn = std::make_shared<ServerConn>(loop_, c, handler_, tls_.get());
@@ -747,6 +760,7 @@ class Listener : public IoObj {
   std::function<void(const std::shared_ptr<ServerConn>&)> on_accept;
 
  private:
+  bool unix_ = false;
   Loop& loop_;
   Handler& handler_;
   std::shared_ptr<TlsContext> tls_;
@@ -1025,6 +1039,7 @@ class Client {
       // listener's accept queue is full -- the caller retries then, rather than parking the
       // whole event loop in connect() until the peer gets round to accept()
       fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      widen_local_sndbuf(fd);
       sockaddr_un a{};
       a.sun_family = AF_UNIX;
       std::strncpy(a.sun_path, ep.path.c_str(), sizeof a.sun_path - 1);

@@ -148,6 +148,13 @@ class HttpServerProtocol(asyncio.Protocol):
                 sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             except OSError:
                 pass
+        elif sock is not None and sock.family == socket.AF_UNIX:
+            # a page of query results or a bulk save (200-300 KB) in one write, not split over
+            # several loop turns of a busy reader (native/src/evhttp.hpp widen_local_sndbuf)
+            try:
+                sock.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+            except OSError:
+                pass
         self.server._conns.add(self)
 
     def connection_lost(self, exc: Exception | None) -> None:

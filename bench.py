@@ -262,8 +262,11 @@ def sweep_trace(telemetry_dir: str, trace_ids: list[str]) -> dict | None:
                 durs[k] = []
             durs[k].append(float(sp.get("durationMs", 0.0)))
             for ak, av in (sp.get("attributes") or {}).items():
-                if ak.endswith("_ms") and isinstance(av, (int, float)):
-                    attrs.setdefault(f"{k} {ak}", []).append(float(av))
+                if ak.endswith("_ms"):  # numbers, or numeric text (the native planes' attributes)
+                    try:
+                        attrs.setdefault(f"{k} {ak}", []).append(float(av))
+                    except (TypeError, ValueError):
+                        pass
 
     def med(xs: list[float]) -> float:
         return round(sorted(xs)[len(xs) // 2], 2)
