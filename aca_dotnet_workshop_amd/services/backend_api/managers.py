@@ -33,6 +33,7 @@ from datetime import datetime, timedelta
 from ...models import (TaskModel, create_task_wire, format_fixed, mark_overdue_wire, naive_utc, tasks_from_query_wire,
                        today, utcnow)
 from ...sdk.client import InvocationError, RawJson, SidecarClient
+from ...telemetry.logging import info_each
 
 log = logging.getLogger("TasksManager")
 
@@ -323,8 +324,7 @@ class TasksStoreManager(TasksManager):
         if made is None:
             return False
         ids, bulk = made
-        for tid in ids:
-            log.info("Mark task with Id: '%s' as OverDue task", tid)
+        info_each(log, "Mark task with Id: '%s' as OverDue task", [(tid,) for tid in ids])
         if ids:
             await save_body(self.store, bulk)
         return True

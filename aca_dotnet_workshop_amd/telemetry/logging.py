@@ -123,6 +123,31 @@ class BufferedSink(logging.Handler):
             line = f"{self._hms} {_NET_LEVEL.get(level, 'info')[:4].lower()}: {self.role} {name}: {message}\n"
         self._put(line)
 
+    def write_fast_many(self, level: int, name: str, messages: list[str], trace_id: str, span_id: str) -> None:
+        """``write_fast`` for a run of records emitted back to back (one timestamp for the run)."""
+        now = time.time()
+        if self.json_lines:
+            pre = self._prefix.get((level, name))
+            if pre is None:
+                pre = self._prefix[(level, name)] = '{"level":"%s","role":%s,"category":%s' % (
+                    _NET_LEVEL.get(level, logging.getLevelName(level)), self.role_json, encode_basestring(name))
+            head = '%s,"ts":%.6f,"message":' % (pre, now)
+            tail = ',"traceId":"%s","spanId":"%s"}\n' % (trace_id, span_id) if trace_id else "}\n"
+            lines = [head + encode_basestring(m) + tail for m in messages]
+        else:
+            sec = int(now)
+            if sec != self._sec:
+                self._sec, self._hms = sec, time.strftime("%H:%M:%S", time.localtime(now))
+            head = f"{self._hms} {_NET_LEVEL.get(level, 'info')[:4].lower()}: {self.role} {name}: "
+            lines = [head + m + "\n" for m in messages]
+        if not self.buffered:
+            self._put("".join(lines))
+            return
+        self._buf.extend(lines)
+        self._size += sum(map(len, lines))
+        if self._size >= 65536:
+            self.flush()
+
     def _put(self, line: str) -> None:
         if not self.buffered:
             try:
@@ -211,6 +236,22 @@ class FastLogger(logging.Logger):
                     sink.write_fast(level, self.name, message, tid, sid)
         return True
 
+    def info_each(self, msg: str, args_seq) -> None:
+        """One Information record per argument tuple -- the same lines as ``info(msg, *args)``
+        in a loop (e.g. one per task of a bulk operation), formatted as one batch."""
+        if self.handlers or len(_root.handlers) != _State.root_handlers or not self.propagate:
+            for args in args_seq:
+                super().info(msg, *args)
+            return
+        if not self.isEnabledFor(logging.INFO):
+            return
+        messages = [msg % args for args in args_seq]
+        s = current_span()
+        tid, sid = (s.trace_id, s.span_id) if s is not None else ("", "")
+        for sink in _State.sinks:
+            if logging.INFO >= sink.level:
+                sink.write_fast_many(logging.INFO, self.name, messages, tid, sid)
+
     def debug(self, msg, *args, **kw):
         if not self._fast(logging.DEBUG, msg, args, kw):
             super().debug(msg, *args, **kw)
@@ -273,6 +314,16 @@ def configure_logging(role: str, config: Any = None, json_console: bool | None =
     # fast path only while the root logger's handlers are exactly these sinks
     _State.root_handlers = len(root.handlers) if all(getattr(h, "_tt", False) for h in root.handlers) else -1
     _adopt_fast_loggers()
+
+
+def info_each(logger: logging.Logger, msg: str, args_seq) -> None:
+    """``logger.info(msg, *args)`` for every tuple of ``args_seq``: batched on a ``FastLogger``,
+    a plain loop on any other logger."""
+    if isinstance(logger, FastLogger):
+        logger.info_each(msg, args_seq)
+    else:
+        for args in args_seq:
+            logger.info(msg, *args)
 
 
 def flush_logs() -> None:

@@ -104,3 +104,51 @@ def test_log_retention_prunes_whole_days(tmp_path):
     f.close()
     assert (tmp_path / f"logs-x-9-{utc_day()}.jsonl").read_text() == "a\n"
     assert prune(tmp_path, 0, now)["removed"] == []  # 0 = keep forever
+
+
+def test_info_each_writes_the_same_lines_as_a_loop(tmp_path, monkeypatch):
+    """telemetry.logging.info_each (the bulk operations' per-task lines, e.g. markoverdue's
+    'Mark task with Id ... as OverDue task'): the JSON lines equal those of ``info`` in a loop
+    (apart from the timestamp), carry the span's trace ids, and on a logger with a foreign
+    handler (the standard path) it is a plain loop."""
+    import glob
+    from aca_dotnet_workshop_amd.telemetry.logging import configure_logging, flush_logs, info_each
+
+    monkeypatch.setenv("TT_TELEMETRY_DIR", str(tmp_path))
+    monkeypatch.setenv("TT_LOG_CONSOLE", "0")
+    root = logging.getLogger()
+    saved, saved_tracer = list(root.handlers), tracing._tracer
+    try:
+        configure_logging("api")
+        lg = logging.getLogger("BulkCat")
+        t = tracing.configure("api", str(tmp_path / "spans"))
+        with t.start_span("op", "server") as sp:
+            for i in range(3):
+                lg.info("Mark task with Id: '%s' as OverDue task", f"t{i}")
+            info_each(lg, "Mark task with Id: '%s' as OverDue task", [(f"t{i}",) for i in range(3)])
+        flush_logs()
+        recs = [json.loads(x) for f in glob.glob(str(tmp_path / "logs-api-*")) for x in open(f)]
+        assert len(recs) == 6
+        strip = [{k: v for k, v in r.items() if k != "ts"} for r in recs]
+        assert strip[:3] == strip[3:]
+        assert strip[0]["traceId"] == sp.trace_id and strip[2]["message"] == "Mark task with Id: 't2' as OverDue task"
+        # a foreign handler: the standard logging path, one record per tuple
+        seen = []
+
+        class H(logging.Handler):
+            def emit(self, record):
+                seen.append(record.getMessage())
+        h = H()
+        lg.addHandler(h)
+        info_each(lg, "x %s %s", [(1, 2), (3, 4)])
+        lg.removeHandler(h)
+        assert seen == ["x 1 2", "x 3 4"]
+    finally:
+        tracing._tracer = saved_tracer
+        for h in list(root.handlers):
+            if getattr(h, "_tt", False):
+                root.removeHandler(h)
+                h.close()
+        for h in saved:
+            if h not in root.handlers:
+                root.addHandler(h)
