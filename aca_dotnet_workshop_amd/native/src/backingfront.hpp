@@ -419,26 +419,36 @@ class BackingFront {
     }
     if (!authorize(m, r, "cosmos.write", "cosmos/" + seg[1])) return true;
     count("doc.bulkset");
-    double ru = 0;
-    for (auto& it : items.items) {
-      const Value* v = it.get("value");
-      ru += DocStore::write_ru(v ? (v->t == Value::String ? v->s.size() : dump(*v).size()) : 4);
-    }
-    if (throttled(r, c->store, ru)) return true;
     std::vector<DocStore::BulkItem> batch(items.items.size());
+    double ru = 0;
     for (size_t i = 0; i < items.items.size(); ++i) {
       Value& it = items.items[i];
       DocStore::BulkItem& b = batch[i];
+      bool have_value = false;
       for (size_t f = 0; f < it.keys.size(); ++f) {  // the body is ours: move its strings out
         Value& v = it.items[f];
         const std::string& k = it.keys[f];
-        if (k == "key") b.key = std::move(v.s);
-        else if (k == "value") b.value = v.t == Value::String ? std::move(v.s) : dump(v);
-        else if (k == "etag" && v.t == Value::String && !v.s.empty()) b.etag = std::move(v.s);
-        else if (k == "firstWrite" && v.t == Value::Bool) b.first_write = v.b;
+        if (k == "key") {
+          b.key = std::move(v.s);
+        } else if (k == "value") {
+          have_value = true;
+          if (v.t == Value::String) {
+            b.value = std::move(v.s);  // JSON text: parsed by the store
+          } else {                     // a JSON value: stored as its canonical text, tree kept
+            b.value = dump(v);
+            b.parsed = std::move(v);
+            b.have_parsed = true;
+          }
+        } else if (k == "etag" && v.t == Value::String && !v.s.empty()) {
+          b.etag = std::move(v.s);
+        } else if (k == "firstWrite" && v.t == Value::Bool) {
+          b.first_write = v.b;
+        }
       }
-      if (!it.get("value")) b.value = "null";
+      if (!have_value) b.value = "null";
+      ru += DocStore::write_ru(have_value ? b.value.size() : 4);
     }
+    if (throttled(r, c->store, ru)) return true;
     const std::vector<DocStore::BulkResult> res = c->store->set_many(batch);
     std::string out = "[";
     bool etag_err = false, other_err = false;

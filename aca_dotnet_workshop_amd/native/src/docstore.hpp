@@ -220,23 +220,32 @@ class DocStore {
   std::string set(const std::string& key, const std::string& value, const std::optional<std::string>& etag,
                   bool first_write, int64_t ttl_ms) {
     Value parsed = parse(value);  // validate before taking the lock
+    std::string text(value);
+    std::vector<Doc> graveyard;  // declared before the lock: the replaced version is freed after it
     std::lock_guard<std::mutex> g(mu_);
     int64_t now = now_ms();
-    check_etag(key, etag, first_write, now);
-    uint64_t e = put(key, value, std::move(parsed), ttl_ms > 0 ? now + ttl_ms : 0);
-    log_put(key, value, e, docs_[key].expire_ms);
+    auto it = docs_.find(key);
+    check_etag_at(it, etag, first_write, now);
+    it = put_at(it, key, std::move(text), std::move(parsed), ttl_ms > 0 ? now + ttl_ms : 0, &graveyard);
+    log_put(key, it->second.value, it->second.etag, it->second.expire_ms);
     maybe_compact();
-    return std::to_string(e);
+    return std::to_string(it->second.etag);
   }
 
   // Bulk write (Dapr BulkSet: not atomic -- every item succeeds or fails on its own): values
   // parsed before the lock, then ONE lock hold and ONE log write(2) for the whole batch, instead
   // of one of each per item.  Per item: the new etag, or err 1 (etag precondition) / 2 (invalid
   // JSON) with its detail.
+  // Per item, one lookup of the key (etag check, write and log record share it); a caller that
+  // already holds the value's parse tree (the native front parsed the request body) passes it
+  // in `parsed` with `have_parsed`, and `value` is then its canonical text.  The replaced
+  // documents are freed after the lock is released.
   struct BulkItem {
     std::string key, value;
     std::optional<std::string> etag;
     bool first_write = false;
+    bool have_parsed = false;
+    Value parsed;
   };
   struct BulkResult {
     std::string etag;
@@ -245,35 +254,45 @@ class DocStore {
   };
   std::vector<BulkResult> set_many(std::vector<BulkItem>& items) {
     std::vector<BulkResult> out(items.size());
-    std::vector<Value> parsed(items.size());
     for (size_t i = 0; i < items.size(); ++i) {
+      if (items[i].have_parsed) continue;
       try {
-        parsed[i] = parse(items[i].value);
+        items[i].parsed = parse(items[i].value);
       } catch (const ParseError& e) {
         out[i].err = 2;
         out[i].detail = std::string("invalid JSON: ") + e.what();
       }
     }
-    std::lock_guard<std::mutex> g(mu_);
+    std::vector<Doc> graveyard;
+    graveyard.reserve(items.size());
     {
-      AppLog::BatchScope batch(log_);
-      const int64_t now = now_ms();
-      for (size_t i = 0; i < items.size(); ++i) {
-        if (out[i].err) continue;
-        BulkItem& it = items[i];
-        try {
-          check_etag(it.key, it.etag, it.first_write, now);
-        } catch (const EtagMismatch& e) {
-          out[i].err = 1;
-          out[i].detail = e.what();
-          continue;
+      std::lock_guard<std::mutex> g(mu_);
+      {
+        AppLog::BatchScope batch(log_);
+        const int64_t now = now_ms();
+        for (size_t i = 0; i < items.size(); ++i) {
+          if (out[i].err) continue;
+          BulkItem& it = items[i];
+          auto dit = docs_.find(it.key);
+          const bool exists = dit != docs_.end() && !expired(dit->second, now);
+          if (it.etag && !it.etag->empty()) {
+            if (!exists || *it.etag != std::to_string(dit->second.etag)) {
+              out[i].err = 1;
+              out[i].detail = "possible etag mismatch";
+              continue;
+            }
+          } else if (it.first_write && exists) {
+            out[i].err = 1;
+            out[i].detail = "possible etag mismatch: first-write on existing key without etag";
+            continue;
+          }
+          dit = put_at(dit, it.key, std::move(it.value), std::move(it.parsed), 0, &graveyard);
+          log_put(it.key, dit->second.value, dit->second.etag, dit->second.expire_ms);
+          out[i].etag = std::to_string(dit->second.etag);
         }
-        const uint64_t e = put(it.key, it.value, std::move(parsed[i]), 0);
-        log_put(it.key, it.value, e, docs_[it.key].expire_ms);
-        out[i].etag = std::to_string(e);
       }
+      maybe_compact();
     }
-    maybe_compact();
     return out;
   }
 
@@ -698,7 +717,11 @@ class DocStore {
   static bool expired(const Doc& d, int64_t now) { return d.expire_ms && d.expire_ms <= now; }
 
   void check_etag(const std::string& key, const std::optional<std::string>& etag, bool first_write, int64_t now) {
-    auto it = docs_.find(key);
+    check_etag_at(docs_.find(key), etag, first_write, now);
+  }
+
+  void check_etag_at(std::unordered_map<std::string, Doc>::iterator it, const std::optional<std::string>& etag,
+                     bool first_write, int64_t now) {
     bool exists = it != docs_.end() && !expired(it->second, now);
     if (etag && !etag->empty()) {
       if (!exists || *etag != std::to_string(it->second.etag)) throw EtagMismatch("possible etag mismatch");
@@ -708,32 +731,67 @@ class DocStore {
   }
 
   uint64_t put(const std::string& key, const std::string& value, Value parsed, int64_t expire_ms) {
-    auto it = docs_.find(key);
+    return put_at(docs_.find(key), key, std::string(value), std::move(parsed), expire_ms, nullptr)->second.etag;
+  }
+
+  // Strict equality of two scalars (same type, same bits): equal values have equal index keys
+  // and equal mirror dictionary keys, so an update that leaves a path unchanged keeps its index
+  // entry and its dictionary id without re-keying.
+  static bool same_scalar(const Value* a, const Value* b) {
+    if (!a || !b) return a == b;
+    if (a->t != b->t) return false;
+    switch (a->t) {
+      case Value::Null: return true;
+      case Value::Bool: return a->b == b->b;
+      case Value::Number: return std::memcmp(&a->n, &b->n, sizeof(double)) == 0;
+      case Value::String: return a->s == b->s;
+      default: return false;
+    }
+  }
+
+  // The write itself, at `it` = docs_.find(key) done once by the caller.  Bulk writes pass a
+  // `graveyard` that takes the replaced document's parsed tree and text, so their frees run
+  // after the store lock is released.
+  std::unordered_map<std::string, Doc>::iterator put_at(std::unordered_map<std::string, Doc>::iterator it,
+                                                       const std::string& key, std::string&& value, Value parsed,
+                                                       int64_t expire_ms, std::vector<Doc>* graveyard) {
     uint64_t e = ++etag_;
     if (expire_ms && mirror_.on) mirror_disable();
+    int32_t* reuse = nullptr;
     if (it == docs_.end()) {
       Doc d;
-      d.value = value;
+      live_bytes_ += key.size() + value.size();
+      d.value = std::move(value);
       d.parsed = std::move(parsed);
       d.etag = e;
       d.seq = ++seq_;
       d.expire_ms = expire_ms;
-      live_bytes_ += key.size() + value.size();
       index_add(key, d.parsed);
       it = docs_.emplace(key, std::move(d)).first;
     } else {
-      index_remove(key, it->second.parsed);
+      Doc& d = it->second;
+      index_update(key, d.parsed, parsed);
+      if (mirror_.on && d.mrow < mirror_.live.size() && mirror_.live[d.mrow]) {
+        reuse_.resize(mirror_.cols.size());
+        for (size_t c = 0; c < mirror_.cols.size(); ++c)
+          reuse_[c] = same_column_value(mirror_.cols[c], d.parsed, parsed) ? mirror_.cols[c].ids[d.mrow] : kEncode;
+        reuse = reuse_.data();
+      }
       live_bytes_ += value.size();
-      live_bytes_ -= it->second.value.size();
-      it->second.value = value;
-      it->second.parsed = std::move(parsed);
-      it->second.etag = e;
-      it->second.expire_ms = expire_ms;
-      index_add(key, it->second.parsed);
-      mirror_kill(it->second);
+      live_bytes_ -= d.value.size();
+      if (graveyard) {
+        graveyard->emplace_back();
+        graveyard->back().value.swap(d.value);
+        graveyard->back().parsed = std::move(d.parsed);
+      }
+      d.value = std::move(value);
+      d.parsed = std::move(parsed);
+      d.etag = e;
+      d.expire_ms = expire_ms;
+      mirror_kill(d);
     }
-    if (mirror_.on) mirror_append(*it);
-    return e;
+    if (mirror_.on) mirror_append(*it, reuse);
+    return it;
   }
 
   void erase_locked(const std::string& key, bool log) {
@@ -822,13 +880,27 @@ class DocStore {
     return it->second;
   }
 
-  void mirror_append(std::pair<const std::string, Doc>& kv) {
+  // Whether column `col` of the updated document keeps the previous version's dictionary id.
+  static bool same_column_value(const MirrorColumn& col, const Value& before, const Value& after) {
+    static const std::string kPrefix("\x00keyprefix", 10), kValue("\x00value", 6);
+    if (col.path == kPrefix) return true;  // a function of the key alone
+    if (col.path == kValue)
+      return before.t != Value::Object && after.t != Value::Object && same_scalar(&before, &after);
+    return same_scalar(before.path(col.path), after.path(col.path));
+  }
+
+  // `reuse` (optional, one per column): a dictionary id carried over from the replaced row, or
+  // kEncode to look the value up.
+  void mirror_append(std::pair<const std::string, Doc>& kv, const int32_t* reuse = nullptr) {
     uint32_t r = (uint32_t)mirror_.keys.size();
     mirror_.keys.push_back(&kv.first);
     mirror_.seqs.push_back((int64_t)kv.second.seq);
     mirror_.live.push_back(1);
     std::string k;
-    for (auto& col : mirror_.cols) col.ids.push_back(mirror_encode(col, kv.first, kv.second.parsed, k));
+    for (size_t c = 0; c < mirror_.cols.size(); ++c) {
+      MirrorColumn& col = mirror_.cols[c];
+      col.ids.push_back(reuse && reuse[c] != kEncode ? reuse[c] : mirror_encode(col, kv.first, kv.second.parsed, k));
+    }
     kv.second.mrow = r;
     ++mirror_.live_rows;
     if (mirror_.keys.size() > 65536 && mirror_.keys.size() > 2 * mirror_.live_rows) mirror_compact();
@@ -930,6 +1002,23 @@ class DocStore {
     }
   }
 
+  // Re-index an updated document: paths whose value is unchanged keep their entry.
+  void index_update(const std::string& key, const Value& before, const Value& after) {
+    for (auto& [p, idx] : indexes_) {
+      const Value* a = before.path(p);
+      const Value* b = after.path(p);
+      if (same_scalar(a, b)) continue;
+      if (a && a->t != Value::Array && a->t != Value::Object) {
+        auto it = idx.find(index_key(*a));
+        if (it != idx.end()) {
+          it->second.erase(key);
+          if (it->second.empty()) idx.erase(it);
+        }
+      }
+      if (b && b->t != Value::Array && b->t != Value::Object) idx[index_key(*b)].insert(key);
+    }
+  }
+
   void index_remove(const std::string& key, const Value& doc) {
     for (auto& [p, idx] : indexes_) {
       const Value* v = doc.path(p);
@@ -994,6 +1083,8 @@ class DocStore {
   uint64_t stats_scan_queries_ = 0;
   size_t index_threshold_;
   ColumnMirror mirror_;
+  static constexpr int32_t kEncode = INT32_MIN;  // mirror_append: no id carried over
+  std::vector<int32_t> reuse_;                   // put_at's per-column carried ids (under mu_)
   std::mutex ru_mu_;
   double ru_rate_ = 0, ru_tokens_ = 0, ru_last_ = 0, ru_consumed_ = 0;
   uint64_t ru_throttled_ = 0;
