@@ -58,6 +58,65 @@ struct Grant {
 
 }  // namespace bf
 
+// The items of a bulkset body, scanned without building its tree: a value sent as a JSON
+// value (the data plane's form) is kept as its raw text, whitespace compacted, and parsed once
+// by the store; a value sent as a string holds JSON text.  False (left to Python's handler):
+// invalid JSON, not an array of objects, a key that is not a string, or a TTL write.
+inline bool scan_bulk_items(const std::string& body, std::vector<DocStore::BulkItem>& out) {
+  std::string_view text = body.empty() ? std::string_view("[]") : std::string_view(body);
+  if (!valid(text)) return false;
+  const char* p = ws_end(text.data(), text.data() + text.size());
+  const char* e = text.data() + text.size();
+  if (*p != '[') return false;
+  ++p;
+  while (true) {
+    p = ws_end(p, e);
+    if (*p == ']') return true;
+    if (*p != '{') return false;
+    ++p;
+    DocStore::BulkItem b;
+    bool have_key = false, have_value = false;
+    while (true) {
+      p = ws_end(p, e);
+      if (*p == '}') { ++p; break; }
+      const char* ks = p;
+      p = skip_value(p, e);
+      std::string_view ktok(ks, (size_t)(p - ks));
+      std::string k = ktok.find('\\') == std::string_view::npos ? std::string(ktok.substr(1, ktok.size() - 2))
+                                                               : parse(ktok).s;
+      p = ws_end(ws_end(p, e) + 1, e);  // ':'
+      const char* vs = p;
+      p = skip_value(p, e);
+      std::string_view raw(vs, (size_t)(p - vs));
+      if (k == "key") {
+        if (raw.front() != '"') return false;
+        b.key = raw.find('\\') == std::string_view::npos ? std::string(raw.substr(1, raw.size() - 2)) : parse(raw).s;
+        have_key = true;
+      } else if (k == "value") {
+        have_value = true;
+        b.value = raw.front() == '"' ? parse(raw).s : compact(raw);
+      } else if (k == "etag") {
+        b.etag.reset();
+        if (raw.front() == '"') {
+          std::string s = parse(raw).s;
+          if (!s.empty()) b.etag = std::move(s);
+        }
+      } else if (k == "firstWrite") {
+        b.first_write = raw == "true";
+      } else if (k == "ttlMs") {
+        if (raw.front() != 'n' && raw.front() != '"' && std::strtod(std::string(raw).c_str(), nullptr) != 0) return false;
+      }
+      p = ws_end(p, e);
+      if (*p == ',') ++p;
+    }
+    if (!have_key) return false;
+    if (!have_value) b.value = "null";
+    out.push_back(std::move(b));
+    p = ws_end(p, e);
+    if (*p == ',') ++p;
+  }
+}
+
 class BackingFront {
  public:
   // `threads` event loops share the port via SO_REUSEPORT (connections are spread by the kernel).
@@ -404,50 +463,12 @@ class BackingFront {
       if (it != colls_.end() && it->second->store) c = it->second.get();
     }
     if (!c) return false;
-    Value items;
-    try {
-      items = parse(m.body.empty() ? std::string_view("[]") : std::string_view(m.body));
-    } catch (const std::exception&) {
-      return false;  // Python produces the error response
-    }
-    if (items.t != Value::Array) return false;
-    for (auto& it : items.items) {
-      auto* t = it.get("ttlMs");
-      if (t && t->t == Value::Number && t->n != 0) return false;  // TTL writes go through Python
-      auto* k = it.get("key");
-      if (!k || k->t != Value::String) return false;
-    }
+    std::vector<DocStore::BulkItem> batch;
+    if (!scan_bulk_items(m.body, batch)) return false;  // Python produces the error response
     if (!authorize(m, r, "cosmos.write", "cosmos/" + seg[1])) return true;
     count("doc.bulkset");
-    std::vector<DocStore::BulkItem> batch(items.items.size());
     double ru = 0;
-    for (size_t i = 0; i < items.items.size(); ++i) {
-      Value& it = items.items[i];
-      DocStore::BulkItem& b = batch[i];
-      bool have_value = false;
-      for (size_t f = 0; f < it.keys.size(); ++f) {  // the body is ours: move its strings out
-        Value& v = it.items[f];
-        const std::string& k = it.keys[f];
-        if (k == "key") {
-          b.key = std::move(v.s);
-        } else if (k == "value") {
-          have_value = true;
-          if (v.t == Value::String) {
-            b.value = std::move(v.s);  // JSON text: parsed by the store
-          } else {                     // a JSON value: stored as its canonical text, tree kept
-            b.value = dump(v);
-            b.parsed = std::move(v);
-            b.have_parsed = true;
-          }
-        } else if (k == "etag" && v.t == Value::String && !v.s.empty()) {
-          b.etag = std::move(v.s);
-        } else if (k == "firstWrite" && v.t == Value::Bool) {
-          b.first_write = v.b;
-        }
-      }
-      if (!have_value) b.value = "null";
-      ru += DocStore::write_ru(have_value ? b.value.size() : 4);
-    }
+    for (auto& b : batch) ru += DocStore::write_ru(b.value.size());
     if (throttled(r, c->store, ru)) return true;
     const std::vector<DocStore::BulkResult> res = c->store->set_many(batch);
     std::string out = "[";

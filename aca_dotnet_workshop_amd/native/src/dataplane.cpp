@@ -92,39 +92,7 @@ std::string error_json(std::string_view code, std::string_view msg) {
   return "{\"errorCode\":" + json_str(code) + ",\"message\":" + json_str(msg) + "}";
 }
 
-const char* ws_end(const char* p, const char* e) {
-  while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
-  return p;
-}
-
-// End of the JSON value starting at p (input already validated by tt::Parser).
-const char* skip_value(const char* p, const char* e) {
-  p = ws_end(p, e);
-  if (p >= e) return p;
-  if (*p == '"') {
-    ++p;
-    while (p < e && *p != '"') p += (*p == '\\') ? 2 : 1;
-    return p + 1;
-  }
-  if (*p == '{' || *p == '[') {
-    int depth = 0;
-    while (p < e) {
-      char c = *p;
-      if (c == '"') {
-        p = skip_value(p, e);
-        continue;
-      }
-      if (c == '{' || c == '[') ++depth;
-      if (c == '}' || c == ']') {
-        if (--depth == 0) return p + 1;
-      }
-      ++p;
-    }
-    return p;
-  }
-  while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
-  return p;
-}
+// ws_end / skip_value: tt:: (json.hpp), shared with the backing front
 
 bool valid_json(std::string_view s) { return tt::valid(s); }  // compact(): tt::compact
 
@@ -420,9 +388,13 @@ class DataPlane {
   ev::Handler control_handler() {
     return [this](Message&& m, Reply r) { on_control(std::move(m), std::move(r)); };
   }
-  void flush() { tracer_.flush(); }
+  void flush() {
+    flush_api_log();
+    tracer_.flush();
+  }
   size_t inflight() const { return inflight_; }
   void tick(double now) {
+    flush_api_log();
     for (auto& c : consumers_) c->tick(now);
   }
   void begin_stop() {
@@ -477,8 +449,17 @@ class DataPlane {
                        ",\"category\":\"sidecar.http-info\",\"message\":" + json_str(msg) + ",\"traceId\":\"" +
                        std::string(span.tid()) + "\",\"spanId\":\"" + std::string(span.sid()) +
                        "\",\"plane\":\"native\"}\n";
-    std::fwrite(line.data(), 1, line.size(), stderr);
+    api_log_buf_ += line;
+    if (api_log_buf_.size() >= 32768) flush_api_log();
   }
+  // The lines go out in batches: when 32 KB have gathered and on every loop tick (<= ~50 ms),
+  // one write(2) for many API calls instead of one per call on the unbuffered stderr.
+  void flush_api_log() {
+    if (api_log_buf_.empty()) return;
+    std::fwrite(api_log_buf_.data(), 1, api_log_buf_.size(), stderr);
+    api_log_buf_.clear();
+  }
+  std::string api_log_buf_;
 
   void count(const std::string& op, int status) {
     op_counts_[{op, status}]++;
@@ -1288,7 +1269,11 @@ class DataPlane {
     for (size_t i = 0; i < items.size(); ++i) {
       auto& it = items[i];
       if (i) body += ',';
-      body += "{\"key\":" + json_str(full_key(s, it.key)) + ",\"value\":" + json_str(it.value) +
+      // a value that is a JSON object/array/number/literal goes in as itself (the body was
+      // validated and it.value is its compact text): the store parses it once, no escaping
+      // here and no unescaping there; a JSON string value travels as JSON text in a string
+      const bool as_text = it.value.empty() || it.value[0] == '"';
+      body += "{\"key\":" + json_str(full_key(s, it.key)) + ",\"value\":" + (as_text ? json_str(it.value) : it.value) +
               ",\"etag\":" + (it.etag.empty() ? std::string("null") : json_str(it.etag)) +
               ",\"firstWrite\":" + (it.first_write ? "true" : "false") + ",\"ttlMs\":" + std::to_string(it.ttl_ms) + "}";
     }

@@ -416,6 +416,41 @@ class Validator {
 
 inline bool valid(std::string_view s) { return Validator(s).ok(); }
 
+// Scanning a validated JSON text without building values: end of the whitespace at p, and end
+// of the value starting at p (raw slices of a request body, e.g. the state items' values).
+inline const char* ws_end(const char* p, const char* e) {
+  while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  return p;
+}
+
+inline const char* skip_value(const char* p, const char* e) {
+  p = ws_end(p, e);
+  if (p >= e) return p;
+  if (*p == '"') {
+    ++p;
+    while (p < e && *p != '"') p += (*p == '\\') ? 2 : 1;
+    return p + 1;
+  }
+  if (*p == '{' || *p == '[') {
+    int depth = 0;
+    while (p < e) {
+      char c = *p;
+      if (c == '"') {
+        p = skip_value(p, e);
+        continue;
+      }
+      if (c == '{' || c == '[') ++depth;
+      if (c == '}' || c == ']') {
+        if (--depth == 0) return p + 1;
+      }
+      ++p;
+    }
+    return p;
+  }
+  while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+  return p;
+}
+
 // Copy of a valid JSON text without insignificant whitespace; runs without quotes, backslashes
 // or whitespace are copied 16 bytes at a time.
 inline std::string compact(std::string_view s) {

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "../src/backingfront.hpp"
 #include "../src/docstore.hpp"
 
 using namespace tt;
@@ -43,15 +44,8 @@ int main(int argc, char** argv) {
     }
     body += "]";
     auto t0 = clk::now();
-    Value items = parse(body);
-    std::vector<DocStore::BulkItem> batch(items.items.size());
-    for (size_t k = 0; k < items.items.size(); ++k) {
-      Value& it = items.items[k];
-      batch[k].key = it.get("key")->s;
-      batch[k].value = dump(*it.get("value"));  // what the native front does with a JSON value
-      batch[k].parsed = std::move(*it.get("value"));
-      batch[k].have_parsed = true;
-    }
+    std::vector<DocStore::BulkItem> batch;  // the backing front's scan of the data plane's body
+    if (!scan_bulk_items(body, batch)) { std::fprintf(stderr, "scan failed\n"); return 1; }
     auto t1 = clk::now();
     auto res = store.set_many(batch);
     auto t2 = clk::now();
