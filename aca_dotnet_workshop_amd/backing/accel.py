@@ -135,8 +135,9 @@ class CollectionAccelerator:
     def close(self) -> None:
         self._bg_stop.set()
 
-    def query(self, q: dict[str, Any], prefix: str, store) -> str | None:
-        """JSON result text, or None to let the native engine answer.  Blocking."""
+    def query(self, q: dict[str, Any], prefix: str, store) -> bytes | None:
+        """JSON result text (UTF-8 bytes, as the store built it: the page goes out without a
+        decode/encode round trip), or None to let the native engine answer.  Blocking."""
         if not self.should_accelerate(q, store):
             self.stats["native"] += 1
             return None
@@ -188,9 +189,8 @@ class CollectionAccelerator:
                 self.stats["fallback"] += 1
                 return None
             self.stats["gpu" if k is not None else "cpu"] += 1
-            text, skipped = res
+            out, skipped = res
             self.stats["skipped_rows"] += skipped
-            out = text.decode()
             t2 = time.perf_counter()
             # where an accelerated query spends its time (summed; stats route reports them)
             for key, v in (("lock_wait_ms", t0 - t_wait), ("sync_ms", t1 - t0), ("select_and_results_ms", t2 - t1),

@@ -314,7 +314,7 @@ class BackingServices:
                     except (TypeError, ValueError):
                         pass
 
-            def run() -> str:
+            def run() -> str | bytes:
                 inner = tracer().start_span("query run", "internal", parent=span) if span is not None else None
                 try:
                     q = json.loads(raw)
@@ -331,8 +331,8 @@ class BackingServices:
                 if span is not None:
                     span.end()
                 return problem(400, detail=str(ex))
-            s.charge(s.query_ru(len(text)) - s.query_ru(0))  # result size part: charged after the fact
-            body = text.encode()
+            body = text if isinstance(text, bytes) else text.encode()
+            s.charge(s.query_ru(len(body)) - s.query_ru(0))  # result size part: charged after the fact
             if span is not None:
                 span.set("bytes", len(body))
                 span.end()
