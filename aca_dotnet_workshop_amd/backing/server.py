@@ -280,12 +280,14 @@ class BackingServices:
         async def bulk_set(req: Request) -> Response:
             s = st(req, "cosmos.write")
             items = req.json() or []
-            if (t := throttled(s, sum(s.write_ru(len(str(it.get("value", "")))) for it in items) or 1)) is not None:
+            # a value sent as JSON itself (the native data plane's form) is stored as its compact
+            # text, like the native front does; a string value holds JSON text
+            texts = [v if isinstance(v := it.get("value"), str) else _compact_json(v) for it in items]
+            if (t := throttled(s, sum(s.write_ru(len(v)) for v in texts) or 1)) is not None:
                 return t
             out = []
-            for it in items:
+            for it, value in zip(items, texts):
                 try:
-                    value = it["value"] if isinstance(it["value"], str) else json.dumps(it["value"])
                     ttl = int(it.get("ttlMs") or 0)
                     e = s.set(it["key"], value, it.get("etag") or None, bool(it.get("firstWrite")), ttl)
                     out.append({"key": it["key"], "etag": e})
@@ -347,7 +349,7 @@ class BackingServices:
             for o in (req.json() or {}).get("ops", []):
                 is_del = o.get("op") == "delete"
                 val = o.get("value")
-                ops.append(self.N.TxOp(is_del, o["key"], "" if is_del else (val if isinstance(val, str) else json.dumps(val)),
+                ops.append(self.N.TxOp(is_del, o["key"], "" if is_del else (val if isinstance(val, str) else _compact_json(val)),
                                        o.get("etag") or None, bool(o.get("firstWrite")), int(o.get("ttlMs") or 0)))
             try:
                 s.transact(ops)
@@ -730,6 +732,10 @@ def _entity_scope(entity: str) -> str:
         return "topics/" + entity.split("/subscriptions/")[0]
     return "queues/" + entity
 
+
+
+def _compact_json(v) -> str:
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
 
 async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | None = None,
                         policy: dict[str, Any] | None = None, ready=None, stop: asyncio.Event | None = None) -> None:
