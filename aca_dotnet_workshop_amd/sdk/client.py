@@ -62,6 +62,11 @@ class RawJson(str):
     model serialised once can be saved and published without re-encoding."""
 
 
+class RawJsonBytes(bytes):
+    """JSON text already encoded as UTF-8 (e.g. a page a native codec produced): sent verbatim
+    as ``application/json`` without a decode/encode round trip."""
+
+
 def _value_json(v: Any) -> str:
     if isinstance(v, RawJson):
         return v
@@ -73,6 +78,8 @@ def _encode(data: Any) -> tuple[bytes, str]:
         return b"", "application/json"
     if isinstance(data, RawJson):
         return data.encode(), "application/json"
+    if isinstance(data, RawJsonBytes):
+        return bytes(data), "application/json"
     if isinstance(data, (bytes, bytearray)):
         return bytes(data), "application/octet-stream"
     if isinstance(data, str):

@@ -35,7 +35,7 @@ from pathlib import Path
 
 from ...models import TaskModel, naive_utc, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
-from ...sdk.client import InvocationError, RawJson, client_from_config
+from ...sdk.client import InvocationError, RawJsonBytes, client_from_config
 from ...web.app import WebApp, read_model
 from ...web.http import Request, Response, empty, json_response, text_response
 from ..hosting import create_host, map_openapi, run_host
@@ -162,7 +162,7 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                            n_page)
             if n_overdue:
                 log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", n_overdue)
-                data = RawJson(overdue.decode()) if isinstance(overdue, bytes) else overdue
+                data = RawJsonBytes(overdue) if isinstance(overdue, bytes) else overdue
                 t0 = clock()
                 await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
                 t_mark += clock() - t0
