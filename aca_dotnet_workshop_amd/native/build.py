@@ -1,6 +1,8 @@
 """In-tree builder for the native extensions.
 
 * ``_ttnative``  -- C++17 document store + broker engines (g++/clang++, pybind11).
+* ``bin/ttingress`` -- the environment's native HTTP(S) ingress (``src/ingress.cpp``), spawned by
+  ``platform/ingress.py`` (the Container Apps / Envoy edge equivalent).
 * ``bin/ttsidecar-dataplane`` -- native sidecar data plane executable (epoll HTTP/1.1,
   ``src/dataplane.cpp``), spawned by the Python sidecar when ``TT_SIDECAR_DATAPLANE=native``.
 * ``_ttgpu``     -- HIP kernels for gfx950 (see ``aca_dotnet_workshop_amd/ops``), built by
@@ -83,7 +85,8 @@ def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
     return _build_exe(DATAPLANE, SRC / "dataplane.cpp", sources, force, verbose)
 
 
-def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbose: bool) -> Path:
+def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbose: bool,
+               threads: bool = False) -> Path:
     if not force and not _stale(target, sources):
         return target
     with build_lock(target.name):
@@ -92,12 +95,22 @@ def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbo
         cxx = os.environ.get("CXX", "g++")
         tmp = target.with_name(f".{target.name}.tmp{os.getpid()}")
         cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(main), "-o", str(tmp), "-lssl",
-               "-lcrypto"]
+               "-lcrypto"] + (["-pthread"] if threads else [])
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         os.replace(tmp, target)
     return target
+
+
+INGRESS = HERE / "bin" / "ttingress"
+
+
+def build_ingress(force: bool = False, verbose: bool = False) -> Path:
+    """The environment's native HTTP(S) ingress (src/ingress.cpp), spawned by platform/ingress.py."""
+    sources = [SRC / "ingress.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
+               SRC / "textutil.hpp"]
+    return _build_exe(INGRESS, SRC / "ingress.cpp", sources, force, verbose, threads=True)
 
 
 LOADGEN = HERE / "bin" / "ttloadgen"
@@ -113,3 +126,4 @@ if __name__ == "__main__":
     print(build_native(force="--force" in sys.argv, verbose=True))
     print(build_dataplane(force="--force" in sys.argv, verbose=True))
     print(build_loadgen(force="--force" in sys.argv, verbose=True))
+    print(build_ingress(force="--force" in sys.argv, verbose=True))

@@ -222,6 +222,7 @@ struct Message {
   std::string body;
   std::string tls_peer;  // server side over TLS: SAN names of the verified client certificate
   bool tls = false;      // server side: arrived over TLS
+  std::string peer;      // server side, listeners with `record_peer`: the client's IP address
 
   const std::string* header(std::string_view name) const {
     for (auto& h : headers)
@@ -541,8 +542,8 @@ using Handler = std::function<void(Message&&, Reply)>;
 
 class ServerConn : public IoObj {
  public:
-  ServerConn(Loop& loop, int fd, Handler& h, const TlsContext* tls = nullptr)
-      : loop_(loop), handler_(h), parser_(true) {
+  ServerConn(Loop& loop, int fd, Handler& h, const TlsContext* tls = nullptr, bool record_peer = false)
+      : loop_(loop), handler_(h), parser_(true), record_peer_(record_peer) {
     this->fd = fd;
     if (tls) tls_ = std::make_unique<TlsIo>(*tls, fd);
   }
@@ -618,9 +619,25 @@ class ServerConn : public IoObj {
   std::unique_ptr<TlsIo> tls_;
   std::string tls_peer_;
   bool tls_peer_known_ = false;
+  bool record_peer_ = false;
+  std::string peer_;
 
   ssize_t io_recv(char* buf, size_t n) { return tls_ ? tls_->recv(buf, n) : ::recv(fd, buf, n, 0); }
   ssize_t io_send(const char* p, size_t n) { return tls_ ? tls_->send(p, n) : ::send(fd, p, n, MSG_NOSIGNAL); }
+
+  const std::string& peer_ip() {
+    if (peer_.empty()) {
+      sockaddr_storage ss{};
+      socklen_t len = sizeof ss;
+      char buf[INET6_ADDRSTRLEN] = "local";
+      if (::getpeername(fd, (sockaddr*)&ss, &len) == 0) {
+        if (ss.ss_family == AF_INET) inet_ntop(AF_INET, &((sockaddr_in*)&ss)->sin_addr, buf, sizeof buf);
+        else if (ss.ss_family == AF_INET6) inet_ntop(AF_INET6, &((sockaddr_in6*)&ss)->sin6_addr, buf, sizeof buf);
+      }
+      peer_ = buf;
+    }
+    return peer_;
+  }
 
   void drain() {
     while (!pending_.empty() && pending_.front().ready) {
@@ -659,6 +676,7 @@ class ServerConn : public IoObj {
         m.tls = true;
         m.tls_peer = tls_peer_;
       }
+      if (record_peer_) m.peer = peer_ip();
       bool ka = m.keep_alive();
       bool head = m.method == "HEAD";
       uint64_t seq = head_seq_ + pending_.size();
@@ -728,8 +746,8 @@ inline void Reply::send(int status, const HeaderList& headers, std::string_view 
 
 class Listener : public IoObj {
  public:
-  Listener(Loop& loop, int fd, Handler& h, std::shared_ptr<TlsContext> tls = nullptr)
-      : loop_(loop), handler_(h), tls_(std::move(tls)) {
+  Listener(Loop& loop, int fd, Handler& h, std::shared_ptr<TlsContext> tls = nullptr, bool record_peer = false)
+      : loop_(loop), handler_(h), tls_(std::move(tls)), record_peer_(record_peer) {
     this->fd = fd;
     sockaddr_storage ss{};
     socklen_t len = sizeof ss;
@@ -747,7 +765,7 @@ class Listener : public IoObj {
       else setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
       std::shared_ptr<ServerConn> conn;
       try {
-        conn = std::make_shared<ServerConn>(loop_, c, handler_, tls_.get());
+        conn = std::make_shared<ServerConn>(loop_, c, handler_, tls_.get(), record_peer_);
       } catch (const std::exception&) {
         ::close(c);
         continue;
@@ -764,6 +782,7 @@ class Listener : public IoObj {
   Loop& loop_;
   Handler& handler_;
   std::shared_ptr<TlsContext> tls_;
+  bool record_peer_;
 };
 
 // Bind + listen on `ep`; returns the socket, and the bound port in `port` (tcp) or 0 (unix).
@@ -815,11 +834,13 @@ inline int bind_listen(const Endpoint& ep, bool reuseport, int& port) {
 
 // Returns the bound port (tcp) or 0 (unix); throws on failure.
 // `tls`: serve HTTPS (with `verify_peer`: mutual TLS) on this listener.
+// `record_peer`: messages carry the client's address (`Message::peer`; a proxy's X-Forwarded-For).
 inline int listen_on(Loop& loop, const Endpoint& ep, Handler& h, bool reuseport = false,
-                     std::shared_ptr<IoObj>* listener_out = nullptr, std::shared_ptr<TlsContext> tls = nullptr) {
+                     std::shared_ptr<IoObj>* listener_out = nullptr, std::shared_ptr<TlsContext> tls = nullptr,
+                     bool record_peer = false) {
   int port = 0;
   int fd = bind_listen(ep, reuseport, port);
-  auto l = std::make_shared<Listener>(loop, fd, h, std::move(tls));
+  auto l = std::make_shared<Listener>(loop, fd, h, std::move(tls), record_peer);
   loop.add(l, EPOLLIN);
   if (listener_out) *listener_out = l;
   return port;

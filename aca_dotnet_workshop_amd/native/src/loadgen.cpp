@@ -10,6 +10,9 @@
 // Request bodies come from a file with one body per line (cycled); `--header "name: value"`
 // (repeatable) adds request headers (the frontend entry sends its cookies).  Prints one JSON line:
 // {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
+// HTTPS targets: `--target https://127.0.0.1:port` with `--tls-ca ca.crt` verifies the server
+// certificate (name / address) against that CA, the way a browser trusting it would; without
+// `--tls-ca` the connection is encrypted but unverified.
 //
 //   ttloadgen --target unix:/path/a.sock --target unix:/path/b.sock 
 //       --path /v1.0/invoke/api/method/api/tasks --bodies bodies.txt 
@@ -33,6 +36,7 @@ struct Opts {
   std::vector<ev::Endpoint> targets;
   std::string path = "/", method = "POST", ctype = "application/json", until_field = "completed";
   std::vector<std::string> until_urls;
+  std::string tls_ca;
   std::vector<std::string> bodies{""};
   ev::HeaderList headers;
   int concurrency = 64, batch = 512, steps = 1, expect = 0;
@@ -44,6 +48,12 @@ struct Opts {
 class Gen {
  public:
   Gen(ev::Loop& loop, Opts o) : loop_(loop), client_(loop), o_(std::move(o)) {
+    if (!o_.tls_ca.empty()) {
+      ev::TlsConfig tc;
+      tc.ca = o_.tls_ca;
+      tc.verify_peer = true;
+      client_.set_tls(std::make_shared<ev::TlsContext>(tc, false));
+    }
     hdrs_.emplace_back("content-type", o_.ctype);
     for (auto& h : o_.headers) hdrs_.push_back(h);
     for (std::string u : o_.until_urls) {
@@ -225,6 +235,7 @@ int main(int argc, char** argv) {
     else if (a == "--expect") o.expect = std::atoi(next().c_str());
     else if (a == "--until-url") o.until_urls.push_back(next());
     else if (a == "--until-field") o.until_field = next();
+    else if (a == "--tls-ca") o.tls_ca = next();
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--bodies") {

@@ -15,6 +15,7 @@
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
+#include <arpa/inet.h>
 
 #include <atomic>
 #include <cerrno>
@@ -89,9 +90,15 @@ class TlsIo {
     } else {
       SSL_set_connect_state(ssl_);
       if (!peer_name.empty()) {
-        SSL_set_tlsext_host_name(ssl_, peer_name.c_str());
-        SSL_set_hostflags(ssl_, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS);
-        SSL_set1_host(ssl_, peer_name.c_str());
+        in_addr a4{};
+        if (inet_pton(AF_INET, peer_name.c_str(), &a4) == 1) {
+          // an address, as a browser typed it: checked against the certificate's IP SANs (no SNI)
+          X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl_), peer_name.c_str());
+        } else {
+          SSL_set_tlsext_host_name(ssl_, peer_name.c_str());
+          SSL_set_hostflags(ssl_, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS);
+          SSL_set1_host(ssl_, peer_name.c_str());
+        }
       }
     }
   }

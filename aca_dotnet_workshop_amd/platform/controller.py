@@ -35,7 +35,7 @@ from ..backing.shards import PARTITIONED_FAMILIES, ShardedBackingClient
 from ..web.app import WebApp
 from ..web.http import Request, Response, empty, json_response
 from ..web.server import HttpServer
-from .ingress import Backend, Ingress, IngressRoute
+from .ingress import Backend, IngressRoute, make_ingress
 from .limits import Limits, ResourceLimiter
 from .pki import EnvironmentPki
 from .manifest import Manifest, ManifestError, desired_state, identity_of, template_hash, validate
@@ -407,15 +407,15 @@ class EnvironmentController:
         ing = rt.spec["ingress"]
         rt.ingress_sig = self._ingress_sig(ing)
         route = IngressRoute(rt.name, bool(ing.get("external", False)))
-        rt.ingress = Ingress(route)
+        rt.ingress = make_ingress(route, self.stack.sock_dir)
         port = int(ing.get("port") or 0)
         tls = None
         if route.external and str(ing.get("transport", "auto")).lower() != "http":
-            tls = self.pki.server(f"ingress-{rt.name}", [rt.name]).server_context()
+            tls = self.pki.server(f"ingress-{rt.name}", [rt.name])  # certificate files (CertPair)
         await rt.ingress.start(port or None, self._ingress_uds(rt.name), tls=tls,
                                allow_insecure=_truthy(ing.get("allowInsecure", False)))
         self.event("IngressReady", app=rt.name, external=route.external, port=rt.ingress.public_port,
-                   tls=tls is not None, insecurePort=rt.ingress.insecure_port)
+                   tls=tls is not None, insecurePort=rt.ingress.insecure_port, **rt.ingress.describe())
 
     def _refresh_backends(self, rt: AppRuntime) -> None:
         if rt.ingress is None:
@@ -428,9 +428,8 @@ class EnvironmentController:
                 port = rp.app_port
                 if rp.alive() and port:
                     backends.append(Backend(rev.name, f"http://127.0.0.1:{port}"))
-        rt.ingress.route.backends = backends
         traffic = (rt.spec.get("ingress") or {}).get("traffic") or []
-        rt.ingress.route.weights = {t["revision"]: int(t.get("weight", 0)) for t in traffic}
+        rt.ingress.set_backends(backends, {t["revision"]: int(t.get("weight", 0)) for t in traffic})
 
     async def scale_to(self, rt: AppRuntime, n: int, reason: str) -> None:
         async with self._lock:
@@ -534,7 +533,7 @@ class EnvironmentController:
         if rule.type == "http":
             if rt.ingress is None:
                 return 0.0
-            return float(rt.ingress.route.inflight)  # total in-flight; the rule target is per replica
+            return float(rt.ingress.inflight)  # total in-flight; the rule target is per replica
         if rule.type in ("cpu", "memory"):
             import psutil
             vals = []
@@ -589,8 +588,8 @@ class EnvironmentController:
                     "external": ing.route.external,
                     "fqdn": f"{'https' if ing.tls else 'http'}://127.0.0.1:{ing.public_port}",
                     "httpUrl": f"http://127.0.0.1:{ing.insecure_port}" if ing.insecure_port else None,
-                    "internalUrl": f"unix:{self._ingress_uds(rt.name)}:", "inflight": ing.route.inflight,
-                    "requests": ing.route.requests},
+                    "internalUrl": f"unix:{self._ingress_uds(rt.name)}:", "inflight": ing.inflight,
+                    "requests": ing.requests, **ing.describe()},
             }
         limits = {**self.limiter.describe(),
                   "replicas": {n: {"cpu": st.limits.cpu, "memoryBytes": st.limits.memory, "peakRssBytes": st.peak_rss,

@@ -80,6 +80,9 @@ def parse() -> argparse.Namespace:
                     help="frontend: manifest-deployed environment, load at the frontend's POST /Tasks/Create "
                          "(SURVEY §3.1); api-sidecar: round 2's LocalStack with load at the API sidecars")
     ap.add_argument("--frontend-replicas", type=int, default=0, help="frontend replicas (0 = size to the CPU share)")
+    ap.add_argument("--ingress", choices=("native", "python", "bypass"), default="native",
+                    help="where --entry frontend load enters: the frontend's external HTTPS ingress (native/bin/"
+                         "ttingress, or the asyncio proxy), or bypass it and balance over the frontend replicas")
     ap.add_argument("--mtls", type=int, choices=(0, 1), default=1, help="sidecar-to-sidecar mutual TLS (ACA default: on)")
     ap.add_argument("--ru-per-s", type=float, default=0.0,
                     help="Cosmos container throughput budget in RU/s (reference: 4000 autoscale max); 0 = unlimited")
@@ -228,6 +231,7 @@ class OverdueSweeper:
         return {"sweeps": len(self.runs), "errors": len(self.errors),
                 "sweep_p50_ms": round(ms[len(ms) // 2], 2) if ms else None,
                 "sweep_max_ms": round(ms[-1], 2) if ms else None,
+                "sweep_ms": [round(d * 1e3, 2) for d, _ in self.runs],  # every sweep, in run order
                 "tasks_marked_overdue": sum(r.get("markedOverdue", 0) for _, r in self.runs),
                 "pages": sum(r.get("pages", 0) for _, r in self.runs),
                 # the job's two hops (GET api/overduetasks, POST markoverdue), summed over sweeps
@@ -541,13 +545,15 @@ def frontend_topology(cores: float) -> tuple[int, int, int]:
     return fe, fe, max(1, min(8, int(cores / 8)))
 
 
-def _form_session(port: int, created_by: str) -> tuple[str, str]:
+def _form_session(base_url: str, created_by: str, ca_file: str | None = None) -> tuple[str, str]:
     """What a browser holds after opening Tasks/Create: (Cookie header, antiforgery token)."""
     import re
+    import ssl
     import urllib.request
-    req = urllib.request.Request(f"http://127.0.0.1:{port}/Tasks/Create",
+    req = urllib.request.Request(f"{base_url}/Tasks/Create",
                                  headers={"Cookie": f"TasksCreatedByCookie={created_by}"})
-    with urllib.request.urlopen(req, timeout=30) as r:
+    ctx = ssl.create_default_context(cafile=ca_file) if base_url.startswith("https") else None
+    with urllib.request.urlopen(req, timeout=30, context=ctx) as r:
         html = r.read().decode()
         cookies = [c.split(";", 1)[0] for c in r.headers.get_all("Set-Cookie") or []]
     m = re.search(r'name="__RequestVerificationToken" value="([^"]+)"', html)
@@ -569,16 +575,21 @@ def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
             for i in range(batch)]
 
 
-def run_form_loadgen(exe: str, ports: list[int], cookie: str, counts_url: str | list[str], steps: int, batch: int,
-                     conc: int, bodies_file: str, shared: tuple[int, int] | None = None) -> tuple[float, dict]:
+def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int, batch: int,
+                     conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
+                     ca_file: str | None = None) -> tuple[float, dict]:
+    """``targets``: ``host:port`` (a frontend replica) or ``https://host:port`` (the external
+    ingress; ``ca_file`` -- the environment CA -- verifies its certificate like a browser)."""
     import subprocess
     cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies_file, "--content-type",
            "application/x-www-form-urlencoded", "--header", f"Cookie: {cookie}", "--concurrency", str(conc),
            "--batch", str(batch), "--steps", str(steps), "--expect", "302", *_until(counts_url)]
     if shared is not None:
         cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
-    for p in ports:
-        cmd += ["--target", f"127.0.0.1:{p}"]
+    if ca_file:
+        cmd += ["--tls-ca", ca_file]
+    for t in targets:
+        cmd += ["--target", t]
     t0 = time.perf_counter()
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     dt = time.perf_counter() - t0
@@ -598,6 +609,37 @@ def _cpu_by_role(stack) -> dict[str, float]:
                 role = app + "." + k.rsplit(".", 1)[1]
         out[role] = out.get(role, 0.0) + v
     return out
+
+
+# cores held back for the external ingress when load enters through it (uncapped, like Envoy)
+INGRESS_RESERVE = 1.0
+
+
+def _ingress_cpu(env) -> dict[str, float]:
+    """CPU seconds so far of the frontend's native ingress process (empty for the asyncio
+    ingress, which runs inside the controller, or without an ingress)."""
+    import psutil
+    rt = env.ctl.apps.get(FRONTEND)
+    proc = getattr(getattr(rt, "ingress", None), "proc", None)
+    if proc is None:
+        return {}
+    try:
+        t = psutil.Process(proc.pid).cpu_times()
+        return {"ingress": t.user + t.system}
+    except psutil.Error:
+        return {}
+
+
+def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
+    """Microseconds of CPU per created task: in total and per role, from the timed region's
+    cores-busy figures (a box-independent view of the headline: throughput = cores / cost)."""
+    if tasks_per_s <= 0:
+        return {}
+    roles = {k: round(v / tasks_per_s * 1e6, 1) for k, v in sorted(util.items())}
+    return {"total": round(sum(util.values()) / tasks_per_s * 1e6, 1),
+            "apps_frontend_plus_api": round((util.get(f"{FRONTEND}.app", 0.0) + util.get(f"{API}.app", 0.0))
+                                            / tasks_per_s * 1e6, 1),
+            "by_role": roles}
 
 
 # relative CPU per created task of one replica of each app (app process + its sidecar), from the
@@ -624,11 +666,15 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     # replicas in proportion to each app's measured CPU per created task (app + its sidecar; the
     # API does the most work per task, the processor the least: profiles/r3_mtls_cost.md); each
     # reference app module sets its own resources, so the manifest takes one cap per app
+    ingress = a.ingress != "bypass"
     if a.app_cpu:
         caps = {"frontend": a.app_cpu, "api": a.app_cpu, "processor": a.app_cpu}
     else:
         w = CPU_WEIGHT
-        unit = (cores - 2.0) / (fe * w["frontend"] + api * w["api"] + proc * w["processor"])
+        # the platform's own processes are not replicas (no cap): the backing services and the
+        # load generator, plus the external ingress when load enters through it
+        reserve = 2.0 + (INGRESS_RESERVE if ingress else 0.0)
+        unit = (cores - reserve) / (fe * w["frontend"] + api * w["api"] + proc * w["processor"])
         caps = {k: round(max(0.25, unit * w[k]), 2) for k in w}
     app_cpu = caps["frontend"]
     for b in (build_native, build_dataplane, build_loadgen):  # once, before any child needs them
@@ -639,6 +685,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     # the environment's processes inherit these: JSON logs to the telemetry dir only (Log
     # Analytics), the rank's own GPU for the store's query path, the sweep's mirrored columns
     os.environ.update({"TT_LOG_CONSOLE": "0", **rank_device_env()})
+    if ingress:  # the external ingress's data plane and its event loops (platform/ingress.py)
+        os.environ["TT_INGRESS"] = a.ingress
+        os.environ.setdefault("TT_INGRESS_THREADS", str(max(1, min(4, round(cores / 8)))))
     if sweep:
         os.environ["TT_QUERY_MIRROR_PATHS"] = "taskDueDate,isCompleted,isOverDue,taskCreatedOn"
     overrides = {"backendApiMinReplicas": api, "backendApiMaxReplicas": api, "frontendMinReplicas": fe,
@@ -661,11 +710,20 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         env.start()
         lim = env.ctl.limiter.describe()
         fe_ports = [r.app_port for r in env.replicas(FRONTEND)]
+        ca_file = None
+        if ingress:  # a browser's entry: the frontend's external ingress, HTTPS verified by the env CA
+            ing = env.ctl.apps[FRONTEND].ingress
+            ca_file = str(env.ctl.pki.ca_crt)
+            targets = [f"https://127.0.0.1:{ing.public_port}"]
+            session_url = targets[0]
+        else:
+            targets = [f"127.0.0.1:{p}" for p in fe_ports]
+            session_url = f"http://127.0.0.1:{fe_ports[0]}"
         backing = env.backing_url
         shards = env.ctl.shards or [backing]
         entity = "tasksavedtopic/subscriptions/tasksmanager-backend-processor"
         counts_url = [f"{u}/servicebus/taskstracker/counts?entity={entity}" for u in shards]
-        cookie, token = _form_session(fe_ports[0], "bench@bench.local")
+        cookie, token = _form_session(session_url, "bench@bench.local", ca_file)
         bodies_file = os.path.join(root, "form-bodies.txt")
         with open(bodies_file, "wb") as f:
             f.write(b"\n".join(_form_bodies(a.batch, token, a.past_due_every if sweep else 0)) + b"\n")
@@ -679,20 +737,21 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
             sweeper.start()
         if a.warmup:
-            run_form_loadgen(exe, fe_ports, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
-                             (gbase, stride) if shared else None)
+            run_form_loadgen(exe, targets, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
+                             (gbase, stride) if shared else None, ca_file)
         d.barrier()
         device_sync()
         me = psutil.Process()
         cpu0 = _cpu_by_role(env.stack)
         t = me.cpu_times()
         cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
+        cpu0.update(_ingress_cpu(env))
         ru0 = _collection_stats(backing).get("throughput", {})
         acc0 = _accel_stats(shards) if sweeper is not None else {}
         if sweeper is not None:
             sweeper.reset()  # sweeps of the timed region only
-        dt, report = run_form_loadgen(exe, fe_ports, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
-                                      (gbase + stride * a.warmup, stride) if shared else None)
+        dt, report = run_form_loadgen(exe, targets, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
+                                      (gbase + stride * a.warmup, stride) if shared else None, ca_file)
         device_sync()
         d.barrier()
         if sweeper is not None:
@@ -700,6 +759,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         cpu1 = _cpu_by_role(env.stack)
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
+        cpu1.update(_ingress_cpu(env))
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
         util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
@@ -746,11 +806,13 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])
+        cpu_us = cpu_per_task(util, a.batch * a.steps / dt)  # this rank's CPU over this rank's tasks
         ru_used = None
         if ru0 and ru1 and "ru_consumed" in ru1:
             ru_used = round((ru1["ru_consumed"] - ru0.get("ru_consumed", 0.0)) / dt, 1)
         if d.rank == 0:
             print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
+                              "cpu_us_per_task": cpu_us,
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "resource_limits": lim}), file=sys.stderr, flush=True)
             print(json.dumps({
@@ -768,7 +830,10 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "environment": "deploy/main.yaml via the platform controller",
                            "entry": "frontend", "entry_request": "POST /Tasks/Create (form, antiforgery + identity "
                                                                   "cookies) -> 302, redirect not followed",
-                           "ingress": "bypassed: the load generator balances over the frontend replicas",
+                           "ingress": (f"external HTTPS ({a.ingress}), {os.environ.get('TT_INGRESS_THREADS')} event "
+                                       "loops, certificate verified against the environment CA"
+                                       if ingress else "bypassed: the load generator balances over the frontend replicas"),
+                           "cpu_us_per_task": cpu_us,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
                                           "mechanism": lim.get("cpu"), "mode": lim.get("mode")},

@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# Round 3 (b): GPU tests, the 1e8-row page benchmark + kernel trace, then the headline bench
+# under the driver's flags (frontend entry, mTLS) at two concurrencies.
+set -euo pipefail
+export TMPDIR=/tmp
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r3b_pytest_gpu.log 2>&1
+timeout -k 10 400 python bench_query.py --rows 100000000 --iters 20 --page --no-cpu-native > gpurun_out/r3b_bench_query.json 2> gpurun_out/r3b_bench_query.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r3b_prof -o page -- python3 bench_query.py --rows 100000000 --iters 10 --page --no-cpu-native > gpurun_out/r3b_prof.log 2>&1
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/r3b_bench_fe.json 2> gpurun_out/r3b_bench_fe.err
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 --concurrency 384 > gpurun_out/r3b_bench_fe_c384.json 2> gpurun_out/r3b_bench_fe_c384.err
+echo ALL_OK

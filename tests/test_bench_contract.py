@@ -40,6 +40,13 @@ def test_bench_single_process():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 1, 2, 1)
+    cfg = lines[0]["config"]
+    # load enters at the frontend's external HTTPS ingress (native data plane), like a browser's
+    assert cfg["entry"] == "frontend" and cfg["ingress"].startswith("external HTTPS (native)")
+    cpu = cfg["cpu_us_per_task"]
+    assert cpu["total"] > 0 and cpu["by_role"]["ingress"] > 0 and cpu["apps_frontend_plus_api"] > 0
+    sw = cfg["overdue_sweeps"]
+    assert len(sw["sweep_ms"]) == sw["sweeps"] and max(sw["sweep_ms"], default=0) == (sw["sweep_max_ms"] or 0)
 
 
 def test_bench_api_sidecar_entry_single_process():
