@@ -167,7 +167,7 @@ def _lists():
         try:
             from ..native import load
             n = load()
-            _native_lists = (n.tasks_mark_overdue, n.tasks_overdue_filter)
+            _native_lists = (n.tasks_mark_overdue, n.tasks_overdue_filter, n.tasks_conditional_mark)
         except Exception:
             _native_lists = False
     return _native_lists
@@ -179,6 +179,38 @@ def mark_overdue_wire(body: bytes) -> tuple[list[str], bytes] | None:
     ``[TaskModel]`` (``native/src/taskcodec.hpp``)."""
     fns = _lists()
     return fns[0](body) if fns else None
+
+
+def conditional_mark_wire(got: bytes) -> tuple[list[str], bytes, int] | None:
+    """The state API's bulk-get answer for a markoverdue page (``[{"key", "data", "etag"}]``) ->
+    (ids to mark, a bulk-save body setting ``isOverDue`` on the STORED task where it is still
+    open and not yet overdue, each item ETag-guarded with first-write concurrency, the number
+    skipped: completed, already overdue or deleted).  Native (``taskcodec.hpp
+    conditional_mark``) or this module's Python twin; ``None``: outside the TaskModel envelope."""
+    fns = _lists()
+    if fns:
+        return fns[2](got)
+    try:
+        rows = json.loads(got)
+    except ValueError:
+        return None
+    ids, items, skipped = [], [], 0
+    for r in rows:
+        data = r.get("data")
+        if data is None:
+            skipped += 1
+            continue
+        t = TaskModel.model_validate(data)
+        if t.is_completed or t.is_over_due:
+            skipped += 1
+            continue
+        t.is_over_due = True
+        item: dict[str, Any] = {"key": r["key"], "value": t.to_wire(), "options": {"concurrency": "first-write"}}
+        if r.get("etag"):
+            item["etag"] = r["etag"]
+        items.append(item)
+        ids.append(str(t.task_id))
+    return ids, json.dumps(items, separators=(",", ":")).encode(), skipped
 
 
 def tasks_from_query_wire(body: bytes, by_created: bool = False) -> tuple[int, bytes, bool] | None:

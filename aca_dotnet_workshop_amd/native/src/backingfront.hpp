@@ -357,6 +357,8 @@ class BackingFront {
     if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(m, r, seg)) return;
     if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkset" && m.method == "POST" && handle_bulkset(m, r, seg))
       return;
+    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkget" && m.method == "POST" && handle_bulkget(m, r, seg))
+      return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
   }
@@ -486,6 +488,42 @@ class BackingFront {
     }
     out += "]";
     r.send(etag_err ? 412 : other_err ? 400 : 200, {{"content-type", "application/json"}}, out);
+    return true;
+  }
+
+  // POST .../bulkget {"keys": [...]} -> [{"key", "data" (the stored JSON, as is), "etag"} | {"key"}]
+  // in key order (a missing document has no data): the read half of a bulk read-modify-write
+  bool handle_bulkget(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
+    Coll* c = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
+      if (it != colls_.end() && it->second->store) c = it->second.get();
+    }
+    if (!c) return false;
+    Value body;
+    try {
+      body = parse(m.body);
+    } catch (const ParseError&) {
+      return false;  // Python produces the error response
+    }
+    const Value* keys = body.get("keys");
+    if (!keys || keys->t != Value::Array) return false;
+    for (auto& k : keys->items)
+      if (k.t != Value::String) return false;
+    if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
+    count("doc.bulkget");
+    if (throttled(r, c->store, DocStore::read_ru(0) * (double)std::max<size_t>(1, keys->items.size()))) return true;
+    std::string out = "[";
+    for (size_t i = 0; i < keys->items.size(); ++i) {
+      const std::string& k = keys->items[i].s;
+      if (i) out += ", ";
+      out += "{\"key\": " + bf::jstr(k);
+      if (auto v = c->store->get(k)) out += ", \"data\": " + v->first + ", \"etag\": " + bf::jstr(v->second);
+      out += "}";
+    }
+    out += "]";
+    r.send(200, {{"content-type", "application/json"}}, out);
     return true;
   }
 

@@ -9,6 +9,7 @@
 //   POST|GET|...  /v1.0/invoke/{appId}/method/{*path}   service invocation (self or peer)
 //   POST|PUT      /v1.0/state/{store}                   save (backing cosmos / redis stores)
 //   GET|DELETE    /v1.0/state/{store}/{key}             get / delete
+//   POST          /v1.0/state/{store}/bulk              bulk get (per-shard fan-out, raw values)
 //   POST|PUT      /v1.0-alpha1/state/{store}/query      query (forwarded to the backing planner)
 //   POST|PUT      /v1.0/publish/{pubsub}/{*topic}        publish (backing service bus / redis)
 //   internal endpoint                                   peer sidecar -> this app
@@ -878,6 +879,10 @@ class DataPlane {
             state_get(std::move(m), std::move(r), it->second, unquote(seg[3]), path);
             return;
           }
+          if (seg.size() == 4 && (m.method == "POST" || m.method == "PUT") && lower(seg[3]) == "bulk") {
+            state_bulk_get(std::move(m), std::move(r), it->second, path);
+            return;
+          }
           if (seg.size() == 4 && m.method == "DELETE") {
             state_delete(std::move(m), std::move(r), it->second, unquote(seg[3]), path);
             return;
@@ -1303,6 +1308,125 @@ class DataPlane {
                       const std::string* et = res.resp.header("etag");
                       d->send(200, {{"etag", et ? *et : ""}, {"content-type", "application/json"}}, res.resp.body);
                     });
+  }
+
+  // POST /v1.0/state/{store}/bulk {"keys": [...]}: one bulkget per shard the keys hash to,
+  // answered in request order as [{"key", "data", "etag"} | {"key"}] -- the stored JSON goes
+  // through as raw slices (the read half of the API's conditional markoverdue).
+  struct BulkGet {
+    std::vector<std::string> keys, full;  // as asked / with the store's key prefix
+    std::vector<std::string> bodies;      // the shards' answers (the slices below point into them)
+    std::unordered_map<std::string, std::pair<std::string_view, std::string>> found;  // full key -> data, etag
+    size_t left = 0;
+    bool failed = false;
+    std::string error;
+  };
+
+  static bool scan_bulkget(const std::string& body, BulkGet& bg) {
+    const char* p = tt::ws_end(body.data(), body.data() + body.size());
+    const char* e = body.data() + body.size();
+    if (p >= e || *p != '[') return false;
+    ++p;
+    while (true) {
+      p = tt::ws_end(p, e);
+      if (p < e && *p == ']') return true;
+      if (p >= e || *p != '{') return false;
+      ++p;
+      std::string key, etag;
+      std::string_view data;
+      while (true) {
+        p = tt::ws_end(p, e);
+        if (p < e && *p == '}') {
+          ++p;
+          break;
+        }
+        const char* ks = p;
+        p = tt::skip_value(p, e);
+        std::string_view name(ks, (size_t)(p - ks));
+        p = tt::ws_end(p, e);
+        if (p >= e || *p != ':') return false;
+        const char* vs = tt::ws_end(p + 1, e);
+        p = tt::skip_value(vs, e);
+        std::string_view val(vs, (size_t)(p - vs));
+        try {
+          if (name == "\"key\"") key = tt::parse(val).s;
+          else if (name == "\"etag\"") etag = tt::parse(val).s;
+          else if (name == "\"data\"") data = val;
+        } catch (const std::exception&) {
+          return false;
+        }
+        p = tt::ws_end(p, e);
+        if (p < e && *p == ',') ++p;
+      }
+      if (!data.empty()) bg.found[key] = {data, std::move(etag)};
+      p = tt::ws_end(p, e);
+      if (p < e && *p == ',') ++p;
+    }
+  }
+
+  void state_bulk_get(Message&& m, Reply&& r, const Store& s, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.bulkget", path);
+    auto bg = std::make_shared<BulkGet>();
+    try {
+      Value v = parse(m.body.empty() ? std::string("{}") : m.body);
+      const Value* ks = v.get("keys");
+      if (ks && ks->t == Value::Array)
+        for (auto& k : ks->items) {
+          if (k.t != Value::String) throw std::runtime_error("keys must be strings");
+          bg->keys.push_back(k.s);
+          bg->full.push_back(full_key(s, k.s));
+        }
+    } catch (const std::exception& ex) {
+      d->error(400, "ERR_MALFORMED_REQUEST", std::string("bulk get: ") + ex.what());
+      return;
+    }
+    std::map<size_t, std::vector<size_t>> by_shard;
+    for (size_t i = 0; i < bg->full.size(); ++i) by_shard[s.shards.empty() ? 0 : s.shard_of(bg->full[i])].push_back(i);
+    if (by_shard.empty()) {
+      d->send(200, {{"content-type", "application/json"}}, "[]");
+      return;
+    }
+    bg->left = by_shard.size();
+    bg->bodies.resize(by_shard.size());
+    HeaderList h = s.auth;
+    h.emplace_back("content-type", "application/json");
+    size_t slot = 0;
+    for (auto& kv : by_shard) {
+      std::string body = "{\"keys\":[";
+      for (size_t j = 0; j < kv.second.size(); ++j) body += (j ? "," : "") + json_str(bg->full[kv.second[j]]);
+      body += "]}";
+      store_request(s.ep(kv.first), "POST", s.coll_path + "/bulkget", h, std::move(body),
+                    [d, bg, slot](ClientResult&& res) {
+                      if (res.err || res.resp.status != 200) {
+                        bg->failed = true;
+                        if (bg->error.empty())
+                          bg->error = res.err ? errno_text(res.err) : "HTTP " + std::to_string(res.resp.status);
+                      } else {
+                        bg->bodies[slot] = std::move(res.resp.body);
+                        if (!scan_bulkget(bg->bodies[slot], *bg)) bg->failed = true, bg->error = "unreadable bulkget";
+                      }
+                      if (--bg->left) return;
+                      if (bg->failed) {
+                        d->error(500, "ERR_STATE_BULK_GET", "bulk get: " + bg->error);
+                        return;
+                      }
+                      std::string out = "[";
+                      for (size_t i = 0; i < bg->keys.size(); ++i) {
+                        out += i ? ",{\"key\":" : "{\"key\":";
+                        out += json_str(bg->keys[i]);
+                        auto it = bg->found.find(bg->full[i]);
+                        if (it != bg->found.end()) {
+                          out += ",\"data\":";
+                          out.append(it->second.first);
+                          out += ",\"etag\":" + json_str(it->second.second);
+                        }
+                        out += '}';
+                      }
+                      out += ']';
+                      d->send(200, {{"content-type", "application/json"}}, out);
+                    });
+      ++slot;
+    }
   }
 
   // sidecar/runtime.py h_state_query: the filter goes to the backing's query route (hash

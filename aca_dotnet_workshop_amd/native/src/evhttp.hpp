@@ -459,6 +459,16 @@ inline void write_response(std::string& out, int status, const HeaderList& heade
   if (!head_request && status != 204 && status != 304) out.append(body);
 }
 
+// Whether a read loop on level-triggered epoll can stop after a read of `n` bytes into a
+// `cap`-byte buffer without another (failing, EAGAIN) read: plain sockets -- a short read
+// drained the socket; TLS -- a record shorter than the 16 KB maximum with nothing left in
+// OpenSSL's buffer (a full record means more of a large message is probably queued).  Bytes
+// still in the kernel make epoll report the socket again.
+inline bool read_done(const TlsIo* tls, size_t n, size_t cap) {
+  if (!tls) return n < cap;
+  return n < 16384 && !tls->pending();
+}
+
 // ------------------------------------------------------------------------------ endpoints
 struct Endpoint {
   bool unix_socket = true;
@@ -556,7 +566,7 @@ class ServerConn : public IoObj {
         ssize_t n = io_recv(buf, sizeof buf);
         if (n > 0) {
           in_.append(buf, (size_t)n);
-          if (!tls_ && (size_t)n < sizeof buf) break;  // TLS: drain OpenSSL's buffered records too
+          if (short_read((size_t)n, sizeof buf)) break;
           continue;
         }
         if (n == 0) {
@@ -624,6 +634,7 @@ class ServerConn : public IoObj {
 
   ssize_t io_recv(char* buf, size_t n) { return tls_ ? tls_->recv(buf, n) : ::recv(fd, buf, n, 0); }
   ssize_t io_send(const char* p, size_t n) { return tls_ ? tls_->send(p, n) : ::send(fd, p, n, MSG_NOSIGNAL); }
+  bool short_read(size_t n, size_t cap) const { return read_done(tls_.get(), n, cap); }
 
   const std::string& peer_ip() {
     if (peer_.empty()) {
@@ -883,6 +894,7 @@ class ClientConn : public IoObj {
 
   ssize_t io_recv(char* buf, size_t n) { return tls_ ? tls_->recv(buf, n) : ::recv(fd, buf, n, 0); }
   ssize_t io_send(const char* p, size_t n) { return tls_ ? tls_->send(p, n) : ::send(fd, p, n, MSG_NOSIGNAL); }
+  bool short_read(size_t n, size_t cap) const { return read_done(tls_.get(), n, cap); }
 
  private:
   friend class Client;
@@ -1115,7 +1127,7 @@ inline void ClientConn::on_event(uint32_t ev) {
       if (n > 0) {
         in_.append(buf, (size_t)n);
         got_bytes_ = true;
-        if (!tls_ && (size_t)n < sizeof buf) break;
+        if (short_read((size_t)n, sizeof buf)) break;
         continue;
       }
       if (n == 0) {

@@ -292,6 +292,21 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(l, py::bytes(bulk));
   });
 
+  // bulk-get answer for a markoverdue page -> (ids marked, conditional bulk-save body, skipped)
+  // or None (taskcodec.hpp conditional_mark).
+  m.def("tasks_conditional_mark", [](py::bytes got) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(got.ptr(), &p, &n) != 0) throw py::error_already_set();
+    std::vector<std::string> ids;
+    std::string bulk;
+    size_t skipped = 0;
+    if (!taskcodec::conditional_mark(std::string_view(p, (size_t)n), bulk, ids, skipped)) return py::none();
+    py::list l(ids.size());
+    for (size_t i = 0; i < ids.size(); ++i) l[i] = py::str(ids[i]);
+    return py::make_tuple(l, py::bytes(bulk), skipped);
+  });
+
   // overdue page + run date (YYYY-MM-DD) -> (retrieved, kept, TaskModel JSON array) or None.
   m.def("tasks_overdue_filter", [](py::bytes body, const std::string& run_day) -> py::object {
     char* p;

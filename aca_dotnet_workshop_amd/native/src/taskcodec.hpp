@@ -476,6 +476,52 @@ inline bool mark_overdue(std::string_view body, std::vector<std::string>& ids, s
   return true;
 }
 
+// The conditional half of markoverdue: the state API's bulk-get answer for the page's ids
+// ([{"key", "data", "etag"} | {"key"}]) -> a bulk save that sets isOverDue on the STORED task
+// (not the caller's copy) only where it is still open and not yet overdue, each item guarded by
+// the ETag it was read with (first-write): a completion that lands between the sweep's query
+// and this save makes the save fail for that item (409) instead of reverting it.  `ids`: the
+// tasks written; `skipped`: completed / already overdue / deleted ones.
+inline bool conditional_mark(std::string_view got, std::string& bulk, std::vector<std::string>& ids,
+                             size_t& skipped) {
+  tt::Value doc;
+  if (!parse_array(got, doc)) return false;
+  ids.clear();
+  skipped = 0;
+  bulk.assign("[");
+  std::string id, day;
+  for (const auto& it : doc.items) {
+    if (it.t != tt::Value::Object) return false;
+    const tt::Value* key = it.get("key");
+    const tt::Value* data = it.get("data");
+    const tt::Value* etag = it.get("etag");
+    if (key == nullptr || key->t != tt::Value::String) return false;
+    if (data == nullptr || data->t == tt::Value::Null) {  // deleted since the sweep's query
+      ++skipped;
+      continue;
+    }
+    const tt::Value* f[8];
+    if (!task_fields(*data, f)) return false;
+    if ((f[6] && f[6]->t == tt::Value::Bool && f[6]->b) || (f[7] && f[7]->t == tt::Value::Bool && f[7]->b)) {
+      ++skipped;
+      continue;
+    }
+    if (ids.size()) bulk += ',';
+    bulk += "{\"key\":";
+    tt::escape_to(bulk, key->s);
+    bulk += ",\"value\":";
+    if (!write_task(*data, true, bulk, id, day)) return false;
+    if (etag != nullptr && etag->t == tt::Value::String && !etag->s.empty()) {
+      bulk += ",\"etag\":";
+      tt::escape_to(bulk, etag->s);
+    }
+    bulk += ",\"options\":{\"concurrency\":\"first-write\"}}";
+    ids.push_back(id);
+  }
+  bulk += ']';
+  return true;
+}
+
 // The cron job's filter (ScheduledTasksManagerController.cs:31-36): of the API's overdue page,
 // the tasks whose due date is before the run's date (UTC), as a TaskModel JSON array; also the
 // page's size.

@@ -427,7 +427,10 @@ class EnvironmentController:
             for rp in rev.replicas:
                 port = rp.app_port
                 if rp.alive() and port:
-                    backends.append(Backend(rev.name, f"http://127.0.0.1:{port}"))
+                    # the replica's local socket when it serves one (the environment network
+                    # between the ingress and a replica is this host's), else its TCP port
+                    uds = rp.app_uds if rp.app_uds and os.path.exists(rp.app_uds) else None
+                    backends.append(Backend(rev.name, f"unix:{uds}:" if uds else f"http://127.0.0.1:{port}"))
         traffic = (rt.spec.get("ingress") or {}).get("traffic") or []
         rt.ingress.set_backends(backends, {t["revision"]: int(t.get("weight", 0)) for t in traffic})
 

@@ -43,6 +43,7 @@ class ReplicaProc:
     started: float = field(default_factory=time.time)
     fixed_app_port: int | None = None  # container replicas: the port the platform mapped for the app
     container: dict[str, Any] | None = None
+    app_uds: str | None = None  # module replicas: the app also serves this Unix socket (TT_APP_UDS)
 
     @property
     def app_port(self) -> int | None:
@@ -207,7 +208,8 @@ class LocalStack:
         if container is None:
             args += ["--", sys.executable, "-m", module or SERVICE_MODULES[app_id], "--urls", urls]
             p = self._spawn(args, env, name)
-            rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file)
+            rp = ReplicaProc(app_id, name, p, str(self.sock_dir / f"{name}.d.sock"), http_port, port_file,
+                             app_uds=app_uds)
         else:
             app_port = free_port()
             cmd, app_env, isolation = container_command(container, f"http://127.0.0.1:{app_port}")

@@ -255,12 +255,17 @@ class SidecarClient:
         return (await self.get_state_and_etag(store, key))[0]
 
     async def get_bulk_state(self, store: str, keys: list[str], parallelism: int = 10) -> list[StateItem]:
-        body = json.dumps({"keys": keys, "parallelism": parallelism}).encode()
+        return [StateItem(x["key"], x.get("data"), x.get("etag"))
+                for x in json.loads(await self.get_bulk_state_raw(store, keys, parallelism))]
+
+    async def get_bulk_state_raw(self, store: str, keys: list[str], parallelism: int = 10) -> bytes:
+        """The bulk-get answer as the sidecar sent it (``[{"key", "data", "etag"}]``)."""
+        body = json.dumps({"keys": keys, "parallelism": parallelism}, separators=(",", ":")).encode()
         r = await self._call("POST", f"/v1.0/state/{store}/bulk", body, "application/json",
                              span_name=f"state bulkget {store}")
         if r.status >= 300:
             raise InvocationError(r.status, r.body, f"bulk get {store}")
-        return [StateItem(x["key"], x.get("data"), x.get("etag")) for x in r.json()]
+        return r.body
 
     async def delete_state(self, store: str, key: str, etag: str | None = None) -> None:
         extra = {"If-Match": etag} if etag else None

@@ -17,7 +17,10 @@ tests/test_backend_api.py:
 * #5  query filters are built as JSON objects, not by string concatenation;
 * #11 asyncio single-threaded execution makes the fake's list race-free;
 * #12 read-modify-write operations use ETag first-write concurrency with bounded retry
-      instead of last-writer-wins.
+      instead of last-writer-wins -- markoverdue included: it re-reads the page's tasks and
+      marks only those still open, each save guarded by the ETag it read, so a completion that
+      lands between the sweep's query and its save is never reverted (the reference saves the
+      processor's copy, TasksStoreManager.cs:141-149).
 Everything else (status codes, orderings, the ``yyyy-MM-ddTHH:mm:ss`` due-date equality
 trap of #7, publish-on-create and publish-on-assignee-change) is kept.
 """
@@ -30,8 +33,8 @@ import random
 import uuid
 from datetime import datetime, timedelta
 
-from ...models import (TaskModel, create_task_wire, format_fixed, mark_overdue_wire, naive_utc, tasks_from_query_wire,
-                       today, utcnow)
+from ...models import (TaskModel, conditional_mark_wire, create_task_wire, format_fixed, mark_overdue_wire, naive_utc,
+                       tasks_from_query_wire, today, utcnow)
 from ...sdk.client import InvocationError, RawJson, SidecarClient
 from ...telemetry.logging import info_each
 
@@ -316,27 +319,56 @@ class TasksStoreManager(TasksManager):
         return tasks
 
     async def mark_overdue_from_body(self, body: bytes) -> bool:
-        """``mark_overdue_tasks`` straight from the request body (``models.mark_overdue_wire``:
-        binding and the bulk-save body in one native pass); the same log line per task and one
-        bulk save.  False: the body needs the general binder (or the client has no raw save)."""
-        save_body = getattr(self.client, "save_state_body", None)
-        made = mark_overdue_wire(body) if save_body is not None else None
+        """``mark_overdue_tasks`` straight from the request body: the ids come from the native
+        binder (``models.mark_overdue_wire``), then the conditional mark.  False: the body needs
+        the general binder (or the client has no raw bulk calls)."""
+        if getattr(self.client, "save_state_body", None) is None or \
+                getattr(self.client, "get_bulk_state_raw", None) is None:
+            return False
+        made = mark_overdue_wire(body)
         if made is None:
             return False
-        ids, bulk = made
-        info_each(log, "Mark task with Id: '%s' as OverDue task", [(tid,) for tid in ids])
-        if ids:
-            await save_body(self.store, bulk)
+        await self._mark_conditionally(made[0])
         return True
 
     async def mark_overdue_tasks(self, tasks) -> None:
-        items = []
-        for t in tasks:
-            log.info("Mark task with Id: '%s' as OverDue task", t.task_id)
-            t.is_over_due = True
-            items.append({"key": str(t.task_id), "value": t.to_wire()})
-        if items:
-            await self.client.save_bulk_state(self.store, items)
+        await self._mark_conditionally([str(t.task_id) for t in tasks])
+
+    async def _mark_conditionally(self, ids: list[str]) -> None:
+        """Bulk read-modify-write of ``isOverDue``: read the tasks with their
+        ETags, set the flag on the STORED copy of every task still open and not yet overdue, save
+        each guarded by its ETag (first-write).  A conflict (a task changed in between: a
+        completion, an edit) re-reads the tasks of that pass and re-applies; the tasks the save
+        did write are overdue by then and drop out."""
+        pending = list(dict.fromkeys(ids))
+        raw_get = getattr(self.client, "get_bulk_state_raw", None)
+        save_body = getattr(self.client, "save_state_body", None)
+        for _ in range(self.max_retries):
+            if not pending:
+                return
+            if raw_get is not None:
+                got = await raw_get(self.store, pending)
+            else:  # gRPC: bulk get as state items
+                got = json.dumps([{"key": x.key, "data": x.data, "etag": x.etag}
+                                  for x in await self.client.get_bulk_state(self.store, pending)]).encode()
+            made = conditional_mark_wire(got)
+            if made is None:
+                raise ValueError("the task collection holds documents outside the TaskModel shape")
+            marked, bulk, _skipped = made
+            info_each(log, "Mark task with Id: '%s' as OverDue task", [(tid,) for tid in marked])
+            if not marked:
+                return
+            try:
+                if save_body is not None:
+                    await save_body(self.store, bulk)
+                else:
+                    await self.client.save_bulk_state(self.store, json.loads(bulk))
+                return
+            except InvocationError as e:
+                if e.status not in (409, 412):
+                    raise
+                pending = marked  # lost a race on some of them: re-read and re-apply
+        raise ConcurrencyConflict(f"{len(pending)} overdue tasks kept changing under concurrent writers")
 
     async def _publish_task_saved(self, t: TaskModel, payload: RawJson | None = None) -> None:
         log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",

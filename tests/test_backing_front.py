@@ -67,10 +67,17 @@ def test_documents(front, monkeypatch):
             with pytest.raises(EtagConflict):
                 await c.doc_bulk_set("acct", "db", "c", [{"key": "b0", "value": "1", "etag": "nope"}])
             assert (await c.doc_get("acct", "db", "c", "b2"))[0] == b'{"i": 2}'
+            # bulk get (the read half of markoverdue's conditional save): request order, etags,
+            # a missing key without data
+            got = await c.doc_bulk_get("acct", "db", "c", ["b2", "missing", "b0"])
+            etag_b0 = (await c.doc_get("acct", "db", "c", "b0"))[1]
+            assert got == [{"key": "b2", "data": {"i": 2}, "etag": got[0]["etag"]}, {"key": "missing"},
+                           {"key": "b0", "data": {"i": 0}, "etag": etag_b0}]
             fs = (await c.http.get(b.base + "/admin/front")).json()
             assert fs["front"] == front
             if front == "native":
                 assert fs["requests"]["doc.put"] >= 4 and fs["requests"]["doc.get"] >= 2
+                assert fs["requests"]["doc.bulkget"] == 1
             await c.http.close()
     run(main())
 

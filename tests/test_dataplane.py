@@ -141,6 +141,13 @@ def test_state_api(plane, tmp_path):
             for i in range(3):
                 r = await h.get(f"{st}/{quote(f'bulk/{i} é', safe='')}")
                 assert r.status == 200 and r.json() == {"i": i}
+            # bulk get: request order, raw values with their etags, a missing key without data
+            r = await h.post(f"{st}/bulk", json_body={"keys": ["bulk/2 é", "nope", "k1"], "parallelism": 2})
+            assert r.status == 200
+            got = r.json()
+            assert [x["key"] for x in got] == ["bulk/2 é", "nope", "k1"]
+            assert got[0]["data"] == {"i": 2} and got[0]["etag"] and "data" not in got[1]
+            assert got[2]["data"] == 2 and got[2]["etag"] == (await h.get(f"{st}/k1")).headers.get("etag")
             # missing -> 204, delete with bad etag -> 409, delete -> 204 then missing
             assert (await h.get(f"{st}/nope")).status == 204
             r = await h.delete(f"{st}/k1", headers={"If-Match": "123"})
