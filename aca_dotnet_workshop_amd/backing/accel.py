@@ -135,9 +135,11 @@ class CollectionAccelerator:
     def close(self) -> None:
         self._bg_stop.set()
 
-    def query(self, q: dict[str, Any], prefix: str, store) -> bytes | None:
+    def query(self, q: dict[str, Any], prefix: str, store, sort_keys: bool = False) -> bytes | None:
         """JSON result text (UTF-8 bytes, as the store built it: the page goes out without a
-        decode/encode round trip), or None to let the native engine answer.  Blocking."""
+        decode/encode round trip), or None to let the native engine answer.  Blocking.
+        ``sort_keys``: the results as sort-keys projections (``{"key", "etag", "sort"}``, the
+        first phase of a cross-partition page)."""
         if not self.should_accelerate(q, store):
             self.stats["native"] += 1
             return None
@@ -174,7 +176,9 @@ class CollectionAccelerator:
                     self.stats["fallback"] += 1
                     return None
                 tb = time.perf_counter()
-                res = store.mirror_results(rows, prefix, token or "", gen=self.index.generation)
+                res = store.mirror_results(rows, prefix, token or "", gen=self.index.generation,
+                                           sort_paths=[sp["key"] for sp in q.get("sort") or []
+                                                       if isinstance(sp, dict) and "key" in sp] if sort_keys else None)
                 t_sel, t_res = t_sel + tb - ta, t_res + time.perf_counter() - tb
                 if res is not None:
                     break

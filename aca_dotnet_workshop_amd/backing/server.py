@@ -303,6 +303,9 @@ class BackingServices:
             s = st(req, "cosmos.read")
             raw = req.body.decode("utf-8") or "{}"
             prefix = req.query_get("prefix", "") or ""
+            # ?project=sortkeys: {"key", "etag", "sort"} per result -- phase one of a
+            # cross-partition page (the sidecar fetches the merged page's documents after)
+            sort_keys = (req.query_get("project", "") or "").lower() == "sortkeys"
             a = acc(req)
             # a sampled caller (the data plane passes the trace on for queries) gets the
             # store's share as spans: this handler, and the planner + page run on the pool
@@ -320,8 +323,8 @@ class BackingServices:
                 inner = tracer().start_span("query run", "internal", parent=span) if span is not None else None
                 try:
                     q = json.loads(raw)
-                    text = a.query(q, prefix, s) if isinstance(q, dict) else None
-                    return s.query(raw, prefix) if text is None else text
+                    text = a.query(q, prefix, s, sort_keys) if isinstance(q, dict) else None
+                    return s.query(raw, prefix, sort_keys) if text is None else text
                 finally:
                     if inner is not None:
                         inner.end()

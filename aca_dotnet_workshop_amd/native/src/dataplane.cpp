@@ -850,10 +850,11 @@ class DataPlane {
     if (seg.size() == 4 && (lower(seg[0]) == "v1.0-alpha1" || lower(seg[0]) == "v1.0-beta1") &&
         lower(seg[1]) == "state" && lower(seg[3]) == "query" && (m.method == "POST" || m.method == "PUT")) {
       auto it = stores_.find(unquote(seg[2]));
-      // state query: straight to the backing's query planner (a partitioned store's
-      // cross-partition query fans out and merges in the control plane, sidecar/state.py)
-      if (it != stores_.end() && it->second.shards.empty()) {
-        state_query(std::move(m), std::move(r), it->second, path);
+      // state query: straight to the backing's query planner; a partitioned store's
+      // cross-partition query fans out and merges here (two phases: sort keys, then the page)
+      if (it != stores_.end()) {
+        if (it->second.shards.empty()) state_query(std::move(m), std::move(r), it->second, path);
+        else state_query_sharded(std::move(m), std::move(r), it->second, path);
         return;
       }
     }
@@ -932,6 +933,12 @@ class DataPlane {
              "# TYPE sidecar_mtls_handshake_rejected_total counter\n"
              "sidecar_mtls_handshake_rejected_total{app=\"" + app_id_ + "\"} " +
              std::to_string(ev::tls_server_handshake_rejects.load(std::memory_order_relaxed)) + "\n";
+    extra += "# HELP sidecar_partitioned_query_rows_total cross-partition state queries: sort-key entries the "
+             "shards sent (phase keys) and documents fetched for the merged pages (phase documents)\n"
+             "# TYPE sidecar_partitioned_query_rows_total counter\n"
+             "sidecar_partitioned_query_rows_total{app=\"" + app_id_ + "\",phase=\"keys\"} " +
+             std::to_string(keys_moved_) + "\nsidecar_partitioned_query_rows_total{app=\"" + app_id_ +
+             "\",phase=\"documents\"} " + std::to_string(rows_fetched_) + "\n";
     forward_to_control_plane(std::move(m), std::move(r), [extra](std::string& body) { body += extra; });
   }
 
@@ -1364,6 +1371,41 @@ class DataPlane {
     }
   }
 
+  // One bulkget per shard the full keys hash to; `done` runs once every shard has answered,
+  // with bg->found filled (or bg->failed).
+  void fetch_docs(const Store& s, const std::shared_ptr<BulkGet>& bg, std::function<void()> done) {
+    std::map<size_t, std::vector<size_t>> by_shard;
+    for (size_t i = 0; i < bg->full.size(); ++i) by_shard[s.shards.empty() ? 0 : s.shard_of(bg->full[i])].push_back(i);
+    if (by_shard.empty()) {
+      done();
+      return;
+    }
+    bg->left = by_shard.size();
+    bg->bodies.resize(by_shard.size());
+    auto fin = std::make_shared<std::function<void()>>(std::move(done));
+    HeaderList h = s.auth;
+    h.emplace_back("content-type", "application/json");
+    size_t slot = 0;
+    for (auto& kv : by_shard) {
+      std::string body = "{\"keys\":[";
+      for (size_t j = 0; j < kv.second.size(); ++j) body += (j ? "," : "") + json_str(bg->full[kv.second[j]]);
+      body += "]}";
+      store_request(s.ep(kv.first), "POST", s.coll_path + "/bulkget", h, std::move(body),
+                    [bg, slot, fin](ClientResult&& res) {
+                      if (res.err || res.resp.status != 200) {
+                        bg->failed = true;
+                        if (bg->error.empty())
+                          bg->error = res.err ? errno_text(res.err) : "HTTP " + std::to_string(res.resp.status);
+                      } else {
+                        bg->bodies[slot] = std::move(res.resp.body);
+                        if (!scan_bulkget(bg->bodies[slot], *bg)) bg->failed = true, bg->error = "unreadable bulkget";
+                      }
+                      if (--bg->left == 0) (*fin)();
+                    });
+      ++slot;
+    }
+  }
+
   void state_bulk_get(Message&& m, Reply&& r, const Store& s, const std::string& path) {
     auto d = begin(m, std::move(r), "state.bulkget", path);
     auto bg = std::make_shared<BulkGet>();
@@ -1380,54 +1422,253 @@ class DataPlane {
       d->error(400, "ERR_MALFORMED_REQUEST", std::string("bulk get: ") + ex.what());
       return;
     }
-    std::map<size_t, std::vector<size_t>> by_shard;
-    for (size_t i = 0; i < bg->full.size(); ++i) by_shard[s.shards.empty() ? 0 : s.shard_of(bg->full[i])].push_back(i);
-    if (by_shard.empty()) {
-      d->send(200, {{"content-type", "application/json"}}, "[]");
+    fetch_docs(s, bg, [d, bg] {
+      if (bg->failed) {
+        d->error(500, "ERR_STATE_BULK_GET", "bulk get: " + bg->error);
+        return;
+      }
+      std::string out = "[";
+      for (size_t i = 0; i < bg->keys.size(); ++i) {
+        out += i ? ",{\"key\":" : "{\"key\":";
+        out += json_str(bg->keys[i]);
+        auto it = bg->found.find(bg->full[i]);
+        if (it != bg->found.end()) {
+          out += ",\"data\":";
+          out.append(it->second.first);
+          out += ",\"etag\":" + json_str(it->second.second);
+        }
+        out += '}';
+      }
+      out += ']';
+      d->send(200, {{"content-type", "application/json"}}, out);
+    });
+  }
+
+  // ---------------------------------------------------------------- cross-partition query
+  // A partitioned store's state query (backing/shards.py semantics, natively): every shard
+  // still holding matches answers its own sorted page as SORT KEYS only (`?project=sortkeys`:
+  // key, etag and the values at the sort paths); the pages are k-way merged on those values
+  // (the store's JSON order, ties in shard order); then only the merged page's documents are
+  // fetched, one bulkget per shard.  At N shards a page of `limit` moves N x limit small key
+  // entries plus `limit` documents, not N x limit documents.  The continuation token is the
+  // shards' offsets ("p1." + url-safe base64 of a JSON array; null = exhausted), the same one
+  // the Python plane issues.
+  struct ShardPage {
+    std::vector<std::string> keys;        // without the store's key prefix
+    std::vector<std::vector<Value>> sort;  // sort values per result
+    bool more = false;
+    bool present = false;  // asked (offset not null)
+  };
+  struct XQuery {
+    std::vector<std::pair<std::string, bool>> sort;  // path, desc
+    size_t limit = 0;
+    std::vector<long long> offsets;  // -1 = exhausted
+    std::vector<ShardPage> pages;
+    size_t left = 0;
+    bool failed = false;
+    int fail_status = 500;
+    std::string error;
+  };
+
+  static std::string b64url(std::string_view in) {
+    std::string o = base64(in);
+    for (char& c : o) c = c == '+' ? '-' : c == '/' ? '_' : c;
+    while (!o.empty() && o.back() == '=') o.pop_back();
+    return o;
+  }
+  static std::string unb64url(std::string_view in) {
+    std::string t(in);
+    for (char& c : t) c = c == '-' ? '+' : c == '_' ? '/' : c;
+    return unbase64(t);
+  }
+  static bool decode_xtoken(const std::string& tok, size_t n, std::vector<long long>& offs) {
+    offs.assign(n, 0);
+    if (tok.empty()) return true;
+    if (tok.rfind("p1.", 0) != 0) return false;
+    try {
+      Value v = parse(unb64url(std::string_view(tok).substr(3)));
+      if (v.t != Value::Array || v.items.size() != n) return false;
+      for (size_t i = 0; i < n; ++i) {
+        const Value& x = v.items[i];
+        if (x.t == Value::Null) offs[i] = -1;
+        else if (x.t == Value::Number && x.n >= 0 && x.n == (double)(long long)x.n) offs[i] = (long long)x.n;
+        else return false;
+      }
+    } catch (const std::exception&) {
+      return false;
+    }
+    return true;
+  }
+
+  void state_query_sharded(Message&& m, Reply&& r, const Store& s, const std::string& path) {
+    auto d = begin(m, std::move(r), "state.query", path);
+    auto x = std::make_shared<XQuery>();
+    const size_t n = s.shards.size();
+    Value q;
+    std::string token;
+    try {
+      q = parse(m.body.empty() ? std::string("{}") : m.body);
+      if (q.t != Value::Object) throw std::runtime_error("query must be a JSON object");
+      if (const Value* sv = q.get_ci("sort"); sv && sv->t == Value::Array)
+        for (auto& e : sv->items) {
+          const Value* k = e.get_ci("key");
+          if (!k || k->t != Value::String) throw std::runtime_error("sort entry needs a string key");
+          const Value* o = e.get_ci("order");
+          x->sort.emplace_back(k->s, o && o->t == Value::String && lower(o->s) == "desc");
+        }
+      if (Value* pg = const_cast<Value*>(q.get_ci("page")); pg && pg->t == Value::Object) {
+        if (const Value* l = pg->get_ci("limit"); l && l->t == Value::Number && l->n > 0) x->limit = (size_t)l->n;
+        if (const Value* t = pg->get_ci("token"); t && t->t == Value::String) token = t->s;
+      }
+    } catch (const std::exception& ex) {
+      d->error(400, "ERR_STATE_QUERY", std::string("state query: ") + ex.what());
       return;
     }
-    bg->left = by_shard.size();
-    bg->bodies.resize(by_shard.size());
+    if (!decode_xtoken(token, n, x->offsets)) {
+      d->error(400, "ERR_STATE_QUERY", "state query: invalid continuation token for a partitioned collection");
+      return;
+    }
+    x->pages.resize(n);
+    // the shard's sub-query: the same filter and sort, its own offset as the token
+    auto sub_query = [&](long long off) {
+      Value sub = q;
+      Value page;
+      page.t = Value::Object;
+      if (x->limit) page.keys.push_back("limit"), page.items.push_back(Value::number((double)x->limit));
+      if (off > 0) page.keys.push_back("token"), page.items.push_back(Value::string(std::to_string(off)));
+      for (size_t i = 0; i < sub.keys.size(); ++i)
+        if (lower(sub.keys[i]) == "page") {
+          sub.keys.erase(sub.keys.begin() + (long)i);
+          sub.items.erase(sub.items.begin() + (long)i);
+          break;
+        }
+      if (!page.keys.empty()) sub.keys.push_back("page"), sub.items.push_back(std::move(page));
+      return dump(sub);
+    };
+    std::string target = s.coll_path + "/query?project=sortkeys";
+    if (!s.prefix.empty()) target += "&prefix=" + quote_all(s.prefix);
     HeaderList h = s.auth;
     h.emplace_back("content-type", "application/json");
-    size_t slot = 0;
-    for (auto& kv : by_shard) {
-      std::string body = "{\"keys\":[";
-      for (size_t j = 0; j < kv.second.size(); ++j) body += (j ? "," : "") + json_str(bg->full[kv.second[j]]);
-      body += "]}";
-      store_request(s.ep(kv.first), "POST", s.coll_path + "/bulkget", h, std::move(body),
-                    [d, bg, slot](ClientResult&& res) {
-                      if (res.err || res.resp.status != 200) {
-                        bg->failed = true;
-                        if (bg->error.empty())
-                          bg->error = res.err ? errno_text(res.err) : "HTTP " + std::to_string(res.resp.status);
-                      } else {
-                        bg->bodies[slot] = std::move(res.resp.body);
-                        if (!scan_bulkget(bg->bodies[slot], *bg)) bg->failed = true, bg->error = "unreadable bulkget";
-                      }
-                      if (--bg->left) return;
-                      if (bg->failed) {
-                        d->error(500, "ERR_STATE_BULK_GET", "bulk get: " + bg->error);
-                        return;
-                      }
-                      std::string out = "[";
-                      for (size_t i = 0; i < bg->keys.size(); ++i) {
-                        out += i ? ",{\"key\":" : "{\"key\":";
-                        out += json_str(bg->keys[i]);
-                        auto it = bg->found.find(bg->full[i]);
-                        if (it != bg->found.end()) {
-                          out += ",\"data\":";
-                          out.append(it->second.first);
-                          out += ",\"etag\":" + json_str(it->second.second);
-                        }
-                        out += '}';
-                      }
-                      out += ']';
-                      d->send(200, {{"content-type", "application/json"}}, out);
-                    });
-      ++slot;
+    for (size_t i = 0; i < n; ++i)
+      if (x->offsets[i] >= 0) x->left++;
+    if (x->left == 0) {  // every shard exhausted
+      d->send(200, {{"content-type", "application/json"}}, "{\"results\":[]}");
+      return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+      if (x->offsets[i] < 0) continue;
+      x->pages[i].present = true;
+      store_request(s.ep(i), "POST", target, h, sub_query(x->offsets[i]), [this, d, x, i, &s](ClientResult&& res) {
+        if (res.err || res.resp.status != 200) {
+          if (!x->failed) {
+            x->failed = true;
+            x->fail_status = (!res.err && res.resp.status == 400) ? 400 : 500;
+            x->error = res.err ? errno_text(res.err)
+                               : "HTTP " + std::to_string(res.resp.status) + " " + res.resp.body.substr(0, 300);
+          }
+        } else {
+          try {
+            Value v = parse(res.resp.body);
+            ShardPage& pg = x->pages[i];
+            if (const Value* t = v.get("token"); t && t->t == Value::String && !t->s.empty()) pg.more = true;
+            if (const Value* rs = v.get("results"); rs && rs->t == Value::Array)
+              for (auto& it : rs->items) {
+                const Value* k = it.get("key");
+                const Value* sv = it.get("sort");
+                if (!k || k->t != Value::String) continue;
+                pg.keys.push_back(k->s);
+                pg.sort.push_back(sv && sv->t == Value::Array ? sv->items : std::vector<Value>());
+              }
+            keys_moved_ += pg.keys.size();
+          } catch (const std::exception& ex) {
+            x->failed = true;
+            x->error = std::string("unreadable shard page: ") + ex.what();
+          }
+        }
+        if (--x->left == 0) merge_and_fetch(d, x, s);
+      });
     }
   }
+
+  void merge_and_fetch(const std::shared_ptr<Done>& d, const std::shared_ptr<XQuery>& x, const Store& s) {
+    if (x->failed) {
+      d->error(x->fail_status, "ERR_STATE_QUERY", "state query: " + x->error);
+      return;
+    }
+    const size_t n = x->pages.size();
+    std::vector<size_t> pos(n, 0), used(n, 0);
+    static const Value kNull;
+    auto less = [&](size_t a, size_t b) {  // shard a's head before shard b's head
+      const auto& va = x->pages[a].sort[pos[a]];
+      const auto& vb = x->pages[b].sort[pos[b]];
+      for (size_t k = 0; k < x->sort.size(); ++k) {
+        int c = compare(k < va.size() ? va[k] : kNull, k < vb.size() ? vb[k] : kNull);
+        if (c) return x->sort[k].second ? c > 0 : c < 0;
+      }
+      return a < b;
+    };
+    auto bg = std::make_shared<BulkGet>();
+    std::vector<size_t> order_shard;  // the merged page, as (shard) per entry; keys in bg
+    while (!x->limit || bg->full.size() < x->limit) {
+      size_t best = n;
+      for (size_t i = 0; i < n; ++i) {
+        if (pos[i] >= x->pages[i].keys.size()) continue;
+        if (x->sort.empty()) {  // unsorted: shard order
+          best = i;
+          break;
+        }
+        if (best == n || less(i, best)) best = i;
+      }
+      if (best == n) break;
+      bg->keys.push_back(x->pages[best].keys[pos[best]]);
+      bg->full.push_back(full_key(s, bg->keys.back()));
+      ++pos[best];
+      ++used[best];
+    }
+    // next offsets: a shard is exhausted when it said so and every result it gave was used
+    std::string tok;
+    if (x->limit) {
+      bool any = false;
+      std::string arr = "[";
+      for (size_t i = 0; i < n; ++i) {
+        if (i) arr += ',';
+        const ShardPage& pg = x->pages[i];
+        if (!pg.present || (!pg.more && used[i] == pg.keys.size())) {
+          arr += "null";
+        } else {
+          arr += std::to_string(x->offsets[i] + (long long)used[i]);
+          any = true;
+        }
+      }
+      arr += ']';
+      if (any) tok = "p1." + b64url(arr);
+    }
+    rows_fetched_ += bg->full.size();
+    fetch_docs(s, bg, [d, bg, tok] {
+      if (bg->failed) {
+        d->error(500, "ERR_STATE_QUERY", "state query: " + bg->error);
+        return;
+      }
+      std::string out = "{\"results\":[";
+      bool first = true;
+      for (size_t i = 0; i < bg->keys.size(); ++i) {
+        auto it = bg->found.find(bg->full[i]);
+        if (it == bg->found.end()) continue;  // deleted between the two phases
+        out += first ? "{\"key\":" : ",{\"key\":";
+        first = false;
+        out += json_str(bg->keys[i]);
+        out += ",\"data\":";
+        out.append(it->second.first);
+        out += ",\"etag\":" + json_str(it->second.second);
+        out += '}';
+      }
+      out += ']';
+      if (!tok.empty()) out += ",\"token\":" + json_str(tok);
+      out += '}';
+      d->send(200, {{"content-type", "application/json"}}, out);
+    });
+  }
+  uint64_t keys_moved_ = 0, rows_fetched_ = 0;
 
   // sidecar/runtime.py h_state_query: the filter goes to the backing's query route (hash
   // indexes / GPU columnar planner there) with the store's key prefix; 400 from the backing is

@@ -350,8 +350,27 @@ class DocStore {
   }
 
   // ---------------------------------------------------------------- query
-  // Returns {"results":[{"key","data","etag"}...],"token":"..."} as JSON text.
-  std::string query(const std::string& query_json, const std::string& prefix) {
+  // One result of a sort-keys projection: {"key", "etag", "sort": [the document's value at each
+  // sort path, null when missing]} -- the first phase of a cross-partition page (the sidecar
+  // merges the shards' sort keys and fetches only the page's documents, dataplane.cpp).
+  static void sort_keys_to(std::string& out, std::string_view key, const Doc& d, const std::vector<std::string>& paths) {
+    out += "{\"key\":";
+    escape_to(out, key);
+    out += ",\"etag\":\"";
+    out += std::to_string(d.etag);
+    out += "\",\"sort\":[";
+    for (size_t j = 0; j < paths.size(); ++j) {
+      if (j) out += ',';
+      const Value* v = d.parsed.path(paths[j]);
+      if (v) dump_to(out, *v);
+      else out += "null";
+    }
+    out += "]}";
+  }
+
+  // Returns {"results":[{"key","data","etag"}...],"token":"..."} as JSON text; `sort_keys`: the
+  // results as sort-keys projections instead (sort_keys_to).
+  std::string query(const std::string& query_json, const std::string& prefix, bool sort_keys = false) {
     Value q = parse(query_json.empty() ? std::string("{}") : query_json);
     if (q.t != Value::Object) throw QueryError("query must be a JSON object");
     Filter f;
@@ -413,8 +432,15 @@ class DocStore {
     size_t begin = std::min(offset, hits.size());
     size_t end = limit ? std::min(hits.size(), begin + limit) : hits.size();
     std::string out = "{\"results\":[";
+    std::vector<std::string> sort_paths;
+    if (sort_keys)
+      for (auto& sk : sort) sort_paths.push_back(sk.path);
     for (size_t i = begin; i < end; ++i) {
       if (i > begin) out += ',';
+      if (sort_keys) {
+        sort_keys_to(out, std::string_view(*hits[i].first).substr(prefix.size()), *hits[i].second, sort_paths);
+        continue;
+      }
       out += "{\"key\":";
       escape_to(out, std::string_view(*hits[i].first).substr(prefix.size()));
       out += ",\"data\":";
@@ -646,8 +672,10 @@ class DocStore {
   // rows, so a different generation returns false (`*stale` = true) without touching `out` --
   // a stale row number could name another live document, which would then be returned for a
   // filter it does not match.
+  // `sort_paths` (non-null): sort-keys projections instead of documents (sort_keys_to).
   bool mirror_results(const int32_t* rows, size_t nrows, const std::string& prefix, const std::string& token,
-                      uint64_t gen, std::string& out, size_t* skipped = nullptr) {
+                      uint64_t gen, std::string& out, size_t* skipped = nullptr,
+                      const std::vector<std::string>* sort_paths = nullptr) {
     std::lock_guard<std::mutex> g(mu_);
     if (gen != mirror_.gen) return false;
     int64_t now = now_ms();
@@ -662,6 +690,10 @@ class DocStore {
       if (it == docs_.end() || it->second.mrow != r || expired(it->second, now)) { ++skip; continue; }
       if (!first) out += ',';
       first = false;
+      if (sort_paths) {
+        sort_keys_to(out, std::string_view(key).substr(std::min(prefix.size(), key.size())), it->second, *sort_paths);
+        continue;
+      }
       out += "{\"key\":";
       escape_to(out, std::string_view(key).substr(std::min(prefix.size(), key.size())));
       out += ",\"data\":";

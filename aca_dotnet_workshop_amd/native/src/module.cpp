@@ -429,7 +429,7 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("get", &DocStore::get, py::arg("key"))
       .def("delete", &DocStore::del, py::arg("key"), py::arg("etag") = std::nullopt)
       .def("transact", &DocStore::transact, py::arg("ops"), py::call_guard<py::gil_scoped_release>())
-      .def("query", &DocStore::query, py::arg("query"), py::arg("prefix") = "",
+      .def("query", &DocStore::query, py::arg("query"), py::arg("prefix") = "", py::arg("sort_keys") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("keys", &DocStore::keys, py::arg("prefix") = "", py::arg("limit") = 0)
       .def("encode_columns",
@@ -487,7 +487,8 @@ PYBIND11_MODULE(_ttnative, m) {
            py::arg("gen"), py::arg("from_row"), py::arg("kill_from"), py::arg("dict_sizes"))
       .def("mirror_results",
            [](DocStore& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> rows,
-              const std::string& prefix, const std::string& token, uint64_t gen) -> py::object {
+              const std::string& prefix, const std::string& token, uint64_t gen,
+              std::optional<std::vector<std::string>> sort_paths) -> py::object {
              size_t skipped = 0;
              std::string out;
              const int32_t* p = rows.data();
@@ -495,12 +496,13 @@ PYBIND11_MODULE(_ttnative, m) {
              bool ok;
              {
                py::gil_scoped_release r;
-               ok = s.mirror_results(p, n, prefix, token, gen, out, &skipped);
+               ok = s.mirror_results(p, n, prefix, token, gen, out, &skipped, sort_paths ? &*sort_paths : nullptr);
              }
              if (!ok) return py::none();  // the rows come from another mirror generation
              return py::make_tuple(py::bytes(out), skipped);
            },
-           py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "", py::arg("gen") = 0)
+           py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "", py::arg("gen") = 0,
+           py::arg("sort_paths") = py::none())
       .def("mirror_stats", &DocStore::mirror_stats)
       .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"))
       .def("charge", &DocStore::charge, py::arg("ru"))

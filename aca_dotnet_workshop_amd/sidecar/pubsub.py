@@ -62,6 +62,14 @@ class BackingTransport(Transport):
     async def counts(self, entity):
         return await self.client.sb_counts(self.ns, entity)
 
+    def per_shard(self) -> list["BackingTransport"]:
+        """A partitioned namespace (backing/shards.py): one transport per shard, so a consumer
+        long-polls its own shard and settles there -- no receive call scans every shard."""
+        shards = getattr(self.client, "shards", None)
+        if not shards or len(shards) < 2:
+            return [self]
+        return [BackingTransport(c, self.ns) for c in shards]
+
 
 class InMemoryTransport(Transport):
     def __init__(self) -> None:
@@ -298,14 +306,24 @@ class PubSub(ComponentBase):
                 "retryDelayMs": self.comp.get_int("retryDelayMs", 0)}
 
     async def subscribe(self, topic: str, handler: Handler, sub_metadata: dict[str, str],
-                        on_drop=None) -> Consumer:
+                        on_drop=None) -> list[Consumer]:
+        """The subscription's competing consumers in this replica: one, or one per shard of a
+        partitioned namespace with the replica's prefetch and concurrency split over them (the
+        native data plane does the same, sidecar/runtime.py ``_subscribe_native``)."""
         entity = await self.ensure_entity(topic)
         cs = self.consumer_settings()
-        c = Consumer(self.transport, entity, handler, max_concurrent=cs["maxConcurrent"], prefetch=cs["prefetch"],
-                     lock_ms=cs["lockMs"], retry_delay_ms=cs["retryDelayMs"], on_drop=on_drop,
-                     name=f"{self.name}/{topic}")
-        c.start()
-        return c
+        per = getattr(self.transport, "per_shard", None)
+        transports = per() if per is not None else [self.transport]
+        n = len(transports)
+        out = []
+        for i, t in enumerate(transports):
+            c = Consumer(t, entity, handler, max_concurrent=max(1, -(-cs["maxConcurrent"] // n)),
+                         prefetch=max(1, -(-cs["prefetch"] // n)), lock_ms=cs["lockMs"],
+                         retry_delay_ms=cs["retryDelayMs"], on_drop=on_drop,
+                         name=f"{self.name}/{topic}" + (f"#{i}" if n > 1 else ""))
+            c.start()
+            out.append(c)
+        return out
 
 
 @register("pubsub.azure.servicebus", "pubsub.azure.servicebus.topics")

@@ -499,7 +499,7 @@ class Sidecar:
                 self._bg.append(asyncio.ensure_future(again()))
                 return
         try:
-            c = await ps.subscribe(s.topic, self._make_delivery(ps, s), s.metadata, self._make_dead_letter(ps, s))
+            cs = await ps.subscribe(s.topic, self._make_delivery(ps, s), s.metadata, self._make_dead_letter(ps, s))
         except Exception as e:
             log.error("sidecar %s: subscribing %s/%s failed (%s); retrying in %.0fs", self.app_id, s.pubsubname,
                       s.topic, e, delay)
@@ -510,7 +510,7 @@ class Sidecar:
                     await self._subscribe_with_retry(ps, s, min(delay * 2, 30.0))
             self._bg.append(asyncio.ensure_future(later()))
             return
-        self.consumers.append(c)
+        self.consumers.extend(cs)
         log.info("sidecar %s: subscribed %s/%s -> /%s", self.app_id, s.pubsubname, s.topic, s.route)
 
     def _make_delivery(self, ps: PubSub, sub: SubscriptionSpec):

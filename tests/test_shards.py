@@ -179,8 +179,8 @@ def test_partitioned_broker_exactly_once(backings):
 def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
     """An API replica whose sidecar runs the native data plane over two shards: the documents it
     saves land where the Python client's hash says, its publishes spread over both brokers, and
-    the cross-partition query of GET /api/tasks?createdBy= (forwarded to the control plane,
-    which fans out) returns every task."""
+    the cross-partition query of GET /api/tasks?createdBy= (fanned out and merged by the data
+    plane) returns every task."""
     urls = backings[:2]
     stack = LocalStack(root=tmp_path / "app")
     try:
@@ -225,6 +225,87 @@ def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
                 assert after[home] - per[home] == 12 and after[1 - home] == per[1 - home], (per, after)
             finally:
                 await sh.close()
+                await http.close()
+        run(main())
+    finally:
+        stack.stop()
+
+
+def test_native_cross_partition_query_pages_match_one_store(tmp_path, backings):
+    """The native data plane's cross-partition state query (dataplane.cpp state_query_sharded):
+    every shard answers its sorted page as sort keys only, the sidecar k-way merges them and
+    fetches just the merged page's documents.  Page by page -- ASC, DESC, unsorted, two sort
+    keys, continuation tokens -- the results equal one store's; a token from the Python merge
+    is accepted; rows moved are counted per phase."""
+    urls = backings[:3]
+    stack = LocalStack(root=tmp_path / "xq")
+    try:
+        stack.start_backing()
+        stack.base_env["TT_BACKING_SHARDS_COSMOS"] = ",".join(urls)
+        api = stack.start_replica("tasksmanager-backend-api", {"Logging:LogLevel:Default": "Warning"})
+        stack.wait_ready()
+
+        async def main():
+            from aca_dotnet_workshop_amd.web.client import HttpClient
+            http = HttpClient()
+            sh = ShardedBackingClient(urls, identity="platform-admin")
+            one = BackingClient(backings[3], identity="platform-admin")
+            try:
+                docs = {}
+                for i in range(300):
+                    t = _task(50_000 + i)
+                    t["taskCreatedBy"] = "xq@x"
+                    t["rank"] = i % 7  # ties across shards for the two-key sort
+                    docs[f"{PREFIX}{t['taskId']}"] = t
+                items = [{"key": k, "value": json.dumps(v)} for k, v in docs.items()]
+                await sh.doc_bulk_set(ACCT, DB, COLL, items)
+                await one.doc_bulk_set(ACCT, DB, COLL, items)
+                qurl = f"unix:{api.sidecar_uds}:/v1.0-alpha1/state/statestore/query"
+
+                async def via_sidecar(q):
+                    keys, token, pages = [], None, 0
+                    while True:
+                        qq = json.loads(json.dumps(q))
+                        if token:
+                            qq.setdefault("page", {})["token"] = token
+                        r = await http.request("POST", qurl, body=json.dumps(qq).encode(),
+                                               headers=[("Content-Type", "application/json")])
+                        assert r.status == 200, r.body
+                        res = json.loads(r.body)
+                        assert all(x["data"]["taskCreatedBy"] == "xq@x" and x["etag"] for x in res["results"])
+                        keys += [x["key"] for x in res["results"]]
+                        token, pages = res.get("token"), pages + 1
+                        if not token:
+                            return keys, pages
+
+                flt = {"AND": [{"EQ": {"taskCreatedBy": "xq@x"}}, {"LT": {"taskDueDate": "2026-10-20T00:00:00"}}]}
+                for sort, limit in (([{"key": "taskCreatedOn", "order": "ASC"}], 23),
+                                    ([{"key": "taskCreatedOn", "order": "DESC"}], 64),
+                                    ([{"key": "rank"}, {"key": "taskCreatedOn", "order": "DESC"}], 17)):
+                    q = {"filter": flt, "sort": sort, "page": {"limit": limit}}
+                    got, pages = await via_sidecar(q)
+                    want = await _pages(one, q)  # the store strips the key prefix
+                    assert got == want and len(got) > 100 and pages >= len(got) // limit, (sort, len(got), len(want))
+                unsorted, _ = await via_sidecar({"filter": flt, "page": {"limit": 40}})
+                assert sorted(unsorted) == sorted(await _pages(one, {"filter": flt}))
+                # a continuation token issued by the Python plane's merge resumes natively
+                q = {"filter": flt, "sort": [{"key": "taskCreatedOn"}], "page": {"limit": 30}}
+                first = json.loads(await sh.doc_query(ACCT, DB, COLL, json.dumps(q).encode(), PREFIX))
+                q2 = dict(q, page={"limit": 30, "token": first["token"]})
+                r = await http.request("POST", qurl, body=json.dumps(q2).encode(),
+                                       headers=[("Content-Type", "application/json")])
+                py2 = json.loads(await sh.doc_query(ACCT, DB, COLL, json.dumps(q2).encode(), PREFIX))
+                assert [x["key"] for x in json.loads(r.body)["results"]] == [x["key"] for x in py2["results"]]
+                bad = await http.request("POST", qurl, body=json.dumps(dict(q, page={"limit": 5, "token": "42"})).encode(),
+                                         headers=[("Content-Type", "application/json")])
+                assert bad.status == 400
+                m = (await http.request("GET", f"unix:{api.sidecar_uds}:/metrics")).body.decode()
+                keys_moved = int(m.split('phase="keys"} ')[1].split()[0])
+                docs_moved = int(m.split('phase="documents"} ')[1].split()[0])
+                assert 0 < docs_moved <= keys_moved
+            finally:
+                await sh.close()
+                await one.close()
                 await http.close()
         run(main())
     finally:
