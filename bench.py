@@ -226,6 +226,12 @@ class OverdueSweeper:
         finally:
             await c.close()
 
+    def slowest_trace(self) -> str | None:
+        if not self.runs:
+            return None
+        i = max(range(len(self.runs)), key=lambda j: self.runs[j][0])
+        return self.trace_ids[i] if i < len(self.trace_ids) else None
+
     def summary(self) -> dict:
         ms = sorted(d * 1e3 for d, _ in self.runs)
         return {"sweeps": len(self.runs), "errors": len(self.errors),
@@ -240,7 +246,7 @@ class OverdueSweeper:
                 "first_error": self.errors[0] if self.errors else None}
 
 
-def sweep_trace(telemetry_dir: str, trace_ids: list[str]) -> dict | None:
+def sweep_trace(telemetry_dir: str, trace_ids: list[str], slowest: str | None = None) -> dict | None:
     """Per-hop time of the sweeps from their spans (every sweep is a sampled trace): for every
     span of the job -- server spans of each sidecar data plane and app, the apps' client calls
     -- the median duration over the sweeps, in the order of the first sweep.  Keys are
@@ -274,8 +280,20 @@ def sweep_trace(telemetry_dir: str, trace_ids: list[str]) -> dict | None:
 
     def med(xs: list[float]) -> float:
         return round(sorted(xs)[len(xs) // 2], 2)
-    return {"sweeps_traced": len(by_trace), "spans_p50_ms": {k: med(durs[k]) for k in order},
-            "stamps_p50_ms": {k: med(v) for k, v in attrs.items()}}
+
+    def one(tid: str) -> dict:
+        """Every span of one sweep (its slowest): where a tail sweep spent its time."""
+        out: dict[str, float] = {}
+        for sp in sorted(by_trace.get(tid, []), key=lambda x: x.get("ts", 0.0)):
+            k = f"{sp.get('role')} {sp.get('kind')} {sp.get('name')}"
+            out[k if k not in out else f"{k} #{sum(1 for x in out if x.startswith(k))}"] = \
+                round(float(sp.get("durationMs", 0.0)), 2)
+        return out
+    res = {"sweeps_traced": len(by_trace), "spans_p50_ms": {k: med(durs[k]) for k in order},
+           "stamps_p50_ms": {k: med(v) for k, v in attrs.items()}}
+    if slowest and slowest in by_trace:
+        res["slowest_sweep_spans_ms"] = one(slowest)
+    return res
 
 
 def _counts(url: str | list[str]) -> dict:
@@ -802,7 +820,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if sweep_info is not None:  # span exporters flush at least once a second
             if not dsteps:
                 time.sleep(1.5)
-            sweep_info["trace"] = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids)
+            sweep_info["trace"] = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids, sweeper.slowest_trace())
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])

@@ -330,12 +330,12 @@ def _sweep_env(tmp: Path, name: str, shard_urls: list[str] | None, single_url: s
     return stack, proc.sidecar_uds
 
 
-@pytest.fixture
-def sweep_backings(tmp_path):
-    """Fresh backings for the sweep test: two shards and one single store (columnar CPU path)."""
+@pytest.fixture(params=[2, 8], ids=["2shards", "8shards"])
+def sweep_backings(tmp_path, request):
+    """Fresh backings for the sweep test: N shards and one single store (columnar CPU path)."""
     stacks = []
     try:
-        for i in range(3):
+        for i in range(request.param + 1):
             st = LocalStack(root=tmp_path / f"b{i}", env={"TT_QUERY_ACCEL": "cpu", "TT_QUERY_ACCEL_MIN_DOCS": "0",
                                                           "TT_QUERY_MIRROR_PATHS": "taskDueDate,isCompleted,isOverDue,taskCreatedOn"})
             st.start_backing()
@@ -367,11 +367,12 @@ def test_sharded_overdue_sweep_marks_the_same_tasks_as_one_store(tmp_path, sweep
             await client.doc_bulk_set("taskstracker-state-store", DB, COLL, items)
             await client.close()
         backings = sweep_backings
-        run(load(ShardedBackingClient(backings[:2], identity="platform-admin")))
-        one_url = backings[2]
+        n = len(backings) - 1
+        run(load(ShardedBackingClient(backings[:n], identity="platform-admin")))
+        one_url = backings[n]
         run(load(BackingClient(one_url, identity="platform-admin")))
         results = []
-        for name, shard_urls, single in (("sharded", backings[:2], None), ("single", None, one_url)):
+        for name, shard_urls, single in (("sharded", backings[:n], None), ("single", None, one_url)):
             stack, sock = _sweep_env(tmp_path, name, shard_urls, single)
             stacks.append(stack)
 
@@ -394,13 +395,13 @@ def test_sharded_overdue_sweep_marks_the_same_tasks_as_one_store(tmp_path, sweep
                 return {g["key"] for g in got if g.get("data") and g["data"].get("isOverDue")}
             finally:
                 await client.close()
-        sharded = run(marked(ShardedBackingClient(backings[:2], identity="platform-admin")))
+        sharded = run(marked(ShardedBackingClient(backings[:n], identity="platform-admin")))
         single = run(marked(BackingClient(one_url, identity="platform-admin")))
         assert sharded == single == want, (len(sharded), len(single), len(want))
         assert results[0]["markedOverdue"] == results[1]["markedOverdue"] == len(want)
         assert results[0]["pages"] >= len(want) // 50  # paged through the merged order
-        per_shard = {shard_of(k, 2) for k in want}
-        assert per_shard == {0, 1}
+        per_shard = {shard_of(k, n) for k in want}
+        assert per_shard == set(range(n))
     finally:
         for st in stacks:
             st.stop()
@@ -429,4 +430,26 @@ def test_shared_env_four_ranks_exactly_once():
     assert cfg["parallelism"].startswith("shared-env x4 (store and broker partitioned over 4 shards")
     dlv = cfg["delivery"]
     assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] == 4 * 24 * 3, dlv
+    assert dlv["dead_lettered"] == 0
+
+
+@pytest.mark.slow
+def test_shared_env_eight_ranks_exactly_once():
+    """The whole machine: eight ranks (one per GPU of an MI355X node), one partitioned
+    environment -- each rank hosts one shard of the store and of the broker, the eight
+    processors compete on the one subscription over all eight shards -- and every task is
+    delivered and completed exactly once (bench.py --shared-env over gloo, small batch)."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+           "--steps", "2", "--warmup", "1", "--batch", "16", "--api-replicas", "1", "--processor-replicas", "1",
+           "--shared-env", "--overdue-sweep-ms", "0", "--entry", "api-sidecar", "--split-backing", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"metric"' in x]
+    assert len(line) == 1
+    cfg = line[0]["config"]
+    assert cfg["parallelism"].startswith("shared-env x8 (store and broker partitioned over 8 shards")
+    dlv = cfg["delivery"]
+    assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] == 8 * 16 * 3, dlv
     assert dlv["dead_lettered"] == 0
