@@ -10,6 +10,12 @@
 // Request bodies come from a file with one body per line (cycled); `--header "name: value"`
 // (repeatable) adds request headers (the frontend entry sends its cookies).  Prints one JSON line:
 // {"requests", "errors", "elapsed_s", "latency_ms": {"p50", "p99", "max"}}.
+// `--follow`: a 3xx answer's Location is fetched next (GET, same target and headers) -- a
+// browser following Create's redirect to the task list; its latency is reported apart
+// ("follow_latency_ms", expected 200).  `--users N`: "{user}" in header values becomes
+// u<k>@bench.local, k cycling over N users (per-user cookies: bounded task lists).
+// `--duration S`: one step that stops issuing after S seconds; the --until-url counter must
+// then advance by the number of requests issued.  "status_counts" counts answers by status.
 // HTTPS targets: `--target https://127.0.0.1:port` with `--tls-ca ca.crt` verifies the server
 // certificate (name / address) against that CA, the way a browser trusting it would; without
 // `--tls-ca` the connection is encrypted but unverified.
@@ -22,6 +28,7 @@
 #include <csignal>
 #include <cstdio>
 #include <fstream>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -39,7 +46,9 @@ struct Opts {
   std::string tls_ca;
   std::vector<std::string> bodies{""};
   ev::HeaderList headers;
-  int concurrency = 64, batch = 512, steps = 1, expect = 0;
+  int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0;
+  bool follow = false;
+  double duration_s = 0;
   // shared environments (bench.py --shared-env): several generators drive one subscription, so
   // the counter's starting point and its advance per step are global, not this generator's own
   long long until_base = -1, until_stride = 0;
@@ -55,7 +64,14 @@ class Gen {
       client_.set_tls(std::make_shared<ev::TlsContext>(tc, false));
     }
     hdrs_.emplace_back("content-type", o_.ctype);
-    for (auto& h : o_.headers) hdrs_.push_back(h);
+    for (auto& h : o_.headers) {
+      if (h.second.find("{user}") != std::string::npos) templated_ = true;
+      hdrs_.push_back(h);
+    }
+    if (o_.duration_s > 0) {  // one open-ended step, closed by the clock
+      o_.steps = 1;
+      o_.batch = 1 << 30;
+    }
     for (std::string u : o_.until_urls) {
       if (u.rfind("http://", 0) == 0) u = u.substr(7);
       auto slash = u.find('/');
@@ -86,6 +102,21 @@ class Gen {
                   done_total_, errors_, t1_ - t0_, pct(0.5), pct(0.99), l.empty() ? 0.0 : l.back() * 1e3);
     std::string s = buf;
     escape_to(s, first_error_);
+    if (o_.follow) {
+      std::vector<double> f = follow_lat_;
+      std::sort(f.begin(), f.end());
+      auto fp = [&](double p) { return f.empty() ? 0.0 : f[std::min(f.size() - 1, (size_t)(f.size() * p))] * 1e3; };
+      std::snprintf(buf, sizeof buf, ", \"follow_requests\": %zu, \"follow_latency_ms\": {\"p50\": %.3f, \"p99\": %.3f, "
+                    "\"max\": %.3f}", f.size(), fp(0.5), fp(0.99), f.empty() ? 0.0 : f.back() * 1e3);
+      s += buf;
+    }
+    s += ", \"status_counts\": {";
+    bool first = true;
+    for (auto& kv : statuses_) {
+      s += (first ? "\"" : ", \"") + std::to_string(kv.first) + "\": " + std::to_string(kv.second);
+      first = false;
+    }
+    s += "}";
     // per step: [ms until the last create returned, ms until the step completed (counter reached)]
     s += ", \"steps_ms\": [";
     for (size_t i = 0; i < steps_.size(); ++i) {
@@ -110,6 +141,27 @@ class Gen {
   std::string first_error_;
   std::vector<std::pair<double, double>> steps_;
   double step_t0_ = 0, step_creates_ = 0;
+  bool templated_ = false, closed_ = false;
+  std::vector<double> follow_lat_;
+  std::map<int, long long> statuses_;
+  long long user_rr_ = 0;
+
+  ev::HeaderList headers_for(long long k) const {
+    ev::HeaderList h = hdrs_;
+    std::string u = "u" + std::to_string(o_.users > 0 ? k % o_.users : k) + "@bench.local";
+    for (auto& kv : h)
+      for (size_t at; (at = kv.second.find("{user}")) != std::string::npos;) kv.second.replace(at, 6, u);
+    return h;
+  }
+
+  // the redirect's target on the same endpoint: "/path" or "scheme://host[:port]/path"
+  static std::string location_path(const std::string& loc) {
+    if (!loc.empty() && loc[0] == '/') return loc;
+    auto p = loc.find("://");
+    if (p == std::string::npos) return "/" + loc;
+    auto slash = loc.find('/', p + 3);
+    return slash == std::string::npos ? "/" : loc.substr(slash);
+  }
 
   void begin_step() {
     if (step_t0_ > 0) steps_.emplace_back(step_creates_, ev::now_s() - step_t0_);
@@ -125,25 +177,53 @@ class Gen {
   }
 
   void issue() {
-    if (issued_ >= o_.batch) return;
+    if (closed_ || issued_ >= o_.batch) return;
+    if (o_.duration_s > 0 && ev::now_s() - step_t0_ >= o_.duration_s) {  // the clock closes the step
+      closed_ = true;
+      o_.batch = (int)std::min<long long>(issued_, 1 << 30);
+      if (done_ == issued_) end_step();
+      return;
+    }
     long long i = issued_++;
     const ev::Endpoint& ep = o_.targets[rr_++ % o_.targets.size()];
     const std::string& body = o_.bodies[(size_t)((step_ * (long long)o_.batch + i) % (long long)o_.bodies.size())];
     double t = ev::now_s();
-    client_.request(ep, o_.method, o_.path, hdrs_, body, 60, [this, t](ev::ClientResult&& r) {
+    auto hdrs = std::make_shared<ev::HeaderList>(templated_ ? headers_for(user_rr_++) : hdrs_);
+    client_.request(ep, o_.method, o_.path, *hdrs, body, 60, [this, t, &ep, hdrs](ev::ClientResult&& r) {
       lat_.push_back(ev::now_s() - t);
+      if (!r.err) statuses_[r.resp.status]++;
       bool bad = r.err || (o_.expect && r.resp.status != o_.expect);
-      if (bad) {
-        errors_++;
-        if (first_error_.empty())
-          first_error_ = r.err ? std::string("errno ") + std::to_string(r.err)
-                               : "HTTP " + std::to_string(r.resp.status) + " " + r.resp.body.substr(0, 200);
+      if (bad) note_error(r);
+      const std::string* loc = r.err ? nullptr : r.resp.header("location");
+      if (!bad && o_.follow && loc && r.resp.status >= 300 && r.resp.status < 400) {
+        double t2 = ev::now_s();
+        ev::HeaderList fh;
+        for (auto& kv : *hdrs)
+          if (kv.first != "content-type") fh.push_back(kv);
+        client_.request(ep, "GET", location_path(*loc), fh, {}, 60, [this, t2](ev::ClientResult&& r2) {
+          follow_lat_.push_back(ev::now_s() - t2);
+          if (!r2.err) statuses_[r2.resp.status]++;
+          if (r2.err || r2.resp.status != 200) note_error(r2);
+          finish_one();
+        });
+        return;
       }
-      done_++;
-      done_total_++;
-      if (done_ == o_.batch) end_step();
-      else issue();
+      finish_one();
     });
+  }
+
+  void note_error(const ev::ClientResult& r) {
+    errors_++;
+    if (first_error_.empty())
+      first_error_ = r.err ? std::string("errno ") + std::to_string(r.err)
+                           : "HTTP " + std::to_string(r.resp.status) + " " + r.resp.body.substr(0, 200);
+  }
+
+  void finish_one() {
+    done_++;
+    done_total_++;
+    if (done_ == o_.batch || (closed_ && done_ == issued_)) end_step();
+    else issue();
   }
 
   void end_step() {
@@ -236,6 +316,9 @@ int main(int argc, char** argv) {
     else if (a == "--until-url") o.until_urls.push_back(next());
     else if (a == "--until-field") o.until_field = next();
     else if (a == "--tls-ca") o.tls_ca = next();
+    else if (a == "--follow") o.follow = true;
+    else if (a == "--users") o.users = std::max(0, std::atoi(next().c_str()));
+    else if (a == "--duration") o.duration_s = std::atof(next().c_str());
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--bodies") {

@@ -10,6 +10,7 @@
 #include "broker.hpp"
 #include "cpuscan.hpp"
 #include "docstore.hpp"
+#include "dutycycle.hpp"
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
 #include "formcodec.hpp"
@@ -235,6 +236,32 @@ PYBIND11_MODULE(_ttnative, m) {
     }
     return out;
   });
+  // The watchdog CPU duty cycle on a native thread (dutycycle.hpp; platform/limits.py).
+  py::class_<DutyCycle>(m, "DutyCycle")
+      .def(py::init<double>(), py::arg("period_s"))
+      .def("add", &DutyCycle::add, py::arg("name"), py::arg("pid"), py::arg("cpu"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("remove", &DutyCycle::remove, py::arg("name"), py::call_guard<py::gil_scoped_release>())
+      .def("start", &DutyCycle::start)
+      .def("stop", &DutyCycle::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("period_s", &DutyCycle::period_s)
+      .def("stats", [](DutyCycle& d) {
+        std::map<std::string, DutyCycle::Stats> st;
+        {
+          py::gil_scoped_release r;
+          st = d.stats();
+        }
+        py::dict out;
+        for (auto& kv : st) {
+          py::dict x;
+          x["throttled_periods"] = kv.second.throttled_periods;
+          x["cpu_seconds"] = kv.second.cpu_seconds;
+          x["stopped_seconds"] = kv.second.stopped_seconds;
+          x["stopped"] = kv.second.stopped;
+          out[py::str(kv.first)] = x;
+        }
+        return out;
+      });
   m.def("parse_http_head", [](py::bytes raw) {
     std::string_view sv = raw;
     HttpHead h;

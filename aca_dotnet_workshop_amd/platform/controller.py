@@ -152,7 +152,7 @@ class EnvironmentController:
             if rt.autoscaler is not None:
                 self._tasks.append(asyncio.ensure_future(self._scale_loop(rt)))
         self._tasks.append(asyncio.ensure_future(self._retention_loop()))
-        if self.limiter.enforce_cpu and self.limiter.mode == "watchdog":
+        if self.limiter.enforce_cpu and self.limiter.mode == "watchdog" and self.limiter.duty is None:
             self._tasks.append(asyncio.ensure_future(self._throttle_loop()))
         self.event("ResourceLimitsApplied", **self.limiter.describe())
         if serve_control:
@@ -596,7 +596,7 @@ class EnvironmentController:
             }
         limits = {**self.limiter.describe(),
                   "replicas": {n: {"cpu": st.limits.cpu, "memoryBytes": st.limits.memory, "peakRssBytes": st.peak_rss,
-                                   "throttledPeriods": st.throttled_periods}
+                                   "throttledPeriods": self.limiter.throttled_periods(n)}
                                for n, st in self.limiter.replicas.items()}}
         return {"name": self.m.name, "envDir": str(self.dir), "backingUrl": self.stack.backing_url,
                 "tls": {"caCert": str(self.pki.ca_crt), "daprMtls": self.mtls},

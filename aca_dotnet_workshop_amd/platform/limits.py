@@ -20,9 +20,11 @@ enforcement mechanisms, chosen at start-up and reported in the environment statu
   throttle: SIGSTOP the group once it has used its quota of the current period, SIGCONT at the
   next -- otherwise only accounted.  The period is 20 ms (``TT_CPU_PERIOD_MS``), five times
   finer than CFS's 100 ms, so a throttled replica stalls for at most a few ms instead of tens;
-  its CPU time is read per thread from ``/proc/<pid>/task/<tid>/schedstat`` (nanoseconds,
-  one native call per tick for every replica) because ``/proc/<pid>/stat`` counts 10 ms clock
-  ticks -- as coarse as the period itself.
+  its CPU time is read per thread from ``/proc/<pid>/task/<tid>/schedstat`` (nanoseconds)
+  because ``/proc/<pid>/stat`` counts 10 ms clock ticks -- as coarse as the period itself.
+  The duty cycle runs on a native thread (``native/src/dutycycle.hpp``: eight checks per period
+  on an absolute clock, so a stopped replica resumes at the period boundary however busy the
+  controller's Python threads are); ``TT_CPU_DUTY=python`` keeps the controller's own tick.
 
 ``environment.resourceLimits`` in the manifest: ``{memory: true|false, cpu: true|false}``
 (both enforced in ``deploy/main.yaml``; the controller's own default without the key is memory
@@ -246,9 +248,19 @@ class ResourceLimiter:
                     self.cpu_root = None
         self.replicas: dict[str, ReplicaState] = {}
         self._reader = _schedstat_reader() if self.mode == "watchdog" and enforce_cpu else None
+        self.duty = None  # the native duty cycle (dutycycle.hpp), when it can run here
+        if self._reader is not None and os.environ.get("TT_CPU_DUTY", "native").lower() != "python":
+            try:
+                from .. import native
+                self.duty = native.load().DutyCycle(PERIOD_S)
+                self.duty.start()
+            except Exception:
+                self.duty = None
 
     def describe(self) -> dict:
         acct = "per-thread schedstat ns" if self._reader else "process clock ticks"
+        if self.duty is not None:
+            acct += ", native thread"
         cpu = {"cgroup2": "cgroup cpu.max", "cgroup1-cpu": "cgroup v1 cpu.cfs_quota_us",
                "watchdog": f"duty-cycle throttle (SIGSTOP/SIGCONT, {PERIOD_S * 1000:g} ms period, {acct})"}[self.mode] \
             if self.enforce_cpu else "accounted"
@@ -281,6 +293,9 @@ class ResourceLimiter:
                 self._adopt_v1(st)
             except OSError:
                 st.cpu_cgroup = None
+        if self.duty is not None:
+            self.duty.add(name, pid, limits.cpu)
+            return st
         if self._reader is not None:
             st.clock = ThreadClock(pid, self._reader)
         st.period_cpu = self._used(st, time.monotonic())
@@ -300,6 +315,8 @@ class ResourceLimiter:
         st = self.replicas.pop(name, None)
         if st is None:
             return
+        if self.duty is not None:
+            self.duty.remove(name)
         if st.stopped:
             self._signal(st, signal.SIGCONT)
         if st.clock is not None:
@@ -353,7 +370,7 @@ class ResourceLimiter:
     def throttle_tick(self, now: float | None = None) -> None:
         """Call every few ms: stop a replica's group once it has used ``cpu x PERIOD_S`` CPU
         seconds in the current period, resume it when the next period starts."""
-        if not self.enforce_cpu or self.mode != "watchdog":
+        if not self.enforce_cpu or self.mode != "watchdog" or self.duty is not None:
             return
         now = time.monotonic() if now is None else now
         for st in list(self.replicas.values()):
@@ -373,9 +390,21 @@ class ResourceLimiter:
                 st.stopped = True
                 st.throttled_periods += 1
 
+    def throttled_periods(self, name: str) -> int:
+        if self.duty is not None:
+            return int((self.duty.stats().get(name) or {}).get("throttled_periods", 0))
+        st = self.replicas.get(name)
+        return st.throttled_periods if st else 0
+
+    def duty_stats(self) -> dict[str, dict]:
+        """Per replica: periods throttled, CPU and stopped seconds (native duty cycle only)."""
+        return dict(self.duty.stats()) if self.duty is not None else {}
+
     def release_all(self) -> None:
         for name in list(self.replicas):
             self.remove(name)
+        if self.duty is not None:
+            self.duty.stop()
         for root in (self.root, self.cpu_root):
             if root is not None:
                 try:

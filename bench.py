@@ -92,6 +92,10 @@ def parse() -> argparse.Namespace:
                     help="vCPU per replica (reference: 0.25); 0 = this rank's CPUs divided over its replicas")
     ap.add_argument("--trace-sampling", type=float, default=1.0,
                     help="App Insights sampling percentage of request traces (the manifest default is 100)")
+    ap.add_argument("--envelope-s", type=float, default=20.0,
+                    help="seconds of the secondary reference-envelope run (config.reference_envelope: the "
+                         "manifest defaults -- 1/1 frontend/API, processor 1..5 on KEDA, 0.25 vCPU, 4000 RU/s -- "
+                         "with the create's 302 followed to /Tasks/Index); 0 = skip")
     ap.add_argument("--direct-steps", type=int, default=-1,
                     help="steps of the api_sidecar_direct comparison run (-1 = a quarter of --steps, 0 = skip)")
     return ap.parse_args()
@@ -648,6 +652,24 @@ def _ingress_cpu(env) -> dict[str, float]:
         return {}
 
 
+def _throttling(before: dict, after: dict, dt: float) -> dict | None:
+    """Per app, over the timed region: periods in which a replica was stopped by the duty cycle
+    and the share of wall time its replicas spent stopped (native duty cycle only)."""
+    if not after or dt <= 0:
+        return None
+    out: dict[str, dict] = {}
+    for name, st in after.items():
+        app = next((x for x in (FRONTEND, API, PROC) if name.startswith(x + "-")), name)
+        b = before.get(name) or {}
+        o = out.setdefault(app, {"throttled_periods": 0, "stopped_s": 0.0, "replicas": 0})
+        o["throttled_periods"] += int(st["throttled_periods"]) - int(b.get("throttled_periods", 0))
+        o["stopped_s"] += float(st["stopped_seconds"]) - float(b.get("stopped_seconds", 0.0))
+        o["replicas"] += 1
+    for o in out.values():
+        o["stopped_share"] = round(o.pop("stopped_s") / (dt * max(1, o["replicas"])), 3)
+    return out
+
+
 def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
     """Microseconds of CPU per created task: in total and per role, from the timed region's
     cores-busy figures (a box-independent view of the headline: throughput = cores / cost)."""
@@ -663,6 +685,104 @@ def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
 # relative CPU per created task of one replica of each app (app process + its sidecar), from the
 # per-process attribution of the frontend-entry bench at ~40k tasks/s (profiles/r3_mtls_cost.md)
 CPU_WEIGHT = {"frontend": 1.0, "api": 1.32, "processor": 0.6}
+
+
+def _sidecar_counter(uds: str, op: str) -> int:
+    """A native data plane's ``sidecar_native_requests_total`` for one operation (all statuses)."""
+    import socket as _socket
+    s = _socket.socket(_socket.AF_UNIX, _socket.SOCK_STREAM)
+    try:
+        s.settimeout(10)
+        s.connect(uds)
+        s.sendall(b"GET /metrics HTTP/1.1\r\nhost: x\r\nconnection: close\r\n\r\n")
+        buf = b""
+        while chunk := s.recv(65536):
+            buf += chunk
+    except OSError:
+        return 0
+    finally:
+        s.close()
+    total = 0
+    for ln in buf.decode(errors="replace").splitlines():
+        if ln.startswith("sidecar_native_requests_total{") and f'op="{op}"' in ln:
+            total += int(float(ln.rsplit(" ", 1)[1]))
+    return total
+
+
+def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
+    """The reference's own capacity envelope, measured (BASELINE.md "Configured capacity"):
+    ``deploy/main.yaml`` with its defaults -- frontend and API at 1..1 replica, the processor at
+    1..5 on the KEDA Service Bus rule (10 messages per replica), 0.25 vCPU / 0.5 Gi every
+    replica, Cosmos at 4,000 RU/s, mTLS, external HTTPS ingress -- and browser-shaped load: per
+    user (a cookie each, so task lists stay bounded) POST /Tasks/Create, then the 302 followed to
+    GET /Tasks/Index (the read path, Pages/Tasks/Index.cshtml.cs:48).  Only the KEDA polling
+    interval is shortened (5 s instead of ACA's 30 s) so scale-out happens inside the run."""
+    import threading
+
+    from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
+    from aca_dotnet_workshop_amd.platform.manifest import load_manifest
+    m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
+                      {"notifierMode": "log", "kedaPollingIntervalSeconds": 5,
+                       "environmentName": f"cae-envelope-r{rank}"})
+    env = BackgroundEnvironment(m, os.path.join(root, "envelope"), log_level="warning")
+    peak = {"processor": 1}
+    stop = threading.Event()
+
+    def watch() -> None:  # the processor replicas KEDA reached
+        while not stop.wait(0.5):
+            rt = env.ctl.apps.get(PROC) if env.ctl else None
+            if rt is not None and rt.current is not None:
+                peak["processor"] = max(peak["processor"], len([r for r in rt.current.replicas if r.alive()]))
+    try:
+        env.start()
+        ing = env.ctl.apps[FRONTEND].ingress
+        ca = str(env.ctl.pki.ca_crt)
+        base = f"https://127.0.0.1:{ing.public_port}"
+        cookie, token = _form_session(base, "u0@bench.local", ca)
+        af = [c for c in cookie.split("; ") if not c.startswith("TasksCreatedByCookie=")]
+        bodies = os.path.join(root, "envelope-bodies.txt")
+        with open(bodies, "wb") as f:
+            f.write(b"\n".join(_form_bodies(4096, token, 0)) + b"\n")
+        counts = [f"{env.backing_url}/servicebus/taskstracker/counts?entity=tasksavedtopic/subscriptions/{PROC}"]
+        api_uds = [r.sidecar_uds for r in env.replicas(API)]
+        st0 = _collection_stats(env.backing_url).get("throughput", {})
+        retry0 = sum(_sidecar_counter(u, "state.throttled_retry") for u in api_uds)
+        th = threading.Thread(target=watch, daemon=True)
+        th.start()
+        import subprocess
+        cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies, "--content-type",
+               "application/x-www-form-urlencoded", "--header",
+               "Cookie: " + "; ".join(["TasksCreatedByCookie={user}"] + af), "--users", "500", "--follow",
+               "--concurrency", "32", "--duration", str(seconds), "--expect", "302", "--tls-ca", ca,
+               "--target", base, *_until(counts)]
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 600)
+        wall = time.perf_counter() - t0
+        rep = json.loads(p.stdout.strip().splitlines()[-1]) if p.stdout.strip() else {}
+        stop.set()
+        st1 = _collection_stats(env.backing_url).get("throughput", {})
+        retries = sum(_sidecar_counter(u, "state.throttled_retry") for u in api_uds) - retry0
+        tasks = int(rep.get("requests", 0))
+        ru = float(st1.get("ru_consumed", 0.0)) - float(st0.get("ru_consumed", 0.0))
+        el = float(rep.get("elapsed_s") or wall)
+        return {"tasks_per_s": round(tasks / el, 1) if el else None, "tasks": tasks, "seconds": round(el, 2),
+                "errors": rep.get("errors"), "first_error": rep.get("first_error") or None,
+                "create_latency_ms": rep.get("latency_ms"), "list_latency_ms": rep.get("follow_latency_ms"),
+                "lists_followed": rep.get("follow_requests"), "status_counts": rep.get("status_counts"),
+                "ru_per_s_budget": float(st1.get("ru_per_s", 0.0)), "ru_consumed_per_s": round(ru / el, 1) if el else None,
+                "ru_per_task": round(ru / tasks, 2) if tasks else None,
+                "store_429s": int(st1.get("throttled", 0) - st0.get("throttled", 0)),
+                "sidecar_429_retries": retries,
+                "budget_over_ru_per_task": round(float(st1.get("ru_per_s", 0.0)) / (ru / tasks), 1) if tasks and ru else None,
+                "processor_replicas_reached": peak["processor"],
+                "replicas": {"frontend": 1, "api": 1, "processor": "1..5 (KEDA, 10 messages per replica)"},
+                "vcpu_per_replica": 0.25, "users": 500, "concurrency": 32,
+                "keda_polling_s": 5, "loadgen_exit": p.returncode}
+    except Exception as e:  # reported, not fatal to the headline
+        return {"error": repr(e)[:500]}
+    finally:
+        stop.set()
+        env.stop()
 
 
 def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
@@ -764,6 +884,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu0.update(_ingress_cpu(env))
+        duty0 = env.ctl.limiter.duty_stats()
         ru0 = _collection_stats(backing).get("throughput", {})
         acc0 = _accel_stats(shards) if sweeper is not None else {}
         if sweeper is not None:
@@ -778,6 +899,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
+        throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
         util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
@@ -821,6 +943,12 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             if not dsteps:
                 time.sleep(1.5)
             sweep_info["trace"] = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids, sweeper.slowest_trace())
+        envelope = None
+        if a.envelope_s > 0 and not shared:  # after the headline's environment is down
+            env.stop()
+            if d.rank == 0:
+                envelope = reference_envelope(exe, root, a.envelope_s, d.rank)
+            d.barrier()
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])
@@ -854,7 +982,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "cpu_us_per_task": cpu_us,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
-                                          "mechanism": lim.get("cpu"), "mode": lim.get("mode")},
+                                          "mechanism": lim.get("cpu"), "mode": lim.get("mode"),
+                                          "throttling_in_timed_region": throttling},
                            "replicas": {"frontend": fe, "api": api, "processor": proc},
                            "notifier": "TasksNotifier:Mode=log (the shipped controller)",
                            "dapr_api_logging": True, "trace_sampling_percent": a.trace_sampling,
@@ -865,7 +994,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
-                           "overdue_sweeps": sweep_info, "api_sidecar_direct": direct}}), flush=True)
+                           "overdue_sweeps": sweep_info, "api_sidecar_direct": direct,
+                           "reference_envelope": envelope}}), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():
             sweeper.stop()

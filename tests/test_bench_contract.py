@@ -34,7 +34,7 @@ def _check(line: dict, n: int, steps: int, warmup: int) -> None:
 def test_bench_single_process():
     env = dict(os.environ, PYTHONPATH=str(ROOT))
     r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32",
-                        "--api-replicas", "1", "--processor-replicas", "1"],
+                        "--api-replicas", "1", "--processor-replicas", "1", "--envelope-s", "4"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -47,6 +47,12 @@ def test_bench_single_process():
     assert cpu["total"] > 0 and cpu["by_role"]["ingress"] > 0 and cpu["apps_frontend_plus_api"] > 0
     sw = cfg["overdue_sweeps"]
     assert len(sw["sweep_ms"]) == sw["sweeps"] and max(sw["sweep_ms"], default=0) == (sw["sweep_max_ms"] or 0)
+    # the secondary run inside the reference's envelope: 1/1 replicas, 0.25 vCPU, 4000 RU/s, the
+    # create's redirect followed to the task list
+    ev = cfg["reference_envelope"]
+    assert ev["tasks"] > 0 and ev["errors"] == 0 and ev["ru_per_s_budget"] == 4000.0, ev
+    assert ev["lists_followed"] == ev["tasks"] and ev["list_latency_ms"]["p50"] > 0
+    assert ev["processor_replicas_reached"] >= 1 and ev["ru_per_task"] > 5
 
 
 def test_bench_api_sidecar_entry_single_process():
@@ -65,7 +71,8 @@ def test_bench_two_ranks_torchrun():
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--batch", "32", "--api-replicas", "1", "--processor-replicas", "1"]
+           "--steps", "2", "--warmup", "1", "--batch", "32", "--api-replicas", "1", "--processor-replicas", "1",
+           "--envelope-s", "0"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)

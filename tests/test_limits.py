@@ -56,11 +56,16 @@ def test_memory_under_limit_is_left_alone():
         lim.release_all()
 
 
-def test_cpu_throttle_holds_quota():
+@pytest.mark.parametrize("duty", ["native", "python"])
+def test_cpu_throttle_holds_quota(duty, monkeypatch):
+    """The duty cycle on its native thread (dutycycle.hpp; ``throttle_tick`` is then a no-op)
+    and the controller's own Python tick hold a busy loop at its quota."""
+    monkeypatch.setenv("TT_CPU_DUTY", duty)
     p = _spawn("while True: pass")
     lim = ResourceLimiter("t", enforce_cpu=True, allow_cgroup=False)
     try:
-        st = lim.add("busy-0", p.pid, Limits(0.25, parse_memory("0.5Gi")))
+        assert (lim.duty is not None) == (duty == "native")
+        lim.add("busy-0", p.pid, Limits(0.25, parse_memory("0.5Gi")))
         c0, t0 = cpu_seconds(tree(p.pid)), time.monotonic()
         while time.monotonic() - t0 < 3.0:
             lim.throttle_tick()
@@ -68,18 +73,24 @@ def test_cpu_throttle_holds_quota():
         used = cpu_seconds(tree(p.pid)) - c0
         wall = time.monotonic() - t0
         assert 0.15 < used / wall < 0.35, used / wall  # ~0.25 cores, not 1.0
-        assert st.throttled_periods >= 50  # 20 ms periods: a short stall each, not a long one
+        assert lim.throttled_periods("busy-0") >= 50  # 20 ms periods: a short stall each, not a long one
         d = lim.describe()
         assert d["mode"] == "watchdog" and "20 ms period" in d["cpu"] and "schedstat" in d["cpu"], d
+        assert ("native thread" in d["cpu"]) == (duty == "native")
+        if duty == "native":
+            st = lim.duty_stats()["busy-0"]
+            assert 0.5 < st["stopped_seconds"] and 0.4 < st["cpu_seconds"] < 1.2, st
     finally:
         lim.release_all()
         os.killpg(p.pid, 9)
         p.wait()
 
 
-def test_cpu_throttle_counts_threads_started_later():
+@pytest.mark.parametrize("duty", ["native", "python"])
+def test_cpu_throttle_counts_threads_started_later(duty, monkeypatch):
     """A replica whose process starts busy threads after it was added: their CPU counts (the
     per-thread clock picks new threads up from zero) and the group is held at its quota."""
+    monkeypatch.setenv("TT_CPU_DUTY", duty)
     p = _spawn("import threading, time\ntime.sleep(0.3)\n"
                "def spin():\n    while True: pass\n"
                "[threading.Thread(target=spin, daemon=True).start() for _ in range(2)]\nwhile True: time.sleep(1)")
