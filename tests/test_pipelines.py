@@ -130,6 +130,29 @@ def test_ado_pipeline_deploys_published_images_then_tears_down(published):
     assert not env_dir.exists()
 
 
+def test_ado_pipeline_registry_branch_imports_and_deploys(published):
+    """With ``CONTAINER_REGISTRY_NAME`` set, the Azure DevOps pipeline takes the registry branch
+    (reference .ado/infra-deploy.yml:110-179): Create_Import_ACR creates the registry and
+    imports the published images into it, Deploy_With_ACR deploys the environment from that
+    registry (AcrPull), and the published-images Deploy stage is skipped."""
+    env_dir = published / "ado-acr-env"
+    over = {"ENV_DIR": str(env_dir), "CONTAINER_REGISTRY_NAME": "adoacr"}
+    res = P.run(P.load(ADO), {}, env_overrides=over)
+    assert not _failed(res), _failed(res)
+    assert _status(res) == {"Lint": "success", "Validate": "success", "Deploy": "skipped",
+                            "Create_Import_ACR": "success", "Deploy_With_ACR": "success", "Teardown": "skipped"}
+    from aca_dotnet_workshop_amd.platform.registry import LocalRegistry
+    assert {r["repository"] for r in LocalRegistry("adoacr").repositories()} == {
+        f"tasksmanager/{a}" for a in ("tasksmanager-backend-api", "tasksmanager-backend-processor",
+                                      "tasksmanager-frontend-webapp")}
+    state = json.loads((env_dir / "state.json").read_text())["status"]
+    for app in ("tasksmanager-backend-api", "tasksmanager-backend-processor", "tasksmanager-frontend-webapp"):
+        assert state["apps"][app]["image"] == f"adoacr.azurecr.io/tasksmanager/{app}:latest"
+    res = P.run(P.load(ADO), {"parameters": {"teardown": True}}, env_overrides=over)
+    assert _status(res)["Teardown"] == "success"
+    assert not env_dir.exists()
+
+
 def test_docs_pipelines_preview_release_publish(tmp_path):
     pages = tmp_path / "gh-pages"
     env = {"PAGES_DIR": str(pages)}
