@@ -77,6 +77,24 @@ def format_datetime(dt: datetime) -> str:
     return s
 
 
+def format_roundtrip(dt: datetime) -> str:
+    """.NET's round-trip ``"O"`` form: always seven fractional digits (microsecond precision
+    here, the tick digit 0).  The store holds ``TaskCreatedOn`` this way, so the string order it
+    sorts by equals the DateTime order (System.Text.Json's trimmed fraction does not sort:
+    ``...:42Z`` > ``...:42.1Z``); every reader parses both forms."""
+    s = f"{dt.year:04d}-{dt.month:02d}-{dt.day:02d}T{dt.hour:02d}:{dt.minute:02d}:{dt.second:02d}.{dt.microsecond:06d}0"
+    if dt.tzinfo is not None:
+        off = dt.utcoffset() or timedelta(0)
+        if off == timedelta(0):
+            s += "Z"
+        else:
+            total = int(off.total_seconds() // 60)
+            sign = "+" if total >= 0 else "-"
+            total = abs(total)
+            s += f"{sign}{total // 60:02d}:{total % 60:02d}"
+    return s
+
+
 def format_fixed(dt: datetime, fmt: str = "yyyy-MM-ddTHH:mm:ss") -> str:
     """Port of the custom ``DateTimeConverter`` write path
     (reference Utilities/DateTimeConverter.cs:26-29) for the formats the reference uses."""

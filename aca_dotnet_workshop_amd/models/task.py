@@ -20,7 +20,7 @@ from typing import Annotated, Any, ClassVar
 from pydantic import BaseModel, BeforeValidator, ConfigDict, PlainSerializer, model_validator
 from pydantic.alias_generators import to_camel
 
-from .dotnet import DOTNET_MIN, GUID_EMPTY, format_datetime, parse_datetime, parse_guid
+from .dotnet import DOTNET_MIN, GUID_EMPTY, format_datetime, format_roundtrip, parse_datetime, parse_guid
 
 DotNetDateTime = Annotated[
     datetime,
@@ -99,6 +99,15 @@ class TaskModel(WireModel):
     task_assigned_to: str = ""
     is_completed: bool = False
     is_over_due: bool = False
+
+
+    def to_store_json(self) -> str:
+        """The document the store holds (and the tasksaved event carries): the wire JSON with
+        ``taskCreatedOn`` in the round-trip form (``format_roundtrip``), whose string order is the
+        DateTime order -- the ORDER BY the overdue sweep pages by (TasksStoreManager.cs:136)."""
+        s = self.to_json()
+        c = self.task_created_on
+        return s.replace(f'"taskCreatedOn":"{format_datetime(c)}"', f'"taskCreatedOn":"{format_roundtrip(c)}"', 1)
 
 
 class TaskAddModel(WireModel):
@@ -205,7 +214,8 @@ def conditional_mark_wire(got: bytes) -> tuple[list[str], bytes, int] | None:
             skipped += 1
             continue
         t.is_over_due = True
-        item: dict[str, Any] = {"key": r["key"], "value": t.to_wire(), "options": {"concurrency": "first-write"}}
+        item: dict[str, Any] = {"key": r["key"], "value": json.loads(t.to_store_json()),
+                                "options": {"concurrency": "first-write"}}
         if r.get("etag"):
             item["etag"] = r["etag"]
         items.append(item)

@@ -116,11 +116,21 @@ inline bool new_guid(Entropy& rng, std::string& out) {
 inline void put2(std::string& o, int v) { o += (char)('0' + v / 10); o += (char)('0' + v % 10); }
 inline void put4(std::string& o, int v) { put2(o, v / 100); put2(o, v % 100); }
 
-// System.Text.Json DateTime: "yyyy-MM-ddTHH:mm:ss[.f{1,6} trimmed][Z]"
-inline void format_dt(std::string& o, int y, int mo, int d, int h, int mi, int s, int us, bool utc) {
+// System.Text.Json DateTime: "yyyy-MM-ddTHH:mm:ss[.f{1,6} trimmed][Z]"; `fixed7`: the
+// round-trip "O" form instead, always 7 fractional digits -- how the store holds TaskCreatedOn,
+// so the string order the store sorts by is the DateTime order (models/dotnet.py
+// format_roundtrip; the API's ORDER BY page and the reference's OrderBy then agree).
+inline void format_dt(std::string& o, int y, int mo, int d, int h, int mi, int s, int us, bool utc,
+                      bool fixed7 = false) {
   put4(o, y); o += '-'; put2(o, mo); o += '-'; put2(o, d); o += 'T';
   put2(o, h); o += ':'; put2(o, mi); o += ':'; put2(o, s);
-  if (us) {
+  if (fixed7) {
+    char f[8];
+    for (int i = 5; i >= 0; --i) { f[i] = (char)('0' + us % 10); us /= 10; }
+    f[6] = '0';  // microsecond precision: the tick digit
+    o += '.';
+    o.append(f, 7);
+  } else if (us) {
     char f[7];
     for (int i = 5; i >= 0; --i) { f[i] = (char)('0' + us % 10); us /= 10; }
     int n = 6;
@@ -133,8 +143,9 @@ inline void format_dt(std::string& o, int y, int mo, int d, int h, int mi, int s
 
 inline bool leap(int y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
 
-// parse_datetime's grammar minus offsets; false = let the general binder decide.
-inline bool parse_due(std::string_view v, std::string& out) {
+// parse_datetime's grammar minus offsets; false = let the general binder decide.  `fixed7`: the
+// store's round-trip form (format_dt).
+inline bool parse_due(std::string_view v, std::string& out, bool fixed7 = false) {
   auto dig = [&](size_t i, size_t n, int& r) {
     if (i + n > v.size()) return false;
     r = 0;
@@ -168,7 +179,7 @@ inline bool parse_due(std::string_view v, std::string& out) {
   static const int mdays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
   if (y < 1 || mo < 1 || mo > 12 || d < 1 || d > mdays[mo - 1] + (mo == 2 && leap(y)) || h > 23 || mi > 59 || s > 59)
     return false;
-  format_dt(out, y, mo, d, h, mi, s, us, utc);
+  format_dt(out, y, mo, d, h, mi, s, us, utc, fixed7);
   return true;
 }
 
@@ -240,7 +251,7 @@ inline bool create(std::string_view body, Entropy& rng, Created& out) {
   tt::escape_to(j, f[1] ? std::string_view(f[1]->s) : std::string_view());
   j += ",\"taskCreatedOn\":\"";
   format_dt(j, tmv.tm_year + 1900, tmv.tm_mon + 1, tmv.tm_mday, tmv.tm_hour, tmv.tm_min, tmv.tm_sec,
-            (int)(ts.tv_nsec / 1000), true);
+            (int)(ts.tv_nsec / 1000), true, true);
   j += "\",\"taskDueDate\":\"";
   j += due;
   j += "\",\"taskAssignedTo\":";
@@ -408,8 +419,10 @@ inline bool task_fields(const tt::Value& doc, const tt::Value* (&f)[8]) {
 }
 
 // Canonical TaskModel JSON of `doc` (isOverDue forced true when `overdue`); `due_day` receives
-// the due date's "YYYY-MM-DD".  false = outside the envelope.
-inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std::string& id, std::string& due_day) {
+// the due date's "YYYY-MM-DD".  `store_form`: TaskCreatedOn in the store's round-trip form
+// (format_dt fixed7) -- for a document written back to the store.  false = outside the envelope.
+inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std::string& id, std::string& due_day,
+                       bool store_form = false) {
   const tt::Value* f[8];
   if (!task_fields(doc, f)) return false;
   for (int j = 0; j < 6; ++j)
@@ -420,7 +433,7 @@ inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std
   if (!is_guid36(id)) return false;
   for (char& c : id) c = (char)std::tolower((unsigned char)c);
   std::string created = "0001-01-01T00:00:00", due = "0001-01-01T00:00:00";
-  if (f[3] && (created.clear(), !parse_due(f[3]->s, created))) return false;
+  if (f[3] && (created.clear(), !parse_due(f[3]->s, created, store_form))) return false;
   if (f[4] && (due.clear(), !parse_due(f[4]->s, due))) return false;
   due_day = due.substr(0, 10);
   static const std::string empty;
@@ -510,7 +523,7 @@ inline bool conditional_mark(std::string_view got, std::string& bulk, std::vecto
     bulk += "{\"key\":";
     tt::escape_to(bulk, key->s);
     bulk += ",\"value\":";
-    if (!write_task(*data, true, bulk, id, day)) return false;
+    if (!write_task(*data, true, bulk, id, day, true)) return false;
     if (etag != nullptr && etag->t == tt::Value::String && !etag->s.empty()) {
       bulk += ",\"etag\":";
       tt::escape_to(bulk, etag->s);

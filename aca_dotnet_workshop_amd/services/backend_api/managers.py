@@ -172,7 +172,7 @@ class TasksStoreManager(TasksManager):
         t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
                       task_due_date=due_date, task_assigned_to=assigned_to)
         log.info("Save a new task with name: '%s' to state store", t.task_name)
-        payload = RawJson(t.to_json())  # serialised once for the save and the event
+        payload = RawJson(t.to_store_json())  # serialised once for the save and the event
         await self.client.save_state(self.store, str(t.task_id), payload)
         await self._publish_task_saved(t, payload)
         return t.task_id
@@ -231,7 +231,8 @@ class TasksStoreManager(TasksManager):
             before = t.model_copy()
             mutate(t)
             try:
-                await self.client.save_state(self.store, str(t.task_id), t, etag=etag, concurrency="first-write")
+                await self.client.save_state(self.store, str(t.task_id), RawJson(t.to_store_json()), etag=etag,
+                                             concurrency="first-write")
                 return before, t  # type: ignore[return-value]
             except InvocationError as e:
                 if e.status in (409, 412):
@@ -295,8 +296,9 @@ class TasksStoreManager(TasksManager):
     def _range_query(self, limit: int | None) -> tuple[dict, str, int]:
         """The open tasks due before today's midnight, oldest first: ``ORDER BY taskCreatedOn``
         in the store picks the page (reference ``.OrderBy(o => o.TaskCreatedOn)``,
-        TasksStoreManager.cs:136); the page itself is then ordered by the DateTime value (the
-        stored strings carry a trimmed fraction, see ``tasks_from_query_wire``)."""
+        TasksStoreManager.cs:136) -- the stored round-trip strings sort as DateTimes; the page is
+        re-ordered by the DateTime value on the way out all the same (documents written by other
+        clients may carry System.Text.Json's trimmed fraction, see ``tasks_from_query_wire``)."""
         midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
         page = limit if limit and limit > 0 else self.overdue_page
         q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
@@ -309,7 +311,9 @@ class TasksStoreManager(TasksManager):
         """``OverdueTasks:Query=range`` (SURVEY.md §2.12 #7 fixed): every open task due before
         today, whatever its time of day and however many daily runs were missed, filtered by
         the store rather than in the app -- a range leaf plus two boolean leaves, which the
-        backing planner runs as a gfx950 columnar scan.  One page (oldest first) per call: the
+        backing planner runs as a gfx950 columnar scan.  The store orders by the stored
+        ``taskCreatedOn`` (round-trip form, ``TaskModel.to_store_json``), which is the DateTime
+        order of the reference's ``OrderBy``.  One page (oldest first) per call: the
         processor marks a page overdue and asks again, and marked tasks drop out of the filter."""
         q, midnight, page = self._range_query(limit)
         log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
@@ -373,4 +377,5 @@ class TasksStoreManager(TasksManager):
     async def _publish_task_saved(self, t: TaskModel, payload: RawJson | None = None) -> None:
         log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
                  t.task_id, t.task_name, t.task_assigned_to)
-        await self.client.publish_event(self.pubsub, self.topic, payload if payload is not None else t)
+        await self.client.publish_event(self.pubsub, self.topic,
+                                        payload if payload is not None else RawJson(t.to_store_json()))

@@ -80,13 +80,14 @@ def _sweep(monkeypatch, accel: str, n_tasks: int, page_size: int) -> None:
 def _created_order_case(monkeypatch, accel: str) -> None:
     """Range mode answers ``GET /api/overduetasks`` oldest first by ``TaskCreatedOn`` (reference
     ``.OrderBy(o => o.TaskCreatedOn)``, TasksStoreManager.cs:136): the store picks the page with
-    ``ORDER BY taskCreatedOn`` and the page is ordered by the DateTime (fractions are trimmed,
-    so "...:42Z" precedes "...:42.5Z").  An update to an old task re-appends its mirror row at
-    the end; it must still come back in its creation-time position."""
+    ``ORDER BY taskCreatedOn`` over the stored round-trip strings (seven fractional digits, so
+    string order IS DateTime order, ``TaskModel.to_store_json``) -- the page is exactly the
+    oldest tasks by DateTime, in DateTime order.  An update to an old task re-appends its mirror
+    row at the end; it must still come back in its creation-time position."""
     import random
     from datetime import datetime
 
-    from aca_dotnet_workshop_amd.models.dotnet import format_datetime
+    from aca_dotnet_workshop_amd.models.dotnet import format_roundtrip
     monkeypatch.setenv("TT_QUERY_ACCEL", accel)
     monkeypatch.setenv("TT_QUERY_ACCEL_MIN_DOCS", "0")
     monkeypatch.setenv("TT_QUERY_MIRROR_PATHS", "taskDueDate,isCompleted,isOverDue,taskCreatedOn")
@@ -109,7 +110,7 @@ def _created_order_case(monkeypatch, accel: str) -> None:
             st = env.backing.store("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
             for i, t in enumerate(stamps):
                 k, v = _task_doc(i, due)
-                st.set(k, v.replace('"2024-01-01T00:00:00"', f'"{format_datetime(t)}Z"'))
+                st.set(k, v.replace('"2024-01-01T00:00:00"', f'"{format_roundtrip(t)}Z"'))  # as the API stores it
             c = env.replicas[PROC][0].client
             oldest = min(range(n), key=lambda i: stamps[i])
             # an update to the oldest task: a new mirror row at the end of the collection
@@ -119,19 +120,15 @@ def _created_order_case(monkeypatch, accel: str) -> None:
             r = await c.invoke_method_raw("GET", API, "api/overduetasks?limit=250")
             assert r.status == 200 and r.headers.get("x-tt-more-results") == "true"
             got = json.loads(r.body)
-            # the page: the first 250 in the store's ORDER BY taskCreatedOn (string order) ...
-            wire = {i: f"{format_datetime(stamps[i])}Z" for i in range(n)}
-            page = sorted(range(n), key=lambda i: wire[i])[:250]
-            # ... handed out in DateTime order, like the reference's in-app OrderBy
-            want = sorted(page, key=lambda i: stamps[i])
+            # the page: exactly the 250 oldest by DateTime, in DateTime order (the reference's OrderBy)
+            want = sorted(range(n), key=lambda i: stamps[i])[:250]
             assert [t["taskId"] for t in got] == [f"00000000-0000-4000-8000-{i:012d}" for i in want]
             assert got[0]["taskName"] == "renamed"
             from aca_dotnet_workshop_amd.models import parse_datetime
             created = [parse_datetime(t["taskCreatedOn"]) for t in got]
-            assert created == sorted(created)
-            # string and DateTime order differ only inside one second: no older second is left out
-            cut = max(stamps[i] for i in page).replace(microsecond=0)
-            assert all(stamps[i] >= cut for i in set(range(n)) - set(page))
+            assert created == sorted(created) and [c.replace(tzinfo=None) for c in created] == [stamps[i] for i in want]
+            # the API answers in System.Text.Json's form (trimmed fraction), not the store's
+            assert all(".0000000" not in t["taskCreatedOn"] and len(t["taskCreatedOn"]) <= 27 for t in got)
             acc = env.backing.accel("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
             assert acc.stats[accel] >= 1 and acc.stats["fallback"] == 0
         finally:

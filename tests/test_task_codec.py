@@ -2,7 +2,7 @@
 
 Invariant: for any body, the codec either declines (``None``: the general binder decides) or
 produces exactly what binding the body with ``TaskAddModel`` and serialising the new
-``TaskModel`` produces -- and it declines every body the binder rejects (400)."""
+``TaskModel`` for the store (``to_store_json``) produces -- and it declines every body the binder rejects (400)."""
 import json
 import uuid
 
@@ -23,7 +23,7 @@ def _reference(body: bytes, made) -> bytes | None:
         t = TaskModel(task_id=uuid.UUID(made[0]) if made else uuid.uuid4(), task_name=m.task_name,
                       task_created_by=m.task_created_by, task_created_on=parse_datetime(created),
                       task_due_date=m.task_due_date, task_assigned_to=m.task_assigned_to)
-        return t.to_json().encode()
+        return t.to_store_json().encode()  # the stored form: taskCreatedOn round-trip ("O")
     except Exception:  # rejected by the binder (400) or unserialisable (500)
         return None
 
