@@ -132,8 +132,15 @@ class CollectionAccelerator:
                 self.stats["bg_syncs"] = self.stats.get("bg_syncs", 0) + 1
                 self.stats["bg_sync_ms"] = round(self.stats.get("bg_sync_ms", 0.0) + (time.perf_counter() - t0) * 1e3, 3)
 
-    def close(self) -> None:
+    def close(self, timeout: float = 10.0) -> None:
+        """Stop the background sync and wait for it: no sync may still be inside the native
+        store or the HIP kernels when the caller tears those down."""
         self._bg_stop.set()
+        bg = self._bg
+        if bg is not None and bg is not threading.current_thread():
+            bg.join(timeout)
+        with self.lock:  # a query's own sync finishes before close returns
+            pass
 
     def query(self, q: dict[str, Any], prefix: str, store, sort_keys: bool = False) -> bytes | None:
         """JSON result text (UTF-8 bytes, as the store built it: the page goes out without a

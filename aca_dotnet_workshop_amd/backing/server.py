@@ -281,8 +281,11 @@ class BackingServices:
             s = st(req, "cosmos.write")
             items = req.json() or []
             # a value sent as JSON itself (the native data plane's form) is stored as its compact
-            # text, like the native front does; a string value holds JSON text
-            texts = [v if isinstance(v := it.get("value"), str) else _compact_json(v) for it in items]
+            # text -- the very bytes of the request, compacted by the native front's own scanner
+            # (numbers and escapes as sent); a string value holds JSON text
+            texts = self.N.bulk_values(req.body) if len(req.body) else []
+            if texts is None or len(texts) != len(items):
+                texts = [v if isinstance(v := it.get("value"), str) else _compact_json(v) for it in items]
             if (t := throttled(s, sum(s.write_ru(len(v)) for v in texts) or 1)) is not None:
                 return t
             out = []

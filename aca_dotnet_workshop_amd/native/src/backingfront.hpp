@@ -117,6 +117,45 @@ inline bool scan_bulk_items(const std::string& body, std::vector<DocStore::BulkI
   }
 }
 
+// The stored text of every item's value in a bulkset body, as the native front stores it (a
+// JSON string value: the JSON text it holds; anything else: its compact text), for the items
+// the front leaves to Python (TTL writes) -- both paths store the same bytes.  false: not a
+// valid array of objects (Python answers).
+inline bool scan_bulk_values(const std::string& body, std::vector<std::string>& out) {
+  std::string_view text = body.empty() ? std::string_view("[]") : std::string_view(body);
+  if (!valid(text)) return false;
+  const char* p = ws_end(text.data(), text.data() + text.size());
+  const char* e = text.data() + text.size();
+  if (*p != '[') return false;
+  ++p;
+  while (true) {
+    p = ws_end(p, e);
+    if (*p == ']') return true;
+    if (*p != '{') return false;
+    ++p;
+    std::string value = "null";
+    while (true) {
+      p = ws_end(p, e);
+      if (*p == '}') { ++p; break; }
+      const char* ks = p;
+      p = skip_value(p, e);
+      std::string_view ktok(ks, (size_t)(p - ks));
+      std::string k = ktok.find('\\') == std::string_view::npos ? std::string(ktok.substr(1, ktok.size() - 2))
+                                                               : parse(ktok).s;
+      p = ws_end(ws_end(p, e) + 1, e);  // ':'
+      const char* vs = p;
+      p = skip_value(p, e);
+      std::string_view raw(vs, (size_t)(p - vs));
+      if (k == "value") value = raw.front() == '"' ? parse(raw).s : compact(raw);
+      p = ws_end(p, e);
+      if (*p == ',') ++p;
+    }
+    out.push_back(std::move(value));
+    p = ws_end(p, e);
+    if (*p == ',') ++p;
+  }
+}
+
 class BackingFront {
  public:
   // `threads` event loops share the port via SO_REUSEPORT (connections are spread by the kernel).

@@ -1794,7 +1794,10 @@ class DataPlane {
     }
     // partitioned broker: the message's partitionKey metadata (Service Bus partitioning), else
     // its CloudEvent id, picks the shard
-    const std::string pkey = meta.count("partitionKey") ? meta["partitionKey"] : event_id.empty() ? uuid4() : event_id;
+    // (an empty partitionKey is no key: backing/shards.py routes it by the message id too)
+    const std::string pkey = meta.count("partitionKey") && !meta["partitionKey"].empty() ? meta["partitionKey"]
+                             : event_id.empty()                                          ? uuid4()
+                                                                                         : event_id;
     client_.request(b.ep(pkey), "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
                     body, 60, [d, name, topic](ClientResult&& res) {
                       if (res.err || res.resp.status >= 300) {

@@ -22,11 +22,17 @@ def load_library(build: bool = True) -> ctypes.CDLL:
         build_gpu()
     if not LIB.exists():
         raise RuntimeError(f"GPU kernel library {LIB} is missing; run `python -m aca_dotnet_workshop_amd.ops.build`")
-    # PyDLL: calls keep the GIL.  Every entry point is a kernel launch (microseconds) or a
-    # stream synchronise on a query's own kernels (tens of microseconds); releasing the GIL
-    # around them costs more -- a query thread next to a busy event loop waits up to the switch
-    # interval to get it back, once per call
+    # PyDLL: calls keep the GIL.  Every entry point but one is a kernel launch (microseconds);
+    # releasing the GIL around those costs more -- a query thread next to a busy event loop
+    # waits up to the switch interval to get it back, once per call.  The exception is the
+    # stream synchronise (``_sync``): it waits for whatever the shared stream holds (another
+    # thread's mirror sync included), so it goes through a CDLL handle that drops the GIL while
+    # it waits -- the backing's event loop keeps serving meanwhile.
     lib = ctypes.PyDLL(str(LIB))
+    wait = ctypes.CDLL(str(LIB))
+    wait.tt_stream_sync.argtypes = [ctypes.c_void_p]
+    wait.tt_stream_sync.restype = ctypes.c_int
+    lib.blocking_sync = wait.tt_stream_sync
     P, I64, I32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     lib.tt_launch_scan_eval.argtypes = [P, I64, P, P, I32, P, I32, P, P, P]
     lib.tt_launch_scan_eval.restype = ctypes.c_int
@@ -46,8 +52,6 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_select_le_bin.argtypes = [P, P, I64, I32, ctypes.c_uint32, P, P, P, ctypes.c_uint32, P]
     lib.tt_launch_select_le_bin.restype = ctypes.c_int
     lib.tt_hist_bins.restype = ctypes.c_int
-    lib.tt_set_eval_groups.argtypes = [ctypes.c_int]
-    lib.tt_set_eval_groups.restype = ctypes.c_int
     lib.tt_launch_rank_encode.argtypes = [P, P, I32, I64, I64, P, I32, P]
     lib.tt_launch_rank_encode.restype = ctypes.c_int
     lib.tt_page_cap.restype = ctypes.c_int
@@ -92,14 +96,6 @@ class GpuKernels:
         self._bufs: dict[str, Any] = {}
         self._est: dict[int, int] = {}  # last selection count per device program: output sizing
         self.page_cap = int(self.lib.tt_page_cap())
-        # Result ordering sorts (key, row) pairs over the packed key's used bits only
-        # (hip/radix_pairs.hip); False = torch.sort argsort + gather, for A/B runs.
-        self.pair_sort = True
-
-    def set_eval_groups(self, u: int) -> None:
-        """Row groups per lane in ``tt_scan_eval`` (1, 2, 4 or 8): registers vs loads in flight."""
-        if self.lib.tt_set_eval_groups(int(u)) != 0:
-            raise ValueError("eval groups must be 1, 2, 4 or 8")
 
     def _stream(self) -> ctypes.c_void_p:
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -208,7 +204,7 @@ class GpuKernels:
         return mb
 
     def _sync(self, stream) -> None:
-        rc = self.lib.tt_stream_sync(stream)
+        rc = self.lib.blocking_sync(stream)  # GIL released while waiting (see load_library)
         if rc != 0:
             raise RuntimeError(f"stream synchronise failed ({rc})")
 
@@ -331,10 +327,10 @@ class GpuKernels:
         return out[:k] if k is not None else out
 
     def _sorted_rows(self, keys, rows, key_bits: int):
-        """``rows`` ordered by ``keys`` (ascending, stable)."""
-        if not self.pair_sort or rows.dtype != self.torch.int32 or keys.dtype != self.torch.int64:
-            _, idx = self.torch.sort(keys)
-            return rows[idx]
+        """``rows`` ordered by ``keys`` (ascending, stable): ``tt_sort_pairs``, the LSD radix
+        sort of (key, row) pairs over the key's used bits (hip/radix_pairs.hip)."""
+        if rows.dtype != self.torch.int32 or keys.dtype != self.torch.int64:
+            raise ValueError("the pair sort takes int64 keys and int32 rows")
         keys, rows = keys.contiguous(), rows.contiguous()
         n = keys.numel()
         end_bit = max(1, min(64, int(key_bits)))

@@ -314,13 +314,9 @@ tt_group_count(const ColumnDesc* __restrict__ cols, int32_t g, const uint16_t* _
 }
 
 // ------------------------------------------------------------------ host launchers
-// Row groups per lane of the scan kernel (1, 2, 4 or 8); tunable for A/B measurements.
-static int g_eval_groups = 2;  // measured on MI355X: 1 -> 0.183 ms, 2 -> 0.175 ms, 4 -> 0.194 ms per 1e8-row query
-extern "C" int tt_set_eval_groups(int u) {
-  if (u != 1 && u != 2 && u != 4 && u != 8) return -1;
-  g_eval_groups = u;
-  return 0;
-}
+// Row groups per lane of the scan kernel: 2, measured on MI355X over a 1e8-row query --
+// 1 -> 0.183 ms, 2 -> 0.175 ms, 4 -> 0.194 ms (profiles/r1_query_scan_kernels_v3.md).
+constexpr int kEvalGroups = 2;
 
 // Preconditions (checked by the Python wrapper): every column and the live/mask buffers are
 // allocated for a capacity that is a multiple of kTileRows rows, nrows <= capacity.
@@ -332,16 +328,8 @@ extern "C" int tt_launch_scan_eval(const void* cols, int64_t nrows, const uint16
   if (tiles == 0) return 0;
   const size_t lds = bitmap_words <= kMaxLdsBitmapWords ? (size_t)bitmap_words * sizeof(uint32_t) : 0;
   const ColumnDesc* cd = reinterpret_cast<const ColumnDesc*>(cols);
-  switch (g_eval_groups) {
-#define TT_EVAL_CASE(UU)                                                                                   \
-  case UU:                                                                                                  \
-    hipLaunchKernelGGL((tt_scan_eval_t<UU>), dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * UU)), lds, \
-                       stream, cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);    \
-    break;
-    TT_EVAL_CASE(1) TT_EVAL_CASE(4) TT_EVAL_CASE(8)
-    default: TT_EVAL_CASE(2)
-#undef TT_EVAL_CASE
-  }
+  hipLaunchKernelGGL((tt_scan_eval_t<kEvalGroups>), dim3((unsigned)tiles), dim3(kTileRows / (kRowsPerLane * kEvalGroups)),
+                     lds, stream, cd, nrows, live, prog, prog_len, bitmaps, bitmap_words, mask, block_counts);
   return (int)hipGetLastError();
 }
 

@@ -50,6 +50,9 @@ log_notifier = logging.getLogger("TasksNotifierController")
 log_external = logging.getLogger("ExternalTasksProcessorController")
 log_sched = logging.getLogger("ScheduledTasksManagerController")
 
+# consecutive empty pages the API still reports more matches for, before the sweep stops
+EMPTY_MORE_LIMIT = 3
+
 
 def register_controllers(app: WebApp, client: SidecarClient) -> None:
     cfg = app.config
@@ -137,7 +140,7 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
         # -- a marked page drops out of the API's filter, so each request asks for the next one
         page = cfg.get_int("OverdueTasks:PageSize", 0)
         max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
-        retrieved = marked = pages = 0
+        retrieved = marked = pages = empty_more = 0
         run_day = naive_utc(run_at).date().isoformat()
         t_query = t_mark = 0.0  # wall time of the job's two hops (returned for attribution)
         clock = asyncio.get_running_loop().time
@@ -175,10 +178,18 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                 # store's selection were skipped -- ask again; a page of nothing to mark stops
                 if more != "true" or (n_page and not n_overdue):
                     break
+                if not n_page:  # empty yet "more": a few retries, paced, then stop (no hot loop)
+                    empty_more += 1
+                    if empty_more >= EMPTY_MORE_LIMIT:
+                        break
+                    await asyncio.sleep(0.005 * empty_more)
+                else:
+                    empty_more = 0
             elif n_page < page or not n_overdue:
                 break
         return json_response({"runAt": run_at.isoformat(), "retrieved": retrieved, "markedOverdue": marked,
-                              "pages": pages, "queryMs": round(t_query * 1e3, 2), "markMs": round(t_mark * 1e3, 2)})
+                              "pages": pages, "emptyMorePages": empty_more, "queryMs": round(t_query * 1e3, 2),
+                              "markMs": round(t_mark * 1e3, 2)})
 
 
 def create_app(argv: list[str] | None = None, client: SidecarClient | None = None, config=None,

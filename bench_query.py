@@ -33,7 +33,6 @@ def main() -> None:
     ap.add_argument("--no-cpu-native", action="store_true",
                     help="skip the multi-threaded native CPU executor (the fair host baseline)")
     ap.add_argument("--query", action="store_true", help="also time the whole paged query path (ColumnarIndex.query)")
-    ap.add_argument("--eval-groups", type=int, default=0, help="tt_scan_eval row groups per lane (1/2/4/8; 0 = default)")
     ap.add_argument("--page", action="store_true",
                     help="also time the paged sweep query: ORDER BY taskCreatedOn (clustered by insertion) LIMIT 1000 "
                          "through the zone-map page path (hip/page_topk.hip)")
@@ -75,8 +74,6 @@ def main() -> None:
     ix._full_dirty = True
 
     k = GpuKernels("cuda:0")
-    if a.eval_groups:
-        k.set_eval_groups(a.eval_groups)
     flt = {"AND": [{"LT": {"taskDueDate": "2024-07-01T00:00:00"}}, {"EQ": {"isCompleted": False}},
                    {"EQ": {"isOverDue": False}}]}
     prog = ix.compile(flt)
@@ -103,7 +100,7 @@ def main() -> None:
     res = {"metric": "overdue_sweep_rows_per_sec", "value": round(n / dt, 1), "unit": "rows/s", "rows": n,
            "selected": selected, "ms_per_query": round(dt * 1e3, 4), "effective_GBps": round(nbytes / dt / 1e9, 1),
            "device": torch.cuda.get_device_name(0), "tile_rows": TILE,
-           "eval_groups": a.eval_groups or 2, "column_bytes_per_row": widths,
+           "eval_groups": 2, "column_bytes_per_row": widths,
            "range_leaves": int((prog.code[:, 0] == 7).sum())}
     if a.page:
         # creation timestamps: one per 64 rows, rising with the row (rows are appended as tasks
@@ -156,29 +153,25 @@ def main() -> None:
         ix._full_dirty = True
         sort = [{"key": "taskDueDate", "order": "DESC"}]
         st = ix.to_device(k)
-        # A/B: pair radix sort over the used key bits (default) vs torch.sort argsort + gather
-        for pair, suffix in ((False, "_argsort"), (True, "")):
-            k.pair_sort = pair
-            for label, kk in (("top100", 100), ("full", None)):
-                for _ in range(2):
-                    ix.order_gpu(out, sort, k, kk)
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                it = max(1, a.iters // 4)
-                for _ in range(it):
-                    ordered = ix.order_gpu(out, sort, k, kk)
-                torch.cuda.synchronize()
-                res[f"order_{label}{suffix}_ms"] = round((time.perf_counter() - t0) / it * 1e3, 3)
-            if not pair:
-                full_argsort = ordered
+        # the device ordering: tt_sort_keys + the repo's LSD radix sort of (key, row) pairs over
+        # the used key bits (hip/radix_pairs.hip), or radix select + sort for the top 100
+        for label, kk in (("top100", 100), ("full", None)):
+            for _ in range(2):
+                ix.order_gpu(out, sort, k, kk)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            it = max(1, a.iters // 4)
+            for _ in range(it):
+                ordered = ix.order_gpu(out, sort, k, kk)
+            torch.cuda.synchronize()
+            res[f"order_{label}_ms"] = round((time.perf_counter() - t0) / it * 1e3, 3)
         res["ordered_rows"] = int(ordered.numel())
-        res["pair_sort_matches_argsort"] = bool(torch.equal(ordered, full_argsort))
-        # the first page must equal the host ordering of the same selection
+        # the device order equals the host's stable ordering of the same selection, entirely
         sel = out.cpu().numpy()
         plan = ix.sort_specs(sort)
         host_keys = ix.sort_keys_numpy(sel, plan)
-        top = sel[np.argsort(host_keys, kind="stable")[:100]]
-        res["order_match"] = bool(np.array_equal(top, ordered[:100].cpu().numpy()))
+        host_order = sel[np.argsort(host_keys, kind="stable")]
+        res["order_match"] = bool(np.array_equal(host_order, ordered.cpu().numpy()))
     if a.query:
         # the whole state-query path the backing planner runs: filter + ORDER BY + first page
         # (ColumnarIndex.query: select, device ordering/top-k, page copy, keys)

@@ -132,6 +132,33 @@ def test_bulk_set_items_fail_alone_and_persist(front, monkeypatch, tmp_path):
     run(main())
 
 
+def test_ttl_writes_store_the_same_bytes_as_native_writes(monkeypatch):
+    """A bulk item with a TTL is stored by the Python handlers (the native front leaves TTL
+    writes to them), one without by the native front: the same value text is stored either way
+    -- numbers as sent (1e3 stays 1e3), escapes as sent (\u00e9 stays escaped)."""
+    import json as _json
+    raw = b'{"n": 1e3, "f": -0.5E+2, "s": "caf\\u00e9 \\ud83d\\ude00", "big": 12345678901234567890}'
+
+    async def main():
+        async with Backing("native", monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.doc_put("acct", "db", "c", "seed", "0")  # the collection exists: the front takes plain writes
+            for key, ttl in (("plain", 0), ("ttl", 60000)):
+                body = b'[{"key": "%s", "value": %s, "etag": null, "firstWrite": false, "ttlMs": %d}]' % (
+                    key.encode(), raw, ttl)
+                r = await c.http.post(b.base + "/cosmos/acct/db/c/bulkset", body=body,
+                                      headers={"Content-Type": "application/json"})
+                assert r.status == 200, r.body
+            plain = (await c.doc_get("acct", "db", "c", "plain"))[0]
+            ttl = (await c.doc_get("acct", "db", "c", "ttl"))[0]
+            assert plain == ttl == b'{"n":1e3,"f":-0.5E+2,"s":"caf\\u00e9 \\ud83d\\ude00","big":12345678901234567890}'
+            assert _json.loads(ttl)["s"] == "caf\u00e9 \U0001F600"
+            fs = (await c.http.get(b.base + "/admin/front")).json()
+            assert fs["requests"]["doc.bulkset"] == 1 and fs["requests"]["forwarded"] >= 1  # one each way
+            await c.http.close()
+    run(main())
+
+
 @pytest.mark.parametrize("front", FRONTS)
 def test_messaging_and_long_poll(front, monkeypatch):
     async def main():

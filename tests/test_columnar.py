@@ -260,16 +260,11 @@ GPU_FILTERS = [
 def test_gpu_scan_matches_numpy(n):
     k = _kernels()
     ix = _random_collection(n, random.Random(n))
-    try:
-        for u in (1, 2, 4, 8):  # every tt_scan_eval instantiation (row groups per lane)
-            k.set_eval_groups(u)
-            for f in GPU_FILTERS:
-                prog = ix.compile(f)
-                want = ix.select_numpy(prog)
-                got = ix.select_gpu(prog, k)
-                assert np.array_equal(got, want), (n, f, u)
-    finally:
-        k.set_eval_groups(2)
+    for f in GPU_FILTERS:
+        prog = ix.compile(f)
+        want = ix.select_numpy(prog)
+        got = ix.select_gpu(prog, k)
+        assert np.array_equal(got, want), (n, f)
 
 
 @pytest.mark.gpu
@@ -596,23 +591,37 @@ def test_gpu_rank_encode_unaligned_ranges(ndistinct):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5, 2047, 2049, 70_000, 300_001, 3_000_017])
+def test_gpu_radix_pair_sort_matches_stable_argsort(n):
+    """tt_sort_pairs (hip/radix_pairs.hip, the repo's own LSD radix sort) against NumPy's
+    stable argsort of the same keys: every used-bit width from one digit pass to eight, keys
+    crowded into few digits (heavy ties: stability decides the order), partial last tiles and
+    digit-count tables spanning many scan chunks."""
+    import torch
+    k = _kernels()
+    rng = np.random.default_rng(n)
+    for end_bit in (1, 8, 9, 20, 37, 63):
+        hi = 1 << end_bit
+        keys = rng.integers(0, hi, size=n, dtype=np.uint64)
+        if end_bit >= 20:  # a block of equal high digits
+            keys[: n // 2] &= np.uint64(0xFF)
+        rows = rng.permutation(n).astype(np.int32)
+        want = rows[np.argsort(keys, kind="stable")]
+        got = k._sorted_rows(torch.from_numpy(keys.view(np.int64)).to(k.device), torch.from_numpy(rows).to(k.device),
+                             end_bit)
+        assert np.array_equal(got.cpu().numpy(), want), (n, end_bit)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [5, 70_000, 300_001])
-def test_gpu_pair_sort_matches_argsort(n):
-    """tt_sort_pairs over the used key bits orders rows exactly like torch.sort of the keys,
-    for full orderings and top-k pages."""
+def test_gpu_ordered_queries_match_the_host(n):
+    """Full orderings and top-k pages through the device sort equal the host executor's."""
     k = _kernels()
     ix = _random_collection(n, random.Random(n + 3))
-    try:
-        for sort in ([{"key": "taskDueDate", "order": "DESC"}], [{"key": "taskCreatedBy"}, {"key": "prio", "order": "DESC"}]):
-            for page in ({}, {"limit": 25}, {"limit": 40, "token": "7"}):
-                q = {"filter": {"EQ": {"isCompleted": False}}, "sort": sort, "page": page}
-                k.pair_sort = False
-                want = ix.query(q, k)
-                k.pair_sort = True
-                assert ix.query(q, k) == want, (n, sort, page)
-                assert want == ix.query(q), (n, sort, page)
-    finally:
-        k.pair_sort = True
+    for sort in ([{"key": "taskDueDate", "order": "DESC"}], [{"key": "taskCreatedBy"}, {"key": "prio", "order": "DESC"}]):
+        for page in ({}, {"limit": 25}, {"limit": 40, "token": "7"}):
+            q = {"filter": {"EQ": {"isCompleted": False}}, "sort": sort, "page": page}
+            assert ix.query(q, k) == ix.query(q), (n, sort, page)
 
 
 @settings(max_examples=150, deadline=None)

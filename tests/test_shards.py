@@ -223,6 +223,13 @@ def test_native_data_plane_routes_with_the_same_hash(tmp_path, backings):
                 after = [(await c.sb_counts("taskstracker", ent))["enqueued"] for c in sh.shards]
                 home = shard_of("tenant-7", 2)
                 assert after[home] - per[home] == 12 and after[1 - home] == per[1 - home], (per, after)
+                # an empty partitionKey is no key (like shards.py): routed by each event's id
+                for i in range(24):
+                    r = await http.request("POST", pub + "?metadata.partitionKey=", body=b'{"n": 2}',
+                                           headers=[("Content-Type", "application/json")])
+                    assert r.status == 204, r.body
+                final = [(await c.sb_counts("taskstracker", ent))["enqueued"] for c in sh.shards]
+                assert all(final[i] > after[i] for i in range(2)), (after, final)
             finally:
                 await sh.close()
                 await http.close()
