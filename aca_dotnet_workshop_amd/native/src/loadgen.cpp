@@ -49,6 +49,7 @@ struct Opts {
   int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0;
   bool follow = false;
   double duration_s = 0;
+  double until_timeout_s = 0;  // give up waiting for the counter after this long (0 = never)
   // shared environments (bench.py --shared-env): several generators drive one subscription, so
   // the counter's starting point and its advance per step are global, not this generator's own
   long long until_base = -1, until_stride = 0;
@@ -135,7 +136,8 @@ class Gen {
   std::vector<std::pair<ev::Endpoint, std::string>> until_;
   double t0_ = 0, t1_ = 0;
   int step_ = 0;
-  long long issued_ = 0, done_ = 0, done_total_ = 0, errors_ = 0, base_ = 0;
+  long long issued_ = 0, done_ = 0, done_total_ = 0, errors_ = 0, base_ = 0, ok_step_ = 0;
+  double wait_t0_ = 0;
   size_t rr_ = 0;
   std::vector<double> lat_;
   std::string first_error_;
@@ -170,7 +172,7 @@ class Gen {
       loop_.stop();
       return;
     }
-    issued_ = done_ = 0;
+    issued_ = done_ = ok_step_ = 0;
     step_t0_ = ev::now_s();
     int n = std::min(o_.concurrency, o_.batch);
     for (int i = 0; i < n; ++i) issue();
@@ -194,6 +196,7 @@ class Gen {
       if (!r.err) statuses_[r.resp.status]++;
       bool bad = r.err || (o_.expect && r.resp.status != o_.expect);
       if (bad) note_error(r);
+      else ok_step_++;
       const std::string* loc = r.err ? nullptr : r.resp.header("location");
       if (!bad && o_.follow && loc && r.resp.status >= 300 && r.resp.status < 400) {
         double t2 = ev::now_s();
@@ -228,7 +231,9 @@ class Gen {
 
   void end_step() {
     step_creates_ = ev::now_s() - step_t0_;
-    base_ += o_.until_stride > 0 ? o_.until_stride : o_.batch;
+    // the counter advances once per request that succeeded (a failed create sends no message)
+    base_ += o_.until_stride > 0 ? o_.until_stride : (o_.duration_s > 0 ? ok_step_ : o_.batch);
+    wait_t0_ = ev::now_s();
     ++step_;
     if (until_.empty()) {
       begin_step();
@@ -240,6 +245,14 @@ class Gen {
   void wait_counter() {
     poll_counter([this](long long v) {
       if (v >= base_) begin_step();
+      else if (o_.until_timeout_s > 0 && ev::now_s() - wait_t0_ > o_.until_timeout_s) {
+        errors_++;
+        if (first_error_.empty())
+          first_error_ = "counter at " + std::to_string(v) + ", wanted " + std::to_string(base_) + " after " +
+                         std::to_string((int)o_.until_timeout_s) + " s";
+        t1_ = ev::now_s();
+        loop_.stop();
+      }
       // poll again right away: a timer would add up to its 1 ms granularity to every step's
       // measured duration (one counter read is ~50 us)
       else loop_.defer([this] { wait_counter(); });
@@ -319,6 +332,7 @@ int main(int argc, char** argv) {
     else if (a == "--follow") o.follow = true;
     else if (a == "--users") o.users = std::max(0, std::atoi(next().c_str()));
     else if (a == "--duration") o.duration_s = std::atof(next().c_str());
+    else if (a == "--until-timeout") o.until_timeout_s = std::atof(next().c_str());
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--bodies") {

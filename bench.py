@@ -353,7 +353,7 @@ def run_loadgen(exe: str, socks: list[str], counts_url: str | list[str], steps: 
     import subprocess
     cmd = [exe, "--path", "/v1.0/invoke/tasksmanager-backend-api/method/api/tasks", "--bodies", bodies_file,
            "--concurrency", str(conc), "--batch", str(batch), "--steps", str(steps), "--expect", "201",
-           *_until(counts_url)]
+           "--until-timeout", "300", *_until(counts_url)]
     if shared is not None:
         cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     for s in socks:
@@ -550,6 +550,14 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
             shutil.rmtree(root, ignore_errors=True)
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """A phase line on stderr (long runs show they are alive; the JSON result stays on stdout)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def pin_label(pinned) -> str:
     from aca_dotnet_workshop_amd.parallel import PIN_INFO
     if not pinned:
@@ -605,7 +613,8 @@ def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str 
     import subprocess
     cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies_file, "--content-type",
            "application/x-www-form-urlencoded", "--header", f"Cookie: {cookie}", "--concurrency", str(conc),
-           "--batch", str(batch), "--steps", str(steps), "--expect", "302", *_until(counts_url)]
+           "--batch", str(batch), "--steps", str(steps), "--expect", "302", "--until-timeout", "300",
+           *_until(counts_url)]
     if shared is not None:
         cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     if ca_file:
@@ -754,7 +763,7 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                "application/x-www-form-urlencoded", "--header",
                "Cookie: " + "; ".join(["TasksCreatedByCookie={user}"] + af), "--users", "500", "--follow",
                "--concurrency", "32", "--duration", str(seconds), "--expect", "302", "--tls-ca", ca,
-               "--target", base, *_until(counts)]
+               "--until-timeout", "120", "--target", base, *_until(counts)]
         t0 = time.perf_counter()
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 600)
         wall = time.perf_counter() - t0
@@ -845,6 +854,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                 shard_exchange=d.allgather if shared else None)
     sweeper = None
     try:
+        progress(f"environment up: {fe} frontend / {api} API / {proc} processor replicas")
         env.start()
         lim = env.ctl.limiter.describe()
         fe_ports = [r.app_port for r in env.replicas(FRONTEND)]
@@ -875,8 +885,10 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
             sweeper.start()
         if a.warmup:
+            progress(f"warmup: {a.warmup} steps")
             run_form_loadgen(exe, targets, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
                              (gbase, stride) if shared else None, ca_file)
+        progress(f"timed region: {a.steps} steps of {a.batch}")
         d.barrier()
         device_sync()
         me = psutil.Process()
@@ -929,7 +941,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
         dsteps = 0 if shared else a.direct_steps if a.direct_steps >= 0 else max(1, a.steps // 4)
+        progress(f"timed region done: {dt:.2f} s")
         if dsteps:
+            progress(f"api_sidecar_direct: {dsteps} steps")
             socks = [r.sidecar_uds for r in env.replicas(API)]
             jb = os.path.join(root, "json-bodies.jsonl")
             with open(jb, "wb") as f:
@@ -947,7 +961,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if a.envelope_s > 0 and not shared:  # after the headline's environment is down
             env.stop()
             if d.rank == 0:
+                progress(f"reference envelope: {a.envelope_s:g} s")
                 envelope = reference_envelope(exe, root, a.envelope_s, d.rank)
+                progress("reference envelope done")
             d.barrier()
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
