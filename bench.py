@@ -691,9 +691,10 @@ def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
             "by_role": roles}
 
 
-# relative CPU per created task of one replica of each app (app process + its sidecar), from the
-# per-process attribution of the frontend-entry bench at ~40k tasks/s (profiles/r3_mtls_cost.md)
-CPU_WEIGHT = {"frontend": 1.0, "api": 1.32, "processor": 0.6}
+# relative CPU per created task of one replica of each app (app process + its data plane) at the
+# default 4 / 4 / 2 replicas, from the round-4 per-role attribution (config.cpu_us_per_task:
+# frontend 58 + 27, API 67 + 52, processor 20 + 8 us per task; profiles/r4_ingress_cost.md)
+CPU_WEIGHT = {"frontend": 1.0, "api": 1.42, "processor": 0.67}
 
 
 def _sidecar_counter(uds: str, op: str) -> int:
@@ -762,7 +763,7 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies, "--content-type",
                "application/x-www-form-urlencoded", "--header",
                "Cookie: " + "; ".join(["TasksCreatedByCookie={user}"] + af), "--users", "500", "--follow",
-               "--concurrency", "32", "--duration", str(seconds), "--expect", "302", "--tls-ca", ca,
+               "--concurrency", "16", "--duration", str(seconds), "--expect", "302", "--tls-ca", ca,
                "--until-timeout", "120", "--target", base, *_until(counts)]
         t0 = time.perf_counter()
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 600)
@@ -771,10 +772,14 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         stop.set()
         st1 = _collection_stats(env.backing_url).get("throughput", {})
         retries = sum(_sidecar_counter(u, "state.throttled_retry") for u in api_uds) - retry0
-        tasks = int(rep.get("requests", 0))
+        sc = rep.get("status_counts") or {}
+        attempts = int(rep.get("requests", 0))
+        tasks = int(sc.get("302", 0))  # created (the 302 to the list); a 500 here is a create that failed
+        lists_ok = int(sc.get("200", 0))
         ru = float(st1.get("ru_consumed", 0.0)) - float(st0.get("ru_consumed", 0.0))
         el = float(rep.get("elapsed_s") or wall)
         return {"tasks_per_s": round(tasks / el, 1) if el else None, "tasks": tasks, "seconds": round(el, 2),
+                "create_attempts": attempts, "failed_creates": attempts - tasks, "failed_lists": tasks - lists_ok,
                 "errors": rep.get("errors"), "first_error": rep.get("first_error") or None,
                 "create_latency_ms": rep.get("latency_ms"), "list_latency_ms": rep.get("follow_latency_ms"),
                 "lists_followed": rep.get("follow_requests"), "status_counts": rep.get("status_counts"),
@@ -785,7 +790,9 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 "budget_over_ru_per_task": round(float(st1.get("ru_per_s", 0.0)) / (ru / tasks), 1) if tasks and ru else None,
                 "processor_replicas_reached": peak["processor"],
                 "replicas": {"frontend": 1, "api": 1, "processor": "1..5 (KEDA, 10 messages per replica)"},
-                "vcpu_per_replica": 0.25, "users": 500, "concurrency": 32,
+                "vcpu_per_replica": 0.25, "users": 500, "concurrency": 16,
+                "note": "a create or list whose store call is still throttled after the sidecar's 9 retries "
+                        "(the Cosmos SDK policy) answers 500, as the reference's pages would",
                 "keda_polling_s": 5, "loadgen_exit": p.returncode}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:500]}
