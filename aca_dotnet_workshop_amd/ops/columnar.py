@@ -1310,6 +1310,7 @@ class ColumnarIndex:
             if ordered is not None:
                 end = min(total, offset + limit) if limit else total
                 sel = ordered[offset:end].cpu().numpy()
+                kernels.check_sort()
                 token = str(end) if limit and end < total else None
                 return sel.astype(np.int32, copy=False), token
             rows = dev_rows.cpu().numpy()

@@ -38,7 +38,7 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_scan_eval.restype = ctypes.c_int
     lib.tt_sort_pairs_temp_bytes.argtypes = [I64, I32]
     lib.tt_sort_pairs_temp_bytes.restype = ctypes.c_int64
-    lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P]
+    lib.tt_sort_pairs.argtypes = [P, P, P, P, I64, I32, P, I64, P, P]
     lib.tt_sort_pairs.restype = ctypes.c_int
     lib.tt_launch_scan_compact.argtypes = [P, P, P, I64, P, I64, P, P, P]
     lib.tt_launch_compact.argtypes = [P, P, I64, P, I64, P]
@@ -340,13 +340,23 @@ class GpuKernels:
         temp = getattr(self, "_sort_temp", None)
         if temp is None or temp.numel() < need:
             temp = self._sort_temp = self.torch.empty(max(need, 1), dtype=self.torch.uint8, device=self.device)
+        fault = getattr(self, "_sort_fault", None)
+        if fault is None:
+            fault = self._sort_fault = self.torch.zeros(1, dtype=self.torch.int32, device=self.device)
         keys_out = self.torch.empty_like(keys)
         rows_out = self.torch.empty_like(rows)
         rc = self.lib.tt_sort_pairs(keys.data_ptr(), keys_out.data_ptr(), rows.data_ptr(), rows_out.data_ptr(), n,
-                                    end_bit, temp.data_ptr(), need, self._stream())
+                                    end_bit, temp.data_ptr(), need, fault.data_ptr(), self._stream())
         if rc != 0:
             raise RuntimeError(f"tt_sort_pairs failed ({rc})")
         return rows_out
+
+    def check_sort(self) -> None:
+        """Raise if any sort so far saw a look-back spin time out (its output is not trustworthy).
+        Reads one device word: call it where the caller synchronises anyway."""
+        fault = getattr(self, "_sort_fault", None)
+        if fault is not None and int(fault.item()) != 0:
+            raise RuntimeError(f"tt_sort_pairs: {int(fault.item())} look-back spins timed out")
 
     def _top_k(self, keys, rows, k: int, shift: int, hist, key_bits: int = 63):
         import numpy as np

@@ -153,8 +153,8 @@ def main() -> None:
         ix._full_dirty = True
         sort = [{"key": "taskDueDate", "order": "DESC"}]
         st = ix.to_device(k)
-        # the device ordering: tt_sort_keys + the repo's LSD radix sort of (key, row) pairs over
-        # the used key bits (hip/radix_pairs.hip), or radix select + sort for the top 100
+        # the device ordering: tt_sort_keys + the repo's onesweep LSD radix sort of (key, row) pairs
+        # over the used key bits (hip/radix_pairs.hip), or radix select + sort for the top 100
         for label, kk in (("top100", 100), ("full", None)):
             for _ in range(2):
                 ix.order_gpu(out, sort, k, kk)
@@ -172,6 +172,7 @@ def main() -> None:
         host_keys = ix.sort_keys_numpy(sel, plan)
         host_order = sel[np.argsort(host_keys, kind="stable")]
         res["order_match"] = bool(np.array_equal(host_order, ordered.cpu().numpy()))
+        k.check_sort()
     if a.query:
         # the whole state-query path the backing planner runs: filter + ORDER BY + first page
         # (ColumnarIndex.query: select, device ordering/top-k, page copy, keys)

@@ -591,7 +591,7 @@ def test_gpu_rank_encode_unaligned_ranges(ndistinct):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 5, 2047, 2049, 70_000, 300_001, 3_000_017])
+@pytest.mark.parametrize("n", [1, 5, 2047, 2049, 4097, 8192, 8193, 70_000, 300_001, 3_000_017])
 def test_gpu_radix_pair_sort_matches_stable_argsort(n):
     """tt_sort_pairs (hip/radix_pairs.hip, the repo's own LSD radix sort) against NumPy's
     stable argsort of the same keys: every used-bit width from one digit pass to eight, keys
@@ -610,6 +610,7 @@ def test_gpu_radix_pair_sort_matches_stable_argsort(n):
         got = k._sorted_rows(torch.from_numpy(keys.view(np.int64)).to(k.device), torch.from_numpy(rows).to(k.device),
                              end_bit)
         assert np.array_equal(got.cpu().numpy(), want), (n, end_bit)
+    k.check_sort()
 
 
 @pytest.mark.gpu
