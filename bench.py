@@ -92,6 +92,8 @@ def parse() -> argparse.Namespace:
                     help="vCPU per replica (reference: 0.25); 0 = this rank's CPUs divided over its replicas")
     ap.add_argument("--trace-sampling", type=float, default=1.0,
                     help="App Insights sampling percentage of request traces (the manifest default is 100)")
+    ap.add_argument("--cpu-weights", default="",
+                    help="frontend:api:processor relative vCPU per replica (default: CPU_WEIGHT)")
     ap.add_argument("--envelope-s", type=float, default=20.0,
                     help="seconds of the secondary reference-envelope run (config.reference_envelope: the "
                          "manifest defaults -- 1/1 frontend/API, processor 1..5 on KEDA, 0.25 vCPU, 4000 RU/s -- "
@@ -691,10 +693,12 @@ def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
             "by_role": roles}
 
 
-# relative CPU per created task of one replica of each app (app process + its data plane) at the
-# default 4 / 4 / 2 replicas, from the round-4 per-role attribution (config.cpu_us_per_task:
-# frontend 58 + 27, API 67 + 52, processor 20 + 8 us per task; profiles/r4_ingress_cost.md)
-CPU_WEIGHT = {"frontend": 1.0, "api": 1.42, "processor": 0.67}
+# relative vCPU per replica of each app (app process + its data plane) at the default 4 / 4 / 2
+# replicas: the round-4 per-role attribution (config.cpu_us_per_task: frontend 58 + 27, API
+# 67 + 52, processor 20 + 8 us per task; profiles/r4_ingress_cost.md) gives 1 : 1.42 : 0.67, but
+# at 0.67 the duty cycle stopped the processors 8-14 % of the timed region (they also run the
+# cron sweep) and their acks gated the steps: 0.85 measured +7 % (profiles/r4_cpu_weights.md)
+CPU_WEIGHT = {"frontend": 1.0, "api": 1.42, "processor": 0.85}
 
 
 def _sidecar_counter(uds: str, op: str) -> int:
@@ -825,6 +829,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         caps = {"frontend": a.app_cpu, "api": a.app_cpu, "processor": a.app_cpu}
     else:
         w = CPU_WEIGHT
+        if a.cpu_weights:
+            w = dict(zip(("frontend", "api", "processor"), (float(x) for x in a.cpu_weights.split(":"))))
         # the platform's own processes are not replicas (no cap): the backing services and the
         # load generator, plus the external ingress when load enters through it
         reserve = 2.0 + (INGRESS_RESERVE if ingress else 0.0)
