@@ -18,10 +18,27 @@
 // goes from empty to non-empty, so a burst of N requests costs one wake-up on each side.
 // The loop thread never touches Python objects (no GIL); conversion happens in drain(), which
 // the Python thread calls.
+//
+// Native routes (add_route): a service may hand its hottest route to the host, the way the
+// sidecar's data plane serves the hot Dapr routes for its Python control plane.  The loop
+// thread then runs the whole exchange with the same native codec the Python handler calls, the
+// same sidecar calls with the same headers, and the same answer; the Python thread only sees
+// the route's log records (LOG events, written by its own logging sinks) and its request
+// counters (route_stats, folded into the Prometheus registry).  What the native path does not
+// decide goes to Python unchanged:
+//   * bodies outside the codec's envelope, bad antiforgery tokens, other content types;
+//   * sampled traces (the Python pipeline records their spans);
+//   * a new trace the sampler picks, marked `x-tt-native: sample`.
+// A sidecar call that fails is handed over too, marked `x-tt-native: fail <step> <status>
+// <base64 body>` or `err <step> <errno>`: the Python handler raises the error the SDK would
+// have raised, and the pipeline answers it as always.  The host drops that header from what
+// clients send; web/native_host.py moves the host's own into `req.state["tt_native"]`.
 #pragma once
 
 #include <sys/eventfd.h>
 #include <unistd.h>
+
+#include <sys/random.h>
 
 #include <algorithm>
 #include <atomic>
@@ -29,11 +46,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <future>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 
 #include "evhttp.hpp"
+#include "formcodec.hpp"
 #include "h2.hpp"
+#include "taskcodec.hpp"
+#include "textutil.hpp"
 
 namespace tt::apphost {
 
@@ -41,13 +63,49 @@ using ev::HeaderList;
 using ev::Message;
 
 struct Event {
-  enum Kind : int { REQUEST = 0, RESPONSE = 1, ERROR = 2 };
+  enum Kind : int { REQUEST = 0, RESPONSE = 1, ERROR = 2, LOG = 3 };
   int kind = REQUEST;
   uint64_t id = 0;      // REQUEST: reply token; RESPONSE/ERROR: the client request id
   int server = 0;       // REQUEST: which listener group (one per Python HttpServer)
-  int err = 0;          // ERROR: errno-like code
+  int err = 0;          // ERROR: errno-like code; LOG: the level (Python logging's numbers)
   double t = 0;         // loop-thread monotonic time when the event was queued (ev::now_s)
-  Message msg;
+  Message msg;          // LOG: method = logger name, body = message, target/reason = trace/span id
+};
+
+// A route the loop thread serves itself (AppHost::add_route).
+struct NativeRoute {
+  enum Kind { kFrontendCreate = 1, kApiCreate = 2 };
+  int id = 0;
+  int kind = 0;
+  std::string method, path;
+  ev::Endpoint sidecar;
+  std::string token;            // dapr-api-token, when the app has one
+  double timeout_s = 60;
+  double sample_rate = 1.0;     // the app tracer's rate for new traces
+  // kFrontendCreate: the Create page's post -> invoke the API -> 302
+  std::string af_key, af_cookie, id_cookie, invoke_target, location;
+  // kApiCreate: POST api/tasks -> state save -> publish -> 201
+  std::string save_target, publish_target, log_category;
+  std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
+  ::taskcodec::Entropy rng;       // loop thread only
+
+  struct Stat {
+    uint64_t n = 0;
+    double sum = 0;
+    std::vector<uint64_t> buckets;  // bounds.size() + 1
+  };
+  std::mutex mu;
+  std::map<int, Stat> stats;  // by status, since the last take
+
+  void record(int status, double secs) {
+    size_t b = (size_t)(std::lower_bound(bounds.begin(), bounds.end(), secs) - bounds.begin());
+    std::lock_guard<std::mutex> g(mu);
+    Stat& st = stats[status];
+    if (st.buckets.empty()) st.buckets.assign(bounds.size() + 1, 0);
+    ++st.n;
+    st.sum += secs;
+    ++st.buckets[b];
+  }
 };
 
 class AppHost {
@@ -217,7 +275,76 @@ class AppHost {
     return out;
   }
 
-  size_t pending_replies() const { return pending_replies_.load(); }
+  size_t pending_replies() const { return pending_replies_.load() + native_inflight_.load(); }
+
+  // Register a native route on listener group `server`; `cfg` holds the route's settings as
+  // strings (see NativeRoute; web/native_host.py NativeHttpServer.native_route).  Returns its id.
+  int add_route(int server, const std::string& kind, const std::map<std::string, std::string>& cfg,
+                const std::vector<double>& bounds) {
+    auto r = std::make_shared<NativeRoute>();
+    auto get = [&](const char* k) {
+      auto it = cfg.find(k);
+      return it == cfg.end() ? std::string() : it->second;
+    };
+    if (kind == "frontend_create") r->kind = NativeRoute::kFrontendCreate;
+    else if (kind == "api_create") r->kind = NativeRoute::kApiCreate;
+    else throw std::invalid_argument("unknown native route kind: " + kind);
+    r->method = get("method");
+    r->path = get("path");
+    r->sidecar = ev::Endpoint::parse(get("sidecar"));
+    r->token = get("token");
+    if (!get("timeout").empty()) r->timeout_s = std::stod(get("timeout"));
+    if (!get("sample_rate").empty()) r->sample_rate = std::stod(get("sample_rate"));
+    r->af_key = get("af_key");
+    r->af_cookie = get("af_cookie");
+    r->id_cookie = get("id_cookie");
+    r->invoke_target = get("invoke_target");
+    r->location = get("location");
+    r->save_target = get("save_target");
+    r->publish_target = get("publish_target");
+    r->log_category = get("log_category");
+    r->bounds = bounds;
+    if (r->method.empty() || r->path.empty()) throw std::invalid_argument("a native route needs a method and a path");
+    auto p = std::make_shared<std::promise<int>>();
+    auto f = p->get_future();
+    post([this, server, r, p] {
+      r->id = next_route_++;
+      routes_[server].push_back(r);
+      all_routes_.push_back(r);
+      {
+        std::lock_guard<std::mutex> g(routes_mu_);
+        all_routes_snapshot_ = all_routes_;
+      }
+      p->set_value(r->id);
+    });
+    if (!thread_.joinable()) run_commands();
+    return f.get();
+  }
+
+  struct RouteStat {
+    int route = 0, status = 0;
+    uint64_t n = 0;
+    double sum = 0;
+    std::vector<uint64_t> buckets;
+  };
+  // The native routes' request counts and latencies since the last call (then reset).
+  std::vector<RouteStat> take_route_stats() {
+    std::vector<std::shared_ptr<NativeRoute>> rs;
+    {
+      std::lock_guard<std::mutex> g(routes_mu_);
+      rs = all_routes_snapshot_;
+    }
+    std::vector<RouteStat> out;
+    for (auto& r : rs) {
+      std::map<int, NativeRoute::Stat> st;
+      {
+        std::lock_guard<std::mutex> g(r->mu);
+        st.swap(r->stats);
+      }
+      for (auto& [status, x] : st) out.push_back({r->id, status, x.n, x.sum, std::move(x.buckets)});
+    }
+    return out;
+  }
 
  private:
   struct Waker : ev::IoObj {
@@ -258,6 +385,196 @@ class AppHost {
   std::unordered_map<int, std::vector<std::shared_ptr<ev::IoObj>>> listeners_;
   std::unordered_map<int, std::vector<std::weak_ptr<ev::ServerConn>>> conns_;
   std::unordered_map<int, std::unique_ptr<ev::Handler>> handlers_;
+  std::unordered_map<int, std::vector<std::shared_ptr<NativeRoute>>> routes_;  // loop thread
+  std::vector<std::shared_ptr<NativeRoute>> all_routes_;                       // loop thread
+  std::mutex routes_mu_;
+  std::vector<std::shared_ptr<NativeRoute>> all_routes_snapshot_;  // for take_route_stats
+  int next_route_ = 1;
+  std::atomic<size_t> native_inflight_{0};
+  uint64_t rng_s_[2] = {0, 0};
+
+  // -- native routes ---------------------------------------------------------------------
+  uint64_t next_random() {  // xorshift128+ (trace and span ids, the sampler's draw)
+    if (rng_s_[0] == 0 && rng_s_[1] == 0) {
+      if (getrandom(rng_s_, sizeof rng_s_, 0) != (ssize_t)sizeof rng_s_ || (rng_s_[0] | rng_s_[1]) == 0)
+        rng_s_[0] = 0x9e3779b97f4a7c15ull ^ (uint64_t)ev::now_s();
+    }
+    uint64_t a = rng_s_[0];
+    const uint64_t b = rng_s_[1];
+    rng_s_[0] = b;
+    a ^= a << 23;
+    rng_s_[1] = a ^ b ^ (a >> 17) ^ (b >> 26);
+    return rng_s_[1] + b;
+  }
+  static void hex_to(std::string& out, uint64_t v) {
+    static const char* d = "0123456789abcdef";
+    for (int i = 60; i >= 0; i -= 4) out += d[(v >> i) & 15];
+  }
+  std::string new_id(int words) {
+    std::string s;
+    s.reserve(16 * words);
+    for (int i = 0; i < words; ++i) {
+      uint64_t v = next_random();
+      if (v == 0) v = 1;  // all-zero ids are invalid
+      hex_to(s, v);
+    }
+    return s;
+  }
+  static const std::string* header(const Message& m, std::string_view name) {
+    for (auto& kv : m.headers)
+      if (kv.first == name) return &kv.second;
+    return nullptr;
+  }
+  static bool is_hex(std::string_view v) {
+    for (char c : v)
+      if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+    return true;
+  }
+
+  // The request's trace context, the way the Python middleware reads it
+  // (telemetry/tracing.py parse_traceparent + Tracer.start_span).  0: serve natively in trace
+  // `tid` (the route's span is new, unsampled); 1: the Python pipeline records this one;
+  // 2: a new trace the sampler picked -- Python, marked so that it samples it.
+  int trace_context(const NativeRoute& r, const Message& m, std::string& tid) {
+    const std::string* tp = header(m, "traceparent");
+    if (tp) {
+      std::string_view v(*tp);
+      while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+      while (!v.empty() && (v.back() == ' ' || v.back() == '\t')) v.remove_suffix(1);
+      // version(2)-trace(32)-span(16)-flags(2), lowercase hex; anything else goes to Python
+      if (v.size() == 55 && v[2] == '-' && v[35] == '-' && v[52] == '-' && is_hex(v.substr(0, 2)) &&
+          is_hex(v.substr(3, 32)) && is_hex(v.substr(36, 16)) && is_hex(v.substr(53, 2)) &&
+          v.substr(3, 32) != std::string(32, '0') && v.substr(36, 16) != std::string(16, '0')) {
+        int flags = ::formcodec::hexval(v[53]) * 16 + ::formcodec::hexval(v[54]);
+        if (flags & 1) return 1;
+        tid.assign(v.substr(3, 32));
+        return 0;
+      }
+      return 1;
+    }
+    if (r.sample_rate >= 1.0) return 2;
+    if (r.sample_rate > 0 && (double)(next_random() >> 11) * 0x1.0p-53 < r.sample_rate) return 2;
+    tid = new_id(2);
+    return 0;
+  }
+
+  struct NativeJob {
+    std::shared_ptr<NativeRoute> route;
+    Message req;  // kept for a hand-over to Python
+    ev::Reply reply;
+    int server = 0;
+    double t0 = 0;
+    std::string trace_id, span_id, traceparent;
+    ev::HeaderList out_headers;  // traceparent, token, content-type: the SDK's unsampled call
+    ::taskcodec::Created task;
+  };
+
+  void log_event(const NativeRoute& r, const NativeJob& j, std::string message) {
+    Event e;
+    e.kind = Event::LOG;
+    e.err = 20;  // logging.INFO
+    e.msg.method = r.log_category;
+    e.msg.target = j.trace_id;
+    e.msg.reason = j.span_id;
+    e.msg.body = std::move(message);
+    emit(std::move(e));
+  }
+
+  void finish(NativeJob& j, int status, const ev::HeaderList& headers) {
+    j.reply.send(status, headers, {});
+    j.route->record(status, ev::now_s() - j.t0);
+    native_inflight_.fetch_sub(1);
+  }
+
+  // A failed sidecar call: the request goes to Python with the result attached.
+  void hand_over(NativeJob& j, const char* step, const ev::ClientResult& res) {
+    std::string note;
+    if (res.err) {
+      note = std::string("err ") + step + " " + std::to_string(res.err);
+    } else {
+      note = std::string("fail ") + step + " " + std::to_string(res.resp.status) + " " + tt::text::base64(res.resp.body);
+    }
+    j.req.headers.emplace_back("x-tt-native", std::move(note));
+    to_python(j.server, std::move(j.req), std::move(j.reply));
+    native_inflight_.fetch_sub(1);
+  }
+
+  void to_python(int server, Message&& m, ev::Reply reply) {
+    uint64_t token = next_token_++;
+    replies_.emplace(token, std::move(reply));
+    Event e;
+    e.kind = Event::REQUEST;
+    e.id = token;
+    e.server = server;
+    e.msg = std::move(m);
+    emit(std::move(e));
+  }
+
+  // true: the route took the request (answered now or later); false: Python serves `m`
+  // (possibly marked `x-tt-native: sample`).
+  bool serve_native(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply) {
+    if (m.body.size() > (1u << 20)) return false;
+    std::string tid;
+    int tc = trace_context(*r, m, tid);
+    if (tc == 1) return false;
+    if (tc == 2) {
+      m.headers.emplace_back("x-tt-native", "sample");
+      return false;
+    }
+    auto j = std::make_shared<NativeJob>();
+    if (r->kind == NativeRoute::kFrontendCreate) {
+      const std::string* cookie = header(m, "cookie");
+      std::string json;
+      auto v = ::formcodec::create_task(m.body, cookie ? std::string_view(*cookie) : std::string_view(), r->af_key,
+                                      r->af_cookie, r->id_cookie, json);
+      if (v != ::formcodec::Verdict::kOk) return false;  // the page decides (binding errors, 400)
+      j->task.task_json = std::move(json);
+    } else {
+      const std::string* ct = header(m, "content-type");
+      if (ct && !ct->empty()) {
+        std::string low(*ct);
+        for (auto& c : low) c = (char)std::tolower((unsigned char)c);
+        if (low.find("json") == std::string::npos) return false;
+      }
+      if (!::taskcodec::create(m.body, r->rng, j->task)) return false;
+    }
+    j->route = r;
+    j->server = server;
+    j->t0 = ev::now_s();
+    j->trace_id = std::move(tid);
+    j->span_id = new_id(1);
+    j->traceparent = "00-" + j->trace_id + "-" + j->span_id + "-00";
+    j->out_headers.emplace_back("traceparent", j->traceparent);
+    if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
+    j->out_headers.emplace_back("Content-Type", "application/json");
+    j->req = std::move(m);
+    j->reply = std::move(reply);
+    native_inflight_.fetch_add(1);
+    if (r->kind == NativeRoute::kFrontendCreate) {
+      std::string body = std::move(j->task.task_json);
+      client_.request(r->sidecar, "POST", r->invoke_target, j->out_headers, body, r->timeout_s,
+                      [this, j](ev::ClientResult&& res) {
+                        if (res.err || res.resp.status >= 300) return hand_over(*j, "invoke", res);
+                        finish(*j, 302, {{"Location", j->route->location}});
+                      });
+      return true;
+    }
+    log_event(*r, *j, "Save a new task with name: '" + j->task.name + "' to state store");
+    client_.request(r->sidecar, "POST", r->save_target, j->out_headers, j->task.state_body, r->timeout_s,
+                    [this, j](ev::ClientResult&& res) {
+                      if (res.err || res.resp.status >= 300) return hand_over(*j, "save", res);
+                      const NativeRoute& r = *j->route;
+                      log_event(r, *j, "Publish Task Saved event for task with Id: '" + j->task.id + "' and Name: '" +
+                                           j->task.name + "' for Assignee: '" + j->task.assigned_to + "'");
+                      client_.request(r.sidecar, "POST", r.publish_target, j->out_headers, j->task.task_json,
+                                      r.timeout_s, [this, j](ev::ClientResult&& res2) {
+                                        if (res2.err || res2.resp.status >= 300)
+                                          return hand_over(*j, "publish", res2);
+                                        finish(*j, 201, {{"Location", "/api/tasks/" + j->task.id}});
+                                      });
+                    });
+    return true;
+  }
 
   void post(std::function<void()> f) {
     bool was_empty;
@@ -304,14 +621,20 @@ class AppHost {
     auto& h = handlers_[server];
     if (!h) {
       h = std::make_unique<ev::Handler>([this, server](Message&& m, ev::Reply reply) {
-        uint64_t token = next_token_++;
-        replies_.emplace(token, std::move(reply));
-        Event e;
-        e.kind = Event::REQUEST;
-        e.id = token;
-        e.server = server;
-        e.msg = std::move(m);
-        emit(std::move(e));
+        // only the host marks requests: a client's own x-tt-native header never reaches Python
+        for (size_t i = 0; i < m.headers.size(); ++i)
+          if (m.headers[i].first == "x-tt-native") m.headers.erase(m.headers.begin() + (long)i--);
+        auto rit = routes_.find(server);
+        if (rit != routes_.end() && !rit->second.empty()) {
+          std::string_view path(m.target);
+          path = path.substr(0, path.find('?'));
+          for (auto& r : rit->second)
+            if (r->method == m.method && r->path == path) {
+              if (serve_native(r, server, m, reply)) return;
+              break;
+            }
+        }
+        to_python(server, std::move(m), std::move(reply));
       });
     }
     std::shared_ptr<ev::IoObj> l;

@@ -182,6 +182,17 @@ static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) 
       set_item(t.ptr(), 3, headers_dict_fast(e.msg.headers));
       set_item(t.ptr(), 4, PyBytes_FromStringAndSize(e.msg.body.data(), (Py_ssize_t)e.msg.body.size()));
       if (with_times) set_item(t.ptr(), 5, PyFloat_FromDouble(e.t));
+    } else if (e.kind == apphost::Event::LOG) {
+      // (3, level, logger name, message, trace id, span id)
+      t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 7 : 6));
+      if (!t) throw py::error_already_set();
+      set_item(t.ptr(), 0, PyLong_FromLong(3));
+      set_item(t.ptr(), 1, PyLong_FromLong(e.err));
+      set_item(t.ptr(), 2, new_str(e.msg.method));
+      set_item(t.ptr(), 3, new_str(e.msg.body));
+      set_item(t.ptr(), 4, new_str(e.msg.target));
+      set_item(t.ptr(), 5, new_str(e.msg.reason));
+      if (with_times) set_item(t.ptr(), 6, PyFloat_FromDouble(e.t));
     } else {
       if (with_times) t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t);
       else t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)));
@@ -669,6 +680,17 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("close_server", &apphost::AppHost::close_server)
       .def("close_connections", &apphost::AppHost::close_connections)
       .def("pending_replies", &apphost::AppHost::pending_replies)
+      // a route the I/O thread serves itself (apphost.hpp NativeRoute): kind, settings, the
+      // latency histogram's buckets -> route id
+      .def("add_route", &apphost::AppHost::add_route, py::arg("server"), py::arg("kind"), py::arg("cfg"),
+           py::arg("bounds"), py::call_guard<py::gil_scoped_release>())
+      // [(route id, status, count, latency sum s, bucket counts)] since the last call
+      .def("route_stats", [](apphost::AppHost& h) {
+        auto st = h.take_route_stats();
+        py::list out;
+        for (auto& x : st) out.append(py::make_tuple(x.route, x.status, x.n, x.sum, x.buckets));
+        return out;
+      })
       // ops: [(0, token, status, headers, body) | (1, id, endpoint, method, target, headers, body, timeout) |
       //       (2, id, endpoint, "", grpc_path, metadata, message, timeout)]
       .def("submit",

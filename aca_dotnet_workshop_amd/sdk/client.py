@@ -132,6 +132,17 @@ class SidecarClient:
             if key[0] in ("unix", "tcp"):
                 self._at, self._key, self._prefix = http.request_at, key, prefix.rstrip("/")
 
+    def native_endpoint(self) -> dict[str, str] | None:
+        """Where a native route (web/native_host.py ``native_route``) reaches this sidecar the
+        way this client does: the app host's endpoint, the path prefix, the API token and the
+        timeout; None when this client does not run on the native host."""
+        if self._at is None:
+            return None
+        key = self._key
+        ep = f"unix:{key[1]}" if key[0] == "unix" else f"tcp:{key[1]}:{key[2]}"
+        return {"sidecar": ep, "prefix": self._prefix, "token": self.api_token or "",
+                "timeout": repr(float(getattr(self.http, "timeout", 60.0)))}
+
     # -- plumbing -------------------------------------------------------------
     def _headers(self, ctype: str | None = None, extra: dict[str, str] | None = None) -> list[tuple[str, str]]:
         h: list[tuple[str, str]] = []
@@ -391,3 +402,24 @@ def client_from_config(config=None, environ: dict[str, str] | None = None):
 
 def b64(data: bytes) -> str:
     return base64.b64encode(data).decode()
+
+
+def native_route_failure(req: Any, what: dict[str, str]) -> BaseException | None:
+    """The error a native route handed over (``fail <step> <status> <base64 body>`` or ``err
+    <step> <errno>`` in ``req.state["tt_native"]``, set by web/native_host.py only) as the
+    exception this SDK raises for that call (``what``: the step's InvocationError message), or
+    None for an ordinary request."""
+    note = req.state.get("tt_native")
+    if not note or note == "sample":
+        return None
+    parts = note.split(" ")
+    if len(parts) >= 3 and parts[1] in what:
+        if parts[0] == "fail":
+            import base64
+            body = base64.b64decode(parts[3]) if len(parts) > 3 else b""
+            return InvocationError(int(parts[2]), body, what[parts[1]])
+        if parts[0] == "err":
+            from ..web.native_host import _client_error
+            err = int(parts[2])
+            return _client_error(err, os.strerror(err))
+    return RuntimeError(f"malformed native route hand-over: {note[:80]!r}")

@@ -31,7 +31,7 @@ from pathlib import Path
 
 from ...models import TaskAddModel, TaskModel, TaskUpdateModel, tasks_to_json
 from ...models.dotnet import is_guid
-from ...sdk.client import client_from_config
+from ...sdk.client import client_from_config, native_route_failure
 from ...web.app import WebApp, read_model
 from ...web.http import HTTPError, Request, Response, empty
 from ..hosting import create_host, map_openapi, run_host
@@ -71,9 +71,21 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     fast_create = getattr(manager, "create_new_task_from_body", None)
     fast_mark = getattr(manager, "mark_overdue_from_body", None)
     fast_page = getattr(manager, "overdue_page_json", None)
+    native = getattr(manager, "native_create_route", None)
+    spec = native() if fast_create is not None and native is not None else None
+    create_what = spec.pop("what") if spec else {}
+    if spec:
+        # the app host's I/O thread serves POST api/tasks end to end when it can: the same
+        # native codec, log lines, state save and event as create_new_task_from_body, the same
+        # 201; the rest (bodies for the general binder, sampled traces, a failed sidecar call)
+        # comes to this handler
+        app.services.setdefault("native_routes", []).append(spec)
 
     @app.route("/api/tasks", ("POST",), name="CreateTask", tag="Tasks", body=TaskAddModel, responses={201: None})
     async def post_task(req: Request) -> Response:
+        failed = native_route_failure(req, create_what) if create_what else None
+        if failed is not None:  # the native route's save or publish failed: the SDK's error
+            raise failed
         ctype = req.content_type
         if fast_create is not None and (not ctype or "json" in ctype):  # one native pass over the body
             tid = await fast_create(req.body)

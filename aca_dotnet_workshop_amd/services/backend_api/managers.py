@@ -196,6 +196,22 @@ class TasksStoreManager(TasksManager):
         await self.client.publish_event(self.pubsub, self.topic, task_json, content_type="application/json")
         return tid
 
+    def native_create_route(self) -> dict | None:
+        """``create_new_task_from_body`` as a native route of the app host (apphost.hpp
+        ``api_create``: codec, "Save a new task" log line, state save, "Publish Task Saved"
+        log line, publish, 201), or None when this client cannot take one (gRPC, asyncio I/O).
+        ``what``: the SDK's error messages for the two calls, raised when a call fails."""
+        ep_of = getattr(self.client, "native_endpoint", None)
+        ep = ep_of() if ep_of is not None else None
+        if ep is None or getattr(self.client, "save_state_body", None) is None:
+            return None
+        return {"kind": "api_create", "method": "POST", "path": "/api/tasks", "route": "/api/tasks",
+                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                        "save_target": f"{ep['prefix']}/v1.0/state/{self.store}",
+                        "publish_target": f"{ep['prefix']}/v1.0/publish/{self.pubsub}/{self.topic}",
+                        "log_category": log.name},
+                "what": {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}"}}
+
     async def delete_task(self, task_id) -> bool:
         log.info("Delete task with Id: '%s'", task_id)
         data, etag = await self.client.get_state_and_etag(self.store, str(task_id))

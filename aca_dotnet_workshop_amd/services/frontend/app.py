@@ -38,7 +38,7 @@ from jinja2 import Environment, FileSystemLoader, select_autoescape
 from ...models import FIELD_DISPLAY, REQUIRED_FIELDS, TaskModel, parse_datetime, tasks_from_json
 from ...models.dotnet import is_guid, naive_utc
 from ...sdk import SidecarClient
-from ...sdk.client import RawJson
+from ...sdk.client import RawJson, native_route_failure
 from ...web.app import WebApp
 from ...web.client import HttpClient
 from ...web.http import HTTPError, Request, Response, redirect
@@ -199,9 +199,24 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
         return render(req, "tasks_create.html", values={}, errors={}, display=FIELD_DISPLAY)
 
     fast_form = _native_form() if mode == "dapr" else None
+    create_what = {"invoke": f"invoke {API_APP_ID}/api/tasks"}
+    ep = gw.dapr.native_endpoint() if fast_form is not None and isinstance(gw.dapr, SidecarClient) else None
+    if ep is not None:
+        # the app host's I/O thread serves this post end to end when it can: the same native
+        # form binding as below, the same invoke through the sidecar, the same 302; the rest
+        # (binding errors, bad tokens, sampled traces, a failed invoke) comes to this handler
+        app.services.setdefault("native_routes", []).append({
+            "kind": "frontend_create", "method": "POST", "path": "/Tasks/Create", "route": "/Tasks/Create",
+            "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                    "af_key": af.key.decode(), "af_cookie": AF_COOKIE, "id_cookie": COOKIE,
+                    "invoke_target": f"{ep['prefix']}/v1.0/invoke/{API_APP_ID}/method/api/tasks",
+                    "location": "/Tasks/Index"}})
 
     @app.route("/Tasks/Create", ("POST",), name="TasksCreatePost", include_in_schema=False)
     async def create_post(req: Request) -> Response:
+        failed = native_route_failure(req, create_what)
+        if failed is not None:  # the native route's invoke failed: the SDK's error, as below
+            raise failed
         if fast_form is not None:  # form, cookies, antiforgery and binding in one native pass
             made = fast_form(req.body, (req.headers.get("cookie") or "").encode(), af.key)
             if made is not None and made[0]:

@@ -152,6 +152,11 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
     loop = asyncio.get_running_loop()
     from ..web import native_host
     srv = native_host.NativeHttpServer(app, loop) if native_host.enabled(part="server") else HttpServer(app, loop)
+    # routes the service hands to the native host's I/O thread (``native_routes`` specs; off
+    # with TT_NATIVE_ROUTES=0, or on the asyncio server)
+    if isinstance(srv, native_host.NativeHttpServer) and os.environ.get("TT_NATIVE_ROUTES", "1") != "0":
+        for spec in app.services.get("native_routes") or []:
+            srv.native_route(spec["kind"], spec["method"], spec["path"], spec["route"], spec["cfg"])
     await app.startup()
     ports = []
     addrs = listen_addresses(config)

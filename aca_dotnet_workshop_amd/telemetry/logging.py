@@ -236,6 +236,23 @@ class FastLogger(logging.Logger):
                     sink.write_fast(level, self.name, message, tid, sid)
         return True
 
+    def log_ids(self, level: int, message: str, trace_id: str, span_id: str) -> None:
+        """One record with the trace context given (a record made outside this thread's request
+        context: a native route's log line, web/native_host.py)."""
+        if not self.isEnabledFor(level):
+            return
+        if not (self.handlers or len(_root.handlers) != _State.root_handlers or not self.propagate):
+            for sink in _State.sinks:
+                if level >= sink.level:
+                    sink.write_fast(level, self.name, message, trace_id, span_id)
+            return
+        from . import tracing  # the standard path: handlers read the context from the current span
+        tok = tracing._current.set(tracing.Span(tracing.tracer(), "", "server", trace_id, span_id, None, False, None))
+        try:
+            logging.Logger.log(self, level, message)
+        finally:
+            tracing._current.reset(tok)
+
     def info_each(self, msg: str, args_seq) -> None:
         """One Information record per argument tuple -- the same lines as ``info(msg, *args)``
         in a loop (e.g. one per task of a bulk operation), formatted as one batch."""

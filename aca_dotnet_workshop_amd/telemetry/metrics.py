@@ -75,6 +75,17 @@ class Histogram:
             s[1] += value
             s[2] += 1
 
+    def merge_key(self, key: tuple, buckets: list[int], total: float, n: int) -> None:
+        """Add observations counted elsewhere (per-bucket counts on this histogram's buckets)."""
+        with self._lock:
+            s = self.series.get(key)
+            if s is None:
+                s = self.series[key] = [[0] * (len(self.buckets) + 1), 0.0, 0]
+            for i, c in enumerate(buckets):
+                s[0][i] += c
+            s[1] += total
+            s[2] += n
+
     def quantile(self, q: float, **labels: str) -> float:
         s = self.series.get(tuple(sorted(labels.items())))
         if not s or not s[2]:
@@ -103,6 +114,11 @@ class Histogram:
 class Registry:
     def __init__(self) -> None:
         self.metrics: dict[str, object] = {}
+        self.collectors: list = []  # callables folding counts kept elsewhere (native routes) in
+
+    def collect(self) -> None:
+        for c in list(self.collectors):
+            c()
 
     def counter(self, name: str, help: str = "") -> Counter:
         return self.metrics.setdefault(name, Counter(name, help))  # type: ignore[return-value]
@@ -114,6 +130,7 @@ class Registry:
         return self.metrics.setdefault(name, Histogram(name, help))  # type: ignore[return-value]
 
     def expose(self) -> str:
+        self.collect()
         lines: list[str] = []
         for m in self.metrics.values():
             lines.extend(m.expose())  # type: ignore[attr-defined]
@@ -151,7 +168,7 @@ def request_telemetry_middleware(registry: Registry = REGISTRY):
     frame per request instead of two."""
     import time
 
-    from .tracing import parse_traceparent, tracer
+    from .tracing import new_trace_id, parse_traceparent, tracer
     reqs = registry.counter("http_requests_total", "HTTP requests served")
     lat = registry.histogram("http_request_duration_seconds", "HTTP request latency")
     keys: dict[tuple, tuple] = {}
@@ -159,7 +176,13 @@ def request_telemetry_middleware(registry: Registry = REGISTRY):
     async def mw(req, nxt):
         t0 = time.perf_counter()
         tp = req.headers.get("traceparent")
-        span = tracer().start_span(req.method, "server", parse_traceparent(tp) if tp else None)
+        if tp:
+            parent = parse_traceparent(tp)
+        elif req.state.get("tt_native") == "sample":  # a native route's sampler picked it
+            parent = (new_trace_id(), None, True)
+        else:
+            parent = None
+        span = tracer().start_span(req.method, "server", parent)
         req.state["trace_id"] = span.trace_id
         req.state["span"] = span
         try:

@@ -38,6 +38,29 @@ def enabled(environ: dict[str, str] | None = None, part: str = "") -> bool:
     return v == "native" or (bool(part) and v == f"native-{part}")
 
 
+_native_loggers: dict[str, logging.Logger] = {}
+
+
+def _native_log(level: int, name: str, message: str, trace_id: str, span_id: str) -> None:
+    """A native route's log record, written by this process's logging with the route's trace
+    context (what the Python handler's own ``log.info`` inside the request would write)."""
+    lg = _native_loggers.get(name)
+    if lg is None:
+        lg = _native_loggers[name] = logging.getLogger(name)
+    log_ids = getattr(lg, "log_ids", None)  # telemetry.logging.FastLogger
+    if log_ids is not None:
+        log_ids(level, message, trace_id, span_id)
+        return
+    if not lg.isEnabledFor(level):
+        return
+    from ..telemetry import tracing
+    tok = tracing._current.set(tracing.Span(tracing.tracer(), "", "server", trace_id, span_id, None, False, None))
+    try:
+        lg.log(level, message)
+    finally:
+        tracing._current.reset(tok)
+
+
 def _client_error(err: int, msg: str) -> BaseException:
     if err == _errno.ECONNREFUSED:
         return ConnectionRefusedError(err, msg)
@@ -102,6 +125,9 @@ class NativeHost:
         for ev in evs:
             lag = now - ev[-1]
             kind = ev[0]
+            if kind == 3:
+                _native_log(*ev[1:6])
+                continue
             if kind == 0:
                 _, token, sid, method, target, http10, hd, body, _ = ev
                 srv = self.servers.get(sid)
@@ -181,6 +207,8 @@ class NativeHost:
                         self.respond(token, 503, [], b"")
                         continue
                     srv._dispatch(token, method, target, http10, hd, body)
+                elif kind == 3:  # a native route's log record
+                    _native_log(ev[1], ev[2], ev[3], ev[4], ev[5])
                 else:
                     fut = self.pending.pop(ev[1], None)
                     if fut is not None and not fut.done():
@@ -245,6 +273,8 @@ class NativeHttpServer:
         self._inflight = 0
         self._closing = False
         self.ports: list[int] = []
+        self._routes: dict[int, tuple[str, str]] = {}  # native route id -> (method, route template)
+        self._collector = None
 
     async def listen_tcp(self, host: str = "127.0.0.1", port: int = 0, reuse_port: bool = False,
                          sock=None, tls_files: tuple[str, str] | None = None) -> int:
@@ -260,6 +290,37 @@ class NativeHttpServer:
         self.host.h.listen(self.sid, f"unix:{path}")
         return path
 
+    def native_route(self, kind: str, method: str, path: str, route: str, cfg: dict[str, str]) -> int:
+        """Hand ``method path`` to the I/O thread (apphost.hpp NativeRoute ``kind``): it serves
+        the requests it can decide end to end and passes the rest to the app as before.  ``route``
+        is the route template the request metrics carry; ``cfg`` the route's settings (sidecar
+        endpoint, targets, ...).  Its requests are counted into the process's registry."""
+        from ..telemetry import REGISTRY, tracing
+        from ..telemetry.metrics import _DEFAULT_BUCKETS
+        settings = {"method": method, "path": path, "sample_rate": repr(float(tracing.tracer().sample_rate)),
+                    **{k: str(v) for k, v in cfg.items()}}
+        rid = self.host.h.add_route(self.sid, kind, settings, list(_DEFAULT_BUCKETS))
+        self._routes[rid] = (method, route)
+        if self._collector is None:
+            reqs = REGISTRY.counter("http_requests_total", "HTTP requests served")
+            lat = REGISTRY.histogram("http_request_duration_seconds", "HTTP request latency")
+            keys: dict[tuple, tuple] = {}
+
+            def collect() -> None:
+                if self.host.closed:
+                    return
+                for rid_, status, n, total, buckets in self.host.h.route_stats():
+                    m, r = self._routes.get(rid_, ("?", "?"))
+                    k = keys.get((rid_, status))
+                    if k is None:  # the same label keys as the telemetry middleware's
+                        k = keys[(rid_, status)] = (tuple(sorted({"method": m, "route": r, "status": str(status)}.items())),
+                                                    (("route", r),))
+                    reqs.inc_key(k[0], n)
+                    lat.merge_key(k[1], buckets, total, n)
+            self._collector = collect
+            REGISTRY.collectors.append(collect)
+        return rid
+
     @property
     def port(self) -> int:
         if not self.ports:
@@ -269,11 +330,17 @@ class NativeHttpServer:
     def _dispatch(self, token: int, method: str, target: str, http10: bool, hd: dict, body: bytes) -> None:
         if self.host._stall is not None:
             import time as _t
-            self.loop.create_task(self._serve_traced(token, Request(method, target, Headers(hd), body, None,
-                                                                    "HTTP/1.0" if http10 else "HTTP/1.1"), _t.monotonic()))
+            note = hd.pop("x-tt-native", None)
+            req = Request(method, target, Headers(hd), body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
+            if note is not None:
+                req.state["tt_native"] = note
+            self.loop.create_task(self._serve_traced(token, req, _t.monotonic()))
             self._inflight += 1
             return
+        note = hd.pop("x-tt-native", None) if "x-tt-native" in hd else None
         req = Request(method, target, hd, body, None, "HTTP/1.0" if http10 else "HTTP/1.1")
+        if note is not None:  # a native route's hand-over (apphost.hpp; clients cannot send it)
+            req.state["tt_native"] = note
         self._inflight += 1
         self.loop.create_task(self._serve(token, req))
 
@@ -304,11 +371,17 @@ class NativeHttpServer:
         self._closing = True
         self.host.h.close_server(self.sid)
         deadline = self.loop.time() + grace
-        while self._inflight and self.loop.time() < deadline:
+        # Python's requests and the native routes' exchanges still in flight
+        while (self._inflight or (self._routes and self.host.h.pending_replies())) and self.loop.time() < deadline:
             await asyncio.sleep(0.01)
         self.host._flush()  # responses queued this iteration go out before the connections close
         self.host.h.close_connections(self.sid)
         self.host.servers.pop(self.sid, None)
+        if self._collector is not None:
+            from ..telemetry import REGISTRY
+            self._collector()  # the last counts
+            REGISTRY.collectors.remove(self._collector)
+            self._collector = None
         self.host.release()
 
 

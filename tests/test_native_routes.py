@@ -1,0 +1,240 @@
+"""Native routes of the app host (``native/src/apphost.hpp`` NativeRoute, ``web/native_host.py``
+``NativeHttpServer.native_route``): the frontend's ``POST /Tasks/Create`` and the API's
+``POST /api/tasks`` served end to end on the I/O thread, against the same apps with the routes
+off (``TT_NATIVE_ROUTES=0``: the Python handlers).
+
+Each scenario runs the real app under ``serve_host`` on the native host, with a recording
+sidecar on a Unix socket. It compares:
+* the response (status, Location);
+* every sidecar call: method, path, content type, trace context, body;
+* the log lines;
+* the request metrics.
+
+It also checks what goes to Python instead:
+* bodies the codec declines, bad antiforgery tokens, sampled traces;
+* failed sidecar calls, answered with the same error as the Python path;
+* a client's own ``x-tt-native`` header, which never reaches the app.
+"""
+import asyncio
+import json
+import logging
+import re
+
+import pytest
+
+from aca_dotnet_workshop_amd.telemetry import REGISTRY
+from aca_dotnet_workshop_amd.utils.config import Configuration
+from aca_dotnet_workshop_amd.web import WebApp
+from aca_dotnet_workshop_amd.web.client import HttpClient
+from aca_dotnet_workshop_amd.web.http import Response
+from aca_dotnet_workshop_amd.web.server import HttpServer
+
+from helpers import run
+
+TID = "4bf92f3577b34da6a3ce929d0e0e4736"
+UNSAMPLED = f"00-{TID}-00f067aa0ba902b7-00"
+SAMPLED = f"00-{TID}-00f067aa0ba902b7-01"
+
+
+class Sidecar:
+    """Records every call; answers with ``status[path prefix]`` (default 204 / 200)."""
+
+    def __init__(self):
+        self.calls = []
+        self.status: dict[str, tuple[int, bytes]] = {}
+        app = WebApp("fake-sidecar")
+
+        async def any_route(req):
+            self.calls.append((req.method, req.target, dict(req.headers), req.body))
+            for prefix, (st, body) in self.status.items():
+                if req.target.startswith(prefix):
+                    return Response(body, st, None, "application/json")
+            return Response(b"", 204)
+        app.add_route("/{*path}", any_route, ("GET", "POST", "PUT", "DELETE"))
+        self.app = app
+
+
+async def _serve(app, sock, stop, ports):
+    from aca_dotnet_workshop_amd.services.hosting import serve_host
+    await serve_host(app, stop, lambda p: ports.append(p))
+
+
+class _Lines(logging.Handler):
+    def __init__(self):
+        super().__init__(logging.INFO)
+        self.lines = []
+
+    def emit(self, record):
+        self.lines.append(record.getMessage())
+
+
+def _requests_total(route, status):
+    REGISTRY.collect()
+    return REGISTRY.counter("http_requests_total").get(method="POST", route=route, status=str(status))
+
+
+def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
+    """Run ``requests`` [(headers, body)] against the app ``which`` ('api' | 'frontend'); returns
+    (responses, sidecar calls, log lines, metric deltas)."""
+    monkeypatch.setenv("TT_APP_HOST", "native")
+    monkeypatch.setenv("TT_NATIVE_ROUTES", "1" if native else "0")
+    monkeypatch.setenv("TT_TRACE_SAMPLE_RATE", "0")
+    side_sock = str(tmp_path / f"side-{which}-{native}.sock")
+    app_sock = str(tmp_path / f"app-{which}-{native}.sock")
+    from aca_dotnet_workshop_amd.sdk.client import SidecarClient
+    from aca_dotnet_workshop_amd.telemetry import tracing
+    tracing.configure("native-routes-test", None, 0.0)
+    route = "/api/tasks" if which == "api" else "/Tasks/Create"
+    ok_status = 201 if which == "api" else 302
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        side = Sidecar()
+        side.status.update(sidecar_status)
+        srv = HttpServer(side.app, loop)
+        await srv.listen_unix(side_sock)
+        client = SidecarClient(f"unix:{side_sock}:")
+        cfg = Configuration([{"APP_PORT": "0", "Environment": "Production", "TT_APP_UDS": app_sock}])
+        if which == "api":
+            from aca_dotnet_workshop_amd.services.backend_api import create_app
+            from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
+            app = create_app(config=cfg, manager=TasksStoreManager(client))
+            logger = logging.getLogger("TasksManager")
+        else:
+            from aca_dotnet_workshop_amd.services.frontend import create_app
+            app = create_app([], client=client, overrides={"Frontend:AntiforgeryKey": "k3y", "APP_PORT": "0",
+                                                           "Environment": "Production", "TT_APP_UDS": app_sock})
+            logger = logging.getLogger("Frontend")
+        python_calls = []  # the Python handler's own work (not reached when the host serves)
+        if which == "api":
+            real, real_one = client.save_state_body, client.save_state
+
+            async def counted(store, body):
+                python_calls.append(1)
+                return await real(store, body)
+
+            async def counted_one(*a, **kw):
+                python_calls.append(1)
+                return await real_one(*a, **kw)
+            client.save_state_body, client.save_state = counted, counted_one
+        else:
+            gw = app.services["backend"]
+            real_call = gw.call
+
+            async def counted_call(*a, **kw):
+                python_calls.append(1)
+                return await real_call(*a, **kw)
+            gw.call = counted_call
+        lines = _Lines()
+        logger.addHandler(lines)
+        before = _requests_total(route, ok_status)
+        stop, ports = asyncio.Event(), []
+        task = asyncio.create_task(_serve(app, app_sock, stop, ports))
+        for _ in range(200):
+            if ports:
+                break
+            await asyncio.sleep(0.01)
+        c = HttpClient()
+        out = []
+        try:
+            for headers, body in requests:
+                r = await c.post(f"unix:{app_sock}:{route}", body=body, headers=headers)
+                out.append((r.status, r.headers.get("location"), r.headers.get("content-type"), r.body))
+        finally:
+            await c.close()
+            stop.set()
+            await task
+            await srv.close(1)
+            logger.removeHandler(lines)
+        return out, side.calls, lines.lines, _requests_total(route, ok_status) - before, len(python_calls)
+    return run(main())
+
+
+def _api_body(name="Buy milk"):
+    return json.dumps({"taskName": name, "taskCreatedBy": "a@b.c", "taskDueDate": "2030-01-01T00:00:00",
+                       "taskAssignedTo": "x@y.z"}).encode()
+
+
+def _norm_id(s):
+    return re.sub(r"[0-9a-f]{8}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]{12}", "<id>", s)
+
+
+def _norm_call(call):
+    method, target, headers, body = call
+    tp = headers.get("traceparent", "")
+    try:
+        doc = json.loads(body) if body else None
+    except ValueError:
+        doc = body
+    text = _norm_id(json.dumps(doc, sort_keys=True))
+    text = re.sub(r'"taskCreatedOn": "[^"]+"', '"taskCreatedOn": "<now>"', text)
+    return (method, target, headers.get("content-type"), tp[:36], tp[52:], "dapr-api-token" in headers, text)
+
+
+@pytest.mark.parametrize("status", [{}, {"/v1.0/state/": (500, b'{"errorCode":"ERR_STATE_SAVE"}')},
+                                    {"/v1.0/publish/": (404, b'{"errorCode":"ERR_PUBSUB_NOT_FOUND"}')}],
+                         ids=["ok", "save-fails", "publish-fails"])
+def test_api_create_native_equals_python(tmp_path, monkeypatch, status):
+    reqs = [([("Content-Type", "application/json"), ("traceparent", UNSAMPLED)], _api_body()),
+            ([("traceparent", UNSAMPLED)], _api_body("Ünïcode ✓ 'quoted'"))]
+    got = {n: _scenario(tmp_path, monkeypatch, "api", n, status, reqs) for n in (True, False)}
+    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
+    assert pn == 0 and pp == 2  # the host served both; with the routes off, the handler did
+    norm = lambda rs: [(s, _norm_id(loc or ""), ct, json.loads(b).get("status") if b else None) for s, loc, ct, b in rs]
+    assert norm(rn) == norm(rp)
+    assert [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp]
+    # the child span of the caller's context, unsampled, a span id of its own
+    for c in cn:
+        tp = c[2]["traceparent"]
+        assert tp.startswith(f"00-{TID}-") and tp.endswith("-00") and tp != UNSAMPLED
+    assert [_norm_id(x) for x in ln] == [_norm_id(x) for x in lp]
+    assert mn == mp
+    if not status:
+        assert [s for s, *_ in rn] == [201, 201] and mn == 2
+        save, pub = cn[0], cn[1]
+        key = json.loads(save[3])[0]["key"]
+        assert rn[0][1] == f"/api/tasks/{key}" and json.loads(pub[3])["taskId"] == key
+
+
+def test_api_create_goes_to_python_when_native_cannot_decide(tmp_path, monkeypatch):
+    reqs = [([("traceparent", SAMPLED)], _api_body()),                      # a sampled trace
+            ([("traceparent", UNSAMPLED), ("Content-Type", "text/plain")], _api_body()),  # not JSON
+            ([("traceparent", UNSAMPLED)], b'{"task_name": "snake"}'),      # the general binder's
+            ([("traceparent", UNSAMPLED), ("x-tt-native", "fail save 500 eA==")], _api_body())]  # spoofed
+    got = {n: _scenario(tmp_path, monkeypatch, "api", n, {}, reqs) for n in (True, False)}
+    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
+    assert pn == 2 and pp == 3  # the sampled and the snake_case ones were saved by the handler
+    assert [(s, _norm_id(loc or "")) for s, loc, *_ in rn] == [(s, _norm_id(loc or "")) for s, loc, *_ in rp]
+    assert [s for s, *_ in rn][-1] == 201  # the client's own hand-over header is ignored
+    assert [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp]
+    assert mn == mp
+
+
+def _form(token_ok=True, name="Buy+milk"):
+    import hmac
+    import hashlib
+    tok = hmac.new(b"k3y", b"c0ffee", hashlib.sha256).hexdigest() if token_ok else "0" * 64
+    return (f"__RequestVerificationToken={tok}&TaskAdd.TaskName={name}&TaskAdd.TaskDueDate=2030-01-01"
+            "&TaskAdd.TaskAssignedTo=a%40b.c").encode()
+
+
+_FE_HEADERS = [("Content-Type", "application/x-www-form-urlencoded"),
+               ("Cookie", "TasksCreatedByCookie=me%40x.y; .AspNetCore.Antiforgery=c0ffee")]
+
+
+@pytest.mark.parametrize("status", [{}, {"/v1.0/invoke/": (500, b'{"errorCode":"ERR_DIRECT_INVOKE"}')}],
+                         ids=["ok", "invoke-fails"])
+def test_frontend_create_native_equals_python(tmp_path, monkeypatch, status):
+    reqs = [(_FE_HEADERS, _form()), (_FE_HEADERS, _form(name="%C3%9Cn%C3%AF+%27q%27")),
+            (_FE_HEADERS, _form(token_ok=False)),                      # 400 from the page
+            (_FE_HEADERS + [("x-tt-native", "fail invoke 500 eA==")], _form())]  # spoofed
+    got = {n: _scenario(tmp_path, monkeypatch, "frontend", n, status, reqs) for n in (True, False)}
+    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
+    assert (pn, pp) == (1, 3)  # the codec leaves the non-ASCII name to the page; a bad token never calls the API
+    # the error page carries a fresh request id: compare status, location and content type
+    assert [r[:3] for r in rn] == [r[:3] for r in rp]
+    assert [_norm_call(c)[:3] + _norm_call(c)[4:] for c in cn] == [_norm_call(c)[:3] + _norm_call(c)[4:] for c in cp]
+    assert ln == lp and mn == mp
+    if not status:
+        assert [r[0] for r in rn] == [302, 302, 400, 302] and mn == 3
+        assert all(c[2]["traceparent"].endswith("-00") for c in cn)

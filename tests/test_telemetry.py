@@ -152,3 +152,46 @@ def test_info_each_writes_the_same_lines_as_a_loop(tmp_path, monkeypatch):
         for h in saved:
             if h not in root.handlers:
                 root.addHandler(h)
+
+
+def test_native_route_log_records_equal_the_handlers_own(tmp_path, monkeypatch):
+    """A native route's log record (apphost.hpp LOG event -> web/native_host.py _native_log)
+    is the JSON line the handler's own ``log.info`` writes inside its request span: same level,
+    role, category, message and trace ids; also on the standard logging path."""
+    import glob
+    from aca_dotnet_workshop_amd.telemetry.logging import configure_logging, flush_logs
+    from aca_dotnet_workshop_amd.web.native_host import _native_log
+
+    monkeypatch.setenv("TT_TELEMETRY_DIR", str(tmp_path))
+    monkeypatch.setenv("TT_LOG_CONSOLE", "0")
+    root = logging.getLogger()
+    saved, saved_tracer = list(root.handlers), tracing._tracer
+    try:
+        configure_logging("api")
+        lg = logging.getLogger("TasksManager")
+        t = tracing.configure("api", str(tmp_path / "spans"), 0.0)
+        msg = "Save a new task with name: '100% ✓' to state store"
+        with t.start_span("POST", "server") as sp:
+            lg.info("Save a new task with name: '%s' to state store", "100% ✓")
+        _native_log(logging.INFO, "TasksManager", msg, sp.trace_id, sp.span_id)
+        flush_logs()
+        recs = [json.loads(x) for f in glob.glob(str(tmp_path / "logs-api-*")) for x in open(f)]
+        strip = [{k: v for k, v in r.items() if k != "ts"} for r in recs]
+        assert len(strip) == 2 and strip[0] == strip[1] and strip[0]["message"] == msg
+        seen = []
+
+        class H(logging.Handler):
+            def emit(self, record):
+                seen.append((record.getMessage(), tracing.current_trace_id()))
+        h = H()
+        lg.addHandler(h)
+        try:
+            _native_log(logging.INFO, "TasksManager", msg, sp.trace_id, sp.span_id)
+        finally:
+            lg.removeHandler(h)
+        assert seen == [(msg, sp.trace_id)] and tracing.current_span() is None
+    finally:
+        for hd in list(root.handlers):
+            if hd not in saved:
+                root.removeHandler(hd)
+        tracing._tracer = saved_tracer
