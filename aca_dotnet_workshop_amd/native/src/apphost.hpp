@@ -74,7 +74,7 @@ struct Event {
 
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
-  enum Kind { kFrontendCreate = 1, kApiCreate = 2 };
+  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3 };
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -86,6 +86,7 @@ struct NativeRoute {
   std::string af_key, af_cookie, id_cookie, invoke_target, location;
   // kApiCreate: POST api/tasks -> state save -> publish -> 201
   std::string save_target, publish_target, log_category;
+  // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
 
@@ -288,10 +289,11 @@ class AppHost {
     };
     if (kind == "frontend_create") r->kind = NativeRoute::kFrontendCreate;
     else if (kind == "api_create") r->kind = NativeRoute::kApiCreate;
+    else if (kind == "processor_notify") r->kind = NativeRoute::kProcessorNotify;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
-    r->sidecar = ev::Endpoint::parse(get("sidecar"));
+    if (!get("sidecar").empty()) r->sidecar = ev::Endpoint::parse(get("sidecar"));
     r->token = get("token");
     if (!get("timeout").empty()) r->timeout_s = std::stod(get("timeout"));
     if (!get("sample_rate").empty()) r->sample_rate = std::stod(get("sample_rate"));
@@ -510,6 +512,44 @@ class AppHost {
     emit(std::move(e));
   }
 
+  // The content type as the Python request reads it (web/http.py Request.content_type).
+  static std::string media_type(const Message& m) {
+    const std::string* ct = header(m, "content-type");
+    std::string v = ct ? ct->substr(0, ct->find(';')) : std::string();
+    size_t a = v.find_first_not_of(" \t"), b = v.find_last_not_of(" \t");
+    v = a == std::string::npos ? std::string() : v.substr(a, b - a + 1);
+    for (auto& c : v) c = (char)std::tolower((unsigned char)c);
+    return v;
+  }
+
+  // kProcessorNotify: sdk/aspnet.py cloud_events_middleware (the envelope unwrapped by the same
+  // native pass) + the log-mode TasksNotifierController (services/processor/app.py task_saved).
+  bool notify(const std::shared_ptr<NativeRoute>& r, const Message& m, ev::Reply& reply, const std::string& tid) {
+    double t0 = ev::now_s();
+    std::string ctype = media_type(m);
+    std::string_view data(m.body);
+    ::taskcodec::Unwrapped u;
+    if (ctype == "application/cloudevents+json" && !m.body.empty()) {
+      if (!::taskcodec::unwrap_cloudevent(m.body, u)) return false;
+      data = u.data;
+      ctype = u.content_type.substr(0, u.content_type.find(';'));
+      size_t a = ctype.find_first_not_of(" \t"), b = ctype.find_last_not_of(" \t");
+      ctype = a == std::string::npos ? std::string() : ctype.substr(a, b - a + 1);
+      for (auto& c : ctype) c = (char)std::tolower((unsigned char)c);
+    }
+    if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
+    std::string name;
+    if (!::taskcodec::task_model_name(data, name)) return false;
+    NativeJob j;
+    j.trace_id = tid;
+    j.span_id = new_id(1);
+    log_event(*r, j, "Started processing message with Task Name '" + name + "'");
+    reply.send(200, {{"Content-Type", "text/plain; charset=utf-8"}},
+               "Started processing message with Task Name '" + name + "'");
+    r->record(200, ev::now_s() - t0);
+    return true;
+  }
+
   // true: the route took the request (answered now or later); false: Python serves `m`
   // (possibly marked `x-tt-native: sample`).
   bool serve_native(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply) {
@@ -521,6 +561,7 @@ class AppHost {
       m.headers.emplace_back("x-tt-native", "sample");
       return false;
     }
+    if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
     auto j = std::make_shared<NativeJob>();
     if (r->kind == NativeRoute::kFrontendCreate) {
       const std::string* cookie = header(m, "cookie");

@@ -59,6 +59,13 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
     api_app_id = cfg.get_str("Processor:BackendApiAppId", API_APP_ID)
 
     # -- TasksNotifierController ----------------------------------------------
+    if (cfg.get_str("TasksNotifier:Mode") or "log").lower() == "log":
+        # the app host's I/O thread answers the log-mode notification itself when it can: the
+        # same native envelope unwrap and binding check, log line and 200 as below
+        app.services.setdefault("native_routes", []).append({
+            "kind": "processor_notify", "method": "POST", "path": "/api/tasksnotifier/tasksaved",
+            "route": "/api/tasksnotifier/tasksaved", "cfg": {"log_category": log_notifier.name}})
+
     @app.route("/api/tasksnotifier/tasksaved", ("POST",), name="TaskSaved", tag="TasksNotifier", body=TaskModel)
     @topic("dapr-pubsub-servicebus", "tasksavedtopic")
     @topic("taskspubsub", "tasksavedtopic")

@@ -84,8 +84,8 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
     from aca_dotnet_workshop_amd.sdk.client import SidecarClient
     from aca_dotnet_workshop_amd.telemetry import tracing
     tracing.configure("native-routes-test", None, 0.0)
-    route = "/api/tasks" if which == "api" else "/Tasks/Create"
-    ok_status = 201 if which == "api" else 302
+    route = {"api": "/api/tasks", "frontend": "/Tasks/Create", "processor": "/api/tasksnotifier/tasksaved"}[which]
+    ok_status = {"api": 201, "frontend": 302, "processor": 200}[which]
 
     async def main():
         loop = asyncio.get_running_loop()
@@ -100,6 +100,10 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
             from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
             app = create_app(config=cfg, manager=TasksStoreManager(client))
             logger = logging.getLogger("TasksManager")
+        elif which == "processor":
+            from aca_dotnet_workshop_amd.services.processor import create_app
+            app = create_app([], client=client, config=cfg)
+            logger = logging.getLogger("TasksNotifierController")
         else:
             from aca_dotnet_workshop_amd.services.frontend import create_app
             app = create_app([], client=client, overrides={"Frontend:AntiforgeryKey": "k3y", "APP_PORT": "0",
@@ -117,6 +121,14 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
                 python_calls.append(1)
                 return await real_one(*a, **kw)
             client.save_state_body, client.save_state = counted, counted_one
+        elif which == "processor":
+            from aca_dotnet_workshop_amd.services.processor import app as proc
+            real_name = proc.task_model_name
+
+            def counted_name(body):
+                python_calls.append(1)
+                return real_name(body)
+            monkeypatch.setattr(proc, "task_model_name", counted_name)
         else:
             gw = app.services["backend"]
             real_call = gw.call
@@ -238,3 +250,27 @@ def test_frontend_create_native_equals_python(tmp_path, monkeypatch, status):
     if not status:
         assert [r[0] for r in rn] == [302, 302, 400, 302] and mn == 3
         assert all(c[2]["traceparent"].endswith("-00") for c in cn)
+
+
+def _event(data, ctype="application/json"):
+    return json.dumps({"specversion": "1.0", "type": "com.dapr.event.sent", "source": "tasksmanager-backend-api",
+                       "id": "e1", "datacontenttype": ctype, "topic": "tasksavedtopic", "pubsubname": "dapr-pubsub-servicebus",
+                       "traceparent": UNSAMPLED, "data": data}).encode()
+
+
+def test_processor_notify_native_equals_python(tmp_path, monkeypatch):
+    task = {"taskId": "2b0c7a4e-3f51-4a77-9c39-4a1f3d54e0f1", "taskName": "Ünïcode 'q' ✓", "taskCreatedBy": "a@b.c",
+            "taskCreatedOn": "2030-01-01T10:00:00.1234567Z", "taskDueDate": "2030-01-02T00:00:00",
+            "taskAssignedTo": "x@y.z", "isCompleted": False, "isOverDue": False}
+    ce = [("Content-Type", "application/cloudevents+json"), ("traceparent", UNSAMPLED)]
+    reqs = [(ce, _event(task)),                                               # the delivery: native
+            ([("Content-Type", "application/json"), ("traceparent", UNSAMPLED)], json.dumps(task).encode()),  # raw
+            (ce, _event({"task_name": "snake"})),                            # binder decides (400)
+            ([("Content-Type", "application/cloudevents+json"), ("traceparent", SAMPLED)], _event(task)),  # sampled
+            (ce, _event("plain text", "text/plain"))]                        # not JSON: the page's 400/415
+    got = {n: _scenario(tmp_path, monkeypatch, "processor", n, {}, reqs) for n in (True, False)}
+    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
+    assert [(s, ct, b if s == 200 else None) for s, _, ct, b in rn] == [(s, ct, b if s == 200 else None) for s, _, ct, b in rp]
+    assert [r[0] for r in rn][:2] == [200, 200]
+    assert ln == lp and mn == mp and cn == cp == []
+    assert pn == pp - 2  # the delivery and the raw body were answered by the host
