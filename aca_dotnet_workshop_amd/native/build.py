@@ -119,7 +119,7 @@ LOADGEN = HERE / "bin" / "ttloadgen"
 def build_loadgen(force: bool = False, verbose: bool = False) -> Path:
     """Closed-loop HTTP load generator used by bench.py (src/loadgen.cpp)."""
     sources = [SRC / "loadgen.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp"]
-    return _build_exe(LOADGEN, SRC / "loadgen.cpp", sources, force, verbose)
+    return _build_exe(LOADGEN, SRC / "loadgen.cpp", sources, force, verbose, threads=True)
 
 
 if __name__ == "__main__":

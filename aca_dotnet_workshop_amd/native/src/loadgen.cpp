@@ -19,6 +19,9 @@
 // HTTPS targets: `--target https://127.0.0.1:port` with `--tls-ca ca.crt` verifies the server
 // certificate (name / address) against that CA, the way a browser trusting it would; without
 // `--tls-ca` the connection is encrypted but unverified.
+// `--threads T` (stepped mode): T generators on T event loops, each with its share of the
+// in-flight window and of every step's batch; each waits for the counter to advance by the
+// WHOLE batch, so the steps stay in lock-step.  One JSON line merges them.
 //
 //   ttloadgen --target unix:/path/a.sock --target unix:/path/b.sock 
 //       --path /v1.0/invoke/api/method/api/tasks --bodies bodies.txt 
@@ -29,7 +32,9 @@
 #include <cstdio>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "evhttp.hpp"
@@ -46,7 +51,8 @@ struct Opts {
   std::string tls_ca;
   std::vector<std::string> bodies{""};
   ev::HeaderList headers;
-  int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0;
+  int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0, threads = 1;
+  int body_offset = 0;  // this generator's first body (a thread's share of the cycle)
   bool follow = false;
   double duration_s = 0;
   double until_timeout_s = 0;  // give up waiting for the counter after this long (0 = never)
@@ -128,6 +134,37 @@ class Gen {
   }
   long long errors() const { return errors_; }
 
+  // Fold another generator's results into this one (--threads).
+  void merge(const Gen& g) {
+    lat_.insert(lat_.end(), g.lat_.begin(), g.lat_.end());
+    follow_lat_.insert(follow_lat_.end(), g.follow_lat_.begin(), g.follow_lat_.end());
+    for (auto& kv : g.statuses_) statuses_[kv.first] += kv.second;
+    done_total_ += g.done_total_;
+    errors_ += g.errors_;
+    if (first_error_.empty()) first_error_ = g.first_error_;
+    t0_ = std::min(t0_, g.t0_);
+    t1_ = std::max(t1_, g.t1_);
+    for (size_t i = 0; i < steps_.size() && i < g.steps_.size(); ++i) {  // a step lasts as long as its slowest share
+      steps_[i].first = std::max(steps_[i].first, g.steps_[i].first);
+      steps_[i].second = std::max(steps_[i].second, g.steps_[i].second);
+    }
+  }
+
+  // The counter's current value (the sum over every --until-url), read on its own loop.
+  static long long read_counter(const Opts& o) {
+    ev::Loop loop;
+    Opts q = o;
+    q.steps = 0;
+    Gen g(loop, q);
+    long long out = -1;
+    g.poll_counter([&](long long v) {
+      out = v;
+      loop.stop();
+    });
+    loop.run();
+    return out;
+  }
+
  private:
   ev::Loop& loop_;
   ev::Client client_;
@@ -188,7 +225,8 @@ class Gen {
     }
     long long i = issued_++;
     const ev::Endpoint& ep = o_.targets[rr_++ % o_.targets.size()];
-    const std::string& body = o_.bodies[(size_t)((step_ * (long long)o_.batch + i) % (long long)o_.bodies.size())];
+    const std::string& body =
+        o_.bodies[(size_t)((o_.body_offset + step_ * (long long)o_.batch + i) % (long long)o_.bodies.size())];
     double t = ev::now_s();
     auto hdrs = std::make_shared<ev::HeaderList>(templated_ ? headers_for(user_rr_++) : hdrs_);
     client_.request(ep, o_.method, o_.path, *hdrs, body, 60, [this, t, &ep, hdrs](ev::ClientResult&& r) {
@@ -335,6 +373,7 @@ int main(int argc, char** argv) {
     else if (a == "--until-timeout") o.until_timeout_s = std::atof(next().c_str());
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
+    else if (a == "--threads") o.threads = std::max(1, std::atoi(next().c_str()));
     else if (a == "--bodies") {
       std::ifstream in(next());
       o.bodies.clear();
@@ -351,10 +390,43 @@ int main(int argc, char** argv) {
     return 2;
   }
   signal(SIGPIPE, SIG_IGN);
-  ev::Loop loop;
-  Gen g(loop, o);
-  g.start();
-  loop.run();
-  std::printf("%s\n", g.report().c_str());
-  return g.errors() ? 1 : 0;
+  int threads = std::min(o.threads, std::min(o.concurrency, o.batch));
+  if (threads <= 1 || o.duration_s > 0 || o.follow) {  // one generator on this thread
+    ev::Loop loop;
+    Gen g(loop, o);
+    g.start();
+    loop.run();
+    std::printf("%s\n", g.report().c_str());
+    return g.errors() ? 1 : 0;
+  }
+  // --threads: every generator waits for the counter to advance by the whole batch per step
+  if (!o.until_urls.empty() && o.until_base < 0) {
+    o.until_base = Gen::read_counter(o);
+    if (o.until_base < 0) {
+      std::fprintf(stderr, "counter poll failed\n");
+      return 1;
+    }
+  }
+  if (o.until_stride <= 0) o.until_stride = o.batch;
+  std::vector<std::unique_ptr<ev::Loop>> loops;
+  std::vector<std::unique_ptr<Gen>> gens;
+  for (int t = 0; t < threads; ++t) {
+    Opts q = o;
+    q.batch = o.batch / threads + (t < o.batch % threads ? 1 : 0);
+    q.concurrency = std::max(1, o.concurrency / threads + (t < o.concurrency % threads ? 1 : 0));
+    q.body_offset = t * (o.batch / threads);
+    std::rotate(q.targets.begin(), q.targets.begin() + (t % q.targets.size()), q.targets.end());
+    loops.push_back(std::make_unique<ev::Loop>());
+    gens.push_back(std::make_unique<Gen>(*loops.back(), q));
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t)
+    th.emplace_back([&, t] {
+      gens[t]->start();
+      loops[t]->run();
+    });
+  for (auto& x : th) x.join();
+  for (int t = 1; t < threads; ++t) gens[0]->merge(*gens[t]);
+  std::printf("%s\n", gens[0]->report().c_str());
+  return gens[0]->errors() ? 1 : 0;
 }

@@ -92,6 +92,8 @@ def parse() -> argparse.Namespace:
                     help="vCPU per replica (reference: 0.25); 0 = this rank's CPUs divided over its replicas")
     ap.add_argument("--trace-sampling", type=float, default=1.0,
                     help="App Insights sampling percentage of request traces (the manifest default is 100)")
+    ap.add_argument("--loadgen-threads", type=int, default=1,
+                    help="event loops of the native load generator (ttloadgen --threads)")
     ap.add_argument("--cpu-weights", default="",
                     help="frontend:api:processor relative vCPU per replica (default: CPU_WEIGHT)")
     ap.add_argument("--envelope-s", type=float, default=20.0,
@@ -609,7 +611,7 @@ def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
 
 def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int, batch: int,
                      conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
-                     ca_file: str | None = None) -> tuple[float, dict]:
+                     ca_file: str | None = None, threads: int = 1) -> tuple[float, dict]:
     """``targets``: ``host:port`` (a frontend replica) or ``https://host:port`` (the external
     ingress; ``ca_file`` -- the environment CA -- verifies its certificate like a browser)."""
     import subprocess
@@ -621,6 +623,8 @@ def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str 
         cmd += ["--until-base", str(shared[0]), "--until-stride", str(shared[1])]
     if ca_file:
         cmd += ["--tls-ca", ca_file]
+    if threads > 1:
+        cmd += ["--threads", str(threads)]
     for t in targets:
         cmd += ["--target", t]
     t0 = time.perf_counter()
@@ -900,7 +904,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if a.warmup:
             progress(f"warmup: {a.warmup} steps")
             run_form_loadgen(exe, targets, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
-                             (gbase, stride) if shared else None, ca_file)
+                             (gbase, stride) if shared else None, ca_file, a.loadgen_threads)
         progress(f"timed region: {a.steps} steps of {a.batch}")
         d.barrier()
         device_sync()
@@ -915,7 +919,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if sweeper is not None:
             sweeper.reset()  # sweeps of the timed region only
         dt, report = run_form_loadgen(exe, targets, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
-                                      (gbase + stride * a.warmup, stride) if shared else None, ca_file)
+                                      (gbase + stride * a.warmup, stride) if shared else None, ca_file,
+                                      a.loadgen_threads)
         device_sync()
         d.barrier()
         if sweeper is not None:
@@ -1016,7 +1021,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "replicas": {"frontend": fe, "api": api, "processor": proc},
                            "notifier": "TasksNotifier:Mode=log (the shipped controller)",
                            "dapr_api_logging": True, "trace_sampling_percent": a.trace_sampling,
-                           "concurrency_per_rank": conc, "load_generator": "native",
+                           "concurrency_per_rank": conc, "load_generator": "native" if a.loadgen_threads <= 1 else f"native, {a.loadgen_threads} event loops",
                            "cpu_pinning": pin_label(pinned),
                            "create_latency_p50_ms": round(p50, 3), "create_latency_p99_ms": round(p99, 3),
                            "baseline": "reference publishes no throughput",

@@ -22,6 +22,7 @@ for i in 1 2; do
   run fe3proc3_$i X=1 -- --frontend-replicas 3 --processor-replicas 3
   run ing4_$i TT_INGRESS_THREADS=4 --
   run bf4_$i TT_BACKING_FRONT_THREADS=4 --
+  run lg2_$i X=1 -- --loadgen-threads 2
 done
 run nosweep X=1 -- --overdue-sweep-ms 0
 echo ALL_OK
