@@ -70,6 +70,7 @@ struct Event {
   int err = 0;          // ERROR: errno-like code; LOG: the level (Python logging's numbers)
   double t = 0;         // loop-thread monotonic time when the event was queued (ev::now_s)
   Message msg;          // LOG: method = logger name, body = message, target/reason = trace/span id
+  std::string line;     // LOG: the finished JSON line, when the route has its sink's prefix
 };
 
 // A route the loop thread serves itself (AppHost::add_route).
@@ -86,6 +87,7 @@ struct NativeRoute {
   std::string af_key, af_cookie, id_cookie, invoke_target, location;
   // kApiCreate: POST api/tasks -> state save -> publish -> 201
   std::string save_target, publish_target, log_category;
+  std::string log_prefix;  // '{"level":..,"role":..,"category":..' of the process's JSON sink, or ""
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -305,6 +307,7 @@ class AppHost {
     r->save_target = get("save_target");
     r->publish_target = get("publish_target");
     r->log_category = get("log_category");
+    r->log_prefix = get("log_prefix");
     r->bounds = bounds;
     if (r->method.empty() || r->path.empty()) throw std::invalid_argument("a native route needs a method and a path");
     auto p = std::make_shared<std::promise<int>>();
@@ -475,6 +478,16 @@ class AppHost {
     Event e;
     e.kind = Event::LOG;
     e.err = 20;  // logging.INFO
+    if (!r.log_prefix.empty()) {  // telemetry/logging.py BufferedSink.write_fast's JSON line
+      char ts[40];
+      std::snprintf(ts, sizeof ts, ",\"ts\":%.6f,\"message\":",
+                    std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count());
+      e.line.reserve(r.log_prefix.size() + message.size() + 120);
+      e.line = r.log_prefix;
+      e.line += ts;
+      tt::escape_to(e.line, message);
+      e.line += ",\"traceId\":\"" + j.trace_id + "\",\"spanId\":\"" + j.span_id + "\"}\n";
+    }
     e.msg.method = r.log_category;
     e.msg.target = j.trace_id;
     e.msg.reason = j.span_id;

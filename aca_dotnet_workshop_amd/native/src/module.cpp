@@ -183,8 +183,8 @@ static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) 
       set_item(t.ptr(), 4, PyBytes_FromStringAndSize(e.msg.body.data(), (Py_ssize_t)e.msg.body.size()));
       if (with_times) set_item(t.ptr(), 5, PyFloat_FromDouble(e.t));
     } else if (e.kind == apphost::Event::LOG) {
-      // (3, level, logger name, message, trace id, span id)
-      t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 7 : 6));
+      // (3, level, logger name, message, trace id, span id, finished line or "")
+      t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 8 : 7));
       if (!t) throw py::error_already_set();
       set_item(t.ptr(), 0, PyLong_FromLong(3));
       set_item(t.ptr(), 1, PyLong_FromLong(e.err));
@@ -192,7 +192,8 @@ static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) 
       set_item(t.ptr(), 3, new_str(e.msg.body));
       set_item(t.ptr(), 4, new_str(e.msg.target));
       set_item(t.ptr(), 5, new_str(e.msg.reason));
-      if (with_times) set_item(t.ptr(), 6, PyFloat_FromDouble(e.t));
+      set_item(t.ptr(), 6, new_str(e.line));
+      if (with_times) set_item(t.ptr(), 7, PyFloat_FromDouble(e.t));
     } else {
       if (with_times) t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t);
       else t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)));

@@ -103,14 +103,21 @@ class BufferedSink(logging.Handler):
         if buffered:
             _Flusher.add(self)
 
+    def line_prefix(self, level: int, name: str) -> str:
+        """'{"level":..,"role":..,"category":..' of this JSON sink's lines for (level, logger)."""
+        pre = self._prefix.get((level, name))
+        if pre is None:
+            pre = self._prefix[(level, name)] = '{"level":"%s","role":%s,"category":%s' % (
+                _NET_LEVEL.get(level, logging.getLevelName(level)), self.role_json, encode_basestring(name))
+        return pre
+
     # fast path (FastLogger)
     def write_fast(self, level: int, name: str, message: str, trace_id: str, span_id: str) -> None:
         now = time.time()
         if self.json_lines:
             pre = self._prefix.get((level, name))
             if pre is None:  # '{"level":..,"role":..,"category":..' per (level, logger)
-                pre = self._prefix[(level, name)] = '{"level":"%s","role":%s,"category":%s' % (
-                    _NET_LEVEL.get(level, logging.getLevelName(level)), self.role_json, encode_basestring(name))
+                pre = self.line_prefix(level, name)
             if trace_id:
                 line = '%s,"ts":%.6f,"message":%s,"traceId":"%s","spanId":"%s"}\n' % (
                     pre, now, encode_basestring(message), trace_id, span_id)
@@ -331,6 +338,27 @@ def configure_logging(role: str, config: Any = None, json_console: bool | None =
     # fast path only while the root logger's handlers are exactly these sinks
     _State.root_handlers = len(root.handlers) if all(getattr(h, "_tt", False) for h in root.handlers) else -1
     _adopt_fast_loggers()
+
+
+def native_line_sink(name: str, level: int = logging.INFO) -> "BufferedSink | None":
+    """The one JSON sink a record of logger ``name`` at ``level`` goes to when the fast path
+    writes it, or None (another configuration: format the record in Python).  A native route
+    (web/native_host.py) then hands over the finished line."""
+    sinks = _State.sinks
+    if len(sinks) != 1 or not sinks[0].json_lines or level < sinks[0].level:
+        return None
+    lg = logging.getLogger(name)
+    if not isinstance(lg, FastLogger) or lg.handlers or len(_root.handlers) != _State.root_handlers \
+            or not lg.propagate or not lg.isEnabledFor(level):
+        return None
+    return sinks[0]
+
+
+def native_line_prefix(name: str, level: int = logging.INFO) -> str:
+    """The line prefix (``{"level":..,"role":..,"category":..``) ``native_line_sink``'s sink
+    writes for ``name``, or "" when records of ``name`` are not written by the fast path."""
+    sink = native_line_sink(name, level)
+    return sink.line_prefix(level, name) if sink is not None else ""
 
 
 def info_each(logger: logging.Logger, msg: str, args_seq) -> None:

@@ -41,9 +41,17 @@ def enabled(environ: dict[str, str] | None = None, part: str = "") -> bool:
 _native_loggers: dict[str, logging.Logger] = {}
 
 
-def _native_log(level: int, name: str, message: str, trace_id: str, span_id: str) -> None:
+def _native_log(level: int, name: str, message: str, trace_id: str, span_id: str, line: str = "") -> None:
     """A native route's log record, written by this process's logging with the route's trace
-    context (what the Python handler's own ``log.info`` inside the request would write)."""
+    context (what the Python handler's own ``log.info`` inside the request would write).
+    ``line``: the record already formatted by the route (the sink's prefix, handed over at
+    registration) -- appended as is while that sink still writes these records."""
+    if line:
+        from ..telemetry.logging import native_line_sink
+        sink = native_line_sink(name, level)
+        if sink is not None:
+            sink._put(line)
+            return
     lg = _native_loggers.get(name)
     if lg is None:
         lg = _native_loggers[name] = logging.getLogger(name)
@@ -126,7 +134,7 @@ class NativeHost:
             lag = now - ev[-1]
             kind = ev[0]
             if kind == 3:
-                _native_log(*ev[1:6])
+                _native_log(*ev[1:7])
                 continue
             if kind == 0:
                 _, token, sid, method, target, http10, hd, body, _ = ev
@@ -208,7 +216,7 @@ class NativeHost:
                         continue
                     srv._dispatch(token, method, target, http10, hd, body)
                 elif kind == 3:  # a native route's log record
-                    _native_log(ev[1], ev[2], ev[3], ev[4], ev[5])
+                    _native_log(ev[1], ev[2], ev[3], ev[4], ev[5], ev[6])
                 else:
                     fut = self.pending.pop(ev[1], None)
                     if fut is not None and not fut.done():
@@ -299,6 +307,9 @@ class NativeHttpServer:
         from ..telemetry.metrics import _DEFAULT_BUCKETS
         settings = {"method": method, "path": path, "sample_rate": repr(float(tracing.tracer().sample_rate)),
                     **{k: str(v) for k, v in cfg.items()}}
+        if cfg.get("log_category"):  # the route formats its lines itself when the fast path would
+            from ..telemetry.logging import native_line_prefix
+            settings["log_prefix"] = native_line_prefix(cfg["log_category"])
         rid = self.host.h.add_route(self.sid, kind, settings, list(_DEFAULT_BUCKETS))
         self._routes[rid] = (method, route)
         if self._collector is None:

@@ -73,7 +73,7 @@ def _requests_total(route, status):
     return REGISTRY.counter("http_requests_total").get(method="POST", route=route, status=str(status))
 
 
-def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
+def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, attach=True):
     """Run ``requests`` [(headers, body)] against the app ``which`` ('api' | 'frontend'); returns
     (responses, sidecar calls, log lines, metric deltas)."""
     monkeypatch.setenv("TT_APP_HOST", "native")
@@ -138,7 +138,8 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
                 return await real_call(*a, **kw)
             gw.call = counted_call
         lines = _Lines()
-        logger.addHandler(lines)
+        if attach:
+            logger.addHandler(lines)
         before = _requests_total(route, ok_status)
         stop, ports = asyncio.Event(), []
         task = asyncio.create_task(_serve(app, app_sock, stop, ports))
@@ -157,7 +158,8 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
             stop.set()
             await task
             await srv.close(1)
-            logger.removeHandler(lines)
+            if attach:
+                logger.removeHandler(lines)
         return out, side.calls, lines.lines, _requests_total(route, ok_status) - before, len(python_calls)
     return run(main())
 
@@ -274,3 +276,37 @@ def test_processor_notify_native_equals_python(tmp_path, monkeypatch):
     assert [r[0] for r in rn][:2] == [200, 200]
     assert ln == lp and mn == mp and cn == cp == []
     assert pn == pp - 2  # the delivery and the raw body were answered by the host
+
+
+def test_native_log_lines_equal_the_python_sinks(tmp_path, monkeypatch):
+    """With the process's JSON sink on the fast path, the native route writes the finished log
+    line itself (the sink's prefix handed over at registration): the records in the telemetry
+    directory equal the Python handler's, apart from the timestamp and the span / task ids."""
+    import glob
+
+    from aca_dotnet_workshop_amd.telemetry.logging import flush_logs, native_line_prefix
+    root = logging.getLogger()
+    saved = list(root.handlers)
+    for hd in saved:  # pytest's capture handler would take the records off the fast path
+        root.removeHandler(hd)
+    recs = {}
+    try:
+        for n in (True, False):
+            d = tmp_path / f"logs-{n}"
+            monkeypatch.setenv("TT_TELEMETRY_DIR", str(d))
+            monkeypatch.setenv("TT_LOG_CONSOLE", "0")
+            reqs = [([("traceparent", UNSAMPLED)], _api_body("tab\tquote\" ✓"))]
+            _scenario(tmp_path, monkeypatch, "api", n, {}, reqs, attach=False)
+            assert native_line_prefix("TasksManager").startswith('{"level":"Information","role":')
+            flush_logs()
+            lines = [json.loads(x) for f in glob.glob(str(d / "logs-*")) for x in open(f)]
+            recs[n] = [{k: (_norm_id(v) if isinstance(v, str) else v) for k, v in r.items() if k not in ("ts", "spanId")}
+                       for r in lines if r.get("category") == "TasksManager"]
+    finally:
+        for hd in list(root.handlers):
+            if hd not in saved:
+                root.removeHandler(hd)
+        for hd in saved:
+            root.addHandler(hd)
+    assert len(recs[True]) == 2 and recs[True] == recs[False]
+    assert recs[True][0]["traceId"] == TID and "tab\tquote\" ✓" in recs[True][0]["message"]
