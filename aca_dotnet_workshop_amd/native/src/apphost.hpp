@@ -50,7 +50,6 @@
 #include <memory>
 #include <mutex>
 #include <thread>
-#include <unordered_set>
 
 #include "evhttp.hpp"
 #include "formcodec.hpp"
@@ -76,7 +75,7 @@ struct Event {
 
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
-  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kApiOverduePage = 4, kApiMarkOverdue = 5 };
+  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3 };
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -90,11 +89,6 @@ struct NativeRoute {
   std::string save_target, publish_target, log_category;
   std::string log_prefix;  // '{"level":..,"role":..,"category":..' of the process's JSON sink, or ""
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
-  // kApiOverduePage: GET api/overduetasks (range mode) -> state query -> TaskModel page
-  // kApiMarkOverdue: POST api/overduetasks/markoverdue -> bulk get -> conditional bulk save
-  std::string query_target, bulk_target;
-  long page_size = 1000;
-  int max_retries = 5;
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
 
@@ -298,8 +292,6 @@ class AppHost {
     if (kind == "frontend_create") r->kind = NativeRoute::kFrontendCreate;
     else if (kind == "api_create") r->kind = NativeRoute::kApiCreate;
     else if (kind == "processor_notify") r->kind = NativeRoute::kProcessorNotify;
-    else if (kind == "api_overdue_page") r->kind = NativeRoute::kApiOverduePage;
-    else if (kind == "api_mark_overdue") r->kind = NativeRoute::kApiMarkOverdue;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -316,10 +308,6 @@ class AppHost {
     r->publish_target = get("publish_target");
     r->log_category = get("log_category");
     r->log_prefix = get("log_prefix");
-    r->query_target = get("query_target");
-    r->bulk_target = get("bulk_target");
-    if (!get("page_size").empty()) r->page_size = std::stol(get("page_size"));
-    if (!get("max_retries").empty()) r->max_retries = std::stoi(get("max_retries"));
     r->bounds = bounds;
     if (r->method.empty() || r->path.empty()) throw std::invalid_argument("a native route needs a method and a path");
     auto p = std::make_shared<std::promise<int>>();
@@ -484,8 +472,6 @@ class AppHost {
     std::string trace_id, span_id, traceparent;
     ev::HeaderList out_headers;  // traceparent, token, content-type: the SDK's unsampled call
     ::taskcodec::Created task;
-    std::vector<std::string> pending;  // kApiMarkOverdue: the ids still to mark
-    int attempt = 0;
   };
 
   void log_event(const NativeRoute& r, const NativeJob& j, std::string message) {
@@ -512,14 +498,6 @@ class AppHost {
   void finish(NativeJob& j, int status, const ev::HeaderList& headers) {
     j.reply.send(status, headers, {});
     j.route->record(status, ev::now_s() - j.t0);
-    native_inflight_.fetch_sub(1);
-  }
-
-  // The request goes to Python as it came (`note` empty: Python redoes it from the start) or
-  // with a note its handler turns into the error the Python path raises.
-  void hand_over_note(NativeJob& j, std::string note) {
-    if (!note.empty()) j.req.headers.emplace_back("x-tt-native", std::move(note));
-    to_python(j.server, std::move(j.req), std::move(j.reply));
     native_inflight_.fetch_sub(1);
   }
 
@@ -585,140 +563,6 @@ class AppHost {
     return true;
   }
 
-  std::shared_ptr<NativeJob> start_job(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply,
-                                       std::string tid) {
-    auto j = std::make_shared<NativeJob>();
-    j->route = r;
-    j->server = server;
-    j->t0 = ev::now_s();
-    j->trace_id = std::move(tid);
-    j->span_id = new_id(1);
-    j->traceparent = "00-" + j->trace_id + "-" + j->span_id + "-00";
-    j->out_headers.emplace_back("traceparent", j->traceparent);
-    if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
-    j->out_headers.emplace_back("Content-Type", "application/json");
-    j->req = std::move(m);
-    j->reply = std::move(reply);
-    native_inflight_.fetch_add(1);
-    return j;
-  }
-
-  // kApiOverduePage: services/backend_api TasksStoreManager.overdue_page_json (range mode) --
-  // "Getting open tasks due before" log line, the range query ordered by taskCreatedOn, the page
-  // as the TaskModel JSON array ordered by TaskCreatedOn (taskcodec query_tasks), and
-  // x-tt-more-results from the store's continuation token.
-  bool overdue_page(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply, std::string tid) {
-    long page = r->page_size;
-    std::string_view tgt(m.target);
-    size_t q = tgt.find('?');
-    if (q != std::string_view::npos) {  // Request.query_get("limit"): the first value
-      std::string_view qs = tgt.substr(q + 1);
-      for (size_t i = 0; i <= qs.size();) {
-        size_t amp = qs.find('&', i);
-        if (amp == std::string_view::npos) amp = qs.size();
-        std::string_view kv = qs.substr(i, amp - i);
-        size_t eq = kv.find('=');
-        std::string_view k = kv.substr(0, eq), v = eq == std::string_view::npos ? std::string_view() : kv.substr(eq + 1);
-        if (k.find('%') != std::string_view::npos || k.find('+') != std::string_view::npos) return false;
-        if (k == "limit") {
-          if (v.find_first_not_of("0123456789") != std::string_view::npos && (v.find('%') != std::string_view::npos ||
-                                                                               v.find('+') != std::string_view::npos))
-            return false;  // encoded: Python decodes it
-          if (!v.empty() && v.size() <= 9 && v.find_first_not_of("0123456789") == std::string_view::npos) {
-            long lim = std::stol(std::string(v));
-            if (lim > 0) page = lim;
-          }
-          break;
-        }
-        i = amp + 1;
-      }
-    }
-    time_t now = ::time(nullptr);
-    struct tm lt;
-    localtime_r(&now, &lt);  // DateTime.Today (models/dotnet.py today)
-    char midnight[32];
-    std::snprintf(midnight, sizeof midnight, "%04d-%02d-%02dT00:00:00", lt.tm_year + 1900, lt.tm_mon + 1, lt.tm_mday);
-    auto j = start_job(r, server, m, reply, std::move(tid));
-    log_event(*r, *j, std::string("Getting open tasks due before: '") + midnight + "' (page of " + std::to_string(page) +
-                          ")");
-    std::string body = std::string("{\"filter\": {\"AND\": [{\"LT\": {\"taskDueDate\": \"") + midnight +
-                       "\"}}, {\"EQ\": {\"isCompleted\": false}}, {\"EQ\": {\"isOverDue\": false}}]}, \"sort\": "
-                       "[{\"key\": \"taskCreatedOn\", \"order\": \"ASC\"}], \"page\": {\"limit\": " +
-                       std::to_string(page) + "}}";
-    client_.request(r->sidecar, "POST", r->query_target, j->out_headers, body, r->timeout_s,
-                    [this, j](ev::ClientResult&& res) {
-                      if (res.err || res.resp.status >= 300) return hand_over(*j, "query", res);
-                      std::string out;
-                      size_t count = 0;
-                      bool more = false;
-                      if (!::taskcodec::query_tasks(res.resp.body, out, count, true, &more))
-                        return hand_over_note(*j, "");  // documents outside the codec: Python binds them
-                      j->reply.send(200, {{"Content-Type", "application/json; charset=utf-8"},
-                                          {"x-tt-more-results", more ? "true" : "false"}}, out);
-                      j->route->record(200, ev::now_s() - j->t0);
-                      native_inflight_.fetch_sub(1);
-                    });
-    return true;
-  }
-
-  // kApiMarkOverdue: TasksStoreManager.mark_overdue_from_body + _mark_conditionally -- the ids
-  // from the body, then per attempt: bulk get, the conditional mark of the stored copies (open
-  // and not yet overdue, ETag-guarded first-write), a "Mark task ... as OverDue task" line per
-  // task, the bulk save; a 409/412 re-reads the tasks of that attempt, up to max_retries.
-  bool mark_overdue(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply, std::string tid) {
-    std::string ctype = media_type(m);
-    if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
-    std::vector<std::string> ids;
-    std::string unused;
-    if (!::taskcodec::mark_overdue(m.body, ids, unused)) return false;
-    auto j = start_job(r, server, m, reply, std::move(tid));
-    std::unordered_set<std::string> seen;
-    for (auto& id : ids)
-      if (seen.insert(id).second) j->pending.push_back(std::move(id));
-    mark_attempt(j);
-    return true;
-  }
-
-  void mark_attempt(const std::shared_ptr<NativeJob>& j) {
-    const NativeRoute& r = *j->route;
-    if (j->pending.empty()) return finish_ok(*j);
-    if (j->attempt >= r.max_retries)
-      return hand_over_note(*j, "conflict " + std::to_string(j->pending.size()));
-    ++j->attempt;
-    std::string body = "{\"keys\":[";
-    for (size_t i = 0; i < j->pending.size(); ++i) {
-      if (i) body += ',';
-      tt::escape_to(body, j->pending[i]);
-    }
-    body += "],\"parallelism\":10}";
-    client_.request(r.sidecar, "POST", r.bulk_target, j->out_headers, body, r.timeout_s,
-                    [this, j](ev::ClientResult&& res) {
-                      if (res.err || res.resp.status >= 300) return hand_over(*j, "bulkget", res);
-                      std::string bulk;
-                      std::vector<std::string> marked;
-                      size_t skipped = 0;
-                      if (!::taskcodec::conditional_mark(res.resp.body, bulk, marked, skipped))
-                        return hand_over_note(*j, "");  // Python raises the same ValueError
-                      for (auto& id : marked) log_event(*j->route, *j, "Mark task with Id: '" + id + "' as OverDue task");
-                      if (marked.empty()) return finish_ok(*j);
-                      j->pending = std::move(marked);
-                      const NativeRoute& r2 = *j->route;
-                      client_.request(r2.sidecar, "POST", r2.save_target, j->out_headers, bulk, r2.timeout_s,
-                                      [this, j](ev::ClientResult&& res2) {
-                                        if (!res2.err && res2.resp.status < 300) return finish_ok(*j);
-                                        if (!res2.err && (res2.resp.status == 409 || res2.resp.status == 412))
-                                          return mark_attempt(j);  // lost a race: re-read and re-apply
-                                        hand_over(*j, "save", res2);
-                                      });
-                    });
-  }
-
-  void finish_ok(NativeJob& j) {
-    j.reply.send(200, {}, {});
-    j.route->record(200, ev::now_s() - j.t0);
-    native_inflight_.fetch_sub(1);
-  }
-
   // true: the route took the request (answered now or later); false: Python serves `m`
   // (possibly marked `x-tt-native: sample`).
   bool serve_native(const std::shared_ptr<NativeRoute>& r, int server, Message& m, ev::Reply& reply) {
@@ -731,8 +575,6 @@ class AppHost {
       return false;
     }
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
-    if (r->kind == NativeRoute::kApiOverduePage) return overdue_page(r, server, m, reply, std::move(tid));
-    if (r->kind == NativeRoute::kApiMarkOverdue) return mark_overdue(r, server, m, reply, std::move(tid));
     auto j = std::make_shared<NativeJob>();
     if (r->kind == NativeRoute::kFrontendCreate) {
       const std::string* cookie = header(m, "cookie");

@@ -35,7 +35,7 @@ from ...sdk.client import client_from_config, native_route_failure
 from ...web.app import WebApp, read_model
 from ...web.http import HTTPError, Request, Response, empty
 from ..hosting import create_host, map_openapi, run_host
-from .managers import ConcurrencyConflict, FakeTasksManager, TasksManager, TasksStoreManager
+from .managers import FakeTasksManager, TasksManager, TasksStoreManager
 
 ROLE = "tasksmanager-backend-api"
 CONTENT_ROOT = Path(__file__).parent
@@ -80,16 +80,6 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
         # 201; the rest (bodies for the general binder, sampled traces, a failed sidecar call)
         # comes to this handler
         app.services.setdefault("native_routes", []).append(spec)
-    # the overdue sweep's two calls likewise (range mode): the same query / page codec and the
-    # same conditional mark with its retries as overdue_page_json and mark_overdue_from_body
-    overdue = getattr(manager, "native_overdue_routes", None)
-    overdue_specs = overdue() if overdue is not None else []
-    overdue_what = {}
-    for sp in overdue_specs:
-        overdue_what[sp["path"]] = sp.pop("what")
-        app.services.setdefault("native_routes", []).append(sp)
-    page_what = overdue_what.get("/api/overduetasks", {})
-    mark_what = overdue_what.get("/api/overduetasks/markoverdue", {})
 
     @app.route("/api/tasks", ("POST",), name="CreateTask", tag="Tasks", body=TaskAddModel, responses={201: None})
     async def post_task(req: Request) -> Response:
@@ -128,9 +118,6 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/overduetasks", ("GET",), name="GetOverdueTasks", tag="OverdueTasks", query=["limit"],
                responses={200: [TaskModel]})
     async def get_overdue(req: Request) -> Response:
-        failed = native_route_failure(req, page_what) if page_what else None
-        if failed is not None:  # the native route's query failed: the SDK's error
-            raise failed
         raw = req.query_get("limit") or ""
         limit = int(raw) if raw.isdigit() else None  # page size of the range sweep (OverdueTasks:Query=range)
         if fast_page is not None:
@@ -146,13 +133,6 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",
                body=[TaskModel], responses={200: None})
     async def mark_overdue(req: Request) -> Response:
-        if mark_what:
-            note = req.state.get("tt_native") or ""
-            if note.startswith("conflict "):  # the native route's retries ran out
-                raise ConcurrencyConflict(f"{note.split(' ')[1]} overdue tasks kept changing under concurrent writers")
-            failed = native_route_failure(req, mark_what)
-            if failed is not None:  # its bulk get or save failed: the SDK's error
-                raise failed
         ctype = req.content_type
         if fast_mark is not None and (not ctype or "json" in ctype) and await fast_mark(req.body):
             return empty(200)

@@ -212,26 +212,6 @@ class TasksStoreManager(TasksManager):
                         "log_category": log.name},
                 "what": {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}"}}
 
-    def native_overdue_routes(self) -> list[dict]:
-        """``overdue_page_json`` and ``mark_overdue_from_body`` as native routes of the app host
-        (apphost.hpp ``api_overdue_page`` / ``api_mark_overdue``; range mode only), with the SDK's
-        error messages for their calls under ``what``; [] when this client cannot take them."""
-        ep_of = getattr(self.client, "native_endpoint", None)
-        ep = ep_of() if ep_of is not None else None
-        if ep is None or self.overdue_query != "range" or getattr(self.client, "get_bulk_state_raw", None) is None:
-            return []
-        base = {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"], "log_category": log.name}
-        return [{"kind": "api_overdue_page", "method": "GET", "path": "/api/overduetasks", "route": "/api/overduetasks",
-                 "cfg": {**base, "query_target": f"{ep['prefix']}/v1.0-alpha1/state/{self.store}/query",
-                         "page_size": str(self.overdue_page)},
-                 "what": {"query": f"query state {self.store}"}},
-                {"kind": "api_mark_overdue", "method": "POST", "path": "/api/overduetasks/markoverdue",
-                 "route": "/api/overduetasks/markoverdue",
-                 "cfg": {**base, "bulk_target": f"{ep['prefix']}/v1.0/state/{self.store}/bulk",
-                         "save_target": f"{ep['prefix']}/v1.0/state/{self.store}",
-                         "max_retries": str(self.max_retries)},
-                 "what": {"bulkget": f"bulk get {self.store}", "save": f"save state {self.store}"}}]
-
     async def delete_task(self, task_id) -> bool:
         log.info("Delete task with Id: '%s'", task_id)
         data, etag = await self.client.get_state_and_etag(self.store, str(task_id))

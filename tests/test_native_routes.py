@@ -46,9 +46,8 @@ class Sidecar:
 
         async def any_route(req):
             self.calls.append((req.method, req.target, dict(req.headers), req.body))
-            for prefix, ans in self.status.items():
+            for prefix, (st, body) in self.status.items():
                 if req.target.startswith(prefix):
-                    st, body = ans(req) if callable(ans) else ans
                     return Response(body, st, None, "application/json")
             return Response(b"", 204)
         app.add_route("/{*path}", any_route, ("GET", "POST", "PUT", "DELETE"))
@@ -85,10 +84,8 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, at
     from aca_dotnet_workshop_amd.sdk.client import SidecarClient
     from aca_dotnet_workshop_amd.telemetry import tracing
     tracing.configure("native-routes-test", None, 0.0)
-    route = {"api": "/api/tasks", "frontend": "/Tasks/Create", "processor": "/api/tasksnotifier/tasksaved",
-             "overdue": "/api/overduetasks", "mark": "/api/overduetasks/markoverdue"}[which]
-    ok_status = {"api": 201, "frontend": 302, "processor": 200, "overdue": 200, "mark": 200}[which]
-    method = "GET" if which == "overdue" else "POST"
+    route = {"api": "/api/tasks", "frontend": "/Tasks/Create", "processor": "/api/tasksnotifier/tasksaved"}[which]
+    ok_status = {"api": 201, "frontend": 302, "processor": 200}[which]
 
     async def main():
         loop = asyncio.get_running_loop()
@@ -98,11 +95,10 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, at
         await srv.listen_unix(side_sock)
         client = SidecarClient(f"unix:{side_sock}:")
         cfg = Configuration([{"APP_PORT": "0", "Environment": "Production", "TT_APP_UDS": app_sock}])
-        if which in ("api", "overdue", "mark"):
+        if which == "api":
             from aca_dotnet_workshop_amd.services.backend_api import create_app
             from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
-            mgr = TasksStoreManager(client, overdue_query="range" if which != "api" else "equality", max_retries=3)
-            app = create_app(config=cfg, manager=mgr)
+            app = create_app(config=cfg, manager=TasksStoreManager(client))
             logger = logging.getLogger("TasksManager")
         elif which == "processor":
             from aca_dotnet_workshop_amd.services.processor import create_app
@@ -114,18 +110,7 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, at
                                                            "Environment": "Production", "TT_APP_UDS": app_sock})
             logger = logging.getLogger("Frontend")
         python_calls = []  # the Python handler's own work (not reached when the host serves)
-        if which in ("overdue", "mark"):
-            real_q, real_b = client.query_state_raw, client.get_bulk_state_raw
-
-            async def counted_q(*a, **kw):
-                python_calls.append(1)
-                return await real_q(*a, **kw)
-
-            async def counted_b(*a, **kw):
-                python_calls.append(1)
-                return await real_b(*a, **kw)
-            client.query_state_raw, client.get_bulk_state_raw = counted_q, counted_b
-        elif which == "api":
+        if which == "api":
             real, real_one = client.save_state_body, client.save_state
 
             async def counted(store, body):
@@ -165,12 +150,9 @@ def _scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, at
         c = HttpClient()
         out = []
         try:
-            for req in requests:
-                headers, body = req[0], req[1]
-                path = route + (req[2] if len(req) > 2 else "")
-                r = await c.request(method, f"unix:{app_sock}:{path}", body=body or None, headers=headers)
-                out.append((r.status, r.headers.get("location"), r.headers.get("content-type"), r.body,
-                            r.headers.get("x-tt-more-results")))
+            for headers, body in requests:
+                r = await c.post(f"unix:{app_sock}:{route}", body=body, headers=headers)
+                out.append((r.status, r.headers.get("location"), r.headers.get("content-type"), r.body))
         finally:
             await c.close()
             stop.set()
@@ -212,7 +194,7 @@ def test_api_create_native_equals_python(tmp_path, monkeypatch, status):
     got = {n: _scenario(tmp_path, monkeypatch, "api", n, status, reqs) for n in (True, False)}
     (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
     assert pn == 0 and pp == 2  # the host served both; with the routes off, the handler did
-    norm = lambda rs: [(s, _norm_id(loc or ""), ct, json.loads(b).get("status") if b else None) for s, loc, ct, b, _ in rs]
+    norm = lambda rs: [(s, _norm_id(loc or ""), ct, json.loads(b).get("status") if b else None) for s, loc, ct, b in rs]
     assert norm(rn) == norm(rp)
     assert [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp]
     # the child span of the caller's context, unsampled, a span id of its own
@@ -290,7 +272,7 @@ def test_processor_notify_native_equals_python(tmp_path, monkeypatch):
             (ce, _event("plain text", "text/plain"))]                        # not JSON: the page's 400/415
     got = {n: _scenario(tmp_path, monkeypatch, "processor", n, {}, reqs) for n in (True, False)}
     (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
-    assert [(s, ct, b if s == 200 else None) for s, _, ct, b, _m in rn] == [(s, ct, b if s == 200 else None) for s, _, ct, b, _m in rp]
+    assert [(s, ct, b if s == 200 else None) for s, _, ct, b in rn] == [(s, ct, b if s == 200 else None) for s, _, ct, b in rp]
     assert [r[0] for r in rn][:2] == [200, 200]
     assert ln == lp and mn == mp and cn == cp == []
     assert pn == pp - 2  # the delivery and the raw body were answered by the host
@@ -328,73 +310,3 @@ def test_native_log_lines_equal_the_python_sinks(tmp_path, monkeypatch):
             root.addHandler(hd)
     assert len(recs[True]) == 2 and recs[True] == recs[False]
     assert recs[True][0]["traceId"] == TID and "tab\tquote\" ✓" in recs[True][0]["message"]
-
-
-def _task(i, completed=False, overdue=False):
-    return {"taskId": f"00000000-0000-4000-8000-00000000000{i}", "taskName": f"t{i} 'q' ✓", "taskCreatedBy": "a@b.c",
-            "taskCreatedOn": f"2024-01-0{i}T10:00:00.1234567Z", "taskDueDate": "2024-01-01T00:00:00",
-            "taskAssignedTo": "x@y.z", "isCompleted": completed, "isOverDue": overdue}
-
-
-def _query_page(req):
-    q = json.loads(req.body)
-    assert q["sort"] == [{"key": "taskCreatedOn", "order": "ASC"}]
-    rows = [{"key": t["taskId"], "data": t, "etag": str(i)} for i, t in enumerate([_task(3), _task(1), _task(2)])]
-    return 200, json.dumps({"results": rows[: q["page"]["limit"]], "token": "3"}).encode()
-
-
-@pytest.mark.parametrize("status", [{"/v1.0-alpha1/state/": _query_page},
-                                    {"/v1.0-alpha1/state/": (500, b'{"errorCode":"ERR_STATE_QUERY"}')}],
-                         ids=["ok", "query-fails"])
-def test_overdue_page_native_equals_python(tmp_path, monkeypatch, status):
-    tp = [("traceparent", UNSAMPLED)]
-    reqs = [(tp, b"", ""), (tp, b"", "?limit=2"), (tp, b"", "?limit=abc"), (tp, b"", "?limit=0"), (tp, b"", "?limit=%32")]
-    got = {n: _scenario(tmp_path, monkeypatch, "overdue", n, status, reqs) for n in (True, False)}
-    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
-    assert [(s, ct, more, b if s == 200 else None) for s, _, ct, b, more in rn] == \
-        [(s, ct, more, b if s == 200 else None) for s, _, ct, b, more in rp]
-    assert [(m, t, json.loads(b)) for m, t, h, b in cn] == [(m, t, json.loads(b)) for m, t, h, b in cp]
-    assert ln == lp and mn == mp
-    if "ok" in str(status) or callable(status["/v1.0-alpha1/state/"]):
-        assert [r[0] for r in rn] == [200] * 5 and [r[4] for r in rn] == ["true"] * 5
-        assert json.loads(rn[0][3])[0]["taskName"] == "t1 'q' ✓"  # ordered by TaskCreatedOn
-        assert (pn, pp) == (1, 5)  # only the percent-encoded limit reached the handler
-
-
-def _bulk(completed_ids=()):
-    def ans(req):
-        keys = json.loads(req.body)["keys"]
-        rows = [{"key": k, "data": _task(int(k[-1]), completed=k in completed_ids), "etag": "e" + k[-1]} for k in keys]
-        return 200, json.dumps(rows).encode()
-    return ans
-
-
-def _saves(*statuses):
-    seq = list(statuses)
-
-    def ans(req):
-        st = seq.pop(0) if len(seq) > 1 else seq[0]
-        return st, b"" if st < 300 else b'{"errorCode":"ERR_STATE_SAVE"}'
-    return ans
-
-
-@pytest.mark.parametrize("case", ["ok", "retry-then-ok", "always-conflict", "bulkget-fails"])
-def test_mark_overdue_native_equals_python(tmp_path, monkeypatch, case):
-    body = json.dumps([_task(1), _task(2), _task(3), _task(1)]).encode()
-    hdr = [("traceparent", UNSAMPLED), ("Content-Type", "application/json")]
-    def status():  # fresh per run: the save answers are a sequence
-        done = ("00000000-0000-4000-8000-000000000002",)
-        return {"ok": {"/v1.0/state/statestore/bulk": _bulk(done), "/v1.0/state/statestore": _saves(204)},
-                "retry-then-ok": {"/v1.0/state/statestore/bulk": _bulk(), "/v1.0/state/statestore": _saves(409, 204)},
-                "always-conflict": {"/v1.0/state/statestore/bulk": _bulk(), "/v1.0/state/statestore": _saves(412)},
-                "bulkget-fails": {"/v1.0/state/statestore/bulk": (500, b'{"errorCode":"ERR_BULK"}')}}[case]
-    got = {n: _scenario(tmp_path, monkeypatch, "mark", n, status(), [(hdr, body)]) for n in (True, False)}
-    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
-    assert [r[0] for r in rn] == [r[0] for r in rp] == [{"ok": 200, "retry-then-ok": 200}.get(case, 500)]
-    assert [(m, t, json.loads(b)) for m, t, h, b in cn] == [(m, t, json.loads(b)) for m, t, h, b in cp]
-    assert ln == lp and mn == mp
-    if case == "ok":
-        save = json.loads(cn[-1][3])
-        assert [x["key"] for x in save] == ["00000000-0000-4000-8000-000000000001", "00000000-0000-4000-8000-000000000003"]
-        assert all(x["etag"] and x["options"]["concurrency"] == "first-write" and x["value"]["isOverDue"] for x in save)
-        assert pn == 0 and pp == 1
