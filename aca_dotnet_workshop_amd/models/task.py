@@ -257,3 +257,23 @@ def tasks_from_json(data: Any) -> list[TaskModel]:
     if isinstance(data, (bytes, bytearray, str)):
         data = json.loads(data) if data else []
     return [TaskModel.model_validate(d) for d in (data or [])]
+
+
+def json_array_chunks(body: bytes, n: int) -> list[bytes] | None:
+    """A JSON array's items re-grouped into arrays of at most ``n`` (raw slices: the items'
+    bytes are not re-encoded), or None when ``body`` is not a valid JSON array."""
+    try:
+        from ..native import load
+        fn = load().json_array_chunks
+    except Exception:
+        fn = None
+    if fn is not None:
+        return fn(body, n)
+    try:
+        items = json.loads(body)
+    except ValueError:
+        return None
+    if not isinstance(items, list) or n < 1:
+        return None
+    return [json.dumps(items[i:i + n], separators=(",", ":"), ensure_ascii=False).encode()
+            for i in range(0, len(items), n)]

@@ -397,6 +397,45 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(count, py::bytes(out), more);
   }, py::arg("body"), py::arg("by_created") = false);
 
+  // A JSON array -> its items re-grouped into arrays of at most `n` items (raw slices, no
+  // re-encoding), or None when the text is not a valid JSON array (the processor's chunked
+  // markoverdue, services/processor/app.py).
+  m.def("json_array_chunks", [](py::bytes body, long n) -> py::object {
+    char* pb;
+    Py_ssize_t nb;
+    if (PyBytes_AsStringAndSize(body.ptr(), &pb, &nb) != 0) throw py::error_already_set();
+    std::string_view s(pb, (size_t)nb);
+    if (n < 1 || !tt::valid(s)) return py::none();
+    const char* p = tt::ws_end(s.data(), s.data() + s.size());
+    const char* e = s.data() + s.size();
+    if (p >= e || *p != '[') return py::none();
+    ++p;
+    py::list out;
+    std::string cur = "[";
+    long in_cur = 0;
+    while (true) {
+      p = tt::ws_end(p, e);
+      if (p < e && *p == ']') break;
+      const char* vs = p;
+      p = tt::skip_value(p, e);
+      if (in_cur) cur += ',';
+      cur.append(vs, (size_t)(p - vs));
+      if (++in_cur == n) {
+        cur += ']';
+        out.append(py::bytes(cur));
+        cur = "[";
+        in_cur = 0;
+      }
+      p = tt::ws_end(p, e);
+      if (p < e && *p == ',') ++p;
+    }
+    if (in_cur) {
+      cur += ']';
+      out.append(py::bytes(cur));
+    }
+    return out;
+  });
+
   // TaskModel JSON -> taskName when it binds within the codec's envelope, else None.
   m.def("task_model_name", [](py::bytes body) -> py::object {
     char* p;

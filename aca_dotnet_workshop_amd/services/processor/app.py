@@ -24,6 +24,8 @@ Endpoints (reference SURVEY.md §2.2, §2.11):
   ``OverdueTasks:PageSize`` > 0 it sweeps page by page (``GET /api/overduetasks?limit=``)
   until a short page: the API's ``OverdueTasks:Query=range`` mode answers with every open
   task due before today, filtered in the store (GPU columnar scan in the backing services).
+  ``OverdueTasks:MarkChunk`` (default 256; 0 = the reference's one call) marks a page in
+  concurrent calls of at most that many tasks.
 * ``GET /dapr/subscribe`` -- ``MapSubscribeHandler`` (reference Program.cs:33).
 """
 from __future__ import annotations
@@ -33,7 +35,7 @@ import logging
 import uuid
 from pathlib import Path
 
-from ...models import TaskModel, naive_utc, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
+from ...models import TaskModel, json_array_chunks, naive_utc, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
 from ...sdk.client import InvocationError, RawJsonBytes, client_from_config
 from ...web.app import WebApp, read_model
@@ -147,6 +149,10 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
         # -- a marked page drops out of the API's filter, so each request asks for the next one
         page = cfg.get_int("OverdueTasks:PageSize", 0)
         max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
+        # OverdueTasks:MarkChunk > 0: a page's overdue list goes to markoverdue in concurrent
+        # calls of at most this many tasks (disjoint: the same end state as one call, which is
+        # what the reference makes -- 0), so the API's replicas and their sidecars share the work
+        chunk = cfg.get_int("OverdueTasks:MarkChunk", 256)
         retrieved = marked = pages = empty_more = 0
         run_day = naive_utc(run_at).date().isoformat()
         t_query = t_mark = 0.0  # wall time of the job's two hops (returned for attribution)
@@ -172,9 +178,19 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                            n_page)
             if n_overdue:
                 log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", n_overdue)
-                data = RawJsonBytes(overdue) if isinstance(overdue, bytes) else overdue
+                parts = json_array_chunks(overdue, chunk) if isinstance(overdue, bytes) and 0 < chunk < n_overdue \
+                    else None
                 t0 = clock()
-                await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
+                if parts and len(parts) > 1:
+                    results = await asyncio.gather(*(client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue",
+                                                                          RawJsonBytes(p)) for p in parts),
+                                                   return_exceptions=True)
+                    for res in results:  # every call has finished: the first failure fails the job
+                        if isinstance(res, BaseException):
+                            raise res
+                else:
+                    data = RawJsonBytes(overdue) if isinstance(overdue, bytes) else overdue
+                    await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
                 t_mark += clock() - t0
                 marked += n_overdue
             if page <= 0:

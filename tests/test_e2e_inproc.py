@@ -285,13 +285,13 @@ def _task_doc(i, due, done=False, overdue=False):
         % (tid, i, i % 97, due, "true" if done else "false", "true" if overdue else "false"))
 
 
-async def _range_sweep_env(monkeypatch, accel, page):
+async def _range_sweep_env(monkeypatch, accel, page, processor=None):
     monkeypatch.setenv("TT_QUERY_ACCEL", accel)
     monkeypatch.setenv("TT_QUERY_ACCEL_MIN_DOCS", "50")
     env = InProcessEnvironment(extra_components=[_fast_cron()])
     await env.start_backing()
     for s in tasks_tracker_specs(frontend=False, api={"OverdueTasks:Query": "range"},
-                                 processor={"OverdueTasks:PageSize": page}):
+                                 processor={"OverdueTasks:PageSize": page, **(processor or {})}):
         await env.add_app(s)
     await env.wait_ready()
     return env
@@ -331,6 +331,35 @@ def test_cron_range_sweep_marks_every_past_due_task(monkeypatch):
             assert await c.invoke_method("GET", API, "api/overduetasks?limit=5") == []
             acc = env.backing.accel("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
             assert acc.stats["cpu"] >= 2 and acc.stats["fallback"] == 0
+        finally:
+            await env.stop()
+    run(main())
+
+
+def test_cron_sweep_marks_in_concurrent_chunks(monkeypatch):
+    """OverdueTasks:MarkChunk: a page's overdue list goes to markoverdue in concurrent calls of at
+    most that many tasks (disjoint), with the same end state as the reference's single call:
+    every open past-due task overdue, nothing else touched."""
+    async def main():
+        env = await _range_sweep_env(monkeypatch, "cpu", 60, {"OverdueTasks:MarkChunk": 7})
+        try:
+            st = env.backing.store("taskstracker-state-store", "tasksmanagerdb", "taskscollection")
+            past = format_fixed(today() - timedelta(days=1))
+            fut = format_fixed(today() + timedelta(days=2))
+            want = set()
+            for i in range(150):
+                k, v = _task_doc(i, past if i % 5 else fut, done=i % 11 == 3)
+                st.set(k, v)
+                if i % 5 and i % 11 != 3:
+                    want.add(k.split("||")[1])
+
+            async def swept():
+                res = json.loads(st.query(json.dumps({"filter": {"EQ": {"isOverDue": True}}})))["results"]
+                out = {r["data"]["taskId"] for r in res}
+                return out if out == want else None
+            await _until(swept, timeout=15)
+            res = json.loads(st.query(json.dumps({"filter": {"EQ": {"isCompleted": True}}})))["results"]
+            assert all(not r["data"]["isOverDue"] for r in res)
         finally:
             await env.stop()
     run(main())

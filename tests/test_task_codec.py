@@ -321,3 +321,19 @@ def test_query_results_ordered_by_created_datetime():
 def test_query_results_decline(body):
     from aca_dotnet_workshop_amd.models import tasks_from_query_wire
     assert tasks_from_query_wire(body) is None
+
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.recursive(st.none() | st.booleans() | st.integers() | st.text(max_size=8),
+                             lambda ch: st.lists(ch, max_size=3) | st.dictionaries(st.text(max_size=4), ch, max_size=3),
+                             max_leaves=6), max_size=30), st.integers(1, 9), st.booleans())
+def test_json_array_chunks_regroups_the_items(items, n, spaced):
+    """models.json_array_chunks (native): the items of a JSON array, in order, in arrays of at most
+    n; each item's text is kept (raw slices), so the chunks parse back to the same items."""
+    from aca_dotnet_workshop_amd.models import json_array_chunks
+    body = json.dumps(items, separators=(", ", ": ") if spaced else (",", ":"), ensure_ascii=False).encode()
+    chunks = json_array_chunks(body, n)
+    parsed = [json.loads(c) for c in chunks]
+    assert all(1 <= len(c) <= n for c in parsed) and sum(parsed, []) == items
+    assert json_array_chunks(b'{"a": 1}', n) is None and json_array_chunks(b"[1,", n) is None
