@@ -28,6 +28,7 @@ so the first scan-shaped query finds the mirror already built (Cosmos "indexing 
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
@@ -59,6 +60,22 @@ def indexable(f: Any) -> bool:
     if op == "OR":
         return bool(arg) and all(indexable(x) for x in arg)
     return False
+
+
+_STALL = {"file": None, "min_s": None}
+
+
+def _stall_note(what: str, secs: float, **phases: float) -> None:
+    """``TT_STALL_LOG`` diagnostics: one JSON line for a query or background sync slower than
+    ``TT_STALL_MS`` (default 100) ms, with its phases -- both hold the collection lock."""
+    if _STALL["min_s"] is None:
+        path = os.environ.get("TT_STALL_LOG")
+        _STALL["file"] = open(path, "a", buffering=1) if path else None
+        _STALL["min_s"] = float(os.environ.get("TT_STALL_MS", "100") or 100) / 1e3
+    if _STALL["file"] is None or secs <= _STALL["min_s"]:
+        return
+    _STALL["file"].write(json.dumps({"what": what, "ms": round(secs * 1e3, 2), **{k: round(v, 2) for k, v in phases.items()},
+                                     "pid": os.getpid(), "wall": round(time.time(), 4)}) + "\n")
 
 
 class CollectionAccelerator:
@@ -119,8 +136,10 @@ class CollectionAccelerator:
                 if self.index is None or self.disabled:
                     return
                 t0 = time.perf_counter()
+                t1 = t0
                 try:
                     self.index.sync()
+                    t1 = time.perf_counter()
                     k = self._kernels
                     if k is not None:
                         self.index.warm(k)
@@ -129,8 +148,11 @@ class CollectionAccelerator:
                     return
                 except Exception:  # a failed warm-up only leaves the work to the next query
                     log.exception("background mirror sync failed")
+                t2 = time.perf_counter()
                 self.stats["bg_syncs"] = self.stats.get("bg_syncs", 0) + 1
-                self.stats["bg_sync_ms"] = round(self.stats.get("bg_sync_ms", 0.0) + (time.perf_counter() - t0) * 1e3, 3)
+                self.stats["bg_sync_ms"] = round(self.stats.get("bg_sync_ms", 0.0) + (t2 - t0) * 1e3, 3)
+                self.stats["bg_sync_max_ms"] = round(max(self.stats.get("bg_sync_max_ms", 0.0), (t2 - t0) * 1e3), 3)
+                _stall_note("mirror-bg-sync", t2 - t0, sync_ms=(t1 - t0) * 1e3, warm_ms=(t2 - t1) * 1e3)
 
     def close(self, timeout: float = 10.0) -> None:
         """Stop the background sync and wait for it: no sync may still be inside the native
@@ -207,6 +229,8 @@ class CollectionAccelerator:
             for key, v in (("lock_wait_ms", t0 - t_wait), ("sync_ms", t1 - t0), ("select_and_results_ms", t2 - t1),
                            ("select_ms", t_sel), ("results_ms", t_res)):
                 self.stats[key] = round(self.stats.get(key, 0.0) + v * 1e3, 3)
+            _stall_note("accel-query", t2 - t_wait, lock_wait_ms=(t0 - t_wait) * 1e3, sync_ms=(t1 - t0) * 1e3,
+                        select_ms=t_sel * 1e3, results_ms=t_res * 1e3)
             for key, v in self.index.timing.items():  # the paged device path's own breakdown
                 self.stats[key] = round(v, 3)
             return out

@@ -139,6 +139,7 @@ class AppHost {
       }
       // diagnostics: loop iterations > 100 ms apart and slow command batches
       ev::GapTracer gaps("apphost");
+      gaps.attach(loop_);
       loop_.run([&gaps](double now) { gaps.tick(now); });
     });
   }

@@ -12,7 +12,10 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <functional>
@@ -152,7 +155,26 @@ class AppLog {
   void sync() { if (fd_ >= 0) ::fdatasync(fd_); }
 
  private:
+  // TT_STALL_LOG=<file> (diagnostics): a write(2) slower than TT_STALL_MS (default 100) ms is
+  // reported as a JSON line -- the caller holds its engine's mutex meanwhile.
+  static FILE* stall_file(double& min_s) {
+    static double th = [] {
+      const char* p = std::getenv("TT_STALL_MS");
+      double ms = p && *p ? std::atof(p) : 100.0;
+      return (ms > 0 ? ms : 100.0) / 1e3;
+    }();
+    static FILE* f = [] {
+      const char* p = std::getenv("TT_STALL_LOG");
+      return p && *p ? std::fopen(p, "a") : nullptr;
+    }();
+    min_s = th;
+    return f;
+  }
+
   void write_all(const std::string& rec) {
+    double min_s;
+    FILE* stall = stall_file(min_s);
+    auto t0 = stall ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
     size_t off = 0;
     while (off < rec.size()) {
       ssize_t w = ::write(fd_, rec.data() + off, rec.size() - off);
@@ -164,6 +186,15 @@ class AppLog {
     }
     bytes_ += rec.size();
     if (fsync_ == 1) ::fdatasync(fd_);
+    if (stall) {
+      double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (s > min_s) {
+        double wall = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+        std::fprintf(stall, "{\"what\": \"log-write\", \"ms\": %.2f, \"bytes\": %zu, \"log\": \"%s\", \"pid\": %d, \"wall\": %.4f}\n",
+                     s * 1e3, rec.size(), path_.c_str(), (int)::getpid(), wall);
+        std::fflush(stall);
+      }
+    }
   }
 
   int fd_ = -1;

@@ -258,6 +258,7 @@ class BackingFront {
     void start() {
       thread = std::thread([this] {
         ev::GapTracer gaps("backing-front");
+        gaps.attach(loop);
         loop.run([this, &gaps](double t) {
           gaps.tick(t);
           on_tick(t);

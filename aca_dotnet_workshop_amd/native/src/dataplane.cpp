@@ -2282,6 +2282,7 @@ int main(int argc, char** argv) {
   }
   double last_flush = ev::now_s();
   ev::GapTracer gaps("dataplane");
+  gaps.attach(loop);
   loop.run([&](double t) {
     gaps.tick(t);
     if (t - last_flush > 1.0) {

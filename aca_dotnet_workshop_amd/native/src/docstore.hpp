@@ -28,6 +28,7 @@
 
 #include "applog.hpp"
 #include "json.hpp"
+#include "shardedmap.hpp"
 
 namespace tt {
 
@@ -166,7 +167,7 @@ inline void mirror_key(const Value& v, std::string& k) {
 // rows and bumps the generation (readers then reload).
 struct MirrorColumn {
   std::string path;
-  std::unordered_map<std::string, int32_t> dict;  // canonical key -> id
+  ShardedMap<int32_t> dict;                       // canonical key -> id
   std::vector<std::string> values;                // JSON text per id, in order of first use
   std::vector<int32_t> ids;                       // per row (-1 = path missing)
 };
@@ -745,6 +746,7 @@ class DocStore {
 
  private:
   using Index = std::unordered_map<std::string, std::unordered_set<std::string>>;
+  using Docs = ShardedMap<Doc>;  // grows a shard at a time: no whole-collection rehash under mu_
 
   static bool expired(const Doc& d, int64_t now) { return d.expire_ms && d.expire_ms <= now; }
 
@@ -752,7 +754,7 @@ class DocStore {
     check_etag_at(docs_.find(key), etag, first_write, now);
   }
 
-  void check_etag_at(std::unordered_map<std::string, Doc>::iterator it, const std::optional<std::string>& etag,
+  void check_etag_at(Docs::iterator it, const std::optional<std::string>& etag,
                      bool first_write, int64_t now) {
     bool exists = it != docs_.end() && !expired(it->second, now);
     if (etag && !etag->empty()) {
@@ -784,7 +786,7 @@ class DocStore {
   // The write itself, at `it` = docs_.find(key) done once by the caller.  Bulk writes pass a
   // `graveyard` that takes the replaced document's parsed tree and text, so their frees run
   // after the store lock is released.
-  std::unordered_map<std::string, Doc>::iterator put_at(std::unordered_map<std::string, Doc>::iterator it,
+  Docs::iterator put_at(Docs::iterator it,
                                                        const std::string& key, std::string&& value, Value parsed,
                                                        int64_t expire_ms, std::vector<Doc>* graveyard) {
     uint64_t e = ++etag_;
@@ -1105,7 +1107,7 @@ class DocStore {
   }
 
   std::mutex mu_;
-  std::unordered_map<std::string, Doc> docs_;
+  Docs docs_;
   std::unordered_map<std::string, Index> indexes_;
   AppLog log_;
   uint64_t etag_ = 0;

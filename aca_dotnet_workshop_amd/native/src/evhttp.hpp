@@ -116,6 +116,7 @@ class Loop {
         timeout_ms = dt <= 0 ? 0 : std::min(50, (int)(dt * 1000.0) + 1);
       }
       int n = epoll_wait(ep_, evs, 256, timeout_ms);
+      const double t_wake = iter_hook_ ? now_s() : 0.0;
       for (int i = 0; i < n; ++i) {
         auto* o = static_cast<IoObj*>(evs[i].data.ptr);
         if (!o->dead) o->on_event(evs[i].events);
@@ -141,8 +142,11 @@ class Loop {
         if (tick) tick(t);
       }
       graveyard_.clear();
+      if (iter_hook_) iter_hook_(t_wake, now_s(), n);
     }
   }
+  // Diagnostics: called after every iteration with (woke, done, events) -- GapTracer::attach.
+  void set_iter_hook(std::function<void(double, double, int)> f) { iter_hook_ = std::move(f); }
 
  private:
   int ep_;
@@ -151,13 +155,25 @@ class Loop {
   std::vector<std::shared_ptr<IoObj>> graveyard_;
   std::vector<std::function<void()>> deferred_;
   std::multimap<double, std::function<void()>> timers_;
+  std::function<void(double, double, int)> iter_hook_;
 };
 
 // Diagnostics: with TT_STALL_LOG=<file>, a loop's tick reports iterations more than 100 ms
-// apart (the thread was blocked or not scheduled) as JSON lines.
+// apart (the thread was blocked or not scheduled) as JSON lines; attached to its loop, it also
+// reports every iteration that stayed busy (handlers, deferred work, timers) longer than
+// TT_STALL_MS (default 100) ms.
+inline double stall_threshold_s() {
+  static const double s = [] {
+    const char* p = std::getenv("TT_STALL_MS");
+    double ms = p && *p ? std::atof(p) : 100.0;
+    return (ms > 0 ? ms : 100.0) / 1e3;
+  }();
+  return s;
+}
+
 class GapTracer {
  public:
-  explicit GapTracer(const char* who) : who_(who) {
+  explicit GapTracer(const char* who) : who_(who), min_busy_(stall_threshold_s()) {
     if (const char* p = std::getenv("TT_STALL_LOG"); p && *p) f_ = std::fopen(p, "a");
   }
   ~GapTracer() {
@@ -171,9 +187,20 @@ class GapTracer {
           std::fflush(f_);
     last_ = now;
   }
+  void attach(Loop& loop) {
+    if (!f_) return;
+    loop.set_iter_hook([this](double woke, double done, int n) {
+      if (done - woke > min_busy_)
+        std::fprintf(f_, "{\"what\": \"loop-busy\", \"who\": \"%s\", \"ms\": %.2f, \"events\": %d, \"pid\": %d, \"wall\": %.4f}\n",
+                     who_, (done - woke) * 1e3, n, (int)::getpid(),
+                     std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count()),
+            std::fflush(f_);
+    });
+  }
 
  private:
   const char* who_;
+  double min_busy_;
   FILE* f_ = nullptr;
   double last_ = 0;
 };

@@ -471,6 +471,7 @@ int main(int argc, char** argv) {
     });
   }
   ev::GapTracer gaps("ingress");
+  gaps.attach(w0.loop());
   w0.loop().run([&](double t) {
     gaps.tick(t);
     if (stopping.load()) w0.loop().stop();

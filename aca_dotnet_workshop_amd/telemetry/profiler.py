@@ -33,10 +33,20 @@ def _install_gc_log(name: str, path: str, threshold_s: float = 0.02) -> None:
             return
         d = time.perf_counter() - start[0]
         if d > threshold_s:
-            out.write(json.dumps({"what": "gc-pause", "proc": name, "pid": os.getpid(), "gen": info["generation"],
-                                  "ms": round(d * 1e3, 2), "collected": info["collected"],
-                                  "objects": len(gc.get_objects(info["generation"])) if info["generation"] < 2 else None,
+            gen = info["generation"]
+            objs = gc.get_objects(gen)
+            top = None
+            if gen == 2:  # what the full collection had to scan: the survivors' commonest types
+                counts: dict[str, int] = {}
+                for o in objs:
+                    t = type(o).__name__
+                    counts[t] = counts.get(t, 0) + 1
+                top = sorted(counts.items(), key=lambda kv: -kv[1])[:10]
+            out.write(json.dumps({"what": "gc-pause", "proc": name, "pid": os.getpid(), "gen": gen,
+                                  "ms": round(d * 1e3, 2), "collected": info["collected"], "objects": len(objs),
+                                  "frozen": gc.get_freeze_count(), "top": top,
                                   "wall": round(time.time(), 4)}) + "\n")
+            del objs
     gc.callbacks.append(cb)
 
 

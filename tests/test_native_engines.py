@@ -108,6 +108,27 @@ def test_secondary_index_used_and_maintained():
     assert [x["data"]["i"] for x in r["results"]] == [i for i in range(3, 100, 10) if i not in (3, 13)]
 
 
+def test_growth_keeps_lookups_order_and_counts():
+    """The document map grows a shard at a time (native/src/shardedmap.hpp): across many growth
+    steps every key stays reachable, deletes and updates are exact, ``len`` counts the live
+    documents, and an unsorted query still answers in insertion order."""
+    s = N.DocStore("", 0, 1 << 30)  # no secondary index: the scan path walks the whole map
+    n = 20000
+    keys = [f"app||{(i * 7919) % 100003:06d}-{i}" for i in range(n)]
+    for i, k in enumerate(keys):
+        s.set(k, json.dumps({"i": i}))
+    assert len(s) == n
+    for k in keys[::3]:
+        assert s.delete(k) is True
+    s.set(keys[1], json.dumps({"i": 1, "updated": True}))
+    live = [i for i in range(n) if i % 3]
+    assert len(s) == len(live)
+    assert s.get(keys[0]) is None and json.loads(s.get(keys[1])[0])["updated"] is True
+    assert all(json.loads(s.get(keys[i])[0])["i"] == i for i in live[::97])
+    r = json.loads(s.query(json.dumps({"filter": {"GT": {"i": -1}}}), "app||"))
+    assert [x["data"]["i"] for x in r["results"]] == live
+
+
 def test_persistence_and_compaction(tmp_path):
     p = str(tmp_path / "state.log")
     s = N.DocStore(p)
