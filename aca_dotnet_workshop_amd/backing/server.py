@@ -755,7 +755,9 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         # hot routes on the native front (own thread, GIL-free); Python serves the rest privately
         priv_dir = tempfile.mkdtemp(prefix="ttbf-")
         await srv.listen_unix(os.path.join(priv_dir, "py.sock"))
-        threads = int(os.environ.get("TT_BACKING_FRONT_THREADS", "2"))
+        # 4 shards: with 2, the front's loops were the stack's busiest threads (72-78 %) under the
+        # headline, and 4 measured +8 % tasks/s (profiles/r4_hot_threads.md)
+        threads = int(os.environ.get("TT_BACKING_FRONT_THREADS", "4"))
         front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"), threads)
         svc.attach_front(front)
         bound = front.port()

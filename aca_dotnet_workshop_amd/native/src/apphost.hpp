@@ -133,6 +133,7 @@ class AppHost {
     if (thread_.joinable()) return;
     if (const char* p = std::getenv("TT_STALL_LOG"); p && *p) trace_ = std::fopen(p, "a");
     thread_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "tt-apphost-io");  // per-thread CPU reports
       if (!trace_) {
         loop_.run();
         return;

@@ -257,6 +257,7 @@ class BackingFront {
     }
     void start() {
       thread = std::thread([this] {
+        pthread_setname_np(pthread_self(), "tt-front");  // per-thread CPU reports (bench hot_threads)
         ev::GapTracer gaps("backing-front");
         gaps.attach(loop);
         loop.run([this, &gaps](double t) {

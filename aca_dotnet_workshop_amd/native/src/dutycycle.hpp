@@ -70,7 +70,10 @@ class DutyCycle {
 
   void start() {
     if (running_.exchange(true)) return;
-    th_ = std::thread([this] { run(); });
+    th_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "tt-dutycycle");
+      run();
+    });
   }
 
   void stop() {

@@ -283,6 +283,49 @@ class LocalStack:
                 out[f"{r.name}.app"] = sum(cpu(k.pid) for k in kids if k not in dp)
         return out
 
+    def thread_cpu(self, extra: dict[str, int] | None = None) -> dict[tuple[str, str, int], float]:
+        """CPU seconds so far of every thread of the stack's processes (plus ``extra``: role ->
+        pid), keyed by (role, thread name, tid): which single thread saturates first under load
+        (an event loop at 100 % caps throughput while the process as a whole looks idle)."""
+        import psutil
+        tick = os.sysconf("SC_CLK_TCK")
+        procs: dict[str, list[int]] = {}
+        if self.backing_proc is not None:
+            procs["backing"] = [self.backing_proc.pid]
+        for fam, (p, _url) in self.extra_backing.items():
+            procs.setdefault(f"backing-{fam.lower()}", []).append(p.pid)
+        for rs in self.replicas.values():
+            for r in rs:
+                procs[f"{r.name}.sidecar"] = [r.proc.pid]
+                try:
+                    kids = psutil.Process(r.proc.pid).children(recursive=True)
+                except psutil.Error:
+                    kids = []
+                dp = [k for k in kids if _is_dataplane(k)]
+                procs[f"{r.name}.dataplane"] = [k.pid for k in dp]
+                procs[f"{r.name}.app"] = [k.pid for k in kids if k not in dp]
+        for role, pid in (extra or {}).items():
+            procs.setdefault(role, []).append(pid)
+        out: dict[tuple[str, str, int], float] = {}
+        for role, pids in procs.items():
+            for pid in pids:
+                try:
+                    tids = os.listdir(f"/proc/{pid}/task")
+                except OSError:
+                    continue
+                for t in tids:
+                    try:
+                        with open(f"/proc/{pid}/task/{t}/stat", "rb") as f:
+                            raw = f.read()
+                    except OSError:
+                        continue
+                    lp, rp = raw.find(b"("), raw.rfind(b")")
+                    fields = raw[rp + 2:].split()
+                    # fields[11], [12] = utime, stime (stat fields 14 and 15) in clock ticks
+                    out[(role, raw[lp + 1:rp].decode(errors="replace"), int(t))] = \
+                        (int(fields[11]) + int(fields[12])) / tick
+        return out
+
     def stop_replica(self, r: ReplicaProc, timeout: float = 10.0) -> None:
         _terminate(r.proc, timeout)
         if r in self.replicas.get(r.app_id, []):

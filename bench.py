@@ -400,7 +400,7 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
     sweep = a.overdue_sweep_ms > 0
     if sweep:
         api_cfg["OverdueTasks:Query"] = "range"
-        proc_cfg["OverdueTasks:PageSize"] = "1000"
+        proc_cfg["OverdueTasks:PageSize"] = str(OVERDUE_PAGE)
     import tempfile
     root = tempfile.mkdtemp(prefix="tt-bench-")
     env = {"TT_TRACE_SAMPLE_RATE": os.environ.get("TT_TRACE_SAMPLE_RATE", "0.01"),
@@ -502,6 +502,7 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
         if sweeper is not None:
             acc = _accel_stats(shards if shared else [doc_backing])
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
+                          "page_size": OVERDUE_PAGE,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
                           "shards": len(shards)}
@@ -648,6 +649,12 @@ def _cpu_by_role(stack) -> dict[str, float]:
     return out
 
 
+# the sweep's page (OverdueTasks:PageSize): the reference reads every match in one query
+# (ScheduledTasksManagerController.cs:28); a page covers a second's ~1,000 overdue tasks at the
+# headline's create rate with room to spare, and stays within the device top-k (kPageCap 8192).
+# At 1000 a faster box crossed into two pages per sweep and doubled it (profiles/r4_sweep_tail.md)
+OVERDUE_PAGE = 4096
+
 # cores held back for the external ingress when load enters through it (uncapped, like Envoy)
 INGRESS_RESERVE = 1.0
 
@@ -665,6 +672,21 @@ def _ingress_cpu(env) -> dict[str, float]:
         return {"ingress": t.user + t.system}
     except psutil.Error:
         return {}
+
+
+def _ingress_pid(env) -> dict[str, int]:
+    rt = env.ctl.apps.get(FRONTEND)
+    proc = getattr(getattr(rt, "ingress", None), "proc", None)
+    return {"ingress": proc.pid} if proc is not None else {}
+
+
+def hot_threads(before: dict, after: dict, dt: float, top: int = 12) -> list:
+    """The busiest threads of the timed region, [role, thread name, cores busy]: the single
+    thread that saturates first bounds the throughput of a latency-bound closed loop."""
+    if dt <= 0:
+        return []
+    busy = sorted(((v - before.get(k, 0.0)) / dt, k) for k, v in after.items())
+    return [[k[0], k[1], round(c, 3)] for c, k in reversed(busy[-top:])]
 
 
 def _throttling(before: dict, after: dict, dt: float) -> dict | None:
@@ -860,7 +882,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                  "enforceCpuLimits": bool(a.cpu_limits), "appCpu": app_cpu, "frontendCpu": caps["frontend"],
                  "backendApiCpu": caps["api"], "processorCpu": caps["processor"], "appMemory": "2Gi",
                  "appInsightsSamplingPercentage": a.trace_sampling,
-                 "overdueQuery": "range" if sweep else "equality", "overduePageSize": 1000 if sweep else 0,
+                 "overdueQuery": "range" if sweep else "equality", "overduePageSize": OVERDUE_PAGE if sweep else 0,
                  "environmentName": f"cae-bench-r{d.rank}"}
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
                       overrides)
@@ -913,6 +935,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu0.update(_ingress_cpu(env))
+        th0 = env.stack.thread_cpu(_ingress_pid(env))
         duty0 = env.ctl.limiter.duty_stats()
         ru0 = _collection_stats(backing).get("throughput", {})
         acc0 = _accel_stats(shards) if sweeper is not None else {}
@@ -929,6 +952,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
+        hot = hot_threads(th0, env.stack.thread_cpu(_ingress_pid(env)), dt)
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
@@ -939,6 +963,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             acc = {k: (round(v - acc0.get(k, 0), 3) if isinstance(v, (int, float)) and k != "rows" else v)
                    for k, v in acc1.items()}
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
+                          "page_size": OVERDUE_PAGE,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
                           "shards": len(shards),
@@ -1014,6 +1039,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                        "loops, certificate verified against the environment CA"
                                        if ingress else "bypassed: the load generator balances over the frontend replicas"),
                            "cpu_us_per_task": cpu_us,
+                           "hot_threads": hot,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
                                           "mechanism": lim.get("cpu"), "mode": lim.get("mode"),
