@@ -52,9 +52,14 @@ def _stale(target: Path, sources: list[Path]) -> bool:
     return any(s.exists() and s.stat().st_mtime > t for s in sources)
 
 
+EXE_ONLY_HEADERS = {"pcsample.hpp"}
+
+
 def build_native(force: bool = False, verbose: bool = False) -> Path:
     target = ext_path("_ttnative")
-    sources = sorted(SRC.glob("*.hpp")) + [SRC / "module.cpp"]
+    # every header but the executables-only ones (pcsample.hpp: the data plane's and ingress's
+    # self-profiler) -- a change there must not make the extension look stale
+    sources = sorted(h for h in SRC.glob("*.hpp") if h.name not in EXE_ONLY_HEADERS) + [SRC / "module.cpp"]
     if not force and not _stale(target, sources):
         return target
     with build_lock("ttnative"):
@@ -81,7 +86,7 @@ DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
 
 def build_dataplane(force: bool = False, verbose: bool = False) -> Path:
     sources = [SRC / "dataplane.cpp", SRC / "evhttp.hpp", SRC / "h2.hpp", SRC / "pb.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
-               SRC / "textutil.hpp"]
+               SRC / "textutil.hpp", SRC / "pcsample.hpp"]
     return _build_exe(DATAPLANE, SRC / "dataplane.cpp", sources, force, verbose)
 
 
@@ -94,8 +99,9 @@ def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbo
             return target
         cxx = os.environ.get("CXX", "g++")
         tmp = target.with_name(f".{target.name}.tmp{os.getpid()}")
-        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", str(main), "-o", str(tmp), "-lssl",
-               "-lcrypto"] + (["-pthread"] if threads else [])
+        # -rdynamic: the executables' own functions resolve in TT_PC_SAMPLE profiles (pcsample.hpp)
+        cmd = [cxx, "-O2", "-std=c++17", "-Wall", "-Wno-unused-function", "-rdynamic", str(main), "-o", str(tmp),
+               "-lssl", "-lcrypto"] + (["-pthread"] if threads else [])
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
@@ -109,7 +115,7 @@ INGRESS = HERE / "bin" / "ttingress"
 def build_ingress(force: bool = False, verbose: bool = False) -> Path:
     """The environment's native HTTP(S) ingress (src/ingress.cpp), spawned by platform/ingress.py."""
     sources = [SRC / "ingress.cpp", SRC / "evhttp.hpp", SRC / "tls.hpp", SRC / "json.hpp", SRC / "httpparse.hpp",
-               SRC / "textutil.hpp"]
+               SRC / "textutil.hpp", SRC / "pcsample.hpp"]
     return _build_exe(INGRESS, SRC / "ingress.cpp", sources, force, verbose, threads=True)
 
 

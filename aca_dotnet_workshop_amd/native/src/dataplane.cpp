@@ -39,6 +39,7 @@
 #include "h2.hpp"
 #include "json.hpp"
 #include "pb.hpp"
+#include "pcsample.hpp"
 #include "textutil.hpp"
 
 using namespace tt;
@@ -2218,6 +2219,7 @@ int main(int argc, char** argv) {
   }
   prctl(PR_SET_PDEATHSIG, SIGTERM);  // the Python control plane owns our lifetime
   signal(SIGPIPE, SIG_IGN);
+  pcsample::start();  // TT_PC_SAMPLE diagnostics
   std::ifstream in(argv[1]);
   std::stringstream ss;
   ss << in.rdbuf();
@@ -2293,5 +2295,6 @@ int main(int argc, char** argv) {
     if (stopping && (dp.drained() || t > stop_deadline)) loop.stop();
   });
   dp.flush();
+  pcsample::dump("dataplane");
   return 0;
 }

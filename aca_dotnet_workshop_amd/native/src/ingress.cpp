@@ -45,6 +45,7 @@
 
 #include "evhttp.hpp"
 #include "json.hpp"
+#include "pcsample.hpp"
 #include "textutil.hpp"
 
 using namespace tt;
@@ -388,6 +389,7 @@ const std::string* opt_str(const Value& cfg, const char* k) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  pcsample::start();  // TT_PC_SAMPLE diagnostics
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s <config.json>\n", argv[0]);
     return 2;
@@ -477,5 +479,6 @@ int main(int argc, char** argv) {
     if (stopping.load()) w0.loop().stop();
   });
   for (auto& t : threads) t.join();
+  pcsample::dump("ingress");
   return 0;
 }

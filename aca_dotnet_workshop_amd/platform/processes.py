@@ -283,10 +283,11 @@ class LocalStack:
                 out[f"{r.name}.app"] = sum(cpu(k.pid) for k in kids if k not in dp)
         return out
 
-    def thread_cpu(self, extra: dict[str, int] | None = None) -> dict[tuple[str, str, int], float]:
-        """CPU seconds so far of every thread of the stack's processes (plus ``extra``: role ->
-        pid), keyed by (role, thread name, tid): which single thread saturates first under load
-        (an event loop at 100 % caps throughput while the process as a whole looks idle)."""
+    def thread_cpu(self, extra: dict[str, int] | None = None) -> dict[tuple[str, str, int], tuple[float, float]]:
+        """(user, kernel) CPU seconds so far of every thread of the stack's processes (plus
+        ``extra``: role -> pid), keyed by (role, thread name, tid): which single thread saturates
+        first under load (an event loop at 100 % caps throughput while the process as a whole
+        looks idle), and how much of it is system calls."""
         import psutil
         tick = os.sysconf("SC_CLK_TCK")
         procs: dict[str, list[int]] = {}
@@ -323,7 +324,7 @@ class LocalStack:
                     fields = raw[rp + 2:].split()
                     # fields[11], [12] = utime, stime (stat fields 14 and 15) in clock ticks
                     out[(role, raw[lp + 1:rp].decode(errors="replace"), int(t))] = \
-                        (int(fields[11]) + int(fields[12])) / tick
+                        (int(fields[11]) / tick, int(fields[12]) / tick)
         return out
 
     def stop_replica(self, r: ReplicaProc, timeout: float = 10.0) -> None:

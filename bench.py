@@ -681,12 +681,18 @@ def _ingress_pid(env) -> dict[str, int]:
 
 
 def hot_threads(before: dict, after: dict, dt: float, top: int = 12) -> list:
-    """The busiest threads of the timed region, [role, thread name, cores busy]: the single
-    thread that saturates first bounds the throughput of a latency-bound closed loop."""
+    """The busiest threads of the timed region, [role, thread name, cores busy, kernel-mode
+    share]: the single thread that saturates first bounds the throughput of a latency-bound
+    closed loop; the kernel share says whether it is system calls or its own code."""
     if dt <= 0:
         return []
-    busy = sorted(((v - before.get(k, 0.0)) / dt, k) for k, v in after.items())
-    return [[k[0], k[1], round(c, 3)] for c, k in reversed(busy[-top:])]
+    rows = []
+    for k, (u, s) in after.items():
+        u0, s0 = before.get(k, (0.0, 0.0))
+        du, ds = u - u0, s - s0
+        rows.append(((du + ds) / dt, ds / (du + ds) if du + ds > 0 else 0.0, k))
+    rows.sort(key=lambda r: r[0])
+    return [[k[0], k[1], round(c, 3), round(ks, 2)] for c, ks, k in reversed(rows[-top:])]
 
 
 def _throttling(before: dict, after: dict, dt: float) -> dict | None:

@@ -47,6 +47,12 @@ def test_bench_single_process():
     assert cpu["total"] > 0 and cpu["by_role"]["ingress"] > 0 and cpu["apps_frontend_plus_api"] > 0
     sw = cfg["overdue_sweeps"]
     assert len(sw["sweep_ms"]) == sw["sweeps"] and max(sw["sweep_ms"], default=0) == (sw["sweep_max_ms"] or 0)
+    assert sw["page_size"] == 4096
+    # the busiest threads of the timed region: [role, thread name, cores, kernel share], busiest
+    # first
+    hot = cfg["hot_threads"]
+    assert hot and all(len(h) == 4 and h[2] >= 0 and 0 <= h[3] <= 1 for h in hot)
+    assert [h[2] for h in hot] == sorted((h[2] for h in hot), reverse=True)
     # the secondary run inside the reference's envelope: 1/1 replicas, 0.25 vCPU, 4000 RU/s, the
     # create's redirect followed to the task list
     ev = cfg["reference_envelope"]
@@ -54,6 +60,38 @@ def test_bench_single_process():
     assert ev["lists_followed"] == ev["tasks"] and ev["list_latency_ms"]["p50"] > 0
     assert ev["failed_creates"] + ev["failed_lists"] == ev["errors"]
     assert ev["processor_replicas_reached"] >= 1 and ev["ru_per_task"] > 5
+
+
+def test_thread_cpu_and_hot_threads():
+    """ProcessStack.thread_cpu reads every thread of the given processes; hot_threads ranks the
+    deltas by cores busy."""
+    import threading
+    import time
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from aca_dotnet_workshop_amd.platform.processes import LocalStack
+    stack = LocalStack()
+    stop = threading.Event()
+
+    def spin():
+        while not stop.is_set():
+            sum(range(1000))
+    t = threading.Thread(target=spin, name="spinner")
+    t.start()
+    try:
+        before = stack.thread_cpu({"self": os.getpid()})
+        t0 = time.perf_counter()
+        time.sleep(0.5)
+        after = stack.thread_cpu({"self": os.getpid()})
+        dt = time.perf_counter() - t0
+    finally:
+        stop.set()
+        t.join()
+    assert {k[0] for k in after} == {"self"} and len(after) >= 2
+    hot = bench.hot_threads(before, after, dt, top=3)
+    assert hot[0][0] == "self" and hot[0][2] > 0.3 and hot[0][3] < 0.5  # the spinner: user mode
+    assert bench.hot_threads({("a", "x", 1): (1.0, 0.0)}, {("a", "x", 1): (1.5, 0.5), ("b", "y", 2): (0.0, 0.5)},
+                             2.0) == [["a", "x", 0.5, 0.5], ["b", "y", 0.25, 1.0]]
 
 
 def test_bench_api_sidecar_entry_single_process():
