@@ -529,3 +529,23 @@ def test_sidecar_mutual_tls(plane, tmp_path):
             with pytest.raises(ssl.SSLError):
                 await raw(bad)
     run(main())
+
+
+def test_native_pc_sample_profile(tmp_path, monkeypatch):
+    """TT_PC_SAMPLE (native/src/pcsample.hpp): the native data plane samples its own program
+    counter and, when it stops, writes a flat profile by module and symbol to <file>.<pid>."""
+    prof = tmp_path / "prof"
+    monkeypatch.setenv("TT_PC_SAMPLE", str(prof))
+
+    async def main():
+        async with Env("native", tmp_path) as e:
+            st = f"{e.base['app-a']}/v1.0/state/statestore"
+            for i in range(300):
+                assert (await e.http.post(st, json_body=[{"key": f"k{i}", "value": {"i": i}}])).status == 204
+            return e.sidecars["app-a"]._dp_proc.pid
+    pid = run(main())
+    text = (tmp_path / f"prof.{pid}").read_text()
+    assert text.startswith(f"== dataplane pid {pid}: ")
+    n = int(re.match(r"== dataplane pid \d+: (\d+) samples", text).group(1))
+    assert "-- by module" in text and "-- by symbol" in text
+    assert n == 0 or "%" in text.split("-- by module", 1)[1]
