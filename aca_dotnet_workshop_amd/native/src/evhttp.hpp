@@ -177,6 +177,7 @@ class GapTracer {
     if (const char* p = std::getenv("TT_STALL_LOG"); p && *p) f_ = std::fopen(p, "a");
   }
   ~GapTracer() {
+    if (hooked_) hooked_->set_iter_hook(nullptr);  // the loop may outlive this tracer
     if (f_) std::fclose(f_);
   }
   void tick(double now) {
@@ -189,6 +190,7 @@ class GapTracer {
   }
   void attach(Loop& loop) {
     if (!f_) return;
+    hooked_ = &loop;
     loop.set_iter_hook([this](double woke, double done, int n) {
       if (done - woke > min_busy_)
         std::fprintf(f_, "{\"what\": \"loop-busy\", \"who\": \"%s\", \"ms\": %.2f, \"events\": %d, \"pid\": %d, \"wall\": %.4f}\n",
@@ -201,6 +203,7 @@ class GapTracer {
  private:
   const char* who_;
   double min_busy_;
+  Loop* hooked_ = nullptr;
   FILE* f_ = nullptr;
   double last_ = 0;
 };

@@ -36,3 +36,27 @@ def test_gc_log_reports_full_collections_with_survivor_types(tmp_path):
     assert full and full[-1]["proc"] == "unit" and full[-1]["objects"] >= len(keep)
     assert isinstance(full[-1]["top"], list) and any(t == "dict" for t, _ in full[-1]["top"])
     assert "frozen" in full[-1]
+
+
+def test_native_loop_busy_notes(tmp_path, monkeypatch):
+    """A native event loop attached to its GapTracer reports iterations busier than TT_STALL_MS
+    (here 1 µs: every iteration that handled a request) as loop-busy lines."""
+    import asyncio
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).parent))
+    from test_dataplane import Env
+    from helpers import run
+    log = tmp_path / "stall.jsonl"
+    monkeypatch.setenv("TT_STALL_LOG", str(log))
+    monkeypatch.setenv("TT_STALL_MS", "0.001")
+
+    async def main():
+        async with Env("native", tmp_path) as e:
+            st = f"{e.base['app-a']}/v1.0/state/statestore"
+            for i in range(20):
+                assert (await e.http.post(st, json_body=[{"key": f"k{i}", "value": i}])).status == 204
+            await asyncio.sleep(0.05)
+    run(main())
+    rows = [json.loads(x) for x in log.read_text().splitlines() if '"loop-busy"' in x]
+    assert rows and all(r["who"] == "dataplane" and r["ms"] > 0 and r["events"] >= 0 for r in rows)
