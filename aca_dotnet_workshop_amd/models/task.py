@@ -249,6 +249,25 @@ def overdue_filter_wire(body: bytes, run_day: str) -> tuple[int, int, bytes] | N
     return fns[1](body, run_day) if fns else None
 
 
+def overdue_filter_chunks(body: bytes, run_day: str, chunk: int) -> tuple[int, int, list[bytes]] | None:
+    """``overdue_filter_wire`` with the kept tasks cut into TaskModel JSON arrays of at most
+    ``chunk`` tasks (the processor's concurrent markoverdue calls), in one native pass;
+    ``None``: as for ``overdue_filter_wire``."""
+    try:
+        from ..native import load
+        fn = load().tasks_overdue_filter_chunks
+    except Exception:
+        fn = None
+    if fn is not None and chunk > 0:
+        return fn(body, run_day, chunk)
+    got = overdue_filter_wire(body, run_day)
+    if got is None or chunk <= 0:
+        return None
+    n_page, n_kept, kept = got
+    parts = json_array_chunks(kept, chunk) if n_kept else []
+    return None if parts is None else (n_page, n_kept, parts)
+
+
 def tasks_to_json(tasks: list[TaskModel]) -> bytes:
     return ("[" + ",".join(t.to_json() for t in tasks) + "]").encode()
 

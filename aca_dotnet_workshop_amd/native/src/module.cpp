@@ -367,6 +367,33 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(retrieved, kept, py::bytes(out));
   });
 
+  // overdue page + run date + chunk size -> (retrieved, kept, [TaskModel JSON arrays of at most
+  // `chunk` tasks each]) or None: the filter and the processor's markoverdue chunks in one pass.
+  m.def("tasks_overdue_filter_chunks", [](py::bytes body, const std::string& run_day, size_t chunk) -> py::object {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    if (chunk == 0) return py::none();
+    size_t retrieved = 0, kept = 0;
+    std::string out;
+    std::vector<size_t> starts;
+    if (!taskcodec::overdue_filter(std::string_view(p, (size_t)n), run_day, retrieved, kept, out, &starts))
+      return py::none();
+    py::list parts;
+    const size_t body_end = out.size() - 1;  // the closing ']'
+    for (size_t a = 0; a < starts.size(); a += chunk) {
+      const size_t b = std::min(starts.size(), a + chunk);
+      const size_t from = starts[a], to = b < starts.size() ? starts[b] - 1 : body_end;  // drop the ','
+      std::string part;
+      part.reserve(to - from + 2);
+      part += '[';
+      part.append(out, from, to - from);
+      part += ']';
+      parts.append(py::bytes(part));
+    }
+    return py::make_tuple(retrieved, kept, parts);
+  });
+
   // The frontend's Create post (formcodec.hpp): None = the page decides; (True, TaskAddModel JSON)
   // = send it to api/tasks; (False, b"") = the antiforgery token is invalid (400).
   m.def("frontend_create_form", [](py::bytes body, py::bytes cookie, py::bytes key) -> py::object {

@@ -35,7 +35,7 @@ import logging
 import uuid
 from pathlib import Path
 
-from ...models import TaskModel, json_array_chunks, naive_utc, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
+from ...models import TaskModel, json_array_chunks, naive_utc, overdue_filter_chunks, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
 from ...sdk.client import InvocationError, RawJsonBytes, client_from_config
 from ...web.app import WebApp, read_model
@@ -165,9 +165,13 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
             t_query += clock() - t0
             if r.status >= 300:
                 raise InvocationError(r.status, r.body, f"invoke {api_app_id}/{path}")
-            # the page bound and filtered in one native pass; any other shape binds with TaskModel
-            fast = overdue_filter_wire(r.body, run_day) if r.body else None
-            if fast is not None:
+            # the page bound and filtered in one native pass (with MarkChunk, also cut into the
+            # markoverdue chunks); any other shape binds with TaskModel
+            parts = None
+            if (fast := overdue_filter_chunks(r.body, run_day, chunk) if r.body and chunk > 0 else None) is not None:
+                n_page, n_overdue, parts = fast
+                overdue = parts[0] if len(parts) == 1 else None
+            elif (fast := overdue_filter_wire(r.body, run_day) if r.body else None) is not None:
                 n_page, n_overdue, overdue = fast
             else:
                 tasks = tasks_from_json(r.body or b"[]")
@@ -178,8 +182,8 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                            n_page)
             if n_overdue:
                 log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", n_overdue)
-                parts = json_array_chunks(overdue, chunk) if isinstance(overdue, bytes) and 0 < chunk < n_overdue \
-                    else None
+                if parts is None and isinstance(overdue, bytes) and 0 < chunk < n_overdue:
+                    parts = json_array_chunks(overdue, chunk)
                 t0 = clock()
                 if parts and len(parts) > 1:
                     results = await asyncio.gather(*(client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue",

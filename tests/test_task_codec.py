@@ -337,3 +337,25 @@ def test_json_array_chunks_regroups_the_items(items, n, spaced):
     parsed = [json.loads(c) for c in chunks]
     assert all(1 <= len(c) <= n for c in parsed) and sum(parsed, []) == items
     assert json_array_chunks(b'{"a": 1}', n) is None and json_array_chunks(b"[1,", n) is None
+
+
+@settings(max_examples=100, deadline=None)
+@given(st.lists(st.tuples(st.sampled_from(["2026-10-15T00:00:00", "2026-10-16T23:59:59.5Z", "2026-10-17T00:00:00",
+                                           "2026-10-18T08:00:00"]),
+                          st.text(max_size=6), st.booleans()), max_size=40), st.integers(1, 9))
+def test_overdue_filter_chunks_equals_filter_then_chunk(rows, n):
+    """models.overdue_filter_chunks (one native pass) gives the processor exactly what
+    overdue_filter_wire followed by json_array_chunks gives: the page size, the kept count, and
+    the kept tasks' canonical TaskModel JSON cut into arrays of at most n."""
+    import uuid
+    from aca_dotnet_workshop_amd.models import json_array_chunks, overdue_filter_chunks, overdue_filter_wire
+    tasks = [{"taskId": str(uuid.UUID(int=i + 1)), "taskName": name, "taskCreatedBy": "c@x",
+              "taskCreatedOn": "2026-10-14T10:00:00", "taskDueDate": due, "taskAssignedTo": "a@x",
+              "isCompleted": done, "isOverDue": False} for i, (due, name, done) in enumerate(rows)]
+    body = json.dumps(tasks).encode()
+    n_page, n_kept, kept = overdue_filter_wire(body, "2026-10-17")
+    got = overdue_filter_chunks(body, "2026-10-17", n)
+    assert got[0] == n_page == len(tasks) and got[1] == n_kept
+    assert got[2] == (json_array_chunks(kept, n) if n_kept else [])
+    assert [t["taskId"] for p in got[2] for t in json.loads(p)] == \
+        [t["taskId"] for t in tasks if t["taskDueDate"][:10] < "2026-10-17"]
