@@ -577,6 +577,24 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
   return true;
 }
 
+// The same order as a number: "yyyy-MM-ddTHH:mm:ss[.f{1,7}]" (canonical, as write_task writes it)
+// -> (seconds of the calendar fields, mixed radix) * 10^6 + microseconds.  Monotone in the
+// DateTime; the fraction's 7th digit (100 ns) is below the TaskModel's microsecond precision.
+inline uint64_t created_key(std::string_view c) {
+  auto d = [&](size_t i, size_t n) {
+    uint64_t r = 0;
+    for (size_t k = i; k < i + n && k < c.size(); ++k) r = r * 10 + (uint64_t)(c[k] - '0');
+    return r;
+  };
+  uint64_t secs = ((((d(0, 4) * 13 + d(5, 2)) * 32 + d(8, 2)) * 24 + d(11, 2)) * 60 + d(14, 2)) * 60 + d(17, 2);
+  uint64_t us = 0;
+  size_t i = 19, n = 0;
+  if (i < c.size() && c[i] == '.')
+    for (++i; i < c.size() && c[i] >= '0' && c[i] <= '9' && n < 6; ++i, ++n) us = us * 10 + (uint64_t)(c[i] - '0');
+  for (; n < 6; ++n) us *= 10;
+  return secs * 1000000 + us;
+}
+
 // State-query response of the task collection (Dapr `{"results": [{"key", "data", "etag"}],
 // "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data: the API's
 // GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).  With
@@ -584,17 +602,6 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
 // (the reference's `.OrderBy(o => o.TaskCreatedOn)`, TasksStoreManager.cs:136): System.Text.Json
 // trims the fraction, so the strings do not sort chronologically within one second ("...:42Z"
 // is earlier than "...:42.1Z").  `more`: the response carries a continuation token.
-inline std::string created_sort_key(const std::string& canon) {
-  // "yyyy-MM-ddTHH:mm:ss[.f{1,6}][Z]" -> "yyyy-MM-ddTHH:mm:ss.ffffff" (fixed width)
-  std::string k = canon.substr(0, 19);
-  k += '.';
-  size_t i = 19, n = 0;
-  if (i < canon.size() && canon[i] == '.')
-    for (++i; i < canon.size() && canon[i] >= '0' && canon[i] <= '9'; ++i, ++n) k += canon[i];
-  for (; n < 6; ++n) k += '0';
-  return k;
-}
-
 inline bool query_tasks(std::string_view body, std::string& out, size_t& count, bool by_created = false,
                         bool* more = nullptr) {
   if (!valid_utf8(body)) return false;
@@ -630,26 +637,33 @@ inline bool query_tasks(std::string_view body, std::string& out, size_t& count, 
     out += ']';
     return true;
   }
-  std::vector<std::pair<std::string, std::string>> rows;  // (fixed-width created key, task JSON)
+  // every task written once into `buf`; ordered by a numeric DateTime key (the canonical
+  // created-on text sits right after `"taskCreatedOn":"` in write_task's fixed field order)
+  struct Row {
+    uint64_t key;
+    size_t at, len;
+  };
+  std::vector<Row> rows;
   rows.reserve(results->items.size());
+  std::string buf;
+  buf.reserve(body.size());
+  static const std::string_view tag = "\"taskCreatedOn\":\"";
   for (const auto& r : results->items) {
     if (r.t != tt::Value::Object) return false;
     const tt::Value* data = r.get("data");
     if (data == nullptr || data->t == tt::Value::Null) continue;
-    std::string one;
-    if (!write_task(*data, false, one, id, day)) return false;
-    // the canonical created-on string sits at a fixed spot: after `"taskCreatedOn":"`
-    size_t at = one.find("\"taskCreatedOn\":\"");
-    if (at == std::string::npos) return false;
-    at += 17;
-    size_t end = one.find('"', at);
-    rows.emplace_back(created_sort_key(one.substr(at, end - at)), std::move(one));
+    const size_t at = buf.size();
+    if (!write_task(*data, false, buf, id, day)) return false;
+    const size_t c = buf.find(tag, at);
+    if (c == std::string::npos) return false;
+    rows.push_back({created_key(std::string_view(buf).substr(c + tag.size())), at, buf.size() - at});
   }
-  std::stable_sort(rows.begin(), rows.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.key < b.key; });
   out.assign("[");
-  for (auto& r : rows) {
+  out.reserve(buf.size() + rows.size() + 2);
+  for (const Row& r : rows) {
     if (count++) out += ',';
-    out += r.second;
+    out.append(buf, r.at, r.len);
   }
   out += ']';
   return true;

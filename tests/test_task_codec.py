@@ -316,6 +316,27 @@ def test_query_results_ordered_by_created_datetime():
     assert made[2] is False
 
 
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 3), st.integers(0, 59), st.integers(0, 999999), st.integers(0, 6),
+                          st.booleans()), min_size=1, max_size=25))
+def test_query_results_created_order_matches_datetime_order(stamps):
+    """The page codec's numeric DateTime key (taskcodec.hpp created_key) orders like the
+    TaskModel's DateTime (UTC and unspecified kinds on one clock), stably, for any mix of
+    fraction lengths and UTC markers."""
+    from aca_dotnet_workshop_amd.models import naive_utc, tasks_from_query_wire
+    texts = []
+    for day, sec, us, digits, z in stamps:
+        frac = f"{us:06d}"[:digits]
+        texts.append(f"2026-03-{10 + day:02d}T11:22:{sec:02d}" + (f".{frac}" if digits else "") + ("Z" if z else ""))
+    results = [{"key": str(i), "data": {**_TASK, "taskId": f"00000000-0000-0000-0000-{i:012d}", "taskCreatedOn": t}}
+               for i, t in enumerate(texts)]
+    made = tasks_from_query_wire(json.dumps({"results": results}).encode(), by_created=True)
+    got = [int(t["taskId"][-12:]) for t in json.loads(made[1])]
+    want = [i for i, _ in sorted(enumerate(results),
+                                 key=lambda x: naive_utc(TaskModel.model_validate(x[1]["data"]).task_created_on))]
+    assert got == want
+
+
 @pytest.mark.parametrize("body", [b"[]", b'{"results": 5}', b'{"results": [{"data": "text"}]}',
                                   json.dumps({"results": [{"data": {"TaskName": "x"}}]}).encode()])
 def test_query_results_decline(body):
