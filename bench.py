@@ -729,8 +729,11 @@ def cpu_per_task(util: dict[str, float], tasks_per_s: float) -> dict:
 # replicas: the round-4 per-role attribution (config.cpu_us_per_task: frontend 58 + 27, API
 # 67 + 52, processor 20 + 8 us per task; profiles/r4_ingress_cost.md) gives 1 : 1.42 : 0.67, but
 # at 0.67 the duty cycle stopped the processors 8-14 % of the timed region (they also run the
-# cron sweep) and their acks gated the steps: 0.85 measured +7 % (profiles/r4_cpu_weights.md)
-CPU_WEIGHT = {"frontend": 1.0, "api": 1.42, "processor": 0.85}
+# cron sweep) and their acks gated the steps: 0.85 measured +7 % (profiles/r4_cpu_weights.md).
+# At ~61 k tasks/s (4 backing-front loops) 0.85 stopped them 9-13 % again, and a sweep that runs
+# into a stop waits it out through the processor's sidecar (a 42.8 ms sweep max); 1.1 stops them
+# < 1 % at the same throughput (profiles/r4_hot_threads.md)
+CPU_WEIGHT = {"frontend": 1.0, "api": 1.42, "processor": 1.1}
 
 
 def _sidecar_counter(uds: str, op: str) -> int:
