@@ -318,13 +318,13 @@ class LocalStack:
                     try:
                         with open(f"/proc/{pid}/task/{t}/stat", "rb") as f:
                             raw = f.read()
-                    except OSError:
+                        lp, rp = raw.find(b"("), raw.rfind(b")")
+                        fields = raw[rp + 2:].split()
+                        # fields[11], [12] = utime, stime (stat fields 14 and 15) in clock ticks
+                        out[(role, raw[lp + 1:rp].decode(errors="replace"), int(t))] = \
+                            (int(fields[11]) / tick, int(fields[12]) / tick)
+                    except (OSError, IndexError, ValueError):  # the thread ended while being read
                         continue
-                    lp, rp = raw.find(b"("), raw.rfind(b")")
-                    fields = raw[rp + 2:].split()
-                    # fields[11], [12] = utime, stime (stat fields 14 and 15) in clock ticks
-                    out[(role, raw[lp + 1:rp].decode(errors="replace"), int(t))] = \
-                        (int(fields[11]) / tick, int(fields[12]) / tick)
         return out
 
     def stop_replica(self, r: ReplicaProc, timeout: float = 10.0) -> None:
