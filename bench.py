@@ -193,6 +193,7 @@ class OverdueSweeper:
         self.stop_ev = threading.Event()
         self.runs: list[tuple[float, dict]] = []
         self.errors: list[str] = []
+        self.marked_all = 0  # tasks marked overdue by every sweep since start (reset() keeps it)
         self.trace_ids: list[str] = []  # every sweep is a sampled trace (per-hop spans)
         self.thread = threading.Thread(target=self._run, name="overdue-sweeper", daemon=True)
 
@@ -223,6 +224,7 @@ class OverdueSweeper:
                                               "traceparent": f"00-{tid}-{os.urandom(8).hex()}-01"})
                     if r.status == 200:
                         self.runs.append((time.perf_counter() - t, r.json()))
+                        self.marked_all += int(self.runs[-1][1].get("markedOverdue", 0))
                         self.trace_ids.append(tid)
                     else:
                         self.errors.append(f"{r.status} {r.body[:200]!r}")
@@ -233,6 +235,30 @@ class OverdueSweeper:
                     await asyncio.get_running_loop().run_in_executor(None, self.stop_ev.wait, left)
         finally:
             await c.close()
+
+    def drain(self, expected: int, tries: int = 30) -> dict:
+        """After the load: fire the job until a sweep marks nothing, then compare every task
+        marked since the start with the past-due tasks created (``expected``) -- each of them
+        must be marked exactly once, as in a single store, however the store is partitioned."""
+        from aca_dotnet_workshop_amd.web.client import HttpClient
+
+        async def fire() -> int:
+            c = HttpClient()
+            try:
+                r = await c.post(self.url, body=b"{}", timeout=120, headers={"Content-Type": "application/json"})
+                if r.status != 200:
+                    raise RuntimeError(f"drain sweep: {r.status} {r.body[:200]!r}")
+                return int(r.json().get("markedOverdue", 0))
+            finally:
+                await c.close()
+        extra = runs = 0
+        for _ in range(tries):
+            got = asyncio.run(fire())
+            extra, runs = extra + got, runs + 1
+            if got == 0:
+                break
+        return {"expected_past_due": expected, "marked_total": self.marked_all + extra, "drain_sweeps": runs,
+                "marked_by_drain": extra, "exactly_once": self.marked_all + extra == expected}
 
     def slowest_trace(self) -> str | None:
         if not self.runs:
@@ -370,9 +396,52 @@ def run_loadgen(exe: str, socks: list[str], counts_url: str | list[str], steps: 
     return dt, json.loads(p.stdout.strip().splitlines()[-1])
 
 
+def self_launch(gpus: int, argv: list[str]) -> int | None:
+    """``--gpus N > 1`` without a launcher: run the N ranks under ``torch.distributed.run`` as a
+    CHILD process (never exec: nothing here has touched HIP yet, but a replaced process image
+    is not allowed on the GPU pool), relay rank 0's one JSON line, and return the child's exit
+    code.  ``None`` when this process is already a rank (``WORLD_SIZE`` set) or N is 1 -- the
+    reported ``n_gpus`` is always the number of ranks that actually ran (``Dist.world``)."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, TT_BENCH_LAUNCHER="self")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    progress(f"--gpus {gpus} without a launcher: starting {gpus} ranks under torch.distributed.run")
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
+
+    def forward(sig, _frame):  # the driver's timeout reaches every rank, not just this parent
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            pass
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    assert p.stdout is not None
+    for line in p.stdout:  # rank 0's result line to stdout; anything else a rank printed: stderr
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
 def main() -> None:
     a = parse()
+    rc = self_launch(a.gpus, sys.argv[1:])
+    if rc is not None:
+        raise SystemExit(rc)
     d = Dist()
+    if d.world > 1 and a.gpus not in (1, d.world):
+        progress(f"--gpus {a.gpus} but {d.world} ranks were launched: reporting {d.world}")
     local = int(os.environ.get("LOCAL_WORLD_SIZE", d.world if d.world > 1 else 1))
     from aca_dotnet_workshop_amd.parallel import pin_rank
     # ranks sharing a host get disjoint NUMA-local core sets (inherited by the whole stack), on
@@ -386,7 +455,7 @@ def main() -> None:
 
 
 def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
-    n = d.world if d.world > 1 else a.gpus
+    n = d.world  # the ranks that actually ran (self_launch starts them for --gpus N)
     auto_api, auto_proc = topology(cores)
     a.api_replicas = a.api_replicas or auto_api
     a.processor_replicas = a.processor_replicas or auto_proc
@@ -529,7 +598,7 @@ def main_localstack(a: argparse.Namespace, d: Dist, cores: float, pinned) -> Non
                                            f"shards, one per rank; {a.processor_replicas * d.world} competing "
                                            f"processor replicas)"
                                            if shared else f"env-per-rank x{d.world if d.world > 1 else 1}"),
-                           "delivery": delivery,
+                           "delivery": delivery, "launcher": launcher_label(d),
                            "concurrency_per_rank": a.concurrency, "api_replicas": a.api_replicas,
                            "processor_replicas": a.processor_replicas, "load_generator": a.client,
                            "sidecar_api_protocol": a.api_protocol,
@@ -561,6 +630,13 @@ _T0 = time.perf_counter()
 def progress(msg: str) -> None:
     """A phase line on stderr (long runs show they are alive; the JSON result stays on stdout)."""
     print(f"[bench {time.perf_counter() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def launcher_label(d: Dist) -> str:
+    if d.world <= 1:
+        return "single process"
+    how = "self-launched by bench.py" if os.environ.get("TT_BENCH_LAUNCHER") == "self" else "external launcher"
+    return f"torch.distributed.run, {d.world} ranks ({how})"
 
 
 def pin_label(pinned) -> str:
@@ -849,7 +925,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     from aca_dotnet_workshop_amd.native.build import build_dataplane, build_loadgen, build_native
     from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
     from aca_dotnet_workshop_amd.platform.manifest import load_manifest
-    n = d.world if d.world > 1 else a.gpus
+    n = d.world  # the ranks that actually ran (self_launch starts them for --gpus N)
     fe, api, proc = frontend_topology(cores)
     fe = a.frontend_replicas or fe
     api = a.api_replicas or api
@@ -982,6 +1058,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                                                          "page_program_ms", "page_zones_ms",
                                                                          "page_kernels_ms", "page_launches",
                                                                          "page_more_ms")}}
+        if shared and sweeper is not None:  # the partitioned sweep marks what one store would
+            per_step = -(-a.batch // a.past_due_every) if a.past_due_every else 0
+            sweep_info["drain"] = sweeper.drain(per_step * d.world * (a.warmup + a.steps))
         delivery = None
         if shared:  # exactly-once across the competing consumers of every rank, over every shard
             c = _counts(counts_url)
@@ -1040,7 +1119,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "parallelism": (f"shared-env x{d.world} (store and broker partitioned over {len(shards)} "
                                            f"shards, one per rank; {proc * d.world} competing processor replicas)"
                                            if shared else f"env-per-rank x{d.world if d.world > 1 else 1}"),
-                           "delivery": delivery,
+                           "delivery": delivery, "launcher": launcher_label(d),
                            "environment": "deploy/main.yaml via the platform controller",
                            "entry": "frontend", "entry_request": "POST /Tasks/Create (form, antiforgery + identity "
                                                                   "cookies) -> 302, redirect not followed",

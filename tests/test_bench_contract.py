@@ -132,6 +132,35 @@ def test_bench_two_ranks_torchrun():
     assert lines[0]["config"]["cpu_pinning"] == want
 
 
+def test_bench_gpus_two_without_launcher_self_launches():
+    """``bench.py --gpus 2`` run as a plain process (no torchrun): it starts the two ranks itself
+    under torch.distributed.run as a child, and the line it relays counts the ranks that ran --
+    never one environment's throughput labelled as two."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "32",
+                        "--api-replicas", "1", "--processor-replicas", "1", "--envelope-s", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    assert [x for x in r.stdout.splitlines() if x.strip() and not x.startswith("{")] == [], r.stdout
+    _check(lines[0], 2, 2, 1)
+    cfg = lines[0]["config"]
+    assert cfg["parallelism"] == "env-per-rank x2"
+    assert cfg["launcher"] == "torch.distributed.run, 2 ranks (self-launched by bench.py)"
+
+
+def test_bench_self_launch_returns_none_for_a_rank_or_one_gpu(monkeypatch):
+    sys.path.insert(0, str(ROOT))
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.self_launch(2, []) is None  # already a rank
+    monkeypatch.delenv("WORLD_SIZE")
+    assert bench.self_launch(1, []) is None  # one GPU: runs in this process
+
+
 def test_bench_shared_env_two_ranks():
     """--shared-env: the state store and the broker are partitioned over both ranks' backings
     (backing/shards.py); the processors of both ranks compete on the ONE subscription (the
@@ -175,6 +204,8 @@ def test_bench_shared_env_frontend_two_ranks():
     dlv = cfg["delivery"]
     assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] >= 2 * 32 * 3, dlv
     assert cfg["overdue_sweeps"]["shards"] == 2 and cfg["overdue_sweeps"]["errors"] == 0
+    drain = cfg["overdue_sweeps"]["drain"]  # batch 32, every 64th past due: 1 per step per rank
+    assert drain["expected_past_due"] == 2 * 1 * 3 and drain["exactly_once"], drain
 
 
 def test_bench_latency_runs():

@@ -460,3 +460,34 @@ def test_shared_env_eight_ranks_exactly_once():
     dlv = cfg["delivery"]
     assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] == 8 * 16 * 3, dlv
     assert dlv["dead_lettered"] == 0
+
+
+@pytest.mark.slow
+def test_shared_env_frontend_eight_ranks_exactly_once():
+    """The headline's own topology at eight ranks: ``bench.py --gpus 8 --shared-env`` started
+    WITHOUT a launcher (it self-launches the ranks), load at every rank's frontend through its
+    external HTTPS ingress, sidecar mTLS, the manifest's CPU caps, and the overdue cron sweep
+    through the data plane's native cross-partition merge; every task is delivered and
+    completed exactly once and the sweeps run without error."""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--steps", "2", "--warmup", "1", "--batch", "16",
+           "--shared-env", "--overdue-sweep-ms", "500", "--past-due-every", "4"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=1500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{") and '"metric"' in x]
+    assert len(line) == 1 and line[0]["n_gpus"] == 8
+    cfg = line[0]["config"]
+    assert cfg["entry"] == "frontend" and cfg["mtls"] is True and cfg["ingress"].startswith("external HTTPS (native)")
+    assert cfg["launcher"] == "torch.distributed.run, 8 ranks (self-launched by bench.py)"
+    assert cfg["parallelism"].startswith("shared-env x8 (store and broker partitioned over 8 shards")
+    dlv = cfg["delivery"]
+    assert dlv["exactly_once"] and dlv["completed"] == dlv["expected"] == 8 * 16 * 3, dlv
+    assert dlv["dead_lettered"] == 0
+    sw = cfg["overdue_sweeps"]
+    assert sw["shards"] == 8 and sw["errors"] == 0, sw
+    # every past-due task of every rank is marked exactly once over the 8 shards, as one store
+    # marks them (the sweeps of the run, then sweeps until one marks nothing)
+    drain = sw["drain"]
+    assert drain["expected_past_due"] == 8 * 4 * 3 and drain["exactly_once"], drain
