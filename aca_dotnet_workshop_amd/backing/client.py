@@ -59,13 +59,16 @@ class BackingClient:
     async def _req(self, method: str, path: str, body: bytes | None = None, headers: dict[str, str] | None = None,
                    ok: tuple[int, ...] = (200, 201, 202, 204), what: str = "", timeout: float | None = None) -> ClientResponse:
         waited = 0.0
+        hdrs = self._h(headers)
         for attempt in range(self.THROTTLE_RETRIES + 1):
-            r = await self.http.request(method, self.base + path, headers=self._h(headers), body=body, timeout=timeout)
+            r = await self.http.request(method, self.base + path, headers=hdrs, body=body, timeout=timeout)
             if r.status != 429 or attempt == self.THROTTLE_RETRIES:
                 break
             delay = min(max(float(r.headers.get("x-ms-retry-after-ms") or 100) / 1000.0, 0.001), 5.0)
             if waited + delay > self.THROTTLE_MAX_WAIT_S:
                 break
+            ticket = r.headers.get("x-tt-ru-ticket")  # the slot the store reserved for this retry
+            hdrs = [h for h in hdrs if h[0] != "x-tt-ru-ticket"] + ([("x-tt-ru-ticket", ticket)] if ticket else [])
             waited += delay
             self.throttled_retries += 1
             await asyncio.sleep(delay)

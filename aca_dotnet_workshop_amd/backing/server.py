@@ -223,18 +223,21 @@ class BackingServices:
             p = req.path_params
             return self.accel(p["account"], p["db"], p["coll"])
 
-        def throttled(s, ru: float) -> Response | None:
-            """Provisioned-throughput admission (DocStore.charge, shared with the native front)."""
-            wait_ms = s.charge(ru)
+        def throttled(req: Request, s, ru: float) -> Response | None:
+            """Provisioned-throughput admission (DocStore.charge, shared with the native front):
+            a 429 reserves the caller's slot and hands out its ticket (x-tt-ru-ticket)."""
+            wait_ms, ticket = s.charge(ru, int(req.headers.get("x-tt-ru-ticket") or 0))
             if not wait_ms:
                 return None
             r = problem(429, detail="Request rate is large: the container's provisioned throughput is exhausted")
             r.headers += [("x-ms-retry-after-ms", str(wait_ms)), ("Retry-After", str((wait_ms + 999) // 1000))]
+            if ticket:
+                r.headers.append(("x-tt-ru-ticket", str(ticket)))
             return r
 
         async def put_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
-            if (t := throttled(s, s.write_ru(len(req.body)))) is not None:
+            if (t := throttled(req, s, s.write_ru(len(req.body)))) is not None:
                 return t
             etag = req.headers.get("if-match") or None
             value = req.body.decode("utf-8")
@@ -249,7 +252,7 @@ class BackingServices:
 
         async def get_doc(req: Request) -> Response:
             s = st(req, "cosmos.read")
-            if (t := throttled(s, s.read_ru(0))) is not None:
+            if (t := throttled(req, s, s.read_ru(0))) is not None:
                 return t
             r = s.get(req.path_params["key"])
             if r is None:
@@ -258,7 +261,7 @@ class BackingServices:
 
         async def del_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
-            if (t := throttled(s, s.write_ru(0))) is not None:
+            if (t := throttled(req, s, s.write_ru(0))) is not None:
                 return t
             try:
                 ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
@@ -269,7 +272,7 @@ class BackingServices:
         async def bulk_get(req: Request) -> Response:
             s = st(req, "cosmos.read")
             keys = (req.json() or {}).get("keys", [])
-            if (t := throttled(s, s.read_ru(0) * max(1, len(keys)))) is not None:
+            if (t := throttled(req, s, s.read_ru(0) * max(1, len(keys)))) is not None:
                 return t
             out = []
             for k in keys:
@@ -286,7 +289,7 @@ class BackingServices:
             texts = self.N.bulk_values(req.body) if len(req.body) else []
             if texts is None or len(texts) != len(items):
                 texts = [v if isinstance(v := it.get("value"), str) else _compact_json(v) for it in items]
-            if (t := throttled(s, sum(s.write_ru(len(v)) for v in texts) or 1)) is not None:
+            if (t := throttled(req, s, sum(s.write_ru(len(v)) for v in texts) or 1)) is not None:
                 return t
             out = []
             for it, value in zip(items, texts):
@@ -331,7 +334,7 @@ class BackingServices:
                 finally:
                     if inner is not None:
                         inner.end()
-            if (t := throttled(s, s.query_ru(0))) is not None:
+            if (t := throttled(req, s, s.query_ru(0))) is not None:
                 return t
             try:
                 text = await asyncio.get_running_loop().run_in_executor(self.query_pool, run)
@@ -340,7 +343,7 @@ class BackingServices:
                     span.end()
                 return problem(400, detail=str(ex))
             body = text if isinstance(text, bytes) else text.encode()
-            s.charge(s.query_ru(len(body)) - s.query_ru(0))  # result size part: charged after the fact
+            s.debit(s.query_ru(len(body)) - s.query_ru(0))  # result size part: owed after the fact
             if span is not None:
                 span.set("bytes", len(body))
                 span.end()
@@ -349,7 +352,7 @@ class BackingServices:
 
         async def transaction(req: Request) -> Response:
             s = st(req, "cosmos.write")
-            if (t := throttled(s, s.write_ru(len(req.body)))) is not None:
+            if (t := throttled(req, s, s.write_ru(len(req.body)))) is not None:
                 return t
             ops = []
             for o in (req.json() or {}).get("ops", []):

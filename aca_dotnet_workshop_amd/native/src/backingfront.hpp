@@ -434,14 +434,19 @@ class BackingFront {
 
   // Provisioned-throughput admission (DocStore::charge): 429 + x-ms-retry-after-ms when the
   // container's RU/s budget is spent, as Cosmos answers; the sidecars retry after the hint.
-  bool throttled(ev::Reply& r, DocStore* s, double ru) {
-    int64_t wait_ms = s->charge(ru);
+  // The 429 carries the reservation's ticket (x-tt-ru-ticket); a retry presenting it is admitted
+  // at its slot without a second charge (DocStore::charge).
+  bool throttled(ev::Message& m, ev::Reply& r, DocStore* s, double ru) {
+    uint64_t ticket = 0, out = 0;
+    if (const std::string* t = m.header("x-tt-ru-ticket")) ticket = std::strtoull(t->c_str(), nullptr, 10);
+    int64_t wait_ms = s->charge(ru, ticket, out);
     if (!wait_ms) return false;
     count("doc.throttled");
-    r.send(429, {{"x-ms-retry-after-ms", std::to_string(wait_ms)},
-                 {"retry-after", std::to_string((wait_ms + 999) / 1000)},
-                 {"content-type", "application/problem+json; charset=utf-8"}},
-           bf::problem_json(429, "Request rate is large: the container's provisioned throughput is exhausted"));
+    ev::HeaderList h{{"x-ms-retry-after-ms", std::to_string(wait_ms)},
+                     {"retry-after", std::to_string((wait_ms + 999) / 1000)},
+                     {"content-type", "application/problem+json; charset=utf-8"}};
+    if (out) h.emplace_back("x-tt-ru-ticket", std::to_string(out));
+    r.send(429, h, bf::problem_json(429, "Request rate is large: the container's provisioned throughput is exhausted"));
     return true;
   }
 
@@ -459,7 +464,7 @@ class BackingFront {
     if (m.method == "GET") {
       if (!authorize(m, r, "cosmos.read", scope)) return true;
       count("doc.get");
-      if (throttled(r, c->store, DocStore::read_ru(0))) return true;
+      if (throttled(m, r, c->store, DocStore::read_ru(0))) return true;
       auto v = c->store->get(key);
       if (!v) r.empty(404);
       else r.send(200, {{"etag", v->second}, {"content-type", "application/json"}}, v->first);
@@ -473,7 +478,7 @@ class BackingFront {
     std::optional<std::string> etag;
     if (im && !im->empty()) etag = *im;
     const char* pj = "application/problem+json; charset=utf-8";
-    if (throttled(r, c->store, DocStore::write_ru(m.method == "PUT" ? m.body.size() : 0))) return true;
+    if (throttled(m, r, c->store, DocStore::write_ru(m.method == "PUT" ? m.body.size() : 0))) return true;
     if (m.method == "PUT") {
       count("doc.put");
       auto* fw = m.header("x-tt-first-write");
@@ -512,7 +517,7 @@ class BackingFront {
     count("doc.bulkset");
     double ru = 0;
     for (auto& b : batch) ru += DocStore::write_ru(b.value.size());
-    if (throttled(r, c->store, ru)) return true;
+    if (throttled(m, r, c->store, ru)) return true;
     const std::vector<DocStore::BulkResult> res = c->store->set_many(batch);
     std::string out = "[";
     bool etag_err = false, other_err = false;
@@ -554,7 +559,7 @@ class BackingFront {
       if (k.t != Value::String) return false;
     if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
     count("doc.bulkget");
-    if (throttled(r, c->store, DocStore::read_ru(0) * (double)std::max<size_t>(1, keys->items.size()))) return true;
+    if (throttled(m, r, c->store, DocStore::read_ru(0) * (double)std::max<size_t>(1, keys->items.size()))) return true;
     std::string out = "[";
     for (size_t i = 0; i < keys->items.size(); ++i) {
       const std::string& k = keys->items[i].s;

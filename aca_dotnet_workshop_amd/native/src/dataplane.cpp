@@ -1199,6 +1199,12 @@ class DataPlane {
           count("state.throttled_retry", 429);
           c->attempt++;
           c->waited += delay;
+          // the store reserved this call a slot: the retry presents its ticket and is admitted
+          // there without a second charge (DocStore::charge), so waiters do not collide again
+          auto& hs = c->headers;
+          hs.erase(std::remove_if(hs.begin(), hs.end(), [](const auto& h) { return h.first == "x-tt-ru-ticket"; }),
+                   hs.end());
+          if (const std::string* t = res.resp.header("x-tt-ru-ticket")) hs.emplace_back("x-tt-ru-ticket", *t);
           loop_.call_later(delay, [this, c] { store_send(c); });
           return;
         }

@@ -567,10 +567,29 @@ class DocStore {
     ru_rate_ = std::max(0.0, ru_per_s);
     ru_tokens_ = ru_rate_;
     ru_last_ = mono_s();
+    ru_tickets_.clear();
   }
 
+  // Admission with reservations.  A caller the bucket cannot serve now is not just told its own
+  // deficit (every waiter would wake at once and collide again): its RU are RESERVED -- the
+  // bucket goes negative by the demand admitted for later -- and the 429's hint is the moment
+  // the refill has paid for it, i.e. that caller's slot behind every earlier waiter.  The 429
+  // also carries a ticket (`x-tt-ru-ticket`); the retry that presents it at or after its slot
+  // is admitted without being charged again.  Without the ticket a retry is a new request (the
+  // Cosmos wire contract still holds: 429 + x-ms-retry-after-ms).  A reservation more than
+  // kMaxReserveS ahead is refused outright (the SDK's 30 s wait budget could not reach it); a
+  // ticket not claimed within kTicketTtlS of its slot lapses and its RU stay spent.
+  static constexpr double kMaxReserveS = 25.0;
+  static constexpr double kTicketTtlS = 10.0;
+
   int64_t charge(double ru) {
+    uint64_t unused = 0;
+    return charge(ru, 0, unused);
+  }
+
+  int64_t charge(double ru, uint64_t ticket, uint64_t& ticket_out) {
     std::lock_guard<std::mutex> g(ru_mu_);
+    ticket_out = 0;
     if (ru_rate_ <= 0) {  // not provisioned: admitted, still metered (what the workload would need)
       ru_consumed_ += ru;
       return 0;
@@ -578,6 +597,20 @@ class DocStore {
     double now = mono_s();
     ru_tokens_ = std::min(ru_rate_, ru_tokens_ + (now - ru_last_) * ru_rate_);
     ru_last_ = now;
+    if (ticket) {
+      auto it = ru_tickets_.find(ticket);
+      if (it != ru_tickets_.end()) {
+        if (now + 5e-4 >= it->second.first) {  // its slot came: paid for by the reservation
+          ru_consumed_ += it->second.second;
+          ++ru_reserved_admits_;
+          ru_tickets_.erase(it);
+          return 0;
+        }
+        ticket_out = ticket;  // early: keep the slot
+        ++ru_throttled_;
+        return std::max<int64_t>(1, (int64_t)std::ceil((it->second.first - now) * 1000.0));
+      }
+    }
     ru = std::min(ru, ru_rate_);  // a request bigger than a second's budget waits for a full bucket
     if (ru_tokens_ >= ru) {
       ru_tokens_ -= ru;
@@ -585,12 +618,33 @@ class DocStore {
       return 0;
     }
     ++ru_throttled_;
-    return std::max<int64_t>(1, (int64_t)std::ceil((ru - ru_tokens_) / ru_rate_ * 1000.0));
+    double wait = (ru - ru_tokens_) / ru_rate_;  // until the refill has paid every earlier reservation and this one
+    if (wait > kMaxReserveS) return std::max<int64_t>(1, (int64_t)std::ceil(wait * 1000.0));
+    ru_tokens_ -= ru;
+    if (ru_tickets_.size() > 4096) {  // lapsed reservations (their callers gave up)
+      for (auto it = ru_tickets_.begin(); it != ru_tickets_.end();)
+        it = now > it->second.first + kTicketTtlS ? ru_tickets_.erase(it) : std::next(it);
+    }
+    ticket_out = ++ru_ticket_seq_;
+    ru_tickets_.emplace(ticket_out, std::make_pair(now + wait, ru));
+    return std::max<int64_t>(1, (int64_t)std::ceil(wait * 1000.0));
+  }
+
+  // RU owed after the fact (a query's result-size part): spent whatever the balance, so later
+  // callers wait for it.
+  void debit(double ru) {
+    std::lock_guard<std::mutex> g(ru_mu_);
+    ru_consumed_ += ru;
+    if (ru_rate_ <= 0) return;
+    double now = mono_s();
+    ru_tokens_ = std::min(ru_rate_, ru_tokens_ + (now - ru_last_) * ru_rate_) - ru;
+    ru_last_ = now;
   }
 
   std::unordered_map<std::string, double> throughput_stats() {
     std::lock_guard<std::mutex> g(ru_mu_);
-    return {{"ru_per_s", ru_rate_}, {"ru_consumed", ru_consumed_}, {"throttled", (double)ru_throttled_}};
+    return {{"ru_per_s", ru_rate_}, {"ru_consumed", ru_consumed_}, {"throttled", (double)ru_throttled_},
+            {"reserved_admits", (double)ru_reserved_admits_}, {"open_reservations", (double)ru_tickets_.size()}};
   }
 
   // ------------------------------------------------------------ column mirror
@@ -1121,7 +1175,8 @@ class DocStore {
   std::vector<int32_t> reuse_;                   // put_at's per-column carried ids (under mu_)
   std::mutex ru_mu_;
   double ru_rate_ = 0, ru_tokens_ = 0, ru_last_ = 0, ru_consumed_ = 0;
-  uint64_t ru_throttled_ = 0;
+  uint64_t ru_throttled_ = 0, ru_reserved_admits_ = 0, ru_ticket_seq_ = 0;
+  std::unordered_map<uint64_t, std::pair<double, double>> ru_tickets_;  // ticket -> (slot, RU reserved)
   static double mono_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }

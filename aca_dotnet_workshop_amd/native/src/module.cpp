@@ -620,7 +620,13 @@ PYBIND11_MODULE(_ttnative, m) {
            py::arg("sort_paths") = py::none())
       .def("mirror_stats", &DocStore::mirror_stats)
       .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"))
-      .def("charge", &DocStore::charge, py::arg("ru"))
+      .def("charge", [](DocStore& s, double ru, uint64_t ticket) {
+             uint64_t out = 0;
+             int64_t wait = s.charge(ru, ticket, out);
+             return py::make_tuple(wait, out);
+           }, py::arg("ru"), py::arg("ticket") = 0,
+           "(wait_ms, ticket): 0 = admitted; else a 429 whose ticket claims the reserved slot")
+      .def("debit", &DocStore::debit, py::arg("ru"))
       .def("throughput_stats", &DocStore::throughput_stats)
       .def_static("read_ru", &DocStore::read_ru)
       .def_static("write_ru", &DocStore::write_ru)

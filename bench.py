@@ -906,8 +906,12 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 "processor_replicas_reached": peak["processor"],
                 "replicas": {"frontend": 1, "api": 1, "processor": "1..5 (KEDA, 10 messages per replica)"},
                 "vcpu_per_replica": 0.25, "users": 500, "concurrency": 16,
-                "note": "a create or list whose store call is still throttled after the sidecar's 9 retries "
-                        "(the Cosmos SDK policy) answers 500, as the reference's pages would",
+                "store_429s_per_task": round(int(st1.get("throttled", 0) - st0.get("throttled", 0)) / tasks, 2) if tasks else None,
+                "tasks_per_s_over_budget_rate": (round(tasks / el / (float(st1.get("ru_per_s", 0.0)) / (ru / tasks)), 3)
+                                                 if tasks and ru and el and st1.get("ru_per_s") else None),
+                "note": "a throttled store call gets a reserved slot (429 + x-ms-retry-after-ms + ticket) and the "
+                        "sidecar retries there (the Cosmos SDK policy: 9 retries, 30 s); one still throttled after "
+                        "that answers 500, as the reference's pages would",
                 "keda_polling_s": 5, "loadgen_exit": p.returncode}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:500]}
