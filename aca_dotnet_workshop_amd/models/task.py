@@ -195,21 +195,32 @@ def conditional_mark_wire(got: bytes) -> tuple[list[str], bytes, int] | None:
     (ids to mark, a bulk-save body setting ``isOverDue`` on the STORED task where it is still
     open and not yet overdue, each item ETag-guarded with first-write concurrency, the number
     skipped: completed, already overdue or deleted).  Native (``taskcodec.hpp
-    conditional_mark``) or this module's Python twin; ``None``: outside the TaskModel envelope."""
+    conditional_mark``) or this module's Python twin, which also takes the documents the native
+    codec turns down (a null string, a duplicate key, an unusual date form); a stored document
+    that does not bind as a TaskModel at all is skipped, so the rest of the page is still marked
+    and later sweeps do not fail on it forever.  ``None``: the answer is not a bulk-get array."""
     fns = _lists()
     if fns:
-        return fns[2](got)
+        made = fns[2](got)
+        if made is not None:
+            return made
     try:
         rows = json.loads(got)
     except ValueError:
         return None
+    if not isinstance(rows, list):
+        return None
     ids, items, skipped = [], [], 0
     for r in rows:
-        data = r.get("data")
+        data = r.get("data") if isinstance(r, dict) else None
         if data is None:
             skipped += 1
             continue
-        t = TaskModel.model_validate(data)
+        try:
+            t = TaskModel.model_validate(data)
+        except ValueError:  # pydantic's ValidationError: not a task -- leave it as stored
+            skipped += 1
+            continue
         if t.is_completed or t.is_over_due:
             skipped += 1
             continue

@@ -919,6 +919,13 @@ class ClientConn : public IoObj {
   }
   bool busy() const { return busy_; }
   std::string wire_copy;  // kept for the stale-connection retry
+  // An idle connection whose peer already closed it (FIN or RST queued, not yet seen by the
+  // loop): not reused.  Pending bytes (a TLS session ticket) say nothing either way: kept.
+  bool peer_gone() const {
+    char b;
+    ssize_t n = ::recv(fd, &b, 1, MSG_PEEK | MSG_DONTWAIT);
+    return n == 0 || (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR);
+  }
   bool head_req = false;
   std::unique_ptr<TlsIo> tls_;
 
@@ -956,8 +963,11 @@ class Client {
   void set_tls(std::shared_ptr<TlsContext> mesh) { mesh_tls_ = std::move(mesh); }
 
   // Issue `method target` with `headers`/`body` to `ep`; `cb` runs on completion or failure.
+  // `retry_stale`: a reused keep-alive connection that fails with a reset / broken pipe is
+  // retried once on a new one.  That is only safe when re-sending cannot repeat an action: pass
+  // false for a non-idempotent request whose peer may have read it before resetting.
   void request(const Endpoint& ep, std::string_view method, std::string_view target, const HeaderList& headers,
-               std::string_view body, double timeout_s, ClientCallback cb) {
+               std::string_view body, double timeout_s, ClientCallback cb, bool retry_stale = true) {
     std::string w;
     w.reserve(body.size() + 512);
     w.append(method);
@@ -977,7 +987,7 @@ class Client {
     w += std::to_string(body.size());
     w += "\r\n\r\n";
     w.append(body);
-    dispatch(ep, std::move(w), method == "HEAD", timeout_s, std::move(cb), true);
+    dispatch(ep, std::move(w), method == "HEAD", timeout_s, std::move(cb), retry_stale);
   }
 
   void release(const std::shared_ptr<ClientConn>& c) {
@@ -1009,7 +1019,9 @@ class Client {
     while (!v.empty()) {
       c = v.back();
       v.pop_back();
-      if (!c->dead) break;
+      // without the stale retry, first make sure the peer has not closed it meanwhile
+      if (!c->dead && (allow_retry || !c->peer_gone())) break;
+      loop_.remove(c.get());
       c.reset();
     }
     double deadline = timeout_s > 0 ? now_s() + timeout_s : 0;

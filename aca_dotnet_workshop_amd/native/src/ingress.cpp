@@ -350,7 +350,7 @@ class Worker {
       st.inflight.fetch_sub(1, std::memory_order_relaxed);
       st.failures.fetch_add(1, std::memory_order_relaxed);
       send_problem(c->reply, 503, "no healthy replica for " + ing_.app() + ": " + errno_name(c->last_err));
-    });
+    }, /*retry_stale=*/idempotent(q.method));  // a POST a replica may have read is never re-sent
   }
 
   static std::string errno_name(int e) {

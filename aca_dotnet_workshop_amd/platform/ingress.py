@@ -152,7 +152,8 @@ class Ingress:
             last = None
             for b in r.pick()[:3]:
                 try:
-                    resp = await self.http.request(req.method, b.url + req.target, headers=headers, body=req.body)
+                    resp = await self.http.request(req.method, b.url + req.target, headers=headers, body=req.body,
+                                                   retry_stale=req.method in _IDEMPOTENT)
                     out = [(k, x) for k, v in resp.headers.items() if k not in _HOP
                            for x in (v if isinstance(v, list) else [v])]
                     return Response(resp.body, resp.status, out)

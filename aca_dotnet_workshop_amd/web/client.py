@@ -251,7 +251,10 @@ class HttpClient:
 
     async def request(self, method: str, url: str, *, headers: dict[str, str] | list[tuple[str, str]] | None = None,
                       body: bytes | str | None = None, json_body: Any = None,
-                      timeout: float | None = None) -> ClientResponse:
+                      timeout: float | None = None, retry_stale: bool = True) -> ClientResponse:
+        """``retry_stale``: a reused keep-alive connection closed before any response byte is
+        retried once on a fresh one -- pass False for a non-idempotent request the peer may
+        have read (and acted on) before closing."""
         key, target = parse_endpoint(url)
         if json_body is not None:
             body = json.dumps(json_body, separators=(",", ":")).encode()
@@ -295,7 +298,7 @@ class HttpClient:
                 resp, keep = await fut
             except ConnectionClosed:
                 # stale keep-alive connection closed by the server: retry once on a fresh one
-                if conn.reused and not conn.got_bytes and attempt == 0:
+                if retry_stale and conn.reused and not conn.got_bytes and attempt == 0:
                     continue
                 raise
             except BaseException:

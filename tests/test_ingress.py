@@ -249,3 +249,57 @@ def test_native_ingress_least_in_flight_and_stats(tmp_path):
             s1.close()
             s2.close()
     asyncio.run(main())
+
+
+@pytest.mark.parametrize("plane", PLANES)
+def test_ingress_never_resends_a_post_reset_on_a_reused_connection(plane, tmp_path):
+    """A replica reads a POST that arrived on a reused keep-alive connection, acts on it, and
+    dies with a reset (RST).  The ingress must not take that for a stale idle connection and
+    re-send the POST (the client's stale-connection retry): the replica sees the POST
+    once and the caller gets 502.  A GET reset the same way is still retried."""
+    async def main():
+        hits = collections.Counter()
+
+        async def handle(reader, writer):
+            while True:
+                try:
+                    head = await reader.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    break
+                method, target = head.split(b" ", 2)[:2]
+                method = method.decode()
+                n = int((re_len.search(head) or [0, b"0"])[1])
+                if n:
+                    await reader.readexactly(n)
+                hits[method] += 1
+                if target.startswith(b"/api/") and hits[method + "-reset"] == 0:  # first of each method: reset
+                    hits[method + "-reset"] += 1
+                    sock = writer.get_extra_info("socket")
+                    sock.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, b"\x01\x00\x00\x00\x00\x00\x00\x00")
+                    writer.transport.abort()
+                    return
+                hits["served"] += 1
+                writer.write(b"HTTP/1.1 200 OK\r\ncontent-length: 2\r\n\r\nok")
+                await writer.drain()
+            writer.close()
+        import re
+        re_len = re.compile(rb"(?i)content-length:\s*(\d+)")
+        srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+        url = f"http://127.0.0.1:{srv.sockets[0].getsockname()[1]}"
+        ing = NativeIngress(IngressRoute("api", True), tmp_path, threads=1) if plane == "native" else Ingress(
+            IngressRoute("api", True))
+        await ing.start(None, None)
+        ing.set_backends([Backend("r1", url)], {})
+        try:
+            st, _, _ = await asyncio.to_thread(_request, ing.public_port, "GET", "/warm")  # opens the keep-alive
+            assert st == 200
+            st, _, _ = await asyncio.to_thread(_request, ing.public_port, "POST", "/api/tasks", b"{}")
+            assert st == 502 and hits["POST"] == 1, (st, hits)  # read once, never re-sent
+            st, _, _ = await asyncio.to_thread(_request, ing.public_port, "GET", "/warm")  # a new keep-alive
+            assert st == 200
+            st, _, body = await asyncio.to_thread(_request, ing.public_port, "GET", "/api/tasks")
+            assert st == 200 and body == b"ok" and hits["GET"] == 4, (st, hits)  # idempotent: retried
+        finally:
+            await ing.stop()
+            srv.close()
+    asyncio.run(main())

@@ -380,3 +380,29 @@ def test_overdue_filter_chunks_equals_filter_then_chunk(rows, n):
     assert got[2] == (json_array_chunks(kept, n) if n_kept else [])
     assert [t["taskId"] for p in got[2] for t in json.loads(p)] == \
         [t["taskId"] for t in tasks if t["taskDueDate"][:10] < "2026-10-17"]
+
+
+def test_conditional_mark_falls_back_when_the_native_codec_declines():
+    """A markoverdue page holding a stored document the native codec turns down (a null string,
+    a duplicate key, an offset date form) is marked by the Python twin instead of failing the
+    whole chunk; a document that does not bind as a TaskModel at all is skipped and
+    the rest of the page is still marked."""
+    from aca_dotnet_workshop_amd.models.task import _lists, conditional_mark_wire
+
+    def task(**kw):
+        d = {"taskId": str(uuid.uuid4()), "taskName": "n", "taskCreatedBy": "a@x",
+             "taskCreatedOn": "2024-01-01T00:00:00.0000000Z", "taskDueDate": "2024-01-02T00:00:00",
+             "taskAssignedTo": "b@x", "isCompleted": False, "isOverDue": False}
+        d.update(kw)
+        return d
+    ok, null_name, offset, done = task(), task(taskAssignedTo=None), task(taskDueDate="2024-01-02T00:00:00+00:00"), \
+        task(isCompleted=True)
+    rows = [{"key": t["taskId"], "data": t, "etag": str(i)} for i, t in enumerate((ok, null_name, offset, done))]
+    rows.append({"key": "gone", "data": None})
+    got = json.dumps(rows).encode()
+    assert _lists()[2](got) is None  # the native codec declines this page
+    ids, bulk, skipped = conditional_mark_wire(got)
+    assert ids == [ok["taskId"], offset["taskId"]] and skipped == 3
+    items = json.loads(bulk)
+    assert [i["key"] for i in items] == ids and all(i["value"]["isOverDue"] for i in items)
+    assert [i["etag"] for i in items] == ["0", "2"] and all(i["options"] == {"concurrency": "first-write"} for i in items)
