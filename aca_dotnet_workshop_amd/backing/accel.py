@@ -197,7 +197,7 @@ class CollectionAccelerator:
             # from: a write that compacts the mirror between the sync and the lookup (the native
             # front writes without the GIL) renumbers them -- re-sync and select again
             t_sel = t_res = 0.0
-            for _ in range(3):
+            for attempt in range(3):
                 ta = time.perf_counter()
                 try:
                     rows, token = self.index.query_rows(qq, k)
@@ -209,9 +209,13 @@ class CollectionAccelerator:
                                            sort_paths=[sp["key"] for sp in q.get("sort") or []
                                                        if isinstance(sp, dict) and "key" in sp] if sort_keys else None)
                 t_sel, t_res = t_sel + tb - ta, t_res + time.perf_counter() - tb
-                if res is not None:
+                # a page that lost rows to writes since the sync (killed rows are skipped) and has
+                # more matches behind it is selected again on a fresh sync: a short page with a
+                # continuation would let a cross-partition merge run past this shard's order
+                if res is not None and (not res[1] or not token or attempt == 2):
                     break
-                self.stats["stale_retries"] = self.stats.get("stale_retries", 0) + 1
+                key = "stale_retries" if res is None else "short_page_retries"
+                self.stats[key] = self.stats.get(key, 0) + 1
                 try:
                     self.index.sync()
                 except Unsupported:

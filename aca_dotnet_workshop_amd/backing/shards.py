@@ -141,10 +141,21 @@ def merge_pages(query: dict[str, Any], pages: list[tuple[int, dict[str, Any]] | 
         merged = heapq.merge(*streams, key=lambda t: t[0], reverse=specs[0][1] < 0)
     else:
         merged = heapq.merge(*streams, key=functools.cmp_to_key(_sort_cmp(specs)))
-    take = list(itertools.islice(merged, limit)) if limit else list(merged)
+    # a k-way PAGED merge: once a shard that has more matches (it sent a token) runs out of this
+    # page's entries, its unfetched ones may sort before anything left -- the page ends there
+    # (a shard can send a short page: its mirror skipped stale rows)
+    by_shard = {i: resp for i, resp in pages if resp is not None}
+    left = {i: len(resp.get("results") or []) for i, resp in by_shard.items()}
+    more = {i for i, resp in by_shard.items() if resp.get("token")}
+    take: list[tuple] = []
     used = [0] * len(offsets)
-    for _, i, _ in take:
-        used[i] += 1
+    if not any(left[i] == 0 for i in more):
+        for item in merged:
+            take.append(item)
+            i = item[1]
+            used[i] += 1
+            if (limit and len(take) >= limit) or (i in more and used[i] == left[i]):
+                break
     new: list[int | None] = []
     for i, off in enumerate(offsets):
         resp = pages[i][1] if off is not None else None
@@ -152,7 +163,13 @@ def merge_pages(query: dict[str, Any], pages: list[tuple[int, dict[str, Any]] | 
             new.append(None)
             continue
         n_i = len(resp.get("results") or [])
-        new.append(None if (not resp.get("token") and used[i] == n_i) else off + used[i])
+        tok = resp.get("token")
+        if not tok and used[i] == n_i:
+            new.append(None)
+        elif used[i] == n_i and str(tok).isdigit():  # a fully used page resumes where the shard said
+            new.append(int(tok))
+        else:
+            new.append(off + used[i])
     out: dict[str, Any] = {"results": [r for _, _, r in take]}
     tok = encode_token(new) if limit else None
     if tok:

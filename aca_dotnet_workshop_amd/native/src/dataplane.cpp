@@ -1465,6 +1465,7 @@ class DataPlane {
     std::vector<std::vector<Value>> sort;  // sort values per result
     bool more = false;
     bool present = false;  // asked (offset not null)
+    long long next = -1;   // the shard's own continuation (its position after the page), when numeric
   };
   struct XQuery {
     std::vector<std::pair<std::string, bool>> sort;  // path, desc
@@ -1577,7 +1578,12 @@ class DataPlane {
           try {
             Value v = parse(res.resp.body);
             ShardPage& pg = x->pages[i];
-            if (const Value* t = v.get("token"); t && t->t == Value::String && !t->s.empty()) pg.more = true;
+            if (const Value* t = v.get("token"); t && t->t == Value::String && !t->s.empty()) {
+              pg.more = true;
+              char* end = nullptr;
+              long long nx = std::strtoll(t->s.c_str(), &end, 10);
+              if (end && *end == 0 && nx >= 0) pg.next = nx;
+            }
             if (const Value* rs = v.get("results"); rs && rs->t == Value::Array)
               for (auto& it : rs->items) {
                 const Value* k = it.get("key");
@@ -1616,7 +1622,15 @@ class DataPlane {
     };
     auto bg = std::make_shared<BulkGet>();
     std::vector<size_t> order_shard;  // the merged page, as (shard) per entry; keys in bg
-    while (!x->limit || bg->full.size() < x->limit) {
+    // a k-way PAGED merge: once a shard that has more matches (it sent a continuation) runs out
+    // of this page's entries, its unfetched ones may sort before anything left here -- the
+    // merged page ends there (a shard can send a short page: its mirror skipped stale rows)
+    auto starved = [&] {
+      for (size_t i = 0; i < n; ++i)
+        if (x->pages[i].more && pos[i] >= x->pages[i].keys.size()) return true;
+      return false;
+    };
+    while ((!x->limit || bg->full.size() < x->limit) && !starved()) {
       size_t best = n;
       for (size_t i = 0; i < n; ++i) {
         if (pos[i] >= x->pages[i].keys.size()) continue;
@@ -1642,8 +1656,9 @@ class DataPlane {
         const ShardPage& pg = x->pages[i];
         if (!pg.present || (!pg.more && used[i] == pg.keys.size())) {
           arr += "null";
-        } else {
-          arr += std::to_string(x->offsets[i] + (long long)used[i]);
+        } else {  // a fully used page resumes where the shard said (past any rows it skipped)
+          bool all = used[i] == pg.keys.size();
+          arr += std::to_string(all && pg.next >= 0 ? pg.next : x->offsets[i] + (long long)used[i]);
           any = true;
         }
       }

@@ -1310,9 +1310,10 @@ class ColumnarIndex:
             if ordered is not None:
                 end = min(total, offset + limit) if limit else total
                 sel = ordered[offset:end].cpu().numpy()
-                kernels.check_sort()
-                token = str(end) if limit and end < total else None
-                return sel.astype(np.int32, copy=False), token
+                if kernels.check_sort():
+                    token = str(end) if limit and end < total else None
+                    return sel.astype(np.int32, copy=False), token
+                # a look-back timed out in the device sort: this query orders on the host
             rows = dev_rows.cpu().numpy()
         if rows is None:  # no GPU: every core of the CPU share over the same narrow codes
             try:

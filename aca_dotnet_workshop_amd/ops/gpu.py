@@ -351,12 +351,19 @@ class GpuKernels:
             raise RuntimeError(f"tt_sort_pairs failed ({rc})")
         return rows_out
 
-    def check_sort(self) -> None:
-        """Raise if any sort so far saw a look-back spin time out (its output is not trustworthy).
-        Reads one device word: call it where the caller synchronises anyway."""
+    sort_faults = 0  # sorts whose output was discarded (a look-back spin timed out)
+
+    def check_sort(self) -> bool:
+        """False if a sort since the last check saw a look-back spin time out (its output is not
+        trustworthy: the caller orders on the host instead).  The fault word is cleared, so one
+        timeout costs one query its device ordering, not every later one.  Reads one device
+        word: call it where the caller synchronises anyway."""
         fault = getattr(self, "_sort_fault", None)
-        if fault is not None and int(fault.item()) != 0:
-            raise RuntimeError(f"tt_sort_pairs: {int(fault.item())} look-back spins timed out")
+        if fault is None or int(fault.item()) == 0:
+            return True
+        fault.zero_()
+        self.sort_faults += 1
+        return False
 
     def _top_k(self, keys, rows, k: int, shift: int, hist, key_bits: int = 63):
         import numpy as np

@@ -35,7 +35,7 @@ from ..backing.shards import PARTITIONED_FAMILIES, ShardedBackingClient
 from ..web.app import WebApp
 from ..web.http import Request, Response, empty, json_response
 from ..web.server import HttpServer
-from .ingress import Backend, IngressRoute, make_ingress
+from .ingress import Backend, IngressRoute, make_ingress_async
 from .limits import Limits, ResourceLimiter
 from .pki import EnvironmentPki
 from .manifest import Manifest, ManifestError, desired_state, identity_of, template_hash, validate
@@ -407,7 +407,10 @@ class EnvironmentController:
         ing = rt.spec["ingress"]
         rt.ingress_sig = self._ingress_sig(ing)
         route = IngressRoute(rt.name, bool(ing.get("external", False)))
-        rt.ingress = make_ingress(route, self.stack.sock_dir)
+        ingress = await make_ingress_async(route, self.stack.sock_dir)
+        if rt.ingress is not None:  # another reconcile pass got there while this one built
+            return
+        rt.ingress = ingress
         port = int(ing.get("port") or 0)
         tls = None
         if route.external and str(ing.get("transport", "auto")).lower() != "http":

@@ -360,5 +360,11 @@ def make_ingress(route: IngressRoute, work_dir: str | os.PathLike) -> Ingress | 
     return NativeIngress(route, work_dir)
 
 
+async def make_ingress_async(route: IngressRoute, work_dir: str | os.PathLike) -> Ingress | NativeIngress:
+    """``make_ingress`` for an event loop: a first-time native build runs on a worker thread, so
+    the controller's loop (health, scaling, the control API) keeps running meanwhile."""
+    return await asyncio.to_thread(make_ingress, route, work_dir)
+
+
 def now_ms() -> int:
     return int(time.time() * 1000)

@@ -297,8 +297,9 @@ def test_accelerator_keeps_writes_native(monkeypatch):
 
 @pytest.mark.parametrize("front", FRONTS)
 def test_provisioned_throughput_429(front, monkeypatch):
-    """RU token bucket shared by both fronts: 429 with x-ms-retry-after-ms / Retry-After when spent,
-    nothing charged for a rejected call; the backing client retries after the hint."""
+    """RU token bucket shared by both fronts: 429 with x-ms-retry-after-ms / Retry-After when spent;
+    a rejected call is given a reserved slot behind the earlier waiters (the hints are spaced by
+    its RU / the rate) and a ticket; the backing client retries at the hint with the ticket."""
     async def main():
         async with Backing(front, monkeypatch) as b:
             c = BackingClient(b.base, identity="x")
@@ -311,8 +312,10 @@ def test_provisioned_throughput_429(front, monkeypatch):
                 statuses.append(r.status)
                 if r.status == 429:
                     hints.append(int(r.headers["x-ms-retry-after-ms"]))
-                    assert int(r.headers["retry-after"]) >= 1
-            assert statuses[:2] == [200, 200] and 429 in statuses and all(0 < x <= 1000 for x in hints)
+                    assert int(r.headers["retry-after"]) >= 1 and int(r.headers["x-tt-ru-ticket"]) > 0
+            assert statuses == [200, 200, 429, 429, 429]
+            # 5 RU each at 10 RU/s: the waiters' slots are 500 ms apart, not one shared deficit
+            assert len(hints) == 3 and all(abs(b - a - 500) <= 20 for a, b in zip(hints, hints[1:])), hints
             await c.doc_put("acct", "db", "c", "late", '{"a": 2}')  # retried transparently
             assert c.throttled_retries >= 1
             st = await c.doc_stats("acct", "db", "c")

@@ -610,7 +610,21 @@ def test_gpu_radix_pair_sort_matches_stable_argsort(n):
         got = k._sorted_rows(torch.from_numpy(keys.view(np.int64)).to(k.device), torch.from_numpy(rows).to(k.device),
                              end_bit)
         assert np.array_equal(got.cpu().numpy(), want), (n, end_bit)
-    k.check_sort()
+    assert k.check_sort()
+
+
+def test_sort_fault_is_cleared_and_reported_once():
+    """A look-back timeout in the device sort costs the query it hit its device ordering (the
+    caller then orders on the host), not every later query."""
+    import torch
+
+    from aca_dotnet_workshop_amd.ops.gpu import GpuKernels
+    k = GpuKernels.__new__(GpuKernels)
+    k.torch = torch
+    assert k.check_sort()  # no sort yet
+    k._sort_fault = torch.tensor([2], dtype=torch.int32)
+    assert not k.check_sort() and k.sort_faults == 1
+    assert k.check_sort() and int(k._sort_fault.item()) == 0
 
 
 @pytest.mark.gpu

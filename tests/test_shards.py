@@ -60,6 +60,23 @@ def test_merge_pages_offsets():
     assert [r["key"] for r in merge_pages(q2, pages2, [0, 0])["results"]] == ["x", "y", "m"]
 
 
+def test_merge_pages_stops_where_a_short_shard_page_runs_out():
+    """A k-way PAGED merge: shard 0 sent a short page (its mirror skipped stale
+    rows) with a token, so its unfetched matches may sort before shard 1's -- the merged page
+    ends when shard 0's entries run out, and shard 0 resumes at the position IT named."""
+    q = {"sort": [{"key": "v", "order": "ASC"}], "page": {"limit": 3}}
+    pages = [(0, {"results": [{"key": "a", "data": {"v": 1}}], "token": "3"}),
+             (1, {"results": [{"key": "c", "data": {"v": 2}}, {"key": "d", "data": {"v": 3}},
+                              {"key": "e", "data": {"v": 4}}], "token": "3"})]
+    out = merge_pages(q, pages, [0, 0])
+    assert [r["key"] for r in out["results"]] == ["a"]
+    assert decode_token(out["token"], 2) == [3, 0]
+    # an empty page with a token: nothing can be merged yet, but the shard still moves on
+    pages = [(0, {"results": [], "token": "6"}), pages[1]]
+    out = merge_pages(q, pages, [3, 0])
+    assert out["results"] == [] and decode_token(out["token"], 2) == [6, 0]
+
+
 def _task(i: int) -> dict:
     return {"taskId": f"00000000-0000-4000-8000-{i:012d}", "taskName": f"Task {i % 17}",
             "taskCreatedBy": f"user{i % 5}@x", "taskCreatedOn": f"2026-10-{1 + i % 28:02d}T{i // 3600 % 24:02d}:{i % 60:02d}:{i // 60 % 60:02d}",
