@@ -355,10 +355,15 @@ class BackingServices:
             if (t := throttled(req, s, s.write_ru(len(req.body)))) is not None:
                 return t
             ops = []
-            for o in (req.json() or {}).get("ops", []):
+            raw_ops = (req.json() or {}).get("ops", [])
+            # each value stored as the request's own compact bytes (numbers and escapes as sent),
+            # the same text a save or a bulk save of that value stores
+            texts = self.N.tx_values(req.body) if len(req.body) else None
+            if texts is None or len(texts) != len(raw_ops):
+                texts = [v if isinstance(v := o.get("value"), str) else _compact_json(v) for o in raw_ops]
+            for o, text in zip(raw_ops, texts):
                 is_del = o.get("op") == "delete"
-                val = o.get("value")
-                ops.append(self.N.TxOp(is_del, o["key"], "" if is_del else (val if isinstance(val, str) else _compact_json(val)),
+                ops.append(self.N.TxOp(is_del, o["key"], "" if is_del else text,
                                        o.get("etag") or None, bool(o.get("firstWrite")), int(o.get("ttlMs") or 0)))
             try:
                 s.transact(ops)

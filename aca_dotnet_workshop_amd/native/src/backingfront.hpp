@@ -121,11 +121,44 @@ inline bool scan_bulk_items(const std::string& body, std::vector<DocStore::BulkI
 // JSON string value: the JSON text it holds; anything else: its compact text), for the items
 // the front leaves to Python (TTL writes) -- both paths store the same bytes.  false: not a
 // valid array of objects (Python answers).
+inline bool scan_value_array(const char* p, const char* e, std::vector<std::string>& out);
+
 inline bool scan_bulk_values(const std::string& body, std::vector<std::string>& out) {
   std::string_view text = body.empty() ? std::string_view("[]") : std::string_view(body);
   if (!valid(text)) return false;
-  const char* p = ws_end(text.data(), text.data() + text.size());
+  return scan_value_array(ws_end(text.data(), text.data() + text.size()), text.data() + text.size(), out);
+}
+
+// The same for a transaction body (`{"ops": [{"op", "key", "value", ...}]}`): every op's value
+// as stored -- the request's own bytes, compacted -- so a transaction stores what a save does.
+inline bool scan_tx_values(const std::string& body, std::vector<std::string>& out) {
+  std::string_view text(body);
+  if (text.empty() || !valid(text)) return false;
   const char* e = text.data() + text.size();
+  const char* p = ws_end(text.data(), e);
+  if (*p != '{') return false;
+  ++p;
+  bool found = false;
+  while (true) {
+    p = ws_end(p, e);
+    if (*p == '}') return found;
+    const char* ks = p;
+    p = skip_value(p, e);
+    std::string_view ktok(ks, (size_t)(p - ks));
+    std::string k = ktok.find('\\') == std::string_view::npos ? std::string(ktok.substr(1, ktok.size() - 2))
+                                                             : parse(ktok).s;
+    p = ws_end(ws_end(p, e) + 1, e);  // ':'
+    if (k == "ops") {
+      out.clear();  // a repeated key: the last one wins, as in json.loads
+      if (!scan_value_array(p, e, out)) return false;
+      found = true;
+    }
+    p = ws_end(skip_value(p, e), e);
+    if (*p == ',') ++p;
+  }
+}
+
+inline bool scan_value_array(const char* p, const char* e, std::vector<std::string>& out) {
   if (*p != '[') return false;
   ++p;
   while (true) {

@@ -258,6 +258,16 @@ PYBIND11_MODULE(_ttnative, m) {
     return l;
   });
 
+  // transaction body -> the stored text of each op's value (backingfront.hpp scan_tx_values), or None.
+  m.def("tx_values", [](py::bytes body) -> py::object {
+    std::string b = body;
+    std::vector<std::string> vals;
+    if (!scan_tx_values(b, vals)) return py::none();
+    py::list l(vals.size());
+    for (size_t i = 0; i < vals.size(); ++i) l[i] = py::str(vals[i]);
+    return l;
+  });
+
   // The watchdog CPU duty cycle on a native thread (dutycycle.hpp; platform/limits.py).
   py::class_<DutyCycle>(m, "DutyCycle")
       .def(py::init<double>(), py::arg("period_s"))

@@ -160,6 +160,42 @@ def test_ttl_writes_store_the_same_bytes_as_native_writes(monkeypatch):
 
 
 @pytest.mark.parametrize("front", FRONTS)
+def test_transactions_store_the_same_bytes_as_saves(front, monkeypatch):
+    """A transaction's values are stored as the request's own compact bytes, like a save's: 1e3
+    stays 1e3, escapes stay escaped, a 20-digit integer keeps every digit (the
+    transaction route re-serialised them through json.dumps)."""
+    raw = b'{"n": 1e3, "f": -0.5E+2, "s": "caf\\u00e9 \\ud83d\\ude00", "big": 12345678901234567890}'
+    want = b'{"n":1e3,"f":-0.5E+2,"s":"caf\\u00e9 \\ud83d\\ude00","big":12345678901234567890}'
+
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.doc_put("acct", "db", "c", "seed", "0")
+            r = await c.http.post(b.base + "/cosmos/acct/db/c/bulkset", headers={"Content-Type": "application/json"},
+                                  body=b'[{"key": "saved", "value": %s}]' % raw)
+            assert r.status == 200, r.body
+            body = (b'{"ops": [{"op": "upsert", "key": "tx", "value": %s}, {"op": "delete", "key": "seed"}, '
+                    b'{"op": "upsert", "key": "tx-text", "value": "[1.50, \\"x\\"]"}]}' % raw)
+            r = await c.http.post(b.base + "/cosmos/acct/db/c/transaction", body=body,
+                                  headers={"Content-Type": "application/json"})
+            assert r.status == 204, r.body
+            assert (await c.doc_get("acct", "db", "c", "saved"))[0] == want
+            assert (await c.doc_get("acct", "db", "c", "tx"))[0] == want
+            assert (await c.doc_get("acct", "db", "c", "tx-text"))[0] == b'[1.50, "x"]'  # a string holds JSON text
+            assert await c.doc_get("acct", "db", "c", "seed") is None
+            await c.http.close()
+    run(main())
+
+
+def test_tx_values_scanner():
+    from aca_dotnet_workshop_amd import native
+    N = native.load()
+    assert N.tx_values(b'{"ops": [{"value": {"a" : 1e3}}, {"op": "delete"}, {"value": "\\"t\\""}]}') == \
+        ['{"a":1e3}', "null", '"t"']
+    assert N.tx_values(b'{"x": 1}') is None and N.tx_values(b"[1]") is None and N.tx_values(b"{bad") is None
+
+
+@pytest.mark.parametrize("front", FRONTS)
 def test_messaging_and_long_poll(front, monkeypatch):
     async def main():
         async with Backing(front, monkeypatch) as b:
