@@ -100,6 +100,9 @@ def parse() -> argparse.Namespace:
                     help="seconds of the secondary reference-envelope run (config.reference_envelope: the "
                          "manifest defaults -- 1/1 frontend/API, processor 1..5 on KEDA, 0.25 vCPU, 4000 RU/s -- "
                          "with the create's 302 followed to /Tasks/Index); 0 = skip")
+    ap.add_argument("--keda-messages", type=int, default=10000,
+                    help="messages of the envelope's KEDA stage (config.reference_envelope.keda: the module-9 load "
+                         "test, 1 s of simulated work each, processor 1..5 replicas); 0 = skip")
     ap.add_argument("--direct-steps", type=int, default=-1,
                     help="steps of the api_sidecar_direct comparison run (-1 = a quarter of --steps, 0 = skip)")
     return ap.parse_args()
@@ -920,6 +923,106 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         env.stop()
 
 
+def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cooldown_s: float = 15.0,
+               budget_s: float = 360.0) -> dict:
+    """The reference's module-9 load test, measured (docs/aca/09-aca-autoscale-keda/index.md:
+    192-216): ``deploy/main.yaml`` with its defaults -- the notifier with SendGrid off simulates
+    1 s of work per message (TasksNotifierController.cs:60-62), the processor scales 1..5 on the
+    KEDA Service Bus rule at 10 messages per replica (processor-backend-service.bicep:159-183) --
+    and ``messages`` tasksaved events published at 1 ms intervals (100 every 100 ms) through the
+    API's sidecar.  Sampled every 250 ms: the replica timeline 1 -> 5 -> 1, the time to 5
+    replicas, the drain time, and the subscription's counters (each message received and
+    completed exactly once).  Only KEDA's polling interval (30 s -> ``polling_s``) and cooldown
+    (300 s -> ``cooldown_s``) are shortened."""
+    import threading
+
+    from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
+    from aca_dotnet_workshop_amd.platform.manifest import load_manifest
+    from aca_dotnet_workshop_amd.web.client import HttpClient
+    m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
+                      {"kedaPollingIntervalSeconds": polling_s, "kedaCooldownPeriodSeconds": cooldown_s,
+                       "environmentName": f"cae-keda-r{rank}"})
+    env = BackgroundEnvironment(m, os.path.join(root, "keda"), log_level="warning")
+    entity = f"tasksavedtopic/subscriptions/{PROC}"
+    samples: list[tuple[float, int, int]] = []  # (s since the first publish, replicas, completed)
+    stop = threading.Event()
+    try:
+        env.start()
+        counts = f"{env.backing_url}/servicebus/taskstracker/counts?entity={entity}"
+        c0 = _counts(counts)
+        uds = env.replicas(API)[0].sidecar_uds
+        t0 = time.perf_counter()
+
+        def watch() -> None:
+            while not stop.wait(0.25):
+                rt = env.ctl.apps.get(PROC)
+                n = len([r for r in rt.current.replicas if r.alive()]) if rt and rt.current else 0
+                try:
+                    done = int(_counts(counts).get("completed", 0)) - int(c0.get("completed", 0))
+                except Exception:
+                    continue
+                samples.append((round(time.perf_counter() - t0, 2), n, done))
+        th = threading.Thread(target=watch, daemon=True)
+        th.start()
+
+        async def publish() -> None:  # 1 ms apart on average, like Service Bus Explorer's sender
+            c = HttpClient()
+            url = f"unix:{uds}:/v1.0-alpha1/publish/bulk/dapr-pubsub-servicebus/tasksavedtopic"
+            try:
+                for lo in range(0, messages, 100):
+                    entries = [{"entryId": str(i), "contentType": "application/json",
+                                "event": {"taskId": f"00000000-0000-4000-8000-{i:012d}", "taskName": f"Load test {i}",
+                                          "taskCreatedBy": "load@bench.local", "taskCreatedOn": "2030-01-01T00:00:00",
+                                          "taskDueDate": "2030-01-02T00:00:00", "taskAssignedTo": "a@bench.local",
+                                          "isCompleted": False, "isOverDue": False}}
+                               for i in range(lo, min(messages, lo + 100))]
+                    r = await c.post(url, json_body=entries, timeout=60)
+                    if r.status != 204:
+                        raise RuntimeError(f"bulk publish: {r.status} {r.body[:200]!r}")
+                    left = t0 + (lo + 100) / 1000.0 - time.perf_counter()
+                    if left > 0:
+                        await asyncio.sleep(left)
+            finally:
+                await c.close()
+        asyncio.run(publish())
+        sent_s = time.perf_counter() - t0
+        while time.perf_counter() - t0 < budget_s:  # drained, then scaled back in to one replica
+            time.sleep(0.5)
+            if samples and samples[-1][2] >= messages and samples[-1][1] <= 1 and max(s[1] for s in samples) > 1:
+                break
+        stop.set()
+        th.join(5)
+        c1 = _counts(counts)
+        delta = {k: int(c1.get(k, 0)) - int(c0.get(k, 0)) for k in ("enqueued", "received", "completed", "dead_letter")}
+        timeline, last = [], None
+        for t, n, _ in samples:
+            if n != last:
+                timeline.append([t, n])
+                last = n
+        peak = max((n for _, n, _ in samples), default=0)
+        t_peak = next((t for t, n, _ in samples if n == peak), None)
+        t_drain = next((t for t, _, done in samples if done >= messages), None)
+        t_in = next((t for t, n, _ in samples if t_drain is not None and t >= t_drain and n <= 1), None)
+        ev = (env.ctl.apps[PROC].scale_events if env.ctl else [])
+        return {"messages": messages, "published_in_s": round(sent_s, 2), "peak_replicas": peak,
+                "time_to_peak_s": t_peak, "drain_s": t_drain, "scaled_in_to_1_s": t_in,
+                "replica_timeline": timeline,  # [seconds since the first publish, replicas], on change
+                "scale_events": [e["replicas"] for e in ev],
+                "counts": delta,
+                "exactly_once": delta["enqueued"] == delta["received"] == delta["completed"] == messages
+                                and delta["dead_letter"] == 0,
+                "rule": "azure-servicebus, messageCount 10, replicas 1..5 (processor-backend-service.bicep:159-183)",
+                "work_per_message_ms": 1000, "keda_polling_s": polling_s, "keda_cooldown_s": cooldown_s,
+                "note": "reference: 10,000 messages at 1 ms intervals, 1 s simulated work, expects 5 replicas "
+                        "(docs/aca/09-aca-autoscale-keda/index.md:192-216); polling 30 s and cooldown 300 s "
+                        "shortened so the cycle fits the run"}
+    except Exception as e:  # reported, not fatal to the headline
+        return {"error": repr(e)[:500], "replica_timeline": samples[-20:]}
+    finally:
+        stop.set()
+        env.stop()
+
+
 def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     import shutil
     import tempfile
@@ -1099,6 +1202,10 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                 progress(f"reference envelope: {a.envelope_s:g} s")
                 envelope = reference_envelope(exe, root, a.envelope_s, d.rank)
                 progress("reference envelope done")
+                if a.keda_messages > 0:
+                    progress(f"KEDA scale-out: {a.keda_messages} messages with 1 s of work each")
+                    envelope["keda"] = keda_stage(root, d.rank, a.keda_messages)
+                    progress("KEDA stage done")
             d.barrier()
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0

@@ -34,7 +34,8 @@ def _check(line: dict, n: int, steps: int, warmup: int) -> None:
 def test_bench_single_process():
     env = dict(os.environ, PYTHONPATH=str(ROOT))
     r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32",
-                        "--api-replicas", "1", "--processor-replicas", "1", "--envelope-s", "4"],
+                        "--api-replicas", "1", "--processor-replicas", "1", "--envelope-s", "4",
+                        "--keda-messages", "300"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -60,6 +61,10 @@ def test_bench_single_process():
     assert ev["lists_followed"] == ev["tasks"] and ev["list_latency_ms"]["p50"] > 0
     assert ev["failed_creates"] + ev["failed_lists"] == ev["errors"]
     assert ev["processor_replicas_reached"] >= 1 and ev["ru_per_task"] > 5
+    # the module-9 load test: the backlog scales the processor 1 -> 5 -> 1, each message once
+    k = ev["keda"]
+    assert k["peak_replicas"] == 5 and k["exactly_once"] and k["counts"]["completed"] == 300, k
+    assert k["replica_timeline"][0][1] == 1 and k["replica_timeline"][-1][1] == 1 and k["scaled_in_to_1_s"] > k["drain_s"]
 
 
 def test_thread_cpu_and_hot_threads():
