@@ -234,11 +234,13 @@ def conditional_mark_wire(got: bytes) -> tuple[list[str], bytes, int] | None:
     return ids, json.dumps(items, separators=(",", ":")).encode(), skipped
 
 
-def tasks_from_query_wire(body: bytes, by_created: bool = False) -> tuple[int, bytes, bool] | None:
+def tasks_from_query_wire(body: bytes, by_created: bool = False,
+                          descending: bool = False) -> tuple[int, bytes, bool] | None:
     """State-query response -> (tasks, TaskModel JSON array of the results with data, whether the
     response carries a continuation token), each task written like ``to_wire()``; in result
     order, or with ``by_created`` ordered by ``TaskCreatedOn`` as a DateTime (ascending, stable:
-    the reference's ``OrderBy``, TasksStoreManager.cs:136).  ``None``: bind with ``TaskModel``."""
+    the reference's ``OrderBy``, TasksStoreManager.cs:136; ``descending``: newest first, stable,
+    its ``OrderByDescending``, :66).  ``None``: bind with ``TaskModel``."""
     global _native_query
     if _native_query is None:
         try:
@@ -246,7 +248,7 @@ def tasks_from_query_wire(body: bytes, by_created: bool = False) -> tuple[int, b
             _native_query = load().tasks_from_query
         except Exception:
             _native_query = False
-    return _native_query(body, by_created) if _native_query else None
+    return _native_query(body, by_created, descending) if _native_query else None
 
 
 _native_query: Any = None

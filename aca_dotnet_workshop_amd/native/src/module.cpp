@@ -423,16 +423,17 @@ PYBIND11_MODULE(_ttnative, m) {
 
   // state-query response -> (task count, TaskModel JSON array, has a continuation token) or None
   // (taskcodec.hpp query_tasks); `by_created`: ordered by TaskCreatedOn as a DateTime.
-  m.def("tasks_from_query", [](py::bytes body, bool by_created) -> py::object {
+  m.def("tasks_from_query", [](py::bytes body, bool by_created, bool descending) -> py::object {
     char* p;
     Py_ssize_t n;
     if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
     std::string out;
     size_t count = 0;
     bool more = false;
-    if (!taskcodec::query_tasks(std::string_view(p, (size_t)n), out, count, by_created, &more)) return py::none();
+    if (!taskcodec::query_tasks(std::string_view(p, (size_t)n), out, count, by_created, &more, descending))
+      return py::none();
     return py::make_tuple(count, py::bytes(out), more);
-  }, py::arg("body"), py::arg("by_created") = false);
+  }, py::arg("body"), py::arg("by_created") = false, py::arg("descending") = false);
 
   // A JSON array -> its items re-grouped into arrays of at most `n` items (raw slices, no
   // re-encoding), or None when the text is not a valid JSON array (the processor's chunked

@@ -598,12 +598,13 @@ inline uint64_t created_key(std::string_view c) {
 // State-query response of the task collection (Dapr `{"results": [{"key", "data", "etag"}],
 // "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data: the API's
 // GET api/overduetasks page (TasksStoreManager.GetYesterdaysDueTasks, range sweep).  With
-// `by_created` the tasks come out ordered by TaskCreatedOn as a DateTime, ascending and stable
+// `by_created` the tasks come out ordered by TaskCreatedOn as a DateTime, ascending (or with
+// `descending`, newest first: the GET api/tasks list) and stable
 // (the reference's `.OrderBy(o => o.TaskCreatedOn)`, TasksStoreManager.cs:136): System.Text.Json
 // trims the fraction, so the strings do not sort chronologically within one second ("...:42Z"
 // is earlier than "...:42.1Z").  `more`: the response carries a continuation token.
 inline bool query_tasks(std::string_view body, std::string& out, size_t& count, bool by_created = false,
-                        bool* more = nullptr) {
+                        bool* more = nullptr, bool descending = false) {
   if (!valid_utf8(body)) return false;
   tt::Value doc;
   try {
@@ -658,7 +659,12 @@ inline bool query_tasks(std::string_view body, std::string& out, size_t& count, 
     if (c == std::string::npos) return false;
     rows.push_back({created_key(std::string_view(buf).substr(c + tag.size())), at, buf.size() - at});
   }
-  std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.key < b.key; });
+  // `descending`: newest first, ties in result order -- the reference's list,
+  // `.OrderByDescending(o => o.TaskCreatedOn)` (TasksStoreManager.cs:66), is a stable sort too
+  if (descending)
+    std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.key > b.key; });
+  else
+    std::stable_sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) { return a.key < b.key; });
   out.assign("[");
   out.reserve(buf.size() + rows.size() + 2);
   for (const Row& r : rows) {

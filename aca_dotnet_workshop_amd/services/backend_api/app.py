@@ -55,11 +55,17 @@ def _json(body: bytes, status: int = 200) -> Response:
 
 
 def register_controllers(app: WebApp, manager: TasksManager) -> None:
+    fast_list = getattr(manager, "tasks_by_creator_json", None)
     # -- TasksController (reference Controllers/TasksController.cs) --------------
     @app.route("/api/tasks", ("GET",), name="GetTasks", query=["createdBy"], tag="Tasks",
                responses={200: [TaskModel]})
     async def get_tasks(req: Request) -> Response:
-        return _json(tasks_to_json(await manager.get_tasks_by_creator(req.query_get("createdBy") or "")))
+        created_by = req.query_get("createdBy") or ""
+        if fast_list is not None:
+            body = await fast_list(created_by)
+            if body is not None:
+                return _json(body)
+        return _json(tasks_to_json(await manager.get_tasks_by_creator(created_by)))
 
     @app.route("/api/tasks/{taskId}", ("GET",), name="GetTask", tag="Tasks", responses={200: TaskModel, 404: None})
     async def get_task(req: Request) -> Response:

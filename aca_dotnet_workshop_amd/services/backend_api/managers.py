@@ -238,6 +238,21 @@ class TasksStoreManager(TasksManager):
         tasks.sort(key=_created_key, reverse=True)
         return tasks
 
+    async def tasks_by_creator_json(self, created_by: str) -> bytes | None:
+        """``get_tasks_by_creator`` as the response body: the query's results turned into the
+        TaskModel JSON array newest first in one native pass (``tasks_from_query_wire``, the
+        reference's ``OrderByDescending(o => o.TaskCreatedOn)``, TasksStoreManager.cs:54-69) --
+        no TaskModel per task.  ``None``: a response outside the codec's envelope (the caller
+        binds the TaskModels), or no raw query on this client."""
+        raw_query = getattr(self.client, "query_state_raw", None)
+        if raw_query is None:
+            return None
+        if not created_by:
+            return b"[]"
+        raw = await raw_query(self.store, {"filter": {"EQ": {"taskCreatedBy": created_by}}})
+        made = tasks_from_query_wire(raw, by_created=True, descending=True)
+        return made[1] if made is not None else None
+
     async def _read_modify_write(self, task_id: uuid.UUID, mutate) -> TaskModel | None:
         for _ in range(self.max_retries):
             data, etag = await self.client.get_state_and_etag(self.store, str(task_id))

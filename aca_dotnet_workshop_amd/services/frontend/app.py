@@ -126,6 +126,8 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
     env.filters["ddmmyyyy"] = _fmt_date
     env.filters["inputdate"] = _input_date
     app.mount_static("/", HERE / "wwwroot")
+    from .rows import RowRenderer
+    rows = RowRenderer(env)  # Tasks/Index's rows compiled from the template's own task_row macro
 
     def render(req: Request, name: str, status: int = 200, **ctx: Any) -> Response:
         resp = Response(b"", status, None, "text/html; charset=utf-8")
@@ -172,8 +174,11 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
         created_by = req.cookies.get(COOKIE)
         if not created_by:
             return redirect("/")
-        tasks = tasks_from_json(await gw.call("GET", f"api/tasks?createdBy={quote(created_by)}"))
-        return render(req, "tasks_index.html", tasks=tasks, created_by=created_by)
+        data = await gw.call("GET", f"api/tasks?createdBy={quote(created_by)}")
+        fast = rows.render(data)
+        if fast is not None:
+            return render(req, "tasks_index.html", rows_html=fast, created_by=created_by)
+        return render(req, "tasks_index.html", tasks=tasks_from_json(data), created_by=created_by)
 
     @app.route("/Tasks/Index", ("POST",), name="TasksIndexPost", include_in_schema=False)
     async def tasks_index_post(req: Request) -> Response:

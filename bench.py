@@ -103,6 +103,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--keda-messages", type=int, default=10000,
                     help="messages of the envelope's KEDA stage (config.reference_envelope.keda: the module-9 load "
                          "test, 1 s of simulated work each, processor 1..5 replicas); 0 = skip")
+    ap.add_argument("--browser-steps", type=int, default=-1,
+                    help="steps of the browser_flow read-path run (create + the 302 followed to Tasks/Index, "
+                         "per-user cookies; -1 = a quarter of --steps, 0 = skip)")
     ap.add_argument("--direct-steps", type=int, default=-1,
                     help="steps of the api_sidecar_direct comparison run (-1 = a quarter of --steps, 0 = skip)")
     return ap.parse_args()
@@ -691,7 +694,7 @@ def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
 
 def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int, batch: int,
                      conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
-                     ca_file: str | None = None, threads: int = 1) -> tuple[float, dict]:
+                     ca_file: str | None = None, threads: int = 1, extra: list[str] | None = None) -> tuple[float, dict]:
     """``targets``: ``host:port`` (a frontend replica) or ``https://host:port`` (the external
     ingress; ``ca_file`` -- the environment CA -- verifies its certificate like a browser)."""
     import subprocess
@@ -705,6 +708,7 @@ def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str 
         cmd += ["--tls-ca", ca_file]
     if threads > 1:
         cmd += ["--threads", str(threads)]
+    cmd += extra or []
     for t in targets:
         cmd += ["--target", t]
     t0 = time.perf_counter()
@@ -733,6 +737,10 @@ def _cpu_by_role(stack) -> dict[str, float]:
 # headline's create rate with room to spare, and stays within the device top-k (kPageCap 8192).
 # At 1000 a faster box crossed into two pages per sweep and doubled it (profiles/r4_sweep_tail.md)
 OVERDUE_PAGE = 4096
+
+# identities of the browser_flow run: each user's task list stays small (the reference lists a
+# user's whole history on every page view)
+BROWSER_USERS = 4096
 
 # cores held back for the external ingress when load enters through it (uncapped, like Envoy)
 INGRESS_RESERVE = 1.0
@@ -1175,6 +1183,29 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             delivery = {"enqueued": c.get("enqueued"), "completed": c.get("completed"), "received": c.get("received"),
                         "dead_lettered": c.get("dead_letter"), "expected": sent,
                         "exactly_once": c.get("completed") == c.get("received") == c.get("enqueued") == sent}
+        # the read path at the headline's replica counts: browsers with their own
+        # identity cookie (bounded task lists) post Create and follow its 302 to Tasks/Index,
+        # which lists the user's tasks through the API (Index.cshtml.cs:48 -> TasksController.Get)
+        browser = None
+        bsteps = 0 if shared else a.browser_steps if a.browser_steps >= 0 else max(1, a.steps // 4)
+        if bsteps:
+            progress(f"browser_flow: {bsteps} steps of create + follow to Tasks/Index")
+            af = "; ".join(c for c in cookie.split("; ") if not c.startswith("TasksCreatedByCookie="))
+            bb = os.path.join(root, "browser-bodies.txt")
+            with open(bb, "wb") as f:
+                f.write(b"\n".join(_form_bodies(a.batch, token, 0)) + b"\n")
+            bdt, brep = run_form_loadgen(exe, targets, f"TasksCreatedByCookie={{user}}; {af}", counts_url, bsteps,
+                                         a.batch, conc, bb, None, ca_file, 1,
+                                         ["--users", str(BROWSER_USERS), "--follow"])
+            sc = brep.get("status_counts") or {}
+            browser = {"flows_per_s": round(a.batch * bsteps / bdt, 1), "pages_per_s": round(2 * a.batch * bsteps / bdt, 1),
+                       "steps": bsteps, "users": BROWSER_USERS, "concurrency": conc,
+                       "create_latency_ms": brep.get("latency_ms"), "list_latency_ms": brep.get("follow_latency_ms"),
+                       "lists": brep.get("follow_requests"), "status_counts": sc, "errors": brep.get("errors"),
+                       "first_error": brep.get("first_error") or None,
+                       "tasks_per_user_at_end": round(a.batch * bsteps / BROWSER_USERS, 1),
+                       "note": "POST /Tasks/Create (302) then GET /Tasks/Index with the user's cookie: the API "
+                               "queries the store by creator, newest first; one flow = both pages"}
         # the same environment, load straight at the API sidecars' invoke (round 2's topology);
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
@@ -1253,7 +1284,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
-                           "overdue_sweeps": sweep_info, "api_sidecar_direct": direct,
+                           "overdue_sweeps": sweep_info, "browser_flow": browser, "api_sidecar_direct": direct,
                            "reference_envelope": envelope}}), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():

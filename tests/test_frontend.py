@@ -1,5 +1,7 @@
 """Frontend variants: module-2 direct HTTP mode (named HttpClient on BaseUrlExternalHttp) and
 the production error page."""
+import json
+
 import pytest
 
 from aca_dotnet_workshop_amd.services.backend_api import FakeTasksManager
@@ -120,3 +122,50 @@ def test_native_create_post_is_taken_for_a_browser_post():
     import json
     assert made[0] and json.loads(made[1]) == {"taskName": "Buy milk", "taskCreatedBy": "me@x.y",
                                                "taskDueDate": "2030-01-01T00:00:00", "taskAssignedTo": "a@b.c"}
+
+
+def _row_renderer():
+    import os
+
+    from jinja2 import Environment, FileSystemLoader, select_autoescape
+
+    import aca_dotnet_workshop_amd.services.frontend.app as fa
+    from aca_dotnet_workshop_amd.services.frontend.rows import RowRenderer
+    env = Environment(loader=FileSystemLoader(os.path.join(os.path.dirname(fa.__file__), "templates")),
+                      autoescape=select_autoescape(["html"]))
+    env.filters["ddmmyyyy"] = fa._fmt_date
+    env.filters["inputdate"] = fa._input_date
+    return env, RowRenderer(env)
+
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.lists(st.tuples(st.text(max_size=12), st.text(max_size=12), st.booleans(), st.booleans(),
+                          st.datetimes(), st.uuids()), max_size=6))
+def test_task_rows_fast_path_equals_the_template(rows):
+    """Tasks/Index's rows compiled from the task_row macro (services/frontend/rows.py) render
+    byte for byte what the template renders from bound TaskModels, escaping included."""
+    from aca_dotnet_workshop_amd.models import TaskModel
+    env, r = _row_renderer()
+    assert r.ok
+    tpl = env.get_template("tasks_index.html")
+    items = [TaskModel(task_id=u, task_name=n, task_assigned_to=a, task_due_date=due, is_completed=c,
+                       is_over_due=o).to_wire() for n, a, c, o, due, u in rows]
+    items = json.loads(json.dumps(items))  # as the SDK hands the API's answer to the page
+    fast = r.render(items)
+    assert fast is not None
+    ctx = dict(af_field="f", af_token="t", request=None, created_by="u@x", title="T")
+    assert tpl.render(rows_html=fast, **ctx) == tpl.render(tasks=[TaskModel.model_validate(d) for d in items], **ctx)
+
+
+def test_task_rows_fast_path_declines_other_shapes():
+    _, r = _row_renderer()
+    good = {"taskId": "0f8fad5b-d9cb-469f-a165-70867728950e", "taskName": "n", "taskAssignedTo": "a",
+            "taskDueDate": "2026-01-02T00:00:00", "isCompleted": False, "isOverDue": False}
+    assert r.render([good]) is not None
+    for bad in ({**good, "taskId": good["taskId"].upper()}, {**good, "taskDueDate": "2026-01-02T00:00:00+02:00"},
+                {**good, "isCompleted": 0}, {**good, "taskName": None}, "x"):
+        assert r.render([good, bad]) is None

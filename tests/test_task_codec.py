@@ -335,6 +335,15 @@ def test_query_results_created_order_matches_datetime_order(stamps):
     want = [i for i, _ in sorted(enumerate(results),
                                  key=lambda x: naive_utc(TaskModel.model_validate(x[1]["data"]).task_created_on))]
     assert got == want
+    # descending (GET api/tasks: newest first) equals the binder path's stable reverse sort
+    # (managers.get_tasks_by_creator: ``tasks.sort(key=_created_key, reverse=True)``), byte for byte
+    from aca_dotnet_workshop_amd.models import tasks_to_json
+    from aca_dotnet_workshop_amd.services.backend_api.managers import _created_key
+    body = json.dumps({"results": results + [{"key": "gone", "data": None}]}).encode()
+    made = tasks_from_query_wire(body, by_created=True, descending=True)
+    ref = [TaskModel.model_validate(r["data"]) for r in results]
+    ref.sort(key=_created_key, reverse=True)
+    assert made[1] == tasks_to_json(ref)
 
 
 @pytest.mark.parametrize("body", [b"[]", b'{"results": 5}', b'{"results": [{"data": "text"}]}',
