@@ -56,6 +56,8 @@ def _json(body: bytes, status: int = 200) -> Response:
 
 def register_controllers(app: WebApp, manager: TasksManager) -> None:
     fast_list = getattr(manager, "tasks_by_creator_json", None)
+    if os.environ.get("TT_READ_PATH", "").lower() == "bind":  # A/B: bind a TaskModel per task
+        fast_list = None
     # -- TasksController (reference Controllers/TasksController.cs) --------------
     @app.route("/api/tasks", ("GET",), name="GetTasks", query=["createdBy"], tag="Tasks",
                responses={200: [TaskModel]})

@@ -128,6 +128,8 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
     app.mount_static("/", HERE / "wwwroot")
     from .rows import RowRenderer
     rows = RowRenderer(env)  # Tasks/Index's rows compiled from the template's own task_row macro
+    if os.environ.get("TT_READ_PATH", "").lower() == "bind":  # A/B: TaskModel per task + template loop
+        rows.ok = False
 
     def render(req: Request, name: str, status: int = 200, **ctx: Any) -> Response:
         resp = Response(b"", status, None, "text/html; charset=utf-8")
