@@ -752,7 +752,10 @@ def _compact_json(v) -> str:
     return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
 
 async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | None = None,
-                        policy: dict[str, Any] | None = None, ready=None, stop: asyncio.Event | None = None) -> None:
+                        policy: dict[str, Any] | None = None, ready=None, stop: asyncio.Event | None = None,
+                        uds: str | None = None) -> None:
+    """``uds``: serve on that Unix socket too (the environment's processes on this host use it:
+    ``TT_BACKING_UDS``, sidecar/base.py)."""
     from ..web.server import HttpServer
     svc = BackingServices(data_dir, AccessPolicy.from_dict(policy))
     app = svc.build_app()
@@ -766,11 +769,13 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         # 4 shards: with 2, the front's loops were the stack's busiest threads (72-78 %) under the
         # headline, and 4 measured +8 % tasks/s (profiles/r4_hot_threads.md)
         threads = int(os.environ.get("TT_BACKING_FRONT_THREADS", "4"))
-        front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"), threads)
+        front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"), threads, uds or "")
         svc.attach_front(front)
         bound = front.port()
     else:
         bound = await srv.listen_tcp(host, port)
+        if uds:
+            await srv.listen_unix(uds)
     log.info("backing services listening on %s:%d (data=%s, front=%s)", host, bound, data_dir,
              "native" if front is not None else "python")
     if svc.mirror_paths and svc.accel_mode in ("auto", "gpu"):
@@ -805,6 +810,7 @@ def main(argv: list[str] | None = None) -> None:
     ap.add_argument("--data-dir", default=None)
     ap.add_argument("--policy", default=None, help="JSON file with access policy (mode/keys/roleAssignments)")
     ap.add_argument("--port-file", default=None)
+    ap.add_argument("--uds", default=None, help="also serve on this Unix socket (processes on this host)")
     a = ap.parse_args(argv)
     # queries run on worker threads next to the event loop; every native call that releases the
     # GIL (mirror sync, result assembly, device copies) waits for it again, up to the switch
@@ -822,7 +828,7 @@ def main(argv: list[str] | None = None) -> None:
 
     try:
         with maybe_profile(f"backing-{os.path.basename(a.port_file or str(a.port))}"):
-            asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready))
+            asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready, uds=a.uds))
     except KeyboardInterrupt:
         pass
 

@@ -192,7 +192,11 @@ inline bool scan_value_array(const char* p, const char* e, std::vector<std::stri
 class BackingFront {
  public:
   // `threads` event loops share the port via SO_REUSEPORT (connections are spread by the kernel).
-  BackingFront(const std::string& host, int port, const std::string& fallback_uds, int threads = 1)
+  // `uds`: also serve on this Unix socket -- the environment's processes on this host reach the
+  // backing over it (a local stream socket costs about half a loopback TCP exchange's CPU); the
+  // shards share the one listening socket (EPOLLEXCLUSIVE: one loop is woken per connection).
+  BackingFront(const std::string& host, int port, const std::string& fallback_uds, int threads = 1,
+               const std::string& uds = "")
       : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)) {
     ev::reserve_fd_table();  // accept() must not grow the fd table (RCU wait) under load
     threads = std::max(1, std::min(threads, 64));
@@ -206,6 +210,18 @@ class BackingFront {
       if (ep.port == 0) ep.port = p;  // the other shards join the port the first one got
     }
     port_ = ep.port;
+    if (!uds.empty()) {
+      ev::Endpoint u;
+      u.path = uds;
+      int unused = 0;
+      int fd = ev::bind_listen(u, false, unused);
+      for (size_t i = 0; i < shards_.size(); ++i) {
+        int f = i == 0 ? fd : ::fcntl(fd, F_DUPFD_CLOEXEC, 0);
+        if (f < 0) break;
+        auto l = std::make_shared<ev::Listener>(shards_[i]->loop, f, shards_[i]->handler);
+        shards_[i]->loop.add(l, EPOLLIN | EPOLLEXCLUSIVE);
+      }
+    }
     for (auto& sh : shards_) sh->start();
   }
   ~BackingFront() { stop(); }

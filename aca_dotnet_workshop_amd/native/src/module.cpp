@@ -735,8 +735,8 @@ PYBIND11_MODULE(_ttnative, m) {
   // document / message routes on its own thread against the engines attached here and
   // forwards everything else to the Python server on `fallback_uds`.
   py::class_<BackingFront>(m, "BackingFront")
-      .def(py::init<const std::string&, int, const std::string&, int>(), py::arg("host"), py::arg("port"),
-           py::arg("fallback_uds"), py::arg("threads") = 1)
+      .def(py::init<const std::string&, int, const std::string&, int, const std::string&>(), py::arg("host"),
+           py::arg("port"), py::arg("fallback_uds"), py::arg("threads") = 1, py::arg("uds") = "")
       .def("port", &BackingFront::port)
       .def("threads", &BackingFront::threads)
       .def("attach_store",

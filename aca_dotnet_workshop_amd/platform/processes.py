@@ -96,6 +96,7 @@ class LocalStack:
         if pf.exists():
             pf.unlink()
         args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
+        args += self._uds_args("")
         if data_dir:
             args += ["--data-dir", data_dir]
         if policy:
@@ -143,12 +144,29 @@ class LocalStack:
         if pf.exists():
             pf.unlink()
         args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
-        p = self._spawn(args, self.base_env, f"backing-{tag}")
+        uds = self._uds_args(tag)
+        p = self._spawn(args + uds, self.base_env, f"backing-{tag}")
         url = f"http://127.0.0.1:{_wait_file(pf, timeout, p)}"
         for f in families:
             self.extra_backing[f] = (p, url)
             self.base_env[f"TT_BACKING_URL_{f}"] = url
+            if uds:
+                self.base_env[f"TT_BACKING_UDS_{f}"] = uds[1]
         return url
+
+    def _uds_args(self, tag: str) -> list[str]:
+        """The backing process also serves on a Unix socket in this stack's socket dir; the
+        replicas started afterwards reach it there (``TT_BACKING_UDS``, sidecar/base.py) while
+        the TCP URL stays the environment's address for everything else.  ``TT_BACKING_TRANSPORT=
+        tcp`` keeps every process on TCP."""
+        if os.environ.get("TT_BACKING_TRANSPORT", "uds").lower() == "tcp":
+            return []
+        path = str(self.sock_dir / (f"backing-{tag}.sock" if tag else "backing.sock"))
+        if len(path.encode()) >= 104:
+            return []
+        if not tag:
+            self.base_env["TT_BACKING_UDS"] = path
+        return ["--uds", path]
 
     def shared_info(self) -> dict[str, Any]:
         """What another stack needs to join this one's backing services and name registry."""

@@ -32,6 +32,13 @@ class RuntimeContext:
         rank order) make the store / broker partitioned over several backings."""
         family = service_family(comp.type)
         base = comp.get("ttBackingUrl") or self.environ.get(f"TT_BACKING_URL_{family}") or self.backing_url
+        if not comp.get("ttBackingUrl"):
+            # the same backing process on this host's Unix socket (platform/processes.py): the
+            # data path's exchanges skip the loopback TCP stack
+            uds = self.environ.get(f"TT_BACKING_UDS_{family}") if self.environ.get(f"TT_BACKING_URL_{family}") \
+                else self.environ.get("TT_BACKING_UDS") if base == self.environ.get("TT_BACKING_URL") else None
+            if uds:
+                base = f"unix:{uds}:"
         if not comp.get("ttBackingUrl") and family in PARTITIONED_FAMILIES:
             urls = shard_urls(self.environ, family)
             if urls:  # a partitioned collection / namespace (backing/shards.py)
