@@ -73,6 +73,63 @@ struct Event {
   std::string line;     // LOG: the finished JSON line, when the route has its sink's prefix
 };
 
+// Text the Python definitions hand a native route (a log template, a Location): "%s" slots
+// filled in order from named fields of the request's task, "%%" a percent sign.  Compiled when
+// the route is registered; a template the route cannot fill (another directive, a field it does
+// not know, a slot count that differs from the fields) refuses the route -- Python serves it.
+struct Template {
+  enum Field { kId = 0, kName = 1, kAssignedTo = 2 };
+  std::vector<std::string> lits;  // fields.size() + 1 literal pieces
+  std::vector<int> fields;
+  bool set = false;
+
+  static Template compile(const std::string& text, const std::string& args) {
+    Template t;
+    t.set = true;
+    std::vector<int> names;
+    for (size_t a = 0; a < args.size();) {
+      size_t b = args.find(',', a);
+      std::string f = args.substr(a, b == std::string::npos ? std::string::npos : b - a);
+      if (f == "id") names.push_back(kId);
+      else if (f == "name") names.push_back(kName);
+      else if (f == "assigned_to") names.push_back(kAssignedTo);
+      else throw std::invalid_argument("native route template: unknown field " + f);
+      if (b == std::string::npos) break;
+      a = b + 1;
+    }
+    std::string cur;
+    for (size_t i = 0; i < text.size(); ++i) {
+      if (text[i] != '%') {
+        cur += text[i];
+        continue;
+      }
+      char d = i + 1 < text.size() ? text[i + 1] : '\0';
+      ++i;
+      if (d == '%') {
+        cur += '%';
+      } else if (d == 's') {
+        t.lits.push_back(std::move(cur));
+        cur.clear();
+        if (t.fields.size() == names.size()) throw std::invalid_argument("native route template: more slots than fields");
+        t.fields.push_back(names[t.fields.size()]);
+      } else {
+        throw std::invalid_argument("native route template: only %s and %% are supported");
+      }
+    }
+    t.lits.push_back(std::move(cur));
+    if (t.fields.size() != names.size()) throw std::invalid_argument("native route template: fewer slots than fields");
+    return t;
+  }
+  std::string render(const std::string& id, const std::string& name, const std::string& assigned_to) const {
+    std::string out = lits[0];
+    for (size_t i = 0; i < fields.size(); ++i) {
+      out += fields[i] == kId ? id : fields[i] == kName ? name : assigned_to;
+      out += lits[i + 1];
+    }
+    return out;
+  }
+};
+
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
   enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3 };
@@ -84,10 +141,14 @@ struct NativeRoute {
   double timeout_s = 60;
   double sample_rate = 1.0;     // the app tracer's rate for new traces
   // kFrontendCreate: the Create page's post -> invoke the API -> 302
-  std::string af_key, af_cookie, id_cookie, invoke_target, location;
+  std::string af_key, af_cookie, id_cookie, invoke_target;
   // kApiCreate: POST api/tasks -> state save -> publish -> 201
   std::string save_target, publish_target, log_category;
   std::string log_prefix;  // '{"level":..,"role":..,"category":..' of the process's JSON sink, or ""
+  // from the Python definitions: the answer's status, content type and Location; the log lines
+  int status = 0;
+  std::string content_type;
+  Template location, log_save, log_publish, log_notify;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -305,13 +366,30 @@ class AppHost {
     r->af_cookie = get("af_cookie");
     r->id_cookie = get("id_cookie");
     r->invoke_target = get("invoke_target");
-    r->location = get("location");
     r->save_target = get("save_target");
     r->publish_target = get("publish_target");
     r->log_category = get("log_category");
     r->log_prefix = get("log_prefix");
     r->bounds = bounds;
     if (r->method.empty() || r->path.empty()) throw std::invalid_argument("a native route needs a method and a path");
+    // every status, Location and log line comes from the Python definition: a route without
+    // them is refused rather than answering with text of its own
+    if (get("status").empty()) throw std::invalid_argument("a native route needs the handler's status");
+    r->status = std::stoi(get("status"));
+    r->content_type = get("content_type");
+    if (r->kind == NativeRoute::kProcessorNotify) {
+      r->log_notify = Template::compile(get("log_notify"), get("log_notify_args"));
+    } else {
+      r->location = Template::compile(get("location"), get("location_args"));
+    }
+    if (r->kind == NativeRoute::kApiCreate) {
+      r->log_save = Template::compile(get("log_save"), get("log_save_args"));
+      r->log_publish = Template::compile(get("log_publish"), get("log_publish_args"));
+      if (get("log_save").empty() || get("log_publish").empty())
+        throw std::invalid_argument("api_create needs the manager's log templates");
+    }
+    if (r->kind == NativeRoute::kProcessorNotify && get("log_notify").empty())
+      throw std::invalid_argument("processor_notify needs the notifier's log template");
     auto p = std::make_shared<std::promise<int>>();
     auto f = p->get_future();
     post([this, server, r, p] {
@@ -558,10 +636,12 @@ class AppHost {
     NativeJob j;
     j.trace_id = tid;
     j.span_id = new_id(1);
-    log_event(*r, j, "Started processing message with Task Name '" + name + "'");
-    reply.send(200, {{"Content-Type", "text/plain; charset=utf-8"}},
-               "Started processing message with Task Name '" + name + "'");
-    r->record(200, ev::now_s() - t0);
+    std::string text = r->log_notify.render({}, name, {});
+    log_event(*r, j, text);
+    ev::HeaderList h;
+    if (!r->content_type.empty()) h.emplace_back("Content-Type", r->content_type);
+    reply.send(r->status, h, text);
+    r->record(r->status, ev::now_s() - t0);
     return true;
   }
 
@@ -611,22 +691,25 @@ class AppHost {
       client_.request(r->sidecar, "POST", r->invoke_target, j->out_headers, body, r->timeout_s,
                       [this, j](ev::ClientResult&& res) {
                         if (res.err || res.resp.status >= 300) return hand_over(*j, "invoke", res);
-                        finish(*j, 302, {{"Location", j->route->location}});
+                        const NativeRoute& r = *j->route;
+                        finish(*j, r.status, {{"Location", r.location.render({}, {}, {})}});
                       });
       return true;
     }
-    log_event(*r, *j, "Save a new task with name: '" + j->task.name + "' to state store");
+    log_event(*r, *j, r->log_save.render(j->task.id, j->task.name, j->task.assigned_to));
     client_.request(r->sidecar, "POST", r->save_target, j->out_headers, j->task.state_body, r->timeout_s,
                     [this, j](ev::ClientResult&& res) {
                       if (res.err || res.resp.status >= 300) return hand_over(*j, "save", res);
                       const NativeRoute& r = *j->route;
-                      log_event(r, *j, "Publish Task Saved event for task with Id: '" + j->task.id + "' and Name: '" +
-                                           j->task.name + "' for Assignee: '" + j->task.assigned_to + "'");
+                      log_event(r, *j, r.log_publish.render(j->task.id, j->task.name, j->task.assigned_to));
                       client_.request(r.sidecar, "POST", r.publish_target, j->out_headers, j->task.task_json,
                                       r.timeout_s, [this, j](ev::ClientResult&& res2) {
                                         if (res2.err || res2.resp.status >= 300)
                                           return hand_over(*j, "publish", res2);
-                                        finish(*j, 201, {{"Location", "/api/tasks/" + j->task.id}});
+                                        const NativeRoute& r2 = *j->route;
+                                        finish(*j, r2.status,
+                                               {{"Location", r2.location.render(j->task.id, j->task.name,
+                                                                                j->task.assigned_to)}});
                                       });
                     });
     return true;

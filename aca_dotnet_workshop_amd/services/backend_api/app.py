@@ -54,6 +54,12 @@ def _json(body: bytes, status: int = 200) -> Response:
     return Response(body, status, None, "application/json; charset=utf-8")
 
 
+# TasksController.Post's answer (TasksController.cs:44): ``CreatedAtAction`` -> 201 + Location.
+# The Python handler and the app host's native route (apphost.hpp) both answer from these.
+CREATED_STATUS = 201
+CREATED_LOCATION = "/api/tasks/%s"
+
+
 def register_controllers(app: WebApp, manager: TasksManager) -> None:
     fast_list = getattr(manager, "tasks_by_creator_json", None)
     if os.environ.get("TT_READ_PATH", "").lower() == "bind":  # A/B: bind a TaskModel per task
@@ -83,6 +89,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     spec = native() if fast_create is not None and native is not None else None
     create_what = spec.pop("what") if spec else {}
     if spec:
+        spec["cfg"].update({"status": CREATED_STATUS, "location": CREATED_LOCATION, "location_args": "id"})
         # the app host's I/O thread serves POST api/tasks end to end when it can: the same
         # native codec, log lines, state save and event as create_new_task_from_body, the same
         # 201; the rest (bodies for the general binder, sampled traces, a failed sidecar call)
@@ -98,10 +105,10 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
         if fast_create is not None and (not ctype or "json" in ctype):  # one native pass over the body
             tid = await fast_create(req.body)
             if tid is not None:
-                return Response(b"", 201, [("Location", f"/api/tasks/{tid}")])
+                return Response(b"", CREATED_STATUS, [("Location", CREATED_LOCATION % tid)])
         m: TaskAddModel = await read_model(req, TaskAddModel)
         tid = await manager.create_new_task(m.task_name, m.task_created_by, m.task_assigned_to, m.task_due_date)
-        return Response(b"", 201, [("Location", f"/api/tasks/{tid}")])
+        return Response(b"", CREATED_STATUS, [("Location", CREATED_LOCATION % tid)])
 
     @app.route("/api/tasks/{taskId}", ("PUT",), name="UpdateTask", tag="Tasks", body=TaskUpdateModel,
                responses={200: None, 400: None})

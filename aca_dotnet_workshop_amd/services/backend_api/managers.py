@@ -40,6 +40,12 @@ from ...telemetry.logging import info_each
 
 log = logging.getLogger("TasksManager")
 
+# The create flow's log templates (TasksStoreManager.cs:34, :153): the Python manager logs with
+# them and the app host's native route (apphost.hpp api_create) is handed the same text -- one
+# definition, so the native lines follow any edit here
+LOG_SAVE_NEW = "Save a new task with name: '%s' to state store"
+LOG_PUBLISH = "Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'"
+
 STORE_NAME = "statestore"
 PUBSUB_NAME = "dapr-pubsub-servicebus"
 TOPIC_NAME = "tasksavedtopic"
@@ -171,7 +177,7 @@ class TasksStoreManager(TasksManager):
     async def create_new_task(self, task_name, created_by, assigned_to, due_date) -> uuid.UUID:
         t = TaskModel(task_id=uuid.uuid4(), task_name=task_name, task_created_by=created_by, task_created_on=utcnow(),
                       task_due_date=due_date, task_assigned_to=assigned_to)
-        log.info("Save a new task with name: '%s' to state store", t.task_name)
+        log.info(LOG_SAVE_NEW, t.task_name)
         payload = RawJson(t.to_store_json())  # serialised once for the save and the event
         await self.client.save_state(self.store, str(t.task_id), payload)
         await self._publish_task_saved(t, payload)
@@ -185,14 +191,13 @@ class TasksStoreManager(TasksManager):
         if made is None:
             return None
         tid, name, assignee, task_json, state_body = made
-        log.info("Save a new task with name: '%s' to state store", name)
+        log.info(LOG_SAVE_NEW, name)
         save_body = getattr(self.client, "save_state_body", None)  # HTTP: the state API's body as is
         if save_body is not None:
             await save_body(self.store, state_body)
         else:  # gRPC: the value goes into a SaveStateRequest
             await self.client.save_state(self.store, tid, RawJson(task_json.decode()))
-        log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
-                 tid, name, assignee)
+        log.info(LOG_PUBLISH, tid, name, assignee)
         await self.client.publish_event(self.pubsub, self.topic, task_json, content_type="application/json")
         return tid
 
@@ -209,7 +214,10 @@ class TasksStoreManager(TasksManager):
                 "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
                         "save_target": f"{ep['prefix']}/v1.0/state/{self.store}",
                         "publish_target": f"{ep['prefix']}/v1.0/publish/{self.pubsub}/{self.topic}",
-                        "log_category": log.name},
+                        "log_category": log.name,
+                        # the lines create_new_task_from_body logs, with the codec's fields in order
+                        "log_save": LOG_SAVE_NEW, "log_save_args": "name",
+                        "log_publish": LOG_PUBLISH, "log_publish_args": "id,name,assigned_to"},
                 "what": {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}"}}
 
     async def delete_task(self, task_id) -> bool:
@@ -406,7 +414,6 @@ class TasksStoreManager(TasksManager):
         raise ConcurrencyConflict(f"{len(pending)} overdue tasks kept changing under concurrent writers")
 
     async def _publish_task_saved(self, t: TaskModel, payload: RawJson | None = None) -> None:
-        log.info("Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'",
-                 t.task_id, t.task_name, t.task_assigned_to)
+        log.info(LOG_PUBLISH, t.task_id, t.task_name, t.task_assigned_to)
         await self.client.publish_event(self.pubsub, self.topic,
                                         payload if payload is not None else RawJson(t.to_store_json()))

@@ -111,6 +111,11 @@ def _input_date(dt) -> str:
     return f"{d.year:04d}-{d.month:02d}-{d.day:02d}"
 
 
+# CreateModel.OnPostAsync's answer (Create.cshtml.cs:50, ``RedirectToPage("./Index")``): the
+# page's handler and the app host's native route (apphost.hpp frontend_create) both use it
+CREATED_REDIRECT = (302, "/Tasks/Index")
+
+
 def create_app(argv: list[str] | None = None, client: SidecarClient | None = None, config=None,
                overrides: dict | None = None) -> WebApp:
     app = create_host(ROLE, HERE, argv, config=config, overrides=overrides)
@@ -217,7 +222,7 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
             "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
                     "af_key": af.key.decode(), "af_cookie": AF_COOKIE, "id_cookie": COOKIE,
                     "invoke_target": f"{ep['prefix']}/v1.0/invoke/{API_APP_ID}/method/api/tasks",
-                    "location": "/Tasks/Index"}})
+                    "status": CREATED_REDIRECT[0], "location": CREATED_REDIRECT[1]}})
 
     @app.route("/Tasks/Create", ("POST",), name="TasksCreatePost", include_in_schema=False)
     async def create_post(req: Request) -> Response:
@@ -228,7 +233,7 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
             made = fast_form(req.body, (req.headers.get("cookie") or "").encode(), af.key)
             if made is not None and made[0]:
                 await gw.call("POST", "api/tasks", RawJson(made[1].decode()))
-                return redirect("/Tasks/Index")
+                return redirect(CREATED_REDIRECT[1], CREATED_REDIRECT[0])
         form = req.form()
         require_af(req, form)
         values, errors = _bind(form, "TaskAdd")
@@ -238,7 +243,7 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
         if created_by:
             await gw.call("POST", "api/tasks", {"taskName": values["taskName"], "taskCreatedBy": created_by,
                                                 "taskDueDate": values["taskDueDate"], "taskAssignedTo": values["taskAssignedTo"]})
-        return redirect("/Tasks/Index")
+        return redirect(CREATED_REDIRECT[1], CREATED_REDIRECT[0])
 
     # -- Tasks/Edit ---------------------------------------------------------------
     @app.route("/Tasks/Edit/{id:guid}", ("GET",), name="TasksEdit", include_in_schema=False)

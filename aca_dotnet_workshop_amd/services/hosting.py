@@ -156,7 +156,11 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
     # with TT_NATIVE_ROUTES=0, or on the asyncio server)
     if isinstance(srv, native_host.NativeHttpServer) and os.environ.get("TT_NATIVE_ROUTES", "1") != "0":
         for spec in app.services.get("native_routes") or []:
-            srv.native_route(spec["kind"], spec["method"], spec["path"], spec["route"], spec["cfg"])
+            try:
+                srv.native_route(spec["kind"], spec["method"], spec["path"], spec["route"], spec["cfg"])
+            except ValueError as e:  # the definition holds text the native route cannot reproduce
+                log.warning("native route %s %s declined: %s (the Python handler serves it)",
+                            spec["method"], spec["path"], e)
     await app.startup()
     ports = []
     addrs = listen_addresses(config)

@@ -56,6 +56,11 @@ log_sched = logging.getLogger("ScheduledTasksManagerController")
 EMPTY_MORE_LIMIT = 3
 
 
+# TasksNotifierController.TaskSaved's log line and answer (TasksNotifierController.cs:26-32): the
+# Python handler and the app host's native route (apphost.hpp processor_notify) use this text
+NOTIFY_LOG = "Started processing message with Task Name '%s'"
+
+
 def register_controllers(app: WebApp, client: SidecarClient) -> None:
     cfg = app.config
     api_app_id = cfg.get_str("Processor:BackendApiAppId", API_APP_ID)
@@ -66,7 +71,9 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
         # same native envelope unwrap and binding check, log line and 200 as below
         app.services.setdefault("native_routes", []).append({
             "kind": "processor_notify", "method": "POST", "path": "/api/tasksnotifier/tasksaved",
-            "route": "/api/tasksnotifier/tasksaved", "cfg": {"log_category": log_notifier.name}})
+            "route": "/api/tasksnotifier/tasksaved",
+            "cfg": {"log_category": log_notifier.name, "log_notify": NOTIFY_LOG, "log_notify_args": "name",
+                    "status": 200, "content_type": "text/plain; charset=utf-8"}})
 
     @app.route("/api/tasksnotifier/tasksaved", ("POST",), name="TaskSaved", tag="TasksNotifier", body=TaskModel)
     @topic("dapr-pubsub-servicebus", "tasksavedtopic")
@@ -77,12 +84,12 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
             ctype = req.content_type
             name = task_model_name(req.body) if not ctype or "json" in ctype else None
             if name is not None:
-                log_notifier.info("Started processing message with Task Name '%s'", name)
-                return text_response(f"Started processing message with Task Name '{name}'")
+                log_notifier.info(NOTIFY_LOG, name)
+                return text_response(NOTIFY_LOG % name)
         t: TaskModel = await read_model(req, TaskModel)
-        log_notifier.info("Started processing message with Task Name '%s'", t.task_name)
+        log_notifier.info(NOTIFY_LOG, t.task_name)
         if mode == "log":
-            return text_response(f"Started processing message with Task Name '{t.task_name}'")
+            return text_response(NOTIFY_LOG % t.task_name)
         ok = await send_email(t)
         return empty(200) if ok else Response(b"Failed to send an email", 400, None, "text/plain")
 

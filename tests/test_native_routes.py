@@ -310,3 +310,37 @@ def test_native_log_lines_equal_the_python_sinks(tmp_path, monkeypatch):
             root.addHandler(hd)
     assert len(recs[True]) == 2 and recs[True] == recs[False]
     assert recs[True][0]["traceId"] == TID and "tab\tquote\" ✓" in recs[True][0]["message"]
+
+
+def test_native_routes_follow_the_python_definitions(tmp_path, monkeypatch):
+    """The native routes hold no text of their own: a changed log template, status or Location in
+    the Python definitions is what the I/O thread logs and answers -- no C++ edit -- and a
+    template it cannot reproduce (another directive than %s) makes the route decline, so the
+    Python handler serves every request (VERDICT r4 #7)."""
+    from aca_dotnet_workshop_amd.services.backend_api import app as api_app
+    from aca_dotnet_workshop_amd.services.backend_api import managers
+    from aca_dotnet_workshop_amd.services.processor import app as proc_app
+    monkeypatch.setattr(managers, "LOG_SAVE_NEW", "Saving '%s' (edited)")
+    monkeypatch.setattr(managers, "LOG_PUBLISH", "Published %s / %s -> %s (100%%)")
+    monkeypatch.setattr(api_app, "CREATED_STATUS", 202)
+    monkeypatch.setattr(api_app, "CREATED_LOCATION", "/v2/tasks/%s")
+    reqs = [([("Content-Type", "application/json"), ("traceparent", UNSAMPLED)], _api_body())]
+    got = {n: _scenario(tmp_path, monkeypatch, "api", n, {}, reqs) for n in (True, False)}
+    (rn, cn, ln, mn, pn), (rp, cp, lp, mp, pp) = got[True], got[False]
+    assert pn == 0 and pp == 1  # the host served it, with the edited text
+    assert rn[0][0] == rp[0][0] == 202 and _norm_id(rn[0][1]) == _norm_id(rp[0][1]) == "/v2/tasks/<id>"
+    assert [_norm_id(x) for x in ln] == [_norm_id(x) for x in lp] == \
+        ["Saving 'Buy milk' (edited)", "Published <id> / Buy milk -> x@y.z (100%)"]
+    # the notifier's line and answer
+    monkeypatch.setattr(proc_app, "NOTIFY_LOG", "Got '%s'")
+    task = {"taskId": "2b0c7a4e-3f51-4a77-9c39-4a1f3d54e0f1", "taskName": "n1", "taskCreatedBy": "a@b.c",
+            "taskCreatedOn": "2030-01-01T10:00:00Z", "taskDueDate": "2030-01-02T00:00:00", "taskAssignedTo": "x@y.z",
+            "isCompleted": False, "isOverDue": False}
+    reqs = [([("Content-Type", "application/cloudevents+json"), ("traceparent", UNSAMPLED)], _event(task))]
+    (rn, _, ln, _, pn) = _scenario(tmp_path, monkeypatch, "processor", True, {}, reqs)
+    assert pn == 0 and rn[0][0] == 200 and rn[0][3] == b"Got 'n1'" and ln == ["Got 'n1'"]
+    # a template the native route cannot fill: it declines, Python answers
+    monkeypatch.setattr(managers, "LOG_SAVE_NEW", "Save a new task with name: '%r' to state store")
+    reqs = [([("Content-Type", "application/json"), ("traceparent", UNSAMPLED)], _api_body())]
+    (rn, _, ln, _, pn) = _scenario(tmp_path, monkeypatch, "api", True, {}, reqs)
+    assert pn == 1 and rn[0][0] == 202 and ln[0] == "Save a new task with name: ''Buy milk'' to state store"
