@@ -449,6 +449,8 @@ class BackingFront {
       return;
     if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkget" && m.method == "POST" && handle_bulkget(m, r, seg))
       return;
+    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "query" && m.method == "POST" && handle_query(m, r, seg, qs))
+      return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
   }
@@ -619,6 +621,77 @@ class BackingFront {
     }
     out += "]";
     r.send(200, {{"content-type", "application/json"}}, out);
+    return true;
+  }
+
+  // POST .../query whose filter the hash indexes answer (backing/accel.py ``indexable``: the
+  // planner sends those to the native engine, never to the columnar accelerator) -- the list of
+  // a creator's tasks (TasksStoreManager.cs:54-69) -- runs here, on the front's loop, without
+  // the Python server's event loop and GIL in the way.  Everything else (scans the accelerator
+  // may take, sampled traces that record the store's spans, malformed queries) goes to Python.
+  static bool indexable(const Value* f) {
+    if (!f || f->t != Value::Object || f->keys.size() != 1) return false;
+    std::string op = f->keys[0];
+    for (auto& ch : op) ch = (char)std::toupper((unsigned char)ch);
+    const Value& arg = f->items[0];
+    if (op == "EQ" || op == "IN") {
+      // equality on booleans / null is not selective: the planner scans instead
+      if (arg.t != Value::Object || arg.items.empty()) return false;
+      const Value& v = arg.items[0];
+      auto plain = [](const Value& x) { return x.t == Value::Null || x.t == Value::Bool; };
+      if (v.t != Value::Array) return !plain(v);
+      for (auto& x : v.items)
+        if (!plain(x)) return true;
+      return false;
+    }
+    if (op == "AND") {
+      if (arg.t != Value::Array) return false;
+      for (auto& x : arg.items)
+        if (indexable(&x)) return true;
+      return false;
+    }
+    if (op == "OR") {
+      if (arg.t != Value::Array || arg.items.empty()) return false;
+      for (auto& x : arg.items)
+        if (!indexable(&x)) return false;
+      return true;
+    }
+    return false;
+  }
+  static bool sampled(const ev::Message& m) {
+    const std::string* tp = m.header("traceparent");
+    if (!tp || tp->size() < 55) return false;
+    return (std::strtol(tp->c_str() + tp->size() - 2, nullptr, 16) & 1) != 0;
+  }
+
+  bool handle_query(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
+    Coll* c = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
+      if (it != colls_.end() && it->second->store) c = it->second.get();
+    }
+    if (!c || sampled(m)) return false;
+    try {
+      Value q = parse(m.body.empty() ? std::string("{}") : m.body);
+      if (q.t != Value::Object || !indexable(q.get("filter"))) return false;
+    } catch (const ParseError&) {
+      return false;
+    }
+    if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
+    if (throttled(m, r, c->store, DocStore::query_ru(0))) return true;
+    std::string body;
+    try {
+      std::string project = query_get(qs, "project");
+      for (auto& ch : project) ch = (char)std::tolower((unsigned char)ch);
+      body = c->store->query(m.body, query_get(qs, "prefix"), project == "sortkeys");
+    } catch (const std::exception& ex) {  // the caller's query: 400, as the Python handler answers
+      r.send(400, {{"content-type", "application/problem+json; charset=utf-8"}}, bf::problem_json(400, ex.what()));
+      return true;
+    }
+    count("doc.query");
+    c->store->debit(DocStore::query_ru(body.size()) - DocStore::query_ru(0));  // the result-size part
+    r.send(200, {{"content-type", "application/json"}}, body);
     return true;
   }
 

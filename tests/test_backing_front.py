@@ -362,3 +362,45 @@ def test_provisioned_throughput_429(front, monkeypatch):
             await h.close()
             await c.http.close()
     run(main())
+
+
+def test_indexed_queries_run_on_the_native_front(monkeypatch):
+    """A query the hash indexes answer (backing/accel.py ``indexable``: the list of a creator's
+    tasks) runs on the native front's loop; the answers equal the Python handler's, and every
+    other query (scans the accelerator may take, boolean equality, sampled traces) still goes to
+    Python.  The front's choice is the planner's ``indexable`` rule."""
+    import json as _json
+
+    from aca_dotnet_workshop_amd.backing.accel import indexable
+    filters = [{"EQ": {"who": "u1"}}, {"EQ": {"done": True}}, {"IN": {"who": ["u1", "u3"]}}, {"IN": {"who": [None, False]}},
+               {"AND": [{"EQ": {"done": False}}, {"EQ": {"who": "u2"}}]}, {"AND": [{"EQ": {"done": False}}]},
+               {"OR": [{"EQ": {"who": "u1"}}, {"EQ": {"n": 3}}]}, {"OR": [{"EQ": {"who": "u1"}}, {"GT": {"n": 3}}]},
+               {"GT": {"n": 2}}, {}, {"eq": {"who": "u2"}}]
+    queries = [{"filter": f} for f in filters] + [
+        {"filter": {"EQ": {"who": "u1"}}, "sort": [{"key": "n", "order": "DESC"}], "page": {"limit": 2}},
+        {"filter": {"EQ": {"who": "u1"}}, "sort": [{"key": "n"}], "page": {"limit": 2, "token": "2"}}]
+
+    async def answers(front):
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            for i in range(12):
+                await c.doc_put("acct", "db", "c", f"p||k{i}", _json.dumps({"who": f"u{i % 4}", "n": i % 5,
+                                                                             "done": i % 3 == 0}))
+            out = []
+            for q in queries:
+                out.append(_json.loads(await c.doc_query("acct", "db", "c", _json.dumps(q).encode(), "p||")))
+            for kw in ({"sortkeys": True},):
+                r = await c.http.post(b.base + "/cosmos/acct/db/c/query?prefix=p%7C%7C&project=sortkeys",
+                                      body=_json.dumps(queries[-2]).encode(), headers={"x-tt-identity": "x"})
+                out.append(r.json())
+            sampled = await c.http.post(b.base + "/cosmos/acct/db/c/query", body=_json.dumps(queries[0]).encode(),
+                                        headers={"x-tt-identity": "x", "traceparent": "00-" + "a" * 32 + "-" + "b" * 16 + "-01"})
+            out.append(sampled.json())
+            fs = (await c.http.get(b.base + "/admin/front")).json()
+            await c.http.close()
+            return out, fs
+    py, _ = run(answers("python"))
+    nat, fs = run(answers("native"))
+    assert nat == py
+    want_native = sum(1 for q in queries if indexable(q["filter"])) + 1  # + the sort-keys projection
+    assert fs["requests"].get("doc.query", 0) == want_native, (fs["requests"], want_native)
