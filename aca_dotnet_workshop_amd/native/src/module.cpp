@@ -157,8 +157,36 @@ static PyObject* headers_dict_fast(const ev::HeaderList& headers) {
 }
 
 static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) {
-  py::list out(evs.size());
+  // the finished log lines of the batch (native routes' records on the JSON sink's fast path)
+  // go up as ONE event per (level, logger): (4, level, logger name, the lines joined) -- two
+  // lines per created task otherwise cost a tuple, a call and a sink lock each in Python
+  std::vector<size_t> keep;
+  keep.reserve(evs.size());
+  std::vector<std::pair<std::pair<int, std::string>, std::string>> batches;
   for (size_t i = 0; i < evs.size(); ++i) {
+    auto& e = evs[i];
+    if (e.kind != apphost::Event::LOG || e.line.empty() || with_times) {
+      keep.push_back(i);
+      continue;
+    }
+    auto key = std::make_pair(e.err, e.msg.method);
+    size_t b = 0;
+    while (b < batches.size() && batches[b].first != key) ++b;
+    if (b == batches.size()) batches.emplace_back(key, std::string());
+    batches[b].second += e.line;
+  }
+  py::list out(keep.size() + batches.size());
+  for (size_t bi = 0; bi < batches.size(); ++bi) {
+    py::object t = py::reinterpret_steal<py::object>(PyTuple_New(4));
+    if (!t) throw py::error_already_set();
+    set_item(t.ptr(), 0, PyLong_FromLong(4));
+    set_item(t.ptr(), 1, PyLong_FromLong(batches[bi].first.first));
+    set_item(t.ptr(), 2, new_str(batches[bi].first.second));
+    set_item(t.ptr(), 3, new_str(batches[bi].second));
+    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)(keep.size() + bi), t.release().ptr());
+  }
+  for (size_t ki = 0; ki < keep.size(); ++ki) {
+    const size_t i = keep[ki];
     auto& e = evs[i];
     py::object t;
     if (e.kind == apphost::Event::REQUEST) {
@@ -198,7 +226,7 @@ static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) 
       if (with_times) t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)), e.t);
       else t = py::make_tuple(2, e.id, e.err, py::str(std::strerror(e.err)));
     }
-    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, t.release().ptr());
+    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)ki, t.release().ptr());
   }
   return out;
 }

@@ -69,6 +69,22 @@ def _native_log(level: int, name: str, message: str, trace_id: str, span_id: str
         tracing._current.reset(tok)
 
 
+def _native_lines(level: int, name: str, lines: str) -> None:
+    """Native routes' records already formatted as the JSON sink's lines (``_native_log``'s
+    ``line``), several at once: appended in one piece while that sink still writes them."""
+    from ..telemetry.logging import native_line_sink
+    sink = native_line_sink(name, level)
+    if sink is not None:
+        sink._put(lines)
+        return
+    for ln in lines.splitlines():  # the sink changed since the route was registered
+        try:
+            rec = json.loads(ln)
+        except ValueError:
+            continue
+        _native_log(level, name, rec.get("message", ""), rec.get("traceId", ""), rec.get("spanId", ""))
+
+
 def _client_error(err: int, msg: str) -> BaseException:
     if err == _errno.ECONNREFUSED:
         return ConnectionRefusedError(err, msg)
@@ -217,6 +233,8 @@ class NativeHost:
                     srv._dispatch(token, method, target, http10, hd, body)
                 elif kind == 3:  # a native route's log record
                     _native_log(ev[1], ev[2], ev[3], ev[4], ev[5], ev[6])
+                elif kind == 4:  # native routes' finished log lines of one logger, batched
+                    _native_lines(ev[1], ev[2], ev[3])
                 else:
                     fut = self.pending.pop(ev[1], None)
                     if fut is not None and not fut.done():
