@@ -130,9 +130,127 @@ struct Template {
   }
 };
 
+// A page compiled by the Python side from its own Jinja template (services/frontend/rows.py):
+// literal pieces around named slots, as a JSON array [lit, slot, lit, ..., lit].  The route
+// only fills the slots; the markup is the template's.
+struct Pieces {
+  std::vector<std::string> lits;
+  std::vector<int> slots;
+  bool set = false;
+
+  static Pieces parse(const std::string& json, const std::vector<std::string>& names) {
+    Pieces p;
+    tt::Value v = tt::parse(json);
+    if (v.t != tt::Value::Array || v.items.size() % 2 != 1) throw std::invalid_argument("native route page: not pieces");
+    for (size_t i = 0; i < v.items.size(); ++i) {
+      const tt::Value& x = v.items[i];
+      if (x.t != tt::Value::String) throw std::invalid_argument("native route page: a piece is not text");
+      if (i % 2 == 0) {
+        p.lits.push_back(x.s);
+        continue;
+      }
+      auto it = std::find(names.begin(), names.end(), x.s);
+      if (it == names.end()) throw std::invalid_argument("native route page: unknown slot " + x.s);
+      p.slots.push_back((int)(it - names.begin()));
+    }
+    p.set = true;
+    return p;
+  }
+  template <class Fill>
+  void render(std::string& out, Fill&& fill) const {
+    out += lits[0];
+    for (size_t i = 0; i < slots.size(); ++i) {
+      fill(slots[i], out);
+      out += lits[i + 1];
+    }
+  }
+};
+
+// Jinja's autoescape (markupsafe.escape): & < > ' "
+inline void html_escape_to(std::string& out, std::string_view s) {
+  for (char c : s) {
+    switch (c) {
+      case '&': out += "&amp;"; break;
+      case '<': out += "&lt;"; break;
+      case '>': out += "&gt;"; break;
+      case '\'': out += "&#39;"; break;
+      case '"': out += "&#34;"; break;
+      default: out += c;
+    }
+  }
+}
+
+// urllib.parse.quote (safe "/"): letters, digits, "_.-~" and "/" as is, every other byte %XX
+inline void url_quote_to(std::string& out, std::string_view s) {
+  static const char* hx = "0123456789ABCDEF";
+  for (unsigned char c : s) {
+    if (std::isalnum(c) || c == '_' || c == '.' || c == '-' || c == '~' || c == '/') {
+      out += (char)c;
+    } else {
+      out += '%';
+      out += hx[c >> 4];
+      out += hx[c & 15];
+    }
+  }
+}
+
+// Request.query_get of web/http.py: parse_qsl (keep blank values, first value wins), the exact
+// name, else the first name equal ignoring case; false when absent or not decodable.
+inline bool query_param(std::string_view target, std::string_view name, std::string& out) {
+  size_t q = target.find('?');
+  if (q == std::string_view::npos) return false;
+  std::string_view qs = target.substr(q + 1);
+  std::vector<std::pair<std::string, std::string>> kv;
+  for (size_t i = 0; i <= qs.size();) {
+    size_t j = qs.find('&', i);
+    if (j == std::string_view::npos) j = qs.size();
+    std::string_view f = qs.substr(i, j - i);
+    i = j + 1;
+    if (f.empty()) continue;
+    size_t eq = f.find('=');
+    std::string k, v;
+    if (!::formcodec::unquote(f.substr(0, eq), true, k)) return false;
+    if (eq != std::string_view::npos && !::formcodec::unquote(f.substr(eq + 1), true, v)) return false;
+    bool seen = false;
+    for (auto& e : kv) seen = seen || e.first == k;
+    if (!seen) kv.emplace_back(std::move(k), std::move(v));
+  }
+  for (auto& e : kv)
+    if (e.first == name) return out = e.second, true;
+  auto low = [](std::string_view x) {
+    std::string r(x);
+    for (auto& c : r) c = (char)std::tolower((unsigned char)c);
+    return r;
+  };
+  const std::string want = low(name);
+  for (auto& e : kv)
+    if (low(e.first) == want) return out = e.second, true;
+  return false;
+}
+
+// web/http.py Request.cookies: ';'-separated, stripped, name=value, value unquoted, last wins
+inline bool cookie_value(std::string_view cookie, std::string_view name, std::string& out) {
+  bool have = false;
+  std::string tmp;
+  for (size_t i = 0; i <= cookie.size();) {
+    size_t j = cookie.find(';', i);
+    if (j == std::string_view::npos) j = cookie.size();
+    std::string_view part = cookie.substr(i, j - i);
+    i = j + 1;
+    while (!part.empty() && (part.front() == ' ' || part.front() == '\t')) part.remove_prefix(1);
+    while (!part.empty() && (part.back() == ' ' || part.back() == '\t')) part.remove_suffix(1);
+    size_t eq = part.find('=');
+    if (eq == std::string_view::npos || part.substr(0, eq) != name) continue;
+    if (!::formcodec::unquote(part.substr(eq + 1), false, tmp)) return false;
+    out = tmp;
+    have = true;
+  }
+  return have;
+}
+
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
-  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3 };
+  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5 };
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -149,6 +267,14 @@ struct NativeRoute {
   int status = 0;
   std::string content_type;
   Template location, log_save, log_publish, log_notify;
+  // kFrontendList: GET Tasks/Index -> invoke GET api/tasks?createdBy= -> the page, compiled from
+  // the Jinja templates (page slots: created_by, af_token, rows; row slots: task_id, task_name,
+  // task_assigned_to, due -- one row per (isCompleted, isOverDue))
+  std::string list_target;
+  Pieces page, rows[4];
+  // kApiList: GET api/tasks?createdBy= -> state query (the manager's query text around the
+  // JSON-encoded creator) -> the TaskModel array newest first
+  std::string query_target, query_prefix, query_suffix;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -355,6 +481,8 @@ class AppHost {
     if (kind == "frontend_create") r->kind = NativeRoute::kFrontendCreate;
     else if (kind == "api_create") r->kind = NativeRoute::kApiCreate;
     else if (kind == "processor_notify") r->kind = NativeRoute::kProcessorNotify;
+    else if (kind == "frontend_list") r->kind = NativeRoute::kFrontendList;
+    else if (kind == "api_list") r->kind = NativeRoute::kApiList;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -379,6 +507,18 @@ class AppHost {
     r->content_type = get("content_type");
     if (r->kind == NativeRoute::kProcessorNotify) {
       r->log_notify = Template::compile(get("log_notify"), get("log_notify_args"));
+    } else if (r->kind == NativeRoute::kFrontendList) {
+      r->list_target = get("list_target");
+      r->page = Pieces::parse(get("page"), {"created_by", "af_token", "rows"});
+      const char* combos[4] = {"row_ff", "row_ft", "row_tf", "row_tt"};  // (isCompleted, isOverDue)
+      for (int i = 0; i < 4; ++i)
+        r->rows[i] = Pieces::parse(get(combos[i]), {"task_id", "task_name", "task_assigned_to", "due"});
+      if (r->list_target.empty() || r->af_key.empty()) throw std::invalid_argument("frontend_list needs its target and key");
+    } else if (r->kind == NativeRoute::kApiList) {
+      r->query_target = get("query_target");
+      r->query_prefix = get("query_prefix");
+      r->query_suffix = get("query_suffix");
+      if (r->query_target.empty() || r->query_prefix.empty()) throw std::invalid_argument("api_list needs its query");
     } else {
       r->location = Template::compile(get("location"), get("location_args"));
     }
@@ -575,10 +715,131 @@ class AppHost {
     emit(std::move(e));
   }
 
-  void finish(NativeJob& j, int status, const ev::HeaderList& headers) {
-    j.reply.send(status, headers, {});
+  void finish(NativeJob& j, int status, const ev::HeaderList& headers, std::string_view body = {}) {
+    j.reply.send(status, headers, body);
     j.route->record(status, ev::now_s() - j.t0);
     native_inflight_.fetch_sub(1);
+  }
+  // The route cannot decide after all (an answer outside the page's shape): the request goes to
+  // Python from scratch, which makes the same calls again (the list is a read).
+  void decline(NativeJob& j) {
+    to_python(j.server, std::move(j.req), std::move(j.reply));
+    native_inflight_.fetch_sub(1);
+  }
+
+  // One task of GET api/tasks' answer as a Tasks/Index row (services/frontend/rows.py
+  // RowRenderer._fields): false when it is outside the shape the compiled row covers.
+  static bool render_row(const NativeRoute& r, const tt::Value& d, std::string& out) {
+    if (d.t != tt::Value::Object) return false;
+    const tt::Value *id = d.get("taskId"), *name = d.get("taskName"), *who = d.get("taskAssignedTo"),
+                    *due = d.get("taskDueDate"), *done = d.get("isCompleted"), *over = d.get("isOverDue");
+    if (!id || id->t != tt::Value::String || !name || name->t != tt::Value::String || !who ||
+        who->t != tt::Value::String || !due || due->t != tt::Value::String || !done || done->t != tt::Value::Bool ||
+        !over || over->t != tt::Value::Bool)
+      return false;
+    const std::string& g = id->s;  // the canonical lowercase GUID text
+    if (g.size() != 36) return false;
+    for (size_t i = 0; i < 36; ++i) {
+      char c = g[i];
+      bool dash = i == 8 || i == 13 || i == 18 || i == 23;
+      if (dash ? c != '-' : !((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return false;
+    }
+    // yyyy-MM-ddTHH:mm:ss[.f{1,7}][Z]: UTC or unspecified, the calendar day is the text's own
+    const std::string& t = due->s;
+    auto dig = [&](size_t a, size_t n) {
+      if (a + n > t.size()) return false;
+      for (size_t i = a; i < a + n; ++i)
+        if (t[i] < '0' || t[i] > '9') return false;
+      return true;
+    };
+    if (t.size() < 19 || !dig(0, 4) || t[4] != '-' || !dig(5, 2) || t[7] != '-' || !dig(8, 2) || t[10] != 'T' ||
+        !dig(11, 2) || t[13] != ':' || !dig(14, 2) || t[16] != ':' || !dig(17, 2))
+      return false;
+    size_t k = 19;
+    if (k < t.size() && t[k] == '.') {
+      size_t f = k + 1;
+      while (f < t.size() && t[f] >= '0' && t[f] <= '9') ++f;
+      if (f - k - 1 < 1 || f - k - 1 > 7) return false;
+      k = f;
+    }
+    if (k < t.size() && t[k] == 'Z') ++k;
+    if (k != t.size()) return false;
+    const Pieces& p = r.rows[(done->b ? 2 : 0) + (over->b ? 1 : 0)];
+    p.render(out, [&](int slot, std::string& o) {
+      switch (slot) {
+        case 0: o += g; break;
+        case 1: html_escape_to(o, name->s); break;
+        case 2: html_escape_to(o, who->s); break;
+        default: o.append(t, 8, 2), o += '-', o.append(t, 5, 2), o += '-', o.append(t, 0, 4);
+      }
+    });
+    return true;
+  }
+
+  // kFrontendList (services/frontend/app.py tasks_index): the identity and antiforgery cookies,
+  // the list through the sidecar, the page
+  bool frontend_list(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const NativeRoute& r = *j->route;
+    const std::string* cookie = header(m, "cookie");
+    std::string who, af;
+    if (!cookie || !cookie_value(*cookie, r.id_cookie, who) || who.empty() || !cookie_value(*cookie, r.af_cookie, af) ||
+        af.empty())
+      return false;  // no identity (redirect) or a new antiforgery cookie to hand out: the page
+    std::string target = r.list_target;
+    url_quote_to(target, who);
+    ev::HeaderList h{{"traceparent", j->traceparent}};
+    if (!r.token.empty()) h.emplace_back("dapr-api-token", r.token);
+    std::string token = ::formcodec::hmac_sha256_hex(r.af_key, af);
+    native_inflight_.fetch_add(1);
+    client_.request(r.sidecar, "GET", target, h, {}, r.timeout_s,
+                    [this, j, who = std::move(who), token = std::move(token)](ev::ClientResult&& res) {
+                      if (res.err || res.resp.status >= 300) return hand_over(*j, "invoke", res);
+                      const NativeRoute& r = *j->route;
+                      const std::string* ct = res.resp.header("content-type");
+                      if (ct && !ct->empty() && ct->find("json") == std::string::npos) return decline(*j);
+                      std::string rows_html;
+                      if (!res.resp.body.empty()) {
+                        tt::Value list;
+                        try {
+                          list = tt::parse(res.resp.body);
+                        } catch (const std::exception&) {
+                          return decline(*j);
+                        }
+                        if (list.t != tt::Value::Array) return decline(*j);
+                        for (auto& d : list.items)
+                          if (!render_row(r, d, rows_html)) return decline(*j);
+                      }
+                      std::string page;
+                      page.reserve(rows_html.size() + 2048);
+                      r.page.render(page, [&](int slot, std::string& o) {
+                        if (slot == 0) html_escape_to(o, who);
+                        else if (slot == 1) o += token;
+                        else o += rows_html;
+                      });
+                      finish(*j, r.status, {{"Content-Type", r.content_type}}, page);
+                    });
+    return true;
+  }
+
+  // kApiList (services/backend_api/app.py get_tasks + TasksStoreManager.tasks_by_creator_json)
+  bool api_list(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const NativeRoute& r = *j->route;
+    std::string who;
+    if (!query_param(m.target, "createdBy", who) || who.empty()) return false;
+    std::string body = r.query_prefix;
+    tt::escape_to(body, who);
+    body += r.query_suffix;
+    native_inflight_.fetch_add(1);
+    client_.request(r.sidecar, "POST", r.query_target, j->out_headers, body, r.timeout_s, [this, j](ev::ClientResult&& res) {
+      if (res.err || res.resp.status >= 300) return hand_over(*j, "query", res);
+      std::string out;
+      size_t count = 0;
+      bool more = false;
+      if (!::taskcodec::query_tasks(res.resp.body, out, count, true, &more, true)) return decline(*j);
+      const NativeRoute& r = *j->route;
+      finish(*j, r.status, {{"Content-Type", r.content_type}}, out);
+    });
+    return true;
   }
 
   // A failed sidecar call: the request goes to Python with the result attached.
@@ -657,6 +918,23 @@ class AppHost {
       return false;
     }
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
+    if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList) {
+      auto j = std::make_shared<NativeJob>();
+      j->route = r;
+      j->server = server;
+      j->t0 = ev::now_s();
+      j->trace_id = std::move(tid);
+      j->span_id = new_id(1);
+      j->traceparent = "00-" + j->trace_id + "-" + j->span_id + "-00";
+      j->out_headers.emplace_back("traceparent", j->traceparent);
+      if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
+      j->out_headers.emplace_back("Content-Type", "application/json");
+      bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m) : api_list(j, m);
+      if (!taken) return false;
+      j->req = std::move(m);
+      j->reply = std::move(reply);
+      return true;
+    }
     auto j = std::make_shared<NativeJob>();
     if (r->kind == NativeRoute::kFrontendCreate) {
       const std::string* cookie = header(m, "cookie");

@@ -62,12 +62,22 @@ CREATED_LOCATION = "/api/tasks/%s"
 
 def register_controllers(app: WebApp, manager: TasksManager) -> None:
     fast_list = getattr(manager, "tasks_by_creator_json", None)
+    list_native = getattr(manager, "native_list_route", None)
     if os.environ.get("TT_READ_PATH", "").lower() == "bind":  # A/B: bind a TaskModel per task
-        fast_list = None
+        fast_list = list_native = None
+    list_spec = list_native() if fast_list is not None and list_native is not None else None
+    list_what = list_spec.pop("what") if list_spec else {}
+    if list_spec:
+        # GET api/tasks on the app host's I/O thread: the manager's query, the same codec
+        list_spec["cfg"].update({"status": 200, "content_type": "application/json; charset=utf-8"})
+        app.services.setdefault("native_routes", []).append(list_spec)
     # -- TasksController (reference Controllers/TasksController.cs) --------------
     @app.route("/api/tasks", ("GET",), name="GetTasks", query=["createdBy"], tag="Tasks",
                responses={200: [TaskModel]})
     async def get_tasks(req: Request) -> Response:
+        failed = native_route_failure(req, list_what) if list_what else None
+        if failed is not None:  # the native route's query failed: the SDK's error
+            raise failed
         created_by = req.query_get("createdBy") or ""
         if fast_list is not None:
             body = await fast_list(created_by)

@@ -240,11 +240,32 @@ class TasksStoreManager(TasksManager):
     async def get_tasks_by_creator(self, created_by) -> list[TaskModel]:
         if not created_by:
             return []
-        q = {"filter": {"EQ": {"taskCreatedBy": created_by}}}
-        resp = await self.client.query_state(self.store, q)
+        resp = await self.client.query_state(self.store, self._by_creator_query(created_by))
         tasks = [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
         tasks.sort(key=_created_key, reverse=True)
         return tasks
+
+    def _by_creator_query(self, created_by: str) -> dict:
+        return {"filter": {"EQ": {"taskCreatedBy": created_by}}}
+
+    def native_list_route(self) -> dict | None:
+        """``tasks_by_creator_json`` as a native route of the app host (apphost.hpp ``api_list``):
+        the same query text -- this manager's, split around the JSON-encoded creator -- through
+        the same sidecar, the same codec; None when this client cannot take one."""
+        ep_of = getattr(self.client, "native_endpoint", None)
+        ep = ep_of() if ep_of is not None else None
+        if ep is None or getattr(self.client, "query_state_raw", None) is None:
+            return None
+        mark = "zqCREATORqz"
+        text = json.dumps(self._by_creator_query(mark))  # query_state_raw's encoding of the dict
+        at = text.find(json.dumps(mark))
+        if at < 0 or text.count(mark) != 1:
+            return None
+        return {"kind": "api_list", "method": "GET", "path": "/api/tasks", "route": "/api/tasks",
+                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                        "query_target": f"{ep['prefix']}/v1.0-alpha1/state/{self.store}/query",
+                        "query_prefix": text[:at], "query_suffix": text[at + len(json.dumps(mark)):]},
+                "what": {"query": f"query state {self.store}"}}
 
     async def tasks_by_creator_json(self, created_by: str) -> bytes | None:
         """``get_tasks_by_creator`` as the response body: the query's results turned into the
@@ -257,7 +278,7 @@ class TasksStoreManager(TasksManager):
             return None
         if not created_by:
             return b"[]"
-        raw = await raw_query(self.store, {"filter": {"EQ": {"taskCreatedBy": created_by}}})
+        raw = await raw_query(self.store, self._by_creator_query(created_by))
         made = tasks_from_query_wire(raw, by_created=True, descending=True)
         return made[1] if made is not None else None
 

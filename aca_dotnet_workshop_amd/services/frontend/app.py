@@ -25,6 +25,7 @@ antiforgery cookie; the landing page opts out (``[IgnoreAntiforgeryToken]``, Ind
 from __future__ import annotations
 
 import hashlib
+import json
 import hmac
 import logging
 import os
@@ -181,6 +182,9 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
         created_by = req.cookies.get(COOKIE)
         if not created_by:
             return redirect("/")
+        failed = native_route_failure(req, {"invoke": f"invoke {API_APP_ID}/api/tasks?createdBy={quote(created_by)}"})
+        if failed is not None:  # the native route's invoke failed: the SDK's error, as below
+            raise failed
         data = await gw.call("GET", f"api/tasks?createdBy={quote(created_by)}")
         fast = rows.render(data)
         if fast is not None:
@@ -223,6 +227,20 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
                     "af_key": af.key.decode(), "af_cookie": AF_COOKIE, "id_cookie": COOKIE,
                     "invoke_target": f"{ep['prefix']}/v1.0/invoke/{API_APP_ID}/method/api/tasks",
                     "status": CREATED_REDIRECT[0], "location": CREATED_REDIRECT[1]}})
+
+    if ep is not None and rows.ok:
+        # GET Tasks/Index on the app host's I/O thread: the same cookies, the same invoke, the
+        # page from the templates' own pieces (rows.py); the rest -- no identity, a new
+        # antiforgery cookie, an answer outside the rows' shape, a failed invoke -- comes here
+        page = rows.page_pieces(env, "tasks_index.html", af_field=AF_FIELD, request=None, title="Tasks Tracker")
+        if page is not None:
+            app.services.setdefault("native_routes", []).append({
+                "kind": "frontend_list", "method": "GET", "path": "/Tasks/Index", "route": "/Tasks/Index",
+                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                        "af_key": af.key.decode(), "af_cookie": AF_COOKIE, "id_cookie": COOKIE,
+                        "list_target": f"{ep['prefix']}/v1.0/invoke/{API_APP_ID}/method/api/tasks?createdBy=",
+                        "status": 200, "content_type": "text/html; charset=utf-8", "page": json.dumps(page),
+                        **{k: json.dumps(v) for k, v in rows.row_pieces().items()}}})
 
     @app.route("/Tasks/Create", ("POST",), name="TasksCreatePost", include_in_schema=False)
     async def create_post(req: Request) -> Response:

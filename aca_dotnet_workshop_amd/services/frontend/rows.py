@@ -99,6 +99,29 @@ class RowRenderer:
             out.append(fmt[(d["isCompleted"], d["isOverDue"])].format_map(f))
         return Markup("".join(out))
 
+    def page_pieces(self, env, name: str, **ctx: Any) -> list[str] | None:
+        """The page ``name`` rendered around the list as pieces for the app host's native route
+        (apphost.hpp ``Pieces``): [literal, slot, literal, ...] with the slots ``created_by``,
+        ``af_token`` and ``rows`` -- the same render call the page makes, with sentinels in
+        those places.  None when a sentinel does not come through exactly once."""
+        sent = {"created_by": "zqCREATEDBYqz", "af_token": "zqAFTOKENqz", "rows": "zqROWSqz"}
+        html = env.get_template(name).render(created_by=sent["created_by"], af_token=sent["af_token"],
+                                             rows_html=Markup(sent["rows"]), **ctx)
+        names = {v: k for k, v in sent.items()}
+        parts = re.split("(" + "|".join(map(re.escape, names)) + ")", html)
+        slots = [names[p] for p in parts[1::2]]
+        if sorted(slots) != sorted(sent):
+            return None
+        return [p if i % 2 == 0 else names[p] for i, p in enumerate(parts)]
+
+    def row_pieces(self) -> dict[str, list[str]] | None:
+        """The compiled rows for the native route: ``row_<c><o>`` (c, o: ``f`` / ``t`` for
+        isCompleted / isOverDue) -> pieces with the slots task_id, task_name, task_assigned_to, due."""
+        if not self.ok:
+            return None
+        return {f"row_{'t' if c else 'f'}{'t' if o else 'f'}": self.plans[(c, o)] for c in (False, True)
+                for o in (False, True)}
+
     def _selfcheck(self) -> bool:
         from ...models import TaskModel
         probe = [{"taskId": "0f8fad5b-d9cb-469f-a165-70867728950e", "taskName": 'a <b> & "c" \'d\' é 😀',

@@ -344,3 +344,139 @@ def test_native_routes_follow_the_python_definitions(tmp_path, monkeypatch):
     reqs = [([("Content-Type", "application/json"), ("traceparent", UNSAMPLED)], _api_body())]
     (rn, _, ln, _, pn) = _scenario(tmp_path, monkeypatch, "api", True, {}, reqs)
     assert pn == 1 and rn[0][0] == 202 and ln[0] == "Save a new task with name: ''Buy milk'' to state store"
+
+
+def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
+    """GET ``requests`` [(headers, target)] against the frontend's Tasks/Index ('frontend') or
+    the API's api/tasks ('api'); returns (responses, sidecar calls, metric delta, python calls)."""
+    monkeypatch.setenv("TT_APP_HOST", "native")
+    monkeypatch.setenv("TT_NATIVE_ROUTES", "1" if native else "0")
+    monkeypatch.setenv("TT_TRACE_SAMPLE_RATE", "0")
+    side_sock = str(tmp_path / f"gside-{which}-{native}.sock")
+    app_sock = str(tmp_path / f"gapp-{which}-{native}.sock")
+    from aca_dotnet_workshop_amd.sdk.client import SidecarClient
+    from aca_dotnet_workshop_amd.telemetry import tracing
+    tracing.configure("native-routes-test", None, 0.0)
+    route = {"api": "/api/tasks", "frontend": "/Tasks/Index"}[which]
+
+    async def main():
+        loop = asyncio.get_running_loop()
+        side = Sidecar()
+        side.status.update(sidecar_status)
+        srv = HttpServer(side.app, loop)
+        await srv.listen_unix(side_sock)
+        client = SidecarClient(f"unix:{side_sock}:")
+        cfg = Configuration([{"APP_PORT": "0", "Environment": "Production", "TT_APP_UDS": app_sock}])
+        python_calls = []
+        if which == "api":
+            from aca_dotnet_workshop_amd.services.backend_api import create_app
+            from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
+            app = create_app(config=cfg, manager=TasksStoreManager(client))
+            real = client.query_state_raw
+
+            async def counted(*a, **kw):
+                python_calls.append(1)
+                return await real(*a, **kw)
+            client.query_state_raw = counted
+        else:
+            from aca_dotnet_workshop_amd.services.frontend import create_app
+            app = create_app([], client=client, overrides={"Frontend:AntiforgeryKey": "k3y", "APP_PORT": "0",
+                                                           "Environment": "Production", "TT_APP_UDS": app_sock})
+            gw = app.services["backend"]
+            real_call = gw.call
+
+            async def counted_call(*a, **kw):
+                python_calls.append(1)
+                return await real_call(*a, **kw)
+            gw.call = counted_call
+        REGISTRY.collect()
+        ctr = REGISTRY.counter("http_requests_total")
+        before = ctr.get(method="GET", route=route, status="200")
+        stop, ports = asyncio.Event(), []
+        task = asyncio.create_task(_serve(app, app_sock, stop, ports))
+        for _ in range(200):
+            if ports:
+                break
+            await asyncio.sleep(0.01)
+        c = HttpClient()
+        out = []
+        try:
+            for headers, target in requests:
+                r = await c.get(f"unix:{app_sock}:{target}", headers=headers)
+                out.append((r.status, r.headers.get("content-type"), r.headers.get("location"), r.body))
+        finally:
+            await c.close()
+            stop.set()
+            await task
+            await srv.close(1)
+        REGISTRY.collect()
+        return out, side.calls, ctr.get(method="GET", route=route, status="200") - before, len(python_calls)
+    return run(main())
+
+
+_LIST = [{"taskId": "2b0c7a4e-3f51-4a77-9c39-4a1f3d54e0f1", "taskName": "<b>Ünïcode</b> & 'q' \"x\"",
+          "taskCreatedBy": "me@x.y", "taskCreatedOn": "2030-01-01T10:00:00.1234567Z",
+          "taskDueDate": "2030-01-02T00:00:00", "taskAssignedTo": "x@y.z", "isCompleted": False, "isOverDue": True},
+         {"taskId": "0f8fad5b-d9cb-469f-a165-70867728950e", "taskName": "plain", "taskCreatedBy": "me@x.y",
+          "taskCreatedOn": "2030-01-01T09:00:00Z", "taskDueDate": "2029-12-31T23:59:59.5Z",
+          "taskAssignedTo": "a@b.c", "isCompleted": True, "isOverDue": False}]
+
+
+@pytest.mark.parametrize("status", [{}, {"/v1.0/invoke/": (500, b'{"errorCode":"ERR_DIRECT_INVOKE"}')}],
+                         ids=["ok", "invoke-fails"])
+def test_frontend_list_native_equals_python(tmp_path, monkeypatch, status):
+    """GET Tasks/Index on the I/O thread: the page compiled from the templates (rows.py) equals
+    the Python page byte for byte, the same invoke goes to the sidecar, and the requests the
+    route leaves to the page (no identity, no antiforgery cookie yet, a list outside the rows'
+    shape, a failed invoke) are answered as the page answers them."""
+    ok = {"/v1.0/invoke/": (200, json.dumps(_LIST).encode())}
+    ok.update(status)
+    ck = "TasksCreatedByCookie=me%40x.y; .AspNetCore.Antiforgery=c0ffee"
+    reqs = [([("Cookie", ck), ("traceparent", UNSAMPLED)], "/Tasks/Index"),
+            ([("Cookie", "TasksCreatedByCookie=o%27b%3Cr%3E%2Bx%20y@z; .AspNetCore.Antiforgery=c0ffee"),
+              ("traceparent", UNSAMPLED)], "/Tasks/Index"),
+            ([("Cookie", ".AspNetCore.Antiforgery=c0ffee"), ("traceparent", UNSAMPLED)], "/Tasks/Index"),  # redirect
+            ([("Cookie", "TasksCreatedByCookie=me%40x.y"), ("traceparent", UNSAMPLED)], "/Tasks/Index")]  # new af cookie
+    got = {n: _get_scenario(tmp_path, monkeypatch, "frontend", n, ok, reqs) for n in (True, False)}
+    (rn, cn, mn, pn), (rp, cp, mp, pp) = got[True], got[False]
+    assert [r[:3] for r in rn] == [r[:3] for r in rp]
+    assert rn[0][3] == rp[0][3] and rn[1][3] == rp[1][3]  # the 4th hands out a new (random) antiforgery cookie
+    assert [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp]
+    assert mn == mp
+    if not status:
+        assert [r[0] for r in rn] == [200, 200, 302, 200]
+        assert pn == 1 and pp == 3  # the host served the two with both cookies
+        assert b"&lt;b&gt;\xc3\x9cn\xc3\xafcode&lt;/b&gt; &amp; &#39;q&#39; &#34;x&#34;" in rn[0][3]
+        assert cn[1][1].endswith("api/tasks?createdBy=o%27b%3Cr%3E%2Bx%20y%40z")
+    else:
+        assert [r[0] for r in rn][:2] == [500, 500]
+
+
+def test_frontend_list_declines_a_list_outside_the_rows(tmp_path, monkeypatch):
+    odd = [dict(_LIST[0], taskDueDate="2030-01-02T00:00:00+02:00"), _LIST[1]]
+    ok = {"/v1.0/invoke/": (200, json.dumps(odd).encode())}
+    reqs = [([("Cookie", "TasksCreatedByCookie=me%40x.y; .AspNetCore.Antiforgery=c0ffee"), ("traceparent", UNSAMPLED)],
+             "/Tasks/Index")]
+    got = {n: _get_scenario(tmp_path, monkeypatch, "frontend", n, ok, reqs) for n in (True, False)}
+    (rn, cn, mn, pn), (rp, cp, mp, pp) = got[True], got[False]
+    assert rn == rp and pn == 1 and len(cn) == 2 and len(cp) == 1  # asked twice: once native, once by the page
+
+
+@pytest.mark.parametrize("status", [{}, {"/v1.0-alpha1/state/": (500, b'{"errorCode":"ERR_STATE_QUERY"}')}],
+                         ids=["ok", "query-fails"])
+def test_api_list_native_equals_python(tmp_path, monkeypatch, status):
+    results = {"results": [{"key": t["taskId"], "data": t, "etag": "1"} for t in _LIST] + [{"key": "gone", "data": None}]}
+    ok = {"/v1.0-alpha1/state/": (200, json.dumps(results).encode())}
+    ok.update(status)
+    reqs = [([("traceparent", UNSAMPLED)], "/api/tasks?createdBy=me%40x.y"),
+            ([("traceparent", UNSAMPLED)], "/api/tasks?CreatedBy=a+%22b%22&createdby=ignored"),
+            ([("traceparent", UNSAMPLED)], "/api/tasks")]  # no creator: the controller's []
+    got = {n: _get_scenario(tmp_path, monkeypatch, "api", n, ok, reqs) for n in (True, False)}
+    (rn, cn, mn, pn), (rp, cp, mp, pp) = got[True], got[False]
+    assert [r[:2] + (r[3],) for r in rn] == [r[:2] + (r[3],) for r in rp]
+    assert [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp]
+    assert mn == mp
+    if not status:
+        assert pn == 0 and pp == 2
+        assert [t["taskId"][-4:] for t in json.loads(rn[0][3])] == ["e0f1", "950e"]  # newest first
+        assert json.loads(cn[1][3]) == {"filter": {"EQ": {"taskCreatedBy": 'a "b"'}}}
