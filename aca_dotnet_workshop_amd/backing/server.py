@@ -154,6 +154,48 @@ class BackingServices:
                 self.front.attach_store(account, db, coll, s)
         return s
 
+    def run_query(self, account: str, db: str, coll: str, raw: bytes, prefix: str, sort_keys: bool,
+                  traceparent: str = "", sent_mono: str = "", front_mono: str = "") -> tuple[int, bytes, list]:
+        """A state query of the collection, after admission (auth and RU charge are the
+        caller's): the planner sends it to the columnar / GPU accelerator or the native engine.
+        Returns (200, result JSON, headers) -- the result-size RU are debited here -- or (400,
+        the error, []).  Blocking; runs on the query pool (the Python route) or on the native
+        front's query worker (backingfront.hpp ``set_query_fn``), with no HTTP hop in between.
+        A sampled caller (the data plane passes the trace on for queries) gets the store's share
+        as spans: the query, and the planner + page run inside it."""
+        s = self.store(account, db, coll)
+        a = self.accel(account, db, coll)
+        tp = parse_traceparent(traceparent) if traceparent else None
+        span = tracer().start_span("POST query", "server", parent=tp, activate=False) if tp and tp[2] else None
+        if span is not None:  # the hops before this call, from the callers' monotonic stamps
+            now = time.monotonic()
+            for k, at in (("since_sidecar_sent_ms", sent_mono), ("since_front_forwarded_ms", front_mono)):
+                try:
+                    span.set(k, round((now - float(at)) * 1e3, 3))
+                except (TypeError, ValueError):
+                    pass
+        text = raw.decode("utf-8") if raw else "{}"
+        inner = tracer().start_span("query run", "internal", parent=span) if span is not None else None
+        try:
+            q = json.loads(text)
+            res = a.query(q, prefix, s, sort_keys) if isinstance(q, dict) else None
+            res = s.query(text, prefix, sort_keys) if res is None else res
+        except ValueError as ex:
+            if inner is not None:
+                inner.end()
+            if span is not None:
+                span.end()
+            return 400, str(ex).encode(), []
+        if inner is not None:
+            inner.end()
+        body = res if isinstance(res, bytes) else res.encode()
+        s.debit(s.query_ru(len(body)) - s.query_ru(0))  # result size part: owed after the fact
+        if span is None:
+            return 200, body, []
+        span.set("bytes", len(body))
+        span.end()
+        return 200, body, [("x-tt-handler-end-mono", f"{time.monotonic():.6f}")]
+
     def accel(self, account: str, db: str, coll: str) -> CollectionAccelerator:
         key = (account, db, coll)
         a = self.accels.get(key)
@@ -307,48 +349,19 @@ class BackingServices:
 
         async def query(req: Request) -> Response:
             s = st(req, "cosmos.read")
-            raw = req.body.decode("utf-8") or "{}"
-            prefix = req.query_get("prefix", "") or ""
             # ?project=sortkeys: {"key", "etag", "sort"} per result -- phase one of a
             # cross-partition page (the sidecar fetches the merged page's documents after)
             sort_keys = (req.query_get("project", "") or "").lower() == "sortkeys"
-            a = acc(req)
-            # a sampled caller (the data plane passes the trace on for queries) gets the
-            # store's share as spans: this handler, and the planner + page run on the pool
-            tp = parse_traceparent(req.headers.get("traceparent"))
-            span = tracer().start_span("POST query", "server", parent=tp, activate=False) if tp and tp[2] else None
-            if span is not None:  # the hops before this handler, from the callers' monotonic stamps
-                now = time.monotonic()
-                for k, at in (("since_sidecar_sent_ms", "x-tt-sent-mono"), ("since_front_forwarded_ms", "x-tt-front-mono")):
-                    try:
-                        span.set(k, round((now - float(req.headers.get(at))) * 1e3, 3))
-                    except (TypeError, ValueError):
-                        pass
-
-            def run() -> str | bytes:
-                inner = tracer().start_span("query run", "internal", parent=span) if span is not None else None
-                try:
-                    q = json.loads(raw)
-                    text = a.query(q, prefix, s, sort_keys) if isinstance(q, dict) else None
-                    return s.query(raw, prefix, sort_keys) if text is None else text
-                finally:
-                    if inner is not None:
-                        inner.end()
             if (t := throttled(req, s, s.query_ru(0))) is not None:
                 return t
-            try:
-                text = await asyncio.get_running_loop().run_in_executor(self.query_pool, run)
-            except ValueError as ex:
-                if span is not None:
-                    span.end()
-                return problem(400, detail=str(ex))
-            body = text if isinstance(text, bytes) else text.encode()
-            s.debit(s.query_ru(len(body)) - s.query_ru(0))  # result size part: owed after the fact
-            if span is not None:
-                span.set("bytes", len(body))
-                span.end()
-                return Response(body, 200, [("x-tt-handler-end-mono", f"{time.monotonic():.6f}")], "application/json")
-            return Response(body, 200, None, "application/json")
+            p = req.path_params
+            status, body, headers = await asyncio.get_running_loop().run_in_executor(
+                self.query_pool, self.run_query, p["account"], p["db"], p["coll"], req.body,
+                req.query_get("prefix", "") or "", sort_keys, req.headers.get("traceparent") or "",
+                req.headers.get("x-tt-sent-mono") or "", req.headers.get("x-tt-front-mono") or "")
+            if status != 200:
+                return problem(status, detail=body.decode("utf-8", "replace"))
+            return Response(body, 200, headers or None, "application/json")
 
         async def transaction(req: Request) -> Response:
             s = st(req, "cosmos.write")
@@ -771,6 +784,8 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
         threads = int(os.environ.get("TT_BACKING_FRONT_THREADS", "4"))
         front = svc.N.BackingFront(host, port, os.path.join(priv_dir, "py.sock"), threads, uds or "")
         svc.attach_front(front)
+        if os.environ.get("TT_BACKING_QUERY_WORKER", "1") != "0":
+            front.set_query_fn(svc.run_query)  # scans run on the front's query worker (run_query)
         bound = front.port()
     else:
         bound = await srv.listen_tcp(host, port)

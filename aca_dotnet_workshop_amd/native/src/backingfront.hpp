@@ -20,6 +20,9 @@
 // (docstore.hpp ColumnMirror) on every write, whichever front made it.
 #pragma once
 
+#include <condition_variable>
+#include <deque>
+
 #include <sys/eventfd.h>
 
 #include <atomic>
@@ -226,12 +229,47 @@ class BackingFront {
   }
   ~BackingFront() { stop(); }
 
+  // A query the indexes do not answer (a scan the columnar / GPU accelerator may take) runs on
+  // one query worker thread through `query_fn` -- the Python planner, backing/server.py
+  // BackingServices.run_query, called with the GIL -- and its answer goes back from the front's
+  // loop: the page of results makes no extra HTTP hop through the Python server's event loop.
+  struct QueryJob {
+    std::string account, db, coll, body, prefix, traceparent, sent_mono, front_mono;
+    bool sort_keys = false;
+  };
+  struct QueryResult {
+    int status = 0;  // 0: not taken -- the request goes to the Python server
+    std::string body;
+    ev::HeaderList headers;
+  };
+  using QueryFn = std::function<QueryResult(const QueryJob&)>;
+  void set_query_fn(QueryFn fn) {
+    std::lock_guard l(q_mu_);
+    query_fn_ = std::move(fn);
+    if (!q_thread_.joinable() && query_fn_) {
+      q_thread_ = std::thread([this] {
+        pthread_setname_np(pthread_self(), "tt-front-query");
+        query_loop();
+      });
+    }
+  }
+
   int port() const { return port_; }
   int threads() const { return (int)shards_.size(); }
 
   void stop() {
     if (stopped_) return;
     stopped_ = true;
+    {
+      std::lock_guard l(q_mu_);
+      q_stop_ = true;
+    }
+    q_cv_.notify_all();
+    if (q_thread_.joinable()) q_thread_.join();
+    {
+      std::lock_guard l(q_mu_);
+      query_fn_ = nullptr;  // drop the Python callable before the interpreter may go
+    }
     for (auto& sh : shards_) sh->request_stop();
     for (auto& sh : shards_) sh->join();
   }
@@ -268,6 +306,18 @@ class BackingFront {
   struct Coll {
     DocStore* store = nullptr;
   };
+  struct Shard;
+  struct QueuedQuery {
+    std::shared_ptr<QueryJob> job;
+    Shard* sh = nullptr;
+    ev::Reply reply;
+  };
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<QueuedQuery> q_jobs_;
+  QueryFn query_fn_;
+  std::thread q_thread_;
+  bool q_stop_ = false;
   struct Parked {
     std::string ns, entity;
     size_t max;
@@ -292,6 +342,7 @@ class BackingFront {
     std::atomic<bool> stop_flag{false};
     std::mutex mu;
     std::vector<std::string> posted;               // cross-thread notifications
+    std::vector<std::function<void()>> tasks;      // cross-thread work for this loop (query answers)
     std::multimap<std::string, Parked> parked;     // "ns|entity" -> waiting receives
 
     explicit Shard(BackingFront& front) : f(front), client(loop) {
@@ -327,6 +378,13 @@ class BackingFront {
       }
       wake();
     }
+    void post_task(std::function<void()> fn) {
+      {
+        std::lock_guard l(mu);
+        tasks.push_back(std::move(fn));
+      }
+      wake();
+    }
     void request_stop() {
       stop_flag = true;
       wake();
@@ -342,11 +400,14 @@ class BackingFront {
         return;
       }
       std::vector<std::string> keys;
+      std::vector<std::function<void()>> todo;
       {
         std::lock_guard l(mu);
         keys.swap(posted);
+        todo.swap(tasks);
       }
       for (auto& k : keys) f.retry_parked(*this, k);
+      for (auto& fn : todo) fn();
     }
     void on_tick(double now) {
       if (stop_flag) {
@@ -449,7 +510,7 @@ class BackingFront {
       return;
     if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkget" && m.method == "POST" && handle_bulkget(m, r, seg))
       return;
-    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "query" && m.method == "POST" && handle_query(m, r, seg, qs))
+    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "query" && m.method == "POST" && handle_query(sh, m, r, seg, qs))
       return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
@@ -664,20 +725,96 @@ class BackingFront {
     return (std::strtol(tp->c_str() + tp->size() - 2, nullptr, 16) & 1) != 0;
   }
 
-  bool handle_query(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
+  bool to_query_worker(Shard& sh, ev::Message& m, ev::Reply& r, Coll* c, const std::vector<std::string>& seg,
+                       const std::string& qs) {
+    {
+      std::lock_guard l(q_mu_);
+      if (!query_fn_ || q_stop_) return false;  // no worker: the Python server's route
+    }
+    if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
+    if (throttled(m, r, c->store, DocStore::query_ru(0))) return true;
+    count("doc.query_worker");
+    auto job = std::make_shared<QueryJob>();
+    job->account = seg[1];
+    job->db = seg[2];
+    job->coll = seg[3];
+    job->body = std::move(m.body);
+    job->prefix = query_get(qs, "prefix");
+    std::string project = query_get(qs, "project");
+    for (auto& ch : project) ch = (char)std::tolower((unsigned char)ch);
+    job->sort_keys = project == "sortkeys";
+    if (const std::string* tp = m.header("traceparent")) job->traceparent = *tp;
+    if (const std::string* t = m.header("x-tt-sent-mono")) job->sent_mono = *t;
+    char t[32];
+    std::snprintf(t, sizeof t, "%.6f", ev::now_s());
+    job->front_mono = t;
+    {
+      std::lock_guard l(q_mu_);
+      q_jobs_.push_back({job, &sh, r});
+    }
+    q_cv_.notify_one();
+    return true;
+  }
+
+  void query_loop() {
+    while (true) {
+      QueuedQuery qq;
+      QueryFn fn;
+      {
+        std::unique_lock l(q_mu_);
+        q_cv_.wait(l, [this] { return q_stop_ || !q_jobs_.empty(); });
+        if (q_stop_) {
+          for (auto& j : q_jobs_)  // answered from their loops: the front is going down
+            j.sh->post_task([r = j.reply] { r.json(503, bf::problem_json(503, "shutting down")); });
+          q_jobs_.clear();
+          return;
+        }
+        qq = std::move(q_jobs_.front());
+        q_jobs_.pop_front();
+        fn = query_fn_;
+      }
+      QueryResult res;
+      try {
+        res = fn(*qq.job);
+      } catch (const std::exception& ex) {
+        res.status = 500;
+        res.body = ex.what();
+      }
+      qq.sh->post_task([this, qq, res = std::move(res)]() mutable {
+        count("doc.query_worker_done");
+        if (res.status == 200) {
+          if (!res.headers.empty()) {  // a traced query: when the front had the answer
+            char t[32];
+            std::snprintf(t, sizeof t, "%.6f", ev::now_s());
+            res.headers.emplace_back("x-tt-front-rx-mono", t);
+          }
+          res.headers.emplace_back("content-type", "application/json");
+          qq.reply.send(200, res.headers, res.body);
+        } else {
+          qq.reply.send(res.status ? res.status : 500, {{"content-type", "application/problem+json; charset=utf-8"}},
+                        bf::problem_json(res.status ? res.status : 500, res.body));
+        }
+      });
+    }
+  }
+
+  bool handle_query(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
     Coll* c = nullptr;
     {
       std::shared_lock l(cfg_mu_);
       auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
       if (it != colls_.end() && it->second->store) c = it->second.get();
     }
-    if (!c || sampled(m)) return false;
+    if (!c) return false;
+    bool indexed = false;
     try {
       Value q = parse(m.body.empty() ? std::string("{}") : m.body);
-      if (q.t != Value::Object || !indexable(q.get("filter"))) return false;
+      if (q.t != Value::Object) return false;
+      indexed = indexable(q.get("filter"));
     } catch (const ParseError&) {
       return false;
     }
+    if (!indexed || sampled(m)) return to_query_worker(sh, m, r, c, seg, qs);
     if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
     if (throttled(m, r, c->store, DocStore::query_ru(0))) return true;
     std::string body;

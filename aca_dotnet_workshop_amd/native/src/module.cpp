@@ -775,6 +775,31 @@ PYBIND11_MODULE(_ttnative, m) {
       .def("attach_broker", [](BackingFront& f, const std::string& ns, Broker& b) { f.attach_broker(ns, &b); },
            py::keep_alive<1, 3>())
       .def("set_policy", &BackingFront::set_policy, py::arg("mode"), py::arg("keys"), py::arg("grants"))
+      .def("set_query_fn",
+           [](BackingFront& f, py::function fn) {
+             // the worker thread calls back into Python with the GIL; `fn` returns
+             // (status, body bytes, [(header, value)]) -- 0 / None: not taken
+             // released with the GIL held (stop() may drop it on a thread without it)
+             std::shared_ptr<py::function> held(new py::function(std::move(fn)), [](py::function* p) {
+               py::gil_scoped_acquire g;
+               delete p;
+             });
+             f.set_query_fn([held](const BackingFront::QueryJob& j) {
+               BackingFront::QueryResult out;
+               py::gil_scoped_acquire g;
+               py::object r = (*held)(j.account, j.db, j.coll, py::bytes(j.body), j.prefix, j.sort_keys, j.traceparent,
+                                      j.sent_mono, j.front_mono);
+               if (r.is_none()) return out;
+               auto t = r.cast<py::tuple>();
+               out.status = t[0].cast<int>();
+               out.body = t[1].cast<std::string>();
+               for (auto h : t[2]) {
+                 auto kv = h.cast<py::tuple>();
+                 out.headers.emplace_back(kv[0].cast<std::string>(), kv[1].cast<std::string>());
+               }
+               return out;
+             });
+           }, py::arg("fn"))
       .def("notify", &BackingFront::notify)
       .def("stats", &BackingFront::stats)
       .def("stop", &BackingFront::stop, py::call_guard<py::gil_scoped_release>());

@@ -338,9 +338,13 @@ class Column:
             self._rank_lo = n
             return old_r[:n]
         new = np.array(self.values[m:], dtype=str)
-        norder = np.argsort(new, kind="stable")
-        new_sorted = new[norder]
         k = new.size
+        if k < 2 or bool(np.all(new[1:] >= new[:-1])):  # written in order (timestamps): no sort
+            norder = np.arange(k, dtype=np.int64)
+            new_sorted = new
+        else:
+            norder = np.argsort(new, kind="stable")
+            new_sorted = new[norder]
         # insertion point of the smallest new value: only the old values from there on move
         pos0 = m if m == 0 or new_sorted[0] > srt[m - 1] else int(np.searchsorted(srt[:m], new_sorted[0]))
         if new_sorted.dtype.itemsize <= srt.dtype.itemsize and m - pos0 <= 4 * k + 65536:
@@ -361,11 +365,19 @@ class Column:
                 srt[m:n] = new_sorted
                 ids[m:n] = m + norder
             else:
-                vals = np.concatenate([srt[pos0:m], new_sorted])
-                who = np.concatenate([tail_ids, m + norder])
-                o = np.argsort(vals, kind="stable")
-                srt[pos0:n] = vals[o]
-                ids[pos0:n] = who[o]
+                # merge two sorted runs (the old tail, the new values) without a comparison
+                # sort: each new value lands after the old ones equal to it (a stable sort of
+                # old-then-new would do the same)
+                tail = srt[pos0:m].copy()
+                ins = np.searchsorted(tail, new_sorted, side="right")
+                at_new = ins + np.arange(k)                                  # merged positions of new values
+                at_old = np.arange(tail.size) + np.searchsorted(ins, np.arange(tail.size), side="right")
+                seg_v = np.empty(tail.size + k, dtype=srt.dtype)
+                seg_i = np.empty(tail.size + k, dtype=np.int64)
+                seg_v[at_old], seg_v[at_new] = tail, new_sorted
+                seg_i[at_old], seg_i[at_new] = tail_ids, m + norder
+                srt[pos0:n] = seg_v
+                ids[pos0:n] = seg_i
             old_r[ids[pos0:n]] = np.arange(pos0 + 1, n + 1)
             self._str_sorted = (srt, n, old_r, ids)
             self._rank_lo = int(min(int(tail_ids.min()), m)) if tail_ids.size else m

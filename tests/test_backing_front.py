@@ -404,3 +404,6 @@ def test_indexed_queries_run_on_the_native_front(monkeypatch):
     assert nat == py
     want_native = sum(1 for q in queries if indexable(q["filter"])) + 1  # + the sort-keys projection
     assert fs["requests"].get("doc.query", 0) == want_native, (fs["requests"], want_native)
+    # the rest ran on the front's query worker (the Python planner called from C++), not
+    # through the Python server: the sampled one too, which records the store's spans there
+    assert fs["requests"].get("doc.query_worker", 0) == len(queries) + 1 - (want_native - 1), fs["requests"]
