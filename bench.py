@@ -62,6 +62,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--overdue-sweep-ms", type=int, default=1000,
                     help="mixed load: trigger the processor's overdue cron job every N ms during the run "
                          "(OverdueTasks:Query=range -> GPU columnar scan in the backing services); 0 = off")
+    ap.add_argument("--mark-chunk", type=int, default=256,
+                    help="the sweep's markoverdue calls carry at most this many tasks, concurrently "
+                         "(OverdueTasks:MarkChunk; 0 = one call per page, as the reference)")
     ap.add_argument("--past-due-every", type=int, default=64,
                     help="every Nth createTask body is due yesterday, so the sweeps mark real tasks overdue")
     ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "native"),
@@ -1083,6 +1086,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                  "backendApiCpu": caps["api"], "processorCpu": caps["processor"], "appMemory": "2Gi",
                  "appInsightsSamplingPercentage": a.trace_sampling,
                  "overdueQuery": "range" if sweep else "equality", "overduePageSize": OVERDUE_PAGE if sweep else 0,
+                 "overdueMarkChunk": a.mark_chunk,
                  "environmentName": f"cae-bench-r{d.rank}"}
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
                       overrides)
