@@ -464,6 +464,7 @@ class AppHost {
     std::vector<Event> out;
     std::lock_guard<std::mutex> g(ev_mu_);
     out.swap(events_);
+    wake_pending_ = false;
     return out;
   }
 
@@ -602,6 +603,7 @@ class AppHost {
   std::vector<std::function<void()>> cmds_;
   std::mutex ev_mu_;
   std::vector<Event> events_;
+  bool wake_pending_ = false, flush_armed_ = false;  // under ev_mu_
 
   // loop-thread state
   std::unordered_map<uint64_t, ev::Reply> replies_;
@@ -1019,19 +1021,40 @@ class AppHost {
     pending_replies_.store(replies_.size());
   }
 
+  // Python is woken once per batch of events.  A finished log line (a native route's record on
+  // the sink's fast path) is not waited for: it does not wake Python on its own but rides along
+  // with the next request / response event, or goes up within kLogFlushS -- the native routes'
+  // traffic then costs the Python thread a wake-up per flush, not per request.
+  static constexpr double kLogFlushS = 0.005;
   void emit(Event&& e) {
     e.t = ev::now_s();
-    bool was_empty;
+    const bool lazy = e.kind == Event::LOG && !e.line.empty();
+    bool wake = false, arm = false;
     {
       std::lock_guard<std::mutex> g(ev_mu_);
-      was_empty = events_.empty();
       events_.push_back(std::move(e));
+      if (!wake_pending_) {
+        if (!lazy) wake = wake_pending_ = true;
+        else if (!flush_armed_) arm = flush_armed_ = true;
+      }
     }
-    if (was_empty) {
-      uint64_t one = 1;
-      ssize_t n = ::write(to_py_, &one, sizeof one);
-      (void)n;
+    if (wake) wake_python();
+    if (arm) {
+      loop_.call_later(kLogFlushS, [this] {
+        bool w = false;
+        {
+          std::lock_guard<std::mutex> g(ev_mu_);
+          flush_armed_ = false;
+          if (!events_.empty() && !wake_pending_) w = wake_pending_ = true;
+        }
+        if (w) wake_python();
+      });
     }
+  }
+  void wake_python() {
+    uint64_t one = 1;
+    ssize_t n = ::write(to_py_, &one, sizeof one);
+    (void)n;
   }
 
   int listen_now(int server, const ev::Endpoint& ep, std::shared_ptr<ev::TlsContext> tls = nullptr) {

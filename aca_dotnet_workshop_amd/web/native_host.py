@@ -281,6 +281,14 @@ class NativeHost:
         except Exception:
             pass
         self.h.stop()
+        try:  # log records the I/O thread held back for its next flush (apphost.hpp emit)
+            for ev in self.h.drain():
+                if ev[0] == 3:
+                    _native_log(ev[1], ev[2], ev[3], ev[4], ev[5], ev[6])
+                elif ev[0] == 4:
+                    _native_lines(ev[1], ev[2], ev[3])
+        except Exception:
+            log.exception("native host: flushing log records at close failed")
         for fut in self.pending.values():
             if not fut.done():
                 fut.set_exception(ConnectionClosed("native host stopped"))
