@@ -926,22 +926,26 @@ class ColumnarIndex:
                               "seq": seq}
         else:
             lo, hi = st["synced"], self.n
+            # the appended rows of every column, the sequence and the liveness words go up in
+            # one scatter launch (GpuKernels.upload), not one copy each
+            segs = []
             for i, w in enumerate(widths):
                 if w != st["widths"][i]:
                     st["cols"][i] = torch.from_numpy(self._device_codes(i, w)).to(dev)
                     st["widths"][i] = w
                 elif hi > lo and w == 0:  # whole bytes of 4 rows: re-pack the edge bytes
                     a, b = lo // 4, (hi + 3) // 4
-                    st["cols"][i][a:b].copy_(torch.from_numpy(self._narrow(i, 4 * a, 4 * b, 0)))
+                    segs.append((st["cols"][i].data_ptr() + a, self._narrow(i, 4 * a, 4 * b, 0)))
                 elif hi > lo:
-                    st["cols"][i][lo:hi].copy_(torch.from_numpy(self._narrow(i, lo, hi, w)))
+                    segs.append((st["cols"][i].data_ptr() + lo * w, self._narrow(i, lo, hi, w)))
             if hi > lo:
-                st["seq"][lo:hi].copy_(torch.from_numpy(self.seq[lo:hi].astype(np.int32)))
+                segs.append((st["seq"].data_ptr() + 4 * lo, self.seq[lo:hi].astype(np.int32)))
             if self._tomb_dirty:
-                st["live"].copy_(torch.from_numpy(self._live_words(0, nwords)))
+                segs.append((st["live"].data_ptr(), self._live_words(0, nwords)))
             elif hi > lo:
                 w0, w1 = lo // 16, (hi + 15) // 16
-                st["live"][w0:w1].copy_(torch.from_numpy(self._live_words(w0, w1)))
+                segs.append((st["live"].data_ptr() + 2 * w0, self._live_words(w0, w1)))
+            kernels.upload(segs)
             st["synced"] = hi
         self._full_dirty = False
         self._tomb_dirty = False
@@ -982,8 +986,11 @@ class ColumnarIndex:
                                 "ver": c.rank_version, "table": None, "synced": 0}
             table = c.ranks().astype(np.int32) if c.values else np.zeros(1, dtype=np.int32)
             cur["table"] = torch.from_numpy(table).to(kernels.device)
-        src = torch.from_numpy(np.array([[st["cols"][col].data_ptr(), st["widths"][col]]], dtype=np.int64)).to(kernels.device)
-        kernels.rank_encode(src, cur["table"], lo, self.n, cur["t"], w)
+        key = (st["cols"][col].data_ptr(), st["widths"][col])
+        if cur.get("src_key") != key:  # the source column's descriptor: uploaded when it changes
+            cur["src"] = torch.from_numpy(np.array([list(key)], dtype=np.int64)).to(kernels.device)
+            cur["src_key"] = key
+        kernels.rank_encode(cur["src"], cur["table"], lo, self.n, cur["t"], w)
         cur["synced"] = self.n
 
     def device_program(self, prog: Program, kernels):
@@ -1160,7 +1167,7 @@ class ColumnarIndex:
                 if r.size > lo:  # the ids whose rank is new or moved (the newest ones)
                     tail = r[lo:].astype(np.int32)
                     ent["host"][off + lo:off + r.size] = tail
-                    ent["dev"][off + lo:off + r.size].copy_(torch.from_numpy(tail))
+                    kernels.upload([(ent["dev"].data_ptr() + 4 * (off + lo), tail)])
                 ent["seqs"][i] = c.rank_seq
         for row, off in zip(specs_rows, ent["offs"]):
             row[1] = int(off)

@@ -64,6 +64,8 @@ def load_library(build: bool = True) -> ctypes.CDLL:
     lib.tt_launch_page.argtypes = [P, I64, P, P, I32, P, I32, P, I32, P, P, I32, P, I32, P, P, P, I32, I32,
                                    ctypes.c_uint64, P, P, P]
     lib.tt_launch_page.restype = ctypes.c_int
+    lib.tt_launch_scatter_segments.argtypes = [P, I64, I32, I64, P]
+    lib.tt_launch_scatter_segments.restype = ctypes.c_int
     lib.tt_host_alloc.argtypes = [I64]
     lib.tt_host_alloc.restype = ctypes.c_void_p
     lib.tt_host_device_ptr.argtypes = [P]
@@ -202,6 +204,43 @@ class GpuKernels:
             arr = np.ctypeslib.as_array((ctypes.c_int32 * size).from_address(host))
             mb = self._bufs[name] = (host, dev, arr)
         return mb
+
+    uploads = 0  # scatter launches (one per mirror sync)
+    upload_segments = 0
+
+    def upload(self, segments) -> None:
+        """Write ``segments`` -- [(device address, host numpy array)] -- to the device in ONE
+        kernel launch (``hip/mirror_upload.hip`` tt_scatter_segments): the payloads and their
+        segment table are staged in a pinned, device-mapped mailbox the kernel reads directly,
+        instead of one copy (copyBuffer + DMA set-up) per segment.  Stream-ordered with every
+        other launch of this process (the current stream)."""
+        import numpy as np
+        segs = [(int(d), np.ascontiguousarray(a).view(np.uint8).reshape(-1)) for d, a in segments if a.size]
+        if not segs:
+            return
+        table = (24 * len(segs) + 15) & ~15
+        offs, at = [], table
+        for _, b in segs:
+            offs.append(at)
+            at += (b.size + 15) & ~15
+        with self._total_lock:
+            stream = self._stream()
+            host, dev, arr = self._mailbox("upload", (at + 3) // 4)
+            # the previous scatter read this buffer: it has finished before the bytes change
+            # (every page / zone call synchronises anyway, so this rarely waits)
+            self._sync(stream)
+            buf = arr.view(np.uint8)
+            desc = np.empty((len(segs), 3), dtype=np.int64)
+            for i, ((d, b), o) in enumerate(zip(segs, offs)):
+                buf[o:o + b.size] = b
+                desc[i] = (o, d, b.size)
+            buf[:24 * len(segs)] = desc.view(np.uint8).reshape(-1)
+            rc = self.lib.tt_launch_scatter_segments(ctypes.c_void_p(dev), 0, len(segs),
+                                                     max(b.size for _, b in segs), stream)
+            if rc != 0:
+                raise RuntimeError(f"tt_scatter_segments launch failed ({rc})")
+            self.uploads += 1
+            self.upload_segments += len(segs)
 
     def _sync(self, stream) -> None:
         rc = self.lib.blocking_sync(stream)  # GIL released while waiting (see load_library)

@@ -1094,3 +1094,39 @@ def test_gpu_zone_argmin_matches_numpy():
 
 
 TILE_ROWS = 8192
+
+
+@pytest.mark.gpu
+def test_gpu_scatter_upload_writes_every_segment():
+    """GpuKernels.upload (hip/mirror_upload.hip): segments of every size and destination
+    alignment -- 1..70 KB, odd byte offsets, 2- and 4-byte aligned, 16-byte aligned -- land
+    exactly where they go in one launch, and nothing around them changes."""
+    import torch
+    k = _kernels()
+    rng = np.random.default_rng(7)
+    dst = torch.zeros(1 << 20, dtype=torch.uint8, device=k.device)
+    want = np.zeros(1 << 20, dtype=np.uint8)
+    segs, at = [], 0
+    for size in (1, 3, 15, 16, 17, 31, 33, 255, 4096, 4097, 70000, 5, 64):
+        at += int(rng.integers(1, 40))  # any alignment
+        payload = rng.integers(0, 256, size=size, dtype=np.uint8)
+        segs.append((dst.data_ptr() + at, payload))
+        want[at:at + size] = payload
+        at += size
+    for align in (2, 4, 16):
+        at = (at + align - 1) // align * align
+        payload = rng.integers(0, 256, size=1000 + align, dtype=np.uint8)
+        segs.append((dst.data_ptr() + at, payload))
+        want[at:at + payload.size] = payload
+        at += payload.size
+    words = rng.integers(-5, 5, size=333).astype(np.int32)  # typed payloads go up as their bytes
+    at = (at + 3) // 4 * 4
+    segs.append((dst.data_ptr() + at, words))
+    want[at:at + 4 * words.size] = words.view(np.uint8)
+    before = k.uploads
+    k.upload(segs)
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), want)
+    assert k.uploads == before + 1
+    k.upload([])  # nothing to write: no launch
+    assert k.uploads == before + 1
