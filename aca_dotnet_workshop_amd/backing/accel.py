@@ -90,7 +90,8 @@ class CollectionAccelerator:
         self.lock = threading.Lock()  # one query / sync at a time per collection
         self._bg: threading.Thread | None = None
         self._bg_stop = threading.Event()
-        self.sync_interval = max(0.0, float(os.environ.get("TT_QUERY_MIRROR_SYNC_MS", "100")) / 1000.0)
+        # 40 ms: a query then finds at most ~40 ms of writes to sync, rank and upload itself
+        self.sync_interval = max(0.0, float(os.environ.get("TT_QUERY_MIRROR_SYNC_MS", "40")) / 1000.0)
 
     def attach(self, store) -> None:
         """New collection: start mirroring the configured paths from its first write."""

@@ -62,9 +62,11 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--overdue-sweep-ms", type=int, default=1000,
                     help="mixed load: trigger the processor's overdue cron job every N ms during the run "
                          "(OverdueTasks:Query=range -> GPU columnar scan in the backing services); 0 = off")
-    ap.add_argument("--mark-chunk", type=int, default=256,
+    ap.add_argument("--mark-chunk", type=int, default=128,
                     help="the sweep's markoverdue calls carry at most this many tasks, concurrently "
-                         "(OverdueTasks:MarkChunk; 0 = one call per page, as the reference)")
+                         "(OverdueTasks:MarkChunk; 0 = one call per page, as the reference).  ~1,000 "
+                         "tasks a sweep: 128 spreads them over the 4 API replicas in 8 calls; the mark "
+                         "hop took 6.6 ms vs 8.0 ms at 256 (gpurun_out/r5d)")
     ap.add_argument("--past-due-every", type=int, default=64,
                     help="every Nth createTask body is due yesterday, so the sweeps mark real tasks overdue")
     ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "native"),
