@@ -45,6 +45,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <future>
 #include <map>
 #include <memory>
@@ -80,20 +81,21 @@ struct Event {
 struct Template {
   enum Field { kId = 0, kName = 1, kAssignedTo = 2 };
   std::vector<std::string> lits;  // fields.size() + 1 literal pieces
-  std::vector<int> fields;
+  std::vector<int> fields;        // indices into the route's field names
   bool set = false;
 
-  static Template compile(const std::string& text, const std::string& args) {
+  // `known`: the fields this route can fill, by name (default: a created task's)
+  static Template compile(const std::string& text, const std::string& args,
+                          const std::vector<std::string>& known = {"id", "name", "assigned_to"}) {
     Template t;
     t.set = true;
     std::vector<int> names;
     for (size_t a = 0; a < args.size();) {
       size_t b = args.find(',', a);
       std::string f = args.substr(a, b == std::string::npos ? std::string::npos : b - a);
-      if (f == "id") names.push_back(kId);
-      else if (f == "name") names.push_back(kName);
-      else if (f == "assigned_to") names.push_back(kAssignedTo);
-      else throw std::invalid_argument("native route template: unknown field " + f);
+      auto it = std::find(known.begin(), known.end(), f);
+      if (it == known.end()) throw std::invalid_argument("native route template: unknown field " + f);
+      names.push_back((int)(it - known.begin()));
       if (b == std::string::npos) break;
       a = b + 1;
     }
@@ -121,9 +123,13 @@ struct Template {
     return t;
   }
   std::string render(const std::string& id, const std::string& name, const std::string& assigned_to) const {
+    return render_with([&](int f) -> const std::string& { return f == kId ? id : f == kName ? name : assigned_to; });
+  }
+  template <class Value>
+  std::string render_with(Value&& value) const {
     std::string out = lits[0];
     for (size_t i = 0; i < fields.size(); ++i) {
-      out += fields[i] == kId ? id : fields[i] == kName ? name : assigned_to;
+      out += value(fields[i]);
       out += lits[i + 1];
     }
     return out;
@@ -250,7 +256,7 @@ inline bool cookie_value(std::string_view cookie, std::string_view name, std::st
 
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
-  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5 };
+  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6 };
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -275,6 +281,10 @@ struct NativeRoute {
   // kApiList: GET api/tasks?createdBy= -> state query (the manager's query text around the
   // JSON-encoded creator) -> the TaskModel array newest first
   std::string query_target, query_prefix, query_suffix;
+  // kApiOverdue: GET api/overduetasks[?limit=] -> the manager's range query (fields: the local
+  // midnight, the page size) -> the TaskModel page oldest first + whether the store has more
+  Template overdue_query, log_overdue;
+  std::string page_default, more_header;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -484,6 +494,7 @@ class AppHost {
     else if (kind == "processor_notify") r->kind = NativeRoute::kProcessorNotify;
     else if (kind == "frontend_list") r->kind = NativeRoute::kFrontendList;
     else if (kind == "api_list") r->kind = NativeRoute::kApiList;
+    else if (kind == "api_overdue") r->kind = NativeRoute::kApiOverdue;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -515,6 +526,15 @@ class AppHost {
       for (int i = 0; i < 4; ++i)
         r->rows[i] = Pieces::parse(get(combos[i]), {"task_id", "task_name", "task_assigned_to", "due"});
       if (r->list_target.empty() || r->af_key.empty()) throw std::invalid_argument("frontend_list needs its target and key");
+    } else if (r->kind == NativeRoute::kApiOverdue) {
+      r->query_target = get("query_target");
+      r->overdue_query = Template::compile(get("query"), get("query_args"), {"midnight", "page"});
+      r->log_overdue = Template::compile(get("log_overdue"), get("log_overdue_args"), {"midnight", "page"});
+      r->page_default = get("page_default");
+      r->more_header = get("more_header");
+      if (r->query_target.empty() || get("query").empty() || r->page_default.empty() || r->more_header.empty() ||
+          get("log_overdue").empty())
+        throw std::invalid_argument("api_overdue needs its query, page size, log template and header");
     } else if (r->kind == NativeRoute::kApiList) {
       r->query_target = get("query_target");
       r->query_prefix = get("query_prefix");
@@ -823,6 +843,36 @@ class AppHost {
     return true;
   }
 
+  // kApiOverdue (services/backend_api/app.py get_overdue + TasksStoreManager.overdue_page_json)
+  bool api_overdue(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const NativeRoute& r = *j->route;
+    std::string page = r.page_default, limit;
+    if (query_param(m.target, "limit", limit) && !limit.empty() && limit.size() < 10 &&
+        std::all_of(limit.begin(), limit.end(), [](char c) { return c >= '0' && c <= '9'; }) && std::stol(limit) > 0)
+      page = std::to_string(std::stol(limit));  // str.isdigit, then int(): leading zeros go
+    std::time_t now = std::time(nullptr);
+    std::tm lt{};
+    localtime_r(&now, &lt);  // DateTime.Today: the local date (containers run in UTC)
+    char mid[32];
+    std::snprintf(mid, sizeof mid, "%04d-%02d-%02dT00:00:00", lt.tm_year + 1900, lt.tm_mon + 1, lt.tm_mday);
+    const std::string midnight = mid;
+    auto value = [&](int f) -> const std::string& { return f == 0 ? midnight : page; };
+    log_event(r, *j, r.log_overdue.render_with(value));
+    native_inflight_.fetch_add(1);
+    client_.request(r.sidecar, "POST", r.query_target, j->out_headers, r.overdue_query.render_with(value), r.timeout_s,
+                    [this, j](ev::ClientResult&& res) {
+                      if (res.err || res.resp.status >= 300) return hand_over(*j, "query", res);
+                      std::string out;
+                      size_t count = 0;
+                      bool more = false;
+                      if (!::taskcodec::query_tasks(res.resp.body, out, count, true, &more, false)) return decline(*j);
+                      const NativeRoute& r = *j->route;
+                      finish(*j, r.status, {{"Content-Type", r.content_type}, {r.more_header, more ? "true" : "false"}},
+                             out);
+                    });
+    return true;
+  }
+
   // kApiList (services/backend_api/app.py get_tasks + TasksStoreManager.tasks_by_creator_json)
   bool api_list(const std::shared_ptr<NativeJob>& j, const Message& m) {
     const NativeRoute& r = *j->route;
@@ -920,7 +970,8 @@ class AppHost {
       return false;
     }
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
-    if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList) {
+    if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList ||
+        r->kind == NativeRoute::kApiOverdue) {
       auto j = std::make_shared<NativeJob>();
       j->route = r;
       j->server = server;
@@ -931,7 +982,9 @@ class AppHost {
       j->out_headers.emplace_back("traceparent", j->traceparent);
       if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
       j->out_headers.emplace_back("Content-Type", "application/json");
-      bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m) : api_list(j, m);
+      bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m)
+                   : r->kind == NativeRoute::kApiList    ? api_list(j, m)
+                                                         : api_overdue(j, m);
       if (!taken) return false;
       j->req = std::move(m);
       j->reply = std::move(reply);

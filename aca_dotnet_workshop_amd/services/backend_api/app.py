@@ -65,6 +65,15 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     list_native = getattr(manager, "native_list_route", None)
     if os.environ.get("TT_READ_PATH", "").lower() == "bind":  # A/B: bind a TaskModel per task
         fast_list = list_native = None
+    overdue_native = getattr(manager, "native_overdue_route", None)
+    overdue_spec = overdue_native() if overdue_native is not None and getattr(manager, "overdue_page_json", None) \
+        else None
+    overdue_what = overdue_spec.pop("what") if overdue_spec else {}
+    if overdue_spec:
+        # GET api/overduetasks on the app host's I/O thread: the manager's range query and log line
+        overdue_spec["cfg"].update({"status": 200, "content_type": "application/json; charset=utf-8",
+                                    "more_header": MORE_HEADER})
+        app.services.setdefault("native_routes", []).append(overdue_spec)
     list_spec = list_native() if fast_list is not None and list_native is not None else None
     list_what = list_spec.pop("what") if list_spec else {}
     if list_spec:
@@ -143,6 +152,9 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/overduetasks", ("GET",), name="GetOverdueTasks", tag="OverdueTasks", query=["limit"],
                responses={200: [TaskModel]})
     async def get_overdue(req: Request) -> Response:
+        failed = native_route_failure(req, overdue_what) if overdue_what else None
+        if failed is not None:  # the native route's query failed: the SDK's error
+            raise failed
         raw = req.query_get("limit") or ""
         limit = int(raw) if raw.isdigit() else None  # page size of the range sweep (OverdueTasks:Query=range)
         if fast_page is not None:

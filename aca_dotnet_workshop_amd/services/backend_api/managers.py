@@ -45,6 +45,7 @@ log = logging.getLogger("TasksManager")
 # definition, so the native lines follow any edit here
 LOG_SAVE_NEW = "Save a new task with name: '%s' to state store"
 LOG_PUBLISH = "Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'"
+LOG_OVERDUE_PAGE = "Getting open tasks due before: '%s' (page of %d)"
 
 STORE_NAME = "statestore"
 PUBSUB_NAME = "dapr-pubsub-servicebus"
@@ -343,7 +344,7 @@ class TasksStoreManager(TasksManager):
         if self.overdue_query != "range" or raw_query is None:
             return None
         q, midnight, page = self._range_query(limit)
-        log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
+        log.info(LOG_OVERDUE_PAGE, midnight, page)
         raw = await raw_query(self.store, q)
         made = tasks_from_query_wire(raw, by_created=True)
         if made is not None:
@@ -353,13 +354,42 @@ class TasksStoreManager(TasksManager):
         tasks.sort(key=_created_key)
         return ("[" + ",".join(t.to_json() for t in tasks) + "]").encode(), bool(doc.get("token"))
 
-    def _range_query(self, limit: int | None) -> tuple[dict, str, int]:
+    def native_overdue_route(self) -> dict | None:
+        """``overdue_page_json`` as a native route of the app host (apphost.hpp ``api_overdue``):
+        this manager's range query and log line as templates over the two values that change --
+        the local midnight and the page size -- the same codec, the more-results flag; None
+        outside range mode or when this client cannot take one."""
+        ep_of = getattr(self.client, "native_endpoint", None)
+        ep = ep_of() if ep_of is not None else None
+        if self.overdue_query != "range" or ep is None or getattr(self.client, "query_state_raw", None) is None:
+            return None
+        mid, page = "zqMIDNIGHTqz", 987654321
+        q, _, _ = self._range_query(page, midnight=mid)
+        text = json.dumps(q).replace("%", "%%")  # query_state_raw's encoding of the dict
+        jm, jp = json.dumps(mid), str(page)
+        if text.count(jm) != 1 or text.count(jp) != 1:
+            return None
+        args = "midnight,page" if text.find(jm) < text.find(jp) else "page,midnight"
+        text = text.replace(jm, '"%s"').replace(jp, "%s")
+        # the log line fills midnight then page (%d of an int prints as %s of it)
+        log_tpl = LOG_OVERDUE_PAGE
+        if log_tpl.count("%s") != 1 or log_tpl.count("%d") != 1 or log_tpl.find("%s") > log_tpl.find("%d"):
+            return None
+        return {"kind": "api_overdue", "method": "GET", "path": "/api/overduetasks", "route": "/api/overduetasks",
+                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                        "query_target": f"{ep['prefix']}/v1.0-alpha1/state/{self.store}/query",
+                        "query": text, "query_args": args, "page_default": self.overdue_page,
+                        "log_category": log.name, "log_overdue": log_tpl.replace("%d", "%s"),
+                        "log_overdue_args": "midnight,page"},
+                "what": {"query": f"query state {self.store}"}}
+
+    def _range_query(self, limit: int | None, midnight: str | None = None) -> tuple[dict, str, int]:
         """The open tasks due before today's midnight, oldest first: ``ORDER BY taskCreatedOn``
         in the store picks the page (reference ``.OrderBy(o => o.TaskCreatedOn)``,
         TasksStoreManager.cs:136) -- the stored round-trip strings sort as DateTimes; the page is
         re-ordered by the DateTime value on the way out all the same (documents written by other
         clients may carry System.Text.Json's trimmed fraction, see ``tasks_from_query_wire``)."""
-        midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss")
+        midnight = format_fixed(today(), "yyyy-MM-ddTHH:mm:ss") if midnight is None else midnight
         page = limit if limit and limit > 0 else self.overdue_page
         q = {"filter": {"AND": [{"LT": {"taskDueDate": midnight}}, {"EQ": {"isCompleted": False}},
                                 {"EQ": {"isOverDue": False}}]},
@@ -376,7 +406,7 @@ class TasksStoreManager(TasksManager):
         order of the reference's ``OrderBy``.  One page (oldest first) per call: the
         processor marks a page overdue and asks again, and marked tasks drop out of the filter."""
         q, midnight, page = self._range_query(limit)
-        log.info("Getting open tasks due before: '%s' (page of %d)", midnight, page)
+        log.info(LOG_OVERDUE_PAGE, midnight, page)
         resp = await self.client.query_state(self.store, q)
         tasks = [TaskModel.model_validate(r.data) for r in resp.results if r.data is not None]
         tasks.sort(key=_created_key)

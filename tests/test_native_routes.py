@@ -346,7 +346,7 @@ def test_native_routes_follow_the_python_definitions(tmp_path, monkeypatch):
     assert pn == 1 and rn[0][0] == 202 and ln[0] == "Save a new task with name: ''Buy milk'' to state store"
 
 
-def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests):
+def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests, manager_kw=None, route=None):
     """GET ``requests`` [(headers, target)] against the frontend's Tasks/Index ('frontend') or
     the API's api/tasks ('api'); returns (responses, sidecar calls, metric delta, python calls)."""
     monkeypatch.setenv("TT_APP_HOST", "native")
@@ -357,7 +357,7 @@ def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests
     from aca_dotnet_workshop_amd.sdk.client import SidecarClient
     from aca_dotnet_workshop_amd.telemetry import tracing
     tracing.configure("native-routes-test", None, 0.0)
-    route = {"api": "/api/tasks", "frontend": "/Tasks/Index"}[which]
+    route = route or {"api": "/api/tasks", "frontend": "/Tasks/Index"}[which]
 
     async def main():
         loop = asyncio.get_running_loop()
@@ -371,7 +371,7 @@ def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests
         if which == "api":
             from aca_dotnet_workshop_amd.services.backend_api import create_app
             from aca_dotnet_workshop_amd.services.backend_api.managers import TasksStoreManager
-            app = create_app(config=cfg, manager=TasksStoreManager(client))
+            app = create_app(config=cfg, manager=TasksStoreManager(client, **(manager_kw or {})))
             real = client.query_state_raw
 
             async def counted(*a, **kw):
@@ -403,7 +403,8 @@ def _get_scenario(tmp_path, monkeypatch, which, native, sidecar_status, requests
         try:
             for headers, target in requests:
                 r = await c.get(f"unix:{app_sock}:{target}", headers=headers)
-                out.append((r.status, r.headers.get("content-type"), r.headers.get("location"), r.body))
+                out.append((r.status, r.headers.get("content-type"), r.headers.get("location") or
+                            r.headers.get("x-tt-more-results"), r.body))
         finally:
             await c.close()
             stop.set()
@@ -480,3 +481,37 @@ def test_api_list_native_equals_python(tmp_path, monkeypatch, status):
         assert pn == 0 and pp == 2
         assert [t["taskId"][-4:] for t in json.loads(rn[0][3])] == ["e0f1", "950e"]  # newest first
         assert json.loads(cn[1][3]) == {"filter": {"EQ": {"taskCreatedBy": 'a "b"'}}}
+
+
+@pytest.mark.parametrize("status", [{}, {"/v1.0-alpha1/state/": (500, b'{"errorCode":"ERR_STATE_QUERY"}')}],
+                         ids=["ok", "query-fails"])
+def test_api_overdue_native_equals_python(tmp_path, monkeypatch, status):
+    """GET api/overduetasks (range mode) on the I/O thread: the manager's range query -- today's
+    midnight and the page size filled into its own text -- the same page (oldest first) and
+    more-results flag, the same log line; a failed query is the SDK's error."""
+    results = {"results": [{"key": t["taskId"], "data": t, "etag": "1"} for t in _LIST], "token": "2"}
+    ok = {"/v1.0-alpha1/state/": (200, json.dumps(results).encode())}
+    ok.update(status)
+    reqs = [([("traceparent", UNSAMPLED)], "/api/overduetasks?limit=512"),
+            ([("traceparent", UNSAMPLED)], "/api/overduetasks"),
+            ([("traceparent", UNSAMPLED)], "/api/overduetasks?limit=007"),
+            ([("traceparent", UNSAMPLED)], "/api/overduetasks?limit=x")]
+    kw = {"overdue_query": "range", "overdue_page": 100}
+    lines = _Lines()
+    got = {}
+    logger = logging.getLogger("TasksManager")
+    for n in (True, False):
+        logger.addHandler(lines)
+        try:
+            got[n] = _get_scenario(tmp_path, monkeypatch, "api", n, ok, reqs, kw, "/api/overduetasks") + (list(lines.lines),)
+        finally:
+            logger.removeHandler(lines)
+            lines.lines.clear()
+    (rn, cn, mn, pn, ln), (rp, cp, mp, pp, lp) = got[True], got[False]
+    assert rn == rp and [_norm_call(c) for c in cn] == [_norm_call(c) for c in cp] and mn == mp
+    assert ln == lp and ln[0].startswith("Getting open tasks due before: '") and ln[0].endswith("(page of 512)")
+    if not status:
+        assert pn == 0 and pp == 4
+        assert [r[2] for r in rn] == ["true"] * 4  # the store's token: more matches
+        assert [json.loads(c[3])["page"]["limit"] for c in cn] == [512, 100, 7, 100]
+        assert [t["taskId"][-4:] for t in json.loads(rn[0][3])] == ["950e", "e0f1"]  # oldest first
