@@ -439,21 +439,37 @@ class DataPlane {
 
   // Dapr's enableApiLogging: one JSON line per API call on stderr (the replica's log stream),
   // same shape as telemetry/logging.py JsonFormatter.
+  // Appended straight into the batch buffer (no temporaries: three of these per created task on
+  // the API's sidecar).
   void api_log(const std::string& name, int status, const SpanCtx& span) {
     char buf[96];
     std::snprintf(buf, sizeof buf, " status=%d duration_ms=%.3f app_id=", status, (ev::now_s() - span.t0) * 1e3);
     auto sp = name.find(' ');
-    std::string msg = "HTTP API Called method=" + name.substr(0, sp) + " path=" +
-                      (sp == std::string::npos ? "" : name.substr(sp + 1)) + buf + app_id_;
+    std::string& msg = api_log_msg_;
+    msg.assign("HTTP API Called method=");
+    msg.append(name, 0, sp);
+    msg += " path=";
+    if (sp != std::string::npos) msg.append(name, sp + 1, std::string::npos);
+    msg += buf;
+    msg += app_id_;
+    if (api_log_role_.empty()) api_log_role_ = json_str(app_id_ + ".sidecar");
     char ts[32];
     std::snprintf(ts, sizeof ts, "%.6f", wall_now());
-    std::string line = std::string("{\"ts\":") + ts + ",\"level\":\"INFO\",\"role\":" + json_str(app_id_ + ".sidecar") +
-                       ",\"category\":\"sidecar.http-info\",\"message\":" + json_str(msg) + ",\"traceId\":\"" +
-                       std::string(span.tid()) + "\",\"spanId\":\"" + std::string(span.sid()) +
-                       "\",\"plane\":\"native\"}\n";
-    api_log_buf_ += line;
-    if (api_log_buf_.size() >= 32768) flush_api_log();
+    std::string& b = api_log_buf_;
+    b += "{\"ts\":";
+    b += ts;
+    b += ",\"level\":\"INFO\",\"role\":";
+    b += api_log_role_;
+    b += ",\"category\":\"sidecar.http-info\",\"message\":";
+    escape_to(b, msg);
+    b += ",\"traceId\":\"";
+    b += span.tid();
+    b += "\",\"spanId\":\"";
+    b += span.sid();
+    b += "\",\"plane\":\"native\"}\n";
+    if (b.size() >= 32768) flush_api_log();
   }
+  std::string api_log_msg_, api_log_role_;
   // The lines go out in batches: when 32 KB have gathered and on every loop tick (<= ~50 ms),
   // one write(2) for many API calls instead of one per call on the unbuffered stderr.
   void flush_api_log() {
