@@ -1162,7 +1162,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
-        util = {k: round((cpu1.get(k, 0.0) - v) / dt, 2) for k, v in cpu0.items()}
+        busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}  # cores busy per role
+        util = {k: round(v, 2) for k, v in busy.items()}
         sweep_info = None
         if sweeper is not None:
             acc1 = _accel_stats(shards)  # the timed region's share of the accelerator counters
@@ -1247,7 +1248,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         total = a.batch * a.steps * (d.world if d.world > 1 else 1)
         value = total / dt_max if dt_max > 0 else 0.0
         p50, p99 = d.max(report["latency_ms"]["p50"]), d.max(report["latency_ms"]["p99"])
-        cpu_us = cpu_per_task(util, a.batch * a.steps / dt)  # this rank's CPU over this rank's tasks
+        cpu_us = cpu_per_task(busy, a.batch * a.steps / dt)  # this rank's CPU over this rank's tasks
         ru_used = None
         if ru0 and ru1 and "ru_consumed" in ru1:
             ru_used = round((ru1["ru_consumed"] - ru0.get("ru_consumed", 0.0)) / dt, 1)

@@ -844,6 +844,12 @@ class _FakePageKernels:
     def rank_encode(self, *a):  # device rank columns are not read by the emulation
         pass
 
+    def upload(self, segments):  # GpuKernels.upload, on host tensors: the same bytes written in place
+        import ctypes
+        for dst, a in segments:
+            b = np.ascontiguousarray(a)
+            ctypes.memmove(int(dst), b.ctypes.data, b.nbytes)
+
     def _keys(self, rows):
         return self.ix.sort_keys_numpy(rows, self.ix.sort_specs(self.sort)).astype(np.uint64)
 
