@@ -980,16 +980,33 @@ class ColumnarIndex:
         lo = 0 if full else cur["synced"]
         if not full and lo >= self.n:
             return
+        segs = []  # the rank table and the source descriptor: one scatter launch, no copies
         if full:
             dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[w]
-            cur = ranks[col] = {"t": torch.empty(self.cap, dtype=dt, device=kernels.device), "w": w,
-                                "ver": c.rank_version, "table": None, "synced": 0}
+            prev = cur
+            # re-encoded from row 0 into the same buffer when it still fits: its address is in
+            # the column descriptor table, which then needs no new upload
+            keep = prev is not None and prev["w"] == w and prev["t"].numel() == self.cap
+            cur = ranks[col] = {"t": prev["t"] if keep else torch.empty(self.cap, dtype=dt, device=kernels.device),
+                                "w": w, "ver": c.rank_version, "table": None, "synced": 0}
             table = c.ranks().astype(np.int32) if c.values else np.zeros(1, dtype=np.int32)
-            cur["table"] = torch.from_numpy(table).to(kernels.device)
+            # a new dictionary value re-ranks the column (every new due date does): the table's
+            # device buffer is kept across versions and grown by doubling
+            buf = prev.get("table_buf") if prev is not None else None
+            if buf is None or buf.numel() < table.size:
+                buf = torch.empty(max(1024, 1 << (table.size - 1).bit_length()), dtype=torch.int32,
+                                  device=kernels.device)
+            cur["table_buf"], cur["table"] = buf, buf[:table.size]
+            segs.append((buf.data_ptr(), table))
+            if prev is not None and "src" in prev:
+                cur["src"], cur["src_key"] = prev["src"], prev["src_key"]
         key = (st["cols"][col].data_ptr(), st["widths"][col])
         if cur.get("src_key") != key:  # the source column's descriptor: uploaded when it changes
-            cur["src"] = torch.from_numpy(np.array([list(key)], dtype=np.int64)).to(kernels.device)
+            if "src" not in cur:
+                cur["src"] = torch.empty((1, 2), dtype=torch.int64, device=kernels.device)
+            segs.append((cur["src"].data_ptr(), np.array([list(key)], dtype=np.int64)))
             cur["src_key"] = key
+        kernels.upload(segs)
         kernels.rank_encode(cur["src"], cur["table"], lo, self.n, cur["t"], w)
         cur["synced"] = self.n
 
@@ -1157,23 +1174,29 @@ class ColumnarIndex:
             for (r, _), off in zip(tables, offs):
                 host[off:off + r.size] = r
             ent = {"caps": caps, "offs": offs, "seqs": [c.rank_seq for _, c in tables],
-                   "host": host, "dev": torch.from_numpy(host).to(kernels.device), "specs": None, "specs_dev": None}
+                   "host": host, "dev": torch.from_numpy(host).to(kernels.device), "specs": None,
+                   "specs_dev": torch.zeros((len(specs_rows), 8), dtype=torch.int32, device=kernels.device)}
             if len(self._plan_cache) >= 64:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
             self._plan_cache[pkey] = ent
-        else:
+        segs = []  # rank tails and the spec rows: one scatter launch (ops/gpu.py upload)
+        if not rebuild:
             for i, ((r, c), lo) in enumerate(zip(tables, los)):
                 off = int(ent["offs"][i])
                 if r.size > lo:  # the ids whose rank is new or moved (the newest ones)
                     tail = r[lo:].astype(np.int32)
                     ent["host"][off + lo:off + r.size] = tail
-                    kernels.upload([(ent["dev"].data_ptr() + 4 * (off + lo), tail)])
+                    segs.append((ent["dev"].data_ptr() + 4 * (off + lo), tail))
                 ent["seqs"][i] = c.rank_seq
         for row, off in zip(specs_rows, ent["offs"]):
             row[1] = int(off)
         specs = np.array(specs_rows, dtype=np.int32).reshape(-1, 8)
         if ent["specs"] is None or not np.array_equal(specs, ent["specs"]):
-            ent["specs"], ent["specs_dev"] = specs, torch.from_numpy(specs).to(kernels.device)
+            # the spec rows change with every new dictionary value (row[2] is the table's size):
+            # they ride the same launch into a buffer allocated once per plan
+            ent["specs"] = specs
+            segs.append((ent["specs_dev"].data_ptr(), specs))
+        kernels.upload(segs)
         key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
         return ent["specs_dev"], ent["dev"], seq_bits, key_bits, (specs, ent["host"], seq_bits)
 

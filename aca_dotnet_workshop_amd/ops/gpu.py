@@ -225,10 +225,10 @@ class GpuKernels:
             at += (b.size + 15) & ~15
         with self._total_lock:
             stream = self._stream()
-            host, dev, arr = self._mailbox("upload", (at + 3) // 4)
-            # the previous scatter read this buffer: it has finished before the bytes change
-            # (every page / zone call synchronises anyway, so this rarely waits)
+            # the previous scatter read this buffer: it has finished before the bytes change or
+            # the buffer is replaced (every page / zone call synchronises anyway: rarely waits)
             self._sync(stream)
+            host, dev, arr = self._mailbox("upload", (at + 3) // 4)
             buf = arr.view(np.uint8)
             desc = np.empty((len(segs), 3), dtype=np.int64)
             for i, ((d, b), o) in enumerate(zip(segs, offs)):
