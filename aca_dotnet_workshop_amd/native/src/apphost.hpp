@@ -853,7 +853,7 @@ class AppHost {
     std::time_t now = std::time(nullptr);
     std::tm lt{};
     localtime_r(&now, &lt);  // DateTime.Today: the local date (containers run in UTC)
-    char mid[32];
+    char mid[48];
     std::snprintf(mid, sizeof mid, "%04d-%02d-%02dT00:00:00", lt.tm_year + 1900, lt.tm_mon + 1, lt.tm_mday);
     const std::string midnight = mid;
     auto value = [&](int f) -> const std::string& { return f == 0 ? midnight : page; };
@@ -1030,12 +1030,14 @@ class AppHost {
       return true;
     }
     log_event(*r, *j, r->log_save.render(j->task.id, j->task.name, j->task.assigned_to));
-    client_.request(r->sidecar, "POST", r->save_target, j->out_headers, j->task.state_body, r->timeout_s,
+    // the store calls ride the pipelined connections to the sidecar (ev::PipeConn): the creates
+    // of one loop iteration share a send(2) and the sidecar's answers a read
+    client_.request_pipelined(r->sidecar, "POST", r->save_target, j->out_headers, j->task.state_body, r->timeout_s,
                     [this, j](ev::ClientResult&& res) {
                       if (res.err || res.resp.status >= 300) return hand_over(*j, "save", res);
                       const NativeRoute& r = *j->route;
                       log_event(r, *j, r.log_publish.render(j->task.id, j->task.name, j->task.assigned_to));
-                      client_.request(r.sidecar, "POST", r.publish_target, j->out_headers, j->task.task_json,
+                      client_.request_pipelined(r.sidecar, "POST", r.publish_target, j->out_headers, j->task.task_json,
                                       r.timeout_s, [this, j](ev::ClientResult&& res2) {
                                         if (res2.err || res2.resp.status >= 300)
                                           return hand_over(*j, "publish", res2);

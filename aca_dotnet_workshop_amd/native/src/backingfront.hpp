@@ -222,6 +222,16 @@ class BackingFront {
         int f = i == 0 ? fd : ::fcntl(fd, F_DUPFD_CLOEXEC, 0);
         if (f < 0) break;
         auto l = std::make_shared<ev::Listener>(shards_[i]->loop, f, shards_[i]->handler);
+        // whichever loop wakes for a connection, they are dealt to the loops in turn: the local
+        // clients hold few long-lived (pipelined) connections, and an idle loop tends to win
+        // every wake-up, which would leave one loop with all of them
+        l->hand_off = [this, i](int c) {
+          size_t to = next_uds_shard_.fetch_add(1, std::memory_order_relaxed) % shards_.size();
+          if (to == i) return false;
+          Shard* sh = shards_[to].get();
+          sh->post_task([sh, c] { ev::adopt(sh->loop, c, sh->handler); });
+          return true;
+        };
         shards_[i]->loop.add(l, EPOLLIN | EPOLLEXCLUSIVE);
       }
     }
@@ -424,6 +434,7 @@ class BackingFront {
 
   ev::Endpoint fallback_;
   std::vector<std::unique_ptr<Shard>> shards_;
+  std::atomic<size_t> next_uds_shard_{0};  // the Unix listener deals connections in turn
   int port_ = 0;
   bool stopped_ = false;
 

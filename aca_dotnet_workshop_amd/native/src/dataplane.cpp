@@ -950,6 +950,10 @@ class DataPlane {
              "# TYPE sidecar_mtls_handshake_rejected_total counter\n"
              "sidecar_mtls_handshake_rejected_total{app=\"" + app_id_ + "\"} " +
              std::to_string(ev::tls_server_handshake_rejects.load(std::memory_order_relaxed)) + "\n";
+    extra += "# HELP sidecar_pipelined_requests_total requests sent over pipelined local connections "
+             "(store and broker calls to the backing's Unix socket)\n"
+             "# TYPE sidecar_pipelined_requests_total counter\n"
+             "sidecar_pipelined_requests_total{app=\"" + app_id_ + "\"} " + std::to_string(client_.pipelined()) + "\n";
     extra += "# HELP sidecar_partitioned_query_rows_total cross-partition state queries: sort-key entries the "
              "shards sent (phase keys) and documents fetched for the merged pages (phase documents)\n"
              "# TYPE sidecar_partitioned_query_rows_total counter\n"
@@ -1190,11 +1194,15 @@ class DataPlane {
     ev::ClientCallback cb;
     int attempt = 0;
     double waited = 0.0;
+    bool pipeline = true;
   };
 
+  // `pipeline`: over the pipelined connections (ev::Client::request_pipelined) -- every store
+  // call but the queries, which can take milliseconds and would hold up the answers behind them
   void store_request(const Endpoint& ep, std::string method, std::string target, HeaderList h, std::string body,
-                     ev::ClientCallback cb) {
+                     ev::ClientCallback cb, bool pipeline = true) {
     auto c = std::make_shared<StoreCall>();
+    c->pipeline = pipeline;
     c->ep = ep;
     c->method = std::move(method);
     c->target = std::move(target);
@@ -1206,7 +1214,7 @@ class DataPlane {
 
   void store_send(std::shared_ptr<StoreCall> c) {
     StoreCall& k = *c;
-    client_.request(k.ep, k.method, k.target, k.headers, k.body, 60, [this, c](ClientResult&& res) {
+    auto on_done = [this, c](ClientResult&& res) {
       if (!res.err && res.resp.status == 429 && c->attempt < 9) {
         const std::string* ra = res.resp.header("x-ms-retry-after-ms");
         double delay = ra ? std::strtod(ra->c_str(), nullptr) / 1000.0 : 0.1;
@@ -1226,7 +1234,9 @@ class DataPlane {
         }
       }
       c->cb(std::move(res));
-    });
+    };
+    if (k.pipeline) client_.request_pipelined(k.ep, k.method, k.target, k.headers, k.body, 60, std::move(on_done));
+    else client_.request(k.ep, k.method, k.target, k.headers, k.body, 60, std::move(on_done));
   }
 
   void state_save(Message&& m, Reply&& r, const std::string& name, const Store& s, const std::string& path) {
@@ -1615,7 +1625,7 @@ class DataPlane {
           }
         }
         if (--x->left == 0) merge_and_fetch(d, x, s);
-      });
+      }, false);
     }
   }
 
@@ -1744,7 +1754,8 @@ class DataPlane {
                                "state query: " + (res.err ? errno_text(res.err)
                                                           : "HTTP " + std::to_string(res.resp.status) + " " +
                                                                 res.resp.body.substr(0, 300)));
-                    });
+                    },
+                    false);
   }
 
   void state_delete(Message&& m, Reply&& r, const Store& s, const std::string& key, const std::string& path) {
@@ -1836,7 +1847,7 @@ class DataPlane {
     const std::string pkey = meta.count("partitionKey") && !meta["partitionKey"].empty() ? meta["partitionKey"]
                              : event_id.empty()                                          ? uuid4()
                                                                                          : event_id;
-    client_.request(b.ep(pkey), "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
+    client_.request_pipelined(b.ep(pkey), "POST", "/servicebus/" + quote_all(b.ns) + "/topics/" + quote_all(topic) + "/messages", h,
                     body, 60, [d, name, topic](ClientResult&& res) {
                       if (res.err || res.resp.status >= 300) {
                         d->error(500, "ERR_PUBSUB_PUBLISH_MESSAGE",

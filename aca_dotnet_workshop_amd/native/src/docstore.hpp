@@ -608,10 +608,12 @@ class DocStore {
         }
         ticket_out = ticket;  // early: keep the slot
         ++ru_throttled_;
+        ++ru_early_retries_;
         return std::max<int64_t>(1, (int64_t)std::ceil((it->second.first - now) * 1000.0));
       }
     }
     ru = std::min(ru, ru_rate_);  // a request bigger than a second's budget waits for a full bucket
+    ++ru_calls_;
     if (ru_tokens_ >= ru) {
       ru_tokens_ -= ru;
       ru_consumed_ += ru;
@@ -644,7 +646,8 @@ class DocStore {
   std::unordered_map<std::string, double> throughput_stats() {
     std::lock_guard<std::mutex> g(ru_mu_);
     return {{"ru_per_s", ru_rate_}, {"ru_consumed", ru_consumed_}, {"throttled", (double)ru_throttled_},
-            {"reserved_admits", (double)ru_reserved_admits_}, {"open_reservations", (double)ru_tickets_.size()}};
+            {"reserved_admits", (double)ru_reserved_admits_}, {"open_reservations", (double)ru_tickets_.size()},
+            {"calls", (double)ru_calls_}, {"early_retries", (double)ru_early_retries_}};
   }
 
   // ------------------------------------------------------------ column mirror
@@ -734,7 +737,10 @@ class DocStore {
     std::lock_guard<std::mutex> g(mu_);
     if (gen != mirror_.gen) return false;
     int64_t now = now_ms();
-    out = "{\"results\":[";
+    out.clear();
+    // one allocation for the page (~300 KB for the sweep's 1,024 tasks), not a doubling series
+    if (!sort_paths && !docs_.empty()) out.reserve(32 + token.size() + nrows * (live_bytes_ / docs_.size() + 48));
+    out += "{\"results\":[";
     size_t skip = 0;
     bool first = true;
     for (size_t i = 0; i < nrows; ++i) {
@@ -1175,7 +1181,9 @@ class DocStore {
   std::vector<int32_t> reuse_;                   // put_at's per-column carried ids (under mu_)
   std::mutex ru_mu_;
   double ru_rate_ = 0, ru_tokens_ = 0, ru_last_ = 0, ru_consumed_ = 0;
-  uint64_t ru_throttled_ = 0, ru_reserved_admits_ = 0, ru_ticket_seq_ = 0;
+  // calls: charged requests (a ticketed retry is not a new one); early_retries: tickets
+  // presented before their slot (a second 429 for the same call)
+  uint64_t ru_throttled_ = 0, ru_reserved_admits_ = 0, ru_ticket_seq_ = 0, ru_calls_ = 0, ru_early_retries_ = 0;
   std::unordered_map<uint64_t, std::pair<double, double>> ru_tickets_;  // ticket -> (slot, RU reserved)
   static double mono_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();

@@ -68,6 +68,10 @@ struct IoObj : std::enable_shared_from_this<IoObj> {
   }
   virtual void on_event(uint32_t ev) = 0;
   virtual void on_tick(double /*now*/) {}
+  // Output queued during this loop iteration goes out here, once, after every event, deferred
+  // call and timer of the iteration has had its turn (Loop::want_flush).
+  virtual void on_flush() {}
+  bool flush_queued = false;
 };
 
 class Loop {
@@ -100,6 +104,19 @@ class Loop {
     }
   }
   void defer(std::function<void()> f) { deferred_.push_back(std::move(f)); }
+  // Write `o`'s queued output at the end of this iteration: the responses (or pipelined
+  // requests) one connection collects while the iteration's events are handled leave in one
+  // send(2), not one each.
+  void want_flush(IoObj* o) {
+    if (o->dead) return;
+    if (!defer_flushes()) {  // the default: every write goes out at once
+      o->on_flush();
+      return;
+    }
+    if (o->flush_queued) return;
+    o->flush_queued = true;
+    flush_.push_back(o);
+  }
   void call_later(double delay_s, std::function<void()> f) { timers_.emplace(now_s() + delay_s, std::move(f)); }
   void stop() { running_ = false; }
   bool running() const { return running_; }
@@ -110,7 +127,7 @@ class Loop {
     double last_tick = now_s();
     while (running_) {
       int timeout_ms = 50;
-      if (!deferred_.empty()) timeout_ms = 0;
+      if (!deferred_.empty() || !flush_.empty()) timeout_ms = 0;
       else if (!timers_.empty()) {
         double dt = timers_.begin()->first - now_s();
         timeout_ms = dt <= 0 ? 0 : std::min(50, (int)(dt * 1000.0) + 1);
@@ -120,6 +137,10 @@ class Loop {
       for (int i = 0; i < n; ++i) {
         auto* o = static_cast<IoObj*>(evs[i].data.ptr);
         if (!o->dead) o->on_event(evs[i].events);
+        // a long batch of events does not hold back what the first ones produced: the queued
+        // output leaves every kFlushEvery events (batching without adding a whole iteration of
+        // latency to every hop)
+        if ((i + 1) % kFlushEvery == 0 && !flush_.empty()) run_flushes();
       }
       while (!deferred_.empty()) {
         auto d = std::move(deferred_);
@@ -132,6 +153,7 @@ class Loop {
         timers_.erase(timers_.begin());
         f();
       }
+      run_flushes();
       if (t - last_tick >= 0.05) {
         last_tick = t;
         std::vector<std::shared_ptr<IoObj>> snapshot;
@@ -140,9 +162,39 @@ class Loop {
         for (auto& o : snapshot)
           if (!o->dead) o->on_tick(t);
         if (tick) tick(t);
+        run_flushes();  // what the ticks queued (timeouts answered), before the graveyard empties
       }
       graveyard_.clear();
       if (iter_hook_) iter_hook_(t_wake, now_s(), n);
+    }
+  }
+  static constexpr int kFlushEvery = 8;
+  // TT_DEFER_FLUSH=1: hold each connection's output to the end of the event batch (at most
+  // kFlushEvery events).  Fewer sends, but every hop's answer waits for the batch: on the
+  // headline that cost more throughput (69.5 k vs 73.4 k tasks/s, profiles/r5_dataplane.md)
+  // than the sends it saved, so writes go out at once unless asked.
+  static bool defer_flushes() {
+    static const bool on = [] {
+      const char* v = std::getenv("TT_DEFER_FLUSH");
+      return v && v[0] == '1';
+    }();
+    return on;
+  }
+  // Queued flushes, then the deferred calls they caused, until both are empty.  The objects
+  // are alive: a removed one waits in the graveyard until the iteration's end.
+  void run_flushes() {
+    while (!flush_.empty()) {
+      auto f = std::move(flush_);
+      flush_.clear();
+      for (IoObj* o : f) {
+        o->flush_queued = false;
+        if (!o->dead) o->on_flush();
+      }
+      while (!deferred_.empty()) {
+        auto d = std::move(deferred_);
+        deferred_.clear();
+        for (auto& g : d) g();
+      }
     }
   }
   // Diagnostics: called after every iteration with (woke, done, events) -- GapTracer::attach.
@@ -154,6 +206,7 @@ class Loop {
   std::unordered_map<IoObj*, std::shared_ptr<IoObj>> objs_;
   std::vector<std::shared_ptr<IoObj>> graveyard_;
   std::vector<std::function<void()>> deferred_;
+  std::vector<IoObj*> flush_;
   std::multimap<double, std::function<void()>> timers_;
   std::function<void(double, double, int)> iter_hook_;
 };
@@ -687,8 +740,11 @@ class ServerConn : public IoObj {
       pending_.pop_front();
       ++head_seq_;
     }
-    flush();
+    // the answers a read's pipelined requests produce while it is parsed leave together, in
+    // one send at the end of parse(); others go at once (or with the batch, TT_DEFER_FLUSH=1)
+    if (!parsing_) loop_.want_flush(this);
   }
+  void on_flush() override { flush(); }
 
   void parse() {
     parsing_ = true;
@@ -733,6 +789,7 @@ class ServerConn : public IoObj {
       in_.erase(0, in_off_);
       in_off_ = 0;
     }
+    if (out_off_ < out_.size()) loop_.want_flush(this);  // what the parsed requests answered at once
   }
   bool stop_reading_ = false;
 
@@ -804,6 +861,7 @@ class Listener : public IoObj {
       int one = 1;
       if (unix_) widen_local_sndbuf(c);
       else setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      if (hand_off && hand_off(c)) continue;  // another loop serves it
       std::shared_ptr<ServerConn> conn;
       try {
         conn = std::make_shared<ServerConn>(loop_, c, handler_, tls_.get(), record_peer_);
@@ -817,6 +875,8 @@ class Listener : public IoObj {
   }
   // optional: observe accepted connections (the app host closes them when its server stops)
   std::function<void(const std::shared_ptr<ServerConn>&)> on_accept;
+  // optional: give an accepted socket to another loop (true: taken; it calls adopt() there)
+  std::function<bool(int fd)> hand_off;
 
  private:
   bool unix_ = false;
@@ -825,6 +885,18 @@ class Listener : public IoObj {
   std::shared_ptr<TlsContext> tls_;
   bool record_peer_;
 };
+
+// Serve an accepted socket on `loop` (a Listener's hand_off, on the receiving loop's thread).
+inline void adopt(Loop& loop, int fd, Handler& h) {
+  std::shared_ptr<ServerConn> conn;
+  try {
+    conn = std::make_shared<ServerConn>(loop, fd, h);
+  } catch (const std::exception&) {
+    ::close(fd);
+    return;
+  }
+  loop.add(conn, EPOLLIN);
+}
 
 // Bind + listen on `ep`; returns the socket, and the bound port in `port` (tcp) or 0 (unix).
 // Throws on failure.  `reuseport`: several loops (threads) bind the same TCP port and the
@@ -955,6 +1027,61 @@ class ClientConn : public IoObj {
   void finish(Message&& m, bool keep);
 };
 
+// A pipelined connection (HTTP/1.1 pipelining) to a local peer that answers in order -- an
+// evhttp ServerConn: a sidecar's API, the backing's front.  The requests issued during one loop
+// iteration leave in one send(2) at its end (Loop::want_flush), their answers come back in as
+// few reads, and the peer answers a batch with one write (ServerConn::drain): the per-exchange
+// system calls of the busiest hops (app -> sidecar -> store) shrink with the load.  A failure
+// fails every request in flight on it: none is re-sent (the peer may have acted on it).
+class PipeConn : public IoObj {
+ public:
+  PipeConn(Loop& loop, Client& owner, std::string key) : loop_(loop), owner_(owner), key_(std::move(key)), parser_(false) {}
+  size_t inflight() const { return q_.size(); }
+  double idle_since() const { return q_.empty() ? idle_since_ : 0.0; }
+  void send(std::string&& wire, double deadline, ClientCallback&& cb) {
+    if (out_off_ == out_.size()) {
+      out_ = std::move(wire);
+      out_off_ = 0;
+    } else {
+      out_ += wire;
+    }
+    q_.push_back(Pending{std::move(cb), deadline});
+    loop_.want_flush(this);
+  }
+  // the peer closed an idle connection (FIN or RST queued, not yet seen by the loop)
+  bool peer_gone() const {
+    char b;
+    ssize_t n = ::recv(fd, &b, 1, MSG_PEEK | MSG_DONTWAIT);
+    return n == 0 || (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR);
+  }
+  void on_event(uint32_t ev) override;
+  void on_flush() override;
+  void on_tick(double now) override {
+    for (auto& p : q_)
+      if (p.deadline > 0 && now > p.deadline) {
+        fail_all(ETIMEDOUT);  // the answers behind it cannot be told apart any more
+        return;
+      }
+    if (q_.empty() && now - idle_since_ > 30.0) fail_all(0);  // idle pool entry aged out
+  }
+
+ private:
+  struct Pending {
+    ClientCallback cb;
+    double deadline;
+  };
+  Loop& loop_;
+  Client& owner_;
+  std::string key_;
+  MsgParser parser_;
+  std::string in_, out_;
+  size_t in_off_ = 0, out_off_ = 0;
+  std::deque<Pending> q_;
+  double idle_since_ = now_s();
+  bool want_out_ = false;
+  void fail_all(int err);
+};
+
 class Client {
  public:
   explicit Client(Loop& loop) : loop_(loop) {}
@@ -989,6 +1116,60 @@ class Client {
     w.append(body);
     dispatch(ep, std::move(w), method == "HEAD", timeout_s, std::move(cb), retry_stale);
   }
+
+  // `request` over a pipelined connection (PipeConn) when `ep` is a local socket: for peers
+  // that answer in order (evhttp servers) and requests that answer quickly -- a slow one holds
+  // up the answers queued behind it.  No stale-connection retry (a long-idle connection is
+  // checked before reuse instead).  Other endpoints take `request`.
+  void request_pipelined(const Endpoint& ep, std::string_view method, std::string_view target,
+                         const HeaderList& headers, std::string_view body, double timeout_s, ClientCallback cb) {
+    static const bool enabled = [] {  // TT_PIPELINE=0: the ordinary connections (A/B switch)
+      const char* v = std::getenv("TT_PIPELINE");
+      return !(v && v[0] == '0');
+    }();
+    if (!enabled || !ep.unix_socket || ep.tls || method == "HEAD") {
+      request(ep, method, target, headers, body, timeout_s, std::move(cb), false);
+      return;
+    }
+    std::string w;
+    w.reserve(body.size() + 256 + target.size());
+    w.append(method);
+    w += ' ';
+    w.append(target);
+    w += " HTTP/1.1\r\nhost: localhost\r\n";
+    for (auto& h : headers) {
+      if (is_hop_header(h.first)) continue;
+      w += h.first;
+      w += ": ";
+      w += h.second;
+      w += "\r\n";
+    }
+    w += "content-length: ";
+    w += std::to_string(body.size());
+    w += "\r\n\r\n";
+    w.append(body);
+    double deadline = timeout_s > 0 ? now_s() + timeout_s : 0;
+    auto c = pipe_for(ep);
+    if (!c) {  // could not connect now: the ordinary path (it retries a full backlog, reports errors)
+      dispatch(ep, std::move(w), false, timeout_s, std::move(cb), false);
+      return;
+    }
+    c->send(std::move(w), deadline, std::move(cb));
+    ++pipelined_;
+  }
+  // A pipelined connection flushed its batch: the next iteration's requests go to the next one
+  // (the peer's accept spread them over its loops).
+  void pipe_flushed(const std::string& key) {
+    auto it = pipes_.find(key);
+    if (it != pipes_.end()) it->second.cur = (it->second.cur + 1) % kPipeConns;
+  }
+  void pipe_closed(PipeConn* c, const std::string& key) {
+    auto it = pipes_.find(key);
+    if (it == pipes_.end()) return;
+    for (auto& p : it->second.conns)
+      if (p.get() == c) p.reset();
+  }
+  uint64_t pipelined() const { return pipelined_; }
 
   void release(const std::shared_ptr<ClientConn>& c) {
     auto& v = idle_[c->key_];
@@ -1078,6 +1259,46 @@ class Client {
   Loop& loop_;
   std::unordered_map<std::string, std::vector<std::shared_ptr<ClientConn>>> idle_;
   std::shared_ptr<TlsContext> mesh_tls_, insecure_tls_, system_tls_;
+  // pipelined connections per endpoint: a few, one per loop iteration in turn, each holding at
+  // most kPipeDepth requests in flight
+  static constexpr size_t kPipeConns = 4, kPipeDepth = 64;
+  struct PipeGroup {
+    std::shared_ptr<PipeConn> conns[kPipeConns];
+    size_t cur = 0;
+  };
+  std::unordered_map<std::string, PipeGroup> pipes_;
+  uint64_t pipelined_ = 0;
+
+  std::shared_ptr<PipeConn> pipe_for(const Endpoint& ep) {
+    std::string key = ep.key();
+    auto& g = pipes_[key];
+    for (size_t tries = 0; tries < kPipeConns; ++tries) {
+      auto& c = g.conns[g.cur];
+      if (c && (c->dead || (c->idle_since() > 0 && now_s() - c->idle_since() > 1.0 && c->peer_gone()))) {
+        auto gone = c;
+        c.reset();
+        if (!gone->dead) loop_.remove(gone.get());
+      }
+      if (!c) {
+        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+        if (fd < 0) return nullptr;
+        widen_local_sndbuf(fd);
+        sockaddr_un a{};
+        a.sun_family = AF_UNIX;
+        std::strncpy(a.sun_path, ep.path.c_str(), sizeof a.sun_path - 1);
+        if (::connect(fd, (sockaddr*)&a, sizeof a) != 0) {
+          ::close(fd);
+          return nullptr;
+        }
+        c = std::make_shared<PipeConn>(loop_, *this, key);
+        c->fd = fd;
+        loop_.add(c, EPOLLIN);
+      }
+      if (c->inflight() < kPipeDepth) return c;
+      g.cur = (g.cur + 1) % kPipeConns;
+    }
+    return nullptr;
+  }
 
   const TlsContext* tls_for(const Endpoint& ep) {
     if (ep.tls == 1) return mesh_tls_.get();
@@ -1262,6 +1483,103 @@ inline void ClientConn::finish(Message&& m, bool keep) {
   ClientResult r;
   r.resp = std::move(m);
   cb(std::move(r));
+}
+
+inline void PipeConn::on_flush() {
+  while (out_off_ < out_.size()) {
+    ssize_t n = ::send(fd, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+    if (n > 0) {
+      out_off_ += (size_t)n;
+      continue;
+    }
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (n < 0 && errno == EINTR) continue;
+    fail_all(errno == EPIPE ? EPIPE : ECONNRESET);
+    return;
+  }
+  bool need_out = out_off_ < out_.size();
+  if (need_out != want_out_) {
+    want_out_ = need_out;
+    loop_.mod(this, need_out ? (EPOLLIN | EPOLLOUT) : EPOLLIN);
+  }
+  if (!need_out) {
+    out_.clear();
+    out_off_ = 0;
+  }
+  owner_.pipe_flushed(key_);
+}
+
+inline void PipeConn::on_event(uint32_t ev) {
+  auto self = shared_from_this();  // alive through the callbacks
+  if (ev & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
+    char buf[65536];
+    bool eof = false;
+    while (true) {
+      ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+      if (n > 0) {
+        in_.append(buf, (size_t)n);
+        if ((size_t)n < sizeof buf) break;
+        continue;
+      }
+      if (n == 0) {
+        eof = true;
+        break;
+      }
+      if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+      if (errno == EINTR) continue;
+      fail_all(ECONNRESET);
+      return;
+    }
+    while (in_off_ < in_.size()) {
+      if (q_.empty()) {  // an answer nobody asked for: the stream is out of step
+        fail_all(EPROTO);
+        return;
+      }
+      Message m;
+      auto r = parser_.feed(in_, in_off_, m);
+      if (r == MsgParser::NEED_MORE) break;
+      if (r == MsgParser::ERROR) {
+        fail_all(EPROTO);
+        return;
+      }
+      bool keep = m.keep_alive();
+      Pending p = std::move(q_.front());
+      q_.pop_front();
+      if (q_.empty()) idle_since_ = now_s();
+      ClientResult res;
+      res.resp = std::move(m);
+      if (!keep) {  // the peer closes after this answer: the requests behind it were not read
+        auto cb = std::move(p.cb);
+        fail_all(ECONNRESET);
+        cb(std::move(res));
+        return;
+      }
+      p.cb(std::move(res));  // may queue more requests here (answered in later reads)
+      if (dead) return;
+    }
+    if (in_off_ > 0 && (in_off_ == in_.size() || in_off_ > 65536)) {
+      in_.erase(0, in_off_);
+      in_off_ = 0;
+    }
+    if (eof) {
+      fail_all(q_.empty() ? 0 : EIO);
+      return;
+    }
+  }
+  if (!dead && (ev & EPOLLOUT)) on_flush();
+}
+
+inline void PipeConn::fail_all(int err) {
+  auto self = shared_from_this();
+  owner_.pipe_closed(this, key_);
+  loop_.remove(this);
+  auto q = std::move(q_);
+  q_.clear();
+  for (auto& p : q) {
+    ClientResult r;
+    r.err = err ? err : ECONNRESET;
+    p.cb(std::move(r));
+  }
 }
 
 }  // namespace tt::ev

@@ -53,6 +53,10 @@ class TlsContext {
     SSL_CTX_set_mode(ctx_, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
     SSL_CTX_set_options(ctx_, SSL_OP_NO_TICKET);
     SSL_CTX_set_num_tickets(ctx_, 0);
+    // one read(2) per readiness instead of two per record (5-byte header, then the body):
+    // OpenSSL buffers what arrived, and `pending()` reports that buffer (SSL_has_pending), so
+    // the readers keep going until it is empty -- epoll would not wake them for it
+    SSL_CTX_set_read_ahead(ctx_, 1);
     if (!cfg.cert.empty()) {
       if (SSL_CTX_use_certificate_chain_file(ctx_, cfg.cert.c_str()) != 1 ||
           SSL_CTX_use_PrivateKey_file(ctx_, cfg.key.c_str(), SSL_FILETYPE_PEM) != 1)
@@ -128,7 +132,8 @@ class TlsIo {
     }
     return fail(r);
   }
-  bool pending() const { return SSL_pending(ssl_) > 0; }
+  // decrypted bytes not yet returned, or raw bytes read ahead and not yet processed
+  bool pending() const { return SSL_has_pending(ssl_) == 1; }
   // Names (SAN DNS / URI entries) in the verified peer certificate; empty without one.
   std::string peer_names() const {
     std::string out;

@@ -923,6 +923,9 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 "replicas": {"frontend": 1, "api": 1, "processor": "1..5 (KEDA, 10 messages per replica)"},
                 "vcpu_per_replica": 0.25, "users": 500, "concurrency": 16,
                 "store_429s_per_task": round(int(st1.get("throttled", 0) - st0.get("throttled", 0)) / tasks, 2) if tasks else None,
+                # the 429s per charged store call, and how the throttled ones came through: a
+                # ticket at its slot (admitted) or early (a second 429 for the same call)
+                **_throttle_detail(st0, st1),
                 "tasks_per_s_over_budget_rate": (round(tasks / el / (float(st1.get("ru_per_s", 0.0)) / (ru / tasks)), 3)
                                                  if tasks and ru and el and st1.get("ru_per_s") else None),
                 "note": "a throttled store call gets a reserved slot (429 + x-ms-retry-after-ms + ticket) and the "
@@ -934,6 +937,16 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
     finally:
         stop.set()
         env.stop()
+
+
+def _throttle_detail(st0: dict, st1: dict) -> dict:
+    d = {k: int(st1.get(k, 0) - st0.get(k, 0)) for k in ("throttled", "calls", "reserved_admits", "early_retries")}
+    if not d["calls"]:
+        return {}
+    first = d["throttled"] - d["early_retries"]  # calls that met a spent budget
+    return {"store_calls": d["calls"], "store_calls_throttled_share": round(first / d["calls"], 3),
+            "store_429s_per_call": round(d["throttled"] / d["calls"], 3),
+            "throttled_calls_admitted_at_slot": d["reserved_admits"], "early_ticket_retries": d["early_retries"]}
 
 
 def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cooldown_s: float = 15.0,

@@ -512,6 +512,73 @@ def test_throttled_writers_get_slots_not_failures(plane, tmp_path):
     run(main())
 
 
+def test_store_calls_pipelined_over_the_backing_socket(tmp_path, monkeypatch):
+    """With the backing on a Unix socket the native plane sends store and broker calls over
+    pipelined connections (ev::PipeConn): the calls of one loop iteration leave in one write and
+    their answers come back in order.  Concurrent saves, reads and publishes all land, each answer
+    reaches its own caller, and a query (never pipelined) still works alongside."""
+    async def main():
+        loop = asyncio.get_running_loop()
+        backing = BackingServices()
+        bsrv = HttpServer(backing.build_app(), loop)
+        burl = f"http://127.0.0.1:{await bsrv.listen_tcp('127.0.0.1', 0)}"
+        uds = str(tmp_path / "backing.sock")
+        await bsrv.listen_unix(uds)
+        monkeypatch.setenv("TT_BACKING_URL", burl)
+        monkeypatch.setenv("TT_BACKING_UDS", uds)
+        seen = []
+        app = _app("app-a", seen)
+        srv = HttpServer(app, loop)
+        await app.startup()
+        port = await srv.listen_tcp("127.0.0.1", 0)
+        sc = Sidecar("app-a", app_port=port, http_port=0, components=[STORE, BUS, MEM],
+                     resolver=NameResolver(str(tmp_path / "registry")), backing_url=burl,
+                     internal_uds=str(tmp_path / "a.i.sock"), data_plane="native")
+        await sc.start()
+        http = HttpClient()
+        try:
+            await asyncio.wait_for(sc.app_ready.wait(), 10)
+            assert sc.active_data_plane == "native"
+            b = f"http://127.0.0.1:{sc.bound_http_port}"
+
+            async def one(i):
+                r = await http.post(f"{b}/v1.0/state/statestore", json_body=[{"key": f"p{i}", "value": {"i": i}}])
+                assert r.status == 204, r.body
+                r = await http.get(f"{b}/v1.0/state/statestore/p{i}")
+                assert r.status == 200 and r.json() == {"i": i}, (i, r.body)
+                r = await http.post(f"{b}/v1.0/publish/bus/events", json_body={"n": i})
+                assert r.status == 204, r.body
+            await asyncio.gather(*(one(i) for i in range(200)))
+            r = await http.post(f"{b}/v1.0-alpha1/state/statestore/query",
+                                json_body={"filter": {"EQ": {"i": 7}}})
+            assert r.status == 200 and [x["key"] for x in r.json()["results"]] == ["p7"], r.body
+            m = (await http.get(f"{b}/metrics")).body.decode()
+            got = re.search(r'sidecar_pipelined_requests_total\{app="app-a"\} (\d+)', m)
+            assert got and int(got.group(1)) >= 600, m[-800:]  # 200 saves + 200 reads + 200 publishes
+            await _until(lambda: len([x for x in seen if x[0] == "event"]) == 200, 10)
+            assert sorted(x[2]["n"] for x in seen if x[0] == "event") == list(range(200))
+            # the backing goes away: calls fail (500), none hangs; a backing back on the same
+            # socket is reached over new connections
+            await bsrv.close(0.5)
+            r = await asyncio.wait_for(http.post(f"{b}/v1.0/state/statestore", json_body=[{"key": "x", "value": 1}]), 10)
+            assert r.status == 500, r.body
+            bsrv2 = HttpServer(backing.build_app(), loop)
+            await bsrv2.listen_unix(uds)
+            try:
+                r = await asyncio.wait_for(http.post(f"{b}/v1.0/state/statestore", json_body=[{"key": "x", "value": 1}]), 10)
+                assert r.status == 204, r.body
+                r = await http.get(f"{b}/v1.0/state/statestore/p3")
+                assert r.status == 200 and r.json() == {"i": 3}
+            finally:
+                await bsrv2.close(1.0)
+        finally:
+            await sc.stop(1.0)
+            await srv.close(1.0)
+            await bsrv.close(1.0)
+            await http.close()
+    run(main())
+
+
 @pytest.mark.parametrize("plane", PLANES)
 def test_sidecar_mutual_tls(plane, tmp_path):
     """Sidecar-to-sidecar calls over mutual TLS with per-app-id workload certificates from the
