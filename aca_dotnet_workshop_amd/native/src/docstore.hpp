@@ -177,7 +177,8 @@ struct ColumnMirror {
   bool disabled = false;  // TTL writes: expiry is evaluated by the native engine only
   uint64_t gen = 1;
   std::vector<MirrorColumn> cols;
-  std::vector<const std::string*> keys;  // per row: the owning map node's key (valid while live)
+  // per row: the owning map node -- key and document, no lookup by key (valid while live)
+  std::vector<std::pair<const std::string, Doc>*> nodes;
   std::vector<int64_t> seqs;
   std::vector<uint8_t> live;
   std::vector<uint32_t> kills;  // rows killed since this generation began
@@ -677,12 +678,12 @@ class DocStore {
       for (auto& p : add) { mirror_.cols.emplace_back(); mirror_.cols.back().path = p; }
       auto enc = [&](size_t c) {
         MirrorColumn& col = mirror_.cols[c];
-        col.ids.assign(mirror_.keys.size(), -1);
+        col.ids.assign(mirror_.nodes.size(), -1);
         std::string k;
-        for (size_t r = 0; r < mirror_.keys.size(); ++r) {
+        for (size_t r = 0; r < mirror_.nodes.size(); ++r) {
           if (!mirror_.live[r]) continue;
-          auto it = docs_.find(*mirror_.keys[r]);
-          col.ids[r] = mirror_encode(col, it->first, it->second.parsed, k);
+          auto& kv = *mirror_.nodes[r];
+          col.ids[r] = mirror_encode(col, kv.first, kv.second.parsed, k);
         }
       };
       parallel_for_columns(first, mirror_.cols.size(), enc);
@@ -701,7 +702,7 @@ class DocStore {
     d.on = mirror_.on;
     d.disabled = mirror_.disabled;
     if (!mirror_.on) return d;
-    size_t n = mirror_.keys.size();
+    size_t n = mirror_.nodes.size();
     d.full = gen != mirror_.gen || dict_sizes.size() != mirror_.cols.size() || from > n ||
              kill_from > mirror_.kills.size();
     if (d.full) from = 0, kill_from = mirror_.kills.size();
@@ -745,10 +746,10 @@ class DocStore {
     bool first = true;
     for (size_t i = 0; i < nrows; ++i) {
       uint32_t r = (uint32_t)rows[i];
-      if (r >= mirror_.keys.size() || !mirror_.live[r]) { ++skip; continue; }
-      const std::string& key = *mirror_.keys[r];
-      auto it = docs_.find(key);
-      if (it == docs_.end() || it->second.mrow != r || expired(it->second, now)) { ++skip; continue; }
+      if (r >= mirror_.nodes.size() || !mirror_.live[r]) { ++skip; continue; }
+      auto* it = mirror_.nodes[r];  // a live row's node: no hash lookup of the key
+      const std::string& key = it->first;
+      if (it->second.mrow != r || expired(it->second, now)) { ++skip; continue; }
       if (!first) out += ',';
       first = false;
       if (sort_paths) {
@@ -773,7 +774,7 @@ class DocStore {
   std::unordered_map<std::string, uint64_t> mirror_stats() {
     std::lock_guard<std::mutex> g(mu_);
     return {{"on", mirror_.on}, {"disabled", mirror_.disabled}, {"gen", mirror_.gen},
-            {"rows", mirror_.keys.size()}, {"live_rows", mirror_.live_rows}, {"columns", mirror_.cols.size()},
+            {"rows", mirror_.nodes.size()}, {"live_rows", mirror_.live_rows}, {"columns", mirror_.cols.size()},
             {"compactions", mirror_.compactions}};
   }
 
@@ -941,7 +942,7 @@ class DocStore {
   // ----------------------------------------------------------- column mirror (locked)
   template <class F>
   void parallel_for_columns(size_t lo, size_t hi, F&& f) {
-    if (hi - lo <= 1 || mirror_.keys.size() < 100000) {
+    if (hi - lo <= 1 || mirror_.nodes.size() < 100000) {
       for (size_t c = lo; c < hi; ++c) f(c);
       return;
     }
@@ -986,8 +987,8 @@ class DocStore {
   // `reuse` (optional, one per column): a dictionary id carried over from the replaced row, or
   // kEncode to look the value up.
   void mirror_append(std::pair<const std::string, Doc>& kv, const int32_t* reuse = nullptr) {
-    uint32_t r = (uint32_t)mirror_.keys.size();
-    mirror_.keys.push_back(&kv.first);
+    uint32_t r = (uint32_t)mirror_.nodes.size();
+    mirror_.nodes.push_back(&kv);
     mirror_.seqs.push_back((int64_t)kv.second.seq);
     mirror_.live.push_back(1);
     std::string k;
@@ -997,7 +998,7 @@ class DocStore {
     }
     kv.second.mrow = r;
     ++mirror_.live_rows;
-    if (mirror_.keys.size() > 65536 && mirror_.keys.size() > 2 * mirror_.live_rows) mirror_compact();
+    if (mirror_.nodes.size() > 65536 && mirror_.nodes.size() > 2 * mirror_.live_rows) mirror_compact();
   }
 
   void mirror_kill(Doc& d) {
@@ -1024,13 +1025,13 @@ class DocStore {
     rows.reserve(docs_.size());
     for (auto& kv : docs_) rows.emplace_back(kv.second.seq, &kv);
     std::sort(rows.begin(), rows.end(), [](auto& a, auto& b) { return a.first < b.first; });
-    mirror_.keys.clear();
+    mirror_.nodes.clear();
     mirror_.seqs.clear();
     mirror_.kills.clear();
-    mirror_.keys.reserve(rows.size());
+    mirror_.nodes.reserve(rows.size());
     for (auto& r : rows) {
-      r.second->second.mrow = (uint32_t)mirror_.keys.size();
-      mirror_.keys.push_back(&r.second->first);
+      r.second->second.mrow = (uint32_t)mirror_.nodes.size();
+      mirror_.nodes.push_back(r.second);
       mirror_.seqs.push_back((int64_t)r.first);
     }
     mirror_.live.assign(rows.size(), 1);
@@ -1048,18 +1049,18 @@ class DocStore {
 
   // Drop dead rows (renumbering the survivors in row order); dictionaries are kept.
   void mirror_compact() {
-    size_t w = 0, n = mirror_.keys.size();
+    size_t w = 0, n = mirror_.nodes.size();
     for (size_t r = 0; r < n; ++r) {
       if (!mirror_.live[r]) continue;
       if (w != r) {
-        mirror_.keys[w] = mirror_.keys[r];
+        mirror_.nodes[w] = mirror_.nodes[r];
         mirror_.seqs[w] = mirror_.seqs[r];
         for (auto& col : mirror_.cols) col.ids[w] = col.ids[r];
-        docs_.find(*mirror_.keys[w])->second.mrow = (uint32_t)w;
+        mirror_.nodes[w]->second.mrow = (uint32_t)w;
       }
       ++w;
     }
-    mirror_.keys.resize(w);
+    mirror_.nodes.resize(w);
     mirror_.seqs.resize(w);
     for (auto& col : mirror_.cols) col.ids.resize(w);
     mirror_.live.assign(w, 1);
