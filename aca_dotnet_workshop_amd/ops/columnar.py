@@ -1175,7 +1175,7 @@ class ColumnarIndex:
                 host[off:off + r.size] = r
             ent = {"caps": caps, "offs": offs, "seqs": [c.rank_seq for _, c in tables],
                    "host": host, "dev": torch.from_numpy(host).to(kernels.device), "specs": None,
-                   "specs_dev": torch.zeros((len(specs_rows), 8), dtype=torch.int32, device=kernels.device)}
+                   "specs_dev": torch.empty((len(specs_rows), 8), dtype=torch.int32, device=kernels.device)}
             if len(self._plan_cache) >= 64:
                 self._plan_cache.pop(next(iter(self._plan_cache)))
             self._plan_cache[pkey] = ent
