@@ -14,6 +14,7 @@
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
 #include "formcodec.hpp"
+#include "strrank.hpp"
 
 namespace py = pybind11;
 using namespace tt;
@@ -574,6 +575,35 @@ PYBIND11_MODULE(_ttnative, m) {
       .def_readonly("key", &TxOp::key)
       .def_readonly("value", &TxOp::value)
       .def_readonly("ttl_ms", &TxOp::ttl_ms);
+
+  // ops/columnar.py Column: sort ranks of a string dictionary, kept incrementally (strrank.hpp)
+  py::class_<StrRanker>(m, "StrRanker")
+      .def(py::init<>())
+      .def_property_readonly("size", &StrRanker::size)
+      .def(
+          "extend",
+          [](StrRanker& r, py::list values, py::array_t<int64_t, py::array::c_style> ranks) -> int64_t {
+            const size_t n0 = r.size(), n = (size_t)PyList_GET_SIZE(values.ptr());
+            if (n < n0) return -1;  // the dictionary shrank: the caller starts a new ranker
+            if ((size_t)ranks.size() < n || !ranks.writeable()) throw std::invalid_argument("rank buffer too small");
+            // every new value first (a non-str, or one UTF-8 cannot carry, leaves nothing changed)
+            std::vector<std::string_view> vs;
+            vs.reserve(n - n0);
+            for (size_t i = n0; i < n; ++i) {
+              PyObject* o = PyList_GET_ITEM(values.ptr(), (Py_ssize_t)i);
+              if (!PyUnicode_Check(o)) return -1;
+              Py_ssize_t len = 0;
+              const char* p = PyUnicode_AsUTF8AndSize(o, &len);  // cached in the str: alive with the list
+              if (!p) {
+                PyErr_Clear();
+                return -1;
+              }
+              vs.emplace_back(p, (size_t)len);
+            }
+            int64_t* out = ranks.mutable_data();
+            return (int64_t)r.extend(vs.size(), [&](size_t i) { return vs[i]; }, out);
+          },
+          py::arg("values"), py::arg("ranks"));
 
   py::class_<DocStore>(m, "DocStore")
       .def(py::init<const std::string&, int, size_t>(), py::arg("path") = "", py::arg("fsync_mode") = 0,

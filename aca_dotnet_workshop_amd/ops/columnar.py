@@ -182,6 +182,26 @@ class KeyTable:
 _RANK_EPOCHS = itertools.count(1)
 
 
+_NATIVE = []  # [module or None], resolved on first use
+
+
+def _native_module():
+    """The native extension for ``StrRanker`` (None where it cannot load, or with
+    ``TT_NATIVE_RANKS=0``: the numpy ranks then answer)."""
+    if not _NATIVE:
+        mod = None
+        if os.environ.get("TT_NATIVE_RANKS", "1") != "0":
+            try:
+                from ..native import load
+                mod = load()
+                if not hasattr(mod, "StrRanker"):
+                    mod = None
+            except Exception:  # no compiler / stale build: the numpy path is complete on its own
+                mod = None
+        _NATIVE.append(mod)
+    return _NATIVE[0]
+
+
 class Column:
     def __init__(self, path: str) -> None:
         self.path = path
@@ -201,6 +221,8 @@ class Column:
         # the ranks are then positions in the sorted dictionary (_string_ranks)
         self.str_only = True
         self._str_sorted = None
+        self._nr = None       # native/src/strrank.hpp StrRanker (the string-only ranks)
+        self._nr_buf = None   # its rank buffer (int64, capacity-doubled, owned here)
 
     @property
     def ids(self) -> dict[str, int]:
@@ -312,9 +334,40 @@ class Column:
     def _all_strings(self) -> bool:
         if not self.str_only:
             self._str_sorted = None
+            self._nr = self._nr_buf = None
         return self.str_only
 
     def _string_ranks(self) -> np.ndarray:
+        r = self._string_ranks_native()
+        return r if r is not None else self._string_ranks_numpy()
+
+    def _string_ranks_native(self) -> np.ndarray | None:
+        """``_string_ranks`` in C++ (``native/src/strrank.hpp``): the new values are read from
+        the dictionary list as UTF-8 (no numpy string array), sorted alone and merged into the
+        tail of the order; the ranks land in a buffer owned here, so earlier views stay valid.
+        None without the native module (the numpy path then answers)."""
+        mod = _native_module()
+        if mod is None:
+            return None
+        n = len(self.values)
+        nr = self._nr
+        if nr is None or nr.size > n:  # first use, or the dictionary was replaced
+            nr, self._nr_buf = mod.StrRanker(), None
+        buf = self._nr_buf
+        if buf is None or buf.size < n:
+            grown = np.empty(max(1024, 2 * n), dtype=np.int64)
+            if buf is not None:
+                grown[:nr.size] = buf[:nr.size]
+            buf = grown
+        lo = nr.extend(self.values, buf)
+        if lo < 0:  # a value UTF-8 cannot carry (a lone surrogate): the numpy path orders it
+            self._nr = self._nr_buf = None
+            return None
+        self._nr, self._nr_buf = nr, buf
+        self._rank_lo = int(lo)
+        return buf[:n]
+
+    def _string_ranks_numpy(self) -> np.ndarray:
         """A dictionary of strings only (timestamps, e-mails, names): distinct values never tie
         and Python's string order is ``compare``'s, so the ranks are positions in the sorted
         dictionary.  Kept incrementally: values appended since the last call are sorted alone
@@ -706,9 +759,19 @@ class ColumnarIndex:
         return (self._dict_gen,) + tuple((len(c.values), c.rank_version) for c in self.columns)
 
     def compile_cached(self, flt: Any) -> Program:
-        """``compile`` memoised per filter and dictionary state (queries repeat: the cron sweep,
-        the same creator's list page); bounded, oldest entries dropped."""
-        key = (json.dumps(flt, sort_keys=True, default=str), self._dict_state())
+        """``compile`` memoised per filter and the dictionary state of the columns it reads
+        (queries repeat: the cron sweep, the same creator's list page) -- not of every column:
+        the sort key's dictionary (``taskCreatedOn``, one value per write) grows between any two
+        sweeps and would otherwise recompile, and re-upload, the same program every time.
+        Bounded, oldest entries dropped."""
+        fj = json.dumps(flt, sort_keys=True, default=str)
+        cols = [self.col_of.get(p) for p in filter_paths(flt)]
+        if any(c is None for c in cols):  # compile adds the column: key on everything this once
+            state = self._dict_state()
+        else:
+            state = (self._dict_gen,) + tuple((c, len(self.columns[c].values), self.columns[c].rank_version)
+                                              for c in sorted(set(cols)))
+        key = (fj, state)
         prog = self._prog_cache.get(key)
         if prog is None:
             prog = self.compile(flt)

@@ -8,7 +8,7 @@ import random
 
 import numpy as np
 import pytest
-from hypothesis import example, given, settings
+from hypothesis import HealthCheck, example, given, settings
 from hypothesis import strategies as st
 
 from aca_dotnet_workshop_amd import native
@@ -784,9 +784,20 @@ def test_gpu_native_mirror_matches_native():
                                                "c": r < 0.4, "o": r > 0.8}))
 
 
-@settings(max_examples=200, deadline=None)
+@pytest.fixture(params=["native", "numpy"])
+def rank_path(request, monkeypatch):
+    """The string ranks both ways: native/src/strrank.hpp, and the numpy merge it replaced."""
+    from aca_dotnet_workshop_amd.ops import columnar
+    if request.param == "numpy":
+        monkeypatch.setattr(columnar, "_NATIVE", [None])
+    else:
+        assert columnar._native_module() is not None
+    return request.param
+
+
+@settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
 @given(st.lists(st.lists(st.text(max_size=6), max_size=30), min_size=1, max_size=6))
-def test_string_ranks_incremental_match_the_comparison_sort(batches):
+def test_string_ranks_incremental_match_the_comparison_sort(rank_path, batches):
     """The incremental string-dictionary ranks (merge of each batch of new values) equal the
     general comparison sort after every batch; a non-string value switches to the general path."""
     from aca_dotnet_workshop_amd.ops.columnar import Column
@@ -801,7 +812,7 @@ def test_string_ranks_incremental_match_the_comparison_sort(batches):
     assert c.ranks().tolist() == c._general_ranks().tolist()
 
 
-def test_bulk_string_encode_and_append_ranks():
+def test_bulk_string_encode_and_append_ranks(rank_path):
     """``encode_json_many`` (the mirror sync's bulk path) gives the ids per-value ``encode``
     would, the in-place append path (every new value sorts last: new timestamps) keeps the ranks
     equal to the comparison sort, a value already present falls back per value, and non-string
