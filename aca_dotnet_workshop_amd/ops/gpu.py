@@ -98,9 +98,19 @@ class GpuKernels:
         self._bufs: dict[str, Any] = {}
         self._est: dict[int, int] = {}  # last selection count per device program: output sizing
         self.page_cap = int(self.lib.tt_page_cap())
+        # every launch goes to the device's current stream at construction (the default stream:
+        # nothing here switches streams); resolved once -- torch.cuda.current_stream costs
+        # microseconds of device-index lookups per call, several calls per query
+        self._tstream = torch.cuda.current_stream(self.device)
+        self._stream_handle = ctypes.c_void_p(self._tstream.cuda_stream)
+        # staging slots of ``upload`` and the event recorded after the scatter that last read each
+        self._upload_ev: list[Any] = [None] * self.UPLOAD_SLOTS
+        self._upload_slot = 0
+
+    UPLOAD_SLOTS = 4
 
     def _stream(self) -> ctypes.c_void_p:
-        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+        return self._stream_handle
 
     def select(self, table, live16, capacity: int, nrows: int, prog, bitmaps, return_mask: bool = False):
         """Row indices (int32, ascending) of live rows satisfying ``prog``.
@@ -149,7 +159,7 @@ class GpuKernels:
                                                  out.data_ptr(), cap, scratch.data_ptr(), pinned.data_ptr(), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scan_compact launch failed ({rc})")
-            self._total_event.record(torch.cuda.current_stream(self.device))
+            self._total_event.record(self._tstream)
             self._total_event.synchronize()
             total = int(pinned[0])
             if total > cap:
@@ -225,10 +235,15 @@ class GpuKernels:
             at += (b.size + 15) & ~15
         with self._total_lock:
             stream = self._stream()
-            # the previous scatter read this buffer: it has finished before the bytes change or
-            # the buffer is replaced (every page / zone call synchronises anyway: rarely waits)
-            self._sync(stream)
-            host, dev, arr = self._mailbox("upload", (at + 3) // 4)
+            # a ring of staging slots: the scatter that last read this slot has finished before
+            # its bytes change or it is replaced -- its event, not a whole-stream synchronise
+            # (which would wait for every kernel queued since, once per upload)
+            slot = self._upload_slot
+            self._upload_slot = (slot + 1) % self.UPLOAD_SLOTS
+            ev = self._upload_ev[slot]
+            if ev is not None and not ev.query():
+                ev.synchronize()
+            host, dev, arr = self._mailbox(f"upload{slot}", (at + 3) // 4)
             buf = arr.view(np.uint8)
             desc = np.empty((len(segs), 3), dtype=np.int64)
             for i, ((d, b), o) in enumerate(zip(segs, offs)):
@@ -239,6 +254,9 @@ class GpuKernels:
                                                      max(b.size for _, b in segs), stream)
             if rc != 0:
                 raise RuntimeError(f"tt_scatter_segments launch failed ({rc})")
+            if ev is None:
+                ev = self._upload_ev[slot] = self.torch.cuda.Event()
+            ev.record(self._tstream)
             self.uploads += 1
             self.upload_segments += len(segs)
 
