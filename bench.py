@@ -1171,7 +1171,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
-        hot = hot_threads(th0, env.stack.thread_cpu(_ingress_pid(env)), dt)
+        th1 = env.stack.thread_cpu(_ingress_pid(env))
+        hot = hot_threads(th0, th1, dt)
+        threads_all = hot_threads(th0, th1, dt, top=80)  # the stderr diagnostics line only
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
@@ -1269,7 +1271,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
                               "cpu_us_per_task": cpu_us,
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
-                              "overdue_sweeps": sweep_info, "resource_limits": lim}), file=sys.stderr, flush=True)
+                              "overdue_sweeps": sweep_info, "resource_limits": lim,
+                              "threads": threads_all}), file=sys.stderr, flush=True)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
