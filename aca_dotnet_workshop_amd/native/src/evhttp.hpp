@@ -1573,13 +1573,18 @@ inline void PipeConn::fail_all(int err) {
   auto self = shared_from_this();
   owner_.pipe_closed(this, key_);
   loop_.remove(this);
-  auto q = std::move(q_);
+  if (q_.empty()) return;
+  // answered from the loop, never from inside the caller's request_pipelined (a send can fail
+  // at once): callers may still be setting up around the call
+  auto q = std::make_shared<std::deque<Pending>>(std::move(q_));
   q_.clear();
-  for (auto& p : q) {
-    ClientResult r;
-    r.err = err ? err : ECONNRESET;
-    p.cb(std::move(r));
-  }
+  loop_.defer([q, err] {
+    for (auto& p : *q) {
+      ClientResult r;
+      r.err = err ? err : ECONNRESET;
+      p.cb(std::move(r));
+    }
+  });
 }
 
 }  // namespace tt::ev

@@ -512,7 +512,7 @@ def test_throttled_writers_get_slots_not_failures(plane, tmp_path):
     run(main())
 
 
-def test_store_calls_pipelined_over_the_backing_socket(tmp_path, monkeypatch):
+def test_native_store_calls_pipelined_over_the_backing_socket(tmp_path, monkeypatch):
     """With the backing on a Unix socket the native plane sends store and broker calls over
     pipelined connections (ev::PipeConn): the calls of one loop iteration leave in one write and
     their answers come back in order.  Concurrent saves, reads and publishes all land, each answer

@@ -93,3 +93,25 @@ def test_app_host_under_sanitizers(tmp_path, flags, env):
     out = run.stdout + run.stderr
     assert run.returncode == 0 and "ALL OK" in run.stdout, out[-5000:]
     assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out and "runtime error" not in out
+
+
+def test_pipelined_connections_under_address_sanitizer(tmp_path):
+    """The pipelined client connections (``evhttp.hpp`` PipeConn) against an evhttp server that
+    answers out of order from timers and now and then drops every connection: each answer
+    reaches its own request, the requests caught on a dropped connection fail once, later ones
+    get through on new connections -- clean under ASan+UBSan (``native/tests/pipe_stress.cpp``)."""
+    if shutil.which(CXX) is None:
+        pytest.skip("no C++ compiler")
+    src = ROOT / "aca_dotnet_workshop_amd" / "native" / "tests" / "pipe_stress.cpp"
+    exe = tmp_path / "pipe_stress"
+    r = subprocess.run([CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                        "-fno-sanitize-recover=undefined", str(src), "-o", str(exe), "-lpthread", "-lssl", "-lcrypto"],
+                       capture_output=True, text=True)
+    if r.returncode != 0 and "cannot find" in r.stderr:
+        pytest.skip(f"sanitizer runtime unavailable: {r.stderr[-300:]}")
+    assert r.returncode == 0, r.stderr[-3000:]
+    run = subprocess.run([str(exe), "20000", "64", str(tmp_path / "ps.sock")], capture_output=True, text=True,
+                         env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1"), timeout=300)
+    out = run.stdout + run.stderr
+    assert run.returncode == 0 and "ALL OK" in run.stdout, out[-5000:]
+    assert "ERROR: AddressSanitizer" not in out and "runtime error" not in out
