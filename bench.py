@@ -1173,7 +1173,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         cpu1.update(_ingress_cpu(env))
         th1 = env.stack.thread_cpu(_ingress_pid(env))
         hot = hot_threads(th0, th1, dt)
-        threads_all = hot_threads(th0, th1, dt, top=80)  # the stderr diagnostics line only
+        # every thread that did work in the timed region: the stderr diagnostics line only
+        threads_all = [t for t in hot_threads(th0, th1, dt, top=200) if t[2] >= 0.005]
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
