@@ -652,8 +652,14 @@ PYBIND11_MODULE(_ttnative, m) {
                return a;
              };
              py::list cols;
-             for (size_t c = 0; c < d.paths.size(); ++c)
-               cols.append(py::make_tuple(d.paths[c], d.dict_from[c], py::cast(d.new_values[c]), arr(d.ids[c])));
+             for (size_t c = 0; c < d.paths.size(); ++c) {
+               // every new value a JSON string (timestamps, names): the reader decodes them in
+               // one json.loads without checking each text first
+               const auto& nv = d.new_values[c];
+               const bool all_str =
+                   std::all_of(nv.begin(), nv.end(), [](const std::string& v) { return !v.empty() && v[0] == '"'; });
+               cols.append(py::make_tuple(d.paths[c], d.dict_from[c], py::cast(nv), arr(d.ids[c]), all_str));
+             }
              py::dict out;
              out["gen"] = d.gen;
              out["on"] = d.on;

@@ -18,6 +18,7 @@ from __future__ import annotations
 import functools
 import itertools
 import json
+import operator
 import os
 import time
 from dataclasses import dataclass
@@ -182,6 +183,8 @@ class KeyTable:
 _RANK_EPOCHS = itertools.count(1)
 
 
+_starts_with_quote = operator.methodcaller("startswith", '"')
+
 _NATIVE = []  # [module or None], resolved on first use
 
 
@@ -255,13 +258,15 @@ class Column:
             self.rank_version += 1
         return i
 
-    def encode_json_many(self, texts: list[str]) -> np.ndarray:
+    def encode_json_many(self, texts: list[str], all_strings: bool | None = None) -> np.ndarray:
         """Dictionary ids of JSON value texts (the native mirror's new dictionary entries).
         Strings -- timestamps, names, e-mails, the values a growing collection adds on every
         write -- are decoded in one ``json.loads`` and appended in bulk: the native dictionary
         holds each string once (strings compare by value there, as here), so none is already
         here and no per-value ``vkey`` or dictionary probe is needed."""
-        if texts and all(t[:1] == '"' for t in texts):
+        if all_strings is None:  # the mirror says; other callers have it checked (a C-level loop)
+            all_strings = all(map(_starts_with_quote, texts))
+        if texts and all_strings:
             joined = ",".join(texts)
             strs = json.loads("[" + joined + "]")
             base = len(self.values)
@@ -559,7 +564,11 @@ class ColumnarIndex:
         ix.native = store
         ix.docs = None
         ix._ncur = (0, 0, 0)  # (generation, rows seen, kill-log position)
+        # per column: native dictionary id -> this index's id, in a capacity-doubled buffer
+        # (``_remap_n`` entries used): a sync appends the new values' ids in place instead of
+        # copying the whole map (taskCreatedOn's grows by one per write)
         ix._remap: list[np.ndarray] = []
+        ix._remap_n: list[int] = []
         if not store.mirror_enable(list(dict.fromkeys(paths))):
             raise Unsupported("collection cannot be mirrored (TTL writes)")
         ix.sync()
@@ -568,17 +577,18 @@ class ColumnarIndex:
     def sync(self) -> bool:
         """Apply the native mirror's changes; returns True when anything changed."""
         gen, rows, kc = self._ncur
-        d = self.native.mirror_delta(gen, rows, kc, [r.size for r in self._remap])
+        d = self.native.mirror_delta(gen, rows, kc, list(self._remap_n))
         if d["disabled"] or not d["on"]:
             raise Unsupported("collection mirror disabled (TTL writes)")
         lo, hi = int(d["from"]), int(d["n"])
         changed = d["full"] or hi > lo or d["kills"].size > 0
         if d["full"]:
-            self.columns, self.col_of, self._remap = [], {}, []
-            for path, _, _, _ in d["columns"]:
+            self.columns, self.col_of, self._remap, self._remap_n = [], {}, [], []
+            for path, *_ in d["columns"]:
                 self.col_of[path] = len(self.columns)
                 self.columns.append(Column(path))
                 self._remap.append(np.zeros(0, dtype=np.int32))
+                self._remap_n.append(0)
             self.cap = max(TILE, (hi + TILE - 1) // TILE * TILE)
             self.ids = np.full((len(self.columns), self.cap), -1, dtype=np.int32)
             self.live = np.zeros(self.cap, dtype=np.int32)
@@ -589,12 +599,19 @@ class ColumnarIndex:
             self.keys = []
         assert lo == self.n, (lo, self.n)
         self._grow(hi)
-        for c, (path, dict_from, values, ids) in enumerate(d["columns"]):
+        for c, (path, dict_from, values, ids, all_str) in enumerate(d["columns"]):
             col = self.columns[c]
             if values:  # new dictionary values, mapped onto Python's equality (vkey)
-                add = col.encode_json_many(values)
-                self._remap[c] = np.concatenate([self._remap[c][:dict_from], add])
-            rm = self._remap[c]
+                add = col.encode_json_many(values, all_str)
+                need = dict_from + add.size
+                buf = self._remap[c]
+                if buf.size < need:
+                    grown = np.empty(max(need, 2 * buf.size, 1024), dtype=np.int32)
+                    grown[:dict_from] = buf[:dict_from]
+                    buf = self._remap[c] = grown
+                buf[dict_from:need] = add
+                self._remap_n[c] = need
+            rm = self._remap[c][:self._remap_n[c]]
             if hi > lo:
                 self.ids[c, lo:hi] = np.where(ids >= 0, rm[np.maximum(ids, 0)] if rm.size else -1, -1)
         if hi > lo:

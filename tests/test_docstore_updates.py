@@ -31,7 +31,7 @@ def _doc(rnd: random.Random) -> dict:
 def _mirror_rows(store) -> list[tuple[int, dict]]:
     d = store.mirror_delta(0, 0, 0, [])
     assert d["full"] and d["on"]
-    cols = {path: (values, ids) for path, _from, values, ids in d["columns"]}
+    cols = {path: (values, ids) for path, _from, values, ids, _all_str in d["columns"]}
     rows = []
     for r in range(d["n"]):
         if not d["live"][r]:
