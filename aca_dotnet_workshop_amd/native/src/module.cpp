@@ -463,6 +463,14 @@ PYBIND11_MODULE(_ttnative, m) {
       return py::none();
     return py::make_tuple(count, py::bytes(out), more);
   }, py::arg("body"), py::arg("by_created") = false, py::arg("descending") = false);
+  // whether `tasks_from_query` reads this page in its one pass (the store's own layout), for tests
+  m.def("tasks_query_in_store_layout", [](py::bytes body) {
+    std::string_view b = body.cast<std::string_view>();
+    std::string buf;
+    std::vector<taskcodec::TaskRow> rows;
+    bool token = false;
+    return taskcodec::valid_utf8(b) && taskcodec::fast_query_tasks(b, buf, rows, token);
+  });
 
   // A JSON array -> its items re-grouped into arrays of at most `n` items (raw slices, no
   // re-encoding), or None when the text is not a valid JSON array (the processor's chunked

@@ -552,8 +552,203 @@ inline bool conditional_mark(std::string_view got, std::string& bulk, std::vecto
 // the tasks whose due date is before the run's date (UTC), as a TaskModel JSON array; also the
 // page's size.  `starts` (optional): the offset in `out` of each kept task's object, so the
 // caller can cut the array into chunks without scanning it again.
+// The same order as a number: "yyyy-MM-ddTHH:mm:ss[.f{1,7}]" (canonical, as write_task writes it)
+// -> (seconds of the calendar fields, mixed radix) * 10^6 + microseconds.  Monotone in the
+// DateTime; the fraction's 7th digit (100 ns) is below the TaskModel's microsecond precision.
+inline uint64_t created_key(std::string_view c) {
+  auto d = [&](size_t i, size_t n) {
+    uint64_t r = 0;
+    for (size_t k = i; k < i + n && k < c.size(); ++k) r = r * 10 + (uint64_t)(c[k] - '0');
+    return r;
+  };
+  uint64_t secs = ((((d(0, 4) * 13 + d(5, 2)) * 32 + d(8, 2)) * 24 + d(11, 2)) * 60 + d(14, 2)) * 60 + d(17, 2);
+  uint64_t us = 0;
+  size_t i = 19, n = 0;
+  if (i < c.size() && c[i] == '.')
+    for (++i; i < c.size() && c[i] >= '0' && c[i] <= '9' && n < 6; ++i, ++n) us = us * 10 + (uint64_t)(c[i] - '0');
+  for (; n < 6; ++n) us *= 10;
+  return secs * 1000000 + us;
+}
+
+// The closing quote of a JSON string literal whose opening quote is at p[-1], when the literal
+// has no escapes and no raw control characters (16 bytes a step); nullptr otherwise.
+inline const char* plain_string_end(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), ctl = _mm_set1_epi8(0x1f);
+  while (e - p >= 16) {
+    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    const __m128i hit = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)),
+                                     _mm_cmpeq_epi8(_mm_max_epu8(x, ctl), ctl));  // byte <= 0x1f
+    const int m = _mm_movemask_epi8(hit);
+    if (m) {
+      p += __builtin_ctz((unsigned)m);
+      return *p == '"' ? p : nullptr;
+    }
+    p += 16;
+  }
+  for (; p < e; ++p) {
+    if (*p == '"') return p;
+    if (*p == '\\' || (unsigned char)*p < 0x20) return nullptr;
+  }
+  return nullptr;
+}
+
+// A task in the layout the API stores it (write_task, store form: the fields in order, compact,
+// strings without escapes) at t[i..], -> write_task's output for it appended to `out`, `i` past
+// it, `key` its created_key; no value tree.  False = another layout (the caller binds it through
+// the tree; the output would be the same).
+inline bool fast_task_at(std::string_view t, size_t& i, std::string& out, uint64_t& key,
+                         std::string* due_day = nullptr) {
+  const char* const e = t.data() + t.size();
+  auto lit = [&](std::string_view w) {
+    if (t.compare(i, w.size(), w) != 0) return false;
+    i += w.size();
+    return true;
+  };
+  auto str = [&](std::string_view& v) {
+    if (i >= t.size() || t[i] != '"') return false;
+    const char* q = plain_string_end(t.data() + i + 1, e);
+    if (!q) return false;
+    const size_t j = (size_t)(q - t.data());
+    v = t.substr(i, j + 1 - i);
+    i = j + 1;
+    return true;
+  };
+  auto boolean = [&](bool& b) { return lit("true") ? (b = true) : lit("false") ? !(b = false) : false; };
+  std::string_view id, name, by, created, due, to;
+  bool done = false, over = false;
+  if (!lit("{\"taskId\":") || !str(id) || !lit(",\"taskName\":") || !str(name) || !lit(",\"taskCreatedBy\":") ||
+      !str(by) || !lit(",\"taskCreatedOn\":") || !str(created) || !lit(",\"taskDueDate\":") || !str(due) ||
+      !lit(",\"taskAssignedTo\":") || !str(to) || !lit(",\"isCompleted\":") || !boolean(done) ||
+      !lit(",\"isOverDue\":") || !boolean(over) || !lit("}"))
+    return false;
+  id = id.substr(1, id.size() - 2);
+  if (id.size() != 36) return false;
+  for (size_t k = 0; k < 36; ++k) {
+    const char c = id[k];
+    if (k == 8 || k == 13 || k == 18 || k == 23) {
+      if (c != '-') return false;
+    } else if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'))) {
+      return false;
+    }
+  }
+  std::string c, d;  // a 28-byte date does not fit the small-string buffer: one allocation each
+  c.reserve(40);
+  d.reserve(40);
+  if (!parse_due(created.substr(1, created.size() - 2), c) || !parse_due(due.substr(1, due.size() - 2), d)) return false;
+  out += "{\"taskId\":\"";
+  const size_t at = out.size();
+  out.append(id);
+  for (size_t k = at; k < out.size(); ++k) out[k] = (char)std::tolower((unsigned char)out[k]);
+  out += "\",\"taskName\":";
+  out.append(name);
+  out += ",\"taskCreatedBy\":";
+  out.append(by);
+  out += ",\"taskCreatedOn\":\"";
+  out += c;
+  out += "\",\"taskDueDate\":\"";
+  out += d;
+  out += "\",\"taskAssignedTo\":";
+  out.append(to);
+  out += done ? ",\"isCompleted\":true" : ",\"isCompleted\":false";
+  out += over ? ",\"isOverDue\":true}" : ",\"isOverDue\":false}";
+  key = created_key(c);
+  if (due_day) due_day->assign(d, 0, 10);
+  return true;
+}
+
+struct TaskRow {
+  uint64_t key;
+  size_t at, len;
+};
+
+// The state-query response as the backing's page assembly writes it (DocStore::mirror_results,
+// `{"results":[{"key":..,"data":..,"etag":".."},..],"token":".."}`, compact) with every task in
+// the stored layout: the rows written into `buf` in one pass over the text, which the layout
+// itself validates.  False = any other text (the value tree reads it).
+inline bool fast_query_tasks(std::string_view b, std::string& buf, std::vector<TaskRow>& rows, bool& token) {
+  size_t i = 0;
+  const char* const e = b.data() + b.size();
+  auto lit = [&](std::string_view w) {
+    if (b.compare(i, w.size(), w) != 0) return false;
+    i += w.size();
+    return true;
+  };
+  auto str = [&](size_t& len) {
+    if (i >= b.size() || b[i] != '"') return false;
+    const char* q = plain_string_end(b.data() + i + 1, e);
+    if (!q) return false;
+    const size_t j = (size_t)(q - b.data());
+    len = j - i - 1;
+    i = j + 1;
+    return true;
+  };
+  if (!lit("{\"results\":[")) return false;
+  if (!lit("]")) {
+    while (true) {
+      size_t klen = 0, elen = 0;
+      if (!lit("{\"key\":") || !str(klen) || !lit(",\"data\":")) return false;
+      const size_t at = buf.size();
+      uint64_t key = 0;
+      if (!fast_task_at(b, i, buf, key)) return false;
+      rows.push_back({key, at, buf.size() - at});
+      if (!lit(",\"etag\":") || !str(elen) || !lit("}")) return false;
+      if (lit(",")) continue;
+      if (lit("]")) break;
+      return false;
+    }
+  }
+  token = false;
+  if (lit(",\"token\":")) {
+    size_t tlen = 0;
+    if (!str(tlen)) return false;
+    token = tlen > 0;
+  }
+  return lit("}") && i == b.size();
+}
+
+// overdue_filter over a page in the layout the API answers it (query_tasks's output: compact,
+// the fields in order, strings without escapes), in one pass; false = any other text.
+inline bool fast_overdue_filter(std::string_view b, std::string_view run_day, size_t& retrieved, size_t& kept,
+                                std::string& out, std::vector<size_t>* starts) {
+  if (run_day.size() != 10 || !valid_utf8(b) || b.empty() || b[0] != '[') return false;
+  size_t i = 1;
+  retrieved = kept = 0;
+  out.assign("[");
+  out.reserve(b.size() + 2);
+  std::string day;
+  if (b.size() == 2 && b[1] == ']') {
+    out += ']';
+    return true;
+  }
+  while (true) {
+    const size_t mark = out.size();
+    if (kept) out += ',';
+    uint64_t key = 0;
+    if (!fast_task_at(b, i, out, key, &day)) return false;
+    ++retrieved;
+    if (std::string_view(day) < run_day) {
+      if (starts) starts->push_back(mark + (kept ? 1 : 0));
+      ++kept;
+    } else {
+      out.resize(mark);
+    }
+    if (i < b.size() && b[i] == ',') {
+      ++i;
+      continue;
+    }
+    if (i + 1 == b.size() && b[i] == ']') break;
+    return false;
+  }
+  out += ']';
+  return true;
+}
+
 inline bool overdue_filter(std::string_view body, std::string_view run_day, size_t& retrieved, size_t& kept,
                            std::string& out, std::vector<size_t>* starts = nullptr) {
+  // the API's own page: one pass, no value tree (1,000 tasks a sweep); anything else below
+  const size_t nstarts = starts ? starts->size() : 0;
+  if (fast_overdue_filter(body, run_day, retrieved, kept, out, starts)) return true;
+  if (starts) starts->resize(nstarts);
   tt::Value doc;
   if (!parse_array(body, doc) || run_day.size() != 10) return false;
   retrieved = doc.items.size();
@@ -577,23 +772,6 @@ inline bool overdue_filter(std::string_view body, std::string_view run_day, size
   return true;
 }
 
-// The same order as a number: "yyyy-MM-ddTHH:mm:ss[.f{1,7}]" (canonical, as write_task writes it)
-// -> (seconds of the calendar fields, mixed radix) * 10^6 + microseconds.  Monotone in the
-// DateTime; the fraction's 7th digit (100 ns) is below the TaskModel's microsecond precision.
-inline uint64_t created_key(std::string_view c) {
-  auto d = [&](size_t i, size_t n) {
-    uint64_t r = 0;
-    for (size_t k = i; k < i + n && k < c.size(); ++k) r = r * 10 + (uint64_t)(c[k] - '0');
-    return r;
-  };
-  uint64_t secs = ((((d(0, 4) * 13 + d(5, 2)) * 32 + d(8, 2)) * 24 + d(11, 2)) * 60 + d(14, 2)) * 60 + d(17, 2);
-  uint64_t us = 0;
-  size_t i = 19, n = 0;
-  if (i < c.size() && c[i] == '.')
-    for (++i; i < c.size() && c[i] >= '0' && c[i] <= '9' && n < 6; ++i, ++n) us = us * 10 + (uint64_t)(c[i] - '0');
-  for (; n < 6; ++n) us *= 10;
-  return secs * 1000000 + us;
-}
 
 // State-query response of the task collection (Dapr `{"results": [{"key", "data", "etag"}],
 // "token", "metadata"}`) -> the TaskModel JSON array of the results that carry data: the API's
@@ -603,9 +781,41 @@ inline uint64_t created_key(std::string_view c) {
 // (the reference's `.OrderBy(o => o.TaskCreatedOn)`, TasksStoreManager.cs:136): System.Text.Json
 // trims the fraction, so the strings do not sort chronologically within one second ("...:42Z"
 // is earlier than "...:42.1Z").  `more`: the response carries a continuation token.
+inline bool query_tasks_tree(std::string_view body, std::string& out, size_t& count, bool by_created, bool* more,
+                             bool descending);
+
 inline bool query_tasks(std::string_view body, std::string& out, size_t& count, bool by_created = false,
                         bool* more = nullptr, bool descending = false) {
   if (!valid_utf8(body)) return false;
+  // the page as the backing assembles it from the API's own writes: one pass over the text,
+  // every task copied with its dates re-formatted -- no value tree for a 1,000-task sweep page;
+  // any other text goes through the tree
+  std::vector<TaskRow> rows;
+  std::string buf;
+  buf.reserve(body.size());
+  bool token = false;
+  if (!fast_query_tasks(body, buf, rows, token)) return query_tasks_tree(body, out, count, by_created, more, descending);
+  if (more) *more = token;
+  if (by_created) {
+    if (descending)
+      std::stable_sort(rows.begin(), rows.end(), [](const TaskRow& a, const TaskRow& b) { return a.key > b.key; });
+    else
+      std::stable_sort(rows.begin(), rows.end(), [](const TaskRow& a, const TaskRow& b) { return a.key < b.key; });
+  }
+  count = 0;
+  out.assign("[");
+  out.reserve(buf.size() + rows.size() + 2);
+  for (const TaskRow& r : rows) {
+    if (count++) out += ',';
+    out.append(buf, r.at, r.len);
+  }
+  out += ']';
+  return true;
+}
+
+// query_tasks through the value tree (any text the one-pass reader declines)
+inline bool query_tasks_tree(std::string_view body, std::string& out, size_t& count, bool by_created, bool* more,
+                             bool descending) {
   tt::Value doc;
   try {
     doc = tt::parse_strict(body);

@@ -346,6 +346,81 @@ def test_query_results_created_order_matches_datetime_order(stamps):
     assert made[1] == tasks_to_json(ref)
 
 
+def _store_page(datas: list, token: str | None, keys: list[str] | None = None) -> bytes:
+    """A query page laid out as the backing's page assembly writes it (DocStore::mirror_results):
+    compact, key / data / etag per result, then the token."""
+    parts = []
+    for i, d in enumerate(datas):
+        k = json.dumps(keys[i] if keys else f"k{i}")
+        parts.append('{"key":' + k + ',"data":' + d + ',"etag":"' + str(i + 1) + '"}')
+    return ('{"results":[' + ",".join(parts) + "]" + (',"token":' + json.dumps(token) if token is not None else "")
+            + "}").encode()
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.tuples(_text, _text, _text, st.datetimes(min_value=__import__("datetime").datetime(1, 1, 1)),
+                          st.datetimes(min_value=__import__("datetime").datetime(1, 1, 1)), st.booleans(),
+                          st.booleans(), st.booleans(), st.uuids()), max_size=12),
+       st.one_of(st.none(), st.just(""), st.text("0123456789", min_size=1, max_size=4)),
+       st.booleans(), st.booleans())
+def test_query_results_in_the_store_layout_read_in_one_pass(rows, token, by_created, descending):
+    """The page as the backing writes it is read in one pass (taskcodec.hpp fast_query_tasks):
+    the same tasks, order, bytes and continuation flag as the value-tree reader gives for the same
+    page re-spaced (which that pass declines) -- for any names (a page with an escaped one goes
+    to the tree whole), upper-case ids, any dates."""
+    from aca_dotnet_workshop_amd.models import tasks_from_query_wire
+    datas = []
+    for name, by, to, created, due, done, over, upper, uid in rows:
+        t = TaskModel(task_id=str(uid).upper() if upper else str(uid), task_name=name, task_created_by=by,
+                      task_created_on=created, task_due_date=due, task_assigned_to=to, is_completed=done,
+                      is_over_due=over)
+        datas.append(t.to_store_json())
+    page = _store_page(datas, token)
+    spaced = json.dumps(json.loads(page)).encode()  # ", " / ": " separators: not the store's layout
+    fast = tasks_from_query_wire(page, by_created=by_created, descending=descending)
+    tree = tasks_from_query_wire(spaced, by_created=by_created, descending=descending)
+    assert fast is not None and fast == tree
+    assert fast[2] == bool(token)
+    plain = b"\\" not in page  # no escaped (or control) character anywhere
+    assert _native().tasks_query_in_store_layout(page) == plain
+    assert not _native().tasks_query_in_store_layout(spaced) or not datas
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.tuples(_text, st.datetimes(min_value=__import__("datetime").datetime(1, 1, 1)),
+                          st.datetimes(min_value=__import__("datetime").datetime(2000, 1, 1),
+                                       max_value=__import__("datetime").datetime(2040, 1, 1)),
+                          st.booleans(), st.uuids()), max_size=12),
+       st.dates(min_value=__import__("datetime").date(2000, 1, 1), max_value=__import__("datetime").date(2040, 1, 1)),
+       st.integers(1, 5))
+def test_overdue_filter_of_the_api_page_in_one_pass(rows, day, chunk):
+    """The processor's filter over the API's overdue page (the page exactly as the API answers:
+    taskcodec.hpp fast_overdue_filter) gives what the value-tree reader gives for the same page
+    re-spaced: counts, kept tasks and chunk boundaries, byte for byte; and the binder agrees."""
+    page_tasks = [TaskModel(task_id=uid, task_name=name, task_created_on=created, task_due_date=due,
+                            is_completed=done).to_json() for name, created, due, done, uid in rows]
+    page = ("[" + ",".join(page_tasks) + "]").encode()
+    spaced = json.dumps(json.loads(page)).encode()
+    run_day = day.isoformat()
+    assert _native().tasks_overdue_filter(page, run_day) == _native().tasks_overdue_filter(spaced, run_day)
+    assert (_native().tasks_overdue_filter_chunks(page, run_day, chunk)
+            == _native().tasks_overdue_filter_chunks(spaced, run_day, chunk))
+    _check_lists(page, run_day)
+
+
+def test_query_results_one_pass_declines_other_layouts():
+    """Anything but the store's exact layout goes to the value tree, with the same answer."""
+    from aca_dotnet_workshop_amd.models import tasks_from_query_wire
+    t = TaskModel.model_validate(_TASK).to_store_json()
+    pages = [_store_page([t], "7"), _store_page([t, t.replace('"isOverDue":false', '"isOverDue":false,"x":"y"')], None),
+             _store_page([t], None).replace(b'"etag":"1"', b'"etag":"1","extra":1'),
+             _store_page([t], None).replace(b'{"results":', b'{"metadata":{},"results":'),
+             _store_page([], "9"), b'{"results":[]}', b'{"results":null}']
+    for page in pages:
+        want = tasks_from_query_wire(json.dumps(json.loads(page)).encode(), by_created=True)
+        assert tasks_from_query_wire(page, by_created=True) == want, page
+
+
 @pytest.mark.parametrize("body", [b"[]", b'{"results": 5}', b'{"results": [{"data": "text"}]}',
                                   json.dumps({"results": [{"data": {"TaskName": "x"}}]}).encode()])
 def test_query_results_decline(body):
