@@ -480,78 +480,6 @@ inline bool parse_array(std::string_view body, tt::Value& doc) {
   return doc.t == tt::Value::Array;
 }
 
-// POST api/overduetasks/markoverdue: the ids (for the per-task log lines) and the state API's
-// bulk-save body [{"key": id, "value": TaskModel with isOverDue = true}, ...].
-inline bool mark_overdue(std::string_view body, std::vector<std::string>& ids, std::string& bulk) {
-  tt::Value doc;
-  if (!parse_array(body, doc)) return false;
-  ids.clear();
-  bulk.assign("[");
-  std::string id, day;
-  for (size_t i = 0; i < doc.items.size(); ++i) {
-    if (i) bulk += ',';
-    bulk += "{\"key\":\"";
-    const size_t key_at = bulk.size();
-    bulk += "\",\"value\":";
-    if (!write_task(doc.items[i], true, bulk, id, day)) return false;
-    bulk += '}';
-    bulk.insert(key_at, id);
-    ids.push_back(id);
-  }
-  bulk += ']';
-  return true;
-}
-
-// The conditional half of markoverdue: the state API's bulk-get answer for the page's ids
-// ([{"key", "data", "etag"} | {"key"}]) -> a bulk save that sets isOverDue on the STORED task
-// (not the caller's copy) only where it is still open and not yet overdue, each item guarded by
-// the ETag it was read with (first-write): a completion that lands between the sweep's query
-// and this save makes the save fail for that item (409) instead of reverting it.  `ids`: the
-// tasks written; `skipped`: completed / already overdue / deleted ones.
-inline bool conditional_mark(std::string_view got, std::string& bulk, std::vector<std::string>& ids,
-                             size_t& skipped) {
-  tt::Value doc;
-  if (!parse_array(got, doc)) return false;
-  ids.clear();
-  skipped = 0;
-  bulk.assign("[");
-  std::string id, day;
-  for (const auto& it : doc.items) {
-    if (it.t != tt::Value::Object) return false;
-    const tt::Value* key = it.get("key");
-    const tt::Value* data = it.get("data");
-    const tt::Value* etag = it.get("etag");
-    if (key == nullptr || key->t != tt::Value::String) return false;
-    if (data == nullptr || data->t == tt::Value::Null) {  // deleted since the sweep's query
-      ++skipped;
-      continue;
-    }
-    const tt::Value* f[8];
-    if (!task_fields(*data, f)) return false;
-    if ((f[6] && f[6]->t == tt::Value::Bool && f[6]->b) || (f[7] && f[7]->t == tt::Value::Bool && f[7]->b)) {
-      ++skipped;
-      continue;
-    }
-    if (ids.size()) bulk += ',';
-    bulk += "{\"key\":";
-    tt::escape_to(bulk, key->s);
-    bulk += ",\"value\":";
-    if (!write_task(*data, true, bulk, id, day, true)) return false;
-    if (etag != nullptr && etag->t == tt::Value::String && !etag->s.empty()) {
-      bulk += ",\"etag\":";
-      tt::escape_to(bulk, etag->s);
-    }
-    bulk += ",\"options\":{\"concurrency\":\"first-write\"}}";
-    ids.push_back(id);
-  }
-  bulk += ']';
-  return true;
-}
-
-// The cron job's filter (ScheduledTasksManagerController.cs:31-36): of the API's overdue page,
-// the tasks whose due date is before the run's date (UTC), as a TaskModel JSON array; also the
-// page's size.  `starts` (optional): the offset in `out` of each kept task's object, so the
-// caller can cut the array into chunks without scanning it again.
 // The same order as a number: "yyyy-MM-ddTHH:mm:ss[.f{1,7}]" (canonical, as write_task writes it)
 // -> (seconds of the calendar fields, mixed radix) * 10^6 + microseconds.  Monotone in the
 // DateTime; the fraction's 7th digit (100 ns) is below the TaskModel's microsecond precision.
@@ -596,8 +524,12 @@ inline const char* plain_string_end(const char* p, const char* e) {
 // strings without escapes) at t[i..], -> write_task's output for it appended to `out`, `i` past
 // it, `key` its created_key; no value tree.  False = another layout (the caller binds it through
 // the tree; the output would be the same).
+// `overdue`: written with isOverDue set (markoverdue's save); `store_form`: the created date in
+// the store's round-trip form (write_task's); `flags` (optional): the task's own isCompleted and
+// isOverDue as read; `id_out` (optional): the id as written (lower case).
 inline bool fast_task_at(std::string_view t, size_t& i, std::string& out, uint64_t& key,
-                         std::string* due_day = nullptr) {
+                         std::string* due_day = nullptr, bool overdue = false, bool store_form = false,
+                         std::pair<bool, bool>* flags = nullptr, std::string* id_out = nullptr) {
   const char* const e = t.data() + t.size();
   auto lit = [&](std::string_view w) {
     if (t.compare(i, w.size(), w) != 0) return false;
@@ -634,11 +566,14 @@ inline bool fast_task_at(std::string_view t, size_t& i, std::string& out, uint64
   std::string c, d;  // a 28-byte date does not fit the small-string buffer: one allocation each
   c.reserve(40);
   d.reserve(40);
-  if (!parse_due(created.substr(1, created.size() - 2), c) || !parse_due(due.substr(1, due.size() - 2), d)) return false;
+  if (!parse_due(created.substr(1, created.size() - 2), c, store_form) || !parse_due(due.substr(1, due.size() - 2), d))
+    return false;
   out += "{\"taskId\":\"";
   const size_t at = out.size();
   out.append(id);
   for (size_t k = at; k < out.size(); ++k) out[k] = (char)std::tolower((unsigned char)out[k]);
+  if (id_out) id_out->assign(out, at, 36);
+  if (flags) *flags = {done, over};
   out += "\",\"taskName\":";
   out.append(name);
   out += ",\"taskCreatedBy\":";
@@ -650,7 +585,7 @@ inline bool fast_task_at(std::string_view t, size_t& i, std::string& out, uint64
   out += "\",\"taskAssignedTo\":";
   out.append(to);
   out += done ? ",\"isCompleted\":true" : ",\"isCompleted\":false";
-  out += over ? ",\"isOverDue\":true}" : ",\"isOverDue\":false}";
+  out += (over || overdue) ? ",\"isOverDue\":true}" : ",\"isOverDue\":false}";
   key = created_key(c);
   if (due_day) due_day->assign(d, 0, 10);
   return true;
@@ -706,6 +641,148 @@ inline bool fast_query_tasks(std::string_view b, std::string& buf, std::vector<T
   return lit("}") && i == b.size();
 }
 
+// POST api/overduetasks/markoverdue: the ids (for the per-task log lines) and the state API's
+// bulk-save body [{"key": id, "value": TaskModel with isOverDue = true}, ...].
+inline bool mark_overdue(std::string_view body, std::vector<std::string>& ids, std::string& bulk) {
+  tt::Value doc;
+  if (!parse_array(body, doc)) return false;
+  ids.clear();
+  bulk.assign("[");
+  std::string id, day;
+  for (size_t i = 0; i < doc.items.size(); ++i) {
+    if (i) bulk += ',';
+    bulk += "{\"key\":\"";
+    const size_t key_at = bulk.size();
+    bulk += "\",\"value\":";
+    if (!write_task(doc.items[i], true, bulk, id, day)) return false;
+    bulk += '}';
+    bulk.insert(key_at, id);
+    ids.push_back(id);
+  }
+  bulk += ']';
+  return true;
+}
+
+// The conditional half of markoverdue: the state API's bulk-get answer for the page's ids
+// ([{"key", "data", "etag"} | {"key"}]) -> a bulk save that sets isOverDue on the STORED task
+// (not the caller's copy) only where it is still open and not yet overdue, each item guarded by
+// the ETag it was read with (first-write): a completion that lands between the sweep's query
+// and this save makes the save fail for that item (409) instead of reverting it.  `ids`: the
+// tasks written; `skipped`: completed / already overdue / deleted ones.
+// conditional_mark over the sidecar's bulk-get answer as the data plane lays it out
+// (`[{"key":..,"data":<stored task>,"etag":".."}|{"key":..}]`, compact) with every task in the
+// stored layout, in one pass; false = any other text.
+inline bool fast_conditional_mark(std::string_view b, std::string& bulk, std::vector<std::string>& ids,
+                                  size_t& skipped) {
+  if (!valid_utf8(b)) return false;
+  const char* const e = b.data() + b.size();
+  size_t i = 0;
+  auto lit = [&](std::string_view w) {
+    if (b.compare(i, w.size(), w) != 0) return false;
+    i += w.size();
+    return true;
+  };
+  auto str = [&](std::string_view& v) {
+    if (i >= b.size() || b[i] != '"') return false;
+    const char* q = plain_string_end(b.data() + i + 1, e);
+    if (!q) return false;
+    const size_t j = (size_t)(q - b.data());
+    v = b.substr(i, j + 1 - i);
+    i = j + 1;
+    return true;
+  };
+  ids.clear();
+  skipped = 0;
+  bulk.assign("[");
+  bulk.reserve(b.size() + 64 * 128);
+  if (!lit("[")) return false;
+  if (lit("]")) {
+    bulk += ']';
+    return i == b.size();
+  }
+  std::string id;
+  while (true) {
+    std::string_view key, etag;
+    if (!lit("{\"key\":") || !str(key)) return false;
+    if (lit("}")) {
+      ++skipped;  // deleted since the sweep's query
+    } else {
+      if (!lit(",\"data\":")) return false;
+      const size_t mark = bulk.size();
+      if (ids.size()) bulk += ',';
+      bulk += "{\"key\":";
+      bulk.append(key);
+      bulk += ",\"value\":";
+      uint64_t k = 0;
+      std::pair<bool, bool> flags;
+      if (!fast_task_at(b, i, bulk, k, nullptr, true, true, &flags, &id)) return false;
+      if (!lit(",\"etag\":") || !str(etag) || !lit("}")) return false;
+      if (flags.first || flags.second) {  // completed or already overdue: not written
+        bulk.resize(mark);
+        ++skipped;
+      } else {
+        if (etag.size() > 2) {
+          bulk += ",\"etag\":";
+          bulk.append(etag);
+        }
+        bulk += ",\"options\":{\"concurrency\":\"first-write\"}}";
+        ids.push_back(id);
+      }
+    }
+    if (lit(",")) continue;
+    if (lit("]")) break;
+    return false;
+  }
+  bulk += ']';
+  return i == b.size();
+}
+
+inline bool conditional_mark(std::string_view got, std::string& bulk, std::vector<std::string>& ids,
+                             size_t& skipped) {
+  // the data plane's own answer around the stored tasks: one pass; anything else below
+  if (fast_conditional_mark(got, bulk, ids, skipped)) return true;
+  tt::Value doc;
+  if (!parse_array(got, doc)) return false;
+  ids.clear();
+  skipped = 0;
+  bulk.assign("[");
+  std::string id, day;
+  for (const auto& it : doc.items) {
+    if (it.t != tt::Value::Object) return false;
+    const tt::Value* key = it.get("key");
+    const tt::Value* data = it.get("data");
+    const tt::Value* etag = it.get("etag");
+    if (key == nullptr || key->t != tt::Value::String) return false;
+    if (data == nullptr || data->t == tt::Value::Null) {  // deleted since the sweep's query
+      ++skipped;
+      continue;
+    }
+    const tt::Value* f[8];
+    if (!task_fields(*data, f)) return false;
+    if ((f[6] && f[6]->t == tt::Value::Bool && f[6]->b) || (f[7] && f[7]->t == tt::Value::Bool && f[7]->b)) {
+      ++skipped;
+      continue;
+    }
+    if (ids.size()) bulk += ',';
+    bulk += "{\"key\":";
+    tt::escape_to(bulk, key->s);
+    bulk += ",\"value\":";
+    if (!write_task(*data, true, bulk, id, day, true)) return false;
+    if (etag != nullptr && etag->t == tt::Value::String && !etag->s.empty()) {
+      bulk += ",\"etag\":";
+      tt::escape_to(bulk, etag->s);
+    }
+    bulk += ",\"options\":{\"concurrency\":\"first-write\"}}";
+    ids.push_back(id);
+  }
+  bulk += ']';
+  return true;
+}
+
+// The cron job's filter (ScheduledTasksManagerController.cs:31-36): of the API's overdue page,
+// the tasks whose due date is before the run's date (UTC), as a TaskModel JSON array; also the
+// page's size.  `starts` (optional): the offset in `out` of each kept task's object, so the
+// caller can cut the array into chunks without scanning it again.
 // overdue_filter over a page in the layout the API answers it (query_tasks's output: compact,
 // the fields in order, strings without escapes), in one pass; false = any other text.
 inline bool fast_overdue_filter(std::string_view b, std::string_view run_day, size_t& retrieved, size_t& kept,

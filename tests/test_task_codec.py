@@ -408,6 +408,29 @@ def test_overdue_filter_of_the_api_page_in_one_pass(rows, day, chunk):
     _check_lists(page, run_day)
 
 
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.tuples(_text, st.datetimes(min_value=__import__("datetime").datetime(1, 1, 1)),
+                          st.booleans(), st.booleans(), st.uuids(), st.sampled_from(["", "7", "123"]),
+                          st.booleans()), max_size=10))
+def test_conditional_mark_of_the_bulk_get_in_one_pass(rows):
+    """markoverdue's conditional save over the sidecar's bulk-get answer laid out as the data
+    plane writes it (taskcodec.hpp fast_conditional_mark) equals the value-tree reader's answer
+    for the same text re-spaced: the same bulk body, ids and skips (deleted, completed and
+    already-overdue tasks; empty ETags)."""
+    parts = []
+    for name, created, done, over, uid, etag, gone in rows:
+        if gone:
+            parts.append('{"key":' + json.dumps(str(uid)) + "}")
+            continue
+        t = TaskModel(task_id=uid, task_name=name, task_created_on=created, is_completed=done, is_over_due=over)
+        parts.append('{"key":' + json.dumps(str(uid)) + ',"data":' + t.to_store_json() + ',"etag":'
+                     + json.dumps(etag) + "}")
+    got = ("[" + ",".join(parts) + "]").encode()
+    spaced = json.dumps(json.loads(got)).encode()
+    fast, tree = _native().tasks_conditional_mark(got), _native().tasks_conditional_mark(spaced)
+    assert fast is not None and fast == tree
+
+
 def test_query_results_one_pass_declines_other_layouts():
     """Anything but the store's exact layout goes to the value tree, with the same answer."""
     from aca_dotnet_workshop_amd.models import tasks_from_query_wire
