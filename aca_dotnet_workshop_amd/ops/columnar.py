@@ -364,7 +364,10 @@ class Column:
             if buf is not None:
                 grown[:nr.size] = buf[:nr.size]
             buf = grown
-        lo = nr.extend(self.values, buf)
+        try:
+            lo = nr.extend(self.values, buf)
+        except (TypeError, ValueError):  # not a list of values as expected: the numpy path
+            lo = -1
         if lo < 0:  # a value UTF-8 cannot carry (a lone surrogate): the numpy path orders it
             self._nr = self._nr_buf = None
             return None
