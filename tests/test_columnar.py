@@ -1145,5 +1145,27 @@ def test_gpu_scatter_upload_writes_every_segment():
     torch.cuda.synchronize()
     assert np.array_equal(dst.cpu().numpy(), want)
     assert k.uploads == before + 1
+
+
+@pytest.mark.gpu
+def test_gpu_upload_ring_reuses_its_slots_in_order():
+    """Back-to-back uploads with no synchronise between them cycle through the staging ring
+    (GpuKernels.UPLOAD_SLOTS pinned slots, each reused once the scatter that read it has
+    finished -- its event, not a stream synchronise): later writes to the same bytes win in
+    order, growing payloads re-allocate a slot safely, and every segment lands."""
+    import torch
+    k = _kernels()
+    rng = np.random.default_rng(11)
+    dst = torch.zeros(1 << 18, dtype=torch.int32, device=k.device)
+    want = np.zeros(1 << 18, dtype=np.int32)
+    for step in range(5 * k.UPLOAD_SLOTS):
+        size = int(rng.integers(1, 4096)) * (1 + step)  # growing: slots re-allocate on the way
+        at = int(rng.integers(1, want.size - size))  # the two segments of one launch never overlap
+        payload = rng.integers(-1000, 1000, size=size).astype(np.int32)
+        k.upload([(dst.data_ptr() + 4 * at, payload), (dst.data_ptr(), np.array([step], dtype=np.int32))])
+        want[at:at + size] = payload
+        want[0] = step
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy(), want)
     k.upload([])  # nothing to write: no launch
     assert k.uploads == before + 1
