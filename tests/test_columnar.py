@@ -1145,6 +1145,8 @@ def test_gpu_scatter_upload_writes_every_segment():
     torch.cuda.synchronize()
     assert np.array_equal(dst.cpu().numpy(), want)
     assert k.uploads == before + 1
+    k.upload([])  # nothing to write: no launch
+    assert k.uploads == before + 1
 
 
 @pytest.mark.gpu
@@ -1167,5 +1169,52 @@ def test_gpu_upload_ring_reuses_its_slots_in_order():
         want[0] = step
     torch.cuda.synchronize()
     assert np.array_equal(dst.cpu().numpy(), want)
-    k.upload([])  # nothing to write: no launch
-    assert k.uploads == before + 1
+
+
+@pytest.mark.gpu
+def test_gpu_sweep_query_tracks_a_growing_native_mirror():
+    """The sweep's query on the GPU (range on taskDueDate, two booleans, ORDER BY taskCreatedOn,
+    a page) against the host's answer, round after round of writes to a native mirror: new due
+    dates re-rank their column (rank tables re-sent into kept buffers), created stamps arrive a
+    little out of order (native string ranks merge them into the tail), completions and
+    overdue marks kill rows, the filter program stays cached across the sort column's growth,
+    and every upload goes through the staging ring."""
+    import json as _json
+    from aca_dotnet_workshop_amd.native import load
+    N = load()
+    rnd = random.Random(5)
+    store = N.DocStore("", 0, 256)
+    prefix = "api||"
+
+    def put(i, due_day, done=False, over=False, jitter=0):
+        us = 1000 * i + jitter
+        doc = {"taskId": f"{i:08d}-0000-0000-0000-000000000000", "taskName": f"t{i}",
+               "taskCreatedOn": f"2025-01-01T{us // 3_600_000_000 % 24:02d}:{us // 60_000_000 % 60:02d}:"
+                                f"{us // 1_000_000 % 60:02d}.{us % 1_000_000:06d}0",
+               "taskDueDate": f"2024-{1 + due_day // 28:02d}-{1 + due_day % 28:02d}T00:00:00",
+               "isCompleted": done, "isOverDue": over}
+        store.set(f"{prefix}{i:08d}", _json.dumps(doc))
+
+    n = 0
+    for _ in range(30_000):
+        put(n, rnd.randrange(60))
+        n += 1
+    paths = ["\u0000keyprefix", "taskDueDate", "isCompleted", "isOverDue", "taskCreatedOn"]
+    ix = ColumnarIndex.from_native(store, paths)
+    k = _kernels()
+    q = {"filter": {"AND": [{"EQ": {"\u0000keyprefix": prefix}},
+                            {"AND": [{"LT": {"taskDueDate": "2024-02-15T00:00:00"}}, {"EQ": {"isCompleted": False}},
+                                     {"EQ": {"isOverDue": False}}]}]},
+         "sort": [{"key": "taskCreatedOn", "order": "ASC"}], "page": {"limit": 500}}
+    for rnd_i in range(12):
+        for _ in range(1500):  # new tasks, a few with due dates never seen before, stamps a little shuffled
+            put(n, rnd.randrange(60 + rnd_i * 3), jitter=rnd.randrange(-3000, 3000))
+            n += 1
+        for _ in range(200):  # completions and overdue marks of older tasks
+            i = rnd.randrange(n)
+            put(i, rnd.randrange(60), done=rnd.random() < 0.5, over=rnd.random() < 0.5)
+        ix.sync()
+        gpu_rows, gpu_tok = ix.query_rows(q, k)
+        host_rows, host_tok = ix.query_rows(q, None)
+        assert gpu_rows.tolist() == host_rows.tolist() and gpu_tok == host_tok, rnd_i
+    assert k.uploads > 12
