@@ -138,7 +138,9 @@ class BackingServices:
 
     # -- engines ---------------------------------------------------------------
     def _path(self, *parts: str) -> str:
-        if self.data_dir is None:
+        # TT_BACKING_LOGS=0: documents and messages kept in memory only (a measurement switch:
+        # what the append logs cost the write path)
+        if self.data_dir is None or os.environ.get("TT_BACKING_LOGS", "1") == "0":
             return ""
         p = self.data_dir.joinpath(*[_safe(x) for x in parts])
         p.parent.mkdir(parents=True, exist_ok=True)
