@@ -460,6 +460,12 @@ def main() -> None:
     share = cpu_budget() / max(1, local)  # a job-wide CPU quota is shared by the host's ranks
     pinned = pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local)
     cores = min(cpu_budget(), share) if pinned else share
+    # weak scaling: every rank's environment is sized for the same CPU budget whatever N is --
+    # the 1-GPU box's 16-CPU share by default -- so N=1 on a larger node does not get the whole
+    # job's quota and N=8 a sixteenth of it (the driver's efficiency compares per-rank numbers)
+    cap = float(os.environ.get("TT_BENCH_CORES_PER_RANK", "16"))
+    if cap > 0:
+        cores = min(cores, cap)
     if a.entry == "frontend":
         return main_frontend(a, d, cores, pinned)
     return main_localstack(a, d, cores, pinned)
