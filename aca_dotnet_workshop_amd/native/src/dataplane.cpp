@@ -1323,7 +1323,9 @@ class DataPlane {
               ",\"firstWrite\":" + (it.first_write ? "true" : "false") + ",\"ttlMs\":" + std::to_string(it.ttl_ms) + "}";
     }
     body += "]";
-    store_request(s.ep(shard), "POST", s.coll_path + "/bulkset", std::move(h), std::move(body), std::move(done));
+    // a bulk save takes the store a millisecond or two: not on the pipelined connections, where
+    // the single saves queued behind it would wait for it
+    store_request(s.ep(shard), "POST", s.coll_path + "/bulkset", std::move(h), std::move(body), std::move(done), false);
   }
 
   static std::string full_key(const Store& s, const std::string& key) {
@@ -1434,7 +1436,8 @@ class DataPlane {
                         if (!scan_bulkget(bg->bodies[slot], *bg)) bg->failed = true, bg->error = "unreadable bulkget";
                       }
                       if (--bg->left == 0) (*fin)();
-                    });
+                    },
+                    bg->keys.size() <= 16);  // a large bulk get is not pipelined either (see bulkset)
       ++slot;
     }
   }
