@@ -98,6 +98,54 @@ std::string error_json(std::string_view code, std::string_view msg) {
 
 bool valid_json(std::string_view s) { return tt::valid(s); }  // compact(): tt::compact
 
+// The string value of a top-level key of a valid JSON object (the CloudEvent's traceparent),
+// found by scanning, without building the object; false when absent or not a plain string (a
+// key or value with escapes is decoded by the full parser instead).
+bool top_level_string(std::string_view json, std::string_view key, std::string& out) {
+  const char* p = tt::ws_end(json.data(), json.data() + json.size());
+  const char* e = json.data() + json.size();
+  if (p >= e || *p != '{') return false;
+  p = tt::ws_end(p + 1, e);
+  while (p < e && *p == '"') {
+    const char* k = p + 1;
+    const char* q = tt::skip_value(p, e);  // past the key's closing quote
+    std::string_view name(k, (size_t)(q - 1 - k));
+    p = tt::ws_end(q, e);
+    if (p >= e || *p != ':') return false;
+    p = tt::ws_end(p + 1, e);
+    const char* v = p;
+    p = tt::skip_value(p, e);
+    if (name.find('\\') != std::string_view::npos) {  // an escaped key: the parser decides
+      try {
+        Value obj = parse(json);
+        const Value* x = obj.get(key);
+        if (!x || x->t != Value::String) return false;
+        out = x->s;
+        return true;
+      } catch (const std::exception&) {
+        return false;
+      }
+    }
+    if (name == key) {
+      if (*v != '"') return false;
+      std::string_view lit(v + 1, (size_t)(p - 1 - (v + 1)));
+      if (lit.find('\\') != std::string_view::npos) {
+        try {
+          out = parse(std::string_view(v, (size_t)(p - v))).s;
+        } catch (const std::exception&) {
+          return false;
+        }
+      } else {
+        out.assign(lit);
+      }
+      return true;
+    }
+    p = tt::ws_end(p, e);
+    if (p < e && *p == ',') p = tt::ws_end(p + 1, e);
+  }
+  return false;
+}
+
 std::string errno_text(int e) {
   switch (e) {
     case ETIMEDOUT: return "timeout";
@@ -649,13 +697,10 @@ class DataPlane {
       SpanCtx span;
       bool is_ce = false;
       std::string parent_tp;
-      if (ctype.rfind("application/cloudevents", 0) == 0) {
-        try {
-          Value ce = parse(body);
-          is_ce = true;
-          if (auto* tp = ce.get("traceparent"); tp && tp->t == Value::String) parent_tp = tp->s;
-        } catch (const std::exception&) {
-        }
+      if (ctype.rfind("application/cloudevents", 0) == 0 && valid_json(body)) {
+        // the envelope's traceparent by scanning it: no value tree per delivery
+        is_ce = true;
+        top_level_string(body, "traceparent", parent_tp);
       }
       if (!is_ce && !s_.raw) {
         std::string base = lower(ctype.substr(0, ctype.find(';')));

@@ -210,6 +210,16 @@ def test_publish_api(plane, tmp_path):
             assert r.status == 204
             await _until(lambda: sum(x[0] == "event" for x in seen) == 2)
             assert [x for x in seen if x[0] == "event"][1][2] == {"x": 1}
+            # an envelope's own traceparent (after other keys, spaced, one escaped key) is continued
+            tp2 = "00-" + "ef" * 16 + "-" + "12" * 8 + "-01"
+            text = ('{ "specversion" : "1.0", "id":"id2", "sou\\u0072ce": "me", "type": "t", '
+                    '"data": {"traceparent": "nested"}, "traceparent" : "%s" }' % tp2)
+            r = await h.post(f"{b}/v1.0/publish/bus/events", body=text.encode(),
+                             headers={"Content-Type": "application/cloudevents+json"})
+            assert r.status == 204
+            await _until(lambda: sum(x[0] == "event" for x in seen) == 3)
+            third = [x for x in seen if x[0] == "event"][2]
+            assert third[2] == {"traceparent": "nested"} and third[1].split("-")[1] == "ef" * 16
             assert msgs.counts("events/subscriptions/app-a")["completed"] >= 1
     run(main())
 
