@@ -1009,13 +1009,14 @@ class DataPlane {
   }
 
   // ---------------------------------------------------------------- invoke
-  HeaderList fwd_headers(const Message& m, const std::string& traceparent, bool drop_mesh) {
+  // The request's end-to-end headers, moved out of `m` (its headers are not read afterwards).
+  HeaderList fwd_headers(Message& m, const std::string& traceparent, bool drop_mesh) {
     HeaderList h;
     h.reserve(m.headers.size() + 3);
     for (auto& kv : m.headers) {
       if (is_invoke_hop(kv.first)) continue;
       if (drop_mesh && kv.first == "tt-mesh-token") continue;
-      h.push_back(kv);
+      h.push_back(std::move(kv));
     }
     h.emplace_back("traceparent", traceparent);
     return h;
@@ -1118,10 +1119,7 @@ class DataPlane {
     split_target(m.target, path, qs);
     auto d = begin(m, std::move(r), "internal", path);
     if (auto* c = m.header("dapr-caller-app-id")) d->attrs.emplace_back("caller", *c);
-    HeaderList h = fwd_headers(m, d->span.traceparent(), true);
-    if (auto* c = m.header("dapr-caller-app-id")) {
-      (void)c;  // already forwarded with the other headers
-    }
+    HeaderList h = fwd_headers(m, d->span.traceparent(), true);  // dapr-caller-app-id goes along
     std::string app_id = app_id_;
     call_app(m.method, m.target, std::move(h), std::move(m.body), [d, app_id](ClientResult&& res) {
       if (res.err) {

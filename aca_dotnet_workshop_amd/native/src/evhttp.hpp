@@ -376,6 +376,9 @@ class MsgParser {
             if (n < 0 || end == cl->c_str()) return fail("bad content-length");
             if ((size_t)n > kMaxBody) return fail("body too large");
             remaining_ = (size_t)n;
+            // one allocation for a body that arrives over several reads (bounded: the length
+            // is the peer's claim until the bytes come)
+            if (remaining_ > buf.size() - off) msg_.body.reserve(std::min<size_t>(remaining_, 4u << 20));
             st_ = remaining_ ? BODY : FINISH;
           } else if (request_) {
             st_ = FINISH;

@@ -40,6 +40,7 @@ inline HttpHead parse_head(std::string_view head) {
     h.c = std::string(first.substr(s2 + 1));
   }
   size_t pos = eol == std::string_view::npos ? head.size() : eol + 2;
+  h.headers.reserve(16);  // one allocation for a typical head instead of growing 1, 2, 4, 8
   while (pos < head.size()) {
     size_t e = head.find("\r\n", pos);
     if (e == std::string_view::npos) e = head.size();

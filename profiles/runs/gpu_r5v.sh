@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5: confirmation after moving bulk saves off the pipelined connections and scanning the
+# delivered CloudEvent's traceparent -- GPU tests, smoke(), the driver's bench command twice
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r5v
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/gputests.log 2>&1 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit $?
+for i in 1 2; do
+  timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $out/bench_$i.json 2> $out/bench_$i.err || exit $?
+done
