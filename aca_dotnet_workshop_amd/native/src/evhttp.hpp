@@ -685,9 +685,19 @@ class ServerConn : public IoObj {
     size_t idx = (size_t)(seq - head_seq_);
     if (idx >= pending_.size() || pending_[idx].ready) return;
     Slot& sl = pending_[idx];
-    sl.wire.reserve(body.size() + 256);
-    write_response(sl.wire, status, headers, body, head_request, sl.close_after);
-    sl.ready = true;
+    if (idx == 0) {
+      // the oldest answer owed goes straight into the output buffer (which keeps its capacity):
+      // no slot allocation and no second copy
+      const bool close_after = sl.close_after;
+      write_response(out_, status, headers, body, head_request, close_after);
+      if (close_after) close_after_write_ = true;
+      pending_.pop_front();
+      ++head_seq_;
+    } else {
+      sl.wire.reserve(body.size() + 256);
+      write_response(sl.wire, status, headers, body, head_request, sl.close_after);
+      sl.ready = true;
+    }
     drain();
     // resume a pipeline that was paused at its depth limit
     if (!dead && !parsing_ && !close_after_write_ && in_off_ < in_.size()) parse();
