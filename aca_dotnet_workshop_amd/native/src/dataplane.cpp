@@ -1103,7 +1103,7 @@ class DataPlane {
       // mutual TLS: the caller proved an environment workload identity; the app-id it claims
       // must be one its certificate names (no spoofed dapr-caller-app-id)
       auto* c = m.header("dapr-caller-app-id");
-      if (!m.tls || (c && !names_include(m.tls_peer, *c))) {
+      if (!m.tls || (c && !(m.tls_peer && names_include(*m.tls_peer, *c)))) {
         r.json(403, error_json("ERR_MESH_AUTH", "caller identity not proven by its mTLS certificate"));
         return;
       }

@@ -303,7 +303,9 @@ struct Message {
   bool http10 = false;
   HeaderList headers;  // lower-cased names
   std::string body;
-  std::string tls_peer;  // server side over TLS: SAN names of the verified client certificate
+  // server side over TLS: SAN names of the verified client certificate (shared by the
+  // connection's requests)
+  std::shared_ptr<const std::string> tls_peer;
   bool tls = false;      // server side: arrived over TLS
   std::string peer;      // server side, listeners with `record_peer`: the client's IP address
 
@@ -723,8 +725,7 @@ class ServerConn : public IoObj {
   bool parsing_ = false;
   uint32_t interest_ = EPOLLIN;
   std::unique_ptr<TlsIo> tls_;
-  std::string tls_peer_;
-  bool tls_peer_known_ = false;
+  std::shared_ptr<const std::string> tls_peer_;
   bool record_peer_ = false;
   std::string peer_;
 
@@ -782,7 +783,7 @@ class ServerConn : public IoObj {
         break;
       }
       if (tls_) {
-        if (!tls_peer_known_) tls_peer_ = tls_->peer_names(), tls_peer_known_ = true;
+        if (!tls_peer_) tls_peer_ = std::make_shared<const std::string>(tls_->peer_names());
         m.tls = true;
         m.tls_peer = tls_peer_;
       }
