@@ -318,7 +318,7 @@ struct Message {
     auto* c = header("connection");
     if (!c) return !http10;
     std::string v = *c;
-    for (auto& ch : v) ch = (char)std::tolower((unsigned char)ch);
+    for (auto& ch : v) ch = ascii_lower(ch);
     if (v.find("close") != std::string::npos) return false;
     if (http10) return v.find("keep-alive") != std::string::npos;
     return true;

@@ -25,6 +25,9 @@ inline std::string_view trim(std::string_view s) {
   return s.substr(i, j - i);
 }
 
+// ASCII lower case (header names are tokens): no locale lookup per character
+inline char ascii_lower(char c) { return c >= 'A' && c <= 'Z' ? (char)(c + ('a' - 'A')) : c; }
+
 inline HttpHead parse_head(std::string_view head) {
   HttpHead h;
   size_t eol = head.find("\r\n");
@@ -50,7 +53,7 @@ inline HttpHead parse_head(std::string_view head) {
     size_t colon = line.find(':');
     if (colon == std::string_view::npos) throw std::invalid_argument("malformed header line");
     std::string name(trim(line.substr(0, colon)));
-    for (auto& ch : name) ch = (char)std::tolower((unsigned char)ch);
+    for (auto& ch : name) ch = ascii_lower(ch);
     h.headers.emplace_back(std::move(name), std::string(trim(line.substr(colon + 1))));
   }
   return h;

@@ -495,7 +495,13 @@ inline std::string compact(std::string_view s) {
 
 inline void escape_to(std::string& out, std::string_view s) {
   out += '"';
-  for (unsigned char c : s) {
+  const char* run = s.data();  // plain characters go out in runs, not one push_back each
+  const char* e = s.data() + s.size();
+  for (const char* p = run; p < e; ++p) {
+    const unsigned char c = (unsigned char)*p;
+    if (c >= 0x20 && c != '"' && c != '\\') continue;
+    out.append(run, (size_t)(p - run));
+    run = p + 1;
     switch (c) {
       case '"': out += "\\\""; break;
       case '\\': out += "\\\\"; break;
@@ -505,15 +511,12 @@ inline void escape_to(std::string& out, std::string_view s) {
       case '\b': out += "\\b"; break;
       case '\f': out += "\\f"; break;
       default:
-        if (c < 0x20) {
-          char buf[8];
-          std::snprintf(buf, sizeof buf, "\\u%04x", c);
-          out += buf;
-        } else {
-          out += (char)c;
-        }
+        char buf[8];
+        std::snprintf(buf, sizeof buf, "\\u%04x", c);
+        out += buf;
     }
   }
+  out.append(run, (size_t)(e - run));
   out += '"';
 }
 
