@@ -225,7 +225,7 @@ inline bool query_param(std::string_view target, std::string_view name, std::str
     if (e.first == name) return out = e.second, true;
   auto low = [](std::string_view x) {
     std::string r(x);
-    for (auto& c : r) c = (char)std::tolower((unsigned char)c);
+    for (auto& c : r) c = ::tt::ascii_lower(c);
     return r;
   };
   const std::string want = low(name);
@@ -924,7 +924,7 @@ class AppHost {
     std::string v = ct ? ct->substr(0, ct->find(';')) : std::string();
     size_t a = v.find_first_not_of(" \t"), b = v.find_last_not_of(" \t");
     v = a == std::string::npos ? std::string() : v.substr(a, b - a + 1);
-    for (auto& c : v) c = (char)std::tolower((unsigned char)c);
+    for (auto& c : v) c = ::tt::ascii_lower(c);
     return v;
   }
 
@@ -941,7 +941,7 @@ class AppHost {
       ctype = u.content_type.substr(0, u.content_type.find(';'));
       size_t a = ctype.find_first_not_of(" \t"), b = ctype.find_last_not_of(" \t");
       ctype = a == std::string::npos ? std::string() : ctype.substr(a, b - a + 1);
-      for (auto& c : ctype) c = (char)std::tolower((unsigned char)c);
+      for (auto& c : ctype) c = ::tt::ascii_lower(c);
     }
     if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
     std::string name;
@@ -1002,7 +1002,7 @@ class AppHost {
       const std::string* ct = header(m, "content-type");
       if (ct && !ct->empty()) {
         std::string low(*ct);
-        for (auto& c : low) c = (char)std::tolower((unsigned char)c);
+        for (auto& c : low) c = ::tt::ascii_lower(c);
         if (low.find("json") == std::string::npos) return false;
       }
       if (!::taskcodec::create(m.body, r->rng, j->task)) return false;
