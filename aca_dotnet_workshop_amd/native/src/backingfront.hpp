@@ -523,6 +523,7 @@ class BackingFront {
     std::string path, qs;
     split(m.target, path, qs);
     std::vector<std::string> seg;
+    seg.reserve(8);
     for (size_t i = 1; i <= path.size();) {
       size_t j = path.find('/', i);
       if (j == std::string::npos) j = path.size();
@@ -586,14 +587,23 @@ class BackingFront {
     return true;
   }
 
+  // The native collection a cosmos path names (/cosmos/{account}/{db}/{container}/...), or null;
+  // the lookup key is built in a per-thread buffer (no allocation per request).
+  Coll* coll_of(const std::vector<std::string>& seg) {
+    thread_local std::string k;
+    k.assign(seg[1]);
+    k += '\x1f';
+    k += seg[2];
+    k += '\x1f';
+    k += seg[3];
+    std::shared_lock l(cfg_mu_);
+    auto it = colls_.find(k);
+    return it != colls_.end() && it->second->store ? it->second.get() : nullptr;
+  }
+
   // -- cosmos documents ----------------------------------------------------------------------
   bool handle_doc(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
-    Coll* c = nullptr;
-    {
-      std::shared_lock l(cfg_mu_);
-      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
-      if (it != colls_.end() && it->second->store) c = it->second.get();
-    }
+    Coll* c = coll_of(seg);
     if (!c) return false;
     const std::string& key = seg[5];
     const std::string scope = "cosmos/" + seg[1];
@@ -640,12 +650,7 @@ class BackingFront {
 
   // POST .../bulkset: [{"key", "value" (JSON text or value), "etag", "firstWrite", "ttlMs"}]
   bool handle_bulkset(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
-    Coll* c = nullptr;
-    {
-      std::shared_lock l(cfg_mu_);
-      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
-      if (it != colls_.end() && it->second->store) c = it->second.get();
-    }
+    Coll* c = coll_of(seg);
     if (!c) return false;
     std::vector<DocStore::BulkItem> batch;
     if (!scan_bulk_items(m.body, batch)) return false;  // Python produces the error response
@@ -676,12 +681,7 @@ class BackingFront {
   // POST .../bulkget {"keys": [...]} -> [{"key", "data" (the stored JSON, as is), "etag"} | {"key"}]
   // in key order (a missing document has no data): the read half of a bulk read-modify-write
   bool handle_bulkget(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
-    Coll* c = nullptr;
-    {
-      std::shared_lock l(cfg_mu_);
-      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
-      if (it != colls_.end() && it->second->store) c = it->second.get();
-    }
+    Coll* c = coll_of(seg);
     if (!c) return false;
     Value body;
     try {
@@ -823,12 +823,7 @@ class BackingFront {
   }
 
   bool handle_query(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
-    Coll* c = nullptr;
-    {
-      std::shared_lock l(cfg_mu_);
-      auto it = colls_.find(seg[1] + "\x1f" + seg[2] + "\x1f" + seg[3]);
-      if (it != colls_.end() && it->second->store) c = it->second.get();
-    }
+    Coll* c = coll_of(seg);
     if (!c) return false;
     bool indexed = false;
     try {
