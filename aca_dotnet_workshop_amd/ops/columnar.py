@@ -1328,16 +1328,19 @@ class ColumnarIndex:
         if limit <= 0 or k_total > kernels.page_cap:
             return None
         tm = self.timing
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.thread_time()
         hit = self._device_sort_plan(sort, kernels)
         if hit is None:
             return None
         specs_t, ranks_t, seq_bits, _, plan = hit
         t1 = time.perf_counter()
         st, code, bitmaps = self.device_program(prog, kernels)
-        t2 = time.perf_counter()
+        t2, c2 = time.perf_counter(), time.thread_time()
         tm["page_plan_ms"] = tm.get("page_plan_ms", 0.0) + (t1 - t0) * 1e3
         tm["page_program_ms"] = tm.get("page_program_ms", 0.0) + (t2 - t1) * 1e3
+        # this thread's CPU time in plan + program: the wall time above less the waits (GIL,
+        # other threads on the core)
+        tm["page_host_cpu_ms"] = tm.get("page_host_cpu_ms", 0.0) + (c2 - c0) * 1e3
         ntiles = (self.n + TILE - 1) // TILE
         if ntiles == 0:
             return np.zeros(0, dtype=np.int32), None

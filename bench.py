@@ -1199,7 +1199,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                           "store_ms_total": {k2: acc.get(k2) for k2 in ("lock_wait_ms", "sync_ms",
                                                                          "select_and_results_ms", "select_ms",
                                                                          "results_ms", "bg_sync_ms", "bg_syncs", "page_plan_ms",
-                                                                         "page_program_ms", "page_zones_ms",
+                                                                         "page_program_ms", "page_host_cpu_ms",
+                                                                         "page_zones_ms",
                                                                          "page_kernels_ms", "page_launches",
                                                                          "page_more_ms")}}
         if shared and sweeper is not None:  # the partitioned sweep marks what one store would
