@@ -509,6 +509,7 @@ class ColumnarIndex:
         # smallest ordering key, re-computed for the tiles whose rows changed
         self._zones: dict[Any, dict] = {}
         self.timing: dict[str, float] = {}  # where the paged device path spends its time (summed)
+        self._plan_tm: dict[str, float] | None = None  # set while page_gpu plans (sub-step times)
         for p in paths:
             self.add_column(p)
 
@@ -1225,6 +1226,8 @@ class ColumnarIndex:
         task)."""
         if len(sort or []) > kernels.max_sort_keys:
             return None
+        tm = self._plan_tm  # page_gpu's timing dict while it plans (None for the background warm)
+        c0 = time.thread_time()
         cols = [self.add_column(srt["key"]) for srt in sort or []]
         seq_bits = max(1, int(self._next_seq).bit_length())
         if seq_bits > 32:
@@ -1250,6 +1253,10 @@ class ColumnarIndex:
             [c.rank_changes_since(sq) for (_, c), sq in zip(tables, ent["seqs"])]
         rebuild = ent is None or any(lo is None for lo in los) or \
             any(r.size > cap for (r, _), cap in zip(tables, ent["caps"]))
+        c1 = time.thread_time()
+        if tm is not None:
+            tm["plan_ranks_ms"] = tm.get("plan_ranks_ms", 0.0) + (c1 - c0) * 1e3
+            tm["plan_rebuilds"] = tm.get("plan_rebuilds", 0) + int(rebuild)
         if rebuild:
             caps = [max(1024, 1 << max(0, int(r.size * 1.25) + 1).bit_length()) for r, _ in tables]
             offs = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64) if caps else np.zeros(0, np.int64)
@@ -1279,7 +1286,13 @@ class ColumnarIndex:
             # they ride the same launch into a buffer allocated once per plan
             ent["specs"] = specs
             segs.append((ent["specs_dev"].data_ptr(), specs))
+        c2 = time.thread_time()
         kernels.upload(segs)
+        if tm is not None:
+            c3 = time.thread_time()
+            tm["plan_tails_ms"] = tm.get("plan_tails_ms", 0.0) + (c2 - c1) * 1e3
+            tm["plan_upload_ms"] = tm.get("plan_upload_ms", 0.0) + (c3 - c2) * 1e3
+            tm["plan_tail_rows"] = tm.get("plan_tail_rows", 0) + sum(int(t.size) for _, t in segs)
         key_bits = seq_bits + int(specs[:, 3].sum()) if specs.size else seq_bits
         return ent["specs_dev"], ent["dev"], seq_bits, key_bits, (specs, ent["host"], seq_bits)
 
@@ -1329,7 +1342,11 @@ class ColumnarIndex:
             return None
         tm = self.timing
         t0, c0 = time.perf_counter(), time.thread_time()
-        hit = self._device_sort_plan(sort, kernels)
+        self._plan_tm = tm
+        try:
+            hit = self._device_sort_plan(sort, kernels)
+        finally:
+            self._plan_tm = None
         if hit is None:
             return None
         specs_t, ranks_t, seq_bits, _, plan = hit

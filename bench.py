@@ -1200,6 +1200,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                                                          "select_and_results_ms", "select_ms",
                                                                          "results_ms", "bg_sync_ms", "bg_syncs", "page_plan_ms",
                                                                          "page_program_ms", "page_host_cpu_ms",
+                                                                         "plan_ranks_ms", "plan_tails_ms",
+                                                                         "plan_upload_ms", "plan_tail_rows",
+                                                                         "plan_rebuilds",
                                                                          "page_zones_ms",
                                                                          "page_kernels_ms", "page_launches",
                                                                          "page_more_ms")}}
