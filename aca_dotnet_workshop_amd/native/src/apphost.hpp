@@ -55,6 +55,7 @@
 #include "evhttp.hpp"
 #include "formcodec.hpp"
 #include "h2.hpp"
+#include "pb.hpp"
 #include "taskcodec.hpp"
 #include "textutil.hpp"
 
@@ -261,6 +262,12 @@ struct NativeRoute {
   int kind = 0;
   std::string method, path;
   ev::Endpoint sidecar;
+  // protocol=grpc: the store and publish calls go to the sidecar's gRPC port (`sidecar` is
+  // then that endpoint) as dapr.proto.runtime.v1.Dapr SaveState / PublishEvent /
+  // QueryStateAlpha1 -- the transport of the reference's DaprClient for them
+  // (TasksStoreManager.cs:35,61,155); the messages carry the component names below
+  bool grpc = false;
+  std::string store, pubsub, topic;
   std::string token;            // dapr-api-token, when the app has one
   double timeout_s = 60;
   double sample_rate = 1.0;     // the app tracer's rate for new traces
@@ -511,6 +518,18 @@ class AppHost {
     r->log_category = get("log_category");
     r->log_prefix = get("log_prefix");
     r->bounds = bounds;
+    if (get("protocol") == "grpc") {
+      if (r->kind != NativeRoute::kApiCreate && r->kind != NativeRoute::kApiList && r->kind != NativeRoute::kApiOverdue)
+        throw std::invalid_argument("only the API's store routes speak gRPC");
+      r->grpc = true;
+      r->store = get("store");
+      r->pubsub = get("pubsub");
+      r->topic = get("topic");
+      if (r->store.empty() || (r->kind == NativeRoute::kApiCreate && (r->pubsub.empty() || r->topic.empty())))
+        throw std::invalid_argument("a gRPC route needs its store (and pubsub / topic)");
+    } else if (!get("protocol").empty() && get("protocol") != "http") {
+      throw std::invalid_argument("native route protocol must be http or grpc");
+    }
     if (r->method.empty() || r->path.empty()) throw std::invalid_argument("a native route needs a method and a path");
     // every status, Location and log line comes from the Python definition: a route without
     // them is refused rather than answering with text of its own
@@ -713,8 +732,15 @@ class AppHost {
     double t0 = 0;
     std::string trace_id, span_id, traceparent;
     ev::HeaderList out_headers;  // traceparent, token, content-type: the SDK's unsampled call
+    ev::HeaderList grpc_md;      // gRPC routes: traceparent, token (the SDK's call metadata)
     ::taskcodec::Created task;
   };
+
+  // the gRPC SDK's metadata on an unsampled call (sdk/grpc_client.py _call_encoded)
+  static void grpc_metadata(NativeJob& j) {
+    j.grpc_md.emplace_back("traceparent", j.traceparent);
+    if (!j.route->token.empty()) j.grpc_md.emplace_back("dapr-api-token", j.route->token);
+  }
 
   void log_event(const NativeRoute& r, const NativeJob& j, std::string message) {
     Event e;
@@ -859,17 +885,18 @@ class AppHost {
     auto value = [&](int f) -> const std::string& { return f == 0 ? midnight : page; };
     log_event(r, *j, r.log_overdue.render_with(value));
     native_inflight_.fetch_add(1);
-    client_.request(r.sidecar, "POST", r.query_target, j->out_headers, r.overdue_query.render_with(value), r.timeout_s,
-                    [this, j](ev::ClientResult&& res) {
-                      if (res.err || res.resp.status >= 300) return hand_over(*j, "query", res);
-                      std::string out;
-                      size_t count = 0;
-                      bool more = false;
-                      if (!::taskcodec::query_tasks(res.resp.body, out, count, true, &more, false)) return decline(*j);
-                      const NativeRoute& r = *j->route;
-                      finish(*j, r.status, {{"Content-Type", r.content_type}, {r.more_header, more ? "true" : "false"}},
-                             out);
-                    });
+    std::string q = r.overdue_query.render_with(value);
+    if (r.grpc) q = pb_query_state(r.store, q);
+    // the query may take milliseconds (a GPU scan): an ordinary connection, not a pipelined one
+    call_step(j, "query", r.query_target, std::move(q), false, [this, j](std::string&& body) {
+      const NativeRoute& r = *j->route;
+      std::string json, out;
+      if (r.grpc && !query_response_json(body, json)) return decline(*j);
+      size_t count = 0;
+      bool more = false;
+      if (!::taskcodec::query_tasks(r.grpc ? json : body, out, count, true, &more, false)) return decline(*j);
+      finish(*j, r.status, {{"Content-Type", r.content_type}, {r.more_header, more ? "true" : "false"}}, out);
+    });
     return true;
   }
 
@@ -882,13 +909,14 @@ class AppHost {
     tt::escape_to(body, who);
     body += r.query_suffix;
     native_inflight_.fetch_add(1);
-    client_.request(r.sidecar, "POST", r.query_target, j->out_headers, body, r.timeout_s, [this, j](ev::ClientResult&& res) {
-      if (res.err || res.resp.status >= 300) return hand_over(*j, "query", res);
-      std::string out;
+    if (r.grpc) body = pb_query_state(r.store, body);
+    call_step(j, "query", r.query_target, std::move(body), false, [this, j](std::string&& res) {
+      const NativeRoute& r = *j->route;
+      std::string json, out;
+      if (r.grpc && !query_response_json(res, json)) return decline(*j);
       size_t count = 0;
       bool more = false;
-      if (!::taskcodec::query_tasks(res.resp.body, out, count, true, &more, true)) return decline(*j);
-      const NativeRoute& r = *j->route;
+      if (!::taskcodec::query_tasks(r.grpc ? json : res, out, count, true, &more, true)) return decline(*j);
       finish(*j, r.status, {{"Content-Type", r.content_type}}, out);
     });
     return true;
@@ -982,6 +1010,7 @@ class AppHost {
       j->out_headers.emplace_back("traceparent", j->traceparent);
       if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
       j->out_headers.emplace_back("Content-Type", "application/json");
+      if (r->grpc) grpc_metadata(*j);
       bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m)
                    : r->kind == NativeRoute::kApiList    ? api_list(j, m)
                                                          : api_overdue(j, m);
@@ -1016,6 +1045,7 @@ class AppHost {
     j->out_headers.emplace_back("traceparent", j->traceparent);
     if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
     j->out_headers.emplace_back("Content-Type", "application/json");
+    if (r->grpc) grpc_metadata(*j);
     j->req = std::move(m);
     j->reply = std::move(reply);
     native_inflight_.fetch_add(1);
@@ -1030,24 +1060,153 @@ class AppHost {
       return true;
     }
     log_event(*r, *j, r->log_save.render(j->task.id, j->task.name, j->task.assigned_to));
-    // the store calls ride the pipelined connections to the sidecar (ev::PipeConn): the creates
-    // of one loop iteration share a send(2) and the sidecar's answers a read
-    client_.request_pipelined(r->sidecar, "POST", r->save_target, j->out_headers, j->task.state_body, r->timeout_s,
-                    [this, j](ev::ClientResult&& res) {
-                      if (res.err || res.resp.status >= 300) return hand_over(*j, "save", res);
-                      const NativeRoute& r = *j->route;
-                      log_event(r, *j, r.log_publish.render(j->task.id, j->task.name, j->task.assigned_to));
-                      client_.request_pipelined(r.sidecar, "POST", r.publish_target, j->out_headers, j->task.task_json,
-                                      r.timeout_s, [this, j](ev::ClientResult&& res2) {
-                                        if (res2.err || res2.resp.status >= 300)
-                                          return hand_over(*j, "publish", res2);
-                                        const NativeRoute& r2 = *j->route;
-                                        finish(*j, r2.status,
-                                               {{"Location", r2.location.render(j->task.id, j->task.name,
-                                                                                j->task.assigned_to)}});
-                                      });
-                    });
+    // gRPC: SaveStateRequest{store, [StateItem{key, value}]} (sdk/grpc_client.py
+    // encode_save_state); HTTP: the state API's body.  The save takes an ordinary connection:
+    // the sidecar may hold it for seconds through the store's 429 retries, and a pipelined
+    // connection would hold every answer queued behind it
+    std::string save = r->grpc ? pb_save_state(r->store, j->task.id, j->task.task_json) : std::move(j->task.state_body);
+    call_step(j, "save", r->save_target, std::move(save), false, [this, j](std::string&&) {
+      const NativeRoute& r = *j->route;
+      log_event(r, *j, r.log_publish.render(j->task.id, j->task.name, j->task.assigned_to));
+      // the publishes ride the pipelined connections (ev::PipeConn): the broker answers at once,
+      // and the creates of one loop iteration share a send(2) and the sidecar's answers a read
+      std::string pub = r.grpc ? pb_publish_event(r.pubsub, r.topic, j->task.task_json, "application/json")
+                               : j->task.task_json;
+      call_step(j, "publish", r.publish_target, std::move(pub), true, [this, j](std::string&&) {
+        const NativeRoute& r2 = *j->route;
+        finish(*j, r2.status, {{"Location", r2.location.render(j->task.id, j->task.name, j->task.assigned_to)}});
+      });
+    });
     return true;
+  }
+
+  // -- the route's sidecar calls, over its protocol -----------------------------------------
+  // proto3 messages of dapr.proto.runtime.v1 (field numbers: sdk/proto.py), written the way
+  // sdk/grpc_client.py writes them, byte for byte
+  static std::string pb_save_state(std::string_view store, std::string_view key, std::string_view value) {
+    pb::Writer item, w;
+    item.len_field(1, key);
+    item.len_field(2, value);
+    w.len_field(1, store);
+    w.len_field(2, item.s);
+    return w.s;
+  }
+  static std::string pb_publish_event(std::string_view pubsub, std::string_view topic, std::string_view data,
+                                      std::string_view ctype) {
+    pb::Writer w;
+    w.len_field(1, pubsub);
+    w.len_field(2, topic);
+    w.len_field(3, data);
+    w.len_field(4, ctype);
+    return w.s;
+  }
+  static std::string pb_query_state(std::string_view store, std::string_view query) {
+    pb::Writer w;  // QueryStateRequest {store_name = 1, query = 2}, as message.SerializeToString
+    w.str(1, store);
+    w.str(2, query);
+    return w.s;
+  }
+  // QueryStateResponse {results = 1 {key, data, etag, error}, token = 2} as the state query
+  // API's JSON answer ({"results":[{"key","data","etag"}],"token"}), the text the task codec
+  // reads; false when an item's data is not JSON (the page is then Python's).
+  static bool query_response_json(std::string_view msg, std::string& out) {
+    pb::Reader rd(msg);
+    uint32_t f, wt;
+    std::string_view v, token;
+    out.assign("{\"results\":[");
+    bool first = true;
+    while (rd.next(f, wt)) {
+      if (f == 1 && wt == pb::LEN && rd.bytes(v)) {
+        pb::Reader ir(v);
+        uint32_t g, gwt;
+        std::string_view x, key, data, etag;
+        while (ir.next(g, gwt)) {
+          if (g == 1 && gwt == pb::LEN && ir.bytes(x)) key = x;
+          else if (g == 2 && gwt == pb::LEN && ir.bytes(x)) data = x;
+          else if (g == 3 && gwt == pb::LEN && ir.bytes(x)) etag = x;
+          else if (!ir.skip(gwt)) break;
+        }
+        if (!ir.ok) return false;
+        if (!data.empty() && !tt::valid(data)) return false;
+        if (!first) out += ',';
+        first = false;
+        out += "{\"key\":";
+        tt::escape_to(out, key);
+        out += ",\"data\":";
+        if (data.empty()) out += "null";
+        else out.append(data);
+        out += ",\"etag\":";
+        tt::escape_to(out, etag);
+        out += '}';
+      } else if (f == 2 && wt == pb::LEN && rd.bytes(v)) {
+        token = v;
+      } else if (!rd.skip(wt)) {
+        break;
+      }
+    }
+    if (!rd.ok) return false;
+    out += ']';
+    if (!token.empty()) {
+      out += ",\"token\":";
+      tt::escape_to(out, token);
+    }
+    out += '}';
+    return true;
+  }
+
+  // One sidecar call of a native route: `target` is the HTTP API's path, or the RPC's :path
+  // for a gRPC route (`body` its request message).  `done` gets the answer's body (HTTP) or the
+  // response message (gRPC); a failure hands the request to Python with the step's result.
+  // `pipelined`: an HTTP call that answers at once may share a pipelined connection.
+  using StepDone = std::function<void(std::string&&)>;
+  void call_step(const std::shared_ptr<NativeJob>& j, const char* step, const std::string& target, std::string body,
+                 bool pipelined, StepDone done) {
+    const NativeRoute& r = *j->route;
+    if (r.grpc) {
+      grpc_.call(r.sidecar, target, j->grpc_md, body, r.timeout_s,
+                 [this, j, step, done = std::move(done)](h2::GrpcResult&& res) {
+                   if (res.err || res.status != 0) return grpc_hand_over(*j, step, res);
+                   done(std::move(res.payload));
+                 });
+      return;
+    }
+    auto cb = [this, j, step, done = std::move(done)](ev::ClientResult&& res) {
+      if (res.err || res.resp.status >= 300) return hand_over(*j, step, res);
+      done(std::move(res.resp.body));
+    };
+    if (pipelined) client_.request_pipelined(r.sidecar, "POST", target, j->out_headers, body, r.timeout_s, std::move(cb));
+    else client_.request(r.sidecar, "POST", target, j->out_headers, body, r.timeout_s, std::move(cb), false);
+  }
+
+  // A failed gRPC call: the HTTP status the SDK's InvocationError carries (the sidecar's
+  // dapr-http-status, else the gRPC code's HTTP equivalent: sdk/grpc_client.py _HTTP_OF) and
+  // grpc-message as its body; transport errors go over as errno (sdk.client.native_route_failure
+  // turns them into the SDK's 503 / 504).
+  void grpc_hand_over(NativeJob& j, const char* step, const h2::GrpcResult& res) {
+    std::string note;
+    if (res.err) {
+      note = std::string("err ") + step + " " + std::to_string(res.err);
+    } else {
+      int http = 500;
+      switch (res.status) {
+        case 3: http = 400; break;
+        case 16: http = 401; break;
+        case 7: http = 403; break;
+        case 5: http = 404; break;
+        case 10: http = 409; break;
+        case 8: http = 429; break;
+        case 12: http = 501; break;
+        case 14: http = 503; break;
+        case 4: http = 504; break;
+        default: break;
+      }
+      for (auto& kv : res.metadata)
+        if (kv.first == "dapr-http-status") http = std::atoi(kv.second.c_str());
+      note = std::string("fail ") + step + " " + std::to_string(http) + " " + tt::text::base64(res.message);
+    }
+    j.req.headers.emplace_back("x-tt-native", std::move(note));
+    to_python(j.server, std::move(j.req), std::move(j.reply));
+    native_inflight_.fetch_sub(1);
   }
 
   void post(std::function<void()> f) {

@@ -413,7 +413,7 @@ def native_route_failure(req: Any, what: dict[str, str]) -> BaseException | None
     if not note or note == "sample":
         return None
     parts = note.split(" ")
-    if len(parts) >= 3 and parts[1] in what:
+    if len(parts) >= 3 and parts[1] in what and parts[1] != "protocol":
         if parts[0] == "fail":
             import base64
             body = base64.b64decode(parts[3]) if len(parts) > 3 else b""
@@ -421,5 +421,10 @@ def native_route_failure(req: Any, what: dict[str, str]) -> BaseException | None
         if parts[0] == "err":
             from ..web.native_host import _client_error
             err = int(parts[2])
-            return _client_error(err, os.strerror(err))
+            exc = _client_error(err, os.strerror(err))
+            if what.get("protocol") == "grpc":  # GrpcSidecarClient's answer to a transport error
+                if isinstance(exc, asyncio.TimeoutError):
+                    return InvocationError(504, b"Deadline Exceeded", what[parts[1]])
+                return InvocationError(503, f"sidecar unreachable: {exc}".encode(), what[parts[1]])
+            return exc
     return RuntimeError(f"malformed native route hand-over: {note[:80]!r}")

@@ -33,11 +33,32 @@ _CONSISTENCY = {"eventual": 1, "strong": 2}
 
 
 def sidecar_grpc_target(environ: dict[str, str] | None = None) -> str:
+    """``DAPR_GRPC_ENDPOINT``, else the co-located sidecar's gRPC Unix socket
+    (``TT_SIDECAR_GRPC_UDS``, set by the sidecar runner next to ``TT_SIDECAR_UDS``), else
+    ``127.0.0.1:$DAPR_GRPC_PORT``."""
     env = os.environ if environ is None else environ
     ep = env.get("DAPR_GRPC_ENDPOINT")
     if ep:
         return ep.replace("http://", "").replace("https://", "").rstrip("/")
+    uds = env.get("TT_SIDECAR_GRPC_UDS")
+    if uds:
+        return f"unix:{uds}"
     return f"127.0.0.1:{env.get('DAPR_GRPC_PORT', '50001')}"
+
+
+def query_response_json(raw: bytes) -> bytes:
+    """A serialized ``QueryStateResponse`` as the HTTP state-query API's JSON answer
+    (``{"results":[{"key","data","etag"}],"token"}``, the layout the task codec reads and the
+    app host's gRPC routes build: apphost.hpp ``query_response_json``)."""
+    r = P.rt("QueryStateResponse").FromString(raw)
+    parts = []
+    for i in r.results:
+        parts.append('{"key":%s,"data":%s,"etag":%s}' % (json.dumps(i.key), i.data.decode() if i.data else "null",
+                                                        json.dumps(i.etag)))
+    out = '{"results":[' + ",".join(parts) + "]"
+    if r.token:
+        out += ',"token":' + json.dumps(r.token)
+    return (out + "}").encode()
 
 
 def _loads(b: bytes) -> Any:
@@ -154,6 +175,16 @@ class GrpcSidecarClient:
         self._channel: Any = None
         self._stubs: dict[str, Any] = {}
 
+    def native_endpoint(self) -> dict[str, str] | None:
+        """Where a native route of the app host reaches this sidecar's gRPC port the way this
+        client does (SidecarClient.native_endpoint's shape, ``protocol`` = ``grpc``); None on
+        the grpcio transport."""
+        if self.transport != "native":
+            return None
+        ep = self.target if self.target.startswith("unix:") else f"tcp:{self.target}"
+        return {"sidecar": ep, "prefix": "", "token": self.api_token or "", "timeout": repr(float(self.timeout)),
+                "protocol": "grpc"}
+
     def _new_channel(self):
         return _NativeChannel(self.target) if self.transport == "native" else grpc.aio.insecure_channel(self.target)
 
@@ -178,8 +209,8 @@ class GrpcSidecarClient:
             md.append(("dapr-api-token", self.api_token))
         return md
 
-    async def _call_encoded(self, rpc: str, payload: bytes, span_name: str) -> None:
-        """A unary call whose request is already serialized and whose response is ignored
+    async def _call_encoded(self, rpc: str, payload: bytes, span_name: str) -> bytes:
+        """A unary call whose request is already serialized; returns the serialized response
         (SaveState, PublishEvent: ``Empty``).  On the native transport inside an unsampled trace
         it goes straight to the app host's HTTP/2 client, without a span."""
         parent = tracing.current_span()
@@ -201,9 +232,9 @@ class GrpcSidecarClient:
                 if "dapr-http-status" in r.headers:
                     status = int(r.headers["dapr-http-status"])
                 raise InvocationError(status, r.headers.get("grpc-message", "").encode(), rpc)
-            return
+            return r.body
         req_cls, _ = P.rpc_types(rpc)
-        await self._call(rpc, req_cls.FromString(payload), span_name)
+        return (await self._call(rpc, req_cls.FromString(payload), span_name)).SerializeToString()
 
     async def _call(self, rpc: str, req, span_name: str):
         span = tracing.tracer().start_span(span_name, "client")
@@ -340,6 +371,15 @@ class GrpcSidecarClient:
         r = await self._call("QueryStateAlpha1", req, f"state query {store}")
         return QueryResponse([StateItem(i.key, _loads(i.data), i.etag or None) for i in r.results], r.token or None,
                              dict(r.metadata))
+
+    async def query_state_raw(self, store: str, query: dict[str, Any] | str,
+                              metadata: dict[str, str] | None = None) -> bytes:
+        """``query_state``'s answer as the HTTP API's JSON text (``query_response_json``): the
+        managers' one-pass codecs read it whichever protocol carried it."""
+        q = query if isinstance(query, str) else json.dumps(query)
+        req = P.rt("QueryStateRequest")(store_name=store, query=q, metadata=metadata or {})
+        raw = await self._call_encoded("QueryStateAlpha1", req.SerializeToString(), f"state query {store}")
+        return query_response_json(raw)
 
     # -- pub/sub ----------------------------------------------------------------
     async def publish_event(self, pubsub: str, topic: str, data: Any, content_type: str | None = None,

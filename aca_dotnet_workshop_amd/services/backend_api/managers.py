@@ -202,24 +202,48 @@ class TasksStoreManager(TasksManager):
         await self.client.publish_event(self.pubsub, self.topic, task_json, content_type="application/json")
         return tid
 
+    def _native_endpoint(self) -> dict | None:
+        ep_of = getattr(self.client, "native_endpoint", None)
+        return ep_of() if ep_of is not None else None
+
+    def _native_calls(self, ep: dict, **targets: tuple[str, str]) -> tuple[dict, dict]:
+        """The route settings and the ``what`` map of a native route's sidecar calls.
+        ``targets``: step -> (HTTP API path, gRPC method).  Over gRPC (the reference's
+        ``DaprClient`` transport for state and publish) the targets are the RPCs' paths, the
+        route writes the request messages (it gets the component names) and a failed call raises
+        what ``GrpcSidecarClient`` raises (its ``what`` is the RPC); over HTTP the API paths and
+        ``SidecarClient``'s messages."""
+        from ...sdk import proto as P
+        cfg = {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"]}
+        grpc = ep.get("protocol") == "grpc"
+        what: dict[str, str] = {}
+        http_what = {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}",
+                     "query": f"query state {self.store}"}
+        for step, (path, rpc) in targets.items():
+            cfg[f"{step}_target"] = P.method_path(rpc) if grpc else ep["prefix"] + path
+            what[step] = rpc if grpc else http_what[step]
+        if grpc:
+            cfg.update({"protocol": "grpc", "store": self.store, "pubsub": self.pubsub, "topic": self.topic})
+            what["protocol"] = "grpc"
+        return cfg, what
+
     def native_create_route(self) -> dict | None:
         """``create_new_task_from_body`` as a native route of the app host (apphost.hpp
         ``api_create``: codec, "Save a new task" log line, state save, "Publish Task Saved"
-        log line, publish, 201), or None when this client cannot take one (gRPC, asyncio I/O).
-        ``what``: the SDK's error messages for the two calls, raised when a call fails."""
-        ep_of = getattr(self.client, "native_endpoint", None)
-        ep = ep_of() if ep_of is not None else None
-        if ep is None or getattr(self.client, "save_state_body", None) is None:
+        log line, publish, 201) over the client's protocol, or None when this client cannot take
+        one (asyncio I/O).  ``what``: the SDK's error messages for the two calls, raised when a
+        call fails."""
+        ep = self._native_endpoint()
+        if ep is None or (ep.get("protocol") != "grpc" and getattr(self.client, "save_state_body", None) is None):
             return None
+        cfg, what = self._native_calls(ep, save=(f"/v1.0/state/{self.store}", "SaveState"),
+                                       publish=(f"/v1.0/publish/{self.pubsub}/{self.topic}", "PublishEvent"))
+        cfg.update({"log_category": log.name,
+                    # the lines create_new_task_from_body logs, with the codec's fields in order
+                    "log_save": LOG_SAVE_NEW, "log_save_args": "name",
+                    "log_publish": LOG_PUBLISH, "log_publish_args": "id,name,assigned_to"})
         return {"kind": "api_create", "method": "POST", "path": "/api/tasks", "route": "/api/tasks",
-                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
-                        "save_target": f"{ep['prefix']}/v1.0/state/{self.store}",
-                        "publish_target": f"{ep['prefix']}/v1.0/publish/{self.pubsub}/{self.topic}",
-                        "log_category": log.name,
-                        # the lines create_new_task_from_body logs, with the codec's fields in order
-                        "log_save": LOG_SAVE_NEW, "log_save_args": "name",
-                        "log_publish": LOG_PUBLISH, "log_publish_args": "id,name,assigned_to"},
-                "what": {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}"}}
+                "cfg": cfg, "what": what}
 
     async def delete_task(self, task_id) -> bool:
         log.info("Delete task with Id: '%s'", task_id)
@@ -253,8 +277,7 @@ class TasksStoreManager(TasksManager):
         """``tasks_by_creator_json`` as a native route of the app host (apphost.hpp ``api_list``):
         the same query text -- this manager's, split around the JSON-encoded creator -- through
         the same sidecar, the same codec; None when this client cannot take one."""
-        ep_of = getattr(self.client, "native_endpoint", None)
-        ep = ep_of() if ep_of is not None else None
+        ep = self._native_endpoint()
         if ep is None or getattr(self.client, "query_state_raw", None) is None:
             return None
         mark = "zqCREATORqz"
@@ -262,11 +285,10 @@ class TasksStoreManager(TasksManager):
         at = text.find(json.dumps(mark))
         if at < 0 or text.count(mark) != 1:
             return None
-        return {"kind": "api_list", "method": "GET", "path": "/api/tasks", "route": "/api/tasks",
-                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
-                        "query_target": f"{ep['prefix']}/v1.0-alpha1/state/{self.store}/query",
-                        "query_prefix": text[:at], "query_suffix": text[at + len(json.dumps(mark)):]},
-                "what": {"query": f"query state {self.store}"}}
+        cfg, what = self._native_calls(ep, query=(f"/v1.0-alpha1/state/{self.store}/query", "QueryStateAlpha1"))
+        cfg.update({"query_prefix": text[:at], "query_suffix": text[at + len(json.dumps(mark)):]})
+        return {"kind": "api_list", "method": "GET", "path": "/api/tasks", "route": "/api/tasks", "cfg": cfg,
+                "what": what}
 
     async def tasks_by_creator_json(self, created_by: str) -> bytes | None:
         """``get_tasks_by_creator`` as the response body: the query's results turned into the
@@ -359,8 +381,7 @@ class TasksStoreManager(TasksManager):
         this manager's range query and log line as templates over the two values that change --
         the local midnight and the page size -- the same codec, the more-results flag; None
         outside range mode or when this client cannot take one."""
-        ep_of = getattr(self.client, "native_endpoint", None)
-        ep = ep_of() if ep_of is not None else None
+        ep = self._native_endpoint()
         if self.overdue_query != "range" or ep is None or getattr(self.client, "query_state_raw", None) is None:
             return None
         mid, page = "zqMIDNIGHTqz", 987654321
@@ -375,13 +396,12 @@ class TasksStoreManager(TasksManager):
         log_tpl = LOG_OVERDUE_PAGE
         if log_tpl.count("%s") != 1 or log_tpl.count("%d") != 1 or log_tpl.find("%s") > log_tpl.find("%d"):
             return None
+        cfg, what = self._native_calls(ep, query=(f"/v1.0-alpha1/state/{self.store}/query", "QueryStateAlpha1"))
+        cfg.update({"query": text, "query_args": args, "page_default": self.overdue_page,
+                    "log_category": log.name, "log_overdue": log_tpl.replace("%d", "%s"),
+                    "log_overdue_args": "midnight,page"})
         return {"kind": "api_overdue", "method": "GET", "path": "/api/overduetasks", "route": "/api/overduetasks",
-                "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
-                        "query_target": f"{ep['prefix']}/v1.0-alpha1/state/{self.store}/query",
-                        "query": text, "query_args": args, "page_default": self.overdue_page,
-                        "log_category": log.name, "log_overdue": log_tpl.replace("%d", "%s"),
-                        "log_overdue_args": "midnight,page"},
-                "what": {"query": f"query state {self.store}"}}
+                "cfg": cfg, "what": what}
 
     def _range_query(self, limit: int | None, midnight: str | None = None) -> tuple[dict, str, int]:
         """The open tasks due before today's midnight, oldest first: ``ORDER BY taskCreatedOn``

@@ -111,6 +111,8 @@ async def _run(a: argparse.Namespace) -> int:
             env["TT_SIDECAR_UDS"] = sock_api
         if sc.bound_grpc_port:
             env["DAPR_GRPC_PORT"] = str(sc.bound_grpc_port)
+        if sc.grpc_uds and not container:  # the co-located app's gRPC, like its HTTP, on the socket
+            env["TT_SIDECAR_GRPC_UDS"] = sc.grpc_uds
         if a.app_uds:
             env["TT_APP_UDS"] = a.app_uds
         proc = await asyncio.create_subprocess_exec(*cmd, env=env)

@@ -71,8 +71,12 @@ def parse() -> argparse.Namespace:
                     help="every Nth createTask body is due yesterday, so the sweeps mark real tasks overdue")
     ap.add_argument("--app-host", default=os.environ.get("TT_APP_HOST", "native"),
                     help="services' HTTP I/O: python (asyncio) | native (apphost.hpp) | api=native,processor=python")
-    ap.add_argument("--api-protocol", choices=("http", "grpc"), default="http",
-                    help="transport between the services and their sidecars (grpc: the reference .NET SDK's)")
+    ap.add_argument("--api-protocol", choices=("http", "grpc"), default="grpc",
+                    help="transport of the API's state and publish calls to its sidecar (grpc: the reference "
+                         ".NET DaprClient's, TasksStoreManager.cs:35,61,155; http: the sidecar's HTTP API)")
+    ap.add_argument("--alt-steps", type=int, default=-1,
+                    help="steps of config.api_protocol_alt, the headline's flow in a second environment with "
+                         "the other --api-protocol (-1 = half of --steps, 0 = skip)")
     ap.add_argument("--shared-env", action="store_true",
                     help="multi-rank: ONE partitioned environment -- every rank hosts one shard of the state store "
                          "and of the broker (backing/shards.py: documents and messages by partition-key hash, "
@@ -281,6 +285,7 @@ class OverdueSweeper:
         ms = sorted(d * 1e3 for d, _ in self.runs)
         return {"sweeps": len(self.runs), "errors": len(self.errors),
                 "sweep_p50_ms": round(ms[len(ms) // 2], 2) if ms else None,
+                "sweep_p99_ms": round(ms[min(len(ms) - 1, int(len(ms) * 0.99))], 2) if ms else None,
                 "sweep_max_ms": round(ms[-1], 2) if ms else None,
                 "sweep_ms": [round(d * 1e3, 2) for d, _ in self.runs],  # every sweep, in run order
                 "tasks_marked_overdue": sum(r.get("markedOverdue", 0) for _, r in self.runs),
@@ -856,6 +861,78 @@ def _sidecar_counter(uds: str, op: str) -> int:
     return total
 
 
+WIRE_OPS = ("grpc.SaveState", "grpc.PublishEvent", "grpc.QueryStateAlpha1", "state.save", "publish", "state.query")
+
+
+def _api_wire(env) -> dict[str, int]:
+    """The API sidecars' data-plane counters of the calls that carry a task: gRPC RPCs
+    (``grpc.*``) and the HTTP API operations they run as (``state.save`` / ``publish`` count
+    both protocols)."""
+    socks = [r.sidecar_uds for r in env.replicas(API)]
+    return {op: sum(_sidecar_counter(u, op) for u in socks) for op in WIRE_OPS}
+
+
+def _wire_delta(w0: dict, w1: dict) -> dict:
+    return {k: w1.get(k, 0) - w0.get(k, 0) for k in WIRE_OPS}
+
+
+def protocol_alt(a: argparse.Namespace, overrides: dict, exe: str, root: str, steps: int, conc: int,
+                 rank: int) -> dict:
+    """The headline's createTask flow with the API's OTHER Dapr protocol (gRPC <-> HTTP), in a
+    fresh environment of the same manifest, replicas and CPU caps (no sweep): tasks/s, create
+    latency, CPU per task, and the wire counters that show which API carried the calls."""
+    import psutil
+
+    from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
+    from aca_dotnet_workshop_amd.platform.manifest import load_manifest
+    proto = "http" if a.api_protocol == "grpc" else "grpc"
+    ov = dict(overrides, backendApiDaprApiProtocol=proto, overdueQuery="equality", overduePageSize=0,
+              environmentName=f"cae-alt-r{rank}")
+    m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"), ov)
+    env = BackgroundEnvironment(m, os.path.join(root, "alt"), log_level="warning")
+    try:
+        env.start()
+        ca_file = None
+        if a.ingress != "bypass":
+            ca_file = str(env.ctl.pki.ca_crt)
+            targets = [f"https://127.0.0.1:{env.ctl.apps[FRONTEND].ingress.public_port}"]
+            session_url = targets[0]
+        else:
+            targets = [f"127.0.0.1:{r.app_port}" for r in env.replicas(FRONTEND)]
+            session_url = f"http://127.0.0.1:{env.replicas(FRONTEND)[0].app_port}"
+        counts = [f"{env.backing_url}/servicebus/taskstracker/counts?entity=tasksavedtopic/subscriptions/{PROC}"]
+        cookie, token = _form_session(session_url, "alt@bench.local", ca_file)
+        bodies = os.path.join(root, "alt-bodies.txt")
+        with open(bodies, "wb") as f:
+            f.write(b"\n".join(_form_bodies(a.batch, token, 0)) + b"\n")
+        run_form_loadgen(exe, targets, cookie, counts, 2, a.batch, conc, bodies, None, ca_file, a.loadgen_threads)
+        me = psutil.Process()
+        cpu0 = _cpu_by_role(env.stack)
+        t = me.cpu_times()
+        cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
+        cpu0.update(_ingress_cpu(env))
+        w0 = _api_wire(env)
+        dt, rep = run_form_loadgen(exe, targets, cookie, counts, steps, a.batch, conc, bodies, None, ca_file,
+                                   a.loadgen_threads)
+        w1 = _api_wire(env)
+        cpu1 = _cpu_by_role(env.stack)
+        t = me.cpu_times()
+        cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
+        cpu1.update(_ingress_cpu(env))
+        busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}
+        cpu_us = cpu_per_task(busy, a.batch * steps / dt)
+        return {"api_protocol": proto, "value": round(a.batch * steps / dt, 1), "steps": steps,
+                "create_latency_p50_ms": rep["latency_ms"]["p50"], "create_latency_p99_ms": rep["latency_ms"]["p99"],
+                "cpu_us_per_task": {"total": cpu_us.get("total"),
+                                    **{k.replace("tasksmanager-backend-", ""): v
+                                       for k, v in (cpu_us.get("by_role") or {}).items() if k.startswith(API)}},
+                "api_wire": _wire_delta(w0, w1), "errors": rep.get("errors")}
+    except Exception as e:  # reported, not fatal to the headline
+        return {"api_protocol": proto, "error": repr(e)[:300]}
+    finally:
+        env.stop()
+
+
 def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
     """The reference's own capacity envelope, measured (BASELINE.md "Configured capacity"):
     ``deploy/main.yaml`` with its defaults -- frontend and API at 1..1 replica, the processor at
@@ -934,9 +1011,6 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 **_throttle_detail(st0, st1),
                 "tasks_per_s_over_budget_rate": (round(tasks / el / (float(st1.get("ru_per_s", 0.0)) / (ru / tasks)), 3)
                                                  if tasks and ru and el and st1.get("ru_per_s") else None),
-                "note": "a throttled store call gets a reserved slot (429 + x-ms-retry-after-ms + ticket) and the "
-                        "sidecar retries there (the Cosmos SDK policy: 9 retries, 30 s); one still throttled after "
-                        "that answers 500, as the reference's pages would",
                 "keda_polling_s": 5, "loadgen_exit": p.returncode}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:500]}
@@ -1045,14 +1119,40 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
                                 and delta["dead_letter"] == 0,
                 "rule": "azure-servicebus, messageCount 10, replicas 1..5 (processor-backend-service.bicep:159-183)",
                 "work_per_message_ms": 1000, "keda_polling_s": polling_s, "keda_cooldown_s": cooldown_s,
-                "note": "reference: 10,000 messages at 1 ms intervals, 1 s simulated work, expects 5 replicas "
-                        "(docs/aca/09-aca-autoscale-keda/index.md:192-216); polling 30 s and cooldown 300 s "
-                        "shortened so the cycle fits the run"}
+                "reference": "docs/aca/09-aca-autoscale-keda/index.md:192-216 (30 s polling / 300 s cooldown)"}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:500], "replica_timeline": samples[-20:]}
     finally:
         stop.set()
         env.stop()
+
+
+def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
+                   protocol: str, wire: dict, alt: dict | None) -> dict:
+    """The record's key facts in one small object at the head of ``config`` (the driver keeps
+    the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
+    flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
+    s: dict = {"tasks_per_s": round(value, 1), "api_protocol": protocol,
+               "api_grpc_calls_per_task": None, "cpu_us_per_task": cpu_us.get("total"),
+               "cpu_us_per_task_by_role": {k.replace("tasksmanager-", "").replace("backend-", ""): v
+                                           for k, v in (cpu_us.get("by_role") or {}).items()}}
+    if wire.get("state.save"):
+        s["api_grpc_calls_per_task"] = round((wire.get("grpc.SaveState", 0) + wire.get("grpc.PublishEvent", 0))
+                                             / wire["state.save"], 2)
+    if sweep:
+        s["sweep"] = {k: sweep.get(k) for k in ("sweeps", "sweep_p50_ms", "sweep_p99_ms", "sweep_max_ms",
+                                                  "tasks_marked_overdue", "errors")}
+    if browser:
+        s["browser_flows_per_s"] = browser.get("flows_per_s")
+    if alt:
+        s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
+                                 if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
+    if envelope:
+        s["envelope"] = {k: envelope.get(k) for k in ("tasks_per_s", "errors", "tasks_per_s_over_budget_rate",
+                                                       "store_429s_per_task", "store_429s_per_call")}
+        k = envelope.get("keda") or {}
+        s["keda"] = {x: k.get(x) for x in ("peak_replicas", "time_to_peak_s", "exactly_once")}
+    return s
 
 
 def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
@@ -1107,7 +1207,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                  "backendApiCpu": caps["api"], "processorCpu": caps["processor"], "appMemory": "2Gi",
                  "appInsightsSamplingPercentage": a.trace_sampling,
                  "overdueQuery": "range" if sweep else "equality", "overduePageSize": OVERDUE_PAGE if sweep else 0,
-                 "overdueMarkChunk": a.mark_chunk,
+                 "overdueMarkChunk": a.mark_chunk, "backendApiDaprApiProtocol": a.api_protocol,
                  "environmentName": f"cae-bench-r{d.rank}"}
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
                       overrides)
@@ -1164,6 +1264,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         duty0 = env.ctl.limiter.duty_stats()
         ru0 = _collection_stats(backing).get("throughput", {})
         acc0 = _accel_stats(shards) if sweeper is not None else {}
+        wire0 = _api_wire(env)
         if sweeper is not None:
             sweeper.reset()  # sweeps of the timed region only
         dt, report = run_form_loadgen(exe, targets, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
@@ -1173,12 +1274,13 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         d.barrier()
         if sweeper is not None:
             sweeper.stop()
+        wire = _wire_delta(wire0, _api_wire(env))
         cpu1 = _cpu_by_role(env.stack)
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
         th1 = env.stack.thread_cpu(_ingress_pid(env))
-        hot = hot_threads(th0, th1, dt)
+        hot = hot_threads(th0, th1, dt, top=8)
         # every thread that did work in the timed region: the stderr diagnostics line only
         threads_all = [t for t in hot_threads(th0, th1, dt, top=200) if t[2] >= 0.005]
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
@@ -1237,8 +1339,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                        "lists": brep.get("follow_requests"), "status_counts": sc, "errors": brep.get("errors"),
                        "first_error": brep.get("first_error") or None,
                        "tasks_per_user_at_end": round(a.batch * bsteps / BROWSER_USERS, 1),
-                       "note": "POST /Tasks/Create (302) then GET /Tasks/Index with the user's cookie: the API "
-                               "queries the store by creator, newest first; one flow = both pages"}
+                       "flow": "POST /Tasks/Create (302) + GET /Tasks/Index"}
         # the same environment, load straight at the API sidecars' invoke (round 2's topology);
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
@@ -1255,13 +1356,23 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             direct = {"value": round(a.batch * dsteps * (d.world if d.world > 1 else 1) / ddt, 2), "steps": dsteps,
                       "create_latency_p50_ms": drep["latency_ms"]["p50"], "create_latency_p99_ms": drep["latency_ms"]["p99"],
                       "note": "same environment, load at the API sidecars' invoke (no frontend, no mTLS hop)"}
+        trace = None
         if sweep_info is not None:  # span exporters flush at least once a second
             if not dsteps:
                 time.sleep(1.5)
-            sweep_info["trace"] = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids, sweeper.slowest_trace())
-        envelope = None
-        if a.envelope_s > 0 and not shared:  # after the headline's environment is down
+            trace = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids, sweeper.slowest_trace())
+            # the record keeps the sweep's largest hops; every span goes to the stderr diagnostics
+            spans = (trace or {}).get("spans_p50_ms") or {}
+            sweep_info["trace_top_spans_p50_ms"] = dict(sorted(spans.items(), key=lambda kv: -kv[1])[:4])
+        envelope = alt = None
+        asteps = 0 if shared else a.alt_steps if a.alt_steps >= 0 else max(2, a.steps // 2)
+        if (a.envelope_s > 0 or asteps) and not shared:  # after the headline's environment is down
             env.stop()
+        if asteps:
+            progress(f"api_protocol_alt: {asteps} steps with the other Dapr protocol")
+            alt = protocol_alt(a, overrides, exe, root, asteps, conc, d.rank)
+            progress("api_protocol_alt done")
+        if a.envelope_s > 0 and not shared:
             if d.rank == 0:
                 progress(f"reference envelope: {a.envelope_s:g} s")
                 envelope = reference_envelope(exe, root, a.envelope_s, d.rank)
@@ -1282,15 +1393,18 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             print(json.dumps({"cpu_cores_busy": util, "total_cores_busy": round(sum(util.values()), 2),
                               "cpu_us_per_task": cpu_us,
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
-                              "overdue_sweeps": sweep_info, "resource_limits": lim,
+                              "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "threads": threads_all}), file=sys.stderr, flush=True)
+            summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "n/a (JSON over HTTP)",
                 "data": "synthetic createTask form posts",
-                "config": {"model": "tasks-tracker createTask flow, SURVEY §3.1 (frontend -> mTLS -> API -> store + "
+                "config": {"summary": summary,
+                           "model": "tasks-tracker createTask flow, SURVEY §3.1 (frontend -> mTLS -> API -> store + "
                                     "publish -> processor ack)",
+                           "api_protocol": a.api_protocol, "api_wire": wire,
                            "global_batch": a.batch * (d.world if d.world > 1 else 1), "seq_len": None,
                            "parallelism": (f"shared-env x{d.world} (store and broker partitioned over {len(shards)} "
                                            f"shards, one per rank; {proc * d.world} competing processor replicas)"
@@ -1302,7 +1416,6 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "ingress": (f"external HTTPS ({a.ingress}), {os.environ.get('TT_INGRESS_THREADS')} event "
                                        "loops, certificate verified against the environment CA"
                                        if ingress else "bypassed: the load generator balances over the frontend replicas"),
-                           "cpu_us_per_task": cpu_us,
                            "hot_threads": hot,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
@@ -1319,7 +1432,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
                            "overdue_sweeps": sweep_info, "browser_flow": browser, "api_sidecar_direct": direct,
-                           "reference_envelope": envelope}}), flush=True)
+                           "api_protocol_alt": alt, "reference_envelope": envelope}}), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():
             sweeper.stop()

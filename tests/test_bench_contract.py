@@ -44,9 +44,21 @@ def test_bench_single_process():
     cfg = lines[0]["config"]
     # load enters at the frontend's external HTTPS ingress (native data plane), like a browser's
     assert cfg["entry"] == "frontend" and cfg["ingress"].startswith("external HTTPS (native)")
-    cpu = cfg["cpu_us_per_task"]
+    # the record's key facts lead config (the driver keeps the line's head), and the line stays small
+    assert list(cfg)[0] == "summary" and len(r.stdout.strip().splitlines()[-1]) < 9000
+    sm = cfg["summary"]
     # /proc counts CPU in 10 ms ticks: over this run's ~64 timed tasks a cheap role can read 0
-    assert cpu["total"] > 0 and cpu["by_role"]["ingress"] >= 0 and cpu["apps_frontend_plus_api"] >= 0
+    assert sm["cpu_us_per_task"] > 0 and sm["cpu_us_per_task_by_role"]["ingress"] >= 0
+    assert set(sm["sweep"]) >= {"sweeps", "sweep_p50_ms", "sweep_p99_ms", "sweep_max_ms"}
+    # the reference SDK's wire: every task's save and publish went over the sidecar's gRPC API
+    assert cfg["api_protocol"] == sm["api_protocol"] == "grpc"
+    w = cfg["api_wire"]
+    # (a sweep inside the timed region adds its markoverdue saves, over gRPC too)
+    assert w["grpc.PublishEvent"] == w["publish"] == 64 and w["grpc.SaveState"] == w["state.save"] >= 64
+    # the same flow with the other protocol, in its own environment: HTTP, no gRPC call
+    alt = cfg["api_protocol_alt"]
+    assert alt["api_protocol"] == "http" and alt["value"] > 0 and alt["api_wire"]["grpc.SaveState"] == 0
+    assert alt["api_wire"]["state.save"] == 32 * alt["steps"]
     sw = cfg["overdue_sweeps"]
     assert len(sw["sweep_ms"]) == sw["sweeps"] and max(sw["sweep_ms"], default=0) == (sw["sweep_max_ms"] or 0)
     assert sw["page_size"] == 4096
