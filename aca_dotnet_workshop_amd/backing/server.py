@@ -267,10 +267,15 @@ class BackingServices:
             p = req.path_params
             return self.accel(p["account"], p["db"], p["coll"])
 
-        def throttled(req: Request, s, ru: float) -> Response | None:
+        def throttled(req: Request, s, ru: float, kind: int = 1) -> Response | None:
             """Provisioned-throughput admission (DocStore.charge, shared with the native front):
-            a 429 reserves the caller's slot and hands out its ticket (x-tt-ru-ticket)."""
-            wait_ms, ticket = s.charge(ru, int(req.headers.get("x-tt-ru-ticket") or 0))
+            a 429 reserves the caller's slot -- bound to the request: method + target, plus the
+            body of a query or a bulk / transactional write -- and hands out its ticket
+            (x-tt-ru-ticket).  ``kind``: 0 read, 1 write, 2 query, 3 delete."""
+            bind = f"{req.method} {req.target}"
+            if kind == 2 or req.method == "POST":
+                bind += "\xff" + req.body.decode("utf-8", "replace")
+            wait_ms, ticket = s.charge(ru, int(req.headers.get("x-tt-ru-ticket") or 0), bind, kind)
             if not wait_ms:
                 return None
             r = problem(429, detail="Request rate is large: the container's provisioned throughput is exhausted")
@@ -296,7 +301,7 @@ class BackingServices:
 
         async def get_doc(req: Request) -> Response:
             s = st(req, "cosmos.read")
-            if (t := throttled(req, s, s.read_ru(0))) is not None:
+            if (t := throttled(req, s, s.read_ru(0), 0)) is not None:
                 return t
             r = s.get(req.path_params["key"])
             if r is None:
@@ -305,7 +310,7 @@ class BackingServices:
 
         async def del_doc(req: Request) -> Response:
             s = st(req, "cosmos.write")
-            if (t := throttled(req, s, s.write_ru(0))) is not None:
+            if (t := throttled(req, s, s.write_ru(0), 3)) is not None:
                 return t
             try:
                 ok = s.delete(req.path_params["key"], req.headers.get("if-match") or None)
@@ -316,7 +321,7 @@ class BackingServices:
         async def bulk_get(req: Request) -> Response:
             s = st(req, "cosmos.read")
             keys = (req.json() or {}).get("keys", [])
-            if (t := throttled(req, s, s.read_ru(0) * max(1, len(keys)))) is not None:
+            if (t := throttled(req, s, s.read_ru(0) * max(1, len(keys)), 0)) is not None:
                 return t
             out = []
             for k in keys:
@@ -354,7 +359,7 @@ class BackingServices:
             # ?project=sortkeys: {"key", "etag", "sort"} per result -- phase one of a
             # cross-partition page (the sidecar fetches the merged page's documents after)
             sort_keys = (req.query_get("project", "") or "").lower() == "sortkeys"
-            if (t := throttled(req, s, s.query_ru(0))) is not None:
+            if (t := throttled(req, s, s.query_ru(0), 2)) is not None:
                 return t
             p = req.path_params
             status, body, headers = await asyncio.get_running_loop().run_in_executor(

@@ -51,11 +51,12 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 
 #include "evhttp.hpp"
 #include "formcodec.hpp"
+#include "daprpb.hpp"
 #include "h2.hpp"
-#include "pb.hpp"
 #include "taskcodec.hpp"
 #include "textutil.hpp"
 
@@ -257,7 +258,10 @@ inline bool cookie_value(std::string_view cookie, std::string_view name, std::st
 
 // A route the loop thread serves itself (AppHost::add_route).
 struct NativeRoute {
-  enum Kind { kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6 };
+  enum Kind {
+    kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6,
+    kApiMarkOverdue = 7
+  };
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -292,6 +296,12 @@ struct NativeRoute {
   // midnight, the page size) -> the TaskModel page oldest first + whether the store has more
   Template overdue_query, log_overdue;
   std::string page_default, more_header;
+  // kApiMarkOverdue: POST api/overduetasks/markoverdue -> bulk get of the page's ids -> the
+  // conditional mark (taskcodec conditional_mark) -> one log line per marked task -> ETag-guarded
+  // bulk save, re-read and re-applied on a conflict (up to max_retries passes) -> 200
+  std::string bulk_target;
+  Template log_mark;
+  int max_retries = 5, parallelism = 10;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -502,6 +512,7 @@ class AppHost {
     else if (kind == "frontend_list") r->kind = NativeRoute::kFrontendList;
     else if (kind == "api_list") r->kind = NativeRoute::kApiList;
     else if (kind == "api_overdue") r->kind = NativeRoute::kApiOverdue;
+    else if (kind == "api_markoverdue") r->kind = NativeRoute::kApiMarkOverdue;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -519,7 +530,8 @@ class AppHost {
     r->log_prefix = get("log_prefix");
     r->bounds = bounds;
     if (get("protocol") == "grpc") {
-      if (r->kind != NativeRoute::kApiCreate && r->kind != NativeRoute::kApiList && r->kind != NativeRoute::kApiOverdue)
+      if (r->kind != NativeRoute::kApiCreate && r->kind != NativeRoute::kApiList && r->kind != NativeRoute::kApiOverdue &&
+          r->kind != NativeRoute::kApiMarkOverdue)
         throw std::invalid_argument("only the API's store routes speak gRPC");
       r->grpc = true;
       r->store = get("store");
@@ -554,6 +566,14 @@ class AppHost {
       if (r->query_target.empty() || get("query").empty() || r->page_default.empty() || r->more_header.empty() ||
           get("log_overdue").empty())
         throw std::invalid_argument("api_overdue needs its query, page size, log template and header");
+    } else if (r->kind == NativeRoute::kApiMarkOverdue) {
+      r->bulk_target = get("bulk_target");
+      r->log_mark = Template::compile(get("log_mark"), get("log_mark_args"), {"id"});
+      if (!get("max_retries").empty()) r->max_retries = std::stoi(get("max_retries"));
+      if (!get("parallelism").empty()) r->parallelism = std::stoi(get("parallelism"));
+      if (r->bulk_target.empty() || r->save_target.empty() || get("log_mark").empty() ||
+          (!r->grpc && r->store.empty() && false))
+        throw std::invalid_argument("api_markoverdue needs its bulk-get and save targets and its log template");
     } else if (r->kind == NativeRoute::kApiList) {
       r->query_target = get("query_target");
       r->query_prefix = get("query_prefix");
@@ -733,6 +753,8 @@ class AppHost {
     std::string trace_id, span_id, traceparent;
     ev::HeaderList out_headers;  // traceparent, token, content-type: the SDK's unsampled call
     ev::HeaderList grpc_md;      // gRPC routes: traceparent, token (the SDK's call metadata)
+    std::vector<std::string> pending;  // kApiMarkOverdue: the ids this pass reads
+    int pass = 0;
     ::taskcodec::Created task;
   };
 
@@ -886,18 +908,73 @@ class AppHost {
     log_event(r, *j, r.log_overdue.render_with(value));
     native_inflight_.fetch_add(1);
     std::string q = r.overdue_query.render_with(value);
-    if (r.grpc) q = pb_query_state(r.store, q);
+    if (r.grpc) q = daprpb::query_state(r.store, q);
     // the query may take milliseconds (a GPU scan): an ordinary connection, not a pipelined one
     call_step(j, "query", r.query_target, std::move(q), false, [this, j](std::string&& body) {
       const NativeRoute& r = *j->route;
       std::string json, out;
-      if (r.grpc && !query_response_json(body, json)) return decline(*j);
+      if (r.grpc && !daprpb::query_response_json(body, json)) return decline(*j);
       size_t count = 0;
       bool more = false;
       if (!::taskcodec::query_tasks(r.grpc ? json : body, out, count, true, &more, false)) return decline(*j);
       finish(*j, r.status, {{"Content-Type", r.content_type}, {r.more_header, more ? "true" : "false"}}, out);
     });
     return true;
+  }
+
+  // kApiMarkOverdue (services/backend_api/app.py mark_overdue + TasksStoreManager
+  // mark_overdue_from_body / _mark_conditionally): the page's ids from the native binder, then
+  // the conditional mark pass -- the same bulk get, codec, log lines and ETag-guarded bulk save.
+  bool api_markoverdue(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const std::string ctype = media_type(m);
+    if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
+    std::vector<std::string> ids;
+    std::string unused;
+    if (!::taskcodec::mark_overdue(m.body, ids, unused)) return false;  // the general binder's
+    std::unordered_set<std::string> seen;
+    for (auto& id : ids)
+      if (seen.insert(id).second) j->pending.push_back(id);  // dict.fromkeys: first occurrence
+    native_inflight_.fetch_add(1);
+    // the first pass starts once the request is the job's (serve_native moves it in on return)
+    loop_.defer([this, j] { mark_pass(j); });
+    return true;
+  }
+  void mark_pass(const std::shared_ptr<NativeJob>& j) {
+    const NativeRoute& r = *j->route;
+    if (j->pending.empty()) return finish(*j, r.status, {});
+    if (j->pass++ >= r.max_retries) return decline(*j);  // kept conflicting: Python's ConcurrencyConflict
+    std::string body;
+    if (r.grpc) {
+      body = daprpb::get_bulk_state(r.store, j->pending, r.parallelism);
+    } else {  // sdk/client.py get_bulk_state_raw: {"keys":[..],"parallelism":N}, compact
+      body = "{\"keys\":[";
+      for (size_t i = 0; i < j->pending.size(); ++i) {
+        if (i) body += ',';
+        tt::escape_to(body, j->pending[i]);
+      }
+      body += "],\"parallelism\":" + std::to_string(r.parallelism) + "}";
+    }
+    call_step(j, "bulk", r.bulk_target, std::move(body), false, [this, j](std::string&& got) {
+      const NativeRoute& r = *j->route;
+      std::string json, bulk;
+      if (r.grpc && !daprpb::bulk_state_response_json(got, json)) return decline(*j);
+      std::vector<std::string> marked;
+      size_t skipped = 0;
+      if (!::taskcodec::conditional_mark(r.grpc ? json : got, bulk, marked, skipped)) return decline(*j);
+      for (auto& id : marked) log_event(r, *j, r.log_mark.render_with([&](int) -> const std::string& { return id; }));
+      if (marked.empty()) return finish(*j, r.status, {});
+      std::string save;
+      if (r.grpc && !daprpb::save_state_bulk(r.store, bulk, save)) return decline(*j);
+      j->pending = std::move(marked);
+      call_step(
+          j, "save", r.save_target, r.grpc ? std::move(save) : std::move(bulk), false,
+          [this, j](std::string&&) { finish(*j, j->route->status, {}); },
+          [this, j](int status) {  // lost a race on some of them: re-read and re-apply
+            if (status != 409 && status != 412) return false;
+            mark_pass(j);
+            return true;
+          });
+    });
   }
 
   // kApiList (services/backend_api/app.py get_tasks + TasksStoreManager.tasks_by_creator_json)
@@ -909,11 +986,11 @@ class AppHost {
     tt::escape_to(body, who);
     body += r.query_suffix;
     native_inflight_.fetch_add(1);
-    if (r.grpc) body = pb_query_state(r.store, body);
+    if (r.grpc) body = daprpb::query_state(r.store, body);
     call_step(j, "query", r.query_target, std::move(body), false, [this, j](std::string&& res) {
       const NativeRoute& r = *j->route;
       std::string json, out;
-      if (r.grpc && !query_response_json(res, json)) return decline(*j);
+      if (r.grpc && !daprpb::query_response_json(res, json)) return decline(*j);
       size_t count = 0;
       bool more = false;
       if (!::taskcodec::query_tasks(r.grpc ? json : res, out, count, true, &more, true)) return decline(*j);
@@ -999,7 +1076,7 @@ class AppHost {
     }
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
     if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList ||
-        r->kind == NativeRoute::kApiOverdue) {
+        r->kind == NativeRoute::kApiOverdue || r->kind == NativeRoute::kApiMarkOverdue) {
       auto j = std::make_shared<NativeJob>();
       j->route = r;
       j->server = server;
@@ -1013,7 +1090,8 @@ class AppHost {
       if (r->grpc) grpc_metadata(*j);
       bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m)
                    : r->kind == NativeRoute::kApiList    ? api_list(j, m)
-                                                         : api_overdue(j, m);
+                   : r->kind == NativeRoute::kApiOverdue ? api_overdue(j, m)
+                                                         : api_markoverdue(j, m);
       if (!taken) return false;
       j->req = std::move(m);
       j->reply = std::move(reply);
@@ -1064,13 +1142,13 @@ class AppHost {
     // encode_save_state); HTTP: the state API's body.  The save takes an ordinary connection:
     // the sidecar may hold it for seconds through the store's 429 retries, and a pipelined
     // connection would hold every answer queued behind it
-    std::string save = r->grpc ? pb_save_state(r->store, j->task.id, j->task.task_json) : std::move(j->task.state_body);
+    std::string save = r->grpc ? daprpb::save_state(r->store, j->task.id, j->task.task_json) : std::move(j->task.state_body);
     call_step(j, "save", r->save_target, std::move(save), false, [this, j](std::string&&) {
       const NativeRoute& r = *j->route;
       log_event(r, *j, r.log_publish.render(j->task.id, j->task.name, j->task.assigned_to));
       // the publishes ride the pipelined connections (ev::PipeConn): the broker answers at once,
       // and the creates of one loop iteration share a send(2) and the sidecar's answers a read
-      std::string pub = r.grpc ? pb_publish_event(r.pubsub, r.topic, j->task.task_json, "application/json")
+      std::string pub = r.grpc ? daprpb::publish_event(r.pubsub, r.topic, j->task.task_json, "application/json")
                                : j->task.task_json;
       call_step(j, "publish", r.publish_target, std::move(pub), true, [this, j](std::string&&) {
         const NativeRoute& r2 = *j->route;
@@ -1081,96 +1159,27 @@ class AppHost {
   }
 
   // -- the route's sidecar calls, over its protocol -----------------------------------------
-  // proto3 messages of dapr.proto.runtime.v1 (field numbers: sdk/proto.py), written the way
-  // sdk/grpc_client.py writes them, byte for byte
-  static std::string pb_save_state(std::string_view store, std::string_view key, std::string_view value) {
-    pb::Writer item, w;
-    item.len_field(1, key);
-    item.len_field(2, value);
-    w.len_field(1, store);
-    w.len_field(2, item.s);
-    return w.s;
-  }
-  static std::string pb_publish_event(std::string_view pubsub, std::string_view topic, std::string_view data,
-                                      std::string_view ctype) {
-    pb::Writer w;
-    w.len_field(1, pubsub);
-    w.len_field(2, topic);
-    w.len_field(3, data);
-    w.len_field(4, ctype);
-    return w.s;
-  }
-  static std::string pb_query_state(std::string_view store, std::string_view query) {
-    pb::Writer w;  // QueryStateRequest {store_name = 1, query = 2}, as message.SerializeToString
-    w.str(1, store);
-    w.str(2, query);
-    return w.s;
-  }
-  // QueryStateResponse {results = 1 {key, data, etag, error}, token = 2} as the state query
-  // API's JSON answer ({"results":[{"key","data","etag"}],"token"}), the text the task codec
-  // reads; false when an item's data is not JSON (the page is then Python's).
-  static bool query_response_json(std::string_view msg, std::string& out) {
-    pb::Reader rd(msg);
-    uint32_t f, wt;
-    std::string_view v, token;
-    out.assign("{\"results\":[");
-    bool first = true;
-    while (rd.next(f, wt)) {
-      if (f == 1 && wt == pb::LEN && rd.bytes(v)) {
-        pb::Reader ir(v);
-        uint32_t g, gwt;
-        std::string_view x, key, data, etag;
-        while (ir.next(g, gwt)) {
-          if (g == 1 && gwt == pb::LEN && ir.bytes(x)) key = x;
-          else if (g == 2 && gwt == pb::LEN && ir.bytes(x)) data = x;
-          else if (g == 3 && gwt == pb::LEN && ir.bytes(x)) etag = x;
-          else if (!ir.skip(gwt)) break;
-        }
-        if (!ir.ok) return false;
-        if (!data.empty() && !tt::valid(data)) return false;
-        if (!first) out += ',';
-        first = false;
-        out += "{\"key\":";
-        tt::escape_to(out, key);
-        out += ",\"data\":";
-        if (data.empty()) out += "null";
-        else out.append(data);
-        out += ",\"etag\":";
-        tt::escape_to(out, etag);
-        out += '}';
-      } else if (f == 2 && wt == pb::LEN && rd.bytes(v)) {
-        token = v;
-      } else if (!rd.skip(wt)) {
-        break;
-      }
-    }
-    if (!rd.ok) return false;
-    out += ']';
-    if (!token.empty()) {
-      out += ",\"token\":";
-      tt::escape_to(out, token);
-    }
-    out += '}';
-    return true;
-  }
-
   // One sidecar call of a native route: `target` is the HTTP API's path, or the RPC's :path
   // for a gRPC route (`body` its request message).  `done` gets the answer's body (HTTP) or the
   // response message (gRPC); a failure hands the request to Python with the step's result.
   // `pipelined`: an HTTP call that answers at once may share a pipelined connection.
+  // `conflict` (optional): offered the HTTP status of a failed call first; true = it handled it.
   using StepDone = std::function<void(std::string&&)>;
+  using StepConflict = std::function<bool(int)>;
   void call_step(const std::shared_ptr<NativeJob>& j, const char* step, const std::string& target, std::string body,
-                 bool pipelined, StepDone done) {
+                 bool pipelined, StepDone done, StepConflict conflict = nullptr) {
     const NativeRoute& r = *j->route;
     if (r.grpc) {
       grpc_.call(r.sidecar, target, j->grpc_md, body, r.timeout_s,
-                 [this, j, step, done = std::move(done)](h2::GrpcResult&& res) {
+                 [this, j, step, done = std::move(done), conflict = std::move(conflict)](h2::GrpcResult&& res) {
+                   if (!res.err && res.status != 0 && conflict && conflict(grpc_http_status(res))) return;
                    if (res.err || res.status != 0) return grpc_hand_over(*j, step, res);
                    done(std::move(res.payload));
                  });
       return;
     }
-    auto cb = [this, j, step, done = std::move(done)](ev::ClientResult&& res) {
+    auto cb = [this, j, step, done = std::move(done), conflict = std::move(conflict)](ev::ClientResult&& res) {
+      if (!res.err && res.resp.status >= 300 && conflict && conflict(res.resp.status)) return;
       if (res.err || res.resp.status >= 300) return hand_over(*j, step, res);
       done(std::move(res.resp.body));
     };
@@ -1182,27 +1191,31 @@ class AppHost {
   // dapr-http-status, else the gRPC code's HTTP equivalent: sdk/grpc_client.py _HTTP_OF) and
   // grpc-message as its body; transport errors go over as errno (sdk.client.native_route_failure
   // turns them into the SDK's 503 / 504).
+  static int grpc_http_status(const h2::GrpcResult& res) {
+    int http = 500;
+    switch (res.status) {
+      case 3: http = 400; break;
+      case 16: http = 401; break;
+      case 7: http = 403; break;
+      case 5: http = 404; break;
+      case 10: http = 409; break;
+      case 8: http = 429; break;
+      case 12: http = 501; break;
+      case 14: http = 503; break;
+      case 4: http = 504; break;
+      default: break;
+    }
+    for (auto& kv : res.metadata)
+      if (kv.first == "dapr-http-status") http = std::atoi(kv.second.c_str());
+    return http;
+  }
   void grpc_hand_over(NativeJob& j, const char* step, const h2::GrpcResult& res) {
     std::string note;
     if (res.err) {
       note = std::string("err ") + step + " " + std::to_string(res.err);
     } else {
-      int http = 500;
-      switch (res.status) {
-        case 3: http = 400; break;
-        case 16: http = 401; break;
-        case 7: http = 403; break;
-        case 5: http = 404; break;
-        case 10: http = 409; break;
-        case 8: http = 429; break;
-        case 12: http = 501; break;
-        case 14: http = 503; break;
-        case 4: http = 504; break;
-        default: break;
-      }
-      for (auto& kv : res.metadata)
-        if (kv.first == "dapr-http-status") http = std::atoi(kv.second.c_str());
-      note = std::string("fail ") + step + " " + std::to_string(http) + " " + tt::text::base64(res.message);
+      note = std::string("fail ") + step + " " + std::to_string(grpc_http_status(res)) + " " +
+             tt::text::base64(res.message);
     }
     j.req.headers.emplace_back("x-tt-native", std::move(note));
     to_python(j.server, std::move(j.req), std::move(j.reply));

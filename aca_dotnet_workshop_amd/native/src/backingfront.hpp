@@ -573,10 +573,19 @@ class BackingFront {
   // container's RU/s budget is spent, as Cosmos answers; the sidecars retry after the hint.
   // The 429 carries the reservation's ticket (x-tt-ru-ticket); a retry presenting it is admitted
   // at its slot without a second charge (DocStore::charge).
-  bool throttled(ev::Message& m, ev::Reply& r, DocStore* s, double ru) {
+  // `kind`: what the call is for (DocStore::Kind, the throttled-call breakdown); the reservation
+  // is bound to the request: method + target, plus the body of a query or a bulk write.
+  bool throttled(ev::Message& m, ev::Reply& r, DocStore* s, double ru, int kind) {
+    if (!s->provisioned()) {  // unlimited: metered only
+      s->charge(ru);
+      return false;
+    }
     uint64_t ticket = 0, out = 0;
     if (const std::string* t = m.header("x-tt-ru-ticket")) ticket = std::strtoull(t->c_str(), nullptr, 10);
-    int64_t wait_ms = s->charge(ru, ticket, out);
+    const uint64_t bind = DocStore::bind_of(m.method + " " + m.target,
+                                            kind == DocStore::kQuery || m.method == "POST" ? std::string_view(m.body)
+                                                                                           : std::string_view());
+    int64_t wait_ms = s->charge(ru, ticket, out, bind, kind);
     if (!wait_ms) return false;
     count("doc.throttled");
     ev::HeaderList h{{"x-ms-retry-after-ms", std::to_string(wait_ms)},
@@ -610,7 +619,7 @@ class BackingFront {
     if (m.method == "GET") {
       if (!authorize(m, r, "cosmos.read", scope)) return true;
       count("doc.get");
-      if (throttled(m, r, c->store, DocStore::read_ru(0))) return true;
+      if (throttled(m, r, c->store, DocStore::read_ru(0), DocStore::kRead)) return true;
       auto v = c->store->get(key);
       if (!v) r.empty(404);
       else r.send(200, {{"etag", v->second}, {"content-type", "application/json"}}, v->first);
@@ -624,7 +633,9 @@ class BackingFront {
     std::optional<std::string> etag;
     if (im && !im->empty()) etag = *im;
     const char* pj = "application/problem+json; charset=utf-8";
-    if (throttled(m, r, c->store, DocStore::write_ru(m.method == "PUT" ? m.body.size() : 0))) return true;
+    if (throttled(m, r, c->store, DocStore::write_ru(m.method == "PUT" ? m.body.size() : 0),
+                  m.method == "PUT" ? DocStore::kWrite : DocStore::kDelete))
+      return true;
     if (m.method == "PUT") {
       count("doc.put");
       auto* fw = m.header("x-tt-first-write");
@@ -658,7 +669,7 @@ class BackingFront {
     count("doc.bulkset");
     double ru = 0;
     for (auto& b : batch) ru += DocStore::write_ru(b.value.size());
-    if (throttled(m, r, c->store, ru)) return true;
+    if (throttled(m, r, c->store, ru, DocStore::kWrite)) return true;
     const std::vector<DocStore::BulkResult> res = c->store->set_many(batch);
     std::string out = "[";
     bool etag_err = false, other_err = false;
@@ -695,7 +706,8 @@ class BackingFront {
       if (k.t != Value::String) return false;
     if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
     count("doc.bulkget");
-    if (throttled(m, r, c->store, DocStore::read_ru(0) * (double)std::max<size_t>(1, keys->items.size()))) return true;
+    if (throttled(m, r, c->store, DocStore::read_ru(0) * (double)std::max<size_t>(1, keys->items.size()), DocStore::kRead))
+      return true;
     std::string out = "[";
     for (size_t i = 0; i < keys->items.size(); ++i) {
       const std::string& k = keys->items[i].s;
@@ -756,7 +768,7 @@ class BackingFront {
       if (!query_fn_ || q_stop_) return false;  // no worker: the Python server's route
     }
     if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
-    if (throttled(m, r, c->store, DocStore::query_ru(0))) return true;
+    if (throttled(m, r, c->store, DocStore::query_ru(0), DocStore::kQuery)) return true;
     count("doc.query_worker");
     auto job = std::make_shared<QueryJob>();
     job->account = seg[1];
@@ -835,7 +847,7 @@ class BackingFront {
     }
     if (!indexed || sampled(m)) return to_query_worker(sh, m, r, c, seg, qs);
     if (!authorize(m, r, "cosmos.read", "cosmos/" + seg[1])) return true;
-    if (throttled(m, r, c->store, DocStore::query_ru(0))) return true;
+    if (throttled(m, r, c->store, DocStore::query_ru(0), DocStore::kQuery)) return true;
     std::string body;
     try {
       std::string project = query_get(qs, "project");

@@ -2290,6 +2290,53 @@ class DataPlane {
                 });
       return;
     }
+    if (rpc == "GetBulkState") {
+      std::string store, body = "{\"keys\":[";
+      uint64_t parallelism = 0;
+      bool first = true;
+      std::vector<std::pair<std::string, std::string>> meta;
+      while (rd.next(f, wt)) {
+        if (f == 1 && wt == pb::LEN && rd.bytes(v)) store.assign(v);
+        else if (f == 2 && wt == pb::LEN && rd.bytes(v)) {
+          body += first ? "" : ",";
+          body += json_str(v);
+          first = false;
+        } else if (f == 3 && wt == pb::VARINT && rd.varint(parallelism)) {
+        } else if (f == 4 && wt == pb::LEN && rd.bytes(v)) {
+          std::string k, val;
+          if (!pb::map_entry(v, k, val)) return fail_decode();
+          meta.emplace_back(std::move(k), std::move(val));
+        } else if (!rd.skip(wt)) break;
+      }
+      if (!rd.ok) return fail_decode();
+      body += "],\"parallelism\":" + std::to_string(parallelism ? parallelism : 10) + "}";
+      grpc_http(c, "POST", "/v1.0/state/" + quote_all(store) + "/bulk" + meta_qs(meta), std::move(body),
+                "application/json", {}, [r, rpc](int status, const HeaderList&, std::string_view res) {
+                  if (status >= 300) return grpc_fail(r, status, res, rpc);
+                  // GetBulkStateResponse {items = 1: BulkStateItem {key, data, etag, error}}
+                  pb::Writer w;
+                  try {
+                    Value js = res.empty() ? Value() : parse(res);
+                    if (js.t == Value::Array)
+                      for (auto& it : js.items) {
+                        pb::Writer e;
+                        auto sv = [&](const char* k) -> std::string {
+                          const Value* x = it.get(k);
+                          return x && x->t == Value::String ? x->s : std::string();
+                        };
+                        e.str(1, sv("key"));
+                        if (const Value* d = it.get("data"); d && d->t != Value::Null) e.str(2, dump(*d));
+                        e.str(3, sv("etag"));
+                        e.str(4, sv("error"));
+                        w.len_field(1, e.s);
+                      }
+                  } catch (const std::exception& ex) {
+                    return r.error(13, rpc + ": malformed bulk-get response: " + ex.what());
+                  }
+                  r.ok(w.s);
+                });
+      return;
+    }
     if (rpc == "PublishEvent") {
       std::string pubsub, topic, data, ctype;
       std::vector<std::pair<std::string, std::string>> meta;

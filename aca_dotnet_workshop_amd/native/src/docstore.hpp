@@ -13,10 +13,14 @@
 //   * durability through an append-only log with online compaction.
 #pragma once
 
+#include <sys/random.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <optional>
@@ -563,32 +567,54 @@ class DocStore {
   static double write_ru(size_t bytes) { return 5.0 * std::max<double>(1.0, std::ceil(bytes / 1024.0)); }
   static double query_ru(size_t result_bytes) { return 2.5 + std::ceil(result_bytes / 1024.0); }
 
-  void set_throughput(double ru_per_s) {
+  void set_throughput(double ru_per_s, double ticket_ttl_s = kTicketTtlS) {
     std::lock_guard<std::mutex> g(ru_mu_);
+    ru_ticket_ttl_s_ = ticket_ttl_s;
     ru_rate_ = std::max(0.0, ru_per_s);
+    ru_on_.store(ru_rate_ > 0, std::memory_order_relaxed);
     ru_tokens_ = ru_rate_;
     ru_last_ = mono_s();
     ru_tickets_.clear();
+    ru_by_slot_.clear();
+    ru_by_bind_.clear();
   }
 
   // Admission with reservations.  A caller the bucket cannot serve now is not just told its own
   // deficit (every waiter would wake at once and collide again): its RU are RESERVED -- the
-  // bucket goes negative by the demand admitted for later -- and the 429's hint is the moment
-  // the refill has paid for it, i.e. that caller's slot behind every earlier waiter.  The 429
-  // also carries a ticket (`x-tt-ru-ticket`); the retry that presents it at or after its slot
-  // is admitted without being charged again.  Without the ticket a retry is a new request (the
-  // Cosmos wire contract still holds: 429 + x-ms-retry-after-ms).  A reservation more than
-  // kMaxReserveS ahead is refused outright (the SDK's 30 s wait budget could not reach it); a
-  // ticket not claimed within kTicketTtlS of its slot lapses and its RU stay spent.
+  // bucket goes negative by the demand admitted for later -- and the 429's hint
+  // (x-ms-retry-after-ms) is the moment the refill has paid for it, i.e. that caller's slot behind
+  // every earlier waiter.  The reservation is bound to the request (`bind`: a hash of its method
+  // and target, or of a query's text) and the 429 also carries an unguessable ticket
+  // (`x-tt-ru-ticket`).  The retry is admitted at or after its slot without a second charge when
+  //   * it presents the ticket (and is the same request), or
+  //   * it follows only the Cosmos contract -- retries after the hint, no ticket -- and is the
+  //     same request: it claims its own due reservation by `bind`;
+  // an unticketed retry BEFORE its slot just gets the time left (no second reservation).  A
+  // reservation more than kMaxReserveS ahead is refused outright (the SDK's 30 s wait budget
+  // could not reach it).  One not claimed within kTicketTtlS of its slot lapses -- its caller
+  // gave up -- and its RU go back to the bucket.
   static constexpr double kMaxReserveS = 25.0;
   static constexpr double kTicketTtlS = 10.0;
+  // what a charge is for: the throttled-call breakdown of throughput_stats
+  enum Kind : int { kRead = 0, kWrite = 1, kQuery = 2, kDelete = 3 };
 
   int64_t charge(double ru) {
     uint64_t unused = 0;
     return charge(ru, 0, unused);
   }
+  // a provisioned budget (RU/s > 0): only then does admission need the request's `bind`
+  bool provisioned() const { return ru_on_.load(std::memory_order_relaxed); }
 
-  int64_t charge(double ru, uint64_t ticket, uint64_t& ticket_out) {
+  // FNV-1a of a request's identity (method + target, or a query's text): the `bind` of charge.
+  static uint64_t bind_of(std::string_view a, std::string_view b = {}) {
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : a) h = (h ^ c) * 1099511628211ull;
+    h = (h ^ 0xff) * 1099511628211ull;
+    for (unsigned char c : b) h = (h ^ c) * 1099511628211ull;
+    return h ? h : 1;
+  }
+
+  int64_t charge(double ru, uint64_t ticket, uint64_t& ticket_out, uint64_t bind = 0, int kind = kWrite) {
     std::lock_guard<std::mutex> g(ru_mu_);
     ticket_out = 0;
     if (ru_rate_ <= 0) {  // not provisioned: admitted, still metered (what the workload would need)
@@ -598,20 +624,31 @@ class DocStore {
     double now = mono_s();
     ru_tokens_ = std::min(ru_rate_, ru_tokens_ + (now - ru_last_) * ru_rate_);
     ru_last_ = now;
+    lapse(now);
+    // the request's own reservation: by its ticket, else (a Cosmos-contract retry) by `bind`
+    auto own = ru_tickets_.end();
     if (ticket) {
-      auto it = ru_tickets_.find(ticket);
-      if (it != ru_tickets_.end()) {
-        if (now + 5e-4 >= it->second.first) {  // its slot came: paid for by the reservation
-          ru_consumed_ += it->second.second;
-          ++ru_reserved_admits_;
-          ru_tickets_.erase(it);
-          return 0;
-        }
-        ticket_out = ticket;  // early: keep the slot
-        ++ru_throttled_;
-        ++ru_early_retries_;
-        return std::max<int64_t>(1, (int64_t)std::ceil((it->second.first - now) * 1000.0));
+      own = ru_tickets_.find(ticket);
+      if (own != ru_tickets_.end() && bind && own->second.bind != bind) own = ru_tickets_.end();  // another's ticket
+    }
+    if (own == ru_tickets_.end() && bind) {
+      auto range = ru_by_bind_.equal_range(bind);
+      for (auto it = range.first; it != range.second; ++it) {
+        auto t = ru_tickets_.find(it->second);
+        if (t != ru_tickets_.end() && (own == ru_tickets_.end() || t->second.slot < own->second.slot)) own = t;
       }
+    }
+    if (own != ru_tickets_.end()) {
+      if (now + 5e-4 >= own->second.slot) {  // its slot came: paid for by the reservation
+        ru_consumed_ += own->second.ru;
+        ++ru_reserved_admits_;
+        drop(own);
+        return 0;
+      }
+      ticket_out = own->first;  // early: keep the slot
+      ++ru_throttled_;
+      ++ru_early_retries_;
+      return std::max<int64_t>(1, (int64_t)std::ceil((own->second.slot - now) * 1000.0));
     }
     ru = std::min(ru, ru_rate_);  // a request bigger than a second's budget waits for a full bucket
     ++ru_calls_;
@@ -621,15 +658,16 @@ class DocStore {
       return 0;
     }
     ++ru_throttled_;
+    ++ru_throttled_kind_[kind & 3];
     double wait = (ru - ru_tokens_) / ru_rate_;  // until the refill has paid every earlier reservation and this one
     if (wait > kMaxReserveS) return std::max<int64_t>(1, (int64_t)std::ceil(wait * 1000.0));
     ru_tokens_ -= ru;
-    if (ru_tickets_.size() > 4096) {  // lapsed reservations (their callers gave up)
-      for (auto it = ru_tickets_.begin(); it != ru_tickets_.end();)
-        it = now > it->second.first + kTicketTtlS ? ru_tickets_.erase(it) : std::next(it);
-    }
-    ticket_out = ++ru_ticket_seq_;
-    ru_tickets_.emplace(ticket_out, std::make_pair(now + wait, ru));
+    do ticket_out = next_ticket();
+    while (ru_tickets_.count(ticket_out));
+    Reservation res{now + wait, ru, bind};
+    ru_tickets_.emplace(ticket_out, res);
+    ru_by_slot_.emplace(res.slot, ticket_out);
+    if (bind) ru_by_bind_.emplace(bind, ticket_out);
     return std::max<int64_t>(1, (int64_t)std::ceil(wait * 1000.0));
   }
 
@@ -648,7 +686,11 @@ class DocStore {
     std::lock_guard<std::mutex> g(ru_mu_);
     return {{"ru_per_s", ru_rate_}, {"ru_consumed", ru_consumed_}, {"throttled", (double)ru_throttled_},
             {"reserved_admits", (double)ru_reserved_admits_}, {"open_reservations", (double)ru_tickets_.size()},
-            {"calls", (double)ru_calls_}, {"early_retries", (double)ru_early_retries_}};
+            {"calls", (double)ru_calls_}, {"early_retries", (double)ru_early_retries_},
+            {"lapsed_reservations", (double)ru_lapsed_}, {"refunded_ru", ru_refunded_},
+            {"throttled_read", (double)ru_throttled_kind_[kRead]}, {"throttled_write", (double)ru_throttled_kind_[kWrite]},
+            {"throttled_query", (double)ru_throttled_kind_[kQuery]},
+            {"throttled_delete", (double)ru_throttled_kind_[kDelete]}};
   }
 
   // ------------------------------------------------------------ column mirror
@@ -1181,11 +1223,69 @@ class DocStore {
   static constexpr int32_t kEncode = INT32_MIN;  // mirror_append: no id carried over
   std::vector<int32_t> reuse_;                   // put_at's per-column carried ids (under mu_)
   std::mutex ru_mu_;
+  std::atomic<bool> ru_on_{false};
   double ru_rate_ = 0, ru_tokens_ = 0, ru_last_ = 0, ru_consumed_ = 0;
   // calls: charged requests (a ticketed retry is not a new one); early_retries: tickets
   // presented before their slot (a second 429 for the same call)
-  uint64_t ru_throttled_ = 0, ru_reserved_admits_ = 0, ru_ticket_seq_ = 0, ru_calls_ = 0, ru_early_retries_ = 0;
-  std::unordered_map<uint64_t, std::pair<double, double>> ru_tickets_;  // ticket -> (slot, RU reserved)
+  uint64_t ru_throttled_ = 0, ru_reserved_admits_ = 0, ru_calls_ = 0, ru_early_retries_ = 0, ru_lapsed_ = 0;
+  uint64_t ru_throttled_kind_[4] = {0, 0, 0, 0};
+  double ru_refunded_ = 0;
+  double ru_ticket_ttl_s_ = kTicketTtlS;
+  struct Reservation {
+    double slot, ru;
+    uint64_t bind;
+  };
+  std::unordered_map<uint64_t, Reservation> ru_tickets_;      // ticket -> reservation
+  std::multimap<double, uint64_t> ru_by_slot_;                 // slot -> ticket (lapse order)
+  std::unordered_multimap<uint64_t, uint64_t> ru_by_bind_;     // request -> ticket
+  uint64_t ru_rng_[2] = {0, 0};
+  // tickets are random (xorshift128+ seeded from getrandom): a request cannot claim another's slot
+  // by counting
+  uint64_t next_ticket() {
+    if ((ru_rng_[0] | ru_rng_[1]) == 0) {
+      if (getrandom(ru_rng_, sizeof ru_rng_, 0) != (ssize_t)sizeof ru_rng_ || (ru_rng_[0] | ru_rng_[1]) == 0)
+        ru_rng_[0] = 0x9e3779b97f4a7c15ull ^ (uint64_t)(mono_s() * 1e9);
+    }
+    uint64_t a = ru_rng_[0];
+    const uint64_t b = ru_rng_[1];
+    ru_rng_[0] = b;
+    a ^= a << 23;
+    ru_rng_[1] = a ^ b ^ (a >> 17) ^ (b >> 26);
+    uint64_t v = (ru_rng_[1] + b) >> 1;  // 63 bits: the decimal header text parses as unsigned either way
+    return v ? v : 1;
+  }
+  void drop(std::unordered_map<uint64_t, Reservation>::iterator it) {
+    auto range = ru_by_slot_.equal_range(it->second.slot);
+    for (auto s = range.first; s != range.second; ++s)
+      if (s->second == it->first) {
+        ru_by_slot_.erase(s);
+        break;
+      }
+    if (it->second.bind) {
+      auto b = ru_by_bind_.equal_range(it->second.bind);
+      for (auto x = b.first; x != b.second; ++x)
+        if (x->second == it->first) {
+          ru_by_bind_.erase(x);
+          break;
+        }
+    }
+    ru_tickets_.erase(it);
+  }
+  // reservations not claimed within kTicketTtlS of their slot: their callers gave up; the RU
+  // they held go back to the bucket (capped at a second's budget, like any refill)
+  void lapse(double now) {
+    while (!ru_by_slot_.empty() && ru_by_slot_.begin()->first + ru_ticket_ttl_s_ < now) {
+      auto t = ru_tickets_.find(ru_by_slot_.begin()->second);
+      if (t == ru_tickets_.end()) {
+        ru_by_slot_.erase(ru_by_slot_.begin());
+        continue;
+      }
+      ru_tokens_ = std::min(ru_rate_, ru_tokens_ + t->second.ru);
+      ru_refunded_ += t->second.ru;
+      ++ru_lapsed_;
+      drop(t);
+    }
+  }
   static double mono_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }

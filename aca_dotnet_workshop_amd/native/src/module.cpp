@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "apphost.hpp"
+#include "daprpb.hpp"
 #include "backingfront.hpp"
 #include "broker.hpp"
 #include "cpuscan.hpp"
@@ -380,6 +381,36 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(l, py::bytes(bulk));
   });
 
+  // dapr.proto.runtime.v1 messages of the gRPC SDK's hot calls (daprpb.hpp), shared with the app
+  // host's native routes: the same bytes from both.
+  auto view = [](const py::bytes& b) {
+    char* p;
+    Py_ssize_t n;
+    if (PyBytes_AsStringAndSize(b.ptr(), &p, &n) != 0) throw py::error_already_set();
+    return std::string_view(p, (size_t)n);
+  };
+  // the state API's save body -> SaveStateRequest, or None
+  m.def("dapr_pb_save_state_bulk", [view](const std::string& store, py::bytes body) -> py::object {
+    std::string out;
+    if (!tt::daprpb::save_state_bulk(store, view(body), out)) return py::none();
+    return py::bytes(out);
+  });
+  m.def("dapr_pb_get_bulk_state", [](const std::string& store, const std::vector<std::string>& keys, int parallelism) {
+    return py::bytes(tt::daprpb::get_bulk_state(store, keys, parallelism));
+  });
+  // GetBulkStateResponse -> the bulk-get API's JSON ([{"key","data","etag"} | {"key"}]), or None
+  m.def("dapr_pb_bulk_state_json", [view](py::bytes msg) -> py::object {
+    std::string out;
+    if (!tt::daprpb::bulk_state_response_json(view(msg), out)) return py::none();
+    return py::bytes(out);
+  });
+  // QueryStateResponse -> the query API's JSON ({"results":[..],"token"}), or None
+  m.def("dapr_pb_query_json", [view](py::bytes msg) -> py::object {
+    std::string out;
+    if (!tt::daprpb::query_response_json(view(msg), out)) return py::none();
+    return py::bytes(out);
+  });
+
   // bulk-get answer for a markoverdue page -> (ids marked, conditional bulk-save body, skipped)
   // or None (taskcodec.hpp conditional_mark).
   m.def("tasks_conditional_mark", [](py::bytes got) -> py::object {
@@ -702,13 +733,15 @@ PYBIND11_MODULE(_ttnative, m) {
            py::arg("rows"), py::arg("prefix") = "", py::arg("token") = "", py::arg("gen") = 0,
            py::arg("sort_paths") = py::none())
       .def("mirror_stats", &DocStore::mirror_stats)
-      .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"))
-      .def("charge", [](DocStore& s, double ru, uint64_t ticket) {
+      .def("set_throughput", &DocStore::set_throughput, py::arg("ru_per_s"), py::arg("ticket_ttl_s") = DocStore::kTicketTtlS)
+      .def("charge", [](DocStore& s, double ru, uint64_t ticket, std::string bind, int kind) {
              uint64_t out = 0;
-             int64_t wait = s.charge(ru, ticket, out);
+             int64_t wait = s.charge(ru, ticket, out, bind.empty() ? 0 : DocStore::bind_of(bind), kind);
              return py::make_tuple(wait, out);
-           }, py::arg("ru"), py::arg("ticket") = 0,
-           "(wait_ms, ticket): 0 = admitted; else a 429 whose ticket claims the reserved slot")
+           }, py::arg("ru"), py::arg("ticket") = 0, py::arg("bind") = "", py::arg("kind") = (int)DocStore::kWrite,
+           "(wait_ms, ticket): 0 = admitted; else a 429 whose ticket claims the reserved slot.  `bind`: the "
+           "request's identity (method + target [+ query / bulk body]): a retry of the same request without "
+           "the ticket claims its due reservation; `kind`: 0 read, 1 write, 2 query, 3 delete")
       .def("debit", &DocStore::debit, py::arg("ru"))
       .def("throughput_stats", &DocStore::throughput_stats)
       .def_static("read_ru", &DocStore::read_ru)

@@ -46,10 +46,18 @@ def sidecar_grpc_target(environ: dict[str, str] | None = None) -> str:
     return f"127.0.0.1:{env.get('DAPR_GRPC_PORT', '50001')}"
 
 
+def _native():
+    from ..native import load
+    return load()
+
+
 def query_response_json(raw: bytes) -> bytes:
     """A serialized ``QueryStateResponse`` as the HTTP state-query API's JSON answer
     (``{"results":[{"key","data","etag"}],"token"}``, the layout the task codec reads and the
-    app host's gRPC routes build: apphost.hpp ``query_response_json``)."""
+    app host's gRPC routes build: daprpb.hpp ``query_response_json``)."""
+    made = _native().dapr_pb_query_json(raw)
+    if made is not None:
+        return made
     r = P.rt("QueryStateResponse").FromString(raw)
     parts = []
     for i in r.results:
@@ -371,6 +379,28 @@ class GrpcSidecarClient:
         r = await self._call("QueryStateAlpha1", req, f"state query {store}")
         return QueryResponse([StateItem(i.key, _loads(i.data), i.etag or None) for i in r.results], r.token or None,
                              dict(r.metadata))
+
+    async def save_state_body(self, store: str, body: bytes) -> None:
+        """Save with a body in the state HTTP API's form (``[{"key", "value", "etag", "options"}]``,
+        what the task codecs write) as one SaveStateRequest (daprpb.hpp ``save_state_bulk``: each
+        value's JSON text as is) -- the bytes the app host's native routes send."""
+        msg = _native().dapr_pb_save_state_bulk(store, bytes(body))
+        if msg is None:
+            await self.save_bulk_state(store, json.loads(body))
+            return
+        await self._call_encoded("SaveState", msg, f"state save {store}")
+
+    async def get_bulk_state_raw(self, store: str, keys: list[str], parallelism: int = 10) -> bytes:
+        """``get_bulk_state``'s answer as the HTTP bulk-get API's JSON (``[{"key","data","etag"} |
+        {"key"}]``), the text the markoverdue codec reads whichever protocol carried it."""
+        raw = await self._call_encoded("GetBulkState", _native().dapr_pb_get_bulk_state(store, list(keys), parallelism),
+                                       f"state bulkget {store}")
+        made = _native().dapr_pb_bulk_state_json(raw)
+        if made is not None:
+            return made
+        r = P.rt("GetBulkStateResponse").FromString(raw)
+        return json.dumps([{"key": i.key, "data": _loads(i.data), "etag": i.etag} if i.data and i.data != b"null"
+                           else {"key": i.key} for i in r.items], separators=(",", ":")).encode()
 
     async def query_state_raw(self, store: str, query: dict[str, Any] | str,
                               metadata: dict[str, str] | None = None) -> bytes:

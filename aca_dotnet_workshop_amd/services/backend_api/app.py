@@ -167,9 +167,21 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
                 return resp
         return _json(tasks_to_json(await manager.get_yesterdays_due_tasks(limit)))
 
+    mark_native = getattr(manager, "native_markoverdue_route", None)
+    mark_spec = mark_native() if mark_native is not None and fast_mark is not None else None
+    mark_what = mark_spec.pop("what") if mark_spec else {}
+    if mark_spec:
+        # POST markoverdue on the app host's I/O thread: the same binder, conditional mark pass,
+        # log lines and bulk save as mark_overdue_from_body
+        mark_spec["cfg"].update({"status": 200})
+        app.services.setdefault("native_routes", []).append(mark_spec)
+
     @app.route("/api/overduetasks/markoverdue", ("POST",), name="MarkOverdue", tag="OverdueTasks",
                body=[TaskModel], responses={200: None})
     async def mark_overdue(req: Request) -> Response:
+        failed = native_route_failure(req, mark_what) if mark_what else None
+        if failed is not None:  # the native route's bulk get or save failed: the SDK's error
+            raise failed
         ctype = req.content_type
         if fast_mark is not None and (not ctype or "json" in ctype) and await fast_mark(req.body):
             return empty(200)

@@ -46,6 +46,7 @@ log = logging.getLogger("TasksManager")
 LOG_SAVE_NEW = "Save a new task with name: '%s' to state store"
 LOG_PUBLISH = "Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'"
 LOG_OVERDUE_PAGE = "Getting open tasks due before: '%s' (page of %d)"
+LOG_MARK_OVERDUE = "Mark task with Id: '%s' as OverDue task"
 
 STORE_NAME = "statestore"
 PUBSUB_NAME = "dapr-pubsub-servicebus"
@@ -193,11 +194,8 @@ class TasksStoreManager(TasksManager):
             return None
         tid, name, assignee, task_json, state_body = made
         log.info(LOG_SAVE_NEW, name)
-        save_body = getattr(self.client, "save_state_body", None)  # HTTP: the state API's body as is
-        if save_body is not None:
-            await save_body(self.store, state_body)
-        else:  # gRPC: the value goes into a SaveStateRequest
-            await self.client.save_state(self.store, tid, RawJson(task_json.decode()))
+        # the state API's body as is (HTTP) or as a SaveStateRequest of the same items (gRPC)
+        await self.client.save_state_body(self.store, state_body)
         log.info(LOG_PUBLISH, tid, name, assignee)
         await self.client.publish_event(self.pubsub, self.topic, task_json, content_type="application/json")
         return tid
@@ -218,7 +216,7 @@ class TasksStoreManager(TasksManager):
         grpc = ep.get("protocol") == "grpc"
         what: dict[str, str] = {}
         http_what = {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}",
-                     "query": f"query state {self.store}"}
+                     "query": f"query state {self.store}", "bulk": f"bulk get {self.store}"}
         for step, (path, rpc) in targets.items():
             cfg[f"{step}_target"] = P.method_path(rpc) if grpc else ep["prefix"] + path
             what[step] = rpc if grpc else http_what[step]
@@ -403,6 +401,24 @@ class TasksStoreManager(TasksManager):
         return {"kind": "api_overdue", "method": "GET", "path": "/api/overduetasks", "route": "/api/overduetasks",
                 "cfg": cfg, "what": what}
 
+    def native_markoverdue_route(self) -> dict | None:
+        """``mark_overdue_from_body`` as a native route of the app host (apphost.hpp
+        ``api_markoverdue``): the native binder's ids, then this manager's conditional mark pass --
+        bulk get, codec, a log line per marked task, ETag-guarded bulk save, re-read on a conflict
+        up to ``max_retries`` passes -- over the client's protocol; None when this client cannot
+        take one."""
+        ep = self._native_endpoint()
+        if ep is None or getattr(self.client, "get_bulk_state_raw", None) is None:
+            return None
+        cfg, what = self._native_calls(ep, bulk=(f"/v1.0/state/{self.store}/bulk", "GetBulkState"),
+                                       save=(f"/v1.0/state/{self.store}", "SaveState"))
+        if ep.get("protocol") != "grpc":
+            what["bulk"] = f"bulk get {self.store}"
+        cfg.update({"store": self.store, "log_category": log.name, "log_mark": LOG_MARK_OVERDUE, "log_mark_args": "id",
+                    "max_retries": self.max_retries, "parallelism": 10})
+        return {"kind": "api_markoverdue", "method": "POST", "path": "/api/overduetasks/markoverdue",
+                "route": "/api/overduetasks/markoverdue", "cfg": cfg, "what": what}
+
     def _range_query(self, limit: int | None, midnight: str | None = None) -> tuple[dict, str, int]:
         """The open tasks due before today's midnight, oldest first: ``ORDER BY taskCreatedOn``
         in the store picks the page (reference ``.OrderBy(o => o.TaskCreatedOn)``,
@@ -469,7 +485,7 @@ class TasksStoreManager(TasksManager):
             if made is None:
                 raise ValueError("the task collection holds documents outside the TaskModel shape")
             marked, bulk, _skipped = made
-            info_each(log, "Mark task with Id: '%s' as OverDue task", [(tid,) for tid in marked])
+            info_each(log, LOG_MARK_OVERDUE, [(tid,) for tid in marked])
             if not marked:
                 return
             try:

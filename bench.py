@@ -973,6 +973,15 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         retry0 = sum(_sidecar_counter(u, "state.throttled_retry") for u in api_uds)
         th = threading.Thread(target=watch, daemon=True)
         th.start()
+        steady: dict = {}
+
+        def mark_steady() -> None:  # one second in: the bucket's initial second of budget is spent
+            if not stop.wait(1.0):
+                steady.update(t=time.perf_counter(), st=_collection_stats(env.backing_url).get("throughput", {}),
+                              enq=int(_counts(counts).get("enqueued", 0)))
+        th2 = threading.Thread(target=mark_steady, daemon=True)
+        th2.start()
+        enq0 = int(_counts(counts).get("enqueued", 0))
         import subprocess
         cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies, "--content-type",
                "application/x-www-form-urlencoded", "--header",
@@ -983,8 +992,11 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 600)
         wall = time.perf_counter() - t0
         rep = json.loads(p.stdout.strip().splitlines()[-1]) if p.stdout.strip() else {}
-        stop.set()
+        t_end = time.perf_counter()
         st1 = _collection_stats(env.backing_url).get("throughput", {})
+        enq1 = int(_counts(counts).get("enqueued", 0))
+        stop.set()
+        th2.join(5)
         retries = sum(_sidecar_counter(u, "state.throttled_retry") for u in api_uds) - retry0
         sc = rep.get("status_counts") or {}
         attempts = int(rep.get("requests", 0))
@@ -992,7 +1004,19 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         lists_ok = int(sc.get("200", 0))
         ru = float(st1.get("ru_consumed", 0.0)) - float(st0.get("ru_consumed", 0.0))
         el = float(rep.get("elapsed_s") or wall)
+        budget = float(st1.get("ru_per_s", 0.0))
+        # the steady window: from one second in (the bucket starts with a second of budget, as any
+        # idle second refills it) to the end -- RU admitted there over the budget's refill
+        sw = None
+        if steady and t_end - steady["t"] > 1.0 and budget:
+            w = t_end - steady["t"]
+            ru_s = float(st1.get("ru_consumed", 0.0)) - float(steady["st"].get("ru_consumed", 0.0))
+            sw = {"seconds": round(w, 2), "tasks_per_s": round((enq1 - steady["enq"]) / w, 1),
+                  "ru_consumed_per_s": round(ru_s / w, 1), "ru_over_budget": round(ru_s / (budget * w), 3)}
+        by_kind = {k: int(st1.get(f"throttled_{k}", 0) - st0.get(f"throttled_{k}", 0))
+                   for k in ("write", "query", "read", "delete")}
         return {"tasks_per_s": round(tasks / el, 1) if el else None, "tasks": tasks, "seconds": round(el, 2),
+                "steady_window": sw, "throttled_calls_by_kind": by_kind, "published": enq1 - enq0,
                 "create_attempts": attempts, "failed_creates": attempts - tasks, "failed_lists": tasks - lists_ok,
                 "errors": rep.get("errors"), "first_error": rep.get("first_error") or None,
                 "create_latency_ms": rep.get("latency_ms"), "list_latency_ms": rep.get("follow_latency_ms"),
@@ -1150,6 +1174,7 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
     if envelope:
         s["envelope"] = {k: envelope.get(k) for k in ("tasks_per_s", "errors", "tasks_per_s_over_budget_rate",
                                                        "store_429s_per_task", "store_429s_per_call")}
+        s["envelope"]["steady_ru_over_budget"] = (envelope.get("steady_window") or {}).get("ru_over_budget")
         k = envelope.get("keda") or {}
         s["keda"] = {x: k.get(x) for x in ("peak_replicas", "time_to_peak_s", "exactly_once")}
     return s

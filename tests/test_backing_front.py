@@ -364,6 +364,94 @@ def test_provisioned_throughput_429(front, monkeypatch):
     run(main())
 
 
+@pytest.mark.parametrize("front", FRONTS)
+def test_throttled_retry_at_the_hint_without_a_ticket_gets_in(front, monkeypatch):
+    """a client that follows only the Cosmos contract -- retry after
+    x-ms-retry-after-ms, no ticket -- is admitted at its slot: the reservation is bound to the
+    request (method + target), so the same request claims it; an early retry is told the time
+    left without a second reservation.  Tickets are random, and another request presenting a
+    ticket it did not get is not admitted on it."""
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.doc_set_throughput("acct", "db", "c", 20.0)
+            h = HttpClient()
+            hd = {"Content-Type": "application/json", "x-tt-identity": "x"}
+            for i in range(4):  # spend the bucket (5 RU each at 20 RU/s)
+                r = await h.put(f"{b.base}/cosmos/acct/db/c/docs/p{i}", body=b'{"a": 1}', headers=hd)
+                assert r.status == 200
+            url = f"{b.base}/cosmos/acct/db/c/docs/lone"
+            r = await h.put(url, body=b'{"a": 1}', headers=hd)
+            assert r.status == 429
+            hint, ticket = int(r.headers["x-ms-retry-after-ms"]), int(r.headers["x-tt-ru-ticket"])
+            assert 150 <= hint <= 300, hint
+            # someone else's request presenting that ticket: not admitted on it (its own 429)
+            r2 = await h.put(f"{b.base}/cosmos/acct/db/c/docs/thief", body=b'{"a": 1}',
+                             headers={**hd, "x-tt-ru-ticket": str(ticket)})
+            assert r2.status == 429 and r2.headers["x-tt-ru-ticket"] != str(ticket)
+            # an early retry of the same request, no ticket: the time left, same reservation
+            r3 = await h.put(url, body=b'{"a": 1}', headers=hd)
+            assert r3.status == 429 and int(r3.headers["x-ms-retry-after-ms"]) <= hint
+            assert r3.headers.get("x-tt-ru-ticket") == str(ticket)
+            await asyncio.sleep(hint / 1000 + 0.01)
+            r4 = await h.put(url, body=b'{"a": 1}', headers=hd)  # at the hint, no ticket
+            assert r4.status == 200, (r4.status, r4.headers)
+            st = (await c.doc_stats("acct", "db", "c"))["throughput"]
+            assert st["reserved_admits"] == 1 and st["early_retries"] == 1 and st["throttled_write"] == 2
+            assert st["open_reservations"] == 1  # the thief's own, unclaimed
+            await h.close()
+            await c.http.close()
+    run(main())
+
+
+def test_unclaimed_reservations_lapse_and_refund():
+    """A reservation whose caller gave up lapses kTicketTtlS after its slot and its RU go back to
+    the bucket; admitted RU never exceed the budget's refill plus the initial second (+ one call)."""
+    import threading
+    import time as _t
+
+    from aca_dotnet_workshop_amd import native
+    N = native.load()
+    s = N.DocStore()
+    s.set_throughput(200.0)
+    t0 = _t.monotonic()
+    admitted = [0.0]
+    stop = threading.Event()
+
+    def worker(w):
+        i = 0
+        while not stop.is_set():
+            i += 1
+            ticket, bind = 0, f"PUT /w{w}/{i}"
+            while not stop.is_set():
+                wait, ticket = s.charge(5.0, ticket, bind, 1)
+                if not wait:
+                    admitted[0] += 5.0
+                    break
+                _t.sleep(wait / 1000)
+    ts = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in ts:
+        t.start()
+    _t.sleep(1.5)
+    stop.set()
+    for t in ts:
+        t.join()
+    window = _t.monotonic() - t0
+    st = s.throughput_stats()
+    assert st["ru_consumed"] == pytest.approx(admitted[0])
+    assert st["ru_consumed"] <= 200.0 * window + 200.0 + 5.0, (st, window)
+    assert st["throttled"] > 0 and st["reserved_admits"] > 0
+    # reservations of callers that gave up lapse after the ticket TTL and refund their RU
+    s.set_throughput(10.0, 0.2)
+    assert s.charge(10.0, 0, "PUT /a", 1) == (0, 0)  # the bucket's second of budget
+    wait, ticket = s.charge(5.0, 0, "PUT /b", 1)  # reserved 500 ms ahead, never claimed
+    assert wait >= 400 and ticket > 0
+    _t.sleep(0.8)  # slot + TTL passed: ~8 RU refilled less the 5 reserved, plus the 5 refunded
+    assert s.charge(7.5, 0, "PUT /c", 1)[0] == 0  # without the refund: ~3 RU, a 429
+    st = s.throughput_stats()
+    assert st["lapsed_reservations"] == 1 and st["refunded_ru"] == 5.0 and st["open_reservations"] == 0
+
+
 def test_indexed_queries_run_on_the_native_front(monkeypatch):
     """A query the hash indexes answer (backing/accel.py ``indexable``: the list of a creator's
     tasks) runs on the native front's loop; the answers equal the Python handler's, and every

@@ -5,6 +5,8 @@ delete / query, publish, output binding; Backend.Api TasksStoreManager.cs, Proce
 ExternalTasksProcessorController.cs:43) is run through both ``SidecarClient`` (HTTP) and
 ``GrpcSidecarClient`` (gRPC) against one sidecar; results, ETag semantics, delivered CloudEvents
 and error statuses must agree."""
+import json
+
 import grpc
 import pytest
 
@@ -100,6 +102,14 @@ def test_grpc_and_http_clients_agree(plane, tmp_path):
                 assert await c.get_state("statestore", f"missing-{tag}") is None
                 bulk = await c.get_bulk_state("statestore", [f"k-{tag}", f"missing-{tag}"])
                 assert bulk[0].data["n"] == 4 and bulk[1].data is None
+                # the raw forms the task codecs read: the HTTP API's JSON whichever protocol
+                # carried it (gRPC: daprpb.hpp bulk_state_response_json / query_response_json)
+                raw = json.loads(await c.get_bulk_state_raw("statestore", [f"k-{tag}", f"missing-{tag}"]))
+                assert raw[0] == {"key": f"k-{tag}", "data": {**doc, "n": 4}, "etag": bulk[0].etag}
+                assert raw[1]["key"] == f"missing-{tag}" and raw[1].get("data") is None
+                await c.save_state_body("statestore", json.dumps([{"key": f"b-{tag}", "value": {"v": tag}}]).encode())
+                rq = json.loads(await c.query_state_raw("statestore", {"filter": {"EQ": {"v": tag}}}))
+                assert [(r["key"], r["data"]) for r in rq["results"]] == [(f"b-{tag}", {"v": tag})]
                 await c.execute_state_transaction("statestore", [
                     {"operation": "upsert", "request": {"key": f"t1-{tag}", "value": {"taskCreatedBy": tag, "v": 1}}},
                     {"operation": "upsert", "request": {"key": f"t2-{tag}", "value": {"taskCreatedBy": tag, "v": 2}}}])
@@ -142,7 +152,7 @@ def test_grpc_and_http_clients_agree(plane, tmp_path):
                 # the hot RPCs were decoded by the C++ plane (h2.hpp / dataplane.cpp) and ran its
                 # native state / publish paths; the rest were bridged to grpc_api.py
                 metrics = (await h.http.get(h.base + "/metrics")).body.decode()
-                for op in ("grpc.SaveState", "grpc.GetState", "grpc.DeleteState", "grpc.QueryStateAlpha1",
+                for op in ("grpc.SaveState", "grpc.GetState", "grpc.DeleteState", "grpc.QueryStateAlpha1", "grpc.GetBulkState",
                            "grpc.PublishEvent", "grpc.InvokeService", "grpc.GetSecret", "state.save",
                            "state.get", "state.delete", "state.query", "publish"):
                     assert f'op="{op}"' in metrics, op
