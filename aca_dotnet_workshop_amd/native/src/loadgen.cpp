@@ -28,6 +28,8 @@
 //       --concurrency 128 --batch 1024 --steps 20 --expect 201 
 //       --until-url http://127.0.0.1:9000/servicebus/ns/counts?entity=... --until-field completed
 #include <algorithm>
+#include <cctype>
+#include <functional>
 #include <csignal>
 #include <cstdio>
 #include <fstream>
@@ -331,10 +333,173 @@ class Gen {
   }
 };
 
+// --session: the whole browser session of SURVEY §2.11's UI, one flow per user at a time (each
+// in-flight slot owns user s<slot>, so its task list holds only its own flow's task):
+//   POST /Tasks/Create (302) -> GET /Tasks/Index (200: the new task's id from its Edit link, the
+//   list is newest first) -> GET /Tasks/Edit/{id} (200) -> POST /Tasks/Edit/{id} (302; a new name,
+//   due date and assignee: the API publishes the assignee change) -> POST /Tasks/Index?handler=
+//   complete&id= (302) -> POST /Tasks/Index?handler=delete&id= (302) -> GET /Tasks/Index (200)
+// (Pages/Tasks/Create.cshtml.cs:30-51, Index.cshtml.cs:23-71, Edit.cshtml.cs:38-71).  `--batch` x
+// `--steps` flows in all; the report has every page's latency percentiles.
+class SessionGen {
+ public:
+  static constexpr int kPages = 7;
+  static constexpr const char* kNames[kPages] = {"create", "list", "edit_get", "edit_post", "complete", "delete",
+                                                 "list_after"};
+
+  SessionGen(ev::Loop& loop, Opts o, std::string af_token) : loop_(loop), client_(loop), o_(std::move(o)),
+                                                            token_(std::move(af_token)) {
+    if (!o_.tls_ca.empty()) {
+      ev::TlsConfig tc;
+      tc.ca = o_.tls_ca;
+      tc.verify_peer = true;
+      client_.set_tls(std::make_shared<ev::TlsContext>(tc, false));
+    }
+    total_ = (long long)o_.batch * std::max(1, o_.steps);
+  }
+
+  void start() {
+    t0_ = ev::now_s();
+    int n = (int)std::min<long long>(o_.concurrency, total_);
+    for (int s = 0; s < n; ++s) next_flow(s);
+    if (n == 0) loop_.stop();
+  }
+
+  std::string report() const {
+    char buf[512];
+    std::snprintf(buf, sizeof buf, "{\"flows\": %lld, \"errors\": %lld, \"elapsed_s\": %.6f, \"pages\": {", done_,
+                  errors_, t1_ - t0_);
+    std::string s = buf;
+    for (int p = 0; p < kPages; ++p) {
+      std::vector<double> l = lat_[p];
+      std::sort(l.begin(), l.end());
+      auto pct = [&](double q) { return l.empty() ? 0.0 : l[std::min(l.size() - 1, (size_t)(l.size() * q))] * 1e3; };
+      std::snprintf(buf, sizeof buf, "%s\"%s\": {\"n\": %zu, \"p50\": %.3f, \"p99\": %.3f, \"max\": %.3f}", p ? ", " : "",
+                    kNames[p], l.size(), pct(0.5), pct(0.99), l.empty() ? 0.0 : l.back() * 1e3);
+      s += buf;
+    }
+    s += "}, \"status_counts\": {";
+    bool first = true;
+    for (auto& kv : statuses_) {
+      s += (first ? "\"" : ", \"") + std::to_string(kv.first) + "\": " + std::to_string(kv.second);
+      first = false;
+    }
+    s += "}, \"first_error\": ";
+    escape_to(s, first_error_);
+    return s + "}";
+  }
+  long long errors() const { return errors_; }
+
+ private:
+  struct Flow {
+    int slot = 0;
+    long long n = 0;
+    const ev::Endpoint* ep = nullptr;
+    ev::HeaderList get_h, form_h;
+    std::string id;
+  };
+  ev::Loop& loop_;
+  ev::Client client_;
+  Opts o_;
+  std::string token_;
+  long long total_ = 0, issued_ = 0, done_ = 0, errors_ = 0;
+  size_t rr_ = 0;
+  double t0_ = 0, t1_ = 0;
+  std::vector<double> lat_[kPages];
+  std::map<int, long long> statuses_;
+  std::string first_error_;
+
+  static std::string form_escape(const std::string& v) {
+    static const char* hx = "0123456789ABCDEF";
+    std::string o;
+    for (unsigned char c : v) {
+      if (std::isalnum(c) || c == '-' || c == '_' || c == '.') o += (char)c;
+      else if (c == ' ') o += '+';
+      else o += '%', o += hx[c >> 4], o += hx[c & 15];
+    }
+    return o;
+  }
+
+  void next_flow(int slot) {
+    if (issued_ >= total_) {
+      if (done_ == issued_ && t1_ == 0) {
+        t1_ = ev::now_s();
+        loop_.stop();
+      }
+      return;
+    }
+    auto f = std::make_shared<Flow>();
+    f->slot = slot;
+    f->n = issued_++;
+    f->ep = &o_.targets[rr_++ % o_.targets.size()];
+    const std::string user = "s" + std::to_string(slot) + "@bench.local";  // session users: their own lists
+    for (auto h : o_.headers) {  // the cookies, with this slot's identity
+      for (size_t at; (at = h.second.find("{user}")) != std::string::npos;) h.second.replace(at, 6, user);
+      if (h.first != "content-type") f->get_h.push_back(h), f->form_h.push_back(h);
+    }
+    f->form_h.emplace_back("content-type", "application/x-www-form-urlencoded");
+    const std::string& body = o_.bodies[(size_t)(f->n % (long long)o_.bodies.size())];
+    page(f, 0, "POST", "/Tasks/Create", body, 302, [this, f](ev::ClientResult&) {
+      page(f, 1, "GET", "/Tasks/Index", {}, 200, [this, f](ev::ClientResult& r) {
+        const std::string& b = r.resp.body;
+        size_t at = b.find("/Tasks/Edit/");
+        if (at == std::string::npos || at + 12 + 36 > b.size()) return fail(f, "the new task is not on Tasks/Index");
+        f->id = b.substr(at + 12, 36);
+        page(f, 2, "GET", "/Tasks/Edit/" + f->id, {}, 200, [this, f](ev::ClientResult& r2) {
+          if (r2.resp.body.find(f->id) == std::string::npos) return fail(f, "Tasks/Edit does not show the task");
+          std::string n = std::to_string(f->n);
+          std::string edit = "__RequestVerificationToken=" + form_escape(token_) + "&TaskUpdate.TaskId=" + f->id +
+                             "&TaskUpdate.TaskName=" + form_escape("edited task " + n) +
+                             "&TaskUpdate.TaskDueDate=2030-02-0" + std::to_string(1 + f->n % 9) +
+                             "&TaskUpdate.TaskAssignedTo=" + form_escape("editor" + std::to_string(f->n % 7) + "@bench.local");
+          page(f, 3, "POST", "/Tasks/Edit/" + f->id, edit, 302, [this, f](ev::ClientResult&) {
+            std::string af = "__RequestVerificationToken=" + form_escape(token_);
+            page(f, 4, "POST", "/Tasks/Index?handler=complete&id=" + f->id, af, 302, [this, f, af](ev::ClientResult&) {
+              page(f, 5, "POST", "/Tasks/Index?handler=delete&id=" + f->id, af, 302, [this, f](ev::ClientResult&) {
+                page(f, 6, "GET", "/Tasks/Index", {}, 200, [this, f](ev::ClientResult& r3) {
+                  if (r3.resp.body.find(f->id) != std::string::npos) return fail(f, "the deleted task is still listed");
+                  done_++;
+                  next_flow(f->slot);
+                });
+              });
+            });
+          });
+        });
+      });
+    });
+  }
+
+  void page(const std::shared_ptr<Flow>& f, int p, const char* method, const std::string& path, const std::string& body,
+            int expect, std::function<void(ev::ClientResult&)> then) {
+    double t = ev::now_s();
+    client_.request(*f->ep, method, path, body.empty() && std::string(method) == "GET" ? f->get_h : f->form_h, body, 60,
+                    [this, f, p, t, expect, then = std::move(then)](ev::ClientResult&& r) {
+                      lat_[p].push_back(ev::now_s() - t);
+                      if (!r.err) statuses_[r.resp.status]++;
+                      if (r.err || r.resp.status != expect) {
+                        std::string why = std::string(kNames[p]) + ": " +
+                                          (r.err ? "errno " + std::to_string(r.err)
+                                                 : "HTTP " + std::to_string(r.resp.status) + " " + r.resp.body.substr(0, 160));
+                        return fail(f, why);
+                      }
+                      then(r);
+                    });
+  }
+
+  void fail(const std::shared_ptr<Flow>& f, const std::string& why) {
+    errors_++;
+    if (first_error_.empty()) first_error_ = why;
+    done_++;
+    next_flow(f->slot);
+  }
+};
+constexpr const char* SessionGen::kNames[];
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Opts o;
+  std::string session_token;  // --session <antiforgery token>: the browser-session mode
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -374,6 +539,7 @@ int main(int argc, char** argv) {
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--threads") o.threads = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--session") session_token = next();
     else if (a == "--bodies") {
       std::ifstream in(next());
       o.bodies.clear();
@@ -390,6 +556,14 @@ int main(int argc, char** argv) {
     return 2;
   }
   signal(SIGPIPE, SIG_IGN);
+  if (!session_token.empty()) {
+    ev::Loop loop;
+    SessionGen g(loop, o, session_token);
+    g.start();
+    loop.run();
+    std::printf("%s\n", g.report().c_str());
+    return g.errors() ? 1 : 0;
+  }
   int threads = std::min(o.threads, std::min(o.concurrency, o.batch));
   if (threads <= 1 || o.duration_s > 0 || o.follow) {  // one generator on this thread
     ev::Loop loop;

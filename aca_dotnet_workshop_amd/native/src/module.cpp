@@ -411,6 +411,43 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::bytes(out);
   });
 
+  // The API's read-modify-writes (taskcodec.hpp edit_task / bind_update / task_json): one
+  // native pass each, shared with the app host's native routes.
+  // PUT api/tasks/{id} body -> (name, assigned_to, due) or None (the general binder decides)
+  m.def("task_update_bind", [view](py::bytes body) -> py::object {
+    taskcodec::Update u;
+    if (!taskcodec::bind_update(view(body), u)) return py::none();
+    return py::make_tuple(py::str(u.name), py::str(u.assigned_to), py::str(u.due));
+  });
+  // stored task + the edit -> (document to write back, id, stored assignee) or None.  `update`:
+  // (name, assigned_to, due) from task_update_bind, or None (markcomplete: `complete`)
+  m.def("task_edit", [view](py::bytes stored, bool complete, py::object update) -> py::object {
+    taskcodec::Update u;
+    const taskcodec::Update* up = nullptr;
+    if (!update.is_none()) {
+      auto t = update.cast<py::tuple>();
+      u.name = t[0].cast<std::string>();
+      u.assigned_to = t[1].cast<std::string>();
+      u.due = t[2].cast<std::string>();
+      up = &u;
+    }
+    std::string out, id, old;
+    if (!taskcodec::edit_task(view(stored), up, complete, out, id, old)) return py::none();
+    return py::make_tuple(py::bytes(out), py::str(id), py::str(old));
+  });
+  // stored task -> its TaskModel JSON (GET api/tasks/{id}) or None
+  m.def("task_json", [view](py::bytes stored) -> py::object {
+    std::string out;
+    if (!taskcodec::task_json(view(stored), out)) return py::none();
+    return py::bytes(out);
+  });
+  // (a, b) -> True / False (ASCII case-insensitive equality), None when either is not ASCII
+  m.def("ascii_ieq", [](const std::string& a, const std::string& b) -> py::object {
+    int r = taskcodec::ascii_ieq(a, b);
+    if (r < 0) return py::none();
+    return py::bool_(r == 1);
+  });
+
   // bulk-get answer for a markoverdue page -> (ids marked, conditional bulk-save body, skipped)
   // or None (taskcodec.hpp conditional_mark).
   m.def("tasks_conditional_mark", [](py::bytes got) -> py::object {

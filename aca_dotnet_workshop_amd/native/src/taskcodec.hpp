@@ -426,11 +426,19 @@ inline bool task_fields(const tt::Value& doc, const tt::Value* (&f)[8]) {
   return true;
 }
 
+// PUT api/tasks/{id}'s body bound as TaskUpdateModel (TasksController.cs:48-59; its taskId is
+// not used -- the route's id is): the new name, assignee and due date (canonical text).
+struct Update {
+  std::string name, assigned_to, due = "0001-01-01T00:00:00";
+};
+
 // Canonical TaskModel JSON of `doc` (isOverDue forced true when `overdue`); `due_day` receives
 // the due date's "YYYY-MM-DD".  `store_form`: TaskCreatedOn in the store's round-trip form
-// (format_dt fixed7) -- for a document written back to the store.  false = outside the envelope.
+// (format_dt fixed7) -- for a document written back to the store.  `upd`: the task as
+// UpdateTask leaves it (name, assignee, due date replaced: TasksStoreManager.cs:85-99);
+// `complete`: as MarkTaskCompleted leaves it (:71-81).  false = outside the envelope.
 inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std::string& id, std::string& due_day,
-                       bool store_form = false) {
+                       bool store_form = false, const Update* upd = nullptr, bool complete = false) {
   const tt::Value* f[8];
   if (!task_fields(doc, f)) return false;
   for (int j = 0; j < 6; ++j)
@@ -444,16 +452,20 @@ inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std
   // per-thread scratch: a 19+ character date does not fit the small-string buffer, and this
   // runs once per task of a sweep page
   static thread_local std::string created, due;
-  created.assign("0001-01-01T00:00:00");
+  created.assign(store_form ? "0001-01-01T00:00:00.0000000" : "0001-01-01T00:00:00");  // format_roundtrip(MinValue)
   due.assign("0001-01-01T00:00:00");
   if (f[3] && (created.clear(), !parse_due(f[3]->s, created, store_form))) return false;
-  if (f[4] && (due.clear(), !parse_due(f[4]->s, due))) return false;
+  if (f[4] && (due.clear(), !parse_due(f[4]->s, due))) return false;  // the stored task must bind
+  if (upd) {
+    due.clear();
+    if (!parse_due(upd->due, due)) return false;
+  }
   due_day.assign(due, 0, 10);
   static const std::string empty;
   out += "{\"taskId\":\"";
   out += id;
   out += "\",\"taskName\":";
-  tt::escape_to(out, f[1] ? std::string_view(f[1]->s) : std::string_view(empty));
+  tt::escape_to(out, upd ? std::string_view(upd->name) : f[1] ? std::string_view(f[1]->s) : std::string_view(empty));
   out += ",\"taskCreatedBy\":";
   tt::escape_to(out, f[2] ? std::string_view(f[2]->s) : std::string_view(empty));
   out += ",\"taskCreatedOn\":\"";
@@ -461,13 +473,104 @@ inline bool write_task(const tt::Value& doc, bool overdue, std::string& out, std
   out += "\",\"taskDueDate\":\"";
   out += due;
   out += "\",\"taskAssignedTo\":";
-  tt::escape_to(out, f[5] ? std::string_view(f[5]->s) : std::string_view(empty));
+  tt::escape_to(out, upd ? std::string_view(upd->assigned_to) : f[5] ? std::string_view(f[5]->s) : std::string_view(empty));
   out += ",\"isCompleted\":";
-  out += (f[6] && f[6]->b) ? "true" : "false";
+  out += (complete || (f[6] && f[6]->b)) ? "true" : "false";
   out += ",\"isOverDue\":";
   out += (overdue || (f[7] && f[7]->b)) ? "true" : "false";
   out += '}';
   return true;
+}
+
+// TaskUpdateModel's binder for the bodies it shares with the general one (create's envelope
+// rules: the camelCase names once each, other properties only as strings / booleans / null, no
+// name the general binder would remap); false = let it decide.
+inline bool bind_update(std::string_view body, Update& u) {
+  if (!valid_utf8(body)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse_strict(body);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  if (doc.t != tt::Value::Object) return false;
+  static const char* names[4] = {"taskId", "taskName", "taskDueDate", "taskAssignedTo"};
+  static const char* other[8] = {"task_id", "task_name", "task_due_date", "task_assigned_to",
+                                 "taskid", "taskname", "taskduedate", "taskassignedto"};
+  const tt::Value* f[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (size_t k = 0; k < doc.keys.size(); ++k) {
+    const std::string& key = doc.keys[k];
+    int hit = -1;
+    for (int j = 0; j < 4; ++j)
+      if (key == names[j]) hit = j;
+    if (hit >= 0) {
+      if (f[hit] != nullptr) return false;
+      f[hit] = &doc.items[k];
+      continue;
+    }
+    const tt::Value& x = doc.items[k];
+    if (x.t != tt::Value::String && x.t != tt::Value::Bool && x.t != tt::Value::Null) return false;
+    std::string low(key);
+    for (char& c : low) c = (char)std::tolower((unsigned char)c);
+    for (const char* o : other)
+      if (key == o || low == o) return false;
+  }
+  for (int j = 0; j < 4; ++j)
+    if (f[j] != nullptr && (f[j]->t != tt::Value::String || !valid_utf8(f[j]->s))) return false;
+  if (f[0] != nullptr && !is_guid36(f[0]->s)) return false;  // the Guid binder's text forms are its own
+  u.name = f[1] ? f[1]->s : std::string();
+  u.assigned_to = f[3] ? f[3]->s : std::string();
+  u.due.clear();
+  if (f[2] == nullptr) u.due = "0001-01-01T00:00:00";
+  else if (!parse_due(f[2]->s, u.due)) return false;
+  return true;
+}
+
+// A stored task through one of the API's read-modify-writes (TasksStoreManager.cs:71-99):
+// the document written back (store form) with `upd` / `complete` applied, its id and the stored
+// assignee (for the assignee-change publish).  false = outside the envelope (Python decides).
+inline bool edit_task(std::string_view stored, const Update* upd, bool complete, std::string& out, std::string& id,
+                      std::string& old_assignee) {
+  if (!valid_utf8(stored)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse_strict(stored);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  const tt::Value* f[8];
+  if (!task_fields(doc, f)) return false;
+  old_assignee = f[5] && f[5]->t == tt::Value::String ? f[5]->s : std::string();
+  std::string day;
+  out.clear();
+  return write_task(doc, false, out, id, day, true, upd, complete);
+}
+
+// GET api/tasks/{id}'s answer from the stored document: the TaskModel JSON (to_json).
+inline bool task_json(std::string_view stored, std::string& out) {
+  if (!valid_utf8(stored)) return false;
+  tt::Value doc;
+  try {
+    doc = tt::parse_strict(stored);
+  } catch (const tt::ParseError&) {
+    return false;
+  }
+  std::string id, day;
+  out.clear();
+  return write_task(doc, false, out, id, day);
+}
+
+// ASCII-only case-insensitive equality (str.lower() agrees on ASCII); -1 when either side has
+// other characters (Python compares them).
+inline int ascii_ieq(std::string_view a, std::string_view b) {
+  for (unsigned char c : a)
+    if (c >= 0x80) return -1;
+  for (unsigned char c : b)
+    if (c >= 0x80) return -1;
+  if (a.size() != b.size()) return 0;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (std::tolower((unsigned char)a[i]) != std::tolower((unsigned char)b[i])) return 0;
+  return 1;
 }
 
 inline bool parse_array(std::string_view body, tt::Value& doc) {

@@ -265,6 +265,15 @@ class SidecarClient:
     async def get_state(self, store: str, key: str) -> Any:
         return (await self.get_state_and_etag(store, key))[0]
 
+    async def get_state_raw(self, store: str, key: str) -> tuple[bytes | None, str | None]:
+        """``get_state_and_etag`` without decoding: (the stored JSON text or None, its ETag)."""
+        r = await self._call("GET", f"/v1.0/state/{store}/{quote(key, safe='')}", span_name=f"state get {store}")
+        if r.status == 204 or (r.status == 200 and not r.body):
+            return None, None
+        if r.status >= 300:
+            raise InvocationError(r.status, r.body, f"get state {store}/{key}")
+        return r.body, r.headers.get("etag")
+
     async def get_bulk_state(self, store: str, keys: list[str], parallelism: int = 10) -> list[StateItem]:
         return [StateItem(x["key"], x.get("data"), x.get("etag"))
                 for x in json.loads(await self.get_bulk_state_raw(store, keys, parallelism))]

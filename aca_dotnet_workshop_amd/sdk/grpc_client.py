@@ -339,6 +339,13 @@ class GrpcSidecarClient:
     async def get_state(self, store: str, key: str) -> Any:
         return (await self.get_state_and_etag(store, key))[0]
 
+    async def get_state_raw(self, store: str, key: str) -> tuple[bytes | None, str | None]:
+        """``get_state_and_etag`` without decoding the value: (its JSON text or None, its ETag)."""
+        raw = await self._call_encoded("GetState", P.rt("GetStateRequest")(store_name=store, key=key).SerializeToString(),
+                                       f"state get {store}")
+        r = P.rt("GetStateResponse").FromString(raw)
+        return (r.data, r.etag or None) if r.data else (None, None)
+
     async def get_bulk_state(self, store: str, keys: list[str], parallelism: int = 10) -> list[StateItem]:
         r = await self._call("GetBulkState", P.rt("GetBulkStateRequest")(store_name=store, keys=keys,
                                                                          parallelism=parallelism),

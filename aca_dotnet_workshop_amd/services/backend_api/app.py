@@ -94,9 +94,18 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
                 return _json(body)
         return _json(tasks_to_json(await manager.get_tasks_by_creator(created_by)))
 
+    fast_get = getattr(manager, "get_task_json", None)
+    fast_update = getattr(manager, "update_task_from_body", None)
+    fast_complete = getattr(manager, "mark_task_completed_fast", None)
+
     @app.route("/api/tasks/{taskId}", ("GET",), name="GetTask", tag="Tasks", responses={200: TaskModel, 404: None})
     async def get_task(req: Request) -> Response:
-        t = await manager.get_task_by_id(_task_id(req))
+        tid = _task_id(req)
+        if fast_get is not None:  # the stored document -> TaskModel JSON in one native pass
+            body = await fast_get(tid)
+            if body is not False:
+                return empty(404) if body is None else _json(body)
+        t = await manager.get_task_by_id(tid)
         if t is None:
             return empty(404)
         return _json(t.model_dump_json(by_alias=True).encode())
@@ -133,6 +142,11 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
                responses={200: None, 400: None})
     async def put_task(req: Request) -> Response:
         tid = _task_id(req)
+        ctype = req.content_type
+        if fast_update is not None and (not ctype or "json" in ctype):  # binder + RMW codec, one pass each
+            ok = await fast_update(tid, req.body)
+            if ok is not None:
+                return empty(200) if ok else empty(400)
         m: TaskUpdateModel = await read_model(req, TaskUpdateModel)
         ok = await manager.update_task(tid, m.task_name, m.task_assigned_to, m.task_due_date)
         return empty(200) if ok else empty(400)
@@ -140,7 +154,10 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/tasks/{taskId}/markcomplete", ("PUT",), name="MarkComplete", tag="Tasks",
                responses={200: None, 400: None})
     async def mark_complete(req: Request) -> Response:
-        ok = await manager.mark_task_completed(_task_id(req))
+        tid = _task_id(req)
+        ok = await fast_complete(tid) if fast_complete is not None else None
+        if ok is None:
+            ok = await manager.mark_task_completed(tid)
         return empty(200) if ok else empty(400)
 
     @app.route("/api/tasks/{taskId}", ("DELETE",), name="DeleteTask", tag="Tasks", responses={200: None, 404: None})

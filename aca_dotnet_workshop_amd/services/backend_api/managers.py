@@ -47,6 +47,27 @@ LOG_SAVE_NEW = "Save a new task with name: '%s' to state store"
 LOG_PUBLISH = "Publish Task Saved event for task with Id: '%s' and Name: '%s' for Assignee: '%s'"
 LOG_OVERDUE_PAGE = "Getting open tasks due before: '%s' (page of %d)"
 LOG_MARK_OVERDUE = "Mark task with Id: '%s' as OverDue task"
+LOG_GET = "Getting task with Id: '%s'"
+LOG_COMPLETE = "Mark task with Id: '%s' as completed"
+LOG_UPDATE = "Update task with Id: '%s'"
+LOG_DELETE = "Delete task with Id: '%s'"
+
+_codecs: dict = {}
+
+
+def _codec(name: str):
+    """A task codec of the native module (taskcodec.hpp via module.cpp), or None without it."""
+    if name not in _codecs:
+        try:
+            from ...native import load
+            _codecs[name] = getattr(load(), name)
+        except Exception:
+            _codecs[name] = None
+    return _codecs[name]
+
+
+def _complete(t: TaskModel) -> None:
+    t.is_completed = True
 
 STORE_NAME = "statestore"
 PUBSUB_NAME = "dapr-pubsub-servicebus"
@@ -244,8 +265,12 @@ class TasksStoreManager(TasksManager):
                 "cfg": cfg, "what": what}
 
     async def delete_task(self, task_id) -> bool:
-        log.info("Delete task with Id: '%s'", task_id)
-        data, etag = await self.client.get_state_and_etag(self.store, str(task_id))
+        log.info(LOG_DELETE, task_id)
+        raw_get = getattr(self.client, "get_state_raw", None)
+        if raw_get is not None:  # only the ETag is needed: no decode
+            data, etag = await raw_get(self.store, str(task_id))
+        else:
+            data, etag = await self.client.get_state_and_etag(self.store, str(task_id))
         if data is None:
             return False
         try:
@@ -256,7 +281,7 @@ class TasksStoreManager(TasksManager):
         return True
 
     async def get_task_by_id(self, task_id) -> TaskModel | None:
-        log.info("Getting task with Id: '%s'", task_id)
+        log.info(LOG_GET, task_id)
         data = await self.client.get_state(self.store, str(task_id))
         return TaskModel.model_validate(data) if data is not None else None
 
@@ -303,6 +328,94 @@ class TasksStoreManager(TasksManager):
         made = tasks_from_query_wire(raw, by_created=True, descending=True)
         return made[1] if made is not None else None
 
+    async def get_task_json(self, task_id: uuid.UUID) -> bytes | None | bool:
+        """``get_task_by_id`` as the response body: the stored document turned into the TaskModel
+        JSON in one native pass (``taskcodec.hpp task_json``).  None: no such task; False: a
+        document outside the codec's envelope, or no raw read on this client (bind a TaskModel)."""
+        raw_get = getattr(self.client, "get_state_raw", None)
+        codec = _codec("task_json")
+        if raw_get is None or codec is None:
+            return False
+        log.info(LOG_GET, task_id)
+        raw, _ = await raw_get(self.store, str(task_id))
+        if raw is None:
+            return None
+        made = codec(raw)
+        return made if made is not None else TaskModel.model_validate(json.loads(raw)).to_json().encode()
+
+    @staticmethod
+    def _rmw_body(key: str, etag: str | None, value: bytes) -> bytes:
+        """The ETag-guarded save of a read-modify-write, as ``SidecarClient.save_state(..., etag,
+        concurrency="first-write")`` writes it (the app host's routes send these bytes too)."""
+        item: dict = {"key": key}
+        if etag is not None:
+            item["etag"] = etag
+        item["options"] = {"concurrency": "first-write"}
+        return ("[" + json.dumps(item, separators=(",", ":"))[:-1] + ',"value":').encode() + value + b"}]"
+
+    async def _edit(self, task_id: uuid.UUID, complete: bool, update: tuple | None):
+        """The read-modify-write through the native codec (``taskcodec.hpp edit_task``): the
+        stored document read with its ETag, edited, saved back guarded by that ETag (first-write),
+        re-read and re-applied on a conflict.  (document written, stored assignee); None: no such
+        task; False: the codec or this client cannot take it (the TaskModel path)."""
+        raw_get = getattr(self.client, "get_state_raw", None)
+        save_body = getattr(self.client, "save_state_body", None)
+        edit = _codec("task_edit")
+        if raw_get is None or save_body is None or edit is None:
+            return False
+        key = str(task_id)
+        for _ in range(self.max_retries):
+            raw, etag = await raw_get(self.store, key)
+            if raw is None:
+                return None
+            made = edit(raw, complete, update)
+            if made is None:
+                return False
+            doc, _tid, old = made
+            try:
+                await save_body(self.store, self._rmw_body(key, etag, doc))
+                return doc, old
+            except InvocationError as e:
+                if e.status in (409, 412):
+                    continue  # lost a race: re-read and re-apply
+                raise
+        raise ConcurrencyConflict(f"task {task_id} kept changing under concurrent writers")
+
+    async def mark_task_completed_fast(self, task_id: uuid.UUID) -> bool | None:
+        """``mark_task_completed`` through the native codec; None: take the TaskModel path."""
+        if _codec("task_edit") is None or getattr(self.client, "get_state_raw", None) is None:
+            return None
+        log.info(LOG_COMPLETE, task_id)
+        res = await self._edit(task_id, True, None)
+        if res is False:
+            return (await self._read_modify_write(task_id, _complete)) is not None
+        return res is not None
+
+    async def update_task_from_body(self, task_id: uuid.UUID, body: bytes) -> bool | None:
+        """``update_task`` straight from the request body: TaskUpdateModel bound by the native
+        binder, the read-modify-write through the codec, the assignee-change publish
+        (TasksStoreManager.cs:95-98) with the document written.  None: the body needs the
+        general binder (or no native codec / raw client calls)."""
+        bind = _codec("task_update_bind")
+        if bind is None or _codec("task_edit") is None or getattr(self.client, "get_state_raw", None) is None:
+            return None
+        upd = bind(body)
+        if upd is None:
+            return None
+        log.info(LOG_UPDATE, task_id)
+        res = await self._edit(task_id, False, upd)
+        if res is False:  # a stored document outside the codec's envelope: the TaskModel path
+            from ...models.dotnet import parse_datetime
+            name, who, due = upd
+            return await self._update(task_id, name, who, parse_datetime(due))
+        if res is None:
+            return False
+        doc, old = res
+        if upd[1].lower() != old.lower():
+            log.info(LOG_PUBLISH, task_id, upd[0], upd[1])
+            await self.client.publish_event(self.pubsub, self.topic, doc, content_type="application/json")
+        return True
+
     async def _read_modify_write(self, task_id: uuid.UUID, mutate) -> TaskModel | None:
         for _ in range(self.max_retries):
             data, etag = await self.client.get_state_and_etag(self.store, str(task_id))
@@ -322,15 +435,14 @@ class TasksStoreManager(TasksManager):
         raise ConcurrencyConflict(f"task {task_id} kept changing under concurrent writers")
 
     async def mark_task_completed(self, task_id) -> bool:
-        log.info("Mark task with Id: '%s' as completed", task_id)
-
-        def m(t: TaskModel) -> None:
-            t.is_completed = True
-        return (await self._read_modify_write(task_id, m)) is not None
+        log.info(LOG_COMPLETE, task_id)
+        return (await self._read_modify_write(task_id, _complete)) is not None
 
     async def update_task(self, task_id, task_name, assigned_to, due_date) -> bool:
-        log.info("Update task with Id: '%s'", task_id)
+        log.info(LOG_UPDATE, task_id)
+        return await self._update(task_id, task_name, assigned_to, due_date)
 
+    async def _update(self, task_id, task_name, assigned_to, due_date) -> bool:
         def m(t: TaskModel) -> None:
             t.task_name, t.task_assigned_to, t.task_due_date = task_name, assigned_to, due_date
         res = await self._read_modify_write(task_id, m)

@@ -115,6 +115,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--browser-steps", type=int, default=-1,
                     help="steps of the browser_flow read-path run (create + the 302 followed to Tasks/Index, "
                          "per-user cookies; -1 = a quarter of --steps, 0 = skip)")
+    ap.add_argument("--session-flows", type=int, default=-1,
+                    help="flows of the browser_session run (create, list, Edit GET/POST, Complete, Delete, list; "
+                         "-1 = --batch, 0 = skip)")
     ap.add_argument("--direct-steps", type=int, default=-1,
                     help="steps of the api_sidecar_direct comparison run (-1 = a quarter of --steps, 0 = skip)")
     return ap.parse_args()
@@ -735,6 +738,42 @@ def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str 
     return dt, json.loads(p.stdout.strip().splitlines()[-1])
 
 
+def run_session(exe: str, targets: list[str], cookie: str, token: str, flows: int, conc: int, root: str,
+                ca_file: str | None, batch: int) -> dict:
+    """``ttloadgen --session``: ``flows`` browser sessions, one per in-flight user at a time
+    (create -> list -> Edit GET -> Edit POST -> Complete -> Delete -> list), every page's
+    latency; the flow rate and the per-page p50 / p99 (Pages/Tasks/*.cshtml.cs)."""
+    import subprocess
+    af = "; ".join(c for c in cookie.split("; ") if not c.startswith("TasksCreatedByCookie="))
+    bodies = os.path.join(root, "session-bodies.txt")
+    with open(bodies, "wb") as f:
+        f.write(b"\n".join(_form_bodies(min(batch, 4096), token, 0)) + b"\n")
+    cmd = [exe, "--session", token, "--bodies", bodies, "--header", f"Cookie: TasksCreatedByCookie={{user}}; {af}",
+           "--concurrency", str(conc), "--batch", str(flows), "--steps", "1"]
+    if ca_file:
+        cmd += ["--tls-ca", ca_file]
+    for t in targets:
+        cmd += ["--target", t]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    dt = time.perf_counter() - t0
+    try:
+        rep = json.loads(p.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": f"load generator exit {p.returncode}: {p.stderr[-300:]}"}
+    el = float(rep.get("elapsed_s") or dt)
+    pages = rep.get("pages") or {}
+    create_p99 = (pages.get("create") or {}).get("p99") or 0.0
+    return {"flows_per_s": round(rep.get("flows", 0) / el, 1) if el else None,
+            "pages_per_s": round(7 * rep.get("flows", 0) / el, 1) if el else None,
+            "flows": rep.get("flows"), "errors": rep.get("errors"), "first_error": rep.get("first_error") or None,
+            "concurrency": conc, "latency_ms": {k: [v.get("p50"), v.get("p99")] for k, v in pages.items()},
+            "max_page_p99_over_create_p99": round(max((v.get("p99") or 0.0) for v in pages.values()) / create_p99, 2)
+            if create_p99 else None,
+            "status_counts": rep.get("status_counts"), "loadgen_exit": p.returncode,
+            "flow": "Create, Index, Edit GET/POST (assignee change), Complete, Delete, Index; [p50, p99] ms per page"}
+
+
 def _cpu_by_role(stack) -> dict[str, float]:
     """CPU seconds so far per process role (replicas summed per app)."""
     raw = stack.cpu_seconds()
@@ -1152,7 +1191,7 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
 
 
 def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
-                   protocol: str, wire: dict, alt: dict | None) -> dict:
+                   protocol: str, wire: dict, alt: dict | None, session: dict | None = None) -> dict:
     """The record's key facts in one small object at the head of ``config`` (the driver keeps
     the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
     flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
@@ -1168,6 +1207,8 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
                                                   "tasks_marked_overdue", "errors")}
     if browser:
         s["browser_flows_per_s"] = browser.get("flows_per_s")
+    if session:
+        s["browser_session"] = {k: session.get(k) for k in ("flows_per_s", "errors", "max_page_p99_over_create_p99")}
     if alt:
         s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
                                  if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
@@ -1365,6 +1406,13 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                        "first_error": brep.get("first_error") or None,
                        "tasks_per_user_at_end": round(a.batch * bsteps / BROWSER_USERS, 1),
                        "flow": "POST /Tasks/Create (302) + GET /Tasks/Index"}
+        # the whole browser session at the headline's replica counts: create, list,
+        # Edit GET / POST, Complete, Delete, list -- every UI handler and API route of the reference
+        session = None
+        sflows = 0 if shared else a.session_flows if a.session_flows >= 0 else a.batch
+        if sflows:
+            progress(f"browser_session: {sflows} flows of 7 pages")
+            session = run_session(exe, targets, cookie, token, sflows, conc, root, ca_file, a.batch)
         # the same environment, load straight at the API sidecars' invoke (round 2's topology);
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
@@ -1420,7 +1468,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "threads": threads_all}), file=sys.stderr, flush=True)
-            summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt)
+            summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
@@ -1456,7 +1504,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
-                           "overdue_sweeps": sweep_info, "browser_flow": browser, "api_sidecar_direct": direct,
+                           "overdue_sweeps": sweep_info, "browser_flow": browser, "browser_session": session,
+                           "api_sidecar_direct": direct,
                            "api_protocol_alt": alt, "reference_envelope": envelope}}), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():

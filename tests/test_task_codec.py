@@ -513,3 +513,77 @@ def test_conditional_mark_falls_back_when_the_native_codec_declines():
     items = json.loads(bulk)
     assert [i["key"] for i in items] == ids and all(i["value"]["isOverDue"] for i in items)
     assert [i["etag"] for i in items] == ["0", "2"] and all(i["options"] == {"concurrency": "first-write"} for i in items)
+
+
+# ------------------------------------------------------- the API's read-modify-writes (r6)
+def _update_ref(body: bytes):
+    from aca_dotnet_workshop_amd.models import TaskUpdateModel
+    try:
+        return TaskUpdateModel.model_validate(json.loads(body))
+    except Exception:
+        return None
+
+
+def _check_edit(stored: dict, body: bytes | None) -> None:
+    """task_update_bind / task_edit / task_json against TaskUpdateModel + TaskModel: the same
+    document written back (to_store_json), the same GET answer (to_json)."""
+    from aca_dotnet_workshop_amd.models import format_datetime
+    n = _native()
+    raw = json.dumps(stored, ensure_ascii=False).encode()
+    try:
+        ref = TaskModel.model_validate(stored)
+    except Exception:
+        ref = None
+    got = n.task_json(raw)
+    if got is not None:
+        assert ref is not None and got.decode() == ref.to_json(), (stored, got)
+    done = n.task_edit(raw, True, None)
+    if done is not None:
+        assert ref is not None
+        want = ref.model_copy()
+        want.is_completed = True
+        assert done[0].decode() == want.to_store_json() and done[1] == str(ref.task_id)
+        assert done[2] == ref.task_assigned_to
+    if body is None:
+        return
+    upd = n.task_update_bind(body)
+    m = _update_ref(body)
+    if upd is not None:
+        assert m is not None, body
+        assert (upd[0], upd[1]) == (m.task_name, m.task_assigned_to) and upd[2] == format_datetime(m.task_due_date)
+        made = n.task_edit(raw, False, upd)
+        if made is not None:
+            assert ref is not None
+            want = ref.model_copy()
+            want.task_name, want.task_assigned_to, want.task_due_date = m.task_name, m.task_assigned_to, m.task_due_date
+            assert made[0].decode() == want.to_store_json(), (stored, body)
+
+
+_UPD = {"taskId": "0f8fad5b-d9cb-469f-a165-70867728950e", "taskName": "edited ✓ 'q' \"x\"",
+        "taskDueDate": "2030-02-01T00:00:00", "taskAssignedTo": "Other@x"}
+
+
+@pytest.mark.parametrize("stored", [_TASK, {**_TASK, "taskId": _TASK["taskId"].upper(), "isOverDue": True},
+                                    {**_TASK, "taskCreatedOn": "2030-01-01T00:00:00Z", "taskDueDate": "2030-01-02"},
+                                    {"taskName": "defaults only"}, {**_TASK, "extra": "x"}])
+@pytest.mark.parametrize("body", [_UPD, {**_UPD, "taskDueDate": "2030-02-01"}, {"taskName": "only a name"},
+                                  {**_UPD, "taskDueDate": "2030-02-01T10:11:12.5Z", "x": None}])
+def test_rmw_codecs_match_the_models(stored, body):
+    _check_edit(stored, json.dumps(body, ensure_ascii=False).encode())
+    assert _native().task_update_bind(json.dumps(body).encode()) is not None
+
+
+@pytest.mark.parametrize("body", [b"[]", b'{"taskname":"x"}', b'{"task_name":"x"}', b'{"taskDueDate":"2030-02-30"}',
+                                  b'{"taskId":"nope"}', b'{"taskName":1}', b'{"taskDueDate":"2030-02-01T00:00:00+02:00"}'])
+def test_update_bind_declines_what_it_does_not_decide(body):
+    assert _native().task_update_bind(body) is None
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.dictionaries(st.sampled_from(list(_TASK) + ["x"]), st.one_of(_text, st.booleans(), _date, st.uuids().map(str)),
+                       max_size=8),
+       st.dictionaries(st.sampled_from(list(_UPD) + ["y"]), st.one_of(_text, st.booleans(), _date, st.uuids().map(str)),
+                       max_size=5))
+def test_rmw_codecs_fuzz(stored, body):
+    _check_edit(stored, json.dumps(body).encode())
+    _check_edit(stored, json.dumps(body, ensure_ascii=False).encode())
