@@ -260,8 +260,11 @@ inline bool cookie_value(std::string_view cookie, std::string_view name, std::st
 struct NativeRoute {
   enum Kind {
     kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6,
-    kApiMarkOverdue = 7
+    kApiMarkOverdue = 7, kApiGet = 8, kApiUpdate = 9, kApiComplete = 10, kApiDelete = 11
   };
+  // a path with an "{id}" segment (api/tasks/{id}[/markcomplete]) matches a canonical lower-case
+  // GUID there (the route's key); other spellings (upper case, braces) are Python's
+  bool pattern = false;
   int id = 0;
   int kind = 0;
   std::string method, path;
@@ -302,6 +305,14 @@ struct NativeRoute {
   std::string bulk_target;
   Template log_mark;
   int max_retries = 5, parallelism = 10;
+  // kApiGet / kApiUpdate / kApiComplete / kApiDelete (TasksController.cs:26-75 over
+  // TasksStoreManager.cs:40-99): the state read (get_target + key over HTTP), the ETag-guarded
+  // save (save_target), the delete (delete_target + key), the assignee-change publish
+  // (publish_target); `log_op`: the operation's log line (field: id), `missing`: the answer for a
+  // task that is not there (404 / 400)
+  std::string get_target, delete_target;
+  Template log_op;
+  int missing = 404;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -513,6 +524,10 @@ class AppHost {
     else if (kind == "api_list") r->kind = NativeRoute::kApiList;
     else if (kind == "api_overdue") r->kind = NativeRoute::kApiOverdue;
     else if (kind == "api_markoverdue") r->kind = NativeRoute::kApiMarkOverdue;
+    else if (kind == "api_get") r->kind = NativeRoute::kApiGet;
+    else if (kind == "api_update") r->kind = NativeRoute::kApiUpdate;
+    else if (kind == "api_complete") r->kind = NativeRoute::kApiComplete;
+    else if (kind == "api_delete") r->kind = NativeRoute::kApiDelete;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -530,8 +545,8 @@ class AppHost {
     r->log_prefix = get("log_prefix");
     r->bounds = bounds;
     if (get("protocol") == "grpc") {
-      if (r->kind != NativeRoute::kApiCreate && r->kind != NativeRoute::kApiList && r->kind != NativeRoute::kApiOverdue &&
-          r->kind != NativeRoute::kApiMarkOverdue)
+      if (r->kind == NativeRoute::kFrontendCreate || r->kind == NativeRoute::kFrontendList ||
+          r->kind == NativeRoute::kProcessorNotify)
         throw std::invalid_argument("only the API's store routes speak gRPC");
       r->grpc = true;
       r->store = get("store");
@@ -566,6 +581,23 @@ class AppHost {
       if (r->query_target.empty() || get("query").empty() || r->page_default.empty() || r->more_header.empty() ||
           get("log_overdue").empty())
         throw std::invalid_argument("api_overdue needs its query, page size, log template and header");
+    } else if (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kApiDelete) {
+      r->get_target = get("get_target");
+      r->delete_target = get("delete_target");
+      r->log_op = Template::compile(get("log_op"), get("log_op_args"), {"id"});
+      if (!get("max_retries").empty()) r->max_retries = std::stoi(get("max_retries"));
+      if (!get("missing").empty()) r->missing = std::stoi(get("missing"));
+      if (r->kind == NativeRoute::kApiUpdate) {
+        r->log_publish = Template::compile(get("log_publish"), get("log_publish_args"));
+        if (get("log_publish").empty() || r->publish_target.empty())
+          throw std::invalid_argument("api_update needs the publish target and the manager's log template");
+      }
+      if (r->get_target.empty() || get("log_op").empty() ||
+          ((r->kind == NativeRoute::kApiUpdate || r->kind == NativeRoute::kApiComplete) && r->save_target.empty()) ||
+          (r->kind == NativeRoute::kApiDelete && r->delete_target.empty()) || r->path.find("{id}") == std::string::npos)
+        throw std::invalid_argument("a task route needs its targets, its log template and an {id} path");
+      if (r->grpc && r->store.empty()) throw std::invalid_argument("a gRPC task route needs its store");
+      r->pattern = true;
     } else if (r->kind == NativeRoute::kApiMarkOverdue) {
       r->bulk_target = get("bulk_target");
       r->log_mark = Template::compile(get("log_mark"), get("log_mark_args"), {"id"});
@@ -755,6 +787,9 @@ class AppHost {
     ev::HeaderList grpc_md;      // gRPC routes: traceparent, token (the SDK's call metadata)
     std::vector<std::string> pending;  // kApiMarkOverdue: the ids this pass reads
     int pass = 0;
+    std::string key;                   // task routes: the {id} of the path
+    ::taskcodec::Update upd;           // kApiUpdate: the bound body
+    ev::HeaderList plain_headers;      // HTTP GET / DELETE: traceparent, token (no content type)
     ::taskcodec::Created task;
   };
 
@@ -977,6 +1012,162 @@ class AppHost {
     });
   }
 
+  // The {id} of `path` under the route's `pattern` (one "{id}" segment), when it is a canonical
+  // lower-case GUID -- the text uuid.UUID(...) prints back, so logs and keys agree; else "".
+  static std::string path_key(std::string_view pattern, std::string_view path) {
+    size_t at = pattern.find("{id}");
+    if (at == std::string_view::npos) return {};
+    std::string_view pre = pattern.substr(0, at), post = pattern.substr(at + 4);
+    if (path.size() != pre.size() + 36 + post.size() || path.substr(0, pre.size()) != pre ||
+        path.substr(pre.size() + 36) != post)
+      return {};
+    std::string_view g = path.substr(pre.size(), 36);
+    for (size_t i = 0; i < 36; ++i) {
+      char c = g[i];
+      bool dash = i == 8 || i == 13 || i == 18 || i == 23;
+      if (dash ? c != '-' : !((c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'))) return {};
+    }
+    return std::string(g);
+  }
+
+  // kApiGet / kApiUpdate / kApiComplete / kApiDelete: the API's single-task routes
+  // (services/backend_api/app.py get_task / put_task / mark_complete / delete_task over the
+  // manager's get_task_json / update_task_from_body / mark_task_completed_fast / delete_task):
+  // the same codec passes, sidecar calls, log lines and answers.
+  bool api_task(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const NativeRoute& r = *j->route;
+    std::string_view path(m.target);
+    path = path.substr(0, path.find('?'));
+    j->key = path_key(r.path, path);
+    if (j->key.empty()) return false;
+    if (r.kind == NativeRoute::kApiUpdate) {
+      const std::string ctype = media_type(m);
+      if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
+      if (!::taskcodec::bind_update(m.body, j->upd)) return false;  // the general binder's
+    }
+    log_event(r, *j, r.log_op.render_with([&](int) -> const std::string& { return j->key; }));
+    native_inflight_.fetch_add(1);
+    loop_.defer([this, j] { task_read(j); });  // once the request is the job's
+    return true;
+  }
+
+  // The stored task with its ETag (HTTP GET state / gRPC GetState), then the route's step.
+  void task_read(const std::shared_ptr<NativeJob>& j) {
+    const NativeRoute& r = *j->route;
+    if (r.kind != NativeRoute::kApiGet && r.kind != NativeRoute::kApiDelete && j->pass++ >= r.max_retries)
+      return decline(*j);  // kept conflicting: Python's ConcurrencyConflict path decides
+    auto then = [this, j](std::string&& data, std::string&& etag) {
+      const NativeRoute& r = *j->route;
+      if (data.empty()) return finish(*j, r.missing, {});
+      switch (r.kind) {
+        case NativeRoute::kApiGet: {
+          std::string out;
+          if (!::taskcodec::task_json(data, out)) return decline(*j);
+          return finish(*j, r.status, {{"Content-Type", r.content_type}}, out);
+        }
+        case NativeRoute::kApiDelete: return task_delete(j, etag);
+        default: return task_write(j, data, etag);
+      }
+    };
+    if (r.grpc) {
+      pb::Writer w;  // GetStateRequest {store_name = 1, key = 2}
+      w.str(1, r.store);
+      w.str(2, j->key);
+      call_step(j, "get", r.get_target, std::move(w.s), false, [then](std::string&& msg) mutable {
+        pb::Reader rd(msg);  // GetStateResponse {data = 1, etag = 2}
+        uint32_t f, wt;
+        std::string_view v, data, etag;
+        while (rd.next(f, wt)) {
+          if (f == 1 && wt == pb::LEN && rd.bytes(v)) data = v;
+          else if (f == 2 && wt == pb::LEN && rd.bytes(v)) etag = v;
+          else if (!rd.skip(wt)) break;
+        }
+        then(std::string(data), std::string(etag));
+      });
+      return;
+    }
+    client_.request(r.sidecar, "GET", r.get_target + j->key, j->plain_headers, {}, r.timeout_s,
+                    [this, j, then](ev::ClientResult&& res) mutable {
+                      if (res.err || res.resp.status >= 300) return hand_over(*j, "get", res);
+                      const std::string* e = res.resp.header("etag");
+                      then(res.resp.status == 204 ? std::string() : std::move(res.resp.body), e ? std::string(*e) : "");
+                    });
+  }
+
+  // markcomplete / update: the edited document saved back under the ETag it was read with
+  // (first-write), re-read and re-applied on a conflict; an update that changed the assignee
+  // (compared like str.lower(); other than ASCII: Python decides) publishes the document.
+  void task_write(const std::shared_ptr<NativeJob>& j, const std::string& data, const std::string& etag) {
+    const NativeRoute& r = *j->route;
+    const bool update = r.kind == NativeRoute::kApiUpdate;
+    std::string doc, id, old;
+    if (!::taskcodec::edit_task(data, update ? &j->upd : nullptr, !update, doc, id, old)) return decline(*j);
+    bool publish = false;
+    if (update) {
+      int same = ::taskcodec::ascii_ieq(j->upd.assigned_to, old);
+      if (same < 0) return decline(*j);
+      publish = same == 0;
+    }
+    // TasksStoreManager._rmw_body: SidecarClient.save_state's body with the ETag and options
+    std::string body = "[{\"key\":";
+    tt::escape_to(body, j->key);
+    if (!etag.empty()) {
+      body += ",\"etag\":";
+      tt::escape_to(body, etag);
+    }
+    body += ",\"options\":{\"concurrency\":\"first-write\"},\"value\":";
+    body += doc;
+    body += "}]";
+    std::string msg;
+    if (r.grpc && !daprpb::save_state_bulk(r.store, body, msg)) return decline(*j);
+    auto saved = [this, j, publish, doc](std::string&&) {
+      const NativeRoute& r = *j->route;
+      if (!publish) return finish(*j, r.status, {});
+      log_event(r, *j, r.log_publish.render(j->key, j->upd.name, j->upd.assigned_to));
+      std::string pub = r.grpc ? daprpb::publish_event(r.pubsub, r.topic, doc, "application/json") : doc;
+      call_step(j, "publish", r.publish_target, std::move(pub), true,
+                [this, j](std::string&&) { finish(*j, j->route->status, {}); });
+    };
+    call_step(j, "save", r.save_target, r.grpc ? std::move(msg) : std::move(body), false, std::move(saved),
+              [this, j](int status) {  // lost a race: re-read and re-apply
+                if (status != 409 && status != 412) return false;
+                task_read(j);
+                return true;
+              });
+  }
+
+  // delete: guarded by the ETag read; a concurrent change or delete (409 / 412) is fine -- the
+  // task is gone or changed, as TasksStoreManager.delete_task treats it
+  void task_delete(const std::shared_ptr<NativeJob>& j, const std::string& etag) {
+    const NativeRoute& r = *j->route;
+    if (r.grpc) {
+      pb::Writer w, et;  // DeleteStateRequest {store_name = 1, key = 2, etag = 3 {value = 1}}
+      w.str(1, r.store);
+      w.str(2, j->key);
+      if (!etag.empty()) {
+        et.str(1, etag);
+        w.len_field(3, et.s);
+      }
+      call_step(j, "delete", r.delete_target, std::move(w.s), false,
+                [this, j](std::string&&) { finish(*j, j->route->status, {}); },
+                [this, j](int status) {
+                  if (status != 409 && status != 412) return false;
+                  finish(*j, j->route->status, {});
+                  return true;
+                });
+      return;
+    }
+    ev::HeaderList h = j->plain_headers;
+    if (!etag.empty()) h.emplace_back("If-Match", etag);
+    client_.request(r.sidecar, "DELETE", r.delete_target + j->key, h, {}, r.timeout_s,
+                    [this, j](ev::ClientResult&& res) {
+                      if (!res.err && (res.resp.status < 300 || res.resp.status == 409 || res.resp.status == 412))
+                        return finish(*j, j->route->status, {});
+                      hand_over(*j, "delete", res);
+                    },
+                    false);
+  }
+
   // kApiList (services/backend_api/app.py get_tasks + TasksStoreManager.tasks_by_creator_json)
   bool api_list(const std::shared_ptr<NativeJob>& j, const Message& m) {
     const NativeRoute& r = *j->route;
@@ -1076,7 +1267,8 @@ class AppHost {
     }
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
     if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList ||
-        r->kind == NativeRoute::kApiOverdue || r->kind == NativeRoute::kApiMarkOverdue) {
+        r->kind == NativeRoute::kApiOverdue || r->kind == NativeRoute::kApiMarkOverdue ||
+        (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kApiDelete)) {
       auto j = std::make_shared<NativeJob>();
       j->route = r;
       j->server = server;
@@ -1088,10 +1280,13 @@ class AppHost {
       if (!r->token.empty()) j->out_headers.emplace_back("dapr-api-token", r->token);
       j->out_headers.emplace_back("Content-Type", "application/json");
       if (r->grpc) grpc_metadata(*j);
-      bool taken = r->kind == NativeRoute::kFrontendList ? frontend_list(j, m)
-                   : r->kind == NativeRoute::kApiList    ? api_list(j, m)
-                   : r->kind == NativeRoute::kApiOverdue ? api_overdue(j, m)
-                                                         : api_markoverdue(j, m);
+      j->plain_headers.emplace_back("traceparent", j->traceparent);
+      if (!r->token.empty()) j->plain_headers.emplace_back("dapr-api-token", r->token);
+      bool taken = r->kind == NativeRoute::kFrontendList     ? frontend_list(j, m)
+                   : r->kind == NativeRoute::kApiList        ? api_list(j, m)
+                   : r->kind == NativeRoute::kApiOverdue     ? api_overdue(j, m)
+                   : r->kind == NativeRoute::kApiMarkOverdue ? api_markoverdue(j, m)
+                                                             : api_task(j, m);
       if (!taken) return false;
       j->req = std::move(m);
       j->reply = std::move(reply);
@@ -1296,7 +1491,7 @@ class AppHost {
           std::string_view path(m.target);
           path = path.substr(0, path.find('?'));
           for (auto& r : rit->second)
-            if (r->method == m.method && r->path == path) {
+            if (r->method == m.method && (r->pattern ? !path_key(r->path, path).empty() : r->path == path)) {
               if (serve_native(r, server, m, reply)) return;
               break;
             }

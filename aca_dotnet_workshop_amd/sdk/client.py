@@ -413,7 +413,7 @@ def b64(data: bytes) -> str:
     return base64.b64encode(data).decode()
 
 
-def native_route_failure(req: Any, what: dict[str, str]) -> BaseException | None:
+def native_route_failure(req: Any, what: dict[str, str], key: str | None = None) -> BaseException | None:
     """The error a native route handed over (``fail <step> <status> <base64 body>`` or ``err
     <step> <errno>`` in ``req.state["tt_native"]``, set by web/native_host.py only) as the
     exception this SDK raises for that call (``what``: the step's InvocationError message), or
@@ -422,6 +422,8 @@ def native_route_failure(req: Any, what: dict[str, str]) -> BaseException | None
     if not note or note == "sample":
         return None
     parts = note.split(" ")
+    if key is not None and len(parts) >= 2 and "{key}" in what.get(parts[1], ""):
+        what = {**what, parts[1]: what[parts[1]].replace("{key}", key)}
     if len(parts) >= 3 and parts[1] in what and parts[1] != "protocol":
         if parts[0] == "fail":
             import base64

@@ -97,9 +97,25 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     fast_get = getattr(manager, "get_task_json", None)
     fast_update = getattr(manager, "update_task_from_body", None)
     fast_complete = getattr(manager, "mark_task_completed_fast", None)
+    task_routes = getattr(manager, "native_task_routes", None)
+    task_what: dict[str, dict] = {}
+    for spec in (task_routes() if task_routes is not None and os.environ.get("TT_READ_PATH", "").lower() != "bind"
+                 else []):
+        # GET / PUT / PUT markcomplete / DELETE api/tasks/{id} on the app host's I/O thread: the
+        # same codec passes, sidecar calls, log lines and answers as the handlers below
+        task_what[spec["kind"]] = spec.pop("what")
+        spec["cfg"].update({"status": 200, "content_type": "application/json; charset=utf-8"})
+        app.services.setdefault("native_routes", []).append(spec)
+
+    def _failed(req: Request, kind: str) -> None:
+        what = task_what.get(kind)
+        failed = native_route_failure(req, what, req.path_params.get("taskId")) if what else None
+        if failed is not None:  # the native route's sidecar call failed: the SDK's error
+            raise failed
 
     @app.route("/api/tasks/{taskId}", ("GET",), name="GetTask", tag="Tasks", responses={200: TaskModel, 404: None})
     async def get_task(req: Request) -> Response:
+        _failed(req, "api_get")
         tid = _task_id(req)
         if fast_get is not None:  # the stored document -> TaskModel JSON in one native pass
             body = await fast_get(tid)
@@ -141,6 +157,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/tasks/{taskId}", ("PUT",), name="UpdateTask", tag="Tasks", body=TaskUpdateModel,
                responses={200: None, 400: None})
     async def put_task(req: Request) -> Response:
+        _failed(req, "api_update")
         tid = _task_id(req)
         ctype = req.content_type
         if fast_update is not None and (not ctype or "json" in ctype):  # binder + RMW codec, one pass each
@@ -154,6 +171,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
     @app.route("/api/tasks/{taskId}/markcomplete", ("PUT",), name="MarkComplete", tag="Tasks",
                responses={200: None, 400: None})
     async def mark_complete(req: Request) -> Response:
+        _failed(req, "api_complete")
         tid = _task_id(req)
         ok = await fast_complete(tid) if fast_complete is not None else None
         if ok is None:
@@ -162,6 +180,7 @@ def register_controllers(app: WebApp, manager: TasksManager) -> None:
 
     @app.route("/api/tasks/{taskId}", ("DELETE",), name="DeleteTask", tag="Tasks", responses={200: None, 404: None})
     async def delete_task(req: Request) -> Response:
+        _failed(req, "api_delete")
         ok = await manager.delete_task(_task_id(req))
         return empty(200) if ok else empty(404)
 

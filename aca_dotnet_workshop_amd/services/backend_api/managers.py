@@ -237,7 +237,8 @@ class TasksStoreManager(TasksManager):
         grpc = ep.get("protocol") == "grpc"
         what: dict[str, str] = {}
         http_what = {"save": f"save state {self.store}", "publish": f"publish {self.pubsub}/{self.topic}",
-                     "query": f"query state {self.store}", "bulk": f"bulk get {self.store}"}
+                     "query": f"query state {self.store}", "bulk": f"bulk get {self.store}",
+                     "get": f"get state {self.store}", "delete": f"delete state {self.store}"}
         for step, (path, rpc) in targets.items():
             cfg[f"{step}_target"] = P.method_path(rpc) if grpc else ep["prefix"] + path
             what[step] = rpc if grpc else http_what[step]
@@ -512,6 +513,34 @@ class TasksStoreManager(TasksManager):
                     "log_overdue_args": "midnight,page"})
         return {"kind": "api_overdue", "method": "GET", "path": "/api/overduetasks", "route": "/api/overduetasks",
                 "cfg": cfg, "what": what}
+
+    def native_task_routes(self) -> list[dict]:
+        """The single-task routes on the app host's I/O thread (apphost.hpp ``api_task``): GET /
+        PUT / PUT markcomplete / DELETE ``api/tasks/{id}`` -- this manager's codec passes
+        (``get_task_json``, ``update_task_from_body``, ``mark_task_completed_fast``,
+        ``delete_task``), log lines, ETag-guarded saves and the assignee-change publish, over the
+        client's protocol.  Empty when this client cannot take them.  A ``what`` holding
+        ``{key}`` is filled with the request's task id (the HTTP SDK's messages name the key)."""
+        ep = self._native_endpoint()
+        if ep is None or getattr(self.client, "get_state_raw", None) is None or _codec("task_edit") is None:
+            return []
+        routes = []
+        for kind, method, path, log_op, missing in (("api_get", "GET", "/api/tasks/{id}", LOG_GET, 404),
+                                                    ("api_update", "PUT", "/api/tasks/{id}", LOG_UPDATE, 400),
+                                                    ("api_complete", "PUT", "/api/tasks/{id}/markcomplete", LOG_COMPLETE, 400),
+                                                    ("api_delete", "DELETE", "/api/tasks/{id}", LOG_DELETE, 404)):
+            cfg, what = self._native_calls(ep, get=(f"/v1.0/state/{self.store}/", "GetState"),
+                                           save=(f"/v1.0/state/{self.store}", "SaveState"),
+                                           publish=(f"/v1.0/publish/{self.pubsub}/{self.topic}", "PublishEvent"),
+                                           delete=(f"/v1.0/state/{self.store}/", "DeleteState"))
+            if ep.get("protocol") != "grpc":  # the HTTP SDK's messages name the key
+                what.update({"get": f"get state {self.store}/{{key}}", "delete": f"delete state {self.store}/{{key}}"})
+            cfg.update({"store": self.store, "log_category": log.name, "log_op": log_op, "log_op_args": "id",
+                        "max_retries": self.max_retries, "missing": missing, "log_publish": LOG_PUBLISH,
+                        "log_publish_args": "id,name,assigned_to"})
+            route = path.replace("{id}", "{taskId}")
+            routes.append({"kind": kind, "method": method, "path": path, "route": route, "cfg": cfg, "what": what})
+        return routes
 
     def native_markoverdue_route(self) -> dict | None:
         """``mark_overdue_from_body`` as a native route of the app host (apphost.hpp
