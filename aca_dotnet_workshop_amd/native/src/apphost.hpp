@@ -260,7 +260,8 @@ inline bool cookie_value(std::string_view cookie, std::string_view name, std::st
 struct NativeRoute {
   enum Kind {
     kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6,
-    kApiMarkOverdue = 7, kApiGet = 8, kApiUpdate = 9, kApiComplete = 10, kApiDelete = 11
+    kApiMarkOverdue = 7, kApiGet = 8, kApiUpdate = 9, kApiComplete = 10, kApiDelete = 11,
+    kFrontendEditGet = 12, kFrontendEdit = 13, kFrontendIndexPost = 14
   };
   // a path with an "{id}" segment (api/tasks/{id}[/markcomplete]) matches a canonical lower-case
   // GUID there (the route's key); other spellings (upper case, braces) are Python's
@@ -313,6 +314,12 @@ struct NativeRoute {
   std::string get_target, delete_target;
   Template log_op;
   int missing = 404;
+  // kFrontendEditGet: GET Tasks/Edit/{id} -> invoke GET api/tasks/{id} -> the Edit page from the
+  // template's pieces (slots af_token, task_id, task_name, task_assigned_to, due);
+  // kFrontendEdit: POST Tasks/Edit/{id} -> invoke PUT api/tasks/{id} -> 302; kFrontendIndexPost:
+  // POST Tasks/Index?handler=complete|delete&id= -> invoke PUT .../markcomplete | DELETE -> 302.
+  // `invoke_target`: the API's invoke prefix (".../method/api/tasks/")
+  Pieces edit_page;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
@@ -528,6 +535,9 @@ class AppHost {
     else if (kind == "api_update") r->kind = NativeRoute::kApiUpdate;
     else if (kind == "api_complete") r->kind = NativeRoute::kApiComplete;
     else if (kind == "api_delete") r->kind = NativeRoute::kApiDelete;
+    else if (kind == "frontend_edit_get") r->kind = NativeRoute::kFrontendEditGet;
+    else if (kind == "frontend_edit") r->kind = NativeRoute::kFrontendEdit;
+    else if (kind == "frontend_index_post") r->kind = NativeRoute::kFrontendIndexPost;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -546,7 +556,7 @@ class AppHost {
     r->bounds = bounds;
     if (get("protocol") == "grpc") {
       if (r->kind == NativeRoute::kFrontendCreate || r->kind == NativeRoute::kFrontendList ||
-          r->kind == NativeRoute::kProcessorNotify)
+          r->kind == NativeRoute::kProcessorNotify || r->kind >= NativeRoute::kFrontendEditGet)
         throw std::invalid_argument("only the API's store routes speak gRPC");
       r->grpc = true;
       r->store = get("store");
@@ -581,6 +591,16 @@ class AppHost {
       if (r->query_target.empty() || get("query").empty() || r->page_default.empty() || r->more_header.empty() ||
           get("log_overdue").empty())
         throw std::invalid_argument("api_overdue needs its query, page size, log template and header");
+    } else if (r->kind >= NativeRoute::kFrontendEditGet) {
+      if (r->invoke_target.empty() || r->af_key.empty() || r->af_cookie.empty())
+        throw std::invalid_argument("a frontend page route needs its invoke target and antiforgery settings");
+      if (r->kind == NativeRoute::kFrontendEditGet)
+        r->edit_page = Pieces::parse(get("page"), {"af_token", "task_id", "task_name", "task_assigned_to", "due"});
+      if (r->kind != NativeRoute::kFrontendIndexPost) {
+        if (r->path.find("{id}") == std::string::npos) throw std::invalid_argument("an Edit route needs an {id} path");
+        r->pattern = true;
+      }
+      if (r->kind != NativeRoute::kFrontendEditGet) r->location = Template::compile(get("location"), "");
     } else if (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kApiDelete) {
       r->get_target = get("get_target");
       r->delete_target = get("delete_target");
@@ -1012,6 +1032,112 @@ class AppHost {
     });
   }
 
+  // kFrontendEditGet / kFrontendEdit / kFrontendIndexPost (services/frontend/app.py edit_get /
+  // edit_post / tasks_index_post): the same cookies, antiforgery check and form binding
+  // (formcodec.hpp), the same invoke through the sidecar, the same page or 302.  What they do not
+  // decide -- no identity, a new antiforgery cookie, a bad token, a binding error, an answer
+  // outside the page's shape, a failed invoke -- is the page's.
+  bool frontend_page(const std::shared_ptr<NativeJob>& j, const Message& m) {
+    const NativeRoute& r = *j->route;
+    const std::string* cookie = header(m, "cookie");
+    std::string_view path(m.target);
+    path = path.substr(0, path.find('?'));
+    if (r.kind == NativeRoute::kFrontendEditGet) {
+      std::string who, af;
+      if (!cookie || !cookie_value(*cookie, r.id_cookie, who) || who.empty() || !cookie_value(*cookie, r.af_cookie, af) ||
+          af.empty())
+        return false;  // a redirect to the landing page, or a new antiforgery cookie: the page's
+      j->key = path_key(r.path, path);
+      if (j->key.empty()) return false;
+      std::string token = ::formcodec::hmac_sha256_hex(r.af_key, af);
+      native_inflight_.fetch_add(1);
+      client_.request(r.sidecar, "GET", r.invoke_target + j->key, j->plain_headers, {}, r.timeout_s,
+                      [this, j, token = std::move(token)](ev::ClientResult&& res) {
+                        if (res.err || res.resp.status >= 300) return hand_over(*j, "invoke", res);
+                        std::string page;
+                        if (!edit_page_html(*j->route, res.resp.body, token, j->key, page)) return decline(*j);
+                        finish(*j, j->route->status, {{"Content-Type", j->route->content_type}}, page);
+                      });
+      return true;
+    }
+    const std::string_view ck = cookie ? std::string_view(*cookie) : std::string_view();
+    std::string method = "PUT", target, body;
+    if (r.kind == NativeRoute::kFrontendEdit) {
+      std::string pid = path_key(r.path, path), id;
+      if (pid.empty()) return false;
+      if (::formcodec::edit_task(m.body, ck, r.af_key, r.af_cookie, pid, body, id) != ::formcodec::Verdict::kOk)
+        return false;
+      target = r.invoke_target + id;
+    } else {
+      if (::formcodec::index_post(m.body, ck, r.af_key, r.af_cookie) != ::formcodec::Verdict::kOk) return false;
+      std::string handler, id;
+      if (!query_param(m.target, "handler", handler) || !query_param(m.target, "id", id)) return false;
+      for (auto& c : handler) c = ::tt::ascii_lower(c);
+      if (!::taskcodec::is_guid36(id)) return false;  // is_guid's other spellings: the page's
+      if (handler == "complete") target = r.invoke_target + id + "/markcomplete";
+      else if (handler == "delete") method = "DELETE", target = r.invoke_target + id;
+      else return false;  // an unknown handler: the page's 400
+    }
+    native_inflight_.fetch_add(1);
+    auto done = [this, j](ev::ClientResult&& res) {
+      if (res.err || res.resp.status >= 300) return hand_over(*j, "invoke", res);
+      finish(*j, j->route->status, {{"Location", j->route->location.render({}, {}, {})}});
+    };
+    if (body.empty()) client_.request(r.sidecar, method, target, j->plain_headers, {}, r.timeout_s, std::move(done), false);
+    else client_.request(r.sidecar, method, target, j->out_headers, body, r.timeout_s, std::move(done), false);
+    return true;
+  }
+
+  // The Edit page for the API's TaskModel answer (edit_get's values: the id, name, assignee and
+  // the due date's calendar day for the date input), or false outside the plain shape.
+  static bool edit_page_html(const NativeRoute& r, const std::string& body, const std::string& token,
+                             const std::string& key, std::string& out) {
+    if (body.empty()) return false;  // no such task: the page's 404
+    tt::Value d;
+    try {
+      d = tt::parse(body);
+    } catch (const std::exception&) {
+      return false;
+    }
+    if (d.t != tt::Value::Object) return false;
+    const tt::Value *id = d.get("taskId"), *name = d.get("taskName"), *who = d.get("taskAssignedTo"),
+                    *due = d.get("taskDueDate");
+    if (!id || id->t != tt::Value::String || id->s != key || !name || name->t != tt::Value::String || !who ||
+        who->t != tt::Value::String || !due || due->t != tt::Value::String)
+      return false;
+    // yyyy-MM-ddTHH:mm:ss[.f{1,7}][Z] (UTC or unspecified: the calendar day is the text's own)
+    const std::string& t = due->s;
+    auto dig = [&](size_t a, size_t n) {
+      if (a + n > t.size()) return false;
+      for (size_t i = a; i < a + n; ++i)
+        if (t[i] < '0' || t[i] > '9') return false;
+      return true;
+    };
+    if (t.size() < 19 || !dig(0, 4) || t[4] != '-' || !dig(5, 2) || t[7] != '-' || !dig(8, 2) || t[10] != 'T' ||
+        !dig(11, 2) || t[13] != ':' || !dig(14, 2) || t[16] != ':' || !dig(17, 2))
+      return false;
+    size_t k = 19;
+    if (k < t.size() && t[k] == '.') {
+      size_t f = k + 1;
+      while (f < t.size() && t[f] >= '0' && t[f] <= '9') ++f;
+      if (f - k - 1 < 1 || f - k - 1 > 7) return false;
+      k = f;
+    }
+    if (k < t.size() && t[k] == 'Z') ++k;
+    if (k != t.size()) return false;
+    out.reserve(8192);
+    r.edit_page.render(out, [&](int slot, std::string& o) {
+      switch (slot) {
+        case 0: o += token; break;
+        case 1: o += key; break;
+        case 2: html_escape_to(o, name->s); break;
+        case 3: html_escape_to(o, who->s); break;
+        default: o.append(t, 0, 10);
+      }
+    });
+    return true;
+  }
+
   // The {id} of `path` under the route's `pattern` (one "{id}" segment), when it is a canonical
   // lower-case GUID -- the text uuid.UUID(...) prints back, so logs and keys agree; else "".
   static std::string path_key(std::string_view pattern, std::string_view path) {
@@ -1268,7 +1394,7 @@ class AppHost {
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
     if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList ||
         r->kind == NativeRoute::kApiOverdue || r->kind == NativeRoute::kApiMarkOverdue ||
-        (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kApiDelete)) {
+        (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kFrontendIndexPost)) {
       auto j = std::make_shared<NativeJob>();
       j->route = r;
       j->server = server;
@@ -1286,6 +1412,7 @@ class AppHost {
                    : r->kind == NativeRoute::kApiList        ? api_list(j, m)
                    : r->kind == NativeRoute::kApiOverdue     ? api_overdue(j, m)
                    : r->kind == NativeRoute::kApiMarkOverdue ? api_markoverdue(j, m)
+                   : r->kind >= NativeRoute::kFrontendEditGet ? frontend_page(j, m)
                                                              : api_task(j, m);
       if (!taken) return false;
       j->req = std::move(m);

@@ -690,7 +690,8 @@ class DocStore {
             {"lapsed_reservations", (double)ru_lapsed_}, {"refunded_ru", ru_refunded_},
             {"throttled_read", (double)ru_throttled_kind_[kRead]}, {"throttled_write", (double)ru_throttled_kind_[kWrite]},
             {"throttled_query", (double)ru_throttled_kind_[kQuery]},
-            {"throttled_delete", (double)ru_throttled_kind_[kDelete]}};
+            {"throttled_delete", (double)ru_throttled_kind_[kDelete]},
+            {"mono", mono_s()}};  // the store's clock: windows measured on the side that meters them
   }
 
   // ------------------------------------------------------------ column mirror

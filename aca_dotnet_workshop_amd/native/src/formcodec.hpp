@@ -188,4 +188,119 @@ inline Verdict create_task(std::string_view body, std::string_view cookie, std::
   return Verdict::kOk;
 }
 
+// -- the other posts of the UI: Edit (Pages/Tasks/Edit.cshtml.cs:57-71) and Index's Complete /
+// Delete handlers (Pages/Tasks/Index.cshtml.cs:57-71), with the same envelope rules.
+
+// The antiforgery and identity cookies (Request.cookies: `;`-separated, stripped, percent-
+// decoded, the last one wins); false on an undecodable value.
+inline bool read_cookies(std::string_view cookie, std::string_view af_name, std::string_view id_name, std::string& af,
+                         bool& have_af, std::string& who, bool& have_who) {
+  std::string tmp;
+  have_af = have_who = false;
+  for (size_t i = 0; i <= cookie.size();) {
+    size_t j = cookie.find(';', i);
+    if (j == std::string_view::npos) j = cookie.size();
+    std::string_view part = cookie.substr(i, j - i);
+    while (!part.empty() && (part.front() == ' ' || part.front() == '\t')) part.remove_prefix(1);
+    while (!part.empty() && (part.back() == ' ' || part.back() == '\t')) part.remove_suffix(1);
+    size_t eq = part.find('=');
+    if (eq != std::string_view::npos) {
+      std::string_view name = part.substr(0, eq);
+      if (name == af_name || (!id_name.empty() && name == id_name)) {
+        if (!unquote(part.substr(eq + 1), false, tmp)) return false;
+        if (name == af_name) af = tmp, have_af = true;
+        else who = tmp, have_who = true;
+      }
+    }
+    i = j + 1;
+  }
+  return true;
+}
+
+// The form's fields `names[0..n)` (Request.form: `&`-separated, unquote_plus, the first wins);
+// false on a malformed pair.
+inline bool read_form(std::string_view body, const char* const* names, int n, std::string* vals, bool* seen) {
+  std::string name;
+  for (int k = 0; k < n; ++k) seen[k] = false;
+  for (size_t i = 0; i < body.size();) {
+    size_t j = body.find('&', i);
+    if (j == std::string_view::npos) j = body.size();
+    std::string_view field = body.substr(i, j - i);
+    i = j + 1;
+    if (field.empty()) continue;
+    size_t eq = field.find('=');
+    if (eq == std::string_view::npos) return false;
+    if (!unquote(field.substr(0, eq), true, name)) return false;
+    for (int k = 0; k < n; ++k)
+      if (name == names[k] && !seen[k]) {
+        if (!unquote(field.substr(eq + 1), true, vals[k])) return false;
+        seen[k] = true;
+      }
+  }
+  return true;
+}
+
+// Antiforgery.validate for a token in the form (a header token: the page decides).
+inline Verdict check_token(bool seen_token, const std::string& token, bool have_af, const std::string& af,
+                           std::string_view key) {
+  if (!seen_token || token.empty()) return Verdict::kDecline;
+  if (!have_af || af.empty()) return Verdict::kBadToken;
+  const std::string want = hmac_sha256_hex(key, af);
+  if (want.size() != token.size() || CRYPTO_memcmp(want.data(), token.data(), want.size()) != 0)
+    return Verdict::kBadToken;
+  return Verdict::kOk;
+}
+
+// POST Tasks/Edit/{id}: antiforgery, TaskUpdateModel's [Required] binding, the PUT body
+// {"taskId","taskName","taskDueDate","taskAssignedTo"} and the id it goes to (the form's TaskId,
+// else the route's `path_id`; a GUID in the 36-character form, else the page decides).
+inline Verdict edit_task(std::string_view body, std::string_view cookie, std::string_view key,
+                         std::string_view af_cookie_name, std::string_view path_id, std::string& json,
+                         std::string& task_id) {
+  if (!taskcodec::valid_utf8(body) || !taskcodec::valid_utf8(cookie)) return Verdict::kDecline;
+  std::string af, who;
+  bool have_af, have_who;
+  if (!read_cookies(cookie, af_cookie_name, {}, af, have_af, who, have_who)) return Verdict::kDecline;
+  static const char* names[5] = {"__RequestVerificationToken", "TaskUpdate.TaskId", "TaskUpdate.TaskName",
+                                 "TaskUpdate.TaskDueDate", "TaskUpdate.TaskAssignedTo"};
+  std::string vals[5];
+  bool seen[5];
+  if (!read_form(body, names, 5, vals, seen)) return Verdict::kDecline;
+  Verdict v = check_token(seen[0], vals[0], have_af, af, key);
+  if (v != Verdict::kOk) return v;
+  for (int k = 2; k < 5; ++k)
+    if (!seen[k] || !plain_value(vals[k])) return Verdict::kDecline;
+  std::string due;
+  if (!due_date(vals[3], due)) return Verdict::kDecline;
+  task_id = seen[1] && !vals[1].empty() ? vals[1] : std::string(path_id);
+  if (!taskcodec::is_guid36(task_id)) return Verdict::kDecline;
+  json.clear();
+  json += "{\"taskId\":";
+  tt::escape_to(json, task_id);
+  json += ",\"taskName\":";
+  tt::escape_to(json, vals[2]);
+  json += ",\"taskDueDate\":\"";
+  json += due;
+  json += "\",\"taskAssignedTo\":";
+  tt::escape_to(json, vals[4]);
+  json += '}';
+  return Verdict::kOk;
+}
+
+// POST Tasks/Index?handler=complete|delete&id=: the antiforgery check of the form (the handler and
+// the id come from the query string; in the form instead: the page decides).
+inline Verdict index_post(std::string_view body, std::string_view cookie, std::string_view key,
+                          std::string_view af_cookie_name) {
+  if (!taskcodec::valid_utf8(body) || !taskcodec::valid_utf8(cookie)) return Verdict::kDecline;
+  std::string af, who;
+  bool have_af, have_who;
+  if (!read_cookies(cookie, af_cookie_name, {}, af, have_af, who, have_who)) return Verdict::kDecline;
+  static const char* names[3] = {"__RequestVerificationToken", "handler", "id"};
+  std::string vals[3];
+  bool seen[3];
+  if (!read_form(body, names, 3, vals, seen)) return Verdict::kDecline;
+  if (seen[1] || seen[2]) return Verdict::kDecline;
+  return check_token(seen[0], vals[0], have_af, af, key);
+}
+
 }  // namespace formcodec

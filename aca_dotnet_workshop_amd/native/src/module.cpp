@@ -518,6 +518,24 @@ PYBIND11_MODULE(_ttnative, m) {
     return py::make_tuple(true, py::bytes(json));
   });
 
+  // POST Tasks/Edit/{id} (formcodec.hpp edit_task) -> None (the page decides), (False, b"", "")
+  // (a bad antiforgery token: 400) or (True, PUT body, task id)
+  m.def("frontend_edit_form", [view](py::bytes body, py::bytes cookie, py::bytes key, const std::string& path_id)
+            -> py::object {
+    std::string json, id;
+    auto v = formcodec::edit_task(view(body), view(cookie), view(key), ".AspNetCore.Antiforgery", path_id, json, id);
+    if (v == formcodec::Verdict::kDecline) return py::none();
+    if (v == formcodec::Verdict::kBadToken) return py::make_tuple(false, py::bytes(""), py::str(""));
+    return py::make_tuple(true, py::bytes(json), py::str(id));
+  });
+  // POST Tasks/Index's form (formcodec.hpp index_post) -> None (the page decides), False (a bad
+  // token) or True
+  m.def("frontend_index_form", [view](py::bytes body, py::bytes cookie, py::bytes key) -> py::object {
+    auto v = formcodec::index_post(view(body), view(cookie), view(key), ".AspNetCore.Antiforgery");
+    if (v == formcodec::Verdict::kDecline) return py::none();
+    return py::bool_(v == formcodec::Verdict::kOk);
+  });
+
   // state-query response -> (task count, TaskModel JSON array, has a continuation token) or None
   // (taskcodec.hpp query_tasks); `by_created`: ordered by TaskCreatedOn as a DateTime.
   m.def("tasks_from_query", [](py::bytes body, bool by_created, bool descending) -> py::object {

@@ -191,10 +191,19 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
             return render(req, "tasks_index.html", rows_html=fast, created_by=created_by)
         return render(req, "tasks_index.html", tasks=tasks_from_json(data), created_by=created_by)
 
+    index_form = _native_fn("frontend_index_form") if mode == "dapr" else None
+    edit_form = _native_fn("frontend_edit_form") if mode == "dapr" else None
+
     @app.route("/Tasks/Index", ("POST",), name="TasksIndexPost", include_in_schema=False)
     async def tasks_index_post(req: Request) -> Response:
-        form = req.form()
-        require_af(req, form)
+        failed = native_route_failure(req, {"invoke": "invoke {key}"}, _index_invoke_path(req))
+        if failed is not None:  # the native route's invoke failed: the SDK's error, as below
+            raise failed
+        if index_form is not None and index_form(req.body, (req.headers.get("cookie") or "").encode(), af.key) is True:
+            form = {}  # the antiforgery check passed in the native pass; handler and id from the query
+        else:
+            form = req.form()
+            require_af(req, form)
         handler = (req.query_get("handler") or form.get("handler") or "").lower()
         tid = req.query_get("id") or form.get("id") or ""
         if not is_guid(tid):
@@ -264,20 +273,58 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
         return redirect(CREATED_REDIRECT[1], CREATED_REDIRECT[0])
 
     # -- Tasks/Edit ---------------------------------------------------------------
+    if ep is not None:
+        # the Edit page and the Index / Edit posts on the app host's I/O thread: the same cookies,
+        # antiforgery check and form binding (formcodec.hpp), the same invoke, the same page from
+        # the template's own pieces (rows.py edit_page_pieces) or 302; the rest comes here
+        inv = f"{ep['prefix']}/v1.0/invoke/{API_APP_ID}/method/api/tasks/"
+        common = {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"], "af_key": af.key.decode(),
+                  "af_cookie": AF_COOKIE, "id_cookie": COOKIE, "invoke_target": inv}
+        edit_page = rows.edit_page_pieces(env, "tasks_edit.html", af_field=AF_FIELD, request=None, title="Tasks Tracker",
+                                          errors={}, display=FIELD_DISPLAY)
+        if edit_page is not None and rows.ok:
+            app.services.setdefault("native_routes", []).append({
+                "kind": "frontend_edit_get", "method": "GET", "path": "/Tasks/Edit/{id}", "route": "/Tasks/Edit/{id}",
+                "cfg": {**common, "status": 200, "content_type": "text/html; charset=utf-8", "page": json.dumps(edit_page)}})
+        if edit_form is not None:
+            app.services.setdefault("native_routes", []).append({
+                "kind": "frontend_edit", "method": "POST", "path": "/Tasks/Edit/{id}", "route": "/Tasks/Edit/{id}",
+                "cfg": {**common, "status": 302, "location": "/Tasks/Index"}})
+        if index_form is not None:
+            app.services.setdefault("native_routes", []).append({
+                "kind": "frontend_index_post", "method": "POST", "path": "/Tasks/Index", "route": "/Tasks/Index",
+                "cfg": {**common, "status": 302, "location": "/Tasks/Index"}})
+
     @app.route("/Tasks/Edit/{id:guid}", ("GET",), name="TasksEdit", include_in_schema=False)
     async def edit_get(req: Request) -> Response:
         if not req.cookies.get(COOKIE):
             return redirect("/")
-        data = await gw.call("GET", f"api/tasks/{req.path_params['id']}")
+        path = f"api/tasks/{req.path_params['id']}"
+        failed = native_route_failure(req, {"invoke": f"invoke {API_APP_ID}/{path}"})
+        if failed is not None:  # the native route's invoke failed: the SDK's error, as below
+            raise failed
+        data = await gw.call("GET", path)
         if not data:
             return render(req, "not_found.html", 404)
-        t = TaskModel.model_validate(data)
-        values = {"taskId": str(t.task_id), "taskName": t.task_name, "taskAssignedTo": t.task_assigned_to,
-                  "taskDueDate": _input_date(t.task_due_date)}
+        values = rows.edit_values(data) if rows.ok else None  # the plain shape: no TaskModel
+        if values is None:
+            t = TaskModel.model_validate(data)
+            values = {"taskId": str(t.task_id), "taskName": t.task_name, "taskAssignedTo": t.task_assigned_to,
+                      "taskDueDate": _input_date(t.task_due_date)}
         return render(req, "tasks_edit.html", values=values, errors={}, display=FIELD_DISPLAY)
 
     @app.route("/Tasks/Edit/{id:guid}", ("POST",), name="TasksEditPost", include_in_schema=False)
     async def edit_post(req: Request) -> Response:
+        failed = native_route_failure(req, {"invoke": "invoke {key}"}, _edit_invoke_path(req))
+        if failed is not None:  # the native route's invoke failed: the SDK's error, as below
+            raise failed
+        if edit_form is not None:  # antiforgery, binding and the PUT body in one native pass
+            made = edit_form(req.body, (req.headers.get("cookie") or "").encode(), af.key, str(req.path_params["id"]))
+            if made is not None:
+                if not made[0]:
+                    raise HTTPError(400, detail="The antiforgery token could not be validated.")
+                await gw.call("PUT", f"api/tasks/{made[2]}", RawJson(made[1].decode()))
+                return redirect("/Tasks/Index")
         form = req.form()
         require_af(req, form)
         values, errors = _bind(form, "TaskUpdate")
@@ -300,6 +347,33 @@ def create_app(argv: list[str] | None = None, client: SidecarClient | None = Non
 
     app.on_shutdown.append(gw.close)
     return app
+
+
+def _native_fn(name: str):
+    """A form codec of the native module (formcodec.hpp via module.cpp), or None without it."""
+    try:
+        from ...native import load
+        return getattr(load(), name)
+    except Exception:
+        return None
+
+
+def _index_invoke_path(req: Request) -> str:
+    """The SDK's InvocationError text for tasks_index_post's invoke (its path)."""
+    if not req.state.get("tt_native"):
+        return ""
+    handler = (req.query_get("handler") or "").lower()
+    tid = req.query_get("id") or ""
+    return f"{API_APP_ID}/api/tasks/{tid}" + ("/markcomplete" if handler == "complete" else "")
+
+
+def _edit_invoke_path(req: Request) -> str:
+    """The SDK's InvocationError text for edit_post's invoke (its path: the form's TaskId, else
+    the route's id)."""
+    if not req.state.get("tt_native"):
+        return ""
+    tid = req.form().get("TaskUpdate.TaskId") or str(req.path_params.get("id"))
+    return f"{API_APP_ID}/api/tasks/{tid}"
 
 
 def _native_form():

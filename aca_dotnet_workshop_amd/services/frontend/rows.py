@@ -114,6 +114,36 @@ class RowRenderer:
             return None
         return [p if i % 2 == 0 else names[p] for i, p in enumerate(parts)]
 
+    @staticmethod
+    def edit_page_pieces(env, name: str, **ctx: Any) -> list[str] | None:
+        """The Edit page as pieces for the app host's native route (apphost.hpp ``edit_page``):
+        the render call ``edit_get`` makes, with sentinels for the antiforgery token and the
+        task's id, name, assignee and due date; None when a sentinel does not come through intact
+        (the template escapes or cuts it)."""
+        sent = {"af_token": "zqAFTOKENqz", "task_id": "zqTIDqz", "task_name": "zqTNAMEqz",
+                "task_assigned_to": "zqTASSIGNEDqz", "due": "zqDUEqz"}
+        values = {"taskId": sent["task_id"], "taskName": sent["task_name"], "taskAssignedTo": sent["task_assigned_to"],
+                  "taskDueDate": sent["due"]}
+        html = env.get_template(name).render(af_token=sent["af_token"], values=values, **ctx)
+        names = {v: k for k, v in sent.items()}
+        parts = re.split("(" + "|".join(map(re.escape, names)) + ")", html)
+        slots = [names[p] for p in parts[1::2]]
+        if set(slots) != set(sent):
+            return None
+        return [p if i % 2 == 0 else names[p] for i, p in enumerate(parts)]
+
+    @staticmethod
+    def edit_values(d: Any) -> dict[str, str] | None:
+        """``edit_get``'s values straight from the API's TaskModel JSON when it is in the plain
+        shape the native route fills (the due date's calendar day from the text), else None."""
+        if not isinstance(d, dict):
+            return None
+        tid, name, who, due = d.get("taskId"), d.get("taskName"), d.get("taskAssignedTo"), d.get("taskDueDate")
+        if not (isinstance(tid, str) and _GUID.match(tid) and isinstance(name, str) and isinstance(who, str)
+                and isinstance(due, str) and _DAY.match(due)):
+            return None
+        return {"taskId": tid, "taskName": name, "taskAssignedTo": who, "taskDueDate": due[:10]}
+
     def row_pieces(self) -> dict[str, list[str]] | None:
         """The compiled rows for the native route: ``row_<c><o>`` (c, o: ``f`` / ``t`` for
         isCompleted / isOverDue) -> pieces with the slots task_id, task_name, task_assigned_to, due."""

@@ -1049,6 +1049,8 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         sw = None
         if steady and t_end - steady["t"] > 1.0 and budget:
             w = t_end - steady["t"]
+            if st1.get("mono") and steady["st"].get("mono"):  # the store's own clock between the two reads
+                w = float(st1["mono"]) - float(steady["st"]["mono"])
             ru_s = float(st1.get("ru_consumed", 0.0)) - float(steady["st"].get("ru_consumed", 0.0))
             sw = {"seconds": round(w, 2), "tasks_per_s": round((enq1 - steady["enq"]) / w, 1),
                   "ru_consumed_per_s": round(ru_s / w, 1), "ru_over_budget": round(ru_s / (budget * w), 3)}
