@@ -107,43 +107,69 @@ class StorageQueueBinding(Binding):
         self._task = asyncio.ensure_future(self._poll(deliver))
 
     async def _poll(self, deliver: Deliver) -> None:
-        sem = asyncio.Semaphore(self.concurrency)
+        """Continuous delivery: a receive asks for as many messages as there are free delivery
+        slots (``concurrency``, at most 32 a call) and every message is delivered on its own task
+        -- a slot frees the moment its delivery ends and the next receive refills it.  A slow or
+        failing delivery holds only its own slot: the rest of the queue keeps flowing (no wait
+        for a whole batch).  A failed delivery is not deleted: the message reappears once its
+        visibility timeout elapses (docs/aca/06-aca-dapr-bindingsapi/index.md:54-58)."""
+        free = asyncio.Semaphore(self.concurrency)
+        inflight: set[asyncio.Task] = set()
         backoff = 0.1
 
-        async def one(m: dict[str, Any]) -> None:
-            async with sem:
-                raw = m.get("body", "").encode() if "body" in m else base64.b64decode(m.get("bodyB64", ""))
-                if self.decode:
-                    try:
-                        raw = base64.b64decode(raw, validate=True)
-                    except ValueError:
-                        log.warning("%s: message %s is not valid base64; leaving it in the queue", self.name,
-                                    m.get("messageId"))
-                        return
-                ok = False
+        def done(t: asyncio.Task) -> None:
+            inflight.discard(t)
+            free.release()
+        try:
+            while True:
+                await free.acquire()  # one free slot at least, then every other one free right now
+                n = 1
+                while n < 32 and not free.locked():
+                    await free.acquire()
+                    n += 1
                 try:
-                    ok = await deliver(raw, {"MessageId": str(m.get("messageId")), "DequeueCount": str(m.get("dequeueCount")),
-                                             "InsertionTime": str(m.get("insertionMs"))})
+                    msgs = await self.client.queue_get(self.account, self.queue, n, self.visibility_ms,
+                                                       wait_ms=min(self.poll_ms, 5000))
+                    backoff = 0.1
+                except asyncio.CancelledError:
+                    raise
                 except Exception as e:
-                    log.warning("%s: delivery failed: %r", self.name, e)
-                if ok:
-                    await self.client.queue_delete(self.account, self.queue, m["popReceipt"])
-                # on failure the message reappears once its visibility timeout elapses
+                    for _ in range(n):
+                        free.release()
+                    log.warning("%s: queue poll failed: %r", self.name, e)
+                    await asyncio.sleep(backoff)
+                    backoff = min(backoff * 2, 5.0)
+                    continue
+                for _ in range(n - len(msgs)):
+                    free.release()
+                for m in msgs[:n]:
+                    t = asyncio.ensure_future(self._deliver_one(m, deliver))
+                    inflight.add(t)
+                    t.add_done_callback(done)
+        finally:
+            for t in list(inflight):
+                t.cancel()
 
-        while True:
+    async def _deliver_one(self, m: dict[str, Any], deliver: Deliver) -> None:
+        raw = m.get("body", "").encode() if "body" in m else base64.b64decode(m.get("bodyB64", ""))
+        if self.decode:
             try:
-                msgs = await self.client.queue_get(self.account, self.queue, 32, self.visibility_ms,
-                                                   wait_ms=min(self.poll_ms, 5000))
-                backoff = 0.1
-            except asyncio.CancelledError:
-                raise
-            except Exception as e:
-                log.warning("%s: queue poll failed: %r", self.name, e)
-                await asyncio.sleep(backoff)
-                backoff = min(backoff * 2, 5.0)
-                continue
-            if msgs:
-                await asyncio.gather(*(one(m) for m in msgs))
+                raw = base64.b64decode(raw, validate=True)
+            except ValueError:
+                log.warning("%s: message %s is not valid base64; leaving it in the queue", self.name, m.get("messageId"))
+                return
+        ok = False
+        try:
+            ok = await deliver(raw, {"MessageId": str(m.get("messageId")), "DequeueCount": str(m.get("dequeueCount")),
+                                     "InsertionTime": str(m.get("insertionMs"))})
+        except Exception as e:
+            log.warning("%s: delivery failed: %r", self.name, e)
+        if ok:
+            try:
+                await self.client.queue_delete(self.account, self.queue, m["popReceipt"])
+            except Exception as e:  # it reappears after its visibility timeout and is delivered again
+                log.warning("%s: delete of %s failed: %r", self.name, m.get("messageId"), e)
+        # on failure the message reappears once its visibility timeout elapses
 
     async def invoke(self, operation, data, metadata):
         if operation != "create":

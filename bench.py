@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import base64
 import json
 import os
 import sys
@@ -115,6 +116,8 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--browser-steps", type=int, default=-1,
                     help="steps of the browser_flow read-path run (create + the 302 followed to Tasks/Index, "
                          "per-user cookies; -1 = a quarter of --steps, 0 = skip)")
+    ap.add_argument("--ingest-messages", type=int, default=4096,
+                    help="messages of the external_ingest run (storage queue -> processor -> API -> blob; 0 = skip)")
     ap.add_argument("--session-flows", type=int, default=-1,
                     help="flows of the browser_session run (create, list, Edit GET/POST, Complete, Delete, list; "
                          "-1 = --batch, 0 = skip)")
@@ -774,6 +777,75 @@ def run_session(exe: str, targets: list[str], cookie: str, token: str, flows: in
             "flow": "Create, Index, Edit GET/POST (assignee change), Complete, Delete, Index; [p50, p99] ms per page"}
 
 
+def external_ingest(env, n: int, timeout_s: float = 120.0) -> dict:
+    """SURVEY §3.4 measured: ``n`` base64 task messages put on the storage queue the processor's
+    input binding reads (``externaltasksmanager``, decodeBase64), each taken through
+    ExternalTasksProcessorController (invoke POST api/tasks, then the blob output binding
+    ``externaltasksblobstore``), until the container holds a blob per message and the queue
+    completed them all (ExternalTasksProcessorController.cs:22-53; docs/aca/06-aca-dapr-
+    bindingsapi/index.md:267-280).  Messages / s from the first put to the last blob, the
+    deliveries per message (a redelivery after a failure or an expired visibility timeout counts)."""
+    import urllib.request
+
+    from aca_dotnet_workshop_amd.web.client import HttpClient
+    st = env.manifest.resources.get("storage") or {}
+    acct, queue = st.get("account"), (st.get("queues") or [None])[0]
+    container = (st.get("containers") or [None])[0]
+    key = env.ctl.storage_keys.get(acct, "")
+    base = f"{env.stack.backing_url_for('STORAGE')}/storage/{acct}"
+
+    def get(path: str):
+        req = urllib.request.Request(base + path, headers={"x-tt-key": key})
+        with urllib.request.urlopen(req, timeout=30) as r:
+            return json.loads(r.read())
+    try:
+        blobs0 = len(get(f"/blobs/{container}"))
+        q0 = get(f"/queues/{queue}/count")
+        bodies = [base64.b64encode(json.dumps({"taskName": f"external task {i}", "taskAssignedTo": f"ext{i % 7}@bench.local",
+                                               "taskCreatedBy": "ext@bench.local",
+                                               "taskDueDate": "2030-05-01T00:00:00"}).encode()) for i in range(n)]
+
+        async def put_all() -> None:
+            c = HttpClient()
+            sem = asyncio.Semaphore(64)
+
+            async def one(b: bytes) -> None:
+                async with sem:
+                    r = await c.post(f"{base}/queues/{queue}/messages", body=b,
+                                     headers={"x-tt-key": key, "Content-Type": "text/plain"})
+                    if r.status != 201:
+                        raise RuntimeError(f"queue put: {r.status} {r.body[:200]!r}")
+            try:
+                await asyncio.gather(*(one(b) for b in bodies))
+            finally:
+                await c.close()
+        t0 = time.perf_counter()
+        asyncio.run(put_all())
+        t_put = time.perf_counter() - t0
+        blobs = blobs0
+        while time.perf_counter() - t0 < timeout_s:
+            blobs = len(get(f"/blobs/{container}"))
+            if blobs - blobs0 >= n:
+                break
+            time.sleep(0.05)
+        dt = time.perf_counter() - t0
+        for _ in range(40):  # the last deletes follow the last blob
+            q1 = get(f"/queues/{queue}/count")
+            if int(q1.get("completed", 0)) - int(q0.get("completed", 0)) >= n:
+                break
+            time.sleep(0.05)
+        d = {k: int(q1.get(k, 0)) - int(q0.get(k, 0)) for k in ("enqueued", "received", "completed")}
+        made = blobs - blobs0
+        return {"messages": n, "msgs_per_s": round(made / dt, 1) if dt else None, "seconds": round(dt, 3),
+                "enqueue_s": round(t_put, 3), "blobs_written": made, "queue": d,
+                "deliveries_per_message": round(d["received"] / n, 3) if n else None,
+                "left_on_queue": int(q1.get("active", 0)) + int(q1.get("locked", 0)),
+                "dead": int(q1.get("dead_letter", 0)) - int(q0.get("dead_letter", 0)),
+                "all_processed": made == n and d["completed"] == n}
+    except Exception as e:  # reported, not fatal to the headline
+        return {"error": repr(e)[:300]}
+
+
 def _cpu_by_role(stack) -> dict[str, float]:
     """CPU seconds so far per process role (replicas summed per app)."""
     raw = stack.cpu_seconds()
@@ -1193,7 +1265,8 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
 
 
 def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
-                   protocol: str, wire: dict, alt: dict | None, session: dict | None = None) -> dict:
+                   protocol: str, wire: dict, alt: dict | None, session: dict | None = None,
+                   ingest: dict | None = None) -> dict:
     """The record's key facts in one small object at the head of ``config`` (the driver keeps
     the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
     flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
@@ -1211,6 +1284,8 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
         s["browser_flows_per_s"] = browser.get("flows_per_s")
     if session:
         s["browser_session"] = {k: session.get(k) for k in ("flows_per_s", "errors", "max_page_p99_over_create_p99")}
+    if ingest:
+        s["external_ingest"] = {k: ingest.get(k) for k in ("msgs_per_s", "all_processed", "dead", "error") if k in ingest}
     if alt:
         s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
                                  if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
@@ -1415,6 +1490,11 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if sflows:
             progress(f"browser_session: {sflows} flows of 7 pages")
             session = run_session(exe, targets, cookie, token, sflows, conc, root, ca_file, a.batch)
+        # §3.4 external-task ingestion: storage queue -> processor -> API -> blob
+        ingest = None
+        if a.ingest_messages > 0 and not shared:
+            progress(f"external_ingest: {a.ingest_messages} queue messages")
+            ingest = external_ingest(env, a.ingest_messages)
         # the same environment, load straight at the API sidecars' invoke (round 2's topology);
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
@@ -1470,7 +1550,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "threads": threads_all}), file=sys.stderr, flush=True)
-            summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session)
+            summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
+                                     ingest)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
@@ -1507,6 +1588,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
                            "overdue_sweeps": sweep_info, "browser_flow": browser, "browser_session": session,
+                           "external_ingest": ingest,
                            "api_sidecar_direct": direct,
                            "api_protocol_alt": alt, "reference_envelope": envelope}}), flush=True)
     finally:

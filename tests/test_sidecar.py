@@ -174,6 +174,51 @@ def test_input_binding_ack_and_redelivery():
     run(main())
 
 
+def test_input_binding_slow_or_failing_delivery_does_not_stall_the_queue():
+    """the poller delivers each message on its own slot and refills freed
+    slots at once -- one slow delivery (the app holds it 1.5 s) and one failing delivery (500,
+    redelivered after the visibility timeout) do not delay the other messages, which are all
+    delivered and deleted while the slow one is still running."""
+    import base64
+    import time as _t
+    app = WebApp("binder")
+    done: dict[int, float] = {}
+    attempts: dict[int, int] = {}
+    release = asyncio.Event()
+
+    async def handler(req):
+        n = json.loads(req.body)["n"]
+        attempts[n] = attempts.get(n, 0) + 1
+        if n == 0:  # the slow one
+            await asyncio.wait_for(release.wait(), 5)
+        if n == 1 and attempts[n] == 1:  # the failing one: 500 once, then fine
+            return empty(500)
+        done.setdefault(n, _t.monotonic())
+        return empty(200)
+    app.add_route("/jobs", handler, ("POST",))
+    q = _inline("jobs", "bindings.azure.storagequeues", {"storageAccount": "acct", "queue": "q1", "decodeBase64": "true",
+                                                         "visibilityTimeout": "300ms", "pollingInterval": "200ms",
+                                                         "concurrency": "4"})
+
+    async def main():
+        async with Harness(app, [q]) as h:
+            b = h.backing.broker("storage-acct")
+            t0 = _t.monotonic()
+            for n in range(40):
+                b.send("q1", base64.b64encode(json.dumps({"n": n}).encode()))
+            h.backing.waiters.notify("storage-acct|q1")
+            # 38 fast messages through 3 free slots (the 4th is held by the slow one), long before it ends
+            await _until(lambda: len([x for x in done if x >= 2]) == 38, timeout=5)
+            assert 0 not in done and all(done[x] - t0 < 1.5 for x in done if x >= 2)
+            await _until(lambda: 1 in done, timeout=5)  # the failed one came back after its visibility timeout
+            assert attempts[1] == 2 and done[1] - t0 >= 0.3
+            release.set()
+            await _until(lambda: 0 in done and b.counts("q1")["completed"] == 40, timeout=5)
+            # (the slow one outlived its 300 ms visibility timeout, so it was handed out again --
+            # at-least-once, as the storage queue promises -- and still only 40 were completed)
+    run(main())
+
+
 def test_secret_references_and_stores(tmp_path):
     secrets_file = tmp_path / "secrets.json"
     secrets_file.write_text(json.dumps({"db": {"key": "s3cr3t"}, "plain": "p"}))
