@@ -788,17 +788,17 @@ def external_ingest(env, n: int, timeout_s: float = 120.0) -> dict:
     import urllib.request
 
     from aca_dotnet_workshop_amd.web.client import HttpClient
-    st = env.manifest.resources.get("storage") or {}
-    acct, queue = st.get("account"), (st.get("queues") or [None])[0]
-    container = (st.get("containers") or [None])[0]
-    key = env.ctl.storage_keys.get(acct, "")
-    base = f"{env.stack.backing_url_for('STORAGE')}/storage/{acct}"
 
     def get(path: str):
         req = urllib.request.Request(base + path, headers={"x-tt-key": key})
         with urllib.request.urlopen(req, timeout=30) as r:
             return json.loads(r.read())
     try:
+        st = env.manifest.resources.get("storage") or {}
+        acct, queue = st.get("account"), (st.get("queues") or [None])[0]
+        container = (st.get("containers") or [None])[0]
+        key = env.ctl.storage_keys.get(acct, "")
+        base = f"{env.stack.backing_url_for('STORAGE')}/storage/{acct}"
         blobs0 = len(get(f"/blobs/{container}"))
         q0 = get(f"/queues/{queue}/count")
         bodies = [base64.b64encode(json.dumps({"taskName": f"external task {i}", "taskAssignedTo": f"ext{i % 7}@bench.local",
