@@ -341,6 +341,9 @@ class NativeHttpServer:
         if self._collector is None:
             reqs = REGISTRY.counter("http_requests_total", "HTTP requests served")
             lat = REGISTRY.histogram("http_request_duration_seconds", "HTTP request latency")
+            # the share of them the I/O thread served end to end (the rest reached the handlers)
+            nat = REGISTRY.counter("native_route_requests_total",
+                                   "requests the app host's native routes served end to end")
             keys: dict[tuple, tuple] = {}
 
             def collect() -> None:
@@ -353,6 +356,7 @@ class NativeHttpServer:
                         k = keys[(rid_, status)] = (tuple(sorted({"method": m, "route": r, "status": str(status)}.items())),
                                                     (("route", r),))
                     reqs.inc_key(k[0], n)
+                    nat.inc_key(k[0], n)
                     lat.merge_key(k[1], buckets, total, n)
             self._collector = collect
             REGISTRY.collectors.append(collect)
