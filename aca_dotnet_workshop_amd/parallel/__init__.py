@@ -21,7 +21,8 @@ import os
 import sys
 
 __all__ = ["Dist", "cpu_budget", "cpu_quota", "one_thread_per_core", "topology", "cgroup_throttling",
-           "partition_cpus", "pin_rank", "gpu_numa_nodes", "PIN_INFO"]
+           "partition_cpus", "pin_rank", "gpu_numa_nodes", "PIN_INFO", "split_platform", "affinity_from_env",
+           "pin_preexec", "pin_all_threads", "cpus_allowed"]
 
 
 class Dist:
@@ -248,6 +249,79 @@ def pin_rank(local_rank: int, local_world: int, spec: str | None = None,
     if cpus:
         os.sched_setaffinity(0, cpus)
     return cpus
+
+
+def split_platform(cpus: set[int] | None, n: int) -> tuple[set[int], set[int]] | None:
+    """Reserve ``n`` CPUs of a rank's set for the platform's own processes (backing services,
+    ingress, load generator, the controller) and give the replicas the rest, so neither side can
+    run on the other's CPUs: a rank's platform is held to its reserve the way its replicas are
+    held to their caps (the ACA environment's infrastructure is not billed to the apps either).
+    None when the set is too small to split (fewer than ``n`` + 2 CPUs)."""
+    if not cpus or n <= 0 or len(cpus) < n + 2:
+        return None
+    order = sorted(cpus)
+    return set(order[-n:]), set(order[:-n])
+
+
+def affinity_from_env(role: str) -> set[int] | None:
+    """``TT_PLATFORM_CPUS`` / ``TT_REPLICA_CPUS`` (comma-separated CPU ids) for ``role``
+    (``platform`` | ``replica``): the CPUs a process the platform starts is pinned to."""
+    raw = os.environ.get("TT_PLATFORM_CPUS" if role == "platform" else "TT_REPLICA_CPUS", "")
+    try:
+        cpus = {int(x) for x in raw.split(",") if x.strip()}
+    except ValueError:
+        return None
+    return cpus or None
+
+
+def pin_preexec(role: str):
+    """A ``preexec_fn`` pinning the child (and every thread it will start) to ``role``'s CPUs,
+    or None when no such split is configured."""
+    cpus = affinity_from_env(role)
+    if not cpus:
+        return None
+
+    def pin() -> None:
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            pass
+    return pin
+
+
+def pin_all_threads(cpus: set[int]) -> None:
+    """Pin every thread of this process (those already running too) to ``cpus``."""
+    for t in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(t), cpus)
+        except OSError:
+            pass
+
+
+def cpus_allowed(pid: int) -> dict[int, set[int]]:
+    """tid -> the CPUs each thread of ``pid`` may run on (``Cpus_allowed_list``)."""
+    out: dict[int, set[int]] = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for t in tids:
+        try:
+            with open(f"/proc/{pid}/task/{t}/status") as f:
+                for ln in f:
+                    if ln.startswith("Cpus_allowed_list:"):
+                        cpus: set[int] = set()
+                        for part in ln.split(":", 1)[1].strip().split(","):
+                            if "-" in part:
+                                a, b = part.split("-")
+                                cpus.update(range(int(a), int(b) + 1))
+                            elif part:
+                                cpus.add(int(part))
+                        out[int(t)] = cpus
+                        break
+        except (OSError, ValueError):
+            continue
+    return out
 
 
 def cpu_quota() -> float | None:

@@ -317,7 +317,9 @@ class NativeIngress:
                "threads": self.threads, "statsFile": str(self.stats_file), "portFile": str(self.port_file),
                **self._routes()}
         self.cfg_file.write_text(json.dumps(cfg))
-        self.proc = subprocess.Popen([str(exe), str(self.cfg_file)], stdin=subprocess.DEVNULL)
+        from ..parallel import pin_preexec  # the environment's ingress runs on the platform's CPUs
+        self.proc = subprocess.Popen([str(exe), str(self.cfg_file)], stdin=subprocess.DEVNULL,
+                                     preexec_fn=pin_preexec("platform"))
         deadline = time.monotonic() + 30.0
         while not self.port_file.exists():
             if self.proc.poll() is not None:

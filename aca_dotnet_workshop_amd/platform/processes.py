@@ -85,10 +85,14 @@ class LocalStack:
         self._seq = 0
 
     # -- processes --------------------------------------------------------------
-    def _spawn(self, args: list[str], env: dict[str, str], log_name: str) -> subprocess.Popen:
+    def _spawn(self, args: list[str], env: dict[str, str], log_name: str, role: str = "replica") -> subprocess.Popen:
+        """``role``: ``platform`` (the backing services) or ``replica`` (a sidecar and the app it
+        starts): the CPU subset the process is pinned to when the rank's set is split
+        (``TT_PLATFORM_CPUS`` / ``TT_REPLICA_CPUS``, parallel.split_platform)."""
+        from ..parallel import pin_preexec
         out = open(self.log_dir / f"{log_name}.log", "ab")
         return subprocess.Popen(args, env=env, stdout=out, stderr=subprocess.STDOUT, cwd=str(REPO_ROOT),
-                                start_new_session=True)
+                                start_new_session=True, preexec_fn=pin_preexec(role))
 
     def start_backing(self, data_dir: str | None = None, policy: dict[str, Any] | None = None,
                       timeout: float = 60.0) -> str:
@@ -103,7 +107,7 @@ class LocalStack:
             pp = self.root / "policy.json"
             pp.write_text(json.dumps(policy))
             args += ["--policy", str(pp)]
-        self.backing_proc = self._spawn(args, self.base_env, "backing")
+        self.backing_proc = self._spawn(args, self.base_env, "backing", role="platform")
         port = _wait_file(pf, timeout, self.backing_proc)
         self.backing_url = f"http://127.0.0.1:{port}"
         self._backing_args = args
@@ -127,7 +131,7 @@ class LocalStack:
         args[args.index("--port") + 1] = str(self._backing_port)
         deadline = time.time() + timeout
         while True:  # the old listener's port may take a moment to be released
-            self.backing_proc = self._spawn(args, self.base_env, "backing")
+            self.backing_proc = self._spawn(args, self.base_env, "backing", role="platform")
             try:
                 _wait_file(pf, max(1.0, deadline - time.time()), self.backing_proc)
                 return self.backing_url
@@ -145,7 +149,7 @@ class LocalStack:
             pf.unlink()
         args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
         uds = self._uds_args(tag)
-        p = self._spawn(args + uds, self.base_env, f"backing-{tag}")
+        p = self._spawn(args + uds, self.base_env, f"backing-{tag}", role="platform")
         url = f"http://127.0.0.1:{_wait_file(pf, timeout, p)}"
         for f in families:
             self.extra_backing[f] = (p, url)

@@ -116,6 +116,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--browser-steps", type=int, default=-1,
                     help="steps of the browser_flow read-path run (create + the 302 followed to Tasks/Index, "
                          "per-user cookies; -1 = a quarter of --steps, 0 = skip)")
+    ap.add_argument("--platform-split", type=int, choices=(0, 1), default=1,
+                    help="pin the platform's processes (backing, ingress, load generator) to PLATFORM_CPUS of the "
+                         "rank's CPUs and the replicas to the rest (1), or let them share the set (0)")
     ap.add_argument("--ingest-messages", type=int, default=4096,
                     help="messages of the external_ingest run (storage queue -> processor -> API -> blob; 0 = skip)")
     ap.add_argument("--session-flows", type=int, default=-1,
@@ -215,15 +218,23 @@ class OverdueSweeper:
         self.runs: list[tuple[float, dict]] = []
         self.errors: list[str] = []
         self.marked_all = 0  # tasks marked overdue by every sweep since start (reset() keeps it)
-        self.trace_ids: list[str] = []  # every sweep is a sampled trace (per-hop spans)
+        self.trace_ids: list[str] = []  # the sampled sweeps' traces (per-hop spans)
+        # warmup sweeps are sampled traces (their spans attribute the job's hops); the timed
+        # region's are not, as a production cron run at the manifest's 1 % sampling almost never
+        # is -- the native routes serve unsampled requests only, sampled ones take the handlers
+        self.sampled = True
+        self.sampled_trace_ids: list[str] = []
         self.thread = threading.Thread(target=self._run, name="overdue-sweeper", daemon=True)
 
     def start(self) -> None:
         self.thread.start()
 
-    def reset(self) -> None:
-        """Forget the sweeps so far (the warmup's): the summary covers what follows."""
+    def reset(self, sampled: bool = False) -> None:
+        """Forget the sweeps so far (the warmup's): the summary covers what follows; the sampled
+        warmup traces stay for the span attribution (``sampled_trace_ids``)."""
+        self.sampled_trace_ids += self.trace_ids
         self.runs, self.errors, self.trace_ids = [], [], []
+        self.sampled = sampled
 
     def stop(self) -> None:
         self.stop_ev.set()
@@ -240,13 +251,15 @@ class OverdueSweeper:
                 t = time.perf_counter()
                 tid = os.urandom(16).hex()
                 try:
+                    flags = "01" if self.sampled else "00"
                     r = await c.post(self.url, body=b"{}", timeout=60,
                                      headers={"Content-Type": "application/json",
-                                              "traceparent": f"00-{tid}-{os.urandom(8).hex()}-01"})
+                                              "traceparent": f"00-{tid}-{os.urandom(8).hex()}-{flags}"})
                     if r.status == 200:
                         self.runs.append((time.perf_counter() - t, r.json()))
                         self.marked_all += int(self.runs[-1][1].get("markedOverdue", 0))
-                        self.trace_ids.append(tid)
+                        if self.sampled:
+                            self.trace_ids.append(tid)
                     else:
                         self.errors.append(f"{r.status} {r.body[:200]!r}")
                 except Exception as e:  # recorded, reported in the bench line
@@ -871,6 +884,11 @@ BROWSER_USERS = 4096
 
 # cores held back for the external ingress when load enters through it (uncapped, like Envoy)
 INGRESS_RESERVE = 1.0
+# the platform's own processes -- backing services, external ingress, load generator, the
+# controller -- get this many CPUs of the rank's set, pinned, and the replicas the rest:
+# measured at the headline's rate they need ~3.8 cores (backing 26.8 + ingress 15.4 + load
+# generator 9.4 us/task x 73 k/s); the replicas' caps come out of the rest
+PLATFORM_CPUS = 4
 
 
 def _ingress_cpu(env) -> dict[str, float]:
@@ -1264,9 +1282,52 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
         env.stop()
 
 
+PLATFORM_ROLES = ("backing", "ingress", "bench")
+
+
+def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
+    """The platform's share of the rank: cores its processes used in the timed region (backing
+    services, ingress, this process with its load generators) against the CPUs reserved for
+    them, and every thread of the rank's processes checked against its CPU set (the rank's set;
+    the platform / replica subset when split): ``outside_rank_set`` counts threads that may run
+    elsewhere."""
+    from aca_dotnet_workshop_amd.parallel import cpus_allowed
+    used = sum(v for k, v in busy.items() if k.split(".")[0].startswith(PLATFORM_ROLES))
+    pids: dict[str, list[int]] = {"platform": [os.getpid()] + list(_ingress_pid(env).values()), "replica": []}
+    st = env.stack
+    if st.backing_proc is not None:
+        pids["platform"].append(st.backing_proc.pid)
+    pids["platform"] += [p.pid for p, _u in st.extra_backing.values()]
+    import psutil
+    for rs in st.replicas.values():
+        for r in rs:
+            pids["replica"].append(r.proc.pid)
+            try:
+                pids["replica"] += [k.pid for k in psutil.Process(r.proc.pid).children(recursive=True)]
+            except psutil.Error:
+                pass
+    rank = set(pinned) if pinned else None
+    outside = wrong_side = threads = 0
+    for side, ps in pids.items():
+        want = (split[0] if side == "platform" else split[1]) if split is not None else rank
+        for pid in ps:
+            for cpus in cpus_allowed(pid).values():
+                threads += 1
+                if rank is not None and not cpus <= rank:
+                    outside += 1
+                if want is not None and not cpus <= want:
+                    wrong_side += 1
+    return {"reserved_cpus": len(split[0]) if split is not None else None, "cores_used": round(used, 2),
+            "within_reserve": bool(split is None or used <= len(split[0]) + 0.05),
+            "mechanism": (f"pinned: {len(split[0])} of the rank's {len(pinned)} CPUs for backing, ingress and load "
+                          f"generator, the other {len(split[1])} for the replicas") if split is not None
+            else "shared with the replicas (rank set too small to split)",
+            "threads_checked": threads, "outside_rank_set": outside, "outside_own_subset": wrong_side}
+
+
 def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
                    protocol: str, wire: dict, alt: dict | None, session: dict | None = None,
-                   ingest: dict | None = None) -> dict:
+                   ingest: dict | None = None, platform: dict | None = None) -> dict:
     """The record's key facts in one small object at the head of ``config`` (the driver keeps
     the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
     flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
@@ -1289,6 +1350,8 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
     if alt:
         s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
                                  if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
+    if platform:
+        s["platform_cpu"] = {k: platform.get(k) for k in ("cores_used", "reserved_cpus", "outside_rank_set")}
     if envelope:
         s["envelope"] = {k: envelope.get(k) for k in ("tasks_per_s", "errors", "tasks_per_s_over_budget_rate",
                                                        "store_429s_per_task", "store_429s_per_call")}
@@ -1308,6 +1371,13 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
     from aca_dotnet_workshop_amd.platform.manifest import load_manifest
     n = d.world  # the ranks that actually ran (self_launch starts them for --gpus N)
+    from aca_dotnet_workshop_amd.parallel import pin_all_threads, split_platform
+    # the rank's CPU set split: the platform's processes on PLATFORM_CPUS of them, the replicas
+    # on the rest (each process pinned when it is started: parallel.pin_preexec)
+    split = split_platform(set(pinned) if pinned else None, PLATFORM_CPUS) if a.platform_split else None
+    if split is not None:
+        os.environ["TT_PLATFORM_CPUS"] = ",".join(map(str, sorted(split[0])))
+        os.environ["TT_REPLICA_CPUS"] = ",".join(map(str, sorted(split[1])))
     fe, api, proc = frontend_topology(cores)
     fe = a.frontend_replicas or fe
     api = a.api_replicas or api
@@ -1324,9 +1394,12 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         w = CPU_WEIGHT
         if a.cpu_weights:
             w = dict(zip(("frontend", "api", "processor"), (float(x) for x in a.cpu_weights.split(":"))))
-        # the platform's own processes are not replicas (no cap): the backing services and the
-        # load generator, plus the external ingress when load enters through it
+        # the platform's own processes are not replicas: the backing services and the load
+        # generator, plus the external ingress when load enters through it -- held to their
+        # reserve by their own CPU subset when the rank's set can be split (below)
         reserve = 2.0 + (INGRESS_RESERVE if ingress else 0.0)
+        if split is not None:
+            reserve = float(len(split[0]))
         unit = (cores - reserve) / (fe * w["frontend"] + api * w["api"] + proc * w["processor"])
         caps = {k: round(max(0.25, unit * w[k]), 2) for k in w}
     app_cpu = caps["frontend"]
@@ -1363,6 +1436,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     try:
         progress(f"environment up: {fe} frontend / {api} API / {proc} processor replicas")
         env.start()
+        if split is not None:  # this process (controller, duty-cycle limiter, load generators to come)
+            pin_all_threads(split[0])
         lim = env.ctl.limiter.describe()
         fe_ports = [r.app_port for r in env.replicas(FRONTEND)]
         ca_file = None
@@ -1427,6 +1502,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         # every thread that did work in the timed region: the stderr diagnostics line only
         threads_all = [t for t in hot_threads(th0, th1, dt, top=200) if t[2] >= 0.005]
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
+        platform_cpu = _platform_cpu(env, split, pinned, {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()})
+        platform_cpu["outside_rank_set"] = int(d.max(platform_cpu["outside_rank_set"]))
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
         busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}  # cores busy per role
@@ -1515,10 +1592,11 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         if sweep_info is not None:  # span exporters flush at least once a second
             if not dsteps:
                 time.sleep(1.5)
-            trace = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.trace_ids, sweeper.slowest_trace())
+            trace = sweep_trace(str(env.ctl.dir / "telemetry"), sweeper.sampled_trace_ids + sweeper.trace_ids, None)
             # the record keeps the sweep's largest hops; every span goes to the stderr diagnostics
             spans = (trace or {}).get("spans_p50_ms") or {}
             sweep_info["trace_top_spans_p50_ms"] = dict(sorted(spans.items(), key=lambda kv: -kv[1])[:4])
+            sweep_info["trace_of"] = "the warmup's sampled sweeps (the timed region's are unsampled)"
         envelope = alt = None
         asteps = 0 if shared else a.alt_steps if a.alt_steps >= 0 else max(2, a.steps // 2)
         if (a.envelope_s > 0 or asteps) and not shared:  # after the headline's environment is down
@@ -1551,7 +1629,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "threads": threads_all}), file=sys.stderr, flush=True)
             summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
-                                     ingest)
+                                     ingest, platform_cpu)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
@@ -1574,6 +1652,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                        if ingress else "bypassed: the load generator balances over the frontend replicas"),
                            "hot_threads": hot,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
+                           "platform_cpu": platform_cpu,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
                                           "mechanism": lim.get("cpu"), "mode": lim.get("mode"),
                                           "throttling_in_timed_region": throttling},

@@ -35,7 +35,7 @@ def test_bench_single_process():
     env = dict(os.environ, PYTHONPATH=str(ROOT))
     r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--batch", "32",
                         "--api-replicas", "1", "--processor-replicas", "1", "--envelope-s", "4",
-                        "--keda-messages", "300"],
+                        "--keda-messages", "300", "--ingest-messages", "64"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -55,6 +55,15 @@ def test_bench_single_process():
     w = cfg["api_wire"]
     # (a sweep inside the timed region adds its markoverdue saves, over gRPC too)
     assert w["grpc.PublishEvent"] == w["publish"] == 64 and w["grpc.SaveState"] == w["state.save"] >= 64
+    # the whole browser session and the external-task ingestion, at the headline's replica counts
+    bs = cfg["browser_session"]
+    assert bs["errors"] == 0 and bs["flows"] == 32 and set(bs["latency_ms"]) == {
+        "create", "list", "edit_get", "edit_post", "complete", "delete", "list_after"}, bs
+    ing = cfg["external_ingest"]
+    assert ing["all_processed"] and ing["blobs_written"] == 64 and ing["dead"] == 0, ing
+    # the platform's processes on their own CPUs, every thread inside the rank's set
+    pc = cfg["platform_cpu"]
+    assert pc["outside_rank_set"] == 0 and pc["outside_own_subset"] == 0 and pc["threads_checked"] > 10, pc
     # the same flow with the other protocol, in its own environment: HTTP, no gRPC call
     alt = cfg["api_protocol_alt"]
     assert alt["api_protocol"] == "http" and alt["value"] > 0 and alt["api_wire"]["grpc.SaveState"] == 0

@@ -508,3 +508,6 @@ def test_shared_env_frontend_eight_ranks_exactly_once():
     # marks them (the sweeps of the run, then sweeps until one marks nothing)
     drain = sw["drain"]
     assert drain["expected_past_due"] == 8 * 4 * 3 and drain["exactly_once"], drain
+    # no thread of any rank's processes may run outside that rank's CPU set (the max over ranks)
+    pc = cfg["platform_cpu"]
+    assert pc["outside_rank_set"] == 0 and pc["threads_checked"] > 0, pc
