@@ -78,3 +78,25 @@ def test_image_runs_module1_acceptance(built, variant):  # every mode of MODES, 
     # every mode (incl. the gRPC sidecar protocol) finds all the code its paths import
     assert [m["mode"] for m in v["modes"]] == image.MODES["backend_api"]
     assert all(m["clean"] for m in v["modes"]), v["log"][-3000:]
+
+
+def test_module12_table_for_all_three_services(built, tmp_path_factory, capsys):
+    """Module 12's table (docs/aca/12-optimize-containers/index.md:318-326) for every service on
+    the current tree: standard vs chiseled -- files, uncompressed and compressed size, Python
+    distributions, shared libraries -- printed (``pytest -s``) and the chiseled image smaller on
+    every size axis.  The numbers are recorded in profiles/r6_container_images.md."""
+    out = tmp_path_factory.mktemp("images3")
+    rows = [r.row() for r in built.values()]
+    for svc in ("processor", "frontend"):
+        closure = image.full_closure(svc)
+        rows += [image.build_image(svc, v, out, closure).row() for v in ("standard", "chiseled")]
+    by = {(r["service"], r["variant"]): r for r in rows}
+    with capsys.disabled():
+        for r in rows:
+            print(json.dumps({k: r[k] for k in ("service", "variant", "files", "uncompressed_mb", "compressed_mb",
+                                                "python_distributions", "shared_libs")}))
+    for svc in ("backend_api", "processor", "frontend"):
+        std, ch = by[(svc, "standard")], by[(svc, "chiseled")]
+        assert ch["files"] < std["files"] and ch["uncompressed_mb"] < std["uncompressed_mb"]
+        assert ch["compressed_mb"] < std["compressed_mb"] and ch["shared_libs"] < std["shared_libs"]
+        assert ch["python_distributions"] == std["python_distributions"]  # the same code, less base
