@@ -243,9 +243,13 @@ class BackingFront {
   ~BackingFront() { stop(); }
 
   // A query the indexes do not answer (a scan the columnar / GPU accelerator may take) runs on
-  // one query worker thread through `query_fn` -- the Python planner, backing/server.py
+  // a small pool of query worker threads (kQueryWorkers, TT_BACKING_QUERY_THREADS; the Python
+  // route's query_pool had 4) through `query_fn` -- the Python planner, backing/server.py
   // BackingServices.run_query, called with the GIL -- and its answer goes back from the front's
   // loop: the page of results makes no extra HTTP hop through the Python server's event loop.
+  // One slow scan (or a collection's first mirror build) holds one worker, not every other
+  // collection's queries; the accelerator's per-collection lock keeps a collection's GPU use
+  // serial.
   struct QueryJob {
     std::string account, db, coll, body, prefix, traceparent, sent_mono, front_mono;
     bool sort_keys = false;
@@ -259,11 +263,14 @@ class BackingFront {
   void set_query_fn(QueryFn fn) {
     std::lock_guard l(q_mu_);
     query_fn_ = std::move(fn);
-    if (!q_thread_.joinable() && query_fn_) {
-      q_thread_ = std::thread([this] {
-        pthread_setname_np(pthread_self(), "tt-front-query");
-        query_loop();
-      });
+    if (q_threads_.empty() && query_fn_) {
+      int n = 4;
+      if (const char* v = std::getenv("TT_BACKING_QUERY_THREADS"); v && std::atoi(v) > 0) n = std::min(32, std::atoi(v));
+      for (int i = 0; i < n; ++i)
+        q_threads_.emplace_back([this] {
+          pthread_setname_np(pthread_self(), "tt-front-query");
+          query_loop();
+        });
     }
   }
 
@@ -278,7 +285,9 @@ class BackingFront {
       q_stop_ = true;
     }
     q_cv_.notify_all();
-    if (q_thread_.joinable()) q_thread_.join();
+    for (auto& t : q_threads_)
+      if (t.joinable()) t.join();
+    q_threads_.clear();
     {
       std::lock_guard l(q_mu_);
       query_fn_ = nullptr;  // drop the Python callable before the interpreter may go
@@ -331,7 +340,7 @@ class BackingFront {
   std::condition_variable q_cv_;
   std::deque<QueuedQuery> q_jobs_;
   QueryFn query_fn_;
-  std::thread q_thread_;
+  std::vector<std::thread> q_threads_;
   bool q_stop_ = false;
   struct Parked {
     std::string ns, entity;

@@ -1265,7 +1265,13 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
         t_drain = next((t for t, _, done in samples if done >= messages), None)
         t_in = next((t for t, n, _ in samples if t_drain is not None and t >= t_drain and n <= 1), None)
         ev = (env.ctl.apps[PROC].scale_events if env.ctl else [])
+        polls = list(env.ctl.apps[PROC].polls) if env.ctl else []
+        busy = [p[0] for p in polls if p[1]]
+        wall0 = time.time() - (time.perf_counter() - t0)  # t0 on the wall clock (the polls' clock)
+        ins = [e["ts"] for e in ev if busy and e["ts"] > busy[-1] and e["replicas"] <= 1]
         return {"messages": messages, "published_in_s": round(sent_s, 2), "peak_replicas": peak,
+                "polls": len(polls), "last_active_poll_s": round(busy[-1] - wall0, 2) if busy else None,
+                "scale_in_after_last_active_poll_s": round(ins[0] - busy[-1], 2) if ins else None,
                 "time_to_peak_s": t_peak, "drain_s": t_drain, "scaled_in_to_1_s": t_in,
                 "replica_timeline": timeline,  # [seconds since the first publish, replicas], on change
                 "scale_events": [e["replicas"] for e in ev],

@@ -325,3 +325,25 @@ class _NoRedirect(urllib.request.HTTPRedirectHandler):
         return fp
 
     http_error_301 = http_error_302
+
+
+@pytest.mark.slow
+def test_keda_reference_timings_30s_polling_300s_cooldown(tmp_path):
+    """Module 9 at ACA's own KEDA timings (docs/aca/09-aca-autoscale-keda/index.md:224-226):
+    30 s polling and a 300 s cooldown, not the bench's shortened ones.  A scaled-down burst
+    (3,000 messages of 1 s simulated work each, the module-9 notifier) on the processor's
+    subscription scales it 1 -> 5 (messageCount 10 per replica, processor-backend-service.bicep:
+    159-183); after the backlog drains it stays at 5 until a full cooldown past the last poll
+    that saw messages, then returns to 1; every message is completed once."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_keda", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    k = bench.keda_stage(str(tmp_path), 0, 3000, polling_s=30.0, cooldown_s=300.0, budget_s=600.0)
+    assert "error" not in k, k
+    assert k["peak_replicas"] == 5 and k["exactly_once"], k
+    assert k["keda_polling_s"] == 30.0 and k["keda_cooldown_s"] == 300.0
+    # no scale-in before 300 s after the last active poll; and it comes within one more poll
+    assert k["scale_in_after_last_active_poll_s"] is not None, k
+    assert 300.0 <= k["scale_in_after_last_active_poll_s"] <= 300.0 + 2 * 30.0, k
+    assert k["replica_timeline"][0][1] == 1 and k["replica_timeline"][-1][1] == 1
