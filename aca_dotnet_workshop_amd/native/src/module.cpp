@@ -160,36 +160,46 @@ static PyObject* headers_dict_fast(const ev::HeaderList& headers) {
 
 static py::list events_to_py(std::vector<apphost::Event>& evs, bool with_times) {
   // the finished log lines of the batch (native routes' records on the JSON sink's fast path)
-  // go up as ONE event per (level, logger): (4, level, logger name, the lines joined) -- two
-  // lines per created task otherwise cost a tuple, a call and a sink lock each in Python
-  std::vector<size_t> keep;
-  keep.reserve(evs.size());
+  // go up as ONE event per run of consecutive lines of one (level, logger): (4, level, logger
+  // name, the lines joined) -- two lines per created task otherwise cost a tuple, a call and a
+  // sink lock each in Python.  A run keeps its place among the other events, so the log's order
+  // is the order the I/O thread produced it in.
+  struct Item {
+    long batch = -1;  // >= 0: a run of lines; else the event `ev`
+    size_t ev = 0;
+  };
+  std::vector<Item> items;
+  items.reserve(evs.size());
   std::vector<std::pair<std::pair<int, std::string>, std::string>> batches;
   for (size_t i = 0; i < evs.size(); ++i) {
     auto& e = evs[i];
     if (e.kind != apphost::Event::LOG || e.line.empty() || with_times) {
-      keep.push_back(i);
+      items.push_back({-1, i});
       continue;
     }
     auto key = std::make_pair(e.err, e.msg.method);
-    size_t b = 0;
-    while (b < batches.size() && batches[b].first != key) ++b;
-    if (b == batches.size()) batches.emplace_back(key, std::string());
-    batches[b].second += e.line;
+    if (!items.empty() && items.back().batch >= 0 && batches[(size_t)items.back().batch].first == key) {
+      batches[(size_t)items.back().batch].second += e.line;
+      continue;
+    }
+    batches.emplace_back(key, e.line);
+    items.push_back({(long)batches.size() - 1, 0});
   }
-  py::list out(keep.size() + batches.size());
-  for (size_t bi = 0; bi < batches.size(); ++bi) {
+  py::list out(items.size());
+  for (size_t ki = 0; ki < items.size(); ++ki) {
+    if (items[ki].batch < 0) continue;
+    auto& b = batches[(size_t)items[ki].batch];
     py::object t = py::reinterpret_steal<py::object>(PyTuple_New(4));
     if (!t) throw py::error_already_set();
     set_item(t.ptr(), 0, PyLong_FromLong(4));
-    set_item(t.ptr(), 1, PyLong_FromLong(batches[bi].first.first));
-    set_item(t.ptr(), 2, new_str(batches[bi].first.second));
-    set_item(t.ptr(), 3, new_str(batches[bi].second));
-    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)(keep.size() + bi), t.release().ptr());
+    set_item(t.ptr(), 1, PyLong_FromLong(b.first.first));
+    set_item(t.ptr(), 2, new_str(b.first.second));
+    set_item(t.ptr(), 3, new_str(b.second));
+    PyList_SET_ITEM(out.ptr(), (Py_ssize_t)ki, t.release().ptr());
   }
-  for (size_t ki = 0; ki < keep.size(); ++ki) {
-    const size_t i = keep[ki];
-    auto& e = evs[i];
+  for (size_t ki = 0; ki < items.size(); ++ki) {
+    if (items[ki].batch >= 0) continue;
+    auto& e = evs[items[ki].ev];
     py::object t;
     if (e.kind == apphost::Event::REQUEST) {
       t = py::reinterpret_steal<py::object>(PyTuple_New(with_times ? 9 : 8));
