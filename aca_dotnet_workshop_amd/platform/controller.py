@@ -72,10 +72,10 @@ class AppRuntime:
     restarts: int = 0
     last_metrics: dict[str, float] = field(default_factory=dict)
     scale_events: list[dict[str, Any]] = field(default_factory=list)
-    # every scaler poll (wall time, whether a trigger was active, replicas before / decided):
-    # KEDA's polling and cooldown are observable -- a scale-in must not come sooner than one
-    # cooldown after the last active poll
-    polls: list[tuple[float, bool, int, int]] = field(default_factory=list)
+    # every scaler poll (wall time, whether a trigger was active, replicas before, decided, the
+    # poll's own recommendation): KEDA's polling and the HPA's scale-down stabilization window are
+    # observable -- a scale-in comes one window after the last poll that recommended more
+    polls: list[tuple[float, bool, int, int, int]] = field(default_factory=list)
 
     @property
     def name(self) -> str:
@@ -571,7 +571,8 @@ class EnvironmentController:
                 rt.last_metrics = metrics
                 cur = len([r for r in (rt.current.replicas if rt.current else []) if r.alive()])
                 want = rt.autoscaler.decide(metrics, cur)
-                rt.polls.append((time.time(), any(v > 0 for v in metrics.values()), cur, want))
+                rt.polls.append((time.time(), any(v > 0 for v in metrics.values()), cur, want,
+                                 rt.autoscaler.last_rec))
                 del rt.polls[:-2000]
                 if want != cur:
                     await self.scale_to(rt, want, f"metrics={metrics}")

@@ -73,6 +73,7 @@ class Autoscaler:
     cooldown: float = 300.0
     history: list[tuple[float, int]] = field(default_factory=list)
     last_active: float = field(default_factory=time.monotonic)
+    last_rec: int = 0
 
     def decide(self, metrics: dict[str, float], current: int, now: float | None = None) -> int:
         now = time.monotonic() if now is None else now
@@ -87,6 +88,7 @@ class Autoscaler:
                 rec = max(rec, 1)
             elif now - self.last_active < self.cooldown:
                 rec = max(rec, min(current, 1))
+        self.last_rec = rec  # this poll's own recommendation, before the stabilization window
         self.history.append((now, rec))
         self.history = [(t, r) for t, r in self.history if now - t <= self.cooldown]
         if rec >= current:

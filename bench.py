@@ -1266,12 +1266,22 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
         t_in = next((t for t, n, _ in samples if t_drain is not None and t >= t_drain and n <= 1), None)
         ev = (env.ctl.apps[PROC].scale_events if env.ctl else [])
         polls = list(env.ctl.apps[PROC].polls) if env.ctl else []
-        busy = [p[0] for p in polls if p[1]]
+        for _ in range(120):  # the scale-in's event is recorded once its replicas have stopped
+            if not polls or any(e["replicas"] <= 1 and e["ts"] > max(p[0] for p in polls if p[4] > 1)
+                                for e in ev if any(p[4] > 1 for p in polls)):
+                break
+            time.sleep(0.25)
+            polls = list(env.ctl.apps[PROC].polls)
         wall0 = time.time() - (time.perf_counter() - t0)  # t0 on the wall clock (the polls' clock)
-        ins = [e["ts"] for e in ev if busy and e["ts"] > busy[-1] and e["replicas"] <= 1]
+        busy = [p[0] for p in polls if p[1]]
+        high = [p[0] for p in polls if p[4] > 1]  # polls that recommended more than one replica
+        ins = [e["ts"] for e in ev if high and e["ts"] > high[-1] and e["replicas"] <= 1]
         return {"messages": messages, "published_in_s": round(sent_s, 2), "peak_replicas": peak,
                 "polls": len(polls), "last_active_poll_s": round(busy[-1] - wall0, 2) if busy else None,
-                "scale_in_after_last_active_poll_s": round(ins[0] - busy[-1], 2) if ins else None,
+                "last_scale_out_recommendation_s": round(high[-1] - wall0, 2) if high else None,
+                # HPA scale-down stabilization (KEDA cooldown): back to 1 one window after the last
+                # poll that asked for more
+                "scale_in_after_last_recommendation_s": round(ins[0] - high[-1], 2) if ins else None,
                 "time_to_peak_s": t_peak, "drain_s": t_drain, "scaled_in_to_1_s": t_in,
                 "replica_timeline": timeline,  # [seconds since the first publish, replicas], on change
                 "scale_events": [e["replicas"] for e in ev],
