@@ -58,6 +58,7 @@
 #include "daprpb.hpp"
 #include "h2.hpp"
 #include "taskcodec.hpp"
+#include "sweepcodec.hpp"
 #include "textutil.hpp"
 
 namespace tt::apphost {
@@ -968,10 +969,13 @@ class AppHost {
     call_step(j, "query", r.query_target, std::move(q), false, [this, j](std::string&& body) {
       const NativeRoute& r = *j->route;
       std::string json, out;
-      if (r.grpc && !daprpb::query_response_json(body, json)) return decline(*j);
       size_t count = 0;
       bool more = false;
-      if (!::taskcodec::query_tasks(r.grpc ? json : body, out, count, true, &more, false)) return decline(*j);
+      // the sidecar's answer read straight into the page (sweepcodec.hpp); else via its JSON
+      if (!(r.grpc && ::taskcodec::query_pb_tasks(body, out, count, true, &more, false))) {
+        if (r.grpc && !daprpb::query_response_json(body, json)) return decline(*j);
+        if (!::taskcodec::query_tasks(r.grpc ? json : body, out, count, true, &more, false)) return decline(*j);
+      }
       finish(*j, r.status, {{"Content-Type", r.content_type}, {r.more_header, more ? "true" : "false"}}, out);
     });
     return true;
@@ -985,7 +989,8 @@ class AppHost {
     if (!ctype.empty() && ctype.find("json") == std::string::npos) return false;
     std::vector<std::string> ids;
     std::string unused;
-    if (!::taskcodec::mark_overdue(m.body, ids, unused)) return false;  // the general binder's
+    if (!::taskcodec::mark_overdue_ids(m.body, ids) && !::taskcodec::mark_overdue(m.body, ids, unused))
+      return false;  // the general binder's
     std::unordered_set<std::string> seen;
     for (auto& id : ids)
       if (seen.insert(id).second) j->pending.push_back(id);  // dict.fromkeys: first occurrence
@@ -1011,15 +1016,17 @@ class AppHost {
     }
     call_step(j, "bulk", r.bulk_target, std::move(body), false, [this, j](std::string&& got) {
       const NativeRoute& r = *j->route;
-      std::string json, bulk;
-      if (r.grpc && !daprpb::bulk_state_response_json(got, json)) return decline(*j);
+      std::string json, bulk, save;
       std::vector<std::string> marked;
       size_t skipped = 0;
-      if (!::taskcodec::conditional_mark(r.grpc ? json : got, bulk, marked, skipped)) return decline(*j);
+      // the bulk get's answer straight into the guarded save (sweepcodec.hpp); else via JSON
+      if (!(r.grpc && ::taskcodec::conditional_mark_pb(got, r.store, save, marked, skipped))) {
+        if (r.grpc && !daprpb::bulk_state_response_json(got, json)) return decline(*j);
+        if (!::taskcodec::conditional_mark(r.grpc ? json : got, bulk, marked, skipped)) return decline(*j);
+        if (!marked.empty() && r.grpc && !daprpb::save_state_bulk(r.store, bulk, save)) return decline(*j);
+      }
       for (auto& id : marked) log_event(r, *j, r.log_mark.render_with([&](int) -> const std::string& { return id; }));
       if (marked.empty()) return finish(*j, r.status, {});
-      std::string save;
-      if (r.grpc && !daprpb::save_state_bulk(r.store, bulk, save)) return decline(*j);
       j->pending = std::move(marked);
       call_step(
           j, "save", r.save_target, r.grpc ? std::move(save) : std::move(bulk), false,
@@ -1307,10 +1314,12 @@ class AppHost {
     call_step(j, "query", r.query_target, std::move(body), false, [this, j](std::string&& res) {
       const NativeRoute& r = *j->route;
       std::string json, out;
-      if (r.grpc && !daprpb::query_response_json(res, json)) return decline(*j);
       size_t count = 0;
       bool more = false;
-      if (!::taskcodec::query_tasks(r.grpc ? json : res, out, count, true, &more, true)) return decline(*j);
+      if (!(r.grpc && ::taskcodec::query_pb_tasks(res, out, count, true, &more, true))) {
+        if (r.grpc && !daprpb::query_response_json(res, json)) return decline(*j);
+        if (!::taskcodec::query_tasks(r.grpc ? json : res, out, count, true, &more, true)) return decline(*j);
+      }
       finish(*j, r.status, {{"Content-Type", r.content_type}}, out);
     });
     return true;

@@ -169,6 +169,167 @@ inline bool save_state_bulk(std::string_view store, std::string_view body, std::
 }
 
 namespace detail {
+// The end of the JSON string whose opening quote is at p[-1] (past its closing quote), 16 bytes
+// a step; the same end tt::skip_value finds (an escape skips the byte after the backslash).
+inline const char* string_end(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+  while (true) {
+    while (e - p >= 16) {
+      const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+      const int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, bs)));
+      if (m) {
+        p += __builtin_ctz((unsigned)m);
+        break;
+      }
+      p += 16;
+    }
+    while (p < e && *p != '"' && *p != '\\') ++p;
+    if (p >= e) return p + 1;
+    if (*p == '"') return p + 1;
+    p += 2;  // an escape: the next byte is part of it
+    if (p >= e) return p + 1;
+  }
+}
+
+// tt::skip_value's end of the value at p (no leading whitespace), with strings skipped 16 bytes
+// a step; `ws`: whether the value holds whitespace outside its strings (tt::compact would
+// change it).
+inline const char* value_end(const char* p, const char* e, bool& ws) {
+  ws = false;
+  if (p >= e) return p;
+  if (*p == '"') return string_end(p + 1, e);
+  if (*p == '{' || *p == '[') {
+    int depth = 0;
+    while (p < e) {
+      const char c = *p;
+      if (c == '"') {
+        p = string_end(p + 1, e);
+        continue;
+      }
+      if (c == '{' || c == '[') ++depth;
+      else if (c == '}' || c == ']') {
+        if (--depth == 0) return p + 1;
+      } else if (c == ' ' || c == '\n' || c == '\r' || c == '\t') {
+        ws = true;
+      }
+      ++p;
+    }
+    return p;
+  }
+  while (p < e && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+  return p;
+}
+}  // namespace detail
+
+// The state query API's answer ({"results":[{"key","data","etag"[,"error"]}],"token"}) as a
+// QueryStateResponse in one pass, without a value tree: a sweep page of thousands of tasks
+// costs a scan, not a parse and a dump per task.  Keys, etags and the token must be plain
+// strings (no escapes), each data value goes over compacted (as it is when it has no whitespace
+// to drop); any other shape (metadata, escapes) returns false and the tree path encodes it.
+inline bool query_response_pb(std::string_view b, std::string& out) {
+  const char* p = b.data();
+  const char* const e = p + b.size();
+  auto lit = [&](char ch) {
+    p = tt::ws_end(p, e);
+    if (p < e && *p == ch) {
+      ++p;
+      return true;
+    }
+    return false;
+  };
+  auto null = [&] {
+    p = tt::ws_end(p, e);
+    if (e - p >= 4 && std::string_view(p, 4) == "null") {
+      p += 4;
+      return true;
+    }
+    return false;
+  };
+  auto plain = [&](std::string_view& s) {
+    p = tt::ws_end(p, e);
+    if (p >= e || *p != '"') return false;
+    const char* q = detail::string_end(p + 1, e) - 1;  // the closing quote, or a backslash's run
+    if (q >= e || *q != '"') return false;
+    for (const char* x = p + 1; x < q; ++x)
+      if (*x == '\\') return false;
+    s = std::string_view(p + 1, (size_t)(q - p - 1));
+    p = q + 1;
+    return true;
+  };
+  pb::Writer w;
+  w.s.reserve(b.size());
+  std::string squeezed;
+  if (!lit('{')) return false;
+  if (!lit('}')) {
+    while (true) {
+      std::string_view k;
+      if (!plain(k) || !lit(':')) return false;
+      if (k == "results") {
+        if (!null()) {
+          if (!lit('[')) return false;
+          if (!lit(']')) {
+            while (true) {
+              if (!lit('{')) return false;
+              std::string_view key, etag, err, data;
+              if (!lit('}')) {
+                while (true) {
+                  std::string_view f;
+                  if (!plain(f) || !lit(':')) return false;
+                  if (f == "data") {
+                    if (!null()) {
+                      const char* s0 = tt::ws_end(p, e);
+                      bool ws = false;
+                      p = detail::value_end(s0, e, ws);
+                      if (p > e || p == s0) return false;
+                      data = std::string_view(s0, (size_t)(p - s0));
+                      if (ws) {
+                        squeezed = tt::compact(data);
+                        data = squeezed;
+                      }
+                    }
+                  } else if (f == "key" || f == "etag" || f == "error") {
+                    std::string_view v;
+                    if (!null() && !plain(v)) return false;
+                    (f == "key" ? key : f == "etag" ? etag : err) = v;
+                  } else {
+                    return false;
+                  }
+                  if (lit(',')) continue;
+                  if (lit('}')) break;
+                  return false;
+                }
+              }
+              // QueryStateItem {key = 1, data = 2, etag = 3, error = 4}, its length first
+              w.len_header(1, pb::str_size(1, key.size()) + pb::str_size(2, data.size()) +
+                                  pb::str_size(3, etag.size()) + pb::str_size(4, err.size()));
+              w.str(1, key);
+              w.str(2, data);
+              w.str(3, etag);
+              w.str(4, err);
+              if (lit(',')) continue;
+              if (lit(']')) break;
+              return false;
+            }
+          }
+        }
+      } else if (k == "token") {
+        std::string_view t;
+        if (!null() && !plain(t)) return false;
+        w.str(2, t);
+      } else {
+        return false;
+      }
+      if (lit(',')) continue;
+      if (lit('}')) break;
+      return false;
+    }
+  }
+  if (tt::ws_end(p, e) != e) return false;
+  out = std::move(w.s);
+  return true;
+}
+
+namespace detail {
 inline void item_json(std::string& out, std::string_view key, std::string_view data, std::string_view etag,
                       bool etag_always) {
   out += "{\"key\":";

@@ -36,6 +36,7 @@
 #include <sstream>
 
 #include "evhttp.hpp"
+#include "daprpb.hpp"
 #include "h2.hpp"
 #include "json.hpp"
 #include "pb.hpp"
@@ -2057,108 +2058,6 @@ class DataPlane {
     return o + "}";
   }
 
-  // The state query API's answer ({"results":[{"key","data","etag"[,"error"]}],"token"}) as a
-  // QueryStateResponse in one pass, without a value tree: a sweep page of thousands of tasks
-  // costs a scan, not a parse and a dump per task.  Keys, etags and the token must be plain
-  // strings (no escapes), each data value goes over compacted; any other shape (metadata,
-  // escapes) returns false and the tree path encodes it.
-  static bool query_pb_fast(std::string_view b, std::string& out) {
-    const char* p = b.data();
-    const char* const e = p + b.size();
-    auto lit = [&](char ch) {
-      p = tt::ws_end(p, e);
-      if (p < e && *p == ch) {
-        ++p;
-        return true;
-      }
-      return false;
-    };
-    auto null = [&] {
-      p = tt::ws_end(p, e);
-      if (e - p >= 4 && std::string_view(p, 4) == "null") {
-        p += 4;
-        return true;
-      }
-      return false;
-    };
-    auto plain = [&](std::string_view& s) {
-      p = tt::ws_end(p, e);
-      if (p >= e || *p != '"') return false;
-      const char* q = p + 1;
-      while (q < e && *q != '"') {
-        if (*q == '\\') return false;
-        ++q;
-      }
-      if (q >= e) return false;
-      s = std::string_view(p + 1, (size_t)(q - p - 1));
-      p = q + 1;
-      return true;
-    };
-    pb::Writer w;
-    if (!lit('{')) return false;
-    if (!lit('}')) {
-      while (true) {
-        std::string_view k;
-        if (!plain(k) || !lit(':')) return false;
-        if (k == "results") {
-          if (!null()) {
-            if (!lit('[')) return false;
-            if (!lit(']')) {
-              while (true) {
-                if (!lit('{')) return false;
-                std::string_view key, etag, err, data;
-                if (!lit('}')) {
-                  while (true) {
-                    std::string_view f;
-                    if (!plain(f) || !lit(':')) return false;
-                    if (f == "data") {
-                      if (!null()) {
-                        const char* s0 = tt::ws_end(p, e);
-                        p = tt::skip_value(s0, e);
-                        if (p > e || p == s0) return false;
-                        data = std::string_view(s0, (size_t)(p - s0));
-                      }
-                    } else if (f == "key" || f == "etag" || f == "error") {
-                      std::string_view v;
-                      if (!null() && !plain(v)) return false;
-                      (f == "key" ? key : f == "etag" ? etag : err) = v;
-                    } else {
-                      return false;
-                    }
-                    if (lit(',')) continue;
-                    if (lit('}')) break;
-                    return false;
-                  }
-                }
-                pb::Writer it;
-                it.str(1, key);
-                if (!data.empty()) it.str(2, compact(data));
-                it.str(3, etag);
-                it.str(4, err);
-                w.len_field(1, it.s);
-                if (lit(',')) continue;
-                if (lit(']')) break;
-                return false;
-              }
-            }
-          }
-        } else if (k == "token") {
-          std::string_view t;
-          if (!null() && !plain(t)) return false;
-          w.str(2, t);
-        } else {
-          return false;
-        }
-        if (lit(',')) continue;
-        if (lit('}')) break;
-        return false;
-      }
-    }
-    if (tt::ws_end(p, e) != e) return false;
-    out = std::move(w.s);
-    return true;
-  }
-
   void on_grpc(h2::GrpcCall&& c, h2::GrpcReply r) {
     static constexpr std::string_view kSvc = "/dapr.proto.runtime.v1.Dapr/";
     if (c.path.compare(0, kSvc.size(), kSvc) != 0) {
@@ -2262,7 +2161,7 @@ class DataPlane {
                 "application/json", {}, [r, rpc](int status, const HeaderList&, std::string_view body) {
                   if (status >= 300) return grpc_fail(r, status, body, rpc);
                   std::string fast;
-                  if (query_pb_fast(body, fast)) return r.ok(fast);
+                  if (tt::daprpb::query_response_pb(body, fast)) return r.ok(fast);
                   pb::Writer w;  // QueryStateResponse {results = 1 {key, data, etag, error}, token = 2, metadata = 3}
                   try {
                     Value js = body.empty() ? Value() : parse(body);

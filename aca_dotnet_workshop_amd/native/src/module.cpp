@@ -14,6 +14,7 @@
 #include "dutycycle.hpp"
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
+#include "sweepcodec.hpp"
 #include "formcodec.hpp"
 #include "strrank.hpp"
 
@@ -413,6 +414,32 @@ PYBIND11_MODULE(_ttnative, m) {
     std::string out;
     if (!tt::daprpb::bulk_state_response_json(view(msg), out)) return py::none();
     return py::bytes(out);
+  });
+  // the query API's JSON -> QueryStateResponse (the sidecar's one-pass encoder), or None
+  m.def("dapr_pb_query_from_json", [view](py::bytes body) -> py::object {
+    std::string out;
+    if (!tt::daprpb::query_response_pb(view(body), out)) return py::none();
+    return py::bytes(out);
+  });
+  // the sweep's one-pass pb hops (sweepcodec.hpp), or None where the caller runs the chain
+  m.def("tasks_from_query_pb", [view](py::bytes msg, bool by_created, bool descending) -> py::object {
+    std::string out;
+    size_t count = 0;
+    bool more = false;
+    if (!taskcodec::query_pb_tasks(view(msg), out, count, by_created, &more, descending)) return py::none();
+    return py::make_tuple(count, py::bytes(out), more);
+  });
+  m.def("tasks_conditional_mark_pb", [view](py::bytes msg, const std::string& store) -> py::object {
+    std::string save;
+    std::vector<std::string> ids;
+    size_t skipped = 0;
+    if (!taskcodec::conditional_mark_pb(view(msg), store, save, ids, skipped)) return py::none();
+    return py::make_tuple(py::bytes(save), ids, skipped);
+  });
+  m.def("tasks_mark_overdue_ids", [view](py::bytes body) -> py::object {
+    std::vector<std::string> ids;
+    if (!taskcodec::mark_overdue_ids(view(body), ids)) return py::none();
+    return py::cast(ids);
   });
   // QueryStateResponse -> the query API's JSON ({"results":[..],"token"}), or None
   m.def("dapr_pb_query_json", [view](py::bytes msg) -> py::object {

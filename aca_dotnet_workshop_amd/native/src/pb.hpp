@@ -86,8 +86,24 @@ inline bool map_entry(std::string_view entry, std::string& k, std::string& v) {
   return r.ok;
 }
 
+// Encoded sizes, for writing a sub-message's length before its fields (no temporary message).
+inline size_t varint_size(uint64_t v) {
+  size_t n = 1;
+  while (v >= 0x80) v >>= 7, ++n;
+  return n;
+}
+// a length-delimited field of `n` bytes (written always: repeated element / sub-message)
+inline size_t len_field_size(uint32_t field, size_t n) { return varint_size((uint64_t)field << 3) + varint_size(n) + n; }
+// a proto3 singular string / bytes field (not written when empty)
+inline size_t str_size(uint32_t field, size_t n) { return n ? len_field_size(field, n) : 0; }
+
 struct Writer {
   std::string s;
+  // the header of a length-delimited field whose `n` bytes the caller appends next
+  void len_header(uint32_t field, size_t n) {
+    key(field, 2);
+    varint(n);
+  }
   void varint(uint64_t v) {
     while (v >= 0x80) {
       s.push_back((char)(0x80 | (v & 0x7f)));

@@ -666,9 +666,10 @@ inline bool fast_task_at(std::string_view t, size_t& i, std::string& out, uint64
       return false;
     }
   }
-  std::string c, d;  // a 28-byte date does not fit the small-string buffer: one allocation each
-  c.reserve(40);
-  d.reserve(40);
+  // a 28-byte date does not fit the small-string buffer: per-thread scratch, no allocation a task
+  static thread_local std::string c, d;
+  c.clear();
+  d.clear();
   if (!parse_due(created.substr(1, created.size() - 2), c, store_form) || !parse_due(due.substr(1, due.size() - 2), d))
     return false;
   out += "{\"taskId\":\"";

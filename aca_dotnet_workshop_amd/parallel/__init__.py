@@ -298,6 +298,27 @@ def pin_all_threads(cpus: set[int]) -> None:
             pass
 
 
+def enforce_cpuset(pid: int, cpus: set[int]) -> list[str]:
+    """Re-pin every thread of ``pid`` allowed outside ``cpus`` back into them, the way a cgroup
+    cpuset holds all of a container's threads (an affinity inherited at fork does not hold a
+    runtime that sets its own threads' affinity). Returns ``comm/tid`` of each thread moved."""
+    moved = []
+    for tid, allowed in cpus_allowed(pid).items():
+        if allowed <= cpus:
+            continue
+        try:
+            os.sched_setaffinity(tid, cpus)
+        except OSError:
+            continue
+        try:
+            with open(f"/proc/{pid}/task/{tid}/comm") as f:
+                name = f.read().strip()
+        except OSError:
+            name = "?"
+        moved.append(f"{name}/{tid}")
+    return moved
+
+
 def cpus_allowed(pid: int) -> dict[int, set[int]]:
     """tid -> the CPUs each thread of ``pid`` may run on (``Cpus_allowed_list``)."""
     out: dict[int, set[int]] = {}

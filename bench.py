@@ -307,6 +307,8 @@ class OverdueSweeper:
                 "sweep_p99_ms": round(ms[min(len(ms) - 1, int(len(ms) * 0.99))], 2) if ms else None,
                 "sweep_max_ms": round(ms[-1], 2) if ms else None,
                 "sweep_ms": [round(d * 1e3, 2) for d, _ in self.runs],  # every sweep, in run order
+                # per sweep, in run order: [tasks marked, the GET hop's ms, the markoverdue calls' ms]
+                "sweep_detail": [[r.get("markedOverdue", 0), r.get("queryMs"), r.get("markMs")] for _, r in self.runs],
                 "tasks_marked_overdue": sum(r.get("markedOverdue", 0) for _, r in self.runs),
                 "pages": sum(r.get("pages", 0) for _, r in self.runs),
                 # the job's two hops (GET api/overduetasks, POST markoverdue), summed over sweeps
@@ -1301,14 +1303,9 @@ def keda_stage(root: str, rank: int, messages: int, polling_s: float = 5.0, cool
 PLATFORM_ROLES = ("backing", "ingress", "bench")
 
 
-def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
-    """The platform's share of the rank: cores its processes used in the timed region (backing
-    services, ingress, this process with its load generators) against the CPUs reserved for
-    them, and every thread of the rank's processes checked against its CPU set (the rank's set;
-    the platform / replica subset when split): ``outside_rank_set`` counts threads that may run
-    elsewhere."""
-    from aca_dotnet_workshop_amd.parallel import cpus_allowed
-    used = sum(v for k, v in busy.items() if k.split(".")[0].startswith(PLATFORM_ROLES))
+def _rank_pids(env) -> dict[str, list[int]]:
+    """The rank's processes by side: ``platform`` (this process, ingress, backing services) and
+    ``replica`` (every replica with its sidecar and data plane)."""
     pids: dict[str, list[int]] = {"platform": [os.getpid()] + list(_ingress_pid(env).values()), "replica": []}
     st = env.stack
     if st.backing_proc is not None:
@@ -1322,23 +1319,57 @@ def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
                 pids["replica"] += [k.pid for k in psutil.Process(r.proc.pid).children(recursive=True)]
             except psutil.Error:
                 pass
+    return pids
+
+
+def _enforce_cpusets(env, split, pinned) -> list[str]:
+    """Hold every thread of the rank's processes to its side's CPU set (``enforce_cpuset``),
+    after the warmup has started the runtimes' own threads (the GPU runtime's among them)."""
+    from aca_dotnet_workshop_amd.parallel import enforce_cpuset
+    rank = set(pinned) if pinned else None
+    moved: list[str] = []
+    for side, ps in _rank_pids(env).items():
+        want = (split[0] if side == "platform" else split[1]) if split is not None else rank
+        if want:
+            for pid in ps:
+                moved += enforce_cpuset(pid, want)
+    return moved
+
+
+def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
+    """The platform's share of the rank: cores its processes used in the timed region (backing
+    services, ingress, this process with its load generators) against the CPUs reserved for
+    them, and every thread of the rank's processes checked against its CPU set (the rank's set;
+    the platform / replica subset when split): ``outside_rank_set`` counts threads that may run
+    elsewhere, ``outside`` names the first of them."""
+    from aca_dotnet_workshop_amd.parallel import cpus_allowed
+    used = sum(v for k, v in busy.items() if k.split(".")[0].startswith(PLATFORM_ROLES))
+    pids = _rank_pids(env)
     rank = set(pinned) if pinned else None
     outside = wrong_side = threads = 0
+    names: list[str] = []
     for side, ps in pids.items():
         want = (split[0] if side == "platform" else split[1]) if split is not None else rank
         for pid in ps:
-            for cpus in cpus_allowed(pid).values():
+            for tid, cpus in cpus_allowed(pid).items():
                 threads += 1
                 if rank is not None and not cpus <= rank:
                     outside += 1
                 if want is not None and not cpus <= want:
                     wrong_side += 1
+                    if len(names) < 8:
+                        try:
+                            with open(f"/proc/{pid}/task/{tid}/comm") as f:
+                                names.append(f"{side}:{f.read().strip()}/{tid}")
+                        except OSError:
+                            pass
     return {"reserved_cpus": len(split[0]) if split is not None else None, "cores_used": round(used, 2),
             "within_reserve": bool(split is None or used <= len(split[0]) + 0.05),
             "mechanism": (f"pinned: {len(split[0])} of the rank's {len(pinned)} CPUs for backing, ingress and load "
                           f"generator, the other {len(split[1])} for the replicas") if split is not None
             else "shared with the replicas (rank set too small to split)",
-            "threads_checked": threads, "outside_rank_set": outside, "outside_own_subset": wrong_side}
+            "threads_checked": threads, "outside_rank_set": outside, "outside_own_subset": wrong_side,
+            "outside": names}
 
 
 def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
@@ -1486,6 +1517,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             progress(f"warmup: {a.warmup} steps")
             run_form_loadgen(exe, targets, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
                              (gbase, stride) if shared else None, ca_file, a.loadgen_threads)
+        # the warmup started every runtime's threads: hold them all to their side's CPU set
+        repinned = _enforce_cpusets(env, split, pinned)
         progress(f"timed region: {a.steps} steps of {a.batch}")
         d.barrier()
         device_sync()
@@ -1520,6 +1553,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
         platform_cpu = _platform_cpu(env, split, pinned, {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()})
         platform_cpu["outside_rank_set"] = int(d.max(platform_cpu["outside_rank_set"]))
+        platform_cpu["repinned_before_timed"] = repinned[:8]
+        platform_cpu["repinned_threads"] = len(repinned)
         ru1 = _collection_stats(backing).get("throughput", {})
         dt_max = d.max(dt)
         busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}  # cores busy per role
