@@ -104,7 +104,9 @@ class CollectionAccelerator:
         if self._kernels is None and self.mode in ("auto", "gpu"):
             try:
                 from ..ops.gpu import GpuKernels
-                self._kernels = GpuKernels()
+                from ..parallel import hold_affinity
+                with hold_affinity():  # the runtime's threads stay on this process's CPUs
+                    self._kernels = GpuKernels()
             except Exception as e:
                 if self.mode == "gpu":
                     raise

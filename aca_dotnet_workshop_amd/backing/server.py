@@ -398,6 +398,7 @@ class BackingServices:
             d = dict(s.stats())
             d["indexedPaths"] = s.indexed_paths()
             d["throughput"] = dict(s.throughput_stats())
+            d["durability"] = {"fsync_mode": self.fsync, "group_commit": s.group_commit(), **dict(s.commit_stats())}
             a = acc(req)
             d["accelerator"] = {"mode": a.mode, "rows": a.index.live_rows() if a.index else 0, **a.stats,
                                 "mirror": dict(s.mirror_stats())}
@@ -777,7 +778,10 @@ async def serve_backing(host: str = "127.0.0.1", port: int = 0, data_dir: str | 
     """``uds``: serve on that Unix socket too (the environment's processes on this host use it:
     ``TT_BACKING_UDS``, sidecar/base.py)."""
     from ..web.server import HttpServer
-    svc = BackingServices(data_dir, AccessPolicy.from_dict(policy))
+    # TT_BACKING_FSYNC: 0 = a write is on its way to the device when acknowledged (survives a
+    # process crash), 1 = fdatasync per record, 2 = group commit (acknowledged once synced, the
+    # writes of a sync period sharing one fdatasync) -- applog.hpp
+    svc = BackingServices(data_dir, AccessPolicy.from_dict(policy), fsync=int(os.environ.get("TT_BACKING_FSYNC", "0")))
     app = svc.build_app()
     srv = HttpServer(app, asyncio.get_running_loop())
     front = None

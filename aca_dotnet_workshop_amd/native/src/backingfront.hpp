@@ -206,7 +206,10 @@ class BackingFront {
       : fallback_(ev::Endpoint::parse("unix:" + fallback_uds)) {
     ev::reserve_fd_table();  // accept() must not grow the fd table (RCU wait) under load
     threads = std::max(1, std::min(threads, 64));
-    for (int i = 0; i < threads; ++i) shards_.push_back(std::make_unique<Shard>(*this));
+    for (int i = 0; i < threads; ++i) {
+      shards_.push_back(std::make_shared<Shard>(*this));
+      shards_.back()->self = shards_.back();
+    }
     ev::Endpoint ep;
     ep.unix_socket = false;
     ep.host = host;
@@ -368,6 +371,7 @@ class BackingFront {
     std::vector<std::string> posted;               // cross-thread notifications
     std::vector<std::function<void()>> tasks;      // cross-thread work for this loop (query answers)
     std::multimap<std::string, Parked> parked;     // "ns|entity" -> waiting receives
+    std::weak_ptr<Shard> self;                     // for answers posted back after a group commit
 
     explicit Shard(BackingFront& front) : f(front), client(loop) {
       handler = [this](ev::Message&& m, ev::Reply r) { f.on_request(*this, std::move(m), std::move(r)); };
@@ -447,7 +451,7 @@ class BackingFront {
   };
 
   ev::Endpoint fallback_;
-  std::vector<std::unique_ptr<Shard>> shards_;
+  std::vector<std::shared_ptr<Shard>> shards_;
   std::atomic<size_t> next_uds_shard_{0};  // the Unix listener deals connections in turn
   int port_ = 0;
   bool stopped_ = false;
@@ -539,8 +543,9 @@ class BackingFront {
       seg.push_back(bf::unquote(std::string_view(path).substr(i, j - i)));
       i = j + 1;
     }
-    if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(m, r, seg)) return;
-    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkset" && m.method == "POST" && handle_bulkset(m, r, seg))
+    if (seg.size() == 6 && seg[0] == "cosmos" && seg[4] == "docs" && handle_doc(sh, m, r, seg)) return;
+    if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkset" && m.method == "POST" &&
+        handle_bulkset(sh, m, r, seg))
       return;
     if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "bulkget" && m.method == "POST" && handle_bulkget(m, r, seg))
       return;
@@ -619,8 +624,24 @@ class BackingFront {
     return it != colls_.end() && it->second->store ? it->second.get() : nullptr;
   }
 
+  // Answers a write once it is durable: now, or -- group commit (AppLog fsync_mode 2) -- from
+  // the engine's log committer once the sync covering this write is done, handed back to the
+  // shard's loop.  The loop goes on serving meanwhile; the writes of a sync period share one
+  // fdatasync.
+  template <class Engine>
+  void send_durable(Shard& sh, Engine* eng, ev::Reply& r, int status, ev::HeaderList h, std::string body) {
+    if (!eng->group_commit()) {
+      r.send(status, h, body);
+      return;
+    }
+    std::weak_ptr<Shard> w = sh.self;
+    eng->after_durable(eng->log_mark(), [w, r, status, h = std::move(h), body = std::move(body)] {
+      if (auto s = w.lock()) s->post_task([r, status, h, body] { r.send(status, h, body); });
+    });
+  }
+
   // -- cosmos documents ----------------------------------------------------------------------
-  bool handle_doc(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
+  bool handle_doc(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
     Coll* c = coll_of(seg);
     if (!c) return false;
     const std::string& key = seg[5];
@@ -650,7 +671,8 @@ class BackingFront {
       auto* fw = m.header("x-tt-first-write");
       try {
         std::string e = c->store->set(key, m.body, etag, fw && *fw == "1", 0);
-        r.send(200, {{"etag", e}, {"content-type", "application/json"}}, "{\"etag\": " + bf::jstr(e) + "}");
+        send_durable(sh, c->store, r, 200, {{"etag", e}, {"content-type", "application/json"}},
+                     "{\"etag\": " + bf::jstr(e) + "}");
       } catch (const EtagMismatch& ex) {
         r.send(412, {{"content-type", pj}}, bf::problem_json(412, ex.what()));
       } catch (const ParseError& ex) {
@@ -661,7 +683,8 @@ class BackingFront {
     count("doc.delete");
     try {
       bool ok = c->store->del(key, etag);
-      r.empty(ok ? 204 : 404);
+      if (ok) send_durable(sh, c->store, r, 204, {}, {});
+      else r.empty(404);
     } catch (const EtagMismatch& ex) {
       r.send(412, {{"content-type", pj}}, bf::problem_json(412, ex.what()));
     }
@@ -669,7 +692,7 @@ class BackingFront {
   }
 
   // POST .../bulkset: [{"key", "value" (JSON text or value), "etag", "firstWrite", "ttlMs"}]
-  bool handle_bulkset(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
+  bool handle_bulkset(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg) {
     Coll* c = coll_of(seg);
     if (!c) return false;
     std::vector<DocStore::BulkItem> batch;
@@ -694,7 +717,7 @@ class BackingFront {
       }
     }
     out += "]";
-    r.send(etag_err ? 412 : other_err ? 400 : 200, {{"content-type", "application/json"}}, out);
+    send_durable(sh, c->store, r, etag_err ? 412 : other_err ? 400 : 200, {{"content-type", "application/json"}}, out);
     return true;
   }
 
@@ -900,7 +923,7 @@ class BackingFront {
       uint64_t seq = b->publish(seg[3], m.body, ct ? *ct : "application/json", props ? *props : "{}", mid ? *mid : "",
                                 ttl && !ttl->empty() ? std::atoll(ttl->c_str()) : 0,
                                 delay && !delay->empty() ? std::atoll(delay->c_str()) : 0);
-      r.send(201, {{"content-type", "application/json"}}, "{\"seq\": " + std::to_string(seq) + "}");
+      send_durable(sh, b, r, 201, {{"content-type", "application/json"}}, "{\"seq\": " + std::to_string(seq) + "}");
       for (auto& sub : b->subscriptions(seg[3])) broadcast(sh, ns + "|" + seg[3] + "/subscriptions/" + sub);
       return true;
     }
@@ -960,7 +983,7 @@ class BackingFront {
           out += std::string(i ? ", " : "") +
                  (b->renew(entity, str((*l)[i], "token"), num((*l)[i], "lockMs")) ? "true" : "false");
       out += "]}";
-      r.send(200, {{"content-type", "application/json"}}, out);
+      send_durable(sh, b, r, 200, {{"content-type", "application/json"}}, out);
       if (abandoned) broadcast(sh, ns + "|" + entity);
       return true;
     }

@@ -352,6 +352,14 @@ class Broker {
     return total_published_;
   }
 
+  // group commit (AppLog fsync_mode 2): a writer's mark after its write, and the wait for the
+  // sync that covers it (the backing front answers from the callback; Python callers block)
+  bool group_commit() const { return log_.group(); }
+  uint64_t log_mark() const { return log_.mark(); }
+  void after_durable(uint64_t mark, std::function<void()> cb) { log_.after_durable(mark, std::move(cb)); }
+  void wait_durable() { log_.wait_durable(); }
+  AppLog::CommitStats commit_stats() { return log_.commit_stats(); }
+
  private:
   static std::pair<std::string, std::string> split(const std::string& path) {
     auto pos = path.find("/subscriptions/");

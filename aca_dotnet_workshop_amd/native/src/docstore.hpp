@@ -832,6 +832,13 @@ class DocStore {
   }
 
   void sync() { std::lock_guard<std::mutex> g(mu_); log_.sync(); }
+  // group commit (AppLog fsync_mode 2): a writer's mark after its write, and the wait for the
+  // sync that covers it (the backing front answers from the callback; Python callers block)
+  bool group_commit() const { return log_.group(); }
+  uint64_t log_mark() const { return log_.mark(); }
+  void after_durable(uint64_t mark, std::function<void()> cb) { log_.after_durable(mark, std::move(cb)); }
+  void wait_durable() { log_.wait_durable(); }
+  AppLog::CommitStats commit_stats() { return log_.commit_stats(); }
 
   std::unordered_map<std::string, uint64_t> stats() {
     std::lock_guard<std::mutex> g(mu_);

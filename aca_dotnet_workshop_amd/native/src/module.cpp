@@ -739,11 +739,45 @@ PYBIND11_MODULE(_ttnative, m) {
   py::class_<DocStore>(m, "DocStore")
       .def(py::init<const std::string&, int, size_t>(), py::arg("path") = "", py::arg("fsync_mode") = 0,
            py::arg("index_threshold") = 256)
-      .def("set", &DocStore::set, py::arg("key"), py::arg("value"), py::arg("etag") = std::nullopt,
-           py::arg("first_write") = false, py::arg("ttl_ms") = 0, py::call_guard<py::gil_scoped_release>())
+      // writes from Python return once durable under group commit (fsync_mode 2), as the
+      // native front's answers do (a no-op in the other modes)
+      .def("set",
+           [](DocStore& s, const std::string& key, const std::string& value, const std::optional<std::string>& etag,
+              bool first_write, int64_t ttl_ms) {
+             std::string e = s.set(key, value, etag, first_write, ttl_ms);
+             s.wait_durable();
+             return e;
+           },
+           py::arg("key"), py::arg("value"), py::arg("etag") = std::nullopt, py::arg("first_write") = false,
+           py::arg("ttl_ms") = 0, py::call_guard<py::gil_scoped_release>())
       .def("get", &DocStore::get, py::arg("key"))
-      .def("delete", &DocStore::del, py::arg("key"), py::arg("etag") = std::nullopt)
-      .def("transact", &DocStore::transact, py::arg("ops"), py::call_guard<py::gil_scoped_release>())
+      .def("delete",
+           [](DocStore& s, const std::string& key, const std::optional<std::string>& etag) {
+             bool ok = s.del(key, etag);
+             s.wait_durable();
+             return ok;
+           },
+           py::arg("key"), py::arg("etag") = std::nullopt, py::call_guard<py::gil_scoped_release>())
+      .def("transact",
+           [](DocStore& s, const std::vector<TxOp>& ops) {
+             s.transact(ops);
+             s.wait_durable();
+           },
+           py::arg("ops"), py::call_guard<py::gil_scoped_release>())
+      .def("group_commit", &DocStore::group_commit)
+      .def("wait_durable", &DocStore::wait_durable, py::call_guard<py::gil_scoped_release>())
+      .def("commit_stats",
+           [](DocStore& s) {
+             auto c = s.commit_stats();
+             py::dict d;
+             d["syncs"] = c.syncs;
+             d["acks"] = c.acks;
+             d["written_bytes"] = c.written;
+             d["synced_bytes"] = c.synced;
+             d["sync_ms_total"] = c.sync_ms_total;
+             d["sync_ms_max"] = c.sync_ms_max;
+             return d;
+           })
       .def("query", &DocStore::query, py::arg("query"), py::arg("prefix") = "", py::arg("sort_keys") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("keys", &DocStore::keys, py::arg("prefix") = "", py::arg("limit") = 0)
@@ -886,7 +920,9 @@ PYBIND11_MODULE(_ttnative, m) {
               const std::string& id, int64_t ttl_ms, int64_t delay_ms) {
              std::string s = body;
              py::gil_scoped_release r;
-             return b.publish(topic, s, ctype, props, id, ttl_ms, delay_ms);
+             uint64_t seq = b.publish(topic, s, ctype, props, id, ttl_ms, delay_ms);
+             b.wait_durable();
+             return seq;
            },
            py::arg("topic"), py::arg("body"), py::arg("content_type") = "application/json", py::arg("props") = "{}",
            py::arg("id") = "", py::arg("ttl_ms") = 0, py::arg("delay_ms") = 0)
@@ -895,14 +931,47 @@ PYBIND11_MODULE(_ttnative, m) {
               const std::string& id, int64_t ttl_ms, int64_t delay_ms) {
              std::string s = body;
              py::gil_scoped_release r;
-             return b.send(q, s, ctype, props, id, ttl_ms, delay_ms);
+             uint64_t seq = b.send(q, s, ctype, props, id, ttl_ms, delay_ms);
+             b.wait_durable();
+             return seq;
            },
            py::arg("queue"), py::arg("body"), py::arg("content_type") = "application/json", py::arg("props") = "{}",
            py::arg("id") = "", py::arg("ttl_ms") = 0, py::arg("delay_ms") = 0)
       .def("receive", &Broker::receive, py::arg("path"), py::arg("max_messages") = 1, py::arg("lock_ms") = 0)
-      .def("complete", &Broker::complete)
-      .def("abandon", &Broker::abandon, py::arg("path"), py::arg("token"), py::arg("delay_ms") = 0)
-      .def("dead_letter", &Broker::dead_letter, py::arg("path"), py::arg("token"), py::arg("reason") = "")
+      .def("complete",
+           [](Broker& b, const std::string& path, const std::string& token) {
+             bool ok = b.complete(path, token);
+             b.wait_durable();
+             return ok;
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("abandon",
+           [](Broker& b, const std::string& path, const std::string& token, int64_t delay_ms) {
+             bool ok = b.abandon(path, token, delay_ms);
+             b.wait_durable();
+             return ok;
+           },
+           py::arg("path"), py::arg("token"), py::arg("delay_ms") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("dead_letter",
+           [](Broker& b, const std::string& path, const std::string& token, const std::string& reason) {
+             bool ok = b.dead_letter(path, token, reason);
+             b.wait_durable();
+             return ok;
+           },
+           py::arg("path"), py::arg("token"), py::arg("reason") = "", py::call_guard<py::gil_scoped_release>())
+      .def("group_commit", &Broker::group_commit)
+      .def("commit_stats",
+           [](Broker& b) {
+             auto c = b.commit_stats();
+             py::dict d;
+             d["syncs"] = c.syncs;
+             d["acks"] = c.acks;
+             d["written_bytes"] = c.written;
+             d["synced_bytes"] = c.synced;
+             d["sync_ms_total"] = c.sync_ms_total;
+             d["sync_ms_max"] = c.sync_ms_max;
+             return d;
+           })
       .def("renew", &Broker::renew, py::arg("path"), py::arg("token"), py::arg("lock_ms") = 0)
       .def("drain_dead_letters",
            [](Broker& b, const std::string& path, size_t max) {

@@ -298,6 +298,23 @@ def pin_all_threads(cpus: set[int]) -> None:
             pass
 
 
+class hold_affinity:
+    """``with hold_affinity(): <GPU runtime init>`` -- the runtime may widen the calling
+    thread's CPU set (and so every thread started from it later); on exit every thread of this
+    process is put back on the set it had on entry."""
+
+    def __enter__(self):
+        try:
+            self.cpus = set(os.sched_getaffinity(0))
+        except OSError:
+            self.cpus = None
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.cpus and any(c != self.cpus for c in cpus_allowed(os.getpid()).values()):
+            pin_all_threads(self.cpus)
+
+
 def enforce_cpuset(pid: int, cpus: set[int]) -> list[str]:
     """Re-pin every thread of ``pid`` allowed outside ``cpus`` back into them, the way a cgroup
     cpuset holds all of a container's threads (an affinity inherited at fork does not hold a

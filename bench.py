@@ -150,9 +150,12 @@ def device_sync() -> None:
     rank's own GPU (LOCAL_RANK), so N ranks do not all open a context on device 0."""
     try:
         import torch
-        if torch.cuda.is_available():
-            dev = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-            torch.cuda.synchronize(dev)
+
+        from aca_dotnet_workshop_amd.parallel import hold_affinity
+        with hold_affinity():  # the GPU runtime's first call must not widen this process's CPUs
+            if torch.cuda.is_available():
+                dev = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+                torch.cuda.synchronize(dev)
     except Exception:
         pass
 
@@ -1008,21 +1011,32 @@ def _wire_delta(w0: dict, w1: dict) -> dict:
 
 
 def protocol_alt(a: argparse.Namespace, overrides: dict, exe: str, root: str, steps: int, conc: int,
-                 rank: int) -> dict:
+                 rank: int, durable: bool = False) -> dict:
     """The headline's createTask flow with the API's OTHER Dapr protocol (gRPC <-> HTTP), in a
     fresh environment of the same manifest, replicas and CPU caps (no sweep): tasks/s, create
-    latency, CPU per task, and the wire counters that show which API carried the calls."""
+    latency, CPU per task, and the wire counters that show which API carried the calls.
+    ``durable``: the SAME protocol with the backing's logs on group commit instead
+    (``TT_BACKING_FSYNC=2``, applog.hpp): every state save and publish is acknowledged only once
+    fdatasync()ed, as Cosmos and Service Bus acknowledge -- plus the store's sync counts."""
     import psutil
 
     from aca_dotnet_workshop_amd.platform.background import BackgroundEnvironment
     from aca_dotnet_workshop_amd.platform.manifest import load_manifest
-    proto = "http" if a.api_protocol == "grpc" else "grpc"
+    proto = a.api_protocol if durable else "http" if a.api_protocol == "grpc" else "grpc"
     ov = dict(overrides, backendApiDaprApiProtocol=proto, overdueQuery="equality", overduePageSize=0,
-              environmentName=f"cae-alt-r{rank}")
+              environmentName=f"cae-{'durable' if durable else 'alt'}-r{rank}")
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"), ov)
-    env = BackgroundEnvironment(m, os.path.join(root, "alt"), log_level="warning")
+    env = BackgroundEnvironment(m, os.path.join(root, "durable" if durable else "alt"), log_level="warning")
+    fsync0 = os.environ.get("TT_BACKING_FSYNC")
+    if durable:
+        os.environ["TT_BACKING_FSYNC"] = "2"  # the backing process reads it at start
     try:
         env.start()
+        if durable:
+            if fsync0 is None:
+                os.environ.pop("TT_BACKING_FSYNC", None)
+            else:
+                os.environ["TT_BACKING_FSYNC"] = fsync0
         ca_file = None
         if a.ingress != "bypass":
             ca_file = str(env.ctl.pki.ca_crt)
@@ -1043,25 +1057,43 @@ def protocol_alt(a: argparse.Namespace, overrides: dict, exe: str, root: str, st
         cpu0["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu0.update(_ingress_cpu(env))
         w0 = _api_wire(env)
+        d0 = _collection_stats(env.backing_url).get("durability") or {}
         dt, rep = run_form_loadgen(exe, targets, cookie, counts, steps, a.batch, conc, bodies, None, ca_file,
                                    a.loadgen_threads)
         w1 = _api_wire(env)
+        d1 = _collection_stats(env.backing_url).get("durability") or {}
         cpu1 = _cpu_by_role(env.stack)
         t = me.cpu_times()
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
         busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}
         cpu_us = cpu_per_task(busy, a.batch * steps / dt)
-        return {"api_protocol": proto, "value": round(a.batch * steps / dt, 1), "steps": steps,
-                "create_latency_p50_ms": rep["latency_ms"]["p50"], "create_latency_p99_ms": rep["latency_ms"]["p99"],
-                "cpu_us_per_task": {"total": cpu_us.get("total"),
-                                    **{k.replace("tasksmanager-backend-", ""): v
-                                       for k, v in (cpu_us.get("by_role") or {}).items() if k.startswith(API)}},
-                "api_wire": _wire_delta(w0, w1), "errors": rep.get("errors")}
+        out = {"api_protocol": proto, "value": round(a.batch * steps / dt, 1), "steps": steps,
+               "create_latency_p50_ms": rep["latency_ms"]["p50"], "create_latency_p99_ms": rep["latency_ms"]["p99"],
+               "cpu_us_per_task": {"total": cpu_us.get("total"),
+                                   **{k.replace("tasksmanager-backend-", ""): v
+                                      for k, v in (cpu_us.get("by_role") or {}).items() if k.startswith(API)}},
+               "api_wire": _wire_delta(w0, w1), "errors": rep.get("errors")}
+        if durable:
+            syncs = d1.get("syncs", 0) - d0.get("syncs", 0)
+            acks = d1.get("acks", 0) - d0.get("acks", 0)
+            out["durability"] = {
+                "mode": "group commit (fdatasync before every acknowledgement)",
+                "fsync_mode": d1.get("fsync_mode"), "state_store_syncs": syncs, "state_store_acks": acks,
+                "acks_per_sync": round(acks / syncs, 1) if syncs else None,
+                "sync_ms_mean": round((d1.get("sync_ms_total", 0) - d0.get("sync_ms_total", 0)) / syncs, 3) if syncs else None,
+                "sync_ms_max": d1.get("sync_ms_max"),
+                "unsynced_bytes_at_end": d1.get("written_bytes", 0) - d1.get("synced_bytes", 0)}
+        return out
     except Exception as e:  # reported, not fatal to the headline
         return {"api_protocol": proto, "error": repr(e)[:300]}
     finally:
         env.stop()
+        if durable:
+            if fsync0 is None:
+                os.environ.pop("TT_BACKING_FSYNC", None)
+            else:
+                os.environ["TT_BACKING_FSYNC"] = fsync0
 
 
 def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
@@ -1372,9 +1404,14 @@ def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
             "outside": names}
 
 
+def _drop(d: dict | None, *keys: str) -> dict | None:
+    """``d`` without ``keys`` (the record's copy of a block whose bulk goes to stderr)."""
+    return None if d is None else {k: v for k, v in d.items() if k not in keys}
+
+
 def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict | None, envelope: dict | None,
                    protocol: str, wire: dict, alt: dict | None, session: dict | None = None,
-                   ingest: dict | None = None, platform: dict | None = None) -> dict:
+                   ingest: dict | None = None, platform: dict | None = None, durable: dict | None = None) -> dict:
     """The record's key facts in one small object at the head of ``config`` (the driver keeps
     the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
     flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
@@ -1397,6 +1434,9 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
     if alt:
         s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
                                  if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
+    if durable:
+        s["durable"] = {k: durable.get(k) for k in ("value", "create_latency_p99_ms", "error") if k in durable} | {
+            "acks_per_sync": (durable.get("durability") or {}).get("acks_per_sync")}
     if platform:
         s["platform_cpu"] = {k: platform.get(k) for k in ("cores_used", "reserved_cpus", "outside_rank_set")}
     if envelope:
@@ -1547,7 +1587,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         cpu1["bench"] = t.user + t.system + t.children_user + t.children_system
         cpu1.update(_ingress_cpu(env))
         th1 = env.stack.thread_cpu(_ingress_pid(env))
-        hot = hot_threads(th0, th1, dt, top=8)
+        hot = hot_threads(th0, th1, dt, top=6)
         # every thread that did work in the timed region: the stderr diagnostics line only
         threads_all = [t for t in hot_threads(th0, th1, dt, top=200) if t[2] >= 0.005]
         throttling = _throttling(duty0, env.ctl.limiter.duty_stats(), dt)
@@ -1652,10 +1692,14 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         asteps = 0 if shared else a.alt_steps if a.alt_steps >= 0 else max(2, a.steps // 2)
         if (a.envelope_s > 0 or asteps) and not shared:  # after the headline's environment is down
             env.stop()
+        durable = None
         if asteps:
             progress(f"api_protocol_alt: {asteps} steps with the other Dapr protocol")
             alt = protocol_alt(a, overrides, exe, root, asteps, conc, d.rank)
             progress("api_protocol_alt done")
+            progress(f"durable: {asteps} steps with the backing's logs on group commit")
+            durable = protocol_alt(a, overrides, exe, root, asteps, conc, d.rank, durable=True)
+            progress("durable done")
         if a.envelope_s > 0 and not shared:
             if d.rank == 0:
                 progress(f"reference envelope: {a.envelope_s:g} s")
@@ -1680,7 +1724,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "threads": threads_all}), file=sys.stderr, flush=True)
             summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
-                                     ingest, platform_cpu)
+                                     ingest, platform_cpu, durable)
             print(json.dumps({
                 "metric": "tasks_e2e_per_sec", "value": round(value, 2), "unit": "tasks/s", "n_gpus": n,
                 "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt_max / a.steps * 1e3, 3),
@@ -1717,10 +1761,14 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "step_quantum": f"{a.batch} createTask per step per rank (fixed task quantum)",
                            "timed_region_s": round(dt_max, 3), "log_level": "Information",
                            "log_sink": "structured JSON lines in the environment telemetry dir",
-                           "overdue_sweeps": sweep_info, "browser_flow": browser, "browser_session": session,
+                           # the record stays small (the driver keeps its head): the sweep's store
+                           # timings and span dump are in the stderr diagnostics line
+                           "overdue_sweeps": _drop(sweep_info, "store_ms_total", "trace_top_spans_p50_ms", "trace_of"),
+                           "browser_flow": browser, "browser_session": session,
                            "external_ingest": ingest,
                            "api_sidecar_direct": direct,
-                           "api_protocol_alt": alt, "reference_envelope": envelope}}), flush=True)
+                           "api_protocol_alt": alt, "durable": _drop(durable, "api_wire"),
+                           "reference_envelope": envelope}}), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():
             sweeper.stop()

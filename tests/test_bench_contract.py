@@ -68,6 +68,12 @@ def test_bench_single_process():
     alt = cfg["api_protocol_alt"]
     assert alt["api_protocol"] == "http" and alt["value"] > 0 and alt["api_wire"]["grpc.SaveState"] == 0
     assert alt["api_wire"]["state.save"] == 32 * alt["steps"]
+    # the same flow with the backing's logs on group commit: every acknowledgement after a sync
+    dur = cfg["durable"]
+    assert dur["value"] > 0 and dur["errors"] == 0 and dur["api_protocol"] == "grpc", dur
+    dd = dur["durability"]
+    assert dd["fsync_mode"] == 2 and dd["state_store_syncs"] >= 1 and dd["unsynced_bytes_at_end"] == 0, dd
+    assert sm["durable"]["value"] == dur["value"]
     sw = cfg["overdue_sweeps"]
     assert len(sw["sweep_ms"]) == sw["sweeps"] and max(sw["sweep_ms"], default=0) == (sw["sweep_max_ms"] or 0)
     assert sw["page_size"] == 4096
