@@ -60,8 +60,6 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--log-level", default="Information",
                     help="service log level (reference default: Information, appsettings.json); records go as "
                          "structured JSON to the environment's telemetry dir (Log Analytics equivalent)")
-    ap.add_argument("--mark-chunk", type=int, default=0,
-                    help="the processor's OverdueTasks:MarkChunk (0: the manifest's, 256)")
     ap.add_argument("--overdue-sweep-ms", type=int, default=1000,
                     help="mixed load: trigger the processor's overdue cron job every N ms during the run "
                          "(OverdueTasks:Query=range -> GPU columnar scan in the backing services); 0 = off")
@@ -1512,7 +1510,6 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                  "backendApiCpu": caps["api"], "processorCpu": caps["processor"], "appMemory": "2Gi",
                  "appInsightsSamplingPercentage": a.trace_sampling,
                  "overdueQuery": "range" if sweep else "equality", "overduePageSize": OVERDUE_PAGE if sweep else 0,
-                 **({"overdueMarkChunk": a.mark_chunk} if a.mark_chunk > 0 else {}),
                  "overdueMarkChunk": a.mark_chunk, "backendApiDaprApiProtocol": a.api_protocol,
                  "environmentName": f"cae-bench-r{d.rank}"}
     m = load_manifest(os.path.join(ROOT, "deploy", "main.yaml"), os.path.join(ROOT, "deploy", "main.parameters.json"),
@@ -1608,7 +1605,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             acc = {k: (round(v - acc0.get(k, 0), 3) if isinstance(v, (int, float)) and k != "rows" else v)
                    for k, v in acc1.items()}
             sweep_info = {**sweeper.summary(), "period_ms": a.overdue_sweep_ms, "past_due_every": a.past_due_every,
-                          "mark_chunk": a.mark_chunk or 256,
+                          "mark_chunk": a.mark_chunk,
                           "page_size": OVERDUE_PAGE,
                           "gpu_queries": acc.get("gpu"), "cpu_queries": acc.get("cpu"),
                           "native_queries": acc.get("native"), "mirror_rows": acc.get("rows"),
