@@ -262,7 +262,7 @@ struct NativeRoute {
   enum Kind {
     kFrontendCreate = 1, kApiCreate = 2, kProcessorNotify = 3, kFrontendList = 4, kApiList = 5, kApiOverdue = 6,
     kApiMarkOverdue = 7, kApiGet = 8, kApiUpdate = 9, kApiComplete = 10, kApiDelete = 11,
-    kFrontendEditGet = 12, kFrontendEdit = 13, kFrontendIndexPost = 14
+    kFrontendEditGet = 12, kFrontendEdit = 13, kFrontendIndexPost = 14, kProcessorSweep = 15
   };
   // a path with an "{id}" segment (api/tasks/{id}[/markcomplete]) matches a canonical lower-case
   // GUID there (the route's key); other spellings (upper case, braces) are Python's
@@ -322,6 +322,13 @@ struct NativeRoute {
   // `invoke_target`: the API's invoke prefix (".../method/api/tasks/")
   Pieces edit_page;
   // kProcessorNotify: the tasksaved subscription in the notifier's log mode -> log line -> 200
+  // kProcessorSweep: the cron job (ScheduledTasksManagerController.cs:19-46, services/processor/
+  // app.py check_overdue_tasks_job) -> GET api/overduetasks[?limit=] through the sidecar -> the
+  // page filtered and cut into chunks (taskcodec overdue_filter) -> concurrent POST markoverdue
+  // per chunk -> the next page while the API reports more -> the job's JSON summary
+  std::string sweep_get, sweep_mark;
+  int sweep_page = 0, sweep_max_pages = 100000, sweep_chunk = 0, sweep_empty_limit = 3;
+  Template log_triggered, log_retrieved, log_marking;
   std::vector<double> bounds;   // the request-latency histogram's buckets (seconds)
   ::taskcodec::Entropy rng;       // loop thread only
 
@@ -539,6 +546,7 @@ class AppHost {
     else if (kind == "frontend_edit_get") r->kind = NativeRoute::kFrontendEditGet;
     else if (kind == "frontend_edit") r->kind = NativeRoute::kFrontendEdit;
     else if (kind == "frontend_index_post") r->kind = NativeRoute::kFrontendIndexPost;
+    else if (kind == "processor_sweep") r->kind = NativeRoute::kProcessorSweep;
     else throw std::invalid_argument("unknown native route kind: " + kind);
     r->method = get("method");
     r->path = get("path");
@@ -557,7 +565,7 @@ class AppHost {
     r->bounds = bounds;
     if (get("protocol") == "grpc") {
       if (r->kind == NativeRoute::kFrontendCreate || r->kind == NativeRoute::kFrontendList ||
-          r->kind == NativeRoute::kProcessorNotify || r->kind >= NativeRoute::kFrontendEditGet)
+          r->kind == NativeRoute::kProcessorNotify || r->kind >= NativeRoute::kFrontendEditGet)  // sweep too
         throw std::invalid_argument("only the API's store routes speak gRPC");
       r->grpc = true;
       r->store = get("store");
@@ -592,6 +600,20 @@ class AppHost {
       if (r->query_target.empty() || get("query").empty() || r->page_default.empty() || r->more_header.empty() ||
           get("log_overdue").empty())
         throw std::invalid_argument("api_overdue needs its query, page size, log template and header");
+    } else if (r->kind == NativeRoute::kProcessorSweep) {
+      r->sweep_get = get("overdue_target");
+      r->sweep_mark = get("mark_target");
+      r->more_header = get("more_header");
+      r->sweep_page = std::stoi(get("page").empty() ? "0" : get("page"));
+      if (!get("max_pages").empty()) r->sweep_max_pages = std::stoi(get("max_pages"));
+      r->sweep_chunk = std::stoi(get("chunk").empty() ? "0" : get("chunk"));
+      if (!get("empty_more_limit").empty()) r->sweep_empty_limit = std::stoi(get("empty_more_limit"));
+      r->log_triggered = Template::compile(get("log_triggered"), "v", {"v"});
+      r->log_retrieved = Template::compile(get("log_retrieved"), "v", {"v"});
+      r->log_marking = Template::compile(get("log_marking"), "v", {"v"});
+      if (r->sweep_get.empty() || r->sweep_mark.empty() || r->more_header.empty() || r->sweep_chunk <= 0 ||
+          (r->sidecar.path.empty() && r->sidecar.host.empty()))
+        throw std::invalid_argument("processor_sweep needs its targets, the more-results header and a chunk size");
     } else if (r->kind >= NativeRoute::kFrontendEditGet) {
       if (r->invoke_target.empty() || r->af_key.empty() || r->af_cookie.empty())
         throw std::invalid_argument("a frontend page route needs its invoke target and antiforgery settings");
@@ -812,6 +834,16 @@ class AppHost {
     ::taskcodec::Update upd;           // kApiUpdate: the bound body
     ev::HeaderList plain_headers;      // HTTP GET / DELETE: traceparent, token (no content type)
     ::taskcodec::Created task;
+    struct Sweep {                     // kProcessorSweep: the job's loop state
+      std::string run_at_iso, run_day;
+      long long retrieved = 0, marked = 0, pages = 0, empty_more = 0;
+      double t_query = 0, t_mark = 0, t_mark0 = 0;
+      size_t outstanding = 0, failed_at = SIZE_MAX;
+      ev::ClientResult failure;
+      long long n_page = 0, n_kept = 0;
+      std::string more;
+    };
+    std::shared_ptr<Sweep> sweep;
   };
 
   // the gRPC SDK's metadata on an unsampled call (sdk/grpc_client.py _call_encoded)
@@ -1037,6 +1069,149 @@ class AppHost {
             return true;
           });
     });
+  }
+
+  // kProcessorSweep (services/processor/app.py check_overdue_tasks_job): the same page loop,
+  // filter, chunks, log lines and summary.  A failed call goes to Python as that call's error
+  // (hand_over: "fail overdue|mark ..."); a page the native filter does not read goes to Python
+  // with the loop's state ("resume <base64 JSON>"), which asks for that page again and goes on
+  // from there -- nothing the job did is done twice.
+  static std::string py_round2(double v) {  // repr(round(v, 2)) for the job's millisecond fields
+    char b[64];
+    std::snprintf(b, sizeof b, "%.2f", v);
+    std::string s(b);
+    while (s.size() > 1 && s.back() == '0' && s[s.size() - 2] != '.') s.pop_back();
+    return s;
+  }
+  bool processor_sweep(const std::shared_ptr<NativeJob>& j, const Message&) {
+    const NativeRoute& r = *j->route;
+    auto st = std::make_shared<NativeJob::Sweep>();
+    struct timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    const time_t sec = ts.tv_sec;
+    const long us = ts.tv_nsec / 1000;
+    std::tm tm{};
+    gmtime_r(&sec, &tm);
+    char d[40], t[40], f[40];
+    std::snprintf(d, sizeof d, "%04d-%02d-%02d", tm.tm_year + 1900, tm.tm_mon + 1, tm.tm_mday);
+    std::snprintf(t, sizeof t, "%02d:%02d:%02d", tm.tm_hour, tm.tm_min, tm.tm_sec);
+    std::snprintf(f, sizeof f, ".%06ld", us);
+    const std::string frac = us ? f : "";
+    st->run_day = d;
+    st->run_at_iso = std::string(d) + "T" + t + frac + "+00:00";  // datetime.isoformat()
+    const std::string run_at_str = std::string(d) + " " + t + frac + "+00:00";  // str(datetime)
+    j->sweep = st;
+    native_inflight_.fetch_add(1);
+    log_event(r, *j, r.log_triggered.render_with([&](int) -> const std::string& { return run_at_str; }));
+    loop_.defer([this, j] { sweep_page(j); });
+    return true;
+  }
+  void sweep_page(const std::shared_ptr<NativeJob>& j) {
+    const NativeRoute& r = *j->route;
+    auto& st = *j->sweep;
+    st.pages += 1;
+    const double t0 = ev::now_s();
+    client_.request(r.sidecar, "GET", r.sweep_get, j->plain_headers, {}, r.timeout_s,
+                    [this, j, t0](ev::ClientResult&& res) {
+                      const NativeRoute& r = *j->route;
+                      auto& st = *j->sweep;
+                      st.t_query += ev::now_s() - t0;
+                      if (res.err || res.resp.status >= 300) return hand_over(*j, "overdue", res);
+                      size_t n_page = 0, n_kept = 0;
+                      std::string kept;
+                      std::vector<size_t> starts;
+                      if (res.resp.body.empty() ||
+                          !::taskcodec::overdue_filter(res.resp.body, st.run_day, n_page, n_kept, kept, &starts))
+                        return sweep_resume(*j, true);  // Python's binder reads this page
+                      st.retrieved += (long long)n_page;
+                      const std::string n = std::to_string(n_page);
+                      log_event(r, *j, r.log_retrieved.render_with([&](int) -> const std::string& { return n; }));
+                      const std::string* more = res.resp.header(r.more_header);
+                      st.more.clear();
+                      if (more)
+                        for (char c : *more) st.more += ::tt::ascii_lower(c);
+                      st.n_page = (long long)n_page;
+                      st.n_kept = (long long)n_kept;
+                      if (!n_kept) return sweep_next(j);
+                      const std::string k = std::to_string(n_kept);
+                      log_event(r, *j, r.log_marking.render_with([&](int) -> const std::string& { return k; }));
+                      // the chunks, as the module's tasks_overdue_filter_chunks cuts them
+                      std::vector<std::string> parts;
+                      const size_t body_end = kept.size() - 1;  // the closing ']'
+                      const size_t chunk = (size_t)r.sweep_chunk;
+                      for (size_t a = 0; a < starts.size(); a += chunk) {
+                        const size_t b = std::min(starts.size(), a + chunk);
+                        const size_t from = starts[a], to = b < starts.size() ? starts[b] - 1 : body_end;
+                        std::string part;
+                        part.reserve(to - from + 2);
+                        part += '[';
+                        part.append(kept, from, to - from);
+                        part += ']';
+                        parts.push_back(std::move(part));
+                      }
+                      st.outstanding = parts.size();
+                      st.failed_at = SIZE_MAX;
+                      st.t_mark0 = ev::now_s();
+                      for (size_t i = 0; i < parts.size(); ++i)
+                        client_.request(r.sidecar, "POST", r.sweep_mark, j->out_headers, parts[i], r.timeout_s,
+                                        [this, j, i](ev::ClientResult&& res) {
+                                          auto& st = *j->sweep;
+                                          if ((res.err || res.resp.status >= 300) && i < st.failed_at) {
+                                            st.failed_at = i;  // every call finishes; the first fails the job
+                                            st.failure = std::move(res);
+                                          }
+                                          if (--st.outstanding) return;
+                                          st.t_mark += ev::now_s() - st.t_mark0;
+                                          if (st.failed_at != SIZE_MAX) return hand_over(*j, "mark", st.failure);
+                                          st.marked += st.n_kept;
+                                          sweep_next(j);
+                                        },
+                                        false);
+                    });
+  }
+  // the loop's exit conditions after a page (the Python handler's, in its order)
+  void sweep_next(const std::shared_ptr<NativeJob>& j) {
+    const NativeRoute& r = *j->route;
+    auto& st = *j->sweep;
+    if (r.sweep_page <= 0) return sweep_done(j);
+    if (!st.more.empty()) {
+      if (st.more != "true" || (st.n_page && !st.n_kept)) return sweep_done(j);
+      if (!st.n_page) {
+        if (++st.empty_more >= r.sweep_empty_limit) return sweep_done(j);
+        if (st.pages >= r.sweep_max_pages) return sweep_done(j);
+        loop_.call_later(0.005 * (double)st.empty_more, [this, j] { sweep_page(j); });
+        return;
+      }
+      st.empty_more = 0;
+    } else if (st.n_page < r.sweep_page || !st.n_kept) {
+      return sweep_done(j);
+    }
+    if (st.pages >= r.sweep_max_pages) return sweep_done(j);
+    sweep_page(j);
+  }
+  void sweep_done(const std::shared_ptr<NativeJob>& j) {
+    const NativeRoute& r = *j->route;
+    const auto& st = *j->sweep;
+    std::string out = "{\"runAt\":\"" + st.run_at_iso + "\",\"retrieved\":" + std::to_string(st.retrieved) +
+                      ",\"markedOverdue\":" + std::to_string(st.marked) + ",\"pages\":" + std::to_string(st.pages) +
+                      ",\"emptyMorePages\":" + std::to_string(st.empty_more) +
+                      ",\"queryMs\":" + py_round2(st.t_query * 1e3) + ",\"markMs\":" + py_round2(st.t_mark * 1e3) + "}";
+    finish(*j, r.status, {{"Content-Type", r.content_type}}, out);
+  }
+  // Python goes on from here: the page just read is asked for again (a GET), with the counts so far
+  void sweep_resume(NativeJob& j, bool redo_page) {
+    const auto& st = *j.sweep;
+    char tq[40], tm[40];
+    std::snprintf(tq, sizeof tq, "%.9f", st.t_query);
+    std::snprintf(tm, sizeof tm, "%.9f", st.t_mark);
+    std::string state = "{\"runAt\":\"" + st.run_at_iso + "\",\"retrieved\":" + std::to_string(st.retrieved) +
+                        ",\"marked\":" + std::to_string(st.marked) +
+                        ",\"pages\":" + std::to_string(st.pages - (redo_page ? 1 : 0)) +
+                        ",\"emptyMore\":" + std::to_string(st.empty_more) + ",\"queryS\":" + tq +
+                        ",\"markS\":" + tm + "}";
+    j.req.headers.emplace_back("x-tt-native", "resume " + tt::text::base64(state));
+    to_python(j.server, std::move(j.req), std::move(j.reply));
+    native_inflight_.fetch_sub(1);
   }
 
   // kFrontendEditGet / kFrontendEdit / kFrontendIndexPost (services/frontend/app.py edit_get /
@@ -1403,7 +1578,7 @@ class AppHost {
     if (r->kind == NativeRoute::kProcessorNotify) return notify(r, m, reply, tid);
     if (r->kind == NativeRoute::kFrontendList || r->kind == NativeRoute::kApiList ||
         r->kind == NativeRoute::kApiOverdue || r->kind == NativeRoute::kApiMarkOverdue ||
-        (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kFrontendIndexPost)) {
+        (r->kind >= NativeRoute::kApiGet && r->kind <= NativeRoute::kProcessorSweep)) {
       auto j = std::make_shared<NativeJob>();
       j->route = r;
       j->server = server;
@@ -1421,6 +1596,7 @@ class AppHost {
                    : r->kind == NativeRoute::kApiList        ? api_list(j, m)
                    : r->kind == NativeRoute::kApiOverdue     ? api_overdue(j, m)
                    : r->kind == NativeRoute::kApiMarkOverdue ? api_markoverdue(j, m)
+                   : r->kind == NativeRoute::kProcessorSweep ? processor_sweep(j, m)
                    : r->kind >= NativeRoute::kFrontendEditGet ? frontend_page(j, m)
                                                              : api_task(j, m);
       if (!taken) return false;

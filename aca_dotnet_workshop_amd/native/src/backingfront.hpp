@@ -394,7 +394,12 @@ class BackingFront {
         });
       });
     }
+    // one eventfd write per loop wake-up, however many posts land before the loop runs (a
+    // group commit releases a batch of answers at once); the loop clears the flag before it
+    // takes the posted work, so a post after that takes a new write
+    std::atomic<bool> wake_pending{false};
     void wake() {
+      if (wake_pending.exchange(true, std::memory_order_acq_rel)) return;
       uint64_t one = 1;
       ssize_t r = ::write(wake_fd, &one, sizeof one);
       (void)r;
@@ -429,6 +434,7 @@ class BackingFront {
       }
       std::vector<std::string> keys;
       std::vector<std::function<void()>> todo;
+      wake_pending.store(false, std::memory_order_release);
       {
         std::lock_guard l(mu);
         keys.swap(posted);

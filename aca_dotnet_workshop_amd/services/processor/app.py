@@ -31,13 +31,16 @@ Endpoints (reference SURVEY.md §2.2, §2.11):
 from __future__ import annotations
 
 import asyncio
+import base64
+import json
 import logging
 import uuid
+from datetime import datetime
 from pathlib import Path
 
 from ...models import TaskModel, json_array_chunks, naive_utc, overdue_filter_chunks, overdue_filter_wire, task_model_name, tasks_from_json, utcnow
 from ...sdk import SidecarClient, cloud_events_middleware, map_subscribe_handler, topic
-from ...sdk.client import InvocationError, RawJsonBytes, client_from_config
+from ...sdk.client import InvocationError, RawJsonBytes, client_from_config, native_route_failure
 from ...web.app import WebApp, read_model
 from ...web.http import Request, Response, empty, json_response, text_response
 from ..hosting import create_host, map_openapi, run_host
@@ -59,6 +62,12 @@ EMPTY_MORE_LIMIT = 3
 # TasksNotifierController.TaskSaved's log line and answer (TasksNotifierController.cs:26-32): the
 # Python handler and the app host's native route (apphost.hpp processor_notify) use this text
 NOTIFY_LOG = "Started processing message with Task Name '%s'"
+# ScheduledTasksManagerController's log lines (ScheduledTasksManagerController.cs:22-40), shared
+# with the app host's native sweep route (apphost.hpp processor_sweep)
+LOG_TRIGGERED = "ScheduledTasksManager::Timer Services triggered at: %s"
+LOG_RETRIEVED = "ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d"
+LOG_MARKING = "ScheduledTasksManager::marking %d as overdue tasks"
+MORE_HEADER = "x-tt-more-results"
 
 
 def register_controllers(app: WebApp, client: SidecarClient) -> None:
@@ -148,25 +157,54 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
         return empty(200)
 
     # -- ScheduledTasksManagerController ---------------------------------------
+    # OverdueTasks:PageSize > 0 (with the API's OverdueTasks:Query=range): sweep page by page
+    # -- a marked page drops out of the API's filter, so each request asks for the next one
+    page = cfg.get_int("OverdueTasks:PageSize", 0)
+    max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
+    # OverdueTasks:MarkChunk > 0: a page's overdue list goes to markoverdue in concurrent
+    # calls of at most this many tasks (disjoint: the same end state as one call, which is
+    # what the reference makes -- 0), so the API's replicas and their sidecars share the work
+    chunk = cfg.get_int("OverdueTasks:MarkChunk", 256)
+    overdue_path = "api/overduetasks" + (f"?limit={page}" if page > 0 else "")
+    mark_path = "api/overduetasks/markoverdue"
+    sweep_what = {"overdue": f"invoke {api_app_id}/{overdue_path}", "mark": f"invoke {api_app_id}/{mark_path}"}
+    ep = client.native_endpoint() if chunk > 0 and hasattr(client, "native_endpoint") else None
+    if ep is not None and ep.get("protocol", "http") == "http":
+        # the job on the app host's I/O thread: the same loop, filter, chunks, log lines and summary
+        app.services.setdefault("native_routes", []).append({
+            "kind": "processor_sweep", "method": "POST", "path": "/ScheduledTasksManager",
+            "route": "/ScheduledTasksManager",
+            "cfg": {"sidecar": ep["sidecar"], "token": ep["token"], "timeout": ep["timeout"],
+                    "overdue_target": f"{ep['prefix']}/v1.0/invoke/{api_app_id}/method/{overdue_path}",
+                    "mark_target": f"{ep['prefix']}/v1.0/invoke/{api_app_id}/method/{mark_path}",
+                    "page": page, "max_pages": max_pages, "chunk": chunk, "empty_more_limit": EMPTY_MORE_LIMIT,
+                    "more_header": MORE_HEADER, "log_category": log_sched.name,
+                    "log_triggered": LOG_TRIGGERED, "log_retrieved": LOG_RETRIEVED.replace("%d", "%s"),
+                    "log_marking": LOG_MARKING.replace("%d", "%s"),
+                    "status": 200, "content_type": "application/json; charset=utf-8"}})
+
     @app.route("/ScheduledTasksManager", ("POST",), name="CheckOverDueTasksJob", tag="ScheduledTasksManager")
     async def check_overdue_tasks_job(req: Request) -> Response:
-        run_at = utcnow()
-        log_sched.info("ScheduledTasksManager::Timer Services triggered at: %s", run_at)
-        # OverdueTasks:PageSize > 0 (with the API's OverdueTasks:Query=range): sweep page by page
-        # -- a marked page drops out of the API's filter, so each request asks for the next one
-        page = cfg.get_int("OverdueTasks:PageSize", 0)
-        max_pages = cfg.get_int("OverdueTasks:MaxPages", 100000)
-        # OverdueTasks:MarkChunk > 0: a page's overdue list goes to markoverdue in concurrent
-        # calls of at most this many tasks (disjoint: the same end state as one call, which is
-        # what the reference makes -- 0), so the API's replicas and their sidecars share the work
-        chunk = cfg.get_int("OverdueTasks:MarkChunk", 256)
-        retrieved = marked = pages = empty_more = 0
+        note = req.state.get("tt_native") or ""
+        if note.startswith("resume "):
+            # the native route ran the job up to a page its filter does not read: go on from there
+            st = json.loads(base64.b64decode(note[7:]))
+            run_at = datetime.fromisoformat(st["runAt"])
+            retrieved, marked, pages, empty_more = st["retrieved"], st["marked"], st["pages"], st["emptyMore"]
+            t_query, t_mark = float(st["queryS"]), float(st["markS"])
+        else:
+            failed = native_route_failure(req, sweep_what)
+            if failed is not None:  # a call the native route made failed: the same error
+                raise failed
+            run_at = utcnow()
+            log_sched.info(LOG_TRIGGERED, run_at)
+            retrieved = marked = pages = empty_more = 0
+            t_query = t_mark = 0.0  # wall time of the job's two hops (returned for attribution)
         run_day = naive_utc(run_at).date().isoformat()
-        t_query = t_mark = 0.0  # wall time of the job's two hops (returned for attribution)
         clock = asyncio.get_running_loop().time
         while pages < max_pages:
             pages += 1
-            path = "api/overduetasks" + (f"?limit={page}" if page > 0 else "")
+            path = overdue_path
             t0 = clock()
             r = await client.invoke_method_raw("GET", api_app_id, path)
             t_query += clock() - t0
@@ -185,15 +223,14 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                 overdue = [t for t in tasks if naive_utc(run_at).date() > naive_utc(t.task_due_date).date()]
                 n_page, n_overdue = len(tasks), len(overdue)
             retrieved += n_page
-            log_sched.info("ScheduledTasksManager::completed query state store for tasks, retrieved tasks count: %d",
-                           n_page)
+            log_sched.info(LOG_RETRIEVED, n_page)
             if n_overdue:
-                log_sched.info("ScheduledTasksManager::marking %d as overdue tasks", n_overdue)
+                log_sched.info(LOG_MARKING, n_overdue)
                 if parts is None and isinstance(overdue, bytes) and 0 < chunk < n_overdue:
                     parts = json_array_chunks(overdue, chunk)
                 t0 = clock()
                 if parts and len(parts) > 1:
-                    results = await asyncio.gather(*(client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue",
+                    results = await asyncio.gather(*(client.invoke_method("POST", api_app_id, mark_path,
                                                                           RawJsonBytes(p)) for p in parts),
                                                    return_exceptions=True)
                     for res in results:  # every call has finished: the first failure fails the job
@@ -201,12 +238,12 @@ def register_controllers(app: WebApp, client: SidecarClient) -> None:
                             raise res
                 else:
                     data = RawJsonBytes(overdue) if isinstance(overdue, bytes) else overdue
-                    await client.invoke_method("POST", api_app_id, "api/overduetasks/markoverdue", data)
+                    await client.invoke_method("POST", api_app_id, mark_path, data)
                 t_mark += clock() - t0
                 marked += n_overdue
             if page <= 0:
                 break
-            more = (r.headers.get("x-tt-more-results") or "").lower()
+            more = (r.headers.get(MORE_HEADER) or "").lower()
             if more:  # the API says whether the store holds more matches than this page
                 # a short (even empty) page with more matches: rows that changed after the
                 # store's selection were skipped -- ask again; a page of nothing to mark stops

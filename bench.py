@@ -1083,7 +1083,8 @@ def protocol_alt(a: argparse.Namespace, overrides: dict, exe: str, root: str, st
                 "acks_per_sync": round(acks / syncs, 1) if syncs else None,
                 "sync_ms_mean": round((d1.get("sync_ms_total", 0) - d0.get("sync_ms_total", 0)) / syncs, 3) if syncs else None,
                 "sync_ms_max": d1.get("sync_ms_max"),
-                "unsynced_bytes_at_end": d1.get("written_bytes", 0) - d1.get("synced_bytes", 0)}
+                "unsynced_bytes_at_end": d1.get("written_bytes", 0) - d1.get("synced_bytes", 0),
+                "log_file_system": _fs_type(os.path.join(root, "durable"))}
         return out
     except Exception as e:  # reported, not fatal to the headline
         return {"api_protocol": proto, "error": repr(e)[:300]}
@@ -1402,6 +1403,23 @@ def _platform_cpu(env, split, pinned, busy: dict[str, float]) -> dict:
             else "shared with the replicas (rank set too small to split)",
             "threads_checked": threads, "outside_rank_set": outside, "outside_own_subset": wrong_side,
             "outside": names}
+
+
+def _fs_type(path: str) -> str:
+    """The file system ``path`` lives on (/proc/mounts, longest mount point): what a sync costs
+    there (tmpfs / overlay over one) is part of a durability number."""
+    best, fs = "", "?"
+    try:
+        real = os.path.realpath(path)
+        with open("/proc/mounts") as f:
+            for ln in f:
+                parts = ln.split()
+                if len(parts) >= 3 and (real == parts[1] or real.startswith(parts[1].rstrip("/") + "/")) \
+                        and len(parts[1]) > len(best):
+                    best, fs = parts[1], parts[2]
+    except OSError:
+        pass
+    return fs
 
 
 def _drop(d: dict | None, *keys: str) -> dict | None:
