@@ -2439,6 +2439,6 @@ int main(int argc, char** argv) {
     if (stopping && (dp.drained() || t > stop_deadline)) loop.stop();
   });
   dp.flush();
-  pcsample::dump("dataplane");
+  pcsample::dump(("dataplane " + dp.app_id()).c_str());  // the profile names its app
   return 0;
 }
