@@ -282,9 +282,17 @@ class AppLog {
   void commit_loop() {
     pthread_setname_np(pthread_self(), "tt-log-commit");
     std::unique_lock<std::mutex> l(gc_mu_);
+    // TT_LOG_COMMIT_DELAY_US (default 100): once a writer waits, more writers may join the same
+    // sync for this long (PostgreSQL's commit_delay) -- one fdatasync per ~delay x write rate
+    // records instead of one per handful, at the cost of this much latency per acknowledgement
+    static const auto delay = [] {
+      const char* v = std::getenv("TT_LOG_COMMIT_DELAY_US");
+      return std::chrono::microseconds(v && *v ? std::max(0L, std::atol(v)) : 100L);
+    }();
     while (true) {
       gc_cv_.wait(l, [this] { return gc_stop_ || gc_want_; });
       if (gc_stop_ && waiters_.empty()) return;
+      if (delay.count() > 0 && !gc_stop_) gc_cv_.wait_for(l, delay, [this] { return gc_stop_; });
       gc_want_ = false;
       l.unlock();
       const uint64_t target = written_.load(std::memory_order_acquire);
