@@ -572,7 +572,10 @@ class DocStore {
     ru_ticket_ttl_s_ = ticket_ttl_s;
     ru_rate_ = std::max(0.0, ru_per_s);
     ru_on_.store(ru_rate_ > 0, std::memory_order_relaxed);
-    ru_tokens_ = ru_rate_;
+    // the bucket starts empty and refills at the provisioned rate: over any window from the
+    // start, what is admitted stays within rate x window (+ the call in flight) -- no free
+    // first second of budget on top
+    ru_tokens_ = 0;
     ru_last_ = mono_s();
     ru_tickets_.clear();
     ru_by_slot_.clear();

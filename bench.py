@@ -1139,7 +1139,7 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         th.start()
         steady: dict = {}
 
-        def mark_steady() -> None:  # one second in: the bucket's initial second of budget is spent
+        def mark_steady() -> None:  # one second in: past the start-up (the bucket starts empty)
             if not stop.wait(1.0):
                 steady.update(t=time.perf_counter(), st=_collection_stats(env.backing_url).get("throughput", {}),
                               enq=int(_counts(counts).get("enqueued", 0)))
@@ -1169,8 +1169,9 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         ru = float(st1.get("ru_consumed", 0.0)) - float(st0.get("ru_consumed", 0.0))
         el = float(rep.get("elapsed_s") or wall)
         budget = float(st1.get("ru_per_s", 0.0))
-        # the steady window: from one second in (the bucket starts with a second of budget, as any
-        # idle second refills it) to the end -- RU admitted there over the budget's refill
+        # the steady window: from one second in to the end -- RU admitted there over the budget's
+        # refill (the bucket starts empty, so the whole window's ratio is bounded by 1 as well; an
+        # idle second refills up to one second of budget, which the steady window may still hold)
         sw = None
         if steady and t_end - steady["t"] > 1.0 and budget:
             w = t_end - steady["t"]
