@@ -1200,8 +1200,14 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 # the 429s per charged store call, and how the throttled ones came through: a
                 # ticket at its slot (admitted) or early (a second 429 for the same call)
                 **_throttle_detail(st0, st1),
-                "tasks_per_s_over_budget_rate": (round(tasks / el / (float(st1.get("ru_per_s", 0.0)) / (ru / tasks)), 3)
-                                                 if tasks and ru and el and st1.get("ru_per_s") else None),
+                # tasks/s over the rate the budget pays for (budget / RU per task), over the steady
+                # window: the whole window also spends the one second of budget the bucket holds
+                # when the load starts (an idle bucket refills to it, as Cosmos's burst capacity
+                # does) -- that ratio is kept next to it
+                "tasks_per_s_over_budget_rate": (sw or {}).get("ru_over_budget"),
+                "tasks_per_s_over_budget_rate_whole_window": (
+                    round(tasks / el / (float(st1.get("ru_per_s", 0.0)) / (ru / tasks)), 3)
+                    if tasks and ru and el and st1.get("ru_per_s") else None),
                 "keda_polling_s": 5, "loadgen_exit": p.returncode}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:500]}
