@@ -1438,18 +1438,21 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
                    protocol: str, wire: dict, alt: dict | None, session: dict | None = None,
                    ingest: dict | None = None, platform: dict | None = None, durable: dict | None = None) -> dict:
     """The record's key facts in one small object at the head of ``config`` (the driver keeps
-    the line's head): CPU per task in total and per role, the sweep's percentiles, the browser
-    flow, the envelope's budget ratio and KEDA's peak, and the API's wire."""
+    the head of ``config``: under ~1 KB, so every block keeps only its deciding numbers): CPU
+    per task in total and per role, the sweep's percentiles, the browser flow and session, the
+    envelope's budget ratio and KEDA's peak, and the API's wire."""
     s: dict = {"tasks_per_s": round(value, 1), "api_protocol": protocol,
                "api_grpc_calls_per_task": None, "cpu_us_per_task": cpu_us.get("total"),
-               "cpu_us_per_task_by_role": {k.replace("tasksmanager-", "").replace("backend-", ""): v
-                                           for k, v in (cpu_us.get("by_role") or {}).items()}}
+               # the sidecars' Python control planes (~0 µs per task) are left out here
+               "cpu_us_per_task_by_role": {k.replace("tasksmanager-", "").replace("backend-", "")
+                                           .replace("frontend-webapp", "frontend"): v
+                                           for k, v in (cpu_us.get("by_role") or {}).items()
+                                           if not k.endswith(".sidecar")}}
     if wire.get("state.save"):
         s["api_grpc_calls_per_task"] = round((wire.get("grpc.SaveState", 0) + wire.get("grpc.PublishEvent", 0))
                                              / wire["state.save"], 2)
     if sweep:
-        s["sweep"] = {k: sweep.get(k) for k in ("sweeps", "sweep_p50_ms", "sweep_p99_ms", "sweep_max_ms",
-                                                  "tasks_marked_overdue", "errors")}
+        s["sweep"] = {k: sweep.get(k) for k in ("sweeps", "sweep_p50_ms", "sweep_max_ms", "errors")}
     if browser:
         s["browser_flows_per_s"] = browser.get("flows_per_s")
     if session:
@@ -1457,7 +1460,7 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
     if ingest:
         s["external_ingest"] = {k: ingest.get(k) for k in ("msgs_per_s", "all_processed", "dead", "error") if k in ingest}
     if alt:
-        s["api_protocol_alt"] = {k: alt.get(k) for k in ("api_protocol", "value", "error")
+        s["api_protocol_alt"] = {k: alt.get(k) for k in ("value", "error")
                                  if k in alt} | {"cpu_us_per_task": (alt.get("cpu_us_per_task") or {}).get("total")}
     if durable:
         s["durable"] = {k: durable.get(k) for k in ("value", "create_latency_p99_ms", "error") if k in durable} | {
@@ -1466,8 +1469,7 @@ def record_summary(value: float, cpu_us: dict, sweep: dict | None, browser: dict
         s["platform_cpu"] = {k: platform.get(k) for k in ("cores_used", "reserved_cpus", "outside_rank_set")}
     if envelope:
         s["envelope"] = {k: envelope.get(k) for k in ("tasks_per_s", "errors", "tasks_per_s_over_budget_rate",
-                                                       "store_429s_per_task", "store_429s_per_call")}
-        s["envelope"]["steady_ru_over_budget"] = (envelope.get("steady_window") or {}).get("ru_over_budget")
+                                                       "store_429s_per_task")}
         k = envelope.get("keda") or {}
         s["keda"] = {x: k.get(x) for x in ("peak_replicas", "time_to_peak_s", "exactly_once")}
     return s
@@ -1794,7 +1796,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                            "external_ingest": ingest,
                            "api_sidecar_direct": direct,
                            "api_protocol_alt": alt, "durable": _drop(durable, "api_wire"),
-                           "reference_envelope": envelope}}), flush=True)
+                           "reference_envelope": envelope}}, separators=(",", ":")), flush=True)
     finally:
         if sweeper is not None and sweeper.thread.is_alive():
             sweeper.stop()

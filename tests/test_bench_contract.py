@@ -49,7 +49,8 @@ def test_bench_single_process():
     sm = cfg["summary"]
     # /proc counts CPU in 10 ms ticks: over this run's ~64 timed tasks a cheap role can read 0
     assert sm["cpu_us_per_task"] > 0 and sm["cpu_us_per_task_by_role"]["ingress"] >= 0
-    assert set(sm["sweep"]) >= {"sweeps", "sweep_p50_ms", "sweep_p99_ms", "sweep_max_ms"}
+    assert set(sm["sweep"]) >= {"sweeps", "sweep_p50_ms", "sweep_max_ms"}
+    assert len(json.dumps(sm, separators=(",", ":"))) < 1000, sm  # the driver keeps config's head
     # the reference SDK's wire: every task's save and publish went over the sidecar's gRPC API
     assert cfg["api_protocol"] == sm["api_protocol"] == "grpc"
     w = cfg["api_wire"]
