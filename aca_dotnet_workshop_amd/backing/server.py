@@ -852,11 +852,19 @@ def main(argv: list[str] | None = None) -> None:
             Path(tmp).write_text(str(port))
             os.replace(tmp, a.port_file)
 
+    pc = os.environ.get("TT_PC_SAMPLE")  # native PC sampling of this whole process (diagnostics)
+    if pc:
+        from .. import native
+        native.load().pc_sample_start()
     try:
         with maybe_profile(f"backing-{os.path.basename(a.port_file or str(a.port))}"):
             asyncio.run(serve_backing(a.host, a.port, a.data_dir, policy, ready, uds=a.uds))
     except KeyboardInterrupt:
         pass
+    finally:
+        if pc:
+            from .. import native
+            native.load().pc_sample_dump("backing")
 
 
 if __name__ == "__main__":

@@ -52,13 +52,13 @@ def _stale(target: Path, sources: list[Path]) -> bool:
     return any(s.exists() and s.stat().st_mtime > t for s in sources)
 
 
-EXE_ONLY_HEADERS = {"pcsample.hpp"}
+EXE_ONLY_HEADERS: set[str] = set()
 
 
 def build_native(force: bool = False, verbose: bool = False) -> Path:
     target = ext_path("_ttnative")
-    # every header but the executables-only ones (pcsample.hpp: the data plane's and ingress's
-    # self-profiler) -- a change there must not make the extension look stale
+    # every header but the executables-only ones -- a change there must not make the
+    # extension look stale
     sources = sorted(h for h in SRC.glob("*.hpp") if h.name not in EXE_ONLY_HEADERS) + [SRC / "module.cpp"]
     if not force and not _stale(target, sources):
         return target
@@ -72,7 +72,9 @@ def _compile_native(target: Path, verbose: bool) -> None:
     import pybind11
     cxx = os.environ.get("CXX", "g++")
     tmp = target.with_suffix(f".tmp{os.getpid()}.so")
-    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+    # default visibility: the engines' functions are in the dynamic symbol table, so a
+    # TT_PC_SAMPLE profile of a process hosting them (the backing) names them (dladdr)
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-attributes",
            f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", str(SRC / "module.cpp"),
            "-o", str(tmp), "-lpthread", "-lssl", "-lcrypto"]
     if verbose:

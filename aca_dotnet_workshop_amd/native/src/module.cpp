@@ -15,6 +15,7 @@
 #include "httpparse.hpp"
 #include "taskcodec.hpp"
 #include "sweepcodec.hpp"
+#include "pcsample.hpp"
 #include "formcodec.hpp"
 #include "strrank.hpp"
 
@@ -252,6 +253,12 @@ static std::string bytes_of(const py::handle& b) {
 }
 
 PYBIND11_MODULE(_ttnative, m) {
+  // TT_PC_SAMPLE for a Python process that hosts native engines (the backing services): the
+  // process's CPU time sampled by program counter, the interpreter's share included
+  // (pcsample.hpp); dump at exit
+  m.def("pc_sample_start", [] { tt::pcsample::start(); });
+  m.def("pc_sample_dump", [](const std::string& who) { tt::pcsample::dump(who.c_str()); },
+        py::call_guard<py::gil_scoped_release>());
   m.doc() = "Native document store + message broker engines (C++17)";
 
   static py::exception<EtagMismatch> etag_exc(m, "EtagMismatch");

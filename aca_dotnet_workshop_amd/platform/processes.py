@@ -94,6 +94,14 @@ class LocalStack:
         return subprocess.Popen(args, env=env, stdout=out, stderr=subprocess.STDOUT, cwd=str(REPO_ROOT),
                                 start_new_session=True, preexec_fn=pin_preexec(role))
 
+    def _backing_env(self) -> dict[str, str]:
+        """The backing's environment: its math libraries' thread pools at TT_BACKING_MATH_THREADS
+        (default 1).  Its hot work is the native front's loops and the GPU scans; a BLAS or
+        OpenMP pool sized for the whole machine (the box exports OMP_NUM_THREADS=16) only spins on
+        the platform's few reserved CPUs next to the ingress and the load generator."""
+        n = os.environ.get("TT_BACKING_MATH_THREADS", "1")
+        return {**self.base_env, "OMP_NUM_THREADS": n, "OPENBLAS_NUM_THREADS": n, "MKL_NUM_THREADS": n}
+
     def start_backing(self, data_dir: str | None = None, policy: dict[str, Any] | None = None,
                       timeout: float = 60.0) -> str:
         pf = self.root / "backing.port"
@@ -107,7 +115,7 @@ class LocalStack:
             pp = self.root / "policy.json"
             pp.write_text(json.dumps(policy))
             args += ["--policy", str(pp)]
-        self.backing_proc = self._spawn(args, self.base_env, "backing", role="platform")
+        self.backing_proc = self._spawn(args, self._backing_env(), "backing", role="platform")
         port = _wait_file(pf, timeout, self.backing_proc)
         self.backing_url = f"http://127.0.0.1:{port}"
         self._backing_args = args
@@ -131,7 +139,7 @@ class LocalStack:
         args[args.index("--port") + 1] = str(self._backing_port)
         deadline = time.time() + timeout
         while True:  # the old listener's port may take a moment to be released
-            self.backing_proc = self._spawn(args, self.base_env, "backing", role="platform")
+            self.backing_proc = self._spawn(args, self._backing_env(), "backing", role="platform")
             try:
                 _wait_file(pf, max(1.0, deadline - time.time()), self.backing_proc)
                 return self.backing_url
@@ -149,7 +157,7 @@ class LocalStack:
             pf.unlink()
         args = [sys.executable, "-m", "aca_dotnet_workshop_amd.backing.server", "--port", "0", "--port-file", str(pf)]
         uds = self._uds_args(tag)
-        p = self._spawn(args + uds, self.base_env, f"backing-{tag}", role="platform")
+        p = self._spawn(args + uds, self._backing_env(), f"backing-{tag}", role="platform")
         url = f"http://127.0.0.1:{_wait_file(pf, timeout, p)}"
         for f in families:
             self.extra_backing[f] = (p, url)
