@@ -1139,10 +1139,17 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         th.start()
         steady: dict = {}
 
-        def mark_steady() -> None:  # one second in: past the start-up (the bucket starts empty)
-            if not stop.wait(1.0):
-                steady.update(t=time.perf_counter(), st=_collection_stats(env.backing_url).get("throughput", {}),
-                              enq=int(_counts(counts).get("enqueued", 0)))
+        def mark_steady() -> None:
+            # the steady window opens at the first 429: the bucket is empty from there on (before
+            # it, the load spends the budget an idle bucket holds -- up to a second's worth, which
+            # a demand just above the budget takes seconds to drain)
+            t_lim = time.perf_counter() + 5.0
+            while not stop.wait(0.02):
+                st = _collection_stats(env.backing_url).get("throughput", {})
+                if st.get("throttled", 0) > st0.get("throttled", 0) or time.perf_counter() > t_lim:
+                    steady.update(t=time.perf_counter(), st=st, enq=int(_counts(counts).get("enqueued", 0)),
+                                  at_first_429=time.perf_counter() <= t_lim)
+                    return
         th2 = threading.Thread(target=mark_steady, daemon=True)
         th2.start()
         enq0 = int(_counts(counts).get("enqueued", 0))
@@ -1169,9 +1176,8 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
         ru = float(st1.get("ru_consumed", 0.0)) - float(st0.get("ru_consumed", 0.0))
         el = float(rep.get("elapsed_s") or wall)
         budget = float(st1.get("ru_per_s", 0.0))
-        # the steady window: from one second in to the end -- RU admitted there over the budget's
-        # refill (the bucket starts empty, so the whole window's ratio is bounded by 1 as well; an
-        # idle second refills up to one second of budget, which the steady window may still hold)
+        # the steady window: from the first 429 to the end -- RU admitted there over the budget's
+        # refill
         sw = None
         if steady and t_end - steady["t"] > 1.0 and budget:
             w = t_end - steady["t"]
@@ -1179,7 +1185,8 @@ def reference_envelope(exe: str, root: str, seconds: float, rank: int) -> dict:
                 w = float(st1["mono"]) - float(steady["st"]["mono"])
             ru_s = float(st1.get("ru_consumed", 0.0)) - float(steady["st"].get("ru_consumed", 0.0))
             sw = {"seconds": round(w, 2), "tasks_per_s": round((enq1 - steady["enq"]) / w, 1),
-                  "ru_consumed_per_s": round(ru_s / w, 1), "ru_over_budget": round(ru_s / (budget * w), 3)}
+                  "ru_consumed_per_s": round(ru_s / w, 1), "ru_over_budget": round(ru_s / (budget * w), 3),
+                  "opens": "at the first 429" if steady.get("at_first_429") else "5 s in (no 429 by then)"}
         by_kind = {k: int(st1.get(f"throttled_{k}", 0) - st0.get(f"throttled_{k}", 0))
                    for k in ("write", "query", "read", "delete")}
         return {"tasks_per_s": round(tasks / el, 1) if el else None, "tasks": tasks, "seconds": round(el, 2),
