@@ -350,3 +350,4 @@ def test_keda_reference_timings_30s_polling_300s_cooldown(tmp_path):
     # the backlog drained long before: the replicas stayed up for the window, not for the work
     assert k["drain_s"] < k["scaled_in_to_1_s"] - 200.0, k
     assert k["replica_timeline"][0][1] == 1 and k["replica_timeline"][-1][1] == 1
+    print(k)  # the timings (pytest -s): last active poll, last scale-out recommendation, scale-in
