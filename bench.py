@@ -119,6 +119,9 @@ def parse() -> argparse.Namespace:
     ap.add_argument("--platform-split", type=int, choices=(0, 1), default=1,
                     help="pin the platform's processes (backing, ingress, load generator) to PLATFORM_CPUS of the "
                          "rank's CPUs and the replicas to the rest (1), or let them share the set (0)")
+    ap.add_argument("--platform-cpus", type=int, default=PLATFORM_CPUS,
+                    help="CPUs of the rank's set reserved for the platform's processes (the replicas' caps "
+                         "share the rest of the rank's CPU budget)")
     ap.add_argument("--ingest-messages", type=int, default=4096,
                     help="messages of the external_ingest run (storage queue -> processor -> API -> blob; 0 = skip)")
     ap.add_argument("--session-flows", type=int, default=-1,
@@ -1495,7 +1498,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
     from aca_dotnet_workshop_amd.parallel import pin_all_threads, split_platform
     # the rank's CPU set split: the platform's processes on PLATFORM_CPUS of them, the replicas
     # on the rest (each process pinned when it is started: parallel.pin_preexec)
-    split = split_platform(set(pinned) if pinned else None, PLATFORM_CPUS) if a.platform_split else None
+    split = split_platform(set(pinned) if pinned else None, a.platform_cpus) if a.platform_split else None
     if split is not None:
         os.environ["TT_PLATFORM_CPUS"] = ",".join(map(str, sorted(split[0])))
         os.environ["TT_REPLICA_CPUS"] = ",".join(map(str, sorted(split[1])))
