@@ -1000,6 +1000,13 @@ class DataPlane {
              "(store and broker calls to the backing's Unix socket)\n"
              "# TYPE sidecar_pipelined_requests_total counter\n"
              "sidecar_pipelined_requests_total{app=\"" + app_id_ + "\"} " + std::to_string(client_.pipelined()) + "\n";
+    extra += "# HELP sidecar_client_connects_total outbound connections opened (the pools had none idle); "
+             "tls: with a TLS handshake\n"
+             "# TYPE sidecar_client_connects_total counter\n"
+             "sidecar_client_connects_total{app=\"" + app_id_ + "\",transport=\"any\"} " +
+             std::to_string(client_.connects()) + "\n" +
+             "sidecar_client_connects_total{app=\"" + app_id_ + "\",transport=\"tls\"} " +
+             std::to_string(client_.tls_connects()) + "\n";
     extra += "# HELP sidecar_partitioned_query_rows_total cross-partition state queries: sort-key entries the "
              "shards sent (phase keys) and documents fetched for the merged pages (phase documents)\n"
              "# TYPE sidecar_partitioned_query_rows_total counter\n"

@@ -1184,6 +1184,10 @@ class Client {
       if (p.get() == c) p.reset();
   }
   uint64_t pipelined() const { return pipelined_; }
+  // new outbound connections, by transport (a TLS one costs a handshake): how often the pools
+  // had no idle connection to hand out
+  uint64_t connects() const { return connects_; }
+  uint64_t tls_connects() const { return tls_connects_; }
 
   void release(const std::shared_ptr<ClientConn>& c) {
     auto& v = idle_[c->key_];
@@ -1281,7 +1285,7 @@ class Client {
     size_t cur = 0;
   };
   std::unordered_map<std::string, PipeGroup> pipes_;
-  uint64_t pipelined_ = 0;
+  uint64_t pipelined_ = 0, connects_ = 0, tls_connects_ = 0;
 
   std::shared_ptr<PipeConn> pipe_for(const Endpoint& ep) {
     std::string key = ep.key();
@@ -1335,7 +1339,9 @@ class Client {
 
   std::shared_ptr<ClientConn> connect(const Endpoint& ep, const std::string& key, int& err) {
     const TlsContext* tctx = nullptr;
+    ++connects_;
     if (ep.tls) {
+      ++tls_connects_;
       tctx = tls_for(ep);
       if (!tctx) {  // "mtls:" endpoint but this process has no mesh identity
         err = EPROTO;

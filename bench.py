@@ -1001,6 +1001,43 @@ def _sidecar_counter(uds: str, op: str) -> int:
 WIRE_OPS = ("grpc.SaveState", "grpc.PublishEvent", "grpc.QueryStateAlpha1", "state.save", "publish", "state.query")
 
 
+def _sidecar_metric(uds: str, prefix: str) -> dict[str, int]:
+    """The lines of a native data plane's /metrics that start with ``prefix``: label text ->
+    value."""
+    import socket as _socket
+    s = _socket.socket(_socket.AF_UNIX, _socket.SOCK_STREAM)
+    try:
+        s.settimeout(10)
+        s.connect(uds)
+        s.sendall(b"GET /metrics HTTP/1.1\r\nhost: x\r\nconnection: close\r\n\r\n")
+        buf = b""
+        while chunk := s.recv(65536):
+            buf += chunk
+    except OSError:
+        return {}
+    finally:
+        s.close()
+    out = {}
+    for ln in buf.decode(errors="replace").splitlines():
+        if ln.startswith(prefix + "{"):
+            labels, v = ln.rsplit(" ", 1)
+            out[labels[len(prefix):]] = int(float(v))
+    return out
+
+
+def _client_connects(env) -> dict[str, dict[str, int]]:
+    """Per app, the outbound connections its sidecars' data planes opened so far (``any`` /
+    ``tls``: with a handshake) -- how often a pool had no idle connection."""
+    out: dict[str, dict[str, int]] = {}
+    for app in (FRONTEND, API, PROC):
+        tot = {"any": 0, "tls": 0}
+        for r in env.replicas(app):
+            for labels, v in _sidecar_metric(r.sidecar_uds, "sidecar_client_connects_total").items():
+                tot["tls" if 'transport="tls"' in labels else "any"] += v
+        out[app.replace("tasksmanager-", "").replace("backend-", "").replace("-webapp", "")] = tot
+    return out
+
+
 def _api_wire(env) -> dict[str, int]:
     """The API sidecars' data-plane counters of the calls that carry a task: gRPC RPCs
     (``grpc.*``) and the HTTP API operations they run as (``state.save`` / ``publish`` count
@@ -1607,6 +1644,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         th0 = env.stack.thread_cpu(_ingress_pid(env))
         duty0 = env.ctl.limiter.duty_stats()
         ru0 = _collection_stats(backing).get("throughput", {})
+        conn0 = _client_connects(env)
         acc0 = _accel_stats(shards) if sweeper is not None else {}
         wire0 = _api_wire(env)
         if sweeper is not None:
@@ -1633,6 +1671,8 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         platform_cpu["repinned_before_timed"] = repinned[:8]
         platform_cpu["repinned_threads"] = len(repinned)
         ru1 = _collection_stats(backing).get("throughput", {})
+        conn1 = _client_connects(env)
+        connects = {k: {t: v[t] - conn0.get(k, {}).get(t, 0) for t in v} for k, v in conn1.items()}
         dt_max = d.max(dt)
         busy = {k: (cpu1.get(k, 0.0) - v) / dt for k, v in cpu0.items()}  # cores busy per role
         util = {k: round(v, 2) for k, v in busy.items()}
@@ -1760,6 +1800,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "cpu_us_per_task": cpu_us,
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
+                              "sidecar_client_connects": connects,
                               "threads": threads_all}), file=sys.stderr, flush=True)
             summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
                                      ingest, platform_cpu, durable)
@@ -1784,6 +1825,9 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                                        "loops, certificate verified against the environment CA"
                                        if ingress else "bypassed: the load generator balances over the frontend replicas"),
                            "hot_threads": hot,
+                           # outbound connections the sidecars opened in the timed region (tls: a
+                           # mesh handshake each): the pools' misses
+                           "sidecar_client_connects": connects,
                            "mtls": bool(a.mtls), "ru_per_s": a.ru_per_s or "unlimited", "ru_consumed_per_s": ru_used,
                            "platform_cpu": platform_cpu,
                            "cpu_limits": {"enforced": bool(a.cpu_limits), "vcpu_per_replica": caps,
