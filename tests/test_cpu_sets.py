@@ -67,3 +67,26 @@ def test_pin_all_threads_covers_running_threads():
     finally:
         stop.set()
         t.join()
+
+
+@pytest.mark.skipif(len(ALL) < 2, reason="needs two CPUs")
+def test_hold_affinity_puts_every_thread_back():
+    """A runtime that widens the calling thread's set (the GPU runtime's first call does) and
+    starts threads from it: on leaving ``hold_affinity`` every thread of the process is back on
+    the set it had on entry."""
+    code = """
+import os, threading, time
+from aca_dotnet_workshop_amd.parallel import hold_affinity, cpus_allowed
+one = {min(os.sched_getaffinity(0))}
+os.sched_setaffinity(0, one)
+ev = threading.Event()
+with hold_affinity():
+    os.sched_setaffinity(0, set(range(os.cpu_count())) & set(%r))  # the runtime widens it
+    t = threading.Thread(target=ev.wait, daemon=True)
+    t.start()                                  # ... and starts a thread with the wide set
+print(sorted({c for s in cpus_allowed(os.getpid()).values() for c in s}) == sorted(one))
+ev.set()
+""" % (sorted(ALL),)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                         env={**os.environ, "PYTHONPATH": os.path.dirname(os.path.dirname(__file__))})
+    assert out.stdout.strip() == "True", out.stderr[-2000:]
