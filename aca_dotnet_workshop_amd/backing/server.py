@@ -37,6 +37,7 @@ from .. import native
 from ..telemetry import configure, configure_logging
 from ..telemetry.tracing import parse_traceparent, tracer
 from ..telemetry.profiler import maybe_profile
+from ..utils import gctrace
 from ..web.app import WebApp
 from ..web.http import HTTPError, Request, Response, empty, json_response, problem
 from .accel import CollectionAccelerator, accelerator_from_env, mirror_paths_from_env
@@ -852,6 +853,7 @@ def main(argv: list[str] | None = None) -> None:
             Path(tmp).write_text(str(port))
             os.replace(tmp, a.port_file)
 
+    gctrace.install("backing-" + os.path.basename(a.port_file or str(a.port)))
     pc = os.environ.get("TT_PC_SAMPLE")  # native PC sampling of this whole process (diagnostics)
     if pc:
         from .. import native

@@ -256,6 +256,29 @@ PYBIND11_MODULE(_ttnative, m) {
   // TT_PC_SAMPLE for a Python process that hosts native engines (the backing services): the
   // process's CPU time sampled by program counter, the interpreter's share included
   // (pcsample.hpp); dump at exit
+  // Growth points of the store's sharded key map: insert n GUID-like keys (as the task ids are)
+  // and return, per insert at which any shard grew, [insert index, shards grown].
+  m.def("sharded_map_growth", [](size_t n) {
+    tt::ShardedMap<int32_t> map;
+    constexpr size_t S = tt::ShardedMap<int32_t>::shards();
+    std::vector<size_t> bkt(S);
+    for (size_t s = 0; s < S; ++s) bkt[s] = map.bucket_count(s);
+    std::vector<std::pair<size_t, size_t>> out;
+    uint64_t x = 0x9e3779b97f4a7c15ull;
+    char key[37];
+    for (size_t i = 0; i < n; ++i) {
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      uint64_t y = x * 0x2545f4914f6cdd1dull;
+      std::snprintf(key, sizeof key, "%08x-%04x-4%03x-a%03x-%012llx", (unsigned)(x >> 32), (unsigned)(x >> 16) & 0xffff,
+                    (unsigned)x & 0xfff, (unsigned)(y >> 52), (unsigned long long)(y & 0xffffffffffffull));
+      map[key] = (int32_t)i;
+      size_t grown = 0;
+      for (size_t s = 0; s < S; ++s)
+        if (map.bucket_count(s) != bkt[s]) bkt[s] = map.bucket_count(s), ++grown;
+      if (grown) out.emplace_back(i, grown);
+    }
+    return out;
+  }, py::call_guard<py::gil_scoped_release>());
   m.def("pc_sample_start", [] { tt::pcsample::start(); });
   m.def("pc_sample_dump", [](const std::string& who) { tt::pcsample::dump(who.c_str()); },
         py::call_guard<py::gil_scoped_release>());

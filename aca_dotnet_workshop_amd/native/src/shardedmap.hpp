@@ -4,11 +4,16 @@
 // all at once: for the document store's 350k-document collection (or a column dictionary with a
 // value per document) that is ~20-50 ms during which the store lock is held and every front
 // thread waits on it (profiles/r4_sweep_tail.md).  Here each of kShards maps grows on its own,
-// so a growth step relinks 1/kShards of the entries.  Node-based like the maps it is made of:
+// so a growth step relinks 1/kShards of the entries.  Keys spread evenly over the shards, so
+// shards with equal load limits would all reach them within the same few thousand inserts: the
+// whole collection relinked in one burst after all, only in 1/kShards slices.  Each shard has its
+// own load limit instead, 2^(-s/kShards) for shard s (0.5-1.0), so the shards' growth points
+// spread evenly over every doubling of the collection.  Node-based like the maps it is made of:
 // references and pointers to elements stay valid until the element is erased (the column
 // mirror keeps pointers to the keys).  Iteration order is unspecified, as for unordered_map.
 #pragma once
 
+#include <cmath>
 #include <cstddef>
 #include <cstdint>
 #include <string>
@@ -24,6 +29,10 @@ class ShardedMap {
 
  public:
   using value_type = typename Inner::value_type;
+
+  ShardedMap() {
+    for (size_t s = 0; s < kShards; ++s) shards_[s].max_load_factor((float)std::exp2(-(double)s / (double)kShards));
+  }
 
   class iterator {
    public:
@@ -78,6 +87,8 @@ class ShardedMap {
     return n;
   }
   bool empty() const { return size() == 0; }
+  size_t bucket_count(size_t shard) const { return shards_[shard].bucket_count(); }
+  static constexpr size_t shards() { return kShards; }
   void clear() {
     for (auto& s : shards_) s.clear();
   }

@@ -25,6 +25,7 @@ from typing import Any, Callable
 from ..telemetry import REGISTRY, configure, configure_logging
 from ..telemetry.metrics import request_telemetry_middleware
 from ..telemetry.profiler import maybe_profile
+from ..utils import gctrace
 from ..utils.config import Configuration, load_configuration
 from ..web.app import WebApp
 from ..web.http import Response, empty, json_response, text_response
@@ -198,6 +199,7 @@ async def serve_host(app: WebApp, stop: asyncio.Event | None = None,
             pass
     log.info("%s listening on %s%s", app.name, ports, f" + {uds}" if uds else "")
     tune_gc()
+    gctrace.install(app.name)
     if ready:
         ready(ports)
     port_file = config.get_str("TT_PORT_FILE")
