@@ -19,6 +19,9 @@
 // HTTPS targets: `--target https://127.0.0.1:port` with `--tls-ca ca.crt` verifies the server
 // certificate (name / address) against that CA, the way a browser trusting it would; without
 // `--tls-ca` the connection is encrypted but unverified.
+// `--pause-after W` (one generator): after W steps (a warmup) print their JSON line, then wait for
+// a line on stdin before the other steps; the final line covers only those.  The connections
+// opened in the warmup (TLS handshakes included) carry the later steps, as a browser's would.
 // `--threads T` (stepped mode): T generators on T event loops, each with its share of the
 // in-flight window and of every step's batch; each waits for the counter to advance by the
 // WHOLE batch, so the steps stay in lock-step.  One JSON line merges them.
@@ -53,7 +56,7 @@ struct Opts {
   std::string tls_ca;
   std::vector<std::string> bodies{""};
   ev::HeaderList headers;
-  int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0, threads = 1;
+  int concurrency = 64, batch = 512, steps = 1, expect = 0, users = 0, threads = 1, pause_after = 0;
   int body_offset = 0;  // this generator's first body (a thread's share of the cycle)
   bool follow = false;
   double duration_s = 0;
@@ -206,6 +209,7 @@ class Gen {
 
   void begin_step() {
     if (step_t0_ > 0) steps_.emplace_back(step_creates_, ev::now_s() - step_t0_);
+    if (o_.pause_after > 0 && step_ == o_.pause_after && step_ < o_.steps) pause();
     if (step_ == o_.steps) {
       t1_ = ev::now_s();
       loop_.stop();
@@ -215,6 +219,27 @@ class Gen {
     step_t0_ = ev::now_s();
     int n = std::min(o_.concurrency, o_.batch);
     for (int i = 0; i < n; ++i) issue();
+  }
+
+  // the warmup's line, then a blocking wait for the go line (nothing else runs on this loop);
+  // the later steps' figures start from zero
+  void pause() {
+    t1_ = ev::now_s();
+    std::printf("%s\n", report().c_str());
+    std::fflush(stdout);
+    char line[64];
+    if (!std::fgets(line, sizeof line, stdin)) {  // the parent went away: stop here
+      o_.steps = step_;
+      return;
+    }
+    lat_.clear();
+    follow_lat_.clear();
+    statuses_.clear();
+    steps_.clear();
+    done_total_ = errors_ = 0;
+    first_error_.clear();
+    step_t0_ = 0;
+    t0_ = ev::now_s();
   }
 
   void issue() {
@@ -542,6 +567,7 @@ int main(int argc, char** argv) {
     else if (a == "--until-base") o.until_base = std::atoll(next().c_str());
     else if (a == "--until-stride") o.until_stride = std::atoll(next().c_str());
     else if (a == "--threads") o.threads = std::max(1, std::atoi(next().c_str()));
+    else if (a == "--pause-after") o.pause_after = std::max(0, std::atoi(next().c_str()));
     else if (a == "--session") session_token = next();
     else if (a == "--bodies") {
       std::ifstream in(next());
@@ -568,6 +594,10 @@ int main(int argc, char** argv) {
     return g.errors() ? 1 : 0;
   }
   int threads = std::min(o.threads, std::min(o.concurrency, o.batch));
+  if (o.pause_after > 0 && (threads > 1 || o.duration_s > 0)) {
+    std::fprintf(stderr, "--pause-after needs one stepped generator\n");
+    return 2;
+  }
   if (threads <= 1 || o.duration_s > 0 || o.follow) {  // one generator on this thread
     ev::Loop loop;
     Gen g(loop, o);

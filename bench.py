@@ -735,12 +735,9 @@ def _form_bodies(batch: int, token: str, past_due_every: int) -> list[bytes]:
             for i in range(batch)]
 
 
-def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int, batch: int,
-                     conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
-                     ca_file: str | None = None, threads: int = 1, extra: list[str] | None = None) -> tuple[float, dict]:
-    """``targets``: ``host:port`` (a frontend replica) or ``https://host:port`` (the external
-    ingress; ``ca_file`` -- the environment CA -- verifies its certificate like a browser)."""
-    import subprocess
+def _form_loadgen_cmd(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int,
+                      batch: int, conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
+                      ca_file: str | None = None, threads: int = 1, extra: list[str] | None = None) -> list[str]:
     cmd = [exe, "--path", "/Tasks/Create", "--bodies", bodies_file, "--content-type",
            "application/x-www-form-urlencoded", "--header", f"Cookie: {cookie}", "--concurrency", str(conc),
            "--batch", str(batch), "--steps", str(steps), "--expect", "302", "--until-timeout", "300",
@@ -754,6 +751,59 @@ def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str 
     cmd += extra or []
     for t in targets:
         cmd += ["--target", t]
+    return cmd
+
+
+class WarmLoadgen:
+    """One ``ttloadgen --pause-after W`` process for the warmup and the timed steps: it runs the
+    W warmup steps, prints their line and waits; ``timed()`` sends the go line and waits for the
+    timed steps' line.  The timed steps reuse the warmup's connections (TLS handshakes done), as a
+    browser keeps its connections; the timed region holds no process start and no handshake."""
+
+    def __init__(self, cmd: list[str], warmup: int, root: str) -> None:
+        import subprocess
+        self._err = open(os.path.join(root, "loadgen.err"), "w+")
+        self.p = subprocess.Popen(cmd + ["--pause-after", str(warmup)], stdin=subprocess.PIPE,
+                                  stdout=subprocess.PIPE, stderr=self._err, text=True)
+
+    def _fail(self, what: str) -> None:
+        self.p.kill()
+        self.p.wait()
+        self._err.seek(0)
+        raise RuntimeError(f"load generator failed ({what}, rc {self.p.returncode}): {self._err.read()[-500:]}")
+
+    def warmup(self) -> dict:
+        line = self.p.stdout.readline()
+        if not line:
+            self._fail("no warmup line")
+        rep = json.loads(line)
+        if rep.get("errors"):
+            self._fail(f"warmup errors: {rep.get('first_error')}")
+        return rep
+
+    def timed(self) -> tuple[float, dict]:
+        t0 = time.perf_counter()
+        self.p.stdin.write("go\n")
+        self.p.stdin.flush()
+        out = self.p.stdout.read()
+        rc = self.p.wait(timeout=900)
+        dt = time.perf_counter() - t0
+        lines = out.strip().splitlines()
+        if rc != 0 or not lines:
+            self._err.seek(0)
+            raise RuntimeError(f"load generator failed ({rc}): {out[-500:]} {self._err.read()[-500:]}")
+        self._err.close()
+        return dt, json.loads(lines[-1])
+
+
+def run_form_loadgen(exe: str, targets: list[str], cookie: str, counts_url: str | list[str], steps: int, batch: int,
+                     conc: int, bodies_file: str, shared: tuple[int, int] | None = None,
+                     ca_file: str | None = None, threads: int = 1, extra: list[str] | None = None) -> tuple[float, dict]:
+    """``targets``: ``host:port`` (a frontend replica) or ``https://host:port`` (the external
+    ingress; ``ca_file`` -- the environment CA -- verifies its certificate like a browser)."""
+    import subprocess
+    cmd = _form_loadgen_cmd(exe, targets, cookie, counts_url, steps, batch, conc, bodies_file, shared, ca_file,
+                            threads, extra)
     t0 = time.perf_counter()
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
     dt = time.perf_counter() - t0
@@ -1627,7 +1677,14 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             # job (mirror built, device columns and zone maps resident), not its first run
             sweeper = OverdueSweeper(env.replicas(PROC)[0].sidecar_uds, a.overdue_sweep_ms / 1000.0)
             sweeper.start()
-        if a.warmup:
+        warm = None
+        if a.warmup and a.loadgen_threads <= 1:  # one generator process for warmup and timed steps
+            progress(f"warmup: {a.warmup} steps")
+            warm = WarmLoadgen(_form_loadgen_cmd(exe, targets, cookie, counts_url, a.warmup + a.steps, a.batch, conc,
+                                                 bodies_file, (gbase, stride) if shared else None, ca_file),
+                               a.warmup, root)
+            warm.warmup()
+        elif a.warmup:
             progress(f"warmup: {a.warmup} steps")
             run_form_loadgen(exe, targets, cookie, counts_url, a.warmup, a.batch, conc, bodies_file,
                              (gbase, stride) if shared else None, ca_file, a.loadgen_threads)
@@ -1649,9 +1706,13 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
         wire0 = _api_wire(env)
         if sweeper is not None:
             sweeper.reset()  # sweeps of the timed region only
-        dt, report = run_form_loadgen(exe, targets, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
-                                      (gbase + stride * a.warmup, stride) if shared else None, ca_file,
-                                      a.loadgen_threads)
+        wall0 = time.time()
+        if warm is not None:
+            dt, report = warm.timed()
+        else:
+            dt, report = run_form_loadgen(exe, targets, cookie, counts_url, a.steps, a.batch, conc, bodies_file,
+                                          (gbase + stride * a.warmup, stride) if shared else None, ca_file,
+                                          a.loadgen_threads)
         device_sync()
         d.barrier()
         if sweeper is not None:
@@ -1800,7 +1861,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "cpu_us_per_task": cpu_us,
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
-                              "sidecar_client_connects": connects,
+                              "sidecar_client_connects": connects, "timed_wall_start": round(wall0, 6),
                               "threads": threads_all}), file=sys.stderr, flush=True)
             summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
                                      ingest, platform_cpu, durable)
