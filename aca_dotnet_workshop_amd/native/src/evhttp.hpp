@@ -59,6 +59,23 @@ inline void widen_local_sndbuf(int fd) {
   setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
 }
 
+// TCP connections (the sidecars' mutual-TLS mesh, the ingress): no Nagle delay.  With
+// TT_TCP_BUF_KB=<n> (an A/B switch; default 0 = the kernel's autotuning) also fixed send and
+// receive buffers of n KB, so a whole page of query results fits in one write.
+inline void tune_tcp(int fd) {
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  static const int kb = [] {
+    const char* v = std::getenv("TT_TCP_BUF_KB");
+    return v && *v ? std::max(0, std::atoi(v)) : 0;
+  }();
+  if (kb > 0) {
+    int sz = kb << 10;
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
+  }
+}
+
 // ------------------------------------------------------------------------------ loop
 struct IoObj : std::enable_shared_from_this<IoObj> {
   int fd = -1;
@@ -872,9 +889,8 @@ class Listener : public IoObj {
         if (errno == EINTR) continue;
         return;  // EAGAIN or transient error (EMFILE ...): try again on the next readiness event
       }
-      int one = 1;
       if (unix_) widen_local_sndbuf(c);
-      else setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      else tune_tcp(c);
       if (hand_off && hand_off(c)) continue;  // another loop serves it
       std::shared_ptr<ServerConn> conn;
       try {
@@ -1366,8 +1382,7 @@ class Client {
       }
     } else {
       fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
-      int one = 1;
-      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+      tune_tcp(fd);
       sockaddr_in a{};
       a.sin_family = AF_INET;
       a.sin_port = htons((uint16_t)ep.port);
