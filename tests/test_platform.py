@@ -258,7 +258,7 @@ def test_environment_lifecycle(tmp_path, source, request):
             s1 = await ctl.live_metrics()
             rates = live_rates(s0, s1)
             assert rates["tasksmanager-backend-processor"]["replicas"] == len(s1["apps"]["tasksmanager-backend-processor"])
-            for _ in range(100):
+            for _ in range(300):  # the cooldown, then the scaler's next poll (slower on a loaded host)
                 await asyncio.sleep(0.1)
                 if len([r for r in proc.current.replicas if r.alive()]) == 1:
                     break
