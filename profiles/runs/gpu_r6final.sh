@@ -2,7 +2,7 @@
 # round 6 confirmation: GPU tests, the driver's smoke, the driver's bench command twice
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r6s
+out=gpurun_out/${1:-r6s}
 mkdir -p $out
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/gputests.log 2>&1 || exit $?
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit $?
