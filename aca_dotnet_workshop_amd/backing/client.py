@@ -240,6 +240,11 @@ class BackingClient:
             path += "?" + urlencode({"prefix": prefix})
         return (await self._req("GET", path)).json()
 
+    async def blob_count(self, account: str, container: str, prefix: str = "") -> int:
+        """How many blobs the container holds (no listing)."""
+        args = {"count": "true"} | ({"prefix": prefix} if prefix else {})
+        return int((await self._req("GET", f"/storage/{q(account)}/blobs/{q(container)}?" + urlencode(args))).json()["count"])
+
     # -- key vault ------------------------------------------------------------
     async def kv_get(self, vault: str, name: str) -> str | None:
         r = await self._req("GET", f"/keyvault/{q(vault)}/secrets/{q(name)}", ok=(200, 404))

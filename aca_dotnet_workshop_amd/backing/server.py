@@ -616,6 +616,22 @@ class BackingServices:
             p = req.path_params
             return json_response(dict(qbroker(p["account"]).counts(p["queue"])))
 
+        # per container, the names of its blobs (built by one scan on first use, then kept by
+        # put / delete -- this process is the only writer): a count needs no directory walk
+        names: dict[tuple[str, str], set[str]] = {}
+
+        def blob_names(p: dict[str, Any]) -> set[str]:
+            k = (_safe(p["account"]), _safe(p["container"]))
+            got = names.get(k)
+            if got is None:
+                root = self.blob_root / k[0] / k[1]
+                got = names[k] = set()
+                if root.is_dir():
+                    for f in root.rglob("*"):
+                        if f.is_file() and not f.name.endswith((".meta.json", ".tmp")):
+                            got.add(str(f.relative_to(root)))
+            return got
+
         def blob_file(p: dict[str, Any]) -> Path:
             root = (self.blob_root / _safe(p["account"]) / _safe(p["container"])).resolve()
             f = (root / p["name"]).resolve()
@@ -634,6 +650,7 @@ class BackingServices:
             meta = {"contentType": req.headers.get("content-type", "application/octet-stream"),
                     "lastModified": time.time(), "size": len(req.body)}
             f.with_name(f.name + ".meta.json").write_text(json.dumps(meta))
+            blob_names(p).add(os.path.normpath(p["name"]))
             return json_response({"blobURL": f"/storage/{p['account']}/blobs/{p['container']}/{p['name']}"}, 201)
 
         async def get_blob(req: Request) -> Response:
@@ -658,6 +675,7 @@ class BackingServices:
             mf = f.with_name(f.name + ".meta.json")
             if mf.exists():
                 mf.unlink()
+            blob_names(p).discard(os.path.normpath(p["name"]))
             return empty(204)
 
         async def list_blobs(req: Request) -> Response:
@@ -665,6 +683,9 @@ class BackingServices:
             self.authorize(req, "blob.read", f"storage/{p['account']}")
             root = self.blob_root / _safe(p["account"]) / _safe(p["container"])
             prefix = req.query_get("prefix", "") or ""
+            if (req.query_get("count", "") or "").lower() in ("1", "true"):  # {"count": n}, no listing
+                got = blob_names(p)
+                return json_response({"count": sum(1 for x in got if x.startswith(prefix)) if prefix else len(got)})
             out = []
             if root.is_dir():
                 for f in sorted(root.rglob("*")):

@@ -10,8 +10,10 @@
 //   POST           /servicebus/{ns}/receive?entity&max&lockMs&waitMs   (long poll)
 //   POST           /servicebus/{ns}/settle
 //   GET            /servicebus/{ns}/counts?entity
+//   POST / GET     /storage/{account}/queues/{queue}/messages   (put; receive, long poll)
+//   DELETE / PUT   /storage/{account}/queues/{queue}/messages/{receipt}   (delete; visibility)
 //
-// Everything else (entity management, queries, transactions, storage, key vault, sendgrid,
+// Everything else (entity management, queries, transactions, blobs, key vault, sendgrid,
 // admin) and every request for an engine the Python side has not attached yet is forwarded
 // verbatim to the Python server on a private Unix socket.  Responses, status codes and RBAC
 // decisions mirror backing/server.py and backing/auth.py (role assignments are pushed down
@@ -351,6 +353,7 @@ class BackingFront {
     int64_t lock_ms;
     double deadline;
     ev::Reply reply;
+    bool storage = false;  // a storage-queue receive: its answer has the queue API's shape
   };
   struct Shard;
   struct Wake : ev::IoObj {
@@ -471,9 +474,10 @@ class BackingFront {
 
   // Request counters, bumped by every loop on every request: one relaxed atomic per name, no
   // lock and no string (the hottest names first).
-  static constexpr std::array<const char*, 13> kCounters = {
+  static constexpr std::array<const char*, 17> kCounters = {
       "doc.put", "sb.publish", "sb.receive", "sb.settle", "doc.get", "doc.bulkget", "doc.bulkset", "doc.query",
-      "doc.throttled", "doc.delete", "doc.query_worker", "doc.query_worker_done", "forwarded"};
+      "doc.throttled", "doc.delete", "doc.query_worker", "doc.query_worker_done", "forwarded",
+      "queue.put", "queue.get", "queue.delete", "queue.update"};
   std::array<std::atomic<uint64_t>, kCounters.size()> counters_{};
 
   void count(const char* k) {
@@ -558,6 +562,7 @@ class BackingFront {
     if (seg.size() == 5 && seg[0] == "cosmos" && seg[4] == "query" && m.method == "POST" && handle_query(sh, m, r, seg, qs))
       return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
+    if (seg.size() >= 5 && seg[0] == "storage" && seg[2] == "queues" && handle_storage_queue(sh, m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
   }
 
@@ -1004,6 +1009,75 @@ class BackingFront {
     return false;
   }
 
+  // -- storage queues (backing/server.py _storage_routes, the same broker "storage-<account>") --
+  // A query value the Python route would parse differently (not a plain non-negative integer)
+  // leaves the request to it.
+  static bool plain_uint(const std::string& v, int64_t& out) {
+    if (v.empty() || v.size() > 15) return false;
+    int64_t x = 0;
+    for (char c : v) {
+      if (c < '0' || c > '9') return false;
+      x = x * 10 + (c - '0');
+    }
+    out = x;
+    return true;
+  }
+  static bool uint_param(const std::string& qs, const char* name, int64_t dflt, int64_t& out) {
+    std::string v = query_get(qs, name);
+    if (v.empty()) {
+      out = dflt;
+      return true;
+    }
+    return plain_uint(v, out);
+  }
+
+  bool handle_storage_queue(Shard& sh, ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg,
+                            const std::string& qs) {
+    const std::string ns = "storage-" + seg[1];
+    Broker* b = nullptr;
+    {
+      std::shared_lock l(cfg_mu_);
+      auto it = brokers_.find(ns);
+      if (it != brokers_.end()) b = it->second;
+    }
+    if (!b) return false;  // the Python route creates the account's broker on first use
+    const std::string& account = seg[1];
+    const std::string& queue = seg[3];
+    if (seg.size() == 5 && seg[4] == "messages" && m.method == "POST") {
+      int64_t ttl_s, delay_s;
+      if (!uint_param(qs, "messagettl", 0, ttl_s) || !uint_param(qs, "visibilitytimeout", 0, delay_s)) return false;
+      if (!authorize(m, r, "queue.send", "storage/" + account)) return true;
+      count("queue.put");
+      uint64_t seq = b->send(queue, m.body, "text/plain", "{}", "", ttl_s * 1000, delay_s * 1000);
+      send_durable(sh, b, r, 201, {{"content-type", "application/json"}},
+                   "{\"messageId\": \"" + std::to_string(seq) + "\"}");
+      broadcast(sh, ns + "|" + queue);
+      return true;
+    }
+    if (seg.size() == 5 && seg[4] == "messages" && m.method == "GET") {
+      int64_t mx, vis, wait_ms;
+      if (!uint_param(qs, "numofmessages", 1, mx) || mx < 1 || !uint_param(qs, "visibilityMs", 30000, vis) ||
+          !uint_param(qs, "waitMs", 0, wait_ms))
+        return false;
+      if (!authorize(m, r, "queue.receive", "storage/" + account)) return true;
+      count("queue.get");
+      Parked p{ns, queue, (size_t)mx, vis, ev::now_s() + (double)wait_ms / 1000.0, r, true};
+      if (!try_receive(b, p, false)) sh.parked.emplace(ns + "|" + queue, std::move(p));
+      return true;
+    }
+    if (seg.size() == 6 && seg[4] == "messages" && (m.method == "DELETE" || m.method == "PUT")) {
+      int64_t vis = 0;
+      if (m.method == "PUT" && !uint_param(qs, "visibilityMs", 0, vis)) return false;
+      if (!authorize(m, r, "queue.receive", "storage/" + account)) return true;
+      count(m.method == "DELETE" ? "queue.delete" : "queue.update");
+      bool ok = m.method == "DELETE" ? b->complete(queue, seg[5]) : b->abandon(queue, seg[5], vis);
+      send_durable(sh, b, r, ok ? 204 : 404, {}, "");
+      if (m.method == "PUT") broadcast(sh, ns + "|" + queue);
+      return true;
+    }
+    return false;
+  }
+
   // Returns true when the request was answered (messages, or deadline reached).
   bool try_receive(Broker* b, Parked& p, bool expired) {
     // a receiver that went away (its process died mid long poll) must not lock messages it can
@@ -1021,6 +1095,20 @@ class BackingFront {
     }
     if (msgs.empty() && !expired && ev::now_s() < p.deadline) return false;
     std::string out = "[";
+    if (p.storage) {  // backing/server.py get_messages: messageId, popReceipt, dequeueCount, insertionMs, body
+      for (size_t i = 0; i < msgs.size(); ++i) {
+        auto& x = msgs[i];
+        if (i) out += ", ";
+        out += "{\"messageId\": \"" + std::to_string(x.seq) + "\", \"popReceipt\": " + bf::jstr(x.lock_token) +
+               ", \"dequeueCount\": " + std::to_string(x.delivery_count) +
+               ", \"insertionMs\": " + std::to_string(x.enqueued_wall);
+        if (bf::utf8_ok(x.body)) out += ", \"body\": " + bf::jstr(x.body) + "}";
+        else out += ", \"bodyB64\": \"" + bf::b64(x.body) + "\"}";
+      }
+      out += "]";
+      p.reply.send(200, {{"content-type", "application/json"}}, out);
+      return true;
+    }
     for (size_t i = 0; i < msgs.size(); ++i) {
       auto& x = msgs[i];
       if (i) out += ", ";

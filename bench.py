@@ -870,7 +870,7 @@ def external_ingest(env, n: int, timeout_s: float = 120.0) -> dict:
         container = (st.get("containers") or [None])[0]
         key = env.ctl.storage_keys.get(acct, "")
         base = f"{env.stack.backing_url_for('STORAGE')}/storage/{acct}"
-        blobs0 = len(get(f"/blobs/{container}"))
+        blobs0 = get(f"/blobs/{container}?count=true")["count"]
         q0 = get(f"/queues/{queue}/count")
         bodies = [base64.b64encode(json.dumps({"taskName": f"external task {i}", "taskAssignedTo": f"ext{i % 7}@bench.local",
                                                "taskCreatedBy": "ext@bench.local",
@@ -890,12 +890,13 @@ def external_ingest(env, n: int, timeout_s: float = 120.0) -> dict:
                 await asyncio.gather(*(one(b) for b in bodies))
             finally:
                 await c.close()
+        th0 = env.stack.thread_cpu(_ingress_pid(env))
         t0 = time.perf_counter()
         asyncio.run(put_all())
         t_put = time.perf_counter() - t0
         blobs = blobs0
         while time.perf_counter() - t0 < timeout_s:
-            blobs = len(get(f"/blobs/{container}"))
+            blobs = get(f"/blobs/{container}?count=true")["count"]
             if blobs - blobs0 >= n:
                 break
             time.sleep(0.05)
@@ -907,12 +908,14 @@ def external_ingest(env, n: int, timeout_s: float = 120.0) -> dict:
             time.sleep(0.05)
         d = {k: int(q1.get(k, 0)) - int(q0.get(k, 0)) for k in ("enqueued", "received", "completed")}
         made = blobs - blobs0
+        # the busiest threads of the ingest window (the stderr diagnostics line, not the record)
+        hot = hot_threads(th0, env.stack.thread_cpu(_ingress_pid(env)), dt, top=8)
         return {"messages": n, "msgs_per_s": round(made / dt, 1) if dt else None, "seconds": round(dt, 3),
                 "enqueue_s": round(t_put, 3), "blobs_written": made, "queue": d,
                 "deliveries_per_message": round(d["received"] / n, 3) if n else None,
                 "left_on_queue": int(q1.get("active", 0)) + int(q1.get("locked", 0)),
                 "dead": int(q1.get("dead_letter", 0)) - int(q0.get("dead_letter", 0)),
-                "all_processed": made == n and d["completed"] == n}
+                "all_processed": made == n and d["completed"] == n, "hot_threads": hot}
     except Exception as e:  # reported, not fatal to the headline
         return {"error": repr(e)[:300]}
 
@@ -1798,10 +1801,11 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
             progress(f"browser_session: {sflows} flows of 7 pages")
             session = run_session(exe, targets, cookie, token, sflows, conc, root, ca_file, a.batch)
         # §3.4 external-task ingestion: storage queue -> processor -> API -> blob
-        ingest = None
+        ingest = ingest_hot = None
         if a.ingest_messages > 0 and not shared:
             progress(f"external_ingest: {a.ingest_messages} queue messages")
             ingest = external_ingest(env, a.ingest_messages)
+            ingest_hot = ingest.pop("hot_threads", None)
         # the same environment, load straight at the API sidecars' invoke (round 2's topology);
         # not in a shared environment (its counters are global: the two loads would mix)
         direct = None
@@ -1862,6 +1866,7 @@ def main_frontend(a: argparse.Namespace, d: Dist, cores: float, pinned) -> None:
                               "cpu_budget_per_rank": round(cores, 2), "loadgen": report,
                               "overdue_sweeps": sweep_info, "sweep_trace": trace, "resource_limits": lim,
                               "sidecar_client_connects": connects, "timed_wall_start": round(wall0, 6),
+                              "external_ingest_hot_threads": ingest_hot,
                               "threads": threads_all}), file=sys.stderr, flush=True)
             summary = record_summary(value, cpu_us, sweep_info, browser, envelope, a.api_protocol, wire, alt, session,
                                      ingest, platform_cpu, durable)

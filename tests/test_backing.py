@@ -96,6 +96,27 @@ def test_storage_queue_blob_keyvault_sendgrid():
     run(main())
 
 
+def test_blob_count_follows_puts_and_deletes(tmp_path):
+    """``?count=true`` answers from the container's name set: the same number a listing gives,
+    after overwrites, nested names and deletes, and after a restart over the same directory."""
+    async def main():
+        for round_ in range(2):  # the second server starts over the first one's files
+            svc = _svc(tmp_path)
+            async with served(svc.build_app()) as (base, _):
+                c = BackingClient(base)
+                if round_ == 0:
+                    assert await c.blob_count("acct", "box") == 0
+                    for n in ("a.json", "b.json", "dir/c.json", "a.json", "dir/./d.json"):
+                        await c.blob_put("acct", "box", n, b"{}", "application/json")
+                    await c.blob_delete("acct", "box", "b.json")
+                listed = await c.blob_list("acct", "box")
+                assert sorted(b["name"] for b in listed) == ["a.json", "dir/c.json", "dir/d.json"]
+                assert await c.blob_count("acct", "box") == 3
+                assert await c.blob_count("acct", "box", prefix="dir/") == 2
+                await c.close()
+    run(main())
+
+
 def test_rbac_enforcement():
     policy = {"mode": "enforce",
               "keys": {"cosmos/acct": "masterkey"},

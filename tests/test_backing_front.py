@@ -234,6 +234,57 @@ def test_messaging_and_long_poll(front, monkeypatch):
 
 
 @pytest.mark.parametrize("front", FRONTS)
+def test_storage_queue(front, monkeypatch):
+    """The storage queue the processor's input binding reads (backing/server.py _storage_routes):
+    put, long-poll receive woken by a put, the visibility timeout, release, delete, counts and
+    non-UTF-8 bodies -- the same answers on both fronts, and the native front serving them."""
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            await c.queue_put("acct", "q", b"first")  # the account's broker is made by Python's route
+            assert (await c.queue_get("acct", "q", 1, 30000))[0]["body"] == "first"
+            t0 = time.monotonic()
+            recv = asyncio.ensure_future(c.queue_get("acct", "q", 5, 60, 3000))
+            await asyncio.sleep(0.1)
+            mid = await c.queue_put("acct", "q", b"eyJhIjoxfQ==")
+            msgs = await recv
+            assert time.monotonic() - t0 < 1.5
+            assert [(m["messageId"], m["body"], m["dequeueCount"]) for m in msgs] == [(mid, "eyJhIjoxfQ==", 1)]
+            assert msgs[0]["insertionMs"] > 0 and msgs[0]["popReceipt"]
+            await asyncio.sleep(0.1)  # its 60 ms visibility timeout elapses: it is back
+            again = await c.queue_get("acct", "q", 5, 30000)
+            assert [(m["messageId"], m["dequeueCount"]) for m in again] == [(mid, 2)]
+            assert await c.queue_release("acct", "q", again[0]["popReceipt"], 0)  # visible again now
+            third = await c.queue_get("acct", "q", 5, 30000, 1000)
+            assert third[0]["dequeueCount"] == 3
+            assert await c.queue_delete("acct", "q", third[0]["popReceipt"])
+            assert not await c.queue_delete("acct", "q", third[0]["popReceipt"])
+            assert not await c.queue_release("acct", "q", "no-such-receipt", 0)
+            await c.queue_put("acct", "q", b"\xff\x00")
+            m = (await c.queue_get("acct", "q", 1, 30000))[0]
+            assert "body" not in m and m["bodyB64"] == "/wA="
+            assert await c.queue_delete("acct", "q", m["popReceipt"])
+            t0 = time.monotonic()
+            assert await c.queue_get("acct", "q", 1, 30000, 300) == []  # an empty long poll ends at its wait
+            assert 0.25 < time.monotonic() - t0 < 2.0
+            cnt = await c.queue_count("acct", "q")
+            assert (cnt["active"], cnt["locked"], cnt["enqueued"], cnt["completed"]) == (0, 1, 3, 2)  # "first" held
+            h = HttpClient()
+            # a value the Python route parses its own way goes to it (numofmessages=0: no messages)
+            r = await h.get(b.base + "/storage/acct/queues/q/messages?numofmessages=0&waitMs=0",
+                            headers={"x-tt-identity": "x"})
+            assert r.status == 200 and r.json() == []
+            stats = (await h.get(b.base + "/admin/front")).json()
+            if front == "native":
+                req = stats["requests"]
+                assert req["queue.put"] >= 2 and req["queue.get"] >= 5 and req["queue.delete"] == 3
+                assert req["queue.update"] == 2
+            await h.close()
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
 def test_abandoned_long_poll_takes_no_messages(front, monkeypatch):
     """A receiver that disconnects in the middle of its long poll (its process died) must not get
     -- and lock -- the next message: a live receiver gets it at once, not after the lock expires."""
@@ -283,6 +334,12 @@ def test_rbac(front, monkeypatch):
                 assert b"not authorized" in ei.value.body
             await api.sb_publish("ns", "t", b"x")
             assert len(await proc.sb_receive("ns", "t/subscriptions/proc")) == 1
+            await admin.queue_put("sa", "q", b"m")  # the account's broker exists -> front serves
+            for call in (proc.queue_put("sa", "q", b"m"), anon.queue_get("sa", "q")):
+                with pytest.raises(BackingError) as ei:
+                    await call
+                assert ei.value.status == 403 and b"not authorized" in ei.value.body
+            assert len(await admin.queue_get("sa", "q")) == 1
             # a policy change at runtime reaches the front
             h = HttpClient()
             r = await h.put(b.base + "/admin/policy", json_body={"mode": "open"})
