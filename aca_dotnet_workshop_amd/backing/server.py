@@ -129,6 +129,7 @@ class BackingServices:
             front.attach_broker(ns, b)
         self._push_policy()
         self.waiters.listeners.append(lambda key: front.notify(*key.split("|", 1)))
+        front.set_blob_root(str(self.blob_root))
 
     def _push_policy(self) -> None:
         if self.front is None:
@@ -617,8 +618,24 @@ class BackingServices:
             return json_response(dict(qbroker(p["account"]).counts(p["queue"])))
 
         # per container, the names of its blobs (built by one scan on first use, then kept by
-        # put / delete -- this process is the only writer): a count needs no directory walk
+        # put / delete -- this process is the only writer): a count needs no directory walk.
+        # With the native front the set is the front's (it writes blobs too): blob_note / blob_count
         names: dict[tuple[str, str], set[str]] = {}
+
+        def note_blob(p: dict[str, Any], added: bool) -> None:
+            name = os.path.normpath(p["name"])
+            if self.front is not None:
+                self.front.blob_note(_safe(p["account"]), _safe(p["container"]), name, added)
+            elif added:
+                blob_names(p).add(name)
+            else:
+                blob_names(p).discard(name)
+
+        def count_blobs(p: dict[str, Any], prefix: str) -> int:
+            if self.front is not None:
+                return int(self.front.blob_count(_safe(p["account"]), _safe(p["container"]), prefix))
+            got = blob_names(p)
+            return sum(1 for x in got if x.startswith(prefix)) if prefix else len(got)
 
         def blob_names(p: dict[str, Any]) -> set[str]:
             k = (_safe(p["account"]), _safe(p["container"]))
@@ -650,7 +667,7 @@ class BackingServices:
             meta = {"contentType": req.headers.get("content-type", "application/octet-stream"),
                     "lastModified": time.time(), "size": len(req.body)}
             f.with_name(f.name + ".meta.json").write_text(json.dumps(meta))
-            blob_names(p).add(os.path.normpath(p["name"]))
+            note_blob(p, True)
             return json_response({"blobURL": f"/storage/{p['account']}/blobs/{p['container']}/{p['name']}"}, 201)
 
         async def get_blob(req: Request) -> Response:
@@ -675,7 +692,7 @@ class BackingServices:
             mf = f.with_name(f.name + ".meta.json")
             if mf.exists():
                 mf.unlink()
-            blob_names(p).discard(os.path.normpath(p["name"]))
+            note_blob(p, False)
             return empty(204)
 
         async def list_blobs(req: Request) -> Response:
@@ -684,8 +701,7 @@ class BackingServices:
             root = self.blob_root / _safe(p["account"]) / _safe(p["container"])
             prefix = req.query_get("prefix", "") or ""
             if (req.query_get("count", "") or "").lower() in ("1", "true"):  # {"count": n}, no listing
-                got = blob_names(p)
-                return json_response({"count": sum(1 for x in got if x.startswith(prefix)) if prefix else len(got)})
+                return json_response({"count": count_blobs(p, prefix)})
             out = []
             if root.is_dir():
                 for f in sorted(root.rglob("*")):

@@ -8,7 +8,8 @@
 * ``_ttgpu``     -- HIP kernels for gfx950 (see ``aca_dotnet_workshop_amd/ops``), built by
   ``ops/build.py``.
 
-Builds are incremental (skipped when the ``.so`` is newer than every source) and land
+Builds are incremental (skipped when the ``.so`` is as new as every source: it is dated like the
+newest source it was compiled from) and land
 next to this file so the driver's gpurun snapshot carries them to the GPU box.
 """
 from __future__ import annotations
@@ -52,6 +53,26 @@ def _stale(target: Path, sources: list[Path]) -> bool:
     return any(s.exists() and s.stat().st_mtime > t for s in sources)
 
 
+def _newest(sources: list[Path]) -> float:
+    return max((s.stat().st_mtime for s in sources if s.exists()), default=0.0)
+
+
+def _install(tmp: Path, target: Path, stamp: float) -> None:
+    """Move the build into place, dated like the newest source it was compiled from: a source
+    saved while the compiler ran is newer than the result, so the next check rebuilds."""
+    os.replace(tmp, target)
+    if stamp > 0:
+        os.utime(target, (stamp, stamp))
+
+
+def _run_compiler(cmd: list[str], tmp: Path) -> None:
+    try:
+        subprocess.run(cmd, check=True)
+    except BaseException:
+        tmp.unlink(missing_ok=True)  # no half-written output left next to the target
+        raise
+
+
 EXE_ONLY_HEADERS: set[str] = set()
 
 
@@ -64,11 +85,11 @@ def build_native(force: bool = False, verbose: bool = False) -> Path:
         return target
     with build_lock("ttnative"):
         if force or _stale(target, sources):
-            _compile_native(target, verbose)
+            _compile_native(target, verbose, _newest(sources))
     return target
 
 
-def _compile_native(target: Path, verbose: bool) -> None:
+def _compile_native(target: Path, verbose: bool, stamp: float = 0.0) -> None:
     import pybind11
     cxx = os.environ.get("CXX", "g++")
     tmp = target.with_suffix(f".tmp{os.getpid()}.so")
@@ -79,8 +100,8 @@ def _compile_native(target: Path, verbose: bool) -> None:
            "-o", str(tmp), "-lpthread", "-lssl", "-lcrypto"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, target)
+    _run_compiler(cmd, tmp)
+    _install(tmp, target, stamp)
 
 
 DATAPLANE = HERE / "bin" / "ttsidecar-dataplane"
@@ -106,8 +127,9 @@ def _build_exe(target: Path, main: Path, sources: list[Path], force: bool, verbo
                "-lssl", "-lcrypto"] + (["-pthread"] if threads else [])
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
-        os.replace(tmp, target)
+        stamp = _newest(sources)
+        _run_compiler(cmd, tmp)
+        _install(tmp, target, stamp)
     return target
 
 

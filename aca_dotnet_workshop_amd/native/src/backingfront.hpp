@@ -12,6 +12,8 @@
 //   GET            /servicebus/{ns}/counts?entity
 //   POST / GET     /storage/{account}/queues/{queue}/messages   (put; receive, long poll)
 //   DELETE / PUT   /storage/{account}/queues/{queue}/messages/{receipt}   (delete; visibility)
+//   PUT            /storage/{account}/blobs/{container}/{name}   (files under the blob root)
+//   GET            /storage/{account}/blobs/{container}?count=true
 //
 // Everything else (entity management, queries, transactions, blobs, key vault, sendgrid,
 // admin) and every request for an engine the Python side has not attached yet is forwarded
@@ -24,6 +26,11 @@
 
 #include <condition_variable>
 #include <deque>
+#include <filesystem>
+#include <unordered_set>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 #include <sys/eventfd.h>
 
@@ -320,6 +327,30 @@ class BackingFront {
     grants_.clear();
     for (auto& [p, s, a] : grants) grants_.push_back(bf::Grant{p, s, a});
   }
+  // -- blobs --------------------------------------------------------------------------------
+  // backing/server.py blob_root: the front writes blobs there as the Python route does.
+  void set_blob_root(const std::string& root) {
+    std::lock_guard l(blob_mu_);
+    blob_root_ = root;
+  }
+  // A container's blob names: one directory scan on first use, then kept by every put and
+  // delete -- the front's own, and Python's through blob_note -- so a count walks nothing.
+  // `account` / `container` are the on-disk (sanitised) names.
+  void blob_note(const std::string& account, const std::string& container, const std::string& name, bool added) {
+    std::lock_guard l(blob_mu_);
+    auto& names = blob_names_locked(account, container);
+    if (added) names.insert(name);
+    else names.erase(name);
+  }
+  size_t blob_count(const std::string& account, const std::string& container, const std::string& prefix) {
+    std::lock_guard l(blob_mu_);
+    auto& names = blob_names_locked(account, container);
+    if (prefix.empty()) return names.size();
+    size_t n = 0;
+    for (auto& x : names) n += x.compare(0, prefix.size(), prefix) == 0;
+    return n;
+  }
+
   // Python-side broker activity (publish / abandon) for parked native long-polls.
   void notify(const std::string& ns, const std::string& entity) {
     for (auto& sh : shards_) sh->post(ns + "|" + entity);
@@ -471,13 +502,121 @@ class BackingFront {
   bool enforce_ = false;
   std::vector<std::pair<std::string, std::string>> keys_;
   std::vector<bf::Grant> grants_;
+  std::mutex blob_mu_;
+  std::string blob_root_;
+  std::unordered_map<std::string, std::unordered_set<std::string>> blob_names_;  // "account/container"
+
+  std::unordered_set<std::string>& blob_names_locked(const std::string& account, const std::string& container) {
+    std::string key = account + "/" + container;
+    auto it = blob_names_.find(key);
+    if (it != blob_names_.end()) return it->second;
+    auto& names = blob_names_[key];
+    namespace fs = std::filesystem;
+    std::error_code ec;
+    fs::path root = fs::path(blob_root_) / account / container;
+    if (!blob_root_.empty() && fs::is_directory(root, ec))
+      for (auto i = fs::recursive_directory_iterator(root, ec); !ec && i != fs::recursive_directory_iterator();
+           i.increment(ec)) {
+        if (!i->is_regular_file(ec)) continue;
+        std::string n = i->path().lexically_relative(root).string();
+        if (!ends_with(n, ".meta.json") && !ends_with(n, ".tmp")) names.insert(std::move(n));
+      }
+    return names;
+  }
+  static bool ends_with(const std::string& s, const char* suf) {
+    size_t n = std::strlen(suf);
+    return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+  }
+  // backing/server.py _safe for ASCII names (non-ASCII ones stay with Python's regex)
+  static bool safe_name(const std::string& in, std::string& out) {
+    out.clear();
+    for (unsigned char c : in) {
+      if (c >= 0x80) return false;
+      bool keep = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '.' || c == '_' ||
+                  c == '-';
+      out += keep ? (char)c : '_';
+    }
+    return true;
+  }
+  static bool write_file(const std::string& path, std::string_view data) {
+    int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd < 0) return false;
+    size_t off = 0;
+    while (off < data.size()) {
+      ssize_t w = ::write(fd, data.data() + off, data.size() - off);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) {
+        ::close(fd);
+        return false;
+      }
+      off += (size_t)w;
+    }
+    return ::close(fd) == 0;
+  }
+
+  // PUT /storage/{account}/blobs/{container}/{name}: the Python route's files (the blob, written
+  // to a .tmp and renamed; its .meta.json) and answer.  Names Python might resolve differently
+  // (dot segments, non-ASCII, its own .tmp / .meta.json suffixes) go to it.
+  bool handle_blob(ev::Message& m, ev::Reply& r, const std::vector<std::string>& seg, const std::string& qs) {
+    std::string acct, cont, root;
+    if (!safe_name(seg[1], acct) || !safe_name(seg[3], cont)) return false;
+    {
+      std::lock_guard l(blob_mu_);
+      root = blob_root_;
+    }
+    if (root.empty()) return false;
+    if (seg.size() == 4 && m.method == "GET") {
+      std::string c = query_get(qs, "count");
+      for (auto& ch : c) ch = ::tt::ascii_lower(ch);
+      if (c != "1" && c != "true") return false;  // the listing stays with Python
+      if (!authorize(m, r, "blob.read", "storage/" + seg[1])) return true;
+      count("blob.count");
+      r.send(200, {{"content-type", "application/json"}},
+             "{\"count\": " + std::to_string(blob_count(acct, cont, query_get(qs, "prefix"))) + "}");
+      return true;
+    }
+    if (seg.size() < 5 || m.method != "PUT") return false;
+    std::string name;
+    for (size_t i = 4; i < seg.size(); ++i) {
+      const std::string& p = seg[i];
+      if (p.empty() || p == "." || p == ".." || p.find('/') != std::string::npos) return false;
+      for (unsigned char c : p)
+        if (c < 0x20 || c >= 0x80) return false;
+      if (i > 4) name += '/';
+      name += p;
+    }
+    if (ends_with(name, ".tmp") || ends_with(name, ".meta.json")) return false;
+    if (!authorize(m, r, "blob.write", "storage/" + seg[1])) return true;
+    count("blob.put");
+    namespace fs = std::filesystem;
+    fs::path f = fs::path(root) / acct / cont / name;
+    std::error_code ec;
+    fs::create_directories(f.parent_path(), ec);
+    const std::string tmp = f.string() + ".tmp";
+    auto* ct = m.header("content-type");
+    char meta[160];
+    std::snprintf(meta, sizeof meta, ", \"lastModified\": %.6f, \"size\": %zu}",
+                  std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count(),
+                  m.body.size());
+    if (ec || !write_file(tmp, m.body) || ::rename(tmp.c_str(), f.c_str()) != 0 ||
+        !write_file(f.string() + ".meta.json",
+                    "{\"contentType\": " + bf::jstr(ct ? *ct : "application/octet-stream") + meta)) {
+      r.send(500, {{"content-type", "application/problem+json; charset=utf-8"}},
+             bf::problem_json(500, "blob write failed: " + f.string()));
+      return true;
+    }
+    blob_note(acct, cont, name, true);
+    r.send(201, {{"content-type", "application/json"}},
+           "{\"blobURL\": " + bf::jstr("/storage/" + seg[1] + "/blobs/" + seg[3] + "/" + name) + "}");
+    return true;
+  }
 
   // Request counters, bumped by every loop on every request: one relaxed atomic per name, no
   // lock and no string (the hottest names first).
-  static constexpr std::array<const char*, 17> kCounters = {
+  static constexpr std::array<const char*, 19> kCounters = {
       "doc.put", "sb.publish", "sb.receive", "sb.settle", "doc.get", "doc.bulkget", "doc.bulkset", "doc.query",
       "doc.throttled", "doc.delete", "doc.query_worker", "doc.query_worker_done", "forwarded",
-      "queue.put", "queue.get", "queue.delete", "queue.update"};
+      "queue.put", "queue.get", "queue.delete", "queue.update", "blob.put", "blob.count"};
   std::array<std::atomic<uint64_t>, kCounters.size()> counters_{};
 
   void count(const char* k) {
@@ -563,6 +702,7 @@ class BackingFront {
       return;
     if (seg.size() >= 3 && seg[0] == "servicebus" && handle_bus(sh, m, r, seg, qs)) return;
     if (seg.size() >= 5 && seg[0] == "storage" && seg[2] == "queues" && handle_storage_queue(sh, m, r, seg, qs)) return;
+    if (seg.size() >= 4 && seg[0] == "storage" && seg[2] == "blobs" && handle_blob(m, r, seg, qs)) return;
     forward(sh, std::move(m), std::move(r));
   }
 

@@ -1069,6 +1069,11 @@ PYBIND11_MODULE(_ttnative, m) {
              });
            }, py::arg("fn"))
       .def("notify", &BackingFront::notify)
+      .def("set_blob_root", &BackingFront::set_blob_root)
+      .def("blob_note", &BackingFront::blob_note, py::arg("account"), py::arg("container"), py::arg("name"),
+           py::arg("added"), py::call_guard<py::gil_scoped_release>())
+      .def("blob_count", &BackingFront::blob_count, py::arg("account"), py::arg("container"), py::arg("prefix") = "",
+           py::call_guard<py::gil_scoped_release>())
       .def("stats", &BackingFront::stats)
       .def("stop", &BackingFront::stop, py::call_guard<py::gil_scoped_release>());
 

@@ -48,13 +48,15 @@ def build_gpu(force: bool = False, verbose: bool = False) -> Path:
 
 
 def _compile(verbose: bool) -> None:
+    from ..native.build import _install, _newest, _run_compiler
     tmp = LIB.with_suffix(f".tmp{os.getpid()}.so")
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall",
            *map(str, sources()), "-o", str(tmp)]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    stamp = _newest(sources() + sorted(HIP_DIR.glob("*.h")))  # dated like the sources compiled
+    _run_compiler(cmd, tmp)
+    _install(tmp, LIB, stamp)
 
 
 if __name__ == "__main__":

@@ -285,6 +285,36 @@ def test_storage_queue(front, monkeypatch):
 
 
 @pytest.mark.parametrize("front", FRONTS)
+def test_blobs(front, monkeypatch):
+    """The output binding's blobs: a put on either front, read back, listed, counted (the front's
+    name set follows Python's deletes too); names Python resolves its own way stay with it."""
+    async def main():
+        async with Backing(front, monkeypatch) as b:
+            c = BackingClient(b.base, identity="x")
+            assert await c.blob_count("sa", "box") == 0
+            r1 = await c.blob_put("sa", "box", "t1.json", b'{"a": 1}', "application/json")
+            assert r1 == {"blobURL": "/storage/sa/blobs/box/t1.json"}
+            await c.blob_put("sa", "box", "dir/t2.json", b"\xff\x00", "application/octet-stream")
+            await c.blob_put("sa", "box", "t1.json", b'{"a": 2}', "application/json")  # overwrite
+            assert await c.blob_get("sa", "box", "t1.json") == b'{"a": 2}'
+            assert await c.blob_get("sa", "box", "dir/t2.json") == b"\xff\x00"
+            assert sorted(x["name"] for x in await c.blob_list("sa", "box")) == ["dir/t2.json", "t1.json"]
+            assert await c.blob_count("sa", "box") == 2 and await c.blob_count("sa", "box", "dir/") == 1
+            assert await c.blob_delete("sa", "box", "t1.json")
+            assert await c.blob_count("sa", "box") == 1
+            with pytest.raises(BackingError) as ei:  # escapes the container: Python's 400 on both
+                await c.blob_put("sa", "box", "../../escape", b"x")
+            assert ei.value.status == 400
+            await c.blob_put("sa", "box", "a/./b.json", b"{}")  # a dot segment: Python's route
+            assert await c.blob_count("sa", "box") == 2
+            stats = (await c.http.get(b.base + "/admin/front")).json()
+            if front == "native":
+                assert stats["requests"]["blob.put"] == 3 and stats["requests"]["blob.count"] >= 4
+            await c.http.close()
+    run(main())
+
+
+@pytest.mark.parametrize("front", FRONTS)
 def test_abandoned_long_poll_takes_no_messages(front, monkeypatch):
     """A receiver that disconnects in the middle of its long poll (its process died) must not get
     -- and lock -- the next message: a live receiver gets it at once, not after the lock expires."""
