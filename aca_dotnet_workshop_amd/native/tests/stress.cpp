@@ -161,12 +161,15 @@ int main(int argc, char** argv) {
   // "Python" thread reconfigures it (policy, notify) and builds / reads the column mirror.
   {
     DocStore store;
-    Broker broker;
+    Broker broker, storage;
     QueueOptions o;
     broker.create_subscription("t", "s", o);
     BackingFront front("127.0.0.1", 0, "/nonexistent/fallback.sock", 3);
     front.attach_store("a", "d", "c", &store);
     front.attach_broker("ns", &broker);
+    front.attach_broker("storage-sa", &storage);  // the storage queue and blob routes too
+    std::string blob_root = std::string(argc > 3 ? argv[3] : "/tmp/stress") + ".blobs";
+    front.set_blob_root(blob_root);
     int port = front.port();
     auto http = [port](const std::string& req) {
       int fd = ::socket(AF_INET, SOCK_STREAM, 0);
@@ -197,12 +200,24 @@ int main(int argc, char** argv) {
                                 "Connection: close\r\n\r\n{}");
           std::string r4 = http("POST /servicebus/ns/receive?entity=t/subscriptions/s&max=4&waitMs=1 HTTP/1.1\r\n"
                                 "Connection: close\r\n\r\n");
-          if (r1.rfind("HTTP/1.1 ", 0) == 0 && r3.rfind("HTTP/1.1 201", 0) == 0 && r4.rfind("HTTP/1.1 200", 0) == 0) ok++;
+          std::string r5 = http("POST /storage/sa/queues/q/messages HTTP/1.1\r\nContent-Length: 2\r\n"
+                                "Connection: close\r\n\r\nhi");
+          std::string r6 = http("GET /storage/sa/queues/q/messages?numofmessages=2&visibilityMs=1&waitMs=1 HTTP/1.1\r\n"
+                                "Connection: close\r\n\r\n");
+          std::string r7 = http("PUT /storage/sa/blobs/box/d" + std::to_string(t) + "/b" + std::to_string(i % 9) +
+                                ".json HTTP/1.1\r\nContent-Length: 2\r\nConnection: close\r\n\r\n{}");
+          std::string r8 = http("GET /storage/sa/blobs/box?count=true HTTP/1.1\r\nConnection: close\r\n\r\n");
+          if (r1.rfind("HTTP/1.1 ", 0) == 0 && r3.rfind("HTTP/1.1 201", 0) == 0 && r4.rfind("HTTP/1.1 200", 0) == 0 &&
+              r5.rfind("HTTP/1.1 201", 0) == 0 && r6.rfind("HTTP/1.1 200", 0) == 0 && r7.rfind("HTTP/1.1 201", 0) == 0 &&
+              r8.rfind("HTTP/1.1 200", 0) == 0)
+            ok++;
         }
       });
     for (int i = 0; i < 200; ++i) {
       front.set_policy(i % 2 ? "open" : "open", {{"cosmos/a", "key"}}, {{"p", "cosmos/a", {"cosmos.read"}}});
       front.notify("ns", "t/subscriptions/s");
+      front.blob_note("sa", "box", "py" + std::to_string(i % 5) + ".json", i % 3 != 0);  // Python's puts / deletes
+      (void)front.blob_count("sa", "box", i % 2 ? "d1/" : "");
       // the columnar mirror is built and read while the front's threads keep writing natively
       if (i == 50) store.mirror_enable({"v"});
       if (i > 50) {
@@ -215,6 +230,8 @@ int main(int argc, char** argv) {
     }
     for (auto& th : ts) th.join();
     front.stop();
+    std::error_code ec;
+    std::filesystem::remove_all(blob_root, ec);
     if (ok.load() < 100) return fail("backing front served too few requests");
     std::printf("backing front ok: %d request rounds\n", ok.load());
   }
